@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Headline benchmark: peer-topic score updates/s on BASELINE.json configs[2]
+(1M peers x 8 topics, full P1-P7 refreshScores()+score() on one MI355X).
+
+A step is one gsx_refresh(): the purge pass plus the fused refresh+score
+kernel over every (observer, peer, topic) record of the shard, with all state
+resident in HBM.  With --gpus N (launched by torch.distributed.run, one rank
+per GPU) every rank owns its own 1M-observer shard (observers are
+range-partitioned; scoring needs no exchange), so scaling is weak and `value`
+is the records all ranks refreshed / the slowest rank's time.
+
+Rank 0 at N=1 also times the CPU oracle (oracle/, a single-threaded C
+restatement of score.go) on the same state for `cpu_baseline`, and checks
+that the GPU scores of that pass are bit-identical to it.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "go-libp2p-pubsub_amd"))
+
+import gsx  # noqa: E402
+from gsx import abi, synth  # noqa: E402
+
+METRIC = "peer-topic score updates/s + msg deliveries/s @1M peers, 1-8 GPUs, %HBM BW"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_RECORD = 82  # read fmd,mmd,mfp,imd,graftTime,flags; write the same with meshTime
+BYTES_PER_PAIR = 49  # read bp, app, p6, expire, connected; write bp, score
+T0 = 1_700_000_000 * abi.SECOND
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_engine(n, T, d, seed, device):
+    t = time.time()
+    ov = synth.connect_some_overlay(n, d=d, seed=seed)
+    log(f"[bench] overlay n={n} pairs={ov.n_pairs} in {time.time() - t:.1f}s")
+    e = gsx.Engine(T, device=device)
+    e.set_peer_params(synth.bench_peer_params())
+    tp = synth.spam_test_topic_params()
+    for k in range(T):
+        e.set_topic_params(k, tp)
+    t = time.time()
+    e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    e.synthesize_state(
+        abi.SynthSpec(seed=seed, now_ns=T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0, imd_max_sybil=100.0,
+                      p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0, p_disconnected=0.0, p_absent=0.0,
+                      expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n)
+    )
+    e.set_app_scores(np.zeros(ov.n_pairs))
+    log(f"[bench] engine loaded + state synthesized in {time.time() - t:.1f}s")
+    return ov, e
+
+
+def load_traffic(cfg_key):
+    """Per-launch HBM bytes of the fused kernel from the rocprofv3 PMC pass
+    committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)."""
+    path = os.path.join(ROOT, "profiles", "pmc_refresh_score.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("config") == cfg_key:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(e, T, now, passes):
+    """Single-threaded oracle refresh+score on the engine's exact state; also
+    checks the GPU scores of the same pass bit-for-bit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # checker / CPU baseline only
+
+    t = time.time()
+    st = e.export_state()
+    o = orc.Oracle(T)
+    o.set_peer_params(synth.bench_peer_params())
+    tp = synth.spam_test_topic_params()
+    for k in range(T):
+        o.set_topic_params(k, tp)
+    log(f"[bench] state exported in {time.time() - t:.1f}s")
+    return o, st
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--peers", type=int, default=1_000_000)
+    ap.add_argument("--topics", type=int, default=8)
+    ap.add_argument("--degree", type=int, default=6)
+    ap.add_argument("--cpu-passes", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    n, T = args.peers, args.topics
+    seed = synth.SEED + rank  # shard r: its own observers (range partition)
+    ov, e = build_engine(n, T, args.degree, seed, local)
+    E = ov.n_pairs
+    R = E * T
+
+    now = T0
+    for _ in range(args.warmup):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    e.sync()
+    e.timing_begin(max(1, args.steps))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    k_total, k_min, k_max, k_n = e.timing_end()
+
+    recs = float(R) * args.steps
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([recs], dtype=torch.float64, device=dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        recs = float(r.item())
+
+    value = recs / elapsed
+    kavg_ms = k_total / max(1, k_n)
+    bytes_per_launch = BYTES_PER_RECORD * R + BYTES_PER_PAIR * E
+    achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
+    cfg_key = f"n={n},T={T},d={args.degree},E={E}"
+    traffic = load_traffic(cfg_key)
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        o, st = cpu_baseline(e, T, now, args.cpu_passes)
+        t = time.time()
+        o.load_overlay(ov.row_ptr, ov.col, None, ov.node_ips)
+        o.import_state(st)
+        o.set_app_scores(np.zeros(E))
+        log(f"[bench] oracle loaded in {time.time() - t:.1f}s")
+        cpu_s = 0.0
+        cpu_now = now
+        for _ in range(args.cpu_passes):
+            cpu_now += abi.SECOND
+            t = time.perf_counter()
+            o.refresh(cpu_now)
+            want = o.scores()
+            cpu_s += time.perf_counter() - t
+        # the GPU on the same starting state and clock
+        e.import_state(st)
+        g_now = now
+        for _ in range(args.cpu_passes):
+            g_now += abi.SECOND
+            e.refresh(g_now)
+        got = e.scores()
+        parity = "bit-exact" if np.array_equal(got.view(np.uint64), want.view(np.uint64)) else (
+            f"MISMATCH in {int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))} pairs")
+        cpu = {
+            "value": R * args.cpu_passes / cpu_s,
+            "unit": "peer-topic score updates/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"the full cfg3 shard ({R} records, {E} pairs), {args.cpu_passes} refresh+score passes of the "
+                      f"C oracle (oracle/gsx_oracle.c, -O2, 1 thread; restatement, not reference Go: no Go on the box), "
+                      f"{cpu_s:.1f}s",
+        }
+        del o, st
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "peer-topic score updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded counter-based generator, BASELINE.md cfg3 initialisation)",
+        "config": {
+            "workload": "cfg3: 1M peers x 8 topics, full P1-P7 refreshScores()+score() per DecayInterval, "
+                        "connectSome d=6 overlay, spam-test topic params",
+            "peers_per_gpu": n,
+            "topics": T,
+            "pairs_per_gpu": E,
+            "records_per_gpu": R,
+            "parallelism": f"observers range-sharded, {world} shard(s), no exchange",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_refresh_score",
+            "kernel_avg_ms": kavg_ms,
+            "kernel_min_ms": k_min,
+            "kernel_max_ms": k_max,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+        "cpu_baseline": cpu,
+        "parity_vs_oracle": parity,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    e.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

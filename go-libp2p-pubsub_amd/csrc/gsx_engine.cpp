@@ -1,0 +1,941 @@
+// gsx_engine.cpp — host side of the engine behind include/gsx.h.
+//
+// Owns the HBM state, orders all work on one HIP stream, keeps the
+// reference's per-message delivery records (score.go:98-118, 686-870) on the
+// host and turns tracer calls into counter events that the device applies.
+// Every arithmetic update of scoring state happens in the HIP kernels of
+// gsx_kernels.hip; this file only moves data and bookkeeps ids.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gsx.h"
+#include "gsx_device.h"
+
+namespace {
+
+constexpr int64_t kSecond = 1000000000LL;
+constexpr int64_t kTimeCacheDuration = 120 * kSecond;  // pubsub.go:30
+
+bool invalid_number(double x) { return std::isnan(x) || std::isinf(x); }
+
+enum { kDeliveryUnknown = 0, kDeliveryValid, kDeliveryInvalid, kDeliveryIgnored, kDeliveryThrottled };
+
+struct RecKey {
+    uint32_t obs;
+    uint64_t msg;
+    bool operator==(const RecKey& o) const { return obs == o.obs && msg == o.msg; }
+};
+struct RecKeyHash {
+    size_t operator()(const RecKey& k) const {
+        uint64_t x = k.msg ^ (uint64_t(k.obs) * 0x9E3779B97F4A7C15ULL);
+        x ^= x >> 31;
+        x *= 0xbf58476d1ce4e5b9ULL;
+        x ^= x >> 29;
+        return size_t(x);
+    }
+};
+// deliveryRecord, score.go:98-103
+struct DeliveryRecord {
+    int status = kDeliveryUnknown;
+    int64_t first_seen = 0;
+    int64_t validated = 0;
+    bool validated_set = false;  // !validated.IsZero()
+    std::vector<uint64_t> peers;
+    bool peers_nil = false;
+};
+
+}  // namespace
+
+struct gsx_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr, ev_staged = nullptr;
+    std::string err;
+
+    uint32_t T = 0;
+    gsx_peer_score_params pp{};
+    bool pp_set = false;
+    gsx_thresholds th{};
+    gsx_topic_score_params tp[GSX_MAX_TOPICS]{};
+    bool scored[GSX_MAX_TOPICS]{};
+    gsx::DevTopicParams* d_tp = nullptr;
+
+    // overlay
+    bool loaded = false;
+    uint32_t n_nodes = 0;
+    uint64_t E = 0, rs = 0;
+    std::vector<int64_t> row_ptr;
+    std::vector<uint32_t> pair_obs;
+    std::vector<uint32_t> ipg_host;  // 2 per pair, without WL bits
+    std::vector<uint32_t> group_ip;  // IP id of each (observer, IP) group
+    std::vector<uint8_t> ip_wl;      // per IP id: whitelisted
+    uint32_t n_groups = 0;
+
+    // device state
+    double *d_fmd = nullptr, *d_mmd = nullptr, *d_mfp = nullptr, *d_imd = nullptr;
+    int64_t *d_graft = nullptr, *d_mtime = nullptr;
+    uint8_t* d_rflags = nullptr;
+    uint8_t *d_pflags = nullptr, *d_eflags = nullptr;
+    int64_t* d_expire = nullptr;
+    double *d_bp = nullptr, *d_app = nullptr, *d_score = nullptr;
+    uint32_t *d_ipg = nullptr, *d_ipcount = nullptr;
+    int32_t* d_col = nullptr;
+
+    // events
+    std::vector<gsx_event> pending;
+    void* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    void* d_stage = nullptr;
+    size_t d_stage_bytes = 0;
+    bool staged_inflight = false;
+
+    bool scores_valid = false;
+    bool timed = false;
+    // gsx_timing_begin/end: event pairs around each fused launch
+    std::vector<hipEvent_t> tev;
+    uint32_t t_max = 0, t_used = 0;
+    bool t_active = false;
+
+    // delivery records
+    std::unordered_map<RecKey, DeliveryRecord, RecKeyHash> recs;
+    std::unordered_map<uint32_t, std::deque<std::pair<uint64_t, int64_t>>> rec_queue;  // per observer FIFO
+};
+
+namespace {
+
+int fail(gsx_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+#define HIPCHK(e, call)                                                                          \
+    do {                                                                                         \
+        hipError_t _st = (call);                                                                 \
+        if (_st != hipSuccess)                                                                   \
+            return fail((e), GSX_EDEVICE, std::string(#call ": ") + hipGetErrorString(_st));    \
+    } while (0)
+
+gsx::DevState dev_state(const gsx_engine* e) {
+    gsx::DevState s{};
+    s.fmd = e->d_fmd;
+    s.mmd = e->d_mmd;
+    s.mfp = e->d_mfp;
+    s.imd = e->d_imd;
+    s.graft = e->d_graft;
+    s.mtime = e->d_mtime;
+    s.rflags = e->d_rflags;
+    s.pflags = e->d_pflags;
+    s.expire = e->d_expire;
+    s.bp = e->d_bp;
+    s.app = e->d_app;
+    s.ipg = e->d_ipg;
+    s.ipcount = e->d_ipcount;
+    s.score = e->d_score;
+    s.tp = e->d_tp;
+    s.n_pairs = e->E;
+    s.rs = e->rs;
+    s.n_topics = e->T;
+    return s;
+}
+
+gsx::DevPeerParams dev_peer_params(const gsx_engine* e) {
+    gsx::DevPeerParams d{};
+    d.topic_score_cap = e->pp.topic_score_cap;
+    d.w5 = e->pp.app_specific_weight;
+    d.w6 = e->pp.ip_colocation_factor_weight;
+    d.thr6 = e->pp.ip_colocation_factor_threshold;
+    d.w7 = e->pp.behaviour_penalty_weight;
+    d.thr7 = e->pp.behaviour_penalty_threshold;
+    d.d7 = e->pp.behaviour_penalty_decay;
+    d.decay_to_zero = e->pp.decay_to_zero;
+    d.retain_ns = e->pp.retain_score_ns;
+    return d;
+}
+
+int upload_topic_params(gsx_engine* e) {
+    gsx::DevTopicParams h[GSX_MAX_TOPICS]{};
+    for (uint32_t t = 0; t < e->T; ++t) {
+        const gsx_topic_score_params& p = e->tp[t];
+        gsx::DevTopicParams& d = h[t];
+        d.topic_weight = p.topic_weight;
+        d.w1 = p.time_in_mesh_weight;
+        d.cap1 = p.time_in_mesh_cap;
+        d.q1 = p.time_in_mesh_quantum_ns;
+        d.w2 = p.first_message_deliveries_weight;
+        d.d2 = p.first_message_deliveries_decay;
+        d.cap2 = p.first_message_deliveries_cap;
+        d.w3 = p.mesh_message_deliveries_weight;
+        d.d3 = p.mesh_message_deliveries_decay;
+        d.cap3 = p.mesh_message_deliveries_cap;
+        d.thr3 = p.mesh_message_deliveries_threshold;
+        d.win3 = p.mesh_message_deliveries_window_ns;
+        d.act3 = p.mesh_message_deliveries_activation_ns;
+        d.w3b = p.mesh_failure_penalty_weight;
+        d.d3b = p.mesh_failure_penalty_decay;
+        d.w4 = p.invalid_message_deliveries_weight;
+        d.d4 = p.invalid_message_deliveries_decay;
+        d.scored = e->scored[t] ? 1 : 0;
+        if (!e->scored[t]) d.q1 = 1;  // never divided by: unscored topics are skipped
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_tp, h, sizeof(gsx::DevTopicParams) * GSX_MAX_TOPICS, hipMemcpyHostToDevice,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // `h` is on the stack
+    return GSX_OK;
+}
+
+void free_state(gsx_engine* e) {
+    void* ptrs[] = {e->d_fmd,   e->d_mmd,    e->d_mfp,    e->d_imd, e->d_graft, e->d_mtime,
+                    e->d_rflags, e->d_pflags, e->d_eflags, e->d_expire, e->d_bp,  e->d_app,
+                    e->d_score, e->d_ipg,    e->d_ipcount, e->d_col};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    e->d_fmd = e->d_mmd = e->d_mfp = e->d_imd = nullptr;
+    e->d_graft = e->d_mtime = nullptr;
+    e->d_rflags = e->d_pflags = e->d_eflags = nullptr;
+    e->d_expire = nullptr;
+    e->d_bp = e->d_app = e->d_score = nullptr;
+    e->d_ipg = e->d_ipcount = nullptr;
+    e->d_col = nullptr;
+}
+
+template <class T>
+int dalloc(gsx_engine* e, T** p, size_t n) {
+    hipError_t st = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
+    if (st != hipSuccess) return fail(e, GSX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(st));
+    return GSX_OK;
+}
+
+int upload_ipg(gsx_engine* e) {
+    std::vector<uint32_t> ipg(e->ipg_host.size());
+    for (size_t i = 0; i < ipg.size(); ++i) {
+        uint32_t g = e->ipg_host[i];
+        if (g != gsx::IPG_NONE) {
+            uint32_t ip = e->group_ip[g];
+            if (ip < e->ip_wl.size() && e->ip_wl[ip]) g |= gsx::IPG_WL;
+        }
+        ipg[i] = g;
+    }
+    HIPCHK(e, hipMemcpy(e->d_ipg, ipg.data(), sizeof(uint32_t) * (ipg.size() ? ipg.size() : 0),
+                        hipMemcpyHostToDevice));
+    return GSX_OK;
+}
+
+// Applies queued events on the device (score.go:588-974 via k_apply_events).
+int flush(gsx_engine* e) {
+    if (e->pending.empty()) return GSX_OK;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "events before gsx_load_overlay");
+    const size_t n = e->pending.size();
+    // stable grouping by observer: order inside each observer is preserved
+    std::vector<uint32_t> obs(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (e->pending[i].pair >= e->E) {
+            e->pending.clear();
+            return fail(e, GSX_ERANGE, "event pair out of range");
+        }
+        obs[i] = e->pair_obs[e->pending[i].pair];
+    }
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return obs[a] < obs[b]; });
+    std::vector<uint32_t> group_off;
+    group_off.reserve(64);
+    for (size_t i = 0; i < n; ++i)
+        if (i == 0 || obs[order[i]] != obs[order[i - 1]]) group_off.push_back((uint32_t)i);
+    const uint32_t n_groups = (uint32_t)group_off.size();
+    group_off.push_back((uint32_t)n);
+
+    const size_t ev_bytes = sizeof(gsx::DevEvent) * n;
+    const size_t off_bytes = sizeof(uint32_t) * group_off.size();
+    const size_t total = ev_bytes + off_bytes;
+    if (e->staged_inflight) {
+        HIPCHK(e, hipEventSynchronize(e->ev_staged));
+        e->staged_inflight = false;
+    }
+    if (e->h_stage_bytes < total) {
+        if (e->h_stage) (void)hipHostFree(e->h_stage);
+        e->h_stage = nullptr;
+        size_t want = std::max(total, e->h_stage_bytes * 2);
+        HIPCHK(e, hipHostMalloc(&e->h_stage, want, hipHostMallocDefault));
+        e->h_stage_bytes = want;
+    }
+    if (e->d_stage_bytes < total) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (e->d_stage) (void)hipFree(e->d_stage);
+        e->d_stage = nullptr;
+        size_t want = std::max(total, e->d_stage_bytes * 2);
+        HIPCHK(e, hipMalloc(&e->d_stage, want));
+        e->d_stage_bytes = want;
+    }
+    auto* hev = static_cast<gsx::DevEvent*>(e->h_stage);
+    for (size_t i = 0; i < n; ++i) {
+        const gsx_event& s = e->pending[order[i]];
+        hev[i] = gsx::DevEvent{s.kind, s.topic, s.pair, s.now_ns, s.arg};
+    }
+    std::memcpy(static_cast<char*>(e->h_stage) + ev_bytes, group_off.data(), off_bytes);
+    HIPCHK(e, hipMemcpyAsync(e->d_stage, e->h_stage, total, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    e->staged_inflight = true;
+    const auto* dev = static_cast<const gsx::DevEvent*>(e->d_stage);
+    const auto* doff = reinterpret_cast<const uint32_t*>(static_cast<const char*>(e->d_stage) + ev_bytes);
+    HIPCHK(e, gsx::launch_apply_events(dev_state(e), dev_peer_params(e), dev, doff, n_groups, e->stream));
+    e->pending.clear();
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int ensure_scores(gsx_engine* e) {
+    int rc = flush(e);
+    if (rc) return rc;
+    if (!e->scores_valid) {
+        HIPCHK(e, gsx::launch_refresh_score(dev_state(e), dev_peer_params(e), 0, false, e->stream));
+        e->scores_valid = true;
+    }
+    return GSX_OK;
+}
+
+void push_event(gsx_engine* e, uint32_t kind, uint64_t pair, uint32_t topic, int64_t now, int64_t arg) {
+    e->pending.push_back(gsx_event{kind, topic, pair, now, arg});
+}
+
+// messageDeliveries.getRecord, score.go:833-854
+DeliveryRecord& get_record(gsx_engine* e, uint32_t obs, uint64_t msg, int64_t now) {
+    auto it = e->recs.find(RecKey{obs, msg});
+    if (it != e->recs.end()) return it->second;
+    DeliveryRecord& r = e->recs[RecKey{obs, msg}];
+    r.first_seen = now;
+    e->rec_queue[obs].emplace_back(msg, now + kTimeCacheDuration);
+    return r;
+}
+
+// markDuplicateMessageDelivery's window test (score.go:962-967), on the host
+// because it needs only the record's validated time; the inMesh test runs on
+// the device.
+void mark_duplicate(gsx_engine* e, uint64_t pair, uint32_t topic, bool validated_set, int64_t validated,
+                    int64_t now) {
+    if (topic >= e->T || !e->scored[topic]) return;
+    if (validated_set && (now - validated) > e->tp[topic].mesh_message_deliveries_window_ns) return;
+    push_event(e, GSX_EV_MESH_DELIVERY, pair, topic, now, 0);
+}
+
+bool has_peer(const DeliveryRecord& r, uint64_t p) {
+    return std::find(r.peers.begin(), r.peers.end(), p) != r.peers.end();
+}
+
+int check_pair(gsx_engine* e, uint64_t pair) {
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (pair >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
+    return GSX_OK;
+}
+
+}  // namespace
+
+// ==== C ABI ===================================================================
+
+extern "C" {
+
+int gsx_abi_version(void) { return GSX_ABI_VERSION; }
+
+const char* gsx_last_error(gsx_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+// PeerScoreThresholds.validate, score_params.go:34-51
+int gsx_validate_thresholds(const gsx_thresholds* p) {
+    if (!p) return GSX_EINVAL;
+    if (p->gossip_threshold > 0 || invalid_number(p->gossip_threshold)) return GSX_EINVAL;
+    if (p->publish_threshold > 0 || p->publish_threshold > p->gossip_threshold || invalid_number(p->publish_threshold))
+        return GSX_EINVAL;
+    if (p->graylist_threshold > 0 || p->graylist_threshold > p->publish_threshold ||
+        invalid_number(p->graylist_threshold))
+        return GSX_EINVAL;
+    if (p->accept_px_threshold < 0 || invalid_number(p->accept_px_threshold)) return GSX_EINVAL;
+    if (p->opportunistic_graft_threshold < 0 || invalid_number(p->opportunistic_graft_threshold)) return GSX_EINVAL;
+    return GSX_OK;
+}
+
+// PeerScoreParams.validate, score_params.go:151-198 (without the Topics loop)
+int gsx_validate_peer_params(const gsx_peer_score_params* p) {
+    if (!p) return GSX_EINVAL;
+    if (p->topic_score_cap < 0 || invalid_number(p->topic_score_cap)) return GSX_EINVAL;
+    if (!p->app_specific_score_set) return GSX_EINVAL;
+    if (p->ip_colocation_factor_weight > 0 || invalid_number(p->ip_colocation_factor_weight)) return GSX_EINVAL;
+    if (p->ip_colocation_factor_weight != 0 && p->ip_colocation_factor_threshold < 1) return GSX_EINVAL;
+    if (p->behaviour_penalty_weight > 0 || invalid_number(p->behaviour_penalty_weight)) return GSX_EINVAL;
+    if (p->behaviour_penalty_weight != 0 &&
+        (p->behaviour_penalty_decay <= 0 || p->behaviour_penalty_decay >= 1 || invalid_number(p->behaviour_penalty_decay)))
+        return GSX_EINVAL;
+    if (p->behaviour_penalty_threshold < 0 || invalid_number(p->behaviour_penalty_threshold)) return GSX_EINVAL;
+    if (p->decay_interval_ns < kSecond) return GSX_EINVAL;
+    if (p->decay_to_zero <= 0 || p->decay_to_zero >= 1 || invalid_number(p->decay_to_zero)) return GSX_EINVAL;
+    return GSX_OK;
+}
+
+// TopicScoreParams.validate, score_params.go:200-268
+int gsx_validate_topic_params(const gsx_topic_score_params* p) {
+    if (!p) return GSX_EINVAL;
+    if (p->topic_weight < 0 || invalid_number(p->topic_weight)) return GSX_EINVAL;
+    if (p->time_in_mesh_quantum_ns == 0) return GSX_EINVAL;
+    if (p->time_in_mesh_weight < 0 || invalid_number(p->time_in_mesh_weight)) return GSX_EINVAL;
+    if (p->time_in_mesh_weight != 0 && p->time_in_mesh_quantum_ns <= 0) return GSX_EINVAL;
+    if (p->time_in_mesh_weight != 0 && (p->time_in_mesh_cap <= 0 || invalid_number(p->time_in_mesh_cap)))
+        return GSX_EINVAL;
+    const double w2 = p->first_message_deliveries_weight;
+    if (w2 < 0 || invalid_number(w2)) return GSX_EINVAL;
+    if (w2 != 0 && (p->first_message_deliveries_decay <= 0 || p->first_message_deliveries_decay >= 1 ||
+                    invalid_number(p->first_message_deliveries_decay)))
+        return GSX_EINVAL;
+    if (w2 != 0 && (p->first_message_deliveries_cap <= 0 || invalid_number(p->first_message_deliveries_cap)))
+        return GSX_EINVAL;
+    const double w3 = p->mesh_message_deliveries_weight;
+    if (w3 > 0 || invalid_number(w3)) return GSX_EINVAL;
+    if (w3 != 0 && (p->mesh_message_deliveries_decay <= 0 || p->mesh_message_deliveries_decay >= 1 ||
+                    invalid_number(p->mesh_message_deliveries_decay)))
+        return GSX_EINVAL;
+    if (w3 != 0 && (p->mesh_message_deliveries_cap <= 0 || invalid_number(p->mesh_message_deliveries_cap)))
+        return GSX_EINVAL;
+    if (w3 != 0 &&
+        (p->mesh_message_deliveries_threshold <= 0 || invalid_number(p->mesh_message_deliveries_threshold)))
+        return GSX_EINVAL;
+    if (p->mesh_message_deliveries_window_ns < 0) return GSX_EINVAL;
+    if (w3 != 0 && p->mesh_message_deliveries_activation_ns < kSecond) return GSX_EINVAL;
+    const double w3b = p->mesh_failure_penalty_weight;
+    if (w3b > 0 || invalid_number(w3b)) return GSX_EINVAL;
+    if (w3b != 0 && (invalid_number(p->mesh_failure_penalty_decay) || p->mesh_failure_penalty_decay <= 0 ||
+                     p->mesh_failure_penalty_decay >= 1))
+        return GSX_EINVAL;
+    const double w4 = p->invalid_message_deliveries_weight;
+    if (w4 > 0 || invalid_number(w4)) return GSX_EINVAL;
+    if (p->invalid_message_deliveries_decay <= 0 || p->invalid_message_deliveries_decay >= 1 ||
+        invalid_number(p->invalid_message_deliveries_decay))
+        return GSX_EINVAL;
+    return GSX_OK;
+}
+
+// ScoreParameterDecayWithBase, score_params.go:282-287
+double gsx_score_parameter_decay_with_base(int64_t decay_ns, int64_t base_ns, double decay_to_zero) {
+    const double ticks = double(decay_ns / base_ns);
+    return std::pow(decay_to_zero, 1 / ticks);
+}
+
+double gsx_score_parameter_decay(int64_t decay_ns) {
+    return gsx_score_parameter_decay_with_base(decay_ns, kSecond, 0.01);
+}
+
+int gsx_create(const gsx_config* cfg, gsx_engine** out) {
+    if (!cfg || !out) return GSX_EINVAL;
+    *out = nullptr;
+    if (cfg->n_topics == 0 || cfg->n_topics > GSX_MAX_TOPICS) return GSX_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) return GSX_ENODEV;
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GSX_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GSX_ENODEV;  // gfx950-only code objects
+    auto* e = new (std::nothrow) gsx_engine();
+    if (!e) return GSX_ENOMEM;
+    e->device = cfg->device;
+    e->T = cfg->n_topics;
+    if (hipSetDevice(e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&e->ev_start) != hipSuccess || hipEventCreate(&e->ev_stop) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void**)&e->d_tp, sizeof(gsx::DevTopicParams) * GSX_MAX_TOPICS) != hipSuccess) {
+        gsx_destroy(e);
+        return GSX_EDEVICE;
+    }
+    if (upload_topic_params(e) != GSX_OK) {
+        gsx_destroy(e);
+        return GSX_EDEVICE;
+    }
+    *out = e;
+    return GSX_OK;
+}
+
+int gsx_destroy(gsx_engine* e) {
+    if (!e) return GSX_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    free_state(e);
+    if (e->d_tp) (void)hipFree(e->d_tp);
+    if (e->d_stage) (void)hipFree(e->d_stage);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->ev_start) (void)hipEventDestroy(e->ev_start);
+    if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
+    if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
+    for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return GSX_OK;
+}
+
+int gsx_set_peer_params(gsx_engine* e, const gsx_peer_score_params* p) {
+    if (!e || !p) return GSX_EINVAL;
+    int rc = flush(e);  // queued events see the params they were issued under
+    if (rc) return rc;
+    e->pp = *p;
+    e->pp_set = true;
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int gsx_set_thresholds(gsx_engine* e, const gsx_thresholds* t) {
+    if (!e || !t) return GSX_EINVAL;
+    e->th = *t;
+    return GSX_OK;
+}
+
+// SetTopicScoreParams, score.go:194-234
+int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_params* p) {
+    if (!e || !p) return GSX_EINVAL;
+    if (topic >= e->T) return fail(e, GSX_ERANGE, "topic out of range");
+    if (p->time_in_mesh_quantum_ns == 0)  // Go would panic dividing by it in score()
+        return fail(e, GSX_EINVAL, "TimeInMeshQuantum must be non zero");
+    int rc = flush(e);
+    if (rc) return rc;
+    const bool exist = e->scored[topic];
+    const gsx_topic_score_params old = e->tp[topic];
+    e->tp[topic] = *p;
+    e->scored[topic] = true;
+    e->scores_valid = false;
+    rc = upload_topic_params(e);
+    if (rc) return rc;
+    if (!exist || !e->loaded) return GSX_OK;
+    const bool recap = p->first_message_deliveries_cap < old.first_message_deliveries_cap ||
+                       p->mesh_message_deliveries_cap < old.mesh_message_deliveries_cap;
+    if (!recap) return GSX_OK;
+    HIPCHK(e, gsx::launch_recap(dev_state(e), topic, p->first_message_deliveries_cap, p->mesh_message_deliveries_cap,
+                                e->stream));
+    return GSX_OK;
+}
+
+int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
+                     const uint8_t* edge_flags, const uint32_t* node_ips) {
+    if (!e || !row_ptr || (!col && row_ptr[n_nodes] > 0)) return GSX_EINVAL;
+    if (row_ptr[0] != 0) return fail(e, GSX_EINVAL, "row_ptr[0] must be 0");
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        if (row_ptr[i + 1] < row_ptr[i]) return fail(e, GSX_EINVAL, "row_ptr not monotone");
+    const uint64_t E = (uint64_t)row_ptr[n_nodes];
+    for (uint64_t p = 0; p < E; ++p)
+        if (col[p] < 0 || (uint32_t)col[p] >= n_nodes) return fail(e, GSX_EINVAL, "col out of range");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    free_state(e);
+    e->loaded = false;
+    e->pending.clear();
+    e->recs.clear();
+    e->rec_queue.clear();
+    e->n_nodes = n_nodes;
+    e->E = E;
+    e->rs = (E + 63) & ~uint64_t(63);
+    e->row_ptr.assign(row_ptr, row_ptr + n_nodes + 1);
+    e->pair_obs.resize(E);
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        for (int64_t p = row_ptr[i]; p < row_ptr[i + 1]; ++p) e->pair_obs[(size_t)p] = i;
+
+    // (observer, IP) groups: the keys of each observer's ps.peerIPs map
+    e->ipg_host.assign(2 * E, gsx::IPG_NONE);
+    e->group_ip.clear();
+    uint32_t next = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> small;  // (ip, gid) for low-degree observers
+    std::unordered_map<uint32_t, uint32_t> big;
+    for (uint32_t i = 0; i < n_nodes && node_ips; ++i) {
+        const int64_t deg = row_ptr[i + 1] - row_ptr[i];
+        small.clear();
+        big.clear();
+        for (int64_t p = row_ptr[i]; p < row_ptr[i + 1]; ++p) {
+            const uint32_t nb = (uint32_t)col[p];
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t ip = node_ips[2 * (size_t)nb + k];
+                if (ip == GSX_NO_IP) continue;
+                uint32_t gid;
+                if (deg <= 64) {
+                    auto it = std::find_if(small.begin(), small.end(), [&](auto& x) { return x.first == ip; });
+                    if (it == small.end()) {
+                        gid = next++;
+                        small.emplace_back(ip, gid);
+                        e->group_ip.push_back(ip);
+                    } else {
+                        gid = it->second;
+                    }
+                } else {
+                    auto it = big.find(ip);
+                    if (it == big.end()) {
+                        gid = next++;
+                        big.emplace(ip, gid);
+                        e->group_ip.push_back(ip);
+                    } else {
+                        gid = it->second;
+                    }
+                }
+                e->ipg_host[2 * (size_t)p + k] = gid;
+            }
+        }
+    }
+    e->n_groups = next;
+
+    const size_t R = (size_t)e->T * e->rs;
+    int rc = 0;
+    if ((rc = dalloc(e, &e->d_fmd, R)) || (rc = dalloc(e, &e->d_mmd, R)) || (rc = dalloc(e, &e->d_mfp, R)) ||
+        (rc = dalloc(e, &e->d_imd, R)) || (rc = dalloc(e, &e->d_graft, R)) || (rc = dalloc(e, &e->d_mtime, R)) ||
+        (rc = dalloc(e, &e->d_rflags, R)) || (rc = dalloc(e, &e->d_pflags, e->rs)) ||
+        (rc = dalloc(e, &e->d_eflags, e->rs)) || (rc = dalloc(e, &e->d_expire, e->rs)) ||
+        (rc = dalloc(e, &e->d_bp, e->rs)) || (rc = dalloc(e, &e->d_app, e->rs)) ||
+        (rc = dalloc(e, &e->d_score, e->rs)) || (rc = dalloc(e, &e->d_ipg, 2 * e->rs)) ||
+        (rc = dalloc(e, &e->d_ipcount, e->n_groups)) || (rc = dalloc(e, &e->d_col, E))) {
+        free_state(e);
+        return rc;
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_fmd, 0, sizeof(double) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_mmd, 0, sizeof(double) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_mfp, 0, sizeof(double) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_imd, 0, sizeof(double) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_graft, 0, sizeof(int64_t) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_mtime, 0, sizeof(int64_t) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_rflags, 0, R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_pflags, 0, e->rs, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_expire, 0, sizeof(int64_t) * e->rs, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_bp, 0, sizeof(double) * e->rs, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_app, 0, sizeof(double) * e->rs, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_score, 0, sizeof(double) * e->rs, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ipcount, 0, sizeof(uint32_t) * (e->n_groups ? e->n_groups : 1), e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (E) HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * E, hipMemcpyHostToDevice));
+    if (edge_flags) HIPCHK(e, hipMemcpy(e->d_eflags, edge_flags, E, hipMemcpyHostToDevice));
+    else HIPCHK(e, hipMemsetAsync(e->d_eflags, 0, e->rs, e->stream));
+    rc = upload_ipg(e);
+    if (rc) return rc;
+    e->loaded = true;
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int gsx_num_pairs(gsx_engine* e, uint64_t* out) {
+    if (!e || !out) return GSX_EINVAL;
+    *out = e->E;
+    return GSX_OK;
+}
+
+int gsx_set_ip_whitelist(gsx_engine* e, const uint32_t* ip_ids, size_t n) {
+    if (!e || (n && !ip_ids)) return GSX_EINVAL;
+    int rc = flush(e);
+    if (rc) return rc;
+    e->ip_wl.clear();
+    for (size_t i = 0; i < n; ++i) {
+        if (ip_ids[i] == GSX_NO_IP) continue;
+        if (ip_ids[i] >= e->ip_wl.size()) e->ip_wl.resize((size_t)ip_ids[i] + 1, 0);
+        e->ip_wl[ip_ids[i]] = 1;
+    }
+    e->scores_valid = false;
+    if (!e->loaded) return GSX_OK;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return upload_ipg(e);
+}
+
+int gsx_set_app_scores(gsx_engine* e, const double* app, size_t n) {
+    if (!e || !app) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (n != e->E) return fail(e, GSX_EINVAL, "app score count != pairs");
+    int rc = flush(e);  // a queued RemovePeer must see the app score it was issued under
+    if (rc) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->d_app, app, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int gsx_apply_events(gsx_engine* e, const gsx_event* ev, size_t n) {
+    if (!e || (n && !ev)) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    for (size_t i = 0; i < n; ++i) {
+        if (ev[i].pair >= e->E) return fail(e, GSX_ERANGE, "event pair out of range");
+        if (ev[i].kind < GSX_EV_ADD_PEER || ev[i].kind > GSX_EV_PENALTY) return fail(e, GSX_EINVAL, "bad event kind");
+    }
+    e->pending.insert(e->pending.end(), ev, ev + n);
+    return GSX_OK;
+}
+
+int gsx_flush(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    return flush(e);
+}
+
+// ValidateMessage, score.go:686-693
+int gsx_trace_validate(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    (void)topic;
+    if (!e) return GSX_EINVAL;
+    if (int rc = check_pair(e, pair)) return rc;
+    (void)get_record(e, e->pair_obs[pair], msg_id, now);
+    return GSX_OK;
+}
+
+// DeliverMessage, score.go:695-719
+int gsx_trace_deliver(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = check_pair(e, pair)) return rc;
+    push_event(e, GSX_EV_FIRST_DELIVERY, pair, topic, now, 0);
+    DeliveryRecord& r = get_record(e, e->pair_obs[pair], msg_id, now);
+    if (r.status != kDeliveryUnknown) return GSX_OK;
+    r.status = kDeliveryValid;
+    r.validated = now;
+    r.validated_set = true;
+    for (uint64_t q : r.peers)
+        if (q != pair) mark_duplicate(e, q, topic, false, 0, now);
+    return GSX_OK;
+}
+
+// RejectMessage, score.go:721-786
+int gsx_trace_reject(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int32_t reason, int64_t now) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = check_pair(e, pair)) return rc;
+    switch (reason) {
+    case GSX_REJECT_MISSING_SIGNATURE:
+    case GSX_REJECT_INVALID_SIGNATURE:
+    case GSX_REJECT_UNEXPECTED_SIGNATURE:
+    case GSX_REJECT_UNEXPECTED_AUTH_INFO:
+    case GSX_REJECT_SELF_ORIGIN: push_event(e, GSX_EV_INVALID_DELIVERY, pair, topic, now, 0); return GSX_OK;
+    case GSX_REJECT_BLACKLISTED_PEER:
+    case GSX_REJECT_BLACKLISTED_SOURCE:
+    case GSX_REJECT_VALIDATION_QUEUE_FULL: return GSX_OK;
+    case GSX_REJECT_VALIDATION_THROTTLED:
+    case GSX_REJECT_VALIDATION_IGNORED:
+    case GSX_REJECT_VALIDATION_FAILED: break;
+    default: return fail(e, GSX_EINVAL, "unknown reject reason");
+    }
+    DeliveryRecord& r = get_record(e, e->pair_obs[pair], msg_id, now);
+    if (r.status != kDeliveryUnknown) return GSX_OK;
+    if (reason == GSX_REJECT_VALIDATION_THROTTLED || reason == GSX_REJECT_VALIDATION_IGNORED) {
+        r.status = reason == GSX_REJECT_VALIDATION_THROTTLED ? kDeliveryThrottled : kDeliveryIgnored;
+        r.peers.clear();
+        r.peers.shrink_to_fit();
+        r.peers_nil = true;
+        return GSX_OK;
+    }
+    r.status = kDeliveryInvalid;
+    push_event(e, GSX_EV_INVALID_DELIVERY, pair, topic, now, 0);
+    for (uint64_t q : r.peers) push_event(e, GSX_EV_INVALID_DELIVERY, q, topic, now, 0);
+    r.peers.clear();
+    r.peers.shrink_to_fit();
+    r.peers_nil = true;
+    return GSX_OK;
+}
+
+// DuplicateMessage, score.go:788-820
+int gsx_trace_duplicate(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = check_pair(e, pair)) return rc;
+    DeliveryRecord& r = get_record(e, e->pair_obs[pair], msg_id, now);
+    if (!r.peers_nil && has_peer(r, pair)) return GSX_OK;
+    switch (r.status) {
+    case kDeliveryUnknown: r.peers.push_back(pair); break;
+    case kDeliveryValid:
+        r.peers.push_back(pair);
+        mark_duplicate(e, pair, topic, r.validated_set, r.validated, now);
+        break;
+    case kDeliveryInvalid: push_event(e, GSX_EV_INVALID_DELIVERY, pair, topic, now, 0); break;
+    default: break;
+    }
+    return GSX_OK;
+}
+
+// messageDeliveries.gc, score.go:856-870
+int gsx_gc_deliveries(gsx_engine* e, int64_t now) {
+    if (!e) return GSX_EINVAL;
+    for (auto it = e->rec_queue.begin(); it != e->rec_queue.end();) {
+        auto& q = it->second;
+        while (!q.empty() && now > q.front().second) {
+            e->recs.erase(RecKey{it->first, q.front().first});
+            q.pop_front();
+        }
+        it = q.empty() ? e->rec_queue.erase(it) : std::next(it);
+    }
+    return GSX_OK;
+}
+
+int gsx_num_delivery_records(gsx_engine* e, uint64_t* out) {
+    if (!e || !out) return GSX_EINVAL;
+    *out = e->recs.size();
+    return GSX_OK;
+}
+
+// refreshScores, score.go:497-558, fused with score() for every pair
+int gsx_refresh(gsx_engine* e, int64_t now) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    int rc = flush(e);
+    if (rc) return rc;
+    const gsx::DevState s = dev_state(e);
+    HIPCHK(e, gsx::launch_purge(s, now, e->stream));
+    const bool region = e->t_active && e->t_used < e->t_max;
+    HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used] : e->ev_start, e->stream));
+    HIPCHK(e, gsx::launch_refresh_score(s, dev_peer_params(e), now, true, e->stream));
+    HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used + 1] : e->ev_stop, e->stream));
+    if (region) ++e->t_used;
+    e->timed = !region;
+    e->scores_valid = true;
+    return GSX_OK;
+}
+
+int gsx_last_refresh_ms(gsx_engine* e, float* ms) {
+    if (!e || !ms) return GSX_EINVAL;
+    if (!e->timed) return fail(e, GSX_ESTATE, "no refresh timed yet");
+    HIPCHK(e, hipEventSynchronize(e->ev_stop));
+    HIPCHK(e, hipEventElapsedTime(ms, e->ev_start, e->ev_stop));
+    return GSX_OK;
+}
+
+int gsx_timing_begin(gsx_engine* e, uint32_t max_launches) {
+    if (!e || max_launches == 0) return GSX_EINVAL;
+    while (e->tev.size() < 2 * (size_t)max_launches) {
+        hipEvent_t ev;
+        HIPCHK(e, hipEventCreate(&ev));
+        e->tev.push_back(ev);
+    }
+    e->t_max = max_launches;
+    e->t_used = 0;
+    e->t_active = true;
+    return GSX_OK;
+}
+
+int gsx_timing_end(gsx_engine* e, double* total_ms, double* min_ms, double* max_ms, uint32_t* n) {
+    if (!e || !total_ms || !n) return GSX_EINVAL;
+    if (!e->t_active) return fail(e, GSX_ESTATE, "gsx_timing_begin not called");
+    e->t_active = false;
+    double sum = 0, lo = 0, hi = 0;
+    for (uint32_t i = 0; i < e->t_used; ++i) {
+        HIPCHK(e, hipEventSynchronize(e->tev[2 * i + 1]));
+        float ms = 0;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->tev[2 * i], e->tev[2 * i + 1]));
+        sum += ms;
+        lo = i == 0 ? ms : std::min(lo, (double)ms);
+        hi = i == 0 ? ms : std::max(hi, (double)ms);
+    }
+    *total_ms = sum;
+    *n = e->t_used;
+    if (min_ms) *min_ms = lo;
+    if (max_ms) *max_ms = hi;
+    return GSX_OK;
+}
+
+int gsx_scores(gsx_engine* e, double* out, size_t n) {
+    if (!e || (n && !out)) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (n != e->E) return fail(e, GSX_EINVAL, "score buffer size != pairs");
+    if (int rc = ensure_scores(e)) return rc;
+    HIPCHK(e, hipMemcpyAsync(out, e->d_score, sizeof(double) * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+// Score(p), score.go:247-256
+int gsx_score(gsx_engine* e, uint64_t pair, double* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (int rc = check_pair(e, pair)) return rc;
+    if (int rc = ensure_scores(e)) return rc;
+    HIPCHK(e, hipMemcpyAsync(out, e->d_score + pair, sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_device_scores(gsx_engine* e, const double** dptr) {
+    if (!e || !dptr) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = ensure_scores(e)) return rc;
+    *dptr = e->d_score;
+    return GSX_OK;
+}
+
+int gsx_sync(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = flush(e)) return rc;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
+    if (!e || !s) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (!s->first_message_deliveries || !s->mesh_message_deliveries || !s->mesh_failure_penalty ||
+        !s->invalid_message_deliveries || !s->graft_time_ns || !s->mesh_time_ns || !s->rec_flags ||
+        !s->pair_flags || !s->expire_ns || !s->behaviour_penalty)
+        return fail(e, GSX_EINVAL, "import needs every state array");
+    if (int rc = flush(e)) return rc;
+    const size_t E = e->E;
+    for (uint32_t t = 0; t < e->T; ++t) {
+        const size_t src = (size_t)t * E, dst = (size_t)t * e->rs;
+        HIPCHK(e, hipMemcpyAsync(e->d_fmd + dst, s->first_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_mmd + dst, s->mesh_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_mfp + dst, s->mesh_failure_penalty + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_imd + dst, s->invalid_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_graft + dst, s->graft_time_ns + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_mtime + dst, s->mesh_time_ns + src, 8 * E, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_rflags + dst, s->rec_flags + src, E, hipMemcpyHostToDevice, e->stream));
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_pflags, s->pair_flags, E, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_expire, s->expire_ns, 8 * E, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_bp, s->behaviour_penalty, 8 * E, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, gsx::launch_rebuild_ipcount(dev_state(e), e->n_groups, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
+    if (!e || !sp) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = flush(e)) return rc;
+    gsx::DevSynthSpec d{};
+    d.seed = sp->seed;
+    d.now = sp->now_ns;
+    d.fmd_max = sp->fmd_max;
+    d.mmd_max = sp->mmd_max;
+    d.mfp_max = sp->mfp_max;
+    d.imd_max = sp->imd_max_sybil;
+    d.p_in_mesh = sp->p_in_mesh;
+    d.graft_window = sp->graft_window_ns;
+    d.bp_max = sp->bp_max;
+    d.p_disc = sp->p_disconnected;
+    d.p_abs = sp->p_absent;
+    d.expire_jitter = sp->expire_jitter_ns;
+    d.sybil_first = sp->sybil_first_node;
+    const gsx::DevState s = dev_state(e);
+    HIPCHK(e, gsx::launch_synthesize(s, e->d_col, d, e->stream));
+    HIPCHK(e, gsx::launch_rebuild_ipcount(s, e->n_groups, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int gsx_export_state(gsx_engine* e, const gsx_state_view* s) {
+    if (!e || !s) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = flush(e)) return rc;
+    const size_t E = e->E;
+    for (uint32_t t = 0; t < e->T; ++t) {
+        const size_t dst = (size_t)t * E, src = (size_t)t * e->rs;
+        if (s->first_message_deliveries)
+            HIPCHK(e, hipMemcpyAsync(s->first_message_deliveries + dst, e->d_fmd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->mesh_message_deliveries)
+            HIPCHK(e, hipMemcpyAsync(s->mesh_message_deliveries + dst, e->d_mmd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->mesh_failure_penalty)
+            HIPCHK(e, hipMemcpyAsync(s->mesh_failure_penalty + dst, e->d_mfp + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->invalid_message_deliveries)
+            HIPCHK(e, hipMemcpyAsync(s->invalid_message_deliveries + dst, e->d_imd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->graft_time_ns)
+            HIPCHK(e, hipMemcpyAsync(s->graft_time_ns + dst, e->d_graft + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->mesh_time_ns)
+            HIPCHK(e, hipMemcpyAsync(s->mesh_time_ns + dst, e->d_mtime + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        if (s->rec_flags)
+            HIPCHK(e, hipMemcpyAsync(s->rec_flags + dst, e->d_rflags + src, E, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (s->pair_flags) HIPCHK(e, hipMemcpyAsync(s->pair_flags, e->d_pflags, E, hipMemcpyDeviceToHost, e->stream));
+    if (s->expire_ns) HIPCHK(e, hipMemcpyAsync(s->expire_ns, e->d_expire, 8 * E, hipMemcpyDeviceToHost, e->stream));
+    if (s->behaviour_penalty) HIPCHK(e, hipMemcpyAsync(s->behaviour_penalty, e->d_bp, 8 * E, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+}  // extern "C"

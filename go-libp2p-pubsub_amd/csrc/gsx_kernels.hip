@@ -1,0 +1,423 @@
+// gsx_kernels.hip — CDNA4 (gfx950) kernels of the GossipSub scoring engine.
+//
+// Hot path: k_refresh_score, one streaming pass that fuses refreshScores()
+// (score.go:497-558) with score() (score.go:258-335) for every
+// (observer, peer) pair.  HBM-bound integer/FP64 byte work: no MFMA, no LDS;
+// what matters is that every load and store of a wave is one coalesced
+// contiguous span (lane l owns consecutive pairs) and that enough loads are in
+// flight per CU.
+//
+// Build with -ffp-contract=off: each expression is evaluated with the
+// reference's roundings (Go on amd64 does not fuse multiply-add), which is what
+// makes the results bit-identical to the CPU oracle.
+#include "gsx_device.h"
+
+namespace gsx {
+
+// ---- shared pieces ---------------------------------------------------------
+
+// P6, ipColocationFactor (score.go:337-381) from the per-(observer, IP) count
+// of present pairs (the size of ps.peerIPs[ip]).
+__device__ __forceinline__ double ip_colocation(const DevState& s, const DevPeerParams& pp, uint64_t p) {
+    const uint2 g = reinterpret_cast<const uint2*>(s.ipg)[p];
+    double result = 0.0;
+    const uint32_t gs[2] = {g.x, g.y};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t id = gs[k];
+        if (id == IPG_NONE || (id & IPG_WL)) continue;  // no IP / whitelisted (:346-367)
+        const int64_t peers_in_ip = (int64_t)s.ipcount[id];
+        if (peers_in_ip > pp.thr6) {
+            const double surpluss = (double)(peers_in_ip - pp.thr6);
+            result += surpluss * surpluss;
+        }
+    }
+    return result;
+}
+
+// The per-pair tail of score(): topic cap, P5, P6, P7 (score.go:315-332).
+__device__ __forceinline__ double score_tail(const DevState& s, const DevPeerParams& pp, uint64_t p, double score,
+                                             double bp) {
+    if (pp.topic_score_cap > 0 && score > pp.topic_score_cap) score = pp.topic_score_cap;
+    const double p5 = s.app[p];
+    score += p5 * pp.w5;
+    // With w6 == 0 the term is +-0 and score (never -0) is unchanged: skip the gather.
+    if (pp.w6 != 0.0) {
+        const double p6 = ip_colocation(s, pp, p);
+        score += p6 * pp.w6;
+    }
+    if (bp > pp.thr7) {
+        const double excess = bp - pp.thr7;
+        const double p7 = excess * excess;
+        score += p7 * pp.w7;
+    }
+    return score;
+}
+
+// One topic's contribution, score.go:276-311.
+__device__ __forceinline__ double topic_score(const DevTopicParams& tp, uint8_t fl, int64_t mesh_time, double fmd,
+                                              double mmd, double mfp, double imd) {
+    double ts = 0.0;
+    if (fl & REC_IN_MESH) {  // P1, integer Duration division (:280)
+        double p1 = (double)(mesh_time / tp.q1);
+        if (p1 > tp.cap1) p1 = tp.cap1;
+        ts += p1 * tp.w1;
+    }
+    const double p2 = fmd;  // P2
+    ts += p2 * tp.w2;
+    if (fl & REC_ACTIVE) {  // P3
+        if (mmd < tp.thr3) {
+            const double deficit = tp.thr3 - mmd;
+            const double p3 = deficit * deficit;
+            ts += p3 * tp.w3;
+        }
+    }
+    const double p3b = mfp;  // P3b
+    ts += p3b * tp.w3b;
+    const double p4 = (imd * imd);  // P4
+    ts += p4 * tp.w4;
+    return ts * tp.topic_weight;
+}
+
+// score(p) from the stored state, no refresh (used by RemovePeer).
+template <int TT>
+__device__ double eval_pair(const DevState& s, const DevPeerParams& pp, uint64_t p) {
+    if (!(s.pflags[p] & PAIR_PRESENT)) return 0.0;
+    const int T = TT > 0 ? TT : (int)s.n_topics;
+    double score = 0.0;
+    for (int t = 0; t < T; ++t) {
+        const DevTopicParams& tp = s.tp[t];
+        if (!tp.scored) continue;
+        const size_t r = (size_t)t * s.rs + p;
+        const uint8_t fl = s.rflags[r];
+        const int64_t mt = (fl & REC_IN_MESH) ? s.mtime[r] : 0;
+        score += topic_score(tp, fl, mt, s.fmd[r], s.mmd[r], s.mfp[r], s.imd[r]);
+    }
+    return score_tail(s, pp, p, score, s.bp[p]);
+}
+
+// ---- hot path: fused refresh + score ---------------------------------------
+
+// x *= decay; x = 0 if x < DecayToZero   (score.go:527-542, 553-556)
+__device__ __forceinline__ double decay(double x, double d, double dtz) {
+    x *= d;
+    return x < dtz ? 0.0 : x;
+}
+
+template <int TT, bool REFRESH>
+__global__ __launch_bounds__(256) void k_refresh_score(DevState s, DevPeerParams pp, int64_t now) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs) return;
+    const uint8_t st = s.pflags[p];
+    if (!(st & PAIR_PRESENT)) {  // no peerStats: Score() returns 0 (:259-262)
+        s.score[p] = 0.0;
+        return;
+    }
+    // Disconnected (retained) peers are not decayed (:503-516).
+    const bool conn = REFRESH && (st & PAIR_CONNECTED);
+    const int T = TT > 0 ? TT : (int)s.n_topics;
+    double score = 0.0;
+    for (int t = 0; t < T; ++t) {  // constant trip count for TT > 0: fully unrolled
+        const DevTopicParams& tp = s.tp[t];
+        if (!tp.scored) continue;
+        const size_t r = (size_t)t * s.rs + p;
+        double fmd = s.fmd[r];
+        double mmd = s.mmd[r];
+        double mfp = s.mfp[r];
+        double imd = s.imd[r];
+        uint8_t fl = s.rflags[r];
+        int64_t mt = 0;
+        if (conn) {
+            fmd = decay(fmd, tp.d2, pp.decay_to_zero);
+            mmd = decay(mmd, tp.d3, pp.decay_to_zero);
+            mfp = decay(mfp, tp.d3b, pp.decay_to_zero);
+            imd = decay(imd, tp.d4, pp.decay_to_zero);
+            s.fmd[r] = fmd;
+            s.mmd[r] = mmd;
+            s.mfp[r] = mfp;
+            s.imd[r] = imd;
+            if (fl & REC_IN_MESH) {  // :544-549
+                mt = now - s.graft[r];
+                if (mt > tp.act3) fl |= REC_ACTIVE;
+                s.mtime[r] = mt;
+                s.rflags[r] = fl;
+            }
+        } else if (fl & REC_IN_MESH) {
+            mt = s.mtime[r];
+        }
+        score += topic_score(tp, fl, mt, fmd, mmd, mfp, imd);
+    }
+    double bp = s.bp[p];
+    if (conn) {
+        bp = decay(bp, pp.d7, pp.decay_to_zero);
+        s.bp[p] = bp;
+    }
+    s.score[p] = score_tail(s, pp, p, score, bp);
+}
+
+// refreshScores' purge of expired retained peers (score.go:503-515).  Runs
+// before k_refresh_score so that the P6 counts it reads are post-purge.
+__global__ __launch_bounds__(256) void k_purge(DevState s, int64_t now) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs) return;
+    const uint8_t st = s.pflags[p];
+    if ((st & (PAIR_PRESENT | PAIR_CONNECTED)) != PAIR_PRESENT) return;
+    if (!(now > s.expire[p])) return;  // now.After(pstats.expire)
+    s.pflags[p] = 0;                   // delete(ps.peerStats, p)
+    const uint2 g = reinterpret_cast<const uint2*>(s.ipg)[p];
+    if (g.x != IPG_NONE) atomicSub(&s.ipcount[g.x & ~IPG_WL], 1u);  // removeIPs
+    if (g.y != IPG_NONE && g.y != g.x) atomicSub(&s.ipcount[g.y & ~IPG_WL], 1u);
+}
+
+// ---- tracer events (score.go:588-974), one thread per observer ------------
+
+__device__ __forceinline__ void ipcount_add(const DevState& s, uint64_t p, int delta) {
+    const uint2 g = reinterpret_cast<const uint2*>(s.ipg)[p];
+    if (g.x != IPG_NONE) s.ipcount[g.x & ~IPG_WL] += (uint32_t)delta;
+    if (g.y != IPG_NONE && g.y != g.x) s.ipcount[g.y & ~IPG_WL] += (uint32_t)delta;
+}
+
+__device__ void ev_add_peer(const DevState& s, uint64_t p) {  // AddPeer :588-602
+    const uint8_t st = s.pflags[p];
+    if (!(st & PAIR_PRESENT)) {  // new peerStats{topics: {}}
+        for (uint32_t t = 0; t < s.n_topics; ++t) {
+            const size_t r = (size_t)t * s.rs + p;
+            s.fmd[r] = 0.0;
+            s.mmd[r] = 0.0;
+            s.mfp[r] = 0.0;
+            s.imd[r] = 0.0;
+            s.graft[r] = 0;
+            s.mtime[r] = 0;
+            s.rflags[r] = 0;
+        }
+        s.bp[p] = 0.0;
+        s.expire[p] = 0;
+        ipcount_add(s, p, +1);  // setIPs
+    }
+    s.pflags[p] = PAIR_PRESENT | PAIR_CONNECTED;
+}
+
+__device__ void ev_remove_peer(const DevState& s, const DevPeerParams& pp, uint64_t p, int64_t now) {  // :604-637
+    const uint8_t st = s.pflags[p];
+    if (!(st & PAIR_PRESENT)) return;
+    if (eval_pair<0>(s, pp, p) > 0) {  // positive score: forget the peer
+        ipcount_add(s, p, -1);
+        s.pflags[p] = 0;
+        return;
+    }
+    for (uint32_t t = 0; t < s.n_topics; ++t) {
+        const DevTopicParams& tp = s.tp[t];
+        if (!tp.scored) continue;
+        const size_t r = (size_t)t * s.rs + p;
+        s.fmd[r] = 0.0;
+        uint8_t fl = s.rflags[r];
+        const double threshold = tp.thr3;
+        const double mmd = s.mmd[r];
+        if ((fl & REC_IN_MESH) && (fl & REC_ACTIVE) && mmd < threshold) {
+            const double deficit = threshold - mmd;
+            s.mfp[r] = s.mfp[r] + deficit * deficit;
+        }
+        s.rflags[r] = fl & ~REC_IN_MESH;
+    }
+    s.pflags[p] = PAIR_PRESENT;
+    s.expire[p] = now + pp.retain_ns;
+}
+
+__device__ void ev_graft(const DevState& s, uint64_t p, uint32_t topic, int64_t now) {  // :642-660
+    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    const size_t r = (size_t)topic * s.rs + p;
+    s.rflags[r] = REC_IN_MESH;
+    s.graft[r] = now;
+    s.mtime[r] = 0;
+}
+
+__device__ void ev_prune(const DevState& s, uint64_t p, uint32_t topic) {  // :662-684
+    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    const size_t r = (size_t)topic * s.rs + p;
+    const uint8_t fl = s.rflags[r];
+    const double threshold = s.tp[topic].thr3;
+    const double mmd = s.mmd[r];
+    if ((fl & REC_ACTIVE) && mmd < threshold) {
+        const double deficit = threshold - mmd;
+        s.mfp[r] = s.mfp[r] + deficit * deficit;
+    }
+    s.rflags[r] = fl & ~REC_IN_MESH;
+}
+
+__device__ void ev_first(const DevState& s, uint64_t p, uint32_t topic) {  // :912-939
+    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    const DevTopicParams& tp = s.tp[topic];
+    const size_t r = (size_t)topic * s.rs + p;
+    double f = s.fmd[r] + 1;
+    if (f > tp.cap2) f = tp.cap2;
+    s.fmd[r] = f;
+    if (!(s.rflags[r] & REC_IN_MESH)) return;
+    double m = s.mmd[r] + 1;
+    if (m > tp.cap3) m = tp.cap3;
+    s.mmd[r] = m;
+}
+
+__device__ void ev_mesh(const DevState& s, uint64_t p, uint32_t topic) {  // :944-974 (window checked on host)
+    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    const size_t r = (size_t)topic * s.rs + p;
+    if (!(s.rflags[r] & REC_IN_MESH)) return;
+    double m = s.mmd[r] + 1;
+    if (m > s.tp[topic].cap3) m = s.tp[topic].cap3;
+    s.mmd[r] = m;
+}
+
+__device__ void ev_invalid(const DevState& s, uint64_t p, uint32_t topic) {  // :894-907
+    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    const size_t r = (size_t)topic * s.rs + p;
+    s.imd[r] = s.imd[r] + 1;
+}
+
+__device__ void ev_penalty(const DevState& s, uint64_t p, int64_t count) {  // AddPenalty :384-398
+    if (!(s.pflags[p] & PAIR_PRESENT)) return;
+    s.bp[p] = s.bp[p] + (double)count;
+}
+
+// Events are grouped by observer (all state an event touches belongs to its
+// observer, so groups are independent); within a group they run in the order
+// the caller issued them.
+__global__ __launch_bounds__(64) void k_apply_events(DevState s, DevPeerParams pp, const DevEvent* __restrict__ ev,
+                                                     const uint32_t* __restrict__ group_off, uint32_t n_groups) {
+    const uint32_t g = blockIdx.x * 64u + threadIdx.x;
+    if (g >= n_groups) return;
+    for (uint32_t i = group_off[g]; i < group_off[g + 1]; ++i) {
+        const DevEvent e = ev[i];
+        switch (e.kind) {
+        case 1: ev_add_peer(s, e.pair); break;
+        case 2: ev_remove_peer(s, pp, e.pair, e.now_ns); break;
+        case 3: ev_graft(s, e.pair, e.topic, e.now_ns); break;
+        case 4: ev_prune(s, e.pair, e.topic); break;
+        case 5: ev_first(s, e.pair, e.topic); break;
+        case 6: ev_mesh(s, e.pair, e.topic); break;
+        case 7: ev_invalid(s, e.pair, e.topic); break;
+        case 8: ev_penalty(s, e.pair, e.arg); break;
+        default: break;
+        }
+    }
+}
+
+// SetTopicScoreParams recap (score.go:217-231)
+__global__ __launch_bounds__(256) void k_recap(DevState s, uint32_t topic, double cap2, double cap3) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs || !(s.pflags[p] & PAIR_PRESENT)) return;
+    const size_t r = (size_t)topic * s.rs + p;
+    if (s.fmd[r] > cap2) s.fmd[r] = cap2;
+    if (s.mmd[r] > cap3) s.mmd[r] = cap3;
+}
+
+__global__ __launch_bounds__(256) void k_rebuild_ipcount(DevState s) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs || !(s.pflags[p] & PAIR_PRESENT)) return;
+    const uint2 g = reinterpret_cast<const uint2*>(s.ipg)[p];
+    if (g.x != IPG_NONE) atomicAdd(&s.ipcount[g.x & ~IPG_WL], 1u);
+    if (g.y != IPG_NONE && g.y != g.x) atomicAdd(&s.ipcount[g.y & ~IPG_WL], 1u);
+}
+
+// ---- seeded synthetic state (gsx/synth.py restated on the device) ------------
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // SplitMix64 finaliser
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ double unif(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
+    const uint64_t inner = mix64(tag ^ mix64(a ^ mix64(b)));
+    const uint64_t x = mix64(seed + 0x9E3779B97F4A7C15ull * (1ull + inner));
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0);
+}
+
+constexpr uint64_t TAG_STATE = 4;
+
+__global__ __launch_bounds__(256) void k_synth_records(DevState s, const int32_t* __restrict__ col, DevSynthSpec sp) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t t = blockIdx.y;
+    if (p >= s.n_pairs) return;
+    const uint64_t a = (uint64_t)t * s.n_pairs + p;
+    const size_t r = (size_t)t * s.rs + p;
+    s.fmd[r] = unif(sp.seed, TAG_STATE, a, 1) * sp.fmd_max;
+    s.mmd[r] = unif(sp.seed, TAG_STATE, a, 2) * sp.mmd_max;
+    s.mfp[r] = unif(sp.seed, TAG_STATE, a, 3) * sp.mfp_max;
+    const double u4 = unif(sp.seed, TAG_STATE, a, 4) * sp.imd_max;
+    s.imd[r] = ((uint32_t)col[p] >= sp.sybil_first) ? u4 : 0.0;
+    const bool in_mesh = unif(sp.seed, TAG_STATE, a, 5) < sp.p_in_mesh;
+    const int64_t graft = sp.now - (int64_t)(unif(sp.seed, TAG_STATE, a, 6) * (double)sp.graft_window);
+    s.graft[r] = graft;
+    s.mtime[r] = in_mesh ? sp.now - graft : 0;
+    s.rflags[r] = in_mesh ? REC_IN_MESH : 0;
+}
+
+__global__ __launch_bounds__(256) void k_synth_pairs(DevState s, DevSynthSpec sp) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs) return;
+    uint8_t pf = PAIR_PRESENT | PAIR_CONNECTED;
+    if (sp.p_disc > 0 && unif(sp.seed, TAG_STATE, p, 7) < sp.p_disc) pf = PAIR_PRESENT;
+    if (sp.p_abs > 0 && unif(sp.seed, TAG_STATE, p, 8) < sp.p_abs) pf = 0;
+    s.pflags[p] = pf;
+    s.expire[p] = sp.now + (int64_t)((unif(sp.seed, TAG_STATE, p, 9) - 0.5) * (double)sp.expire_jitter);
+    s.bp[p] = unif(sp.seed, TAG_STATE, p, 10) * sp.bp_max;
+}
+
+// ---- launchers -------------------------------------------------------------
+
+hipError_t launch_synthesize(const DevState& s, const int32_t* col, const DevSynthSpec& spec, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    const unsigned nb = (unsigned)((s.n_pairs + 255) / 256);
+    hipLaunchKernelGGL(k_synth_records, dim3(nb, s.n_topics), dim3(256), 0, st, s, col, spec);
+    hipLaunchKernelGGL(k_synth_pairs, dim3(nb), dim3(256), 0, st, s, spec);
+    return hipGetLastError();
+}
+
+static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_purge, dim3(blocks_for(s.n_pairs, 256)), dim3(256), 0, st, s, now);
+    return hipGetLastError();
+}
+
+template <bool R>
+static hipError_t launch_rs(const DevState& s, const DevPeerParams& pp, int64_t now, hipStream_t st) {
+    const dim3 grid(blocks_for(s.n_pairs, 256)), block(256);
+    switch (s.n_topics) {
+    case 1: hipLaunchKernelGGL((k_refresh_score<1, R>), grid, block, 0, st, s, pp, now); break;
+    case 2: hipLaunchKernelGGL((k_refresh_score<2, R>), grid, block, 0, st, s, pp, now); break;
+    case 4: hipLaunchKernelGGL((k_refresh_score<4, R>), grid, block, 0, st, s, pp, now); break;
+    case 8: hipLaunchKernelGGL((k_refresh_score<8, R>), grid, block, 0, st, s, pp, now); break;
+    default: hipLaunchKernelGGL((k_refresh_score<0, R>), grid, block, 0, st, s, pp, now); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_refresh_score(const DevState& s, const DevPeerParams& pp, int64_t now, bool refresh,
+                                hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    return refresh ? launch_rs<true>(s, pp, now, st) : launch_rs<false>(s, pp, now, st);
+}
+
+hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
+                               const uint32_t* group_off, uint32_t n_groups, hipStream_t st) {
+    if (n_groups == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_events, dim3(blocks_for(n_groups, 64)), dim3(64), 0, st, s, pp, ev, group_off,
+                       n_groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_recap, dim3(blocks_for(s.n_pairs, 256)), dim3(256), 0, st, s, topic, cap2, cap3);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebuild_ipcount(const DevState& s, uint32_t n_groups_ip, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(s.ipcount, 0, sizeof(uint32_t) * (n_groups_ip ? n_groups_ip : 1), st);
+    if (e != hipSuccess || s.n_pairs == 0) return e;
+    hipLaunchKernelGGL(k_rebuild_ipcount, dim3(blocks_for(s.n_pairs, 256)), dim3(256), 0, st, s);
+    return hipGetLastError();
+}
+
+}  // namespace gsx

@@ -1,0 +1,273 @@
+"""ctypes mirror of include/gsx.h (types and the shared-library handle).
+
+The structures here are byte-for-byte the C structs of the boundary; the
+engine itself is libgsx.so (HIP, gfx950).  Loading fails loudly when the
+library is missing: there is no Python or CPU fallback for the engine.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgsx.so")
+
+GSX_OK = 0
+GSX_EINVAL = -22
+GSX_ENOMEM = -12
+GSX_ENODEV = -19
+GSX_ERANGE = -34
+GSX_ESTATE = -71
+GSX_EDEVICE = -5
+
+GSX_MAX_TOPICS = 64
+GSX_NO_IP = 0xFFFFFFFF
+
+GSX_EDGE_OUTBOUND = 0x01
+GSX_EDGE_DIRECT = 0x02
+GSX_EDGE_GOSSIPSUB = 0x04
+GSX_EDGE_FLOODSUB = 0x08
+
+GSX_REC_IN_MESH = 0x01
+GSX_REC_ACTIVE = 0x02
+GSX_PAIR_PRESENT = 0x01
+GSX_PAIR_CONNECTED = 0x02
+
+# gsx_event_kind
+EV_ADD_PEER = 1
+EV_REMOVE_PEER = 2
+EV_GRAFT = 3
+EV_PRUNE = 4
+EV_FIRST_DELIVERY = 5
+EV_MESH_DELIVERY = 6
+EV_INVALID_DELIVERY = 7
+EV_PENALTY = 8
+
+# gsx_reject_reason, with the reference's strings (tracer.go:28-38)
+REJECT_REASONS = {
+    "blacklisted peer": 0,
+    "blacklisted source": 1,
+    "missing signature": 2,
+    "unexpected signature": 3,
+    "unexpected auth info": 4,
+    "invalid signature": 5,
+    "validation queue full": 6,
+    "validation throttled": 7,
+    "validation failed": 8,
+    "validation ignored": 9,
+    "self originated message": 10,
+}
+
+SECOND = 1_000_000_000
+MILLISECOND = 1_000_000
+MINUTE = 60 * SECOND
+HOUR = 60 * MINUTE
+
+
+class TopicScoreParams(C.Structure):
+    """TopicScoreParams, score_params.go:98-148 (durations in ns)."""
+
+    _fields_ = [
+        ("topic_weight", C.c_double),
+        ("time_in_mesh_weight", C.c_double),
+        ("time_in_mesh_quantum_ns", C.c_int64),
+        ("time_in_mesh_cap", C.c_double),
+        ("first_message_deliveries_weight", C.c_double),
+        ("first_message_deliveries_decay", C.c_double),
+        ("first_message_deliveries_cap", C.c_double),
+        ("mesh_message_deliveries_weight", C.c_double),
+        ("mesh_message_deliveries_decay", C.c_double),
+        ("mesh_message_deliveries_cap", C.c_double),
+        ("mesh_message_deliveries_threshold", C.c_double),
+        ("mesh_message_deliveries_window_ns", C.c_int64),
+        ("mesh_message_deliveries_activation_ns", C.c_int64),
+        ("mesh_failure_penalty_weight", C.c_double),
+        ("mesh_failure_penalty_decay", C.c_double),
+        ("invalid_message_deliveries_weight", C.c_double),
+        ("invalid_message_deliveries_decay", C.c_double),
+    ]
+
+
+class PeerScoreParams(C.Structure):
+    """PeerScoreParams, score_params.go:53-96 minus Topics/closure/whitelist."""
+
+    _fields_ = [
+        ("topic_score_cap", C.c_double),
+        ("app_specific_weight", C.c_double),
+        ("app_specific_score_set", C.c_int32),
+        ("ip_colocation_factor_threshold", C.c_int32),
+        ("ip_colocation_factor_weight", C.c_double),
+        ("behaviour_penalty_weight", C.c_double),
+        ("behaviour_penalty_threshold", C.c_double),
+        ("behaviour_penalty_decay", C.c_double),
+        ("decay_interval_ns", C.c_int64),
+        ("decay_to_zero", C.c_double),
+        ("retain_score_ns", C.c_int64),
+    ]
+
+
+class Thresholds(C.Structure):
+    """PeerScoreThresholds, score_params.go:12-32."""
+
+    _fields_ = [
+        ("gossip_threshold", C.c_double),
+        ("publish_threshold", C.c_double),
+        ("graylist_threshold", C.c_double),
+        ("accept_px_threshold", C.c_double),
+        ("opportunistic_graft_threshold", C.c_double),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("device", C.c_int32), ("reserved", C.c_uint32 * 6)]
+
+
+class Event(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("topic", C.c_uint32),
+        ("pair", C.c_uint64),
+        ("now_ns", C.c_int64),
+        ("arg", C.c_int64),
+    ]
+
+
+EVENT_DTYPE = None  # numpy dtype matching Event, built lazily
+
+
+def event_dtype():
+    global EVENT_DTYPE
+    if EVENT_DTYPE is None:
+        import numpy as np
+
+        EVENT_DTYPE = np.dtype(
+            [("kind", "<u4"), ("topic", "<u4"), ("pair", "<u8"), ("now_ns", "<i8"), ("arg", "<i8")], align=True
+        )
+        assert EVENT_DTYPE.itemsize == C.sizeof(Event)
+    return EVENT_DTYPE
+
+
+class StateView(C.Structure):
+    _fields_ = [
+        ("first_message_deliveries", C.POINTER(C.c_double)),
+        ("mesh_message_deliveries", C.POINTER(C.c_double)),
+        ("mesh_failure_penalty", C.POINTER(C.c_double)),
+        ("invalid_message_deliveries", C.POINTER(C.c_double)),
+        ("graft_time_ns", C.POINTER(C.c_int64)),
+        ("mesh_time_ns", C.POINTER(C.c_int64)),
+        ("rec_flags", C.POINTER(C.c_uint8)),
+        ("pair_flags", C.POINTER(C.c_uint8)),
+        ("expire_ns", C.POINTER(C.c_int64)),
+        ("behaviour_penalty", C.POINTER(C.c_double)),
+    ]
+
+
+STATE_FIELDS = [f for f, _ in StateView._fields_]
+RECORD_FIELDS = STATE_FIELDS[:7]
+PAIR_FIELDS = STATE_FIELDS[7:]
+STATE_DTYPES = {
+    "first_message_deliveries": "<f8",
+    "mesh_message_deliveries": "<f8",
+    "mesh_failure_penalty": "<f8",
+    "invalid_message_deliveries": "<f8",
+    "graft_time_ns": "<i8",
+    "mesh_time_ns": "<i8",
+    "rec_flags": "u1",
+    "pair_flags": "u1",
+    "expire_ns": "<i8",
+    "behaviour_penalty": "<f8",
+}
+
+class SynthSpec(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("now_ns", C.c_int64),
+        ("fmd_max", C.c_double),
+        ("mmd_max", C.c_double),
+        ("mfp_max", C.c_double),
+        ("imd_max_sybil", C.c_double),
+        ("p_in_mesh", C.c_double),
+        ("graft_window_ns", C.c_int64),
+        ("bp_max", C.c_double),
+        ("p_disconnected", C.c_double),
+        ("p_absent", C.c_double),
+        ("expire_jitter_ns", C.c_int64),
+        ("sybil_first_node", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+P = C.POINTER
+_u64p = P(C.c_uint64)
+
+# Every entry point of include/gsx.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "gsx_abi_version": (C.c_int, []),
+    "gsx_validate_peer_params": (C.c_int, [P(PeerScoreParams)]),
+    "gsx_validate_topic_params": (C.c_int, [P(TopicScoreParams)]),
+    "gsx_validate_thresholds": (C.c_int, [P(Thresholds)]),
+    "gsx_score_parameter_decay_with_base": (C.c_double, [C.c_int64, C.c_int64, C.c_double]),
+    "gsx_score_parameter_decay": (C.c_double, [C.c_int64]),
+    "gsx_create": (C.c_int, [P(Config), P(C.c_void_p)]),
+    "gsx_destroy": (C.c_int, [C.c_void_p]),
+    "gsx_last_error": (C.c_char_p, [C.c_void_p]),
+    "gsx_set_peer_params": (C.c_int, [C.c_void_p, P(PeerScoreParams)]),
+    "gsx_set_thresholds": (C.c_int, [C.c_void_p, P(Thresholds)]),
+    "gsx_set_topic_params": (C.c_int, [C.c_void_p, C.c_uint32, P(TopicScoreParams)]),
+    "gsx_load_overlay": (
+        C.c_int,
+        [C.c_void_p, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint8), P(C.c_uint32)],
+    ),
+    "gsx_num_pairs": (C.c_int, [C.c_void_p, _u64p]),
+    "gsx_set_ip_whitelist": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t]),
+    "gsx_set_app_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
+    "gsx_apply_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "gsx_flush": (C.c_int, [C.c_void_p]),
+    "gsx_trace_validate": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int64]),
+    "gsx_trace_deliver": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int64]),
+    "gsx_trace_reject": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int32, C.c_int64]),
+    "gsx_trace_duplicate": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int64]),
+    "gsx_gc_deliveries": (C.c_int, [C.c_void_p, C.c_int64]),
+    "gsx_num_delivery_records": (C.c_int, [C.c_void_p, _u64p]),
+    "gsx_refresh": (C.c_int, [C.c_void_p, C.c_int64]),
+    "gsx_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
+    "gsx_score": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_double)]),
+    "gsx_device_scores": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
+    "gsx_sync": (C.c_int, [C.c_void_p]),
+    "gsx_import_state": (C.c_int, [C.c_void_p, P(StateView)]),
+    "gsx_export_state": (C.c_int, [C.c_void_p, P(StateView)]),
+    "gsx_last_refresh_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),
+    "gsx_synthesize_state": (C.c_int, [C.c_void_p, P(SynthSpec)]),
+    "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_timing_end": (
+        C.c_int,
+        [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_uint32)],
+    ),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libgsx.so (built by `make -C go-libp2p-pubsub_amd`).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build it with `make -C go-libp2p-pubsub_amd` "
+            "(the engine has no CPU fallback)"
+        )
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class GsxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with {code}")
+        self.code = code

@@ -1,0 +1,203 @@
+"""Python handle on the HIP engine (libgsx.so) through the C ABI of include/gsx.h.
+
+This is plumbing for tests and bench.py: every call goes straight to the
+C ABI; nothing here computes scores.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterable, Optional
+
+import numpy as np
+
+from . import abi
+from .abi import GsxError
+
+
+def _ptr(a: Optional[np.ndarray], ctype):
+    if a is None:
+        return C.cast(None, C.POINTER(ctype))
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+_CTYPES = {"<f8": C.c_double, "<i8": C.c_int64, "u1": C.c_uint8}
+
+
+def make_struct(cls, **kw):
+    s = cls()
+    for k, v in kw.items():
+        if not hasattr(s, k):
+            raise AttributeError(f"{cls.__name__} has no field {k}")
+        setattr(s, k, v)
+    return s
+
+
+class Engine:
+    def __init__(self, n_topics: int, device: int = 0):
+        self.lib = abi.load_library()
+        cfg = abi.Config(n_topics=n_topics, device=device)
+        h = C.c_void_p()
+        rc = self.lib.gsx_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise GsxError(rc, "gsx_create (needs a gfx950 GPU)")
+        self.h = h
+        self.n_topics = n_topics
+        self.n_pairs = 0
+
+    # -- helpers ---------------------------------------------------------------
+    def _chk(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.gsx_last_error(self.h)
+            raise GsxError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gsx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- params ------------------------------------------------------------------
+    def set_peer_params(self, p: abi.PeerScoreParams):
+        self._chk(self.lib.gsx_set_peer_params(self.h, C.byref(p)), "gsx_set_peer_params")
+
+    def set_thresholds(self, t: abi.Thresholds):
+        self._chk(self.lib.gsx_set_thresholds(self.h, C.byref(t)), "gsx_set_thresholds")
+
+    def set_topic_params(self, topic: int, p: abi.TopicScoreParams):
+        self._chk(self.lib.gsx_set_topic_params(self.h, topic, C.byref(p)), "gsx_set_topic_params")
+
+    # -- overlay -------------------------------------------------------------------
+    def load_overlay(self, row_ptr, col, edge_flags=None, node_ips=None):
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        n = len(row_ptr) - 1
+        ef = None if edge_flags is None else np.ascontiguousarray(edge_flags, dtype=np.uint8)
+        ips = None if node_ips is None else np.ascontiguousarray(node_ips, dtype=np.uint32).reshape(-1)
+        self._chk(
+            self.lib.gsx_load_overlay(
+                self.h, n, _ptr(row_ptr, C.c_int64), _ptr(col, C.c_int32), _ptr(ef, C.c_uint8), _ptr(ips, C.c_uint32)
+            ),
+            "gsx_load_overlay",
+        )
+        v = C.c_uint64()
+        self._chk(self.lib.gsx_num_pairs(self.h, C.byref(v)), "gsx_num_pairs")
+        self.n_pairs = int(v.value)
+
+    def set_ip_whitelist(self, ips: Iterable[int]):
+        a = np.ascontiguousarray(list(ips), dtype=np.uint32)
+        self._chk(self.lib.gsx_set_ip_whitelist(self.h, _ptr(a, C.c_uint32), len(a)), "gsx_set_ip_whitelist")
+
+    def set_app_scores(self, app):
+        a = np.ascontiguousarray(app, dtype=np.float64)
+        self._chk(self.lib.gsx_set_app_scores(self.h, _ptr(a, C.c_double), len(a)), "gsx_set_app_scores")
+
+    # -- events ------------------------------------------------------------------
+    def apply_events(self, events):
+        ev = np.ascontiguousarray(events, dtype=abi.event_dtype())
+        self._chk(self.lib.gsx_apply_events(self.h, ev.ctypes.data_as(C.c_void_p), len(ev)), "gsx_apply_events")
+
+    def flush(self):
+        self._chk(self.lib.gsx_flush(self.h), "gsx_flush")
+
+    def trace_validate(self, pair, msg, topic, now):
+        self._chk(self.lib.gsx_trace_validate(self.h, pair, msg, topic, now), "gsx_trace_validate")
+
+    def trace_deliver(self, pair, msg, topic, now):
+        self._chk(self.lib.gsx_trace_deliver(self.h, pair, msg, topic, now), "gsx_trace_deliver")
+
+    def trace_reject(self, pair, msg, topic, reason, now):
+        if isinstance(reason, str):
+            reason = abi.REJECT_REASONS[reason]
+        self._chk(self.lib.gsx_trace_reject(self.h, pair, msg, topic, reason, now), "gsx_trace_reject")
+
+    def trace_duplicate(self, pair, msg, topic, now):
+        self._chk(self.lib.gsx_trace_duplicate(self.h, pair, msg, topic, now), "gsx_trace_duplicate")
+
+    def gc_deliveries(self, now):
+        self._chk(self.lib.gsx_gc_deliveries(self.h, now), "gsx_gc_deliveries")
+
+    def num_delivery_records(self) -> int:
+        v = C.c_uint64()
+        self._chk(self.lib.gsx_num_delivery_records(self.h, C.byref(v)), "gsx_num_delivery_records")
+        return int(v.value)
+
+    # -- refresh / score ---------------------------------------------------------------
+    def refresh(self, now: int):
+        self._chk(self.lib.gsx_refresh(self.h, now), "gsx_refresh")
+
+    def scores(self) -> np.ndarray:
+        out = np.empty(self.n_pairs, dtype=np.float64)
+        self._chk(self.lib.gsx_scores(self.h, _ptr(out, C.c_double), self.n_pairs), "gsx_scores")
+        return out
+
+    def score(self, pair: int) -> float:
+        v = C.c_double()
+        self._chk(self.lib.gsx_score(self.h, pair, C.byref(v)), "gsx_score")
+        return float(v.value)
+
+    def device_scores_ptr(self) -> int:
+        v = C.c_void_p()
+        self._chk(self.lib.gsx_device_scores(self.h, C.byref(v)), "gsx_device_scores")
+        return int(v.value or 0)
+
+    def sync(self):
+        self._chk(self.lib.gsx_sync(self.h), "gsx_sync")
+
+    def last_refresh_ms(self) -> float:
+        v = C.c_float()
+        self._chk(self.lib.gsx_last_refresh_ms(self.h, C.byref(v)), "gsx_last_refresh_ms")
+        return float(v.value)
+
+    def timing_begin(self, max_launches: int):
+        self._chk(self.lib.gsx_timing_begin(self.h, max_launches), "gsx_timing_begin")
+
+    def timing_end(self):
+        """-> (total_ms, min_ms, max_ms, n_launches) of the fused kernel over the region."""
+        tot, lo, hi, n = C.c_double(), C.c_double(), C.c_double(), C.c_uint32()
+        self._chk(
+            self.lib.gsx_timing_end(self.h, C.byref(tot), C.byref(lo), C.byref(hi), C.byref(n)), "gsx_timing_end"
+        )
+        return tot.value, lo.value, hi.value, n.value
+
+    # -- state ---------------------------------------------------------------------------
+    def _view(self, arrays: Dict[str, np.ndarray]) -> abi.StateView:
+        sv = abi.StateView()
+        for f in abi.STATE_FIELDS:
+            a = arrays.get(f)
+            ct = _CTYPES[abi.STATE_DTYPES[f]]
+            setattr(sv, f, _ptr(a, ct))
+        return sv
+
+    def import_state(self, st: Dict[str, np.ndarray]):
+        arrays = {f: np.ascontiguousarray(st[f], dtype=abi.STATE_DTYPES[f]).reshape(-1) for f in abi.STATE_FIELDS}
+        R = self.n_topics * self.n_pairs
+        for f in abi.RECORD_FIELDS:
+            assert arrays[f].size == R, (f, arrays[f].size, R)
+        for f in abi.PAIR_FIELDS:
+            assert arrays[f].size == self.n_pairs, f
+        sv = self._view(arrays)
+        self._chk(self.lib.gsx_import_state(self.h, C.byref(sv)), "gsx_import_state")
+
+    def synthesize_state(self, spec: abi.SynthSpec):
+        self._chk(self.lib.gsx_synthesize_state(self.h, C.byref(spec)), "gsx_synthesize_state")
+
+    def export_state(self) -> Dict[str, np.ndarray]:
+        R = self.n_topics * self.n_pairs
+        out = {}
+        for f in abi.STATE_FIELDS:
+            n = R if f in abi.RECORD_FIELDS else self.n_pairs
+            out[f] = np.empty(n, dtype=abi.STATE_DTYPES[f])
+        sv = self._view(out)
+        self._chk(self.lib.gsx_export_state(self.h, C.byref(sv)), "gsx_export_state")
+        return out

@@ -1,0 +1,329 @@
+/*
+ * gsx.h — C ABI of the MI355X-native GossipSub scoring engine.
+ *
+ * This is the drop-in boundary for the reference's peer-scoring path
+ * (`/root/reference/score.go`, `score_params.go`).  In the reference the scorer
+ * is the concrete type `*peerScore` held by the router (`gossipsub.go:425`) and
+ * reached through `WithPeerScore` (`gossipsub.go:263-304`), `Score()`
+ * (`score.go:247`), `AddPenalty()` (`score.go:384`), `SetTopicScoreParams()`
+ * (`score.go:194`), the RawTracer methods it implements (`score.go:588-830`)
+ * and its background ticker (`score.go:401-438`).  Every entry point below
+ * names the reference function it replaces.
+ *
+ * Model.  One engine holds the state of MANY observers (routers) at once: an
+ * overlay in CSR form, observer i owning the directed "pairs"
+ * row_ptr[i] .. row_ptr[i+1]-1, pair p standing for the reference's
+ * `peerStats` entry that observer keeps for neighbour col[p].  A Go cgo shim
+ * that replaces `score.go` inside one router uses one observer whose pairs
+ * are its peer slots.  Topics are dense indices 0..n_topics-1 (the host maps
+ * topic strings to indices, like `ps.params.Topics[topic]`).
+ *
+ * Conventions.
+ *  - Every function returns 0 on success or a negative errno-style code
+ *    (GSX_E*).  Nothing throws or aborts across the ABI.
+ *  - The caller owns every host buffer; the engine copies to HBM.
+ *  - One engine is externally synchronised (the reference serialises with
+ *    `peerScore`'s own mutex, `score.go:65`).  Work is ordered on the
+ *    engine's HIP stream; gsx_sync() waits for it.
+ *  - Times are int64 nanoseconds on a caller-supplied clock: the reference
+ *    reads `time.Now()` inside the scorer (`score.go:501,636,657,711,839`);
+ *    the engine takes `now_ns` as an argument instead.
+ *  - There is no CPU fallback: without a usable gfx950 device gsx_create
+ *    fails with GSX_ENODEV.
+ */
+#ifndef GSX_H
+#define GSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSX_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define GSX_OK 0
+#define GSX_EINVAL (-22)  /* bad argument / params failed validate()        */
+#define GSX_ENOMEM (-12)  /* host or device allocation failed                */
+#define GSX_ENODEV (-19)  /* no HIP device / kernel image for this device    */
+#define GSX_ERANGE (-34)  /* index out of range                              */
+#define GSX_ESTATE (-71)  /* call out of order (e.g. no overlay loaded)      */
+#define GSX_EDEVICE (-5)  /* HIP runtime error                               */
+
+/* ---- parameters (score_params.go) ---------------------------------------- */
+
+/* TopicScoreParams, score_params.go:98-148.  Durations are nanoseconds. */
+typedef struct gsx_topic_score_params {
+    double topic_weight;
+    /* P1 */
+    double time_in_mesh_weight;
+    int64_t time_in_mesh_quantum_ns;
+    double time_in_mesh_cap;
+    /* P2 */
+    double first_message_deliveries_weight;
+    double first_message_deliveries_decay;
+    double first_message_deliveries_cap;
+    /* P3 */
+    double mesh_message_deliveries_weight;
+    double mesh_message_deliveries_decay;
+    double mesh_message_deliveries_cap;
+    double mesh_message_deliveries_threshold;
+    int64_t mesh_message_deliveries_window_ns;
+    int64_t mesh_message_deliveries_activation_ns;
+    /* P3b */
+    double mesh_failure_penalty_weight;
+    double mesh_failure_penalty_decay;
+    /* P4 */
+    double invalid_message_deliveries_weight;
+    double invalid_message_deliveries_decay;
+} gsx_topic_score_params;
+
+/* PeerScoreParams, score_params.go:53-96, minus the three fields that are not
+ * plain data in Go:
+ *   Topics                      -> gsx_set_topic_params() per topic index
+ *   AppSpecificScore (closure)  -> gsx_set_app_scores() snapshot per pair
+ *   IPColocationFactorWhitelist -> gsx_set_ip_whitelist() per IP id
+ * `app_specific_score_set` mirrors the `AppSpecificScore == nil` check of
+ * validate() (score_params.go:165). */
+typedef struct gsx_peer_score_params {
+    double topic_score_cap;
+    double app_specific_weight;
+    int32_t app_specific_score_set;
+    int32_t ip_colocation_factor_threshold;
+    double ip_colocation_factor_weight;
+    double behaviour_penalty_weight;
+    double behaviour_penalty_threshold;
+    double behaviour_penalty_decay;
+    int64_t decay_interval_ns;
+    double decay_to_zero;
+    int64_t retain_score_ns;
+} gsx_peer_score_params;
+
+/* PeerScoreThresholds, score_params.go:12-32. */
+typedef struct gsx_thresholds {
+    double gossip_threshold;
+    double publish_threshold;
+    double graylist_threshold;
+    double accept_px_threshold;
+    double opportunistic_graft_threshold;
+} gsx_thresholds;
+
+/* validate() twins: PeerScoreParams.validate (score_params.go:151-198, topic
+ * validation is separate), TopicScoreParams.validate (:200-268),
+ * PeerScoreThresholds.validate (:34-51).  Return 0 or GSX_EINVAL. */
+int gsx_validate_peer_params(const gsx_peer_score_params* p);
+int gsx_validate_topic_params(const gsx_topic_score_params* p);
+int gsx_validate_thresholds(const gsx_thresholds* p);
+
+/* ScoreParameterDecayWithBase, score_params.go:282-287 (integer Duration
+ * division, then pow).  ScoreParameterDecay(d) == ..._with_base(d, 1s, 0.01). */
+double gsx_score_parameter_decay_with_base(int64_t decay_ns, int64_t base_ns, double decay_to_zero);
+double gsx_score_parameter_decay(int64_t decay_ns);
+
+/* ---- engine lifecycle ----------------------------------------------------- */
+
+typedef struct gsx_engine gsx_engine;
+
+typedef struct gsx_config {
+    uint32_t n_topics;   /* dense topic indices 0..n_topics-1, <= GSX_MAX_TOPICS */
+    int32_t device;      /* HIP device ordinal                                   */
+    uint32_t reserved[6];
+} gsx_config;
+
+#define GSX_MAX_TOPICS 64
+
+int gsx_create(const gsx_config* cfg, gsx_engine** out);
+int gsx_destroy(gsx_engine* e);
+/* Last HIP / engine error as text (valid until the next call). */
+const char* gsx_last_error(gsx_engine* e);
+int gsx_abi_version(void);
+
+/* newPeerScore(params) / the threshold copy of WithPeerScore
+ * (score.go:180-188, gossipsub.go:282-287).  Like newPeerScore these do NOT
+ * validate: WithPeerScore = gsx_validate_* (gossipsub.go:270-280) followed by
+ * these setters, and the reference's unit tests build scorers from
+ * unvalidated params (e.g. DecayToZero 0). */
+int gsx_set_peer_params(gsx_engine* e, const gsx_peer_score_params* p);
+int gsx_set_thresholds(gsx_engine* e, const gsx_thresholds* t);
+/* SetTopicScoreParams (score.go:194-234): installs params for `topic`; if the
+ * topic was already scored and a delivery cap is lowered, recaps fmd/mmd of
+ * every record of that topic on the device.  Does NOT validate (the reference
+ * notes "assumes that the topic score parameters have already been
+ * validated"); call gsx_validate_topic_params first, as Topic.SetScoreParams
+ * does (topic.go:36-74). */
+int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_params* p);
+
+/* Edge flags, one byte per pair. */
+#define GSX_EDGE_OUTBOUND 0x01u  /* gs.outbound[p] (gossipsub.go:510-537)     */
+#define GSX_EDGE_DIRECT 0x02u    /* gs.direct[p]                               */
+#define GSX_EDGE_GOSSIPSUB 0x04u /* peer speaks a mesh protocol (feature Mesh) */
+#define GSX_EDGE_FLOODSUB 0x08u  /* peer speaks floodsub                       */
+
+#define GSX_NO_IP 0xFFFFFFFFu
+
+/* Overlay in CSR: n_nodes observers; row_ptr[n_nodes+1]; col[row_ptr[n]] are
+ * neighbour node ids (the peer each pair stands for).  edge_flags may be NULL
+ * (all zero).  node_ips[2*n] gives up to two IP ids per node (IPv4, or IPv6
+ * address + /64: score.go:1002-1013), GSX_NO_IP for none; may be NULL.
+ * Every pair starts NOT present (no peerStats), as before AddPeer. */
+int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
+                     const uint8_t* edge_flags, const uint32_t* node_ips);
+int gsx_num_pairs(gsx_engine* e, uint64_t* out_pairs);
+
+/* IPColocationFactorWhitelist (score.go:346-367), resolved on the host to the
+ * list of whitelisted IP ids.  Replaces any previous list. */
+int gsx_set_ip_whitelist(gsx_engine* e, const uint32_t* ip_ids, size_t n);
+
+/* AppSpecificScore snapshot (score.go:320): app[p] for every pair. */
+int gsx_set_app_scores(gsx_engine* e, const double* app, size_t n_pairs);
+
+/* ---- events: the RawTracer calls that mutate counters --------------------- */
+
+enum gsx_event_kind {
+    GSX_EV_ADD_PEER = 1,         /* AddPeer           score.go:588-602                 */
+    GSX_EV_REMOVE_PEER = 2,      /* RemovePeer        score.go:604-637                 */
+    GSX_EV_GRAFT = 3,            /* Graft             score.go:642-660                 */
+    GSX_EV_PRUNE = 4,            /* Prune             score.go:662-684                 */
+    GSX_EV_FIRST_DELIVERY = 5,   /* markFirstMessageDelivery     score.go:912-939      */
+    GSX_EV_MESH_DELIVERY = 6,    /* markDuplicateMessageDelivery score.go:944-974,
+                                    window already checked by the caller               */
+    GSX_EV_INVALID_DELIVERY = 7, /* markInvalidMessageDelivery   score.go:894-907      */
+    GSX_EV_PENALTY = 8           /* AddPenalty(p, arg) score.go:384-398                */
+};
+
+/* 32-byte event record.  `pair` selects (observer, peer); `topic` is used by
+ * GRAFT, PRUNE and the DELIVERY kinds; `arg` is the penalty count for PENALTY. */
+typedef struct gsx_event {
+    uint32_t kind;
+    uint32_t topic;
+    uint64_t pair;
+    int64_t now_ns;
+    int64_t arg;
+} gsx_event;
+
+/* Appends events; they are applied on the device, in the given order per
+ * observer, before the next refresh/score/export call (or at gsx_flush). */
+int gsx_apply_events(gsx_engine* e, const gsx_event* ev, size_t n);
+int gsx_flush(gsx_engine* e);
+
+/* ---- message-level tracer calls (delivery records, score.go:686-870) ----- */
+/* These keep the reference's per-message delivery records (status, validated
+ * time, peers that delivered a duplicate) keyed by (observer, msg_id) on the
+ * host and turn them into the counter events above.  `pair` is the
+ * ReceivedFrom peer as seen by its observer.  Self-published messages must not
+ * be traced (trace.go:98,110,141,171). */
+enum gsx_reject_reason {
+    GSX_REJECT_BLACKLISTED_PEER = 0,   /* "blacklisted peer"        tracer.go:28 */
+    GSX_REJECT_BLACKLISTED_SOURCE = 1, /* "blacklisted source"      tracer.go:29 */
+    GSX_REJECT_MISSING_SIGNATURE = 2,  /* "missing signature"       tracer.go:30 */
+    GSX_REJECT_UNEXPECTED_SIGNATURE = 3,
+    GSX_REJECT_UNEXPECTED_AUTH_INFO = 4,
+    GSX_REJECT_INVALID_SIGNATURE = 5,
+    GSX_REJECT_VALIDATION_QUEUE_FULL = 6,
+    GSX_REJECT_VALIDATION_THROTTLED = 7,
+    GSX_REJECT_VALIDATION_FAILED = 8,
+    GSX_REJECT_VALIDATION_IGNORED = 9,
+    GSX_REJECT_SELF_ORIGIN = 10        /* "self originated message" tracer.go:38 */
+};
+
+int gsx_trace_validate(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+int gsx_trace_deliver(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+int gsx_trace_reject(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int32_t reason,
+                     int64_t now_ns);
+int gsx_trace_duplicate(gsx_engine* e, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+/* messageDeliveries.gc (score.go:856-870): drop records with expire < now. */
+int gsx_gc_deliveries(gsx_engine* e, int64_t now_ns);
+int gsx_num_delivery_records(gsx_engine* e, uint64_t* out);
+
+/* ---- refresh and evaluation ----------------------------------------------- */
+
+/* refreshScores (score.go:497-558): purge expired retained pairs, decay every
+ * connected pair's counters, update meshTime / activation, decay P7 — fused on
+ * the device with the evaluation of score() (score.go:258-335) for every
+ * pair, whose result stays in HBM. */
+int gsx_refresh(gsx_engine* e, int64_t now_ns);
+
+/* score() for every pair (score.go:258-335; 0 for pairs with no peerStats).
+ * Re-evaluates on the device if anything changed since the last refresh. */
+int gsx_scores(gsx_engine* e, double* out, size_t n_pairs);
+/* Score(p) for one pair (score.go:247-256). */
+int gsx_score(gsx_engine* e, uint64_t pair, double* out);
+/* Device pointer of the score vector (valid until the next call). */
+int gsx_device_scores(gsx_engine* e, const double** dptr);
+
+int gsx_sync(gsx_engine* e);
+
+/* ---- state import / export (inspection, synthetic workloads, checkpoints) -- */
+/* Record arrays are topic-major: element [t * n_pairs + p].  Mirrors the
+ * fields of topicStats (score.go:37-62) and peerStats (score.go:17-35). */
+#define GSX_REC_IN_MESH 0x01u
+#define GSX_REC_ACTIVE 0x02u
+#define GSX_PAIR_PRESENT 0x01u   /* a peerStats entry exists              */
+#define GSX_PAIR_CONNECTED 0x02u /* peerStats.connected                   */
+
+typedef struct gsx_state_view {
+    /* per record, n_topics * n_pairs */
+    double* first_message_deliveries;
+    double* mesh_message_deliveries;
+    double* mesh_failure_penalty;
+    double* invalid_message_deliveries;
+    int64_t* graft_time_ns;
+    int64_t* mesh_time_ns;
+    uint8_t* rec_flags; /* GSX_REC_* */
+    /* per pair, n_pairs */
+    uint8_t* pair_flags; /* GSX_PAIR_* */
+    int64_t* expire_ns;
+    double* behaviour_penalty;
+} gsx_state_view;
+
+/* Import overwrites all state (and rebuilds the per-observer IP counters from
+ * the present pairs); export copies it back.  NULL members are skipped on
+ * export; on import every member must be non-NULL. */
+int gsx_import_state(gsx_engine* e, const gsx_state_view* s);
+int gsx_export_state(gsx_engine* e, const gsx_state_view* s);
+
+/* Seeded synthetic counter state, generated on the device (BASELINE.md cfg3
+ * initialisation).  Every draw is u = (h(seed, 4, a, k) >> 11) * 2^-53 with
+ * h the SplitMix64-based counter hash of gsx/synth.py, a = t*n_pairs + p for
+ * records and a = p for pairs:
+ *   fmd = u1*fmd_max, mmd = u2*mmd_max, mfp = u3*mfp_max,
+ *   imd = col[p] >= sybil_first_node ? u4*imd_max_sybil : 0,
+ *   inMesh = u5 < p_in_mesh, graftTime = now - (int64)(u6*graft_window_ns),
+ *   meshTime = inMesh ? now - graftTime : 0,
+ *   pair = present|connected; present only if u7 < p_disconnected; absent if
+ *   u8 < p_absent; expire = now + (int64)((u9 - 0.5)*expire_jitter_ns),
+ *   bp = u10*bp_max.
+ * Rebuilds the IP counters like gsx_import_state. */
+typedef struct gsx_synth_spec {
+    uint64_t seed;
+    int64_t now_ns;
+    double fmd_max, mmd_max, mfp_max, imd_max_sybil;
+    double p_in_mesh;
+    int64_t graft_window_ns;
+    double bp_max;
+    double p_disconnected, p_absent;
+    int64_t expire_jitter_ns;
+    uint32_t sybil_first_node;
+    uint32_t reserved;
+} gsx_synth_spec;
+
+int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* spec);
+
+/* Timing of the most recent fused refresh+score launch, measured with HIP
+ * events on the engine stream (ms).  Requires gsx_sync. */
+int gsx_last_refresh_ms(gsx_engine* e, float* ms);
+
+/* Per-launch timing of the fused refresh+score kernel over a region: after
+ * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls
+ * brackets its kernel with a pair of HIP events on the engine stream;
+ * gsx_timing_end waits for them and returns the sum / min / max of the
+ * per-launch durations (ms) and their count. */
+int gsx_timing_begin(gsx_engine* e, uint32_t max_launches);
+int gsx_timing_end(gsx_engine* e, double* total_ms, double* min_ms, double* max_ms, uint32_t* n_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSX_H */

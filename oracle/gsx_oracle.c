@@ -1,0 +1,908 @@
+/*
+ * gsx_oracle.c — CPU restatement of /root/reference/score.go and
+ * score_params.go.  TEST INFRASTRUCTURE ONLY (see gsx_oracle.h).
+ *
+ * Compile with -ffp-contract=off: every expression below is evaluated as the
+ * reference writes it, one IEEE binary64 rounding per operation.
+ */
+#include "gsx_oracle.h"
+
+#include <math.h>
+#include <stdbool.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TIME_CACHE_DURATION_NS (120LL * 1000000000LL) /* pubsub.go:30 */
+
+/* topicStats, score.go:37-62 */
+typedef struct {
+    bool in_mesh;
+    int64_t graft_time;
+    int64_t mesh_time;
+    double first_message_deliveries;
+    double mesh_message_deliveries;
+    bool mesh_message_deliveries_active;
+    double mesh_failure_penalty;
+    double invalid_message_deliveries;
+} orc_topic_stats;
+
+/* peerStats, score.go:17-35 (topics live in orc_engine.ts[pair*T + t]) */
+typedef struct {
+    bool present; /* the map entry ps.peerStats[p] exists */
+    bool connected;
+    int64_t expire;
+    double behaviour_penalty;
+} orc_peer_stats;
+
+/* deliveryRecord + deliveryEntry, score.go:98-109 */
+enum { DELIVERY_UNKNOWN = 0, DELIVERY_VALID, DELIVERY_INVALID, DELIVERY_IGNORED, DELIVERY_THROTTLED };
+
+typedef struct {
+    uint32_t obs;
+    uint64_t msg;
+    int status;
+    int64_t first_seen;
+    int64_t validated; /* 0 == time.Time{} (IsZero) only before validation */
+    bool validated_set;
+    int64_t expire;
+    uint64_t* peers; /* set of pairs; NULL after `drec.peers = nil` */
+    size_t n_peers, cap_peers;
+    bool peers_nil;
+    bool alive;
+    int64_t hnext; /* hash chain */
+    int64_t qnext; /* per-observer gc queue */
+} orc_record;
+
+/* ps.peerIPs (score.go:73-74) restated as an open-addressing map
+ * (observer << 32 | ip) -> number of tracked peers of that observer on ip. */
+typedef struct {
+    uint64_t* keys;
+    uint32_t* vals;
+    size_t cap;
+} ipcount_map;
+
+struct orc_engine;
+static int ipcount_init(struct orc_engine* o);
+
+struct orc_engine {
+    uint32_t T;
+    ipcount_map ipc;
+    gsx_peer_score_params pp;
+    gsx_topic_score_params tp[GSX_MAX_TOPICS];
+    bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
+
+    uint32_t n_nodes;
+    uint64_t E;
+    int64_t* row_ptr;
+    int32_t* col;
+    uint32_t* node_ips;
+    uint32_t* pair_obs;
+
+    orc_peer_stats* ps;
+    orc_topic_stats* ts;
+    double* app;
+
+    uint32_t* whitelist;
+    size_t n_whitelist;
+
+    /* delivery records */
+    orc_record* recs;
+    size_t n_recs, cap_recs;
+    int64_t* buckets;
+    size_t n_buckets;
+    int64_t* q_head;
+    int64_t* q_tail;
+    uint64_t n_alive;
+};
+
+/* ------------------------------------------------------------------------ */
+/* score_params.go                                                          */
+
+/* isInvalidNumber, score_params.go:291-293 */
+static bool invalid_number(double x) { return isnan(x) || isinf(x); }
+
+/* PeerScoreThresholds.validate, score_params.go:34-51 */
+int orc_validate_thresholds(const gsx_thresholds* p) {
+    if (p->gossip_threshold > 0 || invalid_number(p->gossip_threshold)) return GSX_EINVAL;
+    if (p->publish_threshold > 0 || p->publish_threshold > p->gossip_threshold ||
+        invalid_number(p->publish_threshold))
+        return GSX_EINVAL;
+    if (p->graylist_threshold > 0 || p->graylist_threshold > p->publish_threshold ||
+        invalid_number(p->graylist_threshold))
+        return GSX_EINVAL;
+    if (p->accept_px_threshold < 0 || invalid_number(p->accept_px_threshold)) return GSX_EINVAL;
+    if (p->opportunistic_graft_threshold < 0 || invalid_number(p->opportunistic_graft_threshold))
+        return GSX_EINVAL;
+    return 0;
+}
+
+/* PeerScoreParams.validate, score_params.go:151-198 (topic loop 152-157 is
+ * orc_validate_topic_params per topic, done by the caller). */
+int orc_validate_peer_params(const gsx_peer_score_params* p) {
+    if (p->topic_score_cap < 0 || invalid_number(p->topic_score_cap)) return GSX_EINVAL;
+    if (!p->app_specific_score_set) return GSX_EINVAL;
+    if (p->ip_colocation_factor_weight > 0 || invalid_number(p->ip_colocation_factor_weight)) return GSX_EINVAL;
+    if (p->ip_colocation_factor_weight != 0 && p->ip_colocation_factor_threshold < 1) return GSX_EINVAL;
+    if (p->behaviour_penalty_weight > 0 || invalid_number(p->behaviour_penalty_weight)) return GSX_EINVAL;
+    if (p->behaviour_penalty_weight != 0 &&
+        (p->behaviour_penalty_decay <= 0 || p->behaviour_penalty_decay >= 1 ||
+         invalid_number(p->behaviour_penalty_decay)))
+        return GSX_EINVAL;
+    if (p->behaviour_penalty_threshold < 0 || invalid_number(p->behaviour_penalty_threshold)) return GSX_EINVAL;
+    if (p->decay_interval_ns < 1000000000LL) return GSX_EINVAL;
+    if (p->decay_to_zero <= 0 || p->decay_to_zero >= 1 || invalid_number(p->decay_to_zero)) return GSX_EINVAL;
+    return 0;
+}
+
+/* TopicScoreParams.validate, score_params.go:200-268 */
+int orc_validate_topic_params(const gsx_topic_score_params* p) {
+    if (p->topic_weight < 0 || invalid_number(p->topic_weight)) return GSX_EINVAL;
+    /* P1 */
+    if (p->time_in_mesh_quantum_ns == 0) return GSX_EINVAL;
+    if (p->time_in_mesh_weight < 0 || invalid_number(p->time_in_mesh_weight)) return GSX_EINVAL;
+    if (p->time_in_mesh_weight != 0 && p->time_in_mesh_quantum_ns <= 0) return GSX_EINVAL;
+    if (p->time_in_mesh_weight != 0 && (p->time_in_mesh_cap <= 0 || invalid_number(p->time_in_mesh_cap)))
+        return GSX_EINVAL;
+    /* P2 */
+    if (p->first_message_deliveries_weight < 0 || invalid_number(p->first_message_deliveries_weight))
+        return GSX_EINVAL;
+    if (p->first_message_deliveries_weight != 0 &&
+        (p->first_message_deliveries_decay <= 0 || p->first_message_deliveries_decay >= 1 ||
+         invalid_number(p->first_message_deliveries_decay)))
+        return GSX_EINVAL;
+    if (p->first_message_deliveries_weight != 0 &&
+        (p->first_message_deliveries_cap <= 0 || invalid_number(p->first_message_deliveries_cap)))
+        return GSX_EINVAL;
+    /* P3 */
+    if (p->mesh_message_deliveries_weight > 0 || invalid_number(p->mesh_message_deliveries_weight))
+        return GSX_EINVAL;
+    if (p->mesh_message_deliveries_weight != 0 &&
+        (p->mesh_message_deliveries_decay <= 0 || p->mesh_message_deliveries_decay >= 1 ||
+         invalid_number(p->mesh_message_deliveries_decay)))
+        return GSX_EINVAL;
+    if (p->mesh_message_deliveries_weight != 0 &&
+        (p->mesh_message_deliveries_cap <= 0 || invalid_number(p->mesh_message_deliveries_cap)))
+        return GSX_EINVAL;
+    if (p->mesh_message_deliveries_weight != 0 &&
+        (p->mesh_message_deliveries_threshold <= 0 || invalid_number(p->mesh_message_deliveries_threshold)))
+        return GSX_EINVAL;
+    if (p->mesh_message_deliveries_window_ns < 0) return GSX_EINVAL;
+    if (p->mesh_message_deliveries_weight != 0 && p->mesh_message_deliveries_activation_ns < 1000000000LL)
+        return GSX_EINVAL;
+    /* P3b */
+    if (p->mesh_failure_penalty_weight > 0 || invalid_number(p->mesh_failure_penalty_weight)) return GSX_EINVAL;
+    if (p->mesh_failure_penalty_weight != 0 &&
+        (invalid_number(p->mesh_failure_penalty_decay) || p->mesh_failure_penalty_decay <= 0 ||
+         p->mesh_failure_penalty_decay >= 1))
+        return GSX_EINVAL;
+    /* P4 */
+    if (p->invalid_message_deliveries_weight > 0 || invalid_number(p->invalid_message_deliveries_weight))
+        return GSX_EINVAL;
+    if (p->invalid_message_deliveries_decay <= 0 || p->invalid_message_deliveries_decay >= 1 ||
+        invalid_number(p->invalid_message_deliveries_decay))
+        return GSX_EINVAL;
+    return 0;
+}
+
+/* ScoreParameterDecayWithBase, score_params.go:282-287: `decay / base` is a
+ * Duration (int64) division, truncating. */
+double orc_score_parameter_decay_with_base(int64_t decay_ns, int64_t base_ns, double decay_to_zero) {
+    double ticks = (double)(decay_ns / base_ns);
+    return pow(decay_to_zero, 1 / ticks);
+}
+
+/* ScoreParameterDecay, score_params.go:277-279 (DefaultDecayInterval 1s,
+ * DefaultDecayToZero 0.01, :270-273) */
+double orc_score_parameter_decay(int64_t decay_ns) {
+    return orc_score_parameter_decay_with_base(decay_ns, 1000000000LL, 0.01);
+}
+
+/* ------------------------------------------------------------------------ */
+/* engine                                                                   */
+
+orc_engine* orc_create(uint32_t n_topics) {
+    if (n_topics == 0 || n_topics > GSX_MAX_TOPICS) return NULL;
+    orc_engine* o = (orc_engine*)calloc(1, sizeof(orc_engine));
+    if (!o) return NULL;
+    o->T = n_topics;
+    return o;
+}
+
+static void free_records(orc_engine* o) {
+    for (size_t i = 0; i < o->n_recs; i++) free(o->recs[i].peers);
+    free(o->recs);
+    free(o->buckets);
+    free(o->q_head);
+    free(o->q_tail);
+    o->recs = NULL;
+    o->buckets = NULL;
+    o->q_head = o->q_tail = NULL;
+    o->n_recs = o->cap_recs = 0;
+    o->n_alive = 0;
+}
+
+void orc_destroy(orc_engine* o) {
+    if (!o) return;
+    free(o->row_ptr);
+    free(o->col);
+    free(o->node_ips);
+    free(o->pair_obs);
+    free(o->ps);
+    free(o->ts);
+    free(o->app);
+    free(o->whitelist);
+    free(o->ipc.keys);
+    free(o->ipc.vals);
+    free_records(o);
+    free(o);
+}
+
+uint64_t orc_num_pairs(orc_engine* o) { return o->E; }
+
+int orc_set_peer_params(orc_engine* o, const gsx_peer_score_params* p) {
+    o->pp = *p;
+    return 0;
+}
+
+/* SetTopicScoreParams, score.go:194-234 */
+int orc_set_topic_params(orc_engine* o, uint32_t topic, const gsx_topic_score_params* p) {
+    if (topic >= o->T) return GSX_ERANGE;
+    bool exist = o->scored[topic];
+    gsx_topic_score_params old = o->tp[topic];
+    o->tp[topic] = *p;
+    o->scored[topic] = true;
+    if (!exist) return 0;
+    bool recap = false;
+    if (p->first_message_deliveries_cap < old.first_message_deliveries_cap) recap = true;
+    if (p->mesh_message_deliveries_cap < old.mesh_message_deliveries_cap) recap = true;
+    if (!recap) return 0;
+    for (uint64_t q = 0; q < o->E; q++) {
+        if (!o->ps[q].present) continue;
+        orc_topic_stats* t = &o->ts[q * o->T + topic];
+        if (t->first_message_deliveries > p->first_message_deliveries_cap)
+            t->first_message_deliveries = p->first_message_deliveries_cap;
+        if (t->mesh_message_deliveries > p->mesh_message_deliveries_cap)
+            t->mesh_message_deliveries = p->mesh_message_deliveries_cap;
+    }
+    return 0;
+}
+
+int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
+                     const uint32_t* node_ips) {
+    uint64_t E = (uint64_t)row_ptr[n_nodes];
+    free(o->row_ptr);
+    free(o->col);
+    free(o->node_ips);
+    free(o->pair_obs);
+    free(o->ps);
+    free(o->ts);
+    free(o->app);
+    free_records(o);
+    o->n_nodes = n_nodes;
+    o->E = E;
+    o->row_ptr = (int64_t*)malloc(sizeof(int64_t) * (n_nodes + 1));
+    o->col = (int32_t*)malloc(sizeof(int32_t) * (E ? E : 1));
+    o->node_ips = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (n_nodes ? n_nodes : 1));
+    o->pair_obs = (uint32_t*)malloc(sizeof(uint32_t) * (E ? E : 1));
+    o->ps = (orc_peer_stats*)calloc(E ? E : 1, sizeof(orc_peer_stats));
+    o->ts = (orc_topic_stats*)calloc((E ? E : 1) * o->T, sizeof(orc_topic_stats));
+    o->app = (double*)calloc(E ? E : 1, sizeof(double));
+    o->q_head = (int64_t*)malloc(sizeof(int64_t) * (n_nodes ? n_nodes : 1));
+    o->q_tail = (int64_t*)malloc(sizeof(int64_t) * (n_nodes ? n_nodes : 1));
+    if (!o->row_ptr || !o->col || !o->node_ips || !o->pair_obs || !o->ps || !o->ts || !o->app ||
+        !o->q_head || !o->q_tail)
+        return GSX_ENOMEM;
+    memcpy(o->row_ptr, row_ptr, sizeof(int64_t) * (n_nodes + 1));
+    if (E) memcpy(o->col, col, sizeof(int32_t) * E);
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        o->node_ips[2 * i] = node_ips ? node_ips[2 * i] : GSX_NO_IP;
+        o->node_ips[2 * i + 1] = node_ips ? node_ips[2 * i + 1] : GSX_NO_IP;
+        o->q_head[i] = o->q_tail[i] = -1;
+        for (int64_t p = row_ptr[i]; p < row_ptr[i + 1]; p++) o->pair_obs[p] = i;
+    }
+    if (ipcount_init(o)) return GSX_ENOMEM;
+    o->n_buckets = 1024;
+    o->buckets = (int64_t*)malloc(sizeof(int64_t) * o->n_buckets);
+    for (size_t i = 0; i < o->n_buckets; i++) o->buckets[i] = -1;
+    return 0;
+}
+
+int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n) {
+    free(o->whitelist);
+    o->whitelist = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    if (n) memcpy(o->whitelist, ip_ids, sizeof(uint32_t) * n);
+    o->n_whitelist = n;
+    return 0;
+}
+
+int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs) {
+    if (n_pairs != o->E) return GSX_EINVAL;
+    memcpy(o->app, app, sizeof(double) * n_pairs);
+    return 0;
+}
+
+static bool whitelisted(const orc_engine* o, uint32_t ip) {
+    for (size_t i = 0; i < o->n_whitelist; i++)
+        if (o->whitelist[i] == ip) return true;
+    return false;
+}
+
+/* the IP list of the peer behind pair q (peerStats.ips; getIPs score.go:977-1017) */
+static int pair_ips(const orc_engine* o, uint64_t q, uint32_t out[2]) {
+    uint32_t node = (uint32_t)o->col[q];
+    int n = 0;
+    for (int k = 0; k < 2; k++) {
+        uint32_t ip = o->node_ips[2 * node + k];
+        if (ip != GSX_NO_IP) out[n++] = ip;
+    }
+    return n;
+}
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+static uint32_t* ipcount_slot(ipcount_map* m, uint64_t key, bool insert) {
+    size_t i = (size_t)(mix64(key) & (m->cap - 1));
+    for (;;) {
+        if (m->keys[i] == key) return &m->vals[i];
+        if (m->keys[i] == UINT64_MAX) {
+            if (!insert) return NULL;
+            m->keys[i] = key;
+            m->vals[i] = 0;
+            return &m->vals[i];
+        }
+        i = (i + 1) & (m->cap - 1);
+    }
+}
+
+static int ipcount_init(orc_engine* o) {
+    ipcount_map* m = &o->ipc;
+    free(m->keys);
+    free(m->vals);
+    size_t need = 2 * (size_t)o->E + 16, cap = 16;
+    while (cap < 2 * need) cap <<= 1;
+    m->cap = cap;
+    m->keys = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+    m->vals = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    if (!m->keys || !m->vals) return GSX_ENOMEM;
+    memset(m->keys, 0xff, sizeof(uint64_t) * cap);
+    return 0;
+}
+
+/* setIPs / removeIPs (score.go:1021-1074) for the whole IP list of pair q:
+ * the peer joins (+1) or leaves (-1) each of its IPs' sets once. */
+static void ipcount_add(orc_engine* o, uint64_t q, int delta) {
+    uint32_t ips[2];
+    int k = pair_ips(o, q, ips);
+    for (int j = 0; j < k; j++) {
+        if (j == 1 && ips[1] == ips[0]) continue; /* a set: the peer counts once */
+        uint64_t key = ((uint64_t)o->pair_obs[q] << 32) | ips[j];
+        *ipcount_slot(&o->ipc, key, true) += (uint32_t)delta;
+    }
+}
+
+static void ipcount_rebuild(orc_engine* o) {
+    memset(o->ipc.vals, 0, sizeof(uint32_t) * o->ipc.cap);
+    for (uint64_t q = 0; q < o->E; q++)
+        if (o->ps[q].present) ipcount_add(o, q, +1);
+}
+
+/* ipColocationFactor, score.go:337-381 */
+static double ip_colocation_factor(const orc_engine* o, uint64_t p) {
+    if (!o->ps[p].present) return 0;
+    double result = 0;
+    uint32_t ips[2];
+    int k = pair_ips(o, p, ips);
+    uint32_t obs = o->pair_obs[p];
+    for (int j = 0; j < k; j++) {
+        uint32_t ip = ips[j];
+        if (o->n_whitelist > 0 && whitelisted(o, ip)) continue; /* :346-367 */
+        uint32_t* v = ipcount_slot((ipcount_map*)&o->ipc, ((uint64_t)obs << 32) | ip, false);
+        uint32_t peers_in_ip = v ? *v : 0; /* len(ps.peerIPs[ip]) */
+        if ((int64_t)peers_in_ip > (int64_t)o->pp.ip_colocation_factor_threshold) {
+            double surpluss = (double)((int64_t)peers_in_ip - (int64_t)o->pp.ip_colocation_factor_threshold);
+            result += surpluss * surpluss;
+        }
+    }
+    return result;
+}
+
+/* score(), score.go:258-335; topics in ascending index order */
+static double score_pair(const orc_engine* o, uint64_t p) {
+    const orc_peer_stats* pstats = &o->ps[p];
+    if (!pstats->present) return 0;
+    double score = 0;
+    for (uint32_t t = 0; t < o->T; t++) {
+        if (!o->scored[t]) continue; /* :269-273 */
+        const gsx_topic_score_params* tp = &o->tp[t];
+        const orc_topic_stats* ts = &o->ts[p * o->T + t];
+        double topic_score = 0;
+        /* P1 :279-285 — integer Duration division */
+        if (ts->in_mesh) {
+            double p1 = (double)(ts->mesh_time / tp->time_in_mesh_quantum_ns);
+            if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+            topic_score += p1 * tp->time_in_mesh_weight;
+        }
+        /* P2 :288-289 */
+        double p2 = ts->first_message_deliveries;
+        topic_score += p2 * tp->first_message_deliveries_weight;
+        /* P3 :292-298 */
+        if (ts->mesh_message_deliveries_active) {
+            if (ts->mesh_message_deliveries < tp->mesh_message_deliveries_threshold) {
+                double deficit = tp->mesh_message_deliveries_threshold - ts->mesh_message_deliveries;
+                double p3 = deficit * deficit;
+                topic_score += p3 * tp->mesh_message_deliveries_weight;
+            }
+        }
+        /* P3b :302-303 */
+        double p3b = ts->mesh_failure_penalty;
+        topic_score += p3b * tp->mesh_failure_penalty_weight;
+        /* P4 :307-308 */
+        double p4 = (ts->invalid_message_deliveries * ts->invalid_message_deliveries);
+        topic_score += p4 * tp->invalid_message_deliveries_weight;
+        /* :311 */
+        score += topic_score * tp->topic_weight;
+    }
+    /* :315-317 */
+    if (o->pp.topic_score_cap > 0 && score > o->pp.topic_score_cap) score = o->pp.topic_score_cap;
+    /* P5 :320-321 */
+    double p5 = o->app[p];
+    score += p5 * o->pp.app_specific_weight;
+    /* P6 :324-325 */
+    double p6 = ip_colocation_factor(o, p);
+    score += p6 * o->pp.ip_colocation_factor_weight;
+    /* P7 :328-332 */
+    if (pstats->behaviour_penalty > o->pp.behaviour_penalty_threshold) {
+        double excess = pstats->behaviour_penalty - o->pp.behaviour_penalty_threshold;
+        double p7 = excess * excess;
+        score += p7 * o->pp.behaviour_penalty_weight;
+    }
+    return score;
+}
+
+double orc_score(orc_engine* o, uint64_t pair) {
+    if (pair >= o->E) return 0;
+    return score_pair(o, pair);
+}
+
+int orc_scores(orc_engine* o, double* out, size_t n_pairs) {
+    if (n_pairs != o->E) return GSX_EINVAL;
+    for (uint64_t p = 0; p < o->E; p++) out[p] = score_pair(o, p);
+    return 0;
+}
+
+/* one pair's share of refreshScores, score.go:502-557 (purge handled by caller) */
+static void refresh_pair(orc_engine* o, uint64_t p, int64_t now) {
+    orc_peer_stats* pstats = &o->ps[p];
+    for (uint32_t t = 0; t < o->T; t++) {
+        if (!o->scored[t]) continue; /* :520-524 */
+        const gsx_topic_score_params* tp = &o->tp[t];
+        orc_topic_stats* ts = &o->ts[p * o->T + t];
+        /* :527-542 */
+        ts->first_message_deliveries *= tp->first_message_deliveries_decay;
+        if (ts->first_message_deliveries < o->pp.decay_to_zero) ts->first_message_deliveries = 0;
+        ts->mesh_message_deliveries *= tp->mesh_message_deliveries_decay;
+        if (ts->mesh_message_deliveries < o->pp.decay_to_zero) ts->mesh_message_deliveries = 0;
+        ts->mesh_failure_penalty *= tp->mesh_failure_penalty_decay;
+        if (ts->mesh_failure_penalty < o->pp.decay_to_zero) ts->mesh_failure_penalty = 0;
+        ts->invalid_message_deliveries *= tp->invalid_message_deliveries_decay;
+        if (ts->invalid_message_deliveries < o->pp.decay_to_zero) ts->invalid_message_deliveries = 0;
+        /* :544-549 */
+        if (ts->in_mesh) {
+            ts->mesh_time = now - ts->graft_time;
+            if (ts->mesh_time > tp->mesh_message_deliveries_activation_ns) ts->mesh_message_deliveries_active = true;
+        }
+    }
+    /* :553-556 */
+    pstats->behaviour_penalty *= o->pp.behaviour_penalty_decay;
+    if (pstats->behaviour_penalty < o->pp.decay_to_zero) pstats->behaviour_penalty = 0;
+}
+
+/* refreshScores, score.go:497-558 */
+int orc_refresh(orc_engine* o, int64_t now) {
+    for (uint64_t p = 0; p < o->E; p++) {
+        orc_peer_stats* pstats = &o->ps[p];
+        if (!pstats->present) continue;
+        if (!pstats->connected) {
+            /* :503-516 — `now.After(expire)`: removeIPs + delete */
+            if (now > pstats->expire) {
+                ipcount_add(o, p, -1);
+                pstats->present = false;
+            }
+            continue;
+        }
+        refresh_pair(o, p, now);
+    }
+    return 0;
+}
+
+int orc_refresh_scores_range(orc_engine* o, int64_t now, uint64_t p0, uint64_t p1, double* out) {
+    if (p1 > o->E) p1 = o->E;
+    for (uint64_t p = p0; p < p1; p++) {
+        orc_peer_stats* pstats = &o->ps[p];
+        if (!pstats->present) continue;
+        if (!pstats->connected) {
+            if (now > pstats->expire) {
+                ipcount_add(o, p, -1);
+                pstats->present = false;
+            }
+            continue;
+        }
+        refresh_pair(o, p, now);
+    }
+    for (uint64_t p = p0; p < p1; p++) out[p - p0] = score_pair(o, p);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* tracer events, score.go:588-974                                          */
+
+/* getTopicStats, score.go:875-890: records of scored topics always exist in
+ * this dense model; an unscored topic has none. */
+static orc_topic_stats* topic_stats(orc_engine* o, uint64_t p, uint32_t topic) {
+    if (topic >= o->T || !o->scored[topic]) return NULL;
+    return &o->ts[p * o->T + topic];
+}
+
+/* AddPeer, score.go:588-602 */
+static void add_peer(orc_engine* o, uint64_t p) {
+    orc_peer_stats* pstats = &o->ps[p];
+    if (!pstats->present) {
+        memset(pstats, 0, sizeof(*pstats));
+        memset(&o->ts[p * o->T], 0, sizeof(orc_topic_stats) * o->T);
+        pstats->present = true;
+        ipcount_add(o, p, +1); /* setIPs: the IPs now count for this observer */
+    }
+    pstats->connected = true;
+}
+
+/* RemovePeer, score.go:604-637 */
+static void remove_peer(orc_engine* o, uint64_t p, int64_t now) {
+    orc_peer_stats* pstats = &o->ps[p];
+    if (!pstats->present) return;
+    if (score_pair(o, p) > 0) { /* :615-619 */
+        ipcount_add(o, p, -1);         /* removeIPs */
+        pstats->present = false;       /* delete */
+        return;
+    }
+    for (uint32_t t = 0; t < o->T; t++) { /* :623-633 */
+        orc_topic_stats* ts = topic_stats(o, p, t);
+        if (!ts) continue;
+        ts->first_message_deliveries = 0;
+        double threshold = o->tp[t].mesh_message_deliveries_threshold;
+        if (ts->in_mesh && ts->mesh_message_deliveries_active && ts->mesh_message_deliveries < threshold) {
+            double deficit = threshold - ts->mesh_message_deliveries;
+            ts->mesh_failure_penalty += deficit * deficit;
+        }
+        ts->in_mesh = false;
+    }
+    pstats->connected = false;
+    pstats->expire = now + o->pp.retain_score_ns;
+}
+
+/* Graft, score.go:642-660 */
+static void graft(orc_engine* o, uint64_t p, uint32_t topic, int64_t now) {
+    if (!o->ps[p].present) return;
+    orc_topic_stats* ts = topic_stats(o, p, topic);
+    if (!ts) return;
+    ts->in_mesh = true;
+    ts->graft_time = now;
+    ts->mesh_time = 0;
+    ts->mesh_message_deliveries_active = false;
+}
+
+/* Prune, score.go:662-684 */
+static void prune(orc_engine* o, uint64_t p, uint32_t topic) {
+    if (!o->ps[p].present) return;
+    orc_topic_stats* ts = topic_stats(o, p, topic);
+    if (!ts) return;
+    double threshold = o->tp[topic].mesh_message_deliveries_threshold;
+    if (ts->mesh_message_deliveries_active && ts->mesh_message_deliveries < threshold) {
+        double deficit = threshold - ts->mesh_message_deliveries;
+        ts->mesh_failure_penalty += deficit * deficit;
+    }
+    ts->in_mesh = false;
+}
+
+/* markInvalidMessageDelivery, score.go:894-907 */
+static void mark_invalid(orc_engine* o, uint64_t p, uint32_t topic) {
+    if (!o->ps[p].present) return;
+    orc_topic_stats* ts = topic_stats(o, p, topic);
+    if (!ts) return;
+    ts->invalid_message_deliveries += 1;
+}
+
+/* markFirstMessageDelivery, score.go:912-939 */
+static void mark_first(orc_engine* o, uint64_t p, uint32_t topic) {
+    if (!o->ps[p].present) return;
+    orc_topic_stats* ts = topic_stats(o, p, topic);
+    if (!ts) return;
+    double cap = o->tp[topic].first_message_deliveries_cap;
+    ts->first_message_deliveries += 1;
+    if (ts->first_message_deliveries > cap) ts->first_message_deliveries = cap;
+    if (!ts->in_mesh) return;
+    cap = o->tp[topic].mesh_message_deliveries_cap;
+    ts->mesh_message_deliveries += 1;
+    if (ts->mesh_message_deliveries > cap) ts->mesh_message_deliveries = cap;
+}
+
+/* markDuplicateMessageDelivery, score.go:944-974.  validated_set=false is
+ * time.Time{} (always inside the window). */
+static void mark_duplicate(orc_engine* o, uint64_t p, uint32_t topic, bool validated_set, int64_t validated,
+                           int64_t now) {
+    if (!o->ps[p].present) return;
+    orc_topic_stats* ts = topic_stats(o, p, topic);
+    if (!ts) return;
+    if (!ts->in_mesh) return;
+    const gsx_topic_score_params* tp = &o->tp[topic];
+    if (validated_set && (now - validated) > tp->mesh_message_deliveries_window_ns) return;
+    double cap = tp->mesh_message_deliveries_cap;
+    ts->mesh_message_deliveries += 1;
+    if (ts->mesh_message_deliveries > cap) ts->mesh_message_deliveries = cap;
+}
+
+/* AddPenalty, score.go:384-398 */
+static void add_penalty(orc_engine* o, uint64_t p, int64_t count) {
+    if (!o->ps[p].present) return;
+    o->ps[p].behaviour_penalty += (double)count;
+}
+
+int orc_apply_events(orc_engine* o, const gsx_event* ev, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+        const gsx_event* e = &ev[i];
+        if (e->pair >= o->E) return GSX_ERANGE;
+        switch (e->kind) {
+        case GSX_EV_ADD_PEER: add_peer(o, e->pair); break;
+        case GSX_EV_REMOVE_PEER: remove_peer(o, e->pair, e->now_ns); break;
+        case GSX_EV_GRAFT: graft(o, e->pair, e->topic, e->now_ns); break;
+        case GSX_EV_PRUNE: prune(o, e->pair, e->topic); break;
+        case GSX_EV_FIRST_DELIVERY: mark_first(o, e->pair, e->topic); break;
+        case GSX_EV_MESH_DELIVERY: mark_duplicate(o, e->pair, e->topic, false, 0, e->now_ns); break;
+        case GSX_EV_INVALID_DELIVERY: mark_invalid(o, e->pair, e->topic); break;
+        case GSX_EV_PENALTY: add_penalty(o, e->pair, e->arg); break;
+        default: return GSX_EINVAL;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* delivery records, score.go:686-870                                       */
+
+static size_t rec_bucket(const orc_engine* o, uint32_t obs, uint64_t msg) {
+    return (size_t)(mix64(((uint64_t)obs * 0x9E3779B97F4A7C15ULL) ^ msg) & (o->n_buckets - 1));
+}
+
+static void rehash(orc_engine* o) {
+    size_t nb = o->n_buckets * 2;
+    int64_t* b = (int64_t*)malloc(sizeof(int64_t) * nb);
+    for (size_t i = 0; i < nb; i++) b[i] = -1;
+    free(o->buckets);
+    o->buckets = b;
+    o->n_buckets = nb;
+    for (size_t i = 0; i < o->n_recs; i++) {
+        orc_record* r = &o->recs[i];
+        if (!r->alive) continue;
+        size_t h = rec_bucket(o, r->obs, r->msg);
+        r->hnext = o->buckets[h];
+        o->buckets[h] = (int64_t)i;
+    }
+}
+
+/* messageDeliveries.getRecord, score.go:833-854 */
+static orc_record* get_record(orc_engine* o, uint32_t obs, uint64_t msg, int64_t now) {
+    size_t h = rec_bucket(o, obs, msg);
+    for (int64_t i = o->buckets[h]; i >= 0; i = o->recs[i].hnext)
+        if (o->recs[i].obs == obs && o->recs[i].msg == msg) return &o->recs[i];
+    if (o->n_recs == o->cap_recs) {
+        size_t nc = o->cap_recs ? 2 * o->cap_recs : 256;
+        orc_record* nr = (orc_record*)realloc(o->recs, sizeof(orc_record) * nc);
+        if (!nr) return NULL;
+        o->recs = nr;
+        o->cap_recs = nc;
+    }
+    if (o->n_alive * 2 > o->n_buckets) {
+        rehash(o);
+        h = rec_bucket(o, obs, msg);
+    }
+    int64_t idx = (int64_t)o->n_recs++;
+    orc_record* r = &o->recs[idx];
+    memset(r, 0, sizeof(*r));
+    r->obs = obs;
+    r->msg = msg;
+    r->status = DELIVERY_UNKNOWN;
+    r->first_seen = now;
+    r->expire = now + TIME_CACHE_DURATION_NS;
+    r->alive = true;
+    r->hnext = o->buckets[h];
+    o->buckets[h] = idx;
+    r->qnext = -1;
+    if (o->q_tail[obs] >= 0)
+        o->recs[o->q_tail[obs]].qnext = idx;
+    else
+        o->q_head[obs] = idx;
+    o->q_tail[obs] = idx;
+    o->n_alive++;
+    return r;
+}
+
+static bool rec_has_peer(const orc_record* r, uint64_t p) {
+    for (size_t i = 0; i < r->n_peers; i++)
+        if (r->peers[i] == p) return true;
+    return false;
+}
+
+static void rec_add_peer(orc_record* r, uint64_t p) {
+    if (r->peers_nil || rec_has_peer(r, p)) return;
+    if (r->n_peers == r->cap_peers) {
+        size_t nc = r->cap_peers ? 2 * r->cap_peers : 4;
+        r->peers = (uint64_t*)realloc(r->peers, sizeof(uint64_t) * nc);
+        r->cap_peers = nc;
+    }
+    r->peers[r->n_peers++] = p;
+}
+
+static void rec_nil_peers(orc_record* r) {
+    free(r->peers);
+    r->peers = NULL;
+    r->n_peers = r->cap_peers = 0;
+    r->peers_nil = true;
+}
+
+/* ValidateMessage, score.go:686-693 */
+int orc_trace_validate(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    (void)topic;
+    if (pair >= o->E) return GSX_ERANGE;
+    return get_record(o, o->pair_obs[pair], msg_id, now) ? 0 : GSX_ENOMEM;
+}
+
+/* DeliverMessage, score.go:695-719 */
+int orc_trace_deliver(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    if (pair >= o->E) return GSX_ERANGE;
+    mark_first(o, pair, topic);
+    orc_record* r = get_record(o, o->pair_obs[pair], msg_id, now);
+    if (!r) return GSX_ENOMEM;
+    if (r->status != DELIVERY_UNKNOWN) return 0;
+    r->status = DELIVERY_VALID;
+    r->validated = now;
+    r->validated_set = true;
+    for (size_t i = 0; i < r->n_peers; i++)
+        if (r->peers[i] != pair) mark_duplicate(o, r->peers[i], topic, false, 0, now);
+    return 0;
+}
+
+/* RejectMessage, score.go:721-786 */
+int orc_trace_reject(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int32_t reason, int64_t now) {
+    if (pair >= o->E) return GSX_ERANGE;
+    switch (reason) {
+    case GSX_REJECT_MISSING_SIGNATURE:
+    case GSX_REJECT_INVALID_SIGNATURE:
+    case GSX_REJECT_UNEXPECTED_SIGNATURE:
+    case GSX_REJECT_UNEXPECTED_AUTH_INFO:
+    case GSX_REJECT_SELF_ORIGIN: mark_invalid(o, pair, topic); return 0;
+    case GSX_REJECT_BLACKLISTED_PEER:
+    case GSX_REJECT_BLACKLISTED_SOURCE:
+    case GSX_REJECT_VALIDATION_QUEUE_FULL: return 0;
+    default: break;
+    }
+    orc_record* r = get_record(o, o->pair_obs[pair], msg_id, now);
+    if (!r) return GSX_ENOMEM;
+    if (r->status != DELIVERY_UNKNOWN) return 0;
+    switch (reason) {
+    case GSX_REJECT_VALIDATION_THROTTLED:
+        r->status = DELIVERY_THROTTLED;
+        rec_nil_peers(r);
+        return 0;
+    case GSX_REJECT_VALIDATION_IGNORED:
+        r->status = DELIVERY_IGNORED;
+        rec_nil_peers(r);
+        return 0;
+    default: break;
+    }
+    r->status = DELIVERY_INVALID;
+    mark_invalid(o, pair, topic);
+    for (size_t i = 0; i < r->n_peers; i++) mark_invalid(o, r->peers[i], topic);
+    rec_nil_peers(r);
+    return 0;
+}
+
+/* DuplicateMessage, score.go:788-820 */
+int orc_trace_duplicate(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now) {
+    if (pair >= o->E) return GSX_ERANGE;
+    orc_record* r = get_record(o, o->pair_obs[pair], msg_id, now);
+    if (!r) return GSX_ENOMEM;
+    if (!r->peers_nil && rec_has_peer(r, pair)) return 0;
+    switch (r->status) {
+    case DELIVERY_UNKNOWN: rec_add_peer(r, pair); break;
+    case DELIVERY_VALID:
+        rec_add_peer(r, pair);
+        mark_duplicate(o, pair, topic, r->validated_set, r->validated, now);
+        break;
+    case DELIVERY_INVALID: mark_invalid(o, pair, topic); break;
+    default: break; /* throttled / ignored */
+    }
+    return 0;
+}
+
+/* messageDeliveries.gc, score.go:856-870 (one queue per observer, as each
+ * router owns its own peerScore) */
+int orc_gc_deliveries(orc_engine* o, int64_t now) {
+    for (uint32_t obs = 0; obs < o->n_nodes; obs++) {
+        while (o->q_head[obs] >= 0 && now > o->recs[o->q_head[obs]].expire) {
+            int64_t idx = o->q_head[obs];
+            orc_record* r = &o->recs[idx];
+            size_t h = rec_bucket(o, r->obs, r->msg);
+            int64_t* link = &o->buckets[h];
+            while (*link != idx) link = &o->recs[*link].hnext;
+            *link = r->hnext;
+            r->alive = false;
+            free(r->peers);
+            r->peers = NULL;
+            o->n_alive--;
+            o->q_head[obs] = r->qnext;
+        }
+        if (o->q_head[obs] < 0) o->q_tail[obs] = -1;
+    }
+    return 0;
+}
+
+uint64_t orc_num_delivery_records(orc_engine* o) { return o->n_alive; }
+
+/* ------------------------------------------------------------------------ */
+/* state view                                                               */
+
+int orc_import_state(orc_engine* o, const gsx_state_view* s) {
+    uint64_t E = o->E;
+    for (uint64_t p = 0; p < E; p++) {
+        orc_peer_stats* ps = &o->ps[p];
+        ps->present = (s->pair_flags[p] & GSX_PAIR_PRESENT) != 0;
+        ps->connected = (s->pair_flags[p] & GSX_PAIR_CONNECTED) != 0;
+        ps->expire = s->expire_ns[p];
+        ps->behaviour_penalty = s->behaviour_penalty[p];
+        for (uint32_t t = 0; t < o->T; t++) {
+            size_t r = (size_t)t * E + p;
+            orc_topic_stats* ts = &o->ts[p * o->T + t];
+            ts->first_message_deliveries = s->first_message_deliveries[r];
+            ts->mesh_message_deliveries = s->mesh_message_deliveries[r];
+            ts->mesh_failure_penalty = s->mesh_failure_penalty[r];
+            ts->invalid_message_deliveries = s->invalid_message_deliveries[r];
+            ts->graft_time = s->graft_time_ns[r];
+            ts->mesh_time = s->mesh_time_ns[r];
+            ts->in_mesh = (s->rec_flags[r] & GSX_REC_IN_MESH) != 0;
+            ts->mesh_message_deliveries_active = (s->rec_flags[r] & GSX_REC_ACTIVE) != 0;
+        }
+    }
+    ipcount_rebuild(o);
+    return 0;
+}
+
+int orc_export_state(orc_engine* o, const gsx_state_view* s) {
+    uint64_t E = o->E;
+    for (uint64_t p = 0; p < E; p++) {
+        const orc_peer_stats* ps = &o->ps[p];
+        if (s->pair_flags) s->pair_flags[p] = (uint8_t)((ps->present ? GSX_PAIR_PRESENT : 0) |
+                                                        (ps->connected ? GSX_PAIR_CONNECTED : 0));
+        if (s->expire_ns) s->expire_ns[p] = ps->expire;
+        if (s->behaviour_penalty) s->behaviour_penalty[p] = ps->behaviour_penalty;
+        for (uint32_t t = 0; t < o->T; t++) {
+            size_t r = (size_t)t * E + p;
+            const orc_topic_stats* ts = &o->ts[p * o->T + t];
+            if (s->first_message_deliveries) s->first_message_deliveries[r] = ts->first_message_deliveries;
+            if (s->mesh_message_deliveries) s->mesh_message_deliveries[r] = ts->mesh_message_deliveries;
+            if (s->mesh_failure_penalty) s->mesh_failure_penalty[r] = ts->mesh_failure_penalty;
+            if (s->invalid_message_deliveries) s->invalid_message_deliveries[r] = ts->invalid_message_deliveries;
+            if (s->graft_time_ns) s->graft_time_ns[r] = ts->graft_time;
+            if (s->mesh_time_ns) s->mesh_time_ns[r] = ts->mesh_time;
+            if (s->rec_flags)
+                s->rec_flags[r] = (uint8_t)((ts->in_mesh ? GSX_REC_IN_MESH : 0) |
+                                            (ts->mesh_message_deliveries_active ? GSX_REC_ACTIVE : 0));
+        }
+    }
+    return 0;
+}

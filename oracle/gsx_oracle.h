@@ -1,0 +1,77 @@
+/*
+ * gsx_oracle.h — CPU restatement of the reference's peer-scoring semantics.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the HIP engine in
+ * go-libp2p-pubsub_amd/.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product path never links or calls it.
+ *
+ * It restates, in plain C over an array-of-structs model that follows the
+ * reference's own structs, the functions of /root/reference/score.go and
+ * score_params.go (each function cites the file:line it follows).  It shares
+ * only the parameter/event/state-view TYPE definitions with include/gsx.h
+ * (data layout of the boundary), none of its logic.
+ *
+ * Pinning: the reference is Go and no Go toolchain exists in this container
+ * (SURVEY.md §8c), so the reference cannot be built or run here.  The oracle
+ * is pinned against the known-answer values held by the reference's own tests
+ * (score_test.go, score_params_test.go), restated as fixtures in
+ * tests/golden/ by tests/golden/make_golden.py.
+ *
+ * Determinism contract: the reference iterates Go maps in
+ * random order; the oracle uses ascending topic index for the topic sum of
+ * score() and applies events in the order given.  Floating point is IEEE
+ * binary64 with no contraction (-ffp-contract=off), matching Go on amd64.
+ */
+#ifndef GSX_ORACLE_H
+#define GSX_ORACLE_H
+
+#include "../include/gsx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_engine orc_engine;
+
+orc_engine* orc_create(uint32_t n_topics);
+void orc_destroy(orc_engine* o);
+
+int orc_validate_peer_params(const gsx_peer_score_params* p);
+int orc_validate_topic_params(const gsx_topic_score_params* p);
+int orc_validate_thresholds(const gsx_thresholds* p);
+double orc_score_parameter_decay_with_base(int64_t decay_ns, int64_t base_ns, double decay_to_zero);
+double orc_score_parameter_decay(int64_t decay_ns);
+
+int orc_set_peer_params(orc_engine* o, const gsx_peer_score_params* p);
+int orc_set_topic_params(orc_engine* o, uint32_t topic, const gsx_topic_score_params* p);
+int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
+                     const uint32_t* node_ips);
+int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);
+int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs);
+
+int orc_apply_events(orc_engine* o, const gsx_event* ev, size_t n);
+
+int orc_trace_validate(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+int orc_trace_deliver(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+int orc_trace_reject(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int32_t reason,
+                     int64_t now_ns);
+int orc_trace_duplicate(orc_engine* o, uint64_t pair, uint64_t msg_id, uint32_t topic, int64_t now_ns);
+int orc_gc_deliveries(orc_engine* o, int64_t now_ns);
+uint64_t orc_num_delivery_records(orc_engine* o);
+
+/* refreshScores (score.go:497-558) */
+int orc_refresh(orc_engine* o, int64_t now_ns);
+/* score() for every pair / one pair (score.go:258-335) */
+int orc_scores(orc_engine* o, double* out, size_t n_pairs);
+double orc_score(orc_engine* o, uint64_t pair);
+/* Refresh + score restricted to pairs [p0, p1) (bench sample); returns 0. */
+int orc_refresh_scores_range(orc_engine* o, int64_t now_ns, uint64_t p0, uint64_t p1, double* out);
+
+int orc_import_state(orc_engine* o, const gsx_state_view* s);
+int orc_export_state(orc_engine* o, const gsx_state_view* s);
+uint64_t orc_num_pairs(orc_engine* o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
