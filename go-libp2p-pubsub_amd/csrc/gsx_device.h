@@ -35,32 +35,56 @@ struct DevPeerParams {
     int64_t retain_ns;
 };
 
-// Pointers to the structure-of-arrays state in HBM.  Record arrays are
-// topic-major, element [t * rs + p] with the row stride rs = n_pairs rounded
-// up to a multiple of 64 (every topic row starts 512-B aligned for f64).
+// Topic parameters travel in the kernel argument segment for up to
+// KARG_TOPICS topics, so every read is a scalar (s_load) from the kernarg
+// buffer; larger engines read them through a read-only global pointer.
+constexpr int KARG_TOPICS = 8;
+struct KernParams {
+    DevPeerParams pp;
+    DevTopicParams tp[KARG_TOPICS];
+};
+
+// ---- HBM layout of the per-record state ------------------------------------
+// Records (one per observer, peer, topic: the reference's topicStats,
+// score.go:37-62) are tiled by 64 pairs — one wavefront's lanes:
+//   rec   [p/64][t][field][64]  8-byte fields, field = FMD, MMD, MFP, IMD, GRAFT
+//   rflag [p/64][t][64]         u8: IN_MESH | ACTIVE | FRESH
+// so the lanes of a wave read each field of a topic as one contiguous 512-B
+// span and a wave's whole working set (T x 2.6 KB) is one contiguous block
+// of HBM.  meshTime is not stored: for an in-mesh record it is
+// FRESH ? 0 : (last refresh time - graftTime), which is exactly what
+// refreshScores() would have written (score.go:544-546; Graft zeroes it,
+// score.go:658).
+constexpr int TILE = 64;
+constexpr int NFIELD = 5;
+enum Field { FMD = 0, MMD = 1, MFP = 2, IMD = 3, GRAFT = 4 };
+
+__host__ __device__ __forceinline__ size_t rec_index(uint64_t p, uint32_t t, uint32_t n_topics, int field) {
+    return (((p / TILE) * n_topics + t) * NFIELD + field) * TILE + (p % TILE);
+}
+__host__ __device__ __forceinline__ size_t flag_index(uint64_t p, uint32_t t, uint32_t n_topics) {
+    return ((p / TILE) * n_topics + t) * TILE + (p % TILE);
+}
+
 struct DevState {
-    double* fmd;
-    double* mmd;
-    double* mfp;
-    double* imd;
-    int64_t* graft;
-    int64_t* mtime;
-    uint8_t* rflags;
-    uint8_t* pflags;
-    int64_t* expire;
-    double* bp;
-    const double* app;
+    double* rec;          // tiled records (GRAFT slot holds int64 bits)
+    uint8_t* rflags;      // tiled record flags
+    uint8_t* pflags;      // per pair: PRESENT | CONNECTED
+    int64_t* expire;      // per pair: retention expiry
+    double* bp;           // per pair: behaviourPenalty
+    const double* app;    // per pair: AppSpecificScore snapshot
     const uint32_t* ipg;  // 2 per pair: (observer, ip) group id | WL bit, or NONE
     uint32_t* ipcount;    // per group: number of present pairs carrying it
-    double* score;
-    const DevTopicParams* tp;
+    double* score;        // per pair: output
+    const DevTopicParams* tp;  // all topics (used when n_topics > KARG_TOPICS)
     uint64_t n_pairs;
-    uint64_t rs;
     uint32_t n_topics;
+    int64_t last_refresh;  // time of the last refreshScores() (derives meshTime)
 };
 
 constexpr uint8_t REC_IN_MESH = 0x01;
 constexpr uint8_t REC_ACTIVE = 0x02;
+constexpr uint8_t REC_FRESH = 0x04;  // grafted since the last refresh that covered it: meshTime == 0
 constexpr uint8_t PAIR_PRESENT = 0x01;
 constexpr uint8_t PAIR_CONNECTED = 0x02;
 constexpr uint32_t IPG_NONE = 0xFFFFFFFFu;
@@ -75,18 +99,6 @@ struct DevEvent {
     int64_t arg;
 };
 
-}  // namespace gsx
-
-// launchers (gsx_kernels.hip)
-namespace gsx {
-hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
-hipError_t launch_refresh_score(const DevState& s, const DevPeerParams& pp, int64_t now, bool refresh,
-                                hipStream_t st);
-hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
-                               const uint32_t* group_off, uint32_t n_groups, hipStream_t st);
-hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st);
-hipError_t launch_rebuild_ipcount(const DevState& s, uint32_t n_groups_ip, hipStream_t st);
-
 struct DevSynthSpec {
     uint64_t seed;
     int64_t now;
@@ -97,5 +109,23 @@ struct DevSynthSpec {
     int64_t expire_jitter;
     uint32_t sybil_first;
 };
+
+// ---- launchers (gsx_kernels.hip) ---------------------------------------------
+hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
+hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st);
+hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
+                               const uint32_t* group_off, uint32_t n_groups, hipStream_t st);
+hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st);
+hipError_t launch_rebuild_ipcount(const DevState& s, uint32_t n_groups_ip, hipStream_t st);
 hipError_t launch_synthesize(const DevState& s, const int32_t* col, const DevSynthSpec& spec, hipStream_t st);
+// Topic-major <-> tiled permutation of one record field (import / export).
+// field < NFIELD: 8-byte field; field == NFIELD: the u8 flags (FRESH dropped
+// on export, recomputed on import from mesh_time == 0); mesh_time is handled
+// by launch_mesh_time_{export,import}.
+hipError_t launch_tile_field(const DevState& s, int field, const void* topic_major, hipStream_t st);
+hipError_t launch_untile_field(const DevState& s, int field, void* topic_major, hipStream_t st);
+hipError_t launch_mesh_time_export(const DevState& s, int64_t* topic_major, hipStream_t st);
+// Sets FRESH on in-mesh records whose imported meshTime is 0; counts records
+// whose meshTime is neither 0 nor last_refresh - graftTime into *n_bad.
+hipError_t launch_mesh_time_import(const DevState& s, const int64_t* topic_major, uint32_t* n_bad, hipStream_t st);
 }  // namespace gsx

@@ -71,7 +71,8 @@ struct gsx_engine {
     // overlay
     bool loaded = false;
     uint32_t n_nodes = 0;
-    uint64_t E = 0, rs = 0;
+    uint64_t E = 0, rs = 0, n_tiles = 0;
+    int64_t last_refresh = 0;  // now of the last refreshScores() pass
     std::vector<int64_t> row_ptr;
     std::vector<uint32_t> pair_obs;
     std::vector<uint32_t> ipg_host;  // 2 per pair, without WL bits
@@ -80,9 +81,10 @@ struct gsx_engine {
     uint32_t n_groups = 0;
 
     // device state
-    double *d_fmd = nullptr, *d_mmd = nullptr, *d_mfp = nullptr, *d_imd = nullptr;
-    int64_t *d_graft = nullptr, *d_mtime = nullptr;
-    uint8_t* d_rflags = nullptr;
+    double* d_rec = nullptr;      // tiled records, gsx_device.h
+    uint8_t* d_rflags = nullptr;  // tiled record flags
+    void* d_tmp = nullptr;        // import/export staging of one topic-major field
+    uint32_t* d_nbad = nullptr;
     uint8_t *d_pflags = nullptr, *d_eflags = nullptr;
     int64_t* d_expire = nullptr;
     double *d_bp = nullptr, *d_app = nullptr, *d_score = nullptr;
@@ -125,12 +127,7 @@ int fail(gsx_engine* e, int code, const std::string& msg) {
 
 gsx::DevState dev_state(const gsx_engine* e) {
     gsx::DevState s{};
-    s.fmd = e->d_fmd;
-    s.mmd = e->d_mmd;
-    s.mfp = e->d_mfp;
-    s.imd = e->d_imd;
-    s.graft = e->d_graft;
-    s.mtime = e->d_mtime;
+    s.rec = e->d_rec;
     s.rflags = e->d_rflags;
     s.pflags = e->d_pflags;
     s.expire = e->d_expire;
@@ -141,8 +138,8 @@ gsx::DevState dev_state(const gsx_engine* e) {
     s.score = e->d_score;
     s.tp = e->d_tp;
     s.n_pairs = e->E;
-    s.rs = e->rs;
     s.n_topics = e->T;
+    s.last_refresh = e->last_refresh;
     return s;
 }
 
@@ -160,31 +157,42 @@ gsx::DevPeerParams dev_peer_params(const gsx_engine* e) {
     return d;
 }
 
+gsx::DevTopicParams dev_topic_params(const gsx_engine* e, uint32_t t);
+
+gsx::KernParams kern_params(const gsx_engine* e) {
+    gsx::KernParams k{};
+    k.pp = dev_peer_params(e);
+    for (uint32_t t = 0; t < e->T && t < (uint32_t)gsx::KARG_TOPICS; ++t) k.tp[t] = dev_topic_params(e, t);
+    return k;
+}
+
+gsx::DevTopicParams dev_topic_params(const gsx_engine* e, uint32_t t) {
+    gsx::DevTopicParams d{};
+    const gsx_topic_score_params& p = e->tp[t];
+    d.topic_weight = p.topic_weight;
+    d.w1 = p.time_in_mesh_weight;
+    d.cap1 = p.time_in_mesh_cap;
+    d.q1 = e->scored[t] ? p.time_in_mesh_quantum_ns : 1;  // unscored topics are skipped, never divided by
+    d.w2 = p.first_message_deliveries_weight;
+    d.d2 = p.first_message_deliveries_decay;
+    d.cap2 = p.first_message_deliveries_cap;
+    d.w3 = p.mesh_message_deliveries_weight;
+    d.d3 = p.mesh_message_deliveries_decay;
+    d.cap3 = p.mesh_message_deliveries_cap;
+    d.thr3 = p.mesh_message_deliveries_threshold;
+    d.win3 = p.mesh_message_deliveries_window_ns;
+    d.act3 = p.mesh_message_deliveries_activation_ns;
+    d.w3b = p.mesh_failure_penalty_weight;
+    d.d3b = p.mesh_failure_penalty_decay;
+    d.w4 = p.invalid_message_deliveries_weight;
+    d.d4 = p.invalid_message_deliveries_decay;
+    d.scored = e->scored[t] ? 1 : 0;
+    return d;
+}
+
 int upload_topic_params(gsx_engine* e) {
     gsx::DevTopicParams h[GSX_MAX_TOPICS]{};
-    for (uint32_t t = 0; t < e->T; ++t) {
-        const gsx_topic_score_params& p = e->tp[t];
-        gsx::DevTopicParams& d = h[t];
-        d.topic_weight = p.topic_weight;
-        d.w1 = p.time_in_mesh_weight;
-        d.cap1 = p.time_in_mesh_cap;
-        d.q1 = p.time_in_mesh_quantum_ns;
-        d.w2 = p.first_message_deliveries_weight;
-        d.d2 = p.first_message_deliveries_decay;
-        d.cap2 = p.first_message_deliveries_cap;
-        d.w3 = p.mesh_message_deliveries_weight;
-        d.d3 = p.mesh_message_deliveries_decay;
-        d.cap3 = p.mesh_message_deliveries_cap;
-        d.thr3 = p.mesh_message_deliveries_threshold;
-        d.win3 = p.mesh_message_deliveries_window_ns;
-        d.act3 = p.mesh_message_deliveries_activation_ns;
-        d.w3b = p.mesh_failure_penalty_weight;
-        d.d3b = p.mesh_failure_penalty_decay;
-        d.w4 = p.invalid_message_deliveries_weight;
-        d.d4 = p.invalid_message_deliveries_decay;
-        d.scored = e->scored[t] ? 1 : 0;
-        if (!e->scored[t]) d.q1 = 1;  // never divided by: unscored topics are skipped
-    }
+    for (uint32_t t = 0; t < e->T; ++t) h[t] = dev_topic_params(e, t);
     HIPCHK(e, hipMemcpyAsync(e->d_tp, h, sizeof(gsx::DevTopicParams) * GSX_MAX_TOPICS, hipMemcpyHostToDevice,
                              e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));  // `h` is on the stack
@@ -192,13 +200,14 @@ int upload_topic_params(gsx_engine* e) {
 }
 
 void free_state(gsx_engine* e) {
-    void* ptrs[] = {e->d_fmd,   e->d_mmd,    e->d_mfp,    e->d_imd, e->d_graft, e->d_mtime,
-                    e->d_rflags, e->d_pflags, e->d_eflags, e->d_expire, e->d_bp,  e->d_app,
-                    e->d_score, e->d_ipg,    e->d_ipcount, e->d_col};
+    void* ptrs[] = {e->d_rec,    e->d_rflags, e->d_tmp, e->d_nbad,    e->d_pflags, e->d_eflags,
+                    e->d_expire, e->d_bp,     e->d_app, e->d_score,   e->d_ipg,    e->d_ipcount,
+                    e->d_col};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    e->d_fmd = e->d_mmd = e->d_mfp = e->d_imd = nullptr;
-    e->d_graft = e->d_mtime = nullptr;
+    e->d_rec = nullptr;
+    e->d_tmp = nullptr;
+    e->d_nbad = nullptr;
     e->d_rflags = e->d_pflags = e->d_eflags = nullptr;
     e->d_expire = nullptr;
     e->d_bp = e->d_app = e->d_score = nullptr;
@@ -211,6 +220,20 @@ int dalloc(gsx_engine* e, T** p, size_t n) {
     hipError_t st = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
     if (st != hipSuccess) return fail(e, GSX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(st));
     return GSX_OK;
+}
+
+// Staging buffer for one topic-major record field (import / export only).
+int ensure_tmp(gsx_engine* e) {
+    if (e->d_tmp) return GSX_OK;
+    const size_t bytes = 8 * (size_t)e->T * (e->E ? e->E : 1);
+    hipError_t st = hipMalloc(&e->d_tmp, bytes);
+    if (st != hipSuccess) return fail(e, GSX_ENOMEM, std::string("hipMalloc(staging): ") + hipGetErrorString(st));
+    return GSX_OK;
+}
+
+void release_tmp(gsx_engine* e) {
+    if (e->d_tmp) (void)hipFree(e->d_tmp);
+    e->d_tmp = nullptr;
 }
 
 int upload_ipg(gsx_engine* e) {
@@ -295,7 +318,7 @@ int ensure_scores(gsx_engine* e) {
     int rc = flush(e);
     if (rc) return rc;
     if (!e->scores_valid) {
-        HIPCHK(e, gsx::launch_refresh_score(dev_state(e), dev_peer_params(e), 0, false, e->stream));
+        HIPCHK(e, gsx::launch_refresh_score(dev_state(e), kern_params(e), 0, false, e->stream));
         e->scores_valid = true;
     }
     return GSX_OK;
@@ -531,6 +554,8 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     e->n_nodes = n_nodes;
     e->E = E;
     e->rs = (E + 63) & ~uint64_t(63);
+    e->n_tiles = (E + gsx::TILE - 1) / gsx::TILE;
+    e->last_refresh = 0;
     e->row_ptr.assign(row_ptr, row_ptr + n_nodes + 1);
     e->pair_obs.resize(E);
     for (uint32_t i = 0; i < n_nodes; ++i)
@@ -577,11 +602,10 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     }
     e->n_groups = next;
 
-    const size_t R = (size_t)e->T * e->rs;
+    const size_t R = (size_t)e->T * e->n_tiles * gsx::TILE;  // record slots, tail of the last tile unused
     int rc = 0;
-    if ((rc = dalloc(e, &e->d_fmd, R)) || (rc = dalloc(e, &e->d_mmd, R)) || (rc = dalloc(e, &e->d_mfp, R)) ||
-        (rc = dalloc(e, &e->d_imd, R)) || (rc = dalloc(e, &e->d_graft, R)) || (rc = dalloc(e, &e->d_mtime, R)) ||
-        (rc = dalloc(e, &e->d_rflags, R)) || (rc = dalloc(e, &e->d_pflags, e->rs)) ||
+    if ((rc = dalloc(e, &e->d_rec, R * gsx::NFIELD)) || (rc = dalloc(e, &e->d_rflags, R)) ||
+        (rc = dalloc(e, &e->d_nbad, 1)) || (rc = dalloc(e, &e->d_pflags, e->rs)) ||
         (rc = dalloc(e, &e->d_eflags, e->rs)) || (rc = dalloc(e, &e->d_expire, e->rs)) ||
         (rc = dalloc(e, &e->d_bp, e->rs)) || (rc = dalloc(e, &e->d_app, e->rs)) ||
         (rc = dalloc(e, &e->d_score, e->rs)) || (rc = dalloc(e, &e->d_ipg, 2 * e->rs)) ||
@@ -589,12 +613,7 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
         free_state(e);
         return rc;
     }
-    HIPCHK(e, hipMemsetAsync(e->d_fmd, 0, sizeof(double) * R, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_mmd, 0, sizeof(double) * R, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_mfp, 0, sizeof(double) * R, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_imd, 0, sizeof(double) * R, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_graft, 0, sizeof(int64_t) * R, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_mtime, 0, sizeof(int64_t) * R, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_rec, 0, sizeof(double) * R * gsx::NFIELD, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_rflags, 0, R, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_pflags, 0, e->rs, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_expire, 0, sizeof(int64_t) * e->rs, e->stream));
@@ -771,11 +790,12 @@ int gsx_refresh(gsx_engine* e, int64_t now) {
     HIPCHK(e, gsx::launch_purge(s, now, e->stream));
     const bool region = e->t_active && e->t_used < e->t_max;
     HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used] : e->ev_start, e->stream));
-    HIPCHK(e, gsx::launch_refresh_score(s, dev_peer_params(e), now, true, e->stream));
+    HIPCHK(e, gsx::launch_refresh_score(s, kern_params(e), now, true, e->stream));
     HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used + 1] : e->ev_stop, e->stream));
     if (region) ++e->t_used;
     e->timed = !region;
     e->scores_valid = true;
+    e->last_refresh = now;
     return GSX_OK;
 }
 
@@ -863,23 +883,32 @@ int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
         !s->pair_flags || !s->expire_ns || !s->behaviour_penalty)
         return fail(e, GSX_EINVAL, "import needs every state array");
     if (int rc = flush(e)) return rc;
-    const size_t E = e->E;
-    for (uint32_t t = 0; t < e->T; ++t) {
-        const size_t src = (size_t)t * E, dst = (size_t)t * e->rs;
-        HIPCHK(e, hipMemcpyAsync(e->d_fmd + dst, s->first_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_mmd + dst, s->mesh_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_mfp + dst, s->mesh_failure_penalty + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_imd + dst, s->invalid_message_deliveries + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_graft + dst, s->graft_time_ns + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_mtime + dst, s->mesh_time_ns + src, 8 * E, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_rflags + dst, s->rec_flags + src, E, hipMemcpyHostToDevice, e->stream));
+    const size_t E = e->E, R = (size_t)e->T * E;
+    if (int rc = ensure_tmp(e)) return rc;
+    e->last_refresh = s->last_refresh_ns;
+    const gsx::DevState ds = dev_state(e);
+    const void* fields[gsx::NFIELD] = {s->first_message_deliveries, s->mesh_message_deliveries,
+                                       s->mesh_failure_penalty, s->invalid_message_deliveries, s->graft_time_ns};
+    for (int f = 0; f < gsx::NFIELD; ++f) {
+        HIPCHK(e, hipMemcpyAsync(e->d_tmp, fields[f], 8 * R, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, gsx::launch_tile_field(ds, f, e->d_tmp, e->stream));
     }
+    HIPCHK(e, hipMemcpyAsync(e->d_tmp, s->rec_flags, R, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, gsx::launch_tile_field(ds, gsx::NFIELD, e->d_tmp, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_nbad, 0, sizeof(uint32_t), e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_tmp, s->mesh_time_ns, 8 * R, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, gsx::launch_mesh_time_import(ds, static_cast<const int64_t*>(e->d_tmp), e->d_nbad, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->d_pflags, s->pair_flags, E, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->d_expire, s->expire_ns, 8 * E, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->d_bp, s->behaviour_penalty, 8 * E, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, gsx::launch_rebuild_ipcount(dev_state(e), e->n_groups, e->stream));
+    HIPCHK(e, gsx::launch_rebuild_ipcount(ds, e->n_groups, e->stream));
+    uint32_t n_bad = 0;
+    HIPCHK(e, hipMemcpyAsync(&n_bad, e->d_nbad, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    release_tmp(e);
     e->scores_valid = false;
+    if (n_bad) return fail(e, GSX_EINVAL, std::to_string(n_bad) + " in-mesh records have a meshTime that is neither 0 "
+                                          "nor last_refresh_ns - graftTime");
     return GSX_OK;
 }
 
@@ -901,6 +930,7 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     d.p_abs = sp->p_absent;
     d.expire_jitter = sp->expire_jitter_ns;
     d.sybil_first = sp->sybil_first_node;
+    e->last_refresh = sp->now_ns;  // meshTime = now - graftTime for every in-mesh record
     const gsx::DevState s = dev_state(e);
     HIPCHK(e, gsx::launch_synthesize(s, e->d_col, d, e->stream));
     HIPCHK(e, gsx::launch_rebuild_ipcount(s, e->n_groups, e->stream));
@@ -909,32 +939,34 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     return GSX_OK;
 }
 
-int gsx_export_state(gsx_engine* e, const gsx_state_view* s) {
+int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
     if (!e || !s) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (int rc = flush(e)) return rc;
-    const size_t E = e->E;
-    for (uint32_t t = 0; t < e->T; ++t) {
-        const size_t dst = (size_t)t * E, src = (size_t)t * e->rs;
-        if (s->first_message_deliveries)
-            HIPCHK(e, hipMemcpyAsync(s->first_message_deliveries + dst, e->d_fmd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->mesh_message_deliveries)
-            HIPCHK(e, hipMemcpyAsync(s->mesh_message_deliveries + dst, e->d_mmd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->mesh_failure_penalty)
-            HIPCHK(e, hipMemcpyAsync(s->mesh_failure_penalty + dst, e->d_mfp + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->invalid_message_deliveries)
-            HIPCHK(e, hipMemcpyAsync(s->invalid_message_deliveries + dst, e->d_imd + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->graft_time_ns)
-            HIPCHK(e, hipMemcpyAsync(s->graft_time_ns + dst, e->d_graft + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->mesh_time_ns)
-            HIPCHK(e, hipMemcpyAsync(s->mesh_time_ns + dst, e->d_mtime + src, 8 * E, hipMemcpyDeviceToHost, e->stream));
-        if (s->rec_flags)
-            HIPCHK(e, hipMemcpyAsync(s->rec_flags + dst, e->d_rflags + src, E, hipMemcpyDeviceToHost, e->stream));
+    const size_t E = e->E, R = (size_t)e->T * E;
+    if (int rc = ensure_tmp(e)) return rc;
+    const gsx::DevState ds = dev_state(e);
+    void* fields[gsx::NFIELD] = {s->first_message_deliveries, s->mesh_message_deliveries, s->mesh_failure_penalty,
+                                 s->invalid_message_deliveries, s->graft_time_ns};
+    for (int f = 0; f < gsx::NFIELD; ++f) {
+        if (!fields[f]) continue;
+        HIPCHK(e, gsx::launch_untile_field(ds, f, e->d_tmp, e->stream));
+        HIPCHK(e, hipMemcpyAsync(fields[f], e->d_tmp, 8 * R, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (s->mesh_time_ns) {
+        HIPCHK(e, gsx::launch_mesh_time_export(ds, static_cast<int64_t*>(e->d_tmp), e->stream));
+        HIPCHK(e, hipMemcpyAsync(s->mesh_time_ns, e->d_tmp, 8 * R, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (s->rec_flags) {
+        HIPCHK(e, gsx::launch_untile_field(ds, gsx::NFIELD, e->d_tmp, e->stream));
+        HIPCHK(e, hipMemcpyAsync(s->rec_flags, e->d_tmp, R, hipMemcpyDeviceToHost, e->stream));
     }
     if (s->pair_flags) HIPCHK(e, hipMemcpyAsync(s->pair_flags, e->d_pflags, E, hipMemcpyDeviceToHost, e->stream));
     if (s->expire_ns) HIPCHK(e, hipMemcpyAsync(s->expire_ns, e->d_expire, 8 * E, hipMemcpyDeviceToHost, e->stream));
     if (s->behaviour_penalty) HIPCHK(e, hipMemcpyAsync(s->behaviour_penalty, e->d_bp, 8 * E, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    release_tmp(e);
+    s->last_refresh_ns = e->last_refresh;
     return GSX_OK;
 }
 

@@ -2,10 +2,11 @@
 //
 // Hot path: k_refresh_score, one streaming pass that fuses refreshScores()
 // (score.go:497-558) with score() (score.go:258-335) for every
-// (observer, peer) pair.  HBM-bound integer/FP64 byte work: no MFMA, no LDS;
-// what matters is that every load and store of a wave is one coalesced
-// contiguous span (lane l owns consecutive pairs) and that enough loads are in
-// flight per CU.
+// (observer, peer) pair.  HBM-bound FP64/integer byte work: no MFMA, no LDS.
+// Lane l of a wave owns pair 64*w + l; the records of a wave's 64 pairs form
+// one contiguous tile (gsx_device.h), so every load and store instruction moves
+// one contiguous 512-B span and a wave streams a single HBM block.  Topic
+// parameters are read from the kernel-argument segment (scalar loads).
 //
 // Build with -ffp-contract=off: each expression is evaluated with the
 // reference's roundings (Go on amd64 does not fuse multiply-add), which is what
@@ -14,7 +15,7 @@
 
 namespace gsx {
 
-// ---- shared pieces ---------------------------------------------------------
+// ---- shared arithmetic -------------------------------------------------------
 
 // P6, ipColocationFactor (score.go:337-381) from the per-(observer, IP) count
 // of present pairs (the size of ps.peerIPs[ip]).
@@ -79,19 +80,25 @@ __device__ __forceinline__ double topic_score(const DevTopicParams& tp, uint8_t 
     return ts * tp.topic_weight;
 }
 
-// score(p) from the stored state, no refresh (used by RemovePeer).
-template <int TT>
+// meshTime of a stored record: FRESH (grafted, not refreshed since) -> 0,
+// else the value the last refresh computed (score.go:544-546).
+__device__ __forceinline__ int64_t mesh_time_of(const DevState& s, uint8_t fl, uint64_t p, uint32_t t) {
+    if (!(fl & REC_IN_MESH) || (fl & REC_FRESH)) return 0;
+    const int64_t graft = reinterpret_cast<const int64_t*>(s.rec)[rec_index(p, t, s.n_topics, GRAFT)];
+    return s.last_refresh - graft;
+}
+
+// score(p) from the stored state, no refresh (RemovePeer, score.go:615).
 __device__ double eval_pair(const DevState& s, const DevPeerParams& pp, uint64_t p) {
     if (!(s.pflags[p] & PAIR_PRESENT)) return 0.0;
-    const int T = TT > 0 ? TT : (int)s.n_topics;
     double score = 0.0;
-    for (int t = 0; t < T; ++t) {
+    for (uint32_t t = 0; t < s.n_topics; ++t) {
         const DevTopicParams& tp = s.tp[t];
         if (!tp.scored) continue;
-        const size_t r = (size_t)t * s.rs + p;
-        const uint8_t fl = s.rflags[r];
-        const int64_t mt = (fl & REC_IN_MESH) ? s.mtime[r] : 0;
-        score += topic_score(tp, fl, mt, s.fmd[r], s.mmd[r], s.mfp[r], s.imd[r]);
+        const uint8_t fl = s.rflags[flag_index(p, t, s.n_topics)];
+        const size_t b = rec_index(p, t, s.n_topics, FMD);
+        score += topic_score(tp, fl, mesh_time_of(s, fl, p, t), s.rec[b], s.rec[b + MMD * TILE],
+                             s.rec[b + MFP * TILE], s.rec[b + IMD * TILE]);
     }
     return score_tail(s, pp, p, score, s.bp[p]);
 }
@@ -104,8 +111,14 @@ __device__ __forceinline__ double decay(double x, double d, double dtz) {
     return x < dtz ? 0.0 : x;
 }
 
+template <int TT>
+__device__ __forceinline__ const DevTopicParams& topic_params(const KernParams& kp, const DevState& s, int t) {
+    if constexpr (TT > 0) return kp.tp[t];
+    else return s.tp[t];
+}
+
 template <int TT, bool REFRESH>
-__global__ __launch_bounds__(256) void k_refresh_score(DevState s, DevPeerParams pp, int64_t now) {
+__global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp, int64_t now) {
     const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (p >= s.n_pairs) return;
     const uint8_t st = s.pflags[p];
@@ -113,37 +126,42 @@ __global__ __launch_bounds__(256) void k_refresh_score(DevState s, DevPeerParams
         s.score[p] = 0.0;
         return;
     }
+    const DevPeerParams& pp = kp.pp;
     // Disconnected (retained) peers are not decayed (:503-516).
     const bool conn = REFRESH && (st & PAIR_CONNECTED);
     const int T = TT > 0 ? TT : (int)s.n_topics;
+    const uint64_t lane = p % TILE;
+    double* const tile = s.rec + (p / TILE) * (uint64_t)T * (NFIELD * TILE) + lane;
+    uint8_t* const ftile = s.rflags + (p / TILE) * (uint64_t)T * TILE + lane;
     double score = 0.0;
     for (int t = 0; t < T; ++t) {  // constant trip count for TT > 0: fully unrolled
-        const DevTopicParams& tp = s.tp[t];
+        const DevTopicParams& tp = topic_params<TT>(kp, s, t);
         if (!tp.scored) continue;
-        const size_t r = (size_t)t * s.rs + p;
-        double fmd = s.fmd[r];
-        double mmd = s.mmd[r];
-        double mfp = s.mfp[r];
-        double imd = s.imd[r];
-        uint8_t fl = s.rflags[r];
+        double* const r = tile + (uint64_t)t * (NFIELD * TILE);
+        double fmd = r[FMD * TILE];
+        double mmd = r[MMD * TILE];
+        double mfp = r[MFP * TILE];
+        double imd = r[IMD * TILE];
+        uint8_t fl = ftile[t * TILE];
         int64_t mt = 0;
         if (conn) {
             fmd = decay(fmd, tp.d2, pp.decay_to_zero);
             mmd = decay(mmd, tp.d3, pp.decay_to_zero);
             mfp = decay(mfp, tp.d3b, pp.decay_to_zero);
             imd = decay(imd, tp.d4, pp.decay_to_zero);
-            s.fmd[r] = fmd;
-            s.mmd[r] = mmd;
-            s.mfp[r] = mfp;
-            s.imd[r] = imd;
+            r[FMD * TILE] = fmd;
+            r[MMD * TILE] = mmd;
+            r[MFP * TILE] = mfp;
+            r[IMD * TILE] = imd;
+            uint8_t nf = fl & ~REC_FRESH;
             if (fl & REC_IN_MESH) {  // :544-549
-                mt = now - s.graft[r];
-                if (mt > tp.act3) fl |= REC_ACTIVE;
-                s.mtime[r] = mt;
-                s.rflags[r] = fl;
+                mt = now - reinterpret_cast<const int64_t*>(r)[GRAFT * TILE];
+                if (mt > tp.act3) nf |= REC_ACTIVE;
             }
-        } else if (fl & REC_IN_MESH) {
-            mt = s.mtime[r];
+            if (nf != fl) ftile[t * TILE] = nf;  // rare once the mesh is steady
+            fl = nf;
+        } else if ((fl & REC_IN_MESH) && !(fl & REC_FRESH)) {
+            mt = s.last_refresh - reinterpret_cast<const int64_t*>(r)[GRAFT * TILE];
         }
         score += topic_score(tp, fl, mt, fmd, mmd, mfp, imd);
     }
@@ -177,18 +195,17 @@ __device__ __forceinline__ void ipcount_add(const DevState& s, uint64_t p, int d
     if (g.y != IPG_NONE && g.y != g.x) s.ipcount[g.y & ~IPG_WL] += (uint32_t)delta;
 }
 
+__device__ __forceinline__ bool scored_topic(const DevState& s, uint64_t p, uint32_t topic) {
+    return (s.pflags[p] & PAIR_PRESENT) && topic < s.n_topics && s.tp[topic].scored;
+}
+
 __device__ void ev_add_peer(const DevState& s, uint64_t p) {  // AddPeer :588-602
     const uint8_t st = s.pflags[p];
     if (!(st & PAIR_PRESENT)) {  // new peerStats{topics: {}}
         for (uint32_t t = 0; t < s.n_topics; ++t) {
-            const size_t r = (size_t)t * s.rs + p;
-            s.fmd[r] = 0.0;
-            s.mmd[r] = 0.0;
-            s.mfp[r] = 0.0;
-            s.imd[r] = 0.0;
-            s.graft[r] = 0;
-            s.mtime[r] = 0;
-            s.rflags[r] = 0;
+            const size_t b = rec_index(p, t, s.n_topics, FMD);
+            for (int f = 0; f < NFIELD; ++f) s.rec[b + f * TILE] = 0.0;
+            s.rflags[flag_index(p, t, s.n_topics)] = 0;
         }
         s.bp[p] = 0.0;
         s.expire[p] = 0;
@@ -200,7 +217,7 @@ __device__ void ev_add_peer(const DevState& s, uint64_t p) {  // AddPeer :588-60
 __device__ void ev_remove_peer(const DevState& s, const DevPeerParams& pp, uint64_t p, int64_t now) {  // :604-637
     const uint8_t st = s.pflags[p];
     if (!(st & PAIR_PRESENT)) return;
-    if (eval_pair<0>(s, pp, p) > 0) {  // positive score: forget the peer
+    if (eval_pair(s, pp, p) > 0) {  // positive score: forget the peer
         ipcount_add(s, p, -1);
         s.pflags[p] = 0;
         return;
@@ -208,68 +225,68 @@ __device__ void ev_remove_peer(const DevState& s, const DevPeerParams& pp, uint6
     for (uint32_t t = 0; t < s.n_topics; ++t) {
         const DevTopicParams& tp = s.tp[t];
         if (!tp.scored) continue;
-        const size_t r = (size_t)t * s.rs + p;
-        s.fmd[r] = 0.0;
-        uint8_t fl = s.rflags[r];
+        const size_t b = rec_index(p, t, s.n_topics, FMD);
+        const size_t fi = flag_index(p, t, s.n_topics);
+        s.rec[b + FMD * TILE] = 0.0;
+        const uint8_t fl = s.rflags[fi];
         const double threshold = tp.thr3;
-        const double mmd = s.mmd[r];
+        const double mmd = s.rec[b + MMD * TILE];
         if ((fl & REC_IN_MESH) && (fl & REC_ACTIVE) && mmd < threshold) {
             const double deficit = threshold - mmd;
-            s.mfp[r] = s.mfp[r] + deficit * deficit;
+            s.rec[b + MFP * TILE] = s.rec[b + MFP * TILE] + deficit * deficit;
         }
-        s.rflags[r] = fl & ~REC_IN_MESH;
+        s.rflags[fi] = fl & ~(REC_IN_MESH | REC_FRESH);
     }
     s.pflags[p] = PAIR_PRESENT;
     s.expire[p] = now + pp.retain_ns;
 }
 
 __device__ void ev_graft(const DevState& s, uint64_t p, uint32_t topic, int64_t now) {  // :642-660
-    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
-    const size_t r = (size_t)topic * s.rs + p;
-    s.rflags[r] = REC_IN_MESH;
-    s.graft[r] = now;
-    s.mtime[r] = 0;
+    if (!scored_topic(s, p, topic)) return;
+    reinterpret_cast<int64_t*>(s.rec)[rec_index(p, topic, s.n_topics, GRAFT)] = now;
+    s.rflags[flag_index(p, topic, s.n_topics)] = REC_IN_MESH | REC_FRESH;  // meshTime = 0, not active
 }
 
 __device__ void ev_prune(const DevState& s, uint64_t p, uint32_t topic) {  // :662-684
-    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
-    const size_t r = (size_t)topic * s.rs + p;
-    const uint8_t fl = s.rflags[r];
+    if (!scored_topic(s, p, topic)) return;
+    const size_t b = rec_index(p, topic, s.n_topics, FMD);
+    const size_t fi = flag_index(p, topic, s.n_topics);
+    const uint8_t fl = s.rflags[fi];
     const double threshold = s.tp[topic].thr3;
-    const double mmd = s.mmd[r];
+    const double mmd = s.rec[b + MMD * TILE];
     if ((fl & REC_ACTIVE) && mmd < threshold) {
         const double deficit = threshold - mmd;
-        s.mfp[r] = s.mfp[r] + deficit * deficit;
+        s.rec[b + MFP * TILE] = s.rec[b + MFP * TILE] + deficit * deficit;
     }
-    s.rflags[r] = fl & ~REC_IN_MESH;
+    s.rflags[fi] = fl & ~(REC_IN_MESH | REC_FRESH);
 }
 
 __device__ void ev_first(const DevState& s, uint64_t p, uint32_t topic) {  // :912-939
-    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
+    if (!scored_topic(s, p, topic)) return;
     const DevTopicParams& tp = s.tp[topic];
-    const size_t r = (size_t)topic * s.rs + p;
-    double f = s.fmd[r] + 1;
+    const size_t b = rec_index(p, topic, s.n_topics, FMD);
+    double f = s.rec[b + FMD * TILE] + 1;
     if (f > tp.cap2) f = tp.cap2;
-    s.fmd[r] = f;
-    if (!(s.rflags[r] & REC_IN_MESH)) return;
-    double m = s.mmd[r] + 1;
+    s.rec[b + FMD * TILE] = f;
+    if (!(s.rflags[flag_index(p, topic, s.n_topics)] & REC_IN_MESH)) return;
+    double m = s.rec[b + MMD * TILE] + 1;
     if (m > tp.cap3) m = tp.cap3;
-    s.mmd[r] = m;
+    s.rec[b + MMD * TILE] = m;
 }
 
 __device__ void ev_mesh(const DevState& s, uint64_t p, uint32_t topic) {  // :944-974 (window checked on host)
-    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
-    const size_t r = (size_t)topic * s.rs + p;
-    if (!(s.rflags[r] & REC_IN_MESH)) return;
-    double m = s.mmd[r] + 1;
+    if (!scored_topic(s, p, topic)) return;
+    if (!(s.rflags[flag_index(p, topic, s.n_topics)] & REC_IN_MESH)) return;
+    const size_t b = rec_index(p, topic, s.n_topics, MMD);
+    double m = s.rec[b] + 1;
     if (m > s.tp[topic].cap3) m = s.tp[topic].cap3;
-    s.mmd[r] = m;
+    s.rec[b] = m;
 }
 
 __device__ void ev_invalid(const DevState& s, uint64_t p, uint32_t topic) {  // :894-907
-    if (!(s.pflags[p] & PAIR_PRESENT) || topic >= s.n_topics || !s.tp[topic].scored) return;
-    const size_t r = (size_t)topic * s.rs + p;
-    s.imd[r] = s.imd[r] + 1;
+    if (!scored_topic(s, p, topic)) return;
+    const size_t b = rec_index(p, topic, s.n_topics, IMD);
+    s.rec[b] = s.rec[b] + 1;
 }
 
 __device__ void ev_penalty(const DevState& s, uint64_t p, int64_t count) {  // AddPenalty :384-398
@@ -304,9 +321,9 @@ __global__ __launch_bounds__(64) void k_apply_events(DevState s, DevPeerParams p
 __global__ __launch_bounds__(256) void k_recap(DevState s, uint32_t topic, double cap2, double cap3) {
     const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (p >= s.n_pairs || !(s.pflags[p] & PAIR_PRESENT)) return;
-    const size_t r = (size_t)topic * s.rs + p;
-    if (s.fmd[r] > cap2) s.fmd[r] = cap2;
-    if (s.mmd[r] > cap3) s.mmd[r] = cap3;
+    const size_t b = rec_index(p, topic, s.n_topics, FMD);
+    if (s.rec[b + FMD * TILE] > cap2) s.rec[b + FMD * TILE] = cap2;
+    if (s.rec[b + MMD * TILE] > cap3) s.rec[b + MMD * TILE] = cap3;
 }
 
 __global__ __launch_bounds__(256) void k_rebuild_ipcount(DevState s) {
@@ -315,6 +332,52 @@ __global__ __launch_bounds__(256) void k_rebuild_ipcount(DevState s) {
     const uint2 g = reinterpret_cast<const uint2*>(s.ipg)[p];
     if (g.x != IPG_NONE) atomicAdd(&s.ipcount[g.x & ~IPG_WL], 1u);
     if (g.y != IPG_NONE && g.y != g.x) atomicAdd(&s.ipcount[g.y & ~IPG_WL], 1u);
+}
+
+// ---- import / export permutations ------------------------------------------
+
+__global__ __launch_bounds__(256) void k_tile_field(DevState s, int field, const void* __restrict__ src) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t t = blockIdx.y;
+    if (p >= s.n_pairs) return;
+    const size_t i = (size_t)t * s.n_pairs + p;
+    if (field < NFIELD)
+        s.rec[rec_index(p, t, s.n_topics, field)] = static_cast<const double*>(src)[i];
+    else
+        s.rflags[flag_index(p, t, s.n_topics)] = static_cast<const uint8_t*>(src)[i] & (REC_IN_MESH | REC_ACTIVE);
+}
+
+__global__ __launch_bounds__(256) void k_untile_field(DevState s, int field, void* __restrict__ dst) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t t = blockIdx.y;
+    if (p >= s.n_pairs) return;
+    const size_t i = (size_t)t * s.n_pairs + p;
+    if (field < NFIELD)
+        static_cast<double*>(dst)[i] = s.rec[rec_index(p, t, s.n_topics, field)];
+    else
+        static_cast<uint8_t*>(dst)[i] = s.rflags[flag_index(p, t, s.n_topics)] & (REC_IN_MESH | REC_ACTIVE);
+}
+
+__global__ __launch_bounds__(256) void k_mesh_time_export(DevState s, int64_t* __restrict__ dst) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t t = blockIdx.y;
+    if (p >= s.n_pairs) return;
+    const uint8_t fl = s.rflags[flag_index(p, t, s.n_topics)];
+    dst[(size_t)t * s.n_pairs + p] = mesh_time_of(s, fl, p, t);
+}
+
+__global__ __launch_bounds__(256) void k_mesh_time_import(DevState s, const int64_t* __restrict__ src,
+                                                          uint32_t* n_bad) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t t = blockIdx.y;
+    if (p >= s.n_pairs) return;
+    const size_t fi = flag_index(p, t, s.n_topics);
+    const uint8_t fl = s.rflags[fi];
+    if (!(fl & REC_IN_MESH)) return;
+    const int64_t mt = src[(size_t)t * s.n_pairs + p];
+    const int64_t graft = reinterpret_cast<const int64_t*>(s.rec)[rec_index(p, t, s.n_topics, GRAFT)];
+    if (mt == 0) s.rflags[fi] = fl | REC_FRESH;
+    else if (mt != s.last_refresh - graft) atomicAdd(n_bad, 1u);
 }
 
 // ---- seeded synthetic state (gsx/synth.py restated on the device) ------------
@@ -338,17 +401,16 @@ __global__ __launch_bounds__(256) void k_synth_records(DevState s, const int32_t
     const uint32_t t = blockIdx.y;
     if (p >= s.n_pairs) return;
     const uint64_t a = (uint64_t)t * s.n_pairs + p;
-    const size_t r = (size_t)t * s.rs + p;
-    s.fmd[r] = unif(sp.seed, TAG_STATE, a, 1) * sp.fmd_max;
-    s.mmd[r] = unif(sp.seed, TAG_STATE, a, 2) * sp.mmd_max;
-    s.mfp[r] = unif(sp.seed, TAG_STATE, a, 3) * sp.mfp_max;
+    const size_t b = rec_index(p, t, s.n_topics, FMD);
+    s.rec[b + FMD * TILE] = unif(sp.seed, TAG_STATE, a, 1) * sp.fmd_max;
+    s.rec[b + MMD * TILE] = unif(sp.seed, TAG_STATE, a, 2) * sp.mmd_max;
+    s.rec[b + MFP * TILE] = unif(sp.seed, TAG_STATE, a, 3) * sp.mfp_max;
     const double u4 = unif(sp.seed, TAG_STATE, a, 4) * sp.imd_max;
-    s.imd[r] = ((uint32_t)col[p] >= sp.sybil_first) ? u4 : 0.0;
+    s.rec[b + IMD * TILE] = ((uint32_t)col[p] >= sp.sybil_first) ? u4 : 0.0;
     const bool in_mesh = unif(sp.seed, TAG_STATE, a, 5) < sp.p_in_mesh;
     const int64_t graft = sp.now - (int64_t)(unif(sp.seed, TAG_STATE, a, 6) * (double)sp.graft_window);
-    s.graft[r] = graft;
-    s.mtime[r] = in_mesh ? sp.now - graft : 0;
-    s.rflags[r] = in_mesh ? REC_IN_MESH : 0;
+    reinterpret_cast<int64_t*>(s.rec)[b + GRAFT * TILE] = graft;
+    s.rflags[flag_index(p, t, s.n_topics)] = in_mesh ? REC_IN_MESH : 0;  // meshTime = now - graft
 }
 
 __global__ __launch_bounds__(256) void k_synth_pairs(DevState s, DevSynthSpec sp) {
@@ -364,14 +426,6 @@ __global__ __launch_bounds__(256) void k_synth_pairs(DevState s, DevSynthSpec sp
 
 // ---- launchers -------------------------------------------------------------
 
-hipError_t launch_synthesize(const DevState& s, const int32_t* col, const DevSynthSpec& spec, hipStream_t st) {
-    if (s.n_pairs == 0) return hipSuccess;
-    const unsigned nb = (unsigned)((s.n_pairs + 255) / 256);
-    hipLaunchKernelGGL(k_synth_records, dim3(nb, s.n_topics), dim3(256), 0, st, s, col, spec);
-    hipLaunchKernelGGL(k_synth_pairs, dim3(nb), dim3(256), 0, st, s, spec);
-    return hipGetLastError();
-}
-
 static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st) {
@@ -381,22 +435,21 @@ hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st) {
 }
 
 template <bool R>
-static hipError_t launch_rs(const DevState& s, const DevPeerParams& pp, int64_t now, hipStream_t st) {
+static hipError_t launch_rs(const DevState& s, const KernParams& kp, int64_t now, hipStream_t st) {
     const dim3 grid(blocks_for(s.n_pairs, 256)), block(256);
     switch (s.n_topics) {
-    case 1: hipLaunchKernelGGL((k_refresh_score<1, R>), grid, block, 0, st, s, pp, now); break;
-    case 2: hipLaunchKernelGGL((k_refresh_score<2, R>), grid, block, 0, st, s, pp, now); break;
-    case 4: hipLaunchKernelGGL((k_refresh_score<4, R>), grid, block, 0, st, s, pp, now); break;
-    case 8: hipLaunchKernelGGL((k_refresh_score<8, R>), grid, block, 0, st, s, pp, now); break;
-    default: hipLaunchKernelGGL((k_refresh_score<0, R>), grid, block, 0, st, s, pp, now); break;
+    case 1: hipLaunchKernelGGL((k_refresh_score<1, R>), grid, block, 0, st, s, kp, now); break;
+    case 2: hipLaunchKernelGGL((k_refresh_score<2, R>), grid, block, 0, st, s, kp, now); break;
+    case 4: hipLaunchKernelGGL((k_refresh_score<4, R>), grid, block, 0, st, s, kp, now); break;
+    case 8: hipLaunchKernelGGL((k_refresh_score<8, R>), grid, block, 0, st, s, kp, now); break;
+    default: hipLaunchKernelGGL((k_refresh_score<0, R>), grid, block, 0, st, s, kp, now); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_refresh_score(const DevState& s, const DevPeerParams& pp, int64_t now, bool refresh,
-                                hipStream_t st) {
+hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st) {
     if (s.n_pairs == 0) return hipSuccess;
-    return refresh ? launch_rs<true>(s, pp, now, st) : launch_rs<false>(s, pp, now, st);
+    return refresh ? launch_rs<true>(s, kp, now, st) : launch_rs<false>(s, kp, now, st);
 }
 
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
@@ -417,6 +470,39 @@ hipError_t launch_rebuild_ipcount(const DevState& s, uint32_t n_groups_ip, hipSt
     hipError_t e = hipMemsetAsync(s.ipcount, 0, sizeof(uint32_t) * (n_groups_ip ? n_groups_ip : 1), st);
     if (e != hipSuccess || s.n_pairs == 0) return e;
     hipLaunchKernelGGL(k_rebuild_ipcount, dim3(blocks_for(s.n_pairs, 256)), dim3(256), 0, st, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_synthesize(const DevState& s, const int32_t* col, const DevSynthSpec& spec, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    const unsigned nb = blocks_for(s.n_pairs, 256);
+    hipLaunchKernelGGL(k_synth_records, dim3(nb, s.n_topics), dim3(256), 0, st, s, col, spec);
+    hipLaunchKernelGGL(k_synth_pairs, dim3(nb), dim3(256), 0, st, s, spec);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_field(const DevState& s, int field, const void* src, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_field, dim3(blocks_for(s.n_pairs, 256), s.n_topics), dim3(256), 0, st, s, field, src);
+    return hipGetLastError();
+}
+
+hipError_t launch_untile_field(const DevState& s, int field, void* dst, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_untile_field, dim3(blocks_for(s.n_pairs, 256), s.n_topics), dim3(256), 0, st, s, field, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_mesh_time_export(const DevState& s, int64_t* dst, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mesh_time_export, dim3(blocks_for(s.n_pairs, 256), s.n_topics), dim3(256), 0, st, s, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_mesh_time_import(const DevState& s, const int64_t* src, uint32_t* n_bad, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mesh_time_import, dim3(blocks_for(s.n_pairs, 256), s.n_topics), dim3(256), 0, st, s, src,
+                       n_bad);
     return hipGetLastError();
 }
 

@@ -159,10 +159,11 @@ class StateView(C.Structure):
         ("pair_flags", C.POINTER(C.c_uint8)),
         ("expire_ns", C.POINTER(C.c_int64)),
         ("behaviour_penalty", C.POINTER(C.c_double)),
+        ("last_refresh_ns", C.c_int64),
     ]
 
 
-STATE_FIELDS = [f for f, _ in StateView._fields_]
+STATE_FIELDS = [f for f, _ in StateView._fields_][:-1]  # the array members
 RECORD_FIELDS = STATE_FIELDS[:7]
 PAIR_FIELDS = STATE_FIELDS[7:]
 STATE_DTYPES = {

@@ -187,6 +187,7 @@ class Engine:
         for f in abi.PAIR_FIELDS:
             assert arrays[f].size == self.n_pairs, f
         sv = self._view(arrays)
+        sv.last_refresh_ns = int(st.get("last_refresh_ns", 0))
         self._chk(self.lib.gsx_import_state(self.h, C.byref(sv)), "gsx_import_state")
 
     def synthesize_state(self, spec: abi.SynthSpec):
@@ -200,4 +201,5 @@ class Engine:
             out[f] = np.empty(n, dtype=abi.STATE_DTYPES[f])
         sv = self._view(out)
         self._chk(self.lib.gsx_export_state(self.h, C.byref(sv)), "gsx_export_state")
+        out["last_refresh_ns"] = int(sv.last_refresh_ns)
         return out

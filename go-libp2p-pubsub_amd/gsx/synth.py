@@ -196,4 +196,5 @@ def synthetic_state(ov: Overlay, n_topics: int, now_ns: int, seed: int = SEED, p
     # retained pairs: expiry within now +- 2 s (half expire at the first refresh)
     st["expire_ns"] = now_ns + ((uniform(seed, TAG_STATE, p, 9) - 0.5) * float(4 * abi.SECOND)).astype(np.int64)
     st["behaviour_penalty"] = uniform(seed, TAG_STATE, p, 10) * 5.0
+    st["last_refresh_ns"] = now_ns  # meshTime above is what a refresh at `now` wrote
     return st

@@ -276,13 +276,23 @@ typedef struct gsx_state_view {
     uint8_t* pair_flags; /* GSX_PAIR_* */
     int64_t* expire_ns;
     double* behaviour_penalty;
+    /* time of the last refreshScores() pass (0 if none) */
+    int64_t last_refresh_ns;
 } gsx_state_view;
 
 /* Import overwrites all state (and rebuilds the per-observer IP counters from
  * the present pairs); export copies it back.  NULL members are skipped on
- * export; on import every member must be non-NULL. */
+ * export; on import every member must be non-NULL.
+ *
+ * mesh_time_ns is topicStats.meshTime, which the reference only reads while
+ * the peer is in the mesh (score.go:279, 479-481): export writes 0 for
+ * records not in the mesh, and import requires every in-mesh record's
+ * meshTime to be either 0 (grafted since the last refresh) or
+ * last_refresh_ns - graft_time_ns (what that refresh wrote, score.go:545);
+ * any other value is GSX_EINVAL (the engine derives meshTime instead of
+ * streaming it). */
 int gsx_import_state(gsx_engine* e, const gsx_state_view* s);
-int gsx_export_state(gsx_engine* e, const gsx_state_view* s);
+int gsx_export_state(gsx_engine* e, gsx_state_view* s);
 
 /* Seeded synthetic counter state, generated on the device (BASELINE.md cfg3
  * initialisation).  Every draw is u = (h(seed, 4, a, k) >> 11) * 2^-53 with

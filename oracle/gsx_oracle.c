@@ -67,6 +67,7 @@ static int ipcount_init(struct orc_engine* o);
 struct orc_engine {
     uint32_t T;
     ipcount_map ipc;
+    int64_t last_refresh; /* now of the last refreshScores() (state view only) */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -506,6 +507,7 @@ static void refresh_pair(orc_engine* o, uint64_t p, int64_t now) {
 
 /* refreshScores, score.go:497-558 */
 int orc_refresh(orc_engine* o, int64_t now) {
+    o->last_refresh = now;
     for (uint64_t p = 0; p < o->E; p++) {
         orc_peer_stats* pstats = &o->ps[p];
         if (!pstats->present) continue;
@@ -523,6 +525,7 @@ int orc_refresh(orc_engine* o, int64_t now) {
 }
 
 int orc_refresh_scores_range(orc_engine* o, int64_t now, uint64_t p0, uint64_t p1, double* out) {
+    o->last_refresh = now;
     if (p1 > o->E) p1 = o->E;
     for (uint64_t p = p0; p < p1; p++) {
         orc_peer_stats* pstats = &o->ps[p];
@@ -568,7 +571,8 @@ static void remove_peer(orc_engine* o, uint64_t p, int64_t now) {
     if (!pstats->present) return;
     if (score_pair(o, p) > 0) { /* :615-619 */
         ipcount_add(o, p, -1);         /* removeIPs */
-        pstats->present = false;       /* delete */
+        pstats->present = false;       /* delete(ps.peerStats, p): the entry is gone, */
+        pstats->connected = false;     /* connected with it */
         return;
     }
     for (uint32_t t = 0; t < o->T; t++) { /* :623-633 */
@@ -879,10 +883,12 @@ int orc_import_state(orc_engine* o, const gsx_state_view* s) {
         }
     }
     ipcount_rebuild(o);
+    o->last_refresh = s->last_refresh_ns;
     return 0;
 }
 
-int orc_export_state(orc_engine* o, const gsx_state_view* s) {
+int orc_export_state(orc_engine* o, gsx_state_view* s) {
+    s->last_refresh_ns = o->last_refresh;
     uint64_t E = o->E;
     for (uint64_t p = 0; p < E; p++) {
         const orc_peer_stats* ps = &o->ps[p];
@@ -898,7 +904,8 @@ int orc_export_state(orc_engine* o, const gsx_state_view* s) {
             if (s->mesh_failure_penalty) s->mesh_failure_penalty[r] = ts->mesh_failure_penalty;
             if (s->invalid_message_deliveries) s->invalid_message_deliveries[r] = ts->invalid_message_deliveries;
             if (s->graft_time_ns) s->graft_time_ns[r] = ts->graft_time;
-            if (s->mesh_time_ns) s->mesh_time_ns[r] = ts->mesh_time;
+            /* meshTime is only read while in the mesh (score.go:279, 479-481); the view reports 0 otherwise */
+            if (s->mesh_time_ns) s->mesh_time_ns[r] = ts->in_mesh ? ts->mesh_time : 0;
             if (s->rec_flags)
                 s->rec_flags[r] = (uint8_t)((ts->in_mesh ? GSX_REC_IN_MESH : 0) |
                                             (ts->mesh_message_deliveries_active ? GSX_REC_ACTIVE : 0));

@@ -68,7 +68,7 @@ double orc_score(orc_engine* o, uint64_t pair);
 int orc_refresh_scores_range(orc_engine* o, int64_t now_ns, uint64_t p0, uint64_t p1, double* out);
 
 int orc_import_state(orc_engine* o, const gsx_state_view* s);
-int orc_export_state(orc_engine* o, const gsx_state_view* s);
+int orc_export_state(orc_engine* o, gsx_state_view* s);
 uint64_t orc_num_pairs(orc_engine* o);
 
 #ifdef __cplusplus

@@ -178,6 +178,7 @@ class Oracle:
     def import_state(self, st):
         arrays = {f: np.ascontiguousarray(st[f], dtype=abi.STATE_DTYPES[f]).reshape(-1) for f in abi.STATE_FIELDS}
         sv = self._view(arrays)
+        sv.last_refresh_ns = int(st.get("last_refresh_ns", 0))
         self._chk(self.lib.orc_import_state(self.h, C.byref(sv)), "orc_import_state")
 
     def export_state(self):
@@ -185,6 +186,7 @@ class Oracle:
         out = {f: np.empty(R if f in abi.RECORD_FIELDS else self.n_pairs, dtype=abi.STATE_DTYPES[f]) for f in abi.STATE_FIELDS}
         sv = self._view(out)
         self._chk(self.lib.orc_export_state(self.h, C.byref(sv)), "orc_export_state")
+        out["last_refresh_ns"] = int(sv.last_refresh_ns)
         return out
 
 

@@ -1,0 +1,389 @@
+// Layout study for the fused refresh+score kernel (not product code).
+//
+// Same arithmetic as gsx_kernels.hip's k_refresh_score (cfg3: T = 8 topics,
+// every pair connected), over different HBM layouts of the per-record state:
+//   V0  SoA [t][p], one pair per lane, meshTime stored (masked to in-mesh lanes)
+//   V1  SoA [t][p], two pairs per lane (16-B accesses), meshTime derived
+//   V2  tiled [p/128][t][field][128], two pairs per lane, meshTime derived
+//   V3  tiled [p/64][t][field][64], one pair per lane, meshTime derived
+//   C0  copy ceiling: the same byte volume as V1-V3 as plain 16-B streams
+// "meshTime derived": meshTime = FRESH ? 0 : now_last - graftTime for in-mesh
+// records, so no meshTime stream and no partial-line masked stores.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                   \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+constexpr int T = 8;
+constexpr uint8_t IN_MESH = 1, ACTIVE = 2, FRESH = 4;
+
+struct TP {
+    double tw, w1, cap1;
+    int64_t q1;
+    double w2, d2, w3, d3, thr3;
+    int64_t act3;
+    double w3b, d3b, w4, d4;
+};
+struct PP {
+    double cap, w5, w6, w7, thr7, d7, dtz;
+    int64_t thr6;
+};
+
+__constant__ TP c_tp[T];
+
+__device__ __forceinline__ double decay(double x, double d, double dtz) {
+    x *= d;
+    return x < dtz ? 0.0 : x;
+}
+
+__device__ __forceinline__ double topic_score(const TP& tp, uint8_t fl, int64_t mt, double fmd, double mmd, double mfp,
+                                              double imd) {
+    double ts = 0.0;
+    if (fl & IN_MESH) {
+        double p1 = (double)(mt / tp.q1);
+        if (p1 > tp.cap1) p1 = tp.cap1;
+        ts += p1 * tp.w1;
+    }
+    ts += fmd * tp.w2;
+    if ((fl & ACTIVE) && mmd < tp.thr3) {
+        const double d = tp.thr3 - mmd;
+        ts += (d * d) * tp.w3;
+    }
+    ts += mfp * tp.w3b;
+    ts += (imd * imd) * tp.w4;
+    return ts * tp.tw;
+}
+
+struct Pair {
+    const uint8_t* pf;
+    double* bp;
+    const double* app;
+    const uint2* ipg;
+    const uint32_t* ipc;
+    double* score;
+};
+
+__device__ __forceinline__ double tail(const Pair& q, const PP& pp, uint64_t p, double s, double bp) {
+    if (pp.cap > 0 && s > pp.cap) s = pp.cap;
+    s += q.app[p] * pp.w5;
+    const uint2 g = q.ipg[p];
+    double r = 0;
+    if (g.x != 0xFFFFFFFFu) {
+        const int64_t c = q.ipc[g.x];
+        if (c > pp.thr6) {
+            const double x = (double)(c - pp.thr6);
+            r += x * x;
+        }
+    }
+    if (g.y != 0xFFFFFFFFu) {
+        const int64_t c = q.ipc[g.y];
+        if (c > pp.thr6) {
+            const double x = (double)(c - pp.thr6);
+            r += x * x;
+        }
+    }
+    s += r * pp.w6;
+    if (bp > pp.thr7) {
+        const double e = bp - pp.thr7;
+        s += (e * e) * pp.w7;
+    }
+    return s;
+}
+
+// ---- V0: the engine's current kernel ---------------------------------------
+struct Soa {
+    double *fmd, *mmd, *mfp, *imd;
+    int64_t *graft, *mtime;
+    uint8_t* fl;
+};
+
+__global__ __launch_bounds__(256) void k_v0(Soa a, Pair q, PP pp, uint64_t n, int64_t now) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    double s = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        const size_t r = (size_t)t * n + p;
+        double fmd = decay(a.fmd[r], tp.d2, pp.dtz), mmd = decay(a.mmd[r], tp.d3, pp.dtz);
+        double mfp = decay(a.mfp[r], tp.d3b, pp.dtz), imd = decay(a.imd[r], tp.d4, pp.dtz);
+        uint8_t fl = a.fl[r];
+        a.fmd[r] = fmd;
+        a.mmd[r] = mmd;
+        a.mfp[r] = mfp;
+        a.imd[r] = imd;
+        int64_t mt = 0;
+        if (fl & IN_MESH) {
+            mt = now - a.graft[r];
+            if (mt > tp.act3) fl |= ACTIVE;
+            a.mtime[r] = mt;
+            a.fl[r] = fl;
+        }
+        s += topic_score(tp, fl, mt, fmd, mmd, mfp, imd);
+    }
+    double bp = decay(q.bp[p], pp.d7, pp.dtz);
+    q.bp[p] = bp;
+    q.score[p] = tail(q, pp, p, s, bp);
+}
+
+// ---- V1: SoA, two pairs per lane, derived meshTime -------------------------
+__global__ __launch_bounds__(256) void k_v1(Soa a, Pair q, PP pp, uint64_t n, int64_t now) {
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (p >= n) return;  // n even
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        const size_t r = (size_t)t * n + p;
+        double2 f = *(const double2*)(a.fmd + r), m = *(const double2*)(a.mmd + r);
+        double2 b = *(const double2*)(a.mfp + r), v = *(const double2*)(a.imd + r);
+        const uchar2 fl2 = *(const uchar2*)(a.fl + r);
+        f.x = decay(f.x, tp.d2, pp.dtz);
+        f.y = decay(f.y, tp.d2, pp.dtz);
+        m.x = decay(m.x, tp.d3, pp.dtz);
+        m.y = decay(m.y, tp.d3, pp.dtz);
+        b.x = decay(b.x, tp.d3b, pp.dtz);
+        b.y = decay(b.y, tp.d3b, pp.dtz);
+        v.x = decay(v.x, tp.d4, pp.dtz);
+        v.y = decay(v.y, tp.d4, pp.dtz);
+        *(double2*)(a.fmd + r) = f;
+        *(double2*)(a.mmd + r) = m;
+        *(double2*)(a.mfp + r) = b;
+        *(double2*)(a.imd + r) = v;
+        uint8_t fa = fl2.x, fb = fl2.y;
+        int64_t ma = 0, mb = 0;
+        if ((fa | fb) & IN_MESH) {
+            const longlong2 g = *(const longlong2*)(a.graft + r);
+            if (fa & IN_MESH) ma = now - g.x;
+            if (fb & IN_MESH) mb = now - g.y;
+        }
+        const uint8_t na = ((fa & IN_MESH) && ma > tp.act3) ? ((fa | ACTIVE) & ~FRESH) : (fa & ~FRESH);
+        const uint8_t nb = ((fb & IN_MESH) && mb > tp.act3) ? ((fb | ACTIVE) & ~FRESH) : (fb & ~FRESH);
+        if (na != fa || nb != fb) *(uchar2*)(a.fl + r) = make_uchar2(na, nb);
+        s0 += topic_score(tp, na, ma, f.x, m.x, b.x, v.x);
+        s1 += topic_score(tp, nb, mb, f.y, m.y, b.y, v.y);
+    }
+    double2 bp = *(const double2*)(q.bp + p);
+    bp.x = decay(bp.x, pp.d7, pp.dtz);
+    bp.y = decay(bp.y, pp.d7, pp.dtz);
+    *(double2*)(q.bp + p) = bp;
+    double2 out;
+    out.x = tail(q, pp, p, s0, bp.x);
+    out.y = tail(q, pp, p + 1, s1, bp.y);
+    *(double2*)(q.score + p) = out;
+}
+
+// ---- tiled layouts -----------------------------------------------------------
+// 8-B fields: [blk][t][f][TILE] with f = fmd, mmd, mfp, imd, graft; flags [blk][t][TILE].
+template <int TILE>
+__device__ __forceinline__ size_t tix(uint64_t p, int t, int f) {
+    return (((p / TILE) * T + t) * 5 + f) * TILE + (p % TILE);
+}
+template <int TILE>
+__device__ __forceinline__ size_t tfx(uint64_t p, int t) {
+    return ((p / TILE) * T + t) * TILE + (p % TILE);
+}
+
+__global__ __launch_bounds__(256) void k_v2(double* rec, uint8_t* fl, Pair q, PP pp, uint64_t n, int64_t now) {
+    constexpr int TILE = 128;
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (p >= n) return;
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        double* base = rec + tix<TILE>(p, t, 0);
+        double2 f = *(const double2*)(base), m = *(const double2*)(base + TILE);
+        double2 b = *(const double2*)(base + 2 * TILE), v = *(const double2*)(base + 3 * TILE);
+        uint8_t* fp = fl + tfx<TILE>(p, t);
+        const uchar2 fl2 = *(const uchar2*)fp;
+        f.x = decay(f.x, tp.d2, pp.dtz);
+        f.y = decay(f.y, tp.d2, pp.dtz);
+        m.x = decay(m.x, tp.d3, pp.dtz);
+        m.y = decay(m.y, tp.d3, pp.dtz);
+        b.x = decay(b.x, tp.d3b, pp.dtz);
+        b.y = decay(b.y, tp.d3b, pp.dtz);
+        v.x = decay(v.x, tp.d4, pp.dtz);
+        v.y = decay(v.y, tp.d4, pp.dtz);
+        *(double2*)(base) = f;
+        *(double2*)(base + TILE) = m;
+        *(double2*)(base + 2 * TILE) = b;
+        *(double2*)(base + 3 * TILE) = v;
+        uint8_t fa = fl2.x, fb = fl2.y;
+        int64_t ma = 0, mb = 0;
+        if ((fa | fb) & IN_MESH) {
+            const longlong2 g = *(const longlong2*)(base + 4 * TILE);
+            if (fa & IN_MESH) ma = now - g.x;
+            if (fb & IN_MESH) mb = now - g.y;
+        }
+        const uint8_t na = ((fa & IN_MESH) && ma > tp.act3) ? ((fa | ACTIVE) & ~FRESH) : (fa & ~FRESH);
+        const uint8_t nb = ((fb & IN_MESH) && mb > tp.act3) ? ((fb | ACTIVE) & ~FRESH) : (fb & ~FRESH);
+        if (na != fa || nb != fb) *(uchar2*)fp = make_uchar2(na, nb);
+        s0 += topic_score(tp, na, ma, f.x, m.x, b.x, v.x);
+        s1 += topic_score(tp, nb, mb, f.y, m.y, b.y, v.y);
+    }
+    double2 bp = *(const double2*)(q.bp + p);
+    bp.x = decay(bp.x, pp.d7, pp.dtz);
+    bp.y = decay(bp.y, pp.d7, pp.dtz);
+    *(double2*)(q.bp + p) = bp;
+    double2 out;
+    out.x = tail(q, pp, p, s0, bp.x);
+    out.y = tail(q, pp, p + 1, s1, bp.y);
+    *(double2*)(q.score + p) = out;
+}
+
+__global__ __launch_bounds__(256) void k_v3(double* rec, uint8_t* fl, Pair q, PP pp, uint64_t n, int64_t now) {
+    constexpr int TILE = 64;
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    double s = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        double* base = rec + tix<TILE>(p, t, 0);
+        const double fmd = decay(base[0], tp.d2, pp.dtz), mmd = decay(base[TILE], tp.d3, pp.dtz);
+        const double mfp = decay(base[2 * TILE], tp.d3b, pp.dtz), imd = decay(base[3 * TILE], tp.d4, pp.dtz);
+        base[0] = fmd;
+        base[TILE] = mmd;
+        base[2 * TILE] = mfp;
+        base[3 * TILE] = imd;
+        uint8_t* fp = fl + tfx<TILE>(p, t);
+        const uint8_t f0 = *fp;
+        int64_t mt = 0;
+        if (f0 & IN_MESH) mt = now - ((const int64_t*)base)[4 * TILE];
+        const uint8_t nf = ((f0 & IN_MESH) && mt > tp.act3) ? ((f0 | ACTIVE) & ~FRESH) : (f0 & ~FRESH);
+        if (nf != f0) *fp = nf;
+        s += topic_score(tp, nf, mt, fmd, mmd, mfp, imd);
+    }
+    double bp = decay(q.bp[p], pp.d7, pp.dtz);
+    q.bp[p] = bp;
+    q.score[p] = tail(q, pp, p, s, bp);
+}
+
+// ---- copy ceiling: read 5+1 and write 4+1 double2 streams ---------------------
+__global__ __launch_bounds__(256) void k_copy(const double2* __restrict__ src, double2* __restrict__ dst,
+                                              uint64_t n_rd, uint64_t n_wr) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t k = i; k < n_rd; k += stride) {
+        const double2 x = src[k];
+        if (k < n_wr) dst[k] = x;
+        else if (x.x == 1234.5) dst[0] = x;  // keep the read live
+    }
+}
+
+__global__ void k_init(double* d, uint64_t n, uint64_t seed, double scale) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    d[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * scale;
+}
+__global__ void k_init_i64(int64_t* d, uint64_t n, int64_t now) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) d[i] = now - (int64_t)((i * 2654435761ull) % 7200000000000ull);
+}
+__global__ void k_init_u8(uint8_t* d, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) d[i] = ((i * 2654435761ull) >> 7) & 1;
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 12000000ull;  // pairs (even)
+    const int iters = argc > 2 ? atoi(argv[2]) : 20;
+    const uint64_t R = n * T;
+    TP tp{0.25, 0.0027, 3600, 1000000000ll, 0.664, 0.9916, -0.25, 0.97, 100, 30000000000ll, -0.25, 0.997, -99, 0.9994};
+    TP h[T];
+    for (int t = 0; t < T; ++t) h[t] = tp;
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tp), h, sizeof(h)));
+    PP pp{100, 1, -10, -10, 0, 0.99, 0.01, 1};
+    const int64_t now = 1700000000ll * 1000000000ll;
+
+    Soa a;
+    CHECK(hipMalloc(&a.fmd, R * 8));
+    CHECK(hipMalloc(&a.mmd, R * 8));
+    CHECK(hipMalloc(&a.mfp, R * 8));
+    CHECK(hipMalloc(&a.imd, R * 8));
+    CHECK(hipMalloc(&a.graft, R * 8));
+    CHECK(hipMalloc(&a.mtime, R * 8));
+    CHECK(hipMalloc(&a.fl, R));
+    double* rec;
+    uint8_t* tfl;
+    CHECK(hipMalloc(&rec, R * 5 * 8));
+    CHECK(hipMalloc(&tfl, R));
+    Pair q;
+    uint8_t* pf;
+    double *bp, *app, *score;
+    uint2* ipg;
+    uint32_t* ipc;
+    CHECK(hipMalloc(&pf, n));
+    CHECK(hipMalloc(&bp, n * 8));
+    CHECK(hipMalloc(&app, n * 8));
+    CHECK(hipMalloc(&score, n * 8));
+    CHECK(hipMalloc(&ipg, n * 8));
+    CHECK(hipMalloc(&ipc, n * 4));
+    q = Pair{pf, bp, app, ipg, ipc, score};
+    const unsigned gR = (unsigned)((R + 255) / 256), gN = (unsigned)((n + 255) / 256);
+    k_init<<<gR, 256>>>(a.fmd, R, 1, 1500);
+    k_init<<<gR, 256>>>(a.mmd, R, 2, 400);
+    k_init<<<gR, 256>>>(a.mfp, R, 3, 50);
+    CHECK(hipMemset(a.imd, 0, R * 8));
+    k_init_i64<<<gR, 256>>>(a.graft, R, now);
+    k_init_u8<<<gR, 256>>>(a.fl, R);
+    const unsigned g5 = (unsigned)((R * 5 + 255) / 256);
+    k_init<<<g5, 256>>>(rec, R * 5, 9, 100);
+    k_init_u8<<<gR, 256>>>(tfl, R);
+    CHECK(hipMemset(pf, 3, n));
+    k_init<<<gN, 256>>>(bp, n, 5, 5);
+    CHECK(hipMemset(app, 0, n * 8));
+    std::vector<uint2> hg(n);
+    for (uint64_t i = 0; i < n; ++i) hg[i] = make_uint2((uint32_t)i, 0xFFFFFFFFu);
+    CHECK(hipMemcpy(ipg, hg.data(), n * 8, hipMemcpyHostToDevice));
+    CHECK(hipMemset(ipc, 0, n * 4));
+    double2 *csrc, *cdst;
+    const uint64_t rd16 = (R * 41 + n * 33) / 16, wr16 = (R * 32 + n * 16) / 16;
+    CHECK(hipMalloc(&csrc, rd16 * 16));
+    CHECK(hipMalloc(&cdst, wr16 * 16));
+    CHECK(hipMemset(csrc, 0, rd16 * 16));
+    CHECK(hipDeviceSynchronize());
+
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const double bytes_alg = 82.0 * R + 49.0 * n;
+    const double bytes_min = 73.0 * R + 49.0 * n - 8.0 * n;  // derived meshTime: no mtime stream, flags rarely written
+    auto timeit = [&](const char* name, double bytes, auto launch) {
+        for (int i = 0; i < 3; ++i) launch();
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(e0));
+        for (int i = 0; i < iters; ++i) launch();
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= iters;
+        printf("%-4s %8.4f ms  %7.1f Grec/s  alg(82B) %6.0f GB/s  own-bytes %6.0f GB/s\n", name, ms, R / ms / 1e6,
+               bytes_alg / ms / 1e6, bytes / ms / 1e6);
+    };
+    for (int round = 0; round < 2; ++round) {
+        timeit("V0", bytes_alg, [&] { k_v0<<<gN, 256>>>(a, q, pp, n, now); });
+        timeit("V1", bytes_min, [&] { k_v1<<<(unsigned)((n / 2 + 255) / 256), 256>>>(a, q, pp, n, now); });
+        timeit("V2", bytes_min, [&] { k_v2<<<(unsigned)((n / 2 + 255) / 256), 256>>>(rec, tfl, q, pp, n, now); });
+        timeit("V3", bytes_min, [&] { k_v3<<<gN, 256>>>(rec, tfl, q, pp, n, now); });
+        timeit("C0", (rd16 + wr16) * 16.0, [&] { k_copy<<<256 * 16, 256>>>(csrc, cdst, rd16, wr16); });
+    }
+    CHECK(hipGetLastError());
+    return 0;
+}
