@@ -110,6 +110,52 @@ struct DevSynthSpec {
     uint32_t sybil_first;
 };
 
+// ---- propagation (gsx_propagate.hip) -------------------------------------------
+constexpr uint8_t EDGE_OUTBOUND = 0x01, EDGE_DIRECT = 0x02, EDGE_GOSSIPSUB = 0x04, EDGE_FLOODSUB = 0x08;
+constexpr uint32_t ROUTER_FLOODSUB = 0, ROUTER_GOSSIPSUB = 1, ROUTER_RANDOMSUB = 2;
+constexpr uint32_t NO_PAIR = 0xFFFFFFFFu;
+constexpr uint8_t FWD_FORWARD = 0x01;    // v sends messages it received to u
+constexpr uint8_t FWD_PUBLISH = 0x02;    // v sends messages it published to u
+constexpr uint8_t FWD_RSUB_CAND = 0x04;  // u is one of v's RandomSub peers (drawn per message)
+constexpr int RANDOMSUB_D = 6;           // randomsub.go:16-18
+constexpr int RSUB_MAX_DEG = 256;
+constexpr int MAX_HOPS = 64;
+enum { STAT_DUPS = 0, STAT_HOP0 = 1, STAT_WORDS = STAT_HOP0 + MAX_HOPS + 1 };
+
+struct DevMsg {
+    uint32_t source;
+    uint32_t reserved;
+    uint64_t msg_id;
+};
+
+struct PropState {
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const uint32_t* rev;   // pair (u -> v) -> pair (v -> u), NO_PAIR if absent
+    const uint8_t* eflags;
+    uint8_t* fwd;          // per pair, this call: FWD_*
+    const DevMsg* msgs;
+    uint64_t* seen;        // [word][node]
+    uint64_t* origin;      // [word][node] messages the node published
+    uint64_t* from_mask;   // [word][pair (u -> v)] messages u first received from v
+    uint64_t* sel;         // [word][pair] RandomSub draws (null for other routers)
+    uint8_t* hop;          // [message][node] arrival hop, 0xFF never
+    uint32_t* dupcnt;      // per pair: duplicates inside the P3 window
+    unsigned long long* stats;  // STAT_*
+    uint64_t n_pairs;
+    uint32_t n_nodes, n_words, n_msgs;
+    uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt;
+    double publish_threshold;
+    int64_t hop_latency, window;
+    uint64_t seed;
+};
+
+hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st);
+hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
+hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
+hipError_t launch_prop_credit(const PropState& ps, const DevState& s, hipStream_t st);
+hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
+
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
 hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st);

@@ -90,6 +90,22 @@ struct gsx_engine {
     double *d_bp = nullptr, *d_app = nullptr, *d_score = nullptr;
     uint32_t *d_ipg = nullptr, *d_ipcount = nullptr;
     int32_t* d_col = nullptr;
+    int64_t* d_row_ptr = nullptr;
+    uint32_t* d_rev = nullptr;  // pair (u -> v) -> pair (v -> u)
+    std::vector<uint8_t> eflags_host;
+
+    // propagation buffers (grown on demand) and the last call's shape
+    struct {
+        uint64_t *seen = nullptr, *front = nullptr, *nxt = nullptr, *origin = nullptr, *from = nullptr,
+                 *sel = nullptr;
+        uint8_t *hop = nullptr, *fwd = nullptr;
+        uint32_t* dup = nullptr;
+        gsx::DevMsg* msgs = nullptr;
+        unsigned long long* stats = nullptr;
+        uint32_t words_cap = 0, msgs_cap = 0;
+        gsx::PropState last{};
+        bool have_last = false;
+    } prop;
 
     // events
     std::vector<gsx_event> pending;
@@ -212,6 +228,15 @@ void free_state(gsx_engine* e) {
     e->d_expire = nullptr;
     e->d_bp = e->d_app = e->d_score = nullptr;
     e->d_ipg = e->d_ipcount = nullptr;
+    if (e->d_row_ptr) (void)hipFree(e->d_row_ptr);
+    if (e->d_rev) (void)hipFree(e->d_rev);
+    e->d_row_ptr = nullptr;
+    e->d_rev = nullptr;
+    void* pp[] = {e->prop.seen, e->prop.front, e->prop.nxt, e->prop.origin, e->prop.from, e->prop.sel,
+                  e->prop.hop,  e->prop.fwd,   e->prop.dup, e->prop.msgs,   e->prop.stats};
+    for (void* p : pp)
+        if (p) (void)hipFree(p);
+    e->prop = {};
     e->d_col = nullptr;
 }
 
@@ -544,6 +569,11 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     const uint64_t E = (uint64_t)row_ptr[n_nodes];
     for (uint64_t p = 0; p < E; ++p)
         if (col[p] < 0 || (uint32_t)col[p] >= n_nodes) return fail(e, GSX_EINVAL, "col out of range");
+    // each observer tracks a peer once, rows ascending: the order first
+    // deliverers are chosen in (lowest sender first)
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        for (int64_t p = row_ptr[i] + 1; p < row_ptr[i + 1]; ++p)
+            if (col[p] <= col[p - 1]) return fail(e, GSX_EINVAL, "each row of col must be strictly ascending");
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     free_state(e);
@@ -623,6 +653,24 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     HIPCHK(e, hipMemsetAsync(e->d_ipcount, 0, sizeof(uint32_t) * (e->n_groups ? e->n_groups : 1), e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (E) HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * E, hipMemcpyHostToDevice));
+    {  // reverse pairs for the pull-based propagation
+        std::vector<uint32_t> rev(E, gsx::NO_PAIR);
+        for (uint32_t u = 0; u < n_nodes; ++u)
+            for (int64_t q = row_ptr[u]; q < row_ptr[u + 1]; ++q) {
+                const uint32_t v = (uint32_t)col[q];
+                const int32_t* b = col + row_ptr[v];
+                const int32_t* en = col + row_ptr[v + 1];
+                const int32_t* it = std::lower_bound(b, en, (int32_t)u);
+                if (it != en && *it == (int32_t)u) rev[(size_t)q] = (uint32_t)(it - col);
+            }
+        if ((rc = dalloc(e, &e->d_rev, E)) || (rc = dalloc(e, &e->d_row_ptr, (size_t)n_nodes + 1))) {
+            free_state(e);
+            return rc;
+        }
+        if (E) HIPCHK(e, hipMemcpy(e->d_rev, rev.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_row_ptr, row_ptr, sizeof(int64_t) * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
+        e->eflags_host.assign(edge_flags ? edge_flags : nullptr, edge_flags ? edge_flags + E : nullptr);
+    }
     if (edge_flags) HIPCHK(e, hipMemcpy(e->d_eflags, edge_flags, E, hipMemcpyHostToDevice));
     else HIPCHK(e, hipMemsetAsync(e->d_eflags, 0, e->rs, e->stream));
     rc = upload_ipg(e);
@@ -967,6 +1015,129 @@ int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     release_tmp(e);
     s->last_refresh_ns = e->last_refresh;
+    return GSX_OK;
+}
+
+// Message propagation, see gsx.h and gsx_propagate.hip.
+int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out) {
+    if (!e || !cfg || !out || (m && !msgs)) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (cfg->max_hops > GSX_MAX_HOPS || cfg->router > GSX_ROUTER_RANDOMSUB || m > 0xFFFFFFFFull)
+        return fail(e, GSX_EINVAL, "bad propagation config");
+    for (size_t k = 0; k < m; ++k)
+        if (msgs[k].source >= e->n_nodes) return fail(e, GSX_ERANGE, "message source out of range");
+    std::memset(out, 0, sizeof(*out));
+    if (int rc = ensure_scores(e)) return rc;  // publishThreshold tests read current scores
+    const uint32_t W = (uint32_t)((m + 63) / 64);
+    const size_t N = e->n_nodes, E = e->E;
+    auto& P = e->prop;
+    if (W > P.words_cap || m > P.msgs_cap || !P.fwd) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        void* pp[] = {P.seen, P.front, P.nxt, P.origin, P.from, P.sel, P.hop, P.fwd, P.dup, P.msgs, P.stats};
+        for (void* p : pp)
+            if (p) (void)hipFree(p);
+        P = {};
+        const size_t w = std::max<uint32_t>(W, 1), mm = std::max<size_t>(m, 1);
+        int rc = 0;
+        if ((rc = dalloc(e, &P.seen, w * N)) || (rc = dalloc(e, &P.front, w * N)) || (rc = dalloc(e, &P.nxt, w * N)) ||
+            (rc = dalloc(e, &P.origin, w * N)) || (rc = dalloc(e, &P.from, w * E)) || (rc = dalloc(e, &P.hop, mm * N)) ||
+            (rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.dup, E)) || (rc = dalloc(e, &P.msgs, mm)) ||
+            (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
+            return rc;
+        P.words_cap = (uint32_t)w;
+        P.msgs_cap = (uint32_t)mm;
+    }
+    const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
+    if (rsub && !P.sel) {
+        if (int rc = dalloc(e, &P.sel, (size_t)P.words_cap * E)) return rc;
+    }
+    gsx::PropState ps{};
+    ps.row_ptr = e->d_row_ptr;
+    ps.col = e->d_col;
+    ps.rev = e->d_rev;
+    ps.eflags = e->d_eflags;
+    ps.fwd = P.fwd;
+    ps.msgs = P.msgs;
+    ps.seen = P.seen;
+    ps.origin = P.origin;
+    ps.from_mask = P.from;
+    ps.sel = rsub ? P.sel : nullptr;
+    ps.hop = P.hop;
+    ps.dupcnt = P.dup;
+    ps.stats = P.stats;
+    ps.n_pairs = E;
+    ps.n_nodes = (uint32_t)N;
+    ps.n_words = W;
+    ps.n_msgs = (uint32_t)m;
+    ps.router = cfg->router;
+    ps.topic = cfg->topic;
+    ps.flood_publish = cfg->flood_publish;
+    const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
+    ps.credit = (cfg->credit_scores && scored) ? 1 : 0;
+    ps.window = scored ? e->tp[cfg->topic].mesh_message_deliveries_window_ns : 0;
+    ps.hop_latency = cfg->hop_latency_ns;
+    ps.all_dups_in_window = ((int64_t)cfg->max_hops * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
+    ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
+    ps.publish_threshold = e->th.publish_threshold;
+    ps.seed = cfg->seed;
+    e->prop.last = ps;
+    e->prop.have_last = true;
+    if (m == 0) return GSX_OK;
+    // per-call state
+    std::vector<gsx::DevMsg> hm(m);
+    for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
+    HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.front, 0, 8 * (size_t)W * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.hop, 0xFF, m * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
+    if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
+    const gsx::DevState ds = dev_state(e);
+    HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
+    HIPCHK(e, gsx::launch_prop_init(ps, P.front, e->stream));
+    uint64_t* cur = P.front;
+    uint64_t* nxt = P.nxt;
+    for (uint32_t h = 1; h <= cfg->max_hops; ++h) {
+        HIPCHK(e, gsx::launch_prop_hop(ps, h, cur, nxt, e->stream));
+        std::swap(cur, nxt);
+    }
+    if (ps.credit) {
+        HIPCHK(e, gsx::launch_prop_credit(ps, ds, e->stream));
+        e->scores_valid = false;
+    }
+    unsigned long long st[gsx::STAT_WORDS];
+    HIPCHK(e, hipMemcpyAsync(st, P.stats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    out->duplicates = st[gsx::STAT_DUPS];
+    for (uint32_t h = 1; h <= GSX_MAX_HOPS; ++h) {
+        out->hop_deliveries[h] = st[gsx::STAT_HOP0 + h];
+        out->deliveries += st[gsx::STAT_HOP0 + h];
+        if (st[gsx::STAT_HOP0 + h]) out->hops = h;
+    }
+    out->transmissions = out->deliveries + out->duplicates;
+    return GSX_OK;
+}
+
+int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
+    if (!e) return GSX_EINVAL;
+    if (!e->prop.have_last) return fail(e, GSX_ESTATE, "no gsx_propagate call yet");
+    const gsx::PropState& ps = e->prop.last;
+    const size_t cells = (size_t)ps.n_msgs * ps.n_nodes;
+    if (cells == 0) return GSX_OK;
+    if (hop) HIPCHK(e, hipMemcpyAsync(hop, ps.hop, cells, hipMemcpyDeviceToHost, e->stream));
+    if (first_from) {
+        int32_t* d_ff = nullptr;
+        if (int rc = dalloc(e, &d_ff, cells)) return rc;
+        HIPCHK(e, hipMemsetAsync(d_ff, 0xFF, 4 * cells, e->stream));
+        HIPCHK(e, gsx::launch_prop_from(ps, d_ff, e->stream));
+        HIPCHK(e, hipMemcpyAsync(first_from, d_ff, 4 * cells, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(d_ff);
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
 

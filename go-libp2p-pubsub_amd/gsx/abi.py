@@ -198,6 +198,58 @@ class SynthSpec(C.Structure):
     ]
 
 
+GSX_ROUTER_FLOODSUB = 0
+GSX_ROUTER_GOSSIPSUB = 1
+GSX_ROUTER_RANDOMSUB = 2
+GSX_MAX_HOPS = 64
+
+
+class PropConfig(C.Structure):
+    _fields_ = [
+        ("router", C.c_uint32),
+        ("topic", C.c_uint32),
+        ("flood_publish", C.c_uint32),
+        ("max_hops", C.c_uint32),
+        ("hop_latency_ns", C.c_int64),
+        ("now_ns", C.c_int64),
+        ("credit_scores", C.c_uint32),
+        ("randomsub_size", C.c_uint32),
+        ("seed", C.c_uint64),
+    ]
+
+
+class PropOut(C.Structure):
+    _fields_ = [
+        ("deliveries", C.c_uint64),
+        ("duplicates", C.c_uint64),
+        ("transmissions", C.c_uint64),
+        ("hops", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("hop_deliveries", C.c_uint64 * (GSX_MAX_HOPS + 1)),
+    ]
+
+    def as_dict(self):
+        return dict(deliveries=self.deliveries, duplicates=self.duplicates, transmissions=self.transmissions,
+                    hops=self.hops, hop_deliveries=list(self.hop_deliveries)[: self.hops + 1])
+
+
+class Msg(C.Structure):
+    _fields_ = [("source", C.c_uint32), ("reserved", C.c_uint32), ("msg_id", C.c_uint64)]
+
+
+_MSG_DTYPE = None
+
+
+def msg_dtype():
+    global _MSG_DTYPE
+    if _MSG_DTYPE is None:
+        import numpy as np
+
+        _MSG_DTYPE = np.dtype([("source", "<u4"), ("reserved", "<u4"), ("msg_id", "<u8")], align=True)
+        assert _MSG_DTYPE.itemsize == C.sizeof(Msg)
+    return _MSG_DTYPE
+
+
 P = C.POINTER
 _u64p = P(C.c_uint64)
 
@@ -239,6 +291,8 @@ SIGNATURES = {
     "gsx_export_state": (C.c_int, [C.c_void_p, P(StateView)]),
     "gsx_last_refresh_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),
     "gsx_synthesize_state": (C.c_int, [C.c_void_p, P(SynthSpec)]),
+    "gsx_propagate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), P(PropOut)]),
+    "gsx_prop_results": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_int32)]),
     "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_timing_end": (
         C.c_int,

@@ -93,6 +93,7 @@ class Engine:
         v = C.c_uint64()
         self._chk(self.lib.gsx_num_pairs(self.h, C.byref(v)), "gsx_num_pairs")
         self.n_pairs = int(v.value)
+        self.n_nodes = n
 
     def set_ip_whitelist(self, ips: Iterable[int]):
         a = np.ascontiguousarray(list(ips), dtype=np.uint32)
@@ -158,6 +159,22 @@ class Engine:
         v = C.c_float()
         self._chk(self.lib.gsx_last_refresh_ms(self.h, C.byref(v)), "gsx_last_refresh_ms")
         return float(v.value)
+
+    def propagate(self, msgs, cfg: abi.PropConfig, want_results: bool = False):
+        """-> (PropOut, hop [m, n] or None, first_from [m, n] or None)"""
+        ms = np.ascontiguousarray(msgs, dtype=abi.msg_dtype())
+        out = abi.PropOut()
+        self._chk(
+            self.lib.gsx_propagate(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg), C.byref(out)),
+            "gsx_propagate",
+        )
+        hop = frm = None
+        if want_results:
+            n = self.n_nodes
+            hop = np.empty((len(ms), n), dtype=np.uint8)
+            frm = np.empty((len(ms), n), dtype=np.int32)
+            self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
+        return out, hop, frm
 
     def timing_begin(self, max_launches: int):
         self._chk(self.lib.gsx_timing_begin(self.h, max_launches), "gsx_timing_begin")

@@ -325,6 +325,64 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* spec);
  * events on the engine stream (ms).  Requires gsx_sync. */
 int gsx_last_refresh_ms(gsx_engine* e, float* ms);
 
+/* ---- message propagation (floodsub / gossipsub / randomsub forwarding) ---- */
+/* Synchronous-hop restatement of the forwarding path (SURVEY.md §7, §8a
+ * A13-A14): pushMsg's seen-dedup (pubsub.go:1046-1090, 919-936) and the
+ * routers' Publish (floodsub.go:76-100, gossipsub.go:943-1013,
+ * randomsub.go:99-160) over the loaded overlay.
+ *   - hop 0: message m is published at its source (origin = source);
+ *   - hop h: every vertex that first saw m at hop h-1 sends it to its
+ *     router's targets for the topic, except the peer it first got m from and
+ *     the origin (floodsub.go:82, gossipsub.go:1007, randomsub.go:113);
+ *   - a vertex first seeing m at hop h records the LOWEST-indexed sender of
+ *     that hop as its first deliverer; later or other copies are duplicates;
+ *   - "in topic" (ps.topics[topic]) = the pair is present and connected;
+ *     mesh membership = the scorer's inMesh flag of (pair, topic), which the
+ *     router keeps in step through Graft/Prune traces;
+ *   - validation is instantaneous: a duplicate arriving (hop - first hop) *
+ *     hop_latency_ns after the first receipt is inside the P3 window iff
+ *     that is <= MeshMessageDeliveriesWindow (score.go:965).
+ * With credit_scores set, first receipts and duplicates are folded into the
+ * receiver's counters exactly as DeliverMessage / DuplicateMessage would
+ * (score.go:695-719, 788-820: +1 then cap, one step per message). */
+enum gsx_router { GSX_ROUTER_FLOODSUB = 0, GSX_ROUTER_GOSSIPSUB = 1, GSX_ROUTER_RANDOMSUB = 2 };
+
+typedef struct gsx_prop_config {
+    uint32_t router;          /* gsx_router                                        */
+    uint32_t topic;           /* the messages' topic                               */
+    uint32_t flood_publish;   /* WithFloodPublish (gossipsub.go:306-317, 953-960)  */
+    uint32_t max_hops;        /* hop bound, <= GSX_MAX_HOPS                        */
+    int64_t hop_latency_ns;   /* simulated time per hop                           */
+    int64_t now_ns;           /* publish time                                      */
+    uint32_t credit_scores;   /* fold deliveries into P2/P3 counters               */
+    uint32_t randomsub_size;  /* RandomSub's `size` (randomsub.go:21-27)           */
+    uint64_t seed;            /* RandomSub draws: h(seed, 7, vertex, msg_id<<16|k) */
+} gsx_prop_config;
+
+#define GSX_MAX_HOPS 64
+
+typedef struct gsx_msg {
+    uint32_t source;  /* publishing node (the origin)  */
+    uint32_t reserved;
+    uint64_t msg_id;  /* used by RandomSub's draws     */
+} gsx_msg;
+
+typedef struct gsx_prop_out {
+    uint64_t deliveries;     /* first receipts by vertices other than the source */
+    uint64_t duplicates;     /* receipts of an already seen message             */
+    uint64_t transmissions;  /* sends: deliveries + duplicates                  */
+    uint32_t hops;           /* last hop with a first receipt                   */
+    uint32_t reserved;
+    uint64_t hop_deliveries[GSX_MAX_HOPS + 1]; /* first receipts per hop       */
+} gsx_prop_out;
+
+/* Propagates m messages (any m; processed in 64-message words). */
+int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out);
+/* Per (node, message) results of the last gsx_propagate: arrival hop
+ * (0xFF = never; 0 at the source) and first deliverer node (-1 = none), laid
+ * out [message][node].  Either pointer may be NULL. */
+int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from);
+
 /* Per-launch timing of the fused refresh+score kernel over a region: after
  * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls
  * brackets its kernel with a pair of HIP events on the engine stream;

@@ -68,6 +68,8 @@ struct orc_engine {
     uint32_t T;
     ipcount_map ipc;
     int64_t last_refresh; /* now of the last refreshScores() (state view only) */
+    gsx_thresholds th;
+    uint8_t* eflags; /* GSX_EDGE_* per pair */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -232,6 +234,7 @@ void orc_destroy(orc_engine* o) {
     free(o->ts);
     free(o->app);
     free(o->whitelist);
+    free(o->eflags);
     free(o->ipc.keys);
     free(o->ipc.vals);
     free_records(o);
@@ -269,8 +272,12 @@ int orc_set_topic_params(orc_engine* o, uint32_t topic, const gsx_topic_score_pa
 }
 
 int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
-                     const uint32_t* node_ips) {
+                     const uint8_t* edge_flags, const uint32_t* node_ips) {
     uint64_t E = (uint64_t)row_ptr[n_nodes];
+    free(o->eflags);
+    o->eflags = (uint8_t*)calloc(E ? E : 1, 1);
+    if (!o->eflags) return GSX_ENOMEM;
+    if (edge_flags && E) memcpy(o->eflags, edge_flags, E);
     free(o->row_ptr);
     free(o->col);
     free(o->node_ips);
@@ -860,6 +867,217 @@ uint64_t orc_num_delivery_records(orc_engine* o) { return o->n_alive; }
 
 /* ------------------------------------------------------------------------ */
 /* state view                                                               */
+
+/* ------------------------------------------------------------------------ */
+/* propagation: floodsub.go:76-100, gossipsub.go:943-1013, randomsub.go:99-160 */
+
+int orc_set_thresholds(orc_engine* o, const gsx_thresholds* t) {
+    o->th = *t;
+    return 0;
+}
+
+/* p in ps.topics[topic] / ps.peers: connected and tracked */
+static bool in_topic(const orc_engine* o, uint64_t r) { return o->ps[r].present && o->ps[r].connected; }
+
+/* the pair (u -> v) given the pair (v -> u); -1 if u does not track v */
+static int64_t reverse_pair(const orc_engine* o, uint64_t r) {
+    uint32_t v = o->pair_obs[r];
+    uint32_t u = (uint32_t)o->col[r];
+    for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++)
+        if ((uint32_t)o->col[q] == v) return q;
+    return -1;
+}
+
+/* Go's rand.Intn(n) = Int31n (math/rand), with Int31 draws taken from the
+ * counter hash h(seed, 7, vertex, msg_id << 16 | k): the canonical RNG of
+ * SURVEY.md §7 in place of the global math/rand source. */
+static uint64_t splitmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
+    uint64_t inner = splitmix(tag ^ splitmix(a ^ splitmix(b)));
+    return splitmix(seed + 0x9E3779B97F4A7C15ULL * (1 + inner));
+}
+typedef struct {
+    uint64_t seed, vertex, base;
+    uint32_t k;
+} orc_rng;
+static int32_t rng_int31(orc_rng* g) { return (int32_t)(h4(g->seed, 7, g->vertex, g->base | g->k++) >> 33); }
+static int32_t rng_int31n(orc_rng* g, int32_t n) {
+    if ((n & (n - 1)) == 0) return rng_int31(g) & (n - 1);
+    int32_t max = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
+    int32_t v = rng_int31(g);
+    while (v > max) v = rng_int31(g);
+    return v % n;
+}
+/* shufflePeers, gossipsub.go:1890-1895 */
+static void shuffle_pairs(uint64_t* a, int n, orc_rng* g) {
+    for (int i = 0; i < n; i++) {
+        int j = rng_int31n(g, i + 1);
+        uint64_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+}
+
+#define RANDOMSUB_D 6 /* randomsub.go:16-18 */
+
+/* The pairs (v -> u) a vertex sends message m to: rt.Publish with
+ * msg.ReceivedFrom = from (-1 when v published it) and GetFrom() = origin.
+ * Returns the count; `out` has room for deg(v). */
+static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v, uint32_t origin, int64_t from,
+                          uint64_t msg_id, uint64_t* out, uint64_t* scratch) {
+    int n = 0;
+    const int64_t r0 = o->row_ptr[v], r1 = o->row_ptr[v + 1];
+    if (cfg->router == GSX_ROUTER_FLOODSUB) { /* floodsub.go:81-90 */
+        for (int64_t r = r0; r < r1; r++) {
+            uint32_t u = (uint32_t)o->col[r];
+            if (!in_topic(o, r)) continue;
+            if ((int64_t)u == from || u == origin) continue;
+            out[n++] = (uint64_t)r;
+        }
+        return n;
+    }
+    if (cfg->router == GSX_ROUTER_RANDOMSUB) { /* randomsub.go:99-160 */
+        int nrs = 0;
+        for (int64_t r = r0; r < r1; r++) {
+            uint32_t u = (uint32_t)o->col[r];
+            if (!in_topic(o, r)) continue;
+            if ((int64_t)u == from || u == origin) continue;
+            if (o->eflags[r] & GSX_EDGE_FLOODSUB) out[n++] = (uint64_t)r; /* rs.peers[p] == FloodSubID */
+            else scratch[nrs++] = (uint64_t)r;
+        }
+        if (nrs > RANDOMSUB_D) {
+            int target = RANDOMSUB_D;
+            int sq = (int)ceil(sqrt((double)cfg->randomsub_size));
+            if (sq > target) target = sq;
+            if (target > nrs) target = nrs;
+            orc_rng g = {cfg->seed, v, msg_id << 16, 0};
+            shuffle_pairs(scratch, nrs, &g); /* candidates in ascending neighbour order, then shuffled */
+            nrs = target;
+        }
+        for (int i = 0; i < nrs; i++) out[n++] = scratch[i];
+        return n;
+    }
+    /* gossipsub.go:943-1013 */
+    const uint32_t topic = cfg->topic;
+    const double thr = o->th.publish_threshold;
+    for (int64_t r = r0; r < r1; r++) {
+        if (!in_topic(o, r)) continue; /* tmap */
+        const uint8_t ef = o->eflags[r];
+        const bool direct = (ef & GSX_EDGE_DIRECT) != 0;
+        bool send;
+        if (cfg->flood_publish && from < 0) { /* :953-960 */
+            send = direct || score_pair(o, (uint64_t)r) >= thr;
+        } else {
+            const bool mesh_peer = (ef & GSX_EDGE_GOSSIPSUB) != 0; /* gs.feature(GossipSubFeatureMesh, ...) */
+            send = direct;                                          /* :962-968 */
+            if (!send && !mesh_peer) send = score_pair(o, (uint64_t)r) >= thr; /* :970-975 */
+            if (!send && topic < o->T) send = o->ts[(uint64_t)r * o->T + topic].in_mesh; /* gs.mesh[topic], :977-999 */
+        }
+        if (!send) continue;
+        uint32_t u = (uint32_t)o->col[r];
+        if ((int64_t)u == from || u == origin) continue; /* :1006-1009 */
+        out[n++] = (uint64_t)r;
+    }
+    return n;
+}
+
+typedef struct {
+    uint32_t u, v;
+    uint64_t r; /* the sending pair (v -> u) */
+} orc_arrival;
+
+static int arrival_cmp(const void* a, const void* b) {
+    const orc_arrival* x = (const orc_arrival*)a;
+    const orc_arrival* y = (const orc_arrival*)b;
+    if (x->u != y->u) return x->u < y->u ? -1 : 1;
+    if (x->v != y->v) return x->v < y->v ? -1 : 1;
+    return 0;
+}
+
+int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
+                  uint8_t* hop_out, int32_t* from_out) {
+    if (cfg->max_hops > GSX_MAX_HOPS) return GSX_EINVAL;
+    memset(out, 0, sizeof(*out));
+    const uint32_t N = o->n_nodes;
+    uint8_t* hop = (uint8_t*)malloc(N ? N : 1);
+    int32_t* from = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
+    uint32_t* frontier = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+    uint32_t* next = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+    uint64_t max_deg = 0;
+    for (uint32_t i = 0; i < N; i++)
+        if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > max_deg) max_deg = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+    uint64_t* tg = (uint64_t*)malloc(sizeof(uint64_t) * (max_deg ? max_deg : 1));
+    uint64_t* scratch = (uint64_t*)malloc(sizeof(uint64_t) * (max_deg ? max_deg : 1));
+    size_t cap_arr = 1024, n_arr = 0;
+    orc_arrival* arr = (orc_arrival*)malloc(sizeof(orc_arrival) * cap_arr);
+    const bool credit = cfg->credit_scores && cfg->topic < o->T && o->scored[cfg->topic];
+    for (size_t k = 0; k < m; k++) {
+        const uint32_t src = msgs[k].source;
+        if (src >= N) return GSX_ERANGE;
+        memset(hop, 0xFF, N);
+        for (uint32_t i = 0; i < N; i++) from[i] = -1;
+        hop[src] = 0; /* the local publish */
+        uint32_t nf = 1, nn;
+        frontier[0] = src;
+        for (uint32_t h = 1; h <= cfg->max_hops && nf > 0; h++) {
+            n_arr = 0;
+            for (uint32_t i = 0; i < nf; i++) {
+                const uint32_t v = frontier[i];
+                int nt = router_targets(o, cfg, v, src, from[v], msgs[k].msg_id, tg, scratch);
+                for (int j = 0; j < nt; j++) {
+                    if (n_arr == cap_arr) {
+                        cap_arr *= 2;
+                        arr = (orc_arrival*)realloc(arr, sizeof(orc_arrival) * cap_arr);
+                    }
+                    arr[n_arr].u = (uint32_t)o->col[tg[j]];
+                    arr[n_arr].v = v;
+                    arr[n_arr].r = tg[j];
+                    n_arr++;
+                }
+            }
+            /* each receiver handles its copies lowest sender first (pushMsg, pubsub.go:1046-1090) */
+            qsort(arr, n_arr, sizeof(orc_arrival), arrival_cmp);
+            nn = 0;
+            for (size_t a = 0; a < n_arr; a++) {
+                const uint32_t u = arr[a].u, v = arr[a].v;
+                out->transmissions++;
+                const int64_t q = credit ? reverse_pair(o, arr[a].r) : -1; /* u's peerStats for v */
+                if (hop[u] == 0xFF) { /* first receipt: markSeen + DeliverMessage */
+                    hop[u] = (uint8_t)h;
+                    from[u] = (int32_t)v;
+                    next[nn++] = u;
+                    out->deliveries++;
+                    out->hop_deliveries[h]++;
+                    if (q >= 0) mark_first(o, (uint64_t)q, cfg->topic);
+                } else { /* seenMessage -> DuplicateMessage, validated at the first receipt */
+                    out->duplicates++;
+                    if (q >= 0)
+                        mark_duplicate(o, (uint64_t)q, cfg->topic, true, cfg->now_ns + (int64_t)hop[u] * cfg->hop_latency_ns,
+                                       cfg->now_ns + (int64_t)h * cfg->hop_latency_ns);
+                }
+            }
+            if (nn > 0 && h > out->hops) out->hops = h;
+            memcpy(frontier, next, sizeof(uint32_t) * nn); /* already ascending: arrivals sorted by u */
+            nf = nn;
+        }
+        if (hop_out) memcpy(hop_out + k * (size_t)N, hop, N);
+        if (from_out) memcpy(from_out + k * (size_t)N, from, sizeof(int32_t) * N);
+    }
+    free(hop);
+    free(from);
+    free(frontier);
+    free(next);
+    free(tg);
+    free(scratch);
+    free(arr);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 
 int orc_import_state(orc_engine* o, const gsx_state_view* s) {
     uint64_t E = o->E;

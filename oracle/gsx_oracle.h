@@ -45,7 +45,13 @@ double orc_score_parameter_decay(int64_t decay_ns);
 int orc_set_peer_params(orc_engine* o, const gsx_peer_score_params* p);
 int orc_set_topic_params(orc_engine* o, uint32_t topic, const gsx_topic_score_params* p);
 int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
-                     const uint32_t* node_ips);
+                     const uint8_t* edge_flags, const uint32_t* node_ips);
+int orc_set_thresholds(orc_engine* o, const gsx_thresholds* t);
+/* Propagation (floodsub.go:76-100, gossipsub.go:943-1013, randomsub.go:99-160
+ * under the synchronous-hop contract of gsx.h), one message at a time.
+ * hop/from: optional [m][n_nodes] outputs. */
+int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
+                  uint8_t* hop, int32_t* from);
 int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);
 int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs);
 

@@ -29,7 +29,13 @@ _SIG = {
     "orc_score_parameter_decay": (C.c_double, [C.c_int64]),
     "orc_set_peer_params": (C.c_int, [C.c_void_p, P(abi.PeerScoreParams)]),
     "orc_set_topic_params": (C.c_int, [C.c_void_p, C.c_uint32, P(abi.TopicScoreParams)]),
-    "orc_load_overlay": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint32)]),
+    "orc_load_overlay": (
+        C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint8), P(C.c_uint32)]),
+    "orc_set_thresholds": (C.c_int, [C.c_void_p, P(abi.Thresholds)]),
+    "orc_propagate": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_size_t, P(abi.PropConfig), P(abi.PropOut), P(C.c_uint8), P(C.c_int32)],
+    ),
     "orc_set_ip_whitelist": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t]),
     "orc_set_app_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
     "orc_apply_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -100,7 +106,7 @@ class Oracle:
         self._chk(self.lib.orc_set_peer_params(self.h, C.byref(p)), "orc_set_peer_params")
 
     def set_thresholds(self, t):
-        self._chk(self.lib.orc_validate_thresholds(C.byref(t)), "orc_validate_thresholds")
+        self._chk(self.lib.orc_set_thresholds(self.h, C.byref(t)), "orc_set_thresholds")
 
     def set_topic_params(self, topic, p):
         self._chk(self.lib.orc_set_topic_params(self.h, topic, C.byref(p)), "orc_set_topic_params")
@@ -108,12 +114,30 @@ class Oracle:
     def load_overlay(self, row_ptr, col, edge_flags=None, node_ips=None):
         row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
         col = np.ascontiguousarray(col, dtype=np.int32)
+        ef = None if edge_flags is None else np.ascontiguousarray(edge_flags, dtype=np.uint8)
         ips = None if node_ips is None else np.ascontiguousarray(node_ips, dtype=np.uint32).reshape(-1)
         self._chk(
-            self.lib.orc_load_overlay(self.h, len(row_ptr) - 1, _p(row_ptr, C.c_int64), _p(col, C.c_int32), _p(ips, C.c_uint32)),
+            self.lib.orc_load_overlay(self.h, len(row_ptr) - 1, _p(row_ptr, C.c_int64), _p(col, C.c_int32),
+                                      _p(ef, C.c_uint8), _p(ips, C.c_uint32)),
             "orc_load_overlay",
         )
+        self.n_nodes = len(row_ptr) - 1
         self.n_pairs = int(self.lib.orc_num_pairs(self.h))
+
+    def propagate(self, msgs, cfg, want_results=False):
+        """-> (PropOut, hop [m, n] or None, first_from [m, n] or None)"""
+        ms = np.ascontiguousarray(msgs, dtype=abi.msg_dtype())
+        out = abi.PropOut()
+        hop = frm = None
+        if want_results:
+            hop = np.empty((len(ms), self.n_nodes), dtype=np.uint8)
+            frm = np.empty((len(ms), self.n_nodes), dtype=np.int32)
+        self._chk(
+            self.lib.orc_propagate(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg), C.byref(out),
+                                   _p(hop, C.c_uint8), _p(frm, C.c_int32)),
+            "orc_propagate",
+        )
+        return out, hop, frm
 
     def set_ip_whitelist(self, ips: Iterable[int]):
         a = np.ascontiguousarray(list(ips), dtype=np.uint32)

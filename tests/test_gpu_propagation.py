@@ -1,0 +1,70 @@
+"""Propagation on the GPU (through the C ABI) vs the CPU oracle: delivery sets,
+arrival hops, first deliverers, counters and the P2/P3 credits, bit-exact."""
+import numpy as np
+import pytest
+
+import gsx
+import oracle as orc
+import propagation_cases as pc
+from gsx import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # n, d, T, router, flood_publish, m, latency_ms, mix, direct, disconnect
+    (300, 3, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, 10, False, 0.0, 0.0),
+    (500, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 100, 10, True, 0.05, 0.05),
+    (500, 6, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 130, 10, True, 0.02, 0.0),
+    (800, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 64, 10, True, 0.0, 0.03),
+    (2000, 8, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 70, 1, False, 0.0, 0.0),
+    (3000, 6, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 192, 1, False, 0.0, 0.0),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"r{c[3]}-n{c[0]}-m{c[5]}" for c in CASES])
+def test_propagation_matches_oracle(gpu_ok, case):
+    n, d, T, router, fp, m, lat, mix, direct, disc = case
+    seed = n + m
+    ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=direct)
+    ms = pc.messages(n, m, seed)
+    cfg = pc.config(router, topic=T - 1, flood_publish=fp, latency_ms=lat, size=50)
+    res = []
+    for be in (gsx.Engine(T), orc.Oracle(T)):
+        pc.setup(be, ov, T, seed, disconnect_frac=disc)
+        out, hop, frm = be.propagate(ms, cfg, want_results=True)
+        res.append((out.as_dict(), hop, frm, be.export_state(), be.scores()))
+    (go, gh, gf, gs, gsc), (wo, wh, wf, ws, wsc) = res
+    assert go == wo
+    assert np.array_equal(gh, wh), np.argwhere(gh != wh)[:5]
+    assert np.array_equal(gf, wf), np.argwhere(gf != wf)[:5]
+    for f in abi.STATE_FIELDS:
+        assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
+    assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))
+    assert go["deliveries"] > 0
+
+
+def test_propagation_full_size_properties(gpu_ok):
+    """cfg2-style at 100k peers: every message reaches each vertex at most once;
+    floodsub arrival hops are BFS distances (checked on a sample of messages
+    with a numpy BFS); totals add up."""
+    n = 100_000
+    ov = pc.overlay(n, 6, seed=9)
+    e = gsx.Engine(1)
+    e.set_peer_params(synth.bench_peer_params())
+    e.set_topic_params(0, synth.spam_test_topic_params())
+    e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    e.synthesize_state(abi.SynthSpec(seed=9, now_ns=pc.T0, fmd_max=10, mmd_max=10, mfp_max=1, imd_max_sybil=0,
+                                     p_in_mesh=0.5, graft_window_ns=abi.HOUR, bp_max=0, p_disconnected=0,
+                                     p_absent=0, expire_jitter_ns=0, sybil_first_node=n))
+    ms = pc.messages(n, 64, seed=9)
+    out, hop, frm = e.propagate(ms, pc.config(abi.GSX_ROUTER_FLOODSUB, credit=0), want_results=True)
+    assert out.deliveries == int((hop != 0xFF).sum()) - len(ms)
+    assert out.transmissions == out.deliveries + out.duplicates
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import shortest_path
+
+    A = sp.csr_matrix((np.ones(ov.n_pairs), ov.col, ov.row_ptr), shape=(n, n))
+    dist = shortest_path(A, unweighted=True, indices=ms["source"][:4].astype(np.int64))
+    for k in range(4):
+        reach = np.isfinite(dist[k])
+        assert np.array_equal(hop[k][reach].astype(np.int64), dist[k][reach].astype(np.int64))
