@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--degree", type=int, default=6)
     ap.add_argument("--cpu-passes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prop-msgs", type=int, default=256, help="messages per propagation batch (0: skip)")
+    ap.add_argument("--prop-steps", type=int, default=5)
+    ap.add_argument("--prop-hops", type=int, default=24)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -168,6 +171,49 @@ def main():
     achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
     cfg_key = f"n={n},T={T},d={args.degree},E={E}"
     traffic = load_traffic(cfg_key)
+
+    # ---- secondary: message deliveries/s (gossipsub mesh forwarding, A13-A14) ----
+    prop = None
+    if args.prop_msgs > 0:
+        ms = np.zeros(args.prop_msgs, dtype=abi.msg_dtype())
+        ms["source"] = (synth.h(seed, synth.TAG_SRC, np.arange(args.prop_msgs), 0) % np.uint64(n)).astype(np.uint32)
+        ms["msg_id"] = np.arange(args.prop_msgs, dtype=np.uint64)
+        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                        accept_px_threshold=0, opportunistic_graft_threshold=0))
+        pcfg = abi.PropConfig(router=abi.GSX_ROUTER_GOSSIPSUB, topic=0, flood_publish=0, max_hops=args.prop_hops,
+                              hop_latency_ns=10 * abi.MILLISECOND, now_ns=now, credit_scores=1,
+                              randomsub_size=n, seed=seed)
+        e.propagate(ms, pcfg)  # warm-up
+        e.sync()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        tot = None
+        for _ in range(args.prop_steps):
+            out = e.propagate(ms, pcfg)[0]
+            tot = out if tot is None else tot
+        e.sync()
+        torch.cuda.synchronize(dev)
+        pt = time.perf_counter() - t0
+        barrier()
+        dl = float(tot.deliveries) * args.prop_steps
+        if dist is not None:
+            t = torch.tensor([pt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pt = float(t.item())
+            r = torch.tensor([dl], dtype=torch.float64, device=dev)
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            dl = float(r.item())
+        prop = {
+            "metric": "msg deliveries/s",
+            "value": dl / pt,
+            "ms_per_batch": pt / args.prop_steps * 1e3,
+            "messages_per_batch": args.prop_msgs,
+            "deliveries_per_batch": int(tot.deliveries),
+            "duplicates_per_batch": int(tot.duplicates),
+            "hops": int(tot.hops),
+            "router": "gossipsub (synthesized mesh, ~6 of ~12 peers per topic), P2/P3 credits on",
+        }
 
     cpu = None
     parity = None
@@ -243,6 +289,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "parity_vs_oracle": parity,
+        "propagation": prop,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

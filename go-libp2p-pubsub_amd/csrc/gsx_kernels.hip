@@ -352,10 +352,12 @@ __global__ __launch_bounds__(256) void k_untile_field(DevState s, int field, voi
     const uint32_t t = blockIdx.y;
     if (p >= s.n_pairs) return;
     const size_t i = (size_t)t * s.n_pairs + p;
+    const bool present = s.pflags[p] & PAIR_PRESENT;  // no peerStats: no topicStats either (export zeros)
     if (field < NFIELD)
-        static_cast<double*>(dst)[i] = s.rec[rec_index(p, t, s.n_topics, field)];
+        static_cast<double*>(dst)[i] = present ? s.rec[rec_index(p, t, s.n_topics, field)] : 0.0;
     else
-        static_cast<uint8_t*>(dst)[i] = s.rflags[flag_index(p, t, s.n_topics)] & (REC_IN_MESH | REC_ACTIVE);
+        static_cast<uint8_t*>(dst)[i] =
+            present ? (s.rflags[flag_index(p, t, s.n_topics)] & (REC_IN_MESH | REC_ACTIVE)) : 0;
 }
 
 __global__ __launch_bounds__(256) void k_mesh_time_export(DevState s, int64_t* __restrict__ dst) {
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256) void k_mesh_time_export(DevState s, int64_t* _
     const uint32_t t = blockIdx.y;
     if (p >= s.n_pairs) return;
     const uint8_t fl = s.rflags[flag_index(p, t, s.n_topics)];
-    dst[(size_t)t * s.n_pairs + p] = mesh_time_of(s, fl, p, t);
+    dst[(size_t)t * s.n_pairs + p] = (s.pflags[p] & PAIR_PRESENT) ? mesh_time_of(s, fl, p, t) : 0;
 }
 
 __global__ __launch_bounds__(256) void k_mesh_time_import(DevState s, const int64_t* __restrict__ src,

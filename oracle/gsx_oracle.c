@@ -1114,9 +1114,10 @@ int orc_export_state(orc_engine* o, gsx_state_view* s) {
                                                         (ps->connected ? GSX_PAIR_CONNECTED : 0));
         if (s->expire_ns) s->expire_ns[p] = ps->expire;
         if (s->behaviour_penalty) s->behaviour_penalty[p] = ps->behaviour_penalty;
+        static const orc_topic_stats none; /* a deleted peerStats has no topicStats: export zeros */
         for (uint32_t t = 0; t < o->T; t++) {
             size_t r = (size_t)t * E + p;
-            const orc_topic_stats* ts = &o->ts[p * o->T + t];
+            const orc_topic_stats* ts = ps->present ? &o->ts[p * o->T + t] : &none;
             if (s->first_message_deliveries) s->first_message_deliveries[r] = ts->first_message_deliveries;
             if (s->mesh_message_deliveries) s->mesh_message_deliveries[r] = ts->mesh_message_deliveries;
             if (s->mesh_failure_penalty) s->mesh_failure_penalty[r] = ts->mesh_failure_penalty;
