@@ -17,7 +17,7 @@ def overlay(n, d, seed, mix_protocols=False, direct_frac=0.0):
     if mix_protocols:  # some peers speak floodsub only (feature Mesh off)
         fl_nodes = rng.random(n) < 0.15
         fl_pair = fl_nodes[ov.col]
-        ef[fl_pair] = (ef[fl_pair] & ~abi.GSX_EDGE_GOSSIPSUB) | abi.GSX_EDGE_FLOODSUB
+        ef[fl_pair] = (ef[fl_pair] & np.uint8(0xFF ^ abi.GSX_EDGE_GOSSIPSUB)) | np.uint8(abi.GSX_EDGE_FLOODSUB)
     if direct_frac > 0:
         ef[rng.random(len(ef)) < direct_frac] |= abi.GSX_EDGE_DIRECT
     ov.edge_flags = ef
