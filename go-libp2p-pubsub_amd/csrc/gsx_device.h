@@ -156,6 +156,51 @@ hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* fron
 hipError_t launch_prop_credit(const PropState& ps, const DevState& s, hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
 
+// ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------
+constexpr int HB_MAX_DEG = 256;  // per-node pair count the mesh lanes hold (u16 offsets, scratch)
+constexpr int64_t HEARTBEAT_INTERVAL_NS = 1000000000LL;  // GossipSubHeartbeatInterval (clearBackoff slack)
+constexpr uint8_t HB_GRAFT = 1, HB_PRUNE = 2;            // control bytes [topic][pair]
+enum {
+    HB_GRAFTS = 0,
+    HB_PRUNES,
+    HB_ACCEPTED,
+    HB_REJECTED,
+    HB_PRUNES_HANDLED,
+    HB_PENALTIES,
+    HB_BACKOFF_CLEARED,
+    HB_MESH_LINKS,
+    HB_STAT_WORDS
+};  // the order of gsx_heartbeat_out
+
+struct DevGossipParams {
+    int32_t d, d_lo, d_hi, d_score, d_out, og_peers;
+    uint64_t og_ticks;
+    int64_t prune_backoff_ns, graft_flood_threshold_ns;
+};
+
+struct HbState {
+    const int64_t* row_ptr;
+    const uint32_t* rev;
+    const uint8_t* eflags;
+    int64_t* backoff;  // [topic][pair] expiry, 0 = no entry
+    uint8_t* ctl;      // [topic][pair (v -> u)] HB_GRAFT / HB_PRUNE sent by v this round
+    uint8_t* resp;     // [topic][pair (u -> v)] PRUNE answer u sends to a GRAFT of v
+    unsigned long long* stats;
+    uint64_t n_pairs;
+    uint32_t n_nodes;
+    uint64_t tick;
+    int64_t now;
+    uint64_t seed;
+    double og_threshold, graylist;  // PeerScoreThresholds (score_params.go:12-32)
+    DevGossipParams gp;
+};
+
+hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st);
+hipError_t launch_hb_mesh(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st);
+
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
 hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st);

@@ -93,6 +93,13 @@ struct gsx_engine {
     int64_t* d_row_ptr = nullptr;
     uint32_t* d_rev = nullptr;  // pair (u -> v) -> pair (v -> u)
     std::vector<uint8_t> eflags_host;
+    int64_t max_deg = 0;
+
+    // heartbeat: router params, backoff [topic][pair], this round's control bytes
+    gsx_gossipsub_params gp{};
+    int64_t* d_backoff = nullptr;
+    uint8_t *d_hbctl = nullptr, *d_hbresp = nullptr;
+    unsigned long long* d_hbstats = nullptr;
 
     // propagation buffers (grown on demand) and the last call's shape
     struct {
@@ -238,6 +245,12 @@ void free_state(gsx_engine* e) {
         if (p) (void)hipFree(p);
     e->prop = {};
     e->d_col = nullptr;
+    void* hb[] = {e->d_backoff, e->d_hbctl, e->d_hbresp, e->d_hbstats};
+    for (void* p : hb)
+        if (p) (void)hipFree(p);
+    e->d_backoff = nullptr;
+    e->d_hbctl = e->d_hbresp = nullptr;
+    e->d_hbstats = nullptr;
 }
 
 template <class T>
@@ -488,6 +501,7 @@ int gsx_create(const gsx_config* cfg, gsx_engine** out) {
     if (!e) return GSX_ENOMEM;
     e->device = cfg->device;
     e->T = cfg->n_topics;
+    gsx_default_gossipsub_params(&e->gp);
     if (hipSetDevice(e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev_start) != hipSuccess || hipEventCreate(&e->ev_stop) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) != hipSuccess ||
@@ -639,7 +653,8 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
         (rc = dalloc(e, &e->d_eflags, e->rs)) || (rc = dalloc(e, &e->d_expire, e->rs)) ||
         (rc = dalloc(e, &e->d_bp, e->rs)) || (rc = dalloc(e, &e->d_app, e->rs)) ||
         (rc = dalloc(e, &e->d_score, e->rs)) || (rc = dalloc(e, &e->d_ipg, 2 * e->rs)) ||
-        (rc = dalloc(e, &e->d_ipcount, e->n_groups)) || (rc = dalloc(e, &e->d_col, E))) {
+        (rc = dalloc(e, &e->d_ipcount, e->n_groups)) || (rc = dalloc(e, &e->d_col, E)) ||
+        (rc = dalloc(e, &e->d_backoff, (size_t)e->T * E))) {
         free_state(e);
         return rc;
     }
@@ -651,6 +666,9 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     HIPCHK(e, hipMemsetAsync(e->d_app, 0, sizeof(double) * e->rs, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_score, 0, sizeof(double) * e->rs, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_ipcount, 0, sizeof(uint32_t) * (e->n_groups ? e->n_groups : 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_backoff, 0, sizeof(int64_t) * e->T * (E ? E : 1), e->stream));
+    e->max_deg = 0;
+    for (uint32_t i = 0; i < n_nodes; ++i) e->max_deg = std::max<int64_t>(e->max_deg, row_ptr[i + 1] - row_ptr[i]);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (E) HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * E, hipMemcpyHostToDevice));
     {  // reverse pairs for the pull-based propagation
@@ -1137,6 +1155,111 @@ int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         (void)hipFree(d_ff);
     }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+// DefaultGossipSubParams, gossipsub.go:230-260
+int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
+    if (!p) return GSX_EINVAL;
+    std::memset(p, 0, sizeof(*p));
+    p->d = 6;
+    p->d_lo = 5;
+    p->d_hi = 12;
+    p->d_score = 4;
+    p->d_out = 2;
+    p->opportunistic_graft_peers = 2;
+    p->opportunistic_graft_ticks = 60;
+    p->prune_backoff_ns = 60LL * 1000000000LL;
+    p->graft_flood_threshold_ns = 10LL * 1000000000LL;
+    p->d_lazy = 6;
+    p->history_length = 5;
+    p->history_gossip = 5;
+    p->max_ihave_length = 5000;
+    p->gossip_factor = 0.25;
+    return GSX_OK;
+}
+
+// The reference takes GossipSubParams unchecked; the mesh lanes index their
+// peer lists with D / Dscore, so negative or inverted degrees are refused.
+int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
+    if (!e || !p) return GSX_EINVAL;
+    if (p->d_lo < 0 || p->d < p->d_lo || p->d_hi < p->d || p->d_score < 0 || p->d_score > p->d_hi || p->d_out < 0 ||
+        p->opportunistic_graft_peers < 0 || p->prune_backoff_ns < 0)
+        return fail(e, GSX_EINVAL, "need 0 <= Dlo <= D <= Dhi, 0 <= Dscore <= Dhi, Dout, OG peers, backoff >= 0");
+    e->gp = *p;
+    return GSX_OK;
+}
+
+int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->max_deg > gsx::HB_MAX_DEG)
+        return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_MAX_DEG) + " peers per node");
+    std::memset(out, 0, sizeof(*out));
+    const size_t TE = (size_t)e->T * e->E;
+    if (!e->d_hbstats) {
+        int rc = 0;
+        if ((rc = dalloc(e, &e->d_hbctl, TE)) || (rc = dalloc(e, &e->d_hbresp, TE)) ||
+            (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
+            return rc;
+    }
+    // the scores of the heartbeat start (gossipsub.go:1333-1341)
+    if (int rc = ensure_scores(e)) return rc;
+    gsx::HbState h{};
+    h.row_ptr = e->d_row_ptr;
+    h.rev = e->d_rev;
+    h.eflags = e->d_eflags;
+    h.backoff = e->d_backoff;
+    h.ctl = e->d_hbctl;
+    h.resp = e->d_hbresp;
+    h.stats = e->d_hbstats;
+    h.n_pairs = e->E;
+    h.n_nodes = e->n_nodes;
+    h.tick = tick;
+    h.now = now;
+    h.seed = seed;
+    h.og_threshold = e->th.opportunistic_graft_threshold;
+    h.graylist = e->th.graylist_threshold;
+    h.gp = gsx::DevGossipParams{e->gp.d,       e->gp.d_lo,  e->gp.d_hi,
+                                e->gp.d_score, e->gp.d_out, e->gp.opportunistic_graft_peers,
+                                e->gp.opportunistic_graft_ticks, e->gp.prune_backoff_ns,
+                                e->gp.graft_flood_threshold_ns};
+    const gsx::DevState ds = dev_state(e);
+    HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_hbctl, 0, TE ? TE : 1, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_hbresp, 0, TE ? TE : 1, e->stream));
+    if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
+    HIPCHK(e, gsx::launch_hb_mesh(ds, h, e->stream));
+    // the receivers score the senders as the round left them
+    HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
+    HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
+    HIPCHK(e, gsx::launch_hb_mesh_links(ds, h, e->stream));
+    e->scores_valid = false;
+    unsigned long long st[gsx::HB_STAT_WORDS];
+    HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
+    std::memcpy(out, st, sizeof(st));
+    return GSX_OK;
+}
+
+int gsx_export_backoff(gsx_engine* e, int64_t* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    const size_t TE = (size_t)e->T * e->E;
+    if (TE) HIPCHK(e, hipMemcpyAsync(out, e->d_backoff, 8 * TE, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_import_backoff(gsx_engine* e, const int64_t* in) {
+    if (!e || !in) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    const size_t TE = (size_t)e->T * e->E;
+    if (TE) HIPCHK(e, hipMemcpyAsync(e->d_backoff, in, 8 * TE, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }

@@ -1,0 +1,318 @@
+// gsx_heartbeat.hip — the GossipSub heartbeat's mesh maintenance as one
+// synchronous round over the whole overlay (gsx.h, gsx_heartbeat).
+//
+//  (A) k_hb_mesh: one lane per (node v, topic t).  Everything the unit touches
+//      — the records, backoff entries and control bytes of v's own pairs for
+//      topic t — belongs to it alone, so the units run without atomics except
+//      for the round counters.  Candidate and mesh lists are at most
+//      HB_MAX_DEG pair offsets (u16) in scratch.  gossipsub.go:1344-1510.
+//  (B) k_hb_recv: one lane per receiving node u, walking its senders in
+//      ascending order (the Dhi check reads the mesh size the previous
+//      accepts left).  handleGraft / handlePrune, gossipsub.go:718-843.
+//  (C) k_hb_answer: one lane per pair, the GRAFT senders' handlePrune of the
+//      PRUNE answers.
+// Integer/byte work with scattered reads of the per-pair score cache; it runs
+// once per heartbeat, not per refresh, so clarity wins over lane efficiency.
+#include "gsx_ops.h"
+
+namespace gsx {
+
+constexpr uint64_t TAG_HEARTBEAT = 8;
+
+__device__ __forceinline__ void count(unsigned long long* stats, int k, unsigned long long n = 1) {
+    atomicAdd(&stats[k], n);
+}
+
+__device__ __forceinline__ bool hb_in_mesh(const DevState& s, uint64_t r, uint32_t t) {
+    return (s.pflags[r] & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH);
+}
+
+// addBackoff / doAddBackoff, gossipsub.go:845-859 (0 = no entry; the zero
+// time is before every expiry)
+__device__ __forceinline__ void add_backoff(const HbState& h, uint64_t r, uint32_t t, int64_t interval) {
+    int64_t* b = &h.backoff[(size_t)t * h.n_pairs + r];
+    const int64_t expire = h.now + interval;
+    if (*b == 0 || *b < expire) *b = expire;
+}
+
+// clearBackoff, gossipsub.go:1585-1604
+__global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    bool cleared = false;
+    if (i < n) {
+        const int64_t b = h.backoff[i];
+        if (b != 0 && b + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
+            h.backoff[i] = 0;
+            cleared = true;
+        }
+    }
+    const unsigned long long c = __popcll(__ballot(cleared));
+    if (c && (threadIdx.x % 64) == 0) count(h.stats, HB_BACKOFF_CLEARED, c);
+}
+
+struct HbUnit {
+    const DevState& s;
+    const HbState& h;
+    uint32_t t;
+    int64_t r0;  // first pair of the row
+    int deg;
+
+    __device__ bool in_mesh(int i) const { return hb_in_mesh(s, r0 + i, t); }
+    __device__ uint8_t ef(int i) const { return h.eflags[r0 + i]; }
+    __device__ double score(int i) const { return s.score[r0 + i]; }
+
+    __device__ int mesh_list(uint16_t* out) const {
+        int n = 0;
+        for (int i = 0; i < deg; ++i)
+            if (in_mesh(i)) out[n++] = (uint16_t)i;
+        return n;
+    }
+
+    // getPeers, gossipsub.go:1852-1872: mesh-capable topic peers passing the
+    // filter, ascending, shuffled, truncated to count.  score_cmp 0: score >=
+    // ref, 1: score > ref.
+    __device__ int get_peers(int count_max, bool outbound_only, int score_cmp, double ref, uint16_t* out,
+                             Rng& g) const {
+        int n = 0;
+        for (int i = 0; i < deg; ++i) {
+            const uint64_t r = r0 + i;
+            if ((s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED)) continue;
+            const uint8_t f = ef(i);
+            if (!(f & EDGE_GOSSIPSUB)) continue;
+            if (in_mesh(i)) continue;
+            if (h.backoff[(size_t)t * h.n_pairs + r] != 0) continue;  // map presence (:1377)
+            if (f & EDGE_DIRECT) continue;
+            if (outbound_only && !(f & EDGE_OUTBOUND)) continue;
+            const double sc = score(i);
+            if (score_cmp == 0 && !(sc >= ref)) continue;
+            if (score_cmp == 1 && !(sc > ref)) continue;
+            out[n++] = (uint16_t)i;
+        }
+        g.shuffle(out, n);
+        if (count_max > 0 && n > count_max) n = count_max;
+        return n;
+    }
+
+    __device__ void graft(int i) const {  // graftPeer, :1353-1359
+        ev_graft(s, r0 + i, t, h.now);
+        h.ctl[(size_t)t * h.n_pairs + r0 + i] = HB_GRAFT;
+        count(h.stats, HB_GRAFTS);
+    }
+    __device__ void prune(int i) const {  // prunePeer, :1345-1351
+        ev_prune(s, r0 + i, t);
+        add_backoff(h, r0 + i, t, h.gp.prune_backoff_ns);
+        h.ctl[(size_t)t * h.n_pairs + r0 + i] = HB_PRUNE;
+        count(h.stats, HB_PRUNES);
+    }
+
+    // stable insertion sort by cached score
+    __device__ void sort_by_score(uint16_t* a, int n, bool desc) const {
+        for (int i = 1; i < n; ++i) {
+            const uint16_t x = a[i];
+            const double sx = score(x);
+            int j = i - 1;
+            while (j >= 0 && (desc ? score(a[j]) < sx : score(a[j]) > sx)) {
+                a[j + 1] = a[j];
+                --j;
+            }
+            a[j + 1] = x;
+        }
+    }
+
+    __device__ static void rotate(uint16_t* a, int i) {  // :1411-1418
+        const uint16_t p = a[i];
+        for (int j = i; j > 0; --j) a[j] = a[j - 1];
+        a[0] = p;
+    }
+};
+
+__global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h) {
+    const uint64_t u = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (u >= (uint64_t)h.n_nodes * s.n_topics) return;
+    const uint32_t v = (uint32_t)(u / s.n_topics), t = (uint32_t)(u % s.n_topics);
+    const int64_t r0 = h.row_ptr[v];
+    const HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
+    const DevGossipParams& gp = h.gp;
+    Rng g{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), 0};
+    uint16_t plst[HB_MAX_DEG], tmp[HB_MAX_DEG];
+
+    // drop all peers with negative score, without PX (:1361-1368)
+    int n = U.mesh_list(plst);
+    for (int i = 0; i < n; ++i)
+        if (U.score(plst[i]) < 0) U.prune(plst[i]);
+    // do we have enough peers? (:1370-1385)
+    n = U.mesh_list(plst);
+    if (n < gp.d_lo) {
+        const int k = U.get_peers(gp.d - n, false, 0, 0.0, tmp, g);
+        for (int i = 0; i < k; ++i) U.graft(tmp[i]);
+    }
+    // do we have too many peers? (:1387-1448)
+    n = U.mesh_list(plst);
+    if (n > gp.d_hi) {
+        g.shuffle(plst, n);
+        U.sort_by_score(plst, n, true);
+        g.shuffle(plst + gp.d_score, n - gp.d_score);
+        int outbound = 0;
+        for (int i = 0; i < gp.d; ++i)
+            if (U.ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
+        if (outbound < gp.d_out) {
+            if (outbound > 0) {
+                int ihave = outbound;
+                for (int i = 1; i < gp.d && ihave > 0; ++i)
+                    if (U.ef(plst[i]) & EDGE_OUTBOUND) {
+                        HbUnit::rotate(plst, i);
+                        --ihave;
+                    }
+            }
+            int ineed = gp.d_out - outbound;
+            for (int i = gp.d; i < n && ineed > 0; ++i)
+                if (U.ef(plst[i]) & EDGE_OUTBOUND) {
+                    HbUnit::rotate(plst, i);
+                    --ineed;
+                }
+        }
+        for (int i = gp.d; i < n; ++i) U.prune(plst[i]);
+    }
+    // do we have enough outbound peers? (:1450-1476)
+    n = U.mesh_list(plst);
+    if (n >= gp.d_lo) {
+        int outbound = 0;
+        for (int i = 0; i < n; ++i)
+            if (U.ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
+        if (outbound < gp.d_out) {
+            const int k = U.get_peers(gp.d_out - outbound, true, 0, 0.0, tmp, g);
+            for (int i = 0; i < k; ++i) U.graft(tmp[i]);
+        }
+    }
+    // opportunistic grafting (:1478-1510)
+    n = U.mesh_list(plst);
+    if (gp.og_ticks && h.tick % gp.og_ticks == 0 && n > 1) {
+        U.sort_by_score(plst, n, false);
+        const double median = U.score(plst[n / 2]);
+        if (median < h.og_threshold) {
+            const int k = U.get_peers(gp.og_peers, false, 1, median, tmp, g);
+            for (int i = 0; i < k; ++i) U.graft(tmp[i]);
+        }
+    }
+}
+
+// handlePrune at the owner of pair q for topic t (:811-843): the tracer's
+// Prune, then the PRUNE's backoff, which travels in whole seconds (:1821).
+__device__ __forceinline__ void handle_prune(const DevState& s, const HbState& h, uint64_t q, uint32_t t) {
+    ev_prune(s, q, t);
+    const int64_t secs = h.gp.prune_backoff_ns / 1000000000LL;
+    add_backoff(h, q, t, secs > 0 ? secs * 1000000000LL : h.gp.prune_backoff_ns);
+    count(h.stats, HB_PRUNES_HANDLED);
+}
+
+__global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
+    const uint32_t u = blockIdx.x * 64u + threadIdx.x;
+    if (u >= h.n_nodes) return;
+    const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+    const DevGossipParams& gp = h.gp;
+    for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
+        const uint32_t r = h.rev[q];     // r = (v -> u), the sender's pair
+        if (r == NO_PAIR) continue;
+        const double score = s.score[q];  // gs.score.Score(p) once per control message
+        const uint8_t ef = h.eflags[q];
+        // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
+        if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
+        for (uint32_t t = 0; t < s.n_topics; ++t) {  // handleGraft, :718-809
+            if (h.ctl[(size_t)t * h.n_pairs + r] != HB_GRAFT) continue;
+            if (hb_in_mesh(s, q, t)) continue;
+            uint8_t* const resp = &h.resp[(size_t)t * h.n_pairs + q];
+            if (ef & EDGE_DIRECT) {
+                *resp = 1;
+                count(h.stats, HB_REJECTED);
+                continue;
+            }
+            const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
+            if (expire != 0 && h.now < expire) {
+                ev_penalty(s, q, 1);
+                count(h.stats, HB_PENALTIES);
+                if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
+                    ev_penalty(s, q, 1);
+                    count(h.stats, HB_PENALTIES);
+                }
+                add_backoff(h, q, t, gp.prune_backoff_ns);
+                *resp = 1;
+                count(h.stats, HB_REJECTED);
+                continue;
+            }
+            if (score < 0) {
+                *resp = 1;
+                add_backoff(h, q, t, gp.prune_backoff_ns);
+                count(h.stats, HB_REJECTED);
+                continue;
+            }
+            int n = 0;
+            for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
+            if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
+                *resp = 1;
+                add_backoff(h, q, t, gp.prune_backoff_ns);
+                count(h.stats, HB_REJECTED);
+                continue;
+            }
+            ev_graft(s, q, t, h.now);
+            count(h.stats, HB_ACCEPTED);
+        }
+        for (uint32_t t = 0; t < s.n_topics; ++t)  // handlePrune
+            if (h.ctl[(size_t)t * h.n_pairs + r] == HB_PRUNE) handle_prune(s, h, q, t);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;  // r = (v -> u)
+    if (r >= h.n_pairs) return;
+    const uint32_t q = h.rev[r];
+    if (q == NO_PAIR) return;
+    if (!(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) return;  // AcceptFrom
+    for (uint32_t t = 0; t < s.n_topics; ++t)
+        if (h.resp[(size_t)t * h.n_pairs + q]) handle_prune(s, h, r, t);
+}
+
+__global__ __launch_bounds__(256) void k_hb_mesh_links(DevState s, HbState h) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    unsigned long long c = 0;
+    if (r < h.n_pairs)
+        for (uint32_t t = 0; t < s.n_topics; ++t) c += hb_in_mesh(s, r, t);
+    // wave sum
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+    if ((threadIdx.x % 64) == 0 && c) count(h.stats, HB_MESH_LINKS, c);
+}
+
+static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
+    const uint64_t n = (uint64_t)n_topics * h.n_pairs;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(blocks_for(n, 256)), dim3(256), 0, st, h, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_mesh(const DevState& s, const HbState& h, hipStream_t st) {
+    const uint64_t n = (uint64_t)h.n_nodes * s.n_topics;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_mesh, dim3(blocks_for(n, 64)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_recv, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_answer, dim3(blocks_for(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_mesh_links, dim3(blocks_for(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    return hipGetLastError();
+}
+
+}  // namespace gsx

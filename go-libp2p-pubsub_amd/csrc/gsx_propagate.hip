@@ -10,7 +10,7 @@
 // word is written by exactly one thread.  Router semantics: floodsub.go:76-100,
 // gossipsub.go:943-1013, randomsub.go:99-160; dedup: pubsub.go:919-936,
 // 1046-1090.  Integer/bit work only: HBM/L2 bound, no MFMA, no LDS.
-#include "gsx_device.h"
+#include "gsx_ops.h"
 
 namespace gsx {
 
@@ -52,29 +52,8 @@ __global__ __launch_bounds__(256) void k_prop_init(PropState ps, uint64_t* front
     ps.hop[(size_t)k * ps.n_nodes + src] = 0;
 }
 
-// ---- RandomSub's draw -------------------------------------------------------
-__device__ __forceinline__ uint64_t smix(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
-    return smix(seed + 0x9E3779B97F4A7C15ull * (1ull + smix(tag ^ smix(a ^ smix(b)))));
-}
-// math/rand's Int31n over Int31 draws h(seed, 7, vertex, base | k): the
-// canonical RNG standing in for the global rand source.
-struct Rng {
-    uint64_t seed, vertex, base;
-    uint32_t k;
-    __device__ int32_t int31() { return (int32_t)(h4(seed, 7, vertex, base | k++) >> 33); }
-    __device__ int32_t int31n(int32_t n) {
-        if ((n & (n - 1)) == 0) return int31() & (n - 1);
-        const int32_t max = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
-        int32_t v = int31();
-        while (v > max) v = int31();
-        return v % n;
-    }
-};
+// ---- RandomSub's draw: the canonical RNG with tag 7 (gsx_ops.h) ----------
+constexpr uint64_t TAG_RANDOMSUB = 7;
 
 // For every frontier vertex v and message m of this hop (randomsub.go:112-143):
 // candidates = its non-FloodSub topic peers except `from` and the origin, in
@@ -105,13 +84,8 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
                 int target = RANDOMSUB_D;
                 if ((int)ps.rsub_sqrt > target) target = (int)ps.rsub_sqrt;
                 if (target > n) target = n;
-                Rng g{ps.seed, v, ps.msgs[k].msg_id << 16, 0};
-                for (int i = 0; i < n; ++i) {
-                    const int j = g.int31n(i + 1);
-                    const uint32_t t = cand[i];
-                    cand[i] = cand[j];
-                    cand[j] = t;
-                }
+                Rng g{ps.seed, TAG_RANDOMSUB, v, ps.msgs[k].msg_id << 16, 0};
+                g.shuffle(cand, n);
                 keep = target;
             }
             for (int i = 0; i < keep; ++i) ps.sel[(size_t)w * ps.n_pairs + cand[i]] |= 1ull << b;

@@ -250,6 +250,41 @@ def msg_dtype():
     return _MSG_DTYPE
 
 
+class GossipSubParams(C.Structure):
+    _fields_ = [
+        ("d", C.c_int32),
+        ("d_lo", C.c_int32),
+        ("d_hi", C.c_int32),
+        ("d_score", C.c_int32),
+        ("d_out", C.c_int32),
+        ("opportunistic_graft_peers", C.c_int32),
+        ("opportunistic_graft_ticks", C.c_uint64),
+        ("prune_backoff_ns", C.c_int64),
+        ("graft_flood_threshold_ns", C.c_int64),
+        ("d_lazy", C.c_int32),
+        ("history_length", C.c_int32),
+        ("history_gossip", C.c_int32),
+        ("max_ihave_length", C.c_int32),
+        ("gossip_factor", C.c_double),
+    ]
+
+
+class HeartbeatOut(C.Structure):
+    _fields_ = [
+        ("grafts", C.c_uint64),
+        ("prunes", C.c_uint64),
+        ("graft_accepted", C.c_uint64),
+        ("graft_rejected", C.c_uint64),
+        ("prunes_handled", C.c_uint64),
+        ("penalties", C.c_uint64),
+        ("backoff_cleared", C.c_uint64),
+        ("mesh_links", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
 P = C.POINTER
 _u64p = P(C.c_uint64)
 
@@ -293,6 +328,11 @@ SIGNATURES = {
     "gsx_synthesize_state": (C.c_int, [C.c_void_p, P(SynthSpec)]),
     "gsx_propagate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), P(PropOut)]),
     "gsx_prop_results": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_int32)]),
+    "gsx_default_gossipsub_params": (C.c_int, [P(GossipSubParams)]),
+    "gsx_set_gossipsub_params": (C.c_int, [C.c_void_p, P(GossipSubParams)]),
+    "gsx_heartbeat": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64, P(HeartbeatOut)]),
+    "gsx_export_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "gsx_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_timing_end": (
         C.c_int,

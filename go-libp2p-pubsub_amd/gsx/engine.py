@@ -176,6 +176,24 @@ class Engine:
             self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
         return out, hop, frm
 
+    # -- heartbeat (gossipsub.go:1303-1604) ----------------------------------------------
+    def set_gossipsub_params(self, gp: abi.GossipSubParams):
+        self._chk(self.lib.gsx_set_gossipsub_params(self.h, C.byref(gp)), "gsx_set_gossipsub_params")
+
+    def heartbeat(self, tick: int, now: int, seed: int) -> abi.HeartbeatOut:
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.gsx_heartbeat(self.h, tick, now, seed, C.byref(out)), "gsx_heartbeat")
+        return out
+
+    def export_backoff(self) -> np.ndarray:
+        b = np.empty((self.n_topics, self.n_pairs), dtype=np.int64)
+        self._chk(self.lib.gsx_export_backoff(self.h, _ptr(b, C.c_int64)), "gsx_export_backoff")
+        return b
+
+    def import_backoff(self, b):
+        b = np.ascontiguousarray(b, dtype=np.int64).reshape(self.n_topics, self.n_pairs)
+        self._chk(self.lib.gsx_import_backoff(self.h, _ptr(b, C.c_int64)), "gsx_import_backoff")
+
     def timing_begin(self, max_launches: int):
         self._chk(self.lib.gsx_timing_begin(self.h, max_launches), "gsx_timing_begin")
 

@@ -383,6 +383,62 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
  * out [message][node].  Either pointer may be NULL. */
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from);
 
+/* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
+
+/* The GossipSubParams fields the heartbeat and its control handling read
+ * (gossipsub.go:62-199); gsx_default_gossipsub_params gives
+ * DefaultGossipSubParams (gossipsub.go:230-260). */
+typedef struct gsx_gossipsub_params {
+    int32_t d, d_lo, d_hi, d_score, d_out;  /* GossipSubD/Dlo/Dhi/Dscore/Dout   :33-37 */
+    int32_t opportunistic_graft_peers;      /* :54                               */
+    uint64_t opportunistic_graft_ticks;     /* :53                               */
+    int64_t prune_backoff_ns;               /* :47                               */
+    int64_t graft_flood_threshold_ns;       /* :55                               */
+    int32_t d_lazy;                         /* :40                               */
+    int32_t history_length, history_gossip; /* :38, :238 (HistoryGossip = 5!)   */
+    int32_t max_ihave_length;               /* :56                               */
+    double gossip_factor;                   /* :41                               */
+} gsx_gossipsub_params;
+
+int gsx_default_gossipsub_params(gsx_gossipsub_params* out);
+int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
+
+/* One heartbeat of every node at once, a synchronous round:
+ *  (A) every (node, topic) runs the mesh maintenance of gossipsub.go:1344-1510
+ *      with the scores of the heartbeat start (the router's per-heartbeat
+ *      cache, :1333-1341): prune negative-score peers, graft up to D when below
+ *      Dlo, prune down to D keeping Dscore by score and Dout outbound when
+ *      above Dhi, top up outbound peers, opportunistic graft every
+ *      OpportunisticGraftTicks; Graft/Prune traces update the scorer, pruned
+ *      peers are backed off (:845-859);
+ *  (B) every node handles the GRAFTs then PRUNEs sent to it (handleGraft /
+ *      handlePrune, :718-843), senders in ascending order, with the scores of
+ *      that moment: backoff / score / Dhi checks, P7 penalties for GRAFTs
+ *      inside the backoff (:752-770), PRUNE answers;
+ *  (C) the GRAFT senders handle those PRUNE answers.
+ * Randomness (shufflePeers, :1890-1895) is Go's Int31n rejection rule over
+ * draws h(seed, 8, node, tick << 32 | topic << 24 | k); candidate lists are in
+ * ascending peer order; the unstable sort.Slice of :1393 is a stable sort
+ * after the shuffle.  clearBackoff runs when tick % 15 == 0 (:1585-1604).
+ * All nodes are subscribed to (joined) every topic; "in topic" = present and
+ * connected; mesh membership is the scorer's inMesh flag.  */
+typedef struct gsx_heartbeat_out {
+    uint64_t grafts;          /* peers grafted by the heartbeats (A)              */
+    uint64_t prunes;          /* peers pruned by the heartbeats (A)               */
+    uint64_t graft_accepted;  /* GRAFTs accepted by their receivers (B)            */
+    uint64_t graft_rejected;  /* GRAFTs answered with PRUNE (B)                    */
+    uint64_t prunes_handled;  /* handlePrune calls (B + C)                         */
+    uint64_t penalties;       /* AddPenalty(p, 1) calls (B)                        */
+    uint64_t backoff_cleared; /* entries dropped by clearBackoff                   */
+    uint64_t mesh_links;      /* in-mesh (pair, topic) after the round             */
+} gsx_heartbeat_out;
+
+int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
+/* backoff expiry per [topic][pair] (0 = no entry), n_topics * n_pairs
+ * (gs.backoff, gossipsub.go:436; zeroed by gsx_load_overlay) */
+int gsx_export_backoff(gsx_engine* e, int64_t* out);
+int gsx_import_backoff(gsx_engine* e, const int64_t* in);
+
 /* Per-launch timing of the fused refresh+score kernel over a region: after
  * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls
  * brackets its kernel with a pair of HIP events on the engine stream;

@@ -70,6 +70,7 @@ struct orc_engine {
     int64_t last_refresh; /* now of the last refreshScores() (state view only) */
     gsx_thresholds th;
     uint8_t* eflags; /* GSX_EDGE_* per pair */
+    int64_t* backoff; /* gs.backoff[topic][peer] per [t][pair], 0 = no entry (gossipsub.go:436) */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -235,6 +236,7 @@ void orc_destroy(orc_engine* o) {
     free(o->app);
     free(o->whitelist);
     free(o->eflags);
+    free(o->backoff);
     free(o->ipc.keys);
     free(o->ipc.vals);
     free_records(o);
@@ -277,6 +279,9 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     free(o->eflags);
     o->eflags = (uint8_t*)calloc(E ? E : 1, 1);
     if (!o->eflags) return GSX_ENOMEM;
+    free(o->backoff);
+    o->backoff = (int64_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(int64_t));
+    if (!o->backoff) return GSX_ENOMEM;
     if (edge_flags && E) memcpy(o->eflags, edge_flags, E);
     free(o->row_ptr);
     free(o->col);
@@ -901,10 +906,10 @@ static uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
     return splitmix(seed + 0x9E3779B97F4A7C15ULL * (1 + inner));
 }
 typedef struct {
-    uint64_t seed, vertex, base;
+    uint64_t seed, tag, vertex, base;
     uint32_t k;
 } orc_rng;
-static int32_t rng_int31(orc_rng* g) { return (int32_t)(h4(g->seed, 7, g->vertex, g->base | g->k++) >> 33); }
+static int32_t rng_int31(orc_rng* g) { return (int32_t)(h4(g->seed, g->tag, g->vertex, g->base | g->k++) >> 33); }
 static int32_t rng_int31n(orc_rng* g, int32_t n) {
     if ((n & (n - 1)) == 0) return rng_int31(g) & (n - 1);
     int32_t max = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
@@ -954,7 +959,7 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
             int sq = (int)ceil(sqrt((double)cfg->randomsub_size));
             if (sq > target) target = sq;
             if (target > nrs) target = nrs;
-            orc_rng g = {cfg->seed, v, msg_id << 16, 0};
+            orc_rng g = {cfg->seed, 7, v, msg_id << 16, 0};
             shuffle_pairs(scratch, nrs, &g); /* candidates in ascending neighbour order, then shuffled */
             nrs = target;
         }
@@ -1074,6 +1079,303 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     free(tg);
     free(scratch);
     free(arr);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* heartbeat: gossipsub.go:1303-1604, 718-859                               */
+
+int orc_default_gossipsub_params(gsx_gossipsub_params* p) { /* DefaultGossipSubParams, gossipsub.go:230-260 */
+    memset(p, 0, sizeof(*p));
+    p->d = 6;
+    p->d_lo = 5;
+    p->d_hi = 12;
+    p->d_score = 4;
+    p->d_out = 2;
+    p->opportunistic_graft_peers = 2;
+    p->opportunistic_graft_ticks = 60;
+    p->prune_backoff_ns = 60LL * 1000000000LL;
+    p->graft_flood_threshold_ns = 10LL * 1000000000LL;
+    p->d_lazy = 6;
+    p->history_length = 5;
+    p->history_gossip = 5; /* HistoryGossip: GossipSubHistoryLength (:238) */
+    p->max_ihave_length = 5000;
+    p->gossip_factor = 0.25;
+    return 0;
+}
+
+#define HEARTBEAT_INTERVAL_NS (1000000000LL) /* GossipSubHeartbeatInterval, clearBackoff's slack (:1596) */
+
+typedef struct {
+    orc_engine* o;
+    const gsx_gossipsub_params* gp;
+    const double* cache; /* per pair: scores at the heartbeat start */
+    uint8_t* ctl;        /* [t][pair (v -> u)] 1 GRAFT, 2 PRUNE sent by v */
+    uint64_t tick;
+    int64_t now;
+    gsx_heartbeat_out* out;
+} hb_ctx;
+
+static bool hb_in_mesh(const orc_engine* o, uint64_t r, uint32_t t) {
+    return o->ps[r].present && o->ts[r * o->T + t].in_mesh;
+}
+static int64_t* hb_backoff(orc_engine* o, uint64_t r, uint32_t t) { return &o->backoff[(size_t)t * o->E + r]; }
+
+/* addBackoff / doAddBackoff, gossipsub.go:845-859 */
+static void add_backoff(orc_engine* o, uint64_t r, uint32_t t, int64_t now, int64_t interval) {
+    int64_t expire = now + interval;
+    int64_t* b = hb_backoff(o, r, t);
+    if (*b == 0 || *b < expire) *b = expire; /* backoff[p].Before(expire) (zero time is before everything) */
+}
+
+/* getPeers, gossipsub.go:1852-1872: topic peers with the mesh feature that
+ * pass the filter, in ascending order, shuffled, truncated to count. */
+enum { F_NOT_MESH = 1, F_NO_BACKOFF = 2, F_NOT_DIRECT = 4, F_OUTBOUND = 8 };
+static int get_peers(hb_ctx* c, uint32_t v, uint32_t t, int count, int filter, int score_cmp, double score_ref,
+                     uint64_t* out, orc_rng* g) {
+    orc_engine* o = c->o;
+    int n = 0;
+    for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+        if (!in_topic(o, (uint64_t)r)) continue;
+        const uint8_t ef = o->eflags[r];
+        if (!(ef & GSX_EDGE_GOSSIPSUB)) continue; /* gs.feature(GossipSubFeatureMesh, ...) */
+        if ((filter & F_NOT_MESH) && hb_in_mesh(o, (uint64_t)r, t)) continue;
+        if ((filter & F_NO_BACKOFF) && *hb_backoff(o, (uint64_t)r, t) != 0) continue; /* map presence (:1377) */
+        if ((filter & F_NOT_DIRECT) && (ef & GSX_EDGE_DIRECT)) continue;
+        if ((filter & F_OUTBOUND) && !(ef & GSX_EDGE_OUTBOUND)) continue;
+        const double s = c->cache[r];
+        if (score_cmp == 0 && !(s >= score_ref)) continue;
+        if (score_cmp == 1 && !(s > score_ref)) continue;
+        out[n++] = (uint64_t)r;
+    }
+    shuffle_pairs(out, n, g);
+    if (count > 0 && n > count) n = count;
+    return n;
+}
+
+static void hb_graft(hb_ctx* c, uint64_t r, uint32_t t) { /* graftPeer, :1353-1359 */
+    graft(c->o, r, t, c->now);
+    c->ctl[(size_t)t * c->o->E + r] = 1;
+    c->out->grafts++;
+}
+
+static void hb_prune(hb_ctx* c, uint64_t r, uint32_t t) { /* prunePeer, :1345-1351 */
+    prune(c->o, r, t);
+    add_backoff(c->o, r, t, c->now, c->gp->prune_backoff_ns);
+    c->ctl[(size_t)t * c->o->E + r] = 2;
+    c->out->prunes++;
+}
+
+static int mesh_list(const orc_engine* o, uint32_t v, uint32_t t, uint64_t* out) {
+    int n = 0;
+    for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++)
+        if (hb_in_mesh(o, (uint64_t)r, t)) out[n++] = (uint64_t)r;
+    return n;
+}
+
+/* stable sort of pairs by cached score; desc = 1 for descending */
+static void sort_by_score(const double* cache, uint64_t* a, int n, int desc) {
+    for (int i = 1; i < n; i++) { /* insertion sort: stable */
+        uint64_t x = a[i];
+        int j = i - 1;
+        while (j >= 0 && (desc ? cache[a[j]] < cache[x] : cache[a[j]] > cache[x])) {
+            a[j + 1] = a[j];
+            j--;
+        }
+        a[j + 1] = x;
+    }
+}
+
+/* the mesh maintenance of one (node, topic), gossipsub.go:1344-1510 */
+static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, uint64_t seed, uint64_t* plst, uint64_t* tmp) {
+    orc_engine* o = c->o;
+    const gsx_gossipsub_params* gp = c->gp;
+    orc_rng g = {seed, 8, v, (c->tick << 32) | ((uint64_t)t << 24), 0};
+    /* drop all peers with negative score, without PX (:1361-1368) */
+    int n = mesh_list(o, v, t, plst);
+    for (int i = 0; i < n; i++)
+        if (c->cache[plst[i]] < 0) hb_prune(c, plst[i], t);
+    /* do we have enough peers? (:1370-1385) */
+    n = mesh_list(o, v, t, plst);
+    if (n < gp->d_lo) {
+        int ineed = gp->d - n;
+        int k = get_peers(c, v, t, ineed, F_NOT_MESH | F_NO_BACKOFF | F_NOT_DIRECT, 0, 0.0, tmp, &g);
+        for (int i = 0; i < k; i++) hb_graft(c, tmp[i], t);
+    }
+    /* do we have too many peers? (:1387-1448) */
+    n = mesh_list(o, v, t, plst);
+    if (n > gp->d_hi) {
+        shuffle_pairs(plst, n, &g);
+        sort_by_score(c->cache, plst, n, 1);
+        shuffle_pairs(plst + gp->d_score, n - gp->d_score, &g);
+        int outbound = 0;
+        for (int i = 0; i < gp->d; i++)
+            if (o->eflags[plst[i]] & GSX_EDGE_OUTBOUND) outbound++;
+        if (outbound < gp->d_out) {
+            /* rotate(i): move plst[i] to the front (:1411-1418) */
+#define ROTATE(i)                                   \
+    do {                                            \
+        uint64_t p_ = plst[(i)];                    \
+        for (int j_ = (i); j_ > 0; j_--) plst[j_] = plst[j_ - 1]; \
+        plst[0] = p_;                               \
+    } while (0)
+            if (outbound > 0) {
+                int ihave = outbound;
+                for (int i = 1; i < gp->d && ihave > 0; i++)
+                    if (o->eflags[plst[i]] & GSX_EDGE_OUTBOUND) {
+                        ROTATE(i);
+                        ihave--;
+                    }
+            }
+            int ineed = gp->d_out - outbound;
+            for (int i = gp->d; i < n && ineed > 0; i++)
+                if (o->eflags[plst[i]] & GSX_EDGE_OUTBOUND) {
+                    ROTATE(i);
+                    ineed--;
+                }
+#undef ROTATE
+        }
+        for (int i = gp->d; i < n; i++) hb_prune(c, plst[i], t);
+    }
+    /* do we have enough outbound peers? (:1450-1476) */
+    n = mesh_list(o, v, t, plst);
+    if (n >= gp->d_lo) {
+        int outbound = 0;
+        for (int i = 0; i < n; i++)
+            if (o->eflags[plst[i]] & GSX_EDGE_OUTBOUND) outbound++;
+        if (outbound < gp->d_out) {
+            int ineed = gp->d_out - outbound;
+            int k = get_peers(c, v, t, ineed, F_NOT_MESH | F_NO_BACKOFF | F_NOT_DIRECT | F_OUTBOUND, 0, 0.0, tmp, &g);
+            for (int i = 0; i < k; i++) hb_graft(c, tmp[i], t);
+        }
+    }
+    /* opportunistic grafting (:1478-1510) */
+    n = mesh_list(o, v, t, plst);
+    if (gp->opportunistic_graft_ticks && c->tick % gp->opportunistic_graft_ticks == 0 && n > 1) {
+        sort_by_score(c->cache, plst, n, 0);
+        double median = c->cache[plst[n / 2]];
+        if (median < o->th.opportunistic_graft_threshold) {
+            int k = get_peers(c, v, t, gp->opportunistic_graft_peers, F_NOT_MESH | F_NO_BACKOFF | F_NOT_DIRECT, 1,
+                              median, tmp, &g);
+            for (int i = 0; i < k; i++) hb_graft(c, tmp[i], t);
+        }
+    }
+}
+
+/* handlePrune at u for a PRUNE of topic t from the peer of pair q (u -> v), :811-843 */
+static void handle_prune(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t q, uint32_t t, int64_t now,
+                         gsx_heartbeat_out* out) {
+    prune(o, q, t); /* tracer.Prune, unconditional */
+    /* the PRUNE carries PruneBackoff in whole seconds (:1821); 0 means "use our own" (:825-830) */
+    const int64_t secs = gp->prune_backoff_ns / 1000000000LL;
+    add_backoff(o, q, t, now, secs > 0 ? secs * 1000000000LL : gp->prune_backoff_ns);
+    out->prunes_handled++;
+}
+
+int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now, uint64_t seed,
+                  gsx_heartbeat_out* out) {
+    memset(out, 0, sizeof(*out));
+    const uint64_t E = o->E;
+    const uint32_t T = o->T;
+    /* clearBackoff (:1585-1604) */
+    if (tick % 15 == 0)
+        for (size_t i = 0; i < (size_t)T * E; i++)
+            if (o->backoff[i] != 0 && o->backoff[i] + 2 * HEARTBEAT_INTERVAL_NS < now) {
+                o->backoff[i] = 0;
+                out->backoff_cleared++;
+            }
+    double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
+    uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    uint8_t* resp = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    uint64_t max_deg = 1;
+    for (uint32_t i = 0; i < o->n_nodes; i++)
+        if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > max_deg) max_deg = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+    uint64_t* plst = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
+    uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
+    for (uint64_t r = 0; r < E; r++) cache[r] = score_pair(o, r); /* the heartbeat's score cache */
+    hb_ctx c = {o, gp, cache, ctl, tick, now, out};
+    /* (A) every node's heartbeat, every joined topic */
+    for (uint32_t v = 0; v < o->n_nodes; v++)
+        for (uint32_t t = 0; t < T; t++) hb_unit(&c, v, t, seed, plst, tmp);
+    /* (B) receivers: GRAFTs then PRUNEs of each sender, senders ascending */
+    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q); /* gs.score.Score(p) at handling time */
+    for (uint32_t u = 0; u < o->n_nodes; u++) {
+        for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) { /* q = (u -> v), ascending v */
+            const int64_t r = reverse_pair(o, (uint64_t)q);         /* r = (v -> u) */
+            if (r < 0) continue;
+            const double score = cache[q];
+            /* AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped */
+            if (!(o->eflags[q] & GSX_EDGE_DIRECT) && score < o->th.graylist_threshold) continue;
+            for (uint32_t t = 0; t < T; t++) { /* handleGraft, :718-809 */
+                if (ctl[(size_t)t * E + r] != 1) continue;
+                if (hb_in_mesh(o, (uint64_t)q, t)) continue;
+                const uint8_t ef = o->eflags[q];
+                if (ef & GSX_EDGE_DIRECT) {
+                    resp[(size_t)t * E + q] = 1;
+                    out->graft_rejected++;
+                    continue;
+                }
+                const int64_t expire = *hb_backoff(o, (uint64_t)q, t);
+                if (expire != 0 && now < expire) {
+                    add_penalty(o, (uint64_t)q, 1);
+                    out->penalties++;
+                    if (now < expire + (gp->graft_flood_threshold_ns - gp->prune_backoff_ns)) {
+                        add_penalty(o, (uint64_t)q, 1);
+                        out->penalties++;
+                    }
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    resp[(size_t)t * E + q] = 1;
+                    out->graft_rejected++;
+                    continue;
+                }
+                if (score < 0) {
+                    resp[(size_t)t * E + q] = 1;
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    out->graft_rejected++;
+                    continue;
+                }
+                int n = 0;
+                for (int64_t x = o->row_ptr[u]; x < o->row_ptr[u + 1]; x++) n += hb_in_mesh(o, (uint64_t)x, t);
+                if (n >= gp->d_hi && !(ef & GSX_EDGE_OUTBOUND)) {
+                    resp[(size_t)t * E + q] = 1;
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    out->graft_rejected++;
+                    continue;
+                }
+                graft(o, (uint64_t)q, t, now);
+                out->graft_accepted++;
+            }
+            for (uint32_t t = 0; t < T; t++) /* handlePrune */
+                if (ctl[(size_t)t * E + r] == 2) handle_prune(o, gp, (uint64_t)q, t, now, out);
+        }
+    }
+    /* (C) the GRAFT senders handle the PRUNE answers, AcceptFrom-gated */
+    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q);
+    for (uint32_t v = 0; v < o->n_nodes; v++)
+        for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+            const int64_t q = reverse_pair(o, (uint64_t)r);
+            if (q < 0) continue;
+            if (!(o->eflags[r] & GSX_EDGE_DIRECT) && cache[r] < o->th.graylist_threshold) continue;
+            for (uint32_t t = 0; t < T; t++)
+                if (resp[(size_t)t * E + q]) handle_prune(o, gp, (uint64_t)r, t, now, out);
+        }
+    for (uint64_t r = 0; r < E; r++)
+        for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
+    free(cache);
+    free(ctl);
+    free(resp);
+    free(plst);
+    free(tmp);
+    return 0;
+}
+
+int orc_export_backoff(orc_engine* o, int64_t* out) {
+    memcpy(out, o->backoff, sizeof(int64_t) * (size_t)o->T * o->E);
+    return 0;
+}
+
+int orc_import_backoff(orc_engine* o, const int64_t* in) {
+    memcpy(o->backoff, in, sizeof(int64_t) * (size_t)o->T * o->E);
     return 0;
 }
 

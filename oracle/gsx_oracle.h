@@ -52,6 +52,12 @@ int orc_set_thresholds(orc_engine* o, const gsx_thresholds* t);
  * hop/from: optional [m][n_nodes] outputs. */
 int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
                   uint8_t* hop, int32_t* from);
+/* Heartbeat round (gossipsub.go:1303-1604, 718-859) under the contract of gsx.h. */
+int orc_default_gossipsub_params(gsx_gossipsub_params* p);
+int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now_ns, uint64_t seed,
+                  gsx_heartbeat_out* out);
+int orc_export_backoff(orc_engine* o, int64_t* out);
+int orc_import_backoff(orc_engine* o, const int64_t* in);
 int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);
 int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs);
 

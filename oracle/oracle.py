@@ -52,6 +52,11 @@ _SIG = {
     "orc_import_state": (C.c_int, [C.c_void_p, P(abi.StateView)]),
     "orc_export_state": (C.c_int, [C.c_void_p, P(abi.StateView)]),
     "orc_num_pairs": (C.c_uint64, [C.c_void_p]),
+    "orc_default_gossipsub_params": (C.c_int, [P(abi.GossipSubParams)]),
+    "orc_heartbeat": (C.c_int, [C.c_void_p, P(abi.GossipSubParams), C.c_uint64, C.c_int64, C.c_uint64,
+                                P(abi.HeartbeatOut)]),
+    "orc_export_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "orc_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
 }
 
 _lib = None
@@ -86,6 +91,7 @@ class Oracle:
             raise ValueError("orc_create failed")
         self.n_topics = n_topics
         self.n_pairs = 0
+        self.gp = default_gossipsub_params()
 
     def close(self):
         if self.h:
@@ -138,6 +144,23 @@ class Oracle:
             "orc_propagate",
         )
         return out, hop, frm
+
+    def set_gossipsub_params(self, gp):
+        self.gp = gp
+
+    def heartbeat(self, tick, now, seed):
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.orc_heartbeat(self.h, C.byref(self.gp), tick, now, seed, C.byref(out)), "orc_heartbeat")
+        return out
+
+    def export_backoff(self):
+        b = np.empty((self.n_topics, self.n_pairs), dtype=np.int64)
+        self._chk(self.lib.orc_export_backoff(self.h, _p(b, C.c_int64)), "orc_export_backoff")
+        return b
+
+    def import_backoff(self, b):
+        b = np.ascontiguousarray(b, dtype=np.int64).reshape(self.n_topics, self.n_pairs)
+        self._chk(self.lib.orc_import_backoff(self.h, _p(b, C.c_int64)), "orc_import_backoff")
 
     def set_ip_whitelist(self, ips: Iterable[int]):
         a = np.ascontiguousarray(list(ips), dtype=np.uint32)
@@ -215,6 +238,12 @@ class Oracle:
 
 
 # validate / decay twins
+def default_gossipsub_params():
+    gp = abi.GossipSubParams()
+    load().orc_default_gossipsub_params(C.byref(gp))
+    return gp
+
+
 def validate_peer_params(p):
     return load().orc_validate_peer_params(C.byref(p))
 

@@ -270,6 +270,77 @@ __global__ __launch_bounds__(256) void k_v3(double* rec, uint8_t* fl, Pair q, PP
     q.score[p] = tail(q, pp, p, s, bp);
 }
 
+// ---- V4: V3 with non-temporal loads and stores (streamed once per pass) -------
+template <int BS>
+__global__ __launch_bounds__(BS) void k_v4(double* rec, uint8_t* fl, Pair q, PP pp, uint64_t n, int64_t now) {
+    constexpr int TILE = 64;
+    const uint64_t p = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    if (p >= n) return;
+    double s = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        double* base = rec + tix<TILE>(p, t, 0);
+        const double fmd = decay(__builtin_nontemporal_load(base), tp.d2, pp.dtz);
+        const double mmd = decay(__builtin_nontemporal_load(base + TILE), tp.d3, pp.dtz);
+        const double mfp = decay(__builtin_nontemporal_load(base + 2 * TILE), tp.d3b, pp.dtz);
+        const double imd = decay(__builtin_nontemporal_load(base + 3 * TILE), tp.d4, pp.dtz);
+        __builtin_nontemporal_store(fmd, base);
+        __builtin_nontemporal_store(mmd, base + TILE);
+        __builtin_nontemporal_store(mfp, base + 2 * TILE);
+        __builtin_nontemporal_store(imd, base + 3 * TILE);
+        uint8_t* fp = fl + tfx<TILE>(p, t);
+        const uint8_t f0 = *fp;
+        int64_t mt = 0;
+        if (f0 & IN_MESH) mt = now - __builtin_nontemporal_load(((const int64_t*)base) + 4 * TILE);
+        const uint8_t nf = ((f0 & IN_MESH) && mt > tp.act3) ? ((f0 | ACTIVE) & ~FRESH) : (f0 & ~FRESH);
+        if (nf != f0) *fp = nf;
+        s += topic_score(tp, nf, mt, fmd, mmd, mfp, imd);
+    }
+    double bp = decay(q.bp[p], pp.d7, pp.dtz);
+    q.bp[p] = bp;
+    q.score[p] = tail(q, pp, p, s, bp);
+}
+
+// ---- V5: V3 with all loads of a pair issued before any store ------------------
+__global__ __launch_bounds__(256) void k_v5(double* rec, uint8_t* fl, Pair q, PP pp, uint64_t n, int64_t now) {
+    constexpr int TILE = 64;
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    double v[T][4];
+    uint8_t f[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const double* base = rec + tix<TILE>(p, t, 0);
+        v[t][0] = base[0];
+        v[t][1] = base[TILE];
+        v[t][2] = base[2 * TILE];
+        v[t][3] = base[3 * TILE];
+        f[t] = fl[tfx<TILE>(p, t)];
+    }
+    double s = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const TP& tp = c_tp[t];
+        double* base = rec + tix<TILE>(p, t, 0);
+        const double fmd = decay(v[t][0], tp.d2, pp.dtz), mmd = decay(v[t][1], tp.d3, pp.dtz);
+        const double mfp = decay(v[t][2], tp.d3b, pp.dtz), imd = decay(v[t][3], tp.d4, pp.dtz);
+        base[0] = fmd;
+        base[TILE] = mmd;
+        base[2 * TILE] = mfp;
+        base[3 * TILE] = imd;
+        const uint8_t f0 = f[t];
+        int64_t mt = 0;
+        if (f0 & IN_MESH) mt = now - ((const int64_t*)base)[4 * TILE];
+        const uint8_t nf = ((f0 & IN_MESH) && mt > tp.act3) ? ((f0 | ACTIVE) & ~FRESH) : (f0 & ~FRESH);
+        if (nf != f0) fl[tfx<TILE>(p, t)] = nf;
+        s += topic_score(tp, nf, mt, fmd, mmd, mfp, imd);
+    }
+    double bp = decay(q.bp[p], pp.d7, pp.dtz);
+    q.bp[p] = bp;
+    q.score[p] = tail(q, pp, p, s, bp);
+}
+
 // ---- copy ceiling: read 5+1 and write 4+1 double2 streams ---------------------
 __global__ __launch_bounds__(256) void k_copy(const double2* __restrict__ src, double2* __restrict__ dst,
                                               uint64_t n_rd, uint64_t n_wr) {
@@ -382,7 +453,12 @@ int main(int argc, char** argv) {
         timeit("V1", bytes_min, [&] { k_v1<<<(unsigned)((n / 2 + 255) / 256), 256>>>(a, q, pp, n, now); });
         timeit("V2", bytes_min, [&] { k_v2<<<(unsigned)((n / 2 + 255) / 256), 256>>>(rec, tfl, q, pp, n, now); });
         timeit("V3", bytes_min, [&] { k_v3<<<gN, 256>>>(rec, tfl, q, pp, n, now); });
+        timeit("V4nt", bytes_min, [&] { k_v4<256><<<gN, 256>>>(rec, tfl, q, pp, n, now); });
+        timeit("V4b5", bytes_min, [&] { k_v4<512><<<(unsigned)((n + 511) / 512), 512>>>(rec, tfl, q, pp, n, now); });
+        timeit("V5", bytes_min, [&] { k_v5<<<gN, 256>>>(rec, tfl, q, pp, n, now); });
         timeit("C0", (rd16 + wr16) * 16.0, [&] { k_copy<<<256 * 16, 256>>>(csrc, cdst, rd16, wr16); });
+        // plain 1:1 copy of wr16 x 16 B (both buffers hold at least that much)
+        timeit("C1", (wr16 + wr16) * 16.0, [&] { k_copy<<<256 * 16, 256>>>(csrc, cdst, wr16, wr16); });
     }
     CHECK(hipGetLastError());
     return 0;
