@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--prop-msgs", type=int, default=256, help="messages per propagation batch (0: skip)")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
+    ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -215,6 +216,44 @@ def main():
             "router": "gossipsub (synthesized mesh, ~6 of ~12 peers per topic), P2/P3 credits on",
         }
 
+    # ---- heartbeat rounds (A10): every (node, topic) mesh maintained at once ----
+    hb = None
+    if args.hb_steps > 0:
+        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                        accept_px_threshold=0, opportunistic_graft_threshold=5))
+        tick = 58  # the timed rounds include the OpportunisticGraftTicks round 60
+        now += abi.SECOND
+        e.heartbeat(tick, now, seed)  # warm-up
+        e.sync()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        outs = []
+        for _ in range(args.hb_steps):
+            tick += 1
+            now += abi.SECOND
+            outs.append(e.heartbeat(tick, now, seed).as_dict())
+        e.sync()
+        torch.cuda.synchronize(dev)
+        ht = time.perf_counter() - t0
+        barrier()
+        units = float(n) * T * args.hb_steps
+        if dist is not None:
+            t = torch.tensor([ht], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ht = float(t.item())
+            r = torch.tensor([units], dtype=torch.float64, device=dev)
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            units = float(r.item())
+        hb = {
+            "metric": "heartbeat (node, topic) mesh units/s",
+            "value": units / ht,
+            "ms_per_round": ht / args.hb_steps * 1e3,
+            "rounds": args.hb_steps,
+            "first_round": outs[0],
+            "last_round": outs[-1],
+        }
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -290,6 +329,7 @@ def main():
         "cpu_baseline": cpu,
         "parity_vs_oracle": parity,
         "propagation": prop,
+        "heartbeat": hb,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

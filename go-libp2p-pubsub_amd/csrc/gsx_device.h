@@ -169,6 +169,8 @@ enum {
     HB_PENALTIES,
     HB_BACKOFF_CLEARED,
     HB_MESH_LINKS,
+    HB_IHAVE_MSGS,
+    HB_IHAVE_IDS,
     HB_STAT_WORDS
 };  // the order of gsx_heartbeat_out
 
@@ -176,6 +178,16 @@ struct DevGossipParams {
     int32_t d, d_lo, d_hi, d_score, d_out, og_peers;
     uint64_t og_ticks;
     int64_t prune_backoff_ns, graft_flood_threshold_ns;
+    int32_t d_lazy, max_ihave;
+    double gossip_factor;
+};
+
+// One cached gossipsub batch (a gsx_propagate call) of an mcache window:
+// node v has message k iff bit k % 64 of seen[(k / 64) * n_nodes + v].
+struct GossipBatch {
+    const uint64_t* seen;
+    uint32_t n_words;
+    uint32_t slot_base;  // slot of message 0 in HbState::mc_ids
 };
 
 struct HbState {
@@ -186,6 +198,12 @@ struct HbState {
     uint8_t* ctl;      // [topic][pair (v -> u)] HB_GRAFT / HB_PRUNE sent by v this round
     uint8_t* resp;     // [topic][pair (u -> v)] PRUNE answer u sends to a GRAFT of v
     unsigned long long* stats;
+    uint32_t* rngk;         // per node: draw counter after the maintenance of the current topic
+    uint32_t* ihave_len;    // [topic][pair] ids advertised (0 = no IHAVE)
+    uint64_t* ihave_hash;   // [topic][pair] digest of the IHAVE id list
+    const uint64_t* mc_ids; // message id per cache slot
+    DevPeerParams pp;       // live scores of emitGossip
+    double gossip_threshold;
     uint64_t n_pairs;
     uint32_t n_nodes;
     uint64_t tick;
@@ -196,7 +214,10 @@ struct HbState {
 };
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st);
-hipError_t launch_hb_mesh(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipStream_t st);
+hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
+                            uint32_t max_ids, hipStream_t st);
+constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st);

@@ -100,6 +100,22 @@ struct gsx_engine {
     int64_t* d_backoff = nullptr;
     uint8_t *d_hbctl = nullptr, *d_hbresp = nullptr;
     unsigned long long* d_hbstats = nullptr;
+    uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
+    uint64_t* d_ihave_hash = nullptr;
+    bool have_gossip = false;
+
+    // mcache (mcache.go): windows of cached gossipsub batches, front = history[0]
+    struct McBatch {
+        uint32_t topic = 0, n_msgs = 0, n_words = 0;
+        uint64_t* d_seen = nullptr;  // [word][node]
+        std::vector<uint64_t> ids;
+    };
+    std::deque<std::vector<McBatch>> mc;
+    std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
+    std::vector<uint64_t> mc_ids_host;
+    gsx::GossipBatch* d_gb = nullptr;
+    uint64_t* d_mc_ids = nullptr;
+    size_t gb_cap = 0, ids_cap = 0;
 
     // propagation buffers (grown on demand) and the last call's shape
     struct {
@@ -222,6 +238,14 @@ int upload_topic_params(gsx_engine* e) {
     return GSX_OK;
 }
 
+void mcache_clear(gsx_engine* e) {
+    for (auto& w : e->mc)
+        for (auto& b : w)
+            if (b.d_seen) (void)hipFree(b.d_seen);
+    e->mc.clear();
+    e->mc.emplace_back();  // history[0], empty
+}
+
 void free_state(gsx_engine* e) {
     void* ptrs[] = {e->d_rec,    e->d_rflags, e->d_tmp, e->d_nbad,    e->d_pflags, e->d_eflags,
                     e->d_expire, e->d_bp,     e->d_app, e->d_score,   e->d_ipg,    e->d_ipcount,
@@ -245,12 +269,20 @@ void free_state(gsx_engine* e) {
         if (p) (void)hipFree(p);
     e->prop = {};
     e->d_col = nullptr;
-    void* hb[] = {e->d_backoff, e->d_hbctl, e->d_hbresp, e->d_hbstats};
+    void* hb[] = {e->d_backoff, e->d_hbctl, e->d_hbresp, e->d_hbstats, e->d_rngk,
+                  e->d_ihave_len, e->d_ihave_hash, e->d_gb, e->d_mc_ids};
     for (void* p : hb)
         if (p) (void)hipFree(p);
     e->d_backoff = nullptr;
     e->d_hbctl = e->d_hbresp = nullptr;
     e->d_hbstats = nullptr;
+    e->d_rngk = e->d_ihave_len = nullptr;
+    e->d_ihave_hash = nullptr;
+    e->d_gb = nullptr;
+    e->d_mc_ids = nullptr;
+    e->gb_cap = e->ids_cap = 0;
+    e->have_gossip = false;
+    mcache_clear(e);
 }
 
 template <class T>
@@ -1126,6 +1158,18 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
         HIPCHK(e, gsx::launch_prop_credit(ps, ds, e->stream));
         e->scores_valid = false;
     }
+    if (cfg->router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
+        gsx_engine::McBatch b;
+        b.topic = cfg->topic;
+        b.n_msgs = (uint32_t)m;
+        b.n_words = W;
+        if (int rc = dalloc(e, &b.d_seen, (size_t)W * N)) return rc;
+        HIPCHK(e, hipMemcpyAsync(b.d_seen, P.seen, 8 * (size_t)W * N, hipMemcpyDeviceToDevice, e->stream));
+        b.ids.resize(m);
+        for (size_t k = 0; k < m; ++k) b.ids[k] = msgs[k].msg_id;
+        if (e->mc.empty()) e->mc.emplace_back();
+        e->mc.front().push_back(std::move(b));
+    }
     unsigned long long st[gsx::STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, P.stats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1187,6 +1231,11 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
     if (p->d_lo < 0 || p->d < p->d_lo || p->d_hi < p->d || p->d_score < 0 || p->d_score > p->d_hi || p->d_out < 0 ||
         p->opportunistic_graft_peers < 0 || p->prune_backoff_ns < 0)
         return fail(e, GSX_EINVAL, "need 0 <= Dlo <= D <= Dhi, 0 <= Dscore <= Dhi, Dout, OG peers, backoff >= 0");
+    // NewMessageCache panics on gossip > history (mcache.go:24-28)
+    if (p->history_length < 1 || p->history_gossip < 0 || p->history_gossip > p->history_length ||
+        p->d_lazy < 0 || p->max_ihave_length < 0 || !(p->gossip_factor >= 0))
+        return fail(e, GSX_EINVAL, "need 0 <= HistoryGossip <= HistoryLength, HistoryLength >= 1, Dlazy, "
+                                   "MaxIHaveLength, GossipFactor >= 0");
     e->gp = *p;
     return GSX_OK;
 }
@@ -1201,8 +1250,11 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     if (!e->d_hbstats) {
         int rc = 0;
         if ((rc = dalloc(e, &e->d_hbctl, TE)) || (rc = dalloc(e, &e->d_hbresp, TE)) ||
-            (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
+            (rc = dalloc(e, &e->d_rngk, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
+            (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
             return rc;
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
     }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
@@ -1221,16 +1273,78 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     h.seed = seed;
     h.og_threshold = e->th.opportunistic_graft_threshold;
     h.graylist = e->th.graylist_threshold;
-    h.gp = gsx::DevGossipParams{e->gp.d,       e->gp.d_lo,  e->gp.d_hi,
-                                e->gp.d_score, e->gp.d_out, e->gp.opportunistic_graft_peers,
-                                e->gp.opportunistic_graft_ticks, e->gp.prune_backoff_ns,
-                                e->gp.graft_flood_threshold_ns};
+    h.gossip_threshold = e->th.gossip_threshold;
+    h.rngk = e->d_rngk;
+    h.ihave_len = e->d_ihave_len;
+    h.ihave_hash = e->d_ihave_hash;
+    h.pp = dev_peer_params(e);
+    h.gp = gsx::DevGossipParams{e->gp.d,
+                                e->gp.d_lo,
+                                e->gp.d_hi,
+                                e->gp.d_score,
+                                e->gp.d_out,
+                                e->gp.opportunistic_graft_peers,
+                                e->gp.opportunistic_graft_ticks,
+                                e->gp.prune_backoff_ns,
+                                e->gp.graft_flood_threshold_ns,
+                                e->gp.d_lazy,
+                                e->gp.max_ihave_length,
+                                e->gp.gossip_factor};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_hbctl, 0, TE ? TE : 1, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_hbresp, 0, TE ? TE : 1, e->stream));
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
-    HIPCHK(e, gsx::launch_hb_mesh(ds, h, e->stream));
+    // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order
+    e->gb_host.clear();
+    e->mc_ids_host.clear();
+    std::vector<uint32_t> gb_off(e->T + 1, 0), max_ids(e->T, 0);
+    const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
+    for (uint32_t t = 0; t < e->T; ++t) {
+        gb_off[t] = (uint32_t)e->gb_host.size();
+        for (size_t w = 0; w < n_win; ++w)
+            for (const auto& b : e->mc[w]) {
+                if (b.topic != t) continue;
+                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_ids_host.size()});
+                e->mc_ids_host.insert(e->mc_ids_host.end(), b.ids.begin(), b.ids.end());
+                max_ids[t] += b.n_msgs;
+            }
+        if (max_ids[t] > gsx::HB_GOSSIP_MAX_IDS)
+            return fail(e, GSX_ERANGE, "gossip window of topic " + std::to_string(t) + " holds " +
+                                           std::to_string(max_ids[t]) + " messages, more than " +
+                                           std::to_string(gsx::HB_GOSSIP_MAX_IDS) + " (shift the cache more often)");
+    }
+    gb_off[e->T] = (uint32_t)e->gb_host.size();
+    if (e->gb_host.size() > e->gb_cap) {
+        if (e->d_gb) (void)hipFree(e->d_gb);
+        e->d_gb = nullptr;
+        e->gb_cap = std::max<size_t>(e->gb_host.size(), 2 * e->gb_cap);
+        if (int rc = dalloc(e, &e->d_gb, e->gb_cap)) return rc;
+    }
+    if (e->mc_ids_host.size() > e->ids_cap) {
+        if (e->d_mc_ids) (void)hipFree(e->d_mc_ids);
+        e->d_mc_ids = nullptr;
+        e->ids_cap = std::max<size_t>(e->mc_ids_host.size(), 2 * e->ids_cap);
+        if (int rc = dalloc(e, &e->d_mc_ids, e->ids_cap)) return rc;
+    }
+    if (!e->gb_host.empty()) {
+        HIPCHK(e, hipMemcpyAsync(e->d_gb, e->gb_host.data(), sizeof(gsx::GossipBatch) * e->gb_host.size(),
+                                 hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_mc_ids, e->mc_ids_host.data(), 8 * e->mc_ids_host.size(),
+                                 hipMemcpyHostToDevice, e->stream));
+    }
+    h.mc_ids = e->d_mc_ids;
+    if (e->have_gossip || !e->gb_host.empty()) {
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+    }
+    e->have_gossip = !e->gb_host.empty();
+    // (A) per topic, ascending: maintenance, then emitGossip
+    for (uint32_t t = 0; t < e->T; ++t) {
+        HIPCHK(e, gsx::launch_hb_mesh(ds, h, t, e->stream));
+        HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
+                                        e->stream));
+    }
     // the receivers score the senders as the round left them
     HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
@@ -1243,6 +1357,62 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     HIPCHK(e, hipStreamSynchronize(e->stream));
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
+    // mcache.Shift (mcache.go:94-104, gossipsub.go:1563), after the stream drained
+    const size_t hist = (size_t)std::max(e->gp.history_length, 1);
+    while (e->mc.size() >= hist) {
+        for (auto& b : e->mc.back())
+            if (b.d_seen) (void)hipFree(b.d_seen);
+        e->mc.pop_back();
+    }
+    e->mc.emplace_front();
+    return GSX_OK;
+}
+
+int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    const size_t TE = (size_t)e->T * e->E;
+    if (!e->d_ihave_len) {  // no heartbeat yet: nothing was sent
+        if (ihave_len) std::memset(ihave_len, 0, 4 * TE);
+        if (ihave_digest) std::memset(ihave_digest, 0, 8 * TE);
+        return GSX_OK;
+    }
+    if (ihave_len && TE) HIPCHK(e, hipMemcpyAsync(ihave_len, e->d_ihave_len, 4 * TE, hipMemcpyDeviceToHost, e->stream));
+    if (ihave_digest && TE)
+        HIPCHK(e, hipMemcpyAsync(ihave_digest, e->d_ihave_hash, 8 * TE, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
+                   size_t* n_out) {
+    if (!e || !n_out || (cap && !out)) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (node >= e->n_nodes) return fail(e, GSX_ERANGE, "node out of range");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    size_t n = 0;
+    const size_t nw = std::min<size_t>(n_windows, e->mc.size());
+    std::vector<uint64_t> words;
+    for (size_t w = 0; w < nw; ++w)
+        for (const auto& b : e->mc[w]) {
+            if (topic != GSX_ANY_TOPIC && b.topic != topic) continue;
+            words.resize(b.n_words);
+            for (uint32_t k = 0; k < b.n_words; ++k)  // column `node` of the [word][node] bitset
+                HIPCHK(e, hipMemcpy(&words[k], b.d_seen + (size_t)k * e->n_nodes + node, 8, hipMemcpyDeviceToHost));
+            for (uint32_t k = 0; k < b.n_msgs; ++k)
+                if (words[k / 64] >> (k % 64) & 1) {
+                    if (n < cap) out[n] = b.ids[k];
+                    ++n;
+                }
+        }
+    *n_out = n;
+    return GSX_OK;
+}
+
+int gsx_mcache_clear(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    mcache_clear(e);
     return GSX_OK;
 }
 

@@ -1,11 +1,12 @@
 // gsx_heartbeat.hip — the GossipSub heartbeat's mesh maintenance as one
 // synchronous round over the whole overlay (gsx.h, gsx_heartbeat).
 //
-//  (A) k_hb_mesh: one lane per (node v, topic t).  Everything the unit touches
+//  (A) per topic t ascending: k_hb_mesh, one lane per node v, the mesh
+//      maintenance of (v, t) (gossipsub.go:1344-1510); everything it touches
 //      — the records, backoff entries and control bytes of v's own pairs for
-//      topic t — belongs to it alone, so the units run without atomics except
-//      for the round counters.  Candidate and mesh lists are at most
-//      HB_MAX_DEG pair offsets (u16) in scratch.  gossipsub.go:1344-1510.
+//      topic t — belongs to it alone, so lanes need no atomics except for the
+//      round counters (candidate and mesh lists: <= HB_MAX_DEG u16 offsets in
+//      scratch); then k_hb_gossip, one wave per node, its IHAVE emission.
 //  (B) k_hb_recv: one lane per receiving node u, walking its senders in
 //      ascending order (the Dhi check reads the mesh size the previous
 //      accepts left).  handleGraft / handlePrune, gossipsub.go:718-843.
@@ -126,10 +127,10 @@ struct HbUnit {
     }
 };
 
-__global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h) {
-    const uint64_t u = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-    if (u >= (uint64_t)h.n_nodes * s.n_topics) return;
-    const uint32_t v = (uint32_t)(u / s.n_topics), t = (uint32_t)(u % s.n_topics);
+// One launch per topic, ascending: the maintenance of (v, t) for every v.
+__global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
+    const uint32_t v = blockIdx.x * 64u + threadIdx.x;
+    if (v >= h.n_nodes) return;
     const int64_t r0 = h.row_ptr[v];
     const HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
     const DevGossipParams& gp = h.gp;
@@ -193,6 +194,148 @@ __global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h) {
             const int k = U.get_peers(gp.og_peers, false, 1, median, tmp, g);
             for (int i = 0; i < k; ++i) U.graft(tmp[i]);
         }
+    }
+    h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
+}
+
+// ---- emitGossip (gossipsub.go:1669-1723) --------------------------------------
+// One wave per node for topic t, after the maintenance of topic t (so the
+// live scores see topics <= t maintained, > t not yet: the reference's
+// sequential order).  The node's GetGossipIDs list (mcache.go:82-92) is built
+// in LDS from the cached batches' seen words; the shuffles draw 64 Int31s at
+// once (one per lane, Go's rejection rule resolved by a ballot) and lane 0
+// applies the swaps in order.
+
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  // exclusive
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    return incl - x;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+// shuffleStrings (gossipsub.go:1897-1902) of a[0..L) in LDS; g is wave-uniform.
+__device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uint32_t lane) {
+    uint32_t i = 0;
+    while (i < L) {
+        const uint32_t step = i + lane;
+        const bool valid = step < L;
+        const uint32_t n = step + 1;
+        const int32_t x = (int32_t)(h4(g.seed, g.tag, g.vertex, g.base | (g.k + lane)) >> 33);
+        const bool pow2 = (n & (n - 1)) == 0;
+        const int32_t maxv = pow2 ? 0 : (int32_t)((1u << 31) - 1 - (1u << 31) % n);
+        const bool rej = valid && !pow2 && x > maxv;
+        const uint64_t rb = __ballot(rej);
+        const uint32_t l0 = rb ? (uint32_t)__builtin_ctzll(rb) : 64u;
+        const uint32_t nvalid = l0 < L - i ? l0 : L - i;
+        if (lane < nvalid) jbuf[lane] = pow2 ? (x & (int32_t)(n - 1)) : (x % (int32_t)n);
+        __syncthreads();
+        if (lane == 0)
+            for (uint32_t k = 0; k < nvalid; ++k) {
+                const uint32_t j = (uint32_t)jbuf[k];
+                const uint32_t tmp = a[i + k];
+                a[i + k] = a[j];
+                a[j] = tmp;
+            }
+        __syncthreads();
+        if (l0 < 64) {  // step i + l0 redraws after its rejected draw
+            i += l0;
+            g.k += l0 + 1;
+        } else {
+            i += nvalid;
+            g.k += nvalid;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
+                                                  uint32_t n_gb) {
+    extern __shared__ uint32_t mids[];  // message slots, GetGossipIDs order
+    __shared__ uint16_t peers[HB_MAX_DEG];
+    __shared__ int32_t jbuf[64];
+    __shared__ uint32_t kshare;
+    const uint32_t v = blockIdx.x, lane = threadIdx.x;
+    // GetGossipIDs: windows newest first, batches in Put order, ids ascending
+    uint32_t L = 0;
+    for (uint32_t b = 0; b < n_gb; ++b) {
+        const GossipBatch B = gb[b];
+        for (uint32_t w0 = 0; w0 < B.n_words; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            uint64_t word = w < B.n_words ? B.seen[(size_t)w * h.n_nodes + v] : 0;
+            const uint32_t c = (uint32_t)__popcll(word);
+            uint32_t pos = L + wave_prefix(c, lane);
+            while (word) {
+                mids[pos++] = B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word);
+                word &= word - 1;
+            }
+            L += __shfl(pos, 63, 64) - L;  // lane 63's end = the new total
+        }
+    }
+    __syncthreads();
+    if (L == 0) return;
+    Rng g{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), h.rngk[v]};
+    wave_shuffle(mids, L, g, jbuf, lane);
+    // eligible targets, ascending: topic peers with the mesh feature, not in
+    // the mesh, not direct, live score >= GossipThreshold
+    const int64_t r0 = h.row_ptr[v];
+    const int deg = (int)(h.row_ptr[v + 1] - r0);
+    int np = 0;
+    for (int c0 = 0; c0 < deg; c0 += 64) {
+        const int i = c0 + (int)lane;
+        bool ok = false;
+        if (i < deg) {
+            const uint64_t r = r0 + i;
+            const uint8_t f = h.eflags[r];
+            ok = (s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+                 (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && !hb_in_mesh(s, r, t) &&
+                 eval_pair(s, h.pp, r) >= h.gossip_threshold;
+        }
+        const uint64_t bal = __ballot(ok);
+        if (ok) peers[np + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)i;
+        np += __popcll(bal);
+    }
+    __syncthreads();
+    int target = h.gp.d_lazy;
+    const int factor = (int)(h.gp.gossip_factor * (double)np);
+    if (factor > target) target = factor;
+    if (target > np) {
+        target = np;
+    } else {
+        if (lane == 0) {
+            g.shuffle(peers, np);
+            kshare = g.k;
+        }
+        __syncthreads();
+        g.k = kshare;
+    }
+    uint64_t n_ids = 0;
+    for (int p = 0; p < target; ++p) {
+        uint32_t len = L;
+        if (L > (uint32_t)h.gp.max_ihave) {
+            wave_shuffle(mids, L, g, jbuf, lane);
+            len = (uint32_t)h.gp.max_ihave;
+        }
+        uint64_t d = 0;
+        for (uint32_t e = lane; e < len; e += 64) d += smix(h.mc_ids[mids[e]] + 0x9E3779B97F4A7C15ull * (e + 1));
+        d = wave_sum64(d);
+        if (lane == 0) {
+            const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
+            h.ihave_len[x] = len;
+            h.ihave_hash[x] = d;
+        }
+        n_ids += len;
+    }
+    if (lane == 0 && target > 0) {
+        count(h.stats, HB_IHAVE_MSGS, (unsigned long long)target);
+        count(h.stats, HB_IHAVE_IDS, n_ids);
     }
 }
 
@@ -290,10 +433,16 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_hb_mesh(const DevState& s, const HbState& h, hipStream_t st) {
-    const uint64_t n = (uint64_t)h.n_nodes * s.n_topics;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh, dim3(blocks_for(n, 64)), dim3(64), 0, st, s, h);
+hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipStream_t st) {
+    if (h.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_mesh, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
+                            uint32_t max_ids, hipStream_t st) {
+    if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_gossip, dim3(h.n_nodes), dim3(64), sizeof(uint32_t) * max_ids, st, s, h, t, gb, n_gb);
     return hipGetLastError();
 }
 

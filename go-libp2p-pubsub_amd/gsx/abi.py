@@ -202,6 +202,7 @@ GSX_ROUTER_FLOODSUB = 0
 GSX_ROUTER_GOSSIPSUB = 1
 GSX_ROUTER_RANDOMSUB = 2
 GSX_MAX_HOPS = 64
+GSX_ANY_TOPIC = 0xFFFFFFFF
 
 
 class PropConfig(C.Structure):
@@ -279,6 +280,8 @@ class HeartbeatOut(C.Structure):
         ("penalties", C.c_uint64),
         ("backoff_cleared", C.c_uint64),
         ("mesh_links", C.c_uint64),
+        ("ihave_msgs", C.c_uint64),
+        ("ihave_ids", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -333,6 +336,10 @@ SIGNATURES = {
     "gsx_heartbeat": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64, P(HeartbeatOut)]),
     "gsx_export_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "gsx_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
+    "gsx_mcache_clear": (C.c_int, [C.c_void_p]),
+    "gsx_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
+                                 P(C.c_size_t)]),
     "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_timing_end": (
         C.c_int,

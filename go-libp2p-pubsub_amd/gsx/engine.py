@@ -194,6 +194,26 @@ class Engine:
         b = np.ascontiguousarray(b, dtype=np.int64).reshape(self.n_topics, self.n_pairs)
         self._chk(self.lib.gsx_import_backoff(self.h, _ptr(b, C.c_int64)), "gsx_import_backoff")
 
+    def gossip_results(self):
+        """-> (ihave_len [T, E] u32, ihave_digest [T, E] u64) of the last heartbeat."""
+        ln = np.empty((self.n_topics, self.n_pairs), dtype=np.uint32)
+        dg = np.empty((self.n_topics, self.n_pairs), dtype=np.uint64)
+        self._chk(self.lib.gsx_gossip_results(self.h, _ptr(ln, C.c_uint32), _ptr(dg, C.c_uint64)),
+                  "gsx_gossip_results")
+        return ln, dg
+
+    def mcache_clear(self):
+        self._chk(self.lib.gsx_mcache_clear(self.h), "gsx_mcache_clear")
+
+    def mcache_ids(self, node: int, topic: int, n_windows: int) -> np.ndarray:
+        """mcache.GetGossipIDs of `node` over its first n_windows windows."""
+        n = C.c_size_t()
+        self._chk(self.lib.gsx_mcache_ids(self.h, node, topic, n_windows, None, 0, C.byref(n)), "gsx_mcache_ids")
+        out = np.empty(n.value, dtype=np.uint64)
+        self._chk(self.lib.gsx_mcache_ids(self.h, node, topic, n_windows, _ptr(out, C.c_uint64), len(out),
+                                          C.byref(n)), "gsx_mcache_ids")
+        return out
+
     def timing_begin(self, max_launches: int):
         self._chk(self.lib.gsx_timing_begin(self.h, max_launches), "gsx_timing_begin")
 

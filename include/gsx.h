@@ -421,7 +421,18 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  * ascending peer order; the unstable sort.Slice of :1393 is a stable sort
  * after the shuffle.  clearBackoff runs when tick % 15 == 0 (:1585-1604).
  * All nodes are subscribed to (joined) every topic; "in topic" = present and
- * connected; mesh membership is the scorer's inMesh flag.  */
+ * connected; mesh membership is the scorer's inMesh flag.
+ * After the maintenance of (node, topic) the node emits IHAVE gossip for that
+ * topic (emitGossip, :1669-1723) from its message cache (mcache.go): the ids
+ * of the gossipsub batches it saw (gsx_propagate with the gossipsub router
+ * Puts every message a node receives or publishes into its cache window 0;
+ * within a batch the insertion order is ascending message index), read
+ * newest window first over HistoryGossip windows, shuffled with the same
+ * draw stream; targets are the non-mesh, non-direct mesh-capable topic peers
+ * whose live score (after the node's maintenance of topics <= t) is >=
+ * GossipThreshold, max(Dlazy, GossipFactor * |eligible|) of them, shuffled;
+ * lists longer than MaxIHaveLength are reshuffled per target and truncated.
+ * Every heartbeat ends with mcache.Shift() (:1563).  */
 typedef struct gsx_heartbeat_out {
     uint64_t grafts;          /* peers grafted by the heartbeats (A)              */
     uint64_t prunes;          /* peers pruned by the heartbeats (A)               */
@@ -431,6 +442,8 @@ typedef struct gsx_heartbeat_out {
     uint64_t penalties;       /* AddPenalty(p, 1) calls (B)                        */
     uint64_t backoff_cleared; /* entries dropped by clearBackoff                   */
     uint64_t mesh_links;      /* in-mesh (pair, topic) after the round             */
+    uint64_t ihave_msgs;      /* IHAVE control messages emitted (emitGossip)       */
+    uint64_t ihave_ids;       /* message ids advertised over all of them           */
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
@@ -438,6 +451,20 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, g
  * (gs.backoff, gossipsub.go:436; zeroed by gsx_load_overlay) */
 int gsx_export_backoff(gsx_engine* e, int64_t* out);
 int gsx_import_backoff(gsx_engine* e, const int64_t* in);
+/* The IHAVEs of the last gsx_heartbeat, per [topic][pair (sender -> target)]:
+ * number of ids (0 = none sent) and an order-sensitive digest of the id list,
+ * sum over positions i of mix64(id_i + 0x9E3779B97F4A7C15 * (i + 1)) (mod 2^64,
+ * mix64 = SplitMix64's finaliser).  Either pointer may be NULL. */
+int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest);
+/* Drop every cached message window (mcache.go, a fresh cache). */
+int gsx_mcache_clear(gsx_engine* e);
+/* mcache.GetGossipIDs of one node (mcache.go:82-92) over its first n_windows
+ * windows (HistoryGossip for the gossip view, HistoryLength for every id the
+ * cache still holds, i.e. mcache.Get); topic GSX_ANY_TOPIC matches all.
+ * Writes up to cap ids, *n_out = the full count. */
+#define GSX_ANY_TOPIC 0xFFFFFFFFu
+int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
+                   size_t* n_out);
 
 /* Per-launch timing of the fused refresh+score kernel over a region: after
  * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls

@@ -64,6 +64,17 @@ typedef struct {
 struct orc_engine;
 static int ipcount_init(struct orc_engine* o);
 
+typedef struct {
+    uint32_t topic, m, n;
+    uint64_t* ids;
+    uint8_t* has;
+} orc_mc_batch;
+typedef struct orc_mc_window {
+    orc_mc_batch* b;
+    size_t nb, cap;
+} orc_mc_window;
+#define ORC_MC_MAX 64
+
 struct orc_engine {
     uint32_t T;
     ipcount_map ipc;
@@ -71,6 +82,12 @@ struct orc_engine {
     gsx_thresholds th;
     uint8_t* eflags; /* GSX_EDGE_* per pair */
     int64_t* backoff; /* gs.backoff[topic][peer] per [t][pair], 0 = no entry (gossipsub.go:436) */
+    /* mcache (mcache.go): window w holds the gossipsub batches Put while it was
+     * window 0; node v has message k of a batch iff has[k * n + v] */
+    struct orc_mc_window* mc;
+    uint32_t mc_n; /* windows alive (history[0..mc_n-1]) */
+    uint32_t* ihave_len;   /* [t][pair] of the last heartbeat */
+    uint64_t* ihave_hash;
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -225,6 +242,19 @@ static void free_records(orc_engine* o) {
     o->n_alive = 0;
 }
 
+int orc_mcache_clear(orc_engine* o) {
+    for (uint32_t w = 0; w < o->mc_n; w++) {
+        for (size_t i = 0; i < o->mc[w].nb; i++) {
+            free(o->mc[w].b[i].ids);
+            free(o->mc[w].b[i].has);
+        }
+        free(o->mc[w].b);
+        memset(&o->mc[w], 0, sizeof(orc_mc_window));
+    }
+    o->mc_n = o->mc ? 1 : 0; /* history[0] exists, empty */
+    return 0;
+}
+
 void orc_destroy(orc_engine* o) {
     if (!o) return;
     free(o->row_ptr);
@@ -237,6 +267,10 @@ void orc_destroy(orc_engine* o) {
     free(o->whitelist);
     free(o->eflags);
     free(o->backoff);
+    orc_mcache_clear(o);
+    free(o->mc);
+    free(o->ihave_len);
+    free(o->ihave_hash);
     free(o->ipc.keys);
     free(o->ipc.vals);
     free_records(o);
@@ -282,6 +316,14 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     free(o->backoff);
     o->backoff = (int64_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(int64_t));
     if (!o->backoff) return GSX_ENOMEM;
+    free(o->ihave_len);
+    free(o->ihave_hash);
+    o->ihave_len = (uint32_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint32_t));
+    o->ihave_hash = (uint64_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint64_t));
+    if (!o->ihave_len || !o->ihave_hash) return GSX_ENOMEM;
+    if (!o->mc) o->mc = (orc_mc_window*)calloc(ORC_MC_MAX, sizeof(orc_mc_window));
+    if (!o->mc) return GSX_ENOMEM;
+    orc_mcache_clear(o);
     if (edge_flags && E) memcpy(o->eflags, edge_flags, E);
     free(o->row_ptr);
     free(o->col);
@@ -1020,6 +1062,23 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     size_t cap_arr = 1024, n_arr = 0;
     orc_arrival* arr = (orc_arrival*)malloc(sizeof(orc_arrival) * cap_arr);
     const bool credit = cfg->credit_scores && cfg->topic < o->T && o->scored[cfg->topic];
+    /* gossipsub's Publish Puts every message a node processes into its
+     * mcache (gossipsub.go:944); one batch entry in window 0 */
+    orc_mc_batch* mcb = NULL;
+    if (cfg->router == GSX_ROUTER_GOSSIPSUB && m > 0 && o->mc) {
+        orc_mc_window* w0 = &o->mc[0];
+        if (w0->nb == w0->cap) {
+            w0->cap = w0->cap ? 2 * w0->cap : 4;
+            w0->b = (orc_mc_batch*)realloc(w0->b, sizeof(orc_mc_batch) * w0->cap);
+        }
+        mcb = &w0->b[w0->nb++];
+        mcb->topic = cfg->topic;
+        mcb->m = (uint32_t)m;
+        mcb->n = N;
+        mcb->ids = (uint64_t*)malloc(sizeof(uint64_t) * m);
+        mcb->has = (uint8_t*)malloc(m * (size_t)(N ? N : 1));
+        for (size_t k = 0; k < m; k++) mcb->ids[k] = msgs[k].msg_id;
+    }
     for (size_t k = 0; k < m; k++) {
         const uint32_t src = msgs[k].source;
         if (src >= N) return GSX_ERANGE;
@@ -1071,6 +1130,8 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         }
         if (hop_out) memcpy(hop_out + k * (size_t)N, hop, N);
         if (from_out) memcpy(from_out + k * (size_t)N, from, sizeof(int32_t) * N);
+        if (mcb)
+            for (uint32_t i = 0; i < N; i++) mcb->has[k * (size_t)N + i] = hop[i] != 0xFF;
     }
     free(hop);
     free(from);
@@ -1187,10 +1248,10 @@ static void sort_by_score(const double* cache, uint64_t* a, int n, int desc) {
 }
 
 /* the mesh maintenance of one (node, topic), gossipsub.go:1344-1510 */
-static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, uint64_t seed, uint64_t* plst, uint64_t* tmp) {
+static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* gr, uint64_t* plst, uint64_t* tmp) {
     orc_engine* o = c->o;
     const gsx_gossipsub_params* gp = c->gp;
-    orc_rng g = {seed, 8, v, (c->tick << 32) | ((uint64_t)t << 24), 0};
+#define g (*gr)
     /* drop all peers with negative score, without PX (:1361-1368) */
     int n = mesh_list(o, v, t, plst);
     for (int i = 0; i < n; i++)
@@ -1260,6 +1321,92 @@ static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, uint64_t seed, uint64_t* 
             for (int i = 0; i < k; i++) hb_graft(c, tmp[i], t);
         }
     }
+#undef g
+}
+
+static void shuffle_ids(uint64_t* a, size_t n, orc_rng* g) { /* shuffleStrings, gossipsub.go:1897-1902 */
+    for (size_t i = 0; i < n; i++) {
+        size_t j = (size_t)rng_int31n(g, (int32_t)(i + 1));
+        uint64_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+}
+
+static uint64_t ihave_digest(const uint64_t* ids, size_t n) {
+    uint64_t d = 0;
+    for (size_t i = 0; i < n; i++) d += splitmix(ids[i] + 0x9E3779B97F4A7C15ULL * (uint64_t)(i + 1));
+    return d;
+}
+
+/* emitGossip (gossipsub.go:1669-1723) for (v, t) after its maintenance, with
+ * mcache.GetGossipIDs (mcache.go:82-92) over the first HistoryGossip windows */
+static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t* peers, uint64_t** mids,
+                        size_t* mids_cap) {
+    orc_engine* o = c->o;
+    const gsx_gossipsub_params* gp = c->gp;
+    size_t L = 0;
+    const uint32_t nw = (uint32_t)gp->history_gossip < o->mc_n ? (uint32_t)gp->history_gossip : o->mc_n;
+    for (uint32_t w = 0; w < nw; w++)
+        for (size_t b = 0; b < o->mc[w].nb; b++) {
+            const orc_mc_batch* mb = &o->mc[w].b[b];
+            if (mb->topic != t) continue;
+            for (uint32_t k = 0; k < mb->m; k++) {
+                if (!mb->has[(size_t)k * mb->n + v]) continue;
+                if (L == *mids_cap) {
+                    *mids_cap = *mids_cap ? 2 * *mids_cap : 1024;
+                    *mids = (uint64_t*)realloc(*mids, sizeof(uint64_t) * *mids_cap);
+                }
+                (*mids)[L++] = mb->ids[k];
+            }
+        }
+    if (L == 0) return;
+    uint64_t* ids = *mids;
+    shuffle_ids(ids, L, g);
+    int np = 0;
+    for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+        if (!in_topic(o, (uint64_t)r)) continue;
+        const uint8_t ef = o->eflags[r];
+        if (hb_in_mesh(o, (uint64_t)r, t) || (ef & GSX_EDGE_DIRECT) || !(ef & GSX_EDGE_GOSSIPSUB)) continue;
+        if (!(score_pair(o, (uint64_t)r) >= o->th.gossip_threshold)) continue; /* live score */
+        peers[np++] = (uint64_t)r;
+    }
+    int target = gp->d_lazy;
+    const int factor = (int)(gp->gossip_factor * (double)np);
+    if (factor > target) target = factor;
+    if (target > np) target = np;
+    else shuffle_pairs(peers, np, g);
+    for (int i = 0; i < target; i++) {
+        size_t len = L;
+        if (L > (size_t)gp->max_ihave_length) {
+            shuffle_ids(ids, L, g);
+            len = (size_t)gp->max_ihave_length;
+        }
+        const size_t x = (size_t)t * o->E + peers[i];
+        o->ihave_len[x] = (uint32_t)len;
+        o->ihave_hash[x] = ihave_digest(ids, len);
+        c->out->ihave_msgs++;
+        c->out->ihave_ids += len;
+    }
+}
+
+/* mcache.Shift (mcache.go:94-104) */
+static void mcache_shift(orc_engine* o, uint32_t history) {
+    if (!o->mc) return;
+    if (history > ORC_MC_MAX) history = ORC_MC_MAX;
+    while (o->mc_n >= history && o->mc_n > 0) { /* drop history[len-1] */
+        orc_mc_window* w = &o->mc[o->mc_n - 1];
+        for (size_t i = 0; i < w->nb; i++) {
+            free(w->b[i].ids);
+            free(w->b[i].has);
+        }
+        free(w->b);
+        memset(w, 0, sizeof(*w));
+        o->mc_n--;
+    }
+    memmove(&o->mc[1], &o->mc[0], sizeof(orc_mc_window) * o->mc_n);
+    memset(&o->mc[0], 0, sizeof(orc_mc_window));
+    o->mc_n++;
 }
 
 /* handlePrune at u for a PRUNE of topic t from the peer of pair q (u -> v), :811-843 */
@@ -1294,9 +1441,19 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
     for (uint64_t r = 0; r < E; r++) cache[r] = score_pair(o, r); /* the heartbeat's score cache */
     hb_ctx c = {o, gp, cache, ctl, tick, now, out};
-    /* (A) every node's heartbeat, every joined topic */
+    memset(o->ihave_len, 0, sizeof(uint32_t) * (size_t)T * (E ? E : 1));
+    memset(o->ihave_hash, 0, sizeof(uint64_t) * (size_t)T * (E ? E : 1));
+    uint64_t* mids = NULL;
+    size_t mids_cap = 0;
+    /* (A) every node's heartbeat, every joined topic in ascending order:
+     * mesh maintenance, then IHAVE gossip, one draw stream per (node, topic) */
     for (uint32_t v = 0; v < o->n_nodes; v++)
-        for (uint32_t t = 0; t < T; t++) hb_unit(&c, v, t, seed, plst, tmp);
+        for (uint32_t t = 0; t < T; t++) {
+            orc_rng g = {seed, 8, v, (tick << 32) | ((uint64_t)t << 24), 0};
+            hb_unit(&c, v, t, &g, plst, tmp);
+            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap);
+        }
+    free(mids);
     /* (B) receivers: GRAFTs then PRUNEs of each sender, senders ascending */
     for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q); /* gs.score.Score(p) at handling time */
     for (uint32_t u = 0; u < o->n_nodes; u++) {
@@ -1361,6 +1518,7 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
         }
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
+    mcache_shift(o, (uint32_t)gp->history_length); /* :1563 */
     free(cache);
     free(ctl);
     free(resp);
@@ -1371,6 +1529,30 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
 
 int orc_export_backoff(orc_engine* o, int64_t* out) {
     memcpy(out, o->backoff, sizeof(int64_t) * (size_t)o->T * o->E);
+    return 0;
+}
+
+int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
+                   size_t* n_out) {
+    size_t n = 0;
+    const uint32_t nw = n_windows < o->mc_n ? n_windows : o->mc_n;
+    for (uint32_t w = 0; w < nw; w++)
+        for (size_t b = 0; b < o->mc[w].nb; b++) {
+            const orc_mc_batch* mb = &o->mc[w].b[b];
+            if (topic != GSX_ANY_TOPIC && mb->topic != topic) continue;
+            for (uint32_t k = 0; k < mb->m; k++)
+                if (mb->has[(size_t)k * mb->n + node]) {
+                    if (n < cap) out[n] = mb->ids[k];
+                    n++;
+                }
+        }
+    *n_out = n;
+    return 0;
+}
+
+int orc_gossip_results(orc_engine* o, uint32_t* len, uint64_t* hash) {
+    if (len) memcpy(len, o->ihave_len, sizeof(uint32_t) * (size_t)o->T * o->E);
+    if (hash) memcpy(hash, o->ihave_hash, sizeof(uint64_t) * (size_t)o->T * o->E);
     return 0;
 }
 

@@ -58,6 +58,10 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
                   gsx_heartbeat_out* out);
 int orc_export_backoff(orc_engine* o, int64_t* out);
 int orc_import_backoff(orc_engine* o, const int64_t* in);
+int orc_gossip_results(orc_engine* o, uint32_t* len, uint64_t* hash);
+int orc_mcache_clear(orc_engine* o);
+int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
+                   size_t* n_out);
 int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);
 int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs);
 

@@ -57,6 +57,10 @@ _SIG = {
                                 P(abi.HeartbeatOut)]),
     "orc_export_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "orc_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "orc_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
+    "orc_mcache_clear": (C.c_int, [C.c_void_p]),
+    "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
+                                 P(C.c_size_t)]),
 }
 
 _lib = None
@@ -161,6 +165,23 @@ class Oracle:
     def import_backoff(self, b):
         b = np.ascontiguousarray(b, dtype=np.int64).reshape(self.n_topics, self.n_pairs)
         self._chk(self.lib.orc_import_backoff(self.h, _p(b, C.c_int64)), "orc_import_backoff")
+
+    def gossip_results(self):
+        ln = np.empty((self.n_topics, self.n_pairs), dtype=np.uint32)
+        dg = np.empty((self.n_topics, self.n_pairs), dtype=np.uint64)
+        self._chk(self.lib.orc_gossip_results(self.h, _p(ln, C.c_uint32), _p(dg, C.c_uint64)), "orc_gossip_results")
+        return ln, dg
+
+    def mcache_clear(self):
+        self._chk(self.lib.orc_mcache_clear(self.h), "orc_mcache_clear")
+
+    def mcache_ids(self, node, topic, n_windows):
+        n = C.c_size_t()
+        self.lib.orc_mcache_ids(self.h, node, topic, n_windows, None, 0, C.byref(n))
+        out = np.empty(n.value, dtype=np.uint64)
+        self._chk(self.lib.orc_mcache_ids(self.h, node, topic, n_windows, _p(out, C.c_uint64), len(out), C.byref(n)),
+                  "orc_mcache_ids")
+        return out
 
     def set_ip_whitelist(self, ips: Iterable[int]):
         a = np.ascontiguousarray(list(ips), dtype=np.uint32)

@@ -19,6 +19,7 @@ def snapshot(be):
     st = be.export_state()
     st["backoff"] = be.export_backoff()
     st["scores"] = be.scores()
+    st["ihave_len"], st["ihave_digest"] = be.gossip_results()
     return st
 
 
@@ -148,3 +149,49 @@ def be_default_params():
     import oracle as orc
 
     return orc.default_gossipsub_params()
+
+
+def message_cache_case(be):
+    """TestMessageCache (mcache_test.go:11-154) through the engine: a cache
+    with HistoryGossip 3 / HistoryLength 5; node 0 publishes 10 messages per
+    window (one gossipsub batch, ids 0..59 in order), heartbeats Shift the
+    windows.  Returns the GetGossipIDs / whole-cache views the test checks."""
+    n = 2
+    edges = {(0, 1): abi.GSX_EDGE_GOSSIPSUB, (1, 0): abi.GSX_EDGE_GOSSIPSUB}
+    row_ptr, col, ef, ips, _ = _csr(n, edges)
+    be.set_peer_params(abi.PeerScoreParams(app_specific_score_set=1, decay_interval_ns=S, decay_to_zero=0.01,
+                                           behaviour_penalty_decay=0.5, retain_score_ns=S))
+    be.set_topic_params(0, _zero_weight_topic())
+    be.set_thresholds(abi.Thresholds(gossip_threshold=-10, publish_threshold=-100, graylist_threshold=-1000))
+    gp = be_default_params()
+    gp.history_gossip, gp.history_length = 3, 5
+    be.set_gossipsub_params(gp)
+    be.load_overlay(row_ptr, col, ef, ips)
+    be.apply_events(np.array([(abi.EV_ADD_PEER, 0, p, T0, 0) for p in range(2)], dtype=abi.event_dtype()))
+    views = {}
+
+    def put(lo, hi):
+        ms = np.zeros(hi - lo, dtype=abi.msg_dtype())
+        ms["source"] = 0
+        ms["msg_id"] = np.arange(lo, hi, dtype=np.uint64)
+        be.propagate(ms, pc.config(abi.GSX_ROUTER_GOSSIPSUB, max_hops=2, credit=0))
+
+    tick = [0]
+
+    def shift():
+        tick[0] += 1
+        be.heartbeat(tick[0], T0 + tick[0] * S, 3)
+
+    put(0, 10)
+    views["first"] = be.mcache_ids(0, 0, 3)
+    shift()
+    put(10, 20)
+    views["second"] = be.mcache_ids(0, 0, 3)
+    views["second_all"] = be.mcache_ids(0, abi.GSX_ANY_TOPIC, 5)
+    for lo in (20, 30, 40, 50):
+        shift()
+        put(lo, lo + 10)
+    views["cache"] = be.mcache_ids(0, abi.GSX_ANY_TOPIC, 5)
+    views["gossip"] = be.mcache_ids(0, 0, 3)
+    views["receiver"] = be.mcache_ids(1, 0, 3)  # node 1 Put what it received too
+    return views

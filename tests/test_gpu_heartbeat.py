@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _same(a, b, what):
-    for f in list(abi.STATE_FIELDS) + ["backoff", "scores"]:
+    for f in list(abi.STATE_FIELDS) + ["backoff", "scores", "ihave_len", "ihave_digest"]:
         x, y = np.asarray(a[f]), np.asarray(b[f])
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (what, f, np.argwhere(x != y)[:5])
 
@@ -119,3 +119,27 @@ def test_heartbeat_full_size(gpu_ok):
         assert go == wo
         _same(hc.snapshot(e), hc.snapshot(o), f"tick {tick}")
         assert go["grafts"] > 0 and go["prunes"] > 0
+
+
+def test_message_cache_matches_reference_test(gpu_ok):
+    from test_heartbeat_oracle import _check_message_cache
+
+    _check_message_cache(hc.message_cache_case(gsx.Engine(1)))
+
+
+@pytest.mark.parametrize("max_ihave,msgs", [(5000, 64), (9, 80), (5000, 3000)], ids=["plain", "truncated", "long"])
+def test_gossip_matches_oracle(gpu_ok, max_ihave, msgs):
+    """emitGossip on the GPU: IHAVE targets, lengths and id-list digests
+    bit-exact with the oracle over rounds that see 1..3 cached batches."""
+    gp = orc.default_gossipsub_params()
+    gp.max_ihave_length = max_ihave
+    gp.history_gossip = 3
+    runs = []
+    for be in (gsx.Engine(2), orc.Oracle(2)):
+        runs.append(hc.mesh_run(be, 700, 9, 2, seed=msgs, ticks=4, mesh_degree=5, gp=gp, prop_msgs=msgs,
+                                mostly_positive=True, first_tick=59))
+    (_, go, gs), (_, wo, ws) = runs
+    for k in range(4):
+        assert go[k] == wo[k], (k, go[k], wo[k])
+        _same(gs[k], ws[k], f"tick {k}")
+    assert sum(o["ihave_msgs"] for o in go) > 0
