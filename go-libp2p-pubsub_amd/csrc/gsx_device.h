@@ -187,22 +187,26 @@ struct DevGossipParams {
 struct GossipBatch {
     const uint64_t* seen;
     uint32_t n_words;
-    uint32_t slot_base;  // slot of message 0 in HbState::mc_ids
+    uint32_t slot_base;  // slot of message 0 in HbState::mc_digest
 };
 
 struct HbState {
     const int64_t* row_ptr;
     const uint32_t* rev;
     const uint8_t* eflags;
-    int64_t* backoff;  // [topic][pair] expiry, 0 = no entry
-    uint8_t* ctl;      // [topic][pair (v -> u)] HB_GRAFT / HB_PRUNE sent by v this round
-    uint8_t* resp;     // [topic][pair (u -> v)] PRUNE answer u sends to a GRAFT of v
+    int64_t* backoff;     // [topic][pair] expiry, 0 = no entry
+    uint64_t* ctl_graft;  // per pair (v -> u): bit t = v sent GRAFT(t) this round
+    uint64_t* ctl_prune;  // per pair (v -> u): bit t = v sent PRUNE(t)
+    uint64_t* resp;       // per pair (u -> v): bit t = u answers v's GRAFT(t) with PRUNE
+    uint8_t* dirty;       // per pair: grafted / pruned by its owner's maintenance this round
     unsigned long long* stats;
-    uint32_t* rngk;         // per node: draw counter after the maintenance of the current topic
-    uint32_t* ihave_len;    // [topic][pair] ids advertised (0 = no IHAVE)
-    uint64_t* ihave_hash;   // [topic][pair] digest of the IHAVE id list
-    const uint64_t* mc_ids; // message id per cache slot
-    DevPeerParams pp;       // live scores of emitGossip
+    uint32_t* rngk;        // per node: draw counter after the maintenance of the current topic
+    uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)
+    uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
+    const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
+    uint32_t* long_nodes;  // nodes whose gossip list needs per-target truncation
+    uint32_t* n_long;
+    DevPeerParams pp;  // live scores of emitGossip
     double gossip_threshold;
     uint64_t n_pairs;
     uint32_t n_nodes;

@@ -98,7 +98,9 @@ struct gsx_engine {
     // heartbeat: router params, backoff [topic][pair], this round's control bytes
     gsx_gossipsub_params gp{};
     int64_t* d_backoff = nullptr;
-    uint8_t *d_hbctl = nullptr, *d_hbresp = nullptr;
+    uint64_t *d_ctl_graft = nullptr, *d_ctl_prune = nullptr, *d_resp = nullptr;
+    uint8_t* d_dirty = nullptr;
+    uint32_t *d_long = nullptr, *d_nlong = nullptr;
     unsigned long long* d_hbstats = nullptr;
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
     uint64_t* d_ihave_hash = nullptr;
@@ -112,9 +114,9 @@ struct gsx_engine {
     };
     std::deque<std::vector<McBatch>> mc;
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
-    std::vector<uint64_t> mc_ids_host;
+    std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     gsx::GossipBatch* d_gb = nullptr;
-    uint64_t* d_mc_ids = nullptr;
+    uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
 
     // propagation buffers (grown on demand) and the last call's shape
@@ -269,17 +271,20 @@ void free_state(gsx_engine* e) {
         if (p) (void)hipFree(p);
     e->prop = {};
     e->d_col = nullptr;
-    void* hb[] = {e->d_backoff, e->d_hbctl, e->d_hbresp, e->d_hbstats, e->d_rngk,
-                  e->d_ihave_len, e->d_ihave_hash, e->d_gb, e->d_mc_ids};
+    void* hb[] = {e->d_backoff, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
+                  e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
+                  e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
     e->d_backoff = nullptr;
-    e->d_hbctl = e->d_hbresp = nullptr;
+    e->d_ctl_graft = e->d_ctl_prune = e->d_resp = nullptr;
+    e->d_dirty = nullptr;
+    e->d_long = e->d_nlong = nullptr;
     e->d_hbstats = nullptr;
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_ihave_hash = nullptr;
     e->d_gb = nullptr;
-    e->d_mc_ids = nullptr;
+    e->d_mc_digest = nullptr;
     e->gb_cap = e->ids_cap = 0;
     e->have_gossip = false;
     mcache_clear(e);
@@ -382,6 +387,14 @@ int flush(gsx_engine* e) {
     e->pending.clear();
     e->scores_valid = false;
     return GSX_OK;
+}
+
+// IHAVE digest term of one message id (gsx.h, gsx_gossip_results)
+uint64_t id_digest(uint64_t id) {
+    uint64_t z = id + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
 }
 
 int ensure_scores(gsx_engine* e) {
@@ -1249,7 +1262,10 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     const size_t TE = (size_t)e->T * e->E;
     if (!e->d_hbstats) {
         int rc = 0;
-        if ((rc = dalloc(e, &e->d_hbctl, TE)) || (rc = dalloc(e, &e->d_hbresp, TE)) ||
+        const size_t E = e->E;
+        if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
+            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, E)) ||
+            (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
             (rc = dalloc(e, &e->d_rngk, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
             (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
             return rc;
@@ -1263,8 +1279,12 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     h.rev = e->d_rev;
     h.eflags = e->d_eflags;
     h.backoff = e->d_backoff;
-    h.ctl = e->d_hbctl;
-    h.resp = e->d_hbresp;
+    h.ctl_graft = e->d_ctl_graft;
+    h.ctl_prune = e->d_ctl_prune;
+    h.resp = e->d_resp;
+    h.dirty = e->d_dirty;
+    h.long_nodes = e->d_long;
+    h.n_long = e->d_nlong;
     h.stats = e->d_hbstats;
     h.n_pairs = e->E;
     h.n_nodes = e->n_nodes;
@@ -1292,12 +1312,15 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
                                 e->gp.gossip_factor};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_hbctl, 0, TE ? TE : 1, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_hbresp, 0, TE ? TE : 1, e->stream));
+    const size_t E8 = 8 * (e->E ? e->E : 1);
+    HIPCHK(e, hipMemsetAsync(e->d_ctl_graft, 0, E8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ctl_prune, 0, E8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_resp, 0, E8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, e->E ? e->E : 1, e->stream));
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
     // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order
     e->gb_host.clear();
-    e->mc_ids_host.clear();
+    e->mc_digest_host.clear();
     std::vector<uint32_t> gb_off(e->T + 1, 0), max_ids(e->T, 0);
     const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
     for (uint32_t t = 0; t < e->T; ++t) {
@@ -1305,8 +1328,8 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
         for (size_t w = 0; w < n_win; ++w)
             for (const auto& b : e->mc[w]) {
                 if (b.topic != t) continue;
-                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_ids_host.size()});
-                e->mc_ids_host.insert(e->mc_ids_host.end(), b.ids.begin(), b.ids.end());
+                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_digest_host.size()});
+                for (uint64_t id : b.ids) e->mc_digest_host.push_back(id_digest(id));
                 max_ids[t] += b.n_msgs;
             }
         if (max_ids[t] > gsx::HB_GOSSIP_MAX_IDS)
@@ -1321,19 +1344,19 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
         e->gb_cap = std::max<size_t>(e->gb_host.size(), 2 * e->gb_cap);
         if (int rc = dalloc(e, &e->d_gb, e->gb_cap)) return rc;
     }
-    if (e->mc_ids_host.size() > e->ids_cap) {
-        if (e->d_mc_ids) (void)hipFree(e->d_mc_ids);
-        e->d_mc_ids = nullptr;
-        e->ids_cap = std::max<size_t>(e->mc_ids_host.size(), 2 * e->ids_cap);
-        if (int rc = dalloc(e, &e->d_mc_ids, e->ids_cap)) return rc;
+    if (e->mc_digest_host.size() > e->ids_cap) {
+        if (e->d_mc_digest) (void)hipFree(e->d_mc_digest);
+        e->d_mc_digest = nullptr;
+        e->ids_cap = std::max<size_t>(e->mc_digest_host.size(), 2 * e->ids_cap);
+        if (int rc = dalloc(e, &e->d_mc_digest, e->ids_cap)) return rc;
     }
     if (!e->gb_host.empty()) {
         HIPCHK(e, hipMemcpyAsync(e->d_gb, e->gb_host.data(), sizeof(gsx::GossipBatch) * e->gb_host.size(),
                                  hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_mc_ids, e->mc_ids_host.data(), 8 * e->mc_ids_host.size(),
+        HIPCHK(e, hipMemcpyAsync(e->d_mc_digest, e->mc_digest_host.data(), 8 * e->mc_digest_host.size(),
                                  hipMemcpyHostToDevice, e->stream));
     }
-    h.mc_ids = e->d_mc_ids;
+    h.mc_digest = e->d_mc_digest;
     if (e->have_gossip || !e->gb_host.empty()) {
         HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));

@@ -1,27 +1,47 @@
-// gsx_heartbeat.hip — the GossipSub heartbeat's mesh maintenance as one
-// synchronous round over the whole overlay (gsx.h, gsx_heartbeat).
+// gsx_heartbeat.hip — the GossipSub heartbeat's mesh maintenance and IHAVE
+// gossip as one synchronous round over the whole overlay (gsx.h,
+// gsx_heartbeat).
 //
-//  (A) per topic t ascending: k_hb_mesh, one lane per node v, the mesh
-//      maintenance of (v, t) (gossipsub.go:1344-1510); everything it touches
-//      — the records, backoff entries and control bytes of v's own pairs for
-//      topic t — belongs to it alone, so lanes need no atomics except for the
-//      round counters (candidate and mesh lists: <= HB_MAX_DEG u16 offsets in
-//      scratch); then k_hb_gossip, one wave per node, its IHAVE emission.
-//  (B) k_hb_recv: one lane per receiving node u, walking its senders in
-//      ascending order (the Dhi check reads the mesh size the previous
-//      accepts left).  handleGraft / handlePrune, gossipsub.go:718-843.
+//  (A) per topic t ascending:
+//      k_hb_mesh — one lane per node v: the mesh maintenance of (v, t)
+//        (gossipsub.go:1344-1510).  Everything it touches — the records,
+//        backoff entries and control bits of v's own pairs for topic t —
+//        belongs to it alone.  Mesh and candidate lists are <= HB_MAX_DEG u16
+//        offsets in scratch.
+//      k_hb_gossip — one lane per node: emitGossip (:1669-1723).  The IHAVE
+//        list is the node's GetGossipIDs set (mcache.go:82-92) read straight
+//        from the cached batches' seen words; its order is never observable
+//        (handleIHave collects ids into a map, :641-650), so an untruncated
+//        list is reported by its length and multiset digest and its shuffle
+//        only advances the draw stream.  Nodes whose list exceeds
+//        MaxIHaveLength (per-target reshuffle + truncation, :1708-1716) are
+//        queued for k_hb_gossip_long, one wave per node with the list in LDS.
+//  (B) k_hb_recv: one lane per receiving node u, senders in ascending order
+//      (the Dhi check reads the mesh size the previous accepts left):
+//      handleGraft / handlePrune, :718-843, AcceptFrom-gated (:582-593).
 //  (C) k_hb_answer: one lane per pair, the GRAFT senders' handlePrune of the
 //      PRUNE answers.
-// Integer/byte work with scattered reads of the per-pair score cache; it runs
-// once per heartbeat, not per refresh, so clarity wins over lane efficiency.
+// Control messages are per-pair topic bitmasks (bit t of a u64), so a
+// receiver reads one word per sender.  Round counters are summed per wave
+// before one atomic each.  Integer/byte work with scattered reads of the
+// per-pair score cache: latency-bound, no MFMA/LDS tiling applies.
 #include "gsx_ops.h"
 
 namespace gsx {
 
 constexpr uint64_t TAG_HEARTBEAT = 8;
 
-__device__ __forceinline__ void count(unsigned long long* stats, int k, unsigned long long n = 1) {
-    atomicAdd(&stats[k], n);
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+// Sums a per-lane counter over the wave; lane 0 adds it to the round total.
+// Every lane of the wave must call it.
+__device__ __forceinline__ void flush_count(unsigned long long* stats, int k, uint64_t c) {
+    c = wave_sum64(c);
+    if ((threadIdx.x % 64) == 0 && c) atomicAdd(&stats[k], (unsigned long long)c);
 }
 
 __device__ __forceinline__ bool hb_in_mesh(const DevState& s, uint64_t r, uint32_t t) {
@@ -38,17 +58,15 @@ __device__ __forceinline__ void add_backoff(const HbState& h, uint64_t r, uint32
 
 // clearBackoff, gossipsub.go:1585-1604
 __global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    bool cleared = false;
-    if (i < n) {
+    uint64_t cleared = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
         const int64_t b = h.backoff[i];
         if (b != 0 && b + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
             h.backoff[i] = 0;
-            cleared = true;
+            ++cleared;
         }
     }
-    const unsigned long long c = __popcll(__ballot(cleared));
-    if (c && (threadIdx.x % 64) == 0) count(h.stats, HB_BACKOFF_CLEARED, c);
+    flush_count(h.stats, HB_BACKOFF_CLEARED, cleared);
 }
 
 struct HbUnit {
@@ -57,6 +75,7 @@ struct HbUnit {
     uint32_t t;
     int64_t r0;  // first pair of the row
     int deg;
+    uint64_t grafts = 0, prunes = 0;
 
     __device__ bool in_mesh(int i) const { return hb_in_mesh(s, r0 + i, t); }
     __device__ uint8_t ef(int i) const { return h.eflags[r0 + i]; }
@@ -94,16 +113,20 @@ struct HbUnit {
         return n;
     }
 
-    __device__ void graft(int i) const {  // graftPeer, :1353-1359
-        ev_graft(s, r0 + i, t, h.now);
-        h.ctl[(size_t)t * h.n_pairs + r0 + i] = HB_GRAFT;
-        count(h.stats, HB_GRAFTS);
+    __device__ void graft(int i) {  // graftPeer, :1353-1359
+        const uint64_t r = r0 + i;
+        ev_graft(s, r, t, h.now);
+        h.ctl_graft[r] |= 1ull << t;
+        h.dirty[r] = 1;
+        ++grafts;
     }
-    __device__ void prune(int i) const {  // prunePeer, :1345-1351
-        ev_prune(s, r0 + i, t);
-        add_backoff(h, r0 + i, t, h.gp.prune_backoff_ns);
-        h.ctl[(size_t)t * h.n_pairs + r0 + i] = HB_PRUNE;
-        count(h.stats, HB_PRUNES);
+    __device__ void prune(int i) {  // prunePeer, :1345-1351
+        const uint64_t r = r0 + i;
+        ev_prune(s, r, t);
+        add_backoff(h, r, t, h.gp.prune_backoff_ns);
+        h.ctl_prune[r] |= 1ull << t;
+        h.dirty[r] = 1;
+        ++prunes;
     }
 
     // stable insertion sort by cached score
@@ -125,86 +148,169 @@ struct HbUnit {
         for (int j = i; j > 0; --j) a[j] = a[j - 1];
         a[0] = p;
     }
+
+    __device__ void maintain(Rng& g) {
+        const DevGossipParams& gp = h.gp;
+        uint16_t plst[HB_MAX_DEG], tmp[HB_MAX_DEG];
+        // drop all peers with negative score, without PX (:1361-1368)
+        int n = mesh_list(plst);
+        for (int i = 0; i < n; ++i)
+            if (score(plst[i]) < 0) prune(plst[i]);
+        // do we have enough peers? (:1370-1385)
+        n = mesh_list(plst);
+        if (n < gp.d_lo) {
+            const int k = get_peers(gp.d - n, false, 0, 0.0, tmp, g);
+            for (int i = 0; i < k; ++i) graft(tmp[i]);
+        }
+        // do we have too many peers? (:1387-1448)
+        n = mesh_list(plst);
+        if (n > gp.d_hi) {
+            g.shuffle(plst, n);
+            sort_by_score(plst, n, true);
+            g.shuffle(plst + gp.d_score, n - gp.d_score);
+            int outbound = 0;
+            for (int i = 0; i < gp.d; ++i)
+                if (ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
+            if (outbound < gp.d_out) {
+                if (outbound > 0) {
+                    int ihave = outbound;
+                    for (int i = 1; i < gp.d && ihave > 0; ++i)
+                        if (ef(plst[i]) & EDGE_OUTBOUND) {
+                            rotate(plst, i);
+                            --ihave;
+                        }
+                }
+                int ineed = gp.d_out - outbound;
+                for (int i = gp.d; i < n && ineed > 0; ++i)
+                    if (ef(plst[i]) & EDGE_OUTBOUND) {
+                        rotate(plst, i);
+                        --ineed;
+                    }
+            }
+            for (int i = gp.d; i < n; ++i) prune(plst[i]);
+        }
+        // do we have enough outbound peers? (:1450-1476)
+        n = mesh_list(plst);
+        if (n >= gp.d_lo) {
+            int outbound = 0;
+            for (int i = 0; i < n; ++i)
+                if (ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
+            if (outbound < gp.d_out) {
+                const int k = get_peers(gp.d_out - outbound, true, 0, 0.0, tmp, g);
+                for (int i = 0; i < k; ++i) graft(tmp[i]);
+            }
+        }
+        // opportunistic grafting (:1478-1510)
+        n = mesh_list(plst);
+        if (gp.og_ticks && h.tick % gp.og_ticks == 0 && n > 1) {
+            sort_by_score(plst, n, false);
+            const double median = score(plst[n / 2]);
+            if (median < h.og_threshold) {
+                const int k = get_peers(gp.og_peers, false, 1, median, tmp, g);
+                for (int i = 0; i < k; ++i) graft(tmp[i]);
+            }
+        }
+    }
 };
+
+__device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, uint32_t k) {
+    return Rng{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), k};
+}
 
 // One launch per topic, ascending: the maintenance of (v, t) for every v.
 __global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
     const uint32_t v = blockIdx.x * 64u + threadIdx.x;
-    if (v >= h.n_nodes) return;
-    const int64_t r0 = h.row_ptr[v];
-    const HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
-    const DevGossipParams& gp = h.gp;
-    Rng g{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), 0};
-    uint16_t plst[HB_MAX_DEG], tmp[HB_MAX_DEG];
-
-    // drop all peers with negative score, without PX (:1361-1368)
-    int n = U.mesh_list(plst);
-    for (int i = 0; i < n; ++i)
-        if (U.score(plst[i]) < 0) U.prune(plst[i]);
-    // do we have enough peers? (:1370-1385)
-    n = U.mesh_list(plst);
-    if (n < gp.d_lo) {
-        const int k = U.get_peers(gp.d - n, false, 0, 0.0, tmp, g);
-        for (int i = 0; i < k; ++i) U.graft(tmp[i]);
+    uint64_t grafts = 0, prunes = 0;
+    if (v < h.n_nodes) {
+        const int64_t r0 = h.row_ptr[v];
+        HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
+        Rng g = hb_rng(h, v, t, 0);
+        U.maintain(g);
+        h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
+        grafts = U.grafts;
+        prunes = U.prunes;
     }
-    // do we have too many peers? (:1387-1448)
-    n = U.mesh_list(plst);
-    if (n > gp.d_hi) {
-        g.shuffle(plst, n);
-        U.sort_by_score(plst, n, true);
-        g.shuffle(plst + gp.d_score, n - gp.d_score);
-        int outbound = 0;
-        for (int i = 0; i < gp.d; ++i)
-            if (U.ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
-        if (outbound < gp.d_out) {
-            if (outbound > 0) {
-                int ihave = outbound;
-                for (int i = 1; i < gp.d && ihave > 0; ++i)
-                    if (U.ef(plst[i]) & EDGE_OUTBOUND) {
-                        HbUnit::rotate(plst, i);
-                        --ihave;
-                    }
-            }
-            int ineed = gp.d_out - outbound;
-            for (int i = gp.d; i < n && ineed > 0; ++i)
-                if (U.ef(plst[i]) & EDGE_OUTBOUND) {
-                    HbUnit::rotate(plst, i);
-                    --ineed;
-                }
-        }
-        for (int i = gp.d; i < n; ++i) U.prune(plst[i]);
-    }
-    // do we have enough outbound peers? (:1450-1476)
-    n = U.mesh_list(plst);
-    if (n >= gp.d_lo) {
-        int outbound = 0;
-        for (int i = 0; i < n; ++i)
-            if (U.ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
-        if (outbound < gp.d_out) {
-            const int k = U.get_peers(gp.d_out - outbound, true, 0, 0.0, tmp, g);
-            for (int i = 0; i < k; ++i) U.graft(tmp[i]);
-        }
-    }
-    // opportunistic grafting (:1478-1510)
-    n = U.mesh_list(plst);
-    if (gp.og_ticks && h.tick % gp.og_ticks == 0 && n > 1) {
-        U.sort_by_score(plst, n, false);
-        const double median = U.score(plst[n / 2]);
-        if (median < h.og_threshold) {
-            const int k = U.get_peers(gp.og_peers, false, 1, median, tmp, g);
-            for (int i = 0; i < k; ++i) U.graft(tmp[i]);
-        }
-    }
-    h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
+    flush_count(h.stats, HB_GRAFTS, grafts);
+    flush_count(h.stats, HB_PRUNES, prunes);
 }
 
 // ---- emitGossip (gossipsub.go:1669-1723) --------------------------------------
-// One wave per node for topic t, after the maintenance of topic t (so the
-// live scores see topics <= t maintained, > t not yet: the reference's
-// sequential order).  The node's GetGossipIDs list (mcache.go:82-92) is built
-// in LDS from the cached batches' seen words; the shuffles draw 64 Int31s at
-// once (one per lane, Go's rejection rule resolved by a ballot) and lane 0
-// applies the swaps in order.
+
+// The live score of emitGossip (:1692): the heartbeat-start cache, except for
+// pairs the node's maintenance of topics <= t has grafted or pruned.
+__device__ __forceinline__ double live_score(const DevState& s, const HbState& h, uint64_t r) {
+    return h.dirty[r] ? eval_pair(s, h.pp, r) : s.score[r];
+}
+
+// Eligible targets of (v, t), ascending: topic peers with the mesh feature,
+// not in the mesh, not direct, live score >= GossipThreshold.
+__device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
+    const uint8_t f = h.eflags[r];
+    return (s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+           (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && !hb_in_mesh(s, r, t) &&
+           live_score(s, h, r) >= h.gossip_threshold;
+}
+
+// Advances g over shuffleStrings of an n-element list (gossipsub.go:1897-1902)
+// without materialising it: one Int31n(i + 1) per step, rejections redrawn.
+__device__ __forceinline__ void skip_shuffle(Rng& g, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) (void)g.int31n((int32_t)(i + 1));
+}
+
+__global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
+                                                  uint32_t n_gb) {
+    const uint32_t v = blockIdx.x * 64u + threadIdx.x;
+    uint64_t msgs = 0, ids = 0;
+    if (v < h.n_nodes) {
+        // GetGossipIDs of (v, t): its length and multiset digest
+        uint32_t L = 0;
+        uint64_t dig = 0;
+        for (uint32_t b = 0; b < n_gb; ++b) {
+            const GossipBatch B = gb[b];
+            for (uint32_t w = 0; w < B.n_words; ++w) {
+                uint64_t word = B.seen[(size_t)w * h.n_nodes + v];
+                L += (uint32_t)__popcll(word);
+                while (word) {
+                    dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
+                    word &= word - 1;
+                }
+            }
+        }
+        if (L > 0) {  // emitGossip returns early on an empty list, drawing nothing
+            const int64_t r0 = h.row_ptr[v];
+            const int deg = (int)(h.row_ptr[v + 1] - r0);
+            uint16_t peers[HB_MAX_DEG];
+            int np = 0;
+            for (int i = 0; i < deg; ++i)
+                if (gossip_target(s, h, r0 + i, t)) peers[np++] = (uint16_t)i;
+            int target = h.gp.d_lazy;
+            const int factor = (int)(h.gp.gossip_factor * (double)np);
+            if (factor > target) target = factor;
+            const bool shuffle_peers = target <= np;
+            if (!shuffle_peers) target = np;
+            if (target > 0 && L > (uint32_t)h.gp.max_ihave) {
+                h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // per-target truncation: k_hb_gossip_long
+            } else if (target > 0) {
+                if (shuffle_peers) {  // the list shuffle only matters through the draws it consumes
+                    Rng g = hb_rng(h, v, t, h.rngk[v]);
+                    skip_shuffle(g, L);
+                    g.shuffle(peers, np);
+                }
+                for (int p = 0; p < target; ++p) {
+                    const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
+                    h.ihave_len[x] = L;
+                    h.ihave_hash[x] = dig;
+                }
+                msgs = (uint64_t)target;
+                ids = (uint64_t)target * L;
+            }
+        }
+    }
+    flush_count(h.stats, HB_IHAVE_MSGS, msgs);
+    flush_count(h.stats, HB_IHAVE_IDS, ids);
+}
+
+// ---- lists longer than MaxIHaveLength: one wave per queued node -------------
 
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  // exclusive
     uint32_t incl = x;
@@ -216,13 +322,9 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  //
     return incl - x;
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-}
-
-// shuffleStrings (gossipsub.go:1897-1902) of a[0..L) in LDS; g is wave-uniform.
+// shuffleStrings of a[0..L) in LDS; g is wave-uniform.  64 Int31s are drawn
+// at once (one per lane, Go's rejection rule resolved by a ballot); lane 0
+// applies the swaps in order.
 __device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uint32_t lane) {
     uint32_t i = 0;
     while (i < L) {
@@ -256,88 +358,83 @@ __device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uin
     }
 }
 
-__global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
-                                                  uint32_t n_gb) {
+__global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, uint32_t t,
+                                                       const GossipBatch* __restrict__ gb, uint32_t n_gb) {
     extern __shared__ uint32_t mids[];  // message slots, GetGossipIDs order
     __shared__ uint16_t peers[HB_MAX_DEG];
     __shared__ int32_t jbuf[64];
     __shared__ uint32_t kshare;
-    const uint32_t v = blockIdx.x, lane = threadIdx.x;
-    // GetGossipIDs: windows newest first, batches in Put order, ids ascending
-    uint32_t L = 0;
-    for (uint32_t b = 0; b < n_gb; ++b) {
-        const GossipBatch B = gb[b];
-        for (uint32_t w0 = 0; w0 < B.n_words; w0 += 64) {
-            const uint32_t w = w0 + lane;
-            uint64_t word = w < B.n_words ? B.seen[(size_t)w * h.n_nodes + v] : 0;
-            const uint32_t c = (uint32_t)__popcll(word);
-            uint32_t pos = L + wave_prefix(c, lane);
-            while (word) {
-                mids[pos++] = B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word);
-                word &= word - 1;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t n_long = *h.n_long;
+    uint64_t msgs = 0, ids = 0;
+    for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
+        const uint32_t v = h.long_nodes[li];
+        // GetGossipIDs: windows newest first, batches in Put order, ids ascending
+        uint32_t L = 0;
+        for (uint32_t b = 0; b < n_gb; ++b) {
+            const GossipBatch B = gb[b];
+            for (uint32_t w0 = 0; w0 < B.n_words; w0 += 64) {
+                const uint32_t w = w0 + lane;
+                uint64_t word = w < B.n_words ? B.seen[(size_t)w * h.n_nodes + v] : 0;
+                const uint32_t c = (uint32_t)__popcll(word);
+                uint32_t pos = L + wave_prefix(c, lane);
+                while (word) {
+                    mids[pos++] = B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word);
+                    word &= word - 1;
+                }
+                L = __shfl(pos, 63, 64);  // lane 63's end = the new total
             }
-            L += __shfl(pos, 63, 64) - L;  // lane 63's end = the new total
-        }
-    }
-    __syncthreads();
-    if (L == 0) return;
-    Rng g{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), h.rngk[v]};
-    wave_shuffle(mids, L, g, jbuf, lane);
-    // eligible targets, ascending: topic peers with the mesh feature, not in
-    // the mesh, not direct, live score >= GossipThreshold
-    const int64_t r0 = h.row_ptr[v];
-    const int deg = (int)(h.row_ptr[v + 1] - r0);
-    int np = 0;
-    for (int c0 = 0; c0 < deg; c0 += 64) {
-        const int i = c0 + (int)lane;
-        bool ok = false;
-        if (i < deg) {
-            const uint64_t r = r0 + i;
-            const uint8_t f = h.eflags[r];
-            ok = (s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
-                 (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && !hb_in_mesh(s, r, t) &&
-                 eval_pair(s, h.pp, r) >= h.gossip_threshold;
-        }
-        const uint64_t bal = __ballot(ok);
-        if (ok) peers[np + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)i;
-        np += __popcll(bal);
-    }
-    __syncthreads();
-    int target = h.gp.d_lazy;
-    const int factor = (int)(h.gp.gossip_factor * (double)np);
-    if (factor > target) target = factor;
-    if (target > np) {
-        target = np;
-    } else {
-        if (lane == 0) {
-            g.shuffle(peers, np);
-            kshare = g.k;
         }
         __syncthreads();
-        g.k = kshare;
-    }
-    uint64_t n_ids = 0;
-    for (int p = 0; p < target; ++p) {
-        uint32_t len = L;
-        if (L > (uint32_t)h.gp.max_ihave) {
+        Rng g = hb_rng(h, v, t, h.rngk[v]);
+        wave_shuffle(mids, L, g, jbuf, lane);
+        const int64_t r0 = h.row_ptr[v];
+        const int deg = (int)(h.row_ptr[v + 1] - r0);
+        int np = 0;
+        for (int c0 = 0; c0 < deg; c0 += 64) {
+            const int i = c0 + (int)lane;
+            const bool ok = i < deg && gossip_target(s, h, r0 + i, t);
+            const uint64_t bal = __ballot(ok);
+            if (ok) peers[np + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)i;
+            np += __popcll(bal);
+        }
+        __syncthreads();
+        int target = h.gp.d_lazy;
+        const int factor = (int)(h.gp.gossip_factor * (double)np);
+        if (factor > target) target = factor;
+        if (target > np) {
+            target = np;
+        } else {
+            if (lane == 0) {
+                g.shuffle(peers, np);
+                kshare = g.k;
+            }
+            __syncthreads();
+            g.k = kshare;
+        }
+        const uint32_t len = (uint32_t)h.gp.max_ihave;  // L > MaxIHaveLength here
+        for (int p = 0; p < target; ++p) {
             wave_shuffle(mids, L, g, jbuf, lane);
-            len = (uint32_t)h.gp.max_ihave;
+            uint64_t d = 0;
+            for (uint32_t e = lane; e < len; e += 64) d += h.mc_digest[mids[e]];
+            d = wave_sum64(d);
+            if (lane == 0) {
+                const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
+                h.ihave_len[x] = len;
+                h.ihave_hash[x] = d;
+            }
         }
-        uint64_t d = 0;
-        for (uint32_t e = lane; e < len; e += 64) d += smix(h.mc_ids[mids[e]] + 0x9E3779B97F4A7C15ull * (e + 1));
-        d = wave_sum64(d);
         if (lane == 0) {
-            const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
-            h.ihave_len[x] = len;
-            h.ihave_hash[x] = d;
+            msgs += (uint64_t)target;
+            ids += (uint64_t)target * len;
         }
-        n_ids += len;
+        __syncthreads();
     }
-    if (lane == 0 && target > 0) {
-        count(h.stats, HB_IHAVE_MSGS, (unsigned long long)target);
-        count(h.stats, HB_IHAVE_IDS, n_ids);
-    }
+    flush_count(h.stats, HB_IHAVE_MSGS, msgs);
+    flush_count(h.stats, HB_IHAVE_IDS, ids);
 }
+
+// ---- (B) receivers -------------------------------------------------------------
 
 // handlePrune at the owner of pair q for topic t (:811-843): the tracer's
 // Prune, then the PRUNE's backoff, which travels in whole seconds (:1821).
@@ -345,91 +442,111 @@ __device__ __forceinline__ void handle_prune(const DevState& s, const HbState& h
     ev_prune(s, q, t);
     const int64_t secs = h.gp.prune_backoff_ns / 1000000000LL;
     add_backoff(h, q, t, secs > 0 ? secs * 1000000000LL : h.gp.prune_backoff_ns);
-    count(h.stats, HB_PRUNES_HANDLED);
 }
 
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     const uint32_t u = blockIdx.x * 64u + threadIdx.x;
-    if (u >= h.n_nodes) return;
-    const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-    const DevGossipParams& gp = h.gp;
-    for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
-        const uint32_t r = h.rev[q];     // r = (v -> u), the sender's pair
-        if (r == NO_PAIR) continue;
-        const double score = s.score[q];  // gs.score.Score(p) once per control message
-        const uint8_t ef = h.eflags[q];
-        // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
-        if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
-        for (uint32_t t = 0; t < s.n_topics; ++t) {  // handleGraft, :718-809
-            if (h.ctl[(size_t)t * h.n_pairs + r] != HB_GRAFT) continue;
-            if (hb_in_mesh(s, q, t)) continue;
-            uint8_t* const resp = &h.resp[(size_t)t * h.n_pairs + q];
-            if (ef & EDGE_DIRECT) {
-                *resp = 1;
-                count(h.stats, HB_REJECTED);
-                continue;
-            }
-            const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
-            if (expire != 0 && h.now < expire) {
-                ev_penalty(s, q, 1);
-                count(h.stats, HB_PENALTIES);
-                if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
-                    ev_penalty(s, q, 1);
-                    count(h.stats, HB_PENALTIES);
+    uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
+    if (u < h.n_nodes) {
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        const DevGossipParams& gp = h.gp;
+        for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
+            const uint32_t r = h.rev[q];     // r = (v -> u), the sender's pair
+            if (r == NO_PAIR) continue;
+            uint64_t grafts = h.ctl_graft[r], prunes = h.ctl_prune[r];
+            if (!(grafts | prunes)) continue;
+            const double score = s.score[q];  // gs.score.Score(p) once per control message
+            const uint8_t ef = h.eflags[q];
+            // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
+            if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
+            uint64_t resp = 0;
+            for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
+                const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
+                if (hb_in_mesh(s, q, t)) continue;
+                if (ef & EDGE_DIRECT) {
+                    resp |= 1ull << t;
+                    ++rejected;
+                    continue;
                 }
-                add_backoff(h, q, t, gp.prune_backoff_ns);
-                *resp = 1;
-                count(h.stats, HB_REJECTED);
-                continue;
+                const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
+                if (expire != 0 && h.now < expire) {
+                    ev_penalty(s, q, 1);
+                    ++penalties;
+                    if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
+                        ev_penalty(s, q, 1);
+                        ++penalties;
+                    }
+                    add_backoff(h, q, t, gp.prune_backoff_ns);
+                    resp |= 1ull << t;
+                    ++rejected;
+                    continue;
+                }
+                if (score < 0) {
+                    resp |= 1ull << t;
+                    add_backoff(h, q, t, gp.prune_backoff_ns);
+                    ++rejected;
+                    continue;
+                }
+                int n = 0;
+                for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
+                if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
+                    resp |= 1ull << t;
+                    add_backoff(h, q, t, gp.prune_backoff_ns);
+                    ++rejected;
+                    continue;
+                }
+                ev_graft(s, q, t, h.now);
+                ++accepted;
             }
-            if (score < 0) {
-                *resp = 1;
-                add_backoff(h, q, t, gp.prune_backoff_ns);
-                count(h.stats, HB_REJECTED);
-                continue;
+            h.resp[q] = resp;
+            for (; prunes; prunes &= prunes - 1) {  // handlePrune
+                handle_prune(s, h, q, (uint32_t)__builtin_ctzll(prunes));
+                ++handled;
             }
-            int n = 0;
-            for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
-            if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
-                *resp = 1;
-                add_backoff(h, q, t, gp.prune_backoff_ns);
-                count(h.stats, HB_REJECTED);
-                continue;
-            }
-            ev_graft(s, q, t, h.now);
-            count(h.stats, HB_ACCEPTED);
         }
-        for (uint32_t t = 0; t < s.n_topics; ++t)  // handlePrune
-            if (h.ctl[(size_t)t * h.n_pairs + r] == HB_PRUNE) handle_prune(s, h, q, t);
     }
+    flush_count(h.stats, HB_ACCEPTED, accepted);
+    flush_count(h.stats, HB_REJECTED, rejected);
+    flush_count(h.stats, HB_PENALTIES, penalties);
+    flush_count(h.stats, HB_PRUNES_HANDLED, handled);
 }
+
+// ---- (C) the GRAFT senders handle the PRUNE answers ------------------------------
 
 __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;  // r = (v -> u)
-    if (r >= h.n_pairs) return;
-    const uint32_t q = h.rev[r];
-    if (q == NO_PAIR) return;
-    if (!(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) return;  // AcceptFrom
-    for (uint32_t t = 0; t < s.n_topics; ++t)
-        if (h.resp[(size_t)t * h.n_pairs + q]) handle_prune(s, h, r, t);
+    uint64_t handled = 0;
+    if (r < h.n_pairs) {
+        const uint32_t q = h.rev[r];
+        uint64_t resp = q == NO_PAIR ? 0 : h.resp[q];
+        // AcceptFrom at v for the answering peer
+        if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
+        for (; resp; resp &= resp - 1) {
+            handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp));
+            ++handled;
+        }
+    }
+    flush_count(h.stats, HB_PRUNES_HANDLED, handled);
 }
 
 __global__ __launch_bounds__(256) void k_hb_mesh_links(DevState s, HbState h) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    unsigned long long c = 0;
-    if (r < h.n_pairs)
-        for (uint32_t t = 0; t < s.n_topics; ++t) c += hb_in_mesh(s, r, t);
-    // wave sum
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-    if ((threadIdx.x % 64) == 0 && c) count(h.stats, HB_MESH_LINKS, c);
+    uint64_t c = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u)
+        if (s.pflags[r] & PAIR_PRESENT)
+            for (uint32_t t = 0; t < s.n_topics; ++t) c += (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH) != 0;
+    flush_count(h.stats, HB_MESH_LINKS, c);
 }
 
 static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+static inline unsigned grid_cap(uint64_t n, unsigned bs) {
+    const unsigned b = blocks_for(n, bs);
+    return b < 2048 ? b : 2048;
+}
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
     const uint64_t n = (uint64_t)n_topics * h.n_pairs;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(blocks_for(n, 256)), dim3(256), 0, st, h, n);
+    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(grid_cap(n, 256)), dim3(256), 0, st, h, n);
     return hipGetLastError();
 }
 
@@ -442,7 +559,12 @@ hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipSt
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
                             uint32_t max_ids, hipStream_t st) {
     if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_gossip, dim3(h.n_nodes), dim3(64), sizeof(uint32_t) * max_ids, st, s, h, t, gb, n_gb);
+    hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hb_gossip, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t, gb, n_gb);
+    if (max_ids > (uint32_t)h.gp.max_ihave)  // some node may need the truncating path
+        hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), sizeof(uint32_t) * max_ids, st,
+                           s, h, t, gb, n_gb);
     return hipGetLastError();
 }
 
@@ -460,7 +582,7 @@ hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st)
 
 hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh_links, dim3(blocks_for(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    hipLaunchKernelGGL(k_hb_mesh_links, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, s, h);
     return hipGetLastError();
 }
 

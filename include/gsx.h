@@ -452,9 +452,11 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, g
 int gsx_export_backoff(gsx_engine* e, int64_t* out);
 int gsx_import_backoff(gsx_engine* e, const int64_t* in);
 /* The IHAVEs of the last gsx_heartbeat, per [topic][pair (sender -> target)]:
- * number of ids (0 = none sent) and an order-sensitive digest of the id list,
- * sum over positions i of mix64(id_i + 0x9E3779B97F4A7C15 * (i + 1)) (mod 2^64,
- * mix64 = SplitMix64's finaliser).  Either pointer may be NULL. */
+ * number of ids (0 = none sent) and a digest of the advertised ids, the sum
+ * over the list of mix64(id + 0x9E3779B97F4A7C15) (mod 2^64, mix64 =
+ * SplitMix64's finaliser).  The order inside an IHAVE is not reported: the
+ * receiver collects the ids into a set (handleIHave, gossipsub.go:641-650).
+ * Either pointer may be NULL. */
 int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest);
 /* Drop every cached message window (mcache.go, a fresh cache). */
 int gsx_mcache_clear(gsx_engine* e);

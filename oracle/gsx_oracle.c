@@ -1333,9 +1333,9 @@ static void shuffle_ids(uint64_t* a, size_t n, orc_rng* g) { /* shuffleStrings, 
     }
 }
 
-static uint64_t ihave_digest(const uint64_t* ids, size_t n) {
+static uint64_t ihave_digest(const uint64_t* ids, size_t n) { /* gsx.h, gsx_gossip_results */
     uint64_t d = 0;
-    for (size_t i = 0; i < n; i++) d += splitmix(ids[i] + 0x9E3779B97F4A7C15ULL * (uint64_t)(i + 1));
+    for (size_t i = 0; i < n; i++) d += splitmix(ids[i] + 0x9E3779B97F4A7C15ULL);
     return d;
 }
 
