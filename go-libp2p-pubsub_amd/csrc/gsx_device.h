@@ -120,31 +120,44 @@ constexpr uint8_t FWD_RSUB_CAND = 0x04;  // u is one of v's RandomSub peers (dra
 constexpr int RANDOMSUB_D = 6;           // randomsub.go:16-18
 constexpr int RSUB_MAX_DEG = 256;
 constexpr int MAX_HOPS = 64;
-enum { STAT_DUPS = 0, STAT_HOP0 = 1, STAT_WORDS = STAT_HOP0 + MAX_HOPS + 1 };
+// Propagation counters: duplicates, first receipts per hop, and the
+// push-minimal traffic terms of SURVEY.md §8d (summed over hops and 64-message
+// words): eligible (edge, word) sends and (vertex, word) pairs gaining bits.
+enum { STAT_DUPS = 0, STAT_HOP0 = 1, STAT_EDGE_SENDS = STAT_HOP0 + MAX_HOPS + 1, STAT_NEW_WORDS, STAT_WORDS };
+// rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
+constexpr uint32_t HALO = 0x80000000u;
 
 struct DevMsg {
-    uint32_t source;
+    uint32_t source;  // global node id
     uint32_t reserved;
     uint64_t msg_id;
 };
 
+// Node-major bitsets: a node's (or pair's) n_words message words are
+// contiguous, so one gather brings every word of a neighbour.
 struct PropState {
     const int64_t* row_ptr;
-    const int32_t* col;
-    const uint32_t* rev;   // pair (u -> v) -> pair (v -> u), NO_PAIR if absent
+    const int32_t* col;        // global node ids
+    const uint32_t* rev;       // pair (u -> v) -> pair (v -> u); NO_PAIR; HALO | slot if v is remote
+    const uint32_t* pair_obs;  // per pair: local observer index
     const uint8_t* eflags;
-    uint8_t* fwd;          // per pair, this call: FWD_*
+    uint8_t* fwd;              // per pair r = (v -> u), this call: FWD_* (v sends to u)
+    uint8_t* fwd_in;           // per pair q = (u -> v): fwd[rev[q]] for a local v, else 0
     const DevMsg* msgs;
-    uint64_t* seen;        // [word][node]
-    uint64_t* origin;      // [word][node] messages the node published
-    uint64_t* from_mask;   // [word][pair (u -> v)] messages u first received from v
-    uint64_t* sel;         // [word][pair] RandomSub draws (null for other routers)
-    uint8_t* hop;          // [message][node] arrival hop, 0xFF never
-    uint32_t* dupcnt;      // per pair: duplicates inside the P3 window
-    unsigned long long* stats;  // STAT_*
+    uint64_t* seen;            // [node][word]
+    uint64_t* origin;          // [node][word] messages the node published
+    uint64_t* from_mask;       // [pair (u -> v)][word] messages u first received from v
+    uint64_t* sel;             // [pair][word] RandomSub draws (null for other routers)
+    uint8_t* hop;              // [node][word * 64] arrival hop, 0xFF never
+    uint32_t* dupcnt;          // per pair: duplicates inside the P3 window
+    uint32_t* firstcnt;        // per pair: first receipts (deferred credits), or null
+    unsigned long long* stats; // STAT_*
+    const uint64_t* halo;      // [receive slot][word]: filtered sends of remote neighbours
+    const uint32_t* send_pair; // per send slot: the local pair (v -> u) it carries, NO_PAIR = none
+    uint64_t n_send;
     uint64_t n_pairs;
-    uint32_t n_nodes, n_words, n_msgs;
-    uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt;
+    uint32_t n_nodes, n_words, n_msgs, node_lo;
+    uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt, sharded;
     double publish_threshold;
     int64_t hop_latency, window;
     uint64_t seed;
@@ -152,9 +165,14 @@ struct PropState {
 
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st);
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
+hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStream_t st);
+hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
-hipError_t launch_prop_credit(const PropState& ps, const DevState& s, hipStream_t st);
+hipError_t launch_prop_count(const PropState& ps, hipStream_t st);
+hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
+                            hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
+hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st);
 
 // ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------
 constexpr int HB_MAX_DEG = 256;  // per-node pair count the mesh lanes hold (u16 offsets, scratch)
@@ -183,7 +201,7 @@ struct DevGossipParams {
 };
 
 // One cached gossipsub batch (a gsx_propagate call) of an mcache window:
-// node v has message k iff bit k % 64 of seen[(k / 64) * n_nodes + v].
+// node v has message k iff bit k % 64 of seen[v * n_words + k / 64].
 struct GossipBatch {
     const uint64_t* seen;
     uint32_t n_words;

@@ -74,6 +74,7 @@ struct gsx_engine {
     uint64_t E = 0, rs = 0, n_tiles = 0;
     int64_t last_refresh = 0;  // now of the last refreshScores() pass
     std::vector<int64_t> row_ptr;
+    std::vector<int32_t> col_host;
     std::vector<uint32_t> pair_obs;
     std::vector<uint32_t> ipg_host;  // 2 per pair, without WL bits
     std::vector<uint32_t> group_ip;  // IP id of each (observer, IP) group
@@ -119,18 +120,42 @@ struct gsx_engine {
     uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
 
-    // propagation buffers (grown on demand) and the last call's shape
+    // propagation buffers (grown on demand) and the current / last call's shape
     struct {
         uint64_t *seen = nullptr, *front = nullptr, *nxt = nullptr, *origin = nullptr, *from = nullptr,
                  *sel = nullptr;
-        uint8_t *hop = nullptr, *fwd = nullptr;
-        uint32_t* dup = nullptr;
+        uint8_t *hop = nullptr, *fwd = nullptr, *fwd_in = nullptr;
+        uint32_t *dup = nullptr, *first = nullptr;  // pending P2/P3 credit counts per pair
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
         uint32_t words_cap = 0, msgs_cap = 0;
         gsx::PropState last{};
         bool have_last = false;
+        // the call in flight (gsx_prop_begin .. gsx_prop_end)
+        bool active = false, sel_done = false;
+        uint32_t h = 0;
+        uint64_t *cur = nullptr, *nxtp = nullptr;
+        gsx_prop_config cfg{};
+        std::vector<uint64_t> ids;
+        // pending (deferred) credits: topic they belong to
+        bool credit_pending = false;
+        uint32_t credit_topic = 0;
+        // per-hop kernel timing
+        std::vector<hipEvent_t> ev;
+        uint32_t ev_used = 0;
     } prop;
+
+    // range sharding (gsx_load_overlay_shard / gsx_shard_*_plan)
+    uint32_t n_total = 0, node_lo = 0;
+    uint32_t n_ranks = 1;
+    std::vector<uint32_t> rank_lo;
+    std::vector<uint64_t> recv_counts, send_counts;
+    uint64_t n_recv = 0, n_send = 0;
+    uint32_t* d_send_pair = nullptr;
+    uint32_t* d_pair_obs = nullptr;
+    std::vector<uint32_t> rev_host;
+    bool sharded() const { return n_ranks > 1 || node_lo != 0 || n_total != n_nodes; }
+    hipStream_t own_stream = nullptr;
 
     // events
     std::vector<gsx_event> pending;
@@ -265,11 +290,20 @@ void free_state(gsx_engine* e) {
     if (e->d_rev) (void)hipFree(e->d_rev);
     e->d_row_ptr = nullptr;
     e->d_rev = nullptr;
-    void* pp[] = {e->prop.seen, e->prop.front, e->prop.nxt, e->prop.origin, e->prop.from, e->prop.sel,
-                  e->prop.hop,  e->prop.fwd,   e->prop.dup, e->prop.msgs,   e->prop.stats};
+    void* pp[] = {e->prop.seen, e->prop.front, e->prop.nxt,   e->prop.origin, e->prop.from,
+                  e->prop.sel,  e->prop.hop,   e->prop.fwd,   e->prop.fwd_in, e->prop.dup,
+                  e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs};
     for (void* p : pp)
         if (p) (void)hipFree(p);
+    std::vector<hipEvent_t> evs = std::move(e->prop.ev);
     e->prop = {};
+    e->prop.ev = std::move(evs);
+    e->d_send_pair = e->d_pair_obs = nullptr;
+    e->n_ranks = 1;
+    e->rank_lo.clear();
+    e->recv_counts.clear();
+    e->send_counts.clear();
+    e->n_recv = e->n_send = 0;
     e->d_col = nullptr;
     void* hb[] = {e->d_backoff, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
@@ -554,6 +588,7 @@ int gsx_create(const gsx_config* cfg, gsx_engine** out) {
         gsx_destroy(e);
         return GSX_EDEVICE;
     }
+    e->own_stream = e->stream;
     if (upload_topic_params(e) != GSX_OK) {
         gsx_destroy(e);
         return GSX_EDEVICE;
@@ -574,8 +609,17 @@ int gsx_destroy(gsx_engine* e) {
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-    if (e->stream) (void)hipStreamDestroy(e->stream);
+    for (hipEvent_t ev : e->prop.ev) (void)hipEventDestroy(ev);
+    if (!e->own_stream) e->own_stream = e->stream;  // gsx_create failed before recording it
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
+    return GSX_OK;
+}
+
+int gsx_set_stream(gsx_engine* e, void* stream) {
+    if (!e) return GSX_EINVAL;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->stream = stream ? static_cast<hipStream_t>(stream) : e->own_stream;
     return GSX_OK;
 }
 
@@ -619,15 +663,21 @@ int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_pa
     return GSX_OK;
 }
 
-int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
-                     const uint8_t* edge_flags, const uint32_t* node_ips) {
+namespace {
+// gsx_load_overlay and gsx_load_overlay_shard: rows for nodes
+// node_lo .. node_lo + n_nodes - 1 of an n_total-node overlay; col holds
+// global ids, node_ips covers all n_total nodes.
+int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_nodes, const int64_t* row_ptr,
+                 const int32_t* col, const uint8_t* edge_flags, const uint32_t* node_ips) {
     if (!e || !row_ptr || (!col && row_ptr[n_nodes] > 0)) return GSX_EINVAL;
+    if ((uint64_t)node_lo + n_nodes > n_total) return fail(e, GSX_EINVAL, "shard range outside the overlay");
     if (row_ptr[0] != 0) return fail(e, GSX_EINVAL, "row_ptr[0] must be 0");
     for (uint32_t i = 0; i < n_nodes; ++i)
         if (row_ptr[i + 1] < row_ptr[i]) return fail(e, GSX_EINVAL, "row_ptr not monotone");
     const uint64_t E = (uint64_t)row_ptr[n_nodes];
+    if (E >= gsx::HALO) return fail(e, GSX_EINVAL, "too many pairs for one engine (2^31)");
     for (uint64_t p = 0; p < E; ++p)
-        if (col[p] < 0 || (uint32_t)col[p] >= n_nodes) return fail(e, GSX_EINVAL, "col out of range");
+        if (col[p] < 0 || (uint32_t)col[p] >= n_total) return fail(e, GSX_EINVAL, "col out of range");
     // each observer tracks a peer once, rows ascending: the order first
     // deliverers are chosen in (lowest sender first)
     for (uint32_t i = 0; i < n_nodes; ++i)
@@ -641,11 +691,14 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     e->recs.clear();
     e->rec_queue.clear();
     e->n_nodes = n_nodes;
+    e->n_total = n_total;
+    e->node_lo = node_lo;
     e->E = E;
     e->rs = (E + 63) & ~uint64_t(63);
     e->n_tiles = (E + gsx::TILE - 1) / gsx::TILE;
     e->last_refresh = 0;
     e->row_ptr.assign(row_ptr, row_ptr + n_nodes + 1);
+    e->col_host.assign(col, col + E);
     e->pair_obs.resize(E);
     for (uint32_t i = 0; i < n_nodes; ++i)
         for (int64_t p = row_ptr[i]; p < row_ptr[i + 1]; ++p) e->pair_obs[(size_t)p] = i;
@@ -716,21 +769,26 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     for (uint32_t i = 0; i < n_nodes; ++i) e->max_deg = std::max<int64_t>(e->max_deg, row_ptr[i + 1] - row_ptr[i]);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (E) HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * E, hipMemcpyHostToDevice));
-    {  // reverse pairs for the pull-based propagation
-        std::vector<uint32_t> rev(E, gsx::NO_PAIR);
+    {  // reverse pairs for the pull-based propagation (NO_PAIR for remote neighbours until a shard plan)
+        std::vector<uint32_t>& rev = e->rev_host;
+        rev.assign(E, gsx::NO_PAIR);
         for (uint32_t u = 0; u < n_nodes; ++u)
             for (int64_t q = row_ptr[u]; q < row_ptr[u + 1]; ++q) {
-                const uint32_t v = (uint32_t)col[q];
+                const uint32_t vg = (uint32_t)col[q];
+                if (vg < node_lo || vg - node_lo >= n_nodes) continue;
+                const uint32_t v = vg - node_lo;
                 const int32_t* b = col + row_ptr[v];
                 const int32_t* en = col + row_ptr[v + 1];
-                const int32_t* it = std::lower_bound(b, en, (int32_t)u);
-                if (it != en && *it == (int32_t)u) rev[(size_t)q] = (uint32_t)(it - col);
+                const int32_t* it = std::lower_bound(b, en, (int32_t)(u + node_lo));
+                if (it != en && *it == (int32_t)(u + node_lo)) rev[(size_t)q] = (uint32_t)(it - col);
             }
-        if ((rc = dalloc(e, &e->d_rev, E)) || (rc = dalloc(e, &e->d_row_ptr, (size_t)n_nodes + 1))) {
+        if ((rc = dalloc(e, &e->d_rev, E)) || (rc = dalloc(e, &e->d_row_ptr, (size_t)n_nodes + 1)) ||
+            (rc = dalloc(e, &e->d_pair_obs, E))) {
             free_state(e);
             return rc;
         }
         if (E) HIPCHK(e, hipMemcpy(e->d_rev, rev.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice));
+        if (E) HIPCHK(e, hipMemcpy(e->d_pair_obs, e->pair_obs.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice));
         HIPCHK(e, hipMemcpy(e->d_row_ptr, row_ptr, sizeof(int64_t) * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
         e->eflags_host.assign(edge_flags ? edge_flags : nullptr, edge_flags ? edge_flags + E : nullptr);
     }
@@ -740,6 +798,92 @@ int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, co
     if (rc) return rc;
     e->loaded = true;
     e->scores_valid = false;
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_load_overlay(gsx_engine* e, uint32_t n_nodes, const int64_t* row_ptr, const int32_t* col,
+                     const uint8_t* edge_flags, const uint32_t* node_ips) {
+    return load_overlay(e, n_nodes, 0, n_nodes, row_ptr, col, edge_flags, node_ips);
+}
+
+int gsx_load_overlay_shard(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_local,
+                           const int64_t* row_ptr, const int32_t* col, const uint8_t* edge_flags,
+                           const uint32_t* node_ips) {
+    return load_overlay(e, n_total, node_lo, n_local, row_ptr, col, edge_flags, node_ips);
+}
+
+// Receive side of the shard plan: every pair (u -> v) whose v lives on rank
+// S != this one gets a receive slot; slots run rank by rank, pairs ascending.
+int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo, uint64_t* recv_counts,
+                        uint32_t* recv_u, uint32_t* recv_v) {
+    if (!e || !rank_lo || !recv_counts || n_ranks == 0) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (rank_lo[0] != 0 || rank_lo[n_ranks] != e->n_total) return fail(e, GSX_EINVAL, "rank ranges must cover the overlay");
+    bool mine = false;
+    for (uint32_t k = 0; k < n_ranks; ++k) {
+        if (rank_lo[k + 1] < rank_lo[k]) return fail(e, GSX_EINVAL, "rank ranges not monotone");
+        if (rank_lo[k] == e->node_lo && rank_lo[k + 1] - rank_lo[k] == e->n_nodes) mine = true;
+    }
+    if (!mine) return fail(e, GSX_EINVAL, "no rank owns exactly this engine's nodes");
+    auto owner = [&](uint32_t v) {
+        return (uint32_t)(std::upper_bound(rank_lo, rank_lo + n_ranks + 1, v) - rank_lo) - 1;
+    };
+    const uint32_t self_lo = e->node_lo, self_n = e->n_nodes;
+    std::vector<uint64_t> cnt(n_ranks, 0);
+    std::vector<uint32_t> own(e->E, 0);
+    for (uint64_t q = 0; q < e->E; ++q) {
+        const uint32_t v = (uint32_t)e->col_host[q];
+        if (v >= self_lo && v - self_lo < self_n) continue;
+        own[q] = owner(v);
+        ++cnt[own[q]];
+    }
+    std::vector<uint64_t> base(n_ranks + 1, 0);
+    for (uint32_t k = 0; k < n_ranks; ++k) base[k + 1] = base[k] + cnt[k];
+    std::vector<uint64_t> fill(base.begin(), base.end() - 1);
+    for (uint64_t q = 0; q < e->E; ++q) {
+        const uint32_t v = (uint32_t)e->col_host[q];
+        if (v >= self_lo && v - self_lo < self_n) continue;
+        const uint64_t slot = fill[own[q]]++;
+        e->rev_host[q] = gsx::HALO | (uint32_t)slot;
+        if (recv_u) recv_u[slot] = e->pair_obs[q] + self_lo;
+        if (recv_v) recv_v[slot] = v;
+    }
+    for (uint32_t k = 0; k < n_ranks; ++k) recv_counts[k] = cnt[k];
+    e->n_ranks = n_ranks;
+    e->rank_lo.assign(rank_lo, rank_lo + n_ranks + 1);
+    e->recv_counts = cnt;
+    e->n_recv = base[n_ranks];
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->E) HIPCHK(e, hipMemcpy(e->d_rev, e->rev_host.data(), sizeof(uint32_t) * e->E, hipMemcpyHostToDevice));
+    return GSX_OK;
+}
+
+// Send side: the concatenated (per rank, in rank order) receive lists of the
+// other ranks; entry (u, v) asks this rank what its node v sends to u.
+int gsx_shard_send_plan(gsx_engine* e, const uint64_t* send_counts, const uint32_t* req_u, const uint32_t* req_v) {
+    if (!e || !send_counts) return GSX_EINVAL;
+    if (!e->loaded || e->rank_lo.empty()) return fail(e, GSX_ESTATE, "gsx_shard_recv_plan first");
+    uint64_t n = 0;
+    for (uint32_t k = 0; k < e->n_ranks; ++k) n += send_counts[k];
+    if (n && (!req_u || !req_v)) return GSX_EINVAL;
+    std::vector<uint32_t> sp(n, gsx::NO_PAIR);
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint32_t u = req_u[j], v = req_v[j];
+        if (v < e->node_lo || v - e->node_lo >= e->n_nodes) return fail(e, GSX_EINVAL, "request for a node this rank does not own");
+        const uint32_t lv = v - e->node_lo;
+        const int32_t* b = e->col_host.data() + e->row_ptr[lv];
+        const int32_t* en = e->col_host.data() + e->row_ptr[lv + 1];
+        const int32_t* it = std::lower_bound(b, en, (int32_t)u);
+        if (it != en && *it == (int32_t)u) sp[j] = (uint32_t)(it - e->col_host.data());
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_send_pair) (void)hipFree(e->d_send_pair);
+    e->d_send_pair = nullptr;
+    if (int rc = dalloc(e, &e->d_send_pair, n)) return rc;
+    if (n) HIPCHK(e, hipMemcpy(e->d_send_pair, sp.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    e->send_counts.assign(send_counts, send_counts + e->n_ranks);
+    e->n_send = n;
     return GSX_OK;
 }
 
@@ -1082,56 +1226,54 @@ int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
 }
 
 // Message propagation, see gsx.h and gsx_propagate.hip.
-int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out) {
-    if (!e || !cfg || !out || (m && !msgs)) return GSX_EINVAL;
-    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
-    if (cfg->max_hops > GSX_MAX_HOPS || cfg->router > GSX_ROUTER_RANDOMSUB || m > 0xFFFFFFFFull)
-        return fail(e, GSX_EINVAL, "bad propagation config");
-    for (size_t k = 0; k < m; ++k)
-        if (msgs[k].source >= e->n_nodes) return fail(e, GSX_ERANGE, "message source out of range");
-    std::memset(out, 0, sizeof(*out));
-    if (int rc = ensure_scores(e)) return rc;  // publishThreshold tests read current scores
-    const uint32_t W = (uint32_t)((m + 63) / 64);
-    const size_t N = e->n_nodes, E = e->E;
+namespace {
+
+// Words per call: 1, 2, or a multiple of 4 (the hop kernel's register chunk).
+uint32_t prop_words(size_t m) {
+    const uint32_t w = (uint32_t)((m + 63) / 64);
+    if (w <= 2) return std::max<uint32_t>(w, 1);
+    return (w + 3) & ~3u;
+}
+
+int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
-    if (W > P.words_cap || m > P.msgs_cap || !P.fwd) {
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        void* pp[] = {P.seen, P.front, P.nxt, P.origin, P.from, P.sel, P.hop, P.fwd, P.dup, P.msgs, P.stats};
-        for (void* p : pp)
-            if (p) (void)hipFree(p);
-        P = {};
-        const size_t w = std::max<uint32_t>(W, 1), mm = std::max<size_t>(m, 1);
-        int rc = 0;
-        if ((rc = dalloc(e, &P.seen, w * N)) || (rc = dalloc(e, &P.front, w * N)) || (rc = dalloc(e, &P.nxt, w * N)) ||
-            (rc = dalloc(e, &P.origin, w * N)) || (rc = dalloc(e, &P.from, w * E)) || (rc = dalloc(e, &P.hop, mm * N)) ||
-            (rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.dup, E)) || (rc = dalloc(e, &P.msgs, mm)) ||
-            (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
-            return rc;
-        P.words_cap = (uint32_t)w;
-        P.msgs_cap = (uint32_t)mm;
-    }
-    const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
-    if (rsub && !P.sel) {
-        if (int rc = dalloc(e, &P.sel, (size_t)P.words_cap * E)) return rc;
-    }
+    void* pp[] = {P.seen, P.front, P.nxt, P.origin, P.from, P.sel, P.hop, P.msgs, P.stats};
+    for (void* p : pp)
+        if (p) (void)hipFree(p);
+    P.seen = P.front = P.nxt = P.origin = P.from = P.sel = nullptr;
+    P.hop = nullptr;
+    P.msgs = nullptr;
+    P.stats = nullptr;
+    P.words_cap = P.msgs_cap = 0;
+    return GSX_OK;
+}
+
+gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_config* cfg) {
+    auto& P = e->prop;
     gsx::PropState ps{};
     ps.row_ptr = e->d_row_ptr;
     ps.col = e->d_col;
     ps.rev = e->d_rev;
+    ps.pair_obs = e->d_pair_obs;
     ps.eflags = e->d_eflags;
     ps.fwd = P.fwd;
+    ps.fwd_in = P.fwd_in;
     ps.msgs = P.msgs;
     ps.seen = P.seen;
     ps.origin = P.origin;
     ps.from_mask = P.from;
-    ps.sel = rsub ? P.sel : nullptr;
+    ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
     ps.hop = P.hop;
     ps.dupcnt = P.dup;
+    ps.firstcnt = P.first;
     ps.stats = P.stats;
-    ps.n_pairs = E;
-    ps.n_nodes = (uint32_t)N;
+    ps.send_pair = e->d_send_pair;
+    ps.n_send = e->n_send;
+    ps.n_pairs = e->E;
+    ps.n_nodes = e->n_nodes;
     ps.n_words = W;
     ps.n_msgs = (uint32_t)m;
+    ps.node_lo = e->node_lo;
     ps.router = cfg->router;
     ps.topic = cfg->topic;
     ps.flood_publish = cfg->flood_publish;
@@ -1143,10 +1285,75 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
     ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
     ps.publish_threshold = e->th.publish_threshold;
     ps.seed = cfg->seed;
-    e->prop.last = ps;
-    e->prop.have_last = true;
+    ps.sharded = e->sharded() ? 1 : 0;
+    return ps;
+}
+
+int prop_event_pair(gsx_engine* e, hipEvent_t* a, hipEvent_t* b) {
+    auto& P = e->prop;
+    while (P.ev.size() < (size_t)P.ev_used + 2) {
+        hipEvent_t ev;
+        HIPCHK(e, hipEventCreate(&ev));
+        P.ev.push_back(ev);
+    }
+    *a = P.ev[P.ev_used++];
+    *b = P.ev[P.ev_used++];
+    return GSX_OK;
+}
+
+int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
+    if (!e || !cfg || (m && !msgs)) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (cfg->max_hops > GSX_MAX_HOPS || cfg->router > GSX_ROUTER_RANDOMSUB || m > 0xFFFFFFFFull ||
+        cfg->credit_scores > GSX_CREDIT_DEFER)
+        return fail(e, GSX_EINVAL, "bad propagation config");
+    for (size_t k = 0; k < m; ++k)
+        if (msgs[k].source >= e->n_total) return fail(e, GSX_ERANGE, "message source out of range");
+    auto& P = e->prop;
+    const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
+    if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)
+        return fail(e, GSX_ESTATE, "deferred credits of another topic are pending: gsx_prop_fold_credits first");
+    if (int rc = ensure_scores(e)) return rc;  // publishThreshold tests read current scores
+    const uint32_t W = prop_words(m);
+    const size_t N = e->n_nodes, E = e->E;
+    if (W > P.words_cap || m > P.msgs_cap || !P.fwd) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        prop_free_buffers(e);
+        const size_t mm = std::max<size_t>(m, 1);
+        int rc = 0;
+        if ((rc = dalloc(e, &P.seen, W * N)) || (rc = dalloc(e, &P.front, W * N)) || (rc = dalloc(e, &P.nxt, W * N)) ||
+            (rc = dalloc(e, &P.origin, W * N)) || (rc = dalloc(e, &P.from, W * E)) ||
+            (rc = dalloc(e, &P.hop, (size_t)W * 64 * N)) || (rc = dalloc(e, &P.msgs, mm)) ||
+            (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
+            return rc;
+        if (!P.fwd) {
+            if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.fwd_in, E)) || (rc = dalloc(e, &P.dup, E)) ||
+                (rc = dalloc(e, &P.first, E)))
+                return rc;
+            HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
+            HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * std::max<size_t>(E, 1), e->stream));
+        }
+        P.words_cap = W;
+        P.msgs_cap = (uint32_t)mm;
+    }
+    const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
+    if (rsub && !P.sel) {
+        if (int rc = dalloc(e, &P.sel, (size_t)P.words_cap * E)) return rc;
+    }
+    gsx::PropState ps = prop_state(e, W, m, cfg);
+    P.last = ps;
+    P.have_last = true;
+    P.cfg = *cfg;
+    P.h = 0;
+    P.cur = P.front;
+    P.nxtp = P.nxt;
+    P.sel_done = false;
+    P.ev_used = 0;
+    P.ids.resize(m);
+    for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
+    P.active = true;
+    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
     if (m == 0) return GSX_OK;
-    // per-call state
     std::vector<gsx::DevMsg> hm(m);
     for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
     HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
@@ -1154,32 +1361,70 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
     HIPCHK(e, hipMemsetAsync(P.front, 0, 8 * (size_t)W * N, e->stream));
     HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
     HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.hop, 0xFF, m * N, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.hop, 0xFF, (size_t)W * 64 * N, e->stream));
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
     HIPCHK(e, gsx::launch_prop_init(ps, P.front, e->stream));
-    uint64_t* cur = P.front;
-    uint64_t* nxt = P.nxt;
-    for (uint32_t h = 1; h <= cfg->max_hops; ++h) {
-        HIPCHK(e, gsx::launch_prop_hop(ps, h, cur, nxt, e->stream));
-        std::swap(cur, nxt);
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // `hm` is on the host stack
+    return GSX_OK;
+}
+
+// Runs hop h = ++P.h; halo = the received rows of remote senders (sharded).
+int prop_hop(gsx_engine* e, const uint64_t* halo) {
+    auto& P = e->prop;
+    gsx::PropState ps = P.last;
+    if (ps.n_msgs == 0) {
+        ++P.h;
+        return GSX_OK;
     }
+    ps.halo = halo;
+    const uint32_t h = ++P.h;
+    hipEvent_t a, b;
+    if (int rc = prop_event_pair(e, &a, &b)) return rc;
+    HIPCHK(e, hipEventRecord(a, e->stream));
+    if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, P.cur, e->stream));
+    P.sel_done = false;
+    HIPCHK(e, gsx::launch_prop_hop(ps, h, P.cur, P.nxtp, e->stream));
+    HIPCHK(e, hipEventRecord(b, e->stream));
+    std::swap(P.cur, P.nxtp);
+    return GSX_OK;
+}
+
+int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
+    auto& P = e->prop;
+    HIPCHK(e, gsx::launch_prop_fold(ps, dev_state(e), P.first, P.dup, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * e->E, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * e->E, e->stream));
+    P.credit_pending = false;
+    e->scores_valid = false;
+    return GSX_OK;
+}
+
+int prop_end(gsx_engine* e, gsx_prop_out* out) {
+    auto& P = e->prop;
+    const gsx::PropState& ps = P.last;
+    std::memset(out, 0, sizeof(*out));
+    P.active = false;
+    if (ps.n_msgs == 0) return GSX_OK;
     if (ps.credit) {
-        HIPCHK(e, gsx::launch_prop_credit(ps, ds, e->stream));
-        e->scores_valid = false;
+        HIPCHK(e, gsx::launch_prop_count(ps, e->stream));
+        P.credit_pending = true;
+        P.credit_topic = ps.topic;
+        if (P.cfg.credit_scores != GSX_CREDIT_DEFER) {
+            if (int rc = prop_fold(e, ps)) return rc;
+        }
     }
-    if (cfg->router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
+    const uint32_t W = ps.n_words;
+    const size_t N = e->n_nodes;
+    if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
         gsx_engine::McBatch b;
-        b.topic = cfg->topic;
-        b.n_msgs = (uint32_t)m;
+        b.topic = P.cfg.topic;
+        b.n_msgs = ps.n_msgs;
         b.n_words = W;
         if (int rc = dalloc(e, &b.d_seen, (size_t)W * N)) return rc;
         HIPCHK(e, hipMemcpyAsync(b.d_seen, P.seen, 8 * (size_t)W * N, hipMemcpyDeviceToDevice, e->stream));
-        b.ids.resize(m);
-        for (size_t k = 0; k < m; ++k) b.ids[k] = msgs[k].msg_id;
+        b.ids = P.ids;
         if (e->mc.empty()) e->mc.emplace_back();
         e->mc.front().push_back(std::move(b));
     }
@@ -1193,6 +1438,108 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
         if (st[gsx::STAT_HOP0 + h]) out->hops = h;
     }
     out->transmissions = out->deliveries + out->duplicates;
+    out->edge_sends = st[gsx::STAT_EDGE_SENDS];
+    out->new_words = st[gsx::STAT_NEW_WORDS];
+    double ms = 0;
+    for (uint32_t i = 0; i + 1 < P.ev_used; i += 2) {
+        float t = 0;
+        HIPCHK(e, hipEventElapsedTime(&t, P.ev[i], P.ev[i + 1]));
+        ms += t;
+    }
+    out->hop_kernel_ms = ms;
+    out->hop_launches = P.ev_used / 2;
+    return GSX_OK;
+}
+
+}  // namespace
+
+int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out) {
+    if (!e || !cfg || !out) return GSX_EINVAL;
+    if (e->loaded && e->sharded())
+        return fail(e, GSX_ESTATE, "sharded engine: drive hops with gsx_prop_begin/pack/step/end");
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (int rc = prop_begin(e, msgs, m, cfg)) return rc;
+    for (uint32_t h = 1; h <= cfg->max_hops; ++h)
+        if (int rc = prop_hop(e, nullptr)) return rc;
+    return prop_end(e, out);
+}
+
+int gsx_prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
+    if (!e) return GSX_EINVAL;
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (e->loaded && e->sharded() && (e->n_ranks > 1) && !e->d_send_pair)
+        return fail(e, GSX_ESTATE, "shard plan incomplete: gsx_shard_send_plan first");
+    if (e->loaded && e->sharded() && e->n_ranks == 1 && e->n_total != e->n_nodes)
+        return fail(e, GSX_ESTATE, "shard plan missing: gsx_shard_recv_plan / gsx_shard_send_plan first");
+    return prop_begin(e, msgs, m, cfg);
+}
+
+int gsx_prop_pack(gsx_engine* e, uint64_t* send) {
+    if (!e) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (e->n_send && !send) return GSX_EINVAL;
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    const gsx::PropState& ps = P.last;
+    if (ps.n_msgs == 0 || e->n_send == 0) return GSX_OK;
+    hipEvent_t a, b;
+    if (int rc = prop_event_pair(e, &a, &b)) return rc;
+    HIPCHK(e, hipEventRecord(a, e->stream));
+    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, P.cur, e->stream));
+    P.sel_done = true;
+    HIPCHK(e, gsx::launch_prop_pack(ps, P.cur, send, e->stream));
+    HIPCHK(e, hipEventRecord(b, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new) {
+    if (!e) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (e->n_recv && !recv) return GSX_EINVAL;
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    if (int rc = prop_hop(e, recv)) return rc;
+    if (n_new) {
+        unsigned long long c = 0;
+        if (P.last.n_msgs)
+            HIPCHK(e, hipMemcpyAsync(&c, P.stats + gsx::STAT_HOP0 + P.h, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        *n_new = c;
+    }
+    return GSX_OK;
+}
+
+int gsx_prop_end(gsx_engine* e, gsx_prop_out* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (!e->prop.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    return prop_end(e, out);
+}
+
+int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded || !e->prop.first) return fail(e, GSX_ESTATE, "no propagation yet");
+    if (first) HIPCHK(e, hipMemcpyAsync(first, e->prop.first, 4 * e->E, hipMemcpyDefault, e->stream));
+    if (dup) HIPCHK(e, hipMemcpyAsync(dup, e->prop.dup, 4 * e->E, hipMemcpyDefault, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* dup) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded || !e->prop.first) return fail(e, GSX_ESTATE, "no propagation yet");
+    if ((first == nullptr) != (dup == nullptr)) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (P.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (first) {
+        HIPCHK(e, hipMemcpyAsync(P.first, first, 4 * e->E, hipMemcpyDefault, e->stream));
+        HIPCHK(e, hipMemcpyAsync(P.dup, dup, 4 * e->E, hipMemcpyDefault, e->stream));
+    } else if (!P.credit_pending) {
+        return GSX_OK;
+    }
+    gsx::PropState ps = P.last;
+    ps.topic = P.credit_pending ? P.credit_topic : P.cfg.topic;
+    if (int rc = prop_fold(e, ps)) return rc;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
 
@@ -1202,7 +1549,14 @@ int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
     const gsx::PropState& ps = e->prop.last;
     const size_t cells = (size_t)ps.n_msgs * ps.n_nodes;
     if (cells == 0) return GSX_OK;
-    if (hop) HIPCHK(e, hipMemcpyAsync(hop, ps.hop, cells, hipMemcpyDeviceToHost, e->stream));
+    if (hop) {
+        uint8_t* d_h = nullptr;
+        if (int rc = dalloc(e, &d_h, cells)) return rc;
+        HIPCHK(e, gsx::launch_prop_hops_export(ps, d_h, e->stream));
+        HIPCHK(e, hipMemcpyAsync(hop, d_h, cells, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(d_h);
+    }
     if (first_from) {
         int32_t* d_ff = nullptr;
         if (int rc = dalloc(e, &d_ff, cells)) return rc;
@@ -1213,6 +1567,13 @@ int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
         (void)hipFree(d_ff);
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_shard_counts(gsx_engine* e, uint64_t* n_send, uint64_t* n_recv) {
+    if (!e) return GSX_EINVAL;
+    if (n_send) *n_send = e->n_send;
+    if (n_recv) *n_recv = e->n_recv;
     return GSX_OK;
 }
 
@@ -1256,6 +1617,8 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
     if (!e || !out) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->sharded())  // GRAFT/PRUNE to remote owners needs the control exchange
+        return fail(e, GSX_ESTATE, "heartbeat on a range shard is not supported");
     if (e->max_deg > gsx::HB_MAX_DEG)
         return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_MAX_DEG) + " peers per node");
     std::memset(out, 0, sizeof(*out));
@@ -1420,8 +1783,9 @@ int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_wind
         for (const auto& b : e->mc[w]) {
             if (topic != GSX_ANY_TOPIC && b.topic != topic) continue;
             words.resize(b.n_words);
-            for (uint32_t k = 0; k < b.n_words; ++k)  // column `node` of the [word][node] bitset
-                HIPCHK(e, hipMemcpy(&words[k], b.d_seen + (size_t)k * e->n_nodes + node, 8, hipMemcpyDeviceToHost));
+            // row `node` of the [node][word] bitset
+            HIPCHK(e, hipMemcpy(words.data(), b.d_seen + (size_t)node * b.n_words, 8 * (size_t)b.n_words,
+                                hipMemcpyDeviceToHost));
             for (uint32_t k = 0; k < b.n_msgs; ++k)
                 if (words[k / 64] >> (k % 64) & 1) {
                     if (n < cap) out[n] = b.ids[k];

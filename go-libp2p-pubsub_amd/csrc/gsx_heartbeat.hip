@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
         for (uint32_t b = 0; b < n_gb; ++b) {
             const GossipBatch B = gb[b];
             for (uint32_t w = 0; w < B.n_words; ++w) {
-                uint64_t word = B.seen[(size_t)w * h.n_nodes + v];
+                uint64_t word = B.seen[(size_t)v * B.n_words + w];
                 L += (uint32_t)__popcll(word);
                 while (word) {
                     dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
             const GossipBatch B = gb[b];
             for (uint32_t w0 = 0; w0 < B.n_words; w0 += 64) {
                 const uint32_t w = w0 + lane;
-                uint64_t word = w < B.n_words ? B.seen[(size_t)w * h.n_nodes + v] : 0;
+                uint64_t word = w < B.n_words ? B.seen[(size_t)v * B.n_words + w] : 0;
                 const uint32_t c = (uint32_t)__popcll(word);
                 uint32_t pos = L + wave_prefix(c, lane);
                 while (word) {

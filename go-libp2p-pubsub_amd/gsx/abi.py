@@ -202,6 +202,9 @@ GSX_ROUTER_FLOODSUB = 0
 GSX_ROUTER_GOSSIPSUB = 1
 GSX_ROUTER_RANDOMSUB = 2
 GSX_MAX_HOPS = 64
+GSX_CREDIT_OFF = 0
+GSX_CREDIT_NOW = 1
+GSX_CREDIT_DEFER = 2
 GSX_ANY_TOPIC = 0xFFFFFFFF
 
 
@@ -225,8 +228,11 @@ class PropOut(C.Structure):
         ("duplicates", C.c_uint64),
         ("transmissions", C.c_uint64),
         ("hops", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("hop_launches", C.c_uint32),
         ("hop_deliveries", C.c_uint64 * (GSX_MAX_HOPS + 1)),
+        ("edge_sends", C.c_uint64),
+        ("new_words", C.c_uint64),
+        ("hop_kernel_ms", C.c_double),
     ]
 
     def as_dict(self):
@@ -331,6 +337,20 @@ SIGNATURES = {
     "gsx_synthesize_state": (C.c_int, [C.c_void_p, P(SynthSpec)]),
     "gsx_propagate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), P(PropOut)]),
     "gsx_prop_results": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_int32)]),
+    "gsx_prop_pending_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_prop_fold_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_load_overlay_shard": (
+        C.c_int,
+        [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint8), P(C.c_uint32)],
+    ),
+    "gsx_shard_recv_plan": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32), _u64p, P(C.c_uint32), P(C.c_uint32)]),
+    "gsx_shard_send_plan": (C.c_int, [C.c_void_p, _u64p, P(C.c_uint32), P(C.c_uint32)]),
+    "gsx_shard_counts": (C.c_int, [C.c_void_p, _u64p, _u64p]),
+    "gsx_prop_begin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig)]),
+    "gsx_prop_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_step": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),
+    "gsx_prop_end": (C.c_int, [C.c_void_p, P(PropOut)]),
     "gsx_default_gossipsub_params": (C.c_int, [P(GossipSubParams)]),
     "gsx_set_gossipsub_params": (C.c_int, [C.c_void_p, P(GossipSubParams)]),
     "gsx_heartbeat": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64, P(HeartbeatOut)]),

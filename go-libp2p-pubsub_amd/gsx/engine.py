@@ -176,6 +176,94 @@ class Engine:
             self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
         return out, hop, frm
 
+    # -- stepped / sharded propagation (gsx.h "range sharding") --------------------------
+    def load_overlay_shard(self, n_total, node_lo, row_ptr, col, edge_flags=None, node_ips=None):
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        n = len(row_ptr) - 1
+        ef = None if edge_flags is None else np.ascontiguousarray(edge_flags, dtype=np.uint8)
+        ips = None if node_ips is None else np.ascontiguousarray(node_ips, dtype=np.uint32).reshape(-1)
+        self._chk(
+            self.lib.gsx_load_overlay_shard(self.h, n_total, node_lo, n, _ptr(row_ptr, C.c_int64),
+                                            _ptr(col, C.c_int32), _ptr(ef, C.c_uint8), _ptr(ips, C.c_uint32)),
+            "gsx_load_overlay_shard",
+        )
+        v = C.c_uint64()
+        self._chk(self.lib.gsx_num_pairs(self.h, C.byref(v)), "gsx_num_pairs")
+        self.n_pairs = int(v.value)
+        self.n_nodes = n
+        self.node_lo = node_lo
+        self.n_total = n_total
+
+    def shard_recv_plan(self, rank_lo):
+        """-> (recv_counts [world] u64, recv_u, recv_v): this rank's receive list."""
+        rl = np.ascontiguousarray(rank_lo, dtype=np.uint32)
+        w = len(rl) - 1
+        cnt = np.zeros(w, dtype=np.uint64)
+        self._chk(self.lib.gsx_shard_recv_plan(self.h, w, _ptr(rl, C.c_uint32), _ptr(cnt, C.c_uint64), None, None),
+                  "gsx_shard_recv_plan")
+        n = int(cnt.sum())
+        ru = np.empty(n, dtype=np.uint32)
+        rv = np.empty(n, dtype=np.uint32)
+        self._chk(self.lib.gsx_shard_recv_plan(self.h, w, _ptr(rl, C.c_uint32), _ptr(cnt, C.c_uint64),
+                                               _ptr(ru, C.c_uint32), _ptr(rv, C.c_uint32)), "gsx_shard_recv_plan")
+        return cnt, ru, rv
+
+    def shard_send_plan(self, send_counts, req_u, req_v):
+        sc = np.ascontiguousarray(send_counts, dtype=np.uint64)
+        u = np.ascontiguousarray(req_u, dtype=np.uint32)
+        v = np.ascontiguousarray(req_v, dtype=np.uint32)
+        self._chk(self.lib.gsx_shard_send_plan(self.h, _ptr(sc, C.c_uint64), _ptr(u, C.c_uint32),
+                                               _ptr(v, C.c_uint32)), "gsx_shard_send_plan")
+
+    def shard_counts(self):
+        a, b = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.gsx_shard_counts(self.h, C.byref(a), C.byref(b)), "gsx_shard_counts")
+        return int(a.value), int(b.value)
+
+    def set_stream(self, stream_handle: int):
+        """Order the engine's work on a HIP stream (e.g. torch.cuda.current_stream().cuda_stream); 0 = own."""
+        self._chk(self.lib.gsx_set_stream(self.h, C.c_void_p(stream_handle or None)), "gsx_set_stream")
+
+    def prop_begin(self, msgs, cfg: abi.PropConfig):
+        ms = np.ascontiguousarray(msgs, dtype=abi.msg_dtype())
+        self._chk(self.lib.gsx_prop_begin(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg)),
+                  "gsx_prop_begin")
+        self._prop_msgs = len(ms)
+
+    def prop_pack(self, send):
+        """send: device buffer (torch tensor or pointer) of [n_send][words] u64 rows."""
+        p = send.data_ptr() if hasattr(send, "data_ptr") else send
+        self._chk(self.lib.gsx_prop_pack(self.h, C.c_void_p(p or None)), "gsx_prop_pack")
+
+    def prop_step(self, recv) -> int:
+        """recv: device buffer (torch tensor or pointer) of the received rows; -> this hop's first receipts."""
+        p = recv.data_ptr() if hasattr(recv, "data_ptr") else recv
+        n = C.c_uint64()
+        self._chk(self.lib.gsx_prop_step(self.h, C.c_void_p(p or None), C.byref(n)), "gsx_prop_step")
+        return int(n.value)
+
+    def prop_end(self) -> abi.PropOut:
+        out = abi.PropOut()
+        self._chk(self.lib.gsx_prop_end(self.h, C.byref(out)), "gsx_prop_end")
+        return out
+
+    def prop_results(self, n_msgs: int):
+        """-> (hop [m, n_local] u8, first_from [m, n_local] i32) of the last propagation."""
+        hop = np.empty((n_msgs, self.n_nodes), dtype=np.uint8)
+        frm = np.empty((n_msgs, self.n_nodes), dtype=np.int32)
+        self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
+        return hop, frm
+
+    def pending_credits(self, first_ptr: int, dup_ptr: int):
+        """Copy the pending (GSX_CREDIT_DEFER) counts to caller memory (host or device pointers)."""
+        self._chk(self.lib.gsx_prop_pending_credits(self.h, C.c_void_p(first_ptr or None), C.c_void_p(dup_ptr or None)),
+                  "gsx_prop_pending_credits")
+
+    def fold_credits(self, first_ptr: int = 0, dup_ptr: int = 0):
+        self._chk(self.lib.gsx_prop_fold_credits(self.h, C.c_void_p(first_ptr or None), C.c_void_p(dup_ptr or None)),
+                  "gsx_prop_fold_credits")
+
     # -- heartbeat (gossipsub.go:1303-1604) ----------------------------------------------
     def set_gossipsub_params(self, gp: abi.GossipSubParams):
         self._chk(self.lib.gsx_set_gossipsub_params(self.h, C.byref(gp)), "gsx_set_gossipsub_params")

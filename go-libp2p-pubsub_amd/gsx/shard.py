@@ -1,0 +1,283 @@
+"""Multi-GPU propagation drivers, one process per GPU.
+
+Two ways to spread GossipSub forwarding (floodsub.go:76-100,
+gossipsub.go:943-1013, randomsub.go:99-160) over ranks:
+
+* ``RangeSharded`` — the overlay is range-partitioned by node; every rank's
+  engine holds its nodes' rows (gsx_load_overlay_shard).  Per hop each rank
+  packs what its nodes send across shards (gsx_prop_pack), one all-to-all
+  moves the packed rows (RCCL over xGMI on MI355X: torch.distributed "nccl"),
+  and the hop kernel reads them in place of the local gather
+  (gsx_prop_step).  The loop ends when a hop delivers nothing on any rank.
+  Per-rank results are the single-engine rows of the rank's nodes, bit for bit.
+
+* ``MessageParallel`` — every rank holds the whole overlay and propagates
+  its share of the messages (messages are independent given the call's
+  forwarding state); the deferred P2/P3 credit counts are summed with one
+  all-reduce and folded on every rank, which equals folding them on one engine.
+
+The exchange goes through a tiny transport interface so the same drivers run
+over torch.distributed (any backend) or in-process between several engines
+on one device (``LocalGroup``, tests).  Nothing here computes propagation: the
+engine's HIP kernels do.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+
+_STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words")
+
+
+def prop_words(m: int) -> int:
+    """Words per call (gsx.h): 1, 2, or ceil(m/64) rounded up to a multiple of 4."""
+    w = (m + 63) // 64
+    if w <= 2:
+        return max(w, 1)
+    return (w + 3) & ~3
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class DistTransport:
+    """torch.distributed transport (RCCL for "nccl", gloo on CPU)."""
+
+    def __init__(self, device, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def all_to_all(self, recv, send, recv_splits, send_splits):
+        self.dist.all_to_all_single(recv, send, list(map(int, recv_splits)), list(map(int, send_splits)),
+                                    group=self.group)
+
+    def all_reduce_sum(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+
+    def all_reduce_max(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+
+
+def exchange_plan(backend, rank_lo, transport) -> None:
+    """Build the per-hop exchange: this rank's receive list goes to the owners
+    of the remote neighbours, which resolve it to their local pairs."""
+    torch = _torch()
+    counts, ru, rv = backend.shard_recv_plan(rank_lo)
+    W = transport.world
+    dev = transport.device
+    send_cnt = torch.tensor(counts.astype(np.int64), dtype=torch.int64, device=dev)  # what I ask of rank k
+    recv_cnt = torch.empty(W, dtype=torch.int64, device=dev)
+    transport.all_to_all(recv_cnt, send_cnt, [1] * W, [1] * W)
+    asked = recv_cnt.cpu().numpy()  # how many rows rank k asks of me
+    req = torch.tensor(np.stack([ru, rv], 1).astype(np.int64).reshape(-1, 2), dtype=torch.int64, device=dev)
+    got = torch.empty((int(asked.sum()), 2), dtype=torch.int64, device=dev)
+    transport.all_to_all(got, req, asked, counts)
+    g = got.cpu().numpy()
+    backend.shard_send_plan(asked.astype(np.uint64), g[:, 0].astype(np.uint32), g[:, 1].astype(np.uint32))
+    backend._plan_counts = (asked.astype(np.int64), counts.astype(np.int64))
+
+
+class RangeSharded:
+    """Range-sharded propagation over one engine per rank."""
+
+    def __init__(self, backend, rank_lo, transport):
+        self.be = backend
+        self.rank_lo = np.asarray(rank_lo, dtype=np.uint32)
+        self.tp = transport
+        exchange_plan(backend, self.rank_lo, transport)
+        self.send_counts, self.recv_counts = backend._plan_counts  # rows I send to / receive from rank k
+        self.n_send = int(self.send_counts.sum())
+        self.n_recv = int(self.recv_counts.sum())
+        self._bufs = {}
+        dev = getattr(transport, "device", None)
+        if hasattr(backend, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
+            # engine kernels and the collectives on one stream: pack -> all-to-all -> step in order
+            backend.set_stream(_torch().cuda.current_stream(dev).cuda_stream)
+
+    def _buffers(self, W):
+        torch = _torch()
+        if W not in self._bufs:
+            dev = self.tp.device
+            self._bufs = {W: (torch.zeros((max(self.n_send, 1), W), dtype=torch.int64, device=dev),
+                              torch.zeros((max(self.n_recv, 1), W), dtype=torch.int64, device=dev))}
+        return self._bufs[W]
+
+    def propagate(self, msgs, cfg: abi.PropConfig):
+        """-> (this rank's PropOut as a dict, global totals dict)."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        W = prop_words(len(msgs))
+        send, recv = self._buffers(W)
+        be.prop_begin(msgs, cfg)
+        flag = torch.zeros(1, dtype=torch.int64, device=tp.device)
+        for _ in range(cfg.max_hops):
+            be.prop_pack(send)
+            tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
+            n_new = be.prop_step(recv)
+            flag.fill_(n_new)
+            tp.all_reduce_sum(flag)
+            if int(flag.item()) == 0:
+                break
+        out = be.prop_end()
+        return out_dict(out), totals(out, tp)
+
+
+class MessageParallel:
+    """Every rank propagates its block of the messages over the full overlay."""
+
+    def __init__(self, engine, transport):
+        self.e = engine
+        self.tp = transport
+
+    def share(self, msgs):
+        m = len(msgs)
+        r, w = self.tp.rank, self.tp.world
+        return msgs[(m * r) // w : (m * (r + 1)) // w]
+
+    def propagate(self, msgs, cfg: abi.PropConfig):
+        torch = _torch()
+        mine = self.share(msgs)
+        credit = cfg.credit_scores
+        c = abi.PropConfig()
+        C_fields = [f for f, _ in abi.PropConfig._fields_]
+        for f in C_fields:
+            setattr(c, f, getattr(cfg, f))
+        if credit:
+            c.credit_scores = abi.GSX_CREDIT_DEFER
+        out = self.e.propagate(mine, c)[0]
+        if credit:
+            E = self.e.n_pairs
+            cnt = torch.empty((2, max(E, 1)), dtype=torch.int32, device=self.tp.device)
+            if cnt.is_cuda:
+                torch.cuda.synchronize(cnt.device)
+            self.e.pending_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
+            self.tp.all_reduce_sum(cnt)
+            if cnt.is_cuda:
+                torch.cuda.synchronize(cnt.device)
+            self.e.fold_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
+        return out_dict(out), totals(out, self.tp)
+
+
+def out_dict(out) -> dict:
+    d = out.as_dict()
+    d.update(edge_sends=int(out.edge_sends), new_words=int(out.new_words), hop_kernel_ms=float(out.hop_kernel_ms),
+             hop_launches=int(out.hop_launches))
+    return d
+
+
+def totals(out, tp) -> dict:
+    """Sums over ranks (max for hops and kernel time)."""
+    torch = _torch()
+    v = [int(getattr(out, k)) for k in _STAT_KEYS] + [int(x) for x in out.hop_deliveries]
+    t = torch.tensor(v, dtype=torch.int64, device=tp.device)
+    tp.all_reduce_sum(t)
+    mx = torch.tensor([int(out.hops), int(round(out.hop_kernel_ms * 1e6))], dtype=torch.int64, device=tp.device)
+    tp.all_reduce_max(mx)
+    t = t.cpu().numpy()
+    mx = mx.cpu().numpy()
+    d = {k: int(t[i]) for i, k in enumerate(_STAT_KEYS)}
+    d["hops"] = int(mx[0])
+    d["hop_deliveries"] = [int(x) for x in t[len(_STAT_KEYS) :][: d["hops"] + 1]]
+    d["hop_kernel_ms_max"] = float(mx[1]) / 1e6
+    return d
+
+
+# ---- in-process transport: several engines (shards) in one process ------------------
+class LocalGroup:
+    """Lock-step in-process stand-in for a process group over `world` members
+    (used to run every shard of a test overlay on one GPU).  Member k calls the
+    collectives through LocalTransport(group, k); a collective completes when
+    all members have called it, which happens because the members run as
+    Python threads."""
+
+    def __init__(self, world: int, device):
+        import threading
+
+        self.world = world
+        self.device = device
+        self.barrier = threading.Barrier(world)
+        self.slots: List[Optional[object]] = [None] * world
+
+
+class LocalTransport:
+    def __init__(self, group: LocalGroup, rank: int):
+        self.g = group
+        self.rank = rank
+        self.world = group.world
+        self.device = group.device
+
+    def _gather(self, obj):
+        self.g.slots[self.rank] = obj
+        self.g.barrier.wait()
+        vals = list(self.g.slots)
+        self.g.barrier.wait()
+        return vals
+
+    def all_to_all(self, recv, send, recv_splits, send_splits):
+        torch = _torch()
+        if send.is_cuda:
+            torch.cuda.synchronize(send.device)
+        so = np.concatenate([[0], np.cumsum(np.asarray(send_splits, dtype=np.int64))])
+        vals = self._gather((send, so))
+        parts = [vals[k][0][vals[k][1][self.rank] : vals[k][1][self.rank + 1]] for k in range(self.world)]
+        if parts:
+            recv.copy_(torch.cat(parts, 0).reshape(recv.shape))
+        if recv.is_cuda:
+            torch.cuda.synchronize(recv.device)
+        self._gather(None)  # senders may reuse their buffers only after everyone copied
+
+    def all_reduce_sum(self, t):
+        vals = self._gather(t.clone())
+        acc = vals[0].clone()
+        for v in vals[1:]:
+            acc += v
+        t.copy_(acc)
+        self._gather(None)
+
+    def all_reduce_max(self, t):
+        vals = self._gather(t.clone())
+        acc = vals[0].clone()
+        for v in vals[1:]:
+            acc = acc.maximum(v)
+        t.copy_(acc)
+        self._gather(None)
+
+
+def run_local(world: int, device, fn: "callable", args: Sequence) -> list:
+    """Run fn(transport, *args[k]) for k in range(world) as lock-step threads."""
+    import threading
+
+    torch = _torch()  # import and initialise the device runtime on the calling (main) thread
+    if torch.device(device).type == "cuda":
+        torch.cuda.init()
+        torch.zeros(1, device=device)
+    g = LocalGroup(world, device)
+    res: List[object] = [None] * world
+    err: List[BaseException] = []
+
+    def body(k):
+        try:
+            res[k] = fn(LocalTransport(g, k), *args[k])
+        except BaseException as ex:  # surface the first failure, release the others
+            err.append(ex)
+            g.barrier.abort()
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise err[0]
+    return res

@@ -67,43 +67,51 @@ class Overlay:
         return np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self.row_ptr))
 
 
-def connect_some_overlay(
-    n: int, d: int = 6, seed: int = SEED, sybil_frac: float = 0.0, sybils_per_ip: int = 50, flags: int = abi.GSX_EDGE_GOSSIPSUB
-) -> Overlay:
-    """connectSome-style random overlay (floodsub_test.go:73-87): node i dials d
+def _connect_some_keys(n: int, d: int, seed: int):
+    """Sorted undirected connection keys lo*n+hi and sorted dial keys
+    dialer*n+target of connectSome (floodsub_test.go:73-87): node i dials d
     targets h(seed, OVL, i, k) mod n, a self draw is redrawn once (then i+1);
-    duplicate connections collapse; both ends get a pair; the dialer's pair is
-    outbound."""
+    duplicate connections collapse."""
     i = np.repeat(np.arange(n, dtype=np.uint64), d)
     k = np.tile(np.arange(d, dtype=np.uint64), n)
     j = h(seed, TAG_OVL, i, k) % np.uint64(n)
+    del k
     self_ = j == i
     if self_.any():
-        j2 = h(seed, TAG_OVL_REDRAW, i[self_], k[self_]) % np.uint64(n)
+        j2 = h(seed, TAG_OVL_REDRAW, i[self_], np.nonzero(self_)[0].astype(np.uint64) % np.uint64(d)) % np.uint64(n)
         j2 = np.where(j2 == i[self_], (i[self_] + np.uint64(1)) % np.uint64(n), j2)
         j[self_] = j2
     i = i.astype(np.int64)
     j = j.astype(np.int64)
     dial_key = np.unique(i * n + j)  # (dialer, target)
-    lo = np.minimum(i, j)
-    hi = np.maximum(i, j)
-    und = np.unique(lo * n + hi)
+    und = np.unique(np.minimum(i, j) * n + np.maximum(i, j))
+    return und, dial_key
+
+
+def _rows(n, und, dial_key, lo, hi, flags):
+    """CSR rows lo..hi-1 (col = global ids, ascending) of the undirected keys;
+    the dialer's pair is outbound."""
     a = und // n
     b = und % n
-    src = np.concatenate([a, b])
-    dst = np.concatenate([b, a])
-    order = np.lexsort((dst, src))
-    src = src[order]
-    dst = dst[order]
-    row_ptr = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(np.bincount(src, minlength=n), out=row_ptr[1:])
-    key = src * n + dst
+    m1 = (a >= lo) & (a < hi)
+    m2 = (b >= lo) & (b < hi)
+    key = np.concatenate([und[m1], b[m2] * n + a[m2]])
+    key.sort()
+    src = key // n
+    dst = key % n
+    row_ptr = np.zeros(hi - lo + 1, dtype=np.int64)
+    np.cumsum(np.bincount(src - lo, minlength=hi - lo), out=row_ptr[1:])
     pos = np.searchsorted(dial_key, key)
     pos = np.minimum(pos, len(dial_key) - 1)
     outbound = dial_key[pos] == key
-    ef = np.full(len(src), flags, dtype=np.uint8)
+    ef = np.full(len(key), flags, dtype=np.uint8)
     ef[outbound] |= abi.GSX_EDGE_OUTBOUND
-    # IPs: one unique IPv4 per honest node; sybils share one IP per group
+    return row_ptr, dst.astype(np.int32), ef
+
+
+def _ips(n, sybil_frac, sybils_per_ip):
+    """One unique IPv4 per honest node; the last sybil_frac*n nodes are
+    sybils sharing one IP per sybils_per_ip."""
     sybil = np.zeros(n, dtype=bool)
     n_syb = int(round(sybil_frac * n))
     if n_syb:
@@ -113,7 +121,63 @@ def connect_some_overlay(
     if n_syb:
         sid = np.arange(n_syb, dtype=np.int64) // sybils_per_ip
         ips[n - n_syb :, 0] = (n + sid).astype(np.uint32)
-    return Overlay(n, row_ptr, dst.astype(np.int32), ef, ips, sybil)
+    return ips, sybil
+
+
+def connect_some_overlay(
+    n: int, d: int = 6, seed: int = SEED, sybil_frac: float = 0.0, sybils_per_ip: int = 50, flags: int = abi.GSX_EDGE_GOSSIPSUB
+) -> Overlay:
+    """connectSome-style random overlay (floodsub_test.go:73-87): node i dials d
+    targets h(seed, OVL, i, k) mod n, a self draw is redrawn once (then i+1);
+    duplicate connections collapse; both ends get a pair; the dialer's pair is
+    outbound."""
+    und, dial_key = _connect_some_keys(n, d, seed)
+    row_ptr, col, ef = _rows(n, und, dial_key, 0, n, flags)
+    ips, sybil = _ips(n, sybil_frac, sybils_per_ip)
+    return Overlay(n, row_ptr, col, ef, ips, sybil)
+
+
+@dataclass
+class OverlayShard:
+    """Rows node_lo .. node_hi-1 of an n-node overlay (col = global ids)."""
+    n: int
+    node_lo: int
+    node_hi: int
+    row_ptr: np.ndarray
+    col: np.ndarray
+    edge_flags: np.ndarray
+    node_ips: np.ndarray  # all n nodes
+    sybil: np.ndarray  # all n nodes
+
+    @property
+    def n_pairs(self) -> int:
+        return int(self.row_ptr[-1])
+
+
+def shard_ranges(n: int, world: int) -> np.ndarray:
+    """Balanced contiguous node ranges: rank k owns rank_lo[k] .. rank_lo[k+1]-1."""
+    return np.array([(n * k) // world for k in range(world + 1)], dtype=np.uint32)
+
+
+def connect_some_shards(n: int, rank_lo, d: int = 6, seed: int = SEED, sybil_frac: float = 0.0,
+                        sybils_per_ip: int = 50, flags: int = abi.GSX_EDGE_GOSSIPSUB, ranks=None):
+    """The shards (for `ranks`, default all) of connect_some_overlay(n, ...):
+    the connection draw is global, each shard keeps its rows."""
+    und, dial_key = _connect_some_keys(n, d, seed)
+    ips, sybil = _ips(n, sybil_frac, sybils_per_ip)
+    out = []
+    for k in range(len(rank_lo) - 1) if ranks is None else ranks:
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        row_ptr, col, ef = _rows(n, und, dial_key, lo, hi, flags)
+        out.append(OverlayShard(n, lo, hi, row_ptr, col, ef, ips, sybil))
+    return out
+
+
+def shard_of(ov: Overlay, lo: int, hi: int) -> OverlayShard:
+    """Rows lo..hi-1 of an existing overlay."""
+    a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+    return OverlayShard(ov.n, lo, hi, ov.row_ptr[lo : hi + 1] - a, ov.col[a:b].copy(), ov.edge_flags[a:b].copy(),
+                        ov.node_ips, ov.sybil)
 
 
 def spam_test_topic_params() -> abi.TopicScoreParams:

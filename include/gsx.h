@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSX_ABI_VERSION 1
+#define GSX_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define GSX_OK 0
@@ -354,7 +354,7 @@ typedef struct gsx_prop_config {
     uint32_t max_hops;        /* hop bound, <= GSX_MAX_HOPS                        */
     int64_t hop_latency_ns;   /* simulated time per hop                           */
     int64_t now_ns;           /* publish time                                      */
-    uint32_t credit_scores;   /* fold deliveries into P2/P3 counters               */
+    uint32_t credit_scores;   /* GSX_CREDIT_*: fold deliveries into P2/P3 counters */
     uint32_t randomsub_size;  /* RandomSub's `size` (randomsub.go:21-27)           */
     uint64_t seed;            /* RandomSub draws: h(seed, 7, vertex, msg_id<<16|k) */
 } gsx_prop_config;
@@ -372,16 +372,81 @@ typedef struct gsx_prop_out {
     uint64_t duplicates;     /* receipts of an already seen message             */
     uint64_t transmissions;  /* sends: deliveries + duplicates                  */
     uint32_t hops;           /* last hop with a first receipt                   */
-    uint32_t reserved;
+    uint32_t hop_launches;   /* hop (and pack) launches timed in hop_kernel_ms  */
     uint64_t hop_deliveries[GSX_MAX_HOPS + 1]; /* first receipts per hop       */
+    /* Push-minimal traffic terms of SURVEY.md §8d, summed over hops and
+     * 64-message words: (pair, word) with a non-empty eligible send, and
+     * (vertex, word) gaining new bits. */
+    uint64_t edge_sends;
+    uint64_t new_words;
+    double hop_kernel_ms;    /* device time of the hop / pack kernels (HIP events) */
 } gsx_prop_out;
+
+/* credit_scores values */
+#define GSX_CREDIT_OFF 0u
+#define GSX_CREDIT_NOW 1u   /* fold this call's credits at its end              */
+#define GSX_CREDIT_DEFER 2u /* add them to the pending counts (gsx_prop_fold_credits) */
 
 /* Propagates m messages (any m; processed in 64-message words). */
 int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out);
-/* Per (node, message) results of the last gsx_propagate: arrival hop
- * (0xFF = never; 0 at the source) and first deliverer node (-1 = none), laid
- * out [message][node].  Either pointer may be NULL. */
+/* Per (node, message) results of the last propagation: arrival hop
+ * (0xFF = never; 0 at the source) and first deliverer node (global id, -1 =
+ * none), laid out [message][node] over this engine's nodes.  Either pointer
+ * may be NULL. */
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from);
+
+/* Pending P2/P3 credit counts per pair (first receipts, in-window duplicates)
+ * accumulated by GSX_CREDIT_DEFER calls.  Pointers may be host or device
+ * memory (n_pairs u32 each; NULL skips).  Message-parallel replicas sum
+ * them across ranks (RCCL all-reduce) and fold the sums: folding the sum of
+ * counts is exactly folding every message's steps (they are all "+1 then
+ * cap"). */
+int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup);
+/* Folds credit counts into fmd / mmd of the pending topic (score.go:912-974)
+ * and clears them.  first/dup (both or neither, host or device memory)
+ * replace the pending counts before folding. */
+int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* dup);
+
+/* Orders the engine's work on a caller's HIP stream (hipStream_t; NULL = the
+ * engine's own), e.g. torch's current stream, so that its kernels and the
+ * caller's RCCL collectives on the same device are stream-ordered. */
+int gsx_set_stream(gsx_engine* e, void* stream);
+
+/* ---- range sharding ------------------------------------------ */
+/* One engine per rank owns nodes node_lo .. node_lo + n_local - 1 of an
+ * n_total-node overlay: row_ptr has n_local + 1 entries, col holds GLOBAL
+ * node ids, node_ips covers all n_total nodes.  Scoring needs nothing else
+ * (every pair belongs to its observer's rank).  Propagation exchanges, per
+ * hop, what each cross-shard pair (v -> u) sends:
+ *   gsx_shard_recv_plan  -> this rank's receive list (u local, v remote),
+ *                           grouped by v's rank, pairs ascending; the host
+ *                           sends list k to rank k;
+ *   gsx_shard_send_plan  <- the lists the other ranks sent here, concatenated
+ *                           in rank order;
+ *   gsx_prop_begin, then per hop gsx_prop_pack (send rows, [n_send][words])
+ *   -> all-to-all (send counts per rank x words u64) -> gsx_prop_step (the
+ *   received rows) until a hop delivers nothing on any rank, gsx_prop_end.
+ * Words per call: 1 for m <= 64, 2 for m <= 128, else ceil(m/64) rounded up
+ * to a multiple of 4.  Per-rank results equal the single-engine run's rows
+ * of those nodes bit for bit.  Heartbeats are not supported on a shard. */
+int gsx_load_overlay_shard(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_local,
+                           const int64_t* row_ptr, const int32_t* col, const uint8_t* edge_flags,
+                           const uint32_t* node_ips);
+/* rank_lo[n_ranks + 1]: rank k owns rank_lo[k] .. rank_lo[k+1]-1.  Writes
+ * recv_counts[n_ranks] and, if non-NULL, the (u, v) global ids per slot. */
+int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo, uint64_t* recv_counts,
+                        uint32_t* recv_u, uint32_t* recv_v);
+int gsx_shard_send_plan(gsx_engine* e, const uint64_t* send_counts, const uint32_t* req_u, const uint32_t* req_v);
+int gsx_shard_counts(gsx_engine* e, uint64_t* n_send, uint64_t* n_recv);
+
+/* Stepped propagation (any engine; required on a shard).  gsx_propagate is
+ * begin + max_hops steps + end.  send / recv are device pointers (rows of
+ * the call's word count); gsx_prop_step returns the hop's first receipts on
+ * this rank in *n_new (NULL: no host sync). */
+int gsx_prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg);
+int gsx_prop_pack(gsx_engine* e, uint64_t* send);
+int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new);
+int gsx_prop_end(gsx_engine* e, gsx_prop_out* out);
 
 /* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
 

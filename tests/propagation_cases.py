@@ -64,13 +64,14 @@ def setup(be, ov, T, seed, mesh_degree=6, disconnect_frac=0.0, score_spread=True
         be.apply_events(np.array(back, dtype=abi.event_dtype()))
     if score_spread:
         app = np.where(rng.random(E) < 0.08, -500.0, rng.normal(0, 2, E))
-        be.set_app_scores(app)
     else:
-        be.set_app_scores(np.zeros(E))
+        app = np.zeros(E)
+    be.set_app_scores(app)
     if disconnect_frac > 0:
         rm = np.nonzero(rng.random(E) < disconnect_frac)[0]
         be.apply_events(np.array([(abi.EV_REMOVE_PEER, 0, int(q), T0 + S, 0) for q in rm], dtype=abi.event_dtype()))
     be.refresh(T0 + 2 * S)
+    return app
 
 
 def messages(n_nodes, m, seed):

@@ -1,0 +1,197 @@
+"""CPU stand-in for one range shard of the engine's stepped propagation
+(gsx.h "range sharding": gsx_shard_recv_plan / send_plan, gsx_prop_begin /
+pack / step / end), TEST INFRASTRUCTURE ONLY.
+
+It restates the split of a hop into the sender-side pack (eligibility, the
+`from` exclusion) and the receiver-side merge (origin exclusion, lowest
+sender first) in plain Python over numpy words, so that the multi-process
+driver (gsx/shard.py) can be run over gloo on CPU and its stitched result
+compared with the global oracle (oracle/gsx_oracle.c: orc_propagate).  The
+GPU tests run the same driver over the HIP engine.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from gsx import abi
+from gsx.shard import prop_words
+
+M64 = (1 << 64) - 1
+FWD, PUB = 1, 2
+
+
+def fwd_bytes(router, state, scores, edge_flags, topic, n_topics, publish_threshold, flood_publish):
+    """fwd[r] of every pair (v -> u) (gsx_propagate.hip k_prop_fwd) from an exported state."""
+    E = len(edge_flags)
+    pf = state["pair_flags"]
+    inn = (pf & (abi.GSX_PAIR_PRESENT | abi.GSX_PAIR_CONNECTED)) == (abi.GSX_PAIR_PRESENT | abi.GSX_PAIR_CONNECTED)
+    out = np.zeros(E, dtype=np.uint8)
+    if router == abi.GSX_ROUTER_FLOODSUB:
+        out[inn] = FWD | PUB
+        return out
+    assert router == abi.GSX_ROUTER_GOSSIPSUB
+    direct = (edge_flags & abi.GSX_EDGE_DIRECT) != 0
+    above = scores >= publish_threshold
+    fwd = direct | (((edge_flags & abi.GSX_EDGE_GOSSIPSUB) == 0) & above)
+    mesh = (state["rec_flags"].reshape(n_topics, E)[topic] & abi.GSX_REC_IN_MESH) != 0
+    fwd = fwd | mesh
+    pub = (direct | above) if flood_publish else fwd
+    out = np.where(fwd, FWD, 0) | np.where(pub, PUB, 0)
+    return np.where(inn, out, 0).astype(np.uint8)
+
+
+def _elig(fw, own):
+    m = fw & 3
+    if m == 3:
+        return M64
+    if m == FWD:
+        return ~own & M64
+    if m == PUB:
+        return own
+    return 0
+
+
+class EmuShard:
+    def __init__(self, shard, fwd_local):
+        self.sh = shard
+        self.lo = shard.node_lo
+        self.n = shard.node_hi - shard.node_lo
+        self.row_ptr = shard.row_ptr
+        self.col = shard.col.astype(np.int64)
+        self.fwd = fwd_local
+        self.obs = np.repeat(np.arange(self.n), np.diff(self.row_ptr))
+        E = len(self.col)
+        self.rev = [None] * E  # ("local", r) | ("halo", slot) | None
+        for q in range(E):
+            v = int(self.col[q])
+            if self.lo <= v < self.lo + self.n:
+                lv = v - self.lo
+                row = self.col[self.row_ptr[lv] : self.row_ptr[lv + 1]]
+                i = np.searchsorted(row, self.obs[q] + self.lo)
+                if i < len(row) and row[i] == self.obs[q] + self.lo:
+                    self.rev[q] = ("local", int(self.row_ptr[lv] + i))
+
+    def _find(self, lv, u):
+        row = self.col[self.row_ptr[lv] : self.row_ptr[lv + 1]]
+        i = np.searchsorted(row, u)
+        return int(self.row_ptr[lv] + i) if i < len(row) and row[i] == u else None
+
+    # -- plan ---------------------------------------------------------------------
+    def shard_recv_plan(self, rank_lo):
+        rank_lo = np.asarray(rank_lo, dtype=np.int64)
+        world = len(rank_lo) - 1
+        owner = np.searchsorted(rank_lo, self.col, side="right") - 1
+        remote = (self.col < self.lo) | (self.col >= self.lo + self.n)
+        counts = np.zeros(world, dtype=np.uint64)
+        ru, rv = [], []
+        slot = 0
+        for k in range(world):
+            for q in np.nonzero(remote & (owner == k))[0]:
+                self.rev[q] = ("halo", slot)
+                ru.append(self.obs[q] + self.lo)
+                rv.append(self.col[q])
+                slot += 1
+            counts[k] = int((remote & (owner == k)).sum())
+        return counts, np.array(ru, dtype=np.uint32), np.array(rv, dtype=np.uint32)
+
+    def shard_send_plan(self, send_counts, req_u, req_v):
+        self.send_pair = [self._find(int(v) - self.lo, int(u)) for u, v in zip(req_u, req_v)]
+
+    # -- stepped propagation ----------------------------------------------------------
+    def prop_begin(self, msgs, cfg):
+        self.cfg = cfg
+        self.m = len(msgs)
+        self.W = prop_words(self.m)
+        n, E, W = self.n, len(self.col), self.W
+        self.seen = [[0] * W for _ in range(n)]
+        self.origin = [[0] * W for _ in range(n)]
+        self.front = [[0] * W for _ in range(n)]
+        self.frm = [[0] * W for _ in range(E)]
+        self.hop = np.full((n, W * 64), 0xFF, dtype=np.uint8)
+        self.h = 0
+        self.stats = dict(deliveries=0, duplicates=0, hop=[0] * (abi.GSX_MAX_HOPS + 1))
+        for k, s in enumerate(msgs["source"]):
+            s = int(s)
+            if self.lo <= s < self.lo + n:
+                u = s - self.lo
+                b = 1 << (k % 64)
+                self.origin[u][k // 64] |= b
+                self.seen[u][k // 64] |= b
+                self.front[u][k // 64] |= b
+                self.hop[u, k] = 0
+
+    def _send_row(self, r):
+        v = int(self.obs[r])
+        return [self.front[v][w] & _elig(int(self.fwd[r]), self.origin[v][w]) & ~self.frm[r][w] & M64
+                for w in range(self.W)]
+
+    def prop_pack(self, send):
+        rows = [self._send_row(r) if r is not None else [0] * self.W for r in self.send_pair]
+        a = np.array(rows, dtype=np.uint64).reshape(-1, self.W) if rows else np.zeros((0, self.W), np.uint64)
+        send[: len(rows)].copy_(_as_tensor(a.view(np.int64)))
+
+    def prop_step(self, recv):
+        halo = recv.numpy().view(np.uint64) if len(recv) else None
+        self.h += 1
+        h, W = self.h, self.W
+        nxt = [[0] * W for _ in range(self.n)]
+        n_new = 0
+        for u in range(self.n):
+            for w in range(W):
+                seen, mine, acc = self.seen[u][w], self.origin[u][w], 0
+                for q in range(self.row_ptr[u], self.row_ptr[u + 1]):
+                    rv = self.rev[q]
+                    if rv is None:
+                        continue
+                    if rv[0] == "halo":
+                        c = int(halo[rv[1], w])
+                    else:
+                        c = self._send_row(rv[1])[w]
+                    c &= ~mine & M64
+                    if not c:
+                        continue
+                    newb = c & ~seen & ~acc & M64
+                    self.stats["duplicates"] += bin(c & acc).count("1") + bin(c & seen).count("1")
+                    acc |= newb
+                    self.frm[q][w] |= newb
+                nxt[u][w] = acc
+                if acc:
+                    self.seen[u][w] = seen | acc
+                    c = bin(acc).count("1")
+                    n_new += c
+                    for b in range(64):
+                        if acc >> b & 1:
+                            self.hop[u, w * 64 + b] = h
+        self.front = nxt
+        self.stats["hop"][h] = n_new
+        self.stats["deliveries"] += n_new
+        return n_new
+
+    def prop_end(self):
+        out = abi.PropOut()
+        out.deliveries = self.stats["deliveries"]
+        out.duplicates = self.stats["duplicates"]
+        out.transmissions = out.deliveries + out.duplicates
+        for h, c in enumerate(self.stats["hop"]):
+            out.hop_deliveries[h] = c
+            if c:
+                out.hops = h
+        return out
+
+    def prop_results(self, n_msgs):
+        hop = self.hop[:, :n_msgs].T.copy()
+        frm = np.full((n_msgs, self.n), -1, dtype=np.int32)
+        for u in range(self.n):
+            for q in range(self.row_ptr[u], self.row_ptr[u + 1]):
+                for w in range(self.W):
+                    bits = self.frm[q][w]
+                    for b in range(64):
+                        if bits >> b & 1 and w * 64 + b < n_msgs:
+                            frm[w * 64 + b, u] = self.col[q]
+        return hop, frm
+
+
+def _as_tensor(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a))

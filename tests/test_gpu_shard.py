@@ -1,0 +1,152 @@
+"""Multi-GPU propagation drivers (gsx/shard.py) on one GPU: several engines,
+one per shard (or replica), run as lock-step threads that exchange through
+device copies instead of RCCL.  Every per-node result, counter, credited
+score state and score must equal the single-engine run bit for bit (which
+test_gpu_propagation.py pins to the oracle)."""
+import numpy as np
+import pytest
+import torch  # noqa: F401  (imported on the main thread before the shard threads use it)
+
+import gsx
+import propagation_cases as pc
+from gsx import abi, shard, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(e, T):
+    e.set_peer_params(synth.bench_peer_params())
+    for t in range(T):
+        tp = synth.spam_test_topic_params()
+        tp.mesh_message_deliveries_window_ns = 25 * abi.MILLISECOND
+        e.set_topic_params(t, tp)
+    e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                    accept_px_threshold=0, opportunistic_graft_threshold=0))
+
+
+def _slice_state(st, T, E, a, b):
+    out = {}
+    for f in abi.STATE_FIELDS:
+        x = st[f]
+        out[f] = x.reshape(T, E)[:, a:b].reshape(-1).copy() if f in abi.RECORD_FIELDS else x[a:b].copy()
+    out["last_refresh_ns"] = st["last_refresh_ns"]
+    return out
+
+
+CASES = [
+    # world, n, d, T, router, flood_publish, m, mix, disconnect
+    (2, 1500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, 0.02),
+    (2, 2000, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, True, 0.03),
+    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 100, True, 0.0),
+    (4, 1600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 64, True, 0.02),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"w{c[0]}-r{c[4]}-m{c[6]}" for c in CASES])
+def test_range_sharded_matches_single_engine(gpu_ok, case):
+    world, n, d, T, router, fp, m, mix, disc = case
+    seed = 3 * n + m
+    ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
+    msgs = pc.messages(n, m, seed)
+    cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60)
+    full = gsx.Engine(T)
+    app = pc.setup(full, ov, T, seed, disconnect_frac=disc)
+    st0 = full.export_state()
+    out, hop, frm = full.propagate(msgs, cfg, want_results=True)
+    st1, sc1 = full.export_state(), full.scores()
+
+    rank_lo = synth.shard_ranges(n, world)
+    E = ov.n_pairs
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        e = gsx.Engine(T)
+        _params(e, T)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(_slice_state(st0, T, E, a, b))
+        e.set_app_scores(app[a:b])
+        engines.append((e, a, b))
+
+    def run(tp, e):
+        rs = shard.RangeSharded(e, rank_lo, tp)
+        return rs.propagate(msgs, cfg)
+
+    res = shard.run_local(world, "cuda:0", run, [(e,) for e, _, _ in engines])
+    tot = res[0][1]
+    want = out.as_dict()
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries"):
+        assert tot[k] == want[k], k
+    assert tot["edge_sends"] == out.edge_sends and tot["new_words"] == out.new_words
+    for k, (e, a, b) in enumerate(engines):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        h, f = e.prop_results(m)
+        assert np.array_equal(h, hop[:, lo:hi]), (k, np.argwhere(h != hop[:, lo:hi])[:5])
+        assert np.array_equal(f, frm[:, lo:hi]), (k, np.argwhere(f != frm[:, lo:hi])[:5])
+        st = e.export_state()
+        want_st = _slice_state(st1, T, E, a, b)
+        for fld in abi.STATE_FIELDS:
+            assert np.array_equal(st[fld].view(np.uint8), want_st[fld].view(np.uint8)), (k, fld)
+        assert np.array_equal(e.scores().view(np.uint64), sc1[a:b].view(np.uint64)), k
+    assert want["deliveries"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_message_parallel_matches_single_engine(gpu_ok, world):
+    n, d, T, m = 3000, 6, 1, 300
+    seed = 17 + world
+    ov = pc.overlay(n, d, seed, mix_protocols=True, direct_frac=0.02)
+    msgs = pc.messages(n, m, seed)
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=4)
+    full = gsx.Engine(T)
+    pc.setup(full, ov, T, seed, disconnect_frac=0.02)
+    out = full.propagate(msgs, cfg)[0]
+    st1, sc1 = full.export_state(), full.scores()
+    reps = []
+    for _ in range(world):
+        e = gsx.Engine(T)
+        pc.setup(e, ov, T, seed, disconnect_frac=0.02)
+        reps.append(e)
+
+    def run(tp, e):
+        return shard.MessageParallel(e, tp).propagate(msgs, cfg)
+
+    res = shard.run_local(world, "cuda:0", run, [(e,) for e in reps])
+    tot = res[0][1]
+    want = out.as_dict()
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries"):
+        assert tot[k] == want[k], k
+    for e in reps:
+        st = e.export_state()
+        for fld in abi.STATE_FIELDS:
+            assert np.array_equal(st[fld].view(np.uint8), st1[fld].view(np.uint8)), fld
+        assert np.array_equal(e.scores().view(np.uint64), sc1.view(np.uint64))
+
+
+def test_stepped_api_equals_propagate(gpu_ok):
+    """gsx_prop_begin + steps + end on an unsharded engine == gsx_propagate;
+    deferred credits folded later == credits folded at once."""
+    n, T, m = 2500, 1, 130
+    ov = pc.overlay(n, 5, 5, mix_protocols=True)
+    msgs = pc.messages(n, m, 5)
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=7)
+    a, b = gsx.Engine(T), gsx.Engine(T)
+    for e in (a, b):
+        pc.setup(e, ov, T, 5)
+    oa = a.propagate(msgs, cfg)[0]
+    cfg_d = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=7, credit=abi.GSX_CREDIT_DEFER)
+    b.prop_begin(msgs, cfg_d)
+    for _ in range(cfg_d.max_hops):
+        b.prop_step(0)
+    ob = b.prop_end()
+    assert oa.as_dict() == ob.as_dict()
+    first = np.zeros(ov.n_pairs, dtype=np.uint32)
+    dup = np.zeros(ov.n_pairs, dtype=np.uint32)
+    b.pending_credits(first.ctypes.data, dup.ctypes.data)
+    assert first.sum() == oa.deliveries
+    b.fold_credits()
+    assert np.array_equal(a.scores().view(np.uint64), b.scores().view(np.uint64))
+    ha, fa = a.prop_results(m)
+    hb, fb = b.prop_results(m)
+    assert np.array_equal(ha, hb) and np.array_equal(fa, fb)

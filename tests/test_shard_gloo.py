@@ -1,0 +1,153 @@
+"""Multi-process (world_size 2 and 3, gloo on CPU) runs of the multi-GPU
+propagation drivers of gsx/shard.py, checked against the global oracle.
+
+Range sharding: every rank holds one shard (tests/shard_emulator.py stands in
+for the engine on CPU); the exchange plan and the per-hop all-to-all go
+through torch.distributed exactly as on the GPUs (where the backend is RCCL).
+The ranks' stitched arrival hops, first deliverers and summed counters must
+equal orc_propagate's over the whole overlay.
+
+Message parallel: every rank propagates its block of the messages with the
+oracle standing in for the engine; the all-reduced totals must equal the
+single run's.
+"""
+import multiprocessing as mp
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as orc
+import propagation_cases as pc
+from gsx import abi, synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cfg_dict(cfg):
+    return {f: getattr(cfg, f) for f, _ in abi.PropConfig._fields_}
+
+
+def _worker(rank, world, port, payload, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gsx import shard as gs
+        from gsx.abi import PropConfig
+
+        cfg = PropConfig(**payload["cfg"])
+        tp = gs.DistTransport("cpu")
+        if payload["mode"] == "range":
+            import shard_emulator as emu
+
+            sh = payload["shards"][rank]
+            rp = payload["row_ptr"]
+            be = emu.EmuShard(sh, payload["fwd"][int(rp[sh.node_lo]) : int(rp[sh.node_hi])])
+            rs = gs.RangeSharded(be, payload["rank_lo"], tp)
+            local, tot = rs.propagate(payload["msgs"], cfg)
+            hop, frm = be.prop_results(len(payload["msgs"]))
+            q.put((rank, local, tot, hop, frm))
+        else:
+            o = orc.Oracle(1)
+            pc.setup(o, payload["ov"], 1, payload["seed"])
+            mpar = gs.MessageParallel(o, tp)
+            local, tot = mpar.propagate(payload["msgs"], cfg)
+            q.put((rank, local, tot, None, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as ex:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None, None))
+
+
+def _run(world, payload):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, payload, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=240)
+        assert r[1] != "error", r[2]
+        res[r[0]] = r
+    for p in ps:
+        p.join(60)
+    return [res[r] for r in range(world)]
+
+
+def _reference(ov, T, seed, msgs, cfg):
+    o = orc.Oracle(T)
+    pc.setup(o, ov, T, seed)
+    st = o.export_state()
+    scores = o.scores()
+    out, hop, frm = o.propagate(msgs, cfg, want_results=True)
+    return o, st, scores, out, hop, frm
+
+
+CASES = [
+    # world, n, d, router, flood_publish, m, mix
+    (2, 240, 3, abi.GSX_ROUTER_FLOODSUB, 0, 64, False),
+    (2, 200, 4, abi.GSX_ROUTER_GOSSIPSUB, 0, 100, True),
+    (3, 180, 3, abi.GSX_ROUTER_GOSSIPSUB, 1, 40, True),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"w{c[0]}-r{c[3]}-m{c[5]}" for c in CASES])
+def test_range_sharded_gloo_matches_oracle(case):
+    import shard_emulator as emu
+
+    world, n, d, router, fp, m, mix = case
+    seed = 7 * n + m
+    ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
+    msgs = pc.messages(n, m, seed)
+    cfg = pc.config(router, flood_publish=fp, credit=0, max_hops=30)
+    th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                        accept_px_threshold=0, opportunistic_graft_threshold=0)
+    o, st, scores, out, hop, frm = _reference(ov, 1, seed, msgs, cfg)
+    fwd = emu.fwd_bytes(router, st, scores, ov.edge_flags, 0, 1, th.publish_threshold, fp)
+    rank_lo = synth.shard_ranges(n, world)
+    shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
+    payload = dict(mode="range", shards=shards, fwd=fwd, row_ptr=ov.row_ptr, rank_lo=rank_lo, msgs=msgs,
+                   cfg=_cfg_dict(cfg))
+    res = _run(world, payload)
+    got_hop = np.concatenate([r[3] for r in res], axis=1)
+    got_frm = np.concatenate([r[4] for r in res], axis=1)
+    assert np.array_equal(got_hop, hop), np.argwhere(got_hop != hop)[:5]
+    assert np.array_equal(got_frm, frm), np.argwhere(got_frm != frm)[:5]
+    tot = res[0][2]
+    assert all(r[2] == tot for r in res)  # every rank holds the same totals
+    want = out.as_dict()
+    assert tot["deliveries"] == want["deliveries"] and tot["duplicates"] == want["duplicates"]
+    assert tot["hops"] == want["hops"] and tot["hop_deliveries"] == want["hop_deliveries"]
+    assert sum(r[1]["deliveries"] for r in res) == want["deliveries"]
+    assert want["deliveries"] > 0
+
+
+def test_message_parallel_gloo_totals():
+    world, n, m = 2, 300, 96
+    seed = 11
+    ov = pc.overlay(n, 4, seed)
+    msgs = pc.messages(n, m, seed)
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, credit=0)
+    _, _, _, out, _, _ = _reference(ov, 1, seed, msgs, cfg)
+    payload = dict(mode="replica", ov=ov, seed=seed, msgs=msgs, cfg=_cfg_dict(cfg))
+    res = _run(world, payload)
+    tot = res[0][2]
+    want = out.as_dict()
+    for k in ("deliveries", "duplicates", "transmissions", "hops"):
+        assert tot[k] == want[k], k
+    assert tot["hop_deliveries"] == want["hop_deliveries"]
