@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "go-libp2p-pubsub_amd"))
 
 import gsx  # noqa: E402
 from gsx import abi, synth  # noqa: E402
+from gsx import shard as shard_mod  # noqa: E402
 
 METRIC = "peer-topic score updates/s + msg deliveries/s @1M peers, 1-8 GPUs, %HBM BW"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -94,6 +95,173 @@ def cpu_baseline(e, T, now, passes):
     return o, st
 
 
+def prop_engine(n_total, lo, hi, d, seed, device, th, sharded):
+    """Engine for a propagation leg: T=1, spam-test params, synthesized state
+    (mesh ~ half of each node's peers), one refresh so publishThreshold tests
+    read real scores."""
+    t = time.time()
+    e = gsx.Engine(1, device=device)
+    e.set_peer_params(synth.bench_peer_params())
+    e.set_topic_params(0, synth.spam_test_topic_params())
+    e.set_thresholds(th)
+    if sharded:
+        rl = synth.shard_ranges(n_total, sharded[1])
+        sh = synth.connect_some_shards(n_total, rl, d=d, seed=seed, ranks=[sharded[0]])[0]
+        e.load_overlay_shard(n_total, sh.node_lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        n_pairs = sh.n_pairs
+    else:
+        ov = synth.connect_some_overlay(n_total, d=d, seed=seed)
+        e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+        n_pairs = ov.n_pairs
+        del ov
+    e.synthesize_state(
+        abi.SynthSpec(seed=seed, now_ns=T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0, imd_max_sybil=100.0,
+                      p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0, p_disconnected=0.0, p_absent=0.0,
+                      expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n_total))
+    e.set_app_scores(np.zeros(n_pairs))
+    e.refresh(T0 + abi.SECOND)
+    e.sync()
+    log(f"[bench] propagation engine nodes={hi - lo}/{n_total} pairs={n_pairs} in {time.time() - t:.1f}s")
+    return e
+
+
+def prop_messages(n, m, seed, first=0):
+    ms = np.zeros(m, dtype=abi.msg_dtype())
+    k = np.arange(first, first + m)
+    ms["source"] = (synth.h(seed, synth.TAG_SRC, k, 0) % np.uint64(n)).astype(np.uint32)
+    ms["msg_id"] = k.astype(np.uint64)
+    return ms
+
+
+def prop_config(args, n):
+    return abi.PropConfig(router=abi.GSX_ROUTER_GOSSIPSUB, topic=0, flood_publish=0, max_hops=args.prop_hops,
+                          hop_latency_ns=10 * abi.MILLISECOND, now_ns=T0 + 2 * abi.SECOND,
+                          credit_scores=abi.GSX_CREDIT_NOW, randomsub_size=n, seed=synth.SEED)
+
+
+def prop_roofline(tot, msgs, kernel_ms):
+    """SURVEY.md §8d push-minimal bytes: 8 per frontier (vertex, word), 12 per
+    eligible (edge, word) send, 16 per (vertex, word) gaining bits; the
+    frontier words are the sources' plus every gaining word."""
+    W = shard_mod.prop_words(len(msgs))
+    src_words = len(set((int(s), k // 64) for k, s in enumerate(msgs["source"])))
+    F = src_words + tot["new_words"]
+    B = 8 * F + 12 * tot["edge_sends"] + 16 * tot["new_words"]
+    ach = B / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    return {"bound": "hbm", "algorithmic_bytes_per_batch": B, "hop_kernel_ms_per_batch": kernel_ms,
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "words": W}
+
+
+def _max_over_ranks(x, dist, dev):
+    import torch
+
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def prop_replica(args, rank, world, local, dist, dev, th):
+    import torch
+
+    n = args.peers
+    e = prop_engine(n, 0, n, args.degree, synth.SEED, local, th, None)
+    cfg = prop_config(args, n)
+    M = args.prop_msgs * world
+    tp = shard_mod.DistTransport(dev) if dist is not None else None
+    runner = shard_mod.MessageParallel(e, tp) if tp is not None else None
+
+    def once(b):
+        msgs = prop_messages(n, M, synth.SEED, first=b * M)
+        if runner is not None:
+            return runner.propagate(msgs, cfg), msgs
+        out = e.propagate(msgs, cfg)[0]
+        d = shard_mod.out_dict(out)
+        d2 = dict(d)
+        d2["hop_kernel_ms_max"] = d["hop_kernel_ms"]
+        return (d, d2), msgs
+
+    once(0)  # warm-up
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    res = [once(1 + b) for b in range(args.prop_steps)]
+    torch.cuda.synchronize(dev)
+    el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
+    dl = sum(r[0][1]["deliveries"] for r in res)
+    (loc, tot), msgs = res[-1]
+    mine = prop_messages(n, M, synth.SEED, first=args.prop_steps * M)
+    mine = mine[(M * rank) // world : (M * (rank + 1)) // world]
+    e.close()
+    return {
+        "metric": "msg deliveries/s",
+        "mode": "message-parallel replicas (weak): full overlay per GPU, own messages, one all-reduce of credits",
+        "value": dl / el,
+        "peers": n,
+        "messages_per_batch_per_gpu": args.prop_msgs,
+        "ms_per_batch": el / args.prop_steps * 1e3,
+        "deliveries_per_batch": tot["deliveries"],
+        "duplicates_per_batch": tot["duplicates"],
+        "hops": tot["hops"],
+        "router": "gossipsub (synthesized mesh, ~6 of ~12 peers), P2/P3 credits on",
+        "roofline_rank0": prop_roofline(loc, mine, loc["hop_kernel_ms"]),
+    }
+
+
+def prop_sharded(args, rank, world, local, dist, dev, th):
+    import torch
+
+    n = args.prop_peers
+    rl = synth.shard_ranges(n, world)
+    e = prop_engine(n, int(rl[rank]), int(rl[rank + 1]), args.degree, synth.SEED + 1, local, th,
+                    (rank, world) if world > 1 else None)
+    cfg = prop_config(args, n)
+    M = args.prop_msgs
+    runner = None
+    if dist is not None:
+        runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev))
+
+    def once(b):
+        msgs = prop_messages(n, M, synth.SEED + 1, first=b * M)
+        if runner is not None:
+            return runner.propagate(msgs, cfg), msgs
+        out = e.propagate(msgs, cfg)[0]
+        d = shard_mod.out_dict(out)
+        d2 = dict(d)
+        d2["hop_kernel_ms_max"] = d["hop_kernel_ms"]
+        return (d, d2), msgs
+
+    once(0)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    res = [once(1 + b) for b in range(args.prop_steps)]
+    torch.cuda.synchronize(dev)
+    el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
+    dl = sum(r[0][1]["deliveries"] for r in res)
+    (loc, tot), msgs = res[-1]
+    e.close()
+    out = {
+        "metric": "msg deliveries/s",
+        "mode": f"range-sharded (strong): {n} peers over {world} GPU(s), per-hop all-to-all of packed cross-shard sends",
+        "value": dl / el,
+        "peers": n,
+        "messages_per_batch": M,
+        "ms_per_batch": el / args.prop_steps * 1e3,
+        "deliveries_per_batch": tot["deliveries"],
+        "duplicates_per_batch": tot["duplicates"],
+        "hops": tot["hops"],
+        "router": "gossipsub (synthesized mesh, ~6 of ~12 peers), P2/P3 credits on",
+        "hop_kernel_ms_max_rank": tot["hop_kernel_ms_max"],
+    }
+    if world == 1:
+        out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,6 +273,7 @@ def main():
     ap.add_argument("--cpu-passes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prop-msgs", type=int, default=256, help="messages per propagation batch (0: skip)")
+    ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
@@ -176,49 +345,24 @@ def main():
     # ---- secondary: message deliveries/s (gossipsub mesh forwarding, A13-A14) ----
     prop = None
     if args.prop_msgs > 0:
-        ms = np.zeros(args.prop_msgs, dtype=abi.msg_dtype())
-        ms["source"] = (synth.h(seed, synth.TAG_SRC, np.arange(args.prop_msgs), 0) % np.uint64(n)).astype(np.uint32)
-        ms["msg_id"] = np.arange(args.prop_msgs, dtype=np.uint64)
-        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
-                                        accept_px_threshold=0, opportunistic_graft_threshold=0))
-        pcfg = abi.PropConfig(router=abi.GSX_ROUTER_GOSSIPSUB, topic=0, flood_publish=0, max_hops=args.prop_hops,
-                              hop_latency_ns=10 * abi.MILLISECOND, now_ns=now, credit_scores=1,
-                              randomsub_size=n, seed=seed)
-        e.propagate(ms, pcfg)  # warm-up
-        e.sync()
-        barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        tot = None
-        for _ in range(args.prop_steps):
-            out = e.propagate(ms, pcfg)[0]
-            tot = out if tot is None else tot
-        e.sync()
-        torch.cuda.synchronize(dev)
-        pt = time.perf_counter() - t0
-        barrier()
-        dl = float(tot.deliveries) * args.prop_steps
-        if dist is not None:
-            t = torch.tensor([pt], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            pt = float(t.item())
-            r = torch.tensor([dl], dtype=torch.float64, device=dev)
-            dist.all_reduce(r, op=dist.ReduceOp.SUM)
-            dl = float(r.item())
-        prop = {
-            "metric": "msg deliveries/s",
-            "value": dl / pt,
-            "ms_per_batch": pt / args.prop_steps * 1e3,
-            "messages_per_batch": args.prop_msgs,
-            "deliveries_per_batch": int(tot.deliveries),
-            "duplicates_per_batch": int(tot.duplicates),
-            "hops": int(tot.hops),
-            "router": "gossipsub (synthesized mesh, ~6 of ~12 peers per topic), P2/P3 credits on",
-        }
+        prop = {}
+        th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                            accept_px_threshold=0, opportunistic_graft_threshold=0)
+        # (1) message-parallel replicas (weak): the 1M-peer overlay on every rank,
+        #     prop_msgs messages per rank, credits all-reduced and folded
+        prop["replica"] = prop_replica(args, rank, world, local, dist, dev, th)
+        # (2) range-sharded cfg4 overlay (strong): --prop-peers nodes over all ranks
+        if args.prop_peers > 0:
+            prop["sharded"] = prop_sharded(args, rank, world, local, dist, dev, th)
 
     # ---- heartbeat rounds (A10): every (node, topic) mesh maintained at once ----
     hb = None
     if args.hb_steps > 0:
+        # one gossipsub batch on the scoring shard fills its message caches, so
+        # the heartbeats also emit IHAVE gossip (emitGossip, mcache)
+        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                        accept_px_threshold=0, opportunistic_graft_threshold=0))
+        e.propagate(prop_messages(n, 256, seed), prop_config(args, n))
         e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                                         accept_px_threshold=0, opportunistic_graft_threshold=5))
         tick = 58  # the timed rounds include the OpportunisticGraftTicks round 60

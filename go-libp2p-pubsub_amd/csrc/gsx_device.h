@@ -123,9 +123,19 @@ constexpr int MAX_HOPS = 64;
 // Propagation counters: duplicates, first receipts per hop, and the
 // push-minimal traffic terms of SURVEY.md §8d (summed over hops and 64-message
 // words): eligible (edge, word) sends and (vertex, word) pairs gaining bits.
-enum { STAT_DUPS = 0, STAT_HOP0 = 1, STAT_EDGE_SENDS = STAT_HOP0 + MAX_HOPS + 1, STAT_NEW_WORDS, STAT_WORDS };
+// STAT_BACKSENDS: receipts counted as duplicates that the `from` exclusion removes.
+enum {
+    STAT_DUPS = 0,
+    STAT_HOP0 = 1,
+    STAT_EDGE_SENDS = STAT_HOP0 + MAX_HOPS + 1,
+    STAT_NEW_WORDS,
+    STAT_BACKSENDS,
+    STAT_WORDS
+};
 // rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
 constexpr uint32_t HALO = 0x80000000u;
+constexpr int PIN_FWD_SHIFT = 29;
+constexpr uint32_t PIN_NODE_MASK = (1u << PIN_FWD_SHIFT) - 1;  // nodes per shard < 2^29
 
 struct DevMsg {
     uint32_t source;  // global node id
@@ -142,13 +152,16 @@ struct PropState {
     const uint32_t* pair_obs;  // per pair: local observer index
     const uint8_t* eflags;
     uint8_t* fwd;              // per pair r = (v -> u), this call: FWD_* (v sends to u)
-    uint8_t* fwd_in;           // per pair q = (u -> v): fwd[rev[q]] for a local v, else 0
+    uint32_t* pin;             // per pair q = (u -> v), this call: NO_PAIR | HALO|slot | fwd<<29 | v_local
+    uint32_t* corr;            // per pair (u -> v), this call: in-window back-sends v will not make
     const DevMsg* msgs;
     uint64_t* seen;            // [node][word]
     uint64_t* origin;          // [node][word] messages the node published
     uint64_t* from_mask;       // [pair (u -> v)][word] messages u first received from v
     uint64_t* sel;             // [pair][word] RandomSub draws (null for other routers)
-    uint8_t* hop;              // [node][word * 64] arrival hop, 0xFF never
+    const uint64_t* hist;      // [hop][node][word]: messages first received at that hop (row 0: published)
+    uint32_t n_rows;           // valid history rows (hops run + 1)
+    uint32_t win_hops;         // P3 window in hops: floor(window / latency)
     uint32_t* dupcnt;          // per pair: duplicates inside the P3 window
     uint32_t* firstcnt;        // per pair: first receipts (deferred credits), or null
     unsigned long long* stats; // STAT_*
@@ -158,6 +171,9 @@ struct PropState {
     uint64_t n_pairs;
     uint32_t n_nodes, n_words, n_msgs, node_lo;
     uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt, sharded;
+    uint32_t max_hops, back_in_window;  // back_in_window: 2 * latency <= P3 window
+    uint32_t late;                      // duplicates of local pairs by k_prop_dups at the end of the call
+    uint64_t* occ;                      // [hop][node / 64] bit per node: frontier row non-empty
     double publish_threshold;
     int64_t hop_latency, window;
     uint64_t seed;
@@ -169,6 +185,7 @@ hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStr
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
 hipError_t launch_prop_count(const PropState& ps, hipStream_t st);
+hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, hipStream_t st);
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);

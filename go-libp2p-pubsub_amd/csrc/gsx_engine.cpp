@@ -122,19 +122,20 @@ struct gsx_engine {
 
     // propagation buffers (grown on demand) and the current / last call's shape
     struct {
-        uint64_t *seen = nullptr, *front = nullptr, *nxt = nullptr, *origin = nullptr, *from = nullptr,
-                 *sel = nullptr;
-        uint8_t *hop = nullptr, *fwd = nullptr, *fwd_in = nullptr;
+        uint64_t *seen = nullptr, *hist = nullptr, *origin = nullptr, *from = nullptr, *sel = nullptr, *occ = nullptr;
+        uint32_t* corr = nullptr;
+        uint8_t* fwd = nullptr;
+        uint32_t* pin = nullptr;
         uint32_t *dup = nullptr, *first = nullptr;  // pending P2/P3 credit counts per pair
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
-        uint32_t words_cap = 0, msgs_cap = 0;
+        uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
         gsx::PropState last{};
         bool have_last = false;
         // the call in flight (gsx_prop_begin .. gsx_prop_end)
         bool active = false, sel_done = false;
         uint32_t h = 0;
-        uint64_t *cur = nullptr, *nxtp = nullptr;
+        uint32_t rows_valid = 1;  // frontier-history rows written (skipped empty hops write none)
         gsx_prop_config cfg{};
         std::vector<uint64_t> ids;
         // pending (deferred) credits: topic they belong to
@@ -290,8 +291,8 @@ void free_state(gsx_engine* e) {
     if (e->d_rev) (void)hipFree(e->d_rev);
     e->d_row_ptr = nullptr;
     e->d_rev = nullptr;
-    void* pp[] = {e->prop.seen, e->prop.front, e->prop.nxt,   e->prop.origin, e->prop.from,
-                  e->prop.sel,  e->prop.hop,   e->prop.fwd,   e->prop.fwd_in, e->prop.dup,
+    void* pp[] = {e->prop.seen, e->prop.hist, e->prop.origin, e->prop.from,
+                  e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs};
     for (void* p : pp)
         if (p) (void)hipFree(p);
@@ -1237,14 +1238,13 @@ uint32_t prop_words(size_t m) {
 
 int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
-    void* pp[] = {P.seen, P.front, P.nxt, P.origin, P.from, P.sel, P.hop, P.msgs, P.stats};
+    void* pp[] = {P.seen, P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats};
     for (void* p : pp)
         if (p) (void)hipFree(p);
-    P.seen = P.front = P.nxt = P.origin = P.from = P.sel = nullptr;
-    P.hop = nullptr;
+    P.seen = P.hist = P.origin = P.from = P.sel = P.occ = nullptr;
     P.msgs = nullptr;
     P.stats = nullptr;
-    P.words_cap = P.msgs_cap = 0;
+    P.words_cap = P.msgs_cap = P.rows_cap = 0;
     return GSX_OK;
 }
 
@@ -1257,13 +1257,17 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.pair_obs = e->d_pair_obs;
     ps.eflags = e->d_eflags;
     ps.fwd = P.fwd;
-    ps.fwd_in = P.fwd_in;
+    ps.pin = P.pin;
+    ps.corr = P.corr;
+    ps.occ = P.occ;
+    ps.max_hops = cfg->max_hops;
     ps.msgs = P.msgs;
     ps.seen = P.seen;
     ps.origin = P.origin;
     ps.from_mask = P.from;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
-    ps.hop = P.hop;
+    ps.hist = P.hist;
+    ps.n_rows = 1;
     ps.dupcnt = P.dup;
     ps.firstcnt = P.first;
     ps.stats = P.stats;
@@ -1282,6 +1286,12 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.window = scored ? e->tp[cfg->topic].mesh_message_deliveries_window_ns : 0;
     ps.hop_latency = cfg->hop_latency_ns;
     ps.all_dups_in_window = ((int64_t)cfg->max_hops * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
+    // (h - h0) * latency <= window  <=>  h - h0 <= window / latency (latency > 0)
+    if (ps.window < 0) ps.win_hops = 0;
+    else if (cfg->hop_latency_ns == 0) ps.win_hops = GSX_MAX_HOPS + 1;
+    else ps.win_hops = (uint32_t)std::min<int64_t>(ps.window / cfg->hop_latency_ns, GSX_MAX_HOPS + 1);
+    ps.back_in_window = (2 * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
+    ps.late = (!ps.credit || ps.all_dups_in_window) ? 1 : 0;
     ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
     ps.publish_threshold = e->th.publish_threshold;
     ps.seed = cfg->seed;
@@ -1305,10 +1315,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (!e || !cfg || (m && !msgs)) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (cfg->max_hops > GSX_MAX_HOPS || cfg->router > GSX_ROUTER_RANDOMSUB || m > 0xFFFFFFFFull ||
-        cfg->credit_scores > GSX_CREDIT_DEFER)
+        cfg->credit_scores > GSX_CREDIT_DEFER || cfg->hop_latency_ns < 0)
         return fail(e, GSX_EINVAL, "bad propagation config");
     for (size_t k = 0; k < m; ++k)
         if (msgs[k].source >= e->n_total) return fail(e, GSX_ERANGE, "message source out of range");
+    if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^29 nodes per engine");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)
@@ -1316,18 +1327,22 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (int rc = ensure_scores(e)) return rc;  // publishThreshold tests read current scores
     const uint32_t W = prop_words(m);
     const size_t N = e->n_nodes, E = e->E;
-    if (W > P.words_cap || m > P.msgs_cap || !P.fwd) {
+    const uint32_t rows = cfg->max_hops + 1;
+    if (W > P.words_cap || m > P.msgs_cap || rows > P.rows_cap || !P.fwd) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         prop_free_buffers(e);
         const size_t mm = std::max<size_t>(m, 1);
         int rc = 0;
-        if ((rc = dalloc(e, &P.seen, W * N)) || (rc = dalloc(e, &P.front, W * N)) || (rc = dalloc(e, &P.nxt, W * N)) ||
+        const uint32_t rc_rows = std::max<uint32_t>(rows, GSX_MAX_HOPS / 2 + 1);
+        if ((rc = dalloc(e, &P.seen, W * N)) || (rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
+            (rc = dalloc(e, &P.occ, (size_t)rc_rows * ((N + 63) / 64))) ||
             (rc = dalloc(e, &P.origin, W * N)) || (rc = dalloc(e, &P.from, W * E)) ||
-            (rc = dalloc(e, &P.hop, (size_t)W * 64 * N)) || (rc = dalloc(e, &P.msgs, mm)) ||
+            (rc = dalloc(e, &P.msgs, mm)) ||
             (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
             return rc;
         if (!P.fwd) {
-            if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.fwd_in, E)) || (rc = dalloc(e, &P.dup, E)) ||
+            if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.pin, E)) || (rc = dalloc(e, &P.dup, E)) ||
+                (rc = dalloc(e, &P.corr, E)) ||
                 (rc = dalloc(e, &P.first, E)))
                 return rc;
             HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -1335,6 +1350,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         }
         P.words_cap = W;
         P.msgs_cap = (uint32_t)mm;
+        P.rows_cap = rc_rows;
     }
     const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
     if (rsub && !P.sel) {
@@ -1345,8 +1361,6 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     P.have_last = true;
     P.cfg = *cfg;
     P.h = 0;
-    P.cur = P.front;
-    P.nxtp = P.nxt;
     P.sel_done = false;
     P.ev_used = 0;
     P.ids.resize(m);
@@ -1358,14 +1372,15 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
     HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.front, 0, 8 * (size_t)W * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.hist, 0, 8 * (size_t)W * N, e->stream));  // row 0: the publishes
+    HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
     HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
     HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.hop, 0xFF, (size_t)W * 64 * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
-    HIPCHK(e, gsx::launch_prop_init(ps, P.front, e->stream));
+    HIPCHK(e, gsx::launch_prop_init(ps, P.hist, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));  // `hm` is on the host stack
     return GSX_OK;
 }
@@ -1383,11 +1398,12 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
     hipEvent_t a, b;
     if (int rc = prop_event_pair(e, &a, &b)) return rc;
     HIPCHK(e, hipEventRecord(a, e->stream));
-    if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, P.cur, e->stream));
+    const size_t row = (size_t)ps.n_nodes * ps.n_words;
+    const uint64_t* front = P.hist + (size_t)(h - 1) * row;
+    if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
     P.sel_done = false;
-    HIPCHK(e, gsx::launch_prop_hop(ps, h, P.cur, P.nxtp, e->stream));
+    HIPCHK(e, gsx::launch_prop_hop(ps, h, front, P.hist + (size_t)h * row, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
-    std::swap(P.cur, P.nxtp);
     return GSX_OK;
 }
 
@@ -1407,8 +1423,9 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     std::memset(out, 0, sizeof(*out));
     P.active = false;
     if (ps.n_msgs == 0) return GSX_OK;
+    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, e->stream));
+    if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, e->stream));
     if (ps.credit) {
-        HIPCHK(e, gsx::launch_prop_count(ps, e->stream));
         P.credit_pending = true;
         P.credit_topic = ps.topic;
         if (P.cfg.credit_scores != GSX_CREDIT_DEFER) {
@@ -1431,13 +1448,19 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     unsigned long long st[gsx::STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, P.stats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    out->duplicates = st[gsx::STAT_DUPS];
+    out->duplicates = st[gsx::STAT_DUPS] - st[gsx::STAT_BACKSENDS];
     for (uint32_t h = 1; h <= GSX_MAX_HOPS; ++h) {
         out->hop_deliveries[h] = st[gsx::STAT_HOP0 + h];
         out->deliveries += st[gsx::STAT_HOP0 + h];
         if (st[gsx::STAT_HOP0 + h]) out->hops = h;
     }
     out->transmissions = out->deliveries + out->duplicates;
+    P.rows_valid = P.h + 1;
+    for (uint32_t h = 1; h <= P.h && !ps.sharded; ++h)
+        if (st[gsx::STAT_HOP0 + h] == 0) {  // hop h ran and wrote an empty row; later hops were skipped
+            P.rows_valid = h + 1;
+            break;
+        }
     out->edge_sends = st[gsx::STAT_EDGE_SENDS];
     out->new_words = st[gsx::STAT_NEW_WORDS];
     double ms = 0;
@@ -1485,9 +1508,10 @@ int gsx_prop_pack(gsx_engine* e, uint64_t* send) {
     hipEvent_t a, b;
     if (int rc = prop_event_pair(e, &a, &b)) return rc;
     HIPCHK(e, hipEventRecord(a, e->stream));
-    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, P.cur, e->stream));
+    const uint64_t* front = P.hist + (size_t)P.h * ps.n_nodes * ps.n_words;
+    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
     P.sel_done = true;
-    HIPCHK(e, gsx::launch_prop_pack(ps, P.cur, send, e->stream));
+    HIPCHK(e, gsx::launch_prop_pack(ps, front, send, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     return GSX_OK;
 }
@@ -1546,7 +1570,8 @@ int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* 
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
     if (!e) return GSX_EINVAL;
     if (!e->prop.have_last) return fail(e, GSX_ESTATE, "no gsx_propagate call yet");
-    const gsx::PropState& ps = e->prop.last;
+    gsx::PropState ps = e->prop.last;
+    ps.n_rows = e->prop.rows_valid;
     const size_t cells = (size_t)ps.n_msgs * ps.n_nodes;
     if (cells == 0) return GSX_OK;
     if (hop) {

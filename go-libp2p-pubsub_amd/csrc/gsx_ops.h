@@ -95,6 +95,43 @@ __device__ __forceinline__ double eval_pair(const DevState& s, const DevPeerPara
     return score_tail(s, pp, p, score, s.bp[p]);
 }
 
+// k steps of "x = x + 1; if x > cap { x = cap }" (score.go:925-938, 970-973),
+// bit for bit, in O(log k): x only ever grows until it is capped, and it
+// stays capped, so the result is min(cap, k sequential +1s); within one
+// binade [2^e, 2^(e+1)) with 0 <= e <= 52 adding an integer is exact, so only
+// the step that crosses into the next binade rounds.  Below 1 (and in the
+// never-reached range >= 2^52) the steps are taken one by one.
+__device__ __forceinline__ double add_ones_capped(double x, uint32_t k, double cap) {
+    while (k && !(x >= 1.0 && x < 4503599627370496.0)) {  // [1, 2^52)
+        x = x + 1;
+        --k;
+        if (x > cap) return cap;
+    }
+    while (k) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+        const double top = __longlong_as_double((long long)((((bits >> 52) & 0x7FF) + 1) << 52));  // 2^(e+1)
+        const double gap = top - x;  // exact (Sterbenz)
+        const double s = ceil(gap) - 1;  // steps that stay below top
+        if (s >= (double)k) {
+            x = x + (double)k;
+            k = 0;
+        } else {
+            x = x + s;
+            k -= (uint32_t)s;
+            x = x + 1;  // the crossing step rounds
+            --k;
+        }
+        if (x > cap) return cap;
+        if (!(x < 4503599627370496.0))
+            while (k) {
+                x = x + 1;
+                --k;
+                if (x > cap) return cap;
+            }
+    }
+    return x > cap ? cap : x;
+}
+
 // x *= decay; x = 0 if x < DecayToZero   (score.go:527-542, 553-556)
 __device__ __forceinline__ double decay(double x, double d, double dtz) {
     x *= d;
@@ -206,6 +243,33 @@ __device__ inline void ev_invalid(const DevState& s, uint64_t p, uint32_t topic)
 __device__ inline void ev_penalty(const DevState& s, uint64_t p, int64_t count) {  // AddPenalty :384-398
     if (!(s.pflags[p] & PAIR_PRESENT)) return;
     s.bp[p] = s.bp[p] + (double)count;
+}
+
+// ---- counters --------------------------------------------------------------------
+// Sums NV per-thread counters over a 256-thread block (wave shuffles, then
+// LDS across the four waves) and adds each non-zero total to its global
+// counter with ONE atomic per block.  Same-address atomics serialise at the
+// memory side, so kernels that own counters run grid-stride over a bounded
+// grid (COUNTER_GRID blocks) and reach this once per block, every thread.
+constexpr unsigned COUNTER_GRID = 2048;
+
+template <int NV>
+__device__ __forceinline__ void block_count(unsigned long long (&v)[NV], unsigned long long* stats,
+                                            const uint32_t (&slot)[NV]) {
+    __shared__ unsigned long long part[NV][4];
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        for (int off = 32; off > 0; off >>= 1) v[i] += __shfl_down(v[i], off, 64);
+    const unsigned wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) part[i][wave] = v[i];
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const unsigned i = threadIdx.x;
+        const unsigned long long t = part[i][0] + part[i][1] + part[i][2] + part[i][3];
+        if (t) atomicAdd(&stats[slot[i]], t);
+    }
 }
 
 // ---- canonical RNG ---------------------------------------------

@@ -5,8 +5,9 @@
 // as node-major word rows ([node][word]), so one gather brings every word of
 // a neighbour.  One launch per hop: thread u walks its own pairs (u -> v) in
 // ascending neighbour order and pulls v's frontier row through the reverse
-// pair (v -> u) — its eligibility byte (read through u's own pair, fwd_in),
-// v's "first got it from u" row and the origin rows — so the first deliverer
+// pair (v -> u) — its eligibility (read through u's own pair, pin) and the
+// origin rows; the `from` exclusion is settled without a lookup (see
+// k_prop_hop) — so the first deliverer
 // of every new message is the lowest-indexed sender of that hop without
 // atomics, and every per-receiver word has exactly one writer.
 //
@@ -51,13 +52,25 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
     ps.fwd[r] = out;
 }
 
-// fwd_in[q] = fwd[rev[q]]: the receiver reads the sender's decision through
-// its own pair index (coalesced) instead of gathering it every hop.
-__global__ __launch_bounds__(256) void k_prop_fwd_in(PropState ps) {
+// pin[q], per call, for the receiver's pair q = (u -> v): what the hop
+// kernel needs to pull from v in one coalesced word — NO_PAIR if v never
+// sends to u (no reverse pair, or not in v's targets), HALO | slot if v is
+// remote, else (fwd & 3) << 29 | v_local (FORWARD / PUBLISH bits; RandomSub
+// candidates have neither and go through `sel`).
+__global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= ps.n_pairs) return;
     const uint32_t r = ps.rev[q];
-    ps.fwd_in[q] = (r == NO_PAIR || (r & HALO)) ? 0 : ps.fwd[r];
+    uint32_t out = NO_PAIR;
+    if (r != NO_PAIR) {
+        if (r & HALO) {
+            out = r;
+        } else {
+            const uint8_t fw = ps.fwd[r];
+            if (fw) out = ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | ((uint32_t)ps.col[q] - ps.node_lo);
+        }
+    }
+    ps.pin[q] = out;
 }
 
 // Sources on this shard: seen / frontier / origin bits and hop 0 (the local publish).
@@ -72,7 +85,7 @@ __global__ __launch_bounds__(256) void k_prop_init(PropState ps, uint64_t* front
     atomicOr((unsigned long long*)&ps.origin[i], bit);
     atomicOr((unsigned long long*)&ps.seen[i], bit);
     atomicOr((unsigned long long*)&front[i], bit);
-    ps.hop[(size_t)u * ps.n_words * 64 + k] = 0;
+    atomicOr((unsigned long long*)&ps.occ[u / 64], 1ull << (u % 64));  // occupancy row 0
 }
 
 // What pair (v -> u) lets through for a sender frontier word f:
@@ -133,34 +146,33 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
 // and the `from` exclusion are the sender's and are applied here.
 __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t* __restrict__ front,
                                                    uint64_t* __restrict__ send) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     const uint32_t W = ps.n_words;
-    unsigned long long n_send = 0;
-    if (j < ps.n_send) {
+    unsigned long long cnt[1] = {0};
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < ps.n_send; j += (uint64_t)gridDim.x * 256u) {
         uint64_t* out = send + j * W;
         const uint32_t r = ps.send_pair[j];
         if (r == NO_PAIR) {
             for (uint32_t w = 0; w < W; ++w) out[w] = 0;
-        } else {
-            const uint32_t v = ps.pair_obs[r];
-            const uint8_t fw = ps.fwd[r];
-            for (uint32_t w = 0; w < W; ++w) {
-                const uint64_t f = front[(size_t)v * W + w];
-                uint64_t c = 0;
-                if (f) {
-                    const uint64_t own = ps.origin[(size_t)v * W + w];
-                    uint64_t el = elig_word(fw, own);
-                    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
-                    c = f & el;
-                    n_send += c != 0;
-                    if (c) c &= ~ps.from_mask[(size_t)r * W + w];
-                }
-                out[w] = c;
+            continue;
+        }
+        const uint32_t v = ps.pair_obs[r];
+        const uint8_t fw = ps.fwd[r];
+        for (uint32_t w = 0; w < W; ++w) {
+            const uint64_t f = front[(size_t)v * W + w];
+            uint64_t c = 0;
+            if (f) {
+                const uint64_t own = ps.origin[(size_t)v * W + w];
+                uint64_t el = elig_word(fw, own);
+                if (ps.sel) el |= ps.sel[(size_t)r * W + w];
+                c = f & el;
+                cnt[0] += c != 0;
+                if (c) c &= ~ps.from_mask[(size_t)r * W + w];
             }
+            out[w] = c;
         }
     }
-    for (int off = 32; off > 0; off >>= 1) n_send += __shfl_down(n_send, off, 64);
-    if ((threadIdx.x & 63) == 0 && n_send) atomicAdd((unsigned long long*)&ps.stats[STAT_EDGE_SENDS], n_send);
+    const uint32_t slot[1] = {STAT_EDGE_SENDS};
+    block_count<1>(cnt, ps.stats, slot);
 }
 
 // ---- one hop ----------------------------------------------------------------
@@ -173,153 +185,252 @@ __device__ __forceinline__ void load_words(uint64_t (&d)[CW], const uint64_t* p)
     for (int i = 0; i < CW; ++i) d[i] = p[i];
 }
 
+// The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
+// is never looked up here: a message v would send back to the peer u it
+// first got it from is one u has already seen, so it can only ever count as
+// a duplicate at u.  Duplicates are accounted in one of two ways:
+//  * late (ps.late: every duplicate is inside the P3 window, or no credits):
+//    not per hop at all — k_prop_dups derives each pair's duplicates at the
+//    end of the call as sends - first receipts, where a pair's sends over
+//    the call are v's forwarded set through its eligibility, minus `from`;
+//  * per hop (a window shorter than the run): duplicates are counted as they
+//    arrive, and the hop that gives v a message subtracts the back-send u will
+//    make one hop later (v forwards received messages to u iff its pair
+//    (v -> u) has FORWARD; v first got them at h - 1, so they are inside v's
+//    window iff 2 * latency <= window) — from the duplicate counter and,
+//    through corr[(v -> u)], from u's P3 count at the end of the call.
+// Cross-shard sends arrive packed with the exclusion applied (k_prop_pack)
+// and are counted per hop in both modes.
+//
+// occ (one bit per node and hop, [hop][node / 64]) marks non-empty frontier
+// rows, so the sparse first and last hops skip the row gathers.
 template <int CW>
 __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                   uint64_t* __restrict__ nxt) {
-    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
+    constexpr int U = 4;  // pairs whose rows are in flight together (memory-level parallelism)
     const uint32_t W = ps.n_words;
-    if (!ps.sharded && h > 1 && ps.stats[STAT_HOP0 + h - 1] == 0) {  // nothing arrived last hop: empty frontier
-        if (u < ps.n_nodes)
-            for (uint32_t w = 0; w < W; ++w) nxt[(size_t)u * W + w] = 0;
-        return;
-    }
-    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0;
-    if (u < ps.n_nodes) {
-        const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
-        const size_t un = (size_t)u * W;
-        const size_t hrow = un * 64;
-        for (uint32_t w0 = 0; w0 < W; w0 += CW) {
-            uint64_t seen[CW], mine[CW], acc[CW];
-            load_words<CW>(seen, ps.seen + un + w0);
-            load_words<CW>(mine, ps.origin + un + w0);  // never sent back to its origin
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
+    uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    if (!ps.sharded && h > 1 && prev == 0) return;  // nothing arrived last hop: empty frontier, row h unused
+    // Sparse frontier (at most a quarter of the rows can be non-empty): test
+    // the occupancy bit before gathering a row.  Dense: gather directly.
+    const bool use_occ = prev < ps.n_nodes / 4;
+    // Back-sends of this hop's first receipts would happen at hop h + 1 (if
+    // it runs).  At h = 1 the receipts are the sender's own publishes, which
+    // nobody sends back to their origin anyway.
+    const bool backsend = !ps.late && h >= 2 && h < ps.max_hops;
+    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0;
+    for (uint32_t tile = blockIdx.x * 256u; tile < ps.n_nodes; tile += gridDim.x * 256u) {
+        const uint32_t u = tile + threadIdx.x;
+        bool any_new = false;
+        if (u < ps.n_nodes) {
+            const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
+            const size_t un = (size_t)u * W;
+            for (uint32_t w0 = 0; w0 < W; w0 += CW) {
+                uint64_t seen[CW], mine[CW], acc[CW], inwin[CW];
+                bool have_inwin = false;
+                load_words<CW>(seen, ps.seen + un + w0);
+                load_words<CW>(mine, ps.origin + un + w0);  // never sent back to its origin
 #pragma unroll
-            for (int i = 0; i < CW; ++i) acc[i] = 0;
-            for (int64_t q = q0; q < q1; ++q) {  // ascending sender index
-                const uint32_t r = ps.rev[q];    // the pair (v -> u)
-                if (r == NO_PAIR) continue;
-                uint64_t c[CW];
-                if (r & HALO) {  // remote sender: its rank packed exactly what it sends
-                    load_words<CW>(c, ps.halo + (size_t)(r & ~HALO) * W + w0);
-                } else {
-                    const uint32_t v = (uint32_t)ps.col[q] - ps.node_lo;
-                    uint64_t f[CW];
-                    load_words<CW>(f, front + (size_t)v * W + w0);
-                    uint64_t any = 0;
+                for (int i = 0; i < CW; ++i) acc[i] = 0;
+                for (int64_t qb = q0; qb < q1; qb += U) {
+                    // gather U pairs' rows at once, then merge them in ascending order
+                    uint32_t pv[U];
+                    uint64_t c[U][CW];
 #pragma unroll
-                    for (int i = 0; i < CW; ++i) any |= f[i];
-                    if (!any) continue;
-                    const uint8_t fw = ps.fwd_in[q];
-                    uint64_t own[CW], sl[CW];
-                    const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
-                    if (m == FWD_FORWARD || m == FWD_PUBLISH) load_words<CW>(own, ps.origin + (size_t)v * W + w0);
-                    else
+                    for (int j = 0; j < U; ++j) pv[j] = qb + j < q1 ? ps.pin[qb + j] : NO_PAIR;
+                    if (use_occ)
 #pragma unroll
-                        for (int i = 0; i < CW; ++i) own[i] = 0;
-                    if (ps.sel) load_words<CW>(sl, ps.sel + (size_t)r * W + w0);
-                    else
-#pragma unroll
-                        for (int i = 0; i < CW; ++i) sl[i] = 0;
-                    uint64_t hit = 0;
-#pragma unroll
-                    for (int i = 0; i < CW; ++i) {
-                        c[i] = f[i] & (elig_word(fw, own[i]) | sl[i]);
-                        n_send += c[i] != 0;
-                        hit |= c[i] & seen[i];
-                    }
-                    // Not back to v's `from` (floodsub.go:82, gossipsub.go:1007,
-                    // randomsub.go:113).  Those messages reached v from u, so u
-                    // has already seen them: the row is only needed when a
-                    // duplicate is possible.
-                    if (hit) {
-                        uint64_t fm[CW];
-                        load_words<CW>(fm, ps.from_mask + (size_t)r * W + w0);
-#pragma unroll
-                        for (int i = 0; i < CW; ++i) c[i] &= ~fm[i];
-                    }
-                }
-                uint64_t any = 0;
-#pragma unroll
-                for (int i = 0; i < CW; ++i) {
-                    c[i] &= ~mine[i];
-                    any |= c[i];
-                }
-                if (!any) continue;
-                uint32_t k = 0;
-#pragma unroll
-                for (int i = 0; i < CW; ++i) {
-                    const uint64_t newb = c[i] & ~seen[i] & ~acc[i];
-                    const uint64_t dup_now = c[i] & acc[i];  // first received this hop from a lower sender
-                    const uint64_t dup_old = c[i] & seen[i];  // first received at an earlier hop
-                    acc[i] |= newb;
-                    if (newb) ps.from_mask[(size_t)q * W + w0 + i] |= newb;  // u first got these from v
-                    n_new += __popcll(newb);
-                    n_dup += __popcll(dup_now) + __popcll(dup_old);
-                    if (ps.credit && (dup_now | dup_old)) {
-                        // DuplicateMessage -> markDuplicateMessageDelivery with the
-                        // record validated at u's first receipt (score.go:806-809, 965)
-                        k += __popcll(dup_now);
-                        if (ps.all_dups_in_window) {
-                            k += __popcll(dup_old);
-                        } else {
-                            uint64_t d = dup_old;
-                            while (d) {
-                                const int b = __builtin_ctzll(d);
-                                d &= d - 1;
-                                const int64_t h0 = ps.hop[hrow + (size_t)(w0 + i) * 64 + b];
-                                if (((int64_t)h - h0) * ps.hop_latency <= ps.window) ++k;
+                        for (int j = 0; j < U; ++j)
+                            if (pv[j] != NO_PAIR && !(pv[j] & HALO)) {
+                                const uint32_t v = pv[j] & PIN_NODE_MASK;
+                                if (!((occ_front[v / 64] >> (v % 64)) & 1)) pv[j] = NO_PAIR;  // v's row is empty
                             }
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        if (pv[j] == NO_PAIR) {
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] = 0;
+                        } else if (pv[j] & HALO) {  // remote sender: its rank packed exactly what it sends
+                            load_words<CW>(c[j], ps.halo + (size_t)(pv[j] & ~HALO) * W + w0);
+                        } else {
+                            load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        const uint32_t p = pv[j];
+                        if (p == NO_PAIR) continue;
+                        const int64_t q = qb + j;
+                        const bool halo = p & HALO;
+                        if (!halo) {  // v's frontier row through the pair's eligibility
+                            const uint32_t v = p & PIN_NODE_MASK;
+                            const uint8_t m = (uint8_t)(p >> PIN_FWD_SHIFT);
+                            uint64_t own[CW], sl[CW];
+                            if (m == FWD_FORWARD || m == FWD_PUBLISH) load_words<CW>(own, ps.origin + (size_t)v * W + w0);
+                            else
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) own[i] = 0;
+                            if (ps.sel) load_words<CW>(sl, ps.sel + (size_t)ps.rev[q] * W + w0);
+                            else
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) sl[i] = 0;
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) {
+                                c[j][i] &= elig_word(m, own[i]) | sl[i];
+                                n_send += c[j][i] != 0;
+                            }
+                        }
+                        uint64_t any = 0;
+#pragma unroll
+                        for (int i = 0; i < CW; ++i) {
+                            c[j][i] &= ~mine[i];
+                            any |= c[j][i];
+                        }
+                        if (!any) continue;
+                        const bool count_here = !ps.late || halo;
+                        if (count_here && ps.credit && !ps.all_dups_in_window && !have_inwin) {
+                            // DuplicateMessage -> markDuplicateMessageDelivery with the
+                            // record validated at u's first receipt (score.go:806-809,
+                            // 965): in the window iff (h - h0) * latency <= window, i.e.
+                            // u first got it at one of the last win_hops hops — the OR
+                            // of those hops' frontier rows.
+                            const uint32_t h_lo = h > ps.win_hops ? h - ps.win_hops : 0;
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) inwin[i] = 0;
+                            for (uint32_t h0 = h_lo; h0 < h; ++h0) {
+                                const uint64_t* row = ps.hist + (size_t)h0 * ps.n_nodes * W + un + w0;
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) inwin[i] |= row[i];
+                            }
+                            have_inwin = true;
+                        }
+                        uint64_t nb[CW];
+                        uint64_t newany = 0;
+                        uint32_t k = 0, back = 0;
+#pragma unroll
+                        for (int i = 0; i < CW; ++i) {
+                            nb[i] = c[j][i] & ~seen[i] & ~acc[i];
+                            acc[i] |= nb[i];
+                            newany |= nb[i];
+                            back += __popcll(nb[i]);
+                            if (count_here) {
+                                const uint64_t dup_now = c[j][i] & ~nb[i] & ~seen[i];  // first got this hop, lower sender
+                                const uint64_t dup_old = c[j][i] & seen[i];            // first got at an earlier hop
+                                n_dup += __popcll(dup_now) + __popcll(dup_old);
+                                if (ps.credit)
+                                    k += __popcll(dup_now) +
+                                         __popcll(ps.all_dups_in_window ? dup_old : (dup_old & inwin[i]));
+                            }
+                        }
+                        n_new += back;
+                        if (newany) {  // u first got these from v: one read-modify-write of the pair's row
+                            uint64_t* fr = ps.from_mask + (size_t)q * W + w0;
+                            uint64_t o[CW];
+                            load_words<CW>(o, fr);
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) fr[i] = o[i] | nb[i];
+                        }
+                        if (k) ps.dupcnt[q] += k;
+                        if (back && backsend && !halo && (ps.fwd[q] & FWD_FORWARD)) {
+                            // u forwards them to v at hop h + 1 and v counts duplicates:
+                            // the `from` exclusion's whole effect, taken back here
+                            n_back += back;
+                            if (ps.credit && ps.back_in_window) ps.corr[q] += back;
                         }
                     }
                 }
-                if (k) ps.dupcnt[q] += k;
-            }
 #pragma unroll
-            for (int i = 0; i < CW; ++i) {
-                nxt[un + w0 + i] = acc[i];
-                if (acc[i]) {
-                    ps.seen[un + w0 + i] = seen[i] | acc[i];
-                    ++n_vnew;
-                    uint64_t a = acc[i];
-                    while (a) {
-                        const int b = __builtin_ctzll(a);
-                        a &= a - 1;
-                        ps.hop[hrow + (size_t)(w0 + i) * 64 + b] = (uint8_t)h;
+                for (int i = 0; i < CW; ++i) {
+                    nxt[un + w0 + i] = acc[i];  // this hop's row of the frontier history
+                    if (acc[i]) {
+                        ps.seen[un + w0 + i] = seen[i] | acc[i];
+                        ++n_vnew;
+                        any_new = true;
                     }
                 }
             }
         }
+        // occupancy of this hop's rows: one 64-node word per wave
+        const unsigned long long occ = __ballot(any_new);
+        if ((threadIdx.x & 63) == 0 && u < ps.n_nodes) occ_nxt[u / 64] = occ;
     }
-    // counters: wave reduction, then one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        n_new += __shfl_down(n_new, off, 64);
-        n_dup += __shfl_down(n_dup, off, 64);
-        n_send += __shfl_down(n_send, off, 64);
-        n_vnew += __shfl_down(n_vnew, off, 64);
+    unsigned long long cnt[5] = {n_new, n_dup, n_send, n_vnew, n_back};
+    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS};
+    block_count<5>(cnt, ps.stats, slot);
+}
+
+// Late duplicate accounting (ps.late), once per call, per SENDER pair
+// r = (v -> u) with both ends on this shard: v's sends to u over the call are
+// the messages v forwarded (its seen set minus what it first got at the last
+// hop run, when it no longer sends) through the pair's eligibility and
+// RandomSub draws, minus the ones v first got from u (`from`, v's own row)
+// and the ones u published.  Each is a first receipt or a duplicate at u;
+// k_prop_count subtracts the first receipts at u's pair.  Everything but
+// u's origin row and the receiving pair's counter is v-local.
+__global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run) {
+    unsigned long long cnt[1] = {0};
+    const uint32_t W = ps.n_words;
+    // rows after the first hop that delivered nothing were never written
+    // (skipped hops); that hop's row is empty and nothing was first received
+    // later, so v forwarded its whole seen set
+    for (uint32_t hh = 1; hh < h_run && !ps.sharded; ++hh)
+        if (ps.stats[STAT_HOP0 + hh] == 0) {
+            h_run = hh;
+            break;
+        }
+    const uint64_t* last = ps.hist + (size_t)h_run * ps.n_nodes * W;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < ps.n_pairs; r += (uint64_t)gridDim.x * 256u) {
+        const uint32_t q = ps.rev[r];  // the receiver's pair (u -> v)
+        const uint8_t fw = ps.fwd[r];
+        if (q == NO_PAIR || (q & HALO) || !fw) continue;
+        const uint32_t v = ps.pair_obs[r];
+        const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
+        uint32_t sends = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            const size_t vw = (size_t)v * W + w;
+            uint64_t s = ps.seen[vw] & ~last[vw] & elig_word(fw, ps.origin[vw]);
+            if (ps.sel) s |= ps.sel[r * W + w];
+            s &= ~ps.from_mask[r * W + w] & ~ps.origin[(size_t)u * W + w];
+            sends += __popcll(s);
+        }
+        cnt[0] += sends;
+        if (ps.credit && sends) ps.dupcnt[q] += sends;
     }
-    if ((threadIdx.x & 63) == 0) {
-        if (n_new) atomicAdd((unsigned long long*)&ps.stats[STAT_HOP0 + h], n_new);
-        if (n_dup) atomicAdd((unsigned long long*)&ps.stats[STAT_DUPS], n_dup);
-        if (n_send) atomicAdd((unsigned long long*)&ps.stats[STAT_EDGE_SENDS], n_send);
-        if (n_vnew) atomicAdd((unsigned long long*)&ps.stats[STAT_NEW_WORDS], n_vnew);
-    }
+    const uint32_t slot[1] = {STAT_DUPS};
+    block_count<1>(cnt, ps.stats, slot);
 }
 
 // ---- P2/P3 credits ------------------------------------------------------------
 // Per receiver pair q = (u -> v), add this call's first receipts from v (the
 // popcount of its from row) and in-window duplicates to the pending counts.
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps) {
-    const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (q >= ps.n_pairs) return;
-    uint32_t k1 = 0;
-    for (uint32_t w = 0; w < ps.n_words; ++w) k1 += __popcll(ps.from_mask[(size_t)q * ps.n_words + w]);
-    if (k1) ps.firstcnt[q] += k1;
+    unsigned long long cnt[1] = {0};
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        uint32_t k1 = 0;
+        for (uint32_t w = 0; w < ps.n_words; ++w) k1 += __popcll(ps.from_mask[(size_t)q * ps.n_words + w]);
+        const uint32_t r = ps.rev[q];
+        const bool local = r != NO_PAIR && !(r & HALO);
+        if (ps.credit) {
+            if (k1) ps.firstcnt[q] += k1;
+            if (local) {
+                if (ps.late) ps.dupcnt[q] -= k1;  // k_prop_dups counted every send from v, first receipts too
+                else if (const uint32_t c = ps.corr[r]) ps.dupcnt[q] -= c;  // in-window back-sends taken back
+            }
+        }
+        if (ps.late && local) cnt[0] += k1;
+    }
+    const uint32_t slot[1] = {STAT_BACKSENDS};
+    block_count<1>(cnt, ps.stats, slot);
 }
 
 // Fold pending counts: k1 first receipts, k2 duplicates inside the window.
 // markFirstMessageDelivery: fmd k1 steps of +1 then cap, mmd too when in
 // mesh; markDuplicateMessageDelivery: mmd k2 more steps when in mesh
 // (score.go:912-974).  All steps are identical, so their order does not
-// matter; they are applied one by one because +1 on a fractional counter rounds.
+// matter; add_ones_capped gives the result of the steps one by one.
 __global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, const uint32_t* __restrict__ first,
                                                    const uint32_t* __restrict__ dup) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -331,19 +442,9 @@ __global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, con
     const uint32_t k2 = dup[q];
     if (k1 == 0 && k2 == 0) return;
     const size_t b = rec_index(q, ps.topic, s.n_topics, FMD);
-    double f = s.rec[b + FMD * TILE];
-    for (uint32_t i = 0; i < k1; ++i) {
-        f = f + 1;
-        if (f > tp.cap2) f = tp.cap2;
-    }
-    s.rec[b + FMD * TILE] = f;
+    s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], k1, tp.cap2);
     if (!(s.rflags[flag_index(q, ps.topic, s.n_topics)] & REC_IN_MESH)) return;
-    double m = s.rec[b + MMD * TILE];
-    for (uint32_t i = 0; i < k1 + k2; ++i) {
-        m = m + 1;
-        if (m > tp.cap3) m = tp.cap3;
-    }
-    s.rec[b + MMD * TILE] = m;
+    s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
 }
 
 // First deliverer per (message, node) from the per-pair "first got it from" rows.
@@ -363,12 +464,28 @@ __global__ __launch_bounds__(256) void k_prop_from(PropState ps, int32_t* __rest
         }
 }
 
-// [node][word*64] arrival hops -> the ABI's [message][node].
+// Arrival hops, [message][node] as the ABI lays them out: the hop whose
+// frontier row holds the message's bit (0 at the source), 0xFF never.
 __global__ __launch_bounds__(256) void k_prop_hops_export(PropState ps, uint8_t* __restrict__ out) {
     const uint32_t u = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t k = blockIdx.y;
+    const uint32_t w = blockIdx.y;
     if (u >= ps.n_nodes) return;
-    out[(size_t)k * ps.n_nodes + u] = ps.hop[(size_t)u * ps.n_words * 64 + k];
+    const uint32_t W = ps.n_words;
+    uint8_t hk[64];
+#pragma unroll
+    for (int b = 0; b < 64; ++b) hk[b] = 0xFF;
+    for (uint32_t h = 0; h < ps.n_rows; ++h) {
+        uint64_t x = ps.hist[(size_t)h * ps.n_nodes * W + (size_t)u * W + w];
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            hk[b] = (uint8_t)h;
+        }
+    }
+    for (int b = 0; b < 64; ++b) {
+        const uint32_t k = w * 64 + b;
+        if (k < ps.n_msgs) out[(size_t)k * ps.n_nodes + u] = hk[b];
+    }
 }
 
 // ---- launchers ----------------------------------------------------------------
@@ -381,13 +498,13 @@ hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_
 }
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st) {
     if (ps.n_nodes == 0 || ps.n_msgs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_hops_export, dim3(nblk(ps.n_nodes, 256), ps.n_msgs), dim3(256), 0, st, ps, hop_mn);
+    hipLaunchKernelGGL(k_prop_hops_export, dim3(nblk(ps.n_nodes, 256), ps.n_words), dim3(256), 0, st, ps, hop_mn);
     return hipGetLastError();
 }
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st) {
     if (s.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_fwd, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps, s);
-    hipLaunchKernelGGL(k_prop_fwd_in, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
+    hipLaunchKernelGGL(k_prop_pin, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
     return hipGetLastError();
 }
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st) {
@@ -402,21 +519,26 @@ hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStr
 }
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st) {
     if (ps.n_send == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_pack, dim3(nblk(ps.n_send, 256)), dim3(256), 0, st, ps, front, send);
+    hipLaunchKernelGGL(k_prop_pack, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps, front, send);
     return hipGetLastError();
 }
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     if (ps.n_nodes == 0) return hipSuccess;
-    const dim3 g(nblk(ps.n_nodes, 256)), b(256);
+    const dim3 g(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), b(256);
     // n_words is 1, 2 or a multiple of 4 (the engine pads)
     if (ps.n_words == 1) hipLaunchKernelGGL(k_prop_hop<1>, g, b, 0, st, ps, h, front, nxt);
     else if (ps.n_words == 2) hipLaunchKernelGGL(k_prop_hop<2>, g, b, 0, st, ps, h, front, nxt);
     else hipLaunchKernelGGL(k_prop_hop<4>, g, b, 0, st, ps, h, front, nxt);
     return hipGetLastError();
 }
+hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_dups, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run);
+    return hipGetLastError();
+}
 hipError_t launch_prop_count(const PropState& ps, hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_count, dim3(nblk(ps.n_pairs, 256)), dim3(256), 0, st, ps);
+    hipLaunchKernelGGL(k_prop_count, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps);
     return hipGetLastError();
 }
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Propagation-only workload for rocprofv3 (kernel trace / PMC passes):
+the bench's replica leg — 1M-peer overlay, gossipsub, 256-message batches."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "go-libp2p-pubsub_amd"))
+import bench  # noqa: E402
+from gsx import abi, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--peers", type=int, default=1_000_000)
+ap.add_argument("--msgs", type=int, default=256)
+ap.add_argument("--batches", type=int, default=3)
+ap.add_argument("--router", type=int, default=abi.GSX_ROUTER_GOSSIPSUB)
+a = ap.parse_args()
+th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                    accept_px_threshold=0, opportunistic_graft_threshold=0)
+e = bench.prop_engine(a.peers, 0, a.peers, 6, synth.SEED, 0, th, None)
+
+
+class A:
+    prop_hops = 24
+
+
+cfg = bench.prop_config(A, a.peers)
+cfg.router = a.router
+for b in range(a.batches):
+    out = e.propagate(bench.prop_messages(a.peers, a.msgs, synth.SEED, first=b * a.msgs), cfg)[0]
+    d = out.as_dict()
+    print(json.dumps({"batch": b, "hop_kernel_ms": out.hop_kernel_ms, "deliveries": d["deliveries"],
+                      "hop_deliveries": d["hop_deliveries"], "edge_sends": out.edge_sends,
+                      "new_words": out.new_words}), flush=True)
+e.close()
