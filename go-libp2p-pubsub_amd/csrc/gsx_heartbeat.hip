@@ -219,16 +219,15 @@ __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, 
 
 // One launch per topic, ascending: the maintenance of (v, t) for every v.
 __global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
-    const uint32_t v = blockIdx.x * 64u + threadIdx.x;
     uint64_t grafts = 0, prunes = 0;
-    if (v < h.n_nodes) {
+    for (uint32_t v = blockIdx.x * 64u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[v];
         HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
         Rng g = hb_rng(h, v, t, 0);
         U.maintain(g);
         h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
-        grafts = U.grafts;
-        prunes = U.prunes;
+        grafts += U.grafts;
+        prunes += U.prunes;
     }
     flush_count(h.stats, HB_GRAFTS, grafts);
     flush_count(h.stats, HB_PRUNES, prunes);
@@ -259,9 +258,8 @@ __device__ __forceinline__ void skip_shuffle(Rng& g, uint32_t n) {
 
 __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
                                                   uint32_t n_gb) {
-    const uint32_t v = blockIdx.x * 64u + threadIdx.x;
     uint64_t msgs = 0, ids = 0;
-    if (v < h.n_nodes) {
+    for (uint32_t v = blockIdx.x * 64u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 64u) {
         // GetGossipIDs of (v, t): its length and multiset digest
         uint32_t L = 0;
         uint64_t dig = 0;
@@ -301,8 +299,8 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
                     h.ihave_len[x] = L;
                     h.ihave_hash[x] = dig;
                 }
-                msgs = (uint64_t)target;
-                ids = (uint64_t)target * L;
+                msgs += (uint64_t)target;
+                ids += (uint64_t)target * L;
             }
         }
     }
@@ -445,9 +443,8 @@ __device__ __forceinline__ void handle_prune(const DevState& s, const HbState& h
 }
 
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
-    const uint32_t u = blockIdx.x * 64u + threadIdx.x;
     uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
-    if (u < h.n_nodes) {
+    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         const DevGossipParams& gp = h.gp;
         for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
@@ -514,9 +511,8 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
 // ---- (C) the GRAFT senders handle the PRUNE answers ------------------------------
 
 __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;  // r = (v -> u)
     uint64_t handled = 0;
-    if (r < h.n_pairs) {
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {  // r = (v -> u)
         const uint32_t q = h.rev[r];
         uint64_t resp = q == NO_PAIR ? 0 : h.resp[q];
         // AcceptFrom at v for the answering peer
@@ -542,6 +538,12 @@ static inline unsigned grid_cap(uint64_t n, unsigned bs) {
     const unsigned b = blocks_for(n, bs);
     return b < 2048 ? b : 2048;
 }
+// One-wave blocks, grid-stride over nodes: at most 8192 waves (8 per SIMD),
+// so the per-wave counter atomics stay few (same-address atomics serialise).
+static inline unsigned wave_grid(uint64_t n) {
+    const unsigned b = blocks_for(n, 64);
+    return b < 8192 ? b : 8192;
+}
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
     const uint64_t n = (uint64_t)n_topics * h.n_pairs;
@@ -552,7 +554,7 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
 
 hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t);
+    hipLaunchKernelGGL(k_hb_mesh, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t);
     return hipGetLastError();
 }
 
@@ -561,7 +563,7 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
     if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hb_gossip, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t, gb, n_gb);
+    hipLaunchKernelGGL(k_hb_gossip, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t, gb, n_gb);
     if (max_ids > (uint32_t)h.gp.max_ihave)  // some node may need the truncating path
         hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), sizeof(uint32_t) * max_ids, st,
                            s, h, t, gb, n_gb);
@@ -570,13 +572,13 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
 
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_recv, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h);
+    hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
 
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_answer, dim3(blocks_for(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    hipLaunchKernelGGL(k_hb_answer, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, s, h);
     return hipGetLastError();
 }
 

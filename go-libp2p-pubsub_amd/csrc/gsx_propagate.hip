@@ -56,7 +56,9 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
 // kernel needs to pull from v in one coalesced word — NO_PAIR if v never
 // sends to u (no reverse pair, or not in v's targets), HALO | slot if v is
 // remote, else (fwd & 3) << 29 | v_local (FORWARD / PUBLISH bits; RandomSub
-// candidates have neither and go through `sel`).
+// candidates have neither and go through `sel`).  (Gathering fwd per q here
+// is cheaper than scattering pin from k_prop_fwd: 1-byte reads from a small
+// array vs 4-byte partial-line writes.)
 __global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= ps.n_pairs) return;
@@ -382,18 +384,24 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run)
             break;
         }
     const uint64_t* last = ps.hist + (size_t)h_run * ps.n_nodes * W;
+    const bool last_empty = ps.stats[STAT_HOP0 + h_run] == 0 && (!ps.sharded || h_run < ps.max_hops);
+    const uint64_t* src_occ = ps.occ;  // row 0: nodes that published in this call
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < ps.n_pairs; r += (uint64_t)gridDim.x * 256u) {
         const uint32_t q = ps.rev[r];  // the receiver's pair (u -> v)
         const uint8_t fw = ps.fwd[r];
         if (q == NO_PAIR || (q & HALO) || !fw) continue;
         const uint32_t v = ps.pair_obs[r];
         const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
+        const bool v_src = (src_occ[v / 64] >> (v % 64)) & 1, u_src = (src_occ[u / 64] >> (u % 64)) & 1;
         uint32_t sends = 0;
         for (uint32_t w = 0; w < W; ++w) {
             const size_t vw = (size_t)v * W + w;
-            uint64_t s = ps.seen[vw] & ~last[vw] & elig_word(fw, ps.origin[vw]);
+            uint64_t s = ps.seen[vw];
+            if (!last_empty) s &= ~last[vw];
+            s &= elig_word(fw, v_src ? ps.origin[vw] : 0);
             if (ps.sel) s |= ps.sel[r * W + w];
-            s &= ~ps.from_mask[r * W + w] & ~ps.origin[(size_t)u * W + w];
+            s &= ~ps.from_mask[r * W + w];
+            if (u_src) s &= ~ps.origin[(size_t)u * W + w];
             sends += __popcll(s);
         }
         cnt[0] += sends;
