@@ -152,14 +152,22 @@ def prop_roofline(tot, msgs, kernel_ms):
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "words": W}
 
 
-def _max_over_ranks(x, dist, dev):
+REHEARSE = False  # set by --rehearse: scalars reduce through host memory (gloo)
+
+
+def reduce_scalar(x, dist, dev, op="max"):
+    """MAX / SUM of a host scalar over ranks (x itself without a group)."""
     import torch
 
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if REHEARSE else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def _max_over_ranks(x, dist, dev):
+    return reduce_scalar(x, dist, dev, "max")
 
 
 def prop_replica(args, rank, world, local, dist, dev, th):
@@ -169,7 +177,7 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     e = prop_engine(n, 0, n, args.degree, synth.SEED, local, th, None)
     cfg = prop_config(args, n)
     M = args.prop_msgs * world
-    tp = shard_mod.DistTransport(dev) if dist is not None else None
+    tp = shard_mod.DistTransport(dev, stage_host=args.rehearse) if dist is not None else None
     runner = shard_mod.MessageParallel(e, tp) if tp is not None else None
 
     def once(b):
@@ -221,7 +229,7 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     M = args.prop_msgs
     runner = None
     if dist is not None:
-        runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev))
+        runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
 
     def once(b):
         msgs = prop_messages(n, M, synth.SEED + 1, first=b * M)
@@ -277,11 +285,17 @@ def main():
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 rehearsal on one GPU: all ranks on device 0, gloo (host-staged) instead of RCCL")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse:  # every rank on GPU 0, gloo through host memory: the multi-GPU flow on one card
+        local = 0
+        global REHEARSE
+        REHEARSE = True
     if world != args.gpus:
         log(f"[bench] note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
@@ -292,7 +306,7 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if args.rehearse else "nccl")
     dev = torch.device("cuda", local)
 
     n, T = args.peers, args.topics
@@ -327,13 +341,8 @@ def main():
     k_total, k_min, k_max, k_n = e.timing_end()
 
     recs = float(R) * args.steps
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([recs], dtype=torch.float64, device=dev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        recs = float(r.item())
+    elapsed = reduce_scalar(elapsed, dist, dev, "max")
+    recs = reduce_scalar(recs, dist, dev, "sum")
 
     value = recs / elapsed
     kavg_ms = k_total / max(1, k_n)
@@ -382,13 +391,8 @@ def main():
         ht = time.perf_counter() - t0
         barrier()
         units = float(n) * T * args.hb_steps
-        if dist is not None:
-            t = torch.tensor([ht], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ht = float(t.item())
-            r = torch.tensor([units], dtype=torch.float64, device=dev)
-            dist.all_reduce(r, op=dist.ReduceOp.SUM)
-            units = float(r.item())
+        ht = reduce_scalar(ht, dist, dev, "max")
+        units = reduce_scalar(units, dist, dev, "sum")
         hb = {
             "metric": "heartbeat (node, topic) mesh units/s",
             "value": units / ht,

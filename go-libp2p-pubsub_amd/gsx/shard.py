@@ -47,26 +47,42 @@ def _torch():
 
 
 class DistTransport:
-    """torch.distributed transport (RCCL for "nccl", gloo on CPU)."""
+    """torch.distributed transport (RCCL for "nccl", gloo on CPU).
 
-    def __init__(self, device, group=None):
+    stage_host: device tensors go through host memory around each
+    collective (a gloo group driving GPU buffers, e.g. several ranks
+    rehearsing the multi-GPU flow on one card)."""
+
+    def __init__(self, device, group=None, stage_host=False):
         import torch.distributed as dist
 
         self.dist = dist
         self.group = group
         self.device = device
+        self.stage = stage_host
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
+    def _h(self, t):
+        return t.cpu() if self.stage and t.is_cuda else t
+
     def all_to_all(self, recv, send, recv_splits, send_splits):
-        self.dist.all_to_all_single(recv, send, list(map(int, recv_splits)), list(map(int, send_splits)),
-                                    group=self.group)
+        r, s = self._h(recv), self._h(send)
+        self.dist.all_to_all_single(r, s, list(map(int, recv_splits)), list(map(int, send_splits)), group=self.group)
+        if r is not recv:
+            recv.copy_(r)
 
     def all_reduce_sum(self, t):
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        h = self._h(t)
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+        if h is not t:
+            t.copy_(h)
 
     def all_reduce_max(self, t):
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        h = self._h(t)
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
+        if h is not t:
+            t.copy_(h)
 
 
 def exchange_plan(backend, rank_lo, transport) -> None:
