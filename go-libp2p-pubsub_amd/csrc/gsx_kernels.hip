@@ -52,14 +52,19 @@ __global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp
         uint8_t fl = ftile[t * TILE];
         int64_t mt = 0;
         if (conn) {
+            // a counter that decays stays written back only if it changed: a
+            // zero counter (most peers never send an invalid message, most
+            // meshes never fail) decays to itself, and a wave whose 64 lanes
+            // all hold zero skips the 512-B store entirely
+            const double fmd0 = fmd, mmd0 = mmd, mfp0 = mfp, imd0 = imd;
             fmd = decay(fmd, tp.d2, pp.decay_to_zero);
             mmd = decay(mmd, tp.d3, pp.decay_to_zero);
             mfp = decay(mfp, tp.d3b, pp.decay_to_zero);
             imd = decay(imd, tp.d4, pp.decay_to_zero);
-            __builtin_nontemporal_store(fmd, r + FMD * TILE);
-            __builtin_nontemporal_store(mmd, r + MMD * TILE);
-            __builtin_nontemporal_store(mfp, r + MFP * TILE);
-            __builtin_nontemporal_store(imd, r + IMD * TILE);
+            if (__double_as_longlong(fmd) != __double_as_longlong(fmd0)) __builtin_nontemporal_store(fmd, r + FMD * TILE);
+            if (__double_as_longlong(mmd) != __double_as_longlong(mmd0)) __builtin_nontemporal_store(mmd, r + MMD * TILE);
+            if (__double_as_longlong(mfp) != __double_as_longlong(mfp0)) __builtin_nontemporal_store(mfp, r + MFP * TILE);
+            if (__double_as_longlong(imd) != __double_as_longlong(imd0)) __builtin_nontemporal_store(imd, r + IMD * TILE);
             uint8_t nf = fl & ~REC_FRESH;
             if (fl & REC_IN_MESH) {  // :544-549
                 mt = now - __builtin_nontemporal_load(reinterpret_cast<const int64_t*>(r) + GRAFT * TILE);
