@@ -267,6 +267,9 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     }
     if world == 1:
         out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
+    else:
+        out["exchange"] = {"compacted": runner.compact, "bytes_sent_per_batch_rank": runner.sent_bytes / (args.prop_steps + 1),
+                           "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8}
     return out
 
 

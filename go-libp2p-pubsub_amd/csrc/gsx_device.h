@@ -135,6 +135,7 @@ enum {
 // rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
 constexpr uint32_t HALO = 0x80000000u;
 constexpr int PIN_FWD_SHIFT = 29;
+constexpr uint32_t MAX_RANKS = 64;  // ranks of a shard plan (one node: 8)
 constexpr uint32_t PIN_NODE_MASK = (1u << PIN_FWD_SHIFT) - 1;  // nodes per shard < 2^29
 
 struct DevMsg {
@@ -167,7 +168,11 @@ struct PropState {
     unsigned long long* stats; // STAT_*
     const uint64_t* halo;      // [receive slot][word]: filtered sends of remote neighbours
     const uint32_t* send_pair; // per send slot: the local pair (v -> u) it carries, NO_PAIR = none
+    const uint8_t* send_dest;  // per send slot: destination rank
+    const uint64_t* send_base; // per rank: first send slot of its segment
+    const uint64_t* dest_halo_base;  // per rank: the halo slot its segment starts at, on that rank
     uint64_t n_send;
+    uint32_t n_ranks;
     uint64_t n_pairs;
     uint32_t n_nodes, n_words, n_msgs, node_lo;
     uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt, sharded;
@@ -183,6 +188,11 @@ hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t s
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
 hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStream_t st);
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st);
+hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, uint64_t* out,
+                                    unsigned long long* dcount, hipStream_t st);
+hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st);
+hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
+                               hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
 hipError_t launch_prop_count(const PropState& ps, hipStream_t st);
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, hipStream_t st);

@@ -144,6 +144,12 @@ struct gsx_engine {
         // per-hop kernel timing
         std::vector<hipEvent_t> ev;
         uint32_t ev_used = 0;
+        // compacted shard exchange: the dense halo the received entries are
+        // scattered into, the slots filled last hop, per-destination counts
+        uint64_t* halo = nullptr;
+        uint32_t* halo_idx = nullptr;
+        uint64_t halo_cap = 0, halo_prev = 0;
+        unsigned long long* dcount = nullptr;
     } prop;
 
     // range sharding (gsx_load_overlay_shard / gsx_shard_*_plan)
@@ -153,6 +159,8 @@ struct gsx_engine {
     std::vector<uint64_t> recv_counts, send_counts;
     uint64_t n_recv = 0, n_send = 0;
     uint32_t* d_send_pair = nullptr;
+    uint8_t* d_send_dest = nullptr;
+    uint64_t *d_send_base = nullptr, *d_dest_halo_base = nullptr;
     uint32_t* d_pair_obs = nullptr;
     std::vector<uint32_t> rev_host;
     bool sharded() const { return n_ranks > 1 || node_lo != 0 || n_total != n_nodes; }
@@ -293,13 +301,17 @@ void free_state(gsx_engine* e) {
     e->d_rev = nullptr;
     void* pp[] = {e->prop.seen, e->prop.hist, e->prop.origin, e->prop.from,
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
-                  e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs};
+                  e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
+                  e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
+                  e->d_dest_halo_base};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
     e->prop = {};
     e->prop.ev = std::move(evs);
     e->d_send_pair = e->d_pair_obs = nullptr;
+    e->d_send_dest = nullptr;
+    e->d_send_base = e->d_dest_halo_base = nullptr;
     e->n_ranks = 1;
     e->rank_lo.clear();
     e->recv_counts.clear();
@@ -878,13 +890,42 @@ int gsx_shard_send_plan(gsx_engine* e, const uint64_t* send_counts, const uint32
         const int32_t* it = std::lower_bound(b, en, (int32_t)u);
         if (it != en && *it == (int32_t)u) sp[j] = (uint32_t)(it - e->col_host.data());
     }
+    std::vector<uint8_t> dest(n);
+    std::vector<uint64_t> base(e->n_ranks + 1, 0);
+    for (uint32_t k = 0; k < e->n_ranks; ++k) {
+        base[k + 1] = base[k] + send_counts[k];
+        std::fill(dest.begin() + base[k], dest.begin() + base[k + 1], (uint8_t)k);
+    }
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (e->d_send_pair) (void)hipFree(e->d_send_pair);
+    void* old[] = {e->d_send_pair, e->d_send_dest, e->d_send_base};
+    for (void* p : old)
+        if (p) (void)hipFree(p);
     e->d_send_pair = nullptr;
-    if (int rc = dalloc(e, &e->d_send_pair, n)) return rc;
+    e->d_send_dest = nullptr;
+    e->d_send_base = nullptr;
+    int rc = 0;
+    if ((rc = dalloc(e, &e->d_send_pair, n)) || (rc = dalloc(e, &e->d_send_dest, n)) ||
+        (rc = dalloc(e, &e->d_send_base, (size_t)e->n_ranks + 1)))
+        return rc;
     if (n) HIPCHK(e, hipMemcpy(e->d_send_pair, sp.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    if (n) HIPCHK(e, hipMemcpy(e->d_send_dest, dest.data(), n, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_send_base, base.data(), 8 * base.size(), hipMemcpyHostToDevice));
     e->send_counts.assign(send_counts, send_counts + e->n_ranks);
     e->n_send = n;
+    return GSX_OK;
+}
+
+// For the compacted exchange: where each destination's rows start in ITS
+// halo (the receive slot of the first row this rank sends it).
+int gsx_shard_set_halo_bases(gsx_engine* e, const uint64_t* dest_halo_base) {
+    if (!e || !dest_halo_base) return GSX_EINVAL;
+    if (e->rank_lo.empty()) return fail(e, GSX_ESTATE, "gsx_shard_recv_plan first");
+    if (e->n_ranks > gsx::MAX_RANKS) return fail(e, GSX_ERANGE, "too many ranks for the compacted exchange");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_dest_halo_base) (void)hipFree(e->d_dest_halo_base);
+    e->d_dest_halo_base = nullptr;
+    if (int rc = dalloc(e, &e->d_dest_halo_base, e->n_ranks)) return rc;
+    HIPCHK(e, hipMemcpy(e->d_dest_halo_base, dest_halo_base, 8 * (size_t)e->n_ranks, hipMemcpyHostToDevice));
     return GSX_OK;
 }
 
@@ -1272,6 +1313,10 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.firstcnt = P.first;
     ps.stats = P.stats;
     ps.send_pair = e->d_send_pair;
+    ps.send_dest = e->d_send_dest;
+    ps.send_base = e->d_send_base;
+    ps.dest_halo_base = e->d_dest_halo_base;
+    ps.n_ranks = e->n_ranks;
     ps.n_send = e->n_send;
     ps.n_pairs = e->E;
     ps.n_nodes = e->n_nodes;
@@ -1367,6 +1412,22 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
     P.active = true;
     HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
+    if (e->n_recv) {  // compacted exchange: engine-owned dense halo, empty at the start of a call
+        if (P.halo_cap < (uint64_t)W * e->n_recv || !P.halo_idx) {
+            if (P.halo) (void)hipFree(P.halo);
+            if (P.halo_idx) (void)hipFree(P.halo_idx);
+            P.halo = nullptr;
+            P.halo_idx = nullptr;
+            int rc = 0;
+            if ((rc = dalloc(e, &P.halo, (size_t)W * e->n_recv)) || (rc = dalloc(e, &P.halo_idx, e->n_recv))) return rc;
+            P.halo_cap = (uint64_t)W * e->n_recv;
+        }
+        HIPCHK(e, hipMemsetAsync(P.halo, 0, 8 * (size_t)W * e->n_recv, e->stream));
+        P.halo_prev = 0;
+    }
+    if (!P.dcount) {
+        if (int rc = dalloc(e, &P.dcount, (size_t)gsx::MAX_RANKS)) return rc;
+    }
     if (m == 0) return GSX_OK;
     std::vector<gsx::DevMsg> hm(m);
     for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
@@ -1531,6 +1592,46 @@ int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new) {
         *n_new = c;
     }
     return GSX_OK;
+}
+
+int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
+    if (!e || !counts) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (e->n_send && !out) return GSX_EINVAL;
+    if (e->n_send && !e->d_dest_halo_base) return fail(e, GSX_ESTATE, "gsx_shard_set_halo_bases first");
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    const gsx::PropState& ps = P.last;
+    std::memset(counts, 0, 8 * (size_t)e->n_ranks);
+    if (ps.n_msgs == 0 || e->n_send == 0) return GSX_OK;
+    const uint64_t* front = P.hist + (size_t)P.h * ps.n_nodes * ps.n_words;
+    hipEvent_t a, b;
+    if (int rc = prop_event_pair(e, &a, &b)) return rc;
+    HIPCHK(e, hipEventRecord(a, e->stream));
+    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
+    P.sel_done = true;
+    HIPCHK(e, hipMemsetAsync(P.dcount, 0, 8 * (size_t)e->n_ranks, e->stream));
+    HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, out, P.dcount, e->stream));
+    HIPCHK(e, hipEventRecord(b, e->stream));
+    HIPCHK(e, hipMemcpyAsync(counts, P.dcount, 8 * (size_t)e->n_ranks, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_entries, uint64_t* n_new) {
+    if (!e) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (n_entries && !entries) return GSX_EINVAL;
+    if (n_entries > e->n_recv) return fail(e, GSX_ERANGE, "more entries than receive slots");
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    const gsx::PropState& ps = P.last;
+    if (ps.n_msgs && e->n_recv) {
+        HIPCHK(e, gsx::launch_halo_clear(ps, P.halo, P.halo_idx, P.halo_prev, e->stream));
+        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, e->stream));
+        P.halo_prev = n_entries;
+    }
+    return gsx_prop_step(e, e->n_recv ? P.halo : nullptr, n_new);
 }
 
 int gsx_prop_end(gsx_engine* e, gsx_prop_out* out) {

@@ -177,6 +177,89 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
     block_count<1>(cnt, ps.stats, slot);
 }
 
+// Compacted exchange: only the non-empty rows travel, as entries
+// [halo slot at the receiver][W words].  Each destination rank d owns the
+// entry range of its dense send segment (send_base[d] .. +send_count[d]); a
+// block counts its non-empty rows per destination in LDS, reserves space with
+// one global atomic per (block, destination), and writes the entries.  The
+// order of entries is not deterministic, but each carries its slot, and the
+// receiver only scatters them (k_halo_scatter), so the hop is.
+__global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const uint64_t* __restrict__ front,
+                                                           uint64_t* __restrict__ out, unsigned long long* __restrict__ dcount) {
+    __shared__ uint32_t cnt[MAX_RANKS], base[MAX_RANKS];
+    const uint32_t W = ps.n_words;
+    unsigned long long nsend[1] = {0};
+    for (uint64_t j0 = (uint64_t)blockIdx.x * 256u; j0 < ps.n_send; j0 += (uint64_t)gridDim.x * 256u) {
+        const uint64_t j = j0 + threadIdx.x;
+        if (threadIdx.x < ps.n_ranks) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        bool nz = false;
+        uint32_t d = 0, pos = 0;
+        uint32_t r = NO_PAIR, v = 0;
+        uint8_t fw = 0;
+        if (j < ps.n_send) {
+            r = ps.send_pair[j];
+            d = ps.send_dest[j];
+            if (r != NO_PAIR) {
+                v = ps.pair_obs[r];
+                fw = ps.fwd[r];
+                for (uint32_t w = 0; w < W; ++w) {
+                    const uint64_t f = front[(size_t)v * W + w];
+                    if (!f) continue;
+                    uint64_t el = elig_word(fw, ps.origin[(size_t)v * W + w]);
+                    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
+                    uint64_t c = f & el;
+                    nsend[0] += c != 0;
+                    if (c) c &= ~ps.from_mask[(size_t)r * W + w];
+                    nz |= c != 0;
+                }
+            }
+            if (nz) pos = atomicAdd(&cnt[d], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < ps.n_ranks && cnt[threadIdx.x])
+            base[threadIdx.x] = (uint32_t)atomicAdd(&dcount[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+        __syncthreads();
+        if (nz) {  // recompute the row (its inputs are cache-hot) and write the entry
+            uint64_t* e = out + (ps.send_base[d] + base[d] + pos) * (uint64_t)(W + 1);
+            e[0] = ps.dest_halo_base[d] + (j - ps.send_base[d]);
+            for (uint32_t w = 0; w < W; ++w) {
+                const uint64_t f = front[(size_t)v * W + w];
+                uint64_t c = 0;
+                if (f) {
+                    uint64_t el = elig_word(fw, ps.origin[(size_t)v * W + w]);
+                    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
+                    c = f & el & ~ps.from_mask[(size_t)r * W + w];
+                }
+                e[1 + w] = c;
+            }
+        }
+        __syncthreads();  // cnt / base are reused by the next chunk
+    }
+    const uint32_t slot[1] = {STAT_EDGE_SENDS};
+    block_count<1>(nsend, ps.stats, slot);
+}
+
+// Receiver: clear the halo rows the previous hop filled, then scatter this
+// hop's entries into the dense halo (every slot not received stays empty).
+__global__ __launch_bounds__(256) void k_halo_clear(PropState ps, uint64_t* __restrict__ halo,
+                                                    const uint32_t* __restrict__ idx, uint64_t n) {
+    const uint32_t W = ps.n_words;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+        for (uint32_t w = 0; w < W; ++w) halo[(size_t)idx[i] * W + w] = 0;
+}
+__global__ __launch_bounds__(256) void k_halo_scatter(PropState ps, uint64_t* __restrict__ halo,
+                                                      const uint64_t* __restrict__ ent, uint64_t n,
+                                                      uint32_t* __restrict__ idx) {
+    const uint32_t W = ps.n_words;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
+        const uint64_t* e = ent + i * (uint64_t)(W + 1);
+        const uint32_t slot = (uint32_t)e[0];
+        idx[i] = slot;
+        for (uint32_t w = 0; w < W; ++w) halo[(size_t)slot * W + w] = e[1 + w];
+    }
+}
+
 // ---- one hop ----------------------------------------------------------------
 // `front` holds the messages each vertex first received at hop h-1; `nxt`
 // receives those first received now.  CW words are processed per walk of
@@ -528,6 +611,25 @@ hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStr
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st) {
     if (ps.n_send == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_pack, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps, front, send);
+    return hipGetLastError();
+}
+hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, uint64_t* out,
+                                    unsigned long long* dcount, hipStream_t st) {
+    if (ps.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_pack_compact, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps,
+                       front, out, dcount);
+    return hipGetLastError();
+}
+hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_clear, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, idx, n);
+    return hipGetLastError();
+}
+hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
+                               hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, ent, n,
+                       idx);
     return hipGetLastError();
 }
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {

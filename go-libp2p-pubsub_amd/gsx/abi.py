@@ -347,6 +347,9 @@ SIGNATURES = {
     "gsx_shard_recv_plan": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32), _u64p, P(C.c_uint32), P(C.c_uint32)]),
     "gsx_shard_send_plan": (C.c_int, [C.c_void_p, _u64p, P(C.c_uint32), P(C.c_uint32)]),
     "gsx_shard_counts": (C.c_int, [C.c_void_p, _u64p, _u64p]),
+    "gsx_shard_set_halo_bases": (C.c_int, [C.c_void_p, _u64p]),
+    "gsx_prop_pack_compact": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),
+    "gsx_prop_step_compact": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, _u64p]),
     "gsx_prop_begin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig)]),
     "gsx_prop_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_step": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),

@@ -198,6 +198,7 @@ class Engine:
     def shard_recv_plan(self, rank_lo):
         """-> (recv_counts [world] u64, recv_u, recv_v): this rank's receive list."""
         rl = np.ascontiguousarray(rank_lo, dtype=np.uint32)
+        self._rank_lo = rl
         w = len(rl) - 1
         cnt = np.zeros(w, dtype=np.uint64)
         self._chk(self.lib.gsx_shard_recv_plan(self.h, w, _ptr(rl, C.c_uint32), _ptr(cnt, C.c_uint64), None, None),
@@ -215,6 +216,26 @@ class Engine:
         v = np.ascontiguousarray(req_v, dtype=np.uint32)
         self._chk(self.lib.gsx_shard_send_plan(self.h, _ptr(sc, C.c_uint64), _ptr(u, C.c_uint32),
                                                _ptr(v, C.c_uint32)), "gsx_shard_send_plan")
+
+    def shard_set_halo_bases(self, dest_halo_base):
+        b = np.ascontiguousarray(dest_halo_base, dtype=np.uint64)
+        self._chk(self.lib.gsx_shard_set_halo_bases(self.h, _ptr(b, C.c_uint64)), "gsx_shard_set_halo_bases")
+
+    def prop_pack_compact(self, out) -> np.ndarray:
+        """out: device buffer [n_send][words + 1] u64; -> entries per destination rank."""
+        p = out.data_ptr() if hasattr(out, "data_ptr") else out
+        w = len(self._rank_lo) - 1
+        cnt = np.zeros(w, dtype=np.uint64)
+        self._chk(self.lib.gsx_prop_pack_compact(self.h, C.c_void_p(p or None), _ptr(cnt, C.c_uint64)),
+                  "gsx_prop_pack_compact")
+        return cnt
+
+    def prop_step_compact(self, entries, n: int) -> int:
+        p = entries.data_ptr() if hasattr(entries, "data_ptr") else entries
+        v = C.c_uint64()
+        self._chk(self.lib.gsx_prop_step_compact(self.h, C.c_void_p(p or None), n, C.byref(v)),
+                  "gsx_prop_step_compact")
+        return int(v.value)
 
     def shard_counts(self):
         a, b = C.c_uint64(), C.c_uint64()

@@ -102,13 +102,25 @@ def exchange_plan(backend, rank_lo, transport) -> None:
     g = got.cpu().numpy()
     backend.shard_send_plan(asked.astype(np.uint64), g[:, 0].astype(np.uint32), g[:, 1].astype(np.uint32))
     backend._plan_counts = (asked.astype(np.int64), counts.astype(np.int64))
+    # compacted exchange: tell every source where its rows start in my halo
+    base = np.concatenate([[0], np.cumsum(counts.astype(np.int64))[:-1]])
+    mine = torch.tensor(base, dtype=torch.int64, device=dev)
+    theirs = torch.empty(W, dtype=torch.int64, device=dev)
+    transport.all_to_all(theirs, mine, [1] * W, [1] * W)
+    backend.shard_set_halo_bases(theirs.cpu().numpy().astype(np.uint64))
 
 
 class RangeSharded:
-    """Range-sharded propagation over one engine per rank."""
+    """Range-sharded propagation over one engine per rank.
 
-    def __init__(self, backend, rank_lo, transport):
+    compact=True (default): per hop only the non-empty cross-shard rows
+    travel, as (receive slot, row) entries — one small all-to-all of the
+    entry counts, then the entries; compact=False moves every cross pair's
+    row (fixed splits, one collective per hop)."""
+
+    def __init__(self, backend, rank_lo, transport, compact=True):
         self.be = backend
+        self.compact = compact
         self.rank_lo = np.asarray(rank_lo, dtype=np.uint32)
         self.tp = transport
         exchange_plan(backend, self.rank_lo, transport)
@@ -116,6 +128,7 @@ class RangeSharded:
         self.n_send = int(self.send_counts.sum())
         self.n_recv = int(self.recv_counts.sum())
         self._bufs = {}
+        self.sent_bytes = 0  # exchange volume this rank sent (cumulative)
         dev = getattr(transport, "device", None)
         if hasattr(backend, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
             # engine kernels and the collectives on one stream: pack -> all-to-all -> step in order
@@ -129,18 +142,48 @@ class RangeSharded:
                               torch.zeros((max(self.n_recv, 1), W), dtype=torch.int64, device=dev))}
         return self._bufs[W]
 
+    def _compact_buffers(self, W):
+        torch = _torch()
+        key = ("c", W)
+        if key not in self._bufs:
+            dev = self.tp.device
+            self._bufs = {key: (torch.zeros((max(self.n_send, 1), W + 1), dtype=torch.int64, device=dev),
+                                torch.zeros((max(self.n_recv, 1), W + 1), dtype=torch.int64, device=dev))}
+        return self._bufs[key]
+
+    def _hop_compact(self, W):
+        torch = _torch()
+        be, tp = self.be, self.tp
+        out, recv = self._compact_buffers(W)
+        cnt = be.prop_pack_compact(out).astype(np.int64)  # entries per destination
+        sc = torch.tensor(cnt, dtype=torch.int64, device=tp.device)
+        rc = torch.empty_like(sc)
+        tp.all_to_all(rc, sc, [1] * tp.world, [1] * tp.world)
+        rcnt = rc.cpu().numpy()
+        sb = np.concatenate([[0], np.cumsum(self.send_counts)[:-1]])
+        send = torch.cat([out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(tp.world)], 0)
+        n = int(rcnt.sum())
+        tp.all_to_all(recv[:n], send, rcnt, cnt)
+        self.sent_bytes += int(cnt.sum()) * (W + 1) * 8
+        return be.prop_step_compact(recv, n)
+
     def propagate(self, msgs, cfg: abi.PropConfig):
         """-> (this rank's PropOut as a dict, global totals dict)."""
         torch = _torch()
         be, tp = self.be, self.tp
         W = prop_words(len(msgs))
-        send, recv = self._buffers(W)
+        if not self.compact:
+            send, recv = self._buffers(W)
         be.prop_begin(msgs, cfg)
         flag = torch.zeros(1, dtype=torch.int64, device=tp.device)
         for _ in range(cfg.max_hops):
-            be.prop_pack(send)
-            tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
-            n_new = be.prop_step(recv)
+            if self.compact:
+                n_new = self._hop_compact(W)
+            else:
+                be.prop_pack(send)
+                tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
+                self.sent_bytes += self.n_send * W * 8
+                n_new = be.prop_step(recv)
             flag.fill_(n_new)
             tp.all_reduce_sum(flag)
             if int(flag.item()) == 0:

@@ -438,6 +438,11 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
                         uint32_t* recv_u, uint32_t* recv_v);
 int gsx_shard_send_plan(gsx_engine* e, const uint64_t* send_counts, const uint32_t* req_u, const uint32_t* req_v);
 int gsx_shard_counts(gsx_engine* e, uint64_t* n_send, uint64_t* n_recv);
+/* Compacted exchange (only non-empty rows travel): dest_halo_base[k] = the
+ * receive slot, on rank k, of the first row this rank sends to k (rank k's
+ * receive slots run source rank by source rank, so it is the sum of what
+ * k receives from ranks below this one). */
+int gsx_shard_set_halo_bases(gsx_engine* e, const uint64_t* dest_halo_base);
 
 /* Stepped propagation (any engine; required on a shard).  gsx_propagate is
  * begin + max_hops steps + end.  send / recv are device pointers (rows of
@@ -447,6 +452,14 @@ int gsx_prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
 int gsx_prop_pack(gsx_engine* e, uint64_t* send);
 int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new);
 int gsx_prop_end(gsx_engine* e, gsx_prop_out* out);
+/* Compacted per-hop exchange: out (device, n_send x (words + 1) u64) gets,
+ * for destination k, counts[k] (host) entries [receive slot on k][words]
+ * starting at entry send_base[k] (the dense segment's first slot); only
+ * non-empty rows are written.  The receiver passes the entries it got (in
+ * any order, concatenated) to gsx_prop_step_compact, which scatters them
+ * into the engine's own halo and runs the hop. */
+int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts);
+int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_entries, uint64_t* n_new);
 
 /* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
 

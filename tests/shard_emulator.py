@@ -96,6 +96,12 @@ class EmuShard:
 
     def shard_send_plan(self, send_counts, req_u, req_v):
         self.send_pair = [self._find(int(v) - self.lo, int(u)) for u, v in zip(req_u, req_v)]
+        self.send_counts = np.asarray(send_counts, dtype=np.int64)
+        self.send_base = np.concatenate([[0], np.cumsum(self.send_counts)])
+        self.n_recv = sum(1 for r in self.rev if r is not None and r[0] == "halo")
+
+    def shard_set_halo_bases(self, bases):
+        self.halo_base = np.asarray(bases, dtype=np.int64)
 
     # -- stepped propagation ----------------------------------------------------------
     def prop_begin(self, msgs, cfg):
@@ -129,6 +135,32 @@ class EmuShard:
         rows = [self._send_row(r) if r is not None else [0] * self.W for r in self.send_pair]
         a = np.array(rows, dtype=np.uint64).reshape(-1, self.W) if rows else np.zeros((0, self.W), np.uint64)
         send[: len(rows)].copy_(_as_tensor(a.view(np.int64)))
+
+    def prop_pack_compact(self, out):
+        """Entries [receive slot at the destination][row] of the non-empty rows,
+        destination d's from entry send_base[d] on (gsx_prop_pack_compact)."""
+        cnt = np.zeros(len(self.send_counts), dtype=np.uint64)
+        rows = []
+        for d in range(len(self.send_counts)):
+            for j in range(int(self.send_base[d]), int(self.send_base[d + 1])):
+                r = self.send_pair[j]
+                row = self._send_row(r) if r is not None else [0] * self.W
+                if any(row):
+                    rows.append((int(self.send_base[d] + cnt[d]), [int(self.halo_base[d] + j - self.send_base[d])] + row))
+                    cnt[d] += 1
+        if rows:
+            a = np.zeros((len(self.send_pair), self.W + 1), dtype=np.uint64)
+            for pos, e in rows:
+                a[pos] = e
+            out[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+        return cnt
+
+    def prop_step_compact(self, entries, n):
+        halo = np.zeros((max(self.n_recv, 1), self.W), dtype=np.uint64)
+        e = entries[:n].numpy().view(np.uint64)
+        for row in e:
+            halo[int(row[0])] = row[1:]
+        return self.prop_step(_as_tensor(halo.view(np.int64)))
 
     def prop_step(self, recv):
         halo = recv.numpy().view(np.uint64) if len(recv) else None

@@ -34,17 +34,20 @@ def _slice_state(st, T, E, a, b):
 
 
 CASES = [
-    # world, n, d, T, router, flood_publish, m, mix, disconnect
-    (2, 1500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, 0.02),
-    (2, 2000, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, True, 0.03),
-    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 100, True, 0.0),
-    (4, 1600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 64, True, 0.02),
+    # world, n, d, T, router, flood_publish, m, mix, disconnect, compact
+    (2, 1500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, 0.02, False),
+    (2, 1500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, 0.02, True),
+    (2, 2000, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, True, 0.03, True),
+    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 100, True, 0.0, False),
+    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 100, True, 0.0, True),
+    (4, 1600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 64, True, 0.02, True),
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"w{c[0]}-r{c[4]}-m{c[6]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES,
+                         ids=[f"w{c[0]}-r{c[4]}-m{c[6]}-{'compact' if c[9] else 'dense'}" for c in CASES])
 def test_range_sharded_matches_single_engine(gpu_ok, case):
-    world, n, d, T, router, fp, m, mix, disc = case
+    world, n, d, T, router, fp, m, mix, disc, compact = case
     seed = 3 * n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
     msgs = pc.messages(n, m, seed)
@@ -70,7 +73,7 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
         engines.append((e, a, b))
 
     def run(tp, e):
-        rs = shard.RangeSharded(e, rank_lo, tp)
+        rs = shard.RangeSharded(e, rank_lo, tp, compact=compact)
         return rs.propagate(msgs, cfg)
 
     res = shard.run_local(world, "cuda:0", run, [(e,) for e, _, _ in engines])

@@ -54,7 +54,7 @@ def _worker(rank, world, port, payload, q):
             sh = payload["shards"][rank]
             rp = payload["row_ptr"]
             be = emu.EmuShard(sh, payload["fwd"][int(rp[sh.node_lo]) : int(rp[sh.node_hi])])
-            rs = gs.RangeSharded(be, payload["rank_lo"], tp)
+            rs = gs.RangeSharded(be, payload["rank_lo"], tp, compact=payload["compact"])
             local, tot = rs.propagate(payload["msgs"], cfg)
             hop, frm = be.prop_results(len(payload["msgs"]))
             q.put((rank, local, tot, hop, frm))
@@ -99,18 +99,19 @@ def _reference(ov, T, seed, msgs, cfg):
 
 
 CASES = [
-    # world, n, d, router, flood_publish, m, mix
-    (2, 240, 3, abi.GSX_ROUTER_FLOODSUB, 0, 64, False),
-    (2, 200, 4, abi.GSX_ROUTER_GOSSIPSUB, 0, 100, True),
-    (3, 180, 3, abi.GSX_ROUTER_GOSSIPSUB, 1, 40, True),
+    # world, n, d, router, flood_publish, m, mix, compact
+    (2, 240, 3, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, False),
+    (2, 240, 3, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, True),
+    (2, 200, 4, abi.GSX_ROUTER_GOSSIPSUB, 0, 100, True, True),
+    (3, 180, 3, abi.GSX_ROUTER_GOSSIPSUB, 1, 40, True, True),
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"w{c[0]}-r{c[3]}-m{c[5]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[f"w{c[0]}-r{c[3]}-m{c[5]}-{'compact' if c[7] else 'dense'}" for c in CASES])
 def test_range_sharded_gloo_matches_oracle(case):
     import shard_emulator as emu
 
-    world, n, d, router, fp, m, mix = case
+    world, n, d, router, fp, m, mix, compact = case
     seed = 7 * n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
     msgs = pc.messages(n, m, seed)
@@ -122,7 +123,7 @@ def test_range_sharded_gloo_matches_oracle(case):
     rank_lo = synth.shard_ranges(n, world)
     shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
     payload = dict(mode="range", shards=shards, fwd=fwd, row_ptr=ov.row_ptr, rank_lo=rank_lo, msgs=msgs,
-                   cfg=_cfg_dict(cfg))
+                   cfg=_cfg_dict(cfg), compact=compact)
     res = _run(world, payload)
     got_hop = np.concatenate([r[3] for r in res], axis=1)
     got_frm = np.concatenate([r[4] for r in res], axis=1)
