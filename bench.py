@@ -273,6 +273,86 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     return out
 
 
+def adversarial_leg(args, rank, world, local, dist, dev):
+    """20 % sybils in IP groups of 50 attacking victim nodes
+    (P6) with invalid-message counters (P4); observers range-sharded over the
+    ranks.  Times refreshScores()+score() and reports how the scores treat the
+    sybils; at N=1 also two heartbeats and the sybil mesh links they prune."""
+    import torch
+
+    n = args.adv_peers
+    rl = synth.shard_ranges(n, world)
+    t = time.time()
+    sh = synth.adversarial_shards(n, rl, seed=synth.SEED + 2, ranks=[rank])[0]
+    n_syb = int(round(0.2 * n))
+    e = gsx.Engine(1, device=local)
+    e.set_peer_params(synth.bench_peer_params())
+    e.set_topic_params(0, synth.spam_test_topic_params())
+    th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                        accept_px_threshold=0, opportunistic_graft_threshold=5)
+    e.set_thresholds(th)
+    e.load_overlay_shard(n, sh.node_lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+    E = sh.n_pairs
+    e.synthesize_state(
+        abi.SynthSpec(seed=synth.SEED + 2, now_ns=T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0,
+                      imd_max_sybil=100.0, p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0,
+                      p_disconnected=0.0, p_absent=0.0, expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n - n_syb))
+    e.set_app_scores(np.zeros(E))
+    log(f"[bench] cfg5 shard nodes={sh.node_hi - sh.node_lo}/{n} pairs={E} in {time.time() - t:.1f}s")
+    now = T0
+    for _ in range(2):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+    if dist is not None:
+        dist.barrier()
+    steps = max(1, args.steps)
+    e.timing_begin(steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+    el = reduce_scalar(time.perf_counter() - t0, dist, dev, "max")
+    k_total, _, _, k_n = e.timing_end()
+    recs = reduce_scalar(float(E) * steps, dist, dev, "sum")
+    sc = e.scores()
+    syb = sh.sybil[sh.col]
+    below = np.count_nonzero(sc[syb] < th.graylist_threshold)
+    out = {
+        "metric": "peer-topic score updates/s",
+        "value": recs / el,
+        "peers": n,
+        "sybil_fraction": 0.2,
+        "sybils_per_ip": 50,
+        "pairs_rank0": E,
+        "ms_per_refresh": el / steps * 1e3,
+        "kernel_avg_ms_rank0": k_total / max(1, k_n),
+        "sybil_pairs_rank0": int(syb.sum()),
+        "sybil_pairs_below_graylist_rank0": int(below),
+        "honest_pairs_below_graylist_rank0": int(np.count_nonzero(sc[~syb] < th.graylist_threshold)),
+    }
+    if world == 1 and args.hb_steps > 0:
+        def sybil_links():
+            st = e.export_state()
+            return int(np.count_nonzero(((st["rec_flags"] & abi.GSX_REC_IN_MESH) != 0) & syb))
+
+        before = sybil_links()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        hbs = []
+        for k in range(2):
+            now += abi.SECOND
+            hbs.append(e.heartbeat(59 + k, now, synth.SEED).as_dict())
+        e.sync()
+        out["heartbeat_ms_per_round"] = (time.perf_counter() - t0) / 2 * 1e3
+        out["sybil_mesh_links_before"] = before
+        out["sybil_mesh_links_after"] = sybil_links()
+        out["heartbeat_first_round"] = hbs[0]
+    e.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,6 +368,7 @@ def main():
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
+    ap.add_argument("--adv-peers", type=int, default=4_000_000, help="cfg5 adversarial overlay (0: skip)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on one GPU: all ranks on device 0, gloo (host-staged) instead of RCCL")
     args = ap.parse_args()
@@ -405,6 +486,8 @@ def main():
             "last_round": outs[-1],
         }
 
+    adv = adversarial_leg(args, rank, world, local, dist, dev) if args.adv_peers > 0 else None
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -481,6 +564,7 @@ def main():
         "parity_vs_oracle": parity,
         "propagation": prop,
         "heartbeat": hb,
+        "adversarial": adv,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -24,6 +24,7 @@ TAG_SRC = 3
 TAG_STATE = 4
 TAG_IP = 5
 TAG_EVENT = 6
+TAG_VICTIM = 9
 
 
 def _mix(z: np.ndarray) -> np.ndarray:
@@ -122,6 +123,51 @@ def _ips(n, sybil_frac, sybils_per_ip):
         sid = np.arange(n_syb, dtype=np.int64) // sybils_per_ip
         ips[n - n_syb :, 0] = (n + sid).astype(np.uint32)
     return ips, sybil
+
+
+def _adversarial_keys(n: int, d: int, seed: int, sybil_frac: float, sybils_per_ip: int, victims: int):
+    """BASELINE.md cfg5: honest nodes dial like connectSome over all n nodes;
+    the sybils (the last sybil_frac*n nodes, sybils_per_ip of them per IP)
+    attack in IP groups: every sybil of group g dials the same `victims`
+    honest nodes h(seed, VICTIM, g, k) mod n_honest, so each victim sees a
+    whole group on one IP (P6, score.go:337-381)."""
+    n_syb = int(round(sybil_frac * n))
+    n_h = n - n_syb
+    i = np.repeat(np.arange(n_h, dtype=np.uint64), d)
+    k = np.tile(np.arange(d, dtype=np.uint64), n_h)
+    j = h(seed, TAG_OVL, i, k) % np.uint64(n)
+    self_ = j == i
+    j[self_] = (i[self_] + np.uint64(1)) % np.uint64(n)
+    si = np.repeat(np.arange(n_h, n, dtype=np.uint64), victims)
+    grp = (si - np.uint64(n_h)) // np.uint64(sybils_per_ip)
+    kk = np.tile(np.arange(victims, dtype=np.uint64), n_syb)
+    sj = h(seed, TAG_VICTIM, grp, kk) % np.uint64(max(n_h, 1))
+    i = np.concatenate([i, si]).astype(np.int64)
+    j = np.concatenate([j, sj]).astype(np.int64)
+    dial_key = np.unique(i * n + j)
+    und = np.unique(np.minimum(i, j) * n + np.maximum(i, j))
+    return und, dial_key
+
+
+def adversarial_overlay(n: int, d: int = 6, seed: int = SEED, sybil_frac: float = 0.2, sybils_per_ip: int = 50,
+                        victims: int = 6, flags: int = abi.GSX_EDGE_GOSSIPSUB) -> Overlay:
+    """cfg5 overlay (see _adversarial_keys); IPs as in connect_some_overlay."""
+    und, dial_key = _adversarial_keys(n, d, seed, sybil_frac, sybils_per_ip, victims)
+    row_ptr, col, ef = _rows(n, und, dial_key, 0, n, flags)
+    ips, sybil = _ips(n, sybil_frac, sybils_per_ip)
+    return Overlay(n, row_ptr, col, ef, ips, sybil)
+
+
+def adversarial_shards(n: int, rank_lo, d: int = 6, seed: int = SEED, sybil_frac: float = 0.2,
+                       sybils_per_ip: int = 50, victims: int = 6, flags: int = abi.GSX_EDGE_GOSSIPSUB, ranks=None):
+    und, dial_key = _adversarial_keys(n, d, seed, sybil_frac, sybils_per_ip, victims)
+    ips, sybil = _ips(n, sybil_frac, sybils_per_ip)
+    out = []
+    for k in range(len(rank_lo) - 1) if ranks is None else ranks:
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        row_ptr, col, ef = _rows(n, und, dial_key, lo, hi, flags)
+        out.append(OverlayShard(n, lo, hi, row_ptr, col, ef, ips, sybil))
+    return out
 
 
 def connect_some_overlay(

@@ -1,0 +1,33 @@
+"""cfg5 (sybil IP groups + invalid-message spam) on the GPU vs the CPU
+oracle: scores after refresh and the state after two heartbeats, bit-exact."""
+import numpy as np
+import pytest
+
+import adversarial_cases as ac
+import gsx
+import heartbeat_cases as hc
+import oracle as orc
+from gsx import abi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [2500, 12000])
+def test_adversarial_matches_oracle(gpu_ok, n):
+    res = []
+    for be in (gsx.Engine(1), orc.Oracle(1)):
+        ov = ac.setup(be, n, seed=n)
+        snaps = [hc.snapshot(be)]
+        for k in range(2):
+            out = be.heartbeat(59 + k, ac.T0 + (2 + k) * abi.SECOND, 9).as_dict()
+            be.refresh(ac.T0 + (2 + k) * abi.SECOND + 500 * abi.MILLISECOND)
+            snaps.append((out, hc.snapshot(be)))
+        res.append(snaps)
+    g, w = res
+    for f in list(abi.STATE_FIELDS) + ["scores"]:
+        assert np.array_equal(np.asarray(g[0][f]).view(np.uint8), np.asarray(w[0][f]).view(np.uint8)), f
+    for k in (1, 2):
+        assert g[k][0] == w[k][0], k
+        for f in list(abi.STATE_FIELDS) + ["backoff", "scores", "ihave_len", "ihave_digest"]:
+            assert np.array_equal(np.asarray(g[k][1][f]).view(np.uint8), np.asarray(w[k][1][f]).view(np.uint8)), (k, f)
+    assert g[1][0]["prunes"] > 0
