@@ -332,22 +332,35 @@ def adversarial_leg(args, rank, world, local, dist, dev):
         "sybil_pairs_below_graylist_rank0": int(below),
         "honest_pairs_below_graylist_rank0": int(np.count_nonzero(sc[~syb] < th.graylist_threshold)),
     }
-    if world == 1 and args.hb_steps > 0:
+    if args.hb_steps > 0:
+        # heartbeats over the shards: GRAFT/PRUNE words of cross-shard pairs
+        # go to their receivers' ranks and the answers come back (gsx_hb_*)
+        runner = None
+        if dist is not None:
+            runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
+
         def sybil_links():
             st = e.export_state()
-            return int(np.count_nonzero(((st["rec_flags"] & abi.GSX_REC_IN_MESH) != 0) & syb))
+            return reduce_scalar(float(np.count_nonzero(((st["rec_flags"] & abi.GSX_REC_IN_MESH) != 0) & syb)),
+                                 dist, dev, "sum")
 
         before = sybil_links()
+        if dist is not None:
+            dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         hbs = []
         for k in range(2):
             now += abi.SECOND
-            hbs.append(e.heartbeat(59 + k, now, synth.SEED).as_dict())
+            if runner is None:
+                hbs.append(e.heartbeat(59 + k, now, synth.SEED).as_dict())
+            else:
+                hbs.append(runner.heartbeat(59 + k, now, synth.SEED)[1])
         e.sync()
-        out["heartbeat_ms_per_round"] = (time.perf_counter() - t0) / 2 * 1e3
-        out["sybil_mesh_links_before"] = before
-        out["sybil_mesh_links_after"] = sybil_links()
+        torch.cuda.synchronize(dev)
+        out["heartbeat_ms_per_round"] = reduce_scalar(time.perf_counter() - t0, dist, dev, "max") / 2 * 1e3
+        out["sybil_mesh_links_before"] = int(before)
+        out["sybil_mesh_links_after"] = int(sybil_links())
         out["heartbeat_first_round"] = hbs[0]
     e.close()
     return out

@@ -243,6 +243,8 @@ struct HbState {
     uint64_t* ctl_graft;  // per pair (v -> u): bit t = v sent GRAFT(t) this round
     uint64_t* ctl_prune;  // per pair (v -> u): bit t = v sent PRUNE(t)
     uint64_t* resp;       // per pair (u -> v): bit t = u answers v's GRAFT(t) with PRUNE
+    const uint64_t* halo_ctl;   // [receive slot][2]: GRAFT / PRUNE bits of remote senders (shards)
+    const uint64_t* halo_resp;  // [receive slot]: PRUNE answers of remote receivers (shards)
     uint8_t* dirty;       // per pair: grafted / pruned by its owner's maintenance this round
     unsigned long long* stats;
     uint32_t* rngk;        // per node: draw counter after the maintenance of the current topic
@@ -255,6 +257,7 @@ struct HbState {
     double gossip_threshold;
     uint64_t n_pairs;
     uint32_t n_nodes;
+    uint32_t node_lo;  // global id of local node 0 (range shards)
     uint64_t tick;
     int64_t now;
     uint64_t seed;
@@ -270,6 +273,8 @@ constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip 
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
+                          uint64_t* out, hipStream_t st);
 
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);

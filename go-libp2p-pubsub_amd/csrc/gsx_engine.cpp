@@ -106,6 +106,8 @@ struct gsx_engine {
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
     uint64_t* d_ihave_hash = nullptr;
     bool have_gossip = false;
+    gsx::HbState hb{};  // the round in flight (gsx_hb_begin .. gsx_hb_end)
+    bool hb_active = false;
 
     // mcache (mcache.go): windows of cached gossipsub batches, front = history[0]
     struct McBatch {
@@ -1740,14 +1742,19 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
     return GSX_OK;
 }
 
-int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
-    if (!e || !out) return GSX_EINVAL;
+namespace {
+// The heartbeat round in three steps, so that a range shard can exchange the
+// control words of its cross-shard pairs between them (gsx.h):
+//   hb_begin  (A) maintenance + emitGossip of every (node, topic), GRAFT/PRUNE bits per pair;
+//   hb_recv   (B) handleGraft / handlePrune at the receivers (remote senders' bits from halo_ctl);
+//   hb_end    (C) the senders handle the PRUNE answers (remote answers from halo_resp), counters,
+//             mcache.Shift.
+int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
-    if (e->sharded())  // GRAFT/PRUNE to remote owners needs the control exchange
-        return fail(e, GSX_ESTATE, "heartbeat on a range shard is not supported");
+    if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
+        return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
     if (e->max_deg > gsx::HB_MAX_DEG)
         return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_MAX_DEG) + " peers per node");
-    std::memset(out, 0, sizeof(*out));
     const size_t TE = (size_t)e->T * e->E;
     if (!e->d_hbstats) {
         int rc = 0;
@@ -1777,6 +1784,7 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     h.stats = e->d_hbstats;
     h.n_pairs = e->E;
     h.n_nodes = e->n_nodes;
+    h.node_lo = e->node_lo;
     h.tick = tick;
     h.now = now;
     h.seed = seed;
@@ -1859,8 +1867,26 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     }
     // the receivers score the senders as the round left them
     HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    e->hb = h;
+    e->hb_active = true;
+    return GSX_OK;
+}
+
+int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
+    gsx::HbState h = e->hb;
+    h.halo_ctl = halo_ctl;
+    const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
     HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    return GSX_OK;
+}
+
+int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
+    gsx::HbState h = e->hb;
+    h.halo_resp = halo_resp;
+    const gsx::DevState ds = dev_state(e);
+    e->hb_active = false;
+    std::memset(out, 0, sizeof(*out));
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     HIPCHK(e, gsx::launch_hb_mesh_links(ds, h, e->stream));
     e->scores_valid = false;
@@ -1878,6 +1904,55 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     }
     e->mc.emplace_front();
     return GSX_OK;
+}
+
+}  // namespace
+
+int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (e->loaded && e->sharded()) return fail(e, GSX_ESTATE, "sharded engine: drive the round with gsx_hb_*");
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    if (int rc = hb_begin(e, tick, now, seed)) return rc;
+    if (int rc = hb_recv(e, nullptr)) return rc;
+    return hb_end(e, nullptr, out);
+}
+
+int gsx_hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
+    if (!e) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    return hb_begin(e, tick, now, seed);
+}
+
+int gsx_hb_pack_ctl(gsx_engine* e, uint64_t* send) {
+    if (!e) return GSX_EINVAL;
+    if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
+    if (e->n_send && !send) return GSX_EINVAL;
+    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, e->d_ctl_graft, e->d_ctl_prune, send, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
+    if (!e) return GSX_EINVAL;
+    if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
+    if (e->n_recv && !halo_ctl) return GSX_EINVAL;
+    return hb_recv(e, halo_ctl);
+}
+
+int gsx_hb_pack_resp(gsx_engine* e, uint64_t* send) {
+    if (!e) return GSX_EINVAL;
+    if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
+    if (e->n_send && !send) return GSX_EINVAL;
+    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, e->d_resp, nullptr, send, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
+    if (!e || !out) return GSX_EINVAL;
+    if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
+    if (e->n_recv && !halo_resp) return GSX_EINVAL;
+    return hb_end(e, halo_resp, out);
 }
 
 int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest) {

@@ -213,8 +213,10 @@ struct HbUnit {
     }
 };
 
+// Draws are keyed by the GLOBAL node id, so a range shard draws what the
+// whole-overlay engine draws for the same node.
 __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, uint32_t k) {
-    return Rng{h.seed, TAG_HEARTBEAT, v, (h.tick << 32) | ((uint64_t)t << 24), k};
+    return Rng{h.seed, TAG_HEARTBEAT, (uint64_t)h.node_lo + v, (h.tick << 32) | ((uint64_t)t << 24), k};
 }
 
 // One launch per topic, ascending: the maintenance of (v, t) for every v.
@@ -450,7 +452,14 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
         for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
             const uint32_t r = h.rev[q];     // r = (v -> u), the sender's pair
             if (r == NO_PAIR) continue;
-            uint64_t grafts = h.ctl_graft[r], prunes = h.ctl_prune[r];
+            uint64_t grafts, prunes;
+            if (r & HALO) {  // v on another shard: its control bits came through the exchange
+                grafts = h.halo_ctl[2 * (size_t)(r & ~HALO)];
+                prunes = h.halo_ctl[2 * (size_t)(r & ~HALO) + 1];
+            } else {
+                grafts = h.ctl_graft[r];
+                prunes = h.ctl_prune[r];
+            }
             if (!(grafts | prunes)) continue;
             const double score = s.score[q];  // gs.score.Score(p) once per control message
             const uint8_t ef = h.eflags[q];
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
     uint64_t handled = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {  // r = (v -> u)
         const uint32_t q = h.rev[r];
-        uint64_t resp = q == NO_PAIR ? 0 : h.resp[q];
+        uint64_t resp = q == NO_PAIR ? 0 : (q & HALO) ? h.halo_resp[q & ~HALO] : h.resp[q];
         // AcceptFrom at v for the answering peer
         if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
         for (; resp; resp &= resp - 1) {
@@ -531,6 +540,19 @@ __global__ __launch_bounds__(256) void k_hb_mesh_links(DevState s, HbState h) {
         if (s.pflags[r] & PAIR_PRESENT)
             for (uint32_t t = 0; t < s.n_topics; ++t) c += (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH) != 0;
     flush_count(h.stats, HB_MESH_LINKS, c);
+}
+
+// Shard exchange of per-pair control words: send slot j carries the words of
+// the local pair send_pair[j] (0 for NO_PAIR), K words per slot.
+__global__ __launch_bounds__(256) void k_hb_pack(const uint32_t* __restrict__ send_pair, uint64_t n_send,
+                                                 const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                 uint64_t* __restrict__ out) {
+    const int K = b ? 2 : 1;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = send_pair[j];
+        out[K * j] = r == NO_PAIR ? 0 : a[r];
+        if (b) out[K * j + 1] = r == NO_PAIR ? 0 : b[r];
+    }
 }
 
 static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -579,6 +601,13 @@ hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_answer, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
+                          uint64_t* out, hipStream_t st) {
+    if (n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_pack, dim3(grid_cap(n_send, 256)), dim3(256), 0, st, send_pair, n_send, a, b, out);
     return hipGetLastError();
 }
 

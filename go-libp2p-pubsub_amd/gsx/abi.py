@@ -357,6 +357,11 @@ SIGNATURES = {
     "gsx_default_gossipsub_params": (C.c_int, [P(GossipSubParams)]),
     "gsx_set_gossipsub_params": (C.c_int, [C.c_void_p, P(GossipSubParams)]),
     "gsx_heartbeat": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64, P(HeartbeatOut)]),
+    "gsx_hb_begin": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64]),
+    "gsx_hb_pack_ctl": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_hb_recv": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_hb_pack_resp": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_hb_end": (C.c_int, [C.c_void_p, C.c_void_p, P(HeartbeatOut)]),
     "gsx_export_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),

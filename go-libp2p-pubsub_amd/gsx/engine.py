@@ -294,6 +294,27 @@ class Engine:
         self._chk(self.lib.gsx_heartbeat(self.h, tick, now, seed, C.byref(out)), "gsx_heartbeat")
         return out
 
+    @staticmethod
+    def _p(t):
+        return C.c_void_p((t.data_ptr() if hasattr(t, "data_ptr") else t) or None)
+
+    def hb_begin(self, tick: int, now: int, seed: int):
+        self._chk(self.lib.gsx_hb_begin(self.h, tick, now, seed), "gsx_hb_begin")
+
+    def hb_pack_ctl(self, send):
+        self._chk(self.lib.gsx_hb_pack_ctl(self.h, self._p(send)), "gsx_hb_pack_ctl")
+
+    def hb_recv(self, halo_ctl):
+        self._chk(self.lib.gsx_hb_recv(self.h, self._p(halo_ctl)), "gsx_hb_recv")
+
+    def hb_pack_resp(self, send):
+        self._chk(self.lib.gsx_hb_pack_resp(self.h, self._p(send)), "gsx_hb_pack_resp")
+
+    def hb_end(self, halo_resp) -> abi.HeartbeatOut:
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.gsx_hb_end(self.h, self._p(halo_resp), C.byref(out)), "gsx_hb_end")
+        return out
+
     def export_backoff(self) -> np.ndarray:
         b = np.empty((self.n_topics, self.n_pairs), dtype=np.int64)
         self._chk(self.lib.gsx_export_backoff(self.h, _ptr(b, C.c_int64)), "gsx_export_backoff")

@@ -192,6 +192,33 @@ class RangeSharded:
         return out_dict(out), totals(out, tp)
 
 
+    def heartbeat(self, tick: int, now: int, seed: int):
+        """One heartbeat round of every node on every rank (gossipsub.go:1303-1564
+        with handleGraft / handlePrune): the GRAFT/PRUNE words of the
+        cross-shard pairs go to the receivers' ranks (one all-to-all), the
+        PRUNE answers come back (a second, smaller one).  -> (this rank's
+        counters, summed counters)."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        dev = tp.device
+        s2 = torch.zeros((max(self.n_send, 1), 2), dtype=torch.int64, device=dev)
+        r2 = torch.zeros((max(self.n_recv, 1), 2), dtype=torch.int64, device=dev)
+        be.hb_begin(tick, now, seed)
+        be.hb_pack_ctl(s2)
+        tp.all_to_all(r2[: self.n_recv], s2[: self.n_send], self.recv_counts, self.send_counts)
+        be.hb_recv(r2)
+        s1 = torch.zeros(max(self.n_send, 1), dtype=torch.int64, device=dev)
+        r1 = torch.zeros(max(self.n_recv, 1), dtype=torch.int64, device=dev)
+        be.hb_pack_resp(s1)
+        tp.all_to_all(r1[: self.n_recv], s1[: self.n_send], self.recv_counts, self.send_counts)
+        out = be.hb_end(r1)
+        d = out.as_dict()
+        t = torch.tensor([d[k] for k, _ in abi.HeartbeatOut._fields_], dtype=torch.int64, device=dev)
+        tp.all_reduce_sum(t)
+        t = t.cpu().numpy()
+        return d, {k: int(t[i]) for i, (k, _) in enumerate(abi.HeartbeatOut._fields_)}
+
+
 class MessageParallel:
     """Every rank propagates its block of the messages over the full overlay."""
 

@@ -525,6 +525,18 @@ typedef struct gsx_heartbeat_out {
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
+/* The same round in steps, for a range shard (required there; any engine
+ * may use them): gsx_hb_begin runs (A); gsx_hb_pack_ctl writes, per send
+ * slot of the shard plan, the GRAFT and PRUNE bits of the pair it carries
+ * ([n_send][2] u64, device); after the all-to-all, gsx_hb_recv runs (B) with
+ * the received [n_recv][2] words; gsx_hb_pack_resp writes the PRUNE answers
+ * per send slot ([n_send] u64); after the second all-to-all gsx_hb_end runs
+ * (C), fills *out with this rank's counters and shifts the message cache. */
+int gsx_hb_begin(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed);
+int gsx_hb_pack_ctl(gsx_engine* e, uint64_t* send);
+int gsx_hb_recv(gsx_engine* e, const uint64_t* halo_ctl);
+int gsx_hb_pack_resp(gsx_engine* e, uint64_t* send);
+int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out);
 /* backoff expiry per [topic][pair] (0 = no entry), n_topics * n_pairs
  * (gs.backoff, gossipsub.go:436; zeroed by gsx_load_overlay) */
 int gsx_export_backoff(gsx_engine* e, int64_t* out);

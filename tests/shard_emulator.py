@@ -103,6 +103,55 @@ class EmuShard:
     def shard_set_halo_bases(self, bases):
         self.halo_base = np.asarray(bases, dtype=np.int64)
 
+    # -- stepped heartbeat: exchange plumbing only ---------------------------------------
+    # The control words a pair carries are stand-ins naming the pair
+    # ((sender << 32 | receiver) for GRAFT, its complement for PRUNE, the
+    # answer as (receiver << 32 | sender)); hb_recv / hb_end check that every
+    # receive slot got exactly the words of its pair's reverse.
+    def _pair_ids(self, r):
+        return int(self.obs[r]) + self.lo, int(self.col[r])
+
+    def hb_begin(self, tick, now, seed):
+        self.hb_checked = 0
+
+    def hb_pack_ctl(self, send):
+        a = np.zeros((len(self.send_pair), 2), dtype=np.uint64)
+        for j, r in enumerate(self.send_pair):
+            if r is not None:
+                v, u = self._pair_ids(r)
+                a[j] = (v << 32 | u, ~(v << 32 | u) & M64)
+        send[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+
+    def _halo_pairs(self):
+        for q, rv in enumerate(self.rev):
+            if rv is not None and rv[0] == "halo":
+                yield q, rv[1]
+
+    def hb_recv(self, halo):
+        h = halo.numpy().view(np.uint64)
+        for q, slot in self._halo_pairs():
+            u, v = self._pair_ids(q)
+            assert int(h[slot, 0]) == (v << 32 | u) and int(h[slot, 1]) == (~(v << 32 | u) & M64), (q, slot)
+            self.hb_checked += 1
+
+    def hb_pack_resp(self, send):
+        a = np.zeros(len(self.send_pair), dtype=np.uint64)
+        for j, r in enumerate(self.send_pair):
+            if r is not None:
+                u, v = self._pair_ids(r)  # r = (u -> v) answers v's GRAFT
+                a[j] = u << 32 | v
+        send[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+
+    def hb_end(self, halo):
+        h = halo.numpy().view(np.uint64)
+        for r, slot in self._halo_pairs():
+            v, u = self._pair_ids(r)  # r = (v -> u): u's answer to v
+            assert int(h[slot]) == (u << 32 | v), (r, slot)
+            self.hb_checked += 1
+        out = abi.HeartbeatOut()
+        out.mesh_links = self.hb_checked
+        return out
+
     # -- stepped propagation ----------------------------------------------------------
     def prop_begin(self, msgs, cfg):
         self.cfg = cfg

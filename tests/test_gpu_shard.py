@@ -153,3 +153,58 @@ def test_stepped_api_equals_propagate(gpu_ok):
     ha, fa = a.prop_results(m)
     hb, fb = b.prop_results(m)
     assert np.array_equal(ha, hb) and np.array_equal(fa, fb)
+
+
+def _slice_te(x, T, E, a, b):
+    return np.asarray(x).reshape(T, E)[:, a:b].reshape(-1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_heartbeat_matches_single_engine(gpu_ok, world):
+    """Heartbeat rounds on range shards (GRAFT/PRUNE words and PRUNE answers of
+    cross-shard pairs exchanged between the steps) == one engine, including
+    the IHAVE gossip of a propagated batch; counters summed over ranks."""
+    import heartbeat_cases as hc
+
+    n, d, T, seed = 1500, 7, 2, 41
+    ov = pc.overlay(n, d, seed, mix_protocols=True, direct_frac=0.02)
+    full = gsx.Engine(T)
+    app = pc.setup(full, ov, T, seed, mesh_degree=9, disconnect_frac=0.02)
+    st0 = full.export_state()
+    E = ov.n_pairs
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        e = gsx.Engine(T)
+        _params(e, T)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(_slice_state(st0, T, E, a, b))
+        e.set_app_scores(app[a:b])
+        engines.append((e, a, b))
+    runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
+                              [(e,) for e, _, _ in engines])
+    msgs = pc.messages(n, 100, seed)
+    for k in range(3):
+        tick, now = 59 + k, pc.T0 + (3 + k) * abi.SECOND
+        want = full.heartbeat(tick, now, seed).as_dict()
+        res = shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.heartbeat(tick, now, seed))[1],
+                              [(r,) for r in runners])
+        assert res[0][1] == want, (k, res[0][1], want)
+        snap = hc.snapshot(full)
+        for (e, a, b) in engines:
+            got = hc.snapshot(e)
+            for f in abi.STATE_FIELDS:
+                w = _slice_state(snap, T, E, a, b)[f]
+                assert np.array_equal(got[f].view(np.uint8), w.view(np.uint8)), (k, f)
+            for f in ("backoff", "ihave_len", "ihave_digest"):
+                assert np.array_equal(np.asarray(got[f]).reshape(-1), _slice_te(snap[f], T, E, a, b)), (k, f)
+            assert np.array_equal(got["scores"].view(np.uint64), snap["scores"][a:b].view(np.uint64)), k
+        if k == 0:  # a gossipsub batch for the next rounds' IHAVEs (every engine caches what it saw)
+            cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=0, latency_ms=5)
+            full.propagate(msgs, cfg)
+            shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(msgs, cfg))[1],
+                            [(r,) for r in runners])
+    assert want["grafts"] + want["prunes"] > 0

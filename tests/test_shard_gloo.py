@@ -55,9 +55,13 @@ def _worker(rank, world, port, payload, q):
             rp = payload["row_ptr"]
             be = emu.EmuShard(sh, payload["fwd"][int(rp[sh.node_lo]) : int(rp[sh.node_hi])])
             rs = gs.RangeSharded(be, payload["rank_lo"], tp, compact=payload["compact"])
-            local, tot = rs.propagate(payload["msgs"], cfg)
-            hop, frm = be.prop_results(len(payload["msgs"]))
-            q.put((rank, local, tot, hop, frm))
+            if payload.get("heartbeat"):
+                local, tot = rs.heartbeat(1, 0, 0)
+                q.put((rank, local, tot, be.hb_checked, None))
+            else:
+                local, tot = rs.propagate(payload["msgs"], cfg)
+                hop, frm = be.prop_results(len(payload["msgs"]))
+                q.put((rank, local, tot, hop, frm))
         else:
             o = orc.Oracle(1)
             pc.setup(o, payload["ov"], 1, payload["seed"])
@@ -152,3 +156,24 @@ def test_message_parallel_gloo_totals():
     for k in ("deliveries", "duplicates", "transmissions", "hops"):
         assert tot[k] == want[k], k
     assert tot["hop_deliveries"] == want["hop_deliveries"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_heartbeat_exchange_gloo(world):
+    """The two control exchanges of a sharded heartbeat (GRAFT/PRUNE words to
+    the receivers' ranks, PRUNE answers back) deliver every cross-shard
+    pair's words to exactly its reverse pair's receive slot."""
+    import shard_emulator as emu
+
+    n = 240
+    ov = pc.overlay(n, 4, 3)
+    rank_lo = synth.shard_ranges(n, world)
+    shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
+    cfg = pc.config(abi.GSX_ROUTER_FLOODSUB)
+    payload = dict(mode="range", shards=shards, fwd=np.zeros(ov.n_pairs, np.uint8), row_ptr=ov.row_ptr,
+                   rank_lo=rank_lo, msgs=pc.messages(n, 1, 3), cfg=_cfg_dict(cfg), compact=False, heartbeat=True)
+    res = _run(world, payload)
+    obs = ov.pair_observer()
+    owner = np.searchsorted(rank_lo.astype(np.int64), np.arange(n), side="right") - 1
+    cross = owner[obs] != owner[ov.col]
+    assert sum(r[3] for r in res) == 2 * int(cross.sum()) > 0
