@@ -112,12 +112,14 @@ struct gsx_engine {
     // mcache (mcache.go): windows of cached gossipsub batches, front = history[0]
     struct McBatch {
         uint32_t topic = 0, n_msgs = 0, n_words = 0;
-        uint64_t* d_seen = nullptr;  // [word][node]
+        uint64_t* d_seen = nullptr;  // [node][word]: the call's seen rows, handed over (no copy)
+        size_t seen_words = 0;       // allocation size, for the buffer pool
         std::vector<uint64_t> ids;
     };
     std::deque<std::vector<McBatch>> mc;
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
+    std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
     gsx::GossipBatch* d_gb = nullptr;
     uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
@@ -132,6 +134,7 @@ struct gsx_engine {
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
+        size_t seen_words = 0;
         gsx::PropState last{};
         bool have_last = false;
         // the call in flight (gsx_prop_begin .. gsx_prop_end)
@@ -276,10 +279,31 @@ int upload_topic_params(gsx_engine* e) {
     return GSX_OK;
 }
 
+// Seen-row buffers cycle between the propagation call (its `seen`) and the
+// message cache (a gossipsub batch keeps the call's buffer): a call hands its
+// buffer to the cache instead of copying it, and takes one from this pool.
+void seen_release(gsx_engine* e, uint64_t* p, size_t words) {
+    if (p) e->seen_pool.emplace_back(words, p);
+}
+uint64_t* seen_acquire(gsx_engine* e, size_t words) {
+    for (size_t i = 0; i < e->seen_pool.size(); ++i)
+        if (e->seen_pool[i].first >= words) {
+            uint64_t* p = e->seen_pool[i].second;
+            e->seen_pool.erase(e->seen_pool.begin() + (long)i);
+            return p;
+        }
+    uint64_t* p = nullptr;
+    if (hipMalloc((void**)&p, 8 * std::max<size_t>(words, 1)) != hipSuccess) return nullptr;
+    return p;
+}
+void seen_pool_free(gsx_engine* e) {
+    for (auto& x : e->seen_pool) (void)hipFree(x.second);
+    e->seen_pool.clear();
+}
+
 void mcache_clear(gsx_engine* e) {
     for (auto& w : e->mc)
-        for (auto& b : w)
-            if (b.d_seen) (void)hipFree(b.d_seen);
+        for (auto& b : w) seen_release(e, b.d_seen, b.seen_words);
     e->mc.clear();
     e->mc.emplace_back();  // history[0], empty
 }
@@ -337,6 +361,7 @@ void free_state(gsx_engine* e) {
     e->gb_cap = e->ids_cap = 0;
     e->have_gossip = false;
     mcache_clear(e);
+    seen_pool_free(e);
 }
 
 template <class T>
@@ -1281,7 +1306,8 @@ uint32_t prop_words(size_t m) {
 
 int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
-    void* pp[] = {P.seen, P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats};
+    seen_release(e, P.seen, P.seen_words);
+    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     P.seen = P.hist = P.origin = P.from = P.sel = P.occ = nullptr;
@@ -1381,7 +1407,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         const size_t mm = std::max<size_t>(m, 1);
         int rc = 0;
         const uint32_t rc_rows = std::max<uint32_t>(rows, GSX_MAX_HOPS / 2 + 1);
-        if ((rc = dalloc(e, &P.seen, W * N)) || (rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
+        if ((rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
             (rc = dalloc(e, &P.occ, (size_t)rc_rows * ((N + 63) / 64))) ||
             (rc = dalloc(e, &P.origin, W * N)) || (rc = dalloc(e, &P.from, W * E)) ||
             (rc = dalloc(e, &P.msgs, mm)) ||
@@ -1398,6 +1424,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         P.words_cap = W;
         P.msgs_cap = (uint32_t)mm;
         P.rows_cap = rc_rows;
+    }
+    if (!P.seen) {  // handed to the message cache by the previous gossipsub call
+        P.seen_words = (size_t)P.words_cap * N;
+        P.seen = seen_acquire(e, P.seen_words);
+        if (!P.seen) return fail(e, GSX_ENOMEM, "hipMalloc: seen rows");
     }
     const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
     if (rsub && !P.sel) {
@@ -1496,14 +1527,14 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         }
     }
     const uint32_t W = ps.n_words;
-    const size_t N = e->n_nodes;
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
         gsx_engine::McBatch b;
         b.topic = P.cfg.topic;
         b.n_msgs = ps.n_msgs;
         b.n_words = W;
-        if (int rc = dalloc(e, &b.d_seen, (size_t)W * N)) return rc;
-        HIPCHK(e, hipMemcpyAsync(b.d_seen, P.seen, 8 * (size_t)W * N, hipMemcpyDeviceToDevice, e->stream));
+        b.d_seen = P.seen;  // the cache keeps this call's seen rows; the next call takes a pooled buffer
+        b.seen_words = P.seen_words;
+        P.seen = nullptr;
         b.ids = P.ids;
         if (e->mc.empty()) e->mc.emplace_back();
         e->mc.front().push_back(std::move(b));
@@ -1898,8 +1929,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     // mcache.Shift (mcache.go:94-104, gossipsub.go:1563), after the stream drained
     const size_t hist = (size_t)std::max(e->gp.history_length, 1);
     while (e->mc.size() >= hist) {
-        for (auto& b : e->mc.back())
-            if (b.d_seen) (void)hipFree(b.d_seen);
+        for (auto& b : e->mc.back()) seen_release(e, b.d_seen, b.seen_words);
         e->mc.pop_back();
     }
     e->mc.emplace_front();
