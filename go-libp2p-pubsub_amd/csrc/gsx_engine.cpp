@@ -131,6 +131,9 @@ struct gsx_engine {
         uint8_t* fwd = nullptr;
         uint32_t* pin = nullptr;
         uint32_t *dup = nullptr, *first = nullptr;  // pending P2/P3 credit counts per pair
+        uint32_t* fcnt = nullptr;   // per pair, this call: first receipts
+        uint64_t* flast = nullptr;  // per pair: hop << 32 | first receipts of its last such hop
+        size_t from_words = 0;      // allocation of `from` (tracked first deliverers)
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
@@ -153,9 +156,15 @@ struct gsx_engine {
         // scattered into, the slots filled last hop, per-destination counts
         uint64_t* halo = nullptr;
         uint32_t* halo_idx = nullptr;
-        uint64_t halo_cap = 0, halo_prev = 0;
+        uint64_t* halo_occ = nullptr;  // bit per receive slot: row received this hop
+        uint64_t* hfrom = nullptr;     // [receive slot][word]: first receipts from the remote sender, latest hop
+        uint64_t* touch = nullptr;     // bit per node: marked by a sender (very sparse hops)
+        uint64_t* vcnt = nullptr;      // per node: forwarded-set sizes (late duplicate accounting)
+        bool touch_clear = false;      // touch was cleared for the coming hop (before the halo scatter)
+        uint64_t halo_cap = 0, halo_prev = 0, hfrom_cap = 0;
         unsigned long long* dcount = nullptr;
     } prop;
+    bool prop_track = true;  // gsx_prop_set_tracking: keep first-deliverer rows (gsx_prop_results)
 
     // range sharding (gsx_load_overlay_shard / gsx_shard_*_plan)
     uint32_t n_total = 0, node_lo = 0;
@@ -167,6 +176,7 @@ struct gsx_engine {
     uint8_t* d_send_dest = nullptr;
     uint64_t *d_send_base = nullptr, *d_dest_halo_base = nullptr;
     uint32_t* d_pair_obs = nullptr;
+    uint32_t* d_halo_node = nullptr;  // per receive slot: local node of its pair
     std::vector<uint32_t> rev_host;
     bool sharded() const { return n_ranks > 1 || node_lo != 0 || n_total != n_nodes; }
     hipStream_t own_stream = nullptr;
@@ -329,13 +339,14 @@ void free_state(gsx_engine* e) {
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
-                  e->d_dest_halo_base};
+                  e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom,
+                  e->prop.touch, e->prop.vcnt, e->d_halo_node};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
     e->prop = {};
     e->prop.ev = std::move(evs);
-    e->d_send_pair = e->d_pair_obs = nullptr;
+    e->d_send_pair = e->d_pair_obs = e->d_halo_node = nullptr;
     e->d_send_dest = nullptr;
     e->d_send_base = e->d_dest_halo_base = nullptr;
     e->n_ranks = 1;
@@ -881,11 +892,13 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     std::vector<uint64_t> base(n_ranks + 1, 0);
     for (uint32_t k = 0; k < n_ranks; ++k) base[k + 1] = base[k] + cnt[k];
     std::vector<uint64_t> fill(base.begin(), base.end() - 1);
+    std::vector<uint32_t> hnode(base[n_ranks]);
     for (uint64_t q = 0; q < e->E; ++q) {
         const uint32_t v = (uint32_t)e->col_host[q];
         if (v >= self_lo && v - self_lo < self_n) continue;
         const uint64_t slot = fill[own[q]]++;
         e->rev_host[q] = gsx::HALO | (uint32_t)slot;
+        hnode[slot] = e->pair_obs[q];
         if (recv_u) recv_u[slot] = e->pair_obs[q] + self_lo;
         if (recv_v) recv_v[slot] = v;
     }
@@ -896,6 +909,11 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     e->n_recv = base[n_ranks];
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (e->E) HIPCHK(e, hipMemcpy(e->d_rev, e->rev_host.data(), sizeof(uint32_t) * e->E, hipMemcpyHostToDevice));
+    if (e->d_halo_node) (void)hipFree(e->d_halo_node);
+    e->d_halo_node = nullptr;
+    if (int rc = dalloc(e, &e->d_halo_node, hnode.size())) return rc;
+    if (!hnode.empty())
+        HIPCHK(e, hipMemcpy(e->d_halo_node, hnode.data(), sizeof(uint32_t) * hnode.size(), hipMemcpyHostToDevice));
     return GSX_OK;
 }
 
@@ -1307,10 +1325,11 @@ uint32_t prop_words(size_t m) {
 int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
     seen_release(e, P.seen, P.seen_words);
-    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats};
+    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats, P.touch, P.vcnt};
     for (void* p : pp)
         if (p) (void)hipFree(p);
-    P.seen = P.hist = P.origin = P.from = P.sel = P.occ = nullptr;
+    P.seen = P.hist = P.origin = P.from = P.sel = P.occ = P.touch = P.vcnt = nullptr;
+    P.from_words = 0;
     P.msgs = nullptr;
     P.stats = nullptr;
     P.words_cap = P.msgs_cap = P.rows_cap = 0;
@@ -1333,7 +1352,14 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.msgs = P.msgs;
     ps.seen = P.seen;
     ps.origin = P.origin;
-    ps.from_mask = P.from;
+    // first-deliverer rows: when tracked, and always for RandomSub (its draws exclude `from`)
+    ps.from_mask = (e->prop_track || cfg->router == GSX_ROUTER_RANDOMSUB) ? P.from : nullptr;
+    ps.fcnt = P.fcnt;
+    ps.flast = P.flast;
+    ps.hfrom = P.hfrom;
+    ps.halo_occ = nullptr;
+    ps.touch = P.touch;
+    ps.halo_node = e->d_halo_node;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
     ps.hist = P.hist;
     ps.n_rows = 1;
@@ -1409,13 +1435,14 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         const uint32_t rc_rows = std::max<uint32_t>(rows, GSX_MAX_HOPS / 2 + 1);
         if ((rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
             (rc = dalloc(e, &P.occ, (size_t)rc_rows * ((N + 63) / 64))) ||
-            (rc = dalloc(e, &P.origin, W * N)) || (rc = dalloc(e, &P.from, W * E)) ||
+            (rc = dalloc(e, &P.touch, (N + 63) / 64)) || (rc = dalloc(e, &P.vcnt, std::max<size_t>(N, 1))) ||
+            (rc = dalloc(e, &P.origin, W * N)) ||
             (rc = dalloc(e, &P.msgs, mm)) ||
             (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
             return rc;
         if (!P.fwd) {
             if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.pin, E)) || (rc = dalloc(e, &P.dup, E)) ||
-                (rc = dalloc(e, &P.corr, E)) ||
+                (rc = dalloc(e, &P.corr, E)) || (rc = dalloc(e, &P.fcnt, E)) || (rc = dalloc(e, &P.flast, E)) ||
                 (rc = dalloc(e, &P.first, E)))
                 return rc;
             HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -1434,17 +1461,14 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (rsub && !P.sel) {
         if (int rc = dalloc(e, &P.sel, (size_t)P.words_cap * E)) return rc;
     }
-    gsx::PropState ps = prop_state(e, W, m, cfg);
-    P.last = ps;
-    P.have_last = true;
-    P.cfg = *cfg;
-    P.h = 0;
-    P.sel_done = false;
-    P.ev_used = 0;
-    P.ids.resize(m);
-    for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
-    P.active = true;
-    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
+    const bool track = e->prop_track || rsub;
+    if (track && P.from_words < (size_t)P.words_cap * E) {
+        if (P.from) (void)hipFree(P.from);
+        P.from = nullptr;
+        P.from_words = 0;
+        if (int rc = dalloc(e, &P.from, (size_t)P.words_cap * E)) return rc;
+        P.from_words = (size_t)P.words_cap * E;
+    }
     if (e->n_recv) {  // compacted exchange: engine-owned dense halo, empty at the start of a call
         if (P.halo_cap < (uint64_t)W * e->n_recv || !P.halo_idx) {
             if (P.halo) (void)hipFree(P.halo);
@@ -1458,9 +1482,33 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         HIPCHK(e, hipMemsetAsync(P.halo, 0, 8 * (size_t)W * e->n_recv, e->stream));
         P.halo_prev = 0;
     }
+    if (e->n_recv) {  // receive-slot occupancy (compacted exchange) and first receipts per remote sender
+        if (P.hfrom_cap < (uint64_t)W * e->n_recv || !P.halo_occ) {
+            if (P.hfrom) (void)hipFree(P.hfrom);
+            if (P.halo_occ) (void)hipFree(P.halo_occ);
+            P.hfrom = nullptr;
+            P.halo_occ = nullptr;
+            int rc = 0;
+            if ((rc = dalloc(e, &P.hfrom, (size_t)W * e->n_recv)) || (rc = dalloc(e, &P.halo_occ, (e->n_recv + 63) / 64)))
+                return rc;
+            P.hfrom_cap = (uint64_t)W * e->n_recv;
+        }
+        HIPCHK(e, hipMemsetAsync(P.hfrom, 0, 8 * (size_t)W * e->n_recv, e->stream));
+    }
     if (!P.dcount) {
         if (int rc = dalloc(e, &P.dcount, (size_t)gsx::MAX_RANKS)) return rc;
     }
+    gsx::PropState ps = prop_state(e, W, m, cfg);
+    P.last = ps;
+    P.have_last = true;
+    P.cfg = *cfg;
+    P.h = 0;
+    P.sel_done = false;
+    P.ev_used = 0;
+    P.ids.resize(m);
+    for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
+    P.active = true;
+    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
     if (m == 0) return GSX_OK;
     std::vector<gsx::DevMsg> hm(m);
     for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
@@ -1469,8 +1517,10 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     HIPCHK(e, hipMemsetAsync(P.hist, 0, 8 * (size_t)W * N, e->stream));  // row 0: the publishes
     HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
     HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
+    if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
     HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(P.fcnt, 0, 4 * std::max<size_t>(E, 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(P.flast, 0, 8 * std::max<size_t>(E, 1), e->stream));
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
@@ -1488,13 +1538,20 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
         return GSX_OK;
     }
     ps.halo = halo;
+    ps.halo_occ = (halo && halo == P.halo) ? P.halo_occ : nullptr;  // compacted: rows not received are empty
     const uint32_t h = ++P.h;
     hipEvent_t a, b;
     if (int rc = prop_event_pair(e, &a, &b)) return rc;
     HIPCHK(e, hipEventRecord(a, e->stream));
     const size_t row = (size_t)ps.n_nodes * ps.n_words;
     const uint64_t* front = P.hist + (size_t)(h - 1) * row;
-    if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
+    const uint64_t* front_occ = P.occ + (size_t)(h - 1) * ((ps.n_nodes + 63) / 64);
+    const size_t occ_row = (ps.n_nodes + 63) / 64;
+    HIPCHK(e, hipMemsetAsync(P.occ + (size_t)h * occ_row, 0, 8 * occ_row, e->stream));  // the hop ORs its bits in
+    if (!P.touch_clear) HIPCHK(e, hipMemsetAsync(P.touch, 0, 8 * occ_row, e->stream));
+    P.touch_clear = false;
+    HIPCHK(e, gsx::launch_prop_mark(ps, h, front_occ, e->stream));
+    if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = false;
     HIPCHK(e, gsx::launch_prop_hop(ps, h, front, P.hist + (size_t)h * row, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
@@ -1517,7 +1574,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     std::memset(out, 0, sizeof(*out));
     P.active = false;
     if (ps.n_msgs == 0) return GSX_OK;
-    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, e->stream));
+    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, e->stream));
     if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, e->stream));
     if (ps.credit) {
         P.credit_pending = true;
@@ -1603,9 +1660,10 @@ int gsx_prop_pack(gsx_engine* e, uint64_t* send) {
     if (int rc = prop_event_pair(e, &a, &b)) return rc;
     HIPCHK(e, hipEventRecord(a, e->stream));
     const uint64_t* front = P.hist + (size_t)P.h * ps.n_nodes * ps.n_words;
-    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
+    const uint64_t* front_occ = P.occ + (size_t)P.h * ((ps.n_nodes + 63) / 64);
+    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = true;
-    HIPCHK(e, gsx::launch_prop_pack(ps, front, send, e->stream));
+    HIPCHK(e, gsx::launch_prop_pack(ps, front, front_occ, send, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     return GSX_OK;
 }
@@ -1638,13 +1696,14 @@ int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
     std::memset(counts, 0, 8 * (size_t)e->n_ranks);
     if (ps.n_msgs == 0 || e->n_send == 0) return GSX_OK;
     const uint64_t* front = P.hist + (size_t)P.h * ps.n_nodes * ps.n_words;
+    const uint64_t* front_occ = P.occ + (size_t)P.h * ((ps.n_nodes + 63) / 64);
     hipEvent_t a, b;
     if (int rc = prop_event_pair(e, &a, &b)) return rc;
     HIPCHK(e, hipEventRecord(a, e->stream));
-    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, e->stream));
+    if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = true;
     HIPCHK(e, hipMemsetAsync(P.dcount, 0, 8 * (size_t)e->n_ranks, e->stream));
-    HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, out, P.dcount, e->stream));
+    HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, front_occ, out, P.dcount, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     HIPCHK(e, hipMemcpyAsync(counts, P.dcount, 8 * (size_t)e->n_ranks, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1661,7 +1720,10 @@ int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_ent
     const gsx::PropState& ps = P.last;
     if (ps.n_msgs && e->n_recv) {
         HIPCHK(e, gsx::launch_halo_clear(ps, P.halo, P.halo_idx, P.halo_prev, e->stream));
-        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, e->stream));
+        HIPCHK(e, hipMemsetAsync(P.halo_occ, 0, 8 * ((e->n_recv + 63) / 64), e->stream));
+        HIPCHK(e, hipMemsetAsync(P.touch, 0, 8 * ((ps.n_nodes + 63) / 64), e->stream));
+        P.touch_clear = true;
+        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, P.halo_occ, e->stream));
         P.halo_prev = n_entries;
     }
     return gsx_prop_step(e, e->n_recv ? P.halo : nullptr, n_new);
@@ -1701,6 +1763,13 @@ int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* 
     return GSX_OK;
 }
 
+int gsx_prop_set_tracking(gsx_engine* e, uint32_t first_deliverers) {
+    if (!e) return GSX_EINVAL;
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    e->prop_track = first_deliverers != 0;
+    return GSX_OK;
+}
+
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
     if (!e) return GSX_EINVAL;
     if (!e->prop.have_last) return fail(e, GSX_ESTATE, "no gsx_propagate call yet");
@@ -1717,6 +1786,8 @@ int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
         (void)hipFree(d_h);
     }
     if (first_from) {
+        if (!ps.from_mask)
+            return fail(e, GSX_ESTATE, "first deliverers were not tracked in the last call (gsx_prop_set_tracking)");
         int32_t* d_ff = nullptr;
         if (int rc = dalloc(e, &d_ff, cells)) return rc;
         HIPCHK(e, hipMemsetAsync(d_ff, 0xFF, 4 * cells, e->stream));

@@ -25,6 +25,8 @@
 // only: HBM/L2 bound, no MFMA, no LDS.
 #include "gsx_ops.h"
 
+#include <cstdlib>
+
 namespace gsx {
 
 // Eligibility of every pair (v -> u) for this call (topic, router, scores).
@@ -100,6 +102,13 @@ __device__ __forceinline__ uint64_t elig_word(uint8_t fw, uint64_t own) {
     return 0;
 }
 
+// Frontier-history row h of node v is valid only where occupancy row h has
+// v's bit (a hop writes the rows of the nodes it touched; every other row
+// is empty whatever the memory holds).
+__device__ __forceinline__ bool occ_bit(const uint64_t* __restrict__ occ, uint32_t v) {
+    return (occ[v / 64] >> (v % 64)) & 1;
+}
+
 // ---- RandomSub's draw: the canonical RNG with tag 7 (gsx_ops.h) ----------
 constexpr uint64_t TAG_RANDOMSUB = 7;
 
@@ -108,9 +117,10 @@ constexpr uint64_t TAG_RANDOMSUB = 7;
 // ascending order; above RandomSubD they are shuffled (shufflePeers,
 // gossipsub.go:1890-1895) and the first max(6, ceil(sqrt(size))) kept.  The
 // kept pairs get message m's bit in `sel`.
-__global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t* __restrict__ front) {
+__global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t* __restrict__ front,
+                                                   const uint64_t* __restrict__ front_occ) {
     const uint32_t v = blockIdx.x * 64u + threadIdx.x;
-    if (v >= ps.n_nodes) return;
+    if (v >= ps.n_nodes || !occ_bit(front_occ, v)) return;
     const int64_t r0 = ps.row_ptr[v], r1 = ps.row_ptr[v + 1];
     const uint32_t W = ps.n_words;
     uint32_t cand[RSUB_MAX_DEG];
@@ -147,18 +157,21 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
 // receiver applies only its own origin mask; eligibility, RandomSub draws
 // and the `from` exclusion are the sender's and are applied here.
 __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t* __restrict__ front,
-                                                   uint64_t* __restrict__ send) {
+                                                   const uint64_t* __restrict__ front_occ, uint64_t* __restrict__ send) {
     const uint32_t W = ps.n_words;
     unsigned long long cnt[1] = {0};
     for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < ps.n_send; j += (uint64_t)gridDim.x * 256u) {
         uint64_t* out = send + j * W;
         const uint32_t r = ps.send_pair[j];
-        if (r == NO_PAIR) {
+        const uint32_t v = r == NO_PAIR ? 0 : ps.pair_obs[r];
+        if (r == NO_PAIR || !occ_bit(front_occ, v)) {  // no pair, or v received nothing last hop
             for (uint32_t w = 0; w < W; ++w) out[w] = 0;
             continue;
         }
-        const uint32_t v = ps.pair_obs[r];
         const uint8_t fw = ps.fwd[r];
+        // messages v first got from u at the frontier's hop (u is remote: the
+        // receive slot of pair r), never sent back (floodsub.go:82)
+        const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
         for (uint32_t w = 0; w < W; ++w) {
             const uint64_t f = front[(size_t)v * W + w];
             uint64_t c = 0;
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
                 if (ps.sel) el |= ps.sel[(size_t)r * W + w];
                 c = f & el;
                 cnt[0] += c != 0;
-                if (c) c &= ~ps.from_mask[(size_t)r * W + w];
+                if (c) c &= ~hf[w];
             }
             out[w] = c;
         }
@@ -185,6 +198,7 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
 // order of entries is not deterministic, but each carries its slot, and the
 // receiver only scatters them (k_halo_scatter), so the hop is.
 __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const uint64_t* __restrict__ front,
+                                                           const uint64_t* __restrict__ front_occ,
                                                            uint64_t* __restrict__ out, unsigned long long* __restrict__ dcount) {
     __shared__ uint32_t cnt[MAX_RANKS], base[MAX_RANKS];
     const uint32_t W = ps.n_words;
@@ -200,9 +214,10 @@ __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const u
         if (j < ps.n_send) {
             r = ps.send_pair[j];
             d = ps.send_dest[j];
-            if (r != NO_PAIR) {
-                v = ps.pair_obs[r];
+            if (r != NO_PAIR) v = ps.pair_obs[r];
+            if (r != NO_PAIR && occ_bit(front_occ, v)) {
                 fw = ps.fwd[r];
+                const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
                 for (uint32_t w = 0; w < W; ++w) {
                     const uint64_t f = front[(size_t)v * W + w];
                     if (!f) continue;
@@ -210,7 +225,7 @@ __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const u
                     if (ps.sel) el |= ps.sel[(size_t)r * W + w];
                     uint64_t c = f & el;
                     nsend[0] += c != 0;
-                    if (c) c &= ~ps.from_mask[(size_t)r * W + w];
+                    if (c) c &= ~hf[w];
                     nz |= c != 0;
                 }
             }
@@ -223,13 +238,14 @@ __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const u
         if (nz) {  // recompute the row (its inputs are cache-hot) and write the entry
             uint64_t* e = out + (ps.send_base[d] + base[d] + pos) * (uint64_t)(W + 1);
             e[0] = ps.dest_halo_base[d] + (j - ps.send_base[d]);
+            const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
             for (uint32_t w = 0; w < W; ++w) {
                 const uint64_t f = front[(size_t)v * W + w];
                 uint64_t c = 0;
                 if (f) {
                     uint64_t el = elig_word(fw, ps.origin[(size_t)v * W + w]);
                     if (ps.sel) el |= ps.sel[(size_t)r * W + w];
-                    c = f & el & ~ps.from_mask[(size_t)r * W + w];
+                    c = f & el & ~hf[w];
                 }
                 e[1 + w] = c;
             }
@@ -250,24 +266,63 @@ __global__ __launch_bounds__(256) void k_halo_clear(PropState ps, uint64_t* __re
 }
 __global__ __launch_bounds__(256) void k_halo_scatter(PropState ps, uint64_t* __restrict__ halo,
                                                       const uint64_t* __restrict__ ent, uint64_t n,
-                                                      uint32_t* __restrict__ idx) {
+                                                      uint32_t* __restrict__ idx, uint64_t* __restrict__ halo_occ) {
     const uint32_t W = ps.n_words;
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
         const uint64_t* e = ent + i * (uint64_t)(W + 1);
         const uint32_t slot = (uint32_t)e[0];
         idx[i] = slot;
         for (uint32_t w = 0; w < W; ++w) halo[(size_t)slot * W + w] = e[1 + w];
+        atomicOr((unsigned long long*)&halo_occ[slot / 64], 1ull << (slot % 64));  // occupancy (cleared per hop)
+        const uint32_t u = ps.halo_node[slot];
+        atomicOr((unsigned long long*)&ps.touch[u / 64], 1ull << (u % 64));  // u has a sender this hop
+    }
+}
+
+// Very sparse hops (at most n/16 first receipts last hop): the frontier
+// pushes "you have a sender" bits to its neighbours, so the hop kernel
+// skips every other node with one bitmap load instead of walking its pairs.
+// The touch bitmap was cleared before this hop (and before the halo scatter,
+// which marks the receivers of remote rows).
+__device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    return prev < ps.n_nodes / 16 && !(ps.halo && !ps.halo_occ);
+}
+__global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, const uint64_t* __restrict__ front_occ) {
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    if (!mark_hop(ps, h) || (!ps.sharded && h > 1 && prev == 0)) return;
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < ps.n_nodes; v += gridDim.x * 256u) {
+        if (!((front_occ[v / 64] >> (v % 64)) & 1)) continue;
+        for (int64_t r = ps.row_ptr[v]; r < ps.row_ptr[v + 1]; ++r) {
+            const uint32_t q = ps.rev[r];
+            if (q == NO_PAIR || (q & HALO) || !ps.fwd[r]) continue;  // v sends nothing to a local u
+            const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
+            atomicOr((unsigned long long*)&ps.touch[u / 64], 1ull << (u % 64));
+        }
     }
 }
 
 // ---- one hop ----------------------------------------------------------------
 // `front` holds the messages each vertex first received at hop h-1; `nxt`
-// receives those first received now.  CW words are processed per walk of
-// u's pairs (a 64·CW-message chunk lives in registers).
+// receives those first received now.  A node is handled by a group of LPN
+// lanes (1, 2 or 4): lane c of the group owns the CW-word chunks c, c + LPN,
+// ... of every row, so the group reads a neighbour's row as LPN adjacent
+// chunks of one line (LPN = 4 at 1024 messages: the whole 128-B line of a
+// gathered row is used, where a one-lane walk over 32-B chunks used a
+// quarter of every line it pulled).  Everything per pair (pins, occupancy
+// tests, eligibility) is the same in every lane of a group, so the group
+// walks the pairs in lock step and sums its per-pair counts with shuffles.
 template <int CW>
 __device__ __forceinline__ void load_words(uint64_t (&d)[CW], const uint64_t* p) {
 #pragma unroll
     for (int i = 0; i < CW; ++i) d[i] = p[i];
+}
+
+template <int LPN>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#pragma unroll
+    for (int o = 1; o < LPN; o <<= 1) x += __shfl_xor(x, o, LPN);
+    return x;
 }
 
 // The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
@@ -289,50 +344,92 @@ __device__ __forceinline__ void load_words(uint64_t (&d)[CW], const uint64_t* p)
 //
 // occ (one bit per node and hop, [hop][node / 64]) marks non-empty frontier
 // rows, so the sparse first and last hops skip the row gathers.
-template <int CW>
+template <int CW, int LPN, bool TRACK>
 __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                   uint64_t* __restrict__ nxt) {
-    constexpr int U = 4;  // pairs whose rows are in flight together (memory-level parallelism)
+    constexpr int U = 4;               // pairs whose rows are in flight together (memory-level parallelism)
+    constexpr uint32_t NB = 256 / LPN; // nodes per block tile
+    constexpr uint32_t NW = 64 / LPN;  // nodes per wave (a power of two: its occupancy bits stay in one word)
     const uint32_t W = ps.n_words;
     const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint64_t* __restrict__ occ_src = ps.occ;  // row 0: the nodes that published in this call
     const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     if (!ps.sharded && h > 1 && prev == 0) return;  // nothing arrived last hop: empty frontier, row h unused
-    // Sparse frontier (at most a quarter of the rows can be non-empty): test
-    // the occupancy bit before gathering a row.  Dense: gather directly.
+    // Sparse frontier (at most a quarter of the rows can be non-empty): a row
+    // is gathered only after its occupancy bit.  Very sparse (k_prop_mark):
+    // a node no sender marked is left untouched (no row loads, no row
+    // writes, occupancy bit 0).  Dense: rows are gathered beside their
+    // occupancy bits.
     const bool use_occ = prev < ps.n_nodes / 4;
+    const bool use_mark = mark_hop(ps, h);
     // Back-sends of this hop's first receipts would happen at hop h + 1 (if
     // it runs).  At h = 1 the receipts are the sender's own publishes, which
     // nobody sends back to their origin anyway.
     const bool backsend = !ps.late && h >= 2 && h < ps.max_hops;
+    const bool credit_back = backsend && ps.credit && ps.back_in_window;
+    // DuplicateMessage -> markDuplicateMessageDelivery with the record
+    // validated at u's first receipt (score.go:806-809, 965): in the window
+    // iff (h - h0) * latency <= window, i.e. u first got it at one of the
+    // last win_hops hops.  A duplicate at u is a copy of a message u first
+    // got earlier (seen) or this hop from a lower sender; with dm = ~seen |
+    // (rows of the window hops), the in-window duplicates of a pair are
+    // popcount(c & dm) - first receipts, and all its duplicates
+    // popcount(c) - first receipts.
+    const bool want_inwin = ps.credit && !ps.all_dups_in_window;
+    const uint32_t h_lo = h > ps.win_hops ? h - ps.win_hops : 0;
+    const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;  // node of the tile, lane in the group
     unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0;
-    for (uint32_t tile = blockIdx.x * 256u; tile < ps.n_nodes; tile += gridDim.x * 256u) {
-        const uint32_t u = tile + threadIdx.x;
+    for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
+        const uint32_t u = tile + gi;
         bool any_new = false;
-        if (u < ps.n_nodes) {
+        bool touch = u < ps.n_nodes;
+        if (touch && use_mark) touch = occ_bit(ps.touch, u);
+        if (touch) {
             const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
             const size_t un = (size_t)u * W;
-            for (uint32_t w0 = 0; w0 < W; w0 += CW) {
-                uint64_t seen[CW], mine[CW], acc[CW], inwin[CW];
-                bool have_inwin = false;
+            // a node that published in this call masks its own messages off
+            // every received row (never sent back to the origin); rare, so the
+            // origin chunk is re-read (cache-hot) rather than held
+            const bool u_src = occ_bit(occ_src, u);
+            for (uint32_t w0 = lc * CW; w0 < W; w0 += LPN * CW) {
+                uint64_t seen[CW], sa[CW], dm[CW];
                 load_words<CW>(seen, ps.seen + un + w0);
-                load_words<CW>(mine, ps.origin + un + w0);  // never sent back to its origin
 #pragma unroll
-                for (int i = 0; i < CW; ++i) acc[i] = 0;
+                for (int i = 0; i < CW; ++i) {
+                    sa[i] = seen[i];  // seen | this hop's receipts so far
+                    dm[i] = 0;
+                }
+                if (want_inwin) {
+                    for (uint32_t h0 = h_lo; h0 < h; ++h0) {
+                        if (!occ_bit(ps.occ + (size_t)h0 * occ_row, u)) continue;  // untouched: empty row
+                        const uint64_t* row = ps.hist + (size_t)h0 * ps.n_nodes * W + un + w0;
+#pragma unroll
+                        for (int i = 0; i < CW; ++i) dm[i] |= row[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < CW; ++i) dm[i] |= ~seen[i];
+                }
+                // software pipeline: the next block's pins are in flight
+                // while this block's rows are merged
+                uint32_t pn[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) pn[j] = q0 + j < q1 ? ps.pin[q0 + j] : NO_PAIR;
                 for (int64_t qb = q0; qb < q1; qb += U) {
-                    // gather U pairs' rows at once, then merge them in ascending order
                     uint32_t pv[U];
                     uint64_t c[U][CW];
 #pragma unroll
-                    for (int j = 0; j < U; ++j) pv[j] = qb + j < q1 ? ps.pin[qb + j] : NO_PAIR;
-                    if (use_occ)
+                    for (int j = 0; j < U; ++j) pv[j] = pn[j];
+                    if (use_occ) {
 #pragma unroll
                         for (int j = 0; j < U; ++j)
-                            if (pv[j] != NO_PAIR && !(pv[j] & HALO)) {
-                                const uint32_t v = pv[j] & PIN_NODE_MASK;
-                                if (!((occ_front[v / 64] >> (v % 64)) & 1)) pv[j] = NO_PAIR;  // v's row is empty
+                            if (pv[j] != NO_PAIR) {
+                                const bool live = (pv[j] & HALO) ? (!ps.halo_occ || occ_bit(ps.halo_occ, pv[j] & ~HALO))
+                                                                 : occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
+                                if (!live) pv[j] = NO_PAIR;  // the sender's row is empty
                             }
+                    }
 #pragma unroll
                     for (int j = 0; j < U; ++j) {
                         if (pv[j] == NO_PAIR) {
@@ -344,17 +441,39 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                             load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
                         }
                     }
+                    bool dead[U];  // rows of senders the previous hop left untouched are empty
+#pragma unroll
+                    for (int j = 0; j < U; ++j)
+                        dead[j] = !use_occ && pv[j] != NO_PAIR && !(pv[j] & HALO) &&
+                                  !occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
+                    // the block's per-pair counters travel with its rows (group lane 0
+                    // keeps them): no load-then-store chain per pair below
+                    uint32_t fc[U], dc[U];
+                    uint8_t fq[U];
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        const bool mine0 = pv[j] != NO_PAIR && lc == 0;
+                        fc[j] = mine0 ? ps.fcnt[qb + j] : 0;
+                        dc[j] = mine0 && ps.credit && (!ps.late || (pv[j] & HALO)) ? ps.dupcnt[qb + j] : 0;
+                        fq[j] = mine0 && backsend ? ps.fwd[qb + j] : 0;
+                    }
+#pragma unroll
+                    for (int j = 0; j < U; ++j) pn[j] = qb + U + j < q1 ? ps.pin[qb + U + j] : NO_PAIR;
 #pragma unroll
                     for (int j = 0; j < U; ++j) {
                         const uint32_t p = pv[j];
-                        if (p == NO_PAIR) continue;
+                        if (p == NO_PAIR) continue;  // the same in every lane of the group
                         const int64_t q = qb + j;
                         const bool halo = p & HALO;
+                        if (dead[j])
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] = 0;
                         if (!halo) {  // v's frontier row through the pair's eligibility
                             const uint32_t v = p & PIN_NODE_MASK;
                             const uint8_t m = (uint8_t)(p >> PIN_FWD_SHIFT);
                             uint64_t own[CW], sl[CW];
-                            if (m == FWD_FORWARD || m == FWD_PUBLISH) load_words<CW>(own, ps.origin + (size_t)v * W + w0);
+                            if ((m == FWD_FORWARD || m == FWD_PUBLISH) && occ_bit(occ_src, v))
+                                load_words<CW>(own, ps.origin + (size_t)v * W + w0);
                             else
 #pragma unroll
                                 for (int i = 0; i < CW; ++i) own[i] = 0;
@@ -368,96 +487,98 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                                 n_send += c[j][i] != 0;
                             }
                         }
-                        uint64_t any = 0;
+                        if (u_src) {
+                            uint64_t mine[CW];
+                            load_words<CW>(mine, ps.origin + un + w0);
 #pragma unroll
-                        for (int i = 0; i < CW; ++i) {
-                            c[j][i] &= ~mine[i];
-                            any |= c[j][i];
-                        }
-                        if (!any) continue;
-                        const bool count_here = !ps.late || halo;
-                        if (count_here && ps.credit && !ps.all_dups_in_window && !have_inwin) {
-                            // DuplicateMessage -> markDuplicateMessageDelivery with the
-                            // record validated at u's first receipt (score.go:806-809,
-                            // 965): in the window iff (h - h0) * latency <= window, i.e.
-                            // u first got it at one of the last win_hops hops — the OR
-                            // of those hops' frontier rows.
-                            const uint32_t h_lo = h > ps.win_hops ? h - ps.win_hops : 0;
-#pragma unroll
-                            for (int i = 0; i < CW; ++i) inwin[i] = 0;
-                            for (uint32_t h0 = h_lo; h0 < h; ++h0) {
-                                const uint64_t* row = ps.hist + (size_t)h0 * ps.n_nodes * W + un + w0;
-#pragma unroll
-                                for (int i = 0; i < CW; ++i) inwin[i] |= row[i];
-                            }
-                            have_inwin = true;
+                            for (int i = 0; i < CW; ++i) c[j][i] &= ~mine[i];
                         }
                         uint64_t nb[CW];
-                        uint64_t newany = 0;
-                        uint32_t k = 0, back = 0;
+                        uint32_t fresh = 0, pc = 0, kw = 0;
 #pragma unroll
                         for (int i = 0; i < CW; ++i) {
-                            nb[i] = c[j][i] & ~seen[i] & ~acc[i];
-                            acc[i] |= nb[i];
-                            newany |= nb[i];
-                            back += __popcll(nb[i]);
-                            if (count_here) {
-                                const uint64_t dup_now = c[j][i] & ~nb[i] & ~seen[i];  // first got this hop, lower sender
-                                const uint64_t dup_old = c[j][i] & seen[i];            // first got at an earlier hop
-                                n_dup += __popcll(dup_now) + __popcll(dup_old);
-                                if (ps.credit)
-                                    k += __popcll(dup_now) +
-                                         __popcll(ps.all_dups_in_window ? dup_old : (dup_old & inwin[i]));
+                            nb[i] = c[j][i] & ~sa[i];  // first receipts: not seen, not from a lower sender
+                            sa[i] |= nb[i];
+                            fresh += __popcll(nb[i]);
+                            pc += __popcll(c[j][i]);
+                            if (want_inwin) kw += __popcll(c[j][i] & dm[i]);
+                        }
+                        n_new += fresh;
+                        uint32_t k = 0;
+                        if (!ps.late || halo) {  // duplicates counted here (late: k_prop_dups)
+                            n_dup += pc - fresh;
+                            if (ps.credit) k = (want_inwin ? kw : pc) - fresh;
+                        }
+                        if (fresh) {
+                            if (TRACK) {  // first deliverers tracked: the pair's cumulative row
+                                uint64_t* fr = ps.from_mask + (size_t)q * W + w0;
+                                uint64_t o[CW];
+                                load_words<CW>(o, fr);
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) fr[i] = o[i] | nb[i];
+                            }
+                            if (halo) {  // what u must not send back to this remote sender (k_prop_pack)
+                                uint64_t* hf = ps.hfrom + (size_t)(p & ~HALO) * W + w0;
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) hf[i] = nb[i];
                             }
                         }
-                        n_new += back;
-                        if (newany) {  // u first got these from v: one read-modify-write of the pair's row
-                            uint64_t* fr = ps.from_mask + (size_t)q * W + w0;
-                            uint64_t o[CW];
-                            load_words<CW>(o, fr);
-#pragma unroll
-                            for (int i = 0; i < CW; ++i) fr[i] = o[i] | nb[i];
+                        if (LPN > 1) {  // converged: every lane of the group is here for pair q
+                            k = group_sum<LPN>(k);
+                            fresh = group_sum<LPN>(fresh);
                         }
-                        if (k) ps.dupcnt[q] += k;
-                        if (back && backsend && !halo && (ps.fwd[q] & FWD_FORWARD)) {
-                            // u forwards them to v at hop h + 1 and v counts duplicates:
-                            // the `from` exclusion's whole effect, taken back here
-                            n_back += back;
-                            if (ps.credit && ps.back_in_window) ps.corr[q] += back;
+                        if (lc == 0) {
+                            if (k) ps.dupcnt[q] = dc[j] + k;
+                            if (fresh) {  // first receipts from v: this call's count and the last hop's
+                                ps.fcnt[q] = fc[j] + fresh;
+                                ps.flast[q] = ((uint64_t)h << 32) | fresh;
+                                if (backsend && !halo && (fq[j] & FWD_FORWARD)) {
+                                    // u forwards them to v at hop h + 1 and v counts duplicates:
+                                    // the `from` exclusion's whole effect, taken back here
+                                    n_back += fresh;
+                                    if (credit_back) ps.corr[q] += fresh;
+                                }
+                            }
                         }
                     }
                 }
 #pragma unroll
                 for (int i = 0; i < CW; ++i) {
-                    nxt[un + w0 + i] = acc[i];  // this hop's row of the frontier history
-                    if (acc[i]) {
-                        ps.seen[un + w0 + i] = seen[i] | acc[i];
+                    const uint64_t acc = sa[i] ^ seen[i];
+                    nxt[un + w0 + i] = acc;  // this hop's row of the frontier history (touched nodes only)
+                    if (acc) {
+                        ps.seen[un + w0 + i] = sa[i];
                         ++n_vnew;
                         any_new = true;
                     }
                 }
             }
         }
-        // occupancy of this hop's rows: one 64-node word per wave
-        const unsigned long long occ = __ballot(any_new);
-        if ((threadIdx.x & 63) == 0 && u < ps.n_nodes) occ_nxt[u / 64] = occ;
+        // occupancy of this hop's rows (cleared before the hop): the group's
+        // lanes OR their bits, the wave's NW nodes become NW bits of one word
+        if (LPN > 1) any_new = group_sum<LPN>(any_new ? 1u : 0u) != 0;
+        uint64_t wb = __ballot(any_new && lc == 0);
+        if (LPN > 1) {
+            uint64_t r = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < NW; ++i) r |= ((wb >> (i * LPN)) & 1ull) << i;
+            wb = r;
+        }
+        const uint32_t u0 = tile + (threadIdx.x / 64) * NW;  // the wave's first node
+        if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
     }
     unsigned long long cnt[5] = {n_new, n_dup, n_send, n_vnew, n_back};
     const uint32_t slot[5] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS};
     block_count<5>(cnt, ps.stats, slot);
 }
 
-// Late duplicate accounting (ps.late), once per call, per SENDER pair
-// r = (v -> u) with both ends on this shard: v's sends to u over the call are
-// the messages v forwarded (its seen set minus what it first got at the last
-// hop run, when it no longer sends) through the pair's eligibility and
-// RandomSub draws, minus the ones v first got from u (`from`, v's own row)
-// and the ones u published.  Each is a first receipt or a duplicate at u;
-// k_prop_count subtracts the first receipts at u's pair.  Everything but
-// u's origin row and the receiving pair's counter is v-local.
-__global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run) {
-    unsigned long long cnt[1] = {0};
-    const uint32_t W = ps.n_words;
+struct DupsLast {  // the last hop run and its frontier rows
+    uint32_t h_run;
+    bool empty;
+    const uint64_t* row;
+    const uint64_t* occ;
+};
+__device__ __forceinline__ DupsLast dups_last(const PropState& ps, uint32_t h_run) {
     // rows after the first hop that delivered nothing were never written
     // (skipped hops); that hop's row is empty and nothing was first received
     // later, so v forwarded its whole seen set
@@ -466,8 +587,45 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run)
             h_run = hh;
             break;
         }
-    const uint64_t* last = ps.hist + (size_t)h_run * ps.n_nodes * W;
-    const bool last_empty = ps.stats[STAT_HOP0 + h_run] == 0 && (!ps.sharded || h_run < ps.max_hops);
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    DupsLast L;
+    L.h_run = h_run;
+    L.row = ps.hist + (size_t)h_run * ps.n_nodes * ps.n_words;
+    L.occ = ps.occ + (size_t)h_run * occ_row;
+    L.empty = ps.stats[STAT_HOP0 + h_run] == 0 && (!ps.sharded || h_run < ps.max_hops);
+    return L;
+}
+
+// Per sender v: the size of its forwarded set (seen minus the last hop's
+// receipts) and the part of it v published, packed n_all | n_own << 32.
+__global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_run, uint64_t* __restrict__ vcnt) {
+    const DupsLast L = dups_last(ps, h_run);
+    const uint32_t W = ps.n_words;
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < ps.n_nodes; v += gridDim.x * 256u) {
+        const bool v_src = occ_bit(ps.occ, v);
+        const bool v_last = !L.empty && occ_bit(L.occ, v);
+        uint32_t n_all = 0, n_own = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            const size_t vw = (size_t)v * W + w;
+            uint64_t s = ps.seen[vw];
+            if (v_last) s &= ~L.row[vw];
+            n_all += __popcll(s);
+            if (v_src) n_own += __popcll(s & ps.origin[vw]);
+        }
+        vcnt[v] = (uint64_t)n_all | ((uint64_t)n_own << 32);
+    }
+}
+
+// One thread per sender pair; the sends land in corr[r] (unused by the late
+// accounting otherwise) and k_prop_count moves them to the receiver's pair,
+// so no thread scatters into another pair's counter.  A pair takes the
+// per-word path only for RandomSub draws, tracked `from` rows, or a
+// publishing u; every other pair reads its class's count from vcnt.
+__global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
+    unsigned long long cnt[1] = {0};
+    const uint32_t W = ps.n_words;
+    const DupsLast L = dups_last(ps, h_run);
+    h_run = L.h_run;
     const uint64_t* src_occ = ps.occ;  // row 0: nodes that published in this call
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < ps.n_pairs; r += (uint64_t)gridDim.x * 256u) {
         const uint32_t q = ps.rev[r];  // the receiver's pair (u -> v)
@@ -475,20 +633,40 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run)
         if (q == NO_PAIR || (q & HALO) || !fw) continue;
         const uint32_t v = ps.pair_obs[r];
         const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
-        const bool v_src = (src_occ[v / 64] >> (v % 64)) & 1, u_src = (src_occ[u / 64] >> (u % 64)) & 1;
-        uint32_t sends = 0;
-        for (uint32_t w = 0; w < W; ++w) {
-            const size_t vw = (size_t)v * W + w;
-            uint64_t s = ps.seen[vw];
-            if (!last_empty) s &= ~last[vw];
-            s &= elig_word(fw, v_src ? ps.origin[vw] : 0);
-            if (ps.sel) s |= ps.sel[r * W + w];
-            s &= ~ps.from_mask[r * W + w];
-            if (u_src) s &= ~ps.origin[(size_t)u * W + w];
-            sends += __popcll(s);
+        const bool u_src = occ_bit(src_occ, u);
+        uint32_t sends = 0, pub = 0;
+        if (!u_src && !ps.sel && !ps.from_mask) {
+            const uint64_t vc = vcnt[v];
+            const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
+            const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
+            sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
+                  : m == FWD_PUBLISH ? n_own : 0;
+        } else {
+            const bool v_src = occ_bit(src_occ, v);
+            const bool v_last = !L.empty && occ_bit(L.occ, v);
+            for (uint32_t w = 0; w < W; ++w) {
+                const size_t vw = (size_t)v * W + w;
+                uint64_t s = ps.seen[vw];
+                if (v_last) s &= ~L.row[vw];
+                s &= elig_word(fw, v_src ? ps.origin[vw] : 0);
+                if (ps.sel) s |= ps.sel[r * W + w];
+                if (ps.from_mask) s &= ~ps.from_mask[r * W + w];
+                if (u_src) {
+                    const uint64_t ou = ps.origin[(size_t)u * W + w];
+                    s &= ~ou;
+                    pub += __popcll(ou);
+                }
+                sends += __popcll(s);
+            }
+        }
+        if (!ps.from_mask && (fw & FWD_FORWARD) && h_run >= 1) {
+            const uint64_t fl = ps.flast[r];
+            const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
+            const uint32_t from_pub = (ps.fwd[q] & FWD_PUBLISH) ? pub : 0;
+            sends -= ps.fcnt[r] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
         }
         cnt[0] += sends;
-        if (ps.credit && sends) ps.dupcnt[q] += sends;
+        ps.corr[r] = sends;
     }
     const uint32_t slot[1] = {STAT_DUPS};
     block_count<1>(cnt, ps.stats, slot);
@@ -496,18 +674,17 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run)
 
 // ---- P2/P3 credits ------------------------------------------------------------
 // Per receiver pair q = (u -> v), add this call's first receipts from v (the
-// popcount of its from row) and in-window duplicates to the pending counts.
+// hop kernel's fcnt) and in-window duplicates to the pending counts.
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps) {
     unsigned long long cnt[1] = {0};
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
-        uint32_t k1 = 0;
-        for (uint32_t w = 0; w < ps.n_words; ++w) k1 += __popcll(ps.from_mask[(size_t)q * ps.n_words + w]);
+        const uint32_t k1 = ps.fcnt[q];
         const uint32_t r = ps.rev[q];
         const bool local = r != NO_PAIR && !(r & HALO);
         if (ps.credit) {
             if (k1) ps.firstcnt[q] += k1;
             if (local) {
-                if (ps.late) ps.dupcnt[q] -= k1;  // k_prop_dups counted every send from v, first receipts too
+                if (ps.late) ps.dupcnt[q] += ps.corr[r] - k1;  // k_prop_dups: every send from v, first receipts too
                 else if (const uint32_t c = ps.corr[r]) ps.dupcnt[q] -= c;  // in-window back-sends taken back
             }
         }
@@ -565,7 +742,9 @@ __global__ __launch_bounds__(256) void k_prop_hops_export(PropState ps, uint8_t*
     uint8_t hk[64];
 #pragma unroll
     for (int b = 0; b < 64; ++b) hk[b] = 0xFF;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
     for (uint32_t h = 0; h < ps.n_rows; ++h) {
+        if (!occ_bit(ps.occ + (size_t)h * occ_row, u)) continue;  // untouched at hop h: empty row
         uint64_t x = ps.hist[(size_t)h * ps.n_nodes * W + (size_t)u * W + w];
         while (x) {
             const int b = __builtin_ctzll(x);
@@ -603,21 +782,23 @@ hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st
     hipLaunchKernelGGL(k_prop_init, dim3(nblk(ps.n_msgs, 256)), dim3(256), 0, st, ps, front);
     return hipGetLastError();
 }
-hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, hipStream_t st) {
+hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, hipStream_t st) {
     if (ps.n_nodes == 0 || !ps.sel) return hipSuccess;
-    hipLaunchKernelGGL(k_rsub_select, dim3(nblk(ps.n_nodes, 64)), dim3(64), 0, st, ps, front);
+    hipLaunchKernelGGL(k_rsub_select, dim3(nblk(ps.n_nodes, 64)), dim3(64), 0, st, ps, front, front_occ);
     return hipGetLastError();
 }
-hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, uint64_t* send, hipStream_t st) {
+hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, uint64_t* send,
+                            hipStream_t st) {
     if (ps.n_send == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_pack, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps, front, send);
+    hipLaunchKernelGGL(k_prop_pack, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps, front,
+                       front_occ, send);
     return hipGetLastError();
 }
-hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, uint64_t* out,
-                                    unsigned long long* dcount, hipStream_t st) {
+hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, const uint64_t* front_occ,
+                                    uint64_t* out, unsigned long long* dcount, hipStream_t st) {
     if (ps.n_send == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_pack_compact, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps,
-                       front, out, dcount);
+                       front, front_occ, out, dcount);
     return hipGetLastError();
 }
 hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st) {
@@ -626,24 +807,51 @@ hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t
     return hipGetLastError();
 }
 hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
-                               hipStream_t st) {
+                               uint64_t* halo_occ, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_halo_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, ent, n,
-                       idx);
+                       idx, halo_occ);
     return hipGetLastError();
+}
+template <int CW, int LPN>
+static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
+    const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
+    if (ps.from_mask) hipLaunchKernelGGL((k_prop_hop<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
+    else hipLaunchKernelGGL((k_prop_hop<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
 }
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     if (ps.n_nodes == 0) return hipSuccess;
-    const dim3 g(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), b(256);
-    // n_words is 1, 2 or a multiple of 4 (the engine pads)
-    if (ps.n_words == 1) hipLaunchKernelGGL(k_prop_hop<1>, g, b, 0, st, ps, h, front, nxt);
-    else if (ps.n_words == 2) hipLaunchKernelGGL(k_prop_hop<2>, g, b, 0, st, ps, h, front, nxt);
-    else hipLaunchKernelGGL(k_prop_hop<4>, g, b, 0, st, ps, h, front, nxt);
+    // n_words is 1, 2 or a multiple of 4 (the engine pads).  Words per lane
+    // CW (GSX_HOP_CW = 2 or 4 overrides, for tuning) and lanes per node: the
+    // largest of 4, 2, 1 whose chunks tile the row.
+    static const int cw_env = [] {
+        const char* v = getenv("GSX_HOP_CW");
+        return v ? atoi(v) : 0;
+    }();
+    const uint32_t W = ps.n_words;
+    if (W == 1) hop_launch<1, 1>(ps, h, front, nxt, st);
+    else if (W == 2) hop_launch<2, 1>(ps, h, front, nxt, st);
+    else if (cw_env == 2) {
+        if (W % 8 == 0) hop_launch<2, 4>(ps, h, front, nxt, st);
+        else hop_launch<2, 2>(ps, h, front, nxt, st);
+    } else {
+        if (W % 16 == 0) hop_launch<4, 4>(ps, h, front, nxt, st);
+        else if (W % 8 == 0) hop_launch<4, 2>(ps, h, front, nxt, st);
+        else hop_launch<4, 1>(ps, h, front, nxt, st);
+    }
     return hipGetLastError();
 }
-hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, hipStream_t st) {
+hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st) {
+    if (ps.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_mark, dim3(std::min(nblk(ps.n_nodes, 256), 1024u)), dim3(256), 0, st, ps, h, front_occ);
+    return hipGetLastError();
+}
+hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_dups, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run);
+    hipLaunchKernelGGL(k_prop_vcount, dim3(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
+                       vcnt);
+    hipLaunchKernelGGL(k_prop_dups, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
+                       vcnt);
     return hipGetLastError();
 }
 hipError_t launch_prop_count(const PropState& ps, hipStream_t st) {

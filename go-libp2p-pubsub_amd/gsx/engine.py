@@ -172,9 +172,16 @@ class Engine:
         if want_results:
             n = self.n_nodes
             hop = np.empty((len(ms), n), dtype=np.uint8)
-            frm = np.empty((len(ms), n), dtype=np.int32)
+            frm = np.empty((len(ms), n), dtype=np.int32) if self._track else None
             self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
         return out, hop, frm
+
+    _track = True
+
+    def set_prop_tracking(self, first_deliverers: bool):
+        """gsx_prop_set_tracking: keep first-deliverer rows (results' first_from) or only counts."""
+        self._chk(self.lib.gsx_prop_set_tracking(self.h, 1 if first_deliverers else 0), "gsx_prop_set_tracking")
+        self._track = bool(first_deliverers)
 
     # -- stepped / sharded propagation (gsx.h "range sharding") --------------------------
     def load_overlay_shard(self, n_total, node_lo, row_ptr, col, edge_flags=None, node_ips=None):
@@ -272,7 +279,7 @@ class Engine:
     def prop_results(self, n_msgs: int):
         """-> (hop [m, n_local] u8, first_from [m, n_local] i32) of the last propagation."""
         hop = np.empty((n_msgs, self.n_nodes), dtype=np.uint8)
-        frm = np.empty((n_msgs, self.n_nodes), dtype=np.int32)
+        frm = np.empty((n_msgs, self.n_nodes), dtype=np.int32) if self._track else None
         self._chk(self.lib.gsx_prop_results(self.h, _ptr(hop, C.c_uint8), _ptr(frm, C.c_int32)), "gsx_prop_results")
         return hop, frm
 

@@ -394,6 +394,14 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
  * none), laid out [message][node] over this engine's nodes.  Either pointer
  * may be NULL. */
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from);
+/* Whether propagation keeps, per pair, the messages its observer first got
+ * from the neighbour (the deliveryRecord's first deliverer, score.go:833-854)
+ * for gsx_prop_results' first_from.  On by default.  Off, a call keeps only
+ * per-pair counts (P2/P3 credits and duplicate accounting are unchanged)
+ * and gsx_prop_results(first_from != NULL) fails with GSX_ESTATE; the hop
+ * kernel then does no per-pair row read-modify-writes.  RandomSub keeps the
+ * rows either way (its draws exclude the peer a message came from). */
+int gsx_prop_set_tracking(gsx_engine* e, uint32_t first_deliverers);
 
 /* Pending P2/P3 credit counts per pair (first receipts, in-window duplicates)
  * accumulated by GSX_CREDIT_DEFER calls.  Pointers may be host or device

@@ -11,7 +11,7 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_AN
          "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d "$OUT/p$i" -o pmc --output-format csv -- \
-        python3 tools/prop_profile.py --batches 1 > "$OUT/p$i.log" 2>&1
+        python3 tools/prop_profile.py --batches 1 --msgs ${MSGS:-256} > "$OUT/p$i.log" 2>&1
     rc=$?; echo "pass $i ($C) rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 echo done

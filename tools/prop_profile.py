@@ -17,6 +17,9 @@ ap.add_argument("--peers", type=int, default=1_000_000)
 ap.add_argument("--msgs", type=int, default=256)
 ap.add_argument("--batches", type=int, default=3)
 ap.add_argument("--router", type=int, default=abi.GSX_ROUTER_GOSSIPSUB)
+ap.add_argument("--track", type=int, default=0, help="keep first-deliverer rows (gsx_prop_set_tracking)")
+ap.add_argument("--credit", type=int, default=abi.GSX_CREDIT_NOW)
+ap.add_argument("--latency-us", type=int, default=10_000, help="hop latency (P3 window of the params: 10 ms)")
 a = ap.parse_args()
 th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                     accept_px_threshold=0, opportunistic_graft_threshold=0)
@@ -27,8 +30,11 @@ class A:
     prop_hops = 24
 
 
+e.set_prop_tracking(bool(a.track))
 cfg = bench.prop_config(A, a.peers)
 cfg.router = a.router
+cfg.credit_scores = a.credit
+cfg.hop_latency_ns = a.latency_us * 1000
 for b in range(a.batches):
     out = e.propagate(bench.prop_messages(a.peers, a.msgs, synth.SEED, first=b * a.msgs), cfg)[0]
     d = out.as_dict()
