@@ -120,6 +120,9 @@ def prop_engine(n_total, lo, hi, d, seed, device, th, sharded):
                       expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n_total))
     e.set_app_scores(np.zeros(n_pairs))
     e.refresh(T0 + abi.SECOND)
+    # throughput runs keep per-pair first-receipt counts, not first-deliverer
+    # rows (gsx_prop_set_tracking; credits and duplicates are unchanged)
+    e.set_prop_tracking(False)
     e.sync()
     log(f"[bench] propagation engine nodes={hi - lo}/{n_total} pairs={n_pairs} in {time.time() - t:.1f}s")
     return e
@@ -376,7 +379,8 @@ def main():
     ap.add_argument("--degree", type=int, default=6)
     ap.add_argument("--cpu-passes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--prop-msgs", type=int, default=256, help="messages per propagation batch (0: skip)")
+    ap.add_argument("--prop-msgs", type=int, default=1024,
+                    help="messages per propagation batch (0: skip); 1024 = 16 words, one 128-B line per frontier row")
     ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)

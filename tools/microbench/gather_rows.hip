@@ -189,7 +189,7 @@ int main(int argc, char** argv) {
     Overlay ov = connect_some(n, 6, 42);
     const uint64_t E = ov.rp[n];
     printf("n=%u E=%llu\n", n, (unsigned long long)E);
-    for (int order = 0; order < 2; ++order) {
+    for (int order = 0; order < 1; ++order) {
         Overlay o = order ? renumber_bfs(ov, n) : ov;
         std::vector<uint32_t> pin(E);
         uint64_t x = 7;
@@ -225,6 +225,13 @@ int main(int argc, char** argv) {
         report("group W16 cw2 lpn8", time_it([&] { k_group<2, 8, 4><<<grid(8ull * n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 16);
         report("group W16 cw4 lpn4 U8", time_it([&] { k_group<4, 4, 8><<<grid(4ull * n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 16);
         report("node W16 U2", time_it([&] { k_node<16, 2><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 16);
+        for (int lds : {20 * 1024, 40 * 1024, 80 * 1024}) {  // limits blocks per CU: 8, 4, 2 (of 160 KB)
+            char nm[64];
+            snprintf(nm, sizeof nm, "group W16 lds%dK", lds / 1024);
+            report(nm, time_it([&] { hipLaunchKernelGGL((k_group<4, 4, 4>), grid(4ull * n), B, lds, 0, d_rp, d_pin, d_front, d_nxt, n); }), 16);
+            snprintf(nm, sizeof nm, "node W4 lds%dK", lds / 1024);
+            report(nm, time_it([&] { hipLaunchKernelGGL((k_node<4, 4>), grid(n), B, lds, 0, d_rp, d_pin, d_front, d_nxt, n); }), 4);
+        }
         report("pair W4", time_it([&] { k_pair<4><<<grid(E), B>>>(d_pin, d_front, d_nxt, E); }), 4);
         report("pair W16", time_it([&] { k_pair<16><<<grid(E), B>>>(d_pin, d_front, d_nxt, E); }), 16);
         CHK(hipFree(d_rp));
