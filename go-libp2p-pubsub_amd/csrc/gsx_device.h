@@ -163,7 +163,7 @@ struct PropState {
     uint64_t* flast;           // per pair: hop << 32 | first receipts of the last hop that had any
     uint64_t* hfrom;           // [receive slot][word]: first receipts from the remote sender at its latest such hop
     const uint64_t* halo_occ;  // bit per receive slot: row received this hop (null: every row present)
-    uint64_t* touch;           // bit per node: some sender's row is non-empty this hop (very sparse hops)
+    uint64_t* touch;           // [2][node / 64] bit per node, buffer h & 1: some sender's row is non-empty (very sparse hops)
     const uint32_t* halo_node; // per receive slot: the local node whose pair it feeds
     uint64_t* sel;             // [pair][word] RandomSub draws (null for other routers)
     const uint64_t* hist;      // [hop][node][word]: messages first received at that hop (row 0: published)
@@ -199,10 +199,10 @@ hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, 
                                     uint64_t* out, unsigned long long* dcount, hipStream_t st);
 hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st);
 hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
-                               uint64_t* halo_occ, hipStream_t st);
+                               uint64_t* halo_occ, uint32_t h, hipStream_t st);
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
-hipError_t launch_prop_count(const PropState& ps, hipStream_t st);
+hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st);
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, hipStream_t st);
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
                             hipStream_t st);

@@ -160,7 +160,6 @@ struct gsx_engine {
         uint64_t* hfrom = nullptr;     // [receive slot][word]: first receipts from the remote sender, latest hop
         uint64_t* touch = nullptr;     // bit per node: marked by a sender (very sparse hops)
         uint64_t* vcnt = nullptr;      // per node: forwarded-set sizes (late duplicate accounting)
-        bool touch_clear = false;      // touch was cleared for the coming hop (before the halo scatter)
         uint64_t halo_cap = 0, halo_prev = 0, hfrom_cap = 0;
         unsigned long long* dcount = nullptr;
     } prop;
@@ -1435,7 +1434,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         const uint32_t rc_rows = std::max<uint32_t>(rows, GSX_MAX_HOPS / 2 + 1);
         if ((rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
             (rc = dalloc(e, &P.occ, (size_t)rc_rows * ((N + 63) / 64))) ||
-            (rc = dalloc(e, &P.touch, (N + 63) / 64)) || (rc = dalloc(e, &P.vcnt, std::max<size_t>(N, 1))) ||
+            (rc = dalloc(e, &P.touch, 2 * ((N + 63) / 64))) || (rc = dalloc(e, &P.vcnt, std::max<size_t>(N, 1))) ||
             (rc = dalloc(e, &P.origin, W * N)) ||
             (rc = dalloc(e, &P.msgs, mm)) ||
             (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
@@ -1516,6 +1515,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
     HIPCHK(e, hipMemsetAsync(P.hist, 0, 8 * (size_t)W * N, e->stream));  // row 0: the publishes
     HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
+    HIPCHK(e, hipMemsetAsync(P.touch, 0, 16 * ((N + 63) / 64), e->stream));  // both buffers (k_prop_mark clears them after)
     HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
     if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
     HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -1546,11 +1546,7 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
     const size_t row = (size_t)ps.n_nodes * ps.n_words;
     const uint64_t* front = P.hist + (size_t)(h - 1) * row;
     const uint64_t* front_occ = P.occ + (size_t)(h - 1) * ((ps.n_nodes + 63) / 64);
-    const size_t occ_row = (ps.n_nodes + 63) / 64;
-    HIPCHK(e, hipMemsetAsync(P.occ + (size_t)h * occ_row, 0, 8 * occ_row, e->stream));  // the hop ORs its bits in
-    if (!P.touch_clear) HIPCHK(e, hipMemsetAsync(P.touch, 0, 8 * occ_row, e->stream));
-    P.touch_clear = false;
-    HIPCHK(e, gsx::launch_prop_mark(ps, h, front_occ, e->stream));
+    HIPCHK(e, gsx::launch_prop_mark(ps, h, front_occ, e->stream));  // also clears occupancy row h
     if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = false;
     HIPCHK(e, gsx::launch_prop_hop(ps, h, front, P.hist + (size_t)h * row, e->stream));
@@ -1575,13 +1571,14 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     P.active = false;
     if (ps.n_msgs == 0) return GSX_OK;
     if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, e->stream));
-    if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, e->stream));
+    const bool fold_now = ps.credit && P.cfg.credit_scores != GSX_CREDIT_DEFER;
+    if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, dev_state(e), fold_now, e->stream));
     if (ps.credit) {
-        P.credit_pending = true;
+        // GSX_CREDIT_NOW: k_prop_count folded this call's counts (and any
+        // pending ones of the topic) and left the pending counts empty
+        P.credit_pending = !fold_now;
         P.credit_topic = ps.topic;
-        if (P.cfg.credit_scores != GSX_CREDIT_DEFER) {
-            if (int rc = prop_fold(e, ps)) return rc;
-        }
+        if (fold_now) e->scores_valid = false;
     }
     const uint32_t W = ps.n_words;
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
@@ -1721,9 +1718,7 @@ int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_ent
     if (ps.n_msgs && e->n_recv) {
         HIPCHK(e, gsx::launch_halo_clear(ps, P.halo, P.halo_idx, P.halo_prev, e->stream));
         HIPCHK(e, hipMemsetAsync(P.halo_occ, 0, 8 * ((e->n_recv + 63) / 64), e->stream));
-        HIPCHK(e, hipMemsetAsync(P.touch, 0, 8 * ((ps.n_nodes + 63) / 64), e->stream));
-        P.touch_clear = true;
-        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, P.halo_occ, e->stream));
+        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, P.halo_occ, P.h + 1, e->stream));
         P.halo_prev = n_entries;
     }
     return gsx_prop_step(e, e->n_recv ? P.halo : nullptr, n_new);

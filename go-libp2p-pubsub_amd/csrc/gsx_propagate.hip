@@ -266,8 +266,10 @@ __global__ __launch_bounds__(256) void k_halo_clear(PropState ps, uint64_t* __re
 }
 __global__ __launch_bounds__(256) void k_halo_scatter(PropState ps, uint64_t* __restrict__ halo,
                                                       const uint64_t* __restrict__ ent, uint64_t n,
-                                                      uint32_t* __restrict__ idx, uint64_t* __restrict__ halo_occ) {
+                                                      uint32_t* __restrict__ idx, uint64_t* __restrict__ halo_occ,
+                                                      uint32_t h) {
     const uint32_t W = ps.n_words;
+    uint64_t* touch = ps.touch + (size_t)(h & 1) * (((size_t)ps.n_nodes + 63) / 64);  // the coming hop h's buffer
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
         const uint64_t* e = ent + i * (uint64_t)(W + 1);
         const uint32_t slot = (uint32_t)e[0];
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(256) void k_halo_scatter(PropState ps, uint64_t* __
         for (uint32_t w = 0; w < W; ++w) halo[(size_t)slot * W + w] = e[1 + w];
         atomicOr((unsigned long long*)&halo_occ[slot / 64], 1ull << (slot % 64));  // occupancy (cleared per hop)
         const uint32_t u = ps.halo_node[slot];
-        atomicOr((unsigned long long*)&ps.touch[u / 64], 1ull << (u % 64));  // u has a sender this hop
+        atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));  // u has a sender this hop
     }
 }
 
@@ -289,15 +291,26 @@ __device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
     return prev < ps.n_nodes / 16 && !(ps.halo && !ps.halo_occ);
 }
 __global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, const uint64_t* __restrict__ front_occ) {
+    // housekeeping of this hop: its occupancy row (the hop ORs bits in) and
+    // the other touch buffer (the next hop's, marked by its halo scatter and
+    // its own k_prop_mark) start empty
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    uint64_t* occ_h = ps.occ + (size_t)h * occ_row;
+    uint64_t* touch_next = ps.touch + (size_t)((h + 1) & 1) * occ_row;
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < occ_row; i += (size_t)gridDim.x * 256u) {
+        occ_h[i] = 0;
+        touch_next[i] = 0;
+    }
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     if (!mark_hop(ps, h) || (!ps.sharded && h > 1 && prev == 0)) return;
+    uint64_t* touch = ps.touch + (size_t)(h & 1) * occ_row;
     for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < ps.n_nodes; v += gridDim.x * 256u) {
         if (!((front_occ[v / 64] >> (v % 64)) & 1)) continue;
         for (int64_t r = ps.row_ptr[v]; r < ps.row_ptr[v + 1]; ++r) {
             const uint32_t q = ps.rev[r];
             if (q == NO_PAIR || (q & HALO) || !ps.fwd[r]) continue;  // v sends nothing to a local u
             const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
-            atomicOr((unsigned long long*)&ps.touch[u / 64], 1ull << (u % 64));
+            atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));
         }
     }
 }
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
         const uint32_t u = tile + gi;
         bool any_new = false;
         bool touch = u < ps.n_nodes;
-        if (touch && use_mark) touch = occ_bit(ps.touch, u);
+        if (touch && use_mark) touch = occ_bit(ps.touch + (size_t)(h & 1) * occ_row, u);
         if (touch) {
             const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
             const size_t un = (size_t)u * W;
@@ -597,22 +610,32 @@ __device__ __forceinline__ DupsLast dups_last(const PropState& ps, uint32_t h_ru
 }
 
 // Per sender v: the size of its forwarded set (seen minus the last hop's
-// receipts) and the part of it v published, packed n_all | n_own << 32.
+// receipts) and the part of it v published, packed n_all | n_own << 32.  L
+// lanes per node, 4 words each per step, summed with shuffles.
+template <int L>
 __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_run, uint64_t* __restrict__ vcnt) {
-    const DupsLast L = dups_last(ps, h_run);
+    const DupsLast L_ = dups_last(ps, h_run);
     const uint32_t W = ps.n_words;
-    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < ps.n_nodes; v += gridDim.x * 256u) {
+    const uint32_t lc = threadIdx.x % L;
+    const uint32_t CWv = L > 1 ? 4 : W;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t / L < ps.n_nodes; t += gridDim.x * 256u) {
+        const uint32_t v = t / L;
         const bool v_src = occ_bit(ps.occ, v);
-        const bool v_last = !L.empty && occ_bit(L.occ, v);
+        const bool v_last = !L_.empty && occ_bit(L_.occ, v);
         uint32_t n_all = 0, n_own = 0;
-        for (uint32_t w = 0; w < W; ++w) {
-            const size_t vw = (size_t)v * W + w;
-            uint64_t s = ps.seen[vw];
-            if (v_last) s &= ~L.row[vw];
-            n_all += __popcll(s);
-            if (v_src) n_own += __popcll(s & ps.origin[vw]);
+        for (uint32_t w0 = lc * CWv; w0 < W; w0 += L * CWv)
+            for (uint32_t w = w0; w < w0 + CWv; ++w) {
+                const size_t vw = (size_t)v * W + w;
+                uint64_t s = ps.seen[vw];
+                if (v_last) s &= ~L_.row[vw];
+                n_all += __popcll(s);
+                if (v_src) n_own += __popcll(s & ps.origin[vw]);
+            }
+        if (L > 1) {
+            n_all = group_sum<L>(n_all);
+            n_own = group_sum<L>(n_own);
         }
-        vcnt[v] = (uint64_t)n_all | ((uint64_t)n_own << 32);
+        if (lc == 0) vcnt[v] = (uint64_t)n_all | ((uint64_t)n_own << 32);
     }
 }
 
@@ -675,17 +698,46 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
 // ---- P2/P3 credits ------------------------------------------------------------
 // Per receiver pair q = (u -> v), add this call's first receipts from v (the
 // hop kernel's fcnt) and in-window duplicates to the pending counts.
-__global__ __launch_bounds__(256) void k_prop_count(PropState ps) {
+// Fold pending counts: k1 first receipts, k2 duplicates inside the window.
+// markFirstMessageDelivery: fmd k1 steps of +1 then cap, mmd too when in
+// mesh; markDuplicateMessageDelivery: mmd k2 more steps when in mesh
+// (score.go:912-974).  All steps are identical, so their order does not
+// matter; add_ones_capped gives the result of the steps one by one.
+__device__ __forceinline__ void fold_pair(const PropState& ps, const DevState& s, uint64_t q, uint32_t k1, uint32_t k2) {
+    const DevTopicParams& tp = s.tp[ps.topic];
+    const size_t b = rec_index(q, ps.topic, s.n_topics, FMD);
+    s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], k1, tp.cap2);
+    if (!(s.rflags[flag_index(q, ps.topic, s.n_topics)] & REC_IN_MESH)) return;
+    s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
+}
+
+// Per receiver pair q = (u -> v): this call's first receipts from v (the hop
+// kernel's fcnt) and in-window duplicates join the pending counts; with FOLD
+// (GSX_CREDIT_NOW) they are folded into the record at once.
+template <bool FOLD>
+__global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
     unsigned long long cnt[1] = {0};
+    const bool fold_topic = FOLD && ps.topic < s.n_topics && s.tp[ps.topic].scored;
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
         const uint32_t k1 = ps.fcnt[q];
         const uint32_t r = ps.rev[q];
         const bool local = r != NO_PAIR && !(r & HALO);
         if (ps.credit) {
-            if (k1) ps.firstcnt[q] += k1;
+            const uint32_t f0 = ps.firstcnt[q], d0 = ps.dupcnt[q];
+            uint32_t first = f0 + k1, dup = d0;
             if (local) {
-                if (ps.late) ps.dupcnt[q] += ps.corr[r] - k1;  // k_prop_dups: every send from v, first receipts too
-                else if (const uint32_t c = ps.corr[r]) ps.dupcnt[q] -= c;  // in-window back-sends taken back
+                if (ps.late) dup += ps.corr[r] - k1;  // k_prop_dups: every send from v, first receipts too
+                else dup -= ps.corr[r];               // in-window back-sends taken back
+            }
+            if (FOLD) {  // GSX_CREDIT_NOW: fold at once (k_prop_fold) and leave the counts empty
+                if (f0 | d0) {
+                    ps.firstcnt[q] = 0;
+                    ps.dupcnt[q] = 0;
+                }
+                if ((first | dup) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup);
+            } else {
+                ps.firstcnt[q] = first;
+                ps.dupcnt[q] = dup;
             }
         }
         if (ps.late && local) cnt[0] += k1;
@@ -694,25 +746,17 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps) {
     block_count<1>(cnt, ps.stats, slot);
 }
 
-// Fold pending counts: k1 first receipts, k2 duplicates inside the window.
-// markFirstMessageDelivery: fmd k1 steps of +1 then cap, mmd too when in
-// mesh; markDuplicateMessageDelivery: mmd k2 more steps when in mesh
-// (score.go:912-974).  All steps are identical, so their order does not
-// matter; add_ones_capped gives the result of the steps one by one.
+// Fold of pending counts (gsx_prop_fold_credits; GSX_CREDIT_NOW folds in k_prop_count).
 __global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, const uint32_t* __restrict__ first,
                                                    const uint32_t* __restrict__ dup) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= s.n_pairs) return;
     if (!(s.pflags[q] & PAIR_PRESENT) || ps.topic >= s.n_topics) return;
-    const DevTopicParams& tp = s.tp[ps.topic];
-    if (!tp.scored) return;
+    if (!s.tp[ps.topic].scored) return;
     const uint32_t k1 = first[q];
     const uint32_t k2 = dup[q];
     if (k1 == 0 && k2 == 0) return;
-    const size_t b = rec_index(q, ps.topic, s.n_topics, FMD);
-    s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], k1, tp.cap2);
-    if (!(s.rflags[flag_index(q, ps.topic, s.n_topics)] & REC_IN_MESH)) return;
-    s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
+    fold_pair(ps, s, q, k1, k2);
 }
 
 // First deliverer per (message, node) from the per-pair "first got it from" rows.
@@ -807,10 +851,10 @@ hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t
     return hipGetLastError();
 }
 hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
-                               uint64_t* halo_occ, hipStream_t st) {
+                               uint64_t* halo_occ, uint32_t h, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_halo_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, ent, n,
-                       idx, halo_occ);
+                       idx, halo_occ, h);
     return hipGetLastError();
 }
 template <int CW, int LPN>
@@ -843,20 +887,28 @@ hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* fron
 }
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st) {
     if (ps.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_mark, dim3(std::min(nblk(ps.n_nodes, 256), 1024u)), dim3(256), 0, st, ps, h, front_occ);
+    hipLaunchKernelGGL(k_prop_mark, dim3(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h, front_occ);
     return hipGetLastError();
 }
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_vcount, dim3(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
-                       vcnt);
+    const uint32_t W = ps.n_words;
+    const int L = W % 64 == 0 ? 16 : W % 32 == 0 ? 8 : W % 16 == 0 ? 4 : W % 8 == 0 ? 2 : 1;
+    const dim3 gv(std::min(nblk((uint64_t)ps.n_nodes * L, 256), COUNTER_GRID));
+    if (L == 16) hipLaunchKernelGGL(k_prop_vcount<16>, gv, dim3(256), 0, st, ps, h_run, vcnt);
+    else if (L == 8) hipLaunchKernelGGL(k_prop_vcount<8>, gv, dim3(256), 0, st, ps, h_run, vcnt);
+    else if (L == 4) hipLaunchKernelGGL(k_prop_vcount<4>, gv, dim3(256), 0, st, ps, h_run, vcnt);
+    else if (L == 2) hipLaunchKernelGGL(k_prop_vcount<2>, gv, dim3(256), 0, st, ps, h_run, vcnt);
+    else hipLaunchKernelGGL(k_prop_vcount<1>, gv, dim3(256), 0, st, ps, h_run, vcnt);
     hipLaunchKernelGGL(k_prop_dups, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
                        vcnt);
     return hipGetLastError();
 }
-hipError_t launch_prop_count(const PropState& ps, hipStream_t st) {
+hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_count, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps);
+    const dim3 g(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), b(256);
+    if (fold) hipLaunchKernelGGL(k_prop_count<true>, g, b, 0, st, ps, s);
+    else hipLaunchKernelGGL(k_prop_count<false>, g, b, 0, st, ps, s);
     return hipGetLastError();
 }
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
