@@ -331,11 +331,148 @@ __device__ __forceinline__ void load_words(uint64_t (&d)[CW], const uint64_t* p)
     for (int i = 0; i < CW; ++i) d[i] = p[i];
 }
 
+// Sum over the LPN lanes of a group (aligned), every lane gets the sum.
+// Groups of 2 and 4 use DPP quad permutes (a VALU operand modifier, no LDS
+// crossbar); wider groups fall back to ds_bpermute shuffles.
 template <int LPN>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+    if (LPN == 2 || LPN == 4) {
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        if (LPN == 4) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+        return x;
+    }
 #pragma unroll
     for (int o = 1; o < LPN; o <<= 1) x += __shfl_xor(x, o, LPN);
     return x;
+}
+
+// The common case as its own lean kernel (k_prop_hop_fast): one engine (no
+// halo), no RandomSub draws, no first-deliverer rows, and late duplicate
+// accounting (every duplicate inside the P3 window, or no credits), so the
+// hop only moves first receipts: per pair and word, eligibility, "not seen,
+// not from a lower sender", and a popcount.  Same results as k_prop_hop.
+template <int CW, int LPN>
+__global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
+                                                       uint64_t* __restrict__ nxt) {
+    constexpr int U = 4;
+    constexpr uint32_t NB = 256 / LPN;
+    constexpr uint32_t NW = 64 / LPN;
+    const uint32_t W = ps.n_words;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint64_t* __restrict__ occ_src = ps.occ;
+    const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
+    uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    if (h > 1 && prev == 0) return;
+    const bool use_occ = prev < ps.n_nodes / 4;
+    const bool use_mark = mark_hop(ps, h);
+    // rows of hop h - 1 can be stale only if that hop left nodes untouched
+    const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
+    const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
+    const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;
+    unsigned long long n_new = 0, n_send = 0, n_vnew = 0;
+    for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
+        const uint32_t u = tile + gi;
+        bool any_new = false;
+        bool touch = u < ps.n_nodes;
+        if (touch && use_mark) touch = occ_bit(touch_h, u);
+        if (touch) {
+            const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
+            const size_t un = (size_t)u * W;
+            // (u's own messages need no mask here: they are in `seen` since
+            // hop 0, and duplicates are counted at the end of the call)
+            for (uint32_t w0 = lc * CW; w0 < W; w0 += LPN * CW) {
+                uint64_t seen[CW], sa[CW];
+                load_words<CW>(seen, ps.seen + un + w0);
+#pragma unroll
+                for (int i = 0; i < CW; ++i) sa[i] = seen[i];
+                uint32_t pn[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) pn[j] = q0 + j < q1 ? ps.pin[q0 + j] : NO_PAIR;
+                for (int64_t qb = q0; qb < q1; qb += U) {
+                    uint32_t pv[U];
+                    uint64_t c[U][CW];
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        pv[j] = pn[j];
+                        if (use_occ && pv[j] != NO_PAIR && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK)) pv[j] = NO_PAIR;
+                    }
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        if (pv[j] != NO_PAIR) load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
+                        else
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] = 0;
+                    }
+                    uint32_t fc[U];
+#pragma unroll
+                    for (int j = 0; j < U; ++j) fc[j] = lc == 0 && pv[j] != NO_PAIR ? ps.fcnt[qb + j] : 0;
+#pragma unroll
+                    for (int j = 0; j < U; ++j) pn[j] = qb + U + j < q1 ? ps.pin[qb + U + j] : NO_PAIR;
+                    if (check_rows)
+#pragma unroll
+                        for (int j = 0; j < U; ++j)
+                            if (pv[j] != NO_PAIR && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK))
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) c[j][i] = 0;
+#pragma unroll
+                    for (int j = 0; j < U; ++j) {
+                        if (__ballot(pv[j] != NO_PAIR) == 0) continue;  // no lane of the wave has pair j
+                        // branch-free over the lanes: an absent pair carries an empty row
+                        const uint32_t m = pv[j] == NO_PAIR ? 0u : pv[j] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
+                        // eligibility: FORWARD lets through what v received, PUBLISH what v published
+                        uint64_t own[CW];
+#pragma unroll
+                        for (int i = 0; i < CW; ++i) own[i] = 0;
+                        if (m == FWD_FORWARD || m == FWD_PUBLISH) {
+                            const uint32_t v = pv[j] & PIN_NODE_MASK;
+                            if (occ_bit(occ_src, v)) load_words<CW>(own, ps.origin + (size_t)v * W + w0);
+                        }
+                        const uint64_t fmask = (m & FWD_FORWARD) ? ~0ull : 0ull, pmask = (m & FWD_PUBLISH) ? ~0ull : 0ull;
+                        uint32_t fresh = 0;
+#pragma unroll
+                        for (int i = 0; i < CW; ++i) {
+                            const uint64_t cc = c[j][i] & ((fmask & ~own[i]) | (pmask & own[i]));
+                            n_send += cc != 0;
+                            const uint64_t nb = cc & ~sa[i];  // not seen, not from a lower sender
+                            sa[i] |= nb;
+                            fresh += __popcll(nb);
+                        }
+                        n_new += fresh;
+                        if (LPN > 1) fresh = group_sum<LPN>(fresh);
+                        if (lc == 0 && fresh) {
+                            const int64_t q = qb + j;
+                            ps.fcnt[q] = fc[j] + fresh;
+                            ps.flast[q] = ((uint64_t)h << 32) | fresh;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < CW; ++i) {
+                    const uint64_t acc = sa[i] ^ seen[i];
+                    nxt[un + w0 + i] = acc;
+                    if (acc) {
+                        ps.seen[un + w0 + i] = sa[i];
+                        ++n_vnew;
+                        any_new = true;
+                    }
+                }
+            }
+        }
+        if (LPN > 1) any_new = group_sum<LPN>(any_new ? 1u : 0u) != 0;
+        uint64_t wb = __ballot(any_new && lc == 0);
+        if (LPN > 1) {
+            uint64_t r = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < NW; ++i) r |= ((wb >> (i * LPN)) & 1ull) << i;
+            wb = r;
+        }
+        const uint32_t u0 = tile + (threadIdx.x / 64) * NW;
+        if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
+    }
+    unsigned long long cnt[3] = {n_new, n_send, n_vnew};
+    const uint32_t slot[3] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS};
+    block_count<3>(cnt, ps.stats, slot);
 }
 
 // The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
@@ -377,6 +514,8 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
     // occupancy bits.
     const bool use_occ = prev < ps.n_nodes / 4;
     const bool use_mark = mark_hop(ps, h);
+    // rows of hop h - 1 can be stale only if that hop left nodes untouched
+    const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
     // Back-sends of this hop's first receipts would happen at hop h + 1 (if
     // it runs).  At h = 1 the receipts are the sender's own publishes, which
     // nobody sends back to their origin anyway.
@@ -457,7 +596,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                     bool dead[U];  // rows of senders the previous hop left untouched are empty
 #pragma unroll
                     for (int j = 0; j < U; ++j)
-                        dead[j] = !use_occ && pv[j] != NO_PAIR && !(pv[j] & HALO) &&
+                        dead[j] = check_rows && pv[j] != NO_PAIR && !(pv[j] & HALO) &&
                                   !occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
                     // the block's per-pair counters travel with its rows (group lane 0
                     // keeps them): no load-then-store chain per pair below
@@ -860,7 +999,10 @@ hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64
 template <int CW, int LPN>
 static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
-    if (ps.from_mask) hipLaunchKernelGGL((k_prop_hop<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
+    static const bool no_fast = getenv("GSX_HOP_GENERAL") != nullptr;  // tuning / cross-checks
+    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast)
+        hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN>), g, b, 0, st, ps, h, front, nxt);
+    else if (ps.from_mask) hipLaunchKernelGGL((k_prop_hop<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
     else hipLaunchKernelGGL((k_prop_hop<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
 }
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {

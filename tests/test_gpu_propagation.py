@@ -28,13 +28,17 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("track", [True, False], ids=["rows", "counts"])
+@pytest.mark.parametrize("track", [True, False, "late"], ids=["rows", "counts", "counts-late"])
 @pytest.mark.parametrize("case", CASES, ids=[f"r{c[3]}-n{c[0]}-m{c[5]}" for c in CASES])
 def test_propagation_matches_oracle(gpu_ok, case, track):
     """track=False: no first-deliverer rows (gsx_prop_set_tracking), the
     duplicate accounting counts the `from` exclusion instead of masking it;
-    every counter, hop, credit and score must still match."""
+    every counter, hop, credit and score must still match.  "late": the same
+    with zero hop latency, so every duplicate is inside the P3 window and the
+    hops only move first receipts (the lean hop kernel for flood/gossipsub)."""
     n, d, T, router, fp, m, lat, mix, direct, disc = case
+    if track == "late":
+        track, lat = False, 0
     seed = n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=direct)
     ms = pc.messages(n, m, seed)
