@@ -184,6 +184,7 @@ struct PropState {
     uint32_t router, topic, flood_publish, credit, all_dups_in_window, rsub_sqrt, sharded;
     uint32_t max_hops, back_in_window;  // back_in_window: 2 * latency <= P3 window
     uint32_t late;                      // duplicates of local pairs by k_prop_dups at the end of the call
+    uint32_t pending;                   // the pending credit counts may be non-zero (else they are not read)
     uint64_t* occ;                      // [hop][node / 64] bit per node: frontier row non-empty
     double publish_threshold;
     int64_t hop_latency, window;

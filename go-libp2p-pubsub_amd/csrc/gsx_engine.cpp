@@ -1390,6 +1390,7 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     else ps.win_hops = (uint32_t)std::min<int64_t>(ps.window / cfg->hop_latency_ns, GSX_MAX_HOPS + 1);
     ps.back_in_window = (2 * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
     ps.late = (!ps.credit || ps.all_dups_in_window) ? 1 : 0;
+    ps.pending = (P.credit_pending || !ps.late || e->sharded() || cfg->credit_scores == GSX_CREDIT_DEFER) ? 1 : 0;
     ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
     ps.publish_threshold = e->th.publish_threshold;
     ps.seed = cfg->seed;

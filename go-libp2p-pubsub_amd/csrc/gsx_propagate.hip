@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
             out = (ef & EDGE_FLOODSUB) ? (FWD_FORWARD | FWD_PUBLISH) : FWD_RSUB_CAND;
         } else {  // gossipsub
             const bool direct = ef & EDGE_DIRECT;
-            const bool above = s.score[r] >= ps.publish_threshold;
+            // the score is read only where a threshold decides (floodsub peers, flood publish)
+            const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
+            const bool above = need_score && s.score[r] >= ps.publish_threshold;
             bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
             if (!fwd && ps.topic < s.n_topics)                       // mesh peers (:977-999)
                 fwd = s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH;
@@ -824,7 +826,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
         if (!ps.from_mask && (fw & FWD_FORWARD) && h_run >= 1) {
             const uint64_t fl = ps.flast[r];
             const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
-            const uint32_t from_pub = (ps.fwd[q] & FWD_PUBLISH) ? pub : 0;
+            const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH)) ? pub : 0;  // pub != 0 only if u published
             sends -= ps.fcnt[r] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
         }
         cnt[0] += sends;
@@ -862,7 +864,9 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
         const uint32_t r = ps.rev[q];
         const bool local = r != NO_PAIR && !(r & HALO);
         if (ps.credit) {
-            const uint32_t f0 = ps.firstcnt[q], d0 = ps.dupcnt[q];
+            // (unsharded, late accounting, nothing deferred: the hops wrote no
+            // pending counts and none were left, so they are not read)
+            const uint32_t f0 = ps.pending ? ps.firstcnt[q] : 0, d0 = ps.pending ? ps.dupcnt[q] : 0;
             uint32_t first = f0 + k1, dup = d0;
             if (local) {
                 if (ps.late) dup += ps.corr[r] - k1;  // k_prop_dups: every send from v, first receipts too
@@ -1018,7 +1022,8 @@ hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* fron
     if (W == 1) hop_launch<1, 1>(ps, h, front, nxt, st);
     else if (W == 2) hop_launch<2, 1>(ps, h, front, nxt, st);
     else if (cw_env == 2) {
-        if (W % 8 == 0) hop_launch<2, 4>(ps, h, front, nxt, st);
+        if (W % 16 == 0) hop_launch<2, 8>(ps, h, front, nxt, st);
+        else if (W % 8 == 0) hop_launch<2, 4>(ps, h, front, nxt, st);
         else hop_launch<2, 2>(ps, h, front, nxt, st);
     } else {
         if (W % 16 == 0) hop_launch<4, 4>(ps, h, front, nxt, st);
