@@ -27,6 +27,10 @@
 
 #include <cstdlib>
 
+#ifndef GSX_FAST_U
+#define GSX_FAST_U 4
+#endif
+
 namespace gsx {
 
 // Eligibility of every pair (v -> u) for this call (topic, router, scores).
@@ -356,7 +360,7 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
 template <int CW, int LPN>
 __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                        uint64_t* __restrict__ nxt) {
-    constexpr int U = 4;
+    constexpr int U = GSX_FAST_U;
     constexpr uint32_t NB = 256 / LPN;
     constexpr uint32_t NW = 64 / LPN;
     const uint32_t W = ps.n_words;
@@ -422,19 +426,24 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                         if (__ballot(pv[j] != NO_PAIR) == 0) continue;  // no lane of the wave has pair j
                         // branch-free over the lanes: an absent pair carries an empty row
                         const uint32_t m = pv[j] == NO_PAIR ? 0u : pv[j] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
-                        // eligibility: FORWARD lets through what v received, PUBLISH what v published
-                        uint64_t own[CW];
+                        // eligibility: FORWARD lets through what v received, PUBLISH what v
+                        // published.  An absent pair's row is empty and a FORWARD|PUBLISH pair
+                        // passes everything, so only a wave holding a one-sided pair masks.
+                        if (__ballot(m == FWD_FORWARD || m == FWD_PUBLISH)) {
+                            uint64_t own[CW];
 #pragma unroll
-                        for (int i = 0; i < CW; ++i) own[i] = 0;
-                        if (m == FWD_FORWARD || m == FWD_PUBLISH) {
+                            for (int i = 0; i < CW; ++i) own[i] = 0;
                             const uint32_t v = pv[j] & PIN_NODE_MASK;
-                            if (occ_bit(occ_src, v)) load_words<CW>(own, ps.origin + (size_t)v * W + w0);
+                            if ((m == FWD_FORWARD || m == FWD_PUBLISH) && occ_bit(occ_src, v))
+                                load_words<CW>(own, ps.origin + (size_t)v * W + w0);
+                            const uint64_t fmask = (m & FWD_FORWARD) ? ~0ull : 0ull, pmask = (m & FWD_PUBLISH) ? ~0ull : 0ull;
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] &= (fmask & ~own[i]) | (pmask & own[i]);
                         }
-                        const uint64_t fmask = (m & FWD_FORWARD) ? ~0ull : 0ull, pmask = (m & FWD_PUBLISH) ? ~0ull : 0ull;
                         uint32_t fresh = 0;
 #pragma unroll
                         for (int i = 0; i < CW; ++i) {
-                            const uint64_t cc = c[j][i] & ((fmask & ~own[i]) | (pmask & own[i]));
+                            const uint64_t cc = c[j][i];
                             n_send += cc != 0;
                             const uint64_t nb = cc & ~sa[i];  // not seen, not from a lower sender
                             sa[i] |= nb;
