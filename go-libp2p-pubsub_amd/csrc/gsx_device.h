@@ -130,6 +130,8 @@ enum {
     STAT_EDGE_SENDS = STAT_HOP0 + MAX_HOPS + 1,
     STAT_NEW_WORDS,
     STAT_BACKSENDS,
+    STAT_REJECTED,  // receipts of REJECT messages
+    STAT_IGNORED,   // receipts of IGNORE / THROTTLE messages
     STAT_WORDS
 };
 // rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
@@ -139,8 +141,8 @@ constexpr uint32_t MAX_RANKS = 64;  // ranks of a shard plan (one node: 8)
 constexpr uint32_t PIN_NODE_MASK = (1u << PIN_FWD_SHIFT) - 1;  // nodes per shard < 2^29
 
 struct DevMsg {
-    uint32_t source;  // global node id
-    uint32_t reserved;
+    uint32_t source;      // global node id
+    uint32_t validation;  // GSX_VALIDATION_*
     uint64_t msg_id;
 };
 
@@ -185,6 +187,10 @@ struct PropState {
     uint32_t max_hops, back_in_window;  // back_in_window: 2 * latency <= P3 window
     uint32_t late;                      // duplicates of local pairs by k_prop_dups at the end of the call
     uint32_t pending;                   // the pending credit counts may be non-zero (else they are not read)
+    const uint64_t* drop;               // [word]: messages not accepted (seen, not delivered, not forwarded); null: none
+    const uint64_t* reject;             // [word]: REJECT messages (P4 to the sender)
+    uint32_t* invcnt;                   // per pair: pending invalid deliveries (markInvalidMessageDelivery)
+    uint64_t* dseen;                    // [node][word]: hop-1 receipts of dropped messages (after the call)
     uint64_t* occ;                      // [hop][node / 64] bit per node: frontier row non-empty
     double publish_threshold;
     int64_t hop_latency, window;
@@ -209,6 +215,7 @@ hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st);
+hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st);
 
 // ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------
 constexpr int HB_MAX_DEG = 256;  // per-node pair count the mesh lanes hold (u16 offsets, scratch)

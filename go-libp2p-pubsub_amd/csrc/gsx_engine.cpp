@@ -131,6 +131,11 @@ struct gsx_engine {
         uint8_t* fwd = nullptr;
         uint32_t* pin = nullptr;
         uint32_t *dup = nullptr, *first = nullptr;  // pending P2/P3 credit counts per pair
+        uint32_t* inv = nullptr;    // pending invalid deliveries per pair (P4, REJECT messages)
+        uint64_t* vmask = nullptr;  // [2][word]: messages validation drops / rejects, this call
+        uint64_t* dseen = nullptr;  // [node][word]: hop-1 receipts of dropped messages (gsx_prop_results)
+        size_t dseen_words = 0;
+        bool has_drop = false;
         uint32_t* fcnt = nullptr;   // per pair, this call: first receipts
         uint64_t* flast = nullptr;  // per pair: hop << 32 | first receipts of its last such hop
         size_t from_words = 0;      // allocation of `from` (tracked first deliverers)
@@ -338,7 +343,7 @@ void free_state(gsx_engine* e) {
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
-                  e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom,
+                  e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
                   e->prop.touch, e->prop.vcnt, e->d_halo_node};
     for (void* p : pp)
         if (p) (void)hipFree(p);
@@ -1324,10 +1329,10 @@ uint32_t prop_words(size_t m) {
 int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
     seen_release(e, P.seen, P.seen_words);
-    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats, P.touch, P.vcnt};
+    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats, P.touch, P.vcnt, P.vmask};
     for (void* p : pp)
         if (p) (void)hipFree(p);
-    P.seen = P.hist = P.origin = P.from = P.sel = P.occ = P.touch = P.vcnt = nullptr;
+    P.seen = P.hist = P.origin = P.from = P.sel = P.occ = P.touch = P.vcnt = P.vmask = nullptr;
     P.from_words = 0;
     P.msgs = nullptr;
     P.stats = nullptr;
@@ -1355,6 +1360,10 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.from_mask = (e->prop_track || cfg->router == GSX_ROUTER_RANDOMSUB) ? P.from : nullptr;
     ps.fcnt = P.fcnt;
     ps.flast = P.flast;
+    ps.invcnt = P.inv;
+    ps.drop = P.has_drop ? P.vmask : nullptr;
+    ps.dseen = P.has_drop ? P.dseen : nullptr;
+    ps.reject = P.vmask ? P.vmask + W : nullptr;
     ps.hfrom = P.hfrom;
     ps.halo_occ = nullptr;
     ps.touch = P.touch;
@@ -1383,12 +1392,15 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.credit = (cfg->credit_scores && scored) ? 1 : 0;
     ps.window = scored ? e->tp[cfg->topic].mesh_message_deliveries_window_ns : 0;
     ps.hop_latency = cfg->hop_latency_ns;
-    ps.all_dups_in_window = ((int64_t)cfg->max_hops * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
-    // (h - h0) * latency <= window  <=>  h - h0 <= window / latency (latency > 0)
+    // A hop takes L = latency + validation delay D; a copy arriving g hops
+    // after the first one is (g * L - D) after the first finished validating,
+    // so it is inside the P3 window iff g * L <= window + D.
+    const int64_t L = cfg->hop_latency_ns + cfg->validation_delay_ns, WD = ps.window + cfg->validation_delay_ns;
+    ps.all_dups_in_window = ((int64_t)cfg->max_hops * L <= WD) ? 1 : 0;
     if (ps.window < 0) ps.win_hops = 0;
-    else if (cfg->hop_latency_ns == 0) ps.win_hops = GSX_MAX_HOPS + 1;
-    else ps.win_hops = (uint32_t)std::min<int64_t>(ps.window / cfg->hop_latency_ns, GSX_MAX_HOPS + 1);
-    ps.back_in_window = (2 * cfg->hop_latency_ns <= ps.window) ? 1 : 0;
+    else if (L == 0) ps.win_hops = GSX_MAX_HOPS + 1;
+    else ps.win_hops = (uint32_t)std::min<int64_t>(WD / L, GSX_MAX_HOPS + 1);
+    ps.back_in_window = (2 * L <= WD) ? 1 : 0;
     ps.late = (!ps.credit || ps.all_dups_in_window) ? 1 : 0;
     ps.pending = (P.credit_pending || !ps.late || e->sharded() || cfg->credit_scores == GSX_CREDIT_DEFER) ? 1 : 0;
     ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
@@ -1416,8 +1428,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (cfg->max_hops > GSX_MAX_HOPS || cfg->router > GSX_ROUTER_RANDOMSUB || m > 0xFFFFFFFFull ||
         cfg->credit_scores > GSX_CREDIT_DEFER || cfg->hop_latency_ns < 0)
         return fail(e, GSX_EINVAL, "bad propagation config");
-    for (size_t k = 0; k < m; ++k)
+    for (size_t k = 0; k < m; ++k) {
         if (msgs[k].source >= e->n_total) return fail(e, GSX_ERANGE, "message source out of range");
+        if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return fail(e, GSX_EINVAL, "bad message validation outcome");
+    }
+    if (cfg->validation_delay_ns < 0) return fail(e, GSX_EINVAL, "negative validation delay");
     if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^29 nodes per engine");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
@@ -1436,15 +1451,16 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         if ((rc = dalloc(e, &P.hist, (size_t)rc_rows * W * N)) ||
             (rc = dalloc(e, &P.occ, (size_t)rc_rows * ((N + 63) / 64))) ||
             (rc = dalloc(e, &P.touch, 2 * ((N + 63) / 64))) || (rc = dalloc(e, &P.vcnt, std::max<size_t>(N, 1))) ||
-            (rc = dalloc(e, &P.origin, W * N)) ||
+            (rc = dalloc(e, &P.origin, W * N)) || (rc = dalloc(e, &P.vmask, 2 * (size_t)W)) ||
             (rc = dalloc(e, &P.msgs, mm)) ||
             (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
             return rc;
         if (!P.fwd) {
             if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.pin, E)) || (rc = dalloc(e, &P.dup, E)) ||
                 (rc = dalloc(e, &P.corr, E)) || (rc = dalloc(e, &P.fcnt, E)) || (rc = dalloc(e, &P.flast, E)) ||
-                (rc = dalloc(e, &P.first, E)))
+                (rc = dalloc(e, &P.first, E)) || (rc = dalloc(e, &P.inv, E)))
                 return rc;
+            HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * std::max<size_t>(E, 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * std::max<size_t>(E, 1), e->stream));
         }
@@ -1498,6 +1514,26 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (!P.dcount) {
         if (int rc = dalloc(e, &P.dcount, (size_t)gsx::MAX_RANKS)) return rc;
     }
+    std::vector<uint64_t> vm(2 * (size_t)W, 0);  // (copied before the stream sync at the end)
+    {  // validation outcomes of this call: dropped / rejected message bits
+        P.has_drop = false;
+        for (size_t k = 0; k < m; ++k)
+            if (msgs[k].validation != GSX_VALIDATION_ACCEPT) {
+                vm[k / 64] |= 1ull << (k % 64);
+                if (msgs[k].validation == GSX_VALIDATION_REJECT) vm[W + k / 64] |= 1ull << (k % 64);
+                P.has_drop = true;
+            }
+        if (P.has_drop) {
+            HIPCHK(e, hipMemcpyAsync(P.vmask, vm.data(), 8 * vm.size(), hipMemcpyHostToDevice, e->stream));
+            if (P.dseen_words < (size_t)W * N) {
+                if (P.dseen) (void)hipFree(P.dseen);
+                P.dseen = nullptr;
+                P.dseen_words = 0;
+                if (int rc = dalloc(e, &P.dseen, (size_t)W * N)) return rc;
+                P.dseen_words = (size_t)W * N;
+            }
+        }
+    }
     gsx::PropState ps = prop_state(e, W, m, cfg);
     P.last = ps;
     P.have_last = true;
@@ -1511,7 +1547,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
     if (m == 0) return GSX_OK;
     std::vector<gsx::DevMsg> hm(m);
-    for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, 0, msgs[k].msg_id};
+    for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, msgs[k].validation, msgs[k].msg_id};
     HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
     HIPCHK(e, hipMemsetAsync(P.hist, 0, 8 * (size_t)W * N, e->stream));  // row 0: the publishes
@@ -1560,6 +1596,7 @@ int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
     HIPCHK(e, gsx::launch_prop_fold(ps, dev_state(e), P.first, P.dup, e->stream));
     HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * e->E, e->stream));
     HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * e->E, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * e->E, e->stream));
     P.credit_pending = false;
     e->scores_valid = false;
     return GSX_OK;
@@ -1582,6 +1619,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         if (fold_now) e->scores_valid = false;
     }
     const uint32_t W = ps.n_words;
+    if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
         gsx_engine::McBatch b;
         b.topic = P.cfg.topic;
@@ -1603,7 +1641,9 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         out->deliveries += st[gsx::STAT_HOP0 + h];
         if (st[gsx::STAT_HOP0 + h]) out->hops = h;
     }
-    out->transmissions = out->deliveries + out->duplicates;
+    out->rejected = st[gsx::STAT_REJECTED];
+    out->ignored = st[gsx::STAT_IGNORED];
+    out->transmissions = out->deliveries + out->duplicates + out->rejected + out->ignored;
     P.rows_valid = P.h + 1;
     for (uint32_t h = 1; h <= P.h && !ps.sharded; ++h)
         if (st[gsx::STAT_HOP0 + h] == 0) {  // hop h ran and wrote an empty row; later hops were skipped
@@ -1737,6 +1777,24 @@ int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup) {
     if (first) HIPCHK(e, hipMemcpyAsync(first, e->prop.first, 4 * e->E, hipMemcpyDefault, e->stream));
     if (dup) HIPCHK(e, hipMemcpyAsync(dup, e->prop.dup, 4 * e->E, hipMemcpyDefault, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_pending_invalid(gsx_engine* e, uint32_t* inv) {
+    if (!e || !inv) return GSX_EINVAL;
+    if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
+    HIPCHK(e, hipMemcpyAsync(inv, e->prop.inv, 4 * e->E, hipMemcpyDefault, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_replace_pending_invalid(gsx_engine* e, const uint32_t* inv) {
+    if (!e || !inv) return GSX_EINVAL;
+    if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    HIPCHK(e, hipMemcpyAsync(e->prop.inv, inv, 4 * e->E, hipMemcpyDefault, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->prop.credit_pending = true;
     return GSX_OK;
 }
 

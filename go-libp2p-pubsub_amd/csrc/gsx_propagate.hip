@@ -357,7 +357,7 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
 // accounting (every duplicate inside the P3 window, or no credits), so the
 // hop only moves first receipts: per pair and word, eligibility, "not seen,
 // not from a lower sender", and a popcount.  Same results as k_prop_hop.
-template <int CW, int LPN>
+template <int CW, int LPN, bool DROP>
 __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                        uint64_t* __restrict__ nxt) {
     constexpr int U = GSX_FAST_U;
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
     const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
     const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;
-    unsigned long long n_new = 0, n_send = 0, n_vnew = 0;
+    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0;
     for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
         const uint32_t u = tile + gi;
         bool any_new = false;
@@ -388,8 +388,12 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
             // (u's own messages need no mask here: they are in `seen` since
             // hop 0, and duplicates are counted at the end of the call)
             for (uint32_t w0 = lc * CW; w0 < W; w0 += LPN * CW) {
-                uint64_t seen[CW], sa[CW];
+                uint64_t seen[CW], sa[CW], drp[CW], rej[CW];
                 load_words<CW>(seen, ps.seen + un + w0);
+                if (DROP) {  // messages validation does not accept: seen, not delivered, not forwarded
+                    load_words<CW>(drp, ps.drop + w0);
+                    load_words<CW>(rej, ps.reject + w0);
+                }
 #pragma unroll
                 for (int i = 0; i < CW; ++i) sa[i] = seen[i];
                 uint32_t pn[U];
@@ -440,33 +444,44 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] &= (fmask & ~own[i]) | (pmask & own[i]);
                         }
-                        uint32_t fresh = 0;
+                        uint32_t fresh = 0, inv = 0;
 #pragma unroll
                         for (int i = 0; i < CW; ++i) {
                             const uint64_t cc = c[j][i];
                             n_send += cc != 0;
                             const uint64_t nb = cc & ~sa[i];  // not seen, not from a lower sender
                             sa[i] |= nb;
-                            fresh += __popcll(nb);
+                            if (DROP) {
+                                const uint64_t dv = nb & drp[i];
+                                n_rej += __popcll(dv & rej[i]);
+                                n_ign += __popcll(dv & ~rej[i]);
+                                inv += __popcll(dv & rej[i]);
+                                fresh += __popcll(nb & ~drp[i]);
+                            } else {
+                                fresh += __popcll(nb);
+                            }
                         }
                         n_new += fresh;
                         if (LPN > 1) fresh = group_sum<LPN>(fresh);
+                        if (DROP && LPN > 1) inv = group_sum<LPN>(inv);
                         if (lc == 0 && fresh) {
                             const int64_t q = qb + j;
                             ps.fcnt[q] = fc[j] + fresh;
                             ps.flast[q] = ((uint64_t)h << 32) | fresh;
                         }
+                        if (DROP && lc == 0 && inv && ps.credit) ps.invcnt[qb + j] += inv;  // P4
                     }
                 }
 #pragma unroll
                 for (int i = 0; i < CW; ++i) {
                     const uint64_t acc = sa[i] ^ seen[i];
-                    nxt[un + w0 + i] = acc;
+                    const uint64_t fwd_row = DROP ? acc & ~drp[i] : acc;
+                    nxt[un + w0 + i] = fwd_row;
                     if (acc) {
                         ps.seen[un + w0 + i] = sa[i];
                         ++n_vnew;
-                        any_new = true;
                     }
+                    if (fwd_row) any_new = true;
                 }
             }
         }
@@ -481,9 +496,9 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
         const uint32_t u0 = tile + (threadIdx.x / 64) * NW;
         if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
     }
-    unsigned long long cnt[3] = {n_new, n_send, n_vnew};
-    const uint32_t slot[3] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS};
-    block_count<3>(cnt, ps.stats, slot);
+    unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
+    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
+    block_count<5>(cnt, ps.stats, slot);
 }
 
 // The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
@@ -543,7 +558,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
     const bool want_inwin = ps.credit && !ps.all_dups_in_window;
     const uint32_t h_lo = h > ps.win_hops ? h - ps.win_hops : 0;
     const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;  // node of the tile, lane in the group
-    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0;
+    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0, n_rej = 0, n_ign = 0;
     for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
         const uint32_t u = tile + gi;
         bool any_new = false;
@@ -557,8 +572,15 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
             // origin chunk is re-read (cache-hot) rather than held
             const bool u_src = occ_bit(occ_src, u);
             for (uint32_t w0 = lc * CW; w0 < W; w0 += LPN * CW) {
-                uint64_t seen[CW], sa[CW], dm[CW];
+                uint64_t seen[CW], sa[CW], dm[CW], drp[CW], rej[CW];
                 load_words<CW>(seen, ps.seen + un + w0);
+                if (ps.drop) {  // messages validation does not accept (rare; both rows are per call)
+                    load_words<CW>(drp, ps.drop + w0);
+                    load_words<CW>(rej, ps.reject + w0);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < CW; ++i) drp[i] = rej[i] = 0;
+                }
 #pragma unroll
                 for (int i = 0; i < CW; ++i) {
                     sa[i] = seen[i];  // seen | this hop's receipts so far
@@ -657,14 +679,23 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                             for (int i = 0; i < CW; ++i) c[j][i] &= ~mine[i];
                         }
                         uint64_t nb[CW];
-                        uint32_t fresh = 0, pc = 0, kw = 0;
+                        uint32_t fresh = 0, pc = 0, kw = 0, inv = 0;
+                        bool rx = false;  // any first receipt, delivered or dropped
 #pragma unroll
                         for (int i = 0; i < CW; ++i) {
                             nb[i] = c[j][i] & ~sa[i];  // first receipts: not seen, not from a lower sender
                             sa[i] |= nb[i];
-                            fresh += __popcll(nb[i]);
-                            pc += __popcll(c[j][i]);
-                            if (want_inwin) kw += __popcll(c[j][i] & dm[i]);
+                            rx |= nb[i] != 0;
+                            // a message validation does not accept is seen but not delivered
+                            // (RejectMessage); it only ever arrives from its source, at hop 1
+                            const uint64_t dv = nb[i] & drp[i];
+                            n_rej += __popcll(dv & rej[i]);
+                            n_ign += __popcll(dv & ~rej[i]);
+                            inv += __popcll(dv & rej[i]);
+                            fresh += __popcll(nb[i] & ~drp[i]);
+                            const uint64_t cv = c[j][i] & ~drp[i];
+                            pc += __popcll(cv);
+                            if (want_inwin) kw += __popcll(cv & dm[i]);
                         }
                         n_new += fresh;
                         uint32_t k = 0;
@@ -672,7 +703,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                             n_dup += pc - fresh;
                             if (ps.credit) k = (want_inwin ? kw : pc) - fresh;
                         }
-                        if (fresh) {
+                        if (rx) {
                             if (TRACK) {  // first deliverers tracked: the pair's cumulative row
                                 uint64_t* fr = ps.from_mask + (size_t)q * W + w0;
                                 uint64_t o[CW];
@@ -689,8 +720,10 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                         if (LPN > 1) {  // converged: every lane of the group is here for pair q
                             k = group_sum<LPN>(k);
                             fresh = group_sum<LPN>(fresh);
+                            if (ps.drop) inv = group_sum<LPN>(inv);
                         }
                         if (lc == 0) {
+                            if (inv && ps.credit) ps.invcnt[q] += inv;  // markInvalidMessageDelivery, P4
                             if (k) ps.dupcnt[q] = dc[j] + k;
                             if (fresh) {  // first receipts from v: this call's count and the last hop's
                                 ps.fcnt[q] = fc[j] + fresh;
@@ -708,12 +741,12 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                 for (int i = 0; i < CW; ++i) {
                     const uint64_t acc = sa[i] ^ seen[i];
-                    nxt[un + w0 + i] = acc;  // this hop's row of the frontier history (touched nodes only)
+                    nxt[un + w0 + i] = acc & ~drp[i];  // this hop's frontier row (touched nodes only): forwarded
                     if (acc) {
                         ps.seen[un + w0 + i] = sa[i];
                         ++n_vnew;
-                        any_new = true;
                     }
+                    if (acc & ~drp[i]) any_new = true;
                 }
             }
         }
@@ -730,9 +763,10 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
         const uint32_t u0 = tile + (threadIdx.x / 64) * NW;  // the wave's first node
         if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
     }
-    unsigned long long cnt[5] = {n_new, n_dup, n_send, n_vnew, n_back};
-    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS};
-    block_count<5>(cnt, ps.stats, slot);
+    unsigned long long cnt[7] = {n_new, n_dup, n_send, n_vnew, n_back, n_rej, n_ign};
+    const uint32_t slot[7] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS,
+                              STAT_REJECTED, STAT_IGNORED};
+    block_count<7>(cnt, ps.stats, slot);
 }
 
 struct DupsLast {  // the last hop run and its frontier rows
@@ -777,6 +811,7 @@ __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_ru
             for (uint32_t w = w0; w < w0 + CWv; ++w) {
                 const size_t vw = (size_t)v * W + w;
                 uint64_t s = ps.seen[vw];
+                if (ps.drop) s &= ~ps.drop[w];  // never forwarded, not even by their source's peers
                 if (v_last) s &= ~L_.row[vw];
                 n_all += __popcll(s);
                 if (v_src) n_own += __popcll(s & ps.origin[vw]);
@@ -824,8 +859,9 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
                 s &= elig_word(fw, v_src ? ps.origin[vw] : 0);
                 if (ps.sel) s |= ps.sel[r * W + w];
                 if (ps.from_mask) s &= ~ps.from_mask[r * W + w];
+                if (ps.drop) s &= ~ps.drop[w];  // copies of dropped messages are receipts, not deliveries
                 if (u_src) {
-                    const uint64_t ou = ps.origin[(size_t)u * W + w];
+                    const uint64_t ou = ps.origin[(size_t)u * W + w] & (ps.drop ? ~ps.drop[w] : ~0ull);
                     s &= ~ou;
                     pub += __popcll(ou);
                 }
@@ -853,9 +889,13 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
 // mesh; markDuplicateMessageDelivery: mmd k2 more steps when in mesh
 // (score.go:912-974).  All steps are identical, so their order does not
 // matter; add_ones_capped gives the result of the steps one by one.
-__device__ __forceinline__ void fold_pair(const PropState& ps, const DevState& s, uint64_t q, uint32_t k1, uint32_t k2) {
+__device__ __forceinline__ void fold_pair(const PropState& ps, const DevState& s, uint64_t q, uint32_t k1, uint32_t k2,
+                                          uint32_t k4 = 0) {
     const DevTopicParams& tp = s.tp[ps.topic];
     const size_t b = rec_index(q, ps.topic, s.n_topics, FMD);
+    // markInvalidMessageDelivery (score.go:894-907): k4 steps of +1, no cap
+    if (k4) s.rec[b + IMD * TILE] = add_ones_capped(s.rec[b + IMD * TILE], k4, __builtin_inf());
+    if (k1 == 0 && k2 == 0) return;
     s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], k1, tp.cap2);
     if (!(s.rflags[flag_index(q, ps.topic, s.n_topics)] & REC_IN_MESH)) return;
     s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
@@ -886,7 +926,9 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
                     ps.firstcnt[q] = 0;
                     ps.dupcnt[q] = 0;
                 }
-                if ((first | dup) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup);
+                uint32_t k4 = 0;
+                if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
+                if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup, k4);
             } else {
                 ps.firstcnt[q] = first;
                 ps.dupcnt[q] = dup;
@@ -907,8 +949,9 @@ __global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, con
     if (!s.tp[ps.topic].scored) return;
     const uint32_t k1 = first[q];
     const uint32_t k2 = dup[q];
-    if (k1 == 0 && k2 == 0) return;
-    fold_pair(ps, s, q, k1, k2);
+    const uint32_t k4 = ps.invcnt ? ps.invcnt[q] : 0;
+    if (k1 == 0 && k2 == 0 && k4 == 0) return;
+    fold_pair(ps, s, q, k1, k2, k4);
 }
 
 // First deliverer per (message, node) from the per-pair "first got it from" rows.
@@ -948,10 +991,39 @@ __global__ __launch_bounds__(256) void k_prop_hops_export(PropState ps, uint8_t*
             hk[b] = (uint8_t)h;
         }
     }
+    if (ps.drop && ps.drop[w]) {  // not forwarded, so not in the frontier rows: received at hop 1
+        uint64_t x = ps.dseen[(size_t)u * W + w];
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            hk[b] = 1;
+        }
+    }
     for (int b = 0; b < 64; ++b) {
         const uint32_t k = w * 64 + b;
         if (k < ps.n_msgs) out[(size_t)k * ps.n_nodes + u] = hk[b];
     }
+}
+
+// After a call with dropped messages: keep their hop-1 receipts for
+// gsx_prop_results, and (gossipsub) take them out of the seen rows the
+// message cache keeps, since Publish Puts only what a node processed
+// (gossipsub.go:944): a dropped message stays in its source's row only.
+__global__ __launch_bounds__(256) void k_prop_uncache(PropState ps, bool mask_cache) {
+    const uint32_t W = ps.n_words;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < (uint64_t)ps.n_nodes * W; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t w = (uint32_t)(i % W);
+        const uint64_t d = ps.drop[w];
+        const uint64_t rx = d & ps.seen[i] & ~ps.origin[i];
+        ps.dseen[i] = rx;
+        if (mask_cache && rx) ps.seen[i] &= ~rx;
+    }
+}
+hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st) {
+    if (!ps.drop || ps.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_uncache, dim3(std::min((unsigned)(((uint64_t)ps.n_nodes * ps.n_words + 255) / 256), COUNTER_GRID)),
+                       dim3(256), 0, st, ps, mask_cache);
+    return hipGetLastError();
 }
 
 // ---- launchers ----------------------------------------------------------------
@@ -1013,8 +1085,10 @@ template <int CW, int LPN>
 static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
     static const bool no_fast = getenv("GSX_HOP_GENERAL") != nullptr;  // tuning / cross-checks
-    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast)
-        hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN>), g, b, 0, st, ps, h, front, nxt);
+    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast) {
+        if (ps.drop) hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
+        else hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
+    }
     else if (ps.from_mask) hipLaunchKernelGGL((k_prop_hop<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
     else hipLaunchKernelGGL((k_prop_hop<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
 }

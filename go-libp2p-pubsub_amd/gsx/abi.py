@@ -208,6 +208,9 @@ GSX_CREDIT_DEFER = 2
 GSX_ANY_TOPIC = 0xFFFFFFFF
 
 
+GSX_VALIDATION_ACCEPT, GSX_VALIDATION_REJECT, GSX_VALIDATION_IGNORE, GSX_VALIDATION_THROTTLE = 0, 1, 2, 3
+
+
 class PropConfig(C.Structure):
     _fields_ = [
         ("router", C.c_uint32),
@@ -219,6 +222,7 @@ class PropConfig(C.Structure):
         ("credit_scores", C.c_uint32),
         ("randomsub_size", C.c_uint32),
         ("seed", C.c_uint64),
+        ("validation_delay_ns", C.c_int64),
     ]
 
 
@@ -233,15 +237,18 @@ class PropOut(C.Structure):
         ("edge_sends", C.c_uint64),
         ("new_words", C.c_uint64),
         ("hop_kernel_ms", C.c_double),
+        ("rejected", C.c_uint64),
+        ("ignored", C.c_uint64),
     ]
 
     def as_dict(self):
         return dict(deliveries=self.deliveries, duplicates=self.duplicates, transmissions=self.transmissions,
-                    hops=self.hops, hop_deliveries=list(self.hop_deliveries)[: self.hops + 1])
+                    hops=self.hops, hop_deliveries=list(self.hop_deliveries)[: self.hops + 1],
+                    rejected=self.rejected, ignored=self.ignored)
 
 
 class Msg(C.Structure):
-    _fields_ = [("source", C.c_uint32), ("reserved", C.c_uint32), ("msg_id", C.c_uint64)]
+    _fields_ = [("source", C.c_uint32), ("validation", C.c_uint32), ("msg_id", C.c_uint64)]
 
 
 _MSG_DTYPE = None
@@ -252,7 +259,7 @@ def msg_dtype():
     if _MSG_DTYPE is None:
         import numpy as np
 
-        _MSG_DTYPE = np.dtype([("source", "<u4"), ("reserved", "<u4"), ("msg_id", "<u8")], align=True)
+        _MSG_DTYPE = np.dtype([("source", "<u4"), ("validation", "<u4"), ("msg_id", "<u8")], align=True)
         assert _MSG_DTYPE.itemsize == C.sizeof(Msg)
     return _MSG_DTYPE
 
@@ -338,6 +345,8 @@ SIGNATURES = {
     "gsx_propagate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), P(PropOut)]),
     "gsx_prop_results": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_int32)]),
     "gsx_prop_set_tracking": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_prop_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_replace_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_pending_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "gsx_prop_fold_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "gsx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -288,6 +288,14 @@ class Engine:
         self._chk(self.lib.gsx_prop_pending_credits(self.h, C.c_void_p(first_ptr or None), C.c_void_p(dup_ptr or None)),
                   "gsx_prop_pending_credits")
 
+    def pending_invalid(self, inv_ptr: int):
+        """Copy the pending invalid-delivery counts (P4 of REJECT messages) to caller memory."""
+        self._chk(self.lib.gsx_prop_pending_invalid(self.h, C.c_void_p(inv_ptr or None)), "gsx_prop_pending_invalid")
+
+    def replace_pending_invalid(self, inv_ptr: int):
+        self._chk(self.lib.gsx_prop_replace_pending_invalid(self.h, C.c_void_p(inv_ptr or None)),
+                  "gsx_prop_replace_pending_invalid")
+
     def fold_credits(self, first_ptr: int = 0, dup_ptr: int = 0):
         self._chk(self.lib.gsx_prop_fold_credits(self.h, C.c_void_p(first_ptr or None), C.c_void_p(dup_ptr or None)),
                   "gsx_prop_fold_credits")

@@ -29,7 +29,7 @@ import numpy as np
 
 from . import abi
 
-_STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words")
+_STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words", "rejected", "ignored")
 
 
 def prop_words(m: int) -> int:
@@ -244,13 +244,16 @@ class MessageParallel:
         out = self.e.propagate(mine, c)[0]
         if credit:
             E = self.e.n_pairs
-            cnt = torch.empty((2, max(E, 1)), dtype=torch.int32, device=self.tp.device)
+            # first receipts, in-window duplicates and invalid deliveries (P4)
+            cnt = torch.empty((3, max(E, 1)), dtype=torch.int32, device=self.tp.device)
             if cnt.is_cuda:
                 torch.cuda.synchronize(cnt.device)
             self.e.pending_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
+            self.e.pending_invalid(cnt[2].data_ptr())
             self.tp.all_reduce_sum(cnt)
             if cnt.is_cuda:
                 torch.cuda.synchronize(cnt.device)
+            self.e.replace_pending_invalid(cnt[2].data_ptr())
             self.e.fold_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
         return out_dict(out), totals(out, self.tp)
 

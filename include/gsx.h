@@ -339,9 +339,13 @@ int gsx_last_refresh_ms(gsx_engine* e, float* ms);
  *   - "in topic" (ps.topics[topic]) = the pair is present and connected;
  *     mesh membership = the scorer's inMesh flag of (pair, topic), which the
  *     router keeps in step through Graft/Prune traces;
- *   - validation is instantaneous: a duplicate arriving (hop - first hop) *
- *     hop_latency_ns after the first receipt is inside the P3 window iff
- *     that is <= MeshMessageDeliveriesWindow (score.go:965).
+ *   - a receiver validates for validation_delay_ns before it delivers and
+ *     forwards; a duplicate is inside the P3 window iff it arrives at most
+ *     MeshMessageDeliveriesWindow after the first copy finished validating
+ *     (score.go:965); a message validation does not accept (gsx_msg.validation)
+ *     is seen but neither delivered nor forwarded;
+ *   - score gates (publishThreshold, flood publish) read the scores as they
+ *     stand when the call starts; the call's credits land at its end.
  * With credit_scores set, first receipts and duplicates are folded into the
  * receiver's counters exactly as DeliverMessage / DuplicateMessage would
  * (score.go:695-719, 788-820: +1 then cap, one step per message). */
@@ -357,20 +361,35 @@ typedef struct gsx_prop_config {
     uint32_t credit_scores;   /* GSX_CREDIT_*: fold deliveries into P2/P3 counters */
     uint32_t randomsub_size;  /* RandomSub's `size` (randomsub.go:21-27)           */
     uint64_t seed;            /* RandomSub draws: h(seed, 7, vertex, msg_id<<16|k) */
+    int64_t validation_delay_ns; /* time a receiver validates before forwarding / delivering
+                                  * (validation.go:230-351); >= 0.  A hop takes
+                                  * hop_latency_ns + validation_delay_ns, and a duplicate is inside
+                                  * the P3 window iff it arrives <= window after the first copy
+                                  * finished validating (score.go:806-809, 965). */
 } gsx_prop_config;
 
 #define GSX_MAX_HOPS 64
 
+/* Validation outcome of a message at every receiver (validation.go:230-351,
+ * score.go:721-786).  A message that is not accepted is marked seen but not
+ * delivered, not forwarded and not cached (it travels one hop, from its
+ * source); REJECT (ValidationFailed) adds one invalid delivery (P4) to the
+ * sender's record, IGNORE and THROTTLE penalise nobody. */
+#define GSX_VALIDATION_ACCEPT 0u
+#define GSX_VALIDATION_REJECT 1u
+#define GSX_VALIDATION_IGNORE 2u
+#define GSX_VALIDATION_THROTTLE 3u
+
 typedef struct gsx_msg {
-    uint32_t source;  /* publishing node (the origin)  */
-    uint32_t reserved;
-    uint64_t msg_id;  /* used by RandomSub's draws     */
+    uint32_t source;      /* publishing node (the origin)  */
+    uint32_t validation;  /* GSX_VALIDATION_*              */
+    uint64_t msg_id;      /* used by RandomSub's draws     */
 } gsx_msg;
 
 typedef struct gsx_prop_out {
     uint64_t deliveries;     /* first receipts by vertices other than the source */
     uint64_t duplicates;     /* receipts of an already seen message             */
-    uint64_t transmissions;  /* sends: deliveries + duplicates                  */
+    uint64_t transmissions;  /* sends: deliveries + duplicates + rejected + ignored */
     uint32_t hops;           /* last hop with a first receipt                   */
     uint32_t hop_launches;   /* hop (and pack) launches timed in hop_kernel_ms  */
     uint64_t hop_deliveries[GSX_MAX_HOPS + 1]; /* first receipts per hop       */
@@ -380,6 +399,8 @@ typedef struct gsx_prop_out {
     uint64_t edge_sends;
     uint64_t new_words;
     double hop_kernel_ms;    /* device time of the hop / pack kernels (HIP events) */
+    uint64_t rejected;       /* receipts of REJECT messages (RejectMessage, P4 to the sender) */
+    uint64_t ignored;        /* receipts of IGNORE / THROTTLE messages                      */
 } gsx_prop_out;
 
 /* credit_scores values */
@@ -410,6 +431,11 @@ int gsx_prop_set_tracking(gsx_engine* e, uint32_t first_deliverers);
  * counts is exactly folding every message's steps (they are all "+1 then
  * cap"). */
 int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup);
+/* Pending invalid-delivery counts per pair (REJECT messages, P4), n_pairs
+ * u32, host or device memory: read, or replace (message-parallel replicas sum
+ * them like the credits).  gsx_prop_fold_credits folds them into imd. */
+int gsx_prop_pending_invalid(gsx_engine* e, uint32_t* inv);
+int gsx_prop_replace_pending_invalid(gsx_engine* e, const uint32_t* inv);
 /* Folds credit counts into fmd / mmd of the pending topic (score.go:912-974)
  * and clears them.  first/dup (both or neither, host or device memory)
  * replace the pending counts before folding. */

@@ -975,7 +975,7 @@ static void shuffle_pairs(uint64_t* a, int n, orc_rng* g) {
  * msg.ReceivedFrom = from (-1 when v published it) and GetFrom() = origin.
  * Returns the count; `out` has room for deg(v). */
 static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v, uint32_t origin, int64_t from,
-                          uint64_t msg_id, uint64_t* out, uint64_t* scratch) {
+                          uint64_t msg_id, uint64_t* out, uint64_t* scratch, const double* score0) {
     int n = 0;
     const int64_t r0 = o->row_ptr[v], r1 = o->row_ptr[v + 1];
     if (cfg->router == GSX_ROUTER_FLOODSUB) { /* floodsub.go:81-90 */
@@ -1017,11 +1017,11 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
         const bool direct = (ef & GSX_EDGE_DIRECT) != 0;
         bool send;
         if (cfg->flood_publish && from < 0) { /* :953-960 */
-            send = direct || score_pair(o, (uint64_t)r) >= thr;
+            send = direct || score0[r] >= thr;
         } else {
             const bool mesh_peer = (ef & GSX_EDGE_GOSSIPSUB) != 0; /* gs.feature(GossipSubFeatureMesh, ...) */
             send = direct;                                          /* :962-968 */
-            if (!send && !mesh_peer) send = score_pair(o, (uint64_t)r) >= thr; /* :970-975 */
+            if (!send && !mesh_peer) send = score0[r] >= thr; /* :970-975 */
             if (!send && topic < o->T) send = o->ts[(uint64_t)r * o->T + topic].in_mesh; /* gs.mesh[topic], :977-999 */
         }
         if (!send) continue;
@@ -1045,9 +1045,18 @@ static int arrival_cmp(const void* a, const void* b) {
     return 0;
 }
 
+/* Time of a copy arriving at hop h (h >= 1): every hop is hop_latency_ns of
+ * transit, and a receiver forwards only after validating for
+ * validation_delay_ns (validation.go:230-351). */
+static int64_t arrival_time(const gsx_prop_config* cfg, uint32_t h) {
+    return cfg->now_ns + (int64_t)h * cfg->hop_latency_ns + (h ? (int64_t)(h - 1) * cfg->validation_delay_ns : 0);
+}
+
 int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
                   uint8_t* hop_out, int32_t* from_out) {
-    if (cfg->max_hops > GSX_MAX_HOPS) return GSX_EINVAL;
+    if (cfg->max_hops > GSX_MAX_HOPS || cfg->validation_delay_ns < 0) return GSX_EINVAL;
+    for (size_t k = 0; k < m; k++)
+        if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return GSX_EINVAL;
     memset(out, 0, sizeof(*out));
     const uint32_t N = o->n_nodes;
     uint8_t* hop = (uint8_t*)malloc(N ? N : 1);
@@ -1062,6 +1071,11 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     size_t cap_arr = 1024, n_arr = 0;
     orc_arrival* arr = (orc_arrival*)malloc(sizeof(orc_arrival) * cap_arr);
     const bool credit = cfg->credit_scores && cfg->topic < o->T && o->scored[cfg->topic];
+    /* The synchronous contract (gsx.h): the publishThreshold tests of one
+     * call read the scores as they stand when it starts; the call's own
+     * credits (P2/P3, and P4 of rejected messages) land at its end. */
+    double* score0 = (double*)malloc(sizeof(double) * (o->E ? o->E : 1));
+    for (uint64_t r = 0; r < o->E; r++) score0[r] = score_pair(o, r);
     /* gossipsub's Publish Puts every message a node processes into its
      * mcache (gossipsub.go:944); one batch entry in window 0 */
     orc_mc_batch* mcb = NULL;
@@ -1082,6 +1096,10 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     for (size_t k = 0; k < m; k++) {
         const uint32_t src = msgs[k].source;
         if (src >= N) return GSX_ERANGE;
+        /* not accepted: seen, but neither delivered nor forwarded (pushMsg ->
+         * validation -> RejectMessage, pubsub.go:1046-1090, score.go:721-786) */
+        const uint32_t val = msgs[k].validation;
+        const bool dropped = val != GSX_VALIDATION_ACCEPT;
         memset(hop, 0xFF, N);
         for (uint32_t i = 0; i < N; i++) from[i] = -1;
         hop[src] = 0; /* the local publish */
@@ -1091,7 +1109,7 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
             n_arr = 0;
             for (uint32_t i = 0; i < nf; i++) {
                 const uint32_t v = frontier[i];
-                int nt = router_targets(o, cfg, v, src, from[v], msgs[k].msg_id, tg, scratch);
+                int nt = router_targets(o, cfg, v, src, from[v], msgs[k].msg_id, tg, scratch, score0);
                 for (int j = 0; j < nt; j++) {
                     if (n_arr == cap_arr) {
                         cap_arr *= 2;
@@ -1110,18 +1128,28 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
                 const uint32_t u = arr[a].u, v = arr[a].v;
                 out->transmissions++;
                 const int64_t q = credit ? reverse_pair(o, arr[a].r) : -1; /* u's peerStats for v */
-                if (hop[u] == 0xFF) { /* first receipt: markSeen + DeliverMessage */
+                if (hop[u] == 0xFF) { /* first receipt: markSeen, then validation */
                     hop[u] = (uint8_t)h;
                     from[u] = (int32_t)v;
-                    next[nn++] = u;
-                    out->deliveries++;
-                    out->hop_deliveries[h]++;
-                    if (q >= 0) mark_first(o, (uint64_t)q, cfg->topic);
-                } else { /* seenMessage -> DuplicateMessage, validated at the first receipt */
+                    if (!dropped) { /* DeliverMessage, then Publish forwards it */
+                        next[nn++] = u;
+                        out->deliveries++;
+                        out->hop_deliveries[h]++;
+                        if (q >= 0) mark_first(o, (uint64_t)q, cfg->topic);
+                    } else if (val == GSX_VALIDATION_REJECT) { /* RejectMessage(ValidationFailed) */
+                        out->rejected++;
+                        if (q >= 0) mark_invalid(o, (uint64_t)q, cfg->topic);
+                    } else { /* RejectMessage(ValidationIgnored / Throttled): no penalty */
+                        out->ignored++;
+                    }
+                } else { /* seenMessage -> DuplicateMessage, validated when the first copy's validation ended */
                     out->duplicates++;
-                    if (q >= 0)
-                        mark_duplicate(o, (uint64_t)q, cfg->topic, true, cfg->now_ns + (int64_t)hop[u] * cfg->hop_latency_ns,
-                                       cfg->now_ns + (int64_t)h * cfg->hop_latency_ns);
+                    if (q >= 0 && !dropped)
+                        mark_duplicate(o, (uint64_t)q, cfg->topic, true,
+                                       arrival_time(cfg, hop[u]) + (hop[u] ? cfg->validation_delay_ns : 0),
+                                       arrival_time(cfg, h));
+                    else if (q >= 0 && val == GSX_VALIDATION_REJECT)
+                        mark_invalid(o, (uint64_t)q, cfg->topic); /* deliveryInvalid, score.go:811-813 */
                 }
             }
             if (nn > 0 && h > out->hops) out->hops = h;
@@ -1130,8 +1158,8 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         }
         if (hop_out) memcpy(hop_out + k * (size_t)N, hop, N);
         if (from_out) memcpy(from_out + k * (size_t)N, from, sizeof(int32_t) * N);
-        if (mcb)
-            for (uint32_t i = 0; i < N; i++) mcb->has[k * (size_t)N + i] = hop[i] != 0xFF;
+        if (mcb) /* Publish Puts what a node processes: a dropped message only at its source */
+            for (uint32_t i = 0; i < N; i++) mcb->has[k * (size_t)N + i] = hop[i] != 0xFF && (!dropped || i == src);
     }
     free(hop);
     free(from);
@@ -1140,6 +1168,7 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     free(tg);
     free(scratch);
     free(arr);
+    free(score0);
     return 0;
 }
 

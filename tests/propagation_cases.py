@@ -74,14 +74,21 @@ def setup(be, ov, T, seed, mesh_degree=6, disconnect_frac=0.0, score_spread=True
     return app
 
 
-def messages(n_nodes, m, seed):
+def messages(n_nodes, m, seed, invalid=0.0):
+    """`invalid`: fraction of messages validation does not accept (REJECT,
+    IGNORE, THROTTLE in 3:1:1), drawn from the seed."""
     ms = np.zeros(m, dtype=abi.msg_dtype())
     ms["source"] = (synth.h(seed, synth.TAG_SRC, np.arange(m), 0) % np.uint64(n_nodes)).astype(np.uint32)
     ms["msg_id"] = np.arange(m, dtype=np.uint64) + 1000 * seed
+    if invalid > 0:
+        rng = np.random.default_rng(seed + 77)
+        bad = rng.random(m) < invalid
+        kind = rng.choice([abi.GSX_VALIDATION_REJECT] * 3 + [abi.GSX_VALIDATION_IGNORE, abi.GSX_VALIDATION_THROTTLE], m)
+        ms["validation"] = np.where(bad, kind, abi.GSX_VALIDATION_ACCEPT).astype(np.uint32)
     return ms
 
 
-def config(router, topic=0, flood_publish=0, max_hops=40, latency_ms=10, credit=1, size=0, seed=5):
+def config(router, topic=0, flood_publish=0, max_hops=40, latency_ms=10, credit=1, size=0, seed=5, delay_ms=0.0):
     return abi.PropConfig(router=router, topic=topic, flood_publish=flood_publish, max_hops=max_hops,
                           hop_latency_ns=latency_ms * abi.MILLISECOND, now_ns=T0 + 3 * S, credit_scores=credit,
-                          randomsub_size=size, seed=seed)
+                          randomsub_size=size, seed=seed, validation_delay_ns=int(delay_ms * abi.MILLISECOND))

@@ -88,3 +88,44 @@ def test_propagation_full_size_properties(gpu_ok):
     for k in range(4):
         reach = np.isfinite(dist[k])
         assert np.array_equal(hop[k][reach].astype(np.int64), dist[k][reach].astype(np.int64))
+
+
+VCASES = [
+    # n, d, T, router, flood_publish, m, latency_ms, delay_ms, invalid, mix
+    (700, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, 5, 7.0, 0.25, True),
+    (600, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 1024, 10, 3.0, 0.2, True),
+    (500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 130, 4, 12.0, 0.3, False),
+    (800, 5, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 100, 6, 2.0, 0.2, True),
+]
+
+
+@pytest.mark.parametrize("track", [True, False, "late"], ids=["rows", "counts", "counts-late"])
+@pytest.mark.parametrize("case", VCASES, ids=[f"r{c[3]}-n{c[0]}-m{c[5]}-v{c[7]}" for c in VCASES])
+def test_propagation_validation_matches_oracle(gpu_ok, case, track):
+    """Validation outcomes (REJECT / IGNORE / THROTTLE: seen, not delivered,
+    not forwarded; REJECT adds P4 to the sender) and a validation delay that
+    stretches every hop and the P3 window (validation.go:230-351,
+    score.go:721-820): counters, hops, first deliverers, P2/P3/P4, scores."""
+    n, d, T, router, fp, m, lat, delay, invalid, mix = case
+    seed = 3 * n + m
+    if track == "late":
+        track, lat = False, 0
+    ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.02)
+    ms = pc.messages(n, m, seed, invalid=invalid)
+    cfg = pc.config(router, topic=T - 1, flood_publish=fp, latency_ms=lat, size=50, delay_ms=delay)
+    res = []
+    eng = gsx.Engine(T)
+    eng.set_prop_tracking(track)
+    for be in (eng, orc.Oracle(T)):
+        pc.setup(be, ov, T, seed, disconnect_frac=0.02)
+        out, hop, frm = be.propagate(ms, cfg, want_results=True)
+        res.append((out.as_dict(), hop, frm, be.export_state(), be.scores()))
+    (go, gh, gf, gs, gsc), (wo, wh, wf, ws, wsc) = res
+    assert go == wo
+    assert go["rejected"] > 0 and go["ignored"] > 0
+    assert np.array_equal(gh, wh), np.argwhere(gh != wh)[:5]
+    if track:
+        assert np.array_equal(gf, wf), np.argwhere(gf != wf)[:5]
+    for f in abi.STATE_FIELDS:
+        assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
+    assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))

@@ -47,6 +47,10 @@ CASES = [
     (2, 2000, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, True, 0.03, "compact-counts"),
     (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 1024, True, 0.02, "dense-counts"),
     (2, 1500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 300, False, 0.02, "compact-counts"),
+    # validation outcomes (dropped / rejected messages) and a validation delay
+    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 300, True, 0.02, "compact-invalid"),
+    (2, 1500, 5, 2, abi.GSX_ROUTER_GOSSIPSUB, 1, 200, True, 0.02, "dense-counts-invalid"),
+    (2, 1600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 100, True, 0.02, "compact-invalid"),
 ]
 
 
@@ -55,13 +59,16 @@ CASES = [
                               for c in CASES])
 def test_range_sharded_matches_single_engine(gpu_ok, case):
     world, n, d, T, router, fp, m, mix, disc, compact = case
-    track = True
-    if isinstance(compact, str):  # "<exchange>-counts": shards keep no first-deliverer rows
-        compact, track = compact.startswith("compact"), False
+    track, invalid, delay = True, 0.0, 0.0
+    if isinstance(compact, str):  # "<exchange>[-counts][-invalid]"
+        track = "counts" not in compact
+        if "invalid" in compact:  # messages validation drops, and a validation delay
+            invalid, delay = 0.25, 3.0
+        compact = compact.startswith("compact")
     seed = 3 * n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
-    msgs = pc.messages(n, m, seed)
-    cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60)
+    msgs = pc.messages(n, m, seed, invalid=invalid)
+    cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60, delay_ms=delay)
     full = gsx.Engine(T)
     app = pc.setup(full, ov, T, seed, disconnect_frac=disc)
     st0 = full.export_state()
@@ -90,7 +97,7 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
     res = shard.run_local(world, "cuda:0", run, [(e,) for e, _, _ in engines])
     tot = res[0][1]
     want = out.as_dict()
-    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries"):
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored"):
         assert tot[k] == want[k], k
     assert tot["edge_sends"] == out.edge_sends and tot["new_words"] == out.new_words
     for k, (e, a, b) in enumerate(engines):
@@ -107,12 +114,12 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
     assert want["deliveries"] > 0
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_message_parallel_matches_single_engine(gpu_ok, world):
+@pytest.mark.parametrize("world,invalid", [(2, 0.0), (3, 0.0), (3, 0.2)])
+def test_message_parallel_matches_single_engine(gpu_ok, world, invalid):
     n, d, T, m = 3000, 6, 1, 300
     seed = 17 + world
     ov = pc.overlay(n, d, seed, mix_protocols=True, direct_frac=0.02)
-    msgs = pc.messages(n, m, seed)
+    msgs = pc.messages(n, m, seed, invalid=invalid)
     cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=4)
     full = gsx.Engine(T)
     pc.setup(full, ov, T, seed, disconnect_frac=0.02)
@@ -130,7 +137,7 @@ def test_message_parallel_matches_single_engine(gpu_ok, world):
     res = shard.run_local(world, "cuda:0", run, [(e,) for e in reps])
     tot = res[0][1]
     want = out.as_dict()
-    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries"):
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored"):
         assert tot[k] == want[k], k
     for e in reps:
         st = e.export_state()

@@ -93,3 +93,32 @@ def test_credits_follow_deliveries():
     dfmd = after["first_message_deliveries"] - before["first_message_deliveries"]
     assert dfmd.sum() > 0 and dfmd.min() >= 0
     assert abs(dfmd.sum() - out.deliveries) < 1e-6 * out.deliveries + 1  # fmd caps are far away here
+
+
+def test_dropped_messages_travel_one_hop_and_penalise_rejects():
+    """score.go:721-786 / pubsub.go:1046-1090 restated: a message validation
+    does not accept reaches only its source's neighbours (hop 1), is counted
+    as rejected / ignored there, never delivered or forwarded; every REJECT
+    receipt adds one invalid delivery to the receiver's record of the source."""
+    ov = pc.overlay(300, 4, seed=11)
+    o = orc.Oracle(1)
+    pc.setup(o, ov, 1, seed=11, score_spread=False)
+    ms = pc.messages(ov.n, 60, seed=11, invalid=0.4)
+    imd0 = o.export_state()["invalid_message_deliveries"].copy()
+    out, hop, frm = o.propagate(ms, pc.config(abi.GSX_ROUTER_FLOODSUB, latency_ms=2), want_results=True)
+    dropped = ms["validation"] != abi.GSX_VALIDATION_ACCEPT
+    assert dropped.any() and (~dropped).any()
+    assert set(np.unique(hop[dropped])) <= {0, 1, 0xFF}
+    rej = int((hop[ms["validation"] == abi.GSX_VALIDATION_REJECT] == 1).sum())
+    ign = int((hop[dropped & (ms["validation"] != abi.GSX_VALIDATION_REJECT)] == 1).sum())
+    assert (out.rejected, out.ignored) == (rej, ign)
+    assert out.deliveries == int((hop[~dropped] != 0xFF).sum()) - int((~dropped).sum())
+    assert out.transmissions == out.deliveries + out.duplicates + out.rejected + out.ignored
+    # floodsub sends to every neighbour: each source's rejects reach all its neighbours
+    for k in np.nonzero(ms["validation"] == abi.GSX_VALIDATION_REJECT)[0]:
+        src = int(ms["source"][k])
+        nb = ov.col[ov.row_ptr[src]: ov.row_ptr[src + 1]]
+        assert np.array_equal(np.sort(np.nonzero(hop[k] == 1)[0]), np.sort(nb))
+        assert np.all(frm[k][nb] == src)
+    imd1 = o.export_state()["invalid_message_deliveries"]
+    assert float(imd1.sum() - imd0.sum()) == float(out.rejected)
