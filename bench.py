@@ -335,6 +335,44 @@ def adversarial_leg(args, rank, world, local, dist, dev):
         "sybil_pairs_below_graylist_rank0": int(below),
         "honest_pairs_below_graylist_rank0": int(np.count_nonzero(sc[~syb] < th.graylist_threshold)),
     }
+    if args.prop_msgs > 0:
+        # invalid-message spam through the router: three quarters
+        # of a batch published by sybils and rejected by validation (seen, not
+        # forwarded, P4 to the sybil at every receiver), the rest honest
+        M = args.prop_msgs
+        k = np.arange(M)
+        hsh = synth.h(synth.SEED + 3, synth.TAG_SRC, k, 0)
+        spam = (hsh % np.uint64(4)) != 0
+        n_hon = n - n_syb
+        ms = np.zeros(M, dtype=abi.msg_dtype())
+        ms["source"] = np.where(spam, n_hon + (hsh >> np.uint64(8)) % np.uint64(n_syb),
+                                (hsh >> np.uint64(8)) % np.uint64(n_hon)).astype(np.uint32)
+        ms["msg_id"] = (k + (1 << 40)).astype(np.uint64)
+        ms["validation"] = np.where(spam, abi.GSX_VALIDATION_REJECT, abi.GSX_VALIDATION_ACCEPT).astype(np.uint32)
+        cfg = prop_config(args, n)
+        cfg.now_ns = now + abi.SECOND // 2
+        e.set_prop_tracking(False)
+        sp_runner = None
+        if dist is not None:
+            sp_runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if sp_runner is None:
+            d = shard_mod.out_dict(e.propagate(ms, cfg)[0])
+        else:
+            d = sp_runner.propagate(ms, cfg)[1]
+        e.sync()
+        torch.cuda.synchronize(dev)
+        out["spam"] = {
+            "messages": M, "rejected_by_validation": int(spam.sum()),
+            "ms_per_batch": reduce_scalar(time.perf_counter() - t0, dist, dev, "max") * 1e3,
+            "deliveries": d["deliveries"], "rejected_receipts_p4": d["rejected"], "duplicates": d["duplicates"],
+        }
+        now += abi.SECOND
+        e.refresh(now)
+        sc = e.scores()
+        out["spam"]["sybil_pairs_below_graylist_after_rank0"] = int(np.count_nonzero(sc[syb] < th.graylist_threshold))
     if args.hb_steps > 0:
         # heartbeats over the shards: GRAFT/PRUNE words of cross-shard pairs
         # go to their receivers' ranks and the answers come back (gsx_hb_*)
