@@ -1434,6 +1434,8 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     }
     if (cfg->validation_delay_ns < 0) return fail(e, GSX_EINVAL, "negative validation delay");
     if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^29 nodes per engine");
+    if (cfg->router == GSX_ROUTER_RANDOMSUB && e->max_deg > (int64_t)gsx::RSUB_MAX_DEG)
+        return fail(e, GSX_ERANGE, "RandomSub draws support at most " + std::to_string(gsx::RSUB_MAX_DEG) + " peers per node");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)

@@ -340,6 +340,19 @@ __device__ __forceinline__ void load_words(uint64_t (&d)[CW], const uint64_t* p)
 // Sum over the LPN lanes of a group (aligned), every lane gets the sum.
 // Groups of 2 and 4 use DPP quad permutes (a VALU operand modifier, no LDS
 // crossbar); wider groups fall back to ds_bpermute shuffles.
+// flast of pair q after `fresh` more first receipts at hop h: hop << 32 |
+// count.  When a lane walks the pairs once per chunk of its row (rows longer
+// than LPN * CW words), the chunks of one hop add up.
+__device__ __forceinline__ uint64_t last_count(const PropState& ps, uint64_t q, uint32_t h, uint32_t fresh,
+                                               bool chunks) {
+    uint32_t base = 0;
+    if (chunks) {
+        const uint64_t fl = ps.flast[q];
+        if ((uint32_t)(fl >> 32) == h) base = (uint32_t)fl;
+    }
+    return ((uint64_t)h << 32) | (base + fresh);
+}
+
 template <int LPN>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
     if (LPN == 2 || LPN == 4) {
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                         if (lc == 0 && fresh) {
                             const int64_t q = qb + j;
                             ps.fcnt[q] = fc[j] + fresh;
-                            ps.flast[q] = ((uint64_t)h << 32) | fresh;
+                            ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
                         }
                         if (DROP && lc == 0 && inv && ps.credit) ps.invcnt[qb + j] += inv;  // P4
                     }
@@ -727,7 +740,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                             if (k) ps.dupcnt[q] = dc[j] + k;
                             if (fresh) {  // first receipts from v: this call's count and the last hop's
                                 ps.fcnt[q] = fc[j] + fresh;
-                                ps.flast[q] = ((uint64_t)h << 32) | fresh;
+                                ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
                                 if (backsend && !halo && (fq[j] & FWD_FORWARD)) {
                                     // u forwards them to v at hop h + 1 and v counts duplicates:
                                     // the `from` exclusion's whole effect, taken back here

@@ -129,3 +129,83 @@ def test_propagation_validation_matches_oracle(gpu_ok, case, track):
     for f in abi.STATE_FIELDS:
         assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
     assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))
+
+
+def _overlay_from_edges(n, edges):
+    """Symmetric overlay from undirected edges (u, v); the lower id dials."""
+    rows = [[] for _ in range(n)]
+    for u, v in edges:
+        rows[u].append(v)
+        rows[v].append(u)
+    row_ptr = np.zeros(n + 1, dtype=np.int64)
+    col, ef = [], []
+    for i in range(n):
+        nb = sorted(set(rows[i]))
+        row_ptr[i + 1] = row_ptr[i] + len(nb)
+        col += nb
+        ef += [abi.GSX_EDGE_GOSSIPSUB | (abi.GSX_EDGE_OUTBOUND if i < j else 0) for j in nb]
+    ips = np.stack([np.arange(n, dtype=np.uint32) + 1, np.full(n, 0xFFFFFFFF, dtype=np.uint32)], axis=1)
+    return synth.Overlay(n=n, row_ptr=row_ptr, col=np.array(col, dtype=np.int32), edge_flags=np.array(ef, dtype=np.uint8),
+                         node_ips=ips, sybil=np.zeros(n, dtype=bool))
+
+
+def _hub_overlay(n, seed):
+    """Node 0 peers with everyone (degree n - 1 > 256), the rest form a ring
+    with random chords, plus a few isolated nodes at the end."""
+    rng = np.random.default_rng(seed)
+    core = n - 5
+    edges = [(0, i) for i in range(1, core)]
+    edges += [(i, i + 1) for i in range(1, core - 1)]
+    edges += [tuple(sorted(rng.choice(np.arange(1, core), 2, replace=False))) for _ in range(core)]
+    return _overlay_from_edges(n, [e for e in edges if e[0] != e[1]])
+
+
+EDGE_CASES = [
+    # router, m, max_hops, latency_ms, track
+    (abi.GSX_ROUTER_GOSSIPSUB, 300, 40, 10, True),
+    (abi.GSX_ROUTER_FLOODSUB, 1100, 40, 0, False),   # late accounting, 18 words (LPN 1, 4-word chunks + pad)
+    (abi.GSX_ROUTER_GOSSIPSUB, 200, 1, 0, False),    # cut after hop 1: the last hop still delivers
+    (abi.GSX_ROUTER_GOSSIPSUB, 200, 2, 0, False),
+    (abi.GSX_ROUTER_FLOODSUB, 4096, 3, 0, False),    # 64 words, cut at hop 3
+    (abi.GSX_ROUTER_GOSSIPSUB, 0, 40, 10, True),     # empty batch
+]
+
+
+@pytest.mark.parametrize("case", EDGE_CASES, ids=[f"r{c[0]}-m{c[1]}-h{c[2]}-l{c[3]}" for c in EDGE_CASES])
+def test_propagation_edge_cases_match_oracle(gpu_ok, case):
+    """A hub of degree ~600 (one lane group walks 600 pairs), isolated nodes
+    and isolated sources, batches cut short by max_hops (the late accounting's
+    last hop still delivers), a 64-word batch, an empty batch."""
+    router, m, max_hops, lat, track = case
+    n, T = 640, 1
+    ov = _hub_overlay(n, seed=m + max_hops)
+    ms = pc.messages(n, m, seed=m + 7)
+    if m:
+        ms["source"][: min(m, 3)] = [n - 1, n - 2, 0][: min(m, 3)]  # two isolated sources and the hub
+    cfg = pc.config(router, max_hops=max_hops, latency_ms=lat)
+    res = []
+    eng = gsx.Engine(T)
+    eng.set_prop_tracking(track)
+    for be in (eng, orc.Oracle(T)):
+        pc.setup(be, ov, T, seed=5, disconnect_frac=0.02)
+        out, hop, frm = be.propagate(ms, cfg, want_results=True)
+        res.append((out.as_dict(), hop, frm, be.export_state(), be.scores()))
+    (go, gh, gf, gs, gsc), (wo, wh, wf, ws, wsc) = res
+    assert go == wo
+    assert np.array_equal(gh, wh), np.argwhere(gh != wh)[:5]
+    if track:
+        assert np.array_equal(gf, wf), np.argwhere(gf != wf)[:5]
+    for f in abi.STATE_FIELDS:
+        assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
+    assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))
+    if m == 0:
+        assert go["deliveries"] == 0 and go["transmissions"] == 0
+
+
+def test_randomsub_degree_limit_fails_loudly(gpu_ok):
+    """RandomSub draws hold at most 256 candidates per node: a hub above that is refused, not truncated."""
+    ov = _hub_overlay(400, seed=1)
+    e = gsx.Engine(1)
+    pc.setup(e, ov, 1, seed=5)
+    with pytest.raises(gsx.GsxError):
+        e.propagate(pc.messages(400, 10, seed=3), pc.config(abi.GSX_ROUTER_RANDOMSUB, size=50))
