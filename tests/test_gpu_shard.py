@@ -51,6 +51,9 @@ CASES = [
     (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 300, True, 0.02, "compact-invalid"),
     (2, 1500, 5, 2, abi.GSX_ROUTER_GOSSIPSUB, 1, 200, True, 0.02, "dense-counts-invalid"),
     (2, 1600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 100, True, 0.02, "compact-invalid"),
+    # batches cut short by max_hops (the last hop still delivers), rows of several chunks per lane
+    (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 1100, True, 0.02, "compact-counts-cut"),
+    (3, 1200, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 2048, False, 0.0, "compact-cut"),
 ]
 
 
@@ -59,16 +62,18 @@ CASES = [
                               for c in CASES])
 def test_range_sharded_matches_single_engine(gpu_ok, case):
     world, n, d, T, router, fp, m, mix, disc, compact = case
-    track, invalid, delay = True, 0.0, 0.0
-    if isinstance(compact, str):  # "<exchange>[-counts][-invalid]"
+    track, invalid, delay, max_hops = True, 0.0, 0.0, 40
+    if isinstance(compact, str):  # "<exchange>[-counts][-invalid][-cut]"
         track = "counts" not in compact
         if "invalid" in compact:  # messages validation drops, and a validation delay
             invalid, delay = 0.25, 3.0
+        if "cut" in compact:
+            max_hops = 3
         compact = compact.startswith("compact")
     seed = 3 * n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
     msgs = pc.messages(n, m, seed, invalid=invalid)
-    cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60, delay_ms=delay)
+    cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60, delay_ms=delay, max_hops=max_hops)
     full = gsx.Engine(T)
     app = pc.setup(full, ov, T, seed, disconnect_frac=disc)
     st0 = full.export_state()
