@@ -249,6 +249,8 @@ struct GossipBatch {
     const uint64_t* seen;
     uint32_t n_words;
     uint32_t slot_base;  // slot of message 0 in HbState::mc_digest
+    uint32_t wdig_base;  // HbState::mc_digest[wdig_base + w]: digest sum of all of word w's messages
+    uint32_t n_msgs;
 };
 
 struct HbState {
@@ -295,6 +297,7 @@ hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
 hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st);
+hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const uint8_t* only, hipStream_t st);
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
                                const uint32_t* group_off, uint32_t n_groups, hipStream_t st);
 hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st);

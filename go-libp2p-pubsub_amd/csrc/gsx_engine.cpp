@@ -1977,14 +1977,22 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     e->gb_host.clear();
     e->mc_digest_host.clear();
     std::vector<uint32_t> gb_off(e->T + 1, 0), max_ids(e->T, 0);
+    std::vector<uint64_t> wdig;  // per batch word: the digest sum of all its messages (a full word's digest)
     const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
     for (uint32_t t = 0; t < e->T; ++t) {
         gb_off[t] = (uint32_t)e->gb_host.size();
         for (size_t w = 0; w < n_win; ++w)
             for (const auto& b : e->mc[w]) {
                 if (b.topic != t) continue;
-                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_digest_host.size()});
-                for (uint64_t id : b.ids) e->mc_digest_host.push_back(id_digest(id));
+                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_digest_host.size(),
+                                                      (uint32_t)wdig.size(), b.n_msgs});
+                for (size_t k = 0; k < b.ids.size(); ++k) {
+                    const uint64_t d = id_digest(b.ids[k]);
+                    e->mc_digest_host.push_back(d);
+                    if (k % 64 == 0) wdig.push_back(0);
+                    wdig.back() += d;
+                }
+                for (size_t k = (b.ids.size() + 63) / 64; k < b.n_words; ++k) wdig.push_back(0);
                 max_ids[t] += b.n_msgs;
             }
         if (max_ids[t] > gsx::HB_GOSSIP_MAX_IDS)
@@ -1993,6 +2001,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                            std::to_string(gsx::HB_GOSSIP_MAX_IDS) + " (shift the cache more often)");
     }
     gb_off[e->T] = (uint32_t)e->gb_host.size();
+    for (auto& g : e->gb_host) g.wdig_base += (uint32_t)e->mc_digest_host.size();  // word digests follow the slots
+    e->mc_digest_host.insert(e->mc_digest_host.end(), wdig.begin(), wdig.end());
     if (e->gb_host.size() > e->gb_cap) {
         if (e->d_gb) (void)hipFree(e->d_gb);
         e->d_gb = nullptr;
@@ -2024,7 +2034,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                         e->stream));
     }
     // the receivers score the senders as the round left them
-    HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the pairs (A) touched
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
@@ -2035,7 +2045,7 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
-    HIPCHK(e, gsx::launch_refresh_score(ds, kern_params(e), 0, false, e->stream));
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
     return GSX_OK;
 }
 
@@ -2046,8 +2056,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     e->hb_active = false;
     std::memset(out, 0, sizeof(*out));
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
     HIPCHK(e, gsx::launch_hb_mesh_links(ds, h, e->stream));
-    e->scores_valid = false;
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));

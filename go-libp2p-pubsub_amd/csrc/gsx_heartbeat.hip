@@ -222,9 +222,38 @@ __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, 
 // One launch per topic, ascending: the maintenance of (v, t) for every v.
 __global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
     uint64_t grafts = 0, prunes = 0;
+    const DevGossipParams& gp = h.gp;
+    const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
     for (uint32_t v = blockIdx.x * 64u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[v];
-        HbUnit U{s, h, t, r0, (int)(h.row_ptr[v + 1] - r0)};
+        const int deg = (int)(h.row_ptr[v + 1] - r0);
+        // One pass decides whether any step of maintain() acts (a steady mesh:
+        // no negative score, Dlo <= |mesh| <= Dhi, enough outbound peers, not
+        // an opportunistic-graft tick); such a unit draws nothing and is done.
+        // A graft step with no candidate (getPeers over an empty list) draws
+        // nothing either.
+        int n = 0, neg = 0, outb = 0, cand = 0, cand_out = 0;
+        for (int i = 0; i < deg; ++i) {
+            const uint64_t r = r0 + i;
+            const uint8_t f = h.eflags[r];
+            if (hb_in_mesh(s, r, t)) {
+                ++n;
+                neg += s.score[r] < 0;
+                outb += (f & EDGE_OUTBOUND) != 0;
+            } else if ((s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+                       (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && h.backoff[(size_t)t * h.n_pairs + r] == 0 &&
+                       s.score[r] >= 0.0) {  // getPeers' filter of the graft steps (:1370-1385, :1450-1476)
+                ++cand;
+                cand_out += (f & EDGE_OUTBOUND) != 0;
+            }
+        }
+        const bool grow = n < gp.d_lo && cand > 0;                               // :1370-1385
+        const bool outbound = n >= gp.d_lo && outb < gp.d_out && cand_out > 0;  // :1450-1476
+        if (!neg && n <= gp.d_hi && !grow && !outbound && !(og_tick && n > 1)) {
+            h.rngk[v] = 0;
+            continue;
+        }
+        HbUnit U{s, h, t, r0, deg};
         Rng g = hb_rng(h, v, t, 0);
         U.maintain(g);
         h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
@@ -270,6 +299,14 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
             for (uint32_t w = 0; w < B.n_words; ++w) {
                 uint64_t word = B.seen[(size_t)v * B.n_words + w];
                 L += (uint32_t)__popcll(word);
+                // a node holding every message of the word (the common case once a
+                // batch has spread) adds the word's precomputed digest sum
+                const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
+                const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                if (word && word == full) {
+                    dig += h.mc_digest[B.wdig_base + w];
+                    continue;
+                }
                 while (word) {
                     dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
                     word &= word - 1;
@@ -465,6 +502,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             const uint8_t ef = h.eflags[q];
             // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
             if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
+            h.dirty[q] = 1;  // its record may change below: its score is re-evaluated after (B)
             uint64_t resp = 0;
             for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
                 const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
@@ -526,6 +564,7 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
         uint64_t resp = q == NO_PAIR ? 0 : (q & HALO) ? h.halo_resp[q & ~HALO] : h.resp[q];
         // AcceptFrom at v for the answering peer
         if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
+        if (resp) h.dirty[r] = 1;
         for (; resp; resp &= resp - 1) {
             handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp));
             ++handled;
