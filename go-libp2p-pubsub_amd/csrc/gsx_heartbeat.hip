@@ -281,12 +281,6 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
-// Advances g over shuffleStrings of an n-element list (gossipsub.go:1897-1902)
-// without materialising it: one Int31n(i + 1) per step, rejections redrawn.
-__device__ __forceinline__ void skip_shuffle(Rng& g, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i) (void)g.int31n((int32_t)(i + 1));
-}
-
 __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
                                                   uint32_t n_gb) {
     uint64_t msgs = 0, ids = 0;
@@ -328,9 +322,8 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
             if (target > 0 && L > (uint32_t)h.gp.max_ihave) {
                 h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // per-target truncation: k_hb_gossip_long
             } else if (target > 0) {
-                if (shuffle_peers) {  // the list shuffle only matters through the draws it consumes
+                if (shuffle_peers) {  // an untruncated list is not shuffled (its order is never observable)
                     Rng g = hb_rng(h, v, t, h.rngk[v]);
-                    skip_shuffle(g, L);
                     g.shuffle(peers, np);
                 }
                 for (int p = 0; p < target; ++p) {

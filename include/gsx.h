@@ -539,8 +539,9 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  * of the gossipsub batches it saw (gsx_propagate with the gossipsub router
  * Puts every message a node receives or publishes into its cache window 0;
  * within a batch the insertion order is ascending message index), read
- * newest window first over HistoryGossip windows, shuffled with the same
- * draw stream; targets are the non-mesh, non-direct mesh-capable topic peers
+ * newest window first over HistoryGossip windows; a list longer than
+ * MaxIHaveLength is shuffled with the same draw stream (a shorter one is sent
+ * whole, so its order is never observable and consumes no draws); targets are the non-mesh, non-direct mesh-capable topic peers
  * whose live score (after the node's maintenance of topics <= t) is >=
  * GossipThreshold, max(Dlazy, GossipFactor * |eligible|) of them, shuffled;
  * lists longer than MaxIHaveLength are reshuffled per target and truncated.

@@ -1391,7 +1391,10 @@ static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t*
         }
     if (L == 0) return;
     uint64_t* ids = *mids;
-    shuffle_ids(ids, L, g);
+    /* shuffleStrings(mids) (:1676): the order is observable only through the
+     * per-target truncation, so the canonical draws shuffle only a list
+     * longer than MaxIHaveLength (gsx.h, heartbeat draws) */
+    if (L > (size_t)gp->max_ihave_length) shuffle_ids(ids, L, g);
     int np = 0;
     for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
         if (!in_topic(o, (uint64_t)r)) continue;
