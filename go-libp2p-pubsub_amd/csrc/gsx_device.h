@@ -195,6 +195,8 @@ struct PropState {
     double publish_threshold;
     int64_t hop_latency, window;
     uint64_t seed;
+    uint32_t* hop_flag;  // host-mapped, [hop]: k_prop_mark(h) stores (hop_seq << 1) | (hop h-1 delivered); null: off
+    uint32_t hop_seq;
 };
 
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st);

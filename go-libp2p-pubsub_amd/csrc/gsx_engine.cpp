@@ -94,6 +94,7 @@ struct gsx_engine {
     int64_t* d_row_ptr = nullptr;
     uint32_t* d_rev = nullptr;  // pair (u -> v) -> pair (v -> u)
     std::vector<uint8_t> eflags_host;
+    bool floodsub_peers = true;  // some non-direct pair speaks no gossipsub (its publishes are score-gated)
     int64_t max_deg = 0;
 
     // heartbeat: router params, backoff [topic][pair], this round's control bytes
@@ -154,9 +155,22 @@ struct gsx_engine {
         // pending (deferred) credits: topic they belong to
         bool credit_pending = false;
         uint32_t credit_topic = 0;
-        // per-hop kernel timing
+        // per-hop kernel timing (gsx_propagate: one pair around its hop loop)
         std::vector<hipEvent_t> ev;
         uint32_t ev_used = 0;
+        bool loop_timing = false;
+        uint32_t launches = 0;
+        // gsx_propagate's early stop: k_prop_mark reports every finished hop here
+        uint32_t* hop_flag = nullptr;    // host-mapped [GSX_MAX_HOPS + 1]
+        uint32_t* d_hop_flag = nullptr;  // its device address
+        uint32_t hop_seq = 0;
+        // fwd / pin of the last call, reused while nothing they read changed
+        struct {
+            bool valid = false;
+            uint32_t router = 0, topic = 0, flood_publish = 0;
+            uint64_t flag_gen = 0, score_gen = 0;
+            double publish_threshold = 0;
+        } fwd_key;
         // compacted shard exchange: the dense halo the received entries are
         // scattered into, the slots filled last hop, per-destination counts
         uint64_t* halo = nullptr;
@@ -194,6 +208,14 @@ struct gsx_engine {
     bool staged_inflight = false;
 
     bool scores_valid = false;
+    // generations: flag_gen moves with anything that may change pair / record
+    // flags, the overlay or the thresholds; score_gen with anything that may
+    // change a score (both with the former)
+    uint64_t flag_gen = 1, score_gen = 1;
+    void state_changed() {
+        ++flag_gen;
+        ++score_gen;
+    }
     bool timed = false;
     // gsx_timing_begin/end: event pairs around each fused launch
     std::vector<hipEvent_t> tev;
@@ -348,8 +370,13 @@ void free_state(gsx_engine* e) {
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
+    uint32_t *hf = e->prop.hop_flag, *dhf = e->prop.d_hop_flag;
+    const uint32_t hseq = e->prop.hop_seq;
     e->prop = {};
     e->prop.ev = std::move(evs);
+    e->prop.hop_flag = hf;
+    e->prop.d_hop_flag = dhf;
+    e->prop.hop_seq = hseq;
     e->d_send_pair = e->d_pair_obs = e->d_halo_node = nullptr;
     e->d_send_dest = nullptr;
     e->d_send_base = e->d_dest_halo_base = nullptr;
@@ -475,6 +502,7 @@ int flush(gsx_engine* e) {
     HIPCHK(e, gsx::launch_apply_events(dev_state(e), dev_peer_params(e), dev, doff, n_groups, e->stream));
     e->pending.clear();
     e->scores_valid = false;
+    e->state_changed();
     return GSX_OK;
 }
 
@@ -665,6 +693,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->prop.ev) (void)hipEventDestroy(ev);
+    if (e->prop.hop_flag) (void)hipHostFree(e->prop.hop_flag);
     if (!e->own_stream) e->own_stream = e->stream;  // gsx_create failed before recording it
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -685,12 +714,14 @@ int gsx_set_peer_params(gsx_engine* e, const gsx_peer_score_params* p) {
     e->pp = *p;
     e->pp_set = true;
     e->scores_valid = false;
+    e->state_changed();
     return GSX_OK;
 }
 
 int gsx_set_thresholds(gsx_engine* e, const gsx_thresholds* t) {
     if (!e || !t) return GSX_EINVAL;
     e->th = *t;
+    e->state_changed();
     return GSX_OK;
 }
 
@@ -707,6 +738,7 @@ int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_pa
     e->tp[topic] = *p;
     e->scored[topic] = true;
     e->scores_valid = false;
+    e->state_changed();
     rc = upload_topic_params(e);
     if (rc) return rc;
     if (!exist || !e->loaded) return GSX_OK;
@@ -847,12 +879,16 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
         HIPCHK(e, hipMemcpy(e->d_row_ptr, row_ptr, sizeof(int64_t) * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
         e->eflags_host.assign(edge_flags ? edge_flags : nullptr, edge_flags ? edge_flags + E : nullptr);
     }
+    e->floodsub_peers = !edge_flags || std::any_of(edge_flags, edge_flags + E, [](uint8_t f) {
+        return !(f & gsx::EDGE_GOSSIPSUB) && !(f & gsx::EDGE_DIRECT);
+    });
     if (edge_flags) HIPCHK(e, hipMemcpy(e->d_eflags, edge_flags, E, hipMemcpyHostToDevice));
     else HIPCHK(e, hipMemsetAsync(e->d_eflags, 0, e->rs, e->stream));
     rc = upload_ipg(e);
     if (rc) return rc;
     e->loaded = true;
     e->scores_valid = false;
+    e->state_changed();
     return GSX_OK;
 }
 }  // namespace
@@ -995,6 +1031,7 @@ int gsx_set_ip_whitelist(gsx_engine* e, const uint32_t* ip_ids, size_t n) {
         e->ip_wl[ip_ids[i]] = 1;
     }
     e->scores_valid = false;
+    e->state_changed();
     if (!e->loaded) return GSX_OK;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return upload_ipg(e);
@@ -1009,6 +1046,7 @@ int gsx_set_app_scores(gsx_engine* e, const double* app, size_t n) {
     HIPCHK(e, hipMemcpyAsync(e->d_app, app, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->scores_valid = false;
+    e->state_changed();
     return GSX_OK;
 }
 
@@ -1141,6 +1179,7 @@ int gsx_refresh(gsx_engine* e, int64_t now) {
     if (region) ++e->t_used;
     e->timed = !region;
     e->scores_valid = true;
+    e->state_changed();
     e->last_refresh = now;
     return GSX_OK;
 }
@@ -1253,6 +1292,7 @@ int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     release_tmp(e);
     e->scores_valid = false;
+    e->state_changed();
     if (n_bad) return fail(e, GSX_EINVAL, std::to_string(n_bad) + " in-mesh records have a meshTime that is neither 0 "
                                           "nor last_refresh_ns - graftTime");
     return GSX_OK;
@@ -1282,6 +1322,7 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     HIPCHK(e, gsx::launch_rebuild_ipcount(s, e->n_groups, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->scores_valid = false;
+    e->state_changed();
     return GSX_OK;
 }
 
@@ -1440,7 +1481,10 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)
         return fail(e, GSX_ESTATE, "deferred credits of another topic are pending: gsx_prop_fold_credits first");
-    if (int rc = ensure_scores(e)) return rc;  // publishThreshold tests read current scores
+    // publishThreshold tests read current scores; gossipsub reads them only for
+    // floodsub peers and flood publishing (k_prop_fwd), the other routers never
+    const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB && (cfg->flood_publish || e->floodsub_peers);
+    if (int rc = need_score ? ensure_scores(e) : flush(e)) return rc;  // queued events land first either way
     const uint32_t W = prop_words(m);
     const size_t N = e->n_nodes, E = e->E;
     const uint32_t rows = cfg->max_hops + 1;
@@ -1543,6 +1587,8 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     P.h = 0;
     P.sel_done = false;
     P.ev_used = 0;
+    P.launches = 0;
+    P.loop_timing = false;
     P.ids.resize(m);
     for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
     P.active = true;
@@ -1562,7 +1608,24 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     HIPCHK(e, hipMemsetAsync(P.flast, 0, 8 * std::max<size_t>(E, 1), e->stream));
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
-    HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
+    // fwd / pin (k_prop_fwd, k_prop_pin) read the router config, the pair and
+    // record flags, the overlay and, where a threshold decides, the scores:
+    // the last call's are reused while none of those moved (unsharded only:
+    // a shard plan rewrites the reverse pairs)
+    auto& K = P.fwd_key;
+    const bool fwd_same = K.valid && !e->sharded() && K.router == cfg->router && K.topic == cfg->topic &&
+                          K.flood_publish == cfg->flood_publish && K.flag_gen == e->flag_gen &&
+                          K.publish_threshold == e->th.publish_threshold && (!need_score || K.score_gen == e->score_gen);
+    if (!fwd_same) {
+        HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
+        K.valid = true;
+        K.router = cfg->router;
+        K.topic = cfg->topic;
+        K.flood_publish = cfg->flood_publish;
+        K.flag_gen = e->flag_gen;
+        K.score_gen = e->score_gen;
+        K.publish_threshold = e->th.publish_threshold;
+    }
     HIPCHK(e, gsx::launch_prop_init(ps, P.hist, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));  // `hm` is on the host stack
     return GSX_OK;
@@ -1579,9 +1642,12 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
     ps.halo = halo;
     ps.halo_occ = (halo && halo == P.halo) ? P.halo_occ : nullptr;  // compacted: rows not received are empty
     const uint32_t h = ++P.h;
-    hipEvent_t a, b;
-    if (int rc = prop_event_pair(e, &a, &b)) return rc;
-    HIPCHK(e, hipEventRecord(a, e->stream));
+    ++P.launches;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (!P.loop_timing) {
+        if (int rc = prop_event_pair(e, &a, &b)) return rc;
+        HIPCHK(e, hipEventRecord(a, e->stream));
+    }
     const size_t row = (size_t)ps.n_nodes * ps.n_words;
     const uint64_t* front = P.hist + (size_t)(h - 1) * row;
     const uint64_t* front_occ = P.occ + (size_t)(h - 1) * ((ps.n_nodes + 63) / 64);
@@ -1589,8 +1655,29 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
     if (ps.sel && !P.sel_done) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = false;
     HIPCHK(e, gsx::launch_prop_hop(ps, h, front, P.hist + (size_t)h * row, e->stream));
-    HIPCHK(e, hipEventRecord(b, e->stream));
+    if (!P.loop_timing) HIPCHK(e, hipEventRecord(b, e->stream));
     return GSX_OK;
+}
+
+// gsx_propagate's early stop: whether hop h delivered anything, from the
+// report k_prop_mark(h + 1) stores in host-mapped memory once hop h is done.
+// Waits for the report; without one (the stream drained first, or failed)
+// the answer is "yes" (the caller just launches the hop, which then does
+// nothing).
+bool hop_delivered(gsx_engine* e, uint32_t h) {
+    auto& P = e->prop;
+    const uint32_t want = P.hop_seq << 1;
+    for (uint32_t spin = 1;; ++spin) {
+        const uint32_t v = __atomic_load_n(P.hop_flag + h, __ATOMIC_ACQUIRE);
+        if ((v & ~1u) == want) return v & 1u;
+        if (spin % 64 == 0) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q != hipErrorNotReady) {
+                const uint32_t w = __atomic_load_n(P.hop_flag + h, __ATOMIC_ACQUIRE);
+                return (w & ~1u) == want ? (w & 1u) : true;
+            }
+        }
+    }
 }
 
 int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
@@ -1601,6 +1688,7 @@ int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
     HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * e->E, e->stream));
     P.credit_pending = false;
     e->scores_valid = false;
+    ++e->score_gen;
     return GSX_OK;
 }
 
@@ -1618,7 +1706,10 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         // pending ones of the topic) and left the pending counts empty
         P.credit_pending = !fold_now;
         P.credit_topic = ps.topic;
-        if (fold_now) e->scores_valid = false;
+        if (fold_now) {
+            e->scores_valid = false;
+            ++e->score_gen;
+        }
     }
     const uint32_t W = ps.n_words;
     if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
@@ -1661,7 +1752,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         ms += t;
     }
     out->hop_kernel_ms = ms;
-    out->hop_launches = P.ev_used / 2;
+    out->hop_launches = P.launches;
     return GSX_OK;
 }
 
@@ -1673,8 +1764,38 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
         return fail(e, GSX_ESTATE, "sharded engine: drive hops with gsx_prop_begin/pack/step/end");
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
     if (int rc = prop_begin(e, msgs, m, cfg)) return rc;
-    for (uint32_t h = 1; h <= cfg->max_hops; ++h)
+    auto& P = e->prop;
+    // Hops run back to back under one event pair.  Once a hop has delivered
+    // nothing every later one is empty (its kernels return at once), so the
+    // loop stops launching: before hop h it waits for hop h - 2's report
+    // (hop h - 1 is queued meanwhile, the device never idles on the host).
+    if (P.last.n_msgs && !P.hop_flag) {
+        void* hf = nullptr;
+        HIPCHK(e, hipHostMalloc(&hf, 4 * (GSX_MAX_HOPS + 1), hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hf, 0, 4 * (GSX_MAX_HOPS + 1));
+        P.hop_flag = static_cast<uint32_t*>(hf);
+        void* dp = nullptr;
+        HIPCHK(e, hipHostGetDevicePointer(&dp, hf, 0));
+        P.d_hop_flag = static_cast<uint32_t*>(dp);
+    }
+    if (P.last.n_msgs) {
+        P.hop_seq = (P.hop_seq + 1) & 0x7FFFFFFFu;
+        if (P.hop_seq == 0) P.hop_seq = 1;
+        P.last.hop_flag = P.d_hop_flag;
+        P.last.hop_seq = P.hop_seq;
+        P.loop_timing = true;
+    }
+    hipEvent_t a = nullptr, b = nullptr;
+    if (P.loop_timing) {
+        if (int rc = prop_event_pair(e, &a, &b)) return rc;
+        HIPCHK(e, hipEventRecord(a, e->stream));
+    }
+    for (uint32_t h = 1; h <= cfg->max_hops; ++h) {
+        if (P.loop_timing && h >= 3 && !hop_delivered(e, h - 2)) break;
         if (int rc = prop_hop(e, nullptr)) return rc;
+    }
+    if (P.loop_timing) HIPCHK(e, hipEventRecord(b, e->stream));
+    P.last.hop_flag = nullptr;  // the stepped entry points leave it off
     return prop_end(e, out);
 }
 
@@ -1703,6 +1824,7 @@ int gsx_prop_pack(gsx_engine* e, uint64_t* send) {
     const uint64_t* front_occ = P.occ + (size_t)P.h * ((ps.n_nodes + 63) / 64);
     if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = true;
+    ++P.launches;
     HIPCHK(e, gsx::launch_prop_pack(ps, front, front_occ, send, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     return GSX_OK;
@@ -1743,6 +1865,7 @@ int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
     if (ps.sel) HIPCHK(e, gsx::launch_rsub_select(ps, front, front_occ, e->stream));
     P.sel_done = true;
     HIPCHK(e, hipMemsetAsync(P.dcount, 0, 8 * (size_t)e->n_ranks, e->stream));
+    ++P.launches;
     HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, front_occ, out, P.dcount, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     HIPCHK(e, hipMemcpyAsync(counts, P.dcount, 8 * (size_t)e->n_ranks, hipMemcpyDeviceToHost, e->stream));
@@ -1909,6 +2032,7 @@ namespace {
 //             mcache.Shift.
 int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    e->state_changed();
     if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
         return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
     if (e->max_deg > gsx::HB_MAX_DEG)
@@ -2041,6 +2165,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
 }
 
 int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
+    e->state_changed();
     gsx::HbState h = e->hb;
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
@@ -2050,6 +2175,7 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
 }
 
 int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
+    e->state_changed();
     gsx::HbState h = e->hb;
     h.halo_resp = halo_resp;
     const gsx::DevState ds = dev_state(e);

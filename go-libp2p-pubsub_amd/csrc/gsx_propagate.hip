@@ -308,6 +308,9 @@ __global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, con
         touch_next[i] = 0;
     }
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    if (ps.hop_flag && blockIdx.x == 0 && threadIdx.x == 0)  // hop h - 1 is complete: tell the launching host
+        __hip_atomic_store(ps.hop_flag + (h - 1), (ps.hop_seq << 1) | (prev != 0 ? 1u : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     if (!mark_hop(ps, h) || (!ps.sharded && h > 1 && prev == 0)) return;
     uint64_t* touch = ps.touch + (size_t)(h & 1) * occ_row;
     for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < ps.n_nodes; v += gridDim.x * 256u) {
@@ -842,53 +845,83 @@ __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_ru
 // so no thread scatters into another pair's counter.  A pair takes the
 // per-word path only for RandomSub draws, tracked `from` rows, or a
 // publishing u; every other pair reads its class's count from vcnt.
+// Batches of DU pairs per thread (q0 + i * stride): the loads of a batch are
+// issued together, so a thread waits for one round of latencies per batch
+// rather than one per pair.
+constexpr int DU = 4;
 __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
     unsigned long long cnt[1] = {0};
     const uint32_t W = ps.n_words;
     const DupsLast L = dups_last(ps, h_run);
     h_run = L.h_run;
     const uint64_t* src_occ = ps.occ;  // row 0: nodes that published in this call
-    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < ps.n_pairs; r += (uint64_t)gridDim.x * 256u) {
-        const uint32_t q = ps.rev[r];  // the receiver's pair (u -> v)
-        const uint8_t fw = ps.fwd[r];
-        if (q == NO_PAIR || (q & HALO) || !fw) continue;
-        const uint32_t v = ps.pair_obs[r];
-        const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
-        const bool u_src = occ_bit(src_occ, u);
-        uint32_t sends = 0, pub = 0;
-        if (!u_src && !ps.sel && !ps.from_mask) {
-            const uint64_t vc = vcnt[v];
-            const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
-            const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
-            sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
-                  : m == FWD_PUBLISH ? n_own : 0;
-        } else {
-            const bool v_src = occ_bit(src_occ, v);
-            const bool v_last = !L.empty && occ_bit(L.occ, v);
-            for (uint32_t w = 0; w < W; ++w) {
-                const size_t vw = (size_t)v * W + w;
-                uint64_t s = ps.seen[vw];
-                if (v_last) s &= ~L.row[vw];
-                s &= elig_word(fw, v_src ? ps.origin[vw] : 0);
-                if (ps.sel) s |= ps.sel[r * W + w];
-                if (ps.from_mask) s &= ~ps.from_mask[r * W + w];
-                if (ps.drop) s &= ~ps.drop[w];  // copies of dropped messages are receipts, not deliveries
-                if (u_src) {
-                    const uint64_t ou = ps.origin[(size_t)u * W + w] & (ps.drop ? ~ps.drop[w] : ~0ull);
-                    s &= ~ou;
-                    pub += __popcll(ou);
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t r0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; r0 < ps.n_pairs; r0 += stride * DU) {
+        uint32_t qa[DU], va[DU], ua[DU];
+        uint8_t fa[DU];
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t r = r0 + i * stride;
+            const bool in = r < ps.n_pairs;
+            qa[i] = in ? ps.rev[r] : NO_PAIR;  // the receiver's pair (u -> v)
+            fa[i] = in ? ps.fwd[r] : 0;
+            va[i] = in ? ps.pair_obs[r] : 0;
+            ua[i] = in ? (uint32_t)ps.col[r] - ps.node_lo : 0;
+        }
+        uint64_t vca[DU], fla[DU];
+        uint32_t fca[DU];
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t r = r0 + i * stride;
+            const bool live = qa[i] != NO_PAIR && !(qa[i] & HALO) && fa[i];
+            vca[i] = live ? vcnt[va[i]] : 0;
+            const bool fl = live && !ps.from_mask && (fa[i] & FWD_FORWARD) && h_run >= 1;
+            fca[i] = fl ? ps.fcnt[r] : 0;
+            fla[i] = fl ? ps.flast[r] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t r = r0 + i * stride;
+            const uint32_t q = qa[i];
+            const uint8_t fw = fa[i];
+            if (q == NO_PAIR || (q & HALO) || !fw) continue;
+            const uint32_t v = va[i], u = ua[i];
+            const bool u_src = occ_bit(src_occ, u);
+            uint32_t sends = 0, pub = 0;
+            if (!u_src && !ps.sel && !ps.from_mask) {
+                const uint64_t vc = vca[i];
+                const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
+                const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
+                sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
+                      : m == FWD_PUBLISH ? n_own : 0;
+            } else {
+                const bool v_src = occ_bit(src_occ, v);
+                const bool v_last = !L.empty && occ_bit(L.occ, v);
+                for (uint32_t w = 0; w < W; ++w) {
+                    const size_t vw = (size_t)v * W + w;
+                    uint64_t sb = ps.seen[vw];
+                    if (v_last) sb &= ~L.row[vw];
+                    sb &= elig_word(fw, v_src ? ps.origin[vw] : 0);
+                    if (ps.sel) sb |= ps.sel[r * W + w];
+                    if (ps.from_mask) sb &= ~ps.from_mask[r * W + w];
+                    if (ps.drop) sb &= ~ps.drop[w];  // copies of dropped messages are receipts, not deliveries
+                    if (u_src) {
+                        const uint64_t ou = ps.origin[(size_t)u * W + w] & (ps.drop ? ~ps.drop[w] : ~0ull);
+                        sb &= ~ou;
+                        pub += __popcll(ou);
+                    }
+                    sends += __popcll(sb);
                 }
-                sends += __popcll(s);
             }
+            if (!ps.from_mask && (fw & FWD_FORWARD) && h_run >= 1) {
+                const uint64_t fl = fla[i];
+                const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
+                const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH)) ? pub : 0;  // pub != 0 only if u published
+                sends -= fca[i] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
+            }
+            cnt[0] += sends;
+            ps.corr[r] = sends;
         }
-        if (!ps.from_mask && (fw & FWD_FORWARD) && h_run >= 1) {
-            const uint64_t fl = ps.flast[r];
-            const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
-            const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH)) ? pub : 0;  // pub != 0 only if u published
-            sends -= ps.fcnt[r] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
-        }
-        cnt[0] += sends;
-        ps.corr[r] = sends;
     }
     const uint32_t slot[1] = {STAT_DUPS};
     block_count<1>(cnt, ps.stats, slot);
@@ -921,33 +954,52 @@ template <bool FOLD>
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
     unsigned long long cnt[1] = {0};
     const bool fold_topic = FOLD && ps.topic < s.n_topics && s.tp[ps.topic].scored;
-    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
-        const uint32_t k1 = ps.fcnt[q];
-        const uint32_t r = ps.rev[q];
-        const bool local = r != NO_PAIR && !(r & HALO);
-        if (ps.credit) {
-            // (unsharded, late accounting, nothing deferred: the hops wrote no
-            // pending counts and none were left, so they are not read)
-            const uint32_t f0 = ps.pending ? ps.firstcnt[q] : 0, d0 = ps.pending ? ps.dupcnt[q] : 0;
-            uint32_t first = f0 + k1, dup = d0;
-            if (local) {
-                if (ps.late) dup += ps.corr[r] - k1;  // k_prop_dups: every send from v, first receipts too
-                else dup -= ps.corr[r];               // in-window back-sends taken back
-            }
-            if (FOLD) {  // GSX_CREDIT_NOW: fold at once (k_prop_fold) and leave the counts empty
-                if (f0 | d0) {
-                    ps.firstcnt[q] = 0;
-                    ps.dupcnt[q] = 0;
-                }
-                uint32_t k4 = 0;
-                if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
-                if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup, k4);
-            } else {
-                ps.firstcnt[q] = first;
-                ps.dupcnt[q] = dup;
-            }
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; q0 < ps.n_pairs; q0 += stride * DU) {
+        uint32_t k1a[DU], ra[DU], ca[DU];
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t q = q0 + i * stride;
+            const bool in = q < ps.n_pairs;
+            k1a[i] = in ? ps.fcnt[q] : 0;
+            ra[i] = in ? ps.rev[q] : NO_PAIR;
         }
-        if (ps.late && local) cnt[0] += k1;
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {  // the sender pair's sends (k_prop_dups), one gather per pair
+            const bool local = ra[i] != NO_PAIR && !(ra[i] & HALO);
+            ca[i] = (local && ps.credit) ? ps.corr[ra[i]] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t q = q0 + i * stride;
+            if (q >= ps.n_pairs) break;
+            const uint32_t k1 = k1a[i];
+            const uint32_t r = ra[i];
+            const bool local = r != NO_PAIR && !(r & HALO);
+            if (ps.credit) {
+                // (unsharded, late accounting, nothing deferred: the hops wrote no
+                // pending counts and none were left, so they are not read)
+                const uint32_t f0 = ps.pending ? ps.firstcnt[q] : 0, d0 = ps.pending ? ps.dupcnt[q] : 0;
+                uint32_t first = f0 + k1, dup = d0;
+                if (local) {
+                    if (ps.late) dup += ca[i] - k1;  // k_prop_dups: every send from v, first receipts too
+                    else dup -= ca[i];               // in-window back-sends taken back
+                }
+                if (FOLD) {  // GSX_CREDIT_NOW: fold at once (k_prop_fold) and leave the counts empty
+                    if (f0 | d0) {
+                        ps.firstcnt[q] = 0;
+                        ps.dupcnt[q] = 0;
+                    }
+                    uint32_t k4 = 0;
+                    if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
+                    if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup, k4);
+                } else {
+                    ps.firstcnt[q] = first;
+                    ps.dupcnt[q] = dup;
+                }
+            }
+            if (ps.late && local) cnt[0] += k1;
+        }
     }
     const uint32_t slot[1] = {STAT_BACKSENDS};
     block_count<1>(cnt, ps.stats, slot);

@@ -209,3 +209,60 @@ def test_randomsub_degree_limit_fails_loudly(gpu_ok):
     pc.setup(e, ov, 1, seed=5)
     with pytest.raises(gsx.GsxError):
         e.propagate(pc.messages(400, 10, seed=3), pc.config(abi.GSX_ROUTER_RANDOMSUB, size=50))
+
+
+@pytest.mark.parametrize("mix", [False, True], ids=["gossipsub-only", "with-floodsub-peers"])
+def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
+    """One engine, many calls: the forwarding state (k_prop_fwd / k_prop_pin)
+    is kept between calls while nothing it reads changed and rebuilt after
+    GRAFT / PRUNE / RemovePeer events, a refresh, new thresholds, app scores
+    (floodsub peers are score-gated), a heartbeat, a topic or router switch.
+    Every call must match the oracle running the same sequence."""
+    n, T = 600, 2
+    ov = pc.overlay(n, 5, seed=31, mix_protocols=mix)
+    E = ov.n_pairs
+    rng = np.random.default_rng(31)
+    eng, ref = gsx.Engine(T), orc.Oracle(T)
+    gp = orc.default_gossipsub_params()
+    for be in (eng, ref):
+        pc.setup(be, ov, T, 31, disconnect_frac=0.02)
+    steps = [
+        ("gossipsub", None),
+        ("gossipsub again", None),
+        ("graft+prune", [(abi.EV_GRAFT, 0, int(q), pc.T0 + 3 * pc.S, 0) for q in rng.choice(E, 40, replace=False)]
+         + [(abi.EV_PRUNE, 0, int(q), pc.T0 + 3 * pc.S, 0) for q in rng.choice(E, 40, replace=False)]),
+        ("remove peers", [(abi.EV_REMOVE_PEER, 0, int(q), pc.T0 + 3 * pc.S, 0) for q in rng.choice(E, 25, replace=False)]),
+        ("refresh", "refresh"),
+        ("thresholds", "thresholds"),
+        ("app scores", "app"),
+        ("heartbeat", "heartbeat"),
+        ("topic 1", None),
+        ("floodsub", None),
+        ("gossipsub after floodsub", None),
+    ]
+    for k, (name, action) in enumerate(steps):
+        for be in (eng, ref):
+            if isinstance(action, list):
+                be.apply_events(np.array(action, dtype=abi.event_dtype()))
+            elif action == "refresh":
+                be.refresh(pc.T0 + 4 * pc.S)
+            elif action == "thresholds":
+                be.set_thresholds(abi.Thresholds(gossip_threshold=-50, publish_threshold=-60, graylist_threshold=-300,
+                                                 accept_px_threshold=0, opportunistic_graft_threshold=0))
+            elif action == "app":
+                be.set_app_scores(np.where(np.arange(E) % 7 == 0, -1000.0, 1.0))
+            elif action == "heartbeat":
+                be.set_gossipsub_params(gp)
+                be.heartbeat(1, pc.T0 + 5 * pc.S, 77)
+        router = abi.GSX_ROUTER_FLOODSUB if name == "floodsub" else abi.GSX_ROUTER_GOSSIPSUB
+        topic = 1 if name == "topic 1" else 0
+        ms = pc.messages(n, 96, seed=100 + k)
+        cfg = pc.config(router, topic=topic, latency_ms=10)
+        res = [be.propagate(ms, cfg, want_results=True) for be in (eng, ref)]
+        (go, gh, _), (wo, wh, _) = res
+        assert go.as_dict() == wo.as_dict(), name
+        assert np.array_equal(gh, wh), name
+        gs, ws = eng.export_state(), ref.export_state()
+        for f in abi.STATE_FIELDS:
+            assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), (name, f)
+        assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
