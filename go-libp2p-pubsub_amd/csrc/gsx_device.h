@@ -266,6 +266,8 @@ struct HbState {
     const uint64_t* halo_ctl;   // [receive slot][2]: GRAFT / PRUNE bits of remote senders (shards)
     const uint64_t* halo_resp;  // [receive slot]: PRUNE answers of remote receivers (shards)
     uint8_t* dirty;       // per pair: grafted / pruned by its owner's maintenance this round
+    uint8_t* inbox;       // per pair (u -> v): v sent GRAFT / PRUNE bits on (v -> u) this round (unsharded reads)
+    uint8_t* answer;      // per pair (v -> u): u answered with PRUNE bits on (u -> v) this round
     unsigned long long* stats;
     uint32_t* rngk;        // per node: draw counter after the maintenance of the current topic
     uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)

@@ -107,6 +107,7 @@ struct gsx_engine {
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
     uint64_t* d_ihave_hash = nullptr;
     bool have_gossip = false;
+    bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
     gsx::HbState hb{};  // the round in flight (gsx_hb_begin .. gsx_hb_end)
     bool hb_active = false;
 
@@ -2042,13 +2043,14 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         int rc = 0;
         const size_t E = e->E;
         if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
-            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, E)) ||
+            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 3 * E)) ||
             (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
             (rc = dalloc(e, &e->d_rngk, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
             (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
             return rc;
         HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+        e->hb_clean = false;
     }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
@@ -2061,6 +2063,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.ctl_prune = e->d_ctl_prune;
     h.resp = e->d_resp;
     h.dirty = e->d_dirty;
+    h.inbox = e->d_dirty + e->E;
+    h.answer = e->d_dirty + 2 * e->E;
     h.long_nodes = e->d_long;
     h.n_long = e->d_nlong;
     h.stats = e->d_hbstats;
@@ -2092,10 +2096,18 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     const size_t E8 = 8 * (e->E ? e->E : 1);
-    HIPCHK(e, hipMemsetAsync(e->d_ctl_graft, 0, E8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_ctl_prune, 0, E8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_resp, 0, E8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, e->E ? e->E : 1, e->stream));
+    // Unsharded, (B) and (C) clear the control words, answers and marks they
+    // read, and nothing else is ever set: after one cleared round they stay
+    // clean.  Shards pack them for the exchange and clear them here.
+    if (e->sharded() || !e->hb_clean) {
+        HIPCHK(e, hipMemsetAsync(e->d_ctl_graft, 0, E8, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_ctl_prune, 0, E8, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_resp, 0, E8, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, 3 * (e->E ? e->E : 1), e->stream));
+    } else {
+        HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, e->E ? e->E : 1, e->stream));
+    }
+    e->hb_clean = false;  // until this round's (C) has run
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
     // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order
     e->gb_host.clear();
@@ -2182,6 +2194,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     e->hb_active = false;
     std::memset(out, 0, sizeof(*out));
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
+    e->hb_clean = !e->sharded();
     HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
     HIPCHK(e, gsx::launch_hb_mesh_links(ds, h, e->stream));
     unsigned long long st[gsx::HB_STAT_WORDS];

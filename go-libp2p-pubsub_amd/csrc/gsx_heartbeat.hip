@@ -113,11 +113,17 @@ struct HbUnit {
         return n;
     }
 
+    // the receiver's pair (u -> v) of r = (v -> u) has control to read in (B)
+    __device__ void mark_inbox(uint64_t r) const {
+        const uint32_t q = h.rev[r];
+        if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
+    }
     __device__ void graft(int i) {  // graftPeer, :1353-1359
         const uint64_t r = r0 + i;
         ev_graft(s, r, t, h.now);
         h.ctl_graft[r] |= 1ull << t;
         h.dirty[r] = 1;
+        mark_inbox(r);
         ++grafts;
     }
     __device__ void prune(int i) {  // prunePeer, :1345-1351
@@ -126,6 +132,7 @@ struct HbUnit {
         add_backoff(h, r, t, h.gp.prune_backoff_ns);
         h.ctl_prune[r] |= 1ull << t;
         h.dirty[r] = 1;
+        mark_inbox(r);
         ++prunes;
     }
 
@@ -220,45 +227,69 @@ __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, 
 }
 
 // One launch per topic, ascending: the maintenance of (v, t) for every v.
+// A wave takes 64 consecutive nodes.  One pass over their pairs — coalesced,
+// lane j reading pairs j, j + 64, ... of the wave's contiguous pair range,
+// counted into the owner's LDS slot — decides whether any step of
+// maintain() acts (a steady mesh: no negative score, Dlo <= |mesh| <= Dhi,
+// enough outbound peers, not an opportunistic-graft tick); such a unit draws
+// nothing and is done.  A graft step with no candidate (getPeers over an
+// empty list) draws nothing either.  Lanes whose unit acts then run
+// maintain() over their own row.
 __global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
+    __shared__ int64_t rs[65];    // row starts of the wave's nodes, rs[nv] = end
+    __shared__ int cnt[5][64];    // per node: |mesh|, negative, outbound in mesh, candidates, outbound candidates
     uint64_t grafts = 0, prunes = 0;
     const DevGossipParams& gp = h.gp;
     const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
-    for (uint32_t v = blockIdx.x * 64u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 64u) {
-        const int64_t r0 = h.row_ptr[v];
-        const int deg = (int)(h.row_ptr[v + 1] - r0);
-        // One pass decides whether any step of maintain() acts (a steady mesh:
-        // no negative score, Dlo <= |mesh| <= Dhi, enough outbound peers, not
-        // an opportunistic-graft tick); such a unit draws nothing and is done.
-        // A graft step with no candidate (getPeers over an empty list) draws
-        // nothing either.
-        int n = 0, neg = 0, outb = 0, cand = 0, cand_out = 0;
-        for (int i = 0; i < deg; ++i) {
-            const uint64_t r = r0 + i;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t v0 = blockIdx.x * 64u; v0 < h.n_nodes; v0 += gridDim.x * 64u) {
+        const uint32_t nv = min(64u, h.n_nodes - v0);
+        rs[lane] = h.row_ptr[v0 + min(lane, nv)];
+        if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) cnt[k][lane] = 0;
+        __syncthreads();
+        const int64_t pa = rs[0], pb = rs[64];
+        for (int64_t r = pa + lane; r < pb; r += 64) {
+            int lo = 0, hi = (int)nv;  // owner: rs[lo] <= r < rs[lo + 1]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (rs[mid] <= r) lo = mid;
+                else hi = mid;
+            }
             const uint8_t f = h.eflags[r];
-            if (hb_in_mesh(s, r, t)) {
-                ++n;
-                neg += s.score[r] < 0;
-                outb += (f & EDGE_OUTBOUND) != 0;
-            } else if ((s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+            const uint8_t pf = s.pflags[r];
+            if ((pf & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH)) {
+                atomicAdd(&cnt[0][lo], 1);
+                if (s.score[r] < 0) atomicAdd(&cnt[1][lo], 1);
+                if (f & EDGE_OUTBOUND) atomicAdd(&cnt[2][lo], 1);
+            } else if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
                        (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && h.backoff[(size_t)t * h.n_pairs + r] == 0 &&
                        s.score[r] >= 0.0) {  // getPeers' filter of the graft steps (:1370-1385, :1450-1476)
-                ++cand;
-                cand_out += (f & EDGE_OUTBOUND) != 0;
+                atomicAdd(&cnt[3][lo], 1);
+                if (f & EDGE_OUTBOUND) atomicAdd(&cnt[4][lo], 1);
             }
         }
-        const bool grow = n < gp.d_lo && cand > 0;                               // :1370-1385
-        const bool outbound = n >= gp.d_lo && outb < gp.d_out && cand_out > 0;  // :1450-1476
-        if (!neg && n <= gp.d_hi && !grow && !outbound && !(og_tick && n > 1)) {
-            h.rngk[v] = 0;
-            continue;
+        __syncthreads();
+        if (lane < nv) {
+            const uint32_t v = v0 + lane;
+            const int n = cnt[0][lane], neg = cnt[1][lane], outb = cnt[2][lane];
+            const int cand = cnt[3][lane], cand_out = cnt[4][lane];
+            const bool grow = n < gp.d_lo && cand > 0;                               // :1370-1385
+            const bool outbound = n >= gp.d_lo && outb < gp.d_out && cand_out > 0;  // :1450-1476
+            if (!neg && n <= gp.d_hi && !grow && !outbound && !(og_tick && n > 1)) {
+                h.rngk[v] = 0;
+            } else {
+                const int64_t r0 = rs[lane];
+                HbUnit U{s, h, t, r0, (int)(rs[lane + 1] - r0)};
+                Rng g = hb_rng(h, v, t, 0);
+                U.maintain(g);
+                h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
+                grafts += U.grafts;
+                prunes += U.prunes;
+            }
         }
-        HbUnit U{s, h, t, r0, deg};
-        Rng g = hb_rng(h, v, t, 0);
-        U.maintain(g);
-        h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
-        grafts += U.grafts;
-        prunes += U.prunes;
+        __syncthreads();  // rs / cnt are rewritten by the next wave-tile
     }
     flush_count(h.stats, HB_GRAFTS, grafts);
     flush_count(h.stats, HB_PRUNES, prunes);
@@ -480,7 +511,13 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         const DevGossipParams& gp = h.gp;
         for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
-            const uint32_t r = h.rev[q];     // r = (v -> u), the sender's pair
+            // unsharded, only pairs whose sender marked them carry control;
+            // what is read is cleared (the next round starts from zeros)
+            if (!h.halo_ctl) {
+                if (!h.inbox[q]) continue;
+                h.inbox[q] = 0;
+            }
+            const uint32_t r = h.rev[q];  // r = (v -> u), the sender's pair
             if (r == NO_PAIR) continue;
             uint64_t grafts, prunes;
             if (r & HALO) {  // v on another shard: its control bits came through the exchange
@@ -489,6 +526,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             } else {
                 grafts = h.ctl_graft[r];
                 prunes = h.ctl_prune[r];
+                if (!h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
             }
             if (!(grafts | prunes)) continue;
             const double score = s.score[q];  // gs.score.Score(p) once per control message
@@ -536,6 +574,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 ++accepted;
             }
             h.resp[q] = resp;
+            if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
             for (; prunes; prunes &= prunes - 1) {  // handlePrune
                 handle_prune(s, h, q, (uint32_t)__builtin_ctzll(prunes));
                 ++handled;
@@ -553,8 +592,13 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
 __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
     uint64_t handled = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {  // r = (v -> u)
+        if (!h.halo_resp) {  // unsharded: only marked pairs have an answer; what is read is cleared
+            if (!h.answer[r]) continue;
+            h.answer[r] = 0;
+        }
         const uint32_t q = h.rev[r];
         uint64_t resp = q == NO_PAIR ? 0 : (q & HALO) ? h.halo_resp[q & ~HALO] : h.resp[q];
+        if (!h.halo_resp && q != NO_PAIR) h.resp[q] = 0;
         // AcceptFrom at v for the answering peer
         if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
         if (resp) h.dirty[r] = 1;
@@ -566,11 +610,22 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
     flush_count(h.stats, HB_PRUNES_HANDLED, handled);
 }
 
+// In-mesh (pair, topic) count: one thread per 16 pairs of a tile, reading
+// their pair flags and, per topic, the tile's 16 record-flag bytes as uint4.
 __global__ __launch_bounds__(256) void k_hb_mesh_links(DevState s, HbState h) {
+    static_assert(TILE % 16 == 0 && REC_IN_MESH == 0x01 && PAIR_PRESENT == 0x01, "byte-lane counting below");
     uint64_t c = 0;
-    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u)
-        if (s.pflags[r] & PAIR_PRESENT)
-            for (uint32_t t = 0; t < s.n_topics; ++t) c += (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH) != 0;
+    const uint64_t n_chunks = (h.n_pairs + 15) / 16;  // pflags / rflags are padded to whole tiles
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n_chunks; k += (uint64_t)gridDim.x * 256u) {
+        const uint64_t p0 = k * 16;
+        const uint4 pf = *reinterpret_cast<const uint4*>(s.pflags + p0);
+        const uint32_t pw[4] = {pf.x & 0x01010101u, pf.y & 0x01010101u, pf.z & 0x01010101u, pf.w & 0x01010101u};
+        if (!(pw[0] | pw[1] | pw[2] | pw[3])) continue;
+        for (uint32_t t = 0; t < s.n_topics; ++t) {
+            const uint4 rf = *reinterpret_cast<const uint4*>(s.rflags + flag_index(p0, t, s.n_topics));
+            c += __popc(rf.x & pw[0]) + __popc(rf.y & pw[1]) + __popc(rf.z & pw[2]) + __popc(rf.w & pw[3]);
+        }
+    }
     flush_count(h.stats, HB_MESH_LINKS, c);
 }
 
@@ -645,7 +700,7 @@ hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint
 
 hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh_links, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    hipLaunchKernelGGL(k_hb_mesh_links, dim3(grid_cap((h.n_pairs + 15) / 16, 256)), dim3(256), 0, st, s, h);
     return hipGetLastError();
 }
 
