@@ -1,0 +1,210 @@
+"""Trace export: engine results as ``pb.TraceEvent`` records.
+
+The reference's tracer builds one ``TraceEvent`` per router action
+(``trace.go:136-164`` DuplicateMessage, ``trace.go:166-194`` DeliverMessage,
+``trace.go:468-520`` Graft / Prune) and ``PBTracer`` writes them to a file as
+varint-length-delimited protobufs (``tracer.go:131-170``), so existing trace
+tooling reads a stream of such records.  This module turns what the engine
+already computes on the GPU into that stream:
+
+* ``mesh_trace``     — GRAFT / PRUNE events from the scorer's inMesh flags
+  before and after a heartbeat (``export_state()['rec_flags']``): one GRAFT
+  per (observer, topic, peer) that entered the mesh, one PRUNE per one that
+  left it.  The engine's rounds are synchronous, so what it reports is the net
+  mesh change of the round; the reference emits the same set (its order within
+  a heartbeat follows Go map iteration and is not observable).
+* ``delivery_trace`` — DELIVER_MESSAGE events from ``prop_results()``: one per
+  (node, message) first receipt, ``receivedFrom`` = the first deliverer, and
+  ``timestamp`` = ``now + hop * hop_latency``.  The publisher itself gets no
+  event (``trace.go:171``: only messages received from another peer).
+
+Field numbers and wire types follow ``pb/trace.proto:5-104``; fields are
+written in field-number order, as the gogo marshaller does.  This is host-side
+formatting of device results (I/O, not the data-parallel path): nothing here
+computes scores or forwarding.
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .abi import GSX_REC_IN_MESH, GSX_VALIDATION_ACCEPT
+
+# TraceEvent.Type (pb/trace.proto:24-38)
+PUBLISH_MESSAGE = 0
+REJECT_MESSAGE = 1
+DUPLICATE_MESSAGE = 2
+DELIVER_MESSAGE = 3
+GRAFT = 11
+PRUNE = 12
+
+# TraceEvent sub-message field numbers (pb/trace.proto:10-22)
+_SUB_FIELD = {DUPLICATE_MESSAGE: 6, DELIVER_MESSAGE: 7, GRAFT: 15, PRUNE: 16}
+
+
+def _varint(n: int) -> bytes:
+    if n < 0:  # int64 / enum: two's complement in ten bytes
+        n &= (1 << 64) - 1
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _len_field(field: int, payload: bytes) -> bytes:
+    return _varint(field << 3 | 2) + _varint(len(payload)) + payload
+
+
+def _varint_field(field: int, v: int) -> bytes:
+    return _varint(field << 3) + _varint(v)
+
+
+def _s(x) -> bytes:
+    return x.encode() if isinstance(x, str) else bytes(x)
+
+
+def encode_event(etype: int, peer_id: bytes, timestamp: int, sub: bytes) -> bytes:
+    """One TraceEvent{type, peerID, timestamp, <sub-message>} (pb/trace.proto:5-22)."""
+    return (
+        _varint_field(1, etype)
+        + _len_field(2, _s(peer_id))
+        + _varint_field(3, timestamp)
+        + _len_field(_SUB_FIELD[etype], sub)
+    )
+
+
+def graft_event(observer: bytes, peer: bytes, topic: str, timestamp: int) -> bytes:
+    """trace.go:468-493: Graft{peerID = p, topic}, emitted by the grafting node."""
+    return encode_event(GRAFT, observer, timestamp, _len_field(1, _s(peer)) + _len_field(2, _s(topic)))
+
+
+def prune_event(observer: bytes, peer: bytes, topic: str, timestamp: int) -> bytes:
+    """trace.go:495-520: Prune{peerID = p, topic}."""
+    return encode_event(PRUNE, observer, timestamp, _len_field(1, _s(peer)) + _len_field(2, _s(topic)))
+
+
+def deliver_event(node: bytes, msg_id: bytes, topic: str, received_from: bytes, timestamp: int) -> bytes:
+    """trace.go:166-194: DeliverMessage{messageID, topic, receivedFrom} (proto :58-62)."""
+    sub = _len_field(1, _s(msg_id)) + _len_field(2, _s(topic)) + _len_field(3, _s(received_from))
+    return encode_event(DELIVER_MESSAGE, node, timestamp, sub)
+
+
+def duplicate_event(node: bytes, msg_id: bytes, received_from: bytes, topic: str, timestamp: int) -> bytes:
+    """trace.go:136-164: DuplicateMessage{messageID, receivedFrom, topic} (proto :52-56)."""
+    sub = _len_field(1, _s(msg_id)) + _len_field(2, _s(received_from)) + _len_field(3, _s(topic))
+    return encode_event(DUPLICATE_MESSAGE, node, timestamp, sub)
+
+
+def write_delimited(events: Iterable[bytes]) -> bytes:
+    """PBTracer's stream (tracer.go:156-167, protoio delimited writer): varint length + record."""
+    return b"".join(_varint(len(e)) + e for e in events)
+
+
+def read_delimited(buf: bytes) -> List[bytes]:
+    """Split a delimited stream back into records; raises ValueError on a truncated record."""
+    out, i = [], 0
+    while i < len(buf):
+        n, shift = 0, 0
+        while True:
+            if i >= len(buf):
+                raise ValueError("truncated length prefix")
+            b = buf[i]
+            i += 1
+            n |= (b & 0x7F) << shift
+            shift += 7
+            if not b & 0x80:
+                break
+        if i + n > len(buf):
+            raise ValueError("truncated record")
+        out.append(bytes(buf[i : i + n]))
+        i += n
+    return out
+
+
+def default_peer_id(node: int) -> bytes:
+    """Simulated nodes carry no libp2p key: their id is 'gsx-' + the node index."""
+    return b"gsx-%d" % node
+
+
+def default_msg_id(source: int, seqno: int) -> bytes:
+    """DefaultMsgIdFn (pubsub.go) is string(from) + string(seqno): source id + 8-byte big-endian seqno."""
+    return default_peer_id(source) + int(seqno).to_bytes(8, "big")
+
+
+def pair_endpoints(row_ptr, col) -> Tuple[np.ndarray, np.ndarray]:
+    """(observer, peer) of every pair of a CSR overlay: pair p is edge p (gsx.h overlay)."""
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    obs = np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int64), np.diff(row_ptr))
+    return obs, np.asarray(col, dtype=np.int64)
+
+
+def mesh_changes(before_flags, after_flags, n_topics: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(topic, pair, grafted) of every record whose inMesh flag changed, in (pair, topic) order.
+
+    Flags are ``rec_flags`` as export_state() returns them: topic-major,
+    element [t * n_pairs + p] (gsx.h state import/export).
+    """
+    b = np.asarray(before_flags, dtype=np.uint8).reshape(n_topics, -1) & GSX_REC_IN_MESH
+    a = np.asarray(after_flags, dtype=np.uint8).reshape(n_topics, -1) & GSX_REC_IN_MESH
+    pair, topic = np.nonzero((a != b).T)
+    return topic, pair, a[topic, pair] != 0
+
+
+def mesh_trace(
+    before_flags,
+    after_flags,
+    row_ptr,
+    col,
+    topics: Sequence[str],
+    timestamp: int,
+    peer_id: Callable[[int], bytes] = default_peer_id,
+) -> Iterator[bytes]:
+    """GRAFT / PRUNE events of one heartbeat, ordered by (observer, peer, topic)."""
+    obs, peer = pair_endpoints(row_ptr, col)
+    topic, pair, grafted = mesh_changes(before_flags, after_flags, len(topics))
+    for t, p, g in zip(topic.tolist(), pair.tolist(), grafted.tolist()):
+        mk = graft_event if g else prune_event
+        yield mk(peer_id(int(obs[p])), peer_id(int(peer[p])), topics[t], timestamp)
+
+
+def delivery_trace(
+    hop,
+    first_from,
+    msgs,
+    topic: str,
+    now: int,
+    hop_latency_ns: int,
+    peer_id: Callable[[int], bytes] = default_peer_id,
+    msg_id: Optional[Callable[[int, int], bytes]] = None,
+    node_base: int = 0,
+) -> Iterator[bytes]:
+    """DELIVER_MESSAGE events of one propagation on ``topic``, ordered by (message, node).
+
+    ``hop`` / ``first_from`` are prop_results() rows ([m, n] arrival hop, 0xFF
+    = never, 0 at the source; first deliverer, global id); ``msgs`` the
+    published records (gsx.h GsxMsg: ``source``, ``validation``,
+    ``msg_id``).  Message ids default to ``default_msg_id(source, msg_id)``.
+    A message validation does not accept is seen but never delivered
+    (validation.go:230-351), so it yields no DELIVER_MESSAGE.  ``node_base``
+    is the shard's first global node id for range-sharded results.
+    """
+    if first_from is None:
+        raise ValueError("delivery_trace needs first-deliverer rows (gsx_prop_set_tracking on)")
+    hop = np.asarray(hop)
+    first_from = np.asarray(first_from)
+    mid = msg_id or default_msg_id
+    for m in range(hop.shape[0]):
+        if int(msgs["validation"][m]) != GSX_VALIDATION_ACCEPT:
+            continue
+        ident = mid(int(msgs["source"][m]), int(msgs["msg_id"][m]))
+        for u in np.nonzero((hop[m] != 0xFF) & (hop[m] != 0))[0].tolist():
+            yield deliver_event(
+                peer_id(node_base + u), ident, topic, peer_id(int(first_from[m, u])),
+                now + int(hop[m, u]) * hop_latency_ns,
+            )

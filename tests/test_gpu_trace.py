@@ -1,0 +1,26 @@
+"""Trace export from GPU results (gsx/trace.py): the GRAFT /
+PRUNE stream of a heartbeat and the DELIVER_MESSAGE stream of a propagation
+are byte-identical to the streams built from the oracle's results."""
+import pytest
+
+import gsx
+import oracle as orc
+import trace_cases as tc
+
+pytestmark = pytest.mark.gpu
+
+
+def test_heartbeat_trace_gpu_equals_oracle(gpu_ok):
+    T = len(tc.TOPICS)
+    g = tc.heartbeat_stream(gsx.Engine(T))
+    w = tc.heartbeat_stream(orc.Oracle(T))
+    assert g[1] == w[1] and g[2] == w[2]
+    assert len(g[0]) > 0 and g[0] == w[0]
+
+
+@pytest.mark.parametrize("invalid", [0.0, 0.3])
+def test_delivery_trace_gpu_equals_oracle(gpu_ok, invalid):
+    T = len(tc.TOPICS)
+    g = tc.delivery_stream(gsx.Engine(T), invalid=invalid)[0]
+    w = tc.delivery_stream(orc.Oracle(T), invalid=invalid)[0]
+    assert len(g) > 0 and g == w

@@ -1,0 +1,133 @@
+"""Trace export (gsx/trace.py).
+
+Wire format: every encoder is checked byte-for-byte against the protobuf
+library's own serializer for a TraceEvent schema built at run time from
+pb/trace.proto's field numbers (stated below), and parsed back by it.
+Content: GRAFT / PRUNE streams from a heartbeat and DELIVER_MESSAGE streams
+from a propagation are checked against the backend's own counters and
+first-deliverer rows (oracle here; GPU == oracle byte-for-byte in
+test_gpu_trace.py)."""
+import numpy as np
+import pytest
+
+import oracle as orc
+import trace_cases as tc
+from gsx import abi
+from gsx import trace as tr
+
+pb = pytest.importorskip("google.protobuf")
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory  # noqa: E402
+
+F = descriptor_pb2.FieldDescriptorProto
+
+
+def _trace_event_class():
+    """TraceEvent with the fields the exporter writes (pb/trace.proto:5-104)."""
+    fd = descriptor_pb2.FileDescriptorProto(name="gsx_trace_test.proto", package="gsxtest", syntax="proto2")
+    ev = fd.message_type.add(name="TraceEvent")
+    en = ev.enum_type.add(name="Type")
+    for name, num in [("PUBLISH_MESSAGE", 0), ("REJECT_MESSAGE", 1), ("DUPLICATE_MESSAGE", 2),
+                      ("DELIVER_MESSAGE", 3), ("GRAFT", 11), ("PRUNE", 12)]:
+        en.value.add(name=name, number=num)
+
+    def sub(name, fields):
+        m = ev.nested_type.add(name=name)
+        for fname, num, typ in fields:
+            m.field.add(name=fname, number=num, type=typ, label=F.LABEL_OPTIONAL)
+
+    B, S = F.TYPE_BYTES, F.TYPE_STRING
+    sub("DuplicateMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("topic", 3, S)])
+    sub("DeliverMessage", [("messageID", 1, B), ("topic", 2, S), ("receivedFrom", 3, B)])
+    sub("Graft", [("peerID", 1, B), ("topic", 2, S)])
+    sub("Prune", [("peerID", 1, B), ("topic", 2, S)])
+    ev.field.add(name="type", number=1, type=F.TYPE_ENUM, type_name=".gsxtest.TraceEvent.Type", label=F.LABEL_OPTIONAL)
+    ev.field.add(name="peerID", number=2, type=B, label=F.LABEL_OPTIONAL)
+    ev.field.add(name="timestamp", number=3, type=F.TYPE_INT64, label=F.LABEL_OPTIONAL)
+    for fname, num, tname in [("duplicateMessage", 6, "DuplicateMessage"), ("deliverMessage", 7, "DeliverMessage"),
+                              ("graft", 15, "Graft"), ("prune", 16, "Prune")]:
+        ev.field.add(name=fname, number=num, type=F.TYPE_MESSAGE, type_name=f".gsxtest.TraceEvent.{tname}",
+                     label=F.LABEL_OPTIONAL)
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    return message_factory.GetMessageClass(pool.FindMessageTypeByName("gsxtest.TraceEvent"))
+
+
+TE = _trace_event_class()
+TS = [0, 1, 1_700_000_000_123_456_789, -5, (1 << 63) - 1]
+
+
+@pytest.mark.parametrize("ts", TS)
+def test_graft_prune_bytes_match_protobuf(ts):
+    for kind, enc, field in [(11, tr.graft_event, "graft"), (12, tr.prune_event, "prune")]:
+        want = TE(type=kind, peerID=b"obs\x00\xff", timestamp=ts)
+        getattr(want, field).peerID = b"peer-7"
+        getattr(want, field).topic = "té"
+        got = enc(b"obs\x00\xff", b"peer-7", "té", ts)
+        assert got == want.SerializeToString(deterministic=True)
+        assert TE.FromString(got) == want
+
+
+@pytest.mark.parametrize("ts", TS)
+def test_deliver_duplicate_bytes_match_protobuf(ts):
+    mid = tr.default_msg_id(12, 300)
+    want = TE(type=3, peerID=b"n1", timestamp=ts)
+    want.deliverMessage.messageID, want.deliverMessage.topic, want.deliverMessage.receivedFrom = mid, "x", b"n2"
+    assert tr.deliver_event(b"n1", mid, "x", b"n2", ts) == want.SerializeToString(deterministic=True)
+    want = TE(type=2, peerID=b"n1", timestamp=ts)
+    want.duplicateMessage.messageID, want.duplicateMessage.receivedFrom, want.duplicateMessage.topic = mid, b"n3", "x"
+    assert tr.duplicate_event(b"n1", mid, b"n3", "x", ts) == want.SerializeToString(deterministic=True)
+
+
+def test_delimited_round_trip_and_truncation():
+    evs = [tr.graft_event(b"a" * k, b"b", "t", k) for k in (0, 1, 200, 5000)]  # 1- and 2-byte prefixes
+    buf = tr.write_delimited(evs)
+    assert tr.read_delimited(buf) == evs
+    assert tr.read_delimited(b"") == []
+    with pytest.raises(ValueError):
+        tr.read_delimited(buf[:-1])
+    with pytest.raises(ValueError):
+        tr.read_delimited(b"\x80")
+
+
+def test_mesh_changes_ordering():
+    # 3 pairs x 2 topics, topic-major flags
+    before = np.array([1, 0, 1, 0, 0, 1], dtype=np.uint8)
+    after = np.array([1, 1, 0, 0, 1, 1], dtype=np.uint8) | np.uint8(0x80)  # other bits ignored
+    t, p, g = tr.mesh_changes(before, after, 2)
+    assert list(zip(p.tolist(), t.tolist(), g.tolist())) == [(1, 0, True), (1, 1, True), (2, 0, False)]
+    row_ptr, col = np.array([0, 2, 3]), np.array([5, 6, 7])
+    ev = [TE.FromString(e) for e in tr.mesh_trace(before, after, row_ptr, col, ["a", "b"], 9)]
+    assert [(e.type, e.peerID, (e.graft if e.type == 11 else e.prune).peerID, e.timestamp) for e in ev] == [
+        (11, b"gsx-0", b"gsx-6", 9), (11, b"gsx-0", b"gsx-6", 9), (12, b"gsx-1", b"gsx-7", 9)]
+    assert [e.graft.topic or e.prune.topic for e in ev] == ["a", "b", "a"]
+
+
+def test_heartbeat_trace_matches_counters():
+    buf, out, links_before = tc.heartbeat_stream(orc.Oracle(len(tc.TOPICS)))
+    ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
+    n_graft = sum(e.type == 11 for e in ev)
+    n_prune = sum(e.type == 12 for e in ev)
+    assert n_graft > 0 and n_prune > 0
+    assert links_before + n_graft - n_prune == out["mesh_links"]
+    assert all(e.HasField("graft") != e.HasField("prune") for e in ev)
+
+
+@pytest.mark.parametrize("invalid", [0.0, 0.3])
+def test_delivery_trace_matches_results(invalid):
+    buf, hop, frm, ms = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid)
+    ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
+    ok = ms["validation"] == abi.GSX_VALIDATION_ACCEPT
+    recv = (hop != 0xFF) & (hop != 0) & ok[:, None]
+    assert len(ev) == int(recv.sum()) > 0
+    m_idx, u_idx = np.nonzero(recv)
+    for e, m, u in zip(ev, m_idx.tolist(), u_idx.tolist()):
+        assert e.type == 3 and e.peerID == tr.default_peer_id(u)
+        assert e.deliverMessage.messageID == tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
+        assert e.deliverMessage.receivedFrom == tr.default_peer_id(int(frm[m, u]))
+        assert e.deliverMessage.topic == tc.TOPICS[1]
+        assert e.timestamp == tc.pc.T0 + 3 * tc.pc.S + int(hop[m, u]) * 10 * abi.MILLISECOND
+
+
+def test_delivery_trace_needs_first_deliverers():
+    with pytest.raises(ValueError):
+        list(tr.delivery_trace(np.zeros((1, 2), np.uint8), None, np.zeros(1, abi.msg_dtype()), "t", 0, 1))
