@@ -1,7 +1,7 @@
 """Trace export: engine results as ``pb.TraceEvent`` records.
 
 The reference's tracer builds one ``TraceEvent`` per router action
-(``trace.go:136-164`` DuplicateMessage, ``trace.go:166-194`` DeliverMessage,
+(``trace.go:105-134`` RejectMessage, ``trace.go:136-164`` DuplicateMessage, ``trace.go:166-194`` DeliverMessage,
 ``trace.go:468-520`` Graft / Prune) and ``PBTracer`` writes them to a file as
 varint-length-delimited protobufs (``tracer.go:131-170``), so existing trace
 tooling reads a stream of such records.  This module turns what the engine
@@ -13,9 +13,9 @@ already computes on the GPU into that stream:
   left it.  The engine's rounds are synchronous, so what it reports is the net
   mesh change of the round; the reference emits the same set (its order within
   a heartbeat follows Go map iteration and is not observable).
-* ``delivery_trace`` — DELIVER_MESSAGE events from ``prop_results()``: one per
-  (node, message) first receipt, ``receivedFrom`` = the first deliverer, and
-  ``timestamp`` = ``now + hop * hop_latency``.  The publisher itself gets no
+* ``delivery_trace`` — DELIVER_MESSAGE (or, for a message validation does not
+  accept, REJECT_MESSAGE with its reason) events from ``prop_results()``: one
+  per (node, message) first receipt, ``receivedFrom`` = the first deliverer.  The publisher itself gets no
   event (``trace.go:171``: only messages received from another peer).
 
 Field numbers and wire types follow ``pb/trace.proto:5-104``; fields are
@@ -29,7 +29,13 @@ from typing import Callable, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .abi import GSX_REC_IN_MESH, GSX_VALIDATION_ACCEPT
+from .abi import (
+    GSX_REC_IN_MESH,
+    GSX_VALIDATION_ACCEPT,
+    GSX_VALIDATION_IGNORE,
+    GSX_VALIDATION_REJECT,
+    GSX_VALIDATION_THROTTLE,
+)
 
 # TraceEvent.Type (pb/trace.proto:24-38)
 PUBLISH_MESSAGE = 0
@@ -40,7 +46,14 @@ GRAFT = 11
 PRUNE = 12
 
 # TraceEvent sub-message field numbers (pb/trace.proto:10-22)
-_SUB_FIELD = {DUPLICATE_MESSAGE: 6, DELIVER_MESSAGE: 7, GRAFT: 15, PRUNE: 16}
+_SUB_FIELD = {REJECT_MESSAGE: 5, DUPLICATE_MESSAGE: 6, DELIVER_MESSAGE: 7, GRAFT: 15, PRUNE: 16}
+
+# RejectMessage reasons of the validation outcomes (tracer.go:26-38, validation.go:320-383)
+REJECT_REASON = {
+    GSX_VALIDATION_REJECT: "validation failed",
+    GSX_VALIDATION_IGNORE: "validation ignored",
+    GSX_VALIDATION_THROTTLE: "validation throttled",
+}
 
 
 def _varint(n: int) -> bytes:
@@ -93,6 +106,13 @@ def deliver_event(node: bytes, msg_id: bytes, topic: str, received_from: bytes, 
     """trace.go:166-194: DeliverMessage{messageID, topic, receivedFrom} (proto :58-62)."""
     sub = _len_field(1, _s(msg_id)) + _len_field(2, _s(topic)) + _len_field(3, _s(received_from))
     return encode_event(DELIVER_MESSAGE, node, timestamp, sub)
+
+
+def reject_event(node: bytes, msg_id: bytes, received_from: bytes, reason: str, topic: str, timestamp: int) -> bytes:
+    """trace.go:105-134: RejectMessage{messageID, receivedFrom, reason, topic} (proto :45-50)."""
+    sub = (_len_field(1, _s(msg_id)) + _len_field(2, _s(received_from)) + _len_field(3, _s(reason))
+           + _len_field(4, _s(topic)))
+    return encode_event(REJECT_MESSAGE, node, timestamp, sub)
 
 
 def duplicate_event(node: bytes, msg_id: bytes, received_from: bytes, topic: str, timestamp: int) -> bytes:
@@ -183,28 +203,34 @@ def delivery_trace(
     peer_id: Callable[[int], bytes] = default_peer_id,
     msg_id: Optional[Callable[[int, int], bytes]] = None,
     node_base: int = 0,
+    validation_delay_ns: int = 0,
 ) -> Iterator[bytes]:
-    """DELIVER_MESSAGE events of one propagation on ``topic``, ordered by (message, node).
+    """DELIVER_MESSAGE / REJECT_MESSAGE events of one propagation on ``topic``,
+    ordered by (message, node).
 
     ``hop`` / ``first_from`` are prop_results() rows ([m, n] arrival hop, 0xFF
     = never, 0 at the source; first deliverer, global id); ``msgs`` the
     published records (gsx.h GsxMsg: ``source``, ``validation``,
     ``msg_id``).  Message ids default to ``default_msg_id(source, msg_id)``.
-    A message validation does not accept is seen but never delivered
-    (validation.go:230-351), so it yields no DELIVER_MESSAGE.  ``node_base``
-    is the shard's first global node id for range-sharded results.
+    Every first receipt is validated: an accepted message yields
+    DELIVER_MESSAGE, one that is not yields REJECT_MESSAGE with its reason
+    (validation.go:320-383; it is seen but never delivered or forwarded).  The
+    event time is the end of validation: ``now + hop * (hop_latency +
+    validation_delay)``.  ``node_base`` is the shard's first global node id
+    for range-sharded results.
     """
     if first_from is None:
         raise ValueError("delivery_trace needs first-deliverer rows (gsx_prop_set_tracking on)")
     hop = np.asarray(hop)
     first_from = np.asarray(first_from)
     mid = msg_id or default_msg_id
+    step = hop_latency_ns + validation_delay_ns
     for m in range(hop.shape[0]):
-        if int(msgs["validation"][m]) != GSX_VALIDATION_ACCEPT:
-            continue
+        v = int(msgs["validation"][m])
         ident = mid(int(msgs["source"][m]), int(msgs["msg_id"][m]))
         for u in np.nonzero((hop[m] != 0xFF) & (hop[m] != 0))[0].tolist():
-            yield deliver_event(
-                peer_id(node_base + u), ident, topic, peer_id(int(first_from[m, u])),
-                now + int(hop[m, u]) * hop_latency_ns,
-            )
+            node, frm, ts = peer_id(node_base + u), peer_id(int(first_from[m, u])), now + int(hop[m, u]) * step
+            if v == GSX_VALIDATION_ACCEPT:
+                yield deliver_event(node, ident, topic, frm, ts)
+            else:
+                yield reject_event(node, ident, frm, REJECT_REASON[v], topic, ts)

@@ -1,5 +1,5 @@
 """Trace export from GPU results (gsx/trace.py): the GRAFT /
-PRUNE stream of a heartbeat and the DELIVER_MESSAGE stream of a propagation
+PRUNE stream of a heartbeat and the DELIVER_MESSAGE / REJECT_MESSAGE stream of a propagation
 are byte-identical to the streams built from the oracle's results."""
 import pytest
 
@@ -18,9 +18,9 @@ def test_heartbeat_trace_gpu_equals_oracle(gpu_ok):
     assert len(g[0]) > 0 and g[0] == w[0]
 
 
-@pytest.mark.parametrize("invalid", [0.0, 0.3])
-def test_delivery_trace_gpu_equals_oracle(gpu_ok, invalid):
+@pytest.mark.parametrize("invalid,delay_ms", [(0.0, 0.0), (0.3, 0.0), (0.3, 4.0)])
+def test_delivery_trace_gpu_equals_oracle(gpu_ok, invalid, delay_ms):
     T = len(tc.TOPICS)
-    g = tc.delivery_stream(gsx.Engine(T), invalid=invalid)[0]
-    w = tc.delivery_stream(orc.Oracle(T), invalid=invalid)[0]
+    g = tc.delivery_stream(gsx.Engine(T), invalid=invalid, delay_ms=delay_ms)[0]
+    w = tc.delivery_stream(orc.Oracle(T), invalid=invalid, delay_ms=delay_ms)[0]
     assert len(g) > 0 and g == w

@@ -3,8 +3,8 @@
 Wire format: every encoder is checked byte-for-byte against the protobuf
 library's own serializer for a TraceEvent schema built at run time from
 pb/trace.proto's field numbers (stated below), and parsed back by it.
-Content: GRAFT / PRUNE streams from a heartbeat and DELIVER_MESSAGE streams
-from a propagation are checked against the backend's own counters and
+Content: GRAFT / PRUNE streams from a heartbeat and DELIVER_MESSAGE /
+REJECT_MESSAGE streams from a propagation are checked against the backend's own counters and
 first-deliverer rows (oracle here; GPU == oracle byte-for-byte in
 test_gpu_trace.py)."""
 import numpy as np
@@ -36,6 +36,7 @@ def _trace_event_class():
             m.field.add(name=fname, number=num, type=typ, label=F.LABEL_OPTIONAL)
 
     B, S = F.TYPE_BYTES, F.TYPE_STRING
+    sub("RejectMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("reason", 3, S), ("topic", 4, S)])
     sub("DuplicateMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("topic", 3, S)])
     sub("DeliverMessage", [("messageID", 1, B), ("topic", 2, S), ("receivedFrom", 3, B)])
     sub("Graft", [("peerID", 1, B), ("topic", 2, S)])
@@ -43,7 +44,7 @@ def _trace_event_class():
     ev.field.add(name="type", number=1, type=F.TYPE_ENUM, type_name=".gsxtest.TraceEvent.Type", label=F.LABEL_OPTIONAL)
     ev.field.add(name="peerID", number=2, type=B, label=F.LABEL_OPTIONAL)
     ev.field.add(name="timestamp", number=3, type=F.TYPE_INT64, label=F.LABEL_OPTIONAL)
-    for fname, num, tname in [("duplicateMessage", 6, "DuplicateMessage"), ("deliverMessage", 7, "DeliverMessage"),
+    for fname, num, tname in [("rejectMessage", 5, "RejectMessage"), ("duplicateMessage", 6, "DuplicateMessage"), ("deliverMessage", 7, "DeliverMessage"),
                               ("graft", 15, "Graft"), ("prune", 16, "Prune")]:
         ev.field.add(name=fname, number=num, type=F.TYPE_MESSAGE, type_name=f".gsxtest.TraceEvent.{tname}",
                      label=F.LABEL_OPTIONAL)
@@ -76,6 +77,10 @@ def test_deliver_duplicate_bytes_match_protobuf(ts):
     want = TE(type=2, peerID=b"n1", timestamp=ts)
     want.duplicateMessage.messageID, want.duplicateMessage.receivedFrom, want.duplicateMessage.topic = mid, b"n3", "x"
     assert tr.duplicate_event(b"n1", mid, b"n3", "x", ts) == want.SerializeToString(deterministic=True)
+    want = TE(type=1, peerID=b"n1", timestamp=ts)
+    r = want.rejectMessage
+    r.messageID, r.receivedFrom, r.reason, r.topic = mid, b"n4", "validation failed", "x"
+    assert tr.reject_event(b"n1", mid, b"n4", "validation failed", "x", ts) == want.SerializeToString(deterministic=True)
 
 
 def test_delimited_round_trip_and_truncation():
@@ -112,20 +117,29 @@ def test_heartbeat_trace_matches_counters():
     assert all(e.HasField("graft") != e.HasField("prune") for e in ev)
 
 
-@pytest.mark.parametrize("invalid", [0.0, 0.3])
-def test_delivery_trace_matches_results(invalid):
-    buf, hop, frm, ms = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid)
+@pytest.mark.parametrize("invalid,delay_ms", [(0.0, 0.0), (0.3, 0.0), (0.3, 4.0)])
+def test_delivery_trace_matches_results(invalid, delay_ms):
+    buf, hop, frm, ms = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid, delay_ms=delay_ms)
     ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
-    ok = ms["validation"] == abi.GSX_VALIDATION_ACCEPT
-    recv = (hop != 0xFF) & (hop != 0) & ok[:, None]
+    recv = (hop != 0xFF) & (hop != 0)
     assert len(ev) == int(recv.sum()) > 0
     m_idx, u_idx = np.nonzero(recv)
+    n_rej = 0
     for e, m, u in zip(ev, m_idx.tolist(), u_idx.tolist()):
-        assert e.type == 3 and e.peerID == tr.default_peer_id(u)
-        assert e.deliverMessage.messageID == tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
-        assert e.deliverMessage.receivedFrom == tr.default_peer_id(int(frm[m, u]))
-        assert e.deliverMessage.topic == tc.TOPICS[1]
-        assert e.timestamp == tc.pc.T0 + 3 * tc.pc.S + int(hop[m, u]) * 10 * abi.MILLISECOND
+        v = int(ms["validation"][m])
+        mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
+        assert e.peerID == tr.default_peer_id(u)
+        assert e.timestamp == tc.pc.T0 + 3 * tc.pc.S + int(hop[m, u]) * int((10 + delay_ms) * abi.MILLISECOND)
+        if v == abi.GSX_VALIDATION_ACCEPT:
+            d = e.deliverMessage
+            assert e.type == 3 and not e.HasField("rejectMessage")
+        else:  # not accepted: seen one hop from its source, rejected with the reason
+            d = e.rejectMessage
+            assert e.type == 1 and d.reason == tr.REJECT_REASON[v] and hop[m, u] == 1
+            n_rej += 1
+        assert d.messageID == mid and d.receivedFrom == tr.default_peer_id(int(frm[m, u]))
+        assert d.topic == tc.TOPICS[1]
+    assert (n_rej > 0) == (invalid > 0)
 
 
 def test_delivery_trace_needs_first_deliverers():

@@ -23,13 +23,14 @@ def heartbeat_stream(be, n=400, d=6, seed=11):
     return tr.write_delimited(ev), out, links_before
 
 
-def delivery_stream(be, n=500, m=40, seed=7, invalid=0.0):
+def delivery_stream(be, n=500, m=40, seed=7, invalid=0.0, delay_ms=0.0):
     """One gossipsub propagation with first-deliverer rows: (stream, hop, first_from, msgs)."""
     T = len(TOPICS)
     ov = pc.overlay(n, 6, seed)
     pc.setup(be, ov, T, seed)
     ms = pc.messages(n, m, seed, invalid=invalid)
-    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=1, latency_ms=10)
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=1, latency_ms=10, delay_ms=delay_ms)
     _, hop, frm = be.propagate(ms, cfg, want_results=True)
-    ev = tr.delivery_trace(hop, frm, ms, TOPICS[1], int(cfg.now_ns), int(cfg.hop_latency_ns))
+    ev = tr.delivery_trace(hop, frm, ms, TOPICS[1], int(cfg.now_ns), int(cfg.hop_latency_ns),
+                          validation_delay_ns=int(cfg.validation_delay_ns))
     return tr.write_delimited(ev), hop, frm, ms
