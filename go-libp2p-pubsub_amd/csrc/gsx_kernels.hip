@@ -17,12 +17,6 @@ namespace gsx {
 
 // ---- hot path: fused refresh + score ---------------------------------------
 
-template <int TT>
-__device__ __forceinline__ const DevTopicParams& topic_params(const KernParams& kp, const DevState& s, int t) {
-    if constexpr (TT > 0) return kp.tp[t];
-    else return s.tp[t];
-}
-
 template <int TT, bool REFRESH>
 __global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp, int64_t now,
                                                        const uint8_t* __restrict__ only) {
@@ -44,16 +38,11 @@ __global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp
     double* const tile = s.rec + (p / TILE) * (uint64_t)T * (NFIELD * TILE) + lane;
     uint8_t* const ftile = s.rflags + (p / TILE) * (uint64_t)T * TILE + lane;
     double score = 0.0;
-    for (int t = 0; t < T; ++t) {  // constant trip count for TT > 0: fully unrolled
-        const DevTopicParams& tp = topic_params<TT>(kp, s, t);
-        if (!tp.scored) continue;
+    // One topic's refresh (decay, write-back of changed counters, meshTime /
+    // activation) and score term, from its already-loaded record.
+    auto topic_step = [&](int t, const DevTopicParams& tp, double fmd, double mmd, double mfp, double imd,
+                          int64_t graft, uint8_t fl) {
         double* const r = tile + (uint64_t)t * (NFIELD * TILE);
-        // streamed once per pass: non-temporal loads/stores (measured +4 %, tools/microbench)
-        double fmd = __builtin_nontemporal_load(r + FMD * TILE);
-        double mmd = __builtin_nontemporal_load(r + MMD * TILE);
-        double mfp = __builtin_nontemporal_load(r + MFP * TILE);
-        double imd = __builtin_nontemporal_load(r + IMD * TILE);
-        uint8_t fl = ftile[t * TILE];
         int64_t mt = 0;
         if (conn) {
             // a counter that decays stays written back only if it changed: a
@@ -71,15 +60,56 @@ __global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp
             if (__double_as_longlong(imd) != __double_as_longlong(imd0)) __builtin_nontemporal_store(imd, r + IMD * TILE);
             uint8_t nf = fl & ~REC_FRESH;
             if (fl & REC_IN_MESH) {  // :544-549
-                mt = now - __builtin_nontemporal_load(reinterpret_cast<const int64_t*>(r) + GRAFT * TILE);
+                mt = now - graft;
                 if (mt > tp.act3) nf |= REC_ACTIVE;
             }
             if (nf != fl) ftile[t * TILE] = nf;  // rare once the mesh is steady
             fl = nf;
         } else if ((fl & REC_IN_MESH) && !(fl & REC_FRESH)) {
-            mt = s.last_refresh - reinterpret_cast<const int64_t*>(r)[GRAFT * TILE];
+            mt = s.last_refresh - graft;
         }
         score += topic_score(tp, fl, mt, fmd, mmd, mfp, imd);
+    };
+    // streamed once per pass: non-temporal loads/stores (measured +4 %, tools/microbench)
+    if constexpr (TT > 0) {
+        // Every scored topic's record is loaded before any is used, so a wave
+        // has all T x 5 loads (T x 2.5 KB) in flight at once instead of one
+        // topic's at a time.  graftTime is loaded whether or not the record
+        // is in the mesh (T > 1): some lane of the wave nearly always is, so
+        // its line is fetched anyway, and the load no longer waits on the flag.
+        double fmd[TT], mmd[TT], mfp[TT], imd[TT];
+        int64_t gr[TT];
+        uint8_t fl[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            if (!kp.tp[t].scored) continue;
+            const double* const r = tile + (uint64_t)t * (NFIELD * TILE);
+            fmd[t] = __builtin_nontemporal_load(r + FMD * TILE);
+            mmd[t] = __builtin_nontemporal_load(r + MMD * TILE);
+            mfp[t] = __builtin_nontemporal_load(r + MFP * TILE);
+            imd[t] = __builtin_nontemporal_load(r + IMD * TILE);
+            fl[t] = ftile[t * TILE];
+            // with one topic there is nothing to overlap the flag load with,
+            // and skipping graftTime outside the mesh saves its line (cfg5)
+            gr[t] = (TT > 1 || (fl[t] & REC_IN_MESH))
+                        ? __builtin_nontemporal_load(reinterpret_cast<const int64_t*>(r) + GRAFT * TILE)
+                        : 0;
+        }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            if (!kp.tp[t].scored) continue;
+            topic_step(t, kp.tp[t], fmd[t], mmd[t], mfp[t], imd[t], gr[t], fl[t]);
+        }
+    } else {
+        for (int t = 0; t < T; ++t) {
+            const DevTopicParams& tp = s.tp[t];
+            if (!tp.scored) continue;
+            const double* const r = tile + (uint64_t)t * (NFIELD * TILE);
+            const uint8_t fl = ftile[t * TILE];
+            const int64_t graft = (fl & REC_IN_MESH) ? reinterpret_cast<const int64_t*>(r)[GRAFT * TILE] : 0;
+            topic_step(t, tp, __builtin_nontemporal_load(r + FMD * TILE), __builtin_nontemporal_load(r + MMD * TILE),
+                       __builtin_nontemporal_load(r + MFP * TILE), __builtin_nontemporal_load(r + IMD * TILE), graft, fl);
+        }
     }
     double bp = s.bp[p];
     if (conn) {
