@@ -117,6 +117,11 @@ constexpr uint32_t NO_PAIR = 0xFFFFFFFFu;
 constexpr uint8_t FWD_FORWARD = 0x01;    // v sends messages it received to u
 constexpr uint8_t FWD_PUBLISH = 0x02;    // v sends messages it published to u
 constexpr uint8_t FWD_RSUB_CAND = 0x04;  // u is one of v's RandomSub peers (drawn per message)
+constexpr uint8_t FWD_SEND = 0x07;       // any of the above: v sends something to u
+// Not about sending: the pair's observer drops every RPC from the pair's
+// neighbour (gossipsub AcceptFrom: score < GraylistThreshold and not a direct
+// peer, gossipsub.go:583-594, pubsub.go:1014-1017), this call.
+constexpr uint8_t FWD_GIN = 0x08;
 constexpr int RANDOMSUB_D = 6;           // randomsub.go:16-18
 constexpr int RSUB_MAX_DEG = 256;
 constexpr int MAX_HOPS = 64;
@@ -132,13 +137,19 @@ enum {
     STAT_BACKSENDS,
     STAT_REJECTED,  // receipts of REJECT messages
     STAT_IGNORED,   // receipts of IGNORE / THROTTLE messages
+    STAT_GRAY,      // copies the receiver's AcceptFrom dropped (graylisted sender), counted apart from STAT_DUPS
     STAT_WORDS
 };
 // rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
 constexpr uint32_t HALO = 0x80000000u;
+constexpr uint32_t HALO_GRAY = 0x40000000u;  // pin of a remote pair whose copies u's AcceptFrom drops
+constexpr uint32_t HALO_SLOT = 0x3FFFFFFFu;  // receive slots < 2^30
 constexpr int PIN_FWD_SHIFT = 29;
 constexpr uint32_t MAX_RANKS = 64;  // ranks of a shard plan (one node: 8)
-constexpr uint32_t PIN_NODE_MASK = (1u << PIN_FWD_SHIFT) - 1;  // nodes per shard < 2^29
+// pin of a local pair: bit 28 = v drops what u sends it (graylisted u), so the
+// back-sends the `from` exclusion removes were never counted as duplicates
+constexpr uint32_t PIN_RDROP = 1u << 28;
+constexpr uint32_t PIN_NODE_MASK = PIN_RDROP - 1;  // nodes per shard < 2^28
 
 struct DevMsg {
     uint32_t source;      // global node id
@@ -155,7 +166,7 @@ struct PropState {
     const uint32_t* pair_obs;  // per pair: local observer index
     const uint8_t* eflags;
     uint8_t* fwd;              // per pair r = (v -> u), this call: FWD_* (v sends to u)
-    uint32_t* pin;             // per pair q = (u -> v), this call: NO_PAIR | HALO|slot | fwd<<29 | v_local
+    uint32_t* pin;             // per pair q = (u -> v), this call: NO_PAIR | HALO[|HALO_GRAY]|slot | fwd<<29 [| RDROP] | v_local
     uint32_t* corr;            // per pair (u -> v), this call: in-window back-sends v will not make
     const DevMsg* msgs;
     uint64_t* seen;            // [node][word]
@@ -193,6 +204,9 @@ struct PropState {
     uint64_t* dseen;                    // [node][word]: hop-1 receipts of dropped messages (after the call)
     uint64_t* occ;                      // [hop][node / 64] bit per node: frontier row non-empty
     double publish_threshold;
+    double graylist_threshold;          // AcceptFrom's gate (gossipsub only: ps.gate)
+    uint32_t gate;                      // gossipsub: receivers drop copies from graylisted senders (FWD_GIN)
+    unsigned long long* gray_pairs;     // pairs with FWD_GIN (counted by k_prop_fwd, kept with fwd)
     int64_t hop_latency, window;
     uint64_t seed;
     uint32_t* hop_flag;  // host-mapped, [hop]: k_prop_mark(h) stores (hop_seq << 1) | (hop h-1 delivered); null: off
@@ -212,7 +226,9 @@ hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
 hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st);
-hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, hipStream_t st);
+// gray_only: count the sends on pairs whose receiver graylists the sender
+// (STAT_GRAY) and nothing else (per-hop accounting); else the late accounting.
+hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, bool gray_only, hipStream_t st);
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);

@@ -143,6 +143,7 @@ struct gsx_engine {
         size_t from_words = 0;      // allocation of `from` (tracked first deliverers)
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
+        unsigned long long* gray_pairs = nullptr;  // pairs with FWD_GIN of the current fwd (k_prop_fwd)
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
         size_t seen_words = 0;
         gsx::PropState last{};
@@ -170,7 +171,7 @@ struct gsx_engine {
             bool valid = false;
             uint32_t router = 0, topic = 0, flood_publish = 0;
             uint64_t flag_gen = 0, score_gen = 0;
-            double publish_threshold = 0;
+            double publish_threshold = 0, graylist_threshold = 0;
         } fwd_key;
         // compacted shard exchange: the dense halo the received entries are
         // scattered into, the slots filled last hop, per-destination counts
@@ -367,7 +368,7 @@ void free_state(gsx_engine* e) {
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
                   e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
-                  e->prop.touch, e->prop.vcnt, e->d_halo_node};
+                  e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
@@ -932,6 +933,7 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     }
     std::vector<uint64_t> base(n_ranks + 1, 0);
     for (uint32_t k = 0; k < n_ranks; ++k) base[k + 1] = base[k] + cnt[k];
+    if (base[n_ranks] > gsx::HALO_SLOT) return fail(e, GSX_ERANGE, "too many cross-shard pairs (2^30 receive slots)");
     std::vector<uint64_t> fill(base.begin(), base.end() - 1);
     std::vector<uint32_t> hnode(base[n_ranks]);
     for (uint64_t q = 0; q < e->E; ++q) {
@@ -1447,6 +1449,11 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.pending = (P.credit_pending || !ps.late || e->sharded() || cfg->credit_scores == GSX_CREDIT_DEFER) ? 1 : 0;
     ps.rsub_sqrt = (uint32_t)std::ceil(std::sqrt((double)cfg->randomsub_size));
     ps.publish_threshold = e->th.publish_threshold;
+    // AcceptFrom (gossipsub.go:583-594): only gossipsub graylists; floodsub and
+    // RandomSub accept every RPC (their AcceptFrom returns AcceptAll)
+    ps.gate = cfg->router == GSX_ROUTER_GOSSIPSUB ? 1 : 0;
+    ps.graylist_threshold = e->th.graylist_threshold;
+    ps.gray_pairs = P.gray_pairs;
     ps.seed = cfg->seed;
     ps.sharded = e->sharded() ? 1 : 0;
     return ps;
@@ -1475,16 +1482,17 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return fail(e, GSX_EINVAL, "bad message validation outcome");
     }
     if (cfg->validation_delay_ns < 0) return fail(e, GSX_EINVAL, "negative validation delay");
-    if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^29 nodes per engine");
+    if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^28 nodes per engine");
     if (cfg->router == GSX_ROUTER_RANDOMSUB && e->max_deg > (int64_t)gsx::RSUB_MAX_DEG)
         return fail(e, GSX_ERANGE, "RandomSub draws support at most " + std::to_string(gsx::RSUB_MAX_DEG) + " peers per node");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)
         return fail(e, GSX_ESTATE, "deferred credits of another topic are pending: gsx_prop_fold_credits first");
-    // publishThreshold tests read current scores; gossipsub reads them only for
-    // floodsub peers and flood publishing (k_prop_fwd), the other routers never
-    const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB && (cfg->flood_publish || e->floodsub_peers);
+    // gossipsub reads current scores (AcceptFrom's graylist gate on every pair,
+    // publishThreshold for floodsub peers and flood publishing: k_prop_fwd);
+    // the other routers never
+    const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB;
     if (int rc = need_score ? ensure_scores(e) : flush(e)) return rc;  // queued events land first either way
     const uint32_t W = prop_words(m);
     const size_t N = e->n_nodes, E = e->E;
@@ -1505,7 +1513,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         if (!P.fwd) {
             if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.pin, E)) || (rc = dalloc(e, &P.dup, E)) ||
                 (rc = dalloc(e, &P.corr, E)) || (rc = dalloc(e, &P.fcnt, E)) || (rc = dalloc(e, &P.flast, E)) ||
-                (rc = dalloc(e, &P.first, E)) || (rc = dalloc(e, &P.inv, E)))
+                (rc = dalloc(e, &P.first, E)) || (rc = dalloc(e, &P.inv, E)) || (rc = dalloc(e, &P.gray_pairs, 1)))
                 return rc;
             HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * std::max<size_t>(E, 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -1616,8 +1624,10 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     auto& K = P.fwd_key;
     const bool fwd_same = K.valid && !e->sharded() && K.router == cfg->router && K.topic == cfg->topic &&
                           K.flood_publish == cfg->flood_publish && K.flag_gen == e->flag_gen &&
-                          K.publish_threshold == e->th.publish_threshold && (!need_score || K.score_gen == e->score_gen);
+                          K.publish_threshold == e->th.publish_threshold &&
+                          K.graylist_threshold == e->th.graylist_threshold && (!need_score || K.score_gen == e->score_gen);
     if (!fwd_same) {
+        HIPCHK(e, hipMemsetAsync(P.gray_pairs, 0, 8, e->stream));
         HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
         K.valid = true;
         K.router = cfg->router;
@@ -1626,6 +1636,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         K.flag_gen = e->flag_gen;
         K.score_gen = e->score_gen;
         K.publish_threshold = e->th.publish_threshold;
+        K.graylist_threshold = e->th.graylist_threshold;
     }
     HIPCHK(e, gsx::launch_prop_init(ps, P.hist, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));  // `hm` is on the host stack
@@ -1699,7 +1710,11 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     std::memset(out, 0, sizeof(*out));
     P.active = false;
     if (ps.n_msgs == 0) return GSX_OK;
-    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, e->stream));
+    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, false, e->stream));
+    // per-hop accounting counts duplicates on arrival; the copies graylisting
+    // receivers drop from local senders are counted here (the kernels return at
+    // once when no pair is gated)
+    else if (ps.gate) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, true, e->stream));
     const bool fold_now = ps.credit && P.cfg.credit_scores != GSX_CREDIT_DEFER;
     if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, dev_state(e), fold_now, e->stream));
     if (ps.credit) {
@@ -1737,7 +1752,8 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     }
     out->rejected = st[gsx::STAT_REJECTED];
     out->ignored = st[gsx::STAT_IGNORED];
-    out->transmissions = out->deliveries + out->duplicates + out->rejected + out->ignored;
+    out->graylisted = st[gsx::STAT_GRAY];
+    out->transmissions = out->deliveries + out->duplicates + out->rejected + out->ignored + out->graylisted;
     P.rows_valid = P.h + 1;
     for (uint32_t h = 1; h <= P.h && !ps.sharded; ++h)
         if (st[gsx::STAT_HOP0 + h] == 0) {  // hop h ran and wrote an empty row; later hops were skipped

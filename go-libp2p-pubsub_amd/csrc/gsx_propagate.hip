@@ -33,31 +33,45 @@
 
 namespace gsx {
 
-// Eligibility of every pair (v -> u) for this call (topic, router, scores).
+// Eligibility of every pair (v -> u) for this call (topic, router, scores),
+// and FWD_GIN: gossipsub's AcceptFrom at the pair's observer drops every RPC
+// of the pair's neighbour (score < GraylistThreshold, not a direct peer;
+// gossipsub.go:583-594 -> pubsub.go:1014-1017: the payload is never pushed,
+// so no seen mark, no trace, no P2/P3/P4).  Floodsub and RandomSub accept all.
+// The score is the one of the call start, like the publishThreshold tests.
 __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (r >= s.n_pairs) return;
-    const uint8_t pf = s.pflags[r];
-    uint8_t out = 0;
-    if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED)) {  // in ps.topics[topic]
+    unsigned long long n_gray[1] = {0};
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < s.n_pairs; r += (uint64_t)gridDim.x * 256u) {
+        const uint8_t pf = s.pflags[r];
         const uint8_t ef = ps.eflags[r];
-        if (ps.router == ROUTER_FLOODSUB) {  // every topic peer (floodsub.go:81-90)
-            out = FWD_FORWARD | FWD_PUBLISH;
-        } else if (ps.router == ROUTER_RANDOMSUB) {  // FloodSub peers always, the rest by draw (randomsub.go:112-143)
-            out = (ef & EDGE_FLOODSUB) ? (FWD_FORWARD | FWD_PUBLISH) : FWD_RSUB_CAND;
-        } else {  // gossipsub
-            const bool direct = ef & EDGE_DIRECT;
-            // the score is read only where a threshold decides (floodsub peers, flood publish)
-            const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
-            const bool above = need_score && s.score[r] >= ps.publish_threshold;
-            bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
-            if (!fwd && ps.topic < s.n_topics)                       // mesh peers (:977-999)
-                fwd = s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH;
-            const bool pub = ps.flood_publish ? (direct || above) : fwd;  // flood publish (:953-960)
-            out = (fwd ? FWD_FORWARD : 0) | (pub ? FWD_PUBLISH : 0);
+        uint8_t out = 0;
+        if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED)) {  // in ps.topics[topic]
+            if (ps.router == ROUTER_FLOODSUB) {  // every topic peer (floodsub.go:81-90)
+                out = FWD_FORWARD | FWD_PUBLISH;
+            } else if (ps.router == ROUTER_RANDOMSUB) {  // FloodSub peers always, the rest by draw (randomsub.go:112-143)
+                out = (ef & EDGE_FLOODSUB) ? (FWD_FORWARD | FWD_PUBLISH) : FWD_RSUB_CAND;
+            } else {  // gossipsub
+                const bool direct = ef & EDGE_DIRECT;
+                // the score is read only where a threshold decides (floodsub peers, flood publish)
+                const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
+                const bool above = need_score && s.score[r] >= ps.publish_threshold;
+                bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
+                if (!fwd && ps.topic < s.n_topics)                       // mesh peers (:977-999)
+                    fwd = s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH;
+                const bool pub = ps.flood_publish ? (direct || above) : fwd;  // flood publish (:953-960)
+                out = (fwd ? FWD_FORWARD : 0) | (pub ? FWD_PUBLISH : 0);
+            }
         }
+        // Score() of a peer without peerStats is 0 (score.go:247-256), never below the
+        // (non-positive) threshold; the score vector holds 0 for those pairs.
+        if (ps.gate && !(ef & EDGE_DIRECT) && s.score[r] < ps.graylist_threshold) {
+            out |= FWD_GIN;
+            ++n_gray[0];
+        }
+        ps.fwd[r] = out;
     }
-    ps.fwd[r] = out;
+    const uint32_t slot[1] = {0};
+    block_count<1>(n_gray, ps.gray_pairs, slot);
 }
 
 // pin[q], per call, for the receiver's pair q = (u -> v): what the hop
@@ -71,13 +85,18 @@ __global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= ps.n_pairs) return;
     const uint32_t r = ps.rev[q];
+    const bool gin = ps.fwd[q] & FWD_GIN;  // u drops whatever v sends (AcceptFrom)
     uint32_t out = NO_PAIR;
     if (r != NO_PAIR) {
         if (r & HALO) {
-            out = r;
-        } else {
+            // remote v: its rank packs what it sends either way; u counts the
+            // copies it drops (k_prop_hop)
+            out = gin ? (r | HALO_GRAY) : r;
+        } else if (!gin) {
             const uint8_t fw = ps.fwd[r];
-            if (fw) out = ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | ((uint32_t)ps.col[q] - ps.node_lo);
+            if (fw & FWD_SEND)
+                out = ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | ((fw & FWD_GIN) ? PIN_RDROP : 0u) |
+                      ((uint32_t)ps.col[q] - ps.node_lo);
         }
     }
     ps.pin[q] = out;
@@ -317,7 +336,7 @@ __global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, con
         if (!((front_occ[v / 64] >> (v % 64)) & 1)) continue;
         for (int64_t r = ps.row_ptr[v]; r < ps.row_ptr[v + 1]; ++r) {
             const uint32_t q = ps.rev[r];
-            if (q == NO_PAIR || (q & HALO) || !ps.fwd[r]) continue;  // v sends nothing to a local u
+            if (q == NO_PAIR || (q & HALO) || !(ps.fwd[r] & FWD_SEND)) continue;  // v sends nothing to a local u
             const uint32_t u = (uint32_t)ps.col[r] - ps.node_lo;
             atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));
         }
@@ -574,7 +593,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
     const bool want_inwin = ps.credit && !ps.all_dups_in_window;
     const uint32_t h_lo = h > ps.win_hops ? h - ps.win_hops : 0;
     const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;  // node of the tile, lane in the group
-    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0, n_rej = 0, n_ign = 0;
+    unsigned long long n_new = 0, n_dup = 0, n_send = 0, n_vnew = 0, n_back = 0, n_rej = 0, n_ign = 0, n_gray = 0;
     for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
         const uint32_t u = tile + gi;
         bool any_new = false;
@@ -626,7 +645,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                         for (int j = 0; j < U; ++j)
                             if (pv[j] != NO_PAIR) {
-                                const bool live = (pv[j] & HALO) ? (!ps.halo_occ || occ_bit(ps.halo_occ, pv[j] & ~HALO))
+                                const bool live = (pv[j] & HALO) ? (!ps.halo_occ || occ_bit(ps.halo_occ, pv[j] & HALO_SLOT))
                                                                  : occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
                                 if (!live) pv[j] = NO_PAIR;  // the sender's row is empty
                             }
@@ -637,7 +656,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] = 0;
                         } else if (pv[j] & HALO) {  // remote sender: its rank packed exactly what it sends
-                            load_words<CW>(c[j], ps.halo + (size_t)(pv[j] & ~HALO) * W + w0);
+                            load_words<CW>(c[j], ps.halo + (size_t)(pv[j] & HALO_SLOT) * W + w0);
                         } else {
                             load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
                         }
@@ -694,6 +713,11 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] &= ~mine[i];
                         }
+                        if (p & HALO_GRAY) {  // u's AcceptFrom drops the remote sender's RPCs whole
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) n_gray += __popcll(c[j][i]);
+                            continue;  // the same in every lane of the group
+                        }
                         uint64_t nb[CW];
                         uint32_t fresh = 0, pc = 0, kw = 0, inv = 0;
                         bool rx = false;  // any first receipt, delivered or dropped
@@ -728,7 +752,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                                 for (int i = 0; i < CW; ++i) fr[i] = o[i] | nb[i];
                             }
                             if (halo) {  // what u must not send back to this remote sender (k_prop_pack)
-                                uint64_t* hf = ps.hfrom + (size_t)(p & ~HALO) * W + w0;
+                                uint64_t* hf = ps.hfrom + (size_t)(p & HALO_SLOT) * W + w0;
 #pragma unroll
                                 for (int i = 0; i < CW; ++i) hf[i] = nb[i];
                             }
@@ -744,7 +768,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                             if (fresh) {  // first receipts from v: this call's count and the last hop's
                                 ps.fcnt[q] = fc[j] + fresh;
                                 ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
-                                if (backsend && !halo && (fq[j] & FWD_FORWARD)) {
+                                if (backsend && !halo && (fq[j] & FWD_FORWARD) && !(p & PIN_RDROP)) {
                                     // u forwards them to v at hop h + 1 and v counts duplicates:
                                     // the `from` exclusion's whole effect, taken back here
                                     n_back += fresh;
@@ -779,10 +803,10 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
         const uint32_t u0 = tile + (threadIdx.x / 64) * NW;  // the wave's first node
         if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
     }
-    unsigned long long cnt[7] = {n_new, n_dup, n_send, n_vnew, n_back, n_rej, n_ign};
-    const uint32_t slot[7] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS,
-                              STAT_REJECTED, STAT_IGNORED};
-    block_count<7>(cnt, ps.stats, slot);
+    unsigned long long cnt[8] = {n_new, n_dup, n_send, n_vnew, n_back, n_rej, n_ign, n_gray};
+    const uint32_t slot[8] = {STAT_HOP0 + h, STAT_DUPS, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_BACKSENDS,
+                              STAT_REJECTED, STAT_IGNORED, STAT_GRAY};
+    block_count<8>(cnt, ps.stats, slot);
 }
 
 struct DupsLast {  // the last hop run and its frontier rows
@@ -813,7 +837,9 @@ __device__ __forceinline__ DupsLast dups_last(const PropState& ps, uint32_t h_ru
 // receipts) and the part of it v published, packed n_all | n_own << 32.  L
 // lanes per node, 4 words each per step, summed with shuffles.
 template <int L>
-__global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_run, uint64_t* __restrict__ vcnt) {
+__global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_run, uint64_t* __restrict__ vcnt,
+                                                     bool gray_only) {
+    if (gray_only && *ps.gray_pairs == 0) return;  // no gated pair: k_prop_dups<true> has nothing to count
     const DupsLast L_ = dups_last(ps, h_run);
     const uint32_t W = ps.n_words;
     const uint32_t lc = threadIdx.x % L;
@@ -849,8 +875,18 @@ __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_ru
 // issued together, so a thread waits for one round of latencies per batch
 // rather than one per pair.
 constexpr int DU = 4;
+// With the graylist gate (ps.gate), a pair whose receiver drops the sender's
+// RPCs (FWD_GIN on the receiver's pair q) sends the same copies, but they are
+// dropped at u before pushMsg: they count as STAT_GRAY, never as duplicates,
+// and leave no correction in corr[r].  Those copies include the messages v
+// published that validation does not accept (their copies to accepting
+// receivers are rejected/ignored receipts of the hop kernels).  GRAY_ONLY
+// (per-hop accounting, where duplicates are counted on arrival) visits only
+// the gated pairs.
+template <bool GRAY_ONLY>
 __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
-    unsigned long long cnt[1] = {0};
+    if (GRAY_ONLY && *ps.gray_pairs == 0) return;
+    unsigned long long cnt[2] = {0, 0};
     const uint32_t W = ps.n_words;
     const DupsLast L = dups_last(ps, h_run);
     h_run = L.h_run;
@@ -868,12 +904,19 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             va[i] = in ? ps.pair_obs[r] : 0;
             ua[i] = in ? (uint32_t)ps.col[r] - ps.node_lo : 0;
         }
+        bool ga[DU];  // u drops v's copies
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const bool local = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
+            ga[i] = local && ps.gate && (ps.fwd[qa[i]] & FWD_GIN);
+            if (GRAY_ONLY && !ga[i]) qa[i] = NO_PAIR;
+        }
         uint64_t vca[DU], fla[DU];
         uint32_t fca[DU];
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
             const uint64_t r = r0 + i * stride;
-            const bool live = qa[i] != NO_PAIR && !(qa[i] & HALO) && fa[i];
+            const bool live = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
             vca[i] = live ? vcnt[va[i]] : 0;
             const bool fl = live && !ps.from_mask && (fa[i] & FWD_FORWARD) && h_run >= 1;
             fca[i] = fl ? ps.fcnt[r] : 0;
@@ -884,9 +927,10 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             const uint64_t r = r0 + i * stride;
             const uint32_t q = qa[i];
             const uint8_t fw = fa[i];
-            if (q == NO_PAIR || (q & HALO) || !fw) continue;
+            if (q == NO_PAIR || (q & HALO) || !(fw & FWD_SEND)) continue;
             const uint32_t v = va[i], u = ua[i];
             const bool u_src = occ_bit(src_occ, u);
+            const bool v_src = occ_bit(src_occ, v);
             uint32_t sends = 0, pub = 0;
             if (!u_src && !ps.sel && !ps.from_mask) {
                 const uint64_t vc = vca[i];
@@ -895,7 +939,6 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
                 sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
                       : m == FWD_PUBLISH ? n_own : 0;
             } else {
-                const bool v_src = occ_bit(src_occ, v);
                 const bool v_last = !L.empty && occ_bit(L.occ, v);
                 for (uint32_t w = 0; w < W; ++w) {
                     const size_t vw = (size_t)v * W + w;
@@ -919,12 +962,19 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
                 const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH)) ? pub : 0;  // pub != 0 only if u published
                 sends -= fca[i] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
             }
-            cnt[0] += sends;
-            ps.corr[r] = sends;
+            if (ga[i]) {
+                if (ps.drop && v_src && (fw & FWD_PUBLISH))  // v's own unaccepted messages, sent at hop 1
+                    for (uint32_t w = 0; w < W; ++w) sends += __popcll(ps.origin[(size_t)v * W + w] & ps.drop[w]);
+                cnt[1] += sends;
+                if (!GRAY_ONLY) ps.corr[r] = 0;
+            } else {
+                cnt[0] += sends;
+                ps.corr[r] = sends;
+            }
         }
     }
-    const uint32_t slot[1] = {STAT_DUPS};
-    block_count<1>(cnt, ps.stats, slot);
+    const uint32_t slot[2] = {STAT_DUPS, STAT_GRAY};
+    block_count<2>(cnt, ps.stats, slot);
 }
 
 // ---- P2/P3 credits ------------------------------------------------------------
@@ -1106,7 +1156,7 @@ hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStre
 }
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st) {
     if (s.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_fwd, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps, s);
+    hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
     hipLaunchKernelGGL(k_prop_pin, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
     return hipGetLastError();
 }
@@ -1185,18 +1235,19 @@ hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* fro
     hipLaunchKernelGGL(k_prop_mark, dim3(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h, front_occ);
     return hipGetLastError();
 }
-hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, hipStream_t st) {
+hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, bool gray_only, hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
     const uint32_t W = ps.n_words;
     const int L = W % 64 == 0 ? 16 : W % 32 == 0 ? 8 : W % 16 == 0 ? 4 : W % 8 == 0 ? 2 : 1;
     const dim3 gv(std::min(nblk((uint64_t)ps.n_nodes * L, 256), COUNTER_GRID));
-    if (L == 16) hipLaunchKernelGGL(k_prop_vcount<16>, gv, dim3(256), 0, st, ps, h_run, vcnt);
-    else if (L == 8) hipLaunchKernelGGL(k_prop_vcount<8>, gv, dim3(256), 0, st, ps, h_run, vcnt);
-    else if (L == 4) hipLaunchKernelGGL(k_prop_vcount<4>, gv, dim3(256), 0, st, ps, h_run, vcnt);
-    else if (L == 2) hipLaunchKernelGGL(k_prop_vcount<2>, gv, dim3(256), 0, st, ps, h_run, vcnt);
-    else hipLaunchKernelGGL(k_prop_vcount<1>, gv, dim3(256), 0, st, ps, h_run, vcnt);
-    hipLaunchKernelGGL(k_prop_dups, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
-                       vcnt);
+    if (L == 16) hipLaunchKernelGGL(k_prop_vcount<16>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
+    else if (L == 8) hipLaunchKernelGGL(k_prop_vcount<8>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
+    else if (L == 4) hipLaunchKernelGGL(k_prop_vcount<4>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
+    else if (L == 2) hipLaunchKernelGGL(k_prop_vcount<2>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
+    else hipLaunchKernelGGL(k_prop_vcount<1>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
+    const dim3 gd(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID));
+    if (gray_only) hipLaunchKernelGGL(k_prop_dups<true>, gd, dim3(256), 0, st, ps, h_run, vcnt);
+    else hipLaunchKernelGGL(k_prop_dups<false>, gd, dim3(256), 0, st, ps, h_run, vcnt);
     return hipGetLastError();
 }
 hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st) {

@@ -239,12 +239,13 @@ class PropOut(C.Structure):
         ("hop_kernel_ms", C.c_double),
         ("rejected", C.c_uint64),
         ("ignored", C.c_uint64),
+        ("graylisted", C.c_uint64),
     ]
 
     def as_dict(self):
         return dict(deliveries=self.deliveries, duplicates=self.duplicates, transmissions=self.transmissions,
                     hops=self.hops, hop_deliveries=list(self.hop_deliveries)[: self.hops + 1],
-                    rejected=self.rejected, ignored=self.ignored)
+                    rejected=self.rejected, ignored=self.ignored, graylisted=self.graylisted)
 
 
 class Msg(C.Structure):

@@ -29,7 +29,8 @@ import numpy as np
 
 from . import abi
 
-_STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words", "rejected", "ignored")
+_STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words", "rejected", "ignored",
+              "graylisted")
 
 
 def prop_words(m: int) -> int:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSX_ABI_VERSION 2
+#define GSX_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define GSX_OK 0
@@ -344,8 +344,16 @@ int gsx_last_refresh_ms(gsx_engine* e, float* ms);
  *     MeshMessageDeliveriesWindow after the first copy finished validating
  *     (score.go:965); a message validation does not accept (gsx_msg.validation)
  *     is seen but neither delivered nor forwarded;
- *   - score gates (publishThreshold, flood publish) read the scores as they
- *     stand when the call starts; the call's credits land at its end.
+ *   - gossipsub only: a receiver u drops every copy from a sender v that is
+ *     not one of its direct peers and whose score (u's record of v) is below
+ *     GraylistThreshold — AcceptFrom (gossipsub.go:583-594) returns
+ *     AcceptNone and handleIncomingRPC drops the whole RPC before pushMsg
+ *     (pubsub.go:1014-1017): not seen, no Deliver / Duplicate / Reject trace,
+ *     no P2 / P3 / P4; counted in gsx_prop_out.graylisted.  Floodsub and
+ *     RandomSub accept everything (AcceptAll);
+ *   - score gates (graylist, publishThreshold, flood publish) read the scores
+ *     as they stand when the call starts; the call's credits land at its end
+ *     (a sequence of calls is a sequence of RPCs: the next call sees them).
  * With credit_scores set, first receipts and duplicates are folded into the
  * receiver's counters exactly as DeliverMessage / DuplicateMessage would
  * (score.go:695-719, 788-820: +1 then cap, one step per message). */
@@ -389,7 +397,7 @@ typedef struct gsx_msg {
 typedef struct gsx_prop_out {
     uint64_t deliveries;     /* first receipts by vertices other than the source */
     uint64_t duplicates;     /* receipts of an already seen message             */
-    uint64_t transmissions;  /* sends: deliveries + duplicates + rejected + ignored */
+    uint64_t transmissions;  /* sends: deliveries + duplicates + rejected + ignored + graylisted */
     uint32_t hops;           /* last hop with a first receipt                   */
     uint32_t hop_launches;   /* hop (and pack) launches timed in hop_kernel_ms  */
     uint64_t hop_deliveries[GSX_MAX_HOPS + 1]; /* first receipts per hop       */
@@ -401,6 +409,8 @@ typedef struct gsx_prop_out {
     double hop_kernel_ms;    /* device time of the hop / pack kernels (HIP events) */
     uint64_t rejected;       /* receipts of REJECT messages (RejectMessage, P4 to the sender) */
     uint64_t ignored;        /* receipts of IGNORE / THROTTLE messages                      */
+    uint64_t graylisted;     /* copies dropped by the receiver's AcceptFrom (gossipsub only):
+                              * sender not direct and scored below GraylistThreshold       */
 } gsx_prop_out;
 
 /* credit_scores values */

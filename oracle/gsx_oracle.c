@@ -1071,9 +1071,10 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     size_t cap_arr = 1024, n_arr = 0;
     orc_arrival* arr = (orc_arrival*)malloc(sizeof(orc_arrival) * cap_arr);
     const bool credit = cfg->credit_scores && cfg->topic < o->T && o->scored[cfg->topic];
-    /* The synchronous contract (gsx.h): the publishThreshold tests of one
-     * call read the scores as they stand when it starts; the call's own
-     * credits (P2/P3, and P4 of rejected messages) land at its end. */
+    const bool gate = cfg->router == GSX_ROUTER_GOSSIPSUB; /* floodsub / randomsub: AcceptAll */
+    /* The synchronous contract (gsx.h): the graylist and publishThreshold
+     * tests of one call read the scores as they stand when it starts; the
+     * call's own credits (P2/P3, and P4 of rejected messages) land at its end. */
     double* score0 = (double*)malloc(sizeof(double) * (o->E ? o->E : 1));
     for (uint64_t r = 0; r < o->E; r++) score0[r] = score_pair(o, r);
     /* gossipsub's Publish Puts every message a node processes into its
@@ -1127,7 +1128,18 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
             for (size_t a = 0; a < n_arr; a++) {
                 const uint32_t u = arr[a].u, v = arr[a].v;
                 out->transmissions++;
-                const int64_t q = credit ? reverse_pair(o, arr[a].r) : -1; /* u's peerStats for v */
+                const int64_t qr = (credit || gate) ? reverse_pair(o, arr[a].r) : -1; /* u's peerStats for v */
+                /* handleIncomingRPC asks the router first (pubsub.go:1014-1017):
+                 * gossipsub's AcceptFrom (gossipsub.go:583-594) returns AcceptNone
+                 * for a non-direct sender scoring below GraylistThreshold, and the
+                 * RPC is dropped whole: no seen mark, no trace, no credit.  A
+                 * sender u keeps no peerStats for scores 0 (score.go:247-256). */
+                if (gate && qr >= 0 && !(o->eflags[qr] & GSX_EDGE_DIRECT) &&
+                    score0[qr] < o->th.graylist_threshold) {
+                    out->graylisted++;
+                    continue;
+                }
+                const int64_t q = credit ? qr : -1;
                 if (hop[u] == 0xFF) { /* first receipt: markSeen, then validation */
                     hop[u] = (uint8_t)h;
                     from[u] = (int32_t)v;

@@ -18,9 +18,11 @@ from gsx.shard import prop_words
 
 M64 = (1 << 64) - 1
 FWD, PUB = 1, 2
+GIN = 8  # the pair's observer drops its neighbour's RPCs (gossipsub AcceptFrom, graylist)
 
 
-def fwd_bytes(router, state, scores, edge_flags, topic, n_topics, publish_threshold, flood_publish):
+def fwd_bytes(router, state, scores, edge_flags, topic, n_topics, publish_threshold, flood_publish,
+              graylist_threshold=float("-inf")):
     """fwd[r] of every pair (v -> u) (gsx_propagate.hip k_prop_fwd) from an exported state."""
     E = len(edge_flags)
     pf = state["pair_flags"]
@@ -37,7 +39,9 @@ def fwd_bytes(router, state, scores, edge_flags, topic, n_topics, publish_thresh
     fwd = fwd | mesh
     pub = (direct | above) if flood_publish else fwd
     out = np.where(fwd, FWD, 0) | np.where(pub, PUB, 0)
-    return np.where(inn, out, 0).astype(np.uint8)
+    out = np.where(inn, out, 0)
+    gin = ~direct & (scores < graylist_threshold)  # gossipsub.go:583-594
+    return (out | np.where(gin, GIN, 0)).astype(np.uint8)
 
 
 def _elig(fw, own):
@@ -164,7 +168,7 @@ class EmuShard:
         self.frm = [[0] * W for _ in range(E)]
         self.hop = np.full((n, W * 64), 0xFF, dtype=np.uint8)
         self.h = 0
-        self.stats = dict(deliveries=0, duplicates=0, hop=[0] * (abi.GSX_MAX_HOPS + 1))
+        self.stats = dict(deliveries=0, duplicates=0, graylisted=0, hop=[0] * (abi.GSX_MAX_HOPS + 1))
         for k, s in enumerate(msgs["source"]):
             s = int(s)
             if self.lo <= s < self.lo + n:
@@ -231,6 +235,9 @@ class EmuShard:
                     c &= ~mine & M64
                     if not c:
                         continue
+                    if int(self.fwd[q]) & GIN:  # u's AcceptFrom drops v's RPCs whole
+                        self.stats["graylisted"] += bin(c).count("1")
+                        continue
                     newb = c & ~seen & ~acc & M64
                     self.stats["duplicates"] += bin(c & acc).count("1") + bin(c & seen).count("1")
                     acc |= newb
@@ -252,7 +259,8 @@ class EmuShard:
         out = abi.PropOut()
         out.deliveries = self.stats["deliveries"]
         out.duplicates = self.stats["duplicates"]
-        out.transmissions = out.deliveries + out.duplicates
+        out.graylisted = self.stats["graylisted"]
+        out.transmissions = out.deliveries + out.duplicates + out.graylisted
         for h, c in enumerate(self.stats["hop"]):
             out.hop_deliveries[h] = c
             if c:

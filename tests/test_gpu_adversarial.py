@@ -31,3 +31,15 @@ def test_adversarial_matches_oracle(gpu_ok, n):
         for f in list(abi.STATE_FIELDS) + ["backoff", "scores", "ihave_len", "ihave_digest"]:
             assert np.array_equal(np.asarray(g[k][1][f]).view(np.uint8), np.asarray(w[k][1][f]).view(np.uint8)), (k, f)
     assert g[1][0]["prunes"] > 0
+
+
+def test_invalid_message_spam_stops_at_graylist(gpu_ok):
+    """TestGossipsubAttackInvalidMessageSpam (gossipsub_spam_test.go:615-763)
+    through the engine: 100 rejected single-message RPCs, the attacker is
+    graylisted after the 4th (score -396 < -300) and every later RPC is dropped
+    by AcceptFrom (tests/spam_cases.py); every call matches the oracle."""
+    import spam_cases as sc
+
+    g = sc.run(gsx.Engine(1))
+    sc.check(g)
+    assert g == sc.run(orc.Oracle(1))

@@ -61,6 +61,10 @@ def test_propagation_matches_oracle(gpu_ok, case, track):
         assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
     assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))
     assert go["deliveries"] > 0
+    if router == abi.GSX_ROUTER_GOSSIPSUB:
+        assert go["graylisted"] > 0  # the setup puts ~8 % of the senders below GraylistThreshold
+    else:
+        assert go["graylisted"] == 0  # floodsub / randomsub: AcceptFrom accepts all
 
 
 def test_propagation_full_size_properties(gpu_ok):

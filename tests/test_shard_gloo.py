@@ -123,7 +123,8 @@ def test_range_sharded_gloo_matches_oracle(case):
     th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                         accept_px_threshold=0, opportunistic_graft_threshold=0)
     o, st, scores, out, hop, frm = _reference(ov, 1, seed, msgs, cfg)
-    fwd = emu.fwd_bytes(router, st, scores, ov.edge_flags, 0, 1, th.publish_threshold, fp)
+    gl = th.graylist_threshold if router == abi.GSX_ROUTER_GOSSIPSUB else float("-inf")
+    fwd = emu.fwd_bytes(router, st, scores, ov.edge_flags, 0, 1, th.publish_threshold, fp, gl)
     rank_lo = synth.shard_ranges(n, world)
     shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
     payload = dict(mode="range", shards=shards, fwd=fwd, row_ptr=ov.row_ptr, rank_lo=rank_lo, msgs=msgs,
@@ -137,6 +138,9 @@ def test_range_sharded_gloo_matches_oracle(case):
     assert all(r[2] == tot for r in res)  # every rank holds the same totals
     want = out.as_dict()
     assert tot["deliveries"] == want["deliveries"] and tot["duplicates"] == want["duplicates"]
+    assert tot["graylisted"] == want["graylisted"] and tot["transmissions"] == want["transmissions"]
+    if router == abi.GSX_ROUTER_GOSSIPSUB:
+        assert want["graylisted"] > 0  # the setup's app scores put some senders below the graylist
     assert tot["hops"] == want["hops"] and tot["hop_deliveries"] == want["hop_deliveries"]
     assert sum(r[1]["deliveries"] for r in res) == want["deliveries"]
     assert want["deliveries"] > 0

@@ -31,7 +31,7 @@ rocm-smi --showproductname > "$OUT/device.txt" 2>&1 || true
 nproc > "$OUT/nproc.txt"
 
 if [[ $STEPS == all || $STEPS == *test* ]]; then
-    run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+    run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider
 fi
 if [[ $STEPS == all || $STEPS == *smoke* ]]; then
     run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
