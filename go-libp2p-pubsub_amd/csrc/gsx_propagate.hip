@@ -713,7 +713,8 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] &= ~mine[i];
                         }
-                        if (p & HALO_GRAY) {  // u's AcceptFrom drops the remote sender's RPCs whole
+                        if (halo && (p & HALO_GRAY)) {  // u's AcceptFrom drops the remote sender's RPCs whole
+                            // (bit 30 of a local pin is FWD_PUBLISH: tested under HALO only)
 #pragma unroll
                             for (int i = 0; i < CW; ++i) n_gray += __popcll(c[j][i]);
                             continue;  // the same in every lane of the group
