@@ -960,7 +960,9 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             if (!ps.from_mask && (fw & FWD_FORWARD) && h_run >= 1) {
                 const uint64_t fl = fla[i];
                 const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
-                const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH)) ? pub : 0;  // pub != 0 only if u published
+                // u's own messages v first got from u: all of them iff u publishes to v
+                // and v accepts u's RPCs (pub != 0 only if u published)
+                const uint32_t from_pub = (pub && (ps.fwd[q] & FWD_PUBLISH) && !(fw & FWD_GIN)) ? pub : 0;
                 sends -= fca[i] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
             }
             if (ga[i]) {
