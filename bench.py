@@ -78,6 +78,50 @@ def load_traffic(cfg_key):
     return None
 
 
+def single_observer_leg(args, device):
+    """SURVEY.md §8 secondary view: ONE router scoring 1M peers on T topics
+    (R = 8e6 records at T = 8): the drop-in shape of a single gossipsub node's
+    score.go, as opposed to the 1M-observer overlay of the headline."""
+    n_peers, T = args.peers, args.topics
+    row_ptr = np.zeros(n_peers + 2, dtype=np.int64)
+    row_ptr[1:] = n_peers  # node 0 observes nodes 1..n_peers
+    col = np.arange(1, n_peers + 1, dtype=np.int32)
+    ef = np.full(n_peers, abi.GSX_EDGE_GOSSIPSUB, dtype=np.uint8)
+    ips = np.stack([np.arange(n_peers + 1, dtype=np.uint32) + 1, np.full(n_peers + 1, 0xFFFFFFFF, np.uint32)], axis=1)
+    e = gsx.Engine(T, device=device)
+    e.set_peer_params(synth.bench_peer_params())
+    for k in range(T):
+        e.set_topic_params(k, synth.spam_test_topic_params())
+    e.load_overlay(row_ptr, col, ef, ips)
+    e.synthesize_state(
+        abi.SynthSpec(seed=synth.SEED + 5, now_ns=T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0, imd_max_sybil=100.0,
+                      p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0, p_disconnected=0.0, p_absent=0.0,
+                      expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n_peers + 1))
+    e.set_app_scores(np.zeros(n_peers))
+    now = T0
+    for _ in range(3):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+    steps = max(1, args.steps)
+    e.timing_begin(steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        now += abi.SECOND
+        e.refresh(now)
+    e.sync()
+    el = time.perf_counter() - t0
+    k_total, _, _, k_n = e.timing_end()
+    e.close()
+    R = n_peers * T
+    kavg = k_total / max(1, k_n)
+    B = BYTES_PER_RECORD * R + BYTES_PER_PAIR * n_peers
+    return {"metric": "peer-topic score updates/s", "value": R * steps / el, "records": R, "peers": n_peers,
+            "topics": T, "ms_per_refresh": el / steps * 1e3, "kernel_avg_ms": kavg,
+            "roofline": {"bound": "hbm", "algorithmic_bytes_per_launch": B, "achieved": B / (kavg * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+
+
 def cpu_baseline(e, T, now, passes):
     """Single-threaded oracle refresh+score on the engine's exact state; also
     checks the GPU scores of the same pass bit-for-bit."""
@@ -205,8 +249,10 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     (loc, tot), msgs = res[-1]
     mine = prop_messages(n, M, synth.SEED, first=args.prop_steps * M)
     mine = mine[(M * rank) // world : (M * (rank + 1)) // world]
+    legs = prop_variant_legs(args, e, n) if world == 1 else None
     e.close()
     return {
+        "variants": legs,
         "metric": "msg deliveries/s",
         "mode": "message-parallel replicas (weak): full overlay per GPU, own messages, one all-reduce of credits",
         "value": dl / el,
@@ -219,6 +265,54 @@ def prop_replica(args, rank, world, local, dist, dev, th):
         "router": "gossipsub (synthesized mesh, ~6 of ~12 peers), P2/P3 credits on",
         "roofline_rank0": prop_roofline(loc, mine, loc["hop_kernel_ms"]),
     }
+
+
+def prop_leg(e, n, M, cfg, steps, seed, first):
+    """Times `steps` batches of M messages on one engine (after one warm-up
+    batch): deliveries/s, ms per batch, hop-kernel time and the push-minimal
+    roofline of the last batch."""
+    import torch
+
+    e.propagate(prop_messages(n, M, seed, first=first), cfg)
+    e.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = []
+    for b in range(steps):
+        msgs = prop_messages(n, M, seed, first=first + (1 + b) * M)
+        outs.append(shard_mod.out_dict(e.propagate(msgs, cfg)[0]))
+    e.sync()
+    el = time.perf_counter() - t0
+    last = outs[-1]
+    kms = sum(o["hop_kernel_ms"] for o in outs) / steps
+    return {"value": sum(o["deliveries"] for o in outs) / el, "unit": "msg deliveries/s", "messages_per_batch": M,
+            "ms_per_batch": el / steps * 1e3, "hop_kernel_ms_per_batch": kms, "hops": last["hops"],
+            "deliveries_per_batch": last["deliveries"], "duplicates_per_batch": last["duplicates"],
+            "graylisted_per_batch": last["graylisted"], "roofline": prop_roofline(last, msgs, last["hop_kernel_ms"])}
+
+
+def prop_variant_legs(args, e, n):
+    """BASELINE.md's other propagation shapes on the replica engine: 64-message
+    batches (cfg2/cfg4's batch size), the floodsub router, and gossipsub with a
+    P3 window shorter than the run (duplicates counted per hop by the general
+    k_prop_hop kernel instead of the lean k_prop_hop_fast)."""
+    steps = max(3, args.prop_steps)
+    seed = synth.SEED + 7
+    out = {}
+    cfg = prop_config(args, n)
+    out["gossipsub_64msg"] = prop_leg(e, n, 64, cfg, 4 * steps, seed, 10_000_000)
+    fcfg = prop_config(args, n)
+    fcfg.router = abi.GSX_ROUTER_FLOODSUB
+    out["floodsub_1024msg"] = prop_leg(e, n, args.prop_msgs, fcfg, steps, seed, 20_000_000)
+    out["floodsub_64msg"] = prop_leg(e, n, 64, fcfg, 4 * steps, seed, 30_000_000)
+    tp = synth.spam_test_topic_params()
+    tp.mesh_message_deliveries_window_ns = 25 * abi.MILLISECOND  # 2 hops of 10 ms: late copies fall outside
+    e.set_topic_params(0, tp)
+    leg = prop_leg(e, n, args.prop_msgs, cfg, steps, seed, 40_000_000)
+    leg["note"] = "P3 window 25 ms < run: per-hop duplicate accounting, general k_prop_hop kernel"
+    out["gossipsub_1024msg_short_window"] = leg
+    e.set_topic_params(0, synth.spam_test_topic_params())
+    return out
 
 
 def prop_sharded(args, rank, world, local, dist, dev, th):
@@ -368,6 +462,7 @@ def adversarial_leg(args, rank, world, local, dist, dev):
             "messages": M, "rejected_by_validation": int(spam.sum()),
             "ms_per_batch": reduce_scalar(time.perf_counter() - t0, dist, dev, "max") * 1e3,
             "deliveries": d["deliveries"], "rejected_receipts_p4": d["rejected"], "duplicates": d["duplicates"],
+            "graylisted_copies": d["graylisted"],
         }
         now += abi.SECOND
         e.refresh(now)
@@ -417,12 +512,15 @@ def main():
     ap.add_argument("--degree", type=int, default=6)
     ap.add_argument("--cpu-passes", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-single-observer", dest="single_observer", action="store_false",
+                    help="skip the one-observer-with-1M-peers view (SURVEY §8)")
     ap.add_argument("--prop-msgs", type=int, default=1024,
                     help="messages per propagation batch (0: skip); 1024 = 16 words, one 128-B line per frontier row")
     ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
+    ap.add_argument("--hb-msgs", type=int, default=256, help="gossipsub messages propagated before every heartbeat")
     ap.add_argument("--adv-peers", type=int, default=4_000_000, help="cfg5 adversarial overlay (0: skip)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on one GPU: all ranks on device 0, gloo (host-staged) instead of RCCL")
@@ -490,6 +588,9 @@ def main():
     cfg_key = f"n={n},T={T},d={args.degree},E={E}"
     traffic = load_traffic(cfg_key)
 
+    # ---- SURVEY §8 secondary view: one observer with 1M neighbours x T topics ----
+    single_obs = single_observer_leg(args, local) if (args.single_observer and rank == 0) else None
+
     # ---- secondary: message deliveries/s (gossipsub mesh forwarding, A13-A14) ----
     prop = None
     if args.prop_msgs > 0:
@@ -506,39 +607,61 @@ def main():
     # ---- heartbeat rounds (A10): every (node, topic) mesh maintained at once ----
     hb = None
     if args.hb_steps > 0:
-        # one gossipsub batch on the scoring shard fills its message caches, so
-        # the heartbeats also emit IHAVE gossip (emitGossip, mcache)
-        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
-                                        accept_px_threshold=0, opportunistic_graft_threshold=0))
-        e.propagate(prop_messages(n, 256, seed), prop_config(args, n))
-        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
-                                        accept_px_threshold=0, opportunistic_graft_threshold=5))
-        tick = 58  # the timed rounds include the OpportunisticGraftTicks round 60
-        now += abi.SECOND
-        e.heartbeat(tick, now, seed)  # warm-up
-        e.sync()
-        barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        outs = []
-        for _ in range(args.hb_steps):
+        # steady state: a gossipsub batch arrives before every heartbeat (untimed),
+        # so every round's emitGossip advertises the cached windows (mcache);
+        # the rounds run through the OpportunisticGraftTicks round 60, where every
+        # unit with a mesh sorts its scores (the "active" round)
+        th_hb = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                               accept_px_threshold=0, opportunistic_graft_threshold=5)
+        e.set_thresholds(th_hb)
+        tick = 57
+        hb_cfg = prop_config(args, n)
+        rounds = []
+        for k in range(args.hb_steps + 1):  # the first round is a warm-up
             tick += 1
             now += abi.SECOND
-            outs.append(e.heartbeat(tick, now, seed).as_dict())
-        e.sync()
-        torch.cuda.synchronize(dev)
-        ht = time.perf_counter() - t0
-        barrier()
-        units = float(n) * T * args.hb_steps
-        ht = reduce_scalar(ht, dist, dev, "max")
-        units = reduce_scalar(units, dist, dev, "sum")
+            hb_cfg.now_ns = now - abi.SECOND // 2
+            e.propagate(prop_messages(n, args.hb_msgs, seed, first=50_000_000 + k * args.hb_msgs), hb_cfg)
+            e.sync()
+            barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            o = e.heartbeat(tick, now, seed).as_dict()
+            e.sync()
+            ms = (time.perf_counter() - t0) * 1e3
+            ms = reduce_scalar(ms, dist, dev, "max")
+            if k:
+                rounds.append({"tick": tick, "og_tick": tick % 60 == 0, "ms": ms, **o})
+        units = float(n) * T
+        deg = E / n
+        d_hi = 12
+        bpu = 21 * deg + 4 * d_hi  # 4*deg + 8*deg + 9*deg + 4*Dhi per (node, topic)
+        active = [r for r in rounds if r["og_tick"]]
+        steady = [r for r in rounds if not r["og_tick"]]
+        mean = lambda xs: sum(xs) / len(xs) if xs else None  # noqa: E731
+        steady_ms = mean([r["ms"] for r in steady])
+        active_ms = mean([r["ms"] for r in active])
+        tot_ms = sum(r["ms"] for r in rounds)
+
+        def roof(ms_):
+            if not ms_:
+                return None
+            ach = units * bpu / (ms_ * 1e-3) / 1e9
+            return {"bound": "hbm", "bytes_per_round": units * bpu, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "timing": "wall clock of gsx_heartbeat incl. launches"}
+
+        units_all = reduce_scalar(units * len(rounds), dist, dev, "sum")
         hb = {
             "metric": "heartbeat (node, topic) mesh units/s",
-            "value": units / ht,
-            "ms_per_round": ht / args.hb_steps * 1e3,
-            "rounds": args.hb_steps,
-            "first_round": outs[0],
-            "last_round": outs[-1],
+            "value": units_all / (tot_ms * 1e-3),
+            "ms_per_round": tot_ms / len(rounds),
+            "rounds": len(rounds),
+            "messages_between_rounds": args.hb_msgs,
+            "steady_ms_per_round": steady_ms,
+            "active_ms_per_round": active_ms,
+            "roofline_steady": roof(steady_ms),
+            "roofline_active": roof(active_ms),
+            "per_round": rounds,
         }
 
     adv = adversarial_leg(args, rank, world, local, dist, dev) if args.adv_peers > 0 else None
@@ -549,17 +672,26 @@ def main():
         o, st = cpu_baseline(e, T, now, args.cpu_passes)
         t = time.time()
         o.load_overlay(ov.row_ptr, ov.col, None, ov.node_ips)
-        o.import_state(st)
-        o.set_app_scores(np.zeros(E))
         log(f"[bench] oracle loaded in {time.time() - t:.1f}s")
-        cpu_s = 0.0
-        cpu_now = now
-        for _ in range(args.cpu_passes):
-            cpu_now += abi.SECOND
-            t = time.perf_counter()
-            o.refresh(cpu_now)
-            want = o.scores()
-            cpu_s += time.perf_counter() - t
+        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+        def cpu_leg(parallel):
+            o.import_state(st)
+            o.set_app_scores(np.zeros(E))
+            secs, c_now, sc = 0.0, now, None
+            for _ in range(args.cpu_passes):
+                c_now += abi.SECOND
+                t = time.perf_counter()
+                if parallel:
+                    sc = o.refresh_scores_parallel(c_now, threads)
+                else:
+                    o.refresh(c_now)
+                    sc = o.scores()
+                secs += time.perf_counter() - t
+            return secs, sc
+
+        cpu_s1, want1 = cpu_leg(False)
+        cpu_sp, want = cpu_leg(True)
         # the GPU on the same starting state and clock
         e.import_state(st)
         g_now = now
@@ -567,16 +699,20 @@ def main():
             g_now += abi.SECOND
             e.refresh(g_now)
         got = e.scores()
-        parity = "bit-exact" if np.array_equal(got.view(np.uint64), want.view(np.uint64)) else (
-            f"MISMATCH in {int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))} pairs")
+        bad = int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))
+        bad1 = int(np.count_nonzero(want1.view(np.uint64) != want.view(np.uint64)))
+        parity = "bit-exact" if bad == 0 and bad1 == 0 else f"MISMATCH in {bad} pairs (serial vs parallel oracle: {bad1})"
         cpu = {
-            "value": R * args.cpu_passes / cpu_s,
+            "value": R * args.cpu_passes / cpu_sp,
             "unit": "peer-topic score updates/s",
-            "cores": 1,
+            "cores": threads,
             "kind": "port",
+            "single_thread_value": R * args.cpu_passes / cpu_s1,
+            "nproc": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"the full cfg3 shard ({R} records, {E} pairs), {args.cpu_passes} refresh+score passes of the "
-                      f"C oracle (oracle/gsx_oracle.c, -O2, 1 thread; restatement, not reference Go: no Go on the box), "
-                      f"{cpu_s:.1f}s",
+                      f"C oracle (oracle/gsx_oracle.c, gcc -O3, OpenMP over pairs with {threads} threads: "
+                      f"{cpu_sp:.2f}s; 1 thread: {cpu_s1:.2f}s; restatement, not reference Go: no Go on the box)",
         }
         del o, st
 
@@ -614,7 +750,12 @@ def main():
             "kernel_min_ms": k_min,
             "kernel_max_ms": k_max,
             "algorithmic_bytes_per_launch": bytes_per_launch,
+            # on the bytes the kernel actually moves (PMC traffic: the meshTime
+            # stream and unchanged zero counters are never stored)
+            "achieved_traffic": (traffic / (kavg_ms * 1e-3) / 1e9) if traffic else None,
+            "frac_traffic": (traffic / (kavg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
         },
+        "single_observer": single_obs,
         "cpu_baseline": cpu,
         "parity_vs_oracle": parity,
         "propagation": prop,

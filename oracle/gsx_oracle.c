@@ -597,6 +597,29 @@ int orc_refresh_scores_range(orc_engine* o, int64_t now, uint64_t p0, uint64_t p
     return 0;
 }
 
+/* refreshScores + score() over every pair with n_threads OpenMP threads (the
+ * bench's multi-core CPU baseline).  The purge (removeIPs changes the shared
+ * per-observer IP counts) runs first and serially; then every connected pair
+ * decays its own counters and is scored, independently of the others (the
+ * IP counts are only read).  Same results as orc_refresh + orc_scores. */
+int orc_refresh_scores_parallel(orc_engine* o, int64_t now, double* out, int n_threads) {
+    o->last_refresh = now;
+    for (uint64_t p = 0; p < o->E; p++) {
+        orc_peer_stats* pstats = &o->ps[p];
+        if (pstats->present && !pstats->connected && now > pstats->expire) {
+            ipcount_add(o, p, -1);
+            pstats->present = false;
+        }
+    }
+    const int64_t E = (int64_t)o->E;
+#pragma omp parallel for num_threads(n_threads) schedule(static, 4096)
+    for (int64_t p = 0; p < E; p++) {
+        if (o->ps[p].present && o->ps[p].connected) refresh_pair(o, (uint64_t)p, now);
+        out[p] = score_pair(o, (uint64_t)p);
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* tracer events, score.go:588-974                                          */
 

@@ -82,6 +82,8 @@ int orc_scores(orc_engine* o, double* out, size_t n_pairs);
 double orc_score(orc_engine* o, uint64_t pair);
 /* Refresh + score restricted to pairs [p0, p1) (bench sample); returns 0. */
 int orc_refresh_scores_range(orc_engine* o, int64_t now_ns, uint64_t p0, uint64_t p1, double* out);
+/* refresh + score of every pair on n_threads OpenMP threads (bench CPU baseline) */
+int orc_refresh_scores_parallel(orc_engine* o, int64_t now_ns, double* out, int n_threads);
 
 int orc_import_state(orc_engine* o, const gsx_state_view* s);
 int orc_export_state(orc_engine* o, gsx_state_view* s);

@@ -49,6 +49,7 @@ _SIG = {
     "orc_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
     "orc_score": (C.c_double, [C.c_void_p, C.c_uint64]),
     "orc_refresh_scores_range": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, P(C.c_double)]),
+    "orc_refresh_scores_parallel": (C.c_int, [C.c_void_p, C.c_int64, P(C.c_double), C.c_int]),
     "orc_import_state": (C.c_int, [C.c_void_p, P(abi.StateView)]),
     "orc_export_state": (C.c_int, [C.c_void_p, P(abi.StateView)]),
     "orc_num_pairs": (C.c_uint64, [C.c_void_p]),
@@ -232,6 +233,13 @@ class Oracle:
     def refresh_scores_range(self, now, p0, p1):
         out = np.empty(p1 - p0, dtype=np.float64)
         self._chk(self.lib.orc_refresh_scores_range(self.h, now, p0, p1, _p(out, C.c_double)), "orc_refresh_scores_range")
+        return out
+
+    def refresh_scores_parallel(self, now, n_threads):
+        """refresh + scores of every pair on n_threads OpenMP threads."""
+        out = np.empty(self.n_pairs, dtype=np.float64)
+        self._chk(self.lib.orc_refresh_scores_parallel(self.h, now, _p(out, C.c_double), int(n_threads)),
+                  "orc_refresh_scores_parallel")
         return out
 
     def sync(self):

@@ -102,9 +102,16 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
     res = shard.run_local(world, "cuda:0", run, [(e,) for e, _, _ in engines])
     tot = res[0][1]
     want = out.as_dict()
-    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored"):
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored", "graylisted"):
         assert tot[k] == want[k], k
-    assert tot["edge_sends"] == out.edge_sends and tot["new_words"] == out.new_words
+    assert tot["new_words"] == out.new_words
+    # edge_sends is the traffic term of the exchange: a shard packs a row for a
+    # remote receiver that graylists the sender (the copies cross xGMI and are
+    # dropped there), while one engine never gathers such a row
+    if want["graylisted"]:
+        assert tot["edge_sends"] >= out.edge_sends
+    else:
+        assert tot["edge_sends"] == out.edge_sends
     for k, (e, a, b) in enumerate(engines):
         lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
         h, f = e.prop_results(m)
@@ -142,7 +149,7 @@ def test_message_parallel_matches_single_engine(gpu_ok, world, invalid):
     res = shard.run_local(world, "cuda:0", run, [(e,) for e in reps])
     tot = res[0][1]
     want = out.as_dict()
-    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored"):
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "rejected", "ignored", "graylisted"):
         assert tot[k] == want[k], k
     for e in reps:
         st = e.export_state()
