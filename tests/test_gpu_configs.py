@@ -1,0 +1,199 @@
+"""Every BASELINE.json config at its own size on the GPU:
+
+- cfg1  20-peer TestSparseGossipsub-shaped run (tests/sparse_cases.py), engine == oracle,
+        every peer receives every message (gossipsub_test.go:43-82);
+- cfg2  10k-peer random d=6 overlay, floodsub and gossipsub propagation == oracle;
+- cfg3  1M peers x 8 topics: heartbeats (the OpportunisticGraftTicks round and the
+        next one) == oracle on the exported state, mesh maintenance, IHAVE gossip,
+        backoff, scores bit for bit;
+- cfg4  10M-peer overlay on one GPU, floodsub: arrival hops == BFS distances on
+        sampled messages, totals consistent (each node reached at most once);
+- cfg5  4M peers, 20 % colocated sybils with invalid-message counters: sybils at
+        their victims score below GraylistThreshold, and after heartbeats no peer
+        whose round-start score was negative is in any mesh, while honest nodes keep
+        honest mesh peers (the invariant of gossipsub_test.go:1755-1774).
+"""
+import numpy as np
+import pytest
+
+import adversarial_cases as ac
+import gsx
+import heartbeat_cases as hc
+import oracle as orc
+import propagation_cases as pc
+from gsx import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+S = abi.SECOND
+
+
+def _same(a, b, what):
+    assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), what
+
+
+def test_cfg1_sparse_gossipsub_20_peers(gpu_ok):
+    import sparse_cases as sc
+
+    g = sc.run(gsx.Engine(1))
+    w = sc.run(orc.Oracle(1))
+    sc.check(*g)
+    assert g[0] == w[0]
+    for (go, gh), (wo, wh) in zip(g[1], w[1]):
+        assert go == wo
+        assert np.array_equal(gh, wh)
+
+
+@pytest.mark.parametrize("router", [abi.GSX_ROUTER_FLOODSUB, abi.GSX_ROUTER_GOSSIPSUB], ids=["floodsub", "gossipsub"])
+@pytest.mark.parametrize("m", [64, 130])
+def test_cfg2_10k_peers_matches_oracle(gpu_ok, router, m):
+    n, seed = 10_000, 17
+    ov = pc.overlay(n, 6, seed, mix_protocols=router == abi.GSX_ROUTER_GOSSIPSUB, direct_frac=0.01)
+    ms = pc.messages(n, m, seed)
+    cfg = pc.config(router, latency_ms=10)
+    res = []
+    for be in (gsx.Engine(1), orc.Oracle(1)):
+        pc.setup(be, ov, 1, seed, disconnect_frac=0.01)
+        out, hop, frm = be.propagate(ms, cfg, want_results=True)
+        res.append((out.as_dict(), hop, frm, be.export_state(), be.scores()))
+    (go, gh, gf, gs, gsc), (wo, wh, wf, ws, wsc) = res
+    assert go == wo
+    assert np.array_equal(gh, wh) and np.array_equal(gf, wf)
+    for f in abi.STATE_FIELDS:
+        _same(gs[f], ws[f], f)
+    _same(gsc, wsc, "scores")
+    assert go["deliveries"] > 0.9 * m * (n - 1)
+
+
+def _cfg3_backend(be, ov, T, st):
+    be.set_peer_params(synth.bench_peer_params())
+    for t in range(T):
+        be.set_topic_params(t, synth.spam_test_topic_params())
+    be.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                     accept_px_threshold=0, opportunistic_graft_threshold=5))
+    be.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    be.import_state(st)
+    be.set_app_scores(np.zeros(ov.n_pairs))
+
+
+@pytest.mark.timeout(1200)
+def test_cfg3_heartbeat_1m_x_8_matches_oracle(gpu_ok):
+    """The bench's cfg3 state: two heartbeats (ticks 60 and 61; 60 is an
+    opportunistic-graft round, where every unit with a mesh sorts it) after a
+    4-message gossipsub batch fills the message caches."""
+    n, T, seed = 1_000_000, 8, synth.SEED
+    T0 = pc.T0
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    e = gsx.Engine(T)
+    e.set_peer_params(synth.bench_peer_params())
+    for t in range(T):
+        e.set_topic_params(t, synth.spam_test_topic_params())
+    e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    e.synthesize_state(abi.SynthSpec(seed=seed, now_ns=T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0,
+                                     imd_max_sybil=100.0, p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0,
+                                     p_disconnected=0.0, p_absent=0.0, expire_jitter_ns=4 * S, sybil_first_node=n))
+    e.set_app_scores(np.zeros(ov.n_pairs))
+    e.refresh(T0 + S)
+    st = e.export_state()
+    o = orc.Oracle(T)
+    _cfg3_backend(o, ov, T, st)
+    _cfg3_backend(e, ov, T, st)
+    del st
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=10)
+    cfg.now_ns = T0 + 2 * S
+    ms = pc.messages(n, 4, seed)
+    outs = [be.propagate(ms, cfg)[0].as_dict() for be in (e, o)]
+    assert outs[0] == outs[1]
+    for k, tick in enumerate((60, 61)):
+        now = T0 + (3 + k) * S
+        ho = [be.heartbeat(tick, now, seed).as_dict() for be in (e, o)]
+        assert ho[0] == ho[1], tick
+        assert ho[0]["grafts"] > 0 and ho[0]["ihave_msgs"] > 0
+        for f in ("backoff", "scores", "ihave_len", "ihave_digest"):
+            a = {"backoff": lambda be: be.export_backoff(), "scores": lambda be: be.scores()}.get(f)
+            if a is not None:
+                _same(a(e), a(o), (tick, f))
+        gl, gd = e.gossip_results()
+        wl, wd = o.gossip_results()
+        _same(gl, wl, (tick, "ihave_len"))
+        _same(gd, wd, (tick, "ihave_digest"))
+        del gl, gd, wl, wd
+        gs, ws = e.export_state(), o.export_state()
+        for f in abi.STATE_FIELDS:
+            _same(gs[f], ws[f], (tick, f))
+        del gs, ws
+
+
+def _bfs(row_ptr, col, src):
+    """Level-synchronous BFS over a CSR overlay (numpy): hop distance per node, -1 unreached."""
+    n = len(row_ptr) - 1
+    dist = np.full(n, -1, dtype=np.int64)
+    dist[src] = 0
+    front = np.array([src], dtype=np.int64)
+    d = 0
+    while len(front):
+        d += 1
+        starts, ends = row_ptr[front], row_ptr[front + 1]
+        lens = ends - starts
+        idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+        nb = np.unique(col[idx])
+        nb = nb[dist[nb] < 0]
+        dist[nb] = d
+        front = nb
+    return dist
+
+
+@pytest.mark.timeout(1200)
+def test_cfg4_10m_floodsub_properties(gpu_ok):
+    n, seed = 10_000_000, synth.SEED + 1
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    e = gsx.Engine(1)
+    e.set_peer_params(synth.bench_peer_params())
+    e.set_topic_params(0, synth.spam_test_topic_params())
+    e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    e.synthesize_state(abi.SynthSpec(seed=seed, now_ns=pc.T0, fmd_max=10, mmd_max=10, mfp_max=1, imd_max_sybil=0,
+                                     p_in_mesh=0.5, graft_window_ns=abi.HOUR, bp_max=0, p_disconnected=0,
+                                     p_absent=0, expire_jitter_ns=0, sybil_first_node=n))
+    e.set_prop_tracking(False)
+    ms = pc.messages(n, 64, seed)
+    out, hop, _ = e.propagate(ms, pc.config(abi.GSX_ROUTER_FLOODSUB, credit=0), want_results=True)
+    reached = hop != 0xFF
+    assert out.deliveries == int(reached.sum()) - len(ms)  # each (node, message) reached at most once
+    assert out.transmissions == out.deliveries + out.duplicates
+    assert reached.mean() > 0.999
+    for k in range(2):
+        dist = _bfs(ov.row_ptr, ov.col.astype(np.int64), int(ms["source"][k]))
+        r = dist >= 0
+        assert np.array_equal(reached[k], r)
+        assert np.array_equal(hop[k][r].astype(np.int64), dist[r])
+
+
+@pytest.mark.timeout(1200)
+def test_cfg5_4m_adversarial_properties(gpu_ok):
+    n = 4_000_000
+    e = gsx.Engine(1)
+    ov = ac.setup(e, n, seed=23)
+    sc = e.scores()
+    syb = ac.sybil_pairs(ov)
+    vic = ac.victim_pairs(ov)
+    th = ac.TH.graylist_threshold
+    assert (sc[vic & syb] < th).all()  # P6 (colocation) + P4 (invalid spam) graylist the attackers
+    assert (sc[~syb] >= th).mean() > 0.75
+    obs = ov.pair_observer()
+    honest_node = ~ov.sybil
+    for k, tick in enumerate((59, 60)):
+        start = e.scores()
+        e.heartbeat(tick, ac.T0 + (2 + k) * S, 9)
+        e.refresh(ac.T0 + (2 + k) * S + 500 * abi.MILLISECOND)
+        inm = (e.export_state()["rec_flags"] & abi.GSX_REC_IN_MESH) != 0
+        # (A) prunes negative-score mesh peers and grafts only score >= 0; (B)
+        # accepts GRAFTs only from score >= 0 peers: a peer scoring below zero at
+        # the round start is in nobody's mesh at its end
+        assert not (inm & (start < 0)).any(), tick
+    # honest observers keep honest mesh peers (gossipsub_test.go:1755-1774: >= 3)
+    honest_links = inm & ~syb & honest_node[obs]
+    per_node = np.bincount(obs[honest_links], minlength=ov.n)
+    has3 = np.bincount(obs[~syb & honest_node[obs] & (start >= 0)], minlength=ov.n) >= 3
+    frac = (per_node[honest_node & has3] >= 3).mean()
+    assert frac > 0.95, frac
+    assert not (inm & syb & vic).any()  # no colocated sybil stays in a victim's mesh
