@@ -101,7 +101,7 @@ def test_cfg3_heartbeat_1m_x_8_matches_oracle(gpu_ok):
     del st
     cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=10)
     cfg.now_ns = T0 + 2 * S
-    ms = pc.messages(n, 4, seed)
+    ms = pc.messages(n, 4, 11)
     outs = [be.propagate(ms, cfg)[0].as_dict() for be in (e, o)]
     assert outs[0] == outs[1]
     for k, tick in enumerate((60, 61)):
