@@ -155,7 +155,7 @@ def test_cfg4_10m_floodsub_properties(gpu_ok):
                                      p_in_mesh=0.5, graft_window_ns=abi.HOUR, bp_max=0, p_disconnected=0,
                                      p_absent=0, expire_jitter_ns=0, sybil_first_node=n))
     e.set_prop_tracking(False)
-    ms = pc.messages(n, 64, seed)
+    ms = pc.messages(n, 64, 12)
     out, hop, _ = e.propagate(ms, pc.config(abi.GSX_ROUTER_FLOODSUB, credit=0), want_results=True)
     reached = hop != 0xFF
     assert out.deliveries == int(reached.sum()) - len(ms)  # each (node, message) reached at most once
