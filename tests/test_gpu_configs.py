@@ -181,6 +181,10 @@ def test_cfg5_4m_adversarial_properties(gpu_ok):
     assert (sc[~syb] >= th).mean() > 0.75
     obs = ov.pair_observer()
     honest_node = ~ov.sybil
+    # the reference test's honest peers score >= 0 (AppSpecificScore 0 and good
+    # deliveries, gossipsub_test.go:1680-1700): give every honest pair a positive
+    # application score, the sybils keep theirs (P6 + P4 negative)
+    e.set_app_scores(np.where(syb, 0.0, 1000.0))
     for k, tick in enumerate((59, 60)):
         start = e.scores()
         e.heartbeat(tick, ac.T0 + (2 + k) * S, 9)
@@ -195,5 +199,5 @@ def test_cfg5_4m_adversarial_properties(gpu_ok):
     per_node = np.bincount(obs[honest_links], minlength=ov.n)
     has3 = np.bincount(obs[~syb & honest_node[obs] & (start >= 0)], minlength=ov.n) >= 3
     frac = (per_node[honest_node & has3] >= 3).mean()
-    assert frac > 0.95, frac
+    assert frac > 0.99, frac
     assert not (inm & syb & vic).any()  # no colocated sybil stays in a victim's mesh
