@@ -236,7 +236,8 @@ hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStre
 hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st);
 
 // ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------
-constexpr int HB_MAX_DEG = 256;  // per-node pair count the mesh lanes hold (u16 offsets, scratch)
+constexpr int HB_LANE_DEG = 64;     // units up to this degree: one lane each, row staged in LDS
+constexpr int HB_HUB_MAX = 12000;   // hub rows (one wave each) live in dynamic LDS: 13 B per pair
 constexpr int64_t HEARTBEAT_INTERVAL_NS = 1000000000LL;  // GossipSubHeartbeatInterval (clearBackoff slack)
 constexpr uint8_t HB_GRAFT = 1, HB_PRUNE = 2;            // control bytes [topic][pair]
 enum {
@@ -285,7 +286,13 @@ struct HbState {
     uint8_t* inbox;       // per pair (u -> v): v sent GRAFT / PRUNE bits on (v -> u) this round (unsharded reads)
     uint8_t* answer;      // per pair (v -> u): u answered with PRUNE bits on (u -> v) this round
     unsigned long long* stats;
-    uint32_t* rngk;        // per node: draw counter after the maintenance of the current topic
+    uint32_t* rngk;        // [topic][node]: draw counter after the unit's maintenance (emitGossip continues it)
+    uint32_t* work;        // [topic][node]: units the scan found acting (lane-per-unit maintenance)
+    uint32_t* n_work;      // [topic]
+    uint32_t* hub_work;    // [topic][node]: acting units of nodes with more than HB_LANE_DEG peers
+    uint32_t* n_hub;       // [topic]
+    const uint32_t* hubs;  // nodes with more than HB_LANE_DEG peers (k_hb_recv_hub)
+    uint32_t n_hubs;
     uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)
     uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
     const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
@@ -304,13 +311,13 @@ struct HbState {
 };
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st);
-hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipStream_t st);
+hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st);
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
-                            uint32_t max_ids, hipStream_t st);
+                            uint32_t max_ids, int64_t max_deg, hipStream_t st);
 constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
-hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
                           uint64_t* out, hipStream_t st);
 

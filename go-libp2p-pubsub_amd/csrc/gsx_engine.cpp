@@ -105,6 +105,9 @@ struct gsx_engine {
     uint32_t *d_long = nullptr, *d_nlong = nullptr;
     unsigned long long* d_hbstats = nullptr;
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
+    uint32_t *d_work = nullptr, *d_nwork = nullptr, *d_hubwork = nullptr, *d_hubs = nullptr;  // heartbeat worklists
+    std::vector<uint32_t> hubs_host;  // nodes with more than HB_LANE_DEG pairs
+    std::vector<uint8_t> gossip_prev;  // per topic: IHAVE slots written last round
     uint64_t* d_ihave_hash = nullptr;
     bool have_gossip = false;
     bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
@@ -388,7 +391,8 @@ void free_state(gsx_engine* e) {
     e->send_counts.clear();
     e->n_recv = e->n_send = 0;
     e->d_col = nullptr;
-    void* hb[] = {e->d_backoff, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
+    void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs,
+                  e->d_backoff, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
@@ -399,6 +403,7 @@ void free_state(gsx_engine* e) {
     e->d_long = e->d_nlong = nullptr;
     e->d_hbstats = nullptr;
     e->d_rngk = e->d_ihave_len = nullptr;
+    e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_ihave_hash = nullptr;
     e->d_gb = nullptr;
     e->d_mc_digest = nullptr;
@@ -855,7 +860,11 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
     HIPCHK(e, hipMemsetAsync(e->d_ipcount, 0, sizeof(uint32_t) * (e->n_groups ? e->n_groups : 1), e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_backoff, 0, sizeof(int64_t) * e->T * (E ? E : 1), e->stream));
     e->max_deg = 0;
-    for (uint32_t i = 0; i < n_nodes; ++i) e->max_deg = std::max<int64_t>(e->max_deg, row_ptr[i + 1] - row_ptr[i]);
+    e->hubs_host.clear();
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+        e->max_deg = std::max<int64_t>(e->max_deg, row_ptr[i + 1] - row_ptr[i]);
+        if (row_ptr[i + 1] - row_ptr[i] > gsx::HB_LANE_DEG) e->hubs_host.push_back(i);
+    }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (E) HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * E, hipMemcpyHostToDevice));
     {  // reverse pairs for the pull-based propagation (NO_PAIR for remote neighbours until a shard plan)
@@ -2052,8 +2061,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     e->state_changed();
     if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
         return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
-    if (e->max_deg > gsx::HB_MAX_DEG)
-        return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_MAX_DEG) + " peers per node");
+    if (e->max_deg > gsx::HB_HUB_MAX)
+        return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_HUB_MAX) + " peers per node");
     const size_t TE = (size_t)e->T * e->E;
     if (!e->d_hbstats) {
         int rc = 0;
@@ -2061,11 +2070,19 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
             (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 3 * E)) ||
             (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
-            (rc = dalloc(e, &e->d_rngk, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
+            (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
+            (rc = dalloc(e, &e->d_work, (size_t)e->T * e->n_nodes)) ||
+            (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
+            (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
+            (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
             (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
             return rc;
         HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+        if (!e->hubs_host.empty())
+            HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
+                                     e->stream));
+        e->gossip_prev.assign(e->T, 0);
         e->hb_clean = false;
     }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
@@ -2094,6 +2111,12 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.graylist = e->th.graylist_threshold;
     h.gossip_threshold = e->th.gossip_threshold;
     h.rngk = e->d_rngk;
+    h.work = e->d_work;
+    h.n_work = e->d_nwork;
+    h.hub_work = e->d_hubwork;
+    h.n_hub = e->d_nwork + e->T;
+    h.hubs = e->d_hubs;
+    h.n_hubs = (uint32_t)e->hubs_host.size();
     h.ihave_len = e->d_ihave_len;
     h.ihave_hash = e->d_ihave_hash;
     h.pp = dev_peer_params(e);
@@ -2111,6 +2134,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                 e->gp.gossip_factor};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
     const size_t E8 = 8 * (e->E ? e->E : 1);
     // Unsharded, (B) and (C) clear the control words, answers and marks they
     // read, and nothing else is ever set: after one cleared round they stay
@@ -2174,16 +2198,23 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                  hipMemcpyHostToDevice, e->stream));
     }
     h.mc_digest = e->d_mc_digest;
-    if (e->have_gossip || !e->gb_host.empty()) {
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+    // IHAVE slots: a topic with gossip this round has its slots rewritten by
+    // k_hb_gossip; one that had gossip last round but none now is cleared here
+    for (uint32_t t = 0; t < e->T; ++t) {
+        const bool now_g = gb_off[t + 1] > gb_off[t] && max_ids[t] > 0;
+        if (!now_g && e->gossip_prev[t]) {
+            HIPCHK(e, hipMemsetAsync(e->d_ihave_len + (size_t)t * e->E, 0, 4 * e->E, e->stream));
+            HIPCHK(e, hipMemsetAsync(e->d_ihave_hash + (size_t)t * e->E, 0, 8 * e->E, e->stream));
+        }
+        e->gossip_prev[t] = now_g;
     }
     e->have_gossip = !e->gb_host.empty();
-    // (A) per topic, ascending: maintenance, then emitGossip
+    // (A) the scan of every unit, then per topic, ascending: maintenance, then emitGossip
+    HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
     for (uint32_t t = 0; t < e->T; ++t) {
-        HIPCHK(e, gsx::launch_hb_mesh(ds, h, t, e->stream));
+        HIPCHK(e, gsx::launch_hb_maintain(ds, h, t, e->max_deg, e->stream));
         HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
-                                        e->stream));
+                                        e->max_deg, e->stream));
     }
     // the receivers score the senders as the round left them
     HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the pairs (A) touched
@@ -2212,7 +2243,6 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded();
     HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
-    HIPCHK(e, gsx::launch_hb_mesh_links(ds, h, e->stream));
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));

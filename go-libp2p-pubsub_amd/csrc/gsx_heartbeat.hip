@@ -2,29 +2,37 @@
 // gossip as one synchronous round over the whole overlay (gsx.h,
 // gsx_heartbeat).
 //
-//  (A) per topic t ascending:
-//      k_hb_mesh — one lane per node v: the mesh maintenance of (v, t)
-//        (gossipsub.go:1344-1510).  Everything it touches — the records,
-//        backoff entries and control bits of v's own pairs for topic t —
-//        belongs to it alone.  Mesh and candidate lists are <= HB_MAX_DEG u16
-//        offsets in scratch.
-//      k_hb_gossip — one lane per node: emitGossip (:1669-1723).  The IHAVE
-//        list is the node's GetGossipIDs set (mcache.go:82-92) read straight
-//        from the cached batches' seen words; its order is never observable
+//  (A) k_hb_scan — one coalesced pass over every wave's 64 nodes' pairs counts
+//        each (node, topic) unit's mesh, negative-score and outbound members
+//        and lists the units where some step of the maintenance can act
+//        (per topic; hub nodes apart).  Then per topic t ascending:
+//      k_hb_maintain — one lane per listed unit, its row (scores and
+//        mesh / candidate / outbound / backoff bits) and its mesh and candidate
+//        lists staged in LDS: the mesh maintenance of (v, t)
+//        (gossipsub.go:1344-1510); k_hb_maintain_hub — the same for nodes
+//        with more than HB_LANE_DEG peers, one wave each, the row in dynamic
+//        LDS.  Everything a unit touches — the records, backoff entries and
+//        control bits of v's own pairs for topic t — belongs to it alone.
+//      k_hb_gossip — emitGossip (:1669-1723): a coalesced pass over each
+//        wave's pairs stages the IHAVE target eligibility in LDS and rewrites
+//        the topic's IHAVE slots, then one lane per node.  The IHAVE list is
+//        the node's GetGossipIDs set (mcache.go:82-92) read straight from the
+//        cached batches' seen words; its order is never observable
 //        (handleIHave collects ids into a map, :641-650), so an untruncated
-//        list is reported by its length and multiset digest and its shuffle
-//        only advances the draw stream.  Nodes whose list exceeds
-//        MaxIHaveLength (per-target reshuffle + truncation, :1708-1716) are
-//        queued for k_hb_gossip_long, one wave per node with the list in LDS.
-//  (B) k_hb_recv: one lane per receiving node u, senders in ascending order
-//      (the Dhi check reads the mesh size the previous accepts left):
+//        list is reported by its length and multiset digest.  Nodes whose
+//        list exceeds MaxIHaveLength (per-target reshuffle + truncation,
+//        :1708-1716), or whose tile holds a hub row, go to k_hb_gossip_long,
+//        one wave per node with the list in LDS.
+//  (B) k_hb_recv: one lane per receiving node u (k_hb_recv_hub: one wave per
+//      hub), senders in ascending order (the Dhi check reads the mesh size the
+//      previous accepts and prunes left, a running count per topic):
 //      handleGraft / handlePrune, :718-843, AcceptFrom-gated (:582-593).
 //  (C) k_hb_answer: one lane per pair, the GRAFT senders' handlePrune of the
 //      PRUNE answers.
 // Control messages are per-pair topic bitmasks (bit t of a u64), so a
 // receiver reads one word per sender.  Round counters are summed per wave
-// before one atomic each.  Integer/byte work with scattered reads of the
-// per-pair score cache: latency-bound, no MFMA/LDS tiling applies.
+// before one atomic each; the in-mesh link count is the scan's plus every
+// step's change.  Integer/byte work: HBM / latency bound, no MFMA.
 #include "gsx_ops.h"
 
 namespace gsx {
@@ -69,17 +77,60 @@ __global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint64_t n)
     flush_count(h.stats, HB_BACKOFF_CLEARED, cleared);
 }
 
+// ---- (A) mesh maintenance ---------------------------------------------------------
+// The round starts with one scan of every (node, topic) unit (k_hb_scan): a
+// coalesced pass over each wave's 64 nodes' pairs counts, per unit, its mesh,
+// the negative-score and outbound peers in it; units where no step of
+// maintain() can act (a steady mesh: no negative score, Dlo <= |mesh| <= Dhi,
+// enough outbound peers, not an opportunistic-graft tick) draw nothing and are
+// done.  The others go to the topic's worklist — or to its hub list when the
+// node has more than HB_LANE_DEG peers.  Per topic (ascending) k_hb_maintain
+// then runs maintain() one lane per unit with the unit's row staged in LDS
+// (scores, mesh / candidate / outbound / backoff bits; the mesh and candidate
+// lists live in LDS too), and k_hb_maintain_hub one wave per hub unit with
+// its row in dynamic LDS.  Only topic t's records, backoff entries and
+// control bits of the node's own pairs change, so the scan's decisions for
+// later topics stay valid, and every unit is independent of the others.
+
+// Staged pair bits (u8, LDS)
+constexpr uint8_t ST_MESH = 1;     // present and in the topic's mesh (gs.mesh[topic][p])
+constexpr uint8_t ST_CAND = 2;     // present, connected, mesh-capable, not direct: getPeers' base filter
+constexpr uint8_t ST_OUT = 4;      // outbound (gs.outbound[p])
+constexpr uint8_t ST_BACKOFF = 8;  // gs.backoff[topic][p] present (map presence, :1377)
+
+__device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
+    const uint8_t pf = s.pflags[r], ef = h.eflags[r];
+    uint8_t f = 0;
+    if ((pf & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH)) f |= ST_MESH;
+    if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) &&
+        !(ef & EDGE_DIRECT))
+        f |= ST_CAND;
+    if (ef & EDGE_OUTBOUND) f |= ST_OUT;
+    // only a candidate's backoff is ever tested (a pruned mesh peer gets the bit when pruned)
+    if ((f & ST_CAND) && !(f & ST_MESH) && h.backoff[(size_t)t * h.n_pairs + r] != 0) f |= ST_BACKOFF;
+    return f;
+}
+
+// One unit (v, t) over its staged row: sc / fl are the row's scores and bits,
+// la / lb two lists of row offsets (deg entries each).  Indices are u16: the
+// heartbeat refuses rows longer than HB_HUB_MAX.
 struct HbUnit {
     const DevState& s;
     const HbState& h;
     uint32_t t;
     int64_t r0;  // first pair of the row
     int deg;
+    const double* sc;
+    uint8_t* fl;
+    uint16_t* la;
+    uint16_t* lb;
+    bool scored;  // the topic has score params: Graft / Prune traces set / clear inMesh
     uint64_t grafts = 0, prunes = 0;
+    int64_t links = 0;  // in-mesh (pair, topic) delta
 
-    __device__ bool in_mesh(int i) const { return hb_in_mesh(s, r0 + i, t); }
-    __device__ uint8_t ef(int i) const { return h.eflags[r0 + i]; }
-    __device__ double score(int i) const { return s.score[r0 + i]; }
+    __device__ bool in_mesh(int i) const { return fl[i] & ST_MESH; }
+    __device__ double score(int i) const { return sc[i]; }
+    __device__ bool outbound(int i) const { return fl[i] & ST_OUT; }
 
     __device__ int mesh_list(uint16_t* out) const {
         int n = 0;
@@ -95,17 +146,12 @@ struct HbUnit {
                              Rng& g) const {
         int n = 0;
         for (int i = 0; i < deg; ++i) {
-            const uint64_t r = r0 + i;
-            if ((s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED)) continue;
-            const uint8_t f = ef(i);
-            if (!(f & EDGE_GOSSIPSUB)) continue;
-            if (in_mesh(i)) continue;
-            if (h.backoff[(size_t)t * h.n_pairs + r] != 0) continue;  // map presence (:1377)
-            if (f & EDGE_DIRECT) continue;
-            if (outbound_only && !(f & EDGE_OUTBOUND)) continue;
-            const double sc = score(i);
-            if (score_cmp == 0 && !(sc >= ref)) continue;
-            if (score_cmp == 1 && !(sc > ref)) continue;
+            const uint8_t f = fl[i];
+            if ((f & (ST_CAND | ST_MESH | ST_BACKOFF)) != ST_CAND) continue;
+            if (outbound_only && !(f & ST_OUT)) continue;
+            const double x = sc[i];
+            if (score_cmp == 0 && !(x >= ref)) continue;
+            if (score_cmp == 1 && !(x > ref)) continue;
             out[n++] = (uint16_t)i;
         }
         g.shuffle(out, n);
@@ -121,14 +167,23 @@ struct HbUnit {
     __device__ void graft(int i) {  // graftPeer, :1353-1359
         const uint64_t r = r0 + i;
         ev_graft(s, r, t, h.now);
+        if (scored) {  // (a topic without params keeps no inMesh flag)
+            fl[i] |= ST_MESH;
+            ++links;
+        }
         h.ctl_graft[r] |= 1ull << t;
         h.dirty[r] = 1;
         mark_inbox(r);
         ++grafts;
     }
-    __device__ void prune(int i) {  // prunePeer, :1345-1351
+    __device__ void prune(int i) {  // prunePeer, :1345-1351 (only mesh peers are pruned)
         const uint64_t r = r0 + i;
         ev_prune(s, r, t);
+        if (scored) {  // (an unscored topic's imported inMesh flag stays, as in the record)
+            fl[i] &= ~ST_MESH;
+            --links;
+        }
+        fl[i] |= ST_BACKOFF;
         add_backoff(h, r, t, h.gp.prune_backoff_ns);
         h.ctl_prune[r] |= 1ull << t;
         h.dirty[r] = 1;
@@ -136,18 +191,41 @@ struct HbUnit {
         ++prunes;
     }
 
-    // stable insertion sort by cached score
-    __device__ void sort_by_score(uint16_t* a, int n, bool desc) const {
-        for (int i = 1; i < n; ++i) {
-            const uint16_t x = a[i];
-            const double sx = score(x);
-            int j = i - 1;
-            while (j >= 0 && (desc ? score(a[j]) < sx : score(a[j]) > sx)) {
-                a[j + 1] = a[j];
-                --j;
+    // stable sort by score (desc or asc) — the unstable sort.Slice of
+    // :1393 / :1489 after the shuffle, made stable (gsx.h).  Insertion sort for
+    // short lists, bottom-up merge sort (through `buf`) for long ones; both
+    // keep equal scores in list order, so they agree exactly.
+    __device__ bool before(uint16_t a, uint16_t b, bool desc) const {  // a strictly ahead of b
+        return desc ? sc[a] > sc[b] : sc[a] < sc[b];
+    }
+    __device__ void sort_by_score(uint16_t* a, int n, bool desc, uint16_t* buf) const {
+        if (n <= 32) {
+            for (int i = 1; i < n; ++i) {
+                const uint16_t x = a[i];
+                int j = i - 1;
+                while (j >= 0 && before(x, a[j], desc)) {
+                    a[j + 1] = a[j];
+                    --j;
+                }
+                a[j + 1] = x;
             }
-            a[j + 1] = x;
+            return;
         }
+        uint16_t *src = a, *dst = buf;
+        for (int w = 1; w < n; w *= 2) {
+            for (int lo = 0; lo < n; lo += 2 * w) {
+                const int mid = min(lo + w, n), hi = min(lo + 2 * w, n);
+                int i = lo, j = mid, k = lo;
+                while (i < mid && j < hi) dst[k++] = before(src[j], src[i], desc) ? src[j++] : src[i++];
+                while (i < mid) dst[k++] = src[i++];
+                while (j < hi) dst[k++] = src[j++];
+            }
+            uint16_t* x = src;
+            src = dst;
+            dst = x;
+        }
+        if (src != a)
+            for (int i = 0; i < n; ++i) a[i] = src[i];
     }
 
     __device__ static void rotate(uint16_t* a, int i) {  // :1411-1418
@@ -158,7 +236,8 @@ struct HbUnit {
 
     __device__ void maintain(Rng& g) {
         const DevGossipParams& gp = h.gp;
-        uint16_t plst[HB_MAX_DEG], tmp[HB_MAX_DEG];
+        uint16_t* plst = la;
+        uint16_t* tmp = lb;
         // drop all peers with negative score, without PX (:1361-1368)
         int n = mesh_list(plst);
         for (int i = 0; i < n; ++i)
@@ -173,23 +252,23 @@ struct HbUnit {
         n = mesh_list(plst);
         if (n > gp.d_hi) {
             g.shuffle(plst, n);
-            sort_by_score(plst, n, true);
+            sort_by_score(plst, n, true, tmp);
             g.shuffle(plst + gp.d_score, n - gp.d_score);
-            int outbound = 0;
+            int outb = 0;
             for (int i = 0; i < gp.d; ++i)
-                if (ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
-            if (outbound < gp.d_out) {
-                if (outbound > 0) {
-                    int ihave = outbound;
+                if (outbound(plst[i])) ++outb;
+            if (outb < gp.d_out) {
+                if (outb > 0) {
+                    int ihave = outb;
                     for (int i = 1; i < gp.d && ihave > 0; ++i)
-                        if (ef(plst[i]) & EDGE_OUTBOUND) {
+                        if (outbound(plst[i])) {
                             rotate(plst, i);
                             --ihave;
                         }
                 }
-                int ineed = gp.d_out - outbound;
+                int ineed = gp.d_out - outb;
                 for (int i = gp.d; i < n && ineed > 0; ++i)
-                    if (ef(plst[i]) & EDGE_OUTBOUND) {
+                    if (outbound(plst[i])) {
                         rotate(plst, i);
                         --ineed;
                     }
@@ -199,18 +278,18 @@ struct HbUnit {
         // do we have enough outbound peers? (:1450-1476)
         n = mesh_list(plst);
         if (n >= gp.d_lo) {
-            int outbound = 0;
+            int outb = 0;
             for (int i = 0; i < n; ++i)
-                if (ef(plst[i]) & EDGE_OUTBOUND) ++outbound;
-            if (outbound < gp.d_out) {
-                const int k = get_peers(gp.d_out - outbound, true, 0, 0.0, tmp, g);
+                if (outbound(plst[i])) ++outb;
+            if (outb < gp.d_out) {
+                const int k = get_peers(gp.d_out - outb, true, 0, 0.0, tmp, g);
                 for (int i = 0; i < k; ++i) graft(tmp[i]);
             }
         }
         // opportunistic grafting (:1478-1510)
         n = mesh_list(plst);
         if (gp.og_ticks && h.tick % gp.og_ticks == 0 && n > 1) {
-            sort_by_score(plst, n, false);
+            sort_by_score(plst, n, false, tmp);
             const double median = score(plst[n / 2]);
             if (median < h.og_threshold) {
                 const int k = get_peers(gp.og_peers, false, 1, median, tmp, g);
@@ -226,73 +305,186 @@ __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, 
     return Rng{h.seed, TAG_HEARTBEAT, (uint64_t)h.node_lo + v, (h.tick << 32) | ((uint64_t)t << 24), k};
 }
 
-// One launch per topic, ascending: the maintenance of (v, t) for every v.
-// A wave takes 64 consecutive nodes.  One pass over their pairs — coalesced,
-// lane j reading pairs j, j + 64, ... of the wave's contiguous pair range,
-// counted into the owner's LDS slot — decides whether any step of
-// maintain() acts (a steady mesh: no negative score, Dlo <= |mesh| <= Dhi,
-// enough outbound peers, not an opportunistic-graft tick); such a unit draws
-// nothing and is done.  A graft step with no candidate (getPeers over an
-// empty list) draws nothing either.  Lanes whose unit acts then run
-// maintain() over their own row.
-__global__ __launch_bounds__(64) void k_hb_mesh(DevState s, HbState h, uint32_t t) {
-    __shared__ int64_t rs[65];    // row starts of the wave's nodes, rs[nv] = end
-    __shared__ int cnt[5][64];    // per node: |mesh|, negative, outbound in mesh, candidates, outbound candidates
-    uint64_t grafts = 0, prunes = 0;
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  // exclusive
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    return incl - x;
+}
+
+// Appends the lanes with `want` to list[0 ..) (count in *n): one atomic per wave.
+__device__ __forceinline__ void wave_append(bool want, uint32_t value, uint32_t* list, uint32_t* n, uint32_t lane) {
+    const uint64_t b = __ballot(want);
+    if (!b) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(n, (uint32_t)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (want) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1))] = value;
+}
+
+constexpr int SCAN_TOPICS = 8;  // topics counted per pass over a wave's pairs
+
+// (A) scan: every unit of every topic; worklists, rngk = 0, mesh links before the round.
+__global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
+    __shared__ int64_t rs[65];
+    __shared__ int cnt[SCAN_TOPICS][3][64];  // |mesh|, negative in mesh, outbound in mesh
     const DevGossipParams& gp = h.gp;
     const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
     const uint32_t lane = threadIdx.x;
+    const uint32_t T = s.n_topics;
+    uint64_t links = 0;
     for (uint32_t v0 = blockIdx.x * 64u; v0 < h.n_nodes; v0 += gridDim.x * 64u) {
         const uint32_t nv = min(64u, h.n_nodes - v0);
         rs[lane] = h.row_ptr[v0 + min(lane, nv)];
         if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) cnt[k][lane] = 0;
         __syncthreads();
         const int64_t pa = rs[0], pb = rs[64];
-        for (int64_t r = pa + lane; r < pb; r += 64) {
-            int lo = 0, hi = (int)nv;  // owner: rs[lo] <= r < rs[lo + 1]
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (rs[mid] <= r) lo = mid;
-                else hi = mid;
+        const uint32_t v = v0 + lane;
+        const int deg = lane < nv ? (int)(rs[lane + 1] - rs[lane]) : 0;
+        for (uint32_t t0 = 0; t0 < T; t0 += SCAN_TOPICS) {
+            const uint32_t nt = min((uint32_t)SCAN_TOPICS, T - t0);
+            for (uint32_t k = 0; k < nt; ++k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) cnt[k][c][lane] = 0;
+            __syncthreads();
+            for (int64_t r = pa + lane; r < pb; r += 64) {
+                if (!(s.pflags[r] & PAIR_PRESENT)) continue;
+                int lo = 0, hi = (int)nv;  // owner: rs[lo] <= r < rs[lo + 1]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (rs[mid] <= r) lo = mid;
+                    else hi = mid;
+                }
+                uint8_t rf[SCAN_TOPICS];
+#pragma unroll
+                for (int k = 0; k < SCAN_TOPICS; ++k)
+                    rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, T)] : 0;
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < SCAN_TOPICS; ++k) any |= (rf[k] & REC_IN_MESH) != 0;
+                if (!any) continue;
+                const bool neg = s.score[r] < 0;
+                const bool outb = h.eflags[r] & EDGE_OUTBOUND;
+#pragma unroll
+                for (int k = 0; k < SCAN_TOPICS; ++k)
+                    if (rf[k] & REC_IN_MESH) {
+                        atomicAdd(&cnt[k][0][lo], 1);
+                        if (neg) atomicAdd(&cnt[k][1][lo], 1);
+                        if (outb) atomicAdd(&cnt[k][2][lo], 1);
+                    }
             }
-            const uint8_t f = h.eflags[r];
-            const uint8_t pf = s.pflags[r];
-            if ((pf & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH)) {
-                atomicAdd(&cnt[0][lo], 1);
-                if (s.score[r] < 0) atomicAdd(&cnt[1][lo], 1);
-                if (f & EDGE_OUTBOUND) atomicAdd(&cnt[2][lo], 1);
-            } else if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
-                       (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && h.backoff[(size_t)t * h.n_pairs + r] == 0 &&
-                       s.score[r] >= 0.0) {  // getPeers' filter of the graft steps (:1370-1385, :1450-1476)
-                atomicAdd(&cnt[3][lo], 1);
-                if (f & EDGE_OUTBOUND) atomicAdd(&cnt[4][lo], 1);
+            __syncthreads();
+            for (uint32_t k = 0; k < nt; ++k) {
+                const uint32_t t = t0 + k;
+                bool active = false;
+                if (lane < nv) {
+                    const int n = cnt[k][0][lane], neg = cnt[k][1][lane], outb = cnt[k][2][lane];
+                    links += (uint64_t)n;
+                    // a unit below Dlo or short of outbound peers acts only if it has a
+                    // candidate; maintain() finds none otherwise and draws nothing
+                    active = neg > 0 || n > gp.d_hi || (og_tick && n > 1) || n < gp.d_lo || outb < gp.d_out;
+                    h.rngk[(size_t)t * h.n_nodes + v] = 0;
+                }
+                wave_append(active && deg <= HB_LANE_DEG, v, h.work + (size_t)t * h.n_nodes, h.n_work + t, lane);
+                wave_append(active && deg > HB_LANE_DEG, v, h.hub_work + (size_t)t * h.n_nodes, h.n_hub + t, lane);
             }
+            __syncthreads();  // cnt is rewritten by the next topic chunk / tile
         }
-        __syncthreads();
-        if (lane < nv) {
-            const uint32_t v = v0 + lane;
-            const int n = cnt[0][lane], neg = cnt[1][lane], outb = cnt[2][lane];
-            const int cand = cnt[3][lane], cand_out = cnt[4][lane];
-            const bool grow = n < gp.d_lo && cand > 0;                               // :1370-1385
-            const bool outbound = n >= gp.d_lo && outb < gp.d_out && cand_out > 0;  // :1450-1476
-            if (!neg && n <= gp.d_hi && !grow && !outbound && !(og_tick && n > 1)) {
-                h.rngk[v] = 0;
-            } else {
-                const int64_t r0 = rs[lane];
-                HbUnit U{s, h, t, r0, (int)(rs[lane + 1] - r0)};
+    }
+    flush_count(h.stats, HB_MESH_LINKS, links);
+}
+
+constexpr int HB_STAGE = 1024;  // pairs a lane-per-unit wave stages at once
+
+// (A) per topic: the listed units, one lane each, rows staged in LDS.  A wave
+// takes 64 units; when their rows exceed the stage, it runs them in windows
+// of whole rows.
+__global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint32_t t) {
+    __shared__ double sc[HB_STAGE];
+    __shared__ uint8_t fl[HB_STAGE];
+    __shared__ uint16_t la[HB_STAGE], lb[HB_STAGE];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nw = h.n_work[t];
+    const uint32_t* work = h.work + (size_t)t * h.n_nodes;
+    const bool scored = t < s.n_topics && s.tp[t].scored;
+    uint64_t grafts = 0, prunes = 0;
+    int64_t links = 0;
+    for (uint32_t c0 = blockIdx.x * 64u; c0 < nw; c0 += gridDim.x * 64u) {
+        const bool valid = c0 + lane < nw;
+        const uint32_t v = valid ? work[c0 + lane] : 0;
+        const int64_t r0 = valid ? h.row_ptr[v] : 0;
+        const int deg = valid ? (int)(h.row_ptr[v + 1] - r0) : 0;
+        const uint32_t off = wave_prefix((uint32_t)deg, lane);
+        bool done = !valid;
+        uint32_t base = 0;
+        while (__ballot(!done)) {
+            if (!done && off >= base && off + deg <= base + HB_STAGE) {
+                const uint32_t o = off - base;
+                for (int i = 0; i < deg; ++i) {
+                    sc[o + i] = s.score[r0 + i];
+                    fl[o + i] = stage_bits(s, h, r0 + i, t);
+                }
+                HbUnit U{s, h, t, r0, deg, sc + o, fl + o, la + o, lb + o, scored};
                 Rng g = hb_rng(h, v, t, 0);
                 U.maintain(g);
-                h.rngk[v] = g.k;  // emitGossip continues this (node, topic) draw stream
+                h.rngk[(size_t)t * h.n_nodes + v] = g.k;  // emitGossip continues this (node, topic) draw stream
                 grafts += U.grafts;
                 prunes += U.prunes;
+                links += U.links;
+                done = true;
             }
+            // the next window starts at the lowest row not yet run
+            uint32_t mo = done ? 0xFFFFFFFFu : off;
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) mo = min(mo, (uint32_t)__shfl_xor((int)mo, sh, 64));
+            base = mo;
         }
-        __syncthreads();  // rs / cnt are rewritten by the next wave-tile
     }
     flush_count(h.stats, HB_GRAFTS, grafts);
     flush_count(h.stats, HB_PRUNES, prunes);
+    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
+}
+
+// (A) per topic: hub units (more than HB_LANE_DEG peers), one wave each, the
+// row in dynamic LDS (13 B per pair); the wave stages it, lane 0 runs maintain().
+__global__ __launch_bounds__(64) void k_hb_maintain_hub(DevState s, HbState h, uint32_t t) {
+    extern __shared__ double dyn[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nw = h.n_hub[t];
+    const uint32_t* work = h.hub_work + (size_t)t * h.n_nodes;
+    const bool scored = t < s.n_topics && s.tp[t].scored;
+    uint64_t grafts = 0, prunes = 0;
+    int64_t links = 0;
+    for (uint32_t w = blockIdx.x; w < nw; w += gridDim.x) {
+        const uint32_t v = work[w];
+        const int64_t r0 = h.row_ptr[v];
+        const int deg = (int)(h.row_ptr[v + 1] - r0);
+        double* sc = dyn;
+        uint16_t* la = reinterpret_cast<uint16_t*>(sc + deg);
+        uint16_t* lb = la + deg;
+        uint8_t* fl = reinterpret_cast<uint8_t*>(lb + deg);
+        for (int i = lane; i < deg; i += 64) {
+            sc[i] = s.score[r0 + i];
+            fl[i] = stage_bits(s, h, r0 + i, t);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            HbUnit U{s, h, t, r0, deg, sc, fl, la, lb, scored};
+            Rng g = hb_rng(h, v, t, 0);
+            U.maintain(g);
+            h.rngk[(size_t)t * h.n_nodes + v] = g.k;
+            grafts += U.grafts;
+            prunes += U.prunes;
+            links += U.links;
+        }
+        __syncthreads();  // the LDS row is restaged by the next unit
+    }
+    flush_count(h.stats, HB_GRAFTS, grafts);
+    flush_count(h.stats, HB_PRUNES, prunes);
+    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
 }
 
 // ---- emitGossip (gossipsub.go:1669-1723) --------------------------------------
@@ -312,76 +504,104 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
+// GetGossipIDs of (v, t): its length and multiset digest, straight from the
+// cached batches' seen words.
+__device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, const GossipBatch* __restrict__ gb,
+                                               uint32_t n_gb, uint64_t& dig) {
+    uint32_t L = 0;
+    dig = 0;
+    for (uint32_t b = 0; b < n_gb; ++b) {
+        const GossipBatch B = gb[b];
+        for (uint32_t w = 0; w < B.n_words; ++w) {
+            uint64_t word = B.seen[(size_t)v * B.n_words + w];
+            L += (uint32_t)__popcll(word);
+            // a node holding every message of the word (the common case once a
+            // batch has spread) adds the word's precomputed digest sum
+            const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
+            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+            if (word && word == full) {
+                dig += h.mc_digest[B.wdig_base + w];
+                continue;
+            }
+            while (word) {
+                dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
+                word &= word - 1;
+            }
+        }
+    }
+    return L;
+}
+
+// emitGossip of topic t for every node.  A wave takes 64 consecutive nodes:
+// one coalesced pass over their pairs rewrites the topic's IHAVE slots of the
+// range (0 = none) and stages each pair's target eligibility in LDS; then a
+// lane per node counts its GetGossipIDs, lists its eligible peers in LDS,
+// shuffles and writes the targets.  A tile whose rows exceed the stage, and
+// every list longer than MaxIHaveLength (per-target reshuffle + truncation,
+// :1708-1716), goes to k_hb_gossip_long, one wave per node.
 __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
                                                   uint32_t n_gb) {
+    __shared__ int64_t rs[65];
+    __shared__ uint8_t el[HB_STAGE];
+    __shared__ uint16_t pl[HB_STAGE];
     uint64_t msgs = 0, ids = 0;
-    for (uint32_t v = blockIdx.x * 64u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 64u) {
-        // GetGossipIDs of (v, t): its length and multiset digest
-        uint32_t L = 0;
-        uint64_t dig = 0;
-        for (uint32_t b = 0; b < n_gb; ++b) {
-            const GossipBatch B = gb[b];
-            for (uint32_t w = 0; w < B.n_words; ++w) {
-                uint64_t word = B.seen[(size_t)v * B.n_words + w];
-                L += (uint32_t)__popcll(word);
-                // a node holding every message of the word (the common case once a
-                // batch has spread) adds the word's precomputed digest sum
-                const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
-                const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
-                if (word && word == full) {
-                    dig += h.mc_digest[B.wdig_base + w];
-                    continue;
-                }
-                while (word) {
-                    dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
-                    word &= word - 1;
+    const uint32_t lane = threadIdx.x;
+    const size_t tslot = (size_t)t * h.n_pairs;
+    for (uint32_t v0 = blockIdx.x * 64u; v0 < h.n_nodes; v0 += gridDim.x * 64u) {
+        const uint32_t nv = min(64u, h.n_nodes - v0);
+        rs[lane] = h.row_ptr[v0 + min(lane, nv)];
+        if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+        __syncthreads();
+        const int64_t pa = rs[0], pb = rs[64];
+        const bool staged = pb - pa <= HB_STAGE;
+        for (int64_t r = pa + lane; r < pb; r += 64) {
+            h.ihave_len[tslot + r] = 0;
+            h.ihave_hash[tslot + r] = 0;
+            if (staged) el[r - pa] = gossip_target(s, h, r, t);
+        }
+        __syncthreads();
+        if (lane < nv) {
+            const uint32_t v = v0 + lane;
+            uint64_t dig;
+            const uint32_t L = gossip_ids(h, v, gb, n_gb, dig);
+            if (L > 0) {  // emitGossip returns early on an empty list, drawing nothing
+                if (!staged || L > (uint32_t)h.gp.max_ihave) {
+                    h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // one wave per node: k_hb_gossip_long
+                } else {
+                    const uint32_t o = (uint32_t)(rs[lane] - pa);
+                    const int deg = (int)(rs[lane + 1] - rs[lane]);
+                    uint16_t* peers = pl + o;
+                    int np = 0;
+                    for (int i = 0; i < deg; ++i)
+                        if (el[o + i]) peers[np++] = (uint16_t)i;
+                    int target = h.gp.d_lazy;
+                    const int factor = (int)(h.gp.gossip_factor * (double)np);
+                    if (factor > target) target = factor;
+                    const bool shuffle_peers = target <= np;
+                    if (!shuffle_peers) target = np;
+                    if (target > 0) {
+                        if (shuffle_peers) {  // an untruncated list is not shuffled (its order is never observable)
+                            Rng g = hb_rng(h, v, t, h.rngk[(size_t)t * h.n_nodes + v]);
+                            g.shuffle(peers, np);
+                        }
+                        for (int p = 0; p < target; ++p) {
+                            const size_t x = tslot + rs[lane] + peers[p];
+                            h.ihave_len[x] = L;
+                            h.ihave_hash[x] = dig;
+                        }
+                        msgs += (uint64_t)target;
+                        ids += (uint64_t)target * L;
+                    }
                 }
             }
         }
-        if (L > 0) {  // emitGossip returns early on an empty list, drawing nothing
-            const int64_t r0 = h.row_ptr[v];
-            const int deg = (int)(h.row_ptr[v + 1] - r0);
-            uint16_t peers[HB_MAX_DEG];
-            int np = 0;
-            for (int i = 0; i < deg; ++i)
-                if (gossip_target(s, h, r0 + i, t)) peers[np++] = (uint16_t)i;
-            int target = h.gp.d_lazy;
-            const int factor = (int)(h.gp.gossip_factor * (double)np);
-            if (factor > target) target = factor;
-            const bool shuffle_peers = target <= np;
-            if (!shuffle_peers) target = np;
-            if (target > 0 && L > (uint32_t)h.gp.max_ihave) {
-                h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // per-target truncation: k_hb_gossip_long
-            } else if (target > 0) {
-                if (shuffle_peers) {  // an untruncated list is not shuffled (its order is never observable)
-                    Rng g = hb_rng(h, v, t, h.rngk[v]);
-                    g.shuffle(peers, np);
-                }
-                for (int p = 0; p < target; ++p) {
-                    const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
-                    h.ihave_len[x] = L;
-                    h.ihave_hash[x] = dig;
-                }
-                msgs += (uint64_t)target;
-                ids += (uint64_t)target * L;
-            }
-        }
+        __syncthreads();  // rs / el / pl are rewritten by the next tile
     }
     flush_count(h.stats, HB_IHAVE_MSGS, msgs);
     flush_count(h.stats, HB_IHAVE_IDS, ids);
 }
 
 // ---- lists longer than MaxIHaveLength: one wave per queued node -------------
-
-__device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  // exclusive
-    uint32_t incl = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= (uint32_t)off) incl += y;
-    }
-    return incl - x;
-}
 
 // shuffleStrings of a[0..L) in LDS; g is wave-uniform.  64 Int31s are drawn
 // at once (one per lane, Go's rejection rule resolved by a ballot); lane 0
@@ -419,14 +639,19 @@ __device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uin
     }
 }
 
+// One wave per queued node: lists longer than MaxIHaveLength, and nodes of
+// tiles whose rows did not fit the stage.  Dynamic LDS: the message slots
+// (max_ids u32, GetGossipIDs order) then the eligible peers (max_deg u16).
 __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, uint32_t t,
-                                                       const GossipBatch* __restrict__ gb, uint32_t n_gb) {
+                                                       const GossipBatch* __restrict__ gb, uint32_t n_gb,
+                                                       uint32_t max_ids) {
     extern __shared__ uint32_t mids[];  // message slots, GetGossipIDs order
-    __shared__ uint16_t peers[HB_MAX_DEG];
+    uint16_t* peers = reinterpret_cast<uint16_t*>(mids + max_ids);
     __shared__ int32_t jbuf[64];
     __shared__ uint32_t kshare;
     const uint32_t lane = threadIdx.x;
     const uint32_t n_long = *h.n_long;
+    const size_t tslot = (size_t)t * h.n_pairs;
     uint64_t msgs = 0, ids = 0;
     for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
         const uint32_t v = h.long_nodes[li];
@@ -447,8 +672,9 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
             }
         }
         __syncthreads();
-        Rng g = hb_rng(h, v, t, h.rngk[v]);
-        wave_shuffle(mids, L, g, jbuf, lane);
+        const uint32_t maxl = (uint32_t)h.gp.max_ihave;
+        Rng g = hb_rng(h, v, t, h.rngk[(size_t)t * h.n_nodes + v]);
+        if (L > maxl) wave_shuffle(mids, L, g, jbuf, lane);  // shuffleStrings, then truncation (:1708-1716)
         const int64_t r0 = h.row_ptr[v];
         const int deg = (int)(h.row_ptr[v + 1] - r0);
         int np = 0;
@@ -473,21 +699,35 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
             __syncthreads();
             g.k = kshare;
         }
-        const uint32_t len = (uint32_t)h.gp.max_ihave;  // L > MaxIHaveLength here
-        for (int p = 0; p < target; ++p) {
-            wave_shuffle(mids, L, g, jbuf, lane);
+        if (L <= maxl) {  // the whole list to every target
             uint64_t d = 0;
-            for (uint32_t e = lane; e < len; e += 64) d += h.mc_digest[mids[e]];
+            for (uint32_t e = lane; e < L; e += 64) d += h.mc_digest[mids[e]];
             d = wave_sum64(d);
-            if (lane == 0) {
-                const size_t x = (size_t)t * h.n_pairs + r0 + peers[p];
-                h.ihave_len[x] = len;
+            for (int p = lane; p < target; p += 64) {
+                const size_t x = tslot + r0 + peers[p];
+                h.ihave_len[x] = L;
                 h.ihave_hash[x] = d;
             }
-        }
-        if (lane == 0) {
-            msgs += (uint64_t)target;
-            ids += (uint64_t)target * len;
+            if (lane == 0) {
+                msgs += (uint64_t)target;
+                ids += (uint64_t)target * L;
+            }
+        } else {
+            for (int p = 0; p < target; ++p) {
+                wave_shuffle(mids, L, g, jbuf, lane);
+                uint64_t d = 0;
+                for (uint32_t e = lane; e < maxl; e += 64) d += h.mc_digest[mids[e]];
+                d = wave_sum64(d);
+                if (lane == 0) {
+                    const size_t x = tslot + r0 + peers[p];
+                    h.ihave_len[x] = maxl;
+                    h.ihave_hash[x] = d;
+                }
+            }
+            if (lane == 0) {
+                msgs += (uint64_t)target;
+                ids += (uint64_t)target * maxl;
+            }
         }
         __syncthreads();
     }
@@ -499,36 +739,58 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
 
 // handlePrune at the owner of pair q for topic t (:811-843): the tracer's
 // Prune, then the PRUNE's backoff, which travels in whole seconds (:1821).
-__device__ __forceinline__ void handle_prune(const DevState& s, const HbState& h, uint64_t q, uint32_t t) {
+// Returns whether it removed a mesh link.
+__device__ __forceinline__ bool handle_prune(const DevState& s, const HbState& h, uint64_t q, uint32_t t) {
+    const bool was = hb_in_mesh(s, q, t) && scored_topic(s, q, t);
     ev_prune(s, q, t);
     const int64_t secs = h.gp.prune_backoff_ns / 1000000000LL;
     add_backoff(h, q, t, secs > 0 ? secs * 1000000000LL : h.gp.prune_backoff_ns);
+    return was;
 }
 
+// The control a receiver u reads from the sender of its pair q (unsharded:
+// only marked pairs carry any, and what is read is cleared, so the next round
+// starts from zeros).  Returns false when there is nothing to handle.
+__device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool write, uint32_t& r, uint64_t& grafts,
+                                             uint64_t& prunes) {
+    r = h.rev[q];  // r = (v -> u), the sender's pair
+    if (r == NO_PAIR) return false;
+    if (r & HALO) {  // v on another shard: its control bits came through the exchange
+        grafts = h.halo_ctl[2 * (size_t)(r & ~HALO)];
+        prunes = h.halo_ctl[2 * (size_t)(r & ~HALO) + 1];
+    } else {
+        grafts = h.ctl_graft[r];
+        prunes = h.ctl_prune[r];
+        if (write && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+    }
+    return (grafts | prunes) != 0;
+}
+
+constexpr int RECV_TOPICS = 32;  // topics whose receiver mesh counts are cached (LDS, u8 per lane)
+
+// (B) one lane per receiving node u (up to HB_LANE_DEG peers; hubs run in
+// k_hb_recv_hub), senders in ascending order: handleGraft then handlePrune
+// per sender (:718-843), AcceptFrom-gated (:582-593).  The Dhi check reads
+// the mesh size the previous accepts and prunes of this round left: a
+// running count per topic, taken from the row on first use.
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
+    __shared__ uint8_t mcnt[RECV_TOPICS][64];
+    const uint32_t lane = threadIdx.x;
     uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
-    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
+    int64_t links = 0;
+    const DevGossipParams& gp = h.gp;
+    for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        const DevGossipParams& gp = h.gp;
+        if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
+        uint32_t have = 0;  // topics < RECV_TOPICS with a cached count
         for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
-            // unsharded, only pairs whose sender marked them carry control;
-            // what is read is cleared (the next round starts from zeros)
             if (!h.halo_ctl) {
                 if (!h.inbox[q]) continue;
                 h.inbox[q] = 0;
             }
-            const uint32_t r = h.rev[q];  // r = (v -> u), the sender's pair
-            if (r == NO_PAIR) continue;
+            uint32_t r;
             uint64_t grafts, prunes;
-            if (r & HALO) {  // v on another shard: its control bits came through the exchange
-                grafts = h.halo_ctl[2 * (size_t)(r & ~HALO)];
-                prunes = h.halo_ctl[2 * (size_t)(r & ~HALO) + 1];
-            } else {
-                grafts = h.ctl_graft[r];
-                prunes = h.ctl_prune[r];
-                if (!h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
-            }
-            if (!(grafts | prunes)) continue;
+            if (!recv_control(h, q, true, r, grafts, prunes)) continue;
             const double score = s.score[q];  // gs.score.Score(p) once per control message
             const uint8_t ef = h.eflags[q];
             // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
@@ -562,8 +824,17 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                     ++rejected;
                     continue;
                 }
-                int n = 0;
-                for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
+                int n;
+                if (t < RECV_TOPICS && (have >> t & 1)) {
+                    n = mcnt[t][lane];
+                } else {
+                    n = 0;
+                    for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
+                    if (t < RECV_TOPICS) {
+                        mcnt[t][lane] = (uint8_t)n;
+                        have |= 1u << t;
+                    }
+                }
                 if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
                     resp |= 1ull << t;
                     add_backoff(h, q, t, gp.prune_backoff_ns);
@@ -572,11 +843,19 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 }
                 ev_graft(s, q, t, h.now);
                 ++accepted;
+                if (scored_topic(s, q, t)) {
+                    ++links;
+                    if (t < RECV_TOPICS) mcnt[t][lane] = (uint8_t)(n + 1);
+                }
             }
             h.resp[q] = resp;
             if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
             for (; prunes; prunes &= prunes - 1) {  // handlePrune
-                handle_prune(s, h, q, (uint32_t)__builtin_ctzll(prunes));
+                const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
+                if (handle_prune(s, h, q, t)) {
+                    --links;
+                    if (t < RECV_TOPICS && (have >> t & 1)) mcnt[t][lane] = (uint8_t)(mcnt[t][lane] - 1);
+                }
                 ++handled;
             }
         }
@@ -585,12 +864,139 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     flush_count(h.stats, HB_REJECTED, rejected);
     flush_count(h.stats, HB_PENALTIES, penalties);
     flush_count(h.stats, HB_PRUNES_HANDLED, handled);
+    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
+}
+
+// In-mesh count of topic t over u's row, summed by the whole wave.
+__device__ __forceinline__ int wave_mesh_count(const DevState& s, int64_t r0, int64_t r1, uint32_t t, uint32_t lane) {
+    uint64_t c = 0;
+    for (int64_t x = r0 + lane; x < r1; x += 64) c += hb_in_mesh(s, x, t);
+    return (int)wave_sum64(c);
+}
+
+// (B) for hub receivers (more than HB_LANE_DEG peers): one wave per node.
+// The wave finds the marked pairs 64 at a time (ballot); every lane then runs
+// the same sequential handling of each sender in ascending order (its values
+// are uniform across the wave), lane 0 writing, and mesh sizes are counted by
+// the whole wave.
+__global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
+    __shared__ int mc[64];
+    const uint32_t lane = threadIdx.x;
+    const bool w0 = lane == 0;
+    uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
+    int64_t links = 0;
+    const DevGossipParams& gp = h.gp;
+    for (uint32_t k = blockIdx.x; k < h.n_hubs; k += gridDim.x) {
+        const uint32_t u = h.hubs[k];
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        uint64_t have = 0;  // topics with a cached count in mc[]
+        for (int64_t c0 = r0; c0 < r1; c0 += 64) {
+            const int64_t ql = c0 + lane;
+            bool mine = ql < r1;
+            if (mine && !h.halo_ctl) mine = h.inbox[ql] != 0;
+            uint64_t mask = __ballot(mine);
+            __syncthreads();  // every lane has read its inbox byte before lane 0 clears any
+            for (; mask; mask &= mask - 1) {
+                const uint64_t q = (uint64_t)c0 + (uint32_t)__builtin_ctzll(mask);
+                if (!h.halo_ctl && w0) h.inbox[q] = 0;
+                uint32_t r;
+                uint64_t grafts, prunes;
+                if (!recv_control(h, q, false, r, grafts, prunes)) continue;
+                __syncthreads();  // every lane has the words before lane 0 clears them
+                if (w0 && !(r & HALO) && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                const double score = s.score[q];
+                const uint8_t ef = h.eflags[q];
+                if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
+                if (w0) h.dirty[q] = 1;
+                uint64_t resp = 0;
+                for (; grafts; grafts &= grafts - 1) {
+                    const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
+                    if (hb_in_mesh(s, q, t)) continue;
+                    if (ef & EDGE_DIRECT) {
+                        resp |= 1ull << t;
+                        rejected += w0;
+                        continue;
+                    }
+                    const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
+                    if (expire != 0 && h.now < expire) {
+                        const bool twice = h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns);
+                        if (w0) {
+                            ev_penalty(s, q, 1);
+                            if (twice) ev_penalty(s, q, 1);
+                            add_backoff(h, q, t, gp.prune_backoff_ns);
+                        }
+                        penalties += w0 ? (twice ? 2 : 1) : 0;
+                        resp |= 1ull << t;
+                        rejected += w0;
+                        __syncthreads();
+                        continue;
+                    }
+                    if (score < 0) {
+                        resp |= 1ull << t;
+                        if (w0) add_backoff(h, q, t, gp.prune_backoff_ns);
+                        rejected += w0;
+                        __syncthreads();
+                        continue;
+                    }
+                    int n;
+                    if (t < 64 && (have >> t & 1)) {
+                        n = mc[t];
+                    } else {
+                        n = wave_mesh_count(s, r0, r1, t, lane);
+                        __syncthreads();
+                        if (t < 64) {
+                            if (w0) mc[t] = n;
+                            have |= 1ull << t;
+                        }
+                    }
+                    if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
+                        resp |= 1ull << t;
+                        if (w0) add_backoff(h, q, t, gp.prune_backoff_ns);
+                        rejected += w0;
+                        __syncthreads();
+                        continue;
+                    }
+                    const bool sc_t = scored_topic(s, q, t);
+                    __syncthreads();  // every lane has read the flags before lane 0 grafts
+                    if (w0) {
+                        ev_graft(s, q, t, h.now);
+                        if (sc_t && t < 64) mc[t] = n + 1;
+                    }
+                    accepted += w0;
+                    if (sc_t) links += w0;
+                    __syncthreads();
+                }
+                if (w0) {
+                    h.resp[q] = resp;
+                    if (resp && !(r & HALO)) h.answer[r] = 1;
+                }
+                for (; prunes; prunes &= prunes - 1) {
+                    const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
+                    const bool was = hb_in_mesh(s, q, t) && scored_topic(s, q, t);
+                    __syncthreads();
+                    if (w0) {
+                        handle_prune(s, h, q, t);
+                        if (was && t < 64 && (have >> t & 1)) mc[t] = mc[t] - 1;
+                    }
+                    if (was) links -= w0;
+                    handled += w0;
+                    __syncthreads();
+                }
+            }
+        }
+    }
+    flush_count(h.stats, HB_ACCEPTED, accepted);
+    flush_count(h.stats, HB_REJECTED, rejected);
+    flush_count(h.stats, HB_PENALTIES, penalties);
+    flush_count(h.stats, HB_PRUNES_HANDLED, handled);
+    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
 }
 
 // ---- (C) the GRAFT senders handle the PRUNE answers ------------------------------
 
 __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
     uint64_t handled = 0;
+    int64_t links = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {  // r = (v -> u)
         if (!h.halo_resp) {  // unsharded: only marked pairs have an answer; what is read is cleared
             if (!h.answer[r]) continue;
@@ -603,30 +1009,12 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
         if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
         if (resp) h.dirty[r] = 1;
         for (; resp; resp &= resp - 1) {
-            handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp));
+            if (handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp))) --links;
             ++handled;
         }
     }
     flush_count(h.stats, HB_PRUNES_HANDLED, handled);
-}
-
-// In-mesh (pair, topic) count: one thread per 16 pairs of a tile, reading
-// their pair flags and, per topic, the tile's 16 record-flag bytes as uint4.
-__global__ __launch_bounds__(256) void k_hb_mesh_links(DevState s, HbState h) {
-    static_assert(TILE % 16 == 0 && REC_IN_MESH == 0x01 && PAIR_PRESENT == 0x01, "byte-lane counting below");
-    uint64_t c = 0;
-    const uint64_t n_chunks = (h.n_pairs + 15) / 16;  // pflags / rflags are padded to whole tiles
-    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n_chunks; k += (uint64_t)gridDim.x * 256u) {
-        const uint64_t p0 = k * 16;
-        const uint4 pf = *reinterpret_cast<const uint4*>(s.pflags + p0);
-        const uint32_t pw[4] = {pf.x & 0x01010101u, pf.y & 0x01010101u, pf.z & 0x01010101u, pf.w & 0x01010101u};
-        if (!(pw[0] | pw[1] | pw[2] | pw[3])) continue;
-        for (uint32_t t = 0; t < s.n_topics; ++t) {
-            const uint4 rf = *reinterpret_cast<const uint4*>(s.rflags + flag_index(p0, t, s.n_topics));
-            c += __popc(rf.x & pw[0]) + __popc(rf.y & pw[1]) + __popc(rf.z & pw[2]) + __popc(rf.w & pw[3]);
-        }
-    }
-    flush_count(h.stats, HB_MESH_LINKS, c);
+    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
 }
 
 // Shard exchange of per-pair control words: send slot j carries the words of
@@ -661,27 +1049,52 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_hb_mesh(const DevState& s, const HbState& h, uint32_t t, hipStream_t st) {
+hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t);
+    hipLaunchKernelGGL(k_hb_scan, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st) {
+    if (h.n_nodes == 0) return hipSuccess;
+    // the grid strides over the topic's worklist, whose length only the device knows
+    hipLaunchKernelGGL(k_hb_maintain, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t);
+    if (max_deg > HB_LANE_DEG) {
+        const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
+        static bool attr = false;
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_hb_maintain_hub, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(HB_HUB_MAX * (sizeof(double) + 2 * sizeof(uint16_t) + 1)));
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_hb_maintain_hub, dim3(1024), dim3(64), lds, st, s, h, t);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
-                            uint32_t max_ids, hipStream_t st) {
+                            uint32_t max_ids, int64_t max_deg, hipStream_t st) {
     if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hb_gossip, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t, gb, n_gb);
-    if (max_ids > (uint32_t)h.gp.max_ihave)  // some node may need the truncating path
-        hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), sizeof(uint32_t) * max_ids, st,
-                           s, h, t, gb, n_gb);
+    // queued nodes (long lists, tiles with hub rows): the kernel returns at once without any
+    const size_t lds = sizeof(uint32_t) * max_ids + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
+    static size_t attr = 0;
+    if (lds > 65536 && lds > attr) {
+        e = hipFuncSetAttribute((const void*)k_hb_gossip_long, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = lds;
+    }
+    hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), lds, st, s, h, t, gb, n_gb, max_ids);
     return hipGetLastError();
 }
 
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
+    if (h.n_hubs) hipLaunchKernelGGL(k_hb_recv_hub, dim3(std::min<uint32_t>(h.n_hubs, 4096)), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
 
@@ -695,12 +1108,6 @@ hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint
                           uint64_t* out, hipStream_t st) {
     if (n_send == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_pack, dim3(grid_cap(n_send, 256)), dim3(256), 0, st, send_pair, n_send, a, b, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_hb_mesh_links(const DevState& s, const HbState& h, hipStream_t st) {
-    if (h.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_mesh_links, dim3(grid_cap((h.n_pairs + 15) / 16, 256)), dim3(256), 0, st, s, h);
     return hipGetLastError();
 }
 

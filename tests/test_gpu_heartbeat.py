@@ -24,6 +24,9 @@ CASES = [
     (400, 9, 2, 5, 14, True, 0.03, 0.03, 0, 13),
     (600, 6, 2, 6, 6, True, 0.02, 0.05, 64, 58),
     (2000, 8, 1, 3, 3, False, 0.0, 0.0, 128, 59),
+    # ~50 peers per node: a wave's 64 rows exceed the LDS stage (windows of
+    # rows), meshes of ~40 are pruned through the merge sort (> 32 entries)
+    (500, 25, 1, 3, 40, False, 0.02, 0.0, 64, 59),
 ]
 
 
@@ -81,8 +84,8 @@ def test_heartbeat_rejects_bad_params_and_degree(gpu_ok):
     gp.d_score = -1
     with pytest.raises(gsx.GsxError):
         e.set_gossipsub_params(gp)
-    # a hub above the per-node limit of the mesh lanes is refused, not truncated
-    n = 300
+    # a hub above the per-node limit of the hub rows (HB_HUB_MAX) is refused, not truncated
+    n = 12_100
     cols = [list(range(1, n))] + [[0] for _ in range(1, n)]
     row_ptr = np.cumsum([0] + [len(c) for c in cols]).astype(np.int64)
     col = np.concatenate([np.array(c, dtype=np.int32) for c in cols])
@@ -143,3 +146,42 @@ def test_gossip_matches_oracle(gpu_ok, max_ihave, msgs):
         assert go[k] == wo[k], (k, go[k], wo[k])
         _same(gs[k], ws[k], f"tick {k}")
     assert sum(o["ihave_msgs"] for o in go) > 0
+
+
+@pytest.mark.parametrize("md", [8, 300])
+def test_heartbeat_hub_nodes_match_oracle(gpu_ok, md):
+    """Nodes with more than 64 peers (HB_LANE_DEG) run their maintenance, gossip
+    and GRAFT handling one wave each: a hub peering with 700 nodes (with a mesh
+    of ~300 at md=300: over Dhi, a 300-entry sort) plus a second hub, over
+    rounds with gossip, vs the oracle."""
+    from test_gpu_propagation import _hub_overlay, _overlay_from_edges
+
+    n, T = 705, 2
+    ov = _hub_overlay(n, seed=3)
+    edges = set()
+    for u in range(n):
+        for v in ov.col[ov.row_ptr[u]:ov.row_ptr[u + 1]]:
+            edges.add((min(u, int(v)), max(u, int(v))))
+    edges |= {(1, k) for k in range(2, 200)}  # a second hub
+    ov = _overlay_from_edges(n, sorted(edges))
+    gp = orc.default_gossipsub_params()
+    gp.history_gossip = 3
+    runs = []
+    for be in (gsx.Engine(T), orc.Oracle(T)):
+        hc.pc.setup(be, ov, T, seed=11, mesh_degree=md, disconnect_frac=0.02)
+        be.set_gossipsub_params(gp)
+        outs, snaps = [], []
+        for k in range(4):
+            now = hc.T0 + (3 + k) * abi.SECOND
+            outs.append(be.heartbeat(59 + k, now, 1234).as_dict())
+            snaps.append(hc.snapshot(be))
+            cfg = hc.pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % T, latency_ms=5, seed=k)
+            cfg.now_ns = now + 100 * abi.MILLISECOND
+            be.propagate(hc.pc.messages(n, 70, 100 + k), cfg)
+            be.refresh(now + 500 * abi.MILLISECOND)
+        runs.append((outs, snaps))
+    (go, gs), (wo, ws) = runs
+    for k in range(4):
+        assert go[k] == wo[k], (k, go[k], wo[k])
+        _same(gs[k], ws[k], f"tick {k}")
+    assert sum(o["grafts"] + o["prunes"] for o in go) > 0 and sum(o["ihave_msgs"] for o in go) > 0
