@@ -325,12 +325,41 @@ __device__ __forceinline__ void wave_append(bool want, uint32_t value, uint32_t*
     if (want) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1))] = value;
 }
 
-constexpr int SCAN_TOPICS = 8;  // topics counted per pass over a wave's pairs
+constexpr int SCAN_TOPICS = 8;     // topics decided per pass over a wave's pairs
+constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (2 B each) for the per-node counts
 
-// (A) scan: every unit of every topic; worklists, rngk = 0, mesh links before the round.
+// A pair's scan bits for topics t0 .. t0+7: bit k = in the mesh of topic t0+k,
+// bit 8 = score < 0, bit 9 = outbound, bit 10 = getPeers' base filter with
+// score >= 0 (present, connected, mesh-capable, not direct).
+constexpr uint16_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;
+__device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
+                                              uint32_t nt) {
+    const uint8_t pf = s.pflags[r];
+    if (!(pf & PAIR_PRESENT)) return 0;
+    uint16_t m = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_TOPICS; ++k)
+        if (k < (int)nt && (s.rflags[flag_index(r, t0 + k, s.n_topics)] & REC_IN_MESH)) m |= 1u << k;
+    const uint8_t ef = h.eflags[r];
+    const double sc = s.score[r];
+    if (sc < 0) m |= SC_NEG;
+    if (ef & EDGE_OUTBOUND) m |= SC_OUT;
+    if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0) m |= SC_CAND;
+    return m;
+}
+
+// (A) scan: every unit of every topic.  A wave takes 64 consecutive nodes:
+// one coalesced pass packs each pair's bits into LDS, then one lane per node
+// counts its row — mesh size, negative and outbound members, and, only for a
+// unit below Dlo or short of outbound peers, its getPeers candidates (the
+// backoff entries are read there alone).  A unit acts iff some step of
+// maintain() would: a negative member, more than Dhi, an opportunistic-graft
+// tick with a mesh of 2+, or a graft step with a candidate.  Acting units go
+// to the topic's worklist (hub nodes to its hub list); every unit's rngk starts
+// at 0; the in-mesh links before the round are counted.
 __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
     __shared__ int64_t rs[65];
-    __shared__ int cnt[SCAN_TOPICS][3][64];  // |mesh|, negative in mesh, outbound in mesh
+    __shared__ uint16_t st[SCAN_STAGE];
     const DevGossipParams& gp = h.gp;
     const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
     const uint32_t lane = threadIdx.x;
@@ -342,56 +371,50 @@ __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
         if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
         __syncthreads();
         const int64_t pa = rs[0], pb = rs[64];
+        const bool staged = pb - pa <= SCAN_STAGE;
         const uint32_t v = v0 + lane;
-        const int deg = lane < nv ? (int)(rs[lane + 1] - rs[lane]) : 0;
+        const int64_t r0 = rs[lane];
+        const int deg = lane < nv ? (int)(rs[lane + 1] - r0) : 0;
         for (uint32_t t0 = 0; t0 < T; t0 += SCAN_TOPICS) {
             const uint32_t nt = min((uint32_t)SCAN_TOPICS, T - t0);
-            for (uint32_t k = 0; k < nt; ++k)
+            if (staged) {
+                for (int64_t r = pa + lane; r < pb; r += 64) st[r - pa] = scan_bits(s, h, r, t0, nt);
+                __syncthreads();
+            }
+            int n[SCAN_TOPICS], neg[SCAN_TOPICS], outb[SCAN_TOPICS];
 #pragma unroll
-                for (int c = 0; c < 3; ++c) cnt[k][c][lane] = 0;
-            __syncthreads();
-            for (int64_t r = pa + lane; r < pb; r += 64) {
-                if (!(s.pflags[r] & PAIR_PRESENT)) continue;
-                int lo = 0, hi = (int)nv;  // owner: rs[lo] <= r < rs[lo + 1]
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (rs[mid] <= r) lo = mid;
-                    else hi = mid;
-                }
-                uint8_t rf[SCAN_TOPICS];
+            for (int k = 0; k < SCAN_TOPICS; ++k) n[k] = neg[k] = outb[k] = 0;
+            for (int i = 0; i < deg; ++i) {
+                const uint16_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
 #pragma unroll
                 for (int k = 0; k < SCAN_TOPICS; ++k)
-                    rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, T)] : 0;
-                bool any = false;
-#pragma unroll
-                for (int k = 0; k < SCAN_TOPICS; ++k) any |= (rf[k] & REC_IN_MESH) != 0;
-                if (!any) continue;
-                const bool neg = s.score[r] < 0;
-                const bool outb = h.eflags[r] & EDGE_OUTBOUND;
-#pragma unroll
-                for (int k = 0; k < SCAN_TOPICS; ++k)
-                    if (rf[k] & REC_IN_MESH) {
-                        atomicAdd(&cnt[k][0][lo], 1);
-                        if (neg) atomicAdd(&cnt[k][1][lo], 1);
-                        if (outb) atomicAdd(&cnt[k][2][lo], 1);
+                    if (m >> k & 1) {
+                        ++n[k];
+                        neg[k] += (m & SC_NEG) != 0;
+                        outb[k] += (m & SC_OUT) != 0;
                     }
             }
-            __syncthreads();
             for (uint32_t k = 0; k < nt; ++k) {
                 const uint32_t t = t0 + k;
                 bool active = false;
                 if (lane < nv) {
-                    const int n = cnt[k][0][lane], neg = cnt[k][1][lane], outb = cnt[k][2][lane];
-                    links += (uint64_t)n;
-                    // a unit below Dlo or short of outbound peers acts only if it has a
-                    // candidate; maintain() finds none otherwise and draws nothing
-                    active = neg > 0 || n > gp.d_hi || (og_tick && n > 1) || n < gp.d_lo || outb < gp.d_out;
+                    links += (uint64_t)n[k];
+                    active = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1);
+                    const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
+                    if (!active && (grow || more_out)) {  // getPeers finds a candidate? (:1370-1385, :1450-1476)
+                        for (int i = 0; i < deg && !active; ++i) {
+                            const uint16_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
+                            if ((m & SC_CAND) && !(m >> k & 1) && (grow || (m & SC_OUT)) &&
+                                h.backoff[(size_t)t * h.n_pairs + r0 + i] == 0)
+                                active = true;
+                        }
+                    }
                     h.rngk[(size_t)t * h.n_nodes + v] = 0;
                 }
                 wave_append(active && deg <= HB_LANE_DEG, v, h.work + (size_t)t * h.n_nodes, h.n_work + t, lane);
                 wave_append(active && deg > HB_LANE_DEG, v, h.hub_work + (size_t)t * h.n_nodes, h.n_hub + t, lane);
             }
-            __syncthreads();  // cnt is rewritten by the next topic chunk / tile
+            __syncthreads();  // st is rewritten by the next topic chunk / tile
         }
     }
     flush_count(h.stats, HB_MESH_LINKS, links);
@@ -406,6 +429,8 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
     __shared__ double sc[HB_STAGE];
     __shared__ uint8_t fl[HB_STAGE];
     __shared__ uint16_t la[HB_STAGE], lb[HB_STAGE];
+    __shared__ uint32_t offs[65];
+    __shared__ int64_t r0s[64];
     const uint32_t lane = threadIdx.x;
     const uint32_t nw = h.n_work[t];
     const uint32_t* work = h.work + (size_t)t * h.n_nodes;
@@ -418,15 +443,32 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
         const int64_t r0 = valid ? h.row_ptr[v] : 0;
         const int deg = valid ? (int)(h.row_ptr[v + 1] - r0) : 0;
         const uint32_t off = wave_prefix((uint32_t)deg, lane);
-        bool done = !valid;
-        uint32_t base = 0;
-        while (__ballot(!done)) {
-            if (!done && off >= base && off + deg <= base + HB_STAGE) {
-                const uint32_t o = off - base;
-                for (int i = 0; i < deg; ++i) {
-                    sc[o + i] = s.score[r0 + i];
-                    fl[o + i] = stage_bits(s, h, r0 + i, t);
+        offs[lane] = off;
+        r0s[lane] = r0;
+        if (lane == 63) offs[64] = off + deg;
+        __syncthreads();
+        // windows of whole rows: lanes [l0, l1) whose rows fit [offs[l0], offs[l0] + HB_STAGE)
+        uint32_t l0 = 0;
+        while (l0 < 64) {
+            const uint32_t base = offs[l0];
+            uint32_t l1 = l0;
+            while (l1 < 64 && offs[l1 + 1] - base <= HB_STAGE) ++l1;  // (uniform: every lane computes it)
+            const uint32_t end = offs[l1];
+            // cooperative staging: item k of the window belongs to the lane whose row holds it
+            for (uint32_t k = base + lane; k < end; k += 64) {
+                uint32_t lo = l0, hi = l1;  // offs[lo] <= k < offs[lo + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (offs[mid] <= k) lo = mid;
+                    else hi = mid;
                 }
+                const uint64_t r = (uint64_t)r0s[lo] + (k - offs[lo]);
+                sc[k - base] = s.score[r];
+                fl[k - base] = stage_bits(s, h, r, t);
+            }
+            __syncthreads();
+            if (lane >= l0 && lane < l1 && valid) {
+                const uint32_t o = off - base;
                 HbUnit U{s, h, t, r0, deg, sc + o, fl + o, la + o, lb + o, scored};
                 Rng g = hb_rng(h, v, t, 0);
                 U.maintain(g);
@@ -434,13 +476,9 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
                 grafts += U.grafts;
                 prunes += U.prunes;
                 links += U.links;
-                done = true;
             }
-            // the next window starts at the lowest row not yet run
-            uint32_t mo = done ? 0xFFFFFFFFu : off;
-#pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) mo = min(mo, (uint32_t)__shfl_xor((int)mo, sh, 64));
-            base = mo;
+            __syncthreads();  // the stage is reused by the next window / chunk
+            l0 = l1;
         }
     }
     flush_count(h.stats, HB_GRAFTS, grafts);
