@@ -332,20 +332,23 @@ constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (2 B each) for the 
 // bit 8 = score < 0, bit 9 = outbound, bit 10 = getPeers' base filter with
 // score >= 0 (present, connected, mesh-capable, not direct).
 constexpr uint16_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;
-__device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
-                                              uint32_t nt) {
-    const uint8_t pf = s.pflags[r];
+__device__ __forceinline__ uint16_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS]) {
     if (!(pf & PAIR_PRESENT)) return 0;
     uint16_t m = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_TOPICS; ++k)
-        if (k < (int)nt && (s.rflags[flag_index(r, t0 + k, s.n_topics)] & REC_IN_MESH)) m |= 1u << k;
-    const uint8_t ef = h.eflags[r];
-    const double sc = s.score[r];
+        if (rf[k] & REC_IN_MESH) m |= 1u << k;
     if (sc < 0) m |= SC_NEG;
     if (ef & EDGE_OUTBOUND) m |= SC_OUT;
     if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0) m |= SC_CAND;
     return m;
+}
+__device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
+                                              uint32_t nt) {
+    uint8_t rf[SCAN_TOPICS];
+#pragma unroll
+    for (int k = 0; k < SCAN_TOPICS; ++k) rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
+    return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf);
 }
 
 // (A) scan: every unit of every topic.  A wave takes 64 consecutive nodes:
@@ -378,7 +381,25 @@ __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
         for (uint32_t t0 = 0; t0 < T; t0 += SCAN_TOPICS) {
             const uint32_t nt = min((uint32_t)SCAN_TOPICS, T - t0);
             if (staged) {
-                for (int64_t r = pa + lane; r < pb; r += 64) st[r - pa] = scan_bits(s, h, r, t0, nt);
+                // four pairs per lane at a time, every load issued before any is used
+                for (int64_t rb = pa + lane; rb < pb; rb += 256) {
+                    uint8_t pf[4], ef[4], rf[4][SCAN_TOPICS];
+                    double sc[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t r = rb + 64 * j;
+                        const bool in = r < pb;
+                        pf[j] = in ? s.pflags[r] : 0;
+                        ef[j] = in ? h.eflags[r] : 0;
+                        sc[j] = in ? s.score[r] : 0.0;
+#pragma unroll
+                        for (int k = 0; k < SCAN_TOPICS; ++k)
+                            rf[j][k] = (in && k < (int)nt) ? s.rflags[flag_index(r, t0 + k, T)] : 0;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (rb + 64 * j < pb) st[rb + 64 * j - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j]);
+                }
                 __syncthreads();
             }
             int n[SCAN_TOPICS], neg[SCAN_TOPICS], outb[SCAN_TOPICS];
@@ -542,34 +563,6 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
-// GetGossipIDs of (v, t): its length and multiset digest, straight from the
-// cached batches' seen words.
-__device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, const GossipBatch* __restrict__ gb,
-                                               uint32_t n_gb, uint64_t& dig) {
-    uint32_t L = 0;
-    dig = 0;
-    for (uint32_t b = 0; b < n_gb; ++b) {
-        const GossipBatch B = gb[b];
-        for (uint32_t w = 0; w < B.n_words; ++w) {
-            uint64_t word = B.seen[(size_t)v * B.n_words + w];
-            L += (uint32_t)__popcll(word);
-            // a node holding every message of the word (the common case once a
-            // batch has spread) adds the word's precomputed digest sum
-            const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
-            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
-            if (word && word == full) {
-                dig += h.mc_digest[B.wdig_base + w];
-                continue;
-            }
-            while (word) {
-                dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
-                word &= word - 1;
-            }
-        }
-    }
-    return L;
-}
-
 // emitGossip of topic t for every node.  A wave takes 64 consecutive nodes:
 // one coalesced pass over their pairs rewrites the topic's IHAVE slots of the
 // range (0 = none) and stages each pair's target eligibility in LDS; then a
@@ -582,6 +575,8 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
     __shared__ int64_t rs[65];
     __shared__ uint8_t el[HB_STAGE];
     __shared__ uint16_t pl[HB_STAGE];
+    __shared__ uint32_t Ls[64];
+    __shared__ unsigned long long Ds[64];
     uint64_t msgs = 0, ids = 0;
     const uint32_t lane = threadIdx.x;
     const size_t tslot = (size_t)t * h.n_pairs;
@@ -592,16 +587,71 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
         __syncthreads();
         const int64_t pa = rs[0], pb = rs[64];
         const bool staged = pb - pa <= HB_STAGE;
-        for (int64_t r = pa + lane; r < pb; r += 64) {
-            h.ihave_len[tslot + r] = 0;
-            h.ihave_hash[tslot + r] = 0;
-            if (staged) el[r - pa] = gossip_target(s, h, r, t);
+        for (int64_t rb = pa + lane; rb < pb; rb += 256) {  // four pairs per lane, loads first
+            uint8_t pf[4], ef[4], rf[4], dt[4];
+            double sc[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t r = rb + 64 * j;
+                const bool in = r < pb;
+                pf[j] = in && staged ? s.pflags[r] : 0;
+                ef[j] = in && staged ? h.eflags[r] : 0;
+                rf[j] = in && staged ? s.rflags[flag_index(r, t, s.n_topics)] : 0;
+                dt[j] = in && staged ? h.dirty[r] : 0;
+                sc[j] = in && staged ? s.score[r] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t r = rb + 64 * j;
+                if (r >= pb) continue;
+                h.ihave_len[tslot + r] = 0;
+                h.ihave_hash[tslot + r] = 0;
+                if (!staged) continue;
+                // gossip_target with the loads above (live score: dirty pairs re-evaluated)
+                bool ok = (pf[j] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+                          (ef[j] & EDGE_GOSSIPSUB) && !(ef[j] & EDGE_DIRECT) && !(rf[j] & REC_IN_MESH);
+                if (ok) ok = (dt[j] ? eval_pair(s, h.pp, r) : sc[j]) >= h.gossip_threshold;
+                el[r - pa] = ok;
+            }
+        }
+        __syncthreads();
+        // GetGossipIDs lengths and digests of the tile's nodes: a coalesced pass
+        // over each cached batch's rows (node-major words), summed per node in LDS
+        Ls[lane] = 0;
+        Ds[lane] = 0;
+        __syncthreads();
+        for (uint32_t b = 0; b < n_gb; ++b) {
+            const GossipBatch B = gb[b];
+            const uint32_t W = B.n_words, cnt = nv * W;
+            const uint64_t* rows = B.seen + (size_t)v0 * W;
+            for (uint32_t i0 = lane; i0 < cnt; i0 += 256) {
+                uint64_t wd[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) wd[j] = i0 + 64 * j < cnt ? rows[i0 + 64 * j] : 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint64_t word = wd[j];
+                    if (!word) continue;
+                    const uint32_t i = i0 + 64 * j, node = i / W, w = i - node * W;
+                    const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
+                    const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                    atomicAdd(&Ls[node], (uint32_t)__popcll(word));
+                    uint64_t d = 0;
+                    if (word == full) {  // every message of the word: its precomputed digest sum
+                        d = h.mc_digest[B.wdig_base + w];
+                    } else {
+                        for (; word; word &= word - 1)
+                            d += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
+                    }
+                    atomicAdd(&Ds[node], (unsigned long long)d);
+                }
+            }
         }
         __syncthreads();
         if (lane < nv) {
             const uint32_t v = v0 + lane;
-            uint64_t dig;
-            const uint32_t L = gossip_ids(h, v, gb, n_gb, dig);
+            const uint64_t dig = Ds[lane];
+            const uint32_t L = Ls[lane];
             if (L > 0) {  // emitGossip returns early on an empty list, drawing nothing
                 if (!staged || L > (uint32_t)h.gp.max_ihave) {
                     h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // one wave per node: k_hb_gossip_long
@@ -1089,7 +1139,7 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
 
 hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_scan, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
+    hipLaunchKernelGGL(k_hb_scan, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h);  // one wave per tile
     return hipGetLastError();
 }
 
@@ -1116,7 +1166,7 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
     if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hb_gossip, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t, gb, n_gb);
+    hipLaunchKernelGGL(k_hb_gossip, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t, gb, n_gb);
     // queued nodes (long lists, tiles with hub rows): the kernel returns at once without any
     const size_t lds = sizeof(uint32_t) * max_ids + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
     static size_t attr = 0;
