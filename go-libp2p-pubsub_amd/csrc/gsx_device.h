@@ -287,8 +287,9 @@ struct HbState {
     uint8_t* answer;      // per pair (v -> u): u answered with PRUNE bits on (u -> v) this round
     unsigned long long* stats;
     uint32_t* rngk;        // [topic][node]: draw counter after the unit's maintenance (emitGossip continues it)
-    uint32_t* work;        // [topic][node]: units the scan found acting (lane-per-unit maintenance)
-    uint32_t* n_work;      // [topic]
+    uint32_t* work;        // [topic][tile * 64 + i]: units the scan found acting, per 64-node tile
+    uint8_t* tcnt;         // [topic][tile]: how many (lane-per-unit maintenance)
+    uint64_t n_tiles64;    // 64 * tiles: the per-topic stride of `work`
     uint32_t* hub_work;    // [topic][node]: acting units of nodes with more than HB_LANE_DEG peers
     uint32_t* n_hub;       // [topic]
     const uint32_t* hubs;  // nodes with more than HB_LANE_DEG peers (k_hb_recv_hub)

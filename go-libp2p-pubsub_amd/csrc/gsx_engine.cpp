@@ -106,6 +106,7 @@ struct gsx_engine {
     unsigned long long* d_hbstats = nullptr;
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
     uint32_t *d_work = nullptr, *d_nwork = nullptr, *d_hubwork = nullptr, *d_hubs = nullptr;  // heartbeat worklists
+    uint8_t* d_tcnt = nullptr;
     std::vector<uint32_t> hubs_host;  // nodes with more than HB_LANE_DEG pairs
     std::vector<uint8_t> gossip_prev;  // per topic: IHAVE slots written last round
     uint64_t* d_ihave_hash = nullptr;
@@ -391,7 +392,7 @@ void free_state(gsx_engine* e) {
     e->send_counts.clear();
     e->n_recv = e->n_send = 0;
     e->d_col = nullptr;
-    void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs,
+    void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt,
                   e->d_backoff, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
                   e->d_mc_digest};
@@ -404,6 +405,7 @@ void free_state(gsx_engine* e) {
     e->d_hbstats = nullptr;
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
+    e->d_tcnt = nullptr;
     e->d_ihave_hash = nullptr;
     e->d_gb = nullptr;
     e->d_mc_digest = nullptr;
@@ -2071,7 +2073,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
             (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 3 * E)) ||
             (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
             (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
-            (rc = dalloc(e, &e->d_work, (size_t)e->T * e->n_nodes)) ||
+            (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
+            (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
             (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
             (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
             (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
@@ -2112,7 +2115,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.gossip_threshold = e->th.gossip_threshold;
     h.rngk = e->d_rngk;
     h.work = e->d_work;
-    h.n_work = e->d_nwork;
+    h.tcnt = e->d_tcnt;
+    h.n_tiles64 = 64 * (((uint64_t)e->n_nodes + 63) / 64);
     h.hub_work = e->d_hubwork;
     h.n_hub = e->d_nwork + e->T;
     h.hubs = e->d_hubs;

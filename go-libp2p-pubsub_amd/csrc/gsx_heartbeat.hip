@@ -351,37 +351,47 @@ __device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& 
     return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf);
 }
 
-// (A) scan: every unit of every topic.  A wave takes 64 consecutive nodes:
-// one coalesced pass packs each pair's bits into LDS, then one lane per node
-// counts its row — mesh size, negative and outbound members, and, only for a
-// unit below Dlo or short of outbound peers, its getPeers candidates (the
-// backoff entries are read there alone).  A unit acts iff some step of
-// maintain() would: a negative member, more than Dhi, an opportunistic-graft
-// tick with a mesh of 2+, or a graft step with a candidate.  Acting units go
-// to the topic's worklist (hub nodes to its hub list); every unit's rngk starts
-// at 0; the in-mesh links before the round are counted.
-__global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
-    __shared__ int64_t rs[65];
-    __shared__ uint16_t st[SCAN_STAGE];
+// (A) scan: every unit of every topic.  A wave takes a tile of 64 consecutive
+// nodes: one coalesced pass packs each pair's bits into LDS (four pairs per
+// lane in flight), then one lane per node counts its row — mesh size, negative
+// and outbound members, and, only for a unit below Dlo or short of outbound
+// peers, its getPeers candidates (the backoff entries are read there alone).
+// A unit acts iff some step of maintain() would: a negative member, more than
+// Dhi, an opportunistic-graft tick with a mesh of 2+, or a graft step with a
+// candidate.  The tile's acting units are listed at work[t][tile * 64 ..]
+// (count tcnt[t][tile]: no atomics); hub nodes go to the topic's hub list;
+// every unit's rngk starts at 0; the in-mesh links before the round are
+// counted.  Blocks of four waves over a bounded grid: one counter atomic per
+// block (same-address atomics serialise at the memory side).
+constexpr int SCAN_WAVES = 4;
+__global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
+    __shared__ int64_t rs_w[SCAN_WAVES][65];
+    __shared__ uint16_t st_w[SCAN_WAVES][SCAN_STAGE];
     const DevGossipParams& gp = h.gp;
     const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    int64_t* rs = rs_w[wave];
+    uint16_t* st = st_w[wave];
     const uint32_t T = s.n_topics;
-    uint64_t links = 0;
-    for (uint32_t v0 = blockIdx.x * 64u; v0 < h.n_nodes; v0 += gridDim.x * 64u) {
-        const uint32_t nv = min(64u, h.n_nodes - v0);
-        rs[lane] = h.row_ptr[v0 + min(lane, nv)];
-        if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+    const uint32_t n_tiles = (h.n_nodes + 63) / 64;
+    unsigned long long links[1] = {0};
+    for (uint32_t tb = blockIdx.x * SCAN_WAVES; tb < n_tiles; tb += gridDim.x * SCAN_WAVES) {
+        const uint32_t tile = tb + wave;  // (block-uniform loop: every wave reaches every barrier)
+        const uint32_t v0 = tile * 64u;
+        const uint32_t nv = tile < n_tiles ? min(64u, h.n_nodes - v0) : 0;
+        if (nv) {
+            rs[lane] = h.row_ptr[v0 + min(lane, nv)];
+            if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+        }
         __syncthreads();
-        const int64_t pa = rs[0], pb = rs[64];
+        const int64_t pa = nv ? rs[0] : 0, pb = nv ? rs[64] : 0;
         const bool staged = pb - pa <= SCAN_STAGE;
         const uint32_t v = v0 + lane;
-        const int64_t r0 = rs[lane];
+        const int64_t r0 = lane < nv ? rs[lane] : 0;
         const int deg = lane < nv ? (int)(rs[lane + 1] - r0) : 0;
         for (uint32_t t0 = 0; t0 < T; t0 += SCAN_TOPICS) {
             const uint32_t nt = min((uint32_t)SCAN_TOPICS, T - t0);
             if (staged) {
-                // four pairs per lane at a time, every load issued before any is used
                 for (int64_t rb = pa + lane; rb < pb; rb += 256) {
                     uint8_t pf[4], ef[4], rf[4][SCAN_TOPICS];
                     double sc[4];
@@ -400,8 +410,8 @@ __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
                     for (int j = 0; j < 4; ++j)
                         if (rb + 64 * j < pb) st[rb + 64 * j - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j]);
                 }
-                __syncthreads();
             }
+            __syncthreads();
             int n[SCAN_TOPICS], neg[SCAN_TOPICS], outb[SCAN_TOPICS];
 #pragma unroll
             for (int k = 0; k < SCAN_TOPICS; ++k) n[k] = neg[k] = outb[k] = 0;
@@ -419,7 +429,7 @@ __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
                 const uint32_t t = t0 + k;
                 bool active = false;
                 if (lane < nv) {
-                    links += (uint64_t)n[k];
+                    links[0] += (uint64_t)n[k];
                     active = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1);
                     const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
                     if (!active && (grow || more_out)) {  // getPeers finds a candidate? (:1370-1385, :1450-1476)
@@ -432,75 +442,104 @@ __global__ __launch_bounds__(64) void k_hb_scan(DevState s, HbState h) {
                     }
                     h.rngk[(size_t)t * h.n_nodes + v] = 0;
                 }
-                wave_append(active && deg <= HB_LANE_DEG, v, h.work + (size_t)t * h.n_nodes, h.n_work + t, lane);
-                wave_append(active && deg > HB_LANE_DEG, v, h.hub_work + (size_t)t * h.n_nodes, h.n_hub + t, lane);
+                if (nv) {
+                    const bool lw = active && deg <= HB_LANE_DEG;
+                    const uint64_t b = __ballot(lw);
+                    if (lw) h.work[(size_t)t * h.n_tiles64 + v0 + (uint32_t)__popcll(b & ((1ull << lane) - 1))] = v;
+                    if (lane == 0) h.tcnt[(size_t)t * n_tiles + tile] = (uint8_t)__popcll(b);
+                    wave_append(active && deg > HB_LANE_DEG, v, h.hub_work + (size_t)t * h.n_nodes, h.n_hub + t, lane);
+                }
             }
             __syncthreads();  // st is rewritten by the next topic chunk / tile
         }
     }
-    flush_count(h.stats, HB_MESH_LINKS, links);
+    const uint32_t slot[1] = {HB_MESH_LINKS};
+    block_count<1>(links, h.stats, slot);
 }
 
 constexpr int HB_STAGE = 1024;  // pairs a lane-per-unit wave stages at once
 
 // (A) per topic: the listed units, one lane each, rows staged in LDS.  A wave
-// takes 64 units; when their rows exceed the stage, it runs them in windows
-// of whole rows.
+// takes a group of 64 tiles, gathers their listed units (a prefix over the
+// per-tile counts: no atomics) 64 at a time, and stages their rows
+// cooperatively (every lane loads items of every row, 64 loads per
+// instruction); when the rows exceed the stage it runs them in windows of
+// whole rows.
 __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint32_t t) {
     __shared__ double sc[HB_STAGE];
     __shared__ uint8_t fl[HB_STAGE];
     __shared__ uint16_t la[HB_STAGE], lb[HB_STAGE];
     __shared__ uint32_t offs[65];
     __shared__ int64_t r0s[64];
+    __shared__ uint32_t pfx[65];
     const uint32_t lane = threadIdx.x;
-    const uint32_t nw = h.n_work[t];
-    const uint32_t* work = h.work + (size_t)t * h.n_nodes;
+    const uint32_t n_tiles = (h.n_nodes + 63) / 64;
+    const uint8_t* tcnt = h.tcnt + (size_t)t * n_tiles;
+    const uint32_t* work = h.work + (size_t)t * h.n_tiles64;
     const bool scored = t < s.n_topics && s.tp[t].scored;
     uint64_t grafts = 0, prunes = 0;
     int64_t links = 0;
-    for (uint32_t c0 = blockIdx.x * 64u; c0 < nw; c0 += gridDim.x * 64u) {
-        const bool valid = c0 + lane < nw;
-        const uint32_t v = valid ? work[c0 + lane] : 0;
-        const int64_t r0 = valid ? h.row_ptr[v] : 0;
-        const int deg = valid ? (int)(h.row_ptr[v + 1] - r0) : 0;
-        const uint32_t off = wave_prefix((uint32_t)deg, lane);
-        offs[lane] = off;
-        r0s[lane] = r0;
-        if (lane == 63) offs[64] = off + deg;
+    for (uint32_t g0 = blockIdx.x * 64u; g0 < n_tiles; g0 += gridDim.x * 64u) {
+        const uint32_t c = g0 + lane < n_tiles ? tcnt[g0 + lane] : 0;
+        const uint32_t p = wave_prefix(c, lane);
+        pfx[lane] = p;
+        if (lane == 63) pfx[64] = p + c;
         __syncthreads();
-        // windows of whole rows: lanes [l0, l1) whose rows fit [offs[l0], offs[l0] + HB_STAGE)
-        uint32_t l0 = 0;
-        while (l0 < 64) {
-            const uint32_t base = offs[l0];
-            uint32_t l1 = l0;
-            while (l1 < 64 && offs[l1 + 1] - base <= HB_STAGE) ++l1;  // (uniform: every lane computes it)
-            const uint32_t end = offs[l1];
-            // cooperative staging: item k of the window belongs to the lane whose row holds it
-            for (uint32_t k = base + lane; k < end; k += 64) {
-                uint32_t lo = l0, hi = l1;  // offs[lo] <= k < offs[lo + 1]
+        const uint32_t total = pfx[64];
+        for (uint32_t u0 = 0; u0 < total; u0 += 64) {
+            const uint32_t u = u0 + lane;
+            const bool valid = u < total;
+            uint32_t v = 0;
+            if (valid) {
+                uint32_t lo = 0, hi = 64;  // pfx[lo] <= u < pfx[lo + 1]
                 while (hi - lo > 1) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (offs[mid] <= k) lo = mid;
+                    if (pfx[mid] <= u) lo = mid;
                     else hi = mid;
                 }
-                const uint64_t r = (uint64_t)r0s[lo] + (k - offs[lo]);
-                sc[k - base] = s.score[r];
-                fl[k - base] = stage_bits(s, h, r, t);
+                v = work[(size_t)(g0 + lo) * 64 + (u - pfx[lo])];
             }
+            const int64_t r0 = valid ? h.row_ptr[v] : 0;
+            const int deg = valid ? (int)(h.row_ptr[v + 1] - r0) : 0;
+            const uint32_t off = wave_prefix((uint32_t)deg, lane);
+            offs[lane] = off;
+            r0s[lane] = r0;
+            if (lane == 63) offs[64] = off + deg;
             __syncthreads();
-            if (lane >= l0 && lane < l1 && valid) {
-                const uint32_t o = off - base;
-                HbUnit U{s, h, t, r0, deg, sc + o, fl + o, la + o, lb + o, scored};
-                Rng g = hb_rng(h, v, t, 0);
-                U.maintain(g);
-                h.rngk[(size_t)t * h.n_nodes + v] = g.k;  // emitGossip continues this (node, topic) draw stream
-                grafts += U.grafts;
-                prunes += U.prunes;
-                links += U.links;
+            // windows of whole rows: lanes [l0, l1) whose rows fit [offs[l0], offs[l0] + HB_STAGE)
+            uint32_t l0 = 0;
+            while (l0 < 64 && offs[l0] < offs[64]) {
+                const uint32_t base = offs[l0];
+                uint32_t l1 = l0;
+                while (l1 < 64 && offs[l1 + 1] - base <= HB_STAGE) ++l1;  // (uniform: every lane computes it)
+                const uint32_t end = offs[l1];
+                for (uint32_t k = base + lane; k < end; k += 64) {  // item k belongs to the row holding it
+                    uint32_t lo = l0, hi = l1;  // offs[lo] <= k < offs[lo + 1]
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (offs[mid] <= k) lo = mid;
+                        else hi = mid;
+                    }
+                    const uint64_t r = (uint64_t)r0s[lo] + (k - offs[lo]);
+                    sc[k - base] = s.score[r];
+                    fl[k - base] = stage_bits(s, h, r, t);
+                }
+                __syncthreads();
+                if (lane >= l0 && lane < l1 && valid) {
+                    const uint32_t o = off - base;
+                    HbUnit U{s, h, t, r0, deg, sc + o, fl + o, la + o, lb + o, scored};
+                    Rng g = hb_rng(h, v, t, 0);
+                    U.maintain(g);
+                    h.rngk[(size_t)t * h.n_nodes + v] = g.k;  // emitGossip continues this (node, topic) draw stream
+                    grafts += U.grafts;
+                    prunes += U.prunes;
+                    links += U.links;
+                }
+                __syncthreads();  // the stage is reused by the next window / batch
+                l0 = l1;
             }
-            __syncthreads();  // the stage is reused by the next window / chunk
-            l0 = l1;
         }
+        __syncthreads();  // pfx is rewritten by the next group
     }
     flush_count(h.stats, HB_GRAFTS, grafts);
     flush_count(h.stats, HB_PRUNES, prunes);
@@ -563,42 +602,50 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
-// emitGossip of topic t for every node.  A wave takes 64 consecutive nodes:
-// one coalesced pass over their pairs rewrites the topic's IHAVE slots of the
-// range (0 = none) and stages each pair's target eligibility in LDS; then a
-// lane per node counts its GetGossipIDs, lists its eligible peers in LDS,
-// shuffles and writes the targets.  A tile whose rows exceed the stage, and
-// every list longer than MaxIHaveLength (per-target reshuffle + truncation,
-// :1708-1716), goes to k_hb_gossip_long, one wave per node.
-__global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
-                                                  uint32_t n_gb) {
-    __shared__ int64_t rs[65];
-    __shared__ uint8_t el[HB_STAGE];
-    __shared__ uint16_t pl[HB_STAGE];
-    __shared__ uint32_t Ls[64];
-    __shared__ unsigned long long Ds[64];
-    uint64_t msgs = 0, ids = 0;
-    const uint32_t lane = threadIdx.x;
+// emitGossip of topic t for every node.  A wave takes a tile of 64
+// consecutive nodes: one coalesced pass over their pairs (four per lane in
+// flight) rewrites the topic's IHAVE slots of the range (0 = none) and stages
+// each pair's target eligibility in LDS; then a lane per node counts its
+// GetGossipIDs, lists its eligible peers in LDS, shuffles and writes the
+// targets.  A tile whose rows exceed the stage, and every list longer than
+// MaxIHaveLength (per-target reshuffle + truncation, :1708-1716), goes to
+// k_hb_gossip_long, one wave per node.  Blocks of four waves over a bounded
+// grid: one counter atomic per block.
+__global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
+                                                   uint32_t n_gb) {
+    __shared__ int64_t rs_w[SCAN_WAVES][65];
+    __shared__ uint8_t el_w[SCAN_WAVES][HB_STAGE];
+    __shared__ uint16_t pl_w[SCAN_WAVES][HB_STAGE];
+    const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    int64_t* rs = rs_w[wave];
+    uint8_t* el = el_w[wave];
+    uint16_t* pl = pl_w[wave];
+    unsigned long long cnt[2] = {0, 0};  // IHAVE messages, ids
     const size_t tslot = (size_t)t * h.n_pairs;
-    for (uint32_t v0 = blockIdx.x * 64u; v0 < h.n_nodes; v0 += gridDim.x * 64u) {
-        const uint32_t nv = min(64u, h.n_nodes - v0);
-        rs[lane] = h.row_ptr[v0 + min(lane, nv)];
-        if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+    const uint32_t n_tiles = (h.n_nodes + 63) / 64;
+    for (uint32_t tb = blockIdx.x * SCAN_WAVES; tb < n_tiles; tb += gridDim.x * SCAN_WAVES) {
+        const uint32_t tile = tb + wave;  // (block-uniform loop: every wave reaches every barrier)
+        const uint32_t v0 = tile * 64u;
+        const uint32_t nv = tile < n_tiles ? min(64u, h.n_nodes - v0) : 0;
+        if (nv) {
+            rs[lane] = h.row_ptr[v0 + min(lane, nv)];
+            if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
+        }
         __syncthreads();
-        const int64_t pa = rs[0], pb = rs[64];
+        const int64_t pa = nv ? rs[0] : 0, pb = nv ? rs[64] : 0;
         const bool staged = pb - pa <= HB_STAGE;
-        for (int64_t rb = pa + lane; rb < pb; rb += 256) {  // four pairs per lane, loads first
+        for (int64_t rb = pa + lane; rb < pb; rb += 256) {
             uint8_t pf[4], ef[4], rf[4], dt[4];
             double sc[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int64_t r = rb + 64 * j;
-                const bool in = r < pb;
-                pf[j] = in && staged ? s.pflags[r] : 0;
-                ef[j] = in && staged ? h.eflags[r] : 0;
-                rf[j] = in && staged ? s.rflags[flag_index(r, t, s.n_topics)] : 0;
-                dt[j] = in && staged ? h.dirty[r] : 0;
-                sc[j] = in && staged ? s.score[r] : 0.0;
+                const bool in = r < pb && staged;
+                pf[j] = in ? s.pflags[r] : 0;
+                ef[j] = in ? h.eflags[r] : 0;
+                rf[j] = in ? s.rflags[flag_index(r, t, s.n_topics)] : 0;
+                dt[j] = in ? h.dirty[r] : 0;
+                sc[j] = in ? s.score[r] : 0.0;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -615,43 +662,10 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
             }
         }
         __syncthreads();
-        // GetGossipIDs lengths and digests of the tile's nodes: a coalesced pass
-        // over each cached batch's rows (node-major words), summed per node in LDS
-        Ls[lane] = 0;
-        Ds[lane] = 0;
-        __syncthreads();
-        for (uint32_t b = 0; b < n_gb; ++b) {
-            const GossipBatch B = gb[b];
-            const uint32_t W = B.n_words, cnt = nv * W;
-            const uint64_t* rows = B.seen + (size_t)v0 * W;
-            for (uint32_t i0 = lane; i0 < cnt; i0 += 256) {
-                uint64_t wd[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) wd[j] = i0 + 64 * j < cnt ? rows[i0 + 64 * j] : 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint64_t word = wd[j];
-                    if (!word) continue;
-                    const uint32_t i = i0 + 64 * j, node = i / W, w = i - node * W;
-                    const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
-                    const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
-                    atomicAdd(&Ls[node], (uint32_t)__popcll(word));
-                    uint64_t d = 0;
-                    if (word == full) {  // every message of the word: its precomputed digest sum
-                        d = h.mc_digest[B.wdig_base + w];
-                    } else {
-                        for (; word; word &= word - 1)
-                            d += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
-                    }
-                    atomicAdd(&Ds[node], (unsigned long long)d);
-                }
-            }
-        }
-        __syncthreads();
         if (lane < nv) {
             const uint32_t v = v0 + lane;
-            const uint64_t dig = Ds[lane];
-            const uint32_t L = Ls[lane];
+            uint64_t dig;
+            const uint32_t L = gossip_ids(h, v, gb, n_gb, dig);
             if (L > 0) {  // emitGossip returns early on an empty list, drawing nothing
                 if (!staged || L > (uint32_t)h.gp.max_ihave) {
                     h.long_nodes[atomicAdd(h.n_long, 1u)] = v;  // one wave per node: k_hb_gossip_long
@@ -672,21 +686,21 @@ __global__ __launch_bounds__(64) void k_hb_gossip(DevState s, HbState h, uint32_
                             Rng g = hb_rng(h, v, t, h.rngk[(size_t)t * h.n_nodes + v]);
                             g.shuffle(peers, np);
                         }
-                        for (int p = 0; p < target; ++p) {
-                            const size_t x = tslot + rs[lane] + peers[p];
+                        for (int q = 0; q < target; ++q) {
+                            const size_t x = tslot + rs[lane] + peers[q];
                             h.ihave_len[x] = L;
                             h.ihave_hash[x] = dig;
                         }
-                        msgs += (uint64_t)target;
-                        ids += (uint64_t)target * L;
+                        cnt[0] += (uint64_t)target;
+                        cnt[1] += (uint64_t)target * L;
                     }
                 }
             }
         }
         __syncthreads();  // rs / el / pl are rewritten by the next tile
     }
-    flush_count(h.stats, HB_IHAVE_MSGS, msgs);
-    flush_count(h.stats, HB_IHAVE_IDS, ids);
+    const uint32_t slot[2] = {HB_IHAVE_MSGS, HB_IHAVE_IDS};
+    block_count<2>(cnt, h.stats, slot);
 }
 
 // ---- lists longer than MaxIHaveLength: one wave per queued node -------------
@@ -1139,14 +1153,15 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
 
 hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_scan, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h);  // one wave per tile
+    hipLaunchKernelGGL(k_hb_scan, dim3(grid_cap(h.n_nodes, 256)), dim3(256), 0, st, s, h);  // a tile per wave
     return hipGetLastError();
 }
 
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    // the grid strides over the topic's worklist, whose length only the device knows
-    hipLaunchKernelGGL(k_hb_maintain, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h, t);
+    // a wave per group of 64 tiles (the per-tile lists of k_hb_scan)
+    const uint64_t groups = ((uint64_t)h.n_nodes + 64 * 64 - 1) / (64 * 64);
+    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 4096)), dim3(64), 0, st, s, h, t);
     if (max_deg > HB_LANE_DEG) {
         const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
         static bool attr = false;
@@ -1166,7 +1181,7 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
     if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hb_gossip, dim3(blocks_for(h.n_nodes, 64)), dim3(64), 0, st, s, h, t, gb, n_gb);
+    hipLaunchKernelGGL(k_hb_gossip, dim3(grid_cap(h.n_nodes, 256)), dim3(256), 0, st, s, h, t, gb, n_gb);
     // queued nodes (long lists, tiles with hub rows): the kernel returns at once without any
     const size_t lds = sizeof(uint32_t) * max_ids + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
     static size_t attr = 0;
