@@ -602,6 +602,34 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
+// GetGossipIDs of (v, t): its length and multiset digest, straight from the
+// cached batches' seen words (node-major rows).
+__device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, const GossipBatch* __restrict__ gb,
+                                               uint32_t n_gb, uint64_t& dig) {
+    uint32_t L = 0;
+    dig = 0;
+    for (uint32_t b = 0; b < n_gb; ++b) {
+        const GossipBatch B = gb[b];
+        for (uint32_t w = 0; w < B.n_words; ++w) {
+            uint64_t word = B.seen[(size_t)v * B.n_words + w];
+            L += (uint32_t)__popcll(word);
+            // a node holding every message of the word (the common case once a
+            // batch has spread) adds the word's precomputed digest sum
+            const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
+            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+            if (word && word == full) {
+                dig += h.mc_digest[B.wdig_base + w];
+                continue;
+            }
+            while (word) {
+                dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
+                word &= word - 1;
+            }
+        }
+    }
+    return L;
+}
+
 // emitGossip of topic t for every node.  A wave takes a tile of 64
 // consecutive nodes: one coalesced pass over their pairs (four per lane in
 // flight) rewrites the topic's IHAVE slots of the range (0 = none) and stages
