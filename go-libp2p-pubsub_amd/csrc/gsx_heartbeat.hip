@@ -459,8 +459,10 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
 
 constexpr int HB_STAGE = 1024;  // pairs a lane-per-unit wave stages at once
 
+constexpr uint32_t MAINT_GROUP = 4;  // tiles per maintenance wave: up to 256 listed units
+
 // (A) per topic: the listed units, one lane each, rows staged in LDS.  A wave
-// takes a group of 64 tiles, gathers their listed units (a prefix over the
+// takes a group of MAINT_GROUP tiles, gathers their listed units (a prefix over the
 // per-tile counts: no atomics) 64 at a time, and stages their rows
 // cooperatively (every lane loads items of every row, 64 loads per
 // instruction); when the rows exceed the stage it runs them in windows of
@@ -479,8 +481,8 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
     const bool scored = t < s.n_topics && s.tp[t].scored;
     uint64_t grafts = 0, prunes = 0;
     int64_t links = 0;
-    for (uint32_t g0 = blockIdx.x * 64u; g0 < n_tiles; g0 += gridDim.x * 64u) {
-        const uint32_t c = g0 + lane < n_tiles ? tcnt[g0 + lane] : 0;
+    for (uint32_t g0 = blockIdx.x * MAINT_GROUP; g0 < n_tiles; g0 += gridDim.x * MAINT_GROUP) {
+        const uint32_t c = (lane < MAINT_GROUP && g0 + lane < n_tiles) ? tcnt[g0 + lane] : 0;
         const uint32_t p = wave_prefix(c, lane);
         pfx[lane] = p;
         if (lane == 63) pfx[64] = p + c;
@@ -1187,9 +1189,9 @@ hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st) {
 
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    // a wave per group of 64 tiles (the per-tile lists of k_hb_scan)
-    const uint64_t groups = ((uint64_t)h.n_nodes + 64 * 64 - 1) / (64 * 64);
-    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 4096)), dim3(64), 0, st, s, h, t);
+    // a wave per group of MAINT_GROUP tiles (the per-tile lists of k_hb_scan)
+    const uint64_t groups = ((uint64_t)h.n_nodes + 64 * MAINT_GROUP - 1) / (64 * MAINT_GROUP);
+    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384)), dim3(64), 0, st, s, h, t);
     if (max_deg > HB_LANE_DEG) {
         const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
         static bool attr = false;
