@@ -266,6 +266,8 @@ struct DevGossipParams {
 // node v has message k iff bit k % 64 of seen[v * n_words + k / 64].
 struct GossipBatch {
     const uint64_t* seen;
+    const uint64_t* dig;  // [node]: multiset digest of the node's ids in this batch (k_mc_summary)
+    const uint32_t* cnt;  // [node]: how many ids the node holds in this batch
     uint32_t n_words;
     uint32_t slot_base;  // slot of message 0 in HbState::mc_digest
     uint32_t wdig_base;  // HbState::mc_digest[wdig_base + w]: digest sum of all of word w's messages
@@ -318,6 +320,13 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
                             uint32_t max_ids, int64_t max_deg, hipStream_t st);
 constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
+// Per-node (count, digest) of a batch the message cache keeps (computed once
+// when it is cached, read by every heartbeat's emitGossip while it is in the
+// gossip window): msg_dig[k] = mix64(id_k + golden), word_dig[w] = the sum of
+// word w's messages' digests.
+hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_words, uint32_t n_msgs,
+                             const uint64_t* msg_dig, const uint64_t* word_dig, uint64_t* dig, uint32_t* cnt,
+                             hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
                           uint64_t* out, hipStream_t st);

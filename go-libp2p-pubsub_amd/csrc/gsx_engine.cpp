@@ -120,6 +120,8 @@ struct gsx_engine {
         uint32_t topic = 0, n_msgs = 0, n_words = 0;
         uint64_t* d_seen = nullptr;  // [node][word]: the call's seen rows, handed over (no copy)
         size_t seen_words = 0;       // allocation size, for the buffer pool
+        uint64_t* d_dig = nullptr;   // [node] summary of the batch (k_mc_summary), in the same allocation
+        uint32_t* d_cnt = nullptr;
         std::vector<uint64_t> ids;
     };
     std::deque<std::vector<McBatch>> mc;
@@ -148,6 +150,8 @@ struct gsx_engine {
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
         unsigned long long* gray_pairs = nullptr;  // pairs with FWD_GIN of the current fwd (k_prop_fwd)
+        uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
+        size_t dig_cap = 0;
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
         size_t seen_words = 0;
         gsx::PropState last{};
@@ -372,7 +376,8 @@ void free_state(gsx_engine* e) {
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
                   e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
-                  e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs};
+                  e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
+                  e->prop.d_dig};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
@@ -1535,7 +1540,8 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         P.rows_cap = rc_rows;
     }
     if (!P.seen) {  // handed to the message cache by the previous gossipsub call
-        P.seen_words = (size_t)P.words_cap * N;
+        // the rows, then (kept by the message cache) the batch's per-node summary: dig[N] u64, cnt[N] u32
+        P.seen_words = (size_t)P.words_cap * N + 2 * N;
         P.seen = seen_acquire(e, P.seen_words);
         if (!P.seen) return fail(e, GSX_ENOMEM, "hipMalloc: seen rows");
     }
@@ -1747,6 +1753,27 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         b.n_words = W;
         b.d_seen = P.seen;  // the cache keeps this call's seen rows; the next call takes a pooled buffer
         b.seen_words = P.seen_words;
+        {  // per-node (count, digest) summary of the batch for emitGossip (id digests: gsx.h)
+            const size_t N = ps.n_nodes;
+            std::vector<uint64_t> dg((size_t)W * 64 + W, 0);
+            for (size_t k = 0; k < P.ids.size(); ++k) {
+                dg[k] = id_digest(P.ids[k]);
+                dg[(size_t)W * 64 + k / 64] += dg[k];
+            }
+            if (P.dig_cap < dg.size()) {
+                if (P.d_dig) (void)hipFree(P.d_dig);
+                P.d_dig = nullptr;
+                P.dig_cap = 0;
+                if (int rc = dalloc(e, &P.d_dig, dg.size())) return rc;
+                P.dig_cap = dg.size();
+            }
+            HIPCHK(e, hipMemcpyAsync(P.d_dig, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
+            b.d_dig = P.seen + (size_t)W * N;
+            b.d_cnt = reinterpret_cast<uint32_t*>(P.seen + (size_t)W * N + N);
+            HIPCHK(e, gsx::launch_mc_summary(P.seen, (uint32_t)N, W, ps.n_msgs, P.d_dig, P.d_dig + (size_t)W * 64,
+                                             b.d_dig, b.d_cnt, e->stream));
+            HIPCHK(e, hipStreamSynchronize(e->stream));  // `dg` is on the host stack
+        }
         P.seen = nullptr;
         b.ids = P.ids;
         if (e->mc.empty()) e->mc.emplace_back();
@@ -2164,8 +2191,9 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         for (size_t w = 0; w < n_win; ++w)
             for (const auto& b : e->mc[w]) {
                 if (b.topic != t) continue;
-                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.n_words, (uint32_t)e->mc_digest_host.size(),
-                                                      (uint32_t)wdig.size(), b.n_msgs});
+                e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.d_dig, b.d_cnt, b.n_words,
+                                                      (uint32_t)e->mc_digest_host.size(), (uint32_t)wdig.size(),
+                                                      b.n_msgs});
                 for (size_t k = 0; k < b.ids.size(); ++k) {
                     const uint64_t d = id_digest(b.ids[k]);
                     e->mc_digest_host.push_back(d);

@@ -433,11 +433,20 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                     active = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1);
                     const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
                     if (!active && (grow || more_out)) {  // getPeers finds a candidate? (:1370-1385, :1450-1476)
-                        for (int i = 0; i < deg && !active; ++i) {
-                            const uint16_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
-                            if ((m & SC_CAND) && !(m >> k & 1) && (grow || (m & SC_OUT)) &&
-                                h.backoff[(size_t)t * h.n_pairs + r0 + i] == 0)
-                                active = true;
+                        // eight backoff entries in flight at a time
+                        for (int i0 = 0; i0 < deg && !active; i0 += 8) {
+                            bool ok[8];
+                            int64_t bo[8];
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const int i = i0 + j;
+                                const uint16_t m =
+                                    i < deg ? (staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt)) : 0;
+                                ok[j] = (m & SC_CAND) && !(m >> k & 1) && (grow || (m & SC_OUT));
+                                bo[j] = ok[j] ? h.backoff[(size_t)t * h.n_pairs + r0 + i] : 1;
+                            }
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) active |= ok[j] && bo[j] == 0;
                         }
                     }
                     h.rngk[(size_t)t * h.n_nodes + v] = 0;
@@ -604,30 +613,40 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
-// GetGossipIDs of (v, t): its length and multiset digest, straight from the
-// cached batches' seen words (node-major rows).
+// A cached batch's per-node summary (count, digest of its ids): once per batch.
+__global__ __launch_bounds__(256) void k_mc_summary(const uint64_t* __restrict__ seen, uint32_t n_nodes,
+                                                    uint32_t n_words, uint32_t n_msgs,
+                                                    const uint64_t* __restrict__ msg_dig,
+                                                    const uint64_t* __restrict__ word_dig, uint64_t* __restrict__ dig,
+                                                    uint32_t* __restrict__ cnt) {
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n_nodes; v += gridDim.x * 256u) {
+        uint32_t L = 0;
+        uint64_t d = 0;
+        for (uint32_t w = 0; w < n_words; ++w) {
+            uint64_t word = seen[(size_t)v * n_words + w];
+            L += (uint32_t)__popcll(word);
+            const uint32_t left = n_msgs > w * 64 ? n_msgs - w * 64 : 0;
+            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+            if (word && word == full) {  // every message of the word (the common case once a batch has spread)
+                d += word_dig[w];
+                continue;
+            }
+            for (; word; word &= word - 1) d += msg_dig[w * 64 + (uint32_t)__builtin_ctzll(word)];
+        }
+        dig[v] = d;
+        cnt[v] = L;
+    }
+}
+
+// GetGossipIDs of (v, t): its length and multiset digest, the sum of the
+// node's summaries over the batches of the gossip window.
 __device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, const GossipBatch* __restrict__ gb,
                                                uint32_t n_gb, uint64_t& dig) {
     uint32_t L = 0;
     dig = 0;
     for (uint32_t b = 0; b < n_gb; ++b) {
-        const GossipBatch B = gb[b];
-        for (uint32_t w = 0; w < B.n_words; ++w) {
-            uint64_t word = B.seen[(size_t)v * B.n_words + w];
-            L += (uint32_t)__popcll(word);
-            // a node holding every message of the word (the common case once a
-            // batch has spread) adds the word's precomputed digest sum
-            const uint32_t left = B.n_msgs > w * 64 ? B.n_msgs - w * 64 : 0;
-            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
-            if (word && word == full) {
-                dig += h.mc_digest[B.wdig_base + w];
-                continue;
-            }
-            while (word) {
-                dig += h.mc_digest[B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word)];
-                word &= word - 1;
-            }
-        }
+        L += gb[b].cnt[v];
+        dig += gb[b].dig[v];
     }
     return L;
 }
@@ -1228,6 +1247,15 @@ hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
     if (h.n_hubs) hipLaunchKernelGGL(k_hb_recv_hub, dim3(std::min<uint32_t>(h.n_hubs, 4096)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_words, uint32_t n_msgs,
+                             const uint64_t* msg_dig, const uint64_t* word_dig, uint64_t* dig, uint32_t* cnt,
+                             hipStream_t st) {
+    if (n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_summary, dim3(grid_cap(n_nodes, 256)), dim3(256), 0, st, seen, n_nodes, n_words, n_msgs,
+                       msg_dig, word_dig, dig, cnt);
     return hipGetLastError();
 }
 
