@@ -57,24 +57,53 @@ __device__ __forceinline__ bool hb_in_mesh(const DevState& s, uint64_t r, uint32
 }
 
 // addBackoff / doAddBackoff, gossipsub.go:845-859 (0 = no entry; the zero
-// time is before every expiry)
+// time is before every expiry).  The presence bit of a new entry is set too.
 __device__ __forceinline__ void add_backoff(const HbState& h, uint64_t r, uint32_t t, int64_t interval) {
     int64_t* b = &h.backoff[(size_t)t * h.n_pairs + r];
     const int64_t expire = h.now + interval;
-    if (*b == 0 || *b < expire) *b = expire;
+    const int64_t old = *b;
+    if (old == 0) atomicOr((unsigned long long*)&h.bo_bits[(size_t)t * h.bo_words + r / 64], 1ull << (r % 64));
+    if (old == 0 || old < expire) *b = expire;
+}
+__device__ __forceinline__ bool backoff_present(const HbState& h, uint64_t r, uint32_t t) {
+    return (h.bo_bits[(size_t)t * h.bo_words + r / 64] >> (r % 64)) & 1;
 }
 
-// clearBackoff, gossipsub.go:1585-1604
-__global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint64_t n) {
+// clearBackoff, gossipsub.go:1585-1604: one wave per (topic, 64-pair word),
+// which also owns that word of the presence bits.
+__global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint32_t n_topics) {
     uint64_t cleared = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
-        const int64_t b = h.backoff[i];
-        if (b != 0 && b + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
-            h.backoff[i] = 0;
-            ++cleared;
+    const uint32_t lane = threadIdx.x % 64;
+    const uint64_t n_words = (uint64_t)n_topics * h.bo_words;
+    for (uint64_t wd = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / 64; wd < n_words;
+         wd += (uint64_t)gridDim.x * 4u) {
+        const uint32_t t = (uint32_t)(wd / h.bo_words);
+        const uint64_t r = (wd % h.bo_words) * 64 + lane;
+        bool clr = false;
+        if (r < h.n_pairs) {
+            int64_t* b = &h.backoff[(size_t)t * h.n_pairs + r];
+            if (*b != 0 && *b + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
+                *b = 0;
+                clr = true;
+                ++cleared;
+            }
         }
+        const uint64_t m = __ballot(clr);
+        if (lane == 0 && m) h.bo_bits[wd] &= ~m;
     }
     flush_count(h.stats, HB_BACKOFF_CLEARED, cleared);
+}
+
+__global__ __launch_bounds__(256) void k_bo_rebuild(const int64_t* __restrict__ backoff, uint64_t* __restrict__ bits,
+                                                    uint64_t n_pairs, uint64_t words, uint32_t n_topics) {
+    const uint32_t lane = threadIdx.x % 64;
+    const uint64_t n_words = (uint64_t)n_topics * words;
+    for (uint64_t wd = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / 64; wd < n_words; wd += (uint64_t)gridDim.x * 4u) {
+        const uint32_t t = (uint32_t)(wd / words);
+        const uint64_t r = (wd % words) * 64 + lane;
+        const uint64_t m = __ballot(r < n_pairs && backoff[(size_t)t * n_pairs + r] != 0);
+        if (lane == 0) bits[wd] = m;
+    }
 }
 
 // ---- (A) mesh maintenance ---------------------------------------------------------
@@ -107,7 +136,7 @@ __device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& 
         f |= ST_CAND;
     if (ef & EDGE_OUTBOUND) f |= ST_OUT;
     // only a candidate's backoff is ever tested (a pruned mesh peer gets the bit when pruned)
-    if ((f & ST_CAND) && !(f & ST_MESH) && h.backoff[(size_t)t * h.n_pairs + r] != 0) f |= ST_BACKOFF;
+    if ((f & ST_CAND) && !(f & ST_MESH) && backoff_present(h, r, t)) f |= ST_BACKOFF;
     return f;
 }
 
@@ -331,10 +360,10 @@ constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (2 B each) for the 
 // A pair's scan bits for topics t0 .. t0+7: bit k = in the mesh of topic t0+k,
 // bit 8 = score < 0, bit 9 = outbound, bit 10 = getPeers' base filter with
 // score >= 0 (present, connected, mesh-capable, not direct).
-constexpr uint16_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;
-__device__ __forceinline__ uint16_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS]) {
+constexpr uint32_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;  // bits 16 + k: backoff entry of t0 + k
+__device__ __forceinline__ uint32_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS]) {
     if (!(pf & PAIR_PRESENT)) return 0;
-    uint16_t m = 0;
+    uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_TOPICS; ++k)
         if (rf[k] & REC_IN_MESH) m |= 1u << k;
@@ -343,12 +372,16 @@ __device__ __forceinline__ uint16_t scan_pack(uint8_t pf, uint8_t ef, double sc,
     if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0) m |= SC_CAND;
     return m;
 }
-__device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
+__device__ __forceinline__ uint32_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
                                               uint32_t nt) {
     uint8_t rf[SCAN_TOPICS];
+    uint32_t bo = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_TOPICS; ++k) rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
-    return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf);
+    for (int k = 0; k < SCAN_TOPICS; ++k) {
+        rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
+        if (k < (int)nt && backoff_present(h, r, t0 + k)) bo |= 1u << (16 + k);
+    }
+    return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf) | bo;
 }
 
 // (A) scan: every unit of every topic.  A wave takes a tile of 64 consecutive
@@ -366,12 +399,12 @@ __device__ __forceinline__ uint16_t scan_bits(const DevState& s, const HbState& 
 constexpr int SCAN_WAVES = 4;
 __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
     __shared__ int64_t rs_w[SCAN_WAVES][65];
-    __shared__ uint16_t st_w[SCAN_WAVES][SCAN_STAGE];
+    __shared__ uint32_t st_w[SCAN_WAVES][SCAN_STAGE];
     const DevGossipParams& gp = h.gp;
     const bool og_tick = gp.og_ticks && h.tick % gp.og_ticks == 0;
     const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
     int64_t* rs = rs_w[wave];
-    uint16_t* st = st_w[wave];
+    uint32_t* st = st_w[wave];
     const uint32_t T = s.n_topics;
     const uint32_t n_tiles = (h.n_nodes + 63) / 64;
     unsigned long long links[1] = {0};
@@ -395,6 +428,7 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                 for (int64_t rb = pa + lane; rb < pb; rb += 256) {
                     uint8_t pf[4], ef[4], rf[4][SCAN_TOPICS];
                     double sc[4];
+                    uint64_t bw[4][SCAN_TOPICS];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t r = rb + 64 * j;
@@ -403,12 +437,20 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                         ef[j] = in ? h.eflags[r] : 0;
                         sc[j] = in ? s.score[r] : 0.0;
 #pragma unroll
-                        for (int k = 0; k < SCAN_TOPICS; ++k)
+                        for (int k = 0; k < SCAN_TOPICS; ++k) {
                             rf[j][k] = (in && k < (int)nt) ? s.rflags[flag_index(r, t0 + k, T)] : 0;
+                            bw[j][k] = (in && k < (int)nt) ? h.bo_bits[(size_t)(t0 + k) * h.bo_words + r / 64] : 0;
+                        }
                     }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (rb + 64 * j < pb) st[rb + 64 * j - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j]);
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t r = rb + 64 * j;
+                        if (r >= pb) continue;
+                        uint32_t bo = 0;
+#pragma unroll
+                        for (int k = 0; k < SCAN_TOPICS; ++k) bo |= (uint32_t)((bw[j][k] >> (r % 64)) & 1) << (16 + k);
+                        st[r - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j]) | bo;
+                    }
                 }
             }
             __syncthreads();
@@ -416,7 +458,7 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
 #pragma unroll
             for (int k = 0; k < SCAN_TOPICS; ++k) n[k] = neg[k] = outb[k] = 0;
             for (int i = 0; i < deg; ++i) {
-                const uint16_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
+                const uint32_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
 #pragma unroll
                 for (int k = 0; k < SCAN_TOPICS; ++k)
                     if (m >> k & 1) {
@@ -433,20 +475,9 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                     active = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1);
                     const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
                     if (!active && (grow || more_out)) {  // getPeers finds a candidate? (:1370-1385, :1450-1476)
-                        // eight backoff entries in flight at a time
-                        for (int i0 = 0; i0 < deg && !active; i0 += 8) {
-                            bool ok[8];
-                            int64_t bo[8];
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                const int i = i0 + j;
-                                const uint16_t m =
-                                    i < deg ? (staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt)) : 0;
-                                ok[j] = (m & SC_CAND) && !(m >> k & 1) && (grow || (m & SC_OUT));
-                                bo[j] = ok[j] ? h.backoff[(size_t)t * h.n_pairs + r0 + i] : 1;
-                            }
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) active |= ok[j] && bo[j] == 0;
+                        for (int i = 0; i < deg && !active; ++i) {
+                            const uint32_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
+                            active = (m & SC_CAND) && !(m >> k & 1) && !(m >> (16 + k) & 1) && (grow || (m & SC_OUT));
                         }
                     }
                     h.rngk[(size_t)t * h.n_nodes + v] = 0;
@@ -1194,9 +1225,18 @@ static inline unsigned wave_grid(uint64_t n) {
 }
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
-    const uint64_t n = (uint64_t)n_topics * h.n_pairs;
+    const uint64_t n = (uint64_t)n_topics * h.bo_words;  // one wave per (topic, word)
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(grid_cap(n, 256)), dim3(256), 0, st, h, n);
+    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(grid_cap(n * 64, 256)), dim3(256), 0, st, h, n_topics);
+    return hipGetLastError();
+}
+
+hipError_t launch_bo_rebuild(const int64_t* backoff, uint64_t* bits, uint64_t n_pairs, uint64_t words,
+                             uint32_t n_topics, hipStream_t st) {
+    const uint64_t n = (uint64_t)n_topics * words;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bo_rebuild, dim3(grid_cap(n * 64, 256)), dim3(256), 0, st, backoff, bits, n_pairs, words,
+                       n_topics);
     return hipGetLastError();
 }
 
