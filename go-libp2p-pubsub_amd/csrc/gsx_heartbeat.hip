@@ -128,15 +128,18 @@ constexpr uint8_t ST_OUT = 4;      // outbound (gs.outbound[p])
 constexpr uint8_t ST_BACKOFF = 8;  // gs.backoff[topic][p] present (map presence, :1377)
 
 __device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
+    // every input loaded unconditionally (no load waits at a divergent join)
     const uint8_t pf = s.pflags[r], ef = h.eflags[r];
+    const uint8_t rf = s.rflags[flag_index(r, t, s.n_topics)];
+    const bool bo = backoff_present(h, r, t);
     uint8_t f = 0;
-    if ((pf & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH)) f |= ST_MESH;
+    if ((pf & PAIR_PRESENT) && (rf & REC_IN_MESH)) f |= ST_MESH;
     if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) &&
         !(ef & EDGE_DIRECT))
         f |= ST_CAND;
     if (ef & EDGE_OUTBOUND) f |= ST_OUT;
     // only a candidate's backoff is ever tested (a pruned mesh peer gets the bit when pruned)
-    if ((f & ST_CAND) && !(f & ST_MESH) && backoff_present(h, r, t)) f |= ST_BACKOFF;
+    if ((f & ST_CAND) && !(f & ST_MESH) && bo) f |= ST_BACKOFF;
     return f;
 }
 
@@ -426,22 +429,32 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
             const uint32_t nt = min((uint32_t)SCAN_TOPICS, T - t0);
             if (staged) {
                 for (int64_t rb = pa + lane; rb < pb; rb += 256) {
+                    // unconditional loads of clamped (valid) addresses, masked after: a
+                    // load under a divergent branch is waited for at the branch's join
                     uint8_t pf[4], ef[4], rf[4][SCAN_TOPICS];
                     double sc[4];
                     uint64_t bw[4][SCAN_TOPICS];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int64_t r = rb + 64 * j;
-                        const bool in = r < pb;
-                        pf[j] = in ? s.pflags[r] : 0;
-                        ef[j] = in ? h.eflags[r] : 0;
-                        sc[j] = in ? s.score[r] : 0.0;
+                        const int64_t r = min(rb + 64 * j, pb - 1);
+                        pf[j] = s.pflags[r];
+                        ef[j] = h.eflags[r];
+                        sc[j] = s.score[r];
 #pragma unroll
                         for (int k = 0; k < SCAN_TOPICS; ++k) {
-                            rf[j][k] = (in && k < (int)nt) ? s.rflags[flag_index(r, t0 + k, T)] : 0;
-                            bw[j][k] = (in && k < (int)nt) ? h.bo_bits[(size_t)(t0 + k) * h.bo_words + r / 64] : 0;
+                            const uint32_t tk = min(t0 + k, T - 1);
+                            rf[j][k] = s.rflags[flag_index(r, tk, T)];
+                            bw[j][k] = h.bo_bits[(size_t)tk * h.bo_words + r / 64];
                         }
                     }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int k = 0; k < SCAN_TOPICS; ++k)
+                            if (k >= (int)nt) {
+                                rf[j][k] = 0;
+                                bw[j][k] = 0;
+                            }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t r = rb + 64 * j;
@@ -718,14 +731,13 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
             uint8_t pf[4], ef[4], rf[4], dt[4];
             double sc[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t r = rb + 64 * j;
-                const bool in = r < pb && staged;
-                pf[j] = in ? s.pflags[r] : 0;
-                ef[j] = in ? h.eflags[r] : 0;
-                rf[j] = in ? s.rflags[flag_index(r, t, s.n_topics)] : 0;
-                dt[j] = in ? h.dirty[r] : 0;
-                sc[j] = in ? s.score[r] : 0.0;
+            for (int j = 0; j < 4; ++j) {  // unconditional loads of clamped addresses (see k_hb_scan)
+                const int64_t r = min(rb + 64 * j, pb - 1);
+                pf[j] = s.pflags[r];
+                ef[j] = h.eflags[r];
+                rf[j] = s.rflags[flag_index(r, t, s.n_topics)];
+                dt[j] = h.dirty[r];
+                sc[j] = s.score[r];
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
