@@ -2256,8 +2256,9 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
                                         e->max_deg, e->stream));
     }
-    // the receivers score the senders as the round left them
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the pairs (A) touched
+    // the receivers score the senders as the round left them: (B) and (C)
+    // re-evaluate a touched pair where they read it (live_score), the cache is
+    // brought up to date once, at the end of the round
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
@@ -2269,7 +2270,6 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
     return GSX_OK;
 }
 

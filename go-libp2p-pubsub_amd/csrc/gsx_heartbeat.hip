@@ -977,19 +977,27 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
         uint32_t have = 0;  // topics < RECV_TOPICS with a cached count
-        for (int64_t q = r0; q < r1; ++q) {  // q = (u -> v), ascending v
+        for (int64_t c0 = r0; c0 < r1; c0 += 8) {
+          // the row's marks eight at a time, loaded unconditionally (clamped)
+          uint8_t ib[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ib[j] = h.inbox[min(c0 + j, r1 - 1)];
+          for (int j = 0; j < 8 && c0 + j < r1; ++j) {
+            const int64_t q = c0 + j;  // q = (u -> v), ascending v
             if (!h.halo_ctl) {
-                if (!h.inbox[q]) continue;
+                if (!ib[j]) continue;
                 h.inbox[q] = 0;
             }
             uint32_t r;
             uint64_t grafts, prunes;
             if (!recv_control(h, q, true, r, grafts, prunes)) continue;
-            const double score = s.score[q];  // gs.score.Score(p) once per control message
+            // gs.score.Score(p) once per control message: the cache, re-evaluated where
+            // u's own maintenance changed the record (the round's state at this point)
+            const double score = live_score(s, h, q);
             const uint8_t ef = h.eflags[q];
             // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
             if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
-            h.dirty[q] = 1;  // its record may change below: its score is re-evaluated after (B)
+            h.dirty[q] = 1;  // its record may change below: read live from now on, re-scored at the end
             uint64_t resp = 0;
             for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
                 const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
@@ -1052,6 +1060,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 }
                 ++handled;
             }
+          }
         }
     }
     flush_count(h.stats, HB_ACCEPTED, accepted);
@@ -1098,9 +1107,10 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
                 if (w0 && !(r & HALO) && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
-                const double score = s.score[q];
+                const double score = live_score(s, h, q);
                 const uint8_t ef = h.eflags[q];
                 if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
+                __syncthreads();  // every lane has read dirty[q] before lane 0 sets it
                 if (w0) h.dirty[q] = 1;
                 uint64_t resp = 0;
                 for (; grafts; grafts &= grafts - 1) {
@@ -1200,7 +1210,7 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
         uint64_t resp = q == NO_PAIR ? 0 : (q & HALO) ? h.halo_resp[q & ~HALO] : h.resp[q];
         if (!h.halo_resp && q != NO_PAIR) h.resp[q] = 0;
         // AcceptFrom at v for the answering peer
-        if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
+        if (resp && !(h.eflags[r] & EDGE_DIRECT) && live_score(s, h, r) < h.graylist) resp = 0;
         if (resp) h.dirty[r] = 1;
         for (; resp; resp &= resp - 1) {
             if (handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp))) --links;
