@@ -325,6 +325,8 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
                             uint32_t max_ids, int64_t max_deg, hipStream_t st);
 constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
+// out[i] = a[i] && b[i] (the pairs a heartbeat step re-scores before the next reads them)
+hipError_t launch_mask_and(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n, hipStream_t st);
 // Per-node (count, digest) of a batch the message cache keeps (computed once
 // when it is cached, read by every heartbeat's emitGossip while it is in the
 // gossip window): msg_dig[k] = mix64(id_k + golden), word_dig[w] = the sum of

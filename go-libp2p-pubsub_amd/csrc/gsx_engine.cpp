@@ -2103,7 +2103,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         int rc = 0;
         const size_t E = e->E;
         if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
-            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 3 * E)) ||
+            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
             (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
             (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
             (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
@@ -2256,9 +2256,15 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
                                         e->max_deg, e->stream));
     }
-    // the receivers score the senders as the round left them: (B) and (C)
-    // re-evaluate a touched pair where they read it (live_score), the cache is
-    // brought up to date once, at the end of the round
+    // the receivers score the senders as the round left them: the pairs (A)
+    // touched that (B) reads (marked in the inbox) are re-scored
+    // (a shard's (B) reads every pair with remote control: all touched pairs)
+    uint8_t* sel = h.dirty;
+    if (!e->sharded()) {
+        sel = e->d_dirty + 3 * e->E;
+        HIPCHK(e, gsx::launch_mask_and(h.dirty, h.inbox, sel, e->E, e->stream));
+    }
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), sel, e->stream));
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
@@ -2270,6 +2276,14 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
+    // the pairs touched so far that (C) reads: those marked with an answer
+    // (a shard's (C) reads every pair with a remote answer: all touched pairs)
+    uint8_t* sel = h.dirty;
+    if (!e->sharded()) {
+        sel = e->d_dirty + 3 * e->E;
+        HIPCHK(e, gsx::launch_mask_and(h.dirty, h.answer, sel, e->E, e->stream));
+    }
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), sel, e->stream));
     return GSX_OK;
 }
 

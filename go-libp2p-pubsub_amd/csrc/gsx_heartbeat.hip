@@ -991,13 +991,13 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             uint32_t r;
             uint64_t grafts, prunes;
             if (!recv_control(h, q, true, r, grafts, prunes)) continue;
-            // gs.score.Score(p) once per control message: the cache, re-evaluated where
-            // u's own maintenance changed the record (the round's state at this point)
-            const double score = live_score(s, h, q);
+            // gs.score.Score(p) once per control message (the cache holds the round's
+            // state for every pair read here: k_mask_and + the subset re-score after (A))
+            const double score = s.score[q];
             const uint8_t ef = h.eflags[q];
             // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
             if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
-            h.dirty[q] = 1;  // its record may change below: read live from now on, re-scored at the end
+            h.dirty[q] = 1;  // its record may change below: re-scored before (C) reads it and at the end
             uint64_t resp = 0;
             for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
                 const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
@@ -1107,10 +1107,9 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
                 if (w0 && !(r & HALO) && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
-                const double score = live_score(s, h, q);
+                const double score = s.score[q];
                 const uint8_t ef = h.eflags[q];
                 if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
-                __syncthreads();  // every lane has read dirty[q] before lane 0 sets it
                 if (w0) h.dirty[q] = 1;
                 uint64_t resp = 0;
                 for (; grafts; grafts &= grafts - 1) {
@@ -1210,7 +1209,7 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
         uint64_t resp = q == NO_PAIR ? 0 : (q & HALO) ? h.halo_resp[q & ~HALO] : h.resp[q];
         if (!h.halo_resp && q != NO_PAIR) h.resp[q] = 0;
         // AcceptFrom at v for the answering peer
-        if (resp && !(h.eflags[r] & EDGE_DIRECT) && live_score(s, h, r) < h.graylist) resp = 0;
+        if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
         if (resp) h.dirty[r] = 1;
         for (; resp; resp &= resp - 1) {
             if (handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp))) --links;
@@ -1309,6 +1308,17 @@ hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
     if (h.n_hubs) hipLaunchKernelGGL(k_hb_recv_hub, dim3(std::min<uint32_t>(h.n_hubs, 4096)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_mask_and(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                  uint8_t* __restrict__ out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+        out[i] = a[i] && b[i];
+}
+hipError_t launch_mask_and(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mask_and, dim3(grid_cap(n, 256)), dim3(256), 0, st, a, b, out, n);
     return hipGetLastError();
 }
 
