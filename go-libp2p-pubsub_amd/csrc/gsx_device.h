@@ -279,8 +279,7 @@ struct HbState {
     const uint32_t* rev;
     const uint8_t* eflags;
     int64_t* backoff;     // [topic][pair] expiry, 0 = no entry
-    uint64_t* bo_bits;    // [topic][pair / 64]: bit per pair, backoff entry present (kept with `backoff`)
-    uint64_t bo_words;    // words per topic of bo_bits
+    uint8_t* bo8;         // [topic / 8][pair]: bit topic % 8, backoff entry present (kept with `backoff`; 4-B aligned)
     uint64_t* ctl_graft;  // per pair (v -> u): bit t = v sent GRAFT(t) this round
     uint64_t* ctl_prune;  // per pair (v -> u): bit t = v sent PRUNE(t)
     uint64_t* resp;       // per pair (u -> v): bit t = u answers v's GRAFT(t) with PRUNE
@@ -291,6 +290,7 @@ struct HbState {
     uint8_t* answer;      // per pair (v -> u): u answered with PRUNE bits on (u -> v) this round
     unsigned long long* stats;
     uint32_t* rngk;        // [topic][node]: draw counter after the unit's maintenance (emitGossip continues it)
+    uint16_t* mcount;      // [topic][node]: mesh size, as the scan found it / (A) left it / (B) keeps it
     uint32_t* work;        // [topic][tile * 64 + i]: units the scan found acting, per 64-node tile
     uint8_t* tcnt;         // [topic][tile]: how many (lane-per-unit maintenance)
     uint64_t n_tiles64;    // 64 * tiles: the per-topic stride of `work`
@@ -317,8 +317,8 @@ struct HbState {
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st);
 // Rebuilds the backoff presence bits from the expiry array (gsx_import_backoff).
-hipError_t launch_bo_rebuild(const int64_t* backoff, uint64_t* bits, uint64_t n_pairs, uint64_t words,
-                             uint32_t n_topics, hipStream_t st);
+hipError_t launch_bo_rebuild(const int64_t* backoff, uint8_t* bo8, uint64_t n_pairs, uint32_t n_topics,
+                             hipStream_t st);
 hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st);
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,

@@ -100,8 +100,7 @@ struct gsx_engine {
     // heartbeat: router params, backoff [topic][pair], this round's control bytes
     gsx_gossipsub_params gp{};
     int64_t* d_backoff = nullptr;
-    uint64_t* d_bobits = nullptr;  // [topic][pair / 64] backoff presence bits
-    uint64_t bo_words = 0;
+    uint8_t* d_bo8 = nullptr;  // [topic / 8][pair] backoff presence bits
     uint64_t *d_ctl_graft = nullptr, *d_ctl_prune = nullptr, *d_resp = nullptr;
     uint8_t* d_dirty = nullptr;
     uint32_t *d_long = nullptr, *d_nlong = nullptr;
@@ -109,6 +108,7 @@ struct gsx_engine {
     uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
     uint32_t *d_work = nullptr, *d_nwork = nullptr, *d_hubwork = nullptr, *d_hubs = nullptr;  // heartbeat worklists
     uint8_t* d_tcnt = nullptr;
+    uint16_t* d_mcount = nullptr;
     std::vector<uint32_t> hubs_host;  // nodes with more than HB_LANE_DEG pairs
     std::vector<uint8_t> gossip_prev;  // per topic: IHAVE slots written last round
     uint64_t* d_ihave_hash = nullptr;
@@ -399,14 +399,14 @@ void free_state(gsx_engine* e) {
     e->send_counts.clear();
     e->n_recv = e->n_send = 0;
     e->d_col = nullptr;
-    void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt,
-                  e->d_backoff, e->d_bobits, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
+    void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
+                  e->d_backoff, e->d_bo8, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
     e->d_backoff = nullptr;
-    e->d_bobits = nullptr;
+    e->d_bo8 = nullptr;
     e->d_ctl_graft = e->d_ctl_prune = e->d_resp = nullptr;
     e->d_dirty = nullptr;
     e->d_long = e->d_nlong = nullptr;
@@ -414,6 +414,7 @@ void free_state(gsx_engine* e) {
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_tcnt = nullptr;
+    e->d_mcount = nullptr;
     e->d_ihave_hash = nullptr;
     e->d_gb = nullptr;
     e->d_mc_digest = nullptr;
@@ -857,7 +858,7 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
         (rc = dalloc(e, &e->d_score, e->rs)) || (rc = dalloc(e, &e->d_ipg, 2 * e->rs)) ||
         (rc = dalloc(e, &e->d_ipcount, e->n_groups)) || (rc = dalloc(e, &e->d_col, E)) ||
         (rc = dalloc(e, &e->d_backoff, (size_t)e->T * E)) ||
-        (rc = dalloc(e, &e->d_bobits, (size_t)e->T * ((E + 63) / 64) + 1))) {
+        (rc = dalloc(e, &e->d_bo8, (size_t)((e->T + 7) / 8) * E + 4))) {
         free_state(e);
         return rc;
     }
@@ -870,8 +871,7 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
     HIPCHK(e, hipMemsetAsync(e->d_score, 0, sizeof(double) * e->rs, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_ipcount, 0, sizeof(uint32_t) * (e->n_groups ? e->n_groups : 1), e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_backoff, 0, sizeof(int64_t) * e->T * (E ? E : 1), e->stream));
-    e->bo_words = (E + 63) / 64;
-    HIPCHK(e, hipMemsetAsync(e->d_bobits, 0, 8 * ((size_t)e->T * e->bo_words + 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_bo8, 0, (size_t)((e->T + 7) / 8) * E + 4, e->stream));
     e->max_deg = 0;
     e->hubs_host.clear();
     for (uint32_t i = 0; i < n_nodes; ++i) {
@@ -2108,6 +2108,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
             (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
             (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
             (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
+            (rc = dalloc(e, &e->d_mcount, (size_t)e->T * e->n_nodes + 1)) ||
             (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
             (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
             (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
@@ -2128,8 +2129,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.rev = e->d_rev;
     h.eflags = e->d_eflags;
     h.backoff = e->d_backoff;
-    h.bo_bits = e->d_bobits;
-    h.bo_words = e->bo_words;
+    h.bo8 = e->d_bo8;
     h.ctl_graft = e->d_ctl_graft;
     h.ctl_prune = e->d_ctl_prune;
     h.resp = e->d_resp;
@@ -2151,6 +2151,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.rngk = e->d_rngk;
     h.work = e->d_work;
     h.tcnt = e->d_tcnt;
+    h.mcount = e->d_mcount;
     h.n_tiles64 = 64 * (((uint64_t)e->n_nodes + 63) / 64);
     h.hub_work = e->d_hubwork;
     h.n_hub = e->d_nwork + e->T;
@@ -2424,7 +2425,7 @@ int gsx_import_backoff(gsx_engine* e, const int64_t* in) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     const size_t TE = (size_t)e->T * e->E;
     if (TE) HIPCHK(e, hipMemcpyAsync(e->d_backoff, in, 8 * TE, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, gsx::launch_bo_rebuild(e->d_backoff, e->d_bobits, e->E, e->bo_words, e->T, e->stream));
+    HIPCHK(e, gsx::launch_bo_rebuild(e->d_backoff, e->d_bo8, e->E, e->T, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }

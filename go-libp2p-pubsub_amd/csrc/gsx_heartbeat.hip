@@ -59,50 +59,56 @@ __device__ __forceinline__ bool hb_in_mesh(const DevState& s, uint64_t r, uint32
 // addBackoff / doAddBackoff, gossipsub.go:845-859 (0 = no entry; the zero
 // time is before every expiry).  The presence bit of a new entry is set too.
 __device__ __forceinline__ void add_backoff(const HbState& h, uint64_t r, uint32_t t, int64_t interval) {
-    int64_t* b = &h.backoff[(size_t)t * h.n_pairs + r];
-    const int64_t expire = h.now + interval;
-    const int64_t old = *b;
-    if (old == 0) atomicOr((unsigned long long*)&h.bo_bits[(size_t)t * h.bo_words + r / 64], 1ull << (r % 64));
-    if (old == 0 || old < expire) *b = expire;
+    // max(old, expire) with 0 = none: one max (expiries are positive), and the
+    // presence bit (set iff the entry is nonzero); no value is read back
+    atomicMax(reinterpret_cast<unsigned long long*>(&h.backoff[(size_t)t * h.n_pairs + r]),
+              (unsigned long long)(h.now + interval));
+    const size_t x = (size_t)(t / 8) * h.n_pairs + r;  // the byte's 32-bit word (the array is 4-B aligned)
+    atomicOr(reinterpret_cast<uint32_t*>(h.bo8 + (x & ~(size_t)3)), (1u << (t % 8)) << (8 * (x & 3)));
 }
 __device__ __forceinline__ bool backoff_present(const HbState& h, uint64_t r, uint32_t t) {
-    return (h.bo_bits[(size_t)t * h.bo_words + r / 64] >> (r % 64)) & 1;
+    return (h.bo8[(size_t)(t / 8) * h.n_pairs + r] >> (t % 8)) & 1;
 }
 
-// clearBackoff, gossipsub.go:1585-1604: one wave per (topic, 64-pair word),
-// which also owns that word of the presence bits.
+// clearBackoff, gossipsub.go:1585-1604: a lane per (pair, 8-topic chunk)
+// presence byte; only the set bits' entries are read.
 __global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint32_t n_topics) {
     uint64_t cleared = 0;
-    const uint32_t lane = threadIdx.x % 64;
-    const uint64_t n_words = (uint64_t)n_topics * h.bo_words;
-    for (uint64_t wd = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / 64; wd < n_words;
-         wd += (uint64_t)gridDim.x * 4u) {
-        const uint32_t t = (uint32_t)(wd / h.bo_words);
-        const uint64_t r = (wd % h.bo_words) * 64 + lane;
-        bool clr = false;
-        if (r < h.n_pairs) {
-            int64_t* b = &h.backoff[(size_t)t * h.n_pairs + r];
-            if (*b != 0 && *b + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
-                *b = 0;
-                clr = true;
+    const uint64_t n_bytes = (uint64_t)((n_topics + 7) / 8) * h.n_pairs;
+    for (uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x; x < n_bytes; x += (uint64_t)gridDim.x * 256u) {
+        const uint8_t b = h.bo8[x];
+        if (!b) continue;
+        const uint32_t c = (uint32_t)(x / h.n_pairs);
+        const uint64_t r = x % h.n_pairs;
+        // every bit's entry loaded at once: a clear bit loads the first set bit's
+        // entry again (a valid address, a cache hit), so no load waits alone
+        const uint32_t k0 = (uint32_t)__builtin_ctz(b);
+        int64_t ex[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) ex[k] = h.backoff[(size_t)(8 * c + ((b >> k & 1) ? k : k0)) * h.n_pairs + r];
+        uint8_t keep = b;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if ((b >> k & 1) && ex[k] + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
+                h.backoff[(size_t)(8 * c + k) * h.n_pairs + r] = 0;
+                keep &= (uint8_t)~(1u << k);
                 ++cleared;
             }
-        }
-        const uint64_t m = __ballot(clr);
-        if (lane == 0 && m) h.bo_bits[wd] &= ~m;
+        if (keep != b) h.bo8[x] = keep;
     }
     flush_count(h.stats, HB_BACKOFF_CLEARED, cleared);
 }
 
-__global__ __launch_bounds__(256) void k_bo_rebuild(const int64_t* __restrict__ backoff, uint64_t* __restrict__ bits,
-                                                    uint64_t n_pairs, uint64_t words, uint32_t n_topics) {
-    const uint32_t lane = threadIdx.x % 64;
-    const uint64_t n_words = (uint64_t)n_topics * words;
-    for (uint64_t wd = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / 64; wd < n_words; wd += (uint64_t)gridDim.x * 4u) {
-        const uint32_t t = (uint32_t)(wd / words);
-        const uint64_t r = (wd % words) * 64 + lane;
-        const uint64_t m = __ballot(r < n_pairs && backoff[(size_t)t * n_pairs + r] != 0);
-        if (lane == 0) bits[wd] = m;
+__global__ __launch_bounds__(256) void k_bo_rebuild(const int64_t* __restrict__ backoff, uint8_t* __restrict__ bo8,
+                                                    uint64_t n_pairs, uint32_t n_topics) {
+    const uint64_t n_bytes = (uint64_t)((n_topics + 7) / 8) * n_pairs;
+    for (uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x; x < n_bytes; x += (uint64_t)gridDim.x * 256u) {
+        const uint32_t c = (uint32_t)(x / n_pairs);
+        const uint64_t r = x % n_pairs;
+        uint32_t b = 0;
+        for (uint32_t k = 0; k < 8 && 8 * c + k < n_topics; ++k)
+            b |= (uint32_t)(backoff[(size_t)(8 * c + k) * n_pairs + r] != 0) << k;
+        bo8[x] = (uint8_t)b;
     }
 }
 
@@ -121,26 +127,48 @@ __global__ __launch_bounds__(256) void k_bo_rebuild(const int64_t* __restrict__ 
 // control bits of the node's own pairs change, so the scan's decisions for
 // later topics stay valid, and every unit is independent of the others.
 
+// Phase timing of k_hb_maintain (build with -DGSX_HB_PROF; development only):
+// wave-level s_memrealtime deltas, printed by a few waves per launch.
+#ifdef GSX_HB_PROF
+#define HBP_DECL uint64_t hbp[10] = {0}; uint64_t hbp_t = wall_clock64();
+#define HBP(i)                              \
+    do {                                    \
+        const uint64_t t_ = wall_clock64(); \
+        hbp[i] += t_ - hbp_t;               \
+        hbp_t = t_;                         \
+    } while (0)
+#else
+#define HBP(i) \
+    do {       \
+    } while (0)
+#endif
+
 // Staged pair bits (u8, LDS)
 constexpr uint8_t ST_MESH = 1;     // present and in the topic's mesh (gs.mesh[topic][p])
 constexpr uint8_t ST_CAND = 2;     // present, connected, mesh-capable, not direct: getPeers' base filter
 constexpr uint8_t ST_OUT = 4;      // outbound (gs.outbound[p])
 constexpr uint8_t ST_BACKOFF = 8;  // gs.backoff[topic][p] present (map presence, :1377)
+constexpr uint8_t ST_GRAFT = 16;   // maintain() grafted the pair (effects applied by apply_events)
+constexpr uint8_t ST_PRUNE = 32;   // maintain() pruned the pair
+constexpr uint8_t ST_ACTIVE = 64;  // the record's mesh-delivery counting is active (REC_ACTIVE)
 
-__device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
-    // every input loaded unconditionally (no load waits at a divergent join)
-    const uint8_t pf = s.pflags[r], ef = h.eflags[r];
-    const uint8_t rf = s.rflags[flag_index(r, t, s.n_topics)];
-    const bool bo = backoff_present(h, r, t);
+__device__ __forceinline__ uint8_t stage_pack(uint8_t pf, uint8_t ef, uint8_t rf, bool bo) {
     uint8_t f = 0;
     if ((pf & PAIR_PRESENT) && (rf & REC_IN_MESH)) f |= ST_MESH;
     if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) &&
         !(ef & EDGE_DIRECT))
         f |= ST_CAND;
     if (ef & EDGE_OUTBOUND) f |= ST_OUT;
+    if (rf & REC_ACTIVE) f |= ST_ACTIVE;
     // only a candidate's backoff is ever tested (a pruned mesh peer gets the bit when pruned)
     if ((f & ST_CAND) && !(f & ST_MESH) && bo) f |= ST_BACKOFF;
     return f;
+}
+__device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
+    // every input loaded unconditionally (no load waits at a divergent join)
+    const uint8_t pf = s.pflags[r], ef = h.eflags[r];
+    const uint8_t rf = s.rflags[flag_index(r, t, s.n_topics)];
+    return stage_pack(pf, ef, rf, backoff_present(h, r, t));
 }
 
 // One unit (v, t) over its staged row: sc / fl are the row's scores and bits,
@@ -159,8 +187,27 @@ struct HbUnit {
     bool scored;  // the topic has score params: Graft / Prune traces set / clear inMesh
     uint64_t grafts = 0, prunes = 0;
     int64_t links = 0;  // in-mesh (pair, topic) delta
+#ifdef GSX_HB_PROF
+    uint64_t* hbp = nullptr;
+    uint64_t* hbp_t = nullptr;
+#define HBPU(i)                                 \
+    do {                                        \
+        const uint64_t t_ = wall_clock64();     \
+        hbp[i] += t_ - *hbp_t;                  \
+        *hbp_t = t_;                            \
+    } while (0)
+#else
+#define HBPU(i) \
+    do {        \
+    } while (0)
+#endif
 
     __device__ bool in_mesh(int i) const { return fl[i] & ST_MESH; }
+    __device__ int mesh_size() const {
+        int n = 0;
+        for (int i = 0; i < deg; ++i) n += (fl[i] & ST_MESH) != 0;
+        return n;
+    }
     __device__ double score(int i) const { return sc[i]; }
     __device__ bool outbound(int i) const { return fl[i] & ST_OUT; }
 
@@ -191,35 +238,23 @@ struct HbUnit {
         return n;
     }
 
-    // the receiver's pair (u -> v) of r = (v -> u) has control to read in (B)
-    __device__ void mark_inbox(uint64_t r) const {
-        const uint32_t q = h.rev[r];
-        if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
-    }
-    __device__ void graft(int i) {  // graftPeer, :1353-1359
-        const uint64_t r = r0 + i;
-        ev_graft(s, r, t, h.now);
+    // graftPeer (:1353-1359) / prunePeer (:1345-1351) on the staged row only;
+    // their memory effects are applied afterwards by apply_events, for the
+    // whole stage at once (no dependent global access in the serial part).
+    __device__ void graft(int i) {
+        fl[i] |= ST_GRAFT;
         if (scored) {  // (a topic without params keeps no inMesh flag)
             fl[i] |= ST_MESH;
             ++links;
         }
-        h.ctl_graft[r] |= 1ull << t;
-        h.dirty[r] = 1;
-        mark_inbox(r);
         ++grafts;
     }
-    __device__ void prune(int i) {  // prunePeer, :1345-1351 (only mesh peers are pruned)
-        const uint64_t r = r0 + i;
-        ev_prune(s, r, t);
+    __device__ void prune(int i) {  // (only mesh peers are pruned)
+        fl[i] |= ST_PRUNE | ST_BACKOFF;
         if (scored) {  // (an unscored topic's imported inMesh flag stays, as in the record)
             fl[i] &= ~ST_MESH;
             --links;
         }
-        fl[i] |= ST_BACKOFF;
-        add_backoff(h, r, t, h.gp.prune_backoff_ns);
-        h.ctl_prune[r] |= 1ull << t;
-        h.dirty[r] = 1;
-        mark_inbox(r);
         ++prunes;
     }
 
@@ -274,12 +309,14 @@ struct HbUnit {
         int n = mesh_list(plst);
         for (int i = 0; i < n; ++i)
             if (score(plst[i]) < 0) prune(plst[i]);
+        HBPU(0);
         // do we have enough peers? (:1370-1385)
         n = mesh_list(plst);
         if (n < gp.d_lo) {
             const int k = get_peers(gp.d - n, false, 0, 0.0, tmp, g);
             for (int i = 0; i < k; ++i) graft(tmp[i]);
         }
+        HBPU(1);
         // do we have too many peers? (:1387-1448)
         n = mesh_list(plst);
         if (n > gp.d_hi) {
@@ -307,6 +344,7 @@ struct HbUnit {
             }
             for (int i = gp.d; i < n; ++i) prune(plst[i]);
         }
+        HBPU(2);
         // do we have enough outbound peers? (:1450-1476)
         n = mesh_list(plst);
         if (n >= gp.d_lo) {
@@ -318,23 +356,74 @@ struct HbUnit {
                 for (int i = 0; i < k; ++i) graft(tmp[i]);
             }
         }
+        HBPU(3);
         // opportunistic grafting (:1478-1510)
         n = mesh_list(plst);
         if (gp.og_ticks && h.tick % gp.og_ticks == 0 && n > 1) {
             sort_by_score(plst, n, false, tmp);
             const double median = score(plst[n / 2]);
+            HBPU(4);
             if (median < h.og_threshold) {
                 const int k = get_peers(gp.og_peers, false, 1, median, tmp, g);
                 for (int i = 0; i < k; ++i) graft(tmp[i]);
             }
         }
+        HBPU(5);
     }
 };
+
+// The memory effects of maintain()'s grafts and prunes of pair r (staged bits
+// f): the score-record events, the backoff entry, the control bits of r, its
+// dirty mark and the receiver's inbox mark ((u -> v) of r = (v -> u) has
+// control to read in (B)).  A pair is grafted or pruned at most once per unit
+// except prune-after-graft, which the graft-then-prune order covers (a pruned
+// peer is backed off, so never grafted again in the same round).
+__device__ __forceinline__ void apply_events(const DevState& s, const HbState& h, uint64_t r, uint32_t t, uint8_t f,
+                                             uint32_t q, bool scored) {
+    if (f & ST_GRAFT) {  // ev_graft (a grafted candidate is present)
+        if (scored) {
+            reinterpret_cast<int64_t*>(s.rec)[rec_index(r, t, s.n_topics, GRAFT)] = h.now;
+            s.rflags[flag_index(r, t, s.n_topics)] = REC_IN_MESH | REC_FRESH;
+        }
+        atomicOr((unsigned long long*)&h.ctl_graft[r], 1ull << t);
+    }
+    if (f & ST_PRUNE) {  // ev_prune (a pruned mesh peer is present)
+        if (scored) {
+            // after a graft in the same unit the record is fresh (not active)
+            const bool active = (f & ST_ACTIVE) && !(f & ST_GRAFT);
+            if (active) {
+                const size_t b = rec_index(r, t, s.n_topics, FMD);
+                const double threshold = s.tp[t].thr3;
+                const double mmd = s.rec[b + MMD * TILE];
+                if (mmd < threshold) {
+                    const double deficit = threshold - mmd;
+                    s.rec[b + MFP * TILE] = s.rec[b + MFP * TILE] + deficit * deficit;
+                }
+            }
+            s.rflags[flag_index(r, t, s.n_topics)] = active ? REC_ACTIVE : 0;
+        }
+        add_backoff(h, r, t, h.gp.prune_backoff_ns);
+        atomicOr((unsigned long long*)&h.ctl_prune[r], 1ull << t);
+    }
+    h.dirty[r] = 1;
+    if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
+}
+
+constexpr int APPLY_UNROLL = 4;  // receiver-pair loads per lane in flight
 
 // Draws are keyed by the GLOBAL node id, so a range shard draws what the
 // whole-overlay engine draws for the same node.
 __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, uint32_t k) {
     return Rng{h.seed, TAG_HEARTBEAT, (uint64_t)h.node_lo + v, (h.tick << 32) | ((uint64_t)t << 24), k};
+}
+
+// LDS hand-off between the lanes of a one-wave block: a wave's LDS accesses
+// are performed in order, so only the compiler must not move them across
+// (no s_waitcnt on outstanding global stores, unlike __syncthreads).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t x, uint32_t lane) {  // exclusive
@@ -358,19 +447,27 @@ __device__ __forceinline__ void wave_append(bool want, uint32_t value, uint32_t*
 }
 
 constexpr int SCAN_TOPICS = 8;     // topics decided per pass over a wave's pairs
-constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (2 B each) for the per-node counts
+constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (scan bits, u32) for the per-node counts
 
-// A pair's scan bits for topics t0 .. t0+7: bit k = in the mesh of topic t0+k,
-// bit 8 = score < 0, bit 9 = outbound, bit 10 = getPeers' base filter with
-// score >= 0 (present, connected, mesh-capable, not direct).
-constexpr uint32_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;  // bits 16 + k: backoff entry of t0 + k
-__device__ __forceinline__ uint32_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS]) {
+// A pair's scan bits for topics t0 .. t0+7 (t0 a multiple of 8): bit k = in
+// the mesh of topic t0+k, bit 8 = score < 0, bit 9 = outbound, bit 10 =
+// getPeers' base filter with score >= 0 (present, connected, mesh-capable, not
+// direct), bit 11 = score below the opportunistic-graft threshold, bit 16+k =
+// a getPeers candidate of topic t0+k (base filter, not in that mesh, no
+// backoff entry; bo = the pair's presence byte of the chunk).
+constexpr uint32_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;
+constexpr uint32_t SC_OGLOW = 1u << 11;
+__device__ __forceinline__ uint32_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS],
+                                              uint8_t bo, uint32_t nt, double og_threshold) {
     if (!(pf & PAIR_PRESENT)) return 0;
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_TOPICS; ++k)
         if (rf[k] & REC_IN_MESH) m |= 1u << k;
+    if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0)
+        m |= (~(m | bo) & ((1u << nt) - 1)) << 16;
     if (sc < 0) m |= SC_NEG;
+    if (sc < og_threshold) m |= SC_OGLOW;
     if (ef & EDGE_OUTBOUND) m |= SC_OUT;
     if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0) m |= SC_CAND;
     return m;
@@ -378,23 +475,21 @@ __device__ __forceinline__ uint32_t scan_pack(uint8_t pf, uint8_t ef, double sc,
 __device__ __forceinline__ uint32_t scan_bits(const DevState& s, const HbState& h, uint64_t r, uint32_t t0,
                                               uint32_t nt) {
     uint8_t rf[SCAN_TOPICS];
-    uint32_t bo = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_TOPICS; ++k) {
-        rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
-        if (k < (int)nt && backoff_present(h, r, t0 + k)) bo |= 1u << (16 + k);
-    }
-    return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf) | bo;
+    for (int k = 0; k < SCAN_TOPICS; ++k) rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
+    return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf, h.bo8[(size_t)(t0 / 8) * h.n_pairs + r], nt,
+                     h.og_threshold);
 }
 
 // (A) scan: every unit of every topic.  A wave takes a tile of 64 consecutive
 // nodes: one coalesced pass packs each pair's bits into LDS (four pairs per
 // lane in flight), then one lane per node counts its row — mesh size, negative
-// and outbound members, and, only for a unit below Dlo or short of outbound
-// peers, its getPeers candidates (the backoff entries are read there alone).
+// and outbound members, members below the opportunistic-graft threshold, and
+// which topics have getPeers candidates (any / outbound; the pair's backoff
+// presence byte is staged with its bits).
 // A unit acts iff some step of maintain() would: a negative member, more than
-// Dhi, an opportunistic-graft tick with a mesh of 2+, or a graft step with a
-// candidate.  The tile's acting units are listed at work[t][tile * 64 ..]
+// Dhi, an opportunistic-graft tick with a mesh of 2+ whose median score is
+// below the threshold, or a graft step with a candidate.  The tile's acting units are listed at work[t][tile * 64 ..]
 // (count tcnt[t][tile]: no atomics); hub nodes go to the topic's hub list;
 // every unit's rngk starts at 0; the in-mesh links before the round are
 // counted.  Blocks of four waves over a bounded grid: one counter atomic per
@@ -411,6 +506,9 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
     const uint32_t T = s.n_topics;
     const uint32_t n_tiles = (h.n_nodes + 63) / 64;
     unsigned long long links[1] = {0};
+#ifdef GSX_HB_PROF
+    HBP_DECL
+#endif
     for (uint32_t tb = blockIdx.x * SCAN_WAVES; tb < n_tiles; tb += gridDim.x * SCAN_WAVES) {
         const uint32_t tile = tb + wave;  // (block-uniform loop: every wave reaches every barrier)
         const uint32_t v0 = tile * 64u;
@@ -420,6 +518,7 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
             if (lane == 0) rs[64] = h.row_ptr[v0 + nv];
         }
         __syncthreads();
+        HBP(0);
         const int64_t pa = nv ? rs[0] : 0, pb = nv ? rs[64] : 0;
         const bool staged = pb - pa <= SCAN_STAGE;
         const uint32_t v = v0 + lane;
@@ -431,70 +530,71 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                 for (int64_t rb = pa + lane; rb < pb; rb += 256) {
                     // unconditional loads of clamped (valid) addresses, masked after: a
                     // load under a divergent branch is waited for at the branch's join
-                    uint8_t pf[4], ef[4], rf[4][SCAN_TOPICS];
+                    uint8_t pf[4], ef[4], bo[4], rf[4][SCAN_TOPICS];
                     double sc[4];
-                    uint64_t bw[4][SCAN_TOPICS];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t r = min(rb + 64 * j, pb - 1);
                         pf[j] = s.pflags[r];
                         ef[j] = h.eflags[r];
                         sc[j] = s.score[r];
+                        bo[j] = h.bo8[(size_t)(t0 / 8) * h.n_pairs + r];
 #pragma unroll
-                        for (int k = 0; k < SCAN_TOPICS; ++k) {
-                            const uint32_t tk = min(t0 + k, T - 1);
-                            rf[j][k] = s.rflags[flag_index(r, tk, T)];
-                            bw[j][k] = h.bo_bits[(size_t)tk * h.bo_words + r / 64];
-                        }
+                        for (int k = 0; k < SCAN_TOPICS; ++k) rf[j][k] = s.rflags[flag_index(r, min(t0 + k, T - 1), T)];
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
 #pragma unroll
                         for (int k = 0; k < SCAN_TOPICS; ++k)
-                            if (k >= (int)nt) {
-                                rf[j][k] = 0;
-                                bw[j][k] = 0;
-                            }
+                            if (k >= (int)nt) rf[j][k] = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t r = rb + 64 * j;
-                        if (r >= pb) continue;
-                        uint32_t bo = 0;
-#pragma unroll
-                        for (int k = 0; k < SCAN_TOPICS; ++k) bo |= (uint32_t)((bw[j][k] >> (r % 64)) & 1) << (16 + k);
-                        st[r - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j]) | bo;
+                        if (r < pb) st[r - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j], bo[j], nt, h.og_threshold);
                     }
                 }
             }
             __syncthreads();
-            int n[SCAN_TOPICS], neg[SCAN_TOPICS], outb[SCAN_TOPICS];
+            HBP(1);
+            int n[SCAN_TOPICS], neg[SCAN_TOPICS], outb[SCAN_TOPICS], low[SCAN_TOPICS];
 #pragma unroll
-            for (int k = 0; k < SCAN_TOPICS; ++k) n[k] = neg[k] = outb[k] = 0;
+            for (int k = 0; k < SCAN_TOPICS; ++k) n[k] = neg[k] = outb[k] = low[k] = 0;
+            uint32_t cg = 0, co = 0;  // topics with a getPeers candidate: any / outbound
             for (int i = 0; i < deg; ++i) {
                 const uint32_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
+                cg |= m >> 16;
+                co |= (m & SC_OUT) ? m >> 16 : 0;
 #pragma unroll
                 for (int k = 0; k < SCAN_TOPICS; ++k)
                     if (m >> k & 1) {
                         ++n[k];
                         neg[k] += (m & SC_NEG) != 0;
                         outb[k] += (m & SC_OUT) != 0;
+                        low[k] += (m & SC_OGLOW) != 0;
                     }
             }
+            HBP(2);
+            // per topic: a step of maintain() acts (getPeers' steps iff it finds a candidate)
+            uint32_t act = 0;
+#pragma unroll
+            for (int k = 0; k < SCAN_TOPICS; ++k) {
+                if (k >= (int)nt || lane >= nv) continue;
+                const uint32_t t = t0 + k;
+                links[0] += (uint64_t)n[k];
+                // opportunistic grafting acts iff the median mesh score (ascending
+                // [n/2]) is below the threshold: iff more than n/2 members are
+                // (scores are finite; the sort and the draws have no other effect)
+                const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
+                const bool a = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1 && low[k] > n[k] / 2) ||
+                               (grow && (cg >> k & 1)) || (more_out && (co >> k & 1));  // :1370-1385, :1450-1476
+                act |= (uint32_t)a << k;
+                h.rngk[(size_t)t * h.n_nodes + v] = 0;
+                h.mcount[(size_t)t * h.n_nodes + v] = (uint16_t)n[k];  // (A) updates it for acting units
+            }
+            HBP(3);
             for (uint32_t k = 0; k < nt; ++k) {
                 const uint32_t t = t0 + k;
-                bool active = false;
-                if (lane < nv) {
-                    links[0] += (uint64_t)n[k];
-                    active = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1);
-                    const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
-                    if (!active && (grow || more_out)) {  // getPeers finds a candidate? (:1370-1385, :1450-1476)
-                        for (int i = 0; i < deg && !active; ++i) {
-                            const uint32_t m = staged ? st[r0 - pa + i] : scan_bits(s, h, r0 + i, t0, nt);
-                            active = (m & SC_CAND) && !(m >> k & 1) && !(m >> (16 + k) & 1) && (grow || (m & SC_OUT));
-                        }
-                    }
-                    h.rngk[(size_t)t * h.n_nodes + v] = 0;
-                }
+                const bool active = lane < nv && (act >> k & 1);
                 if (nv) {
                     const bool lw = active && deg <= HB_LANE_DEG;
                     const uint64_t b = __ballot(lw);
@@ -503,16 +603,21 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                     wave_append(active && deg > HB_LANE_DEG, v, h.hub_work + (size_t)t * h.n_nodes, h.n_hub + t, lane);
                 }
             }
+            HBP(4);
             __syncthreads();  // st is rewritten by the next topic chunk / tile
+            HBP(5);
         }
     }
+#ifdef GSX_HB_PROF
+    if (threadIdx.x == 0 && blockIdx.x % 512 == 0)
+        printf("HBS blk=%u rows=%lu stage=%lu count=%lu decide=%lu out=%lu tail=%lu\n", blockIdx.x, hbp[0], hbp[1],
+               hbp[2], hbp[3], hbp[4], hbp[5]);
+#endif
     const uint32_t slot[1] = {HB_MESH_LINKS};
     block_count<1>(links, h.stats, slot);
 }
 
-constexpr int HB_STAGE = 1024;  // pairs a lane-per-unit wave stages at once
-
-constexpr uint32_t MAINT_GROUP = 4;  // tiles per maintenance wave: up to 256 listed units
+constexpr int GOSSIP_STAGE = 1024;  // pairs of a tile k_hb_gossip stages per wave
 
 // (A) per topic: the listed units, one lane each, rows staged in LDS.  A wave
 // takes a group of MAINT_GROUP tiles, gathers their listed units (a prefix over the
@@ -520,13 +625,19 @@ constexpr uint32_t MAINT_GROUP = 4;  // tiles per maintenance wave: up to 256 li
 // cooperatively (every lane loads items of every row, 64 loads per
 // instruction); when the rows exceed the stage it runs them in windows of
 // whole rows.
+constexpr int MAINT_UNROLL = 4;    // staged pairs per lane in flight
+constexpr uint32_t MAINT_GROUP = 4;  // tiles per maintenance wave (up to 256 listed units, 64 at a time)
+constexpr int HB_STAGE = 1024;       // pairs staged at once (14 KB of LDS per wave)
+
 __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint32_t t) {
-    __shared__ double sc[HB_STAGE];
+    __shared__ double sc[HB_STAGE];  // scores; after maintain(): the events' receiver pairs (u32)
     __shared__ uint8_t fl[HB_STAGE];
+    __shared__ uint8_t owner[HB_STAGE];  // the lane whose row holds the item
     __shared__ uint16_t la[HB_STAGE], lb[HB_STAGE];
     __shared__ uint32_t offs[65];
     __shared__ int64_t r0s[64];
     __shared__ uint32_t pfx[65];
+    uint32_t* qs = reinterpret_cast<uint32_t*>(sc);
     const uint32_t lane = threadIdx.x;
     const uint32_t n_tiles = (h.n_nodes + 63) / 64;
     const uint8_t* tcnt = h.tcnt + (size_t)t * n_tiles;
@@ -534,33 +645,32 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
     const bool scored = t < s.n_topics && s.tp[t].scored;
     uint64_t grafts = 0, prunes = 0;
     int64_t links = 0;
+#ifdef GSX_HB_PROF
+    HBP_DECL
+#endif
     for (uint32_t g0 = blockIdx.x * MAINT_GROUP; g0 < n_tiles; g0 += gridDim.x * MAINT_GROUP) {
         const uint32_t c = (lane < MAINT_GROUP && g0 + lane < n_tiles) ? tcnt[g0 + lane] : 0;
         const uint32_t p = wave_prefix(c, lane);
         pfx[lane] = p;
         if (lane == 63) pfx[64] = p + c;
-        __syncthreads();
+        wave_lds_sync();
         const uint32_t total = pfx[64];
         for (uint32_t u0 = 0; u0 < total; u0 += 64) {
             const uint32_t u = u0 + lane;
             const bool valid = u < total;
-            uint32_t v = 0;
-            if (valid) {
-                uint32_t lo = 0, hi = 64;  // pfx[lo] <= u < pfx[lo + 1]
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (pfx[mid] <= u) lo = mid;
-                    else hi = mid;
-                }
-                v = work[(size_t)(g0 + lo) * 64 + (u - pfx[lo])];
-            }
-            const int64_t r0 = valid ? h.row_ptr[v] : 0;
-            const int deg = valid ? (int)(h.row_ptr[v + 1] - r0) : 0;
+            uint32_t lo = 0;  // pfx[lo] <= u < pfx[lo + 1]
+            for (uint32_t x = 1; x < MAINT_GROUP; ++x) lo += pfx[x] <= u;
+            // (clamped in-range address: loaded by every lane, used by the valid ones)
+            const uint32_t v = work[(size_t)min(g0 + lo, n_tiles - 1) * 64 + min(u - pfx[lo], 63u)];
+            const int64_t ra = h.row_ptr[valid ? v : 0], rb = h.row_ptr[valid ? v + 1 : 0];
+            const int64_t r0 = valid ? ra : 0;
+            const int deg = valid ? (int)(rb - ra) : 0;
             const uint32_t off = wave_prefix((uint32_t)deg, lane);
             offs[lane] = off;
             r0s[lane] = r0;
             if (lane == 63) offs[64] = off + deg;
-            __syncthreads();
+            wave_lds_sync();
+            HBP(6);
             // windows of whole rows: lanes [l0, l1) whose rows fit [offs[l0], offs[l0] + HB_STAGE)
             uint32_t l0 = 0;
             while (l0 < 64 && offs[l0] < offs[64]) {
@@ -568,34 +678,95 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
                 uint32_t l1 = l0;
                 while (l1 < 64 && offs[l1 + 1] - base <= HB_STAGE) ++l1;  // (uniform: every lane computes it)
                 const uint32_t end = offs[l1];
-                for (uint32_t k = base + lane; k < end; k += 64) {  // item k belongs to the row holding it
-                    uint32_t lo = l0, hi = l1;  // offs[lo] <= k < offs[lo + 1]
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (offs[mid] <= k) lo = mid;
-                        else hi = mid;
+                if (lane >= l0 && lane < l1)
+                    for (int i = 0; i < deg; ++i) owner[off - base + i] = (uint8_t)lane;
+                wave_lds_sync();
+                // item k belongs to the row holding it; MAINT_UNROLL items per lane in
+                // flight (all loads issued before any result is used)
+                for (uint32_t k0 = base + lane; k0 < end; k0 += 64 * MAINT_UNROLL) {
+                    uint64_t r[MAINT_UNROLL];
+#pragma unroll
+                    for (int j = 0; j < MAINT_UNROLL; ++j) {
+                        const uint32_t k = min(k0 + 64 * j, end - 1);
+                        const uint32_t o = owner[k - base];
+                        r[j] = (uint64_t)r0s[o] + (k - offs[o]);
                     }
-                    const uint64_t r = (uint64_t)r0s[lo] + (k - offs[lo]);
-                    sc[k - base] = s.score[r];
-                    fl[k - base] = stage_bits(s, h, r, t);
+                    double x[MAINT_UNROLL];
+                    uint8_t pf[MAINT_UNROLL], ef[MAINT_UNROLL], rf[MAINT_UNROLL];
+                    uint8_t bb[MAINT_UNROLL];
+#pragma unroll
+                    for (int j = 0; j < MAINT_UNROLL; ++j) {
+                        x[j] = s.score[r[j]];
+                        pf[j] = s.pflags[r[j]];
+                        ef[j] = h.eflags[r[j]];
+                        rf[j] = s.rflags[flag_index(r[j], t, s.n_topics)];
+                        bb[j] = h.bo8[(size_t)(t / 8) * h.n_pairs + r[j]];
+                    }
+#pragma unroll
+                    for (int j = 0; j < MAINT_UNROLL; ++j) {
+                        const uint32_t k = k0 + 64 * j;
+                        if (k < end) {
+                            sc[k - base] = x[j];
+                            fl[k - base] = stage_pack(pf[j], ef[j], rf[j], (bb[j] >> (t % 8)) & 1);
+                        }
+                    }
                 }
-                __syncthreads();
+                wave_lds_sync();
+                HBP(7);
                 if (lane >= l0 && lane < l1 && valid) {
                     const uint32_t o = off - base;
                     HbUnit U{s, h, t, r0, deg, sc + o, fl + o, la + o, lb + o, scored};
+#ifdef GSX_HB_PROF
+                    U.hbp = hbp;
+                    U.hbp_t = &hbp_t;
+#endif
                     Rng g = hb_rng(h, v, t, 0);
                     U.maintain(g);
                     h.rngk[(size_t)t * h.n_nodes + v] = g.k;  // emitGossip continues this (node, topic) draw stream
+                    h.mcount[(size_t)t * h.n_nodes + v] = (uint16_t)U.mesh_size();  // read by (B)'s Dhi check
                     grafts += U.grafts;
                     prunes += U.prunes;
                     links += U.links;
                 }
-                __syncthreads();  // the stage is reused by the next window / batch
+                wave_lds_sync();
+                HBP(8);
+                // the window's events, the whole wave: first every receiver pair
+                // (loads only, APPLY_UNROLL per lane in flight, into the score stage),
+                // then the stores and atomics (nothing waits on them)
+                for (uint32_t k0 = base + lane; k0 < end; k0 += 64 * APPLY_UNROLL) {
+                    uint32_t q[APPLY_UNROLL];
+                    bool any = false;
+#pragma unroll
+                    for (int j = 0; j < APPLY_UNROLL; ++j) {
+                        const uint32_t k = min(k0 + 64 * j, end - 1);
+                        const uint32_t o = owner[k - base];
+                        any |= k0 + 64 * j < end && (fl[k - base] & (ST_GRAFT | ST_PRUNE));
+                        q[j] = h.rev[(uint64_t)r0s[o] + (k - offs[o])];
+                    }
+                    if (!any) continue;
+#pragma unroll
+                    for (int j = 0; j < APPLY_UNROLL; ++j)
+                        if (k0 + 64 * j < end) qs[k0 + 64 * j - base] = q[j];
+                }
+                wave_lds_sync();
+                for (uint32_t k = base + lane; k < end; k += 64) {
+                    const uint8_t f = fl[k - base];
+                    if (!(f & (ST_GRAFT | ST_PRUNE))) continue;
+                    const uint32_t o = owner[k - base];
+                    apply_events(s, h, (uint64_t)r0s[o] + (k - offs[o]), t, f, qs[k - base], scored);
+                }
+                wave_lds_sync();  // the stage is reused by the next window / batch
+                HBP(9);
                 l0 = l1;
             }
         }
-        __syncthreads();  // pfx is rewritten by the next group
+        wave_lds_sync();  // pfx is rewritten by the next group
     }
+#ifdef GSX_HB_PROF
+    if (lane == 0 && blockIdx.x % 1024 == 0)
+        printf("HBP t=%u blk=%u pre=%lu stage=%lu neg=%lu dlo=%lu dhi=%lu out=%lu ogsort=%lu oggraft=%lu post=%lu apply=%lu\n",
+               t, blockIdx.x, hbp[6], hbp[7], hbp[0], hbp[1], hbp[2], hbp[3], hbp[4], hbp[5], hbp[8], hbp[9]);
+#endif
     flush_count(h.stats, HB_GRAFTS, grafts);
     flush_count(h.stats, HB_PRUNES, prunes);
     flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
@@ -629,9 +800,16 @@ __global__ __launch_bounds__(64) void k_hb_maintain_hub(DevState s, HbState h, u
             Rng g = hb_rng(h, v, t, 0);
             U.maintain(g);
             h.rngk[(size_t)t * h.n_nodes + v] = g.k;
+            h.mcount[(size_t)t * h.n_nodes + v] = (uint16_t)U.mesh_size();
             grafts += U.grafts;
             prunes += U.prunes;
             links += U.links;
+        }
+        __syncthreads();
+        for (int i = lane; i < deg; i += 64) {
+            const uint8_t f = fl[i];
+            const uint32_t q = h.rev[r0 + i];
+            if (f & (ST_GRAFT | ST_PRUNE)) apply_events(s, h, r0 + i, t, f, q, scored);
         }
         __syncthreads();  // the LDS row is restaged by the next unit
     }
@@ -707,8 +885,8 @@ __device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, con
 __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
                                                    uint32_t n_gb) {
     __shared__ int64_t rs_w[SCAN_WAVES][65];
-    __shared__ uint8_t el_w[SCAN_WAVES][HB_STAGE];
-    __shared__ uint16_t pl_w[SCAN_WAVES][HB_STAGE];
+    __shared__ uint8_t el_w[SCAN_WAVES][GOSSIP_STAGE];
+    __shared__ uint16_t pl_w[SCAN_WAVES][GOSSIP_STAGE];
     const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
     int64_t* rs = rs_w[wave];
     uint8_t* el = el_w[wave];
@@ -726,7 +904,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
         }
         __syncthreads();
         const int64_t pa = nv ? rs[0] : 0, pb = nv ? rs[64] : 0;
-        const bool staged = pb - pa <= HB_STAGE;
+        const bool staged = pb - pa <= GOSSIP_STAGE;
         for (int64_t rb = pa + lane; rb < pb; rb += 256) {
             uint8_t pf[4], ef[4], rf[4], dt[4];
             double sc[4];
@@ -960,7 +1138,6 @@ __device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool 
     return (grafts | prunes) != 0;
 }
 
-constexpr int RECV_TOPICS = 32;  // topics whose receiver mesh counts are cached (LDS, u8 per lane)
 
 // (B) one lane per receiving node u (up to HB_LANE_DEG peers; hubs run in
 // k_hb_recv_hub), senders in ascending order: handleGraft then handlePrune
@@ -968,7 +1145,6 @@ constexpr int RECV_TOPICS = 32;  // topics whose receiver mesh counts are cached
 // the mesh size the previous accepts and prunes of this round left: a
 // running count per topic, taken from the row on first use.
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
-    __shared__ uint8_t mcnt[RECV_TOPICS][64];
     const uint32_t lane = threadIdx.x;
     uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
     int64_t links = 0;
@@ -976,7 +1152,6 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
-        uint32_t have = 0;  // topics < RECV_TOPICS with a cached count
         for (int64_t c0 = r0; c0 < r1; c0 += 8) {
           // the row's marks eight at a time, loaded unconditionally (clamped)
           uint8_t ib[8];
@@ -1026,17 +1201,9 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                     ++rejected;
                     continue;
                 }
-                int n;
-                if (t < RECV_TOPICS && (have >> t & 1)) {
-                    n = mcnt[t][lane];
-                } else {
-                    n = 0;
-                    for (int64_t x = r0; x < r1; ++x) n += hb_in_mesh(s, x, t);
-                    if (t < RECV_TOPICS) {
-                        mcnt[t][lane] = (uint8_t)n;
-                        have |= 1u << t;
-                    }
-                }
+                // the mesh size (A) left, kept current by this lane's accepts and prunes
+                uint16_t* mc = h.mcount + (size_t)t * h.n_nodes + u;
+                const int n = *mc;
                 if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
                     resp |= 1ull << t;
                     add_backoff(h, q, t, gp.prune_backoff_ns);
@@ -1047,7 +1214,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 ++accepted;
                 if (scored_topic(s, q, t)) {
                     ++links;
-                    if (t < RECV_TOPICS) mcnt[t][lane] = (uint8_t)(n + 1);
+                    *mc = (uint16_t)(n + 1);
                 }
             }
             h.resp[q] = resp;
@@ -1056,7 +1223,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
                 if (handle_prune(s, h, q, t)) {
                     --links;
-                    if (t < RECV_TOPICS && (have >> t & 1)) mcnt[t][lane] = (uint8_t)(mcnt[t][lane] - 1);
+                    h.mcount[(size_t)t * h.n_nodes + u] -= 1;
                 }
                 ++handled;
             }
@@ -1070,20 +1237,12 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
 }
 
-// In-mesh count of topic t over u's row, summed by the whole wave.
-__device__ __forceinline__ int wave_mesh_count(const DevState& s, int64_t r0, int64_t r1, uint32_t t, uint32_t lane) {
-    uint64_t c = 0;
-    for (int64_t x = r0 + lane; x < r1; x += 64) c += hb_in_mesh(s, x, t);
-    return (int)wave_sum64(c);
-}
-
 // (B) for hub receivers (more than HB_LANE_DEG peers): one wave per node.
 // The wave finds the marked pairs 64 at a time (ballot); every lane then runs
 // the same sequential handling of each sender in ascending order (its values
 // are uniform across the wave), lane 0 writing, and mesh sizes are counted by
 // the whole wave.
 __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
-    __shared__ int mc[64];
     const uint32_t lane = threadIdx.x;
     const bool w0 = lane == 0;
     uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
@@ -1092,7 +1251,6 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
     for (uint32_t k = blockIdx.x; k < h.n_hubs; k += gridDim.x) {
         const uint32_t u = h.hubs[k];
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        uint64_t have = 0;  // topics with a cached count in mc[]
         for (int64_t c0 = r0; c0 < r1; c0 += 64) {
             const int64_t ql = c0 + lane;
             bool mine = ql < r1;
@@ -1141,17 +1299,9 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                         __syncthreads();
                         continue;
                     }
-                    int n;
-                    if (t < 64 && (have >> t & 1)) {
-                        n = mc[t];
-                    } else {
-                        n = wave_mesh_count(s, r0, r1, t, lane);
-                        __syncthreads();
-                        if (t < 64) {
-                            if (w0) mc[t] = n;
-                            have |= 1ull << t;
-                        }
-                    }
+                    uint16_t* mcp = h.mcount + (size_t)t * h.n_nodes + u;
+                    const int n = *mcp;
+                    __syncthreads();  // every lane has read the count before lane 0 updates it
                     if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
                         resp |= 1ull << t;
                         if (w0) add_backoff(h, q, t, gp.prune_backoff_ns);
@@ -1163,7 +1313,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                     __syncthreads();  // every lane has read the flags before lane 0 grafts
                     if (w0) {
                         ev_graft(s, q, t, h.now);
-                        if (sc_t && t < 64) mc[t] = n + 1;
+                        if (sc_t) *mcp = (uint16_t)(n + 1);
                     }
                     accepted += w0;
                     if (sc_t) links += w0;
@@ -1179,7 +1329,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                     __syncthreads();
                     if (w0) {
                         handle_prune(s, h, q, t);
-                        if (was && t < 64 && (have >> t & 1)) mc[t] = mc[t] - 1;
+                        if (was) h.mcount[(size_t)t * h.n_nodes + u] -= 1;
                     }
                     if (was) links -= w0;
                     handled += w0;
@@ -1246,18 +1396,17 @@ static inline unsigned wave_grid(uint64_t n) {
 }
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
-    const uint64_t n = (uint64_t)n_topics * h.bo_words;  // one wave per (topic, word)
+    const uint64_t n = (uint64_t)((n_topics + 7) / 8) * h.n_pairs;  // a lane per presence byte
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(grid_cap(n * 64, 256)), dim3(256), 0, st, h, n_topics);
+    hipLaunchKernelGGL(k_hb_clear_backoff, dim3(grid_cap(n, 256)), dim3(256), 0, st, h, n_topics);
     return hipGetLastError();
 }
 
-hipError_t launch_bo_rebuild(const int64_t* backoff, uint64_t* bits, uint64_t n_pairs, uint64_t words,
-                             uint32_t n_topics, hipStream_t st) {
-    const uint64_t n = (uint64_t)n_topics * words;
+hipError_t launch_bo_rebuild(const int64_t* backoff, uint8_t* bo8, uint64_t n_pairs, uint32_t n_topics,
+                             hipStream_t st) {
+    const uint64_t n = (uint64_t)((n_topics + 7) / 8) * n_pairs;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bo_rebuild, dim3(grid_cap(n * 64, 256)), dim3(256), 0, st, backoff, bits, n_pairs, words,
-                       n_topics);
+    hipLaunchKernelGGL(k_bo_rebuild, dim3(grid_cap(n, 256)), dim3(256), 0, st, backoff, bo8, n_pairs, n_topics);
     return hipGetLastError();
 }
 
@@ -1271,7 +1420,8 @@ hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, i
     if (h.n_nodes == 0) return hipSuccess;
     // a wave per group of MAINT_GROUP tiles (the per-tile lists of k_hb_scan)
     const uint64_t groups = ((uint64_t)h.n_nodes + 64 * MAINT_GROUP - 1) / (64 * MAINT_GROUP);
-    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384)), dim3(64), 0, st, s, h, t);
+    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384)),
+                       dim3(64), 0, st, s, h, t);
     if (max_deg > HB_LANE_DEG) {
         const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
         static bool attr = false;
