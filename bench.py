@@ -483,18 +483,20 @@ def adversarial_leg(args, rank, world, local, dist, dev):
         before = sybil_links()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        hbs = []
-        for k in range(2):
+        hbs, ms = [], []
+        for k in range(2):  # the attack's first round (the synthesized meshes' sybils pruned), then round 60 (OG)
             now += abi.SECOND
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
             if runner is None:
                 hbs.append(e.heartbeat(59 + k, now, synth.SEED).as_dict())
             else:
                 hbs.append(runner.heartbeat(59 + k, now, synth.SEED)[1])
-        e.sync()
-        torch.cuda.synchronize(dev)
-        out["heartbeat_ms_per_round"] = reduce_scalar(time.perf_counter() - t0, dist, dev, "max") / 2 * 1e3
+            e.sync()
+            torch.cuda.synchronize(dev)
+            ms.append(reduce_scalar(time.perf_counter() - t0, dist, dev, "max") * 1e3)
+        out["heartbeat_ms_per_round"] = sum(ms) / len(ms)
+        out["heartbeat_ms_rounds"] = ms
         out["sybil_mesh_links_before"] = int(before)
         out["sybil_mesh_links_after"] = int(sybil_links())
         out["heartbeat_first_round"] = hbs[0]
@@ -521,6 +523,8 @@ def main():
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
     ap.add_argument("--hb-msgs", type=int, default=256, help="gossipsub messages propagated before every heartbeat")
+    ap.add_argument("--hb-settle", type=int, default=8,
+                    help="untimed heartbeat rounds before the timed ones (the synthesized meshes rebalance)")
     ap.add_argument("--adv-peers", type=int, default=4_000_000, help="cfg5 adversarial overlay (0: skip)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on one GPU: all ranks on device 0, gloo (host-staged) instead of RCCL")
@@ -608,16 +612,18 @@ def main():
     hb = None
     if args.hb_steps > 0:
         # steady state: a gossipsub batch arrives before every heartbeat (untimed),
-        # so every round's emitGossip advertises the cached windows (mcache);
-        # the rounds run through the OpportunisticGraftTicks round 60, where every
-        # unit with a mesh sorts its scores (the "active" round)
+        # so every round's emitGossip advertises the cached windows (mcache).
+        # The synthesized meshes (every pair in the mesh with p = 0.5) rebalance
+        # over the first rounds (~3e7 grafts + prunes in the first): --hb-settle
+        # untimed rounds (reported as settle_per_round), then the timed rounds
+        # through the OpportunisticGraftTicks round 60 (the "active" round)
         th_hb = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                                accept_px_threshold=0, opportunistic_graft_threshold=5)
         e.set_thresholds(th_hb)
-        tick = 57
+        tick = 58 - args.hb_settle
         hb_cfg = prop_config(args, n)
-        rounds = []
-        for k in range(args.hb_steps + 1):  # the first round is a warm-up
+        rounds, settle = [], []
+        for k in range(args.hb_settle + args.hb_steps):
             tick += 1
             now += abi.SECOND
             hb_cfg.now_ns = now - abi.SECOND // 2
@@ -630,8 +636,8 @@ def main():
             e.sync()
             ms = (time.perf_counter() - t0) * 1e3
             ms = reduce_scalar(ms, dist, dev, "max")
-            if k:
-                rounds.append({"tick": tick, "og_tick": tick % 60 == 0, "ms": ms, **o})
+            r = {"tick": tick, "og_tick": tick % 60 == 0, "ms": ms, **o}
+            (rounds if k >= args.hb_settle else settle).append(r)
         units = float(n) * T
         deg = E / n
         d_hi = 12
@@ -662,6 +668,7 @@ def main():
             "roofline_steady": roof(steady_ms),
             "roofline_active": roof(active_ms),
             "per_round": rounds,
+            "settle_per_round": [{k: r[k] for k in ("tick", "ms", "grafts", "prunes")} for r in settle],
         }
 
     adv = adversarial_leg(args, rank, world, local, dist, dev) if args.adv_peers > 0 else None
