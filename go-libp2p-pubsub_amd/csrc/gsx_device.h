@@ -291,6 +291,9 @@ struct HbState {
     unsigned long long* stats;
     uint32_t* rngk;        // [topic][node]: draw counter after the unit's maintenance (emitGossip continues it)
     uint16_t* mcount;      // [topic][node]: mesh size, as the scan found it / (A) left it / (B) keeps it
+    uint64_t* tr_acc;      // [pair]: topics whose GRAFT the owner accepted (tracing; else null)
+    uint64_t* tr_hp;       // [pair]: topics whose PRUNE the owner handled (tracing; else null)
+    bool keep_ctl;         // (B) leaves the control words it reads (tracing: gsx_hb_trace_words)
     uint32_t* work;        // [topic][tile * 64 + i]: units the scan found acting, per 64-node tile
     uint8_t* tcnt;         // [topic][tile]: how many (lane-per-unit maintenance)
     uint64_t n_tiles64;    // 64 * tiles: the per-topic stride of `work`

@@ -114,6 +114,9 @@ struct gsx_engine {
     uint64_t* d_ihave_hash = nullptr;
     bool have_gossip = false;
     bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
+    bool hb_tracing = false;           // gsx_hb_set_tracing: keep the round's tracer Graft / Prune words
+    uint64_t* d_tr_acc = nullptr;      // [pair] accepted GRAFT topics of the last round
+    uint64_t* d_tr_hp = nullptr;       // [pair] handled PRUNE topics of the last round
     gsx::HbState hb{};  // the round in flight (gsx_hb_begin .. gsx_hb_end)
     bool hb_active = false;
 
@@ -401,7 +404,7 @@ void free_state(gsx_engine* e) {
     e->d_col = nullptr;
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
                   e->d_backoff, e->d_bo8, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
-                  e->d_nlong,   e->d_hbstats,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
+                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
@@ -411,6 +414,7 @@ void free_state(gsx_engine* e) {
     e->d_dirty = nullptr;
     e->d_long = e->d_nlong = nullptr;
     e->d_hbstats = nullptr;
+    e->d_tr_acc = e->d_tr_hp = nullptr;
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_tcnt = nullptr;
@@ -2152,6 +2156,17 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.work = e->d_work;
     h.tcnt = e->d_tcnt;
     h.mcount = e->d_mcount;
+    if (e->hb_tracing) {
+        if (!e->d_tr_acc) {
+            if (int rc = dalloc(e, &e->d_tr_acc, std::max<size_t>(e->E, 1))) return rc;
+            if (int rc = dalloc(e, &e->d_tr_hp, std::max<size_t>(e->E, 1))) return rc;
+        }
+        HIPCHK(e, hipMemsetAsync(e->d_tr_acc, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_tr_hp, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
+        h.tr_acc = e->d_tr_acc;
+        h.tr_hp = e->d_tr_hp;
+        h.keep_ctl = true;
+    }
     h.n_tiles64 = 64 * (((uint64_t)e->n_nodes + 63) / 64);
     h.hub_work = e->d_hubwork;
     h.n_hub = e->d_nwork + e->T;
@@ -2296,7 +2311,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     e->hb_active = false;
     std::memset(out, 0, sizeof(*out));
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
-    e->hb_clean = !e->sharded();
+    e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
     HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
@@ -2360,6 +2375,30 @@ int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out)
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_recv && !halo_resp) return GSX_EINVAL;
     return hb_end(e, halo_resp, out);
+}
+
+int gsx_hb_set_tracing(gsx_engine* e, uint32_t on) {
+    if (!e) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    e->hb_tracing = on != 0;
+    e->hb_clean = false;
+    return GSX_OK;
+}
+
+int gsx_hb_trace_words(gsx_engine* e, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
+                       uint64_t* handled_prune) {
+    if (!e) return GSX_EINVAL;
+    if (!e->hb_tracing || !e->d_tr_acc) return fail(e, GSX_ESTATE, "no traced heartbeat (gsx_hb_set_tracing)");
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    const size_t n = 8 * (size_t)e->E;
+    if (n) {
+        if (sent_graft) HIPCHK(e, hipMemcpyAsync(sent_graft, e->d_ctl_graft, n, hipMemcpyDeviceToHost, e->stream));
+        if (sent_prune) HIPCHK(e, hipMemcpyAsync(sent_prune, e->d_ctl_prune, n, hipMemcpyDeviceToHost, e->stream));
+        if (acc_graft) HIPCHK(e, hipMemcpyAsync(acc_graft, e->d_tr_acc, n, hipMemcpyDeviceToHost, e->stream));
+        if (handled_prune) HIPCHK(e, hipMemcpyAsync(handled_prune, e->d_tr_hp, n, hipMemcpyDeviceToHost, e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
 }
 
 int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest) {

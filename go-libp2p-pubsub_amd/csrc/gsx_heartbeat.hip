@@ -1115,6 +1115,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
 __device__ __forceinline__ bool handle_prune(const DevState& s, const HbState& h, uint64_t q, uint32_t t) {
     const bool was = hb_in_mesh(s, q, t) && scored_topic(s, q, t);
     ev_prune(s, q, t);
+    if (h.tr_hp) h.tr_hp[q] |= 1ull << t;  // tracer.Prune, :822
     const int64_t secs = h.gp.prune_backoff_ns / 1000000000LL;
     add_backoff(h, q, t, secs > 0 ? secs * 1000000000LL : h.gp.prune_backoff_ns);
     return was;
@@ -1133,7 +1134,7 @@ __device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool 
     } else {
         grafts = h.ctl_graft[r];
         prunes = h.ctl_prune[r];
-        if (write && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+        if (write && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
     }
     return (grafts | prunes) != 0;
 }
@@ -1211,6 +1212,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                     continue;
                 }
                 ev_graft(s, q, t, h.now);
+                if (h.tr_acc) h.tr_acc[q] |= 1ull << t;  // tracer.Graft, :795
                 ++accepted;
                 if (scored_topic(s, q, t)) {
                     ++links;
@@ -1264,7 +1266,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 uint64_t grafts, prunes;
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
-                if (w0 && !(r & HALO) && !h.halo_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                if (w0 && !(r & HALO) && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
                 const double score = s.score[q];
                 const uint8_t ef = h.eflags[q];
                 if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
@@ -1313,6 +1315,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                     __syncthreads();  // every lane has read the flags before lane 0 grafts
                     if (w0) {
                         ev_graft(s, q, t, h.now);
+                        if (h.tr_acc) h.tr_acc[q] |= 1ull << t;  // tracer.Graft, :795
                         if (sc_t) *mcp = (uint16_t)(n + 1);
                     }
                     accepted += w0;

@@ -377,6 +377,8 @@ SIGNATURES = {
     "gsx_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
     "gsx_mcache_clear": (C.c_int, [C.c_void_p]),
+    "gsx_hb_set_tracing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
     "gsx_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
     "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),

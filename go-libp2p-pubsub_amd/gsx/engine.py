@@ -350,6 +350,16 @@ class Engine:
     def mcache_clear(self):
         self._chk(self.lib.gsx_mcache_clear(self.h), "gsx_mcache_clear")
 
+    def hb_set_tracing(self, on: bool = True):
+        self._chk(self.lib.gsx_hb_set_tracing(self.h, 1 if on else 0), "gsx_hb_set_tracing")
+
+    def hb_trace_words(self):
+        """-> (sent_graft, sent_prune, acc_graft, handled_prune) [E] u64 topic words
+        of the last heartbeat (gsx_hb_trace_words; hb_set_tracing first)."""
+        w = [np.empty(self.n_pairs, dtype=np.uint64) for _ in range(4)]
+        self._chk(self.lib.gsx_hb_trace_words(self.h, *[_ptr(x, C.c_uint64) for x in w]), "gsx_hb_trace_words")
+        return tuple(w)
+
     def mcache_ids(self, node: int, topic: int, n_windows: int) -> np.ndarray:
         """mcache.GetGossipIDs of `node` over its first n_windows windows."""
         n = C.c_size_t()

@@ -7,16 +7,25 @@ varint-length-delimited protobufs (``tracer.go:131-170``), so existing trace
 tooling reads a stream of such records.  This module turns what the engine
 already computes on the GPU into that stream:
 
-* ``mesh_trace``     — GRAFT / PRUNE events from the scorer's inMesh flags
-  before and after a heartbeat (``export_state()['rec_flags']``): one GRAFT
-  per (observer, topic, peer) that entered the mesh, one PRUNE per one that
-  left it.  The engine's rounds are synchronous, so what it reports is the net
-  mesh change of the round; the reference emits the same set (its order within
-  a heartbeat follows Go map iteration and is not observable).
-* ``delivery_trace`` — DELIVER_MESSAGE (or, for a message validation does not
-  accept, REJECT_MESSAGE with its reason) events from ``prop_results()``: one
-  per (node, message) first receipt, ``receivedFrom`` = the first deliverer.  The publisher itself gets no
-  event (``trace.go:171``: only messages received from another peer).
+* ``mesh_trace``     — GRAFT / PRUNE events of one heartbeat from the round's
+  tracer words (``hb_trace_words()``, gsx_hb_trace_words): every graftPeer /
+  prunePeer of the maintenance (gossipsub.go:1346, :1355), every GRAFT a
+  receiver accepts (:795) and every PRUNE a node handles, including the PRUNE
+  answers to rejected GRAFTs (:822).  A GRAFT answered with PRUNE therefore
+  yields GRAFT (sender) + PRUNE (sender, handling the answer), as in the
+  reference; the counts are grafts + graft_accepted and prunes +
+  prunes_handled.  The order within a heartbeat follows Go map iteration in
+  the reference and is not observable; here it is (pair, kind, topic).
+* ``delivery_trace`` — per message: PUBLISH_MESSAGE at its source
+  (validation.go:217) and DELIVER_MESSAGE there with receivedFrom = the source
+  itself (pubsub.go:1124-1125, publishMessage delivers locally published
+  messages too) — or, for a message validation does not accept, REJECT_MESSAGE
+  there with its reason (PushLocal's validation, validation.go:216-342); then one
+  DELIVER_MESSAGE (or REJECT_MESSAGE with its reason) per (node, message) first
+  receipt, ``receivedFrom`` = the first deliverer.  DUPLICATE_MESSAGE events
+  (one per further copy, trace.go:136-164) are not in this stream: the engine
+  counts duplicates (gsx_prop_out.duplicates) but does not record who sent
+  each copy; the stream is partial in exactly that class.
 
 Field numbers and wire types follow ``pb/trace.proto:5-104``; fields are
 written in field-number order, as the gogo marshaller does.  This is host-side
@@ -46,7 +55,7 @@ GRAFT = 11
 PRUNE = 12
 
 # TraceEvent sub-message field numbers (pb/trace.proto:10-22)
-_SUB_FIELD = {REJECT_MESSAGE: 5, DUPLICATE_MESSAGE: 6, DELIVER_MESSAGE: 7, GRAFT: 15, PRUNE: 16}
+_SUB_FIELD = {PUBLISH_MESSAGE: 4, REJECT_MESSAGE: 5, DUPLICATE_MESSAGE: 6, DELIVER_MESSAGE: 7, GRAFT: 15, PRUNE: 16}
 
 # RejectMessage reasons of the validation outcomes (tracer.go:26-38, validation.go:320-383)
 REJECT_REASON = {
@@ -100,6 +109,11 @@ def graft_event(observer: bytes, peer: bytes, topic: str, timestamp: int) -> byt
 def prune_event(observer: bytes, peer: bytes, topic: str, timestamp: int) -> bytes:
     """trace.go:495-520: Prune{peerID = p, topic}."""
     return encode_event(PRUNE, observer, timestamp, _len_field(1, _s(peer)) + _len_field(2, _s(topic)))
+
+
+def publish_event(node: bytes, msg_id: bytes, topic: str, timestamp: int) -> bytes:
+    """trace.go:76-103: PublishMessage{messageID, topic} (proto :40-43)."""
+    return encode_event(PUBLISH_MESSAGE, node, timestamp, _len_field(1, _s(msg_id)) + _len_field(2, _s(topic)))
 
 
 def deliver_event(node: bytes, msg_id: bytes, topic: str, received_from: bytes, timestamp: int) -> bytes:
@@ -177,20 +191,29 @@ def mesh_changes(before_flags, after_flags, n_topics: int) -> Tuple[np.ndarray, 
 
 
 def mesh_trace(
-    before_flags,
-    after_flags,
+    words,
     row_ptr,
     col,
     topics: Sequence[str],
     timestamp: int,
     peer_id: Callable[[int], bytes] = default_peer_id,
 ) -> Iterator[bytes]:
-    """GRAFT / PRUNE events of one heartbeat, ordered by (observer, peer, topic)."""
+    """GRAFT / PRUNE events of one heartbeat from its tracer words
+    ``(sent_graft, sent_prune, acc_graft, handled_prune)`` ([E] u64 topic bits
+    per pair, hb_trace_words()), ordered by (pair, kind in that order, topic);
+    every event's observer is the pair's owner and its peer the pair's peer."""
     obs, peer = pair_endpoints(row_ptr, col)
-    topic, pair, grafted = mesh_changes(before_flags, after_flags, len(topics))
-    for t, p, g in zip(topic.tolist(), pair.tolist(), grafted.tolist()):
-        mk = graft_event if g else prune_event
-        yield mk(peer_id(int(obs[p])), peer_id(int(peer[p])), topics[t], timestamp)
+    kinds = (GRAFT, PRUNE, GRAFT, PRUNE)
+    w = np.stack([np.asarray(x, dtype=np.uint64) for x in words])  # [4, E]
+    for p in np.nonzero(np.any(w != 0, axis=0))[0].tolist():
+        o, q = peer_id(int(obs[p])), peer_id(int(peer[p]))
+        for kind, bits in zip(kinds, w[:, p].tolist()):
+            t = 0
+            while bits:
+                if bits & 1:
+                    yield (graft_event if kind == GRAFT else prune_event)(o, q, topics[t], timestamp)
+                bits >>= 1
+                t += 1
 
 
 def delivery_trace(
@@ -205,8 +228,8 @@ def delivery_trace(
     node_base: int = 0,
     validation_delay_ns: int = 0,
 ) -> Iterator[bytes]:
-    """DELIVER_MESSAGE / REJECT_MESSAGE events of one propagation on ``topic``,
-    ordered by (message, node).
+    """PUBLISH_MESSAGE / DELIVER_MESSAGE / REJECT_MESSAGE events of one
+    propagation on ``topic``, ordered by (message, source first, node).
 
     ``hop`` / ``first_from`` are prop_results() rows ([m, n] arrival hop, 0xFF
     = never, 0 at the source; first deliverer, global id); ``msgs`` the
@@ -227,7 +250,16 @@ def delivery_trace(
     step = hop_latency_ns + validation_delay_ns
     for m in range(hop.shape[0]):
         v = int(msgs["validation"][m])
-        ident = mid(int(msgs["source"][m]), int(msgs["msg_id"][m]))
+        src = int(msgs["source"][m])
+        ident = mid(src, int(msgs["msg_id"][m]))
+        if node_base <= src < node_base + hop.shape[1] and hop[m, src - node_base] == 0:
+            # the local publish: PublishMessage, then (accepted) the local delivery
+            me = peer_id(src)
+            yield publish_event(me, ident, topic, now)
+            if v == GSX_VALIDATION_ACCEPT:
+                yield deliver_event(me, ident, topic, me, now)
+            else:  # its local validation (PushLocal -> validate, validation.go:216-342) rejects it
+                yield reject_event(me, ident, me, REJECT_REASON[v], topic, now)
         for u in np.nonzero((hop[m] != 0xFF) & (hop[m] != 0))[0].tolist():
             node, frm, ts = peer_id(node_base + u), peer_id(int(first_from[m, u])), now + int(hop[m, u]) * step
             if v == GSX_VALIDATION_ACCEPT:

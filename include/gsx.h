@@ -593,6 +593,19 @@ int gsx_import_backoff(gsx_engine* e, const int64_t* in);
  * receiver collects the ids into a set (handleIHave, gossipsub.go:641-650).
  * Either pointer may be NULL. */
 int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest);
+/* The tracer's GRAFT / PRUNE calls of the last heartbeat, as topic bit words
+ * per pair p = (observer -> peer), E words each (any pointer may be NULL):
+ *   sent_graft    graftPeer (:1353-1359)             Graft(peer, topic) by observer
+ *   sent_prune    prunePeer (:1345-1351)             Prune(peer, topic) by observer
+ *   acc_graft     handleGraft accepting it (:794-796) Graft(peer, topic) by observer
+ *   handled_prune handlePrune of the peer's PRUNE, (B) and the (C) answers
+ *                 (:821-822)                         Prune(peer, topic) by observer
+ * so popcounts give grafts + graft_accepted GRAFT and prunes + prunes_handled
+ * PRUNE events.  Recorded only while gsx_hb_set_tracing(e, 1) (off by
+ * default: the control words are then kept until the next round's start). */
+int gsx_hb_set_tracing(gsx_engine* e, uint32_t on);
+int gsx_hb_trace_words(gsx_engine* e, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
+                       uint64_t* handled_prune);
 /* Drop every cached message window (mcache.go, a fresh cache). */
 int gsx_mcache_clear(gsx_engine* e);
 /* mcache.GetGossipIDs of one node (mcache.go:82-92) over its first n_windows

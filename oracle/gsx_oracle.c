@@ -88,6 +88,9 @@ struct orc_engine {
     uint32_t mc_n; /* windows alive (history[0..mc_n-1]) */
     uint32_t* ihave_len;   /* [t][pair] of the last heartbeat */
     uint64_t* ihave_hash;
+    /* the last heartbeat's tracer Graft / Prune calls, topic bits per pair
+     * (gsx_hb_trace_words): sent GRAFT, sent PRUNE, accepted GRAFT, handled PRUNE */
+    uint64_t *tr_sg, *tr_sp, *tr_ag, *tr_hp;
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -271,6 +274,10 @@ void orc_destroy(orc_engine* o) {
     free(o->mc);
     free(o->ihave_len);
     free(o->ihave_hash);
+    free(o->tr_sg);
+    free(o->tr_sp);
+    free(o->tr_ag);
+    free(o->tr_hp);
     free(o->ipc.keys);
     free(o->ipc.vals);
     free_records(o);
@@ -321,6 +328,12 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     o->ihave_len = (uint32_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint32_t));
     o->ihave_hash = (uint64_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint64_t));
     if (!o->ihave_len || !o->ihave_hash) return GSX_ENOMEM;
+    uint64_t** tw[4] = {&o->tr_sg, &o->tr_sp, &o->tr_ag, &o->tr_hp};
+    for (int i = 0; i < 4; i++) {
+        free(*tw[i]);
+        *tw[i] = (uint64_t*)calloc(E ? E : 1, sizeof(uint64_t));
+        if (!*tw[i]) return GSX_ENOMEM;
+    }
     if (!o->mc) o->mc = (orc_mc_window*)calloc(ORC_MC_MAX, sizeof(orc_mc_window));
     if (!o->mc) return GSX_ENOMEM;
     orc_mcache_clear(o);
@@ -1281,6 +1294,7 @@ static int get_peers(hb_ctx* c, uint32_t v, uint32_t t, int count, int filter, i
 static void hb_graft(hb_ctx* c, uint64_t r, uint32_t t) { /* graftPeer, :1353-1359 */
     graft(c->o, r, t, c->now);
     c->ctl[(size_t)t * c->o->E + r] = 1;
+    c->o->tr_sg[r] |= 1ull << t; /* tracer.Graft, :1355 */
     c->out->grafts++;
 }
 
@@ -1288,6 +1302,7 @@ static void hb_prune(hb_ctx* c, uint64_t r, uint32_t t) { /* prunePeer, :1345-13
     prune(c->o, r, t);
     add_backoff(c->o, r, t, c->now, c->gp->prune_backoff_ns);
     c->ctl[(size_t)t * c->o->E + r] = 2;
+    c->o->tr_sp[r] |= 1ull << t; /* tracer.Prune, :1346 */
     c->out->prunes++;
 }
 
@@ -1480,6 +1495,7 @@ static void mcache_shift(orc_engine* o, uint32_t history) {
 static void handle_prune(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t q, uint32_t t, int64_t now,
                          gsx_heartbeat_out* out) {
     prune(o, q, t); /* tracer.Prune, unconditional */
+    o->tr_hp[q] |= 1ull << t;
     /* the PRUNE carries PruneBackoff in whole seconds (:1821); 0 means "use our own" (:825-830) */
     const int64_t secs = gp->prune_backoff_ns / 1000000000LL;
     add_backoff(o, q, t, now, secs > 0 ? secs * 1000000000LL : gp->prune_backoff_ns);
@@ -1500,6 +1516,10 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
             }
     double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
     uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    memset(o->tr_sg, 0, 8 * (E ? E : 1));
+    memset(o->tr_sp, 0, 8 * (E ? E : 1));
+    memset(o->tr_ag, 0, 8 * (E ? E : 1));
+    memset(o->tr_hp, 0, 8 * (E ? E : 1));
     uint8_t* resp = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
     uint64_t max_deg = 1;
     for (uint32_t i = 0; i < o->n_nodes; i++)
@@ -1566,7 +1586,8 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
                     out->graft_rejected++;
                     continue;
                 }
-                graft(o, (uint64_t)q, t, now);
+                graft(o, (uint64_t)q, t, now); /* tracer.Graft, :795 */
+                o->tr_ag[q] |= 1ull << t;
                 out->graft_accepted++;
             }
             for (uint32_t t = 0; t < T; t++) /* handlePrune */
@@ -1591,6 +1612,16 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     free(resp);
     free(plst);
     free(tmp);
+    return 0;
+}
+
+int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
+                       uint64_t* handled_prune) {
+    if (!o->tr_sg) return GSX_ESTATE;
+    if (sent_graft) memcpy(sent_graft, o->tr_sg, 8 * o->E);
+    if (sent_prune) memcpy(sent_prune, o->tr_sp, 8 * o->E);
+    if (acc_graft) memcpy(acc_graft, o->tr_ag, 8 * o->E);
+    if (handled_prune) memcpy(handled_prune, o->tr_hp, 8 * o->E);
     return 0;
 }
 

@@ -56,6 +56,9 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
 int orc_default_gossipsub_params(gsx_gossipsub_params* p);
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now_ns, uint64_t seed,
                   gsx_heartbeat_out* out);
+/* gsx_hb_trace_words of the last orc_heartbeat (always recorded). */
+int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
+                       uint64_t* handled_prune);
 int orc_export_backoff(orc_engine* o, int64_t* out);
 int orc_import_backoff(orc_engine* o, const int64_t* in);
 int orc_gossip_results(orc_engine* o, uint32_t* len, uint64_t* hash);

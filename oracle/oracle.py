@@ -60,6 +60,7 @@ _SIG = {
     "orc_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "orc_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
     "orc_mcache_clear": (C.c_int, [C.c_void_p]),
+    "orc_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
     "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
 }
@@ -175,6 +176,14 @@ class Oracle:
 
     def mcache_clear(self):
         self._chk(self.lib.orc_mcache_clear(self.h), "orc_mcache_clear")
+
+    def hb_set_tracing(self, on: bool = True):
+        """(the oracle always records the trace words)"""
+
+    def hb_trace_words(self):
+        w = [np.empty(self.n_pairs, dtype=np.uint64) for _ in range(4)]
+        self._chk(self.lib.orc_hb_trace_words(self.h, *[_p(x, C.c_uint64) for x in w]), "orc_hb_trace_words")
+        return tuple(w)
 
     def mcache_ids(self, node, topic, n_windows):
         n = C.c_size_t()

@@ -1,6 +1,7 @@
 """Trace export from GPU results (gsx/trace.py): the GRAFT /
 PRUNE stream of a heartbeat and the DELIVER_MESSAGE / REJECT_MESSAGE stream of a propagation
 are byte-identical to the streams built from the oracle's results."""
+import numpy as np
 import pytest
 
 import gsx
@@ -15,6 +16,8 @@ def test_heartbeat_trace_gpu_equals_oracle(gpu_ok):
     g = tc.heartbeat_stream(gsx.Engine(T))
     w = tc.heartbeat_stream(orc.Oracle(T))
     assert g[1] == w[1] and g[2] == w[2]
+    for a, b in zip(g[3], w[3]):
+        assert np.array_equal(a, b)
     assert len(g[0]) > 0 and g[0] == w[0]
 
 

@@ -36,6 +36,7 @@ def _trace_event_class():
             m.field.add(name=fname, number=num, type=typ, label=F.LABEL_OPTIONAL)
 
     B, S = F.TYPE_BYTES, F.TYPE_STRING
+    sub("PublishMessage", [("messageID", 1, B), ("topic", 2, S)])
     sub("RejectMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("reason", 3, S), ("topic", 4, S)])
     sub("DuplicateMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("topic", 3, S)])
     sub("DeliverMessage", [("messageID", 1, B), ("topic", 2, S), ("receivedFrom", 3, B)])
@@ -44,7 +45,7 @@ def _trace_event_class():
     ev.field.add(name="type", number=1, type=F.TYPE_ENUM, type_name=".gsxtest.TraceEvent.Type", label=F.LABEL_OPTIONAL)
     ev.field.add(name="peerID", number=2, type=B, label=F.LABEL_OPTIONAL)
     ev.field.add(name="timestamp", number=3, type=F.TYPE_INT64, label=F.LABEL_OPTIONAL)
-    for fname, num, tname in [("rejectMessage", 5, "RejectMessage"), ("duplicateMessage", 6, "DuplicateMessage"), ("deliverMessage", 7, "DeliverMessage"),
+    for fname, num, tname in [("publishMessage", 4, "PublishMessage"), ("rejectMessage", 5, "RejectMessage"), ("duplicateMessage", 6, "DuplicateMessage"), ("deliverMessage", 7, "DeliverMessage"),
                               ("graft", 15, "Graft"), ("prune", 16, "Prune")]:
         ev.field.add(name=fname, number=num, type=F.TYPE_MESSAGE, type_name=f".gsxtest.TraceEvent.{tname}",
                      label=F.LABEL_OPTIONAL)
@@ -66,6 +67,14 @@ def test_graft_prune_bytes_match_protobuf(ts):
         got = enc(b"obs\x00\xff", b"peer-7", "té", ts)
         assert got == want.SerializeToString(deterministic=True)
         assert TE.FromString(got) == want
+
+
+@pytest.mark.parametrize("ts", TS)
+def test_publish_bytes_match_protobuf(ts):
+    mid = tr.default_msg_id(3, 7)
+    want = TE(type=0, peerID=b"src", timestamp=ts)
+    want.publishMessage.messageID, want.publishMessage.topic = mid, "t"
+    assert tr.publish_event(b"src", mid, "t", ts) == want.SerializeToString(deterministic=True)
 
 
 @pytest.mark.parametrize("ts", TS)
@@ -100,21 +109,34 @@ def test_mesh_changes_ordering():
     after = np.array([1, 1, 0, 0, 1, 1], dtype=np.uint8) | np.uint8(0x80)  # other bits ignored
     t, p, g = tr.mesh_changes(before, after, 2)
     assert list(zip(p.tolist(), t.tolist(), g.tolist())) == [(1, 0, True), (1, 1, True), (2, 0, False)]
+
+
+def test_mesh_trace_from_words_ordering():
+    # pairs 0 (0 -> 5), 1 (0 -> 6), 2 (1 -> 7); words: sent GRAFT, sent PRUNE, accepted GRAFT, handled PRUNE
     row_ptr, col = np.array([0, 2, 3]), np.array([5, 6, 7])
-    ev = [TE.FromString(e) for e in tr.mesh_trace(before, after, row_ptr, col, ["a", "b"], 9)]
-    assert [(e.type, e.peerID, (e.graft if e.type == 11 else e.prune).peerID, e.timestamp) for e in ev] == [
-        (11, b"gsx-0", b"gsx-6", 9), (11, b"gsx-0", b"gsx-6", 9), (12, b"gsx-1", b"gsx-7", 9)]
-    assert [e.graft.topic or e.prune.topic for e in ev] == ["a", "b", "a"]
+    words = [np.array(x, dtype=np.uint64) for x in ([0, 3, 0], [0, 0, 1], [2, 0, 0], [0, 1, 1])]
+    ev = [TE.FromString(e) for e in tr.mesh_trace(words, row_ptr, col, ["a", "b"], 9)]
+    got = [(e.type, e.peerID, (e.graft if e.type == 11 else e.prune).peerID,
+            (e.graft if e.type == 11 else e.prune).topic, e.timestamp) for e in ev]
+    assert got == [(11, b"gsx-0", b"gsx-5", "b", 9),                               # pair 0: accepted
+                   (11, b"gsx-0", b"gsx-6", "a", 9), (11, b"gsx-0", b"gsx-6", "b", 9),  # pair 1: sent
+                   (12, b"gsx-0", b"gsx-6", "a", 9),                                 # its PRUNE answer
+                   (12, b"gsx-1", b"gsx-7", "a", 9), (12, b"gsx-1", b"gsx-7", "a", 9)]  # sent + handled
 
 
 def test_heartbeat_trace_matches_counters():
-    buf, out, links_before = tc.heartbeat_stream(orc.Oracle(len(tc.TOPICS)))
+    """GRAFT events = grafts + graft_accepted, PRUNE events = prunes +
+    prunes_handled (gossipsub.go:795, :822, :1346, :1355); a GRAFT answered
+    with PRUNE shows as the sender's GRAFT and then its PRUNE."""
+    buf, out, links_before, words = tc.heartbeat_stream(orc.Oracle(len(tc.TOPICS)))
     ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
     n_graft = sum(e.type == 11 for e in ev)
     n_prune = sum(e.type == 12 for e in ev)
-    assert n_graft > 0 and n_prune > 0
-    assert links_before + n_graft - n_prune == out["mesh_links"]
+    assert n_graft == out["grafts"] + out["graft_accepted"] > 0
+    assert n_prune == out["prunes"] + out["prunes_handled"] > 0
     assert all(e.HasField("graft") != e.HasField("prune") for e in ev)
+    sg, sp, ag, hp = words
+    assert out["graft_rejected"] > 0 and int(np.count_nonzero(sg & hp)) > 0  # rejected: GRAFT then PRUNE
 
 
 @pytest.mark.parametrize("invalid,delay_ms", [(0.0, 0.0), (0.3, 0.0), (0.3, 4.0)])
@@ -122,10 +144,28 @@ def test_delivery_trace_matches_results(invalid, delay_ms):
     buf, hop, frm, ms = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid, delay_ms=delay_ms)
     ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
     recv = (hop != 0xFF) & (hop != 0)
-    assert len(ev) == int(recv.sum()) > 0
+    assert len(ev) == int(recv.sum()) + 2 * len(ms) > 0
+    # per message: the source's PUBLISH_MESSAGE and its own DELIVER (REJECT when not accepted) first
+    pub, rest = [], []
+    k = 0
+    for m in range(len(ms)):
+        pub.append((m, ev[k], ev[k + 1]))
+        n = int(recv[m].sum())
+        rest.extend(ev[k + 2:k + 2 + n])
+        k += 2 + n
+    now = tc.pc.T0 + 3 * tc.pc.S
+    for m, p, d in pub:
+        src = tr.default_peer_id(int(ms["source"][m]))
+        mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
+        assert p.type == 0 and p.peerID == src and p.publishMessage.messageID == mid and p.timestamp == now
+        assert p.publishMessage.topic == tc.TOPICS[1]
+        if int(ms["validation"][m]) == abi.GSX_VALIDATION_ACCEPT:
+            assert d.type == 3 and d.deliverMessage.receivedFrom == src and d.deliverMessage.messageID == mid
+        else:
+            assert d.type == 1 and d.rejectMessage.receivedFrom == src
     m_idx, u_idx = np.nonzero(recv)
     n_rej = 0
-    for e, m, u in zip(ev, m_idx.tolist(), u_idx.tolist()):
+    for e, m, u in zip(rest, m_idx.tolist(), u_idx.tolist()):
         v = int(ms["validation"][m])
         mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
         assert e.peerID == tr.default_peer_id(u)

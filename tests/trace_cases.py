@@ -11,16 +11,18 @@ TOPICS = ["topic-a", "topic-b"]
 
 
 def heartbeat_stream(be, n=400, d=6, seed=11):
-    """One heartbeat after pc.setup's random mesh: (stream, counters, in-mesh count before)."""
+    """One traced heartbeat after pc.setup's random mesh: (stream, counters, in-mesh
+    count before, tracer words)."""
     T = len(TOPICS)
     ov = pc.overlay(n, d, seed)
     pc.setup(be, ov, T, seed, mesh_degree=6)
     before = be.export_state()["rec_flags"].copy()
+    be.hb_set_tracing(True)
     out = be.heartbeat(1, hc.T0 + 3 * hc.S, seed * 31 + 7).as_dict()
-    after = be.export_state()["rec_flags"]
-    ev = list(tr.mesh_trace(before, after, ov.row_ptr, ov.col, TOPICS, hc.T0 + 3 * hc.S))
+    words = be.hb_trace_words()
+    ev = list(tr.mesh_trace(words, ov.row_ptr, ov.col, TOPICS, hc.T0 + 3 * hc.S))
     links_before = int(np.count_nonzero(before & abi.GSX_REC_IN_MESH))
-    return tr.write_delimited(ev), out, links_before
+    return tr.write_delimited(ev), out, links_before, words
 
 
 def delivery_stream(be, n=500, m=40, seed=7, invalid=0.0, delay_ms=0.0):
