@@ -251,6 +251,14 @@ enum {
     HB_MESH_LINKS,
     HB_IHAVE_MSGS,
     HB_IHAVE_IDS,
+    HB_BROKEN_PROMISES,
+    HB_IHAVE_IGNORED,
+    HB_IWANT_MSGS,
+    HB_IWANT_IDS,
+    HB_IWANT_SERVED,
+    HB_GOSSIP_DELIVERED,
+    HB_GOSSIP_REJECTED,
+    HB_GOSSIP_DUPLICATES,
     HB_STAT_WORDS
 };  // the order of gsx_heartbeat_out
 
@@ -260,7 +268,24 @@ struct DevGossipParams {
     int64_t prune_backoff_ns, graft_flood_threshold_ns;
     int32_t d_lazy, max_ihave;
     double gossip_factor;
+    int32_t max_ihave_msgs, retransmission;  // MaxIHaveMessages, GossipRetransmission
+    int64_t followup_ns;                      // IWantFollowupTime
 };
+
+// One advertised batch of the gossip exchange (heartbeat step (D)): the
+// batch's cache rows, and its message set's seen rows (exchange start),
+// receipts of this exchange, validation outcomes and serial (promise handles
+// are serial << 32 | message index).
+struct GxBatch {
+    const uint64_t* mem;  // [node][word]: in the node's cache
+    const uint64_t* all;  // [node][word]: seen by the node
+    uint64_t* x;          // [node][word]: received in this exchange
+    const uint32_t* val;  // [message]: GSX_VALIDATION_*
+    uint8_t* got;         // set to 1 when some node delivers a message of the set
+    uint32_t n_words, serial, topic, avail;  // avail: still cached after this heartbeat's Shift
+};
+constexpr int GX_PROMISE_SLOTS = 8;  // outstanding promises per pair (gossip_tracer.go:24-27)
+constexpr uint64_t TAG_IWANT = 9;
 
 // One cached gossipsub batch (a gsx_propagate call) of an mcache window:
 // node v has message k iff bit k % 64 of seen[v * n_words + k / 64].
@@ -303,6 +328,17 @@ struct HbState {
     uint32_t n_hubs;
     uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)
     uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
+    // the gossip exchange (step (D)); null when it is off
+    uint64_t* ihave_bits;  // [pair (v -> u)]: topics v sent an IHAVE for this round
+    uint32_t* ihave_trunc; // set when an IHAVE list was truncated (not exchanged)
+    const int32_t* col;    // [pair]: the peer (local node id)
+    const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
+    const uint32_t* gx_off;
+    uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
+    uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
+    uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none)
+    uint64_t* prom_h;      // [pair][GX_PROMISE_SLOTS]: promised message handle
+    int64_t* prom_e;       // [pair][GX_PROMISE_SLOTS]: its expiry (0 = free slot)
     const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
     uint32_t* long_nodes;  // nodes whose gossip list needs per-target truncation
     uint32_t* n_long;
@@ -323,6 +359,12 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
 hipError_t launch_bo_rebuild(const int64_t* backoff, uint8_t* bo8, uint64_t n_pairs, uint32_t n_topics,
                              hipStream_t st);
 hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st);
+// The gossip exchange: broken promises at the heartbeat start (P7), step (D),
+// and folding an exchange's receipts into the message set (all |= x; x &= acc).
+hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
+hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
+                           hipStream_t st);
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st);
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
                             uint32_t max_ids, int64_t max_deg, hipStream_t st);

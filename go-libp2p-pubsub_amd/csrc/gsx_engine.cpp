@@ -120,6 +120,21 @@ struct gsx_engine {
     gsx::HbState hb{};  // the round in flight (gsx_hb_begin .. gsx_hb_end)
     bool hb_active = false;
 
+    // The messages of one gossipsub propagate call (gossip exchange, gsx.h (D)):
+    // who has seen each (first receipt or publish, and exchange receipts), the
+    // validation outcomes, ids and digests; shared by the batch that cached
+    // them and the batches of copies recovered later (reference counted).
+    struct MsgSet {
+        uint32_t serial = 0, n_msgs = 0, n_words = 0, topic = 0;
+        uint64_t* d_all = nullptr;  // [node][word] (seen-row pool buffer)
+        size_t all_words = 0;
+        uint32_t* d_val = nullptr;  // [message] GSX_VALIDATION_*
+        uint64_t* d_acc = nullptr;  // [word] accepted messages
+        uint64_t* d_dg = nullptr;   // [W * 64] id digests + [W] word digests (k_mc_summary)
+        std::vector<uint64_t> ids;
+        int refs = 0;
+    };
+    uint32_t msg_serial = 0;
     // mcache (mcache.go): windows of cached gossipsub batches, front = history[0]
     struct McBatch {
         uint32_t topic = 0, n_msgs = 0, n_words = 0;
@@ -128,8 +143,17 @@ struct gsx_engine {
         uint64_t* d_dig = nullptr;   // [node] summary of the batch (k_mc_summary), in the same allocation
         uint32_t* d_cnt = nullptr;
         std::vector<uint64_t> ids;
+        MsgSet* set = nullptr;  // (unsharded engines)
     };
     std::deque<std::vector<McBatch>> mc;
+    // gossip exchange state (allocated when first enabled)
+    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gxflag = nullptr;
+    uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;
+    int64_t* d_prom_e = nullptr;
+    gsx::GxBatch* d_gx = nullptr;
+    uint32_t* d_gx_off = nullptr;
+    uint8_t* d_gx_got = nullptr;
+    size_t gx_cap = 0;
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
@@ -167,6 +191,7 @@ struct gsx_engine {
         uint32_t rows_valid = 1;  // frontier-history rows written (skipped empty hops write none)
         gsx_prop_config cfg{};
         std::vector<uint64_t> ids;
+        std::vector<uint32_t> vals;  // validation outcomes of this call
         // pending (deferred) credits: topic they belong to
         bool credit_pending = false;
         uint32_t credit_topic = 0;
@@ -352,9 +377,24 @@ void seen_pool_free(gsx_engine* e) {
     e->seen_pool.clear();
 }
 
+void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
+    if (!st || --st->refs > 0) return;
+    seen_release(e, st->d_all, st->all_words);
+    if (st->d_val) (void)hipFree(st->d_val);
+    if (st->d_acc) (void)hipFree(st->d_acc);
+    if (st->d_dg) (void)hipFree(st->d_dg);
+    delete st;
+}
+void batch_release(gsx_engine* e, gsx_engine::McBatch& b) {
+    seen_release(e, b.d_seen, b.seen_words);
+    set_release(e, b.set);
+    b.d_seen = nullptr;
+    b.set = nullptr;
+}
+
 void mcache_clear(gsx_engine* e) {
     for (auto& w : e->mc)
-        for (auto& b : w) seen_release(e, b.d_seen, b.seen_words);
+        for (auto& b : w) batch_release(e, b);
     e->mc.clear();
     e->mc.emplace_back();  // history[0], empty
 }
@@ -415,6 +455,19 @@ void free_state(gsx_engine* e) {
     e->d_long = e->d_nlong = nullptr;
     e->d_hbstats = nullptr;
     e->d_tr_acc = e->d_tr_hp = nullptr;
+    {
+        void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
+                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got};
+        for (void* x : gxp)
+            if (x) (void)hipFree(x);
+        e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = nullptr;
+        e->d_prom_h = e->d_ihave_bits = nullptr;
+        e->d_prom_e = nullptr;
+        e->d_gx = nullptr;
+        e->d_gx_off = nullptr;
+        e->d_gx_got = nullptr;
+        e->gx_cap = 0;
+    }
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_tcnt = nullptr;
@@ -1626,7 +1679,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     P.launches = 0;
     P.loop_timing = false;
     P.ids.resize(m);
-    for (size_t k = 0; k < m; ++k) P.ids[k] = msgs[k].msg_id;
+    P.vals.resize(m);
+    for (size_t k = 0; k < m; ++k) {
+        P.ids[k] = msgs[k].msg_id;
+        P.vals[k] = msgs[k].validation;
+    }
     P.active = true;
     HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
     if (m == 0) return GSX_OK;
@@ -1755,6 +1812,31 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         }
     }
     const uint32_t W = ps.n_words;
+    gsx_engine::MsgSet* set = nullptr;
+    if (P.cfg.router == GSX_ROUTER_GOSSIPSUB && !ps.sharded) {  // the call's seen rows, before the uncache
+        const size_t N = ps.n_nodes;
+        set = new gsx_engine::MsgSet;
+        set->serial = ++e->msg_serial;
+        set->n_msgs = ps.n_msgs;
+        set->n_words = W;
+        set->topic = P.cfg.topic;
+        set->ids = P.ids;
+        set->refs = 1;
+        set->all_words = (size_t)W * N;
+        set->d_all = seen_acquire(e, set->all_words);
+        if (!set->d_all) {
+            delete set;
+            return fail(e, GSX_ENOMEM, "seen rows of the message set");
+        }
+        HIPCHK(e, hipMemcpyAsync(set->d_all, P.seen, 8 * set->all_words, hipMemcpyDeviceToDevice, e->stream));
+        std::vector<uint64_t> acc(W, 0);
+        for (size_t k = 0; k < P.vals.size(); ++k)
+            if (P.vals[k] == GSX_VALIDATION_ACCEPT) acc[k / 64] |= 1ull << (k % 64);
+        if (int rc = dalloc(e, &set->d_val, std::max<size_t>(P.vals.size(), 1))) return rc;
+        if (int rc = dalloc(e, &set->d_acc, std::max<size_t>(W, 1))) return rc;
+        HIPCHK(e, hipMemcpy(set->d_val, P.vals.data(), 4 * P.vals.size(), hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice));
+    }
     if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
         gsx_engine::McBatch b;
@@ -1778,6 +1860,10 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
                 P.dig_cap = dg.size();
             }
             HIPCHK(e, hipMemcpyAsync(P.d_dig, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
+            if (set) {
+                if (int rc = dalloc(e, &set->d_dg, dg.size())) return rc;
+                HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
+            }
             b.d_dig = P.seen + (size_t)W * N;
             b.d_cnt = reinterpret_cast<uint32_t*>(P.seen + (size_t)W * N + N);
             HIPCHK(e, gsx::launch_mc_summary(P.seen, (uint32_t)N, W, ps.n_msgs, P.d_dig, P.d_dig + (size_t)W * 64,
@@ -1786,6 +1872,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         }
         P.seen = nullptr;
         b.ids = P.ids;
+        b.set = set;
         if (e->mc.empty()) e->mc.emplace_back();
         e->mc.front().push_back(std::move(b));
     }
@@ -2069,6 +2156,10 @@ int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
     p->history_gossip = 5;
     p->max_ihave_length = 5000;
     p->gossip_factor = 0.25;
+    p->max_ihave_messages = 10;
+    p->gossip_retransmission = 3;
+    p->iwant_followup_ns = 3LL * 1000000000LL;
+    p->gossip_exchange = 0;
     return GSX_OK;
 }
 
@@ -2084,6 +2175,8 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
         p->d_lazy < 0 || p->max_ihave_length < 0 || !(p->gossip_factor >= 0))
         return fail(e, GSX_EINVAL, "need 0 <= HistoryGossip <= HistoryLength, HistoryLength >= 1, Dlazy, "
                                    "MaxIHaveLength, GossipFactor >= 0");
+    if (p->gossip_exchange && (p->max_ihave_messages < 0 || p->gossip_retransmission < 0 || p->iwant_followup_ns < 0))
+        return fail(e, GSX_EINVAL, "need MaxIHaveMessages, GossipRetransmission, IWantFollowupTime >= 0");
     e->gp = *p;
     return GSX_OK;
 }
@@ -2126,8 +2219,41 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         e->gossip_prev.assign(e->T, 0);
         e->hb_clean = false;
     }
+    const bool gx_on = e->gp.gossip_exchange != 0;
+    if (gx_on && e->sharded()) return fail(e, GSX_ESTATE, "the gossip exchange runs on unsharded engines only");
+    if (gx_on && !e->d_prom_e) {
+        int rc = 0;
+        const size_t E = std::max<size_t>(e->E, 1);
+        if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
+            (rc = dalloc(e, &e->d_prom_h, E * gsx::GX_PROMISE_SLOTS)) ||
+            (rc = dalloc(e, &e->d_prom_e, E * gsx::GX_PROMISE_SLOTS)) || (rc = dalloc(e, &e->d_ihave_bits, E)) ||
+            (rc = dalloc(e, &e->d_gxflag, 4)))
+            return rc;
+        HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * gsx::GX_PROMISE_SLOTS, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
+    uint8_t* pen_mask = nullptr;
+    if (e->d_prom_e) {
+        // clearIHaveCounters (:1566-1576); applyIwantPenalties (:1578-1583):
+        // promises expired before now are broken, AddPenalty (P7) on their pairs
+        const size_t E = std::max<size_t>(e->E, 1);
+        HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
+        pen_mask = e->d_dirty + 3 * e->E;
+        HIPCHK(e, hipMemsetAsync(pen_mask, 0, E, e->stream));
+        gsx::HbState hp{};
+        hp.n_pairs = e->E;
+        hp.now = now;
+        hp.prom_h = e->d_prom_h;
+        hp.prom_e = e->d_prom_e;
+        hp.stats = e->d_hbstats;
+        hp.dirty = pen_mask;
+        HIPCHK(e, gsx::launch_gx_promises(dev_state(e), hp, e->stream));
+    }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
+    if (pen_mask) HIPCHK(e, gsx::launch_score_subset(dev_state(e), kern_params(e), pen_mask, e->stream));
     gsx::HbState h{};
     h.row_ptr = e->d_row_ptr;
     h.rev = e->d_rev;
@@ -2186,10 +2312,24 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                 e->gp.graft_flood_threshold_ns,
                                 e->gp.d_lazy,
                                 e->gp.max_ihave_length,
-                                e->gp.gossip_factor};
+                                e->gp.gossip_factor,
+                                e->gp.max_ihave_messages,
+                                e->gp.gossip_retransmission,
+                                e->gp.iwant_followup_ns};
     const gsx::DevState ds = dev_state(e);
-    HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
+    if (gx_on) {
+        h.ihave_bits = e->d_ihave_bits;
+        h.ihave_trunc = e->d_gxflag;
+        h.col = e->d_col;
+        h.peerhave = e->d_peerhave;
+        h.iasked = e->d_iasked;
+        h.gx_req = e->d_gxreq;
+        h.prom_h = e->d_prom_h;
+        h.prom_e = e->d_prom_e;
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 16, e->stream));
+    }
     const size_t E8 = 8 * (e->E ? e->E : 1);
     // Unsharded, (B) and (C) clear the control words, answers and marks they
     // read, and nothing else is ever set: after one cleared round they stay
@@ -2313,18 +2453,106 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
     HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
+    const size_t hist = (size_t)std::max(e->gp.history_length, 1);
+    // (D) the gossip exchange over the batches the IHAVEs advertised (the
+    // windows of hb_begin's list), answered across the Shift below
+    std::vector<gsx_engine::MsgSet*> gx_sets;
+    std::vector<uint64_t*> gx_x;
+    const bool gx_run = e->gp.gossip_exchange && h.ihave_bits && e->have_gossip;
+    if (gx_run) {
+        std::vector<gsx::GxBatch> gx;
+        std::vector<uint32_t> off(e->T + 1, 0);
+        const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
+        const size_t N = e->n_nodes;
+        for (uint32_t t = 0; t < e->T; ++t) {
+            off[t] = (uint32_t)gx.size();
+            for (size_t w = 0; w < n_win; ++w)
+                for (auto& b : e->mc[w]) {
+                    if (b.topic != t || !b.set) continue;
+                    size_t i = 0;
+                    while (i < gx_sets.size() && gx_sets[i] != b.set) ++i;
+                    if (i == gx_sets.size()) {
+                        const size_t words = (size_t)b.set->n_words * N + 2 * N;  // rows + (dig, cnt) tail
+                        uint64_t* x = seen_acquire(e, words);
+                        if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
+                        HIPCHK(e, hipMemsetAsync(x, 0, 8 * (size_t)b.set->n_words * N, e->stream));
+                        gx_sets.push_back(b.set);
+                        gx_x.push_back(x);
+                    }
+                    gx.push_back(gsx::GxBatch{b.d_seen, b.set->d_all, gx_x[i], b.set->d_val, nullptr, b.n_words,
+                                              b.set->serial, t, (uint32_t)(e->mc.size() < hist || w + 1 < hist)});
+                    gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
+                }
+        }
+        off[e->T] = (uint32_t)gx.size();
+        if (gx.size() > e->gx_cap || !e->d_gx) {
+            if (e->d_gx) (void)hipFree(e->d_gx);
+            if (e->d_gx_off) (void)hipFree(e->d_gx_off);
+            if (e->d_gx_got) (void)hipFree(e->d_gx_got);
+            e->d_gx = nullptr;
+            e->d_gx_off = nullptr;
+            e->d_gx_got = nullptr;
+            e->gx_cap = std::max<size_t>(gx.size(), 16);
+            if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
+            if (int rc = dalloc(e, &e->d_gx_off, (size_t)GSX_MAX_TOPICS + 1)) return rc;
+            if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
+        }
+        for (auto& g : gx) g.got = e->d_gx_got + reinterpret_cast<size_t>(g.got);
+        HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
+        HIPCHK(e, hipMemcpy(e->d_gx, gx.data(), sizeof(gsx::GxBatch) * gx.size(), hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_gx_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice));
+        h.gx = e->d_gx;
+        h.gx_off = e->d_gx_off;
+        HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
+        for (size_t i = 0; i < gx_sets.size(); ++i)
+            HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
+                                           e->stream));
+        e->scores_valid = false;  // the receipts credited P2 / P3 / P4
+        ++e->score_gen;
+    }
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    uint32_t gflag[4] = {0, 0, 0, 0};
+    std::vector<uint8_t> got(gx_sets.size(), 0);
+    if (gx_run) {
+        HIPCHK(e, hipMemcpyAsync(gflag, e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
+        if (!got.empty())
+            HIPCHK(e, hipMemcpyAsync(got.data(), e->d_gx_got, got.size(), hipMemcpyDeviceToHost, e->stream));
+    }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
     // mcache.Shift (mcache.go:94-104, gossipsub.go:1563), after the stream drained
-    const size_t hist = (size_t)std::max(e->gp.history_length, 1);
     while (e->mc.size() >= hist) {
-        for (auto& b : e->mc.back()) seen_release(e, b.d_seen, b.seen_words);
+        for (auto& b : e->mc.back()) batch_release(e, b);
         e->mc.pop_back();
     }
     e->mc.emplace_front();
+    // the recovered copies: one batch per message set, Put into the new window 0
+    const size_t N = e->n_nodes;
+    for (size_t i = 0; i < gx_sets.size(); ++i) {
+        gsx_engine::MsgSet* ms = gx_sets[i];
+        if (!got[i]) {
+            seen_release(e, gx_x[i], (size_t)ms->n_words * N + 2 * N);
+            continue;
+        }
+        gsx_engine::McBatch b;
+        b.topic = ms->topic;
+        b.n_msgs = ms->n_msgs;
+        b.n_words = ms->n_words;
+        b.d_seen = gx_x[i];
+        b.seen_words = (size_t)ms->n_words * N + 2 * N;
+        b.d_dig = gx_x[i] + (size_t)ms->n_words * N;
+        b.d_cnt = reinterpret_cast<uint32_t*>(gx_x[i] + (size_t)ms->n_words * N + N);
+        b.ids = ms->ids;
+        b.set = ms;
+        ++ms->refs;
+        HIPCHK(e, gsx::launch_mc_summary(b.d_seen, (uint32_t)N, ms->n_words, ms->n_msgs, ms->d_dg,
+                                         ms->d_dg + (size_t)ms->n_words * 64, b.d_dig, b.d_cnt, e->stream));
+        e->mc.front().push_back(std::move(b));
+    }
+    if (gflag[0] == 1) return fail(e, GSX_ERANGE, "gossip exchange: an IHAVE list was longer than MaxIHaveLength");
+    if (gflag[0] == 2) return fail(e, GSX_ERANGE, "gossip exchange: more than 8 promises outstanding on a pair");
     return GSX_OK;
 }
 

@@ -1,0 +1,283 @@
+// The gossip exchange of a heartbeat (include/gsx.h step (D)): IHAVE handling,
+// IWANT answers and their receipt (gossipsub.go:615-716), and the promise
+// tracking behind the P7 penalty (gossip_tracer.go:48-153, gossipsub.go:1578-1583).
+//
+// One lane per receiving node u walks its pairs q = (u -> v) twice:
+//  pass 1: handleIHave for the one IHAVE RPC v sent (every topic): the score
+//          / MaxIHaveMessages / iasked gates, the ids v advertised that u has
+//          not seen (u's seen rows as the exchange started), the asked subset
+//          and the one promise (serial << 32 | message index of the element at
+//          Int31n(asked) in canonical order);
+//  pass 2: v answers (its score of u, its cache after the Shift) and u
+//          receives the answer: a first receipt (not in u's receipts of this
+//          exchange) is delivered or rejected, fulfils u's promises for it and
+//          is recorded in the set's receipt rows; a further copy is a duplicate.
+// Canonical order: topics ascending, then the advertised batches in cache
+// order (windows newest first, Put order), then message index.  Every
+// per-pair state (peerhave, iasked, promises, records of q) belongs to u's lane.
+#include "gsx_device.h"
+#include "gsx_ops.h"
+
+namespace gsx {
+
+constexpr uint32_t VAL_ACCEPT = 0, VAL_REJECT = 1;  // GSX_VALIDATION_ACCEPT / _REJECT (gsx.h)
+
+namespace {
+
+__device__ __forceinline__ void gx_flush(unsigned long long* stats, int k, uint64_t c) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x % 64) == 0 && c) atomicAdd(&stats[k], (unsigned long long)c);
+}
+
+// Streams the ids v advertised on the topics of `tb` that u had not seen:
+// f(batch index, message index) for each, in canonical order; returns false
+// when f asks to stop.
+template <typename F>
+__device__ __forceinline__ bool gx_walk(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, F&& f) {
+    for (; tb; tb &= tb - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
+            const GxBatch& b = h.gx[g];
+            const uint32_t W = b.n_words;
+            for (uint32_t w = 0; w < W; ++w) {
+                uint64_t m = b.mem[(size_t)v * W + w] & ~b.all[(size_t)u * W + w];
+                for (; m; m &= m - 1)
+                    if (!f(g, w * 64 + (uint32_t)__builtin_ctzll(m))) return false;
+            }
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint64_t gx_topics(const HbState& h, uint32_t r) { return h.ihave_bits[r]; }
+
+}  // namespace
+
+// applyIwantPenalties at the heartbeat start: a promise whose expiry is
+// before now is broken, AddPenalty(peer, count) (GetBrokenPromises :79-115).
+__global__ __launch_bounds__(256) void k_gx_promises(DevState s, HbState h) {
+    uint64_t broken = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        int64_t e[GX_PROMISE_SLOTS];
+#pragma unroll
+        for (int k = 0; k < GX_PROMISE_SLOTS; ++k) e[k] = h.prom_e[q * GX_PROMISE_SLOTS + k];
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < GX_PROMISE_SLOTS; ++k)
+            if (e[k] != 0 && e[k] < h.now) {
+                h.prom_e[q * GX_PROMISE_SLOTS + k] = 0;
+                ++c;
+            }
+        if (c) {
+            ev_penalty(s, q, c);
+            broken += (uint64_t)c;
+            h.dirty[q] = 1;  // re-scored before the heartbeat reads it
+        }
+    }
+    unsigned long long v[1] = {broken};
+    const uint32_t slot[1] = {HB_BROKEN_PROMISES};
+    block_count<1>(v, h.stats, slot);
+}
+
+__global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
+    if (*h.ihave_trunc) return;  // truncated IHAVE lists are not exchanged (the host reports GSX_ERANGE)
+    const DevGossipParams& gp = h.gp;
+    uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0, served = 0, delivered = 0, rejected = 0, dups = 0;
+    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        // ---- pass 1: handleIHave (:615-679), senders ascending
+        for (int64_t q = r0; q < r1; ++q) {
+            const uint32_t r = h.rev[q];
+            if (r == NO_PAIR || (r & HALO)) continue;
+            const uint64_t tb = gx_topics(h, r);
+            if (!tb) continue;
+            if (s.score[q] < h.gossip_threshold) {  // :617-621
+                ++ignored;
+                continue;
+            }
+            const uint32_t ph = h.peerhave[q] + 1;  // :624-628
+            h.peerhave[q] = ph;
+            if ((int64_t)ph > (int64_t)gp.max_ihave_msgs) {
+                ++ignored;
+                continue;
+            }
+            const uint32_t ia = h.iasked[q];
+            if ((int64_t)ia >= (int64_t)gp.max_ihave) {  // :630-633
+                ++ignored;
+                continue;
+            }
+            const uint32_t v = (uint32_t)h.col[q];
+            uint32_t n = 0;
+            gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+                ++n;
+                return true;
+            });
+            if (n == 0) continue;  // :652-654
+            const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)ia);
+            const uint32_t kk = n < budget ? n : budget;
+            Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+            // the asked subset: all, or a uniform kk-subset by selection sampling;
+            // then AddPromise's pick (gossip_tracer.go:53)
+            uint32_t pick_g = 0, pick_k = 0;
+            if (kk == n) {
+                const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
+                uint32_t i = 0;
+                gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+                    if (i++ < j) return true;
+                    pick_g = gi;
+                    pick_k = k;
+                    return false;
+                });
+            } else {
+                uint32_t i = 0, sel = 0;
+                gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+                    if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
+                    ++i;
+                    return sel < kk;
+                });
+                const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
+                Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
+                i = 0;
+                sel = 0;
+                gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+                    const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
+                    ++i;
+                    if (!take) return true;
+                    if (sel++ < j) return true;
+                    pick_g = gi;
+                    pick_k = k;
+                    return false;
+                });
+            }
+            h.iasked[q] = ia + kk;
+            h.gx_req[q] = kk;
+            ++iw_msgs;
+            iw_ids += kk;
+            // AddPromise (:59-74): once per (message, peer)
+            const uint64_t handle = ((uint64_t)h.gx[pick_g].serial << 32) | pick_k;
+            uint64_t* ph_ = h.prom_h + (size_t)q * GX_PROMISE_SLOTS;
+            int64_t* pe_ = h.prom_e + (size_t)q * GX_PROMISE_SLOTS;
+            int free_slot = -1;
+            bool have = false;
+            for (int k = 0; k < GX_PROMISE_SLOTS; ++k) {
+                if (pe_[k] == 0) {
+                    if (free_slot < 0) free_slot = k;
+                } else if (ph_[k] == handle) {
+                    have = true;
+                }
+            }
+            if (!have && free_slot >= 0) {
+                ph_[free_slot] = handle;
+                pe_[free_slot] = h.now + gp.followup_ns;
+            } else if (!have) {
+                *h.ihave_trunc = 2;  // promise table full: reported as an error by the host
+            }
+        }
+        // ---- pass 2: v answers (handleIWant :681-716), u receives, senders ascending
+        for (int64_t q = r0; q < r1; ++q) {
+            const uint32_t kk = h.gx_req[q];
+            if (!kk) continue;
+            h.gx_req[q] = 0;
+            const uint32_t r = h.rev[q];
+            if (s.score[r] < h.gossip_threshold) continue;  // v ignores u's IWANT
+            if (!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) continue;  // AcceptFrom at u
+            const uint32_t v = (uint32_t)h.col[q];
+            const uint64_t tb = gx_topics(h, r);
+            uint32_t n = 0;  // |iwant| again (the selection depends on it)
+            gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+                ++n;
+                return true;
+            });
+            Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+            uint32_t i = 0, sel = 0;
+            gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+                bool take = true;
+                if (kk < n) {
+                    take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
+                    ++i;
+                    if (!take) return true;
+                }
+                ++sel;
+                const GxBatch& b = h.gx[gi];
+                // no longer in v's cache; or GetForPeer's count (1: every (peer,
+                // message) is asked at most once per answer it can receive) above
+                // GossipRetransmission
+                if (!b.avail || gp.retransmission < 1) return sel < kk || kk == n;
+                ++served;
+                const uint32_t W = b.n_words, t = b.topic, val = b.val[k];
+                uint64_t* xw = b.x + (size_t)u * W + k / 64;
+                const uint64_t bit = 1ull << (k % 64);
+                if (*xw & bit) {  // DuplicateMessage
+                    ++dups;
+                    if (val == VAL_ACCEPT) ev_mesh(s, (uint64_t)q, t);
+                    else if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+                } else {
+                    *xw |= bit;
+                    // fulfillPromise (:119-126): every promise of u for this message
+                    const uint64_t handle = ((uint64_t)b.serial << 32) | k;
+                    for (int64_t p = r0; p < r1; ++p)
+                        for (int z = 0; z < GX_PROMISE_SLOTS; ++z)
+                            if (h.prom_e[(size_t)p * GX_PROMISE_SLOTS + z] != 0 &&
+                                h.prom_h[(size_t)p * GX_PROMISE_SLOTS + z] == handle)
+                                h.prom_e[(size_t)p * GX_PROMISE_SLOTS + z] = 0;
+                    if (val == VAL_ACCEPT) {
+                        ++delivered;
+                        ev_first(s, (uint64_t)q, t);
+                        *b.got = 1;
+                    } else {
+                        ++rejected;
+                        if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+                    }
+                }
+                return sel < kk || kk == n;
+            });
+        }
+    }
+    gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);
+    gx_flush(h.stats, HB_IWANT_MSGS, iw_msgs);
+    gx_flush(h.stats, HB_IWANT_IDS, iw_ids);
+    gx_flush(h.stats, HB_IWANT_SERVED, served);
+    gx_flush(h.stats, HB_GOSSIP_DELIVERED, delivered);
+    gx_flush(h.stats, HB_GOSSIP_REJECTED, rejected);
+    gx_flush(h.stats, HB_GOSSIP_DUPLICATES, dups);
+}
+
+// The exchange's receipts into the message set: seen |= x; the receipt rows
+// keep only the accepted messages (they become the recovered copies' cache rows).
+__global__ __launch_bounds__(256) void k_gx_merge(uint64_t* __restrict__ all, uint64_t* __restrict__ x,
+                                                  const uint64_t* __restrict__ acc, uint64_t n, uint32_t W) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
+        const uint64_t v = x[i];
+        if (!v) continue;
+        all[i] |= v;
+        x[i] = v & acc[i % W];
+    }
+}
+
+static inline unsigned gx_blocks(uint64_t n, unsigned bs, unsigned cap) {
+    const uint64_t b = (n + bs - 1) / bs;
+    return (unsigned)(b < cap ? b : cap);
+}
+
+hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_promises, dim3(gx_blocks(h.n_pairs, 256, COUNTER_GRID)), dim3(256), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_exchange, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
+                           hipStream_t st) {
+    const uint64_t n = n_nodes * n_words;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_merge, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, all, x, acc, n, n_words);
+    return hipGetLastError();
+}
+
+}  // namespace gsx

@@ -960,6 +960,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                             const size_t x = tslot + rs[lane] + peers[q];
                             h.ihave_len[x] = L;
                             h.ihave_hash[x] = dig;
+                            if (h.ihave_bits) h.ihave_bits[rs[lane] + peers[q]] |= 1ull << t;  // (D) reads it
                         }
                         cnt[0] += (uint64_t)target;
                         cnt[1] += (uint64_t)target * L;
@@ -1079,6 +1080,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 const size_t x = tslot + r0 + peers[p];
                 h.ihave_len[x] = L;
                 h.ihave_hash[x] = d;
+                if (h.ihave_bits) h.ihave_bits[r0 + peers[p]] |= 1ull << t;
             }
             if (lane == 0) {
                 msgs += (uint64_t)target;
@@ -1094,6 +1096,10 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                     const size_t x = tslot + r0 + peers[p];
                     h.ihave_len[x] = maxl;
                     h.ihave_hash[x] = d;
+                    if (h.ihave_bits) {
+                        h.ihave_bits[r0 + peers[p]] |= 1ull << t;
+                        *h.ihave_trunc = 1;  // a truncated list: not exchanged
+                    }
                 }
             }
             if (lane == 0) {

@@ -281,6 +281,11 @@ class GossipSubParams(C.Structure):
         ("history_gossip", C.c_int32),
         ("max_ihave_length", C.c_int32),
         ("gossip_factor", C.c_double),
+        ("max_ihave_messages", C.c_int32),
+        ("gossip_retransmission", C.c_int32),
+        ("iwant_followup_ns", C.c_int64),
+        ("gossip_exchange", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -296,6 +301,14 @@ class HeartbeatOut(C.Structure):
         ("mesh_links", C.c_uint64),
         ("ihave_msgs", C.c_uint64),
         ("ihave_ids", C.c_uint64),
+        ("broken_promises", C.c_uint64),
+        ("ihave_ignored", C.c_uint64),
+        ("iwant_msgs", C.c_uint64),
+        ("iwant_ids", C.c_uint64),
+        ("iwant_served", C.c_uint64),
+        ("gossip_delivered", C.c_uint64),
+        ("gossip_rejected", C.c_uint64),
+        ("gossip_duplicates", C.c_uint64),
     ]
 
     def as_dict(self):

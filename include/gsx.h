@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSX_ABI_VERSION 3
+#define GSX_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define GSX_OK 0
@@ -520,6 +520,11 @@ typedef struct gsx_gossipsub_params {
     int32_t history_length, history_gossip; /* :38, :238 (HistoryGossip = 5!)   */
     int32_t max_ihave_length;               /* :56                               */
     double gossip_factor;                   /* :41                               */
+    int32_t max_ihave_messages;             /* :57                               */
+    int32_t gossip_retransmission;          /* :42                               */
+    int64_t iwant_followup_ns;              /* :58                               */
+    int32_t gossip_exchange;                /* 1: run step (D) below; 0: IHAVEs are only emitted */
+    int32_t reserved0;
 } gsx_gossipsub_params;
 
 int gsx_default_gossipsub_params(gsx_gossipsub_params* out);
@@ -537,7 +542,29 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      handlePrune, :718-843), senders in ascending order, with the scores of
  *      that moment: backoff / score / Dhi checks, P7 penalties for GRAFTs
  *      inside the backoff (:752-770), PRUNE answers;
- *  (C) the GRAFT senders handle those PRUNE answers.
+ *  (C) the GRAFT senders handle those PRUNE answers;
+ *  (D) (gossip_exchange) the IHAVEs of (A) are handled: every node, senders
+ *      ascending, runs handleIHave (:615-679) on the one IHAVE RPC it got from
+ *      each peer (all topics): score >= GossipThreshold, peerhave <=
+ *      MaxIHaveMessages, iasked < MaxIHaveLength, ids it has not seen; it
+ *      asks for min(|iwant|, MaxIHaveLength - iasked) of them (a uniform
+ *      subset, selection sampling with draws h(seed, 9, pair, tick << 32 | k)
+ *      over the canonical order topic / cache order / message index) and
+ *      tracks one promise (AddPromise, gossip_tracer.go:48-75: the element at
+ *      Int31n(asked) in canonical order, expiring IWantFollowupTime later);
+ *      the peer answers (handleIWant, :681-716) if the asker's score >=
+ *      GossipThreshold, with every asked message still in its cache after
+ *      this heartbeat's Shift (mcache.GetForPeer: the oldest advertised window
+ *      is gone when HistoryGossip == HistoryLength, the reference default);
+ *      the asker then receives them, senders ascending, ids in canonical
+ *      order: a first receipt is delivered (P2/P3 credit, or P4 when its
+ *      validation rejects it), fulfils the node's promises for it
+ *      (gossip_tracer.go:119-153) and is Put into its cache window 0 (after
+ *      the Shift); a further copy is a duplicate.  Recovered messages are not
+ *      forwarded further within the round.  At the start of every heartbeat
+ *      the IHAVE counters are cleared (:1566-1576) and promises that expired
+ *      before now are broken: AddPenalty(peer, count) (:1578-1583, P7).
+ *      Lists longer than MaxIHaveLength are not exchanged (GSX_ERANGE).
  * Randomness (shufflePeers, :1890-1895) is Go's Int31n rejection rule over
  * draws h(seed, 8, node, tick << 32 | topic << 24 | k); candidate lists are in
  * ascending peer order; the unstable sort.Slice of :1393 is a stable sort
@@ -567,6 +594,14 @@ typedef struct gsx_heartbeat_out {
     uint64_t mesh_links;      /* in-mesh (pair, topic) after the round             */
     uint64_t ihave_msgs;      /* IHAVE control messages emitted (emitGossip)       */
     uint64_t ihave_ids;       /* message ids advertised over all of them           */
+    uint64_t broken_promises; /* IWANT promises expired unfulfilled (AddPenalty)   */
+    uint64_t ihave_ignored;   /* IHAVE RPCs ignored: score / MaxIHaveMessages / iasked (D) */
+    uint64_t iwant_msgs;      /* IWANT requests sent (D)                           */
+    uint64_t iwant_ids;       /* message ids requested in them                     */
+    uint64_t iwant_served;    /* messages sent back by handleIWant (D)             */
+    uint64_t gossip_delivered;  /* first receipts of served messages, accepted (D) */
+    uint64_t gossip_rejected;   /* first receipts validation did not accept (D)    */
+    uint64_t gossip_duplicates; /* further copies of served messages (D)           */
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);

@@ -64,11 +64,25 @@ typedef struct {
 struct orc_engine;
 static int ipcount_init(struct orc_engine* o);
 
+/* The messages of one gsx_propagate call: validation outcome and, per
+ * (message, node), whether the node has seen it (first receipt or publish,
+ * and receipts through the gossip exchange); shared by the batch that cached
+ * them and by the batches of copies recovered later (reference counted). */
+typedef struct {
+    uint32_t serial, m, n, refs;
+    uint32_t* val;
+    uint8_t* seen;
+} orc_msgset;
 typedef struct {
     uint32_t topic, m, n;
     uint64_t* ids;
-    uint8_t* has;
+    uint8_t* has; /* [k * n + v]: in v's cache (mcache membership) */
+    orc_msgset* set;
 } orc_mc_batch;
+typedef struct {
+    uint64_t q, handle; /* the asker's pair (u -> v); message set serial << 32 | index */
+    int64_t expire;
+} orc_promise;
 typedef struct orc_mc_window {
     orc_mc_batch* b;
     size_t nb, cap;
@@ -91,6 +105,18 @@ struct orc_engine {
     /* the last heartbeat's tracer Graft / Prune calls, topic bits per pair
      * (gsx_hb_trace_words): sent GRAFT, sent PRUNE, accepted GRAFT, handled PRUNE */
     uint64_t *tr_sg, *tr_sp, *tr_ag, *tr_hp;
+    /* gossip exchange state: peerhave / iasked per pair (gossipsub.go:414-415),
+     * the promises of gossipTracer (gossip_tracer.go:24-27) and mcache.peertx
+     * (mcache.go:40) as (responder pair, handle) -> count */
+    uint32_t *peerhave, *iasked;
+    orc_promise* prom;
+    size_t n_prom, cap_prom;
+    uint64_t* ptx_key; /* (pair << 0) ^ handle mixed; open addressing */
+    uint64_t* ptx_pair;
+    uint32_t* ptx_cnt;
+    size_t ptx_cap, ptx_n;
+    uint32_t msg_serial;
+    bool ihave_trunc; /* the last heartbeat sent an IHAVE list longer than MaxIHaveLength */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -245,12 +271,20 @@ static void free_records(orc_engine* o) {
     o->n_alive = 0;
 }
 
+static void batch_free(orc_mc_batch* b) {
+    free(b->ids);
+    free(b->has);
+    if (b->set && --b->set->refs == 0) {
+        free(b->set->val);
+        free(b->set->seen);
+        free(b->set);
+    }
+    b->set = NULL;
+}
+
 int orc_mcache_clear(orc_engine* o) {
     for (uint32_t w = 0; w < o->mc_n; w++) {
-        for (size_t i = 0; i < o->mc[w].nb; i++) {
-            free(o->mc[w].b[i].ids);
-            free(o->mc[w].b[i].has);
-        }
+        for (size_t i = 0; i < o->mc[w].nb; i++) batch_free(&o->mc[w].b[i]);
         free(o->mc[w].b);
         memset(&o->mc[w], 0, sizeof(orc_mc_window));
     }
@@ -278,6 +312,12 @@ void orc_destroy(orc_engine* o) {
     free(o->tr_sp);
     free(o->tr_ag);
     free(o->tr_hp);
+    free(o->peerhave);
+    free(o->iasked);
+    free(o->prom);
+    free(o->ptx_key);
+    free(o->ptx_pair);
+    free(o->ptx_cnt);
     free(o->ipc.keys);
     free(o->ipc.vals);
     free_records(o);
@@ -328,6 +368,14 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     o->ihave_len = (uint32_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint32_t));
     o->ihave_hash = (uint64_t*)calloc((size_t)o->T * (E ? E : 1), sizeof(uint64_t));
     if (!o->ihave_len || !o->ihave_hash) return GSX_ENOMEM;
+    free(o->peerhave);
+    free(o->iasked);
+    o->peerhave = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
+    o->iasked = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
+    if (!o->peerhave || !o->iasked) return GSX_ENOMEM;
+    o->n_prom = 0;
+    o->ptx_n = 0;
+    if (o->ptx_key) memset(o->ptx_key, 0, sizeof(uint64_t) * o->ptx_cap);
     uint64_t** tw[4] = {&o->tr_sg, &o->tr_sp, &o->tr_ag, &o->tr_hp};
     for (int i = 0; i < 4; i++) {
         free(*tw[i]);
@@ -1127,8 +1175,16 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         mcb->m = (uint32_t)m;
         mcb->n = N;
         mcb->ids = (uint64_t*)malloc(sizeof(uint64_t) * m);
-        mcb->has = (uint8_t*)malloc(m * (size_t)(N ? N : 1));
+        mcb->has = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
         for (size_t k = 0; k < m; k++) mcb->ids[k] = msgs[k].msg_id;
+        mcb->set = (orc_msgset*)calloc(1, sizeof(orc_msgset));
+        mcb->set->serial = ++o->msg_serial;
+        mcb->set->m = (uint32_t)m;
+        mcb->set->n = N;
+        mcb->set->refs = 1;
+        mcb->set->val = (uint32_t*)malloc(sizeof(uint32_t) * m);
+        mcb->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
+        for (size_t k = 0; k < m; k++) mcb->set->val[k] = msgs[k].validation;
     }
     for (size_t k = 0; k < m; k++) {
         const uint32_t src = msgs[k].source;
@@ -1207,7 +1263,10 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         if (hop_out) memcpy(hop_out + k * (size_t)N, hop, N);
         if (from_out) memcpy(from_out + k * (size_t)N, from, sizeof(int32_t) * N);
         if (mcb) /* Publish Puts what a node processes: a dropped message only at its source */
-            for (uint32_t i = 0; i < N; i++) mcb->has[k * (size_t)N + i] = hop[i] != 0xFF && (!dropped || i == src);
+            for (uint32_t i = 0; i < N; i++) {
+                mcb->has[k * (size_t)N + i] = hop[i] != 0xFF && (!dropped || i == src);
+                mcb->set->seen[k * (size_t)N + i] = hop[i] != 0xFF;
+            }
     }
     free(hop);
     free(from);
@@ -1239,6 +1298,10 @@ int orc_default_gossipsub_params(gsx_gossipsub_params* p) { /* DefaultGossipSubP
     p->history_gossip = 5; /* HistoryGossip: GossipSubHistoryLength (:238) */
     p->max_ihave_length = 5000;
     p->gossip_factor = 0.25;
+    p->max_ihave_messages = 10;
+    p->gossip_retransmission = 3;
+    p->iwant_followup_ns = 3LL * 1000000000LL;
+    p->gossip_exchange = 0;
     return 0;
 }
 
@@ -1463,6 +1526,7 @@ static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t*
         if (L > (size_t)gp->max_ihave_length) {
             shuffle_ids(ids, L, g);
             len = (size_t)gp->max_ihave_length;
+            o->ihave_trunc = true;
         }
         const size_t x = (size_t)t * o->E + peers[i];
         o->ihave_len[x] = (uint32_t)len;
@@ -1478,10 +1542,7 @@ static void mcache_shift(orc_engine* o, uint32_t history) {
     if (history > ORC_MC_MAX) history = ORC_MC_MAX;
     while (o->mc_n >= history && o->mc_n > 0) { /* drop history[len-1] */
         orc_mc_window* w = &o->mc[o->mc_n - 1];
-        for (size_t i = 0; i < w->nb; i++) {
-            free(w->b[i].ids);
-            free(w->b[i].has);
-        }
+        for (size_t i = 0; i < w->nb; i++) batch_free(&w->b[i]);
         free(w->b);
         memset(w, 0, sizeof(*w));
         o->mc_n--;
@@ -1502,6 +1563,268 @@ static void handle_prune(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t
     out->prunes_handled++;
 }
 
+/* ---- (D) the gossip exchange: handleIHave / handleIWant (gossipsub.go:615-716)
+ * and the gossipTracer's promises (gossip_tracer.go:48-153) -------------- */
+
+static void add_promise(orc_engine* o, uint64_t q, uint64_t handle, int64_t expire) { /* AddPromise :59-74 */
+    for (size_t i = 0; i < o->n_prom; i++)
+        if (o->prom[i].q == q && o->prom[i].handle == handle) return;
+    if (o->n_prom == o->cap_prom) {
+        o->cap_prom = o->cap_prom ? 2 * o->cap_prom : 64;
+        o->prom = (orc_promise*)realloc(o->prom, sizeof(orc_promise) * o->cap_prom);
+    }
+    o->prom[o->n_prom].q = q;
+    o->prom[o->n_prom].handle = handle;
+    o->prom[o->n_prom].expire = expire;
+    o->n_prom++;
+}
+
+static void fulfill_promises(orc_engine* o, uint32_t u, uint64_t handle) { /* fulfillPromise :119-126 */
+    for (size_t i = 0; i < o->n_prom;) {
+        if (o->pair_obs[o->prom[i].q] == u && o->prom[i].handle == handle) o->prom[i] = o->prom[--o->n_prom];
+        else i++;
+    }
+}
+
+/* mcache.GetForPeer's per-(message, peer) count (mcache.go:66-80), keyed by
+ * the responder's pair and the message handle */
+static uint32_t peertx_inc(orc_engine* o, uint64_t r, uint64_t handle) {
+    if (2 * (o->ptx_n + 1) > o->ptx_cap) {
+        size_t oc = o->ptx_cap, nc = oc ? 2 * oc : 1024;
+        uint64_t *ok = o->ptx_key, *op = o->ptx_pair;
+        uint32_t* ocn = o->ptx_cnt;
+        o->ptx_key = (uint64_t*)calloc(nc, 8);
+        o->ptx_pair = (uint64_t*)calloc(nc, 8);
+        o->ptx_cnt = (uint32_t*)calloc(nc, 4);
+        o->ptx_cap = nc;
+        o->ptx_n = 0;
+        for (size_t i = 0; i < oc; i++)
+            if (ocn && ocn[i]) {
+                size_t j = mix64(op[i] * 0x9E3779B97F4A7C15ULL ^ ok[i]) & (nc - 1);
+                while (o->ptx_cnt[j]) j = (j + 1) & (nc - 1);
+                o->ptx_key[j] = ok[i];
+                o->ptx_pair[j] = op[i];
+                o->ptx_cnt[j] = ocn[i];
+                o->ptx_n++;
+            }
+        free(ok);
+        free(op);
+        free(ocn);
+    }
+    size_t j = mix64(r * 0x9E3779B97F4A7C15ULL ^ handle) & (o->ptx_cap - 1);
+    while (o->ptx_cnt[j] && !(o->ptx_pair[j] == r && o->ptx_key[j] == handle)) j = (j + 1) & (o->ptx_cap - 1);
+    if (!o->ptx_cnt[j]) {
+        o->ptx_pair[j] = r;
+        o->ptx_key[j] = handle;
+        o->ptx_n++;
+    }
+    return ++o->ptx_cnt[j];
+}
+
+typedef struct {
+    orc_mc_batch* b;
+    bool avail; /* still in the cache after this heartbeat's Shift */
+} gx_batch;
+typedef struct {
+    uint32_t gb, k; /* gossip batch index, message index */
+} gx_item;
+typedef struct {
+    uint64_t q;
+    size_t i0, n; /* selected items[i0 .. i0 + n) */
+    bool served;
+} gx_req;
+
+static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now,
+                           uint64_t seed, gsx_heartbeat_out* out, orc_mc_batch** rec_out, size_t* n_rec) {
+    const uint64_t E = o->E;
+    const uint32_t T = o->T, N = o->n_nodes;
+    uint32_t history = (uint32_t)(gp->history_length > 0 ? gp->history_length : 0);
+    if (history > ORC_MC_MAX) history = ORC_MC_MAX;
+    const uint32_t nw = (uint32_t)gp->history_gossip < o->mc_n ? (uint32_t)gp->history_gossip : o->mc_n;
+    /* the advertised batches per topic (GetGossipIDs order: windows newest first, Put order) */
+    size_t nb = 0;
+    for (uint32_t w = 0; w < nw; w++) nb += o->mc[w].nb;
+    gx_batch* gb = (gx_batch*)malloc(sizeof(gx_batch) * (nb ? nb : 1));
+    nb = 0;
+    for (uint32_t w = 0; w < nw; w++)
+        for (size_t i = 0; i < o->mc[w].nb; i++) {
+            gb[nb].b = &o->mc[w].b[i];
+            gb[nb].avail = o->mc_n < history || w + 1 < history;
+            nb++;
+        }
+    double* score0 = (double*)malloc(sizeof(double) * (E ? E : 1));
+    for (uint64_t r = 0; r < E; r++) score0[r] = score_pair(o, r);
+    size_t cap_it = 1024, n_it = 0, cap_rq = 256, n_rq = 0, cap_w = 1024;
+    gx_item* items = (gx_item*)malloc(sizeof(gx_item) * cap_it);
+    gx_req* reqs = (gx_req*)malloc(sizeof(gx_req) * cap_rq);
+    gx_item* W = (gx_item*)malloc(sizeof(gx_item) * cap_w);
+    int rc = o->ihave_trunc ? GSX_ERANGE : 0; /* truncated lists are not exchanged (gsx.h) */
+    /* handleIHave at every node u, one IHAVE RPC per sending peer v, senders ascending */
+    for (uint32_t u = 0; u < N && !rc; u++)
+        for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) {
+            const int64_t r = reverse_pair(o, (uint64_t)q); /* r = (v -> u) carried the IHAVEs */
+            if (r < 0) continue;
+            uint64_t tb = 0;
+            for (uint32_t t = 0; t < T; t++)
+                if (o->ihave_len[(size_t)t * E + r]) tb |= 1ull << t;
+            if (!tb) continue;
+            const uint32_t v = (uint32_t)o->col[q];
+            size_t n = 0;
+            for (uint32_t t = 0; t < T; t++) {
+                if (!(tb >> t & 1)) continue;
+                for (size_t i = 0; i < nb; i++) {
+                    const orc_mc_batch* b = gb[i].b;
+                    if (b->topic != t) continue;
+                    for (uint32_t k = 0; k < b->m; k++) {
+                        if (!b->has[(size_t)k * b->n + v]) continue;
+                        if (b->set->seen[(size_t)k * N + u]) continue; /* seenMessage (:645) */
+                        if (n == cap_w) {
+                            cap_w *= 2;
+                            W = (gx_item*)realloc(W, sizeof(gx_item) * cap_w);
+                        }
+                        W[n].gb = (uint32_t)i;
+                        W[n].k = k;
+                        n++;
+                    }
+                }
+            }
+            if (score0[q] < o->th.gossip_threshold) { /* :617-621 */
+                out->ihave_ignored++;
+                continue;
+            }
+            if (++o->peerhave[q] > (uint32_t)(gp->max_ihave_messages > 0 ? gp->max_ihave_messages : 0)) { /* :624-628 */
+                out->ihave_ignored++;
+                continue;
+            }
+            if ((int64_t)o->iasked[q] >= (int64_t)gp->max_ihave_length) { /* :630-633 */
+                out->ihave_ignored++;
+                continue;
+            }
+            if (n == 0) continue; /* :652-654 */
+            size_t kk = n;
+            const size_t budget = (size_t)((int64_t)gp->max_ihave_length - (int64_t)o->iasked[q]);
+            if (kk > budget) kk = budget;
+            orc_rng g = {seed, 9, (uint64_t)q, tick << 32, 0};
+            if (n_it + kk > cap_it) {
+                while (n_it + kk > cap_it) cap_it *= 2;
+                items = (gx_item*)realloc(items, sizeof(gx_item) * cap_it);
+            }
+            const size_t i0 = n_it;
+            if (kk == n) {
+                memcpy(items + n_it, W, sizeof(gx_item) * n);
+                n_it += n;
+            } else { /* a uniform kk-subset of W in canonical order (selection sampling) */
+                size_t sel = 0;
+                for (size_t i = 0; i < n && sel < kk; i++)
+                    if ((size_t)rng_int31n(&g, (int32_t)(n - i)) < kk - sel) {
+                        items[n_it++] = W[i];
+                        sel++;
+                    }
+            }
+            o->iasked[q] += (uint32_t)kk;
+            const gx_item* pm = &items[i0 + (size_t)rng_int31n(&g, (int32_t)kk)]; /* AddPromise's pick (:53) */
+            add_promise(o, (uint64_t)q, ((uint64_t)gb[pm->gb].b->set->serial << 32) | pm->k,
+                        now + gp->iwant_followup_ns);
+            out->iwant_msgs++;
+            out->iwant_ids += kk;
+            if (n_rq == cap_rq) {
+                cap_rq *= 2;
+                reqs = (gx_req*)realloc(reqs, sizeof(gx_req) * cap_rq);
+            }
+            reqs[n_rq].q = (uint64_t)q;
+            reqs[n_rq].i0 = i0;
+            reqs[n_rq].n = kk;
+            reqs[n_rq].served = false;
+            n_rq++;
+        }
+    /* handleIWant at each asked peer v (:681-716): the asker's score, the cache, GetForPeer's count */
+    for (size_t i = 0; i < n_rq && !rc; i++) {
+        const int64_t r = reverse_pair(o, reqs[i].q);
+        if (score0[r] < o->th.gossip_threshold) continue;
+        reqs[i].served = true;
+        for (size_t j = reqs[i].i0; j < reqs[i].i0 + reqs[i].n; j++) {
+            const gx_batch* x = &gb[items[j].gb];
+            const uint64_t handle = ((uint64_t)x->b->set->serial << 32) | items[j].k;
+            if (!x->avail || peertx_inc(o, (uint64_t)r, handle) > (uint32_t)gp->gossip_retransmission) {
+                items[j].gb = UINT32_MAX; /* not sent */
+                continue;
+            }
+            out->iwant_served++;
+        }
+    }
+    /* the askers receive the answers, senders ascending, ids in canonical order */
+    orc_msgset** rs = NULL;
+    uint8_t** rh = NULL;
+    uint32_t* rt = NULL;
+    size_t nr = 0;
+    for (size_t i = 0; i < n_rq && !rc; i++) {
+        if (!reqs[i].served) continue;
+        const uint64_t q = reqs[i].q;
+        const uint32_t u = o->pair_obs[q];
+        if (!(o->eflags[q] & GSX_EDGE_DIRECT) && score0[q] < o->th.graylist_threshold) continue; /* AcceptFrom */
+        for (size_t j = reqs[i].i0; j < reqs[i].i0 + reqs[i].n; j++) {
+            if (items[j].gb == UINT32_MAX) continue;
+            const orc_mc_batch* b = gb[items[j].gb].b;
+            orc_msgset* st = b->set;
+            const uint32_t k = items[j].k, t = b->topic, val = st->val[k];
+            uint8_t* sn = &st->seen[(size_t)k * N + u];
+            if (*sn) { /* DuplicateMessage */
+                out->gossip_duplicates++;
+                if (val == GSX_VALIDATION_ACCEPT) mark_duplicate(o, q, t, true, now, now);
+                else if (val == GSX_VALIDATION_REJECT) mark_invalid(o, q, t);
+                continue;
+            }
+            *sn = 1;
+            fulfill_promises(o, u, ((uint64_t)st->serial << 32) | k); /* Validate / Deliver / Reject */
+            if (val == GSX_VALIDATION_ACCEPT) {
+                out->gossip_delivered++;
+                mark_first(o, q, t);
+                size_t x = 0;
+                while (x < nr && rs[x] != st) x++;
+                if (x == nr) {
+                    rs = (orc_msgset**)realloc(rs, sizeof(*rs) * (nr + 1));
+                    rh = (uint8_t**)realloc(rh, sizeof(*rh) * (nr + 1));
+                    rt = (uint32_t*)realloc(rt, sizeof(*rt) * (nr + 1));
+                    rs[nr] = st;
+                    rh[nr] = (uint8_t*)calloc((size_t)st->m * N, 1);
+                    rt[nr] = t;
+                    nr++;
+                }
+                rh[x][(size_t)k * N + u] = 1; /* Put into u's cache */
+            } else {
+                out->gossip_rejected++;
+                if (val == GSX_VALIDATION_REJECT) mark_invalid(o, q, t);
+            }
+        }
+    }
+    /* the recovered copies: one batch per message set, Put after the Shift */
+    *rec_out = (orc_mc_batch*)calloc(nr ? nr : 1, sizeof(orc_mc_batch));
+    *n_rec = nr;
+    for (size_t x = 0; x < nr; x++) {
+        orc_mc_batch* rb = &(*rec_out)[x];
+        const orc_mc_batch* src = NULL;
+        for (size_t i = 0; i < nb && !src; i++)
+            if (gb[i].b->set == rs[x]) src = gb[i].b;
+        rb->topic = rt[x];
+        rb->m = rs[x]->m;
+        rb->n = N;
+        rb->ids = (uint64_t*)malloc(sizeof(uint64_t) * rb->m);
+        memcpy(rb->ids, src->ids, sizeof(uint64_t) * rb->m);
+        rb->has = rh[x];
+        rb->set = rs[x];
+        rs[x]->refs++;
+    }
+    free(rs);
+    free(rh);
+    free(rt);
+    free(gb);
+    free(score0);
+    free(items);
+    free(reqs);
+    free(W);
+    return rc;
+}
+
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now, uint64_t seed,
                   gsx_heartbeat_out* out) {
     memset(out, 0, sizeof(*out));
@@ -1514,6 +1837,26 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
                 o->backoff[i] = 0;
                 out->backoff_cleared++;
             }
+    /* clearIHaveCounters (:1566-1576), applyIwantPenalties (:1578-1583): a
+     * promise whose expiry is before now is broken (GetBrokenPromises, :79-115) */
+    o->ihave_trunc = false;
+    memset(o->peerhave, 0, sizeof(uint32_t) * (E ? E : 1));
+    memset(o->iasked, 0, sizeof(uint32_t) * (E ? E : 1));
+    if (o->n_prom) {
+        uint32_t* cnt = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
+        for (size_t i = 0; i < o->n_prom;) {
+            if (o->prom[i].expire < now) {
+                cnt[o->prom[i].q]++;
+                out->broken_promises++;
+                o->prom[i] = o->prom[--o->n_prom];
+            } else {
+                i++;
+            }
+        }
+        for (uint64_t q = 0; q < E; q++) /* AddPenalty(p, count): one addition of the count */
+            if (cnt[q]) add_penalty(o, q, cnt[q]);
+        free(cnt);
+    }
     double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
     uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
     memset(o->tr_sg, 0, 8 * (E ? E : 1));
@@ -1606,13 +1949,30 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
         }
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
+    /* (D) the IHAVEs just emitted are answered across the Shift */
+    orc_mc_batch* rec = NULL;
+    size_t n_rec = 0;
+    int rc = gp->gossip_exchange ? gossip_exchange(o, gp, tick, now, seed, out, &rec, &n_rec) : 0;
     mcache_shift(o, (uint32_t)gp->history_length); /* :1563 */
+    if (n_rec && o->mc_n) {
+        orc_mc_window* w0 = &o->mc[0];
+        for (size_t i = 0; i < n_rec; i++) {
+            if (w0->nb == w0->cap) {
+                w0->cap = w0->cap ? 2 * w0->cap : 4;
+                w0->b = (orc_mc_batch*)realloc(w0->b, sizeof(orc_mc_batch) * w0->cap);
+            }
+            w0->b[w0->nb++] = rec[i];
+        }
+    } else {
+        for (size_t i = 0; i < n_rec; i++) batch_free(&rec[i]);
+    }
+    free(rec);
     free(cache);
     free(ctl);
     free(resp);
     free(plst);
     free(tmp);
-    return 0;
+    return rc;
 }
 
 int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
