@@ -205,6 +205,10 @@ struct PropState {
     uint64_t* occ;                      // [hop][node / 64] bit per node: frontier row non-empty
     double publish_threshold;
     double graylist_threshold;          // AcceptFrom's gate (gossipsub only: ps.gate)
+    // topic membership (null: every node joined every topic, no fanout)
+    const uint64_t* psub;               // [pair]: topics the peer has joined (gs.p.topics)
+    const uint64_t* sub;                // [node]: topics the node has joined (gs.mesh)
+    const uint64_t* fanout;             // [pair]: topics whose fanout holds the peer
     uint32_t gate;                      // gossipsub: receivers drop copies from graylisted senders (FWD_GIN)
     unsigned long long* gray_pairs;     // pairs with FWD_GIN (counted by k_prop_fwd, kept with fwd)
     int64_t hop_latency, window;
@@ -270,6 +274,7 @@ struct DevGossipParams {
     double gossip_factor;
     int32_t max_ihave_msgs, retransmission;  // MaxIHaveMessages, GossipRetransmission
     int64_t followup_ns;                      // IWantFollowupTime
+    int64_t fanout_ttl;                       // FanoutTTL
 };
 
 // One advertised batch of the gossip exchange (heartbeat step (D)): the
@@ -284,6 +289,14 @@ struct GxBatch {
     uint8_t* got;         // set to 1 when some node delivers a message of the set
     uint32_t n_words, serial, topic, avail;  // avail: still cached after this heartbeat's Shift
 };
+// gs.p.topics[t] holds the peer of pair r / node v has joined t (null: all)
+__device__ __forceinline__ bool topic_peer(const uint64_t* psub, uint64_t r, uint32_t t) {
+    return !psub || ((psub[r] >> t) & 1);
+}
+__device__ __forceinline__ bool joined_node(const uint64_t* sub, uint32_t v, uint32_t t) {
+    return !sub || ((sub[v] >> t) & 1);
+}
+constexpr uint64_t TAG_HEARTBEAT = 8, TAG_FANOUT = 10, TAG_JOIN = 11;  // draw tags (gsx.h)
 constexpr int GX_PROMISE_SLOTS = 8;  // outstanding promises per pair (gossip_tracer.go:24-27)
 constexpr uint64_t TAG_IWANT = 9;
 
@@ -339,6 +352,16 @@ struct HbState {
     uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none)
     uint64_t* prom_h;      // [pair][GX_PROMISE_SLOTS]: promised message handle
     int64_t* prom_e;       // [pair][GX_PROMISE_SLOTS]: its expiry (0 = free slot)
+    // topic membership (null: every node joined every topic, no fanout)
+    const uint64_t* psub;  // [pair]: topics the peer has joined (gs.p.topics)
+    const uint64_t* sub;   // [node]: topics the node has joined (gs.mesh)
+    uint64_t* fanout;      // [pair]: topics whose fanout holds the peer (gs.fanout)
+    uint64_t* fan_has;     // [node]: topics with a fanout entry
+    int64_t* lastpub;      // [node][topic] (gs.lastpub; 0 = none)
+    uint32_t fan_mode;     // k_hb_gossip: 0 the joined units' mesh gossip, 1 the fanout units' (:1553)
+    uint32_t* mscratch;    // [pair]: candidate lists of the membership kernels (each row one lane's)
+    const uint32_t* pair_obs;  // [pair]: its owner (local node; set with sub)
+    double publish_threshold;
     const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
     uint32_t* long_nodes;  // nodes whose gossip list needs per-target truncation
     uint32_t* n_long;
@@ -362,6 +385,15 @@ hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st);
 // The gossip exchange: broken promises at the heartbeat start (P7), step (D),
 // and folding an exchange's receipts into the message set (all |= x; x &= acc).
 hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t st);
+// Topic membership (gossipsub.go:943-1083, 1517-1554): psub from sub; the
+// fanout of unjoined publishers (one lane per source); the heartbeat's fanout
+// expiry + maintenance of topic t; Join / Leave of (node, topic) entries.
+hipError_t launch_psub(const int32_t* col, const uint64_t* sub, uint64_t* psub, uint64_t n_pairs, hipStream_t st);
+hipError_t launch_fanout_pick(const DevState& s, const HbState& h, const uint32_t* sources, uint32_t n_src,
+                              uint32_t topic, int64_t now, uint64_t seed, double publish_threshold, hipStream_t st);
+hipError_t launch_hb_fanout(const DevState& s, const HbState& h, uint32_t t, hipStream_t st);
+hipError_t launch_join(const DevState& s, const HbState& h, const uint32_t* nodes, const uint32_t* topics,
+                       uint32_t n, uint32_t leave, hipStream_t st);
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
                            hipStream_t st);

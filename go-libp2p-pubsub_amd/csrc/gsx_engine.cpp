@@ -150,6 +150,14 @@ struct gsx_engine {
     uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gxflag = nullptr;
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;
     int64_t* d_prom_e = nullptr;
+    // topic membership (A13), on once subscriptions / Join / Leave are used
+    bool members_on = false;
+    uint64_t mem_gen = 0;  // bumped whenever subscriptions or a fanout may have changed
+    uint64_t *d_sub = nullptr, *d_psub = nullptr, *d_fanout = nullptr, *d_fan_has = nullptr;
+    int64_t* d_lastpub = nullptr;
+    uint32_t *d_mscratch = nullptr, *d_mlist = nullptr;
+    size_t mlist_cap = 0;
+    std::vector<uint64_t> h_sub;  // host copy of the joined topics per node
     gsx::GxBatch* d_gx = nullptr;
     uint32_t* d_gx_off = nullptr;
     uint8_t* d_gx_got = nullptr;
@@ -208,7 +216,7 @@ struct gsx_engine {
         struct {
             bool valid = false;
             uint32_t router = 0, topic = 0, flood_publish = 0;
-            uint64_t flag_gen = 0, score_gen = 0;
+            uint64_t flag_gen = 0, score_gen = 0, mem_gen = 0;
             double publish_threshold = 0, graylist_threshold = 0;
         } fwd_key;
         // compacted shard exchange: the dense halo the received entries are
@@ -467,6 +475,15 @@ void free_state(gsx_engine* e) {
         e->d_gx_off = nullptr;
         e->d_gx_got = nullptr;
         e->gx_cap = 0;
+        void* mbp[] = {e->d_sub, e->d_psub, e->d_fanout, e->d_fan_has, e->d_lastpub, e->d_mscratch, e->d_mlist};
+        for (void* x : mbp)
+            if (x) (void)hipFree(x);
+        e->d_sub = e->d_psub = e->d_fanout = e->d_fan_has = nullptr;
+        e->d_lastpub = nullptr;
+        e->d_mscratch = e->d_mlist = nullptr;
+        e->mlist_cap = 0;
+        e->members_on = false;
+        e->h_sub.clear();
     }
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
@@ -1463,6 +1480,67 @@ int prop_free_buffers(gsx_engine* e) {
     return GSX_OK;
 }
 
+// ---- topic membership (A13) ---------------------------------------------------
+
+// Allocates the membership state with every node joined to every topic and
+// no fanout (the state before any gsx_set_subscriptions / Join / Leave).
+int members_init(gsx_engine* e) {
+    if (e->members_on) return GSX_OK;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->sharded()) return fail(e, GSX_ESTATE, "topic membership runs on unsharded engines only");
+    const size_t N = std::max<size_t>(e->n_nodes, 1), E = std::max<size_t>(e->E, 1);
+    int rc = 0;
+    if ((rc = dalloc(e, &e->d_sub, N)) || (rc = dalloc(e, &e->d_psub, E)) || (rc = dalloc(e, &e->d_fanout, E)) ||
+        (rc = dalloc(e, &e->d_fan_has, N)) || (rc = dalloc(e, &e->d_lastpub, N * e->T)) ||
+        (rc = dalloc(e, &e->d_mscratch, E)))
+        return rc;
+    const uint64_t all = e->T >= 64 ? ~0ull : ((1ull << e->T) - 1);
+    e->h_sub.assign(e->n_nodes, all);
+    HIPCHK(e, hipMemcpy(e->d_sub, e->h_sub.data(), 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+    HIPCHK(e, gsx::launch_psub(e->d_col, e->d_sub, e->d_psub, e->E, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_fanout, 0, 8 * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_fan_has, 0, 8 * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_lastpub, 0, 8 * N * e->T, e->stream));
+    e->members_on = true;
+    ++e->mem_gen;
+    return GSX_OK;
+}
+
+// The membership fields of a kernel state (the rest of the HbState is filled
+// by hb_begin for heartbeats).
+void member_fill(gsx_engine* e, gsx::HbState& h) {
+    if (!e->members_on) return;
+    h.psub = e->d_psub;
+    h.sub = e->d_sub;
+    h.fanout = e->d_fanout;
+    h.fan_has = e->d_fan_has;
+    h.lastpub = e->d_lastpub;
+    h.mscratch = e->d_mscratch;
+    h.pair_obs = e->d_pair_obs;
+}
+gsx::HbState member_state(gsx_engine* e) {
+    gsx::HbState h{};
+    h.row_ptr = e->d_row_ptr;
+    h.rev = e->d_rev;
+    h.eflags = e->d_eflags;
+    h.n_pairs = e->E;
+    h.n_nodes = e->n_nodes;
+    h.gp.d = e->gp.d;
+    h.publish_threshold = e->th.publish_threshold;
+    member_fill(e, h);
+    return h;
+}
+int member_list(gsx_engine* e, const std::vector<uint32_t>& v) {
+    if (v.size() > e->mlist_cap) {
+        if (e->d_mlist) (void)hipFree(e->d_mlist);
+        e->d_mlist = nullptr;
+        e->mlist_cap = std::max<size_t>(v.size(), 1024);
+        if (int rc = dalloc(e, &e->d_mlist, 2 * e->mlist_cap)) return rc;
+    }
+    if (!v.empty()) HIPCHK(e, hipMemcpy(e->d_mlist, v.data(), 4 * v.size(), hipMemcpyHostToDevice));
+    return GSX_OK;
+}
+
 gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_config* cfg) {
     auto& P = e->prop;
     gsx::PropState ps{};
@@ -1511,6 +1589,11 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.router = cfg->router;
     ps.topic = cfg->topic;
     ps.flood_publish = cfg->flood_publish;
+    if (e->members_on) {
+        ps.psub = e->d_psub;
+        ps.sub = e->d_sub;
+        ps.fanout = e->d_fanout;
+    }
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     ps.credit = (cfg->credit_scores && scored) ? 1 : 0;
     ps.window = scored ? e->tp[cfg->topic].mesh_message_deliveries_window_ns : 0;
@@ -1705,11 +1788,32 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     // record flags, the overlay and, where a threshold decides, the scores:
     // the last call's are reused while none of those moved (unsharded only:
     // a shard plan rewrites the reverse pairs)
+    // Publish at sources that have not joined the topic: their fanout (gossipsub.go:981-998)
+    if (e->members_on && cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < e->T) {
+        std::vector<uint32_t> src;
+        std::vector<uint8_t> done(N, 0);
+        for (size_t k = 0; k < m; ++k) {
+            const uint32_t v = msgs[k].source;
+            if (v < N && !done[v] && !((e->h_sub[v] >> cfg->topic) & 1)) {
+                done[v] = 1;
+                src.push_back(v);
+            }
+        }
+        if (!src.empty()) {
+            if (int rc = member_list(e, src)) return rc;
+            gsx::HbState hm = member_state(e);
+            HIPCHK(e, gsx::launch_fanout_pick(ds, hm, e->d_mlist, (uint32_t)src.size(), cfg->topic, cfg->now_ns,
+                                              cfg->seed, e->th.publish_threshold, e->stream));
+            ++e->mem_gen;
+            HIPCHK(e, hipStreamSynchronize(e->stream));  // `src` is on the host stack
+        }
+    }
     auto& K = P.fwd_key;
     const bool fwd_same = K.valid && !e->sharded() && K.router == cfg->router && K.topic == cfg->topic &&
                           K.flood_publish == cfg->flood_publish && K.flag_gen == e->flag_gen &&
                           K.publish_threshold == e->th.publish_threshold &&
-                          K.graylist_threshold == e->th.graylist_threshold && (!need_score || K.score_gen == e->score_gen);
+                          K.graylist_threshold == e->th.graylist_threshold && K.mem_gen == e->mem_gen &&
+                          (!need_score || K.score_gen == e->score_gen);
     if (!fwd_same) {
         HIPCHK(e, hipMemsetAsync(P.gray_pairs, 0, 8, e->stream));
         HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
@@ -1719,6 +1823,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         K.flood_publish = cfg->flood_publish;
         K.flag_gen = e->flag_gen;
         K.score_gen = e->score_gen;
+        K.mem_gen = e->mem_gen;
         K.publish_threshold = e->th.publish_threshold;
         K.graylist_threshold = e->th.graylist_threshold;
     }
@@ -2160,6 +2265,7 @@ int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
     p->gossip_retransmission = 3;
     p->iwant_followup_ns = 3LL * 1000000000LL;
     p->gossip_exchange = 0;
+    p->fanout_ttl_ns = 60LL * 1000000000LL;
     return GSX_OK;
 }
 
@@ -2188,7 +2294,9 @@ namespace {
 //   hb_recv   (B) handleGraft / handlePrune at the receivers (remote senders' bits from halo_ctl);
 //   hb_end    (C) the senders handle the PRUNE answers (remote answers from halo_resp), counters,
 //             mcache.Shift.
-int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
+// state_only: the round's buffers and kernel state (e->hb) without
+// maintenance, gossip or the promise penalties (Join / Leave use it)
+int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, bool state_only) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     e->state_changed();
     if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
@@ -2234,7 +2342,7 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     }
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     uint8_t* pen_mask = nullptr;
-    if (e->d_prom_e) {
+    if (e->d_prom_e && !state_only) {
         // clearIHaveCounters (:1566-1576); applyIwantPenalties (:1578-1583):
         // promises expired before now are broken, AddPenalty (P7) on their pairs
         const size_t E = std::max<size_t>(e->E, 1);
@@ -2282,6 +2390,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     h.work = e->d_work;
     h.tcnt = e->d_tcnt;
     h.mcount = e->d_mcount;
+    h.publish_threshold = e->th.publish_threshold;
+    member_fill(e, h);
     if (e->hb_tracing) {
         if (!e->d_tr_acc) {
             if (int rc = dalloc(e, &e->d_tr_acc, std::max<size_t>(e->E, 1))) return rc;
@@ -2315,7 +2425,8 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
                                 e->gp.gossip_factor,
                                 e->gp.max_ihave_messages,
                                 e->gp.gossip_retransmission,
-                                e->gp.iwant_followup_ns};
+                                e->gp.iwant_followup_ns,
+                                e->gp.fanout_ttl_ns};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
     if (gx_on) {
@@ -2343,6 +2454,10 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, e->E ? e->E : 1, e->stream));
     }
     e->hb_clean = false;  // until this round's (C) has run
+    if (state_only) {
+        e->hb = h;
+        return GSX_OK;
+    }
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
     // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order
     e->gb_host.clear();
@@ -2412,6 +2527,16 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
         HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
                                         e->max_deg, e->stream));
     }
+    if (e->members_on) {  // the fanout of topics published to but not joined (:1517-1554)
+        for (uint32_t t = 0; t < e->T; ++t) {
+            HIPCHK(e, gsx::launch_hb_fanout(ds, h, t, e->stream));
+            gsx::HbState hf = h;
+            hf.fan_mode = 1;
+            HIPCHK(e, gsx::launch_hb_gossip(ds, hf, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
+                                            e->max_deg, e->stream));
+        }
+        ++e->mem_gen;
+    }
     // the receivers score the senders as the round left them: the pairs (A)
     // touched that (B) reads (marked in the inbox) are re-scored
     // (a shard's (B) reads every pair with remote control: all touched pairs)
@@ -2424,6 +2549,10 @@ int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
+}
+
+int hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
+    return hb_begin_state(e, tick, now, seed, false);
 }
 
 int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
@@ -2603,6 +2732,114 @@ int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out)
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_recv && !halo_resp) return GSX_EINVAL;
     return hb_end(e, halo_resp, out);
+}
+
+// ---- topic membership API (gsx.h) ------------------------------------------------
+
+int gsx_set_subscriptions(gsx_engine* e, const uint64_t* joined) {
+    if (!e || !joined) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    if (int rc = members_init(e)) return rc;
+    const uint64_t all = e->T >= 64 ? ~0ull : ((1ull << e->T) - 1);
+    for (uint32_t v = 0; v < e->n_nodes; ++v) e->h_sub[v] = joined[v] & all;
+    HIPCHK(e, hipMemcpy(e->d_sub, e->h_sub.data(), 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+    HIPCHK(e, gsx::launch_psub(e->d_col, e->d_sub, e->d_psub, e->E, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    ++e->mem_gen;
+    return GSX_OK;
+}
+
+int gsx_export_membership(gsx_engine* e, uint64_t* joined, uint64_t* fanout, int64_t* lastpub) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (!e->members_on) {  // every node joined to every topic, no fanout
+        const uint64_t all = e->T >= 64 ? ~0ull : ((1ull << e->T) - 1);
+        if (joined)
+            for (uint32_t v = 0; v < e->n_nodes; ++v) joined[v] = all;
+        if (fanout) std::memset(fanout, 0, 8 * (size_t)e->E);
+        if (lastpub) std::memset(lastpub, 0, 8 * (size_t)e->n_nodes * e->T);
+        return GSX_OK;
+    }
+    if (joined) std::memcpy(joined, e->h_sub.data(), 8 * (size_t)e->n_nodes);
+    if (fanout && e->E) HIPCHK(e, hipMemcpyAsync(fanout, e->d_fanout, 8 * (size_t)e->E, hipMemcpyDeviceToHost, e->stream));
+    if (lastpub && e->n_nodes)
+        HIPCHK(e, hipMemcpyAsync(lastpub, e->d_lastpub, 8 * (size_t)e->n_nodes * e->T, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+namespace {
+// Join / Leave: the subscriptions are announced first, then each entry's
+// mesh change (one launch per rank of the entry within its node, so one
+// node's row has one lane per launch), then the peers handle the GRAFTs /
+// PRUNEs ((B)) and the joiners the PRUNE answers ((C)), as in a heartbeat.
+int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now, uint64_t seed,
+                 bool leave, gsx_heartbeat_out* out) {
+    if (!e || (!nodes && n) || (!topics && n) || !out) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    if (e->max_deg > gsx::HB_HUB_MAX)
+        return fail(e, GSX_ERANGE, "membership changes support at most " + std::to_string(gsx::HB_HUB_MAX) + " peers per node");
+    if (int rc = members_init(e)) return rc;
+    for (size_t i = 0; i < n; ++i)
+        if (nodes[i] >= e->n_nodes || topics[i] >= e->T) return fail(e, GSX_ERANGE, "node or topic out of range");
+    e->state_changed();
+    // the entries that change something, announced (a repeated entry finds it done)
+    std::vector<std::vector<uint32_t>> rank_nodes, rank_topics;
+    std::unordered_map<uint32_t, uint32_t> per_node;
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t v = nodes[i], t = topics[i];
+        const bool in = (e->h_sub[v] >> t) & 1;
+        if (leave ? !in : in) continue;
+        e->h_sub[v] = leave ? (e->h_sub[v] & ~(1ull << t)) : (e->h_sub[v] | (1ull << t));
+        const uint32_t k = per_node[v]++;
+        if (k >= rank_nodes.size()) {
+            rank_nodes.emplace_back();
+            rank_topics.emplace_back();
+        }
+        rank_nodes[k].push_back(v);
+        rank_topics[k].push_back(t);
+    }
+    HIPCHK(e, hipMemcpy(e->d_sub, e->h_sub.data(), 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+    HIPCHK(e, gsx::launch_psub(e->d_col, e->d_sub, e->d_psub, e->E, e->stream));
+    ++e->mem_gen;
+    // a heartbeat's buffers and state, without maintenance or gossip
+    if (int rc = hb_begin_state(e, 0, now, seed, true)) return rc;
+    gsx::HbState h = e->hb;
+    const gsx::DevState ds = dev_state(e);
+    for (size_t k = 0; k < rank_nodes.size(); ++k) {
+        std::vector<uint32_t> lst(rank_nodes[k]);
+        lst.insert(lst.end(), rank_topics[k].begin(), rank_topics[k].end());
+        if (int rc = member_list(e, lst)) return rc;
+        const uint32_t m = (uint32_t)rank_nodes[k].size();
+        HIPCHK(e, gsx::launch_join(ds, h, e->d_mlist, e->d_mlist + m, m, leave ? 1 : 0, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));  // `lst` is reused
+    }
+    // the receivers' mesh sizes (the scan counts every unit) and the scores of the touched pairs
+    HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
+    e->hb_active = true;
+    if (int rc = hb_recv(e, nullptr)) return rc;
+    std::memset(out, 0, sizeof(*out));
+    e->hb_active = false;
+    HIPCHK(e, gsx::launch_hb_answer(ds, e->hb, e->stream));
+    e->hb_clean = !e->hb_tracing;
+    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
+    unsigned long long st[gsx::HB_STAT_WORDS];
+    HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    std::memcpy(out, st, sizeof(st));
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_join(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now_ns, uint64_t seed,
+             gsx_heartbeat_out* out) {
+    return member_round(e, nodes, topics, n, now_ns, seed, false, out);
+}
+
+int gsx_leave(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now_ns,
+              gsx_heartbeat_out* out) {
+    return member_round(e, nodes, topics, n, now_ns, 0, true, out);
 }
 
 int gsx_hb_set_tracing(gsx_engine* e, uint32_t on) {

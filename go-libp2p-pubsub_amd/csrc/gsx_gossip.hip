@@ -90,8 +90,8 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
         for (int64_t q = r0; q < r1; ++q) {
             const uint32_t r = h.rev[q];
             if (r == NO_PAIR || (r & HALO)) continue;
-            const uint64_t tb = gx_topics(h, r);
-            if (!tb) continue;
+            const uint64_t tb = gx_topics(h, r) & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
+            if (!gx_topics(h, r)) continue;
             if (s.score[q] < h.gossip_threshold) {  // :617-621
                 ++ignored;
                 continue;
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             if (s.score[r] < h.gossip_threshold) continue;  // v ignores u's IWANT
             if (!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) continue;  // AcceptFrom at u
             const uint32_t v = (uint32_t)h.col[q];
-            const uint64_t tb = gx_topics(h, r);
+            const uint64_t tb = gx_topics(h, r) & (h.sub ? h.sub[u] : ~0ull);
             uint32_t n = 0;  // |iwant| again (the selection depends on it)
             gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
                 ++n;

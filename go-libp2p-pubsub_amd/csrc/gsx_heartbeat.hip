@@ -37,7 +37,6 @@
 
 namespace gsx {
 
-constexpr uint64_t TAG_HEARTBEAT = 8;
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
 #pragma unroll
@@ -152,11 +151,11 @@ constexpr uint8_t ST_GRAFT = 16;   // maintain() grafted the pair (effects appli
 constexpr uint8_t ST_PRUNE = 32;   // maintain() pruned the pair
 constexpr uint8_t ST_ACTIVE = 64;  // the record's mesh-delivery counting is active (REC_ACTIVE)
 
-__device__ __forceinline__ uint8_t stage_pack(uint8_t pf, uint8_t ef, uint8_t rf, bool bo) {
+__device__ __forceinline__ uint8_t stage_pack(uint8_t pf, uint8_t ef, uint8_t rf, bool bo, bool in_t = true) {
     uint8_t f = 0;
     if ((pf & PAIR_PRESENT) && (rf & REC_IN_MESH)) f |= ST_MESH;
     if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) &&
-        !(ef & EDGE_DIRECT))
+        !(ef & EDGE_DIRECT) && in_t)
         f |= ST_CAND;
     if (ef & EDGE_OUTBOUND) f |= ST_OUT;
     if (rf & REC_ACTIVE) f |= ST_ACTIVE;
@@ -168,7 +167,7 @@ __device__ __forceinline__ uint8_t stage_bits(const DevState& s, const HbState& 
     // every input loaded unconditionally (no load waits at a divergent join)
     const uint8_t pf = s.pflags[r], ef = h.eflags[r];
     const uint8_t rf = s.rflags[flag_index(r, t, s.n_topics)];
-    return stage_pack(pf, ef, rf, backoff_present(h, r, t));
+    return stage_pack(pf, ef, rf, backoff_present(h, r, t), topic_peer(h.psub, r, t));
 }
 
 // One unit (v, t) over its staged row: sc / fl are the row's scores and bits,
@@ -414,7 +413,8 @@ constexpr int APPLY_UNROLL = 4;  // receiver-pair loads per lane in flight
 // Draws are keyed by the GLOBAL node id, so a range shard draws what the
 // whole-overlay engine draws for the same node.
 __device__ __forceinline__ Rng hb_rng(const HbState& h, uint32_t v, uint32_t t, uint32_t k) {
-    return Rng{h.seed, TAG_HEARTBEAT, (uint64_t)h.node_lo + v, (h.tick << 32) | ((uint64_t)t << 24), k};
+    return Rng{h.seed, TAG_HEARTBEAT, (uint64_t)h.node_lo + v,
+               (h.tick << 32) | ((uint64_t)t << 24) | (h.fan_mode ? (1ull << 23) : 0ull), k};
 }
 
 // LDS hand-off between the lanes of a one-wave block: a wave's LDS accesses
@@ -458,14 +458,14 @@ constexpr int SCAN_STAGE = 2048;   // pairs of a tile staged (scan bits, u32) fo
 constexpr uint32_t SC_NEG = 1u << 8, SC_OUT = 1u << 9, SC_CAND = 1u << 10;
 constexpr uint32_t SC_OGLOW = 1u << 11;
 __device__ __forceinline__ uint32_t scan_pack(uint8_t pf, uint8_t ef, double sc, const uint8_t (&rf)[SCAN_TOPICS],
-                                              uint8_t bo, uint32_t nt, double og_threshold) {
+                                              uint8_t bo, uint32_t nt, double og_threshold, uint32_t in8 = 0xFFu) {
     if (!(pf & PAIR_PRESENT)) return 0;
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_TOPICS; ++k)
         if (rf[k] & REC_IN_MESH) m |= 1u << k;
     if ((pf & PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) && !(ef & EDGE_DIRECT) && sc >= 0.0)
-        m |= (~(m | bo) & ((1u << nt) - 1)) << 16;
+        m |= (~(m | bo) & ((1u << nt) - 1) & in8) << 16;  // (in8: the peer joined t0 + k)
     if (sc < 0) m |= SC_NEG;
     if (sc < og_threshold) m |= SC_OGLOW;
     if (ef & EDGE_OUTBOUND) m |= SC_OUT;
@@ -478,7 +478,7 @@ __device__ __forceinline__ uint32_t scan_bits(const DevState& s, const HbState& 
 #pragma unroll
     for (int k = 0; k < SCAN_TOPICS; ++k) rf[k] = k < (int)nt ? s.rflags[flag_index(r, t0 + k, s.n_topics)] : 0;
     return scan_pack(s.pflags[r], h.eflags[r], s.score[r], rf, h.bo8[(size_t)(t0 / 8) * h.n_pairs + r], nt,
-                     h.og_threshold);
+                     h.og_threshold, h.psub ? (uint32_t)((h.psub[r] >> t0) & 0xFF) : 0xFFu);
 }
 
 // (A) scan: every unit of every topic.  A wave takes a tile of 64 consecutive
@@ -547,10 +547,15 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
 #pragma unroll
                         for (int k = 0; k < SCAN_TOPICS; ++k)
                             if (k >= (int)nt) rf[j][k] = 0;
+                    uint32_t in8[4] = {0xFFu, 0xFFu, 0xFFu, 0xFFu};
+                    if (h.psub) {  // (uniform) the peers' joined topics
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) in8[j] = (uint32_t)((h.psub[min(rb + 64 * j, pb - 1)] >> t0) & 0xFF);
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t r = rb + 64 * j;
-                        if (r < pb) st[r - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j], bo[j], nt, h.og_threshold);
+                        if (r < pb) st[r - pa] = scan_pack(pf[j], ef[j], sc[j], rf[j], bo[j], nt, h.og_threshold, in8[j]);
                     }
                 }
             }
@@ -585,8 +590,9 @@ __global__ __launch_bounds__(256) void k_hb_scan(DevState s, HbState h) {
                 // [n/2]) is below the threshold: iff more than n/2 members are
                 // (scores are finite; the sort and the draws have no other effect)
                 const bool grow = n[k] < gp.d_lo, more_out = !grow && outb[k] < gp.d_out;
-                const bool a = neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1 && low[k] > n[k] / 2) ||
-                               (grow && (cg >> k & 1)) || (more_out && (co >> k & 1));  // :1370-1385, :1450-1476
+                const bool a = joined_node(h.sub, v, t) &&  // gs.mesh holds the joined topics
+                               (neg[k] > 0 || n[k] > gp.d_hi || (og_tick && n[k] > 1 && low[k] > n[k] / 2) ||
+                                (grow && (cg >> k & 1)) || (more_out && (co >> k & 1)));  // :1370-1385, :1450-1476
                 act |= (uint32_t)a << k;
                 h.rngk[(size_t)t * h.n_nodes + v] = 0;
                 h.mcount[(size_t)t * h.n_nodes + v] = (uint16_t)n[k];  // (A) updates it for acting units
@@ -702,12 +708,19 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
                         rf[j] = s.rflags[flag_index(r[j], t, s.n_topics)];
                         bb[j] = h.bo8[(size_t)(t / 8) * h.n_pairs + r[j]];
                     }
+                    bool in_t[MAINT_UNROLL];
+#pragma unroll
+                    for (int j = 0; j < MAINT_UNROLL; ++j) in_t[j] = true;
+                    if (h.psub) {  // (uniform) the peer joined t
+#pragma unroll
+                        for (int j = 0; j < MAINT_UNROLL; ++j) in_t[j] = (h.psub[r[j]] >> t) & 1;
+                    }
 #pragma unroll
                     for (int j = 0; j < MAINT_UNROLL; ++j) {
                         const uint32_t k = k0 + 64 * j;
                         if (k < end) {
                             sc[k - base] = x[j];
-                            fl[k - base] = stage_pack(pf[j], ef[j], rf[j], (bb[j] >> (t % 8)) & 1);
+                            fl[k - base] = stage_pack(pf[j], ef[j], rf[j], (bb[j] >> (t % 8)) & 1, in_t[j]);
                         }
                     }
                 }
@@ -830,8 +843,10 @@ __device__ __forceinline__ double live_score(const DevState& s, const HbState& h
 // not in the mesh, not direct, live score >= GossipThreshold.
 __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& h, uint64_t r, uint32_t t) {
     const uint8_t f = h.eflags[r];
+    // excluded: the mesh, or the fanout for a fanout unit (:1514, :1553)
+    const bool excl = h.fan_mode ? ((h.fanout[r] >> t) & 1) != 0 : hb_in_mesh(s, r, t);
     return (s.pflags[r] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
-           (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && !hb_in_mesh(s, r, t) &&
+           topic_peer(h.psub, r, t) && (f & EDGE_GOSSIPSUB) && !(f & EDGE_DIRECT) && !excl &&
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
@@ -908,6 +923,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
         for (int64_t rb = pa + lane; rb < pb; rb += 256) {
             uint8_t pf[4], ef[4], rf[4], dt[4];
             double sc[4];
+            bool in_t[4] = {true, true, true, true};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {  // unconditional loads of clamped addresses (see k_hb_scan)
                 const int64_t r = min(rb + 64 * j, pb - 1);
@@ -917,22 +933,35 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                 dt[j] = h.dirty[r];
                 sc[j] = s.score[r];
             }
+            if (h.psub) {  // (uniform) the peers' joined topics
+#pragma unroll
+                for (int j = 0; j < 4; ++j) in_t[j] = (h.psub[min(rb + 64 * j, pb - 1)] >> t) & 1;
+            }
+            if (h.fan_mode) {  // (uniform) a fanout pass excludes the fanout, not the mesh
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    rf[j] = ((h.fanout[min(rb + 64 * j, pb - 1)] >> t) & 1) ? REC_IN_MESH : 0;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int64_t r = rb + 64 * j;
                 if (r >= pb) continue;
-                h.ihave_len[tslot + r] = 0;
-                h.ihave_hash[tslot + r] = 0;
+                if (!h.fan_mode) {  // (the fanout pass adds to the slots the mesh pass rewrote)
+                    h.ihave_len[tslot + r] = 0;
+                    h.ihave_hash[tslot + r] = 0;
+                }
                 if (!staged) continue;
                 // gossip_target with the loads above (live score: dirty pairs re-evaluated)
-                bool ok = (pf[j] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+                bool ok = (pf[j] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && in_t[j] &&
                           (ef[j] & EDGE_GOSSIPSUB) && !(ef[j] & EDGE_DIRECT) && !(rf[j] & REC_IN_MESH);
                 if (ok) ok = (dt[j] ? eval_pair(s, h.pp, r) : sc[j]) >= h.gossip_threshold;
                 el[r - pa] = ok;
             }
         }
         __syncthreads();
-        if (lane < nv) {
+        const bool unit = lane < nv && (h.fan_mode ? ((h.fan_has[v0 + lane] >> t) & 1) != 0
+                                                   : joined_node(h.sub, v0 + lane, t));
+        if (unit) {
             const uint32_t v = v0 + lane;
             uint64_t dig;
             const uint32_t L = gossip_ids(h, v, gb, n_gb, dig);
@@ -1173,6 +1202,11 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             uint32_t r;
             uint64_t grafts, prunes;
             if (!recv_control(h, q, true, r, grafts, prunes)) continue;
+            if (h.sub) {  // GRAFT / PRUNE of a topic u has not joined: ignored (:727-733, :816-819)
+                grafts &= h.sub[u];
+                prunes &= h.sub[u];
+                if (!(grafts | prunes)) continue;
+            }
             // gs.score.Score(p) once per control message (the cache holds the round's
             // state for every pair read here: k_mask_and + the subset re-score after (A))
             const double score = s.score[q];
@@ -1273,6 +1307,11 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
                 if (w0 && !(r & HALO) && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                if (h.sub) {  // topics u has not joined: ignored (:727-733, :816-819)
+                    grafts &= h.sub[u];
+                    prunes &= h.sub[u];
+                    if (!(grafts | prunes)) continue;
+                }
                 const double score = s.score[q];
                 const uint8_t ef = h.eflags[q];
                 if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
@@ -1369,6 +1408,7 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
         if (!h.halo_resp && q != NO_PAIR) h.resp[q] = 0;
         // AcceptFrom at v for the answering peer
         if (resp && !(h.eflags[r] & EDGE_DIRECT) && s.score[r] < h.graylist) resp = 0;
+        if (resp && h.sub) resp &= h.sub[h.pair_obs[r]];  // (a PRUNE of a topic v left: ignored)
         if (resp) h.dirty[r] = 1;
         for (; resp; resp &= resp - 1) {
             if (handle_prune(s, h, r, (uint32_t)__builtin_ctzll(resp))) --links;

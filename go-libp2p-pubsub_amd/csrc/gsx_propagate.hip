@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
         const uint8_t pf = s.pflags[r];
         const uint8_t ef = ps.eflags[r];
         uint8_t out = 0;
-        if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED)) {  // in ps.topics[topic]
+        if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+            topic_peer(ps.psub, r, ps.topic)) {  // in ps.topics[topic]
             if (ps.router == ROUTER_FLOODSUB) {  // every topic peer (floodsub.go:81-90)
                 out = FWD_FORWARD | FWD_PUBLISH;
             } else if (ps.router == ROUTER_RANDOMSUB) {  // FloodSub peers always, the rest by draw (randomsub.go:112-143)
@@ -56,8 +57,10 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
                 const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
                 const bool above = need_score && s.score[r] >= ps.publish_threshold;
                 bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
-                if (!fwd && ps.topic < s.n_topics)                       // mesh peers (:977-999)
-                    fwd = s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH;
+                if (!fwd && ps.topic < s.n_topics)  // mesh peers, or the fanout when not joined (:977-999)
+                    fwd = joined_node(ps.sub, ps.pair_obs[r], ps.topic)
+                              ? (s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH) != 0
+                              : ((ps.fanout[r] >> ps.topic) & 1) != 0;
                 const bool pub = ps.flood_publish ? (direct || above) : fwd;  // flood publish (:953-960)
                 out = (fwd ? FWD_FORWARD : 0) | (pub ? FWD_PUBLISH : 0);
             }

@@ -286,6 +286,7 @@ class GossipSubParams(C.Structure):
         ("iwant_followup_ns", C.c_int64),
         ("gossip_exchange", C.c_int32),
         ("reserved0", C.c_int32),
+        ("fanout_ttl_ns", C.c_int64),
     ]
 
 
@@ -391,6 +392,11 @@ SIGNATURES = {
     "gsx_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
     "gsx_mcache_clear": (C.c_int, [C.c_void_p]),
     "gsx_hb_set_tracing": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_set_subscriptions": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "gsx_join": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, C.c_uint64,
+                           P(HeartbeatOut)]),
+    "gsx_leave": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, P(HeartbeatOut)]),
+    "gsx_export_membership": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_int64)]),
     "gsx_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
     "gsx_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),

@@ -350,6 +350,36 @@ class Engine:
     def mcache_clear(self):
         self._chk(self.lib.gsx_mcache_clear(self.h), "gsx_mcache_clear")
 
+    def set_subscriptions(self, joined):
+        """Joined topics per node (bit t of joined[v]); gsx_set_subscriptions."""
+        j = np.ascontiguousarray(joined, dtype=np.uint64)
+        self._chk(self.lib.gsx_set_subscriptions(self.h, _ptr(j, C.c_uint64)), "gsx_set_subscriptions")
+
+    def export_membership(self):
+        """-> (joined [N] u64, fanout [E] u64 topic bits, lastpub [N, T] i64)"""
+        j = np.empty(self.n_nodes, dtype=np.uint64)
+        f = np.empty(self.n_pairs, dtype=np.uint64)
+        lp = np.empty((self.n_nodes, self.n_topics), dtype=np.int64)
+        self._chk(self.lib.gsx_export_membership(self.h, _ptr(j, C.c_uint64), _ptr(f, C.c_uint64),
+                                                 _ptr(lp, C.c_int64)), "gsx_export_membership")
+        return j, f, lp
+
+    def join(self, nodes, topics, now: int, seed: int) -> abi.HeartbeatOut:
+        nd = np.ascontiguousarray(nodes, dtype=np.uint32)
+        tp = np.ascontiguousarray(topics, dtype=np.uint32)
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.gsx_join(self.h, _ptr(nd, C.c_uint32), _ptr(tp, C.c_uint32), len(nd), now, seed,
+                                    C.byref(out)), "gsx_join")
+        return out
+
+    def leave(self, nodes, topics, now: int) -> abi.HeartbeatOut:
+        nd = np.ascontiguousarray(nodes, dtype=np.uint32)
+        tp = np.ascontiguousarray(topics, dtype=np.uint32)
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.gsx_leave(self.h, _ptr(nd, C.c_uint32), _ptr(tp, C.c_uint32), len(nd), now,
+                                     C.byref(out)), "gsx_leave")
+        return out
+
     def hb_set_tracing(self, on: bool = True):
         self._chk(self.lib.gsx_hb_set_tracing(self.h, 1 if on else 0), "gsx_hb_set_tracing")
 

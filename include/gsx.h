@@ -525,6 +525,7 @@ typedef struct gsx_gossipsub_params {
     int64_t iwant_followup_ns;              /* :58                               */
     int32_t gossip_exchange;                /* 1: run step (D) below; 0: IHAVEs are only emitted */
     int32_t reserved0;
+    int64_t fanout_ttl_ns;                  /* :45 (GossipSubFanoutTTL)          */
 } gsx_gossipsub_params;
 
 int gsx_default_gossipsub_params(gsx_gossipsub_params* out);
@@ -628,6 +629,42 @@ int gsx_import_backoff(gsx_engine* e, const int64_t* in);
  * receiver collects the ids into a set (handleIHave, gossipsub.go:641-650).
  * Either pointer may be NULL. */
 int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_digest);
+/* ---- topic membership (gossipsub.go:943-1083, 1517-1554) ------------------
+ * By default every node has joined every topic.  gsx_set_subscriptions sets
+ * the joined topics of every node (bit t of joined[node], n_nodes words) as
+ * the state of the overlay, without protocol effects: gs.mesh[t] exists at a
+ * node iff it joined t (only joined (node, topic) units run the mesh
+ * maintenance and its gossip, and GRAFT / PRUNE / IHAVE of other topics are
+ * ignored, :727-733, :816-819, :638-641), and every node knows its peers'
+ * subscriptions (gs.p.topics: the "in topic" filter of getPeers, of
+ * forwarding and of gossip targets).  A gossipsub publisher that has not
+ * joined the topic sends to its fanout (:981-998): when empty it is filled
+ * with getPeers(D) of non-direct peers with score >= PublishThreshold (draws
+ * h(seed of the call, 10, source, topic << 24 | k)), and lastpub = now.  The
+ * heartbeat then expires fanouts after FanoutTTL and keeps them at D
+ * (:1517-1554; draws h(seed, 8, node, tick << 32 | topic << 24 | 1 << 23 | k),
+ * which the node's fanout gossip continues).  gsx_join / gsx_leave change
+ * membership with the protocol's effects, as one synchronous round: the
+ * call's subscriptions are announced first; Join builds the mesh from the
+ * fanout (negative scores dropped, topped up to D) or getPeers(D) (draws
+ * h(seed, 11, node, topic << 24 | k)) and sends GRAFTs; Leave prunes the mesh
+ * (tracer.Prune, PRUNE sent, no backoff at the leaver); the peers then
+ * handle them as in step (B) and the joiners the PRUNE answers as in (C).
+ * *out gets the round's counters (grafts / prunes of the joiners / leavers,
+ * the receivers' accepted / rejected / handled, mesh_links after).  Copies
+ * forwarded to a mesh peer that has left the topic (the receiver ignores
+ * them, pubsub.go handleIncomingRPC) are not counted as transmissions.
+ * Unsharded engines only (GSX_ESTATE on a range shard). */
+int gsx_set_subscriptions(gsx_engine* e, const uint64_t* joined);
+int gsx_join(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now_ns, uint64_t seed,
+             gsx_heartbeat_out* out);
+int gsx_leave(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now_ns,
+              gsx_heartbeat_out* out);
+/* joined topics per node [n_nodes], fanout topic bits per pair [E] (the
+ * peer is in the owner's fanout), lastpub per [node][topic] (0 = none); any
+ * pointer may be NULL */
+int gsx_export_membership(gsx_engine* e, uint64_t* joined, uint64_t* fanout, int64_t* lastpub);
+
 /* The tracer's GRAFT / PRUNE calls of the last heartbeat, as topic bit words
  * per pair p = (observer -> peer), E words each (any pointer may be NULL):
  *   sent_graft    graftPeer (:1353-1359)             Graft(peer, topic) by observer

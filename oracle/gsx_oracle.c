@@ -116,7 +116,14 @@ struct orc_engine {
     uint32_t* ptx_cnt;
     size_t ptx_cap, ptx_n;
     uint32_t msg_serial;
-    bool ihave_trunc; /* the last heartbeat sent an IHAVE list longer than MaxIHaveLength */
+    bool ihave_trunc;
+    /* topic membership (A13): joined topics per node (gs.mesh[topic] exists;
+     * its neighbours know it: gs.p.topics), fanout (gs.fanout, gs.lastpub) */
+    uint64_t* sub;     /* [node] */
+    uint64_t* fanout;  /* [pair]: topics whose fanout holds the peer */
+    uint64_t* fan_has; /* [node]: topics with a fanout entry */
+    int64_t* lastpub;  /* [node][topic] */
+    gsx_gossipsub_params gp; /* for Publish / Join (D, fanout) */ /* the last heartbeat sent an IHAVE list longer than MaxIHaveLength */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -255,6 +262,7 @@ orc_engine* orc_create(uint32_t n_topics) {
     orc_engine* o = (orc_engine*)calloc(1, sizeof(orc_engine));
     if (!o) return NULL;
     o->T = n_topics;
+    orc_default_gossipsub_params(&o->gp);
     return o;
 }
 
@@ -314,6 +322,10 @@ void orc_destroy(orc_engine* o) {
     free(o->tr_hp);
     free(o->peerhave);
     free(o->iasked);
+    free(o->sub);
+    free(o->fanout);
+    free(o->fan_has);
+    free(o->lastpub);
     free(o->prom);
     free(o->ptx_key);
     free(o->ptx_pair);
@@ -370,6 +382,16 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     if (!o->ihave_len || !o->ihave_hash) return GSX_ENOMEM;
     free(o->peerhave);
     free(o->iasked);
+    free(o->sub);
+    free(o->fanout);
+    free(o->fan_has);
+    free(o->lastpub);
+    o->sub = (uint64_t*)malloc(sizeof(uint64_t) * (n_nodes ? n_nodes : 1));
+    o->fanout = (uint64_t*)calloc(E ? E : 1, sizeof(uint64_t));
+    o->fan_has = (uint64_t*)calloc(n_nodes ? n_nodes : 1, sizeof(uint64_t));
+    o->lastpub = (int64_t*)calloc((size_t)(n_nodes ? n_nodes : 1) * o->T, sizeof(int64_t));
+    if (!o->sub || !o->fanout || !o->fan_has || !o->lastpub) return GSX_ENOMEM;
+    for (uint32_t v = 0; v < n_nodes; v++) o->sub[v] = o->T >= 64 ? ~0ull : ((1ull << o->T) - 1); /* all joined */
     o->peerhave = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
     o->iasked = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
     if (!o->peerhave || !o->iasked) return GSX_ENOMEM;
@@ -1008,7 +1030,11 @@ int orc_set_thresholds(orc_engine* o, const gsx_thresholds* t) {
 }
 
 /* p in ps.topics[topic] / ps.peers: connected and tracked */
-static bool in_topic(const orc_engine* o, uint64_t r) { return o->ps[r].present && o->ps[r].connected; }
+/* the peer of pair r is in gs.p.topics[t] (subscribed, and known: present, connected) */
+static bool in_topic(const orc_engine* o, uint64_t r, uint32_t t) {
+    return o->ps[r].present && o->ps[r].connected && t < 64 && (o->sub[o->col[r]] >> t & 1);
+}
+static bool joined(const orc_engine* o, uint32_t v, uint32_t t) { return t < 64 && (o->sub[v] >> t & 1); }
 
 /* the pair (u -> v) given the pair (v -> u); -1 if u does not track v */
 static int64_t reverse_pair(const orc_engine* o, uint64_t r) {
@@ -1065,7 +1091,7 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
     if (cfg->router == GSX_ROUTER_FLOODSUB) { /* floodsub.go:81-90 */
         for (int64_t r = r0; r < r1; r++) {
             uint32_t u = (uint32_t)o->col[r];
-            if (!in_topic(o, r)) continue;
+            if (!in_topic(o, r, cfg->topic)) continue;
             if ((int64_t)u == from || u == origin) continue;
             out[n++] = (uint64_t)r;
         }
@@ -1075,7 +1101,7 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
         int nrs = 0;
         for (int64_t r = r0; r < r1; r++) {
             uint32_t u = (uint32_t)o->col[r];
-            if (!in_topic(o, r)) continue;
+            if (!in_topic(o, r, cfg->topic)) continue;
             if ((int64_t)u == from || u == origin) continue;
             if (o->eflags[r] & GSX_EDGE_FLOODSUB) out[n++] = (uint64_t)r; /* rs.peers[p] == FloodSubID */
             else scratch[nrs++] = (uint64_t)r;
@@ -1096,7 +1122,7 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
     const uint32_t topic = cfg->topic;
     const double thr = o->th.publish_threshold;
     for (int64_t r = r0; r < r1; r++) {
-        if (!in_topic(o, r)) continue; /* tmap */
+        if (!in_topic(o, r, cfg->topic)) continue; /* tmap */
         const uint8_t ef = o->eflags[r];
         const bool direct = (ef & GSX_EDGE_DIRECT) != 0;
         bool send;
@@ -1106,7 +1132,8 @@ static int router_targets(orc_engine* o, const gsx_prop_config* cfg, uint32_t v,
             const bool mesh_peer = (ef & GSX_EDGE_GOSSIPSUB) != 0; /* gs.feature(GossipSubFeatureMesh, ...) */
             send = direct;                                          /* :962-968 */
             if (!send && !mesh_peer) send = score0[r] >= thr; /* :970-975 */
-            if (!send && topic < o->T) send = o->ts[(uint64_t)r * o->T + topic].in_mesh; /* gs.mesh[topic], :977-999 */
+            if (!send && topic < o->T) /* gs.mesh[topic], or the fanout when not joined (:977-999) */
+                send = joined(o, v, topic) ? o->ts[(uint64_t)r * o->T + topic].in_mesh : (o->fanout[r] >> topic & 1);
         }
         if (!send) continue;
         uint32_t u = (uint32_t)o->col[r];
@@ -1161,6 +1188,38 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
      * call's own credits (P2/P3, and P4 of rejected messages) land at its end. */
     double* score0 = (double*)malloc(sizeof(double) * (o->E ? o->E : 1));
     for (uint64_t r = 0; r < o->E; r++) score0[r] = score_pair(o, r);
+    /* Publish at a source that has not joined the topic (gossipsub.go:981-998):
+     * its fanout, picked when empty (getPeers(D) of non-direct peers with
+     * score >= PublishThreshold, draws h(seed, 10, source, topic << 24 | k)),
+     * and lastpub = now; once per source at the call start */
+    if (cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < o->T) {
+        const uint32_t t = cfg->topic;
+        uint8_t* done = (uint8_t*)calloc(N ? N : 1, 1);
+        for (size_t k = 0; k < m; k++) {
+            const uint32_t src = msgs[k].source;
+            if (src >= N || done[src] || joined(o, src, t)) continue;
+            done[src] = 1;
+            bool empty = true;
+            for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1] && empty; r++)
+                if (o->fanout[r] >> t & 1) empty = false;
+            if (empty) {
+                int n = 0;
+                for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1]; r++) {
+                    const uint8_t ef = o->eflags[r];
+                    if (!in_topic(o, (uint64_t)r, t) || !(ef & GSX_EDGE_GOSSIPSUB) || (ef & GSX_EDGE_DIRECT)) continue;
+                    if (!(score0[r] >= o->th.publish_threshold)) continue;
+                    tg[n++] = (uint64_t)r;
+                }
+                orc_rng g = {cfg->seed, 10, src, (uint64_t)t << 24, 0};
+                shuffle_pairs(tg, n, &g);
+                if (n > o->gp.d) n = o->gp.d;
+                for (int i = 0; i < n; i++) o->fanout[tg[i]] |= 1ull << t;
+                if (n > 0) o->fan_has[src] |= 1ull << t;
+            }
+            o->lastpub[(size_t)src * o->T + t] = cfg->now_ns;
+        }
+        free(done);
+    }
     /* gossipsub's Publish Puts every message a node processes into its
      * mcache (gossipsub.go:944); one batch entry in window 0 */
     orc_mc_batch* mcb = NULL;
@@ -1302,6 +1361,7 @@ int orc_default_gossipsub_params(gsx_gossipsub_params* p) { /* DefaultGossipSubP
     p->gossip_retransmission = 3;
     p->iwant_followup_ns = 3LL * 1000000000LL;
     p->gossip_exchange = 0;
+    p->fanout_ttl_ns = 60LL * 1000000000LL;
     return 0;
 }
 
@@ -1331,19 +1391,20 @@ static void add_backoff(orc_engine* o, uint64_t r, uint32_t t, int64_t now, int6
 
 /* getPeers, gossipsub.go:1852-1872: topic peers with the mesh feature that
  * pass the filter, in ascending order, shuffled, truncated to count. */
-enum { F_NOT_MESH = 1, F_NO_BACKOFF = 2, F_NOT_DIRECT = 4, F_OUTBOUND = 8 };
+enum { F_NOT_MESH = 1, F_NO_BACKOFF = 2, F_NOT_DIRECT = 4, F_OUTBOUND = 8, F_NOT_FANOUT = 16 };
 static int get_peers(hb_ctx* c, uint32_t v, uint32_t t, int count, int filter, int score_cmp, double score_ref,
                      uint64_t* out, orc_rng* g) {
     orc_engine* o = c->o;
     int n = 0;
     for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
-        if (!in_topic(o, (uint64_t)r)) continue;
+        if (!in_topic(o, (uint64_t)r, t)) continue;
         const uint8_t ef = o->eflags[r];
         if (!(ef & GSX_EDGE_GOSSIPSUB)) continue; /* gs.feature(GossipSubFeatureMesh, ...) */
         if ((filter & F_NOT_MESH) && hb_in_mesh(o, (uint64_t)r, t)) continue;
         if ((filter & F_NO_BACKOFF) && *hb_backoff(o, (uint64_t)r, t) != 0) continue; /* map presence (:1377) */
         if ((filter & F_NOT_DIRECT) && (ef & GSX_EDGE_DIRECT)) continue;
         if ((filter & F_OUTBOUND) && !(ef & GSX_EDGE_OUTBOUND)) continue;
+        if ((filter & F_NOT_FANOUT) && (o->fanout[r] >> t & 1)) continue;
         const double s = c->cache[r];
         if (score_cmp == 0 && !(s >= score_ref)) continue;
         if (score_cmp == 1 && !(s > score_ref)) continue;
@@ -1484,7 +1545,7 @@ static uint64_t ihave_digest(const uint64_t* ids, size_t n) { /* gsx.h, gsx_goss
 /* emitGossip (gossipsub.go:1669-1723) for (v, t) after its maintenance, with
  * mcache.GetGossipIDs (mcache.go:82-92) over the first HistoryGossip windows */
 static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t* peers, uint64_t** mids,
-                        size_t* mids_cap) {
+                        size_t* mids_cap, bool fan) {
     orc_engine* o = c->o;
     const gsx_gossipsub_params* gp = c->gp;
     size_t L = 0;
@@ -1510,9 +1571,11 @@ static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t*
     if (L > (size_t)gp->max_ihave_length) shuffle_ids(ids, L, g);
     int np = 0;
     for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
-        if (!in_topic(o, (uint64_t)r)) continue;
+        if (!in_topic(o, (uint64_t)r, t)) continue;
         const uint8_t ef = o->eflags[r];
-        if (hb_in_mesh(o, (uint64_t)r, t) || (ef & GSX_EDGE_DIRECT) || !(ef & GSX_EDGE_GOSSIPSUB)) continue;
+        /* exclude: the mesh peers, or the fanout peers for a fanout topic (:1514, :1553) */
+        const bool excl = fan ? (o->fanout[r] >> t & 1) : hb_in_mesh(o, (uint64_t)r, t);
+        if (excl || (ef & GSX_EDGE_DIRECT) || !(ef & GSX_EDGE_GOSSIPSUB)) continue;
         if (!(score_pair(o, (uint64_t)r) >= o->th.gossip_threshold)) continue; /* live score */
         peers[np++] = (uint64_t)r;
     }
@@ -1671,7 +1734,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             const uint32_t v = (uint32_t)o->col[q];
             size_t n = 0;
             for (uint32_t t = 0; t < T; t++) {
-                if (!(tb >> t & 1)) continue;
+                if (!(tb >> t & 1) || !joined(o, u, t)) continue; /* gs.mesh[topic] (:638-641) */
                 for (size_t i = 0; i < nb; i++) {
                     const orc_mc_batch* b = gb[i].b;
                     if (b->topic != t) continue;
@@ -1825,9 +1888,88 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
     return rc;
 }
 
+/* (B) every node handles the GRAFTs then PRUNEs sent to it (ctl[t][pair of
+ * the sender] 1 / 2), senders ascending; PRUNE answers into resp (:718-843) */
+static void hb_receive(orc_engine* o, const gsx_gossipsub_params* gp, const uint8_t* ctl, uint8_t* resp, double* cache,
+                       int64_t now, gsx_heartbeat_out* out) {
+    const uint64_t E = o->E;
+    const uint32_t T = o->T;
+    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q); /* gs.score.Score(p) at handling time */
+    for (uint32_t u = 0; u < o->n_nodes; u++) {
+        for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) { /* q = (u -> v), ascending v */
+            const int64_t r = reverse_pair(o, (uint64_t)q);         /* r = (v -> u) */
+            if (r < 0) continue;
+            const double score = cache[q];
+            /* AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped */
+            if (!(o->eflags[q] & GSX_EDGE_DIRECT) && score < o->th.graylist_threshold) continue;
+            for (uint32_t t = 0; t < T; t++) { /* handleGraft, :718-809 */
+                if (ctl[(size_t)t * E + r] != 1) continue;
+                if (!joined(o, u, t)) continue; /* unknown topic: ignored (:727-733) */
+                if (hb_in_mesh(o, (uint64_t)q, t)) continue;
+                const uint8_t ef = o->eflags[q];
+                if (ef & GSX_EDGE_DIRECT) {
+                    resp[(size_t)t * E + q] = 1;
+                    out->graft_rejected++;
+                    continue;
+                }
+                const int64_t expire = *hb_backoff(o, (uint64_t)q, t);
+                if (expire != 0 && now < expire) {
+                    add_penalty(o, (uint64_t)q, 1);
+                    out->penalties++;
+                    if (now < expire + (gp->graft_flood_threshold_ns - gp->prune_backoff_ns)) {
+                        add_penalty(o, (uint64_t)q, 1);
+                        out->penalties++;
+                    }
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    resp[(size_t)t * E + q] = 1;
+                    out->graft_rejected++;
+                    continue;
+                }
+                if (score < 0) {
+                    resp[(size_t)t * E + q] = 1;
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    out->graft_rejected++;
+                    continue;
+                }
+                int n = 0;
+                for (int64_t x = o->row_ptr[u]; x < o->row_ptr[u + 1]; x++) n += hb_in_mesh(o, (uint64_t)x, t);
+                if (n >= gp->d_hi && !(ef & GSX_EDGE_OUTBOUND)) {
+                    resp[(size_t)t * E + q] = 1;
+                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
+                    out->graft_rejected++;
+                    continue;
+                }
+                graft(o, (uint64_t)q, t, now); /* tracer.Graft, :795 */
+                o->tr_ag[q] |= 1ull << t;
+                out->graft_accepted++;
+            }
+            for (uint32_t t = 0; t < T; t++) /* handlePrune */
+                if (ctl[(size_t)t * E + r] == 2 && joined(o, u, t)) /* (:816-819) */
+                    handle_prune(o, gp, (uint64_t)q, t, now, out);
+        }
+    }
+}
+
+/* (C) the GRAFT senders handle the PRUNE answers, AcceptFrom-gated */
+static void hb_answers(orc_engine* o, const gsx_gossipsub_params* gp, const uint8_t* resp, double* cache, int64_t now,
+                       gsx_heartbeat_out* out) {
+    const uint64_t E = o->E;
+    const uint32_t T = o->T;
+    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q);
+    for (uint32_t v = 0; v < o->n_nodes; v++)
+        for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+            const int64_t q = reverse_pair(o, (uint64_t)r);
+            if (q < 0) continue;
+            if (!(o->eflags[r] & GSX_EDGE_DIRECT) && cache[r] < o->th.graylist_threshold) continue;
+            for (uint32_t t = 0; t < T; t++)
+                if (resp[(size_t)t * E + q] && joined(o, v, t)) handle_prune(o, gp, (uint64_t)r, t, now, out);
+        }
+}
+
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now, uint64_t seed,
                   gsx_heartbeat_out* out) {
     memset(out, 0, sizeof(*out));
+    o->gp = *gp;
     const uint64_t E = o->E;
     const uint32_t T = o->T;
     /* clearBackoff (:1585-1604) */
@@ -1877,76 +2019,45 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     size_t mids_cap = 0;
     /* (A) every node's heartbeat, every joined topic in ascending order:
      * mesh maintenance, then IHAVE gossip, one draw stream per (node, topic) */
-    for (uint32_t v = 0; v < o->n_nodes; v++)
+    for (uint32_t v = 0; v < o->n_nodes; v++) {
         for (uint32_t t = 0; t < T; t++) {
+            if (!joined(o, v, t)) continue; /* gs.mesh holds the joined topics */
             orc_rng g = {seed, 8, v, (tick << 32) | ((uint64_t)t << 24), 0};
             hb_unit(&c, v, t, &g, plst, tmp);
-            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap);
+            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap, false);
         }
-    free(mids);
-    /* (B) receivers: GRAFTs then PRUNEs of each sender, senders ascending */
-    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q); /* gs.score.Score(p) at handling time */
-    for (uint32_t u = 0; u < o->n_nodes; u++) {
-        for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) { /* q = (u -> v), ascending v */
-            const int64_t r = reverse_pair(o, (uint64_t)q);         /* r = (v -> u) */
-            if (r < 0) continue;
-            const double score = cache[q];
-            /* AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped */
-            if (!(o->eflags[q] & GSX_EDGE_DIRECT) && score < o->th.graylist_threshold) continue;
-            for (uint32_t t = 0; t < T; t++) { /* handleGraft, :718-809 */
-                if (ctl[(size_t)t * E + r] != 1) continue;
-                if (hb_in_mesh(o, (uint64_t)q, t)) continue;
-                const uint8_t ef = o->eflags[q];
-                if (ef & GSX_EDGE_DIRECT) {
-                    resp[(size_t)t * E + q] = 1;
-                    out->graft_rejected++;
-                    continue;
-                }
-                const int64_t expire = *hb_backoff(o, (uint64_t)q, t);
-                if (expire != 0 && now < expire) {
-                    add_penalty(o, (uint64_t)q, 1);
-                    out->penalties++;
-                    if (now < expire + (gp->graft_flood_threshold_ns - gp->prune_backoff_ns)) {
-                        add_penalty(o, (uint64_t)q, 1);
-                        out->penalties++;
-                    }
-                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
-                    resp[(size_t)t * E + q] = 1;
-                    out->graft_rejected++;
-                    continue;
-                }
-                if (score < 0) {
-                    resp[(size_t)t * E + q] = 1;
-                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
-                    out->graft_rejected++;
-                    continue;
-                }
-                int n = 0;
-                for (int64_t x = o->row_ptr[u]; x < o->row_ptr[u + 1]; x++) n += hb_in_mesh(o, (uint64_t)x, t);
-                if (n >= gp->d_hi && !(ef & GSX_EDGE_OUTBOUND)) {
-                    resp[(size_t)t * E + q] = 1;
-                    add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
-                    out->graft_rejected++;
-                    continue;
-                }
-                graft(o, (uint64_t)q, t, now); /* tracer.Graft, :795 */
-                o->tr_ag[q] |= 1ull << t;
-                out->graft_accepted++;
+        /* expire fanout for topics not published to in a while (:1517-1524) */
+        for (uint32_t t = 0; t < T; t++) {
+            int64_t* lp = &o->lastpub[(size_t)v * T + t];
+            if (*lp != 0 && *lp + gp->fanout_ttl_ns < now) {
+                for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) o->fanout[r] &= ~(1ull << t);
+                o->fan_has[v] &= ~(1ull << t);
+                *lp = 0;
             }
-            for (uint32_t t = 0; t < T; t++) /* handlePrune */
-                if (ctl[(size_t)t * E + r] == 2) handle_prune(o, gp, (uint64_t)q, t, now, out);
+        }
+        /* maintain the fanout of topics published to but not joined (:1526-1554);
+         * draws h(seed, 8, node, tick << 32 | topic << 24 | 1 << 23 | k) */
+        for (uint32_t t = 0; t < T; t++) {
+            if (!(o->fan_has[v] >> t & 1)) continue;
+            orc_rng g = {seed, 8, v, (tick << 32) | ((uint64_t)t << 24) | (1ull << 23), 0};
+            int have = 0;
+            for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+                if (!(o->fanout[r] >> t & 1)) continue;
+                if (!in_topic(o, (uint64_t)r, t) || cache[r] < o->th.publish_threshold) o->fanout[r] &= ~(1ull << t);
+                else have++;
+            }
+            if (have < gp->d) {
+                const int k = get_peers(&c, v, t, gp->d - have, F_NOT_FANOUT | F_NOT_DIRECT, 0, o->th.publish_threshold,
+                                        tmp, &g);
+                for (int i = 0; i < k; i++) o->fanout[tmp[i]] |= 1ull << t;
+            }
+            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap, true);
         }
     }
-    /* (C) the GRAFT senders handle the PRUNE answers, AcceptFrom-gated */
-    for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q);
-    for (uint32_t v = 0; v < o->n_nodes; v++)
-        for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
-            const int64_t q = reverse_pair(o, (uint64_t)r);
-            if (q < 0) continue;
-            if (!(o->eflags[r] & GSX_EDGE_DIRECT) && cache[r] < o->th.graylist_threshold) continue;
-            for (uint32_t t = 0; t < T; t++)
-                if (resp[(size_t)t * E + q]) handle_prune(o, gp, (uint64_t)r, t, now, out);
-        }
+    free(mids);
+    /* (B) receivers, (C) the PRUNE answers */
+    hb_receive(o, gp, ctl, resp, cache, now, out);
+    hb_answers(o, gp, resp, cache, now, out);
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
     /* (D) the IHAVEs just emitted are answered across the Shift */
@@ -1973,6 +2084,152 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     free(plst);
     free(tmp);
     return rc;
+}
+
+/* ---- topic membership (A13): subscriptions, Join / Leave, fanout export ---- */
+
+int orc_set_gossipsub_params(orc_engine* o, const gsx_gossipsub_params* gp) {
+    o->gp = *gp;
+    return 0;
+}
+
+int orc_set_subscriptions(orc_engine* o, const uint64_t* joined) {
+    if (!o->sub) return GSX_ESTATE;
+    const uint64_t all = o->T >= 64 ? ~0ull : ((1ull << o->T) - 1);
+    for (uint32_t v = 0; v < o->n_nodes; v++) o->sub[v] = joined[v] & all;
+    return 0;
+}
+
+int orc_export_membership(orc_engine* o, uint64_t* joined, uint64_t* fanout, int64_t* lastpub) {
+    if (!o->sub) return GSX_ESTATE;
+    if (joined) memcpy(joined, o->sub, 8 * (size_t)o->n_nodes);
+    if (fanout) memcpy(fanout, o->fanout, 8 * (size_t)o->E);
+    if (lastpub) memcpy(lastpub, o->lastpub, 8 * (size_t)o->n_nodes * o->T);
+    return 0;
+}
+
+/* candidates of Join / fanout: v's mesh-capable topic peers, not direct, not
+ * in the fanout (skip_fanout), live score >= ref; ascending, shuffled, first count */
+static int join_peers(orc_engine* o, uint32_t v, uint32_t t, int count, bool skip_fanout, double ref, uint64_t* out,
+                      orc_rng* g) {
+    int n = 0;
+    for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+        const uint8_t ef = o->eflags[r];
+        if (!in_topic(o, (uint64_t)r, t) || !(ef & GSX_EDGE_GOSSIPSUB) || (ef & GSX_EDGE_DIRECT)) continue;
+        if (skip_fanout && (o->fanout[r] >> t & 1)) continue;
+        if (!(score_pair(o, (uint64_t)r) >= ref)) continue;
+        out[n++] = (uint64_t)r;
+    }
+    shuffle_pairs(out, n, g);
+    if (count >= 0 && n > count) n = count;
+    return n;
+}
+
+static uint64_t row_max_deg(const orc_engine* o) {
+    uint64_t m = 1;
+    for (uint32_t i = 0; i < o->n_nodes; i++)
+        if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > m) m = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+    return m;
+}
+
+/* Join (gossipsub.go:1015-1064) of (node, topic) entries in order: the mesh
+ * from the fanout (negative scores dropped, topped up to D) or getPeers(D);
+ * each mesh peer gets tracer.Graft and a GRAFT, which the peers then handle
+ * (handleGraft, :718-809) and whose PRUNE answers the joiner handles.
+ * Draws h(seed, 11, node, topic << 24 | k). */
+int orc_join(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now, uint64_t seed,
+             gsx_heartbeat_out* out) {
+    memset(out, 0, sizeof(*out));
+    const uint64_t E = o->E;
+    const uint32_t T = o->T;
+    for (size_t i = 0; i < n; i++)
+        if (nodes[i] >= o->n_nodes || topics[i] >= T) return GSX_ERANGE;
+    uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    uint8_t* resp = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
+    uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * row_max_deg(o));
+    const int D = o->gp.d;
+    /* the call's subscriptions are announced first (a synchronous round: every
+     * joiner sees the others' new subscriptions) */
+    uint8_t* todo = (uint8_t*)calloc(n ? n : 1, 1);
+    for (size_t i = 0; i < n; i++)
+        if (!joined(o, nodes[i], topics[i])) { /* (a repeated entry finds it joined) */
+            o->sub[nodes[i]] |= 1ull << topics[i];
+            todo[i] = 1;
+        }
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t v = nodes[i], t = topics[i];
+        if (!todo[i]) continue;
+        orc_rng g = {seed, 11, v, (uint64_t)t << 24, 0};
+        if (o->fan_has[v] >> t & 1) {
+            int have = 0;
+            for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+                if (!(o->fanout[r] >> t & 1)) continue;
+                if (score_pair(o, (uint64_t)r) < 0) o->fanout[r] &= ~(1ull << t);
+                else have++;
+            }
+            if (have < D) {
+                const int k = join_peers(o, v, t, D - have, true, 0.0, tmp, &g);
+                for (int j = 0; j < k; j++) o->fanout[tmp[j]] |= 1ull << t;
+            }
+        } else {
+            const int k = join_peers(o, v, t, D, false, 0.0, tmp, &g);
+            for (int j = 0; j < k; j++) o->fanout[tmp[j]] |= 1ull << t; /* (the new mesh, staged) */
+        }
+        for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) { /* the mesh: tracer.Graft + sendGraft */
+            if (!(o->fanout[r] >> t & 1)) continue;
+            o->fanout[r] &= ~(1ull << t);
+            graft(o, (uint64_t)r, t, now);
+            ctl[(size_t)t * E + r] = 1;
+            out->grafts++;
+        }
+        o->fan_has[v] &= ~(1ull << t);
+        o->lastpub[(size_t)v * T + t] = 0;
+    }
+    free(todo);
+    gsx_gossipsub_params gp = o->gp;
+    hb_receive(o, &gp, ctl, resp, cache, now, out);
+    hb_answers(o, &gp, resp, cache, now, out);
+    for (uint64_t r = 0; r < E; r++)
+        for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
+    free(ctl);
+    free(resp);
+    free(cache);
+    free(tmp);
+    return 0;
+}
+
+/* Leave (gossipsub.go:1066-1082): every mesh peer gets tracer.Prune and a
+ * PRUNE (handlePrune at the peer, which backs the leaver off). */
+int orc_leave(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now,
+              gsx_heartbeat_out* out) {
+    memset(out, 0, sizeof(*out));
+    const uint64_t E = o->E;
+    const uint32_t T = o->T;
+    for (size_t i = 0; i < n; i++)
+        if (nodes[i] >= o->n_nodes || topics[i] >= T) return GSX_ERANGE;
+    uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    uint8_t* resp = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t v = nodes[i], t = topics[i];
+        if (!joined(o, v, t)) continue;
+        o->sub[v] &= ~(1ull << t);
+        for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
+            if (!hb_in_mesh(o, (uint64_t)r, t)) continue;
+            prune(o, (uint64_t)r, t);
+            ctl[(size_t)t * E + r] = 2;
+            out->prunes++;
+        }
+    }
+    gsx_gossipsub_params gp = o->gp;
+    hb_receive(o, &gp, ctl, resp, cache, now, out);
+    for (uint64_t r = 0; r < E; r++)
+        for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
+    free(ctl);
+    free(resp);
+    free(cache);
+    return 0;
 }
 
 int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,

@@ -57,6 +57,13 @@ int orc_default_gossipsub_params(gsx_gossipsub_params* p);
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now_ns, uint64_t seed,
                   gsx_heartbeat_out* out);
 /* gsx_hb_trace_words of the last orc_heartbeat (always recorded). */
+int orc_set_gossipsub_params(orc_engine* o, const gsx_gossipsub_params* gp);
+int orc_set_subscriptions(orc_engine* o, const uint64_t* joined);
+int orc_export_membership(orc_engine* o, uint64_t* joined, uint64_t* fanout, int64_t* lastpub);
+int orc_join(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now, uint64_t seed,
+             gsx_heartbeat_out* out);
+int orc_leave(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now,
+              gsx_heartbeat_out* out);
 int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
                        uint64_t* handled_prune);
 int orc_export_backoff(orc_engine* o, int64_t* out);

@@ -60,6 +60,12 @@ _SIG = {
     "orc_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "orc_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
     "orc_mcache_clear": (C.c_int, [C.c_void_p]),
+    "orc_set_gossipsub_params": (C.c_int, [C.c_void_p, P(abi.GossipSubParams)]),
+    "orc_set_subscriptions": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "orc_export_membership": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_int64)]),
+    "orc_join": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, C.c_uint64,
+                           P(abi.HeartbeatOut)]),
+    "orc_leave": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, P(abi.HeartbeatOut)]),
     "orc_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
     "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
@@ -126,6 +132,7 @@ class Oracle:
     def load_overlay(self, row_ptr, col, edge_flags=None, node_ips=None):
         row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
         col = np.ascontiguousarray(col, dtype=np.int32)
+        self.n_nodes = len(row_ptr) - 1
         ef = None if edge_flags is None else np.ascontiguousarray(edge_flags, dtype=np.uint8)
         ips = None if node_ips is None else np.ascontiguousarray(node_ips, dtype=np.uint32).reshape(-1)
         self._chk(
@@ -153,6 +160,37 @@ class Oracle:
 
     def set_gossipsub_params(self, gp):
         self.gp = gp
+        self._chk(self.lib.orc_set_gossipsub_params(self.h, C.byref(gp)), "orc_set_gossipsub_params")
+
+    def set_subscriptions(self, joined):
+        j = np.ascontiguousarray(joined, dtype=np.uint64)
+        self._chk(self.lib.orc_set_subscriptions(self.h, _p(j, C.c_uint64)), "orc_set_subscriptions")
+
+    def export_membership(self):
+        """-> (joined [N] u64, fanout [E] u64 topic bits, lastpub [N, T] i64)"""
+        n = self.n_nodes
+        j = np.empty(n, dtype=np.uint64)
+        f = np.empty(self.n_pairs, dtype=np.uint64)
+        lp = np.empty((n, self.n_topics), dtype=np.int64)
+        self._chk(self.lib.orc_export_membership(self.h, _p(j, C.c_uint64), _p(f, C.c_uint64), _p(lp, C.c_int64)),
+                  "orc_export_membership")
+        return j, f, lp
+
+    def join(self, nodes, topics, now, seed):
+        nd = np.ascontiguousarray(nodes, dtype=np.uint32)
+        tp = np.ascontiguousarray(topics, dtype=np.uint32)
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.orc_join(self.h, _p(nd, C.c_uint32), _p(tp, C.c_uint32), len(nd), now, seed, C.byref(out)),
+                  "orc_join")
+        return out
+
+    def leave(self, nodes, topics, now):
+        nd = np.ascontiguousarray(nodes, dtype=np.uint32)
+        tp = np.ascontiguousarray(topics, dtype=np.uint32)
+        out = abi.HeartbeatOut()
+        self._chk(self.lib.orc_leave(self.h, _p(nd, C.c_uint32), _p(tp, C.c_uint32), len(nd), now, C.byref(out)),
+                  "orc_leave")
+        return out
 
     def heartbeat(self, tick, now, seed):
         out = abi.HeartbeatOut()
