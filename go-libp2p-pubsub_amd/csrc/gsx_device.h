@@ -237,6 +237,7 @@ hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st);
+hipError_t launch_prop_dup_rows(const PropState& ps, uint64_t* out, hipStream_t st);
 hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st);
 
 // ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------

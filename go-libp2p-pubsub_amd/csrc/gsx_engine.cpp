@@ -2236,6 +2236,27 @@ int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from) {
     return GSX_OK;
 }
 
+int gsx_prop_duplicates(gsx_engine* e, uint64_t* rows, size_t n_words) {
+    if (!e || !rows) return GSX_EINVAL;
+    if (!e->prop.have_last) return fail(e, GSX_ESTATE, "no gsx_propagate call yet");
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (e->sharded()) return fail(e, GSX_EINVAL, "duplicate rows are exported by unsharded engines only");
+    gsx::PropState ps = e->prop.last;
+    if (!ps.from_mask)
+        return fail(e, GSX_ESTATE, "first deliverers were not tracked in the last call (gsx_prop_set_tracking)");
+    if (n_words != ps.n_words) return fail(e, GSX_EINVAL, "n_words must be the last call's words (ceil(m / 64))");
+    ps.n_rows = e->prop.rows_valid;
+    const size_t cells = (size_t)e->E * ps.n_words;
+    if (cells == 0) return GSX_OK;
+    uint64_t* d = nullptr;
+    if (int rc = dalloc(e, &d, cells)) return rc;
+    HIPCHK(e, gsx::launch_prop_dup_rows(ps, d, e->stream));
+    HIPCHK(e, hipMemcpyAsync(rows, d, 8 * cells, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    (void)hipFree(d);
+    return GSX_OK;
+}
+
 int gsx_shard_counts(gsx_engine* e, uint64_t* n_send, uint64_t* n_recv) {
     if (!e) return GSX_EINVAL;
     if (n_send) *n_send = e->n_send;

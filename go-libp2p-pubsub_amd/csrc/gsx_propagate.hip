@@ -1126,6 +1126,54 @@ __global__ __launch_bounds__(256) void k_prop_hops_export(PropState ps, uint8_t*
     }
 }
 
+// Duplicate receipts per pair (DUPLICATE_MESSAGE, trace.go:136-164): bit m
+// of row q = (u -> v) when v sent u a copy of m that u had already seen
+// (pushMsg's seenMessage test, pubsub.go:1046-1060).  v sends m at hop h + 1
+// when it forwarded m at hop h (frontier-history row h: published at h = 0,
+// accepted first receipts otherwise) and the call ran that hop (h <
+// max_hops), through the eligibility of its pair (v -> u) or RandomSub's
+// draw, never back to the peer it first got m from (from_mask of (v -> u))
+// nor to m's origin (u's row 0).  The copy that gave u the message is the
+// one recorded in from_mask of q; every other copy is a duplicate.  A pair
+// whose copies u's AcceptFrom drops has pin NO_PAIR: no trace, as in
+// pubsub.go:1014-1017.
+__global__ __launch_bounds__(256) void k_prop_dup_rows(PropState ps, uint64_t* __restrict__ out) {
+    const uint32_t W = ps.n_words;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint32_t h_end = ps.n_rows < ps.max_hops ? ps.n_rows : ps.max_hops;  // rows forwarded in a hop that ran
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        const uint32_t pn = ps.pin[q];
+        const uint32_t r = ps.rev[q];
+        const uint32_t u = ps.pair_obs[q];
+        const uint32_t v = pn & PIN_NODE_MASK;
+        const bool sends = pn != NO_PAIR && r != NO_PAIR;
+        const uint8_t fw = sends ? (uint8_t)(pn >> PIN_FWD_SHIFT) : 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t d = 0;
+            if (sends) {
+                uint64_t fset = 0, own = 0;
+                for (uint32_t h = 0; h < h_end; ++h) {
+                    if (!occ_bit(ps.occ + (size_t)h * occ_row, v)) continue;
+                    const uint64_t x = ps.hist[(size_t)h * ps.n_nodes * W + (size_t)v * W + w];
+                    fset |= x;
+                    if (h == 0) own = x;
+                }
+                uint64_t el = elig_word(fw, own);
+                if (ps.sel) el |= ps.sel[(size_t)r * W + w];
+                const uint64_t own_u = occ_bit(ps.occ, u) ? ps.hist[(size_t)u * W + w] : 0;
+                d = fset & el & ~ps.from_mask[(size_t)r * W + w] & ~own_u & ~ps.from_mask[q * W + w];
+            }
+            out[q * W + w] = d;
+        }
+    }
+}
+hipError_t launch_prop_dup_rows(const PropState& ps, uint64_t* out, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_dup_rows, dim3((unsigned)std::min<uint64_t>((ps.n_pairs + 255) / 256, 4096)), dim3(256), 0,
+                       st, ps, out);
+    return hipGetLastError();
+}
+
 // After a call with dropped messages: keep their hop-1 receipts for
 // gsx_prop_results, and (gossipsub) take them out of the seen rows the
 // message cache keeps, since Publish Puts only what a node processed

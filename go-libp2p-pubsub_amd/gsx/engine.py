@@ -178,6 +178,14 @@ class Engine:
 
     _track = True
 
+    def prop_duplicates(self, n_msgs: int) -> np.ndarray:
+        """gsx_prop_duplicates: [n_pairs, ceil(m / 64)] u64, bit m of row q = the
+        pair's neighbour sent its observer a copy of message m it had already seen."""
+        W = (n_msgs + 63) // 64
+        rows = np.zeros((self.n_pairs, W), dtype=np.uint64)
+        self._chk(self.lib.gsx_prop_duplicates(self.h, _ptr(rows, C.c_uint64), W), "gsx_prop_duplicates")
+        return rows
+
     def set_prop_tracking(self, first_deliverers: bool):
         """gsx_prop_set_tracking: keep first-deliverer rows (results' first_from) or only counts."""
         self._chk(self.lib.gsx_prop_set_tracking(self.h, 1 if first_deliverers else 0), "gsx_prop_set_tracking")

@@ -22,10 +22,12 @@ already computes on the GPU into that stream:
   messages too) — or, for a message validation does not accept, REJECT_MESSAGE
   there with its reason (PushLocal's validation, validation.go:216-342); then one
   DELIVER_MESSAGE (or REJECT_MESSAGE with its reason) per (node, message) first
-  receipt, ``receivedFrom`` = the first deliverer.  DUPLICATE_MESSAGE events
-  (one per further copy, trace.go:136-164) are not in this stream: the engine
-  counts duplicates (gsx_prop_out.duplicates) but does not record who sent
-  each copy; the stream is partial in exactly that class.
+  receipt, ``receivedFrom`` = the first deliverer; then, given the call's
+  duplicate rows (gsx_prop_duplicates), one DUPLICATE_MESSAGE per further copy
+  a node pushed (pushMsg's seenMessage branch, pubsub.go:1052-1056 ->
+  trace.go:136-164), ``receivedFrom`` = the copy's sender, stamped with its
+  arrival.  Copies dropped by AcceptFrom (graylisted senders) are never
+  pushed and yield nothing, as in pubsub.go:1014-1017.
 
 Field numbers and wire types follow ``pb/trace.proto:5-104``; fields are
 written in field-number order, as the gogo marshaller does.  This is host-side
@@ -227,9 +229,14 @@ def delivery_trace(
     msg_id: Optional[Callable[[int, int], bytes]] = None,
     node_base: int = 0,
     validation_delay_ns: int = 0,
+    dup_rows=None,
+    row_ptr=None,
+    col=None,
 ) -> Iterator[bytes]:
-    """PUBLISH_MESSAGE / DELIVER_MESSAGE / REJECT_MESSAGE events of one
-    propagation on ``topic``, ordered by (message, source first, node).
+    """PUBLISH_MESSAGE / DELIVER_MESSAGE / REJECT_MESSAGE (and, with
+    ``dup_rows``, DUPLICATE_MESSAGE) events of one propagation on ``topic``,
+    ordered by (message, source first, node), the duplicates of a message
+    after its first receipts, by (receiving pair).
 
     ``hop`` / ``first_from`` are prop_results() rows ([m, n] arrival hop, 0xFF
     = never, 0 at the source; first deliverer, global id); ``msgs`` the
@@ -240,7 +247,11 @@ def delivery_trace(
     (validation.go:320-383; it is seen but never delivered or forwarded).  The
     event time is the end of validation: ``now + hop * (hop_latency +
     validation_delay)``.  ``node_base`` is the shard's first global node id
-    for range-sharded results.
+    for range-sharded results.  ``dup_rows`` ([n_pairs, words] u64 of
+    gsx_prop_duplicates, unsharded only) with the overlay's ``row_ptr`` /
+    ``col``: a duplicate copy sent by v left v when its validation ended and
+    arrived one hop latency later, ``now + h * hop_latency + (h - 1) *
+    validation_delay`` with h = hop(v) + 1 (no validation for duplicates).
     """
     if first_from is None:
         raise ValueError("delivery_trace needs first-deliverer rows (gsx_prop_set_tracking on)")
@@ -248,6 +259,11 @@ def delivery_trace(
     first_from = np.asarray(first_from)
     mid = msg_id or default_msg_id
     step = hop_latency_ns + validation_delay_ns
+    if dup_rows is not None:
+        if node_base != 0 or row_ptr is None or col is None:
+            raise ValueError("duplicate rows need the unsharded overlay (row_ptr, col)")
+        dup_rows = np.asarray(dup_rows, dtype=np.uint64)
+        d_obs, d_peer = pair_endpoints(row_ptr, col)
     for m in range(hop.shape[0]):
         v = int(msgs["validation"][m])
         src = int(msgs["source"][m])
@@ -266,3 +282,10 @@ def delivery_trace(
                 yield deliver_event(node, ident, topic, frm, ts)
             else:
                 yield reject_event(node, ident, frm, REJECT_REASON[v], topic, ts)
+        if dup_rows is not None:
+            bits = (dup_rows[:, m // 64] >> np.uint64(m % 64)) & np.uint64(1)
+            for q in np.nonzero(bits)[0].tolist():
+                sender = int(d_peer[q])
+                h = int(hop[m, sender]) + 1
+                ts = now + h * hop_latency_ns + (h - 1) * validation_delay_ns
+                yield duplicate_event(peer_id(int(d_obs[q])), ident, peer_id(sender), topic, ts)

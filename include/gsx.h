@@ -425,6 +425,18 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
  * none), laid out [message][node] over this engine's nodes.  Either pointer
  * may be NULL. */
 int gsx_prop_results(gsx_engine* e, uint8_t* hop, int32_t* first_from);
+/* Duplicate receipts of the last propagation (the copies pushMsg traces as
+ * DuplicateMessage, pubsub.go:1046-1060 -> trace.go:136-164): rows[pair *
+ * n_words + w] bit b is set when the pair's neighbour sent its observer a
+ * copy of message 64 * w + b that the observer had already seen.  The copy
+ * arrived at hop hop(message, neighbour) + 1.  Copies the observer's
+ * AcceptFrom drops (graylisted senders) are not duplicates: they are never
+ * pushed.  The popcount over all rows equals gsx_prop_out.duplicates.  Needs
+ * first-deliverer tracking (gsx_prop_set_tracking) in that call, an
+ * unsharded engine, and n_words = ceil(m / 64) of the call; replaces the
+ * reference's per-copy tracer call with one export (f4).  Host buffer of
+ * n_pairs * n_words u64. */
+int gsx_prop_duplicates(gsx_engine* e, uint64_t* rows, size_t n_words);
 /* Whether propagation keeps, per pair, the messages its observer first got
  * from the neighbour (the deliveryRecord's first deliverer, score.go:833-854)
  * for gsx_prop_results' first_from.  On by default.  Off, a call keeps only

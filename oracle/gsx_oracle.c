@@ -150,6 +150,13 @@ struct orc_engine {
     int64_t* q_head;
     int64_t* q_tail;
     uint64_t n_alive;
+
+    /* duplicate receipts of the last propagation (orc_prop_set_dup_tracking):
+     * [pair (u -> v)][word] bit per message v sent u after u had it */
+    bool dup_track;
+    uint64_t* dup_rows;
+    size_t dup_words;
+    uint64_t dup_E;
 };
 
 /* ------------------------------------------------------------------------ */
@@ -312,6 +319,7 @@ void orc_destroy(orc_engine* o) {
     free(o->whitelist);
     free(o->eflags);
     free(o->backoff);
+    free(o->dup_rows);
     orc_mcache_clear(o);
     free(o->mc);
     free(o->ihave_len);
@@ -1170,6 +1178,11 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return GSX_EINVAL;
     memset(out, 0, sizeof(*out));
     const uint32_t N = o->n_nodes;
+    free(o->dup_rows);
+    o->dup_rows = NULL;
+    o->dup_words = (m + 63) / 64;
+    o->dup_E = o->E;
+    if (o->dup_track) o->dup_rows = (uint64_t*)calloc(o->E * o->dup_words + 1, sizeof(uint64_t));
     uint8_t* hop = (uint8_t*)malloc(N ? N : 1);
     int32_t* from = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
     uint32_t* frontier = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
@@ -1307,6 +1320,10 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
                     }
                 } else { /* seenMessage -> DuplicateMessage, validated when the first copy's validation ended */
                     out->duplicates++;
+                    if (o->dup_rows) { /* tracer.DuplicateMessage (pubsub.go:1052-1056, trace.go:136-164) */
+                        const int64_t qd = qr >= 0 ? qr : reverse_pair(o, arr[a].r);
+                        if (qd >= 0) o->dup_rows[(size_t)qd * o->dup_words + k / 64] |= 1ull << (k % 64);
+                    }
                     if (q >= 0 && !dropped)
                         mark_duplicate(o, (uint64_t)q, cfg->topic, true,
                                        arrival_time(cfg, hop[u]) + (hop[u] ? cfg->validation_delay_ns : 0),
@@ -1335,6 +1352,18 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
     free(scratch);
     free(arr);
     free(score0);
+    return 0;
+}
+
+int orc_prop_set_dup_tracking(orc_engine* o, int on) {
+    o->dup_track = on != 0;
+    return 0;
+}
+
+int orc_prop_duplicates(orc_engine* o, uint64_t* rows, size_t n_words) {
+    if (!o->dup_rows || o->dup_E != o->E) return GSX_ESTATE;
+    if (n_words != o->dup_words) return GSX_EINVAL;
+    memcpy(rows, o->dup_rows, sizeof(uint64_t) * o->E * n_words);
     return 0;
 }
 

@@ -52,6 +52,11 @@ int orc_set_thresholds(orc_engine* o, const gsx_thresholds* t);
  * hop/from: optional [m][n_nodes] outputs. */
 int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
                   uint8_t* hop, int32_t* from);
+/* With dup tracking on, orc_propagate records which copies were duplicates
+ * (the DuplicateMessage tracer calls, pubsub.go:1052-1056) per receiving
+ * pair, laid out as gsx_prop_duplicates' rows. */
+int orc_prop_set_dup_tracking(orc_engine* o, int on);
+int orc_prop_duplicates(orc_engine* o, uint64_t* rows, size_t n_words);
 /* Heartbeat round (gossipsub.go:1303-1604, 718-859) under the contract of gsx.h. */
 int orc_default_gossipsub_params(gsx_gossipsub_params* p);
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now_ns, uint64_t seed,

@@ -32,6 +32,8 @@ _SIG = {
     "orc_load_overlay": (
         C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint8), P(C.c_uint32)]),
     "orc_set_thresholds": (C.c_int, [C.c_void_p, P(abi.Thresholds)]),
+    "orc_prop_set_dup_tracking": (C.c_int, [C.c_void_p, C.c_int]),
+    "orc_prop_duplicates": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
     "orc_propagate": (
         C.c_int,
         [C.c_void_p, C.c_void_p, C.c_size_t, P(abi.PropConfig), P(abi.PropOut), P(C.c_uint8), P(C.c_int32)],
@@ -157,6 +159,17 @@ class Oracle:
             "orc_propagate",
         )
         return out, hop, frm
+
+    def set_dup_tracking(self, on: bool = True):
+        """Record which copies of the next propagations are duplicates (orc_prop_duplicates)."""
+        self._chk(self.lib.orc_prop_set_dup_tracking(self.h, 1 if on else 0), "orc_prop_set_dup_tracking")
+
+    def prop_duplicates(self, n_msgs: int) -> np.ndarray:
+        """[n_pairs, ceil(m / 64)] u64 duplicate receipts of the last propagation (gsx_prop_duplicates' layout)."""
+        W = (n_msgs + 63) // 64
+        rows = np.zeros((self.n_pairs, W), dtype=np.uint64)
+        self._chk(self.lib.orc_prop_duplicates(self.h, _p(rows, C.c_uint64), W), "orc_prop_duplicates")
+        return rows
 
     def set_gossipsub_params(self, gp):
         self.gp = gp

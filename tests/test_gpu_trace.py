@@ -1,5 +1,5 @@
 """Trace export from GPU results (gsx/trace.py): the GRAFT /
-PRUNE stream of a heartbeat and the DELIVER_MESSAGE / REJECT_MESSAGE stream of a propagation
+PRUNE stream of a heartbeat and the DELIVER_MESSAGE / REJECT_MESSAGE / DUPLICATE_MESSAGE stream of a propagation
 are byte-identical to the streams built from the oracle's results."""
 import numpy as np
 import pytest
@@ -21,9 +21,16 @@ def test_heartbeat_trace_gpu_equals_oracle(gpu_ok):
     assert len(g[0]) > 0 and g[0] == w[0]
 
 
-@pytest.mark.parametrize("invalid,delay_ms", [(0.0, 0.0), (0.3, 0.0), (0.3, 4.0)])
-def test_delivery_trace_gpu_equals_oracle(gpu_ok, invalid, delay_ms):
+@pytest.mark.parametrize("case", test_trace_cases := __import__("test_trace").CASES)
+def test_delivery_trace_gpu_equals_oracle(gpu_ok, case):
+    """PUBLISH / DELIVER / REJECT / DUPLICATE streams (gsx_prop_duplicates for the
+    DUPLICATE events) byte-equal to the oracle's, for every router, graylisted
+    senders and a hop limit."""
+    invalid, delay_ms, router, gray, max_hops = case
     T = len(tc.TOPICS)
-    g = tc.delivery_stream(gsx.Engine(T), invalid=invalid, delay_ms=delay_ms)[0]
-    w = tc.delivery_stream(orc.Oracle(T), invalid=invalid, delay_ms=delay_ms)[0]
-    assert len(g) > 0 and g == w
+    kw = dict(invalid=invalid, delay_ms=delay_ms, router=router, gray=gray, max_hops=max_hops)
+    g = tc.delivery_stream(gsx.Engine(T), **kw)
+    w = tc.delivery_stream(orc.Oracle(T), **kw)
+    assert np.array_equal(g[5], w[5])
+    assert g[4].duplicates == w[4].duplicates == int(sum(bin(int(x)).count("1") for x in g[5].ravel()))
+    assert len(g[0]) > 0 and g[0] == w[0]

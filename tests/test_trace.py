@@ -139,21 +139,42 @@ def test_heartbeat_trace_matches_counters():
     assert out["graft_rejected"] > 0 and int(np.count_nonzero(sg & hp)) > 0  # rejected: GRAFT then PRUNE
 
 
-@pytest.mark.parametrize("invalid,delay_ms", [(0.0, 0.0), (0.3, 0.0), (0.3, 4.0)])
-def test_delivery_trace_matches_results(invalid, delay_ms):
-    buf, hop, frm, ms = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid, delay_ms=delay_ms)
+CASES = [  # (invalid, delay_ms, router, gray, max_hops)
+    (0.0, 0.0, abi.GSX_ROUTER_GOSSIPSUB, False, 40),
+    (0.3, 0.0, abi.GSX_ROUTER_GOSSIPSUB, False, 40),
+    (0.3, 4.0, abi.GSX_ROUTER_GOSSIPSUB, False, 40),
+    (0.3, 0.0, abi.GSX_ROUTER_GOSSIPSUB, True, 40),
+    (0.0, 0.0, abi.GSX_ROUTER_FLOODSUB, False, 3),
+    (0.2, 2.0, abi.GSX_ROUTER_RANDOMSUB, False, 40),
+]
+
+
+@pytest.mark.parametrize("invalid,delay_ms,router,gray,max_hops", CASES)
+def test_delivery_trace_matches_results(invalid, delay_ms, router, gray, max_hops):
+    """PUBLISH / DELIVER / REJECT events follow the first receipts; one
+    DUPLICATE per further pushed copy (as many as the call's duplicates
+    counter), each from a neighbour that had the message one hop earlier and
+    to a node that had already seen it, stamped with the copy's arrival."""
+    buf, hop, frm, ms, out, dup = tc.delivery_stream(orc.Oracle(len(tc.TOPICS)), invalid=invalid, delay_ms=delay_ms,
+                                                     router=router, gray=gray, max_hops=max_hops)
     ev = [TE.FromString(e) for e in tr.read_delimited(buf)]
     recv = (hop != 0xFF) & (hop != 0)
-    assert len(ev) == int(recv.sum()) + 2 * len(ms) > 0
+    n_dup = [int(((dup[:, m // 64] >> np.uint64(m % 64)) & np.uint64(1)).sum()) for m in range(len(ms))]
+    assert sum(n_dup) == out.duplicates > 0
+    assert len(ev) == int(recv.sum()) + 2 * len(ms) + sum(n_dup)
+    if gray:
+        assert out.graylisted > 0
     # per message: the source's PUBLISH_MESSAGE and its own DELIVER (REJECT when not accepted) first
-    pub, rest = [], []
+    pub, rest, dups = [], [], []
     k = 0
     for m in range(len(ms)):
         pub.append((m, ev[k], ev[k + 1]))
         n = int(recv[m].sum())
         rest.extend(ev[k + 2:k + 2 + n])
-        k += 2 + n
+        dups.append(ev[k + 2 + n:k + 2 + n + n_dup[m]])
+        k += 2 + n + n_dup[m]
     now = tc.pc.T0 + 3 * tc.pc.S
+    lat, dly = 10 * abi.MILLISECOND, int(delay_ms * abi.MILLISECOND)
     for m, p, d in pub:
         src = tr.default_peer_id(int(ms["source"][m]))
         mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
@@ -169,7 +190,7 @@ def test_delivery_trace_matches_results(invalid, delay_ms):
         v = int(ms["validation"][m])
         mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
         assert e.peerID == tr.default_peer_id(u)
-        assert e.timestamp == tc.pc.T0 + 3 * tc.pc.S + int(hop[m, u]) * int((10 + delay_ms) * abi.MILLISECOND)
+        assert e.timestamp == now + int(hop[m, u]) * (lat + dly)
         if v == abi.GSX_VALIDATION_ACCEPT:
             d = e.deliverMessage
             assert e.type == 3 and not e.HasField("rejectMessage")
@@ -180,6 +201,16 @@ def test_delivery_trace_matches_results(invalid, delay_ms):
         assert d.messageID == mid and d.receivedFrom == tr.default_peer_id(int(frm[m, u]))
         assert d.topic == tc.TOPICS[1]
     assert (n_rej > 0) == (invalid > 0)
+    node = {tr.default_peer_id(i): i for i in range(hop.shape[1])}
+    for m in range(len(ms)):
+        mid = tr.default_msg_id(int(ms["source"][m]), int(ms["msg_id"][m]))
+        for e in dups[m]:
+            assert e.type == 2 and e.duplicateMessage.messageID == mid and e.duplicateMessage.topic == tc.TOPICS[1]
+            u, v = node[e.peerID], node[e.duplicateMessage.receivedFrom]
+            h = int(hop[m, v]) + 1  # the sender had it one hop earlier
+            assert hop[m, v] != 0xFF and h <= max_hops and u != int(ms["source"][m])
+            assert hop[m, u] < h or (hop[m, u] == h and frm[m, u] != v)  # u had already seen it
+            assert e.timestamp == now + h * lat + (h - 1) * dly
 
 
 def test_delivery_trace_needs_first_deliverers():
