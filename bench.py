@@ -504,6 +504,32 @@ def adversarial_leg(args, rank, world, local, dist, dev):
     return out
 
 
+def dropin_leg(args):
+    """tools/dropin_latency.cpp (built here with g++ against libgsx.so) in a child
+    process: Score() / tracer-call / refreshScores() latency of a single router's
+    peerScore on the engine, the per-call path a cgo shim takes."""
+    import subprocess
+
+    root = os.path.dirname(os.path.abspath(__file__))
+    src = os.path.join(root, "tools", "dropin_latency.cpp")
+    libdir = os.path.join(root, "go-libp2p-pubsub_amd", "gsx")
+    exe = os.path.join(root, "tools", "dropin_latency")
+    try:
+        if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+            subprocess.run(["g++", "-std=c++17", "-O2", src, f"-L{libdir}", "-lgsx", f"-Wl,-rpath,{libdir}", "-o", exe],
+                           check=True, timeout=120)
+        out = {}
+        for k in (100, 1000):
+            r = subprocess.run([exe, str(k), "2000"], capture_output=True, text=True, timeout=120, check=True)
+            out[f"peers_{k}"] = json.loads(r.stdout.strip().splitlines()[-1])
+        out["note"] = ("per call through include/gsx_pubsub.hpp on one GPU engine holding one router's peers; "
+                       "Score() with no change since the last is a host lookup, after a tracer call it re-scores "
+                       "the observer's row on the GPU and copies the vector back")
+        return out
+    except (subprocess.SubprocessError, OSError, ValueError) as ex:
+        return {"error": str(ex)[:300]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -526,6 +552,8 @@ def main():
     ap.add_argument("--hb-settle", type=int, default=8,
                     help="untimed heartbeat rounds before the timed ones (the synthesized meshes rebalance)")
     ap.add_argument("--adv-peers", type=int, default=4_000_000, help="cfg5 adversarial overlay (0: skip)")
+    ap.add_argument("--no-dropin", dest="dropin", action="store_false",
+                    help="skip the drop-in scorer latency leg (tools/dropin_latency.cpp)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on one GPU: all ranks on device 0, gloo (host-staged) instead of RCCL")
     args = ap.parse_args()
@@ -723,6 +751,9 @@ def main():
         }
         del o, st
 
+    # ---- drop-in boundary: per-call latency of one router's scorer (gsx_pubsub.hpp) ----
+    dropin = dropin_leg(args) if (rank == 0 and world == 1 and args.dropin) else None
+
     line = {
         "metric": METRIC,
         "value": value,
@@ -768,6 +799,7 @@ def main():
         "propagation": prop,
         "heartbeat": hb,
         "adversarial": adv,
+        "dropin": dropin,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

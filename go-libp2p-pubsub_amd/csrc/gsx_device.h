@@ -419,6 +419,14 @@ hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------
 hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st);
 hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t now, bool refresh, hipStream_t st);
+struct DevIpMove {
+    uint64_t pair;
+    uint32_t g0, g1;  // the pair's new (observer, IP) groups, IPG_WL flagged, IPG_NONE for none
+};
+hipError_t launch_set_ips(const DevState& s, const DevIpMove* mv, const uint32_t* group_off, uint32_t n_groups,
+                          hipStream_t st);
+hipError_t launch_mark_rows(const int64_t* row_ptr, const uint32_t* obs, uint32_t n, uint8_t* mask, uint8_t val,
+                            hipStream_t st);
 hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const uint8_t* only, hipStream_t st);
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
                                const uint32_t* group_off, uint32_t n_groups, hipStream_t st);

@@ -23,6 +23,7 @@ namespace {
 
 constexpr int64_t kSecond = 1000000000LL;
 constexpr int64_t kTimeCacheDuration = 120 * kSecond;  // pubsub.go:30
+constexpr uint64_t kHostScoreMax = 1u << 16;  // engines up to this many pairs keep a host copy of the scores
 
 bool invalid_number(double x) { return std::isnan(x) || std::isinf(x); }
 
@@ -256,6 +257,31 @@ struct gsx_engine {
     bool staged_inflight = false;
 
     bool scores_valid = false;
+    // Incremental re-scoring (gsx_score after events): an event touches only
+    // its observer's state (the pair's counters, the observer's IP counts), so
+    // when the scores were exact before a flush, only the flushed observers'
+    // rows are re-scored (dirty_only + dirty_obs), through a pair mask.
+    bool dirty_only = false;
+    std::vector<uint32_t> dirty_obs;
+    uint8_t* d_smask = nullptr;       // [pair] mask for launch_score_subset (kept all-zero between uses)
+    uint32_t* d_dirty_obs = nullptr;  // observer list of the marking kernel
+    size_t d_dirty_obs_cap = 0;
+    // Host copy of the score vector for per-call Score() (engines up to
+    // kHostScoreMax pairs, e.g. one router's peers): valid while no kernel has
+    // written scores since it was taken (score_writes == h_score_tag).
+    std::vector<double> h_score;
+    uint64_t score_writes = 0, h_score_tag = ~0ull;
+    bool dirty_zeroed = true;  // d_smask not cleared yet
+    void invalidate_scores() {
+        scores_valid = false;
+        dirty_only = false;
+        dirty_obs.clear();
+    }
+    void scores_exact() {  // every score was just computed
+        scores_valid = true;
+        dirty_only = false;
+        dirty_obs.clear();
+    }
     // generations: flag_gen moves with anything that may change pair / record
     // flags, the overlay or the thresholds; score_gen with anything that may
     // change a score (both with the former)
@@ -424,6 +450,14 @@ void free_state(gsx_engine* e) {
     if (e->d_rev) (void)hipFree(e->d_rev);
     e->d_row_ptr = nullptr;
     e->d_rev = nullptr;
+    if (e->d_smask) (void)hipFree(e->d_smask);
+    if (e->d_dirty_obs) (void)hipFree(e->d_dirty_obs);
+    e->d_smask = nullptr;
+    e->d_dirty_obs = nullptr;
+    e->d_dirty_obs_cap = 0;
+    e->dirty_zeroed = true;
+    e->invalidate_scores();
+    e->h_score_tag = ~0ull;
     void* pp[] = {e->prop.seen, e->prop.hist, e->prop.origin, e->prop.from,
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
@@ -593,7 +627,11 @@ int flush(gsx_engine* e) {
     const auto* doff = reinterpret_cast<const uint32_t*>(static_cast<const char*>(e->d_stage) + ev_bytes);
     HIPCHK(e, gsx::launch_apply_events(dev_state(e), dev_peer_params(e), dev, doff, n_groups, e->stream));
     e->pending.clear();
-    e->scores_valid = false;
+    if (e->scores_valid || e->dirty_only) {  // exact but for these observers
+        for (uint32_t g = 0; g < n_groups; ++g) e->dirty_obs.push_back(obs[order[group_off[g]]]);
+        e->scores_valid = false;
+        e->dirty_only = true;
+    }
     e->state_changed();
     return GSX_OK;
 }
@@ -606,13 +644,52 @@ uint64_t id_digest(uint64_t id) {
     return z ^ (z >> 31);
 }
 
+// Every score write goes through these two (the host score copy keys on score_writes).
+hipError_t rescore_all(gsx_engine* e, const gsx::DevState& ds, int64_t now, bool refresh) {
+    ++e->score_writes;
+    return gsx::launch_refresh_score(ds, kern_params(e), now, refresh, e->stream);
+}
+hipError_t rescore_subset(gsx_engine* e, const gsx::DevState& ds, const gsx::KernParams& kp, const uint8_t* mask) {
+    ++e->score_writes;
+    return gsx::launch_score_subset(ds, kp, mask, e->stream);
+}
+
 int ensure_scores(gsx_engine* e) {
     int rc = flush(e);
     if (rc) return rc;
-    if (!e->scores_valid) {
-        HIPCHK(e, gsx::launch_refresh_score(dev_state(e), kern_params(e), 0, false, e->stream));
-        e->scores_valid = true;
+    if (e->scores_valid) return GSX_OK;
+    std::vector<uint32_t>& d = e->dirty_obs;
+    uint64_t n_dirty = 0;
+    if (e->dirty_only) {
+        std::sort(d.begin(), d.end());
+        d.erase(std::unique(d.begin(), d.end()), d.end());
+        for (uint32_t o : d) n_dirty += (uint64_t)(e->row_ptr[o + 1] - e->row_ptr[o]);
     }
+    if (e->dirty_only && n_dirty * 8 < e->E) {  // a few observers: their rows only
+        if (!e->d_smask && (rc = dalloc(e, &e->d_smask, e->E))) return rc;
+        if (!e->d_dirty_obs || e->d_dirty_obs_cap < d.size()) {
+            if (e->d_dirty_obs) {
+                HIPCHK(e, hipStreamSynchronize(e->stream));
+                (void)hipFree(e->d_dirty_obs);
+                e->d_dirty_obs = nullptr;
+            }
+            e->d_dirty_obs_cap = std::max<size_t>(d.size(), 2 * e->d_dirty_obs_cap);
+            if ((rc = dalloc(e, &e->d_dirty_obs, e->d_dirty_obs_cap))) return rc;
+        }
+        if (e->dirty_zeroed) {  // first use: the mask starts all-zero
+            HIPCHK(e, hipMemsetAsync(e->d_smask, 0, e->E, e->stream));
+            e->dirty_zeroed = false;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_dirty_obs, d.data(), 4 * d.size(), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, gsx::launch_mark_rows(e->d_row_ptr, e->d_dirty_obs, (uint32_t)d.size(), e->d_smask, 1, e->stream));
+        HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), e->d_smask));
+        HIPCHK(e, gsx::launch_mark_rows(e->d_row_ptr, e->d_dirty_obs, (uint32_t)d.size(), e->d_smask, 0, e->stream));
+        // the observer list is read by the kernels above: keep it until they ran
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+    } else {
+        HIPCHK(e, rescore_all(e, dev_state(e), 0, false));
+    }
+    e->scores_exact();
     return GSX_OK;
 }
 
@@ -805,7 +882,7 @@ int gsx_set_peer_params(gsx_engine* e, const gsx_peer_score_params* p) {
     if (rc) return rc;
     e->pp = *p;
     e->pp_set = true;
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     return GSX_OK;
 }
@@ -829,7 +906,7 @@ int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_pa
     const gsx_topic_score_params old = e->tp[topic];
     e->tp[topic] = *p;
     e->scored[topic] = true;
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     rc = upload_topic_params(e);
     if (rc) return rc;
@@ -985,7 +1062,7 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
     rc = upload_ipg(e);
     if (rc) return rc;
     e->loaded = true;
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     return GSX_OK;
 }
@@ -1129,7 +1206,7 @@ int gsx_set_ip_whitelist(gsx_engine* e, const uint32_t* ip_ids, size_t n) {
         if (ip_ids[i] >= e->ip_wl.size()) e->ip_wl.resize((size_t)ip_ids[i] + 1, 0);
         e->ip_wl[ip_ids[i]] = 1;
     }
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     if (!e->loaded) return GSX_OK;
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1144,7 +1221,83 @@ int gsx_set_app_scores(gsx_engine* e, const double* app, size_t n) {
     if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(e->d_app, app, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->scores_valid = false;
+    e->invalidate_scores();
+    e->state_changed();
+    return GSX_OK;
+}
+
+// setIPs for pairs whose peer's IP list changed (refreshIPs, score.go:560-586)
+int gsx_set_pair_ips(gsx_engine* e, const uint64_t* pairs, const uint32_t* ips, size_t n) {
+    if (!e || (n && (!pairs || !ips))) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    for (size_t i = 0; i < n; ++i)
+        if (pairs[i] >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
+    if (n == 0) return GSX_OK;
+    if (int rc = flush(e)) return rc;  // queued events count under the lists they were issued with
+    // the (observer, IP) group of each new IP: an existing key of the
+    // observer's ps.peerIPs map, or a new one
+    const uint32_t groups0 = e->n_groups;
+    auto group_of = [&](uint32_t u, uint32_t ip) -> uint32_t {
+        if (ip == GSX_NO_IP) return gsx::IPG_NONE;
+        for (int64_t q = e->row_ptr[u]; q < e->row_ptr[u + 1]; ++q)
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t g = e->ipg_host[2 * (size_t)q + k];
+                if (g != gsx::IPG_NONE && e->group_ip[g] == ip) return g;
+            }
+        e->group_ip.push_back(ip);
+        return e->n_groups++;
+    };
+    std::vector<uint32_t> obs(n), order(n);
+    std::vector<gsx::DevIpMove> mv(n);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t p = pairs[i];
+        const uint32_t u = e->pair_obs[p];
+        obs[i] = u;
+        order[i] = (uint32_t)i;
+        uint32_t g[2];
+        for (int k = 0; k < 2; ++k) {
+            g[k] = group_of(u, ips[2 * i + k]);
+            e->ipg_host[2 * (size_t)p + k] = g[k];
+            if (g[k] != gsx::IPG_NONE && ips[2 * i + k] < e->ip_wl.size() && e->ip_wl[ips[2 * i + k]]) g[k] |= gsx::IPG_WL;
+        }
+        mv[i] = gsx::DevIpMove{p, g[0], g[1]};
+    }
+    if (e->n_groups > groups0) {  // new keys: a longer count array, the old counts kept
+        uint32_t* nc = nullptr;
+        if (int rc = dalloc(e, &nc, e->n_groups)) return rc;
+        HIPCHK(e, hipMemsetAsync(nc, 0, sizeof(uint32_t) * e->n_groups, e->stream));
+        if (groups0) HIPCHK(e, hipMemcpyAsync(nc, e->d_ipcount, sizeof(uint32_t) * groups0, hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(e->d_ipcount);
+        e->d_ipcount = nc;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return obs[a] < obs[b]; });
+    std::vector<gsx::DevIpMove> sorted(n);
+    std::vector<uint32_t> off;
+    for (size_t i = 0; i < n; ++i) {
+        sorted[i] = mv[order[i]];
+        if (i == 0 || obs[order[i]] != obs[order[i - 1]]) off.push_back((uint32_t)i);
+    }
+    const uint32_t n_grp = (uint32_t)off.size();
+    off.push_back((uint32_t)n);
+    gsx::DevIpMove* d_mv = nullptr;
+    uint32_t* d_off = nullptr;
+    if (int rc = dalloc(e, &d_mv, n)) return rc;
+    if (int rc = dalloc(e, &d_off, off.size())) {
+        (void)hipFree(d_mv);
+        return rc;
+    }
+    HIPCHK(e, hipMemcpyAsync(d_mv, sorted.data(), sizeof(gsx::DevIpMove) * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(d_off, off.data(), sizeof(uint32_t) * off.size(), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, gsx::launch_set_ips(dev_state(e), d_mv, d_off, n_grp, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    (void)hipFree(d_mv);
+    (void)hipFree(d_off);
+    if (e->scores_valid || e->dirty_only) {  // only these observers' P6 moved
+        for (uint32_t g = 0; g < n_grp; ++g) e->dirty_obs.push_back(obs[order[off[g]]]);
+        e->scores_valid = false;
+        e->dirty_only = true;
+    }
     e->state_changed();
     return GSX_OK;
 }
@@ -1273,11 +1426,11 @@ int gsx_refresh(gsx_engine* e, int64_t now) {
     HIPCHK(e, gsx::launch_purge(s, now, e->stream));
     const bool region = e->t_active && e->t_used < e->t_max;
     HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used] : e->ev_start, e->stream));
-    HIPCHK(e, gsx::launch_refresh_score(s, kern_params(e), now, true, e->stream));
+    HIPCHK(e, rescore_all(e, s, now, true));
     HIPCHK(e, hipEventRecord(region ? e->tev[2 * e->t_used + 1] : e->ev_stop, e->stream));
     if (region) ++e->t_used;
     e->timed = !region;
-    e->scores_valid = true;
+    e->scores_exact();
     e->state_changed();
     e->last_refresh = now;
     return GSX_OK;
@@ -1338,7 +1491,19 @@ int gsx_scores(gsx_engine* e, double* out, size_t n) {
 int gsx_score(gsx_engine* e, uint64_t pair, double* out) {
     if (!e || !out) return GSX_EINVAL;
     if (int rc = check_pair(e, pair)) return rc;
+    if (e->pending.empty() && e->scores_valid && e->h_score_tag == e->score_writes) {
+        *out = e->h_score[pair];  // nothing changed since the copy: no device round trip
+        return GSX_OK;
+    }
     if (int rc = ensure_scores(e)) return rc;
+    if (e->E <= kHostScoreMax) {  // small engine (one router's peers): keep the whole vector on the host
+        e->h_score.resize(e->E);
+        HIPCHK(e, hipMemcpyAsync(e->h_score.data(), e->d_score, sizeof(double) * e->E, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        e->h_score_tag = e->score_writes;
+        *out = e->h_score[pair];
+        return GSX_OK;
+    }
     HIPCHK(e, hipMemcpyAsync(out, e->d_score + pair, sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
@@ -1390,7 +1555,7 @@ int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
     HIPCHK(e, hipMemcpyAsync(&n_bad, e->d_nbad, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     release_tmp(e);
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     if (n_bad) return fail(e, GSX_EINVAL, std::to_string(n_bad) + " in-mesh records have a meshTime that is neither 0 "
                                           "nor last_refresh_ns - graftTime");
@@ -1420,7 +1585,7 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     HIPCHK(e, gsx::launch_synthesize(s, e->d_col, d, e->stream));
     HIPCHK(e, gsx::launch_rebuild_ipcount(s, e->n_groups, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->scores_valid = false;
+    e->invalidate_scores();
     e->state_changed();
     return GSX_OK;
 }
@@ -1888,7 +2053,7 @@ int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
     HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * e->E, e->stream));
     HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * e->E, e->stream));
     P.credit_pending = false;
-    e->scores_valid = false;
+    e->invalidate_scores();
     ++e->score_gen;
     return GSX_OK;
 }
@@ -1912,7 +2077,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         P.credit_pending = !fold_now;
         P.credit_topic = ps.topic;
         if (fold_now) {
-            e->scores_valid = false;
+            e->invalidate_scores();
             ++e->score_gen;
         }
     }
@@ -2382,7 +2547,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
-    if (pen_mask) HIPCHK(e, gsx::launch_score_subset(dev_state(e), kern_params(e), pen_mask, e->stream));
+    if (pen_mask) HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), pen_mask));
     gsx::HbState h{};
     h.row_ptr = e->d_row_ptr;
     h.rev = e->d_rev;
@@ -2566,7 +2731,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         sel = e->d_dirty + 3 * e->E;
         HIPCHK(e, gsx::launch_mask_and(h.dirty, h.inbox, sel, e->E, e->stream));
     }
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), sel, e->stream));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), sel));
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
@@ -2589,7 +2754,7 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
         sel = e->d_dirty + 3 * e->E;
         HIPCHK(e, gsx::launch_mask_and(h.dirty, h.answer, sel, e->E, e->stream));
     }
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), sel, e->stream));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), sel));
     return GSX_OK;
 }
 
@@ -2602,7 +2767,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     std::memset(out, 0, sizeof(*out));
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));  // the cache leaves the round exact
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
     const size_t hist = (size_t)std::max(e->gp.history_length, 1);
     // (D) the gossip exchange over the batches the IHAVEs advertised (the
     // windows of hb_begin's list), answered across the Shift below
@@ -2657,7 +2822,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         for (size_t i = 0; i < gx_sets.size(); ++i)
             HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
                                            e->stream));
-        e->scores_valid = false;  // the receipts credited P2 / P3 / P4
+        e->invalidate_scores();  // the receipts credited P2 / P3 / P4
         ++e->score_gen;
     }
     unsigned long long st[gsx::HB_STAT_WORDS];
@@ -2837,14 +3002,14 @@ int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, s
     }
     // the receivers' mesh sizes (the scan counts every unit) and the scores of the touched pairs
     HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));
     e->hb_active = true;
     if (int rc = hb_recv(e, nullptr)) return rc;
     std::memset(out, 0, sizeof(*out));
     e->hb_active = false;
     HIPCHK(e, gsx::launch_hb_answer(ds, e->hb, e->stream));
     e->hb_clean = !e->hb_tracing;
-    HIPCHK(e, gsx::launch_score_subset(ds, kern_params(e), h.dirty, e->stream));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));

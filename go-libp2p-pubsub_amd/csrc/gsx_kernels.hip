@@ -292,6 +292,49 @@ hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const ui
     return launch_rs<false>(s, kp, 0, only, st);
 }
 
+// setIPs (score.go:1021-1059) for pairs whose peer's IP list changed
+// (refreshIPs, score.go:560-586; AddPeer of a peer seen on new addresses):
+// a present peer leaves the sets of its old IPs and joins those of its new
+// ones; an absent one only records the list (AddPeer counts it).  One thread
+// per observer, its moves in the order given (the counts are the observer's).
+__global__ __launch_bounds__(64) void k_set_ips(DevState s, const DevIpMove* __restrict__ mv,
+                                                const uint32_t* __restrict__ group_off, uint32_t n_groups) {
+    const uint32_t g = blockIdx.x * 64u + threadIdx.x;
+    if (g >= n_groups) return;
+    for (uint32_t i = group_off[g]; i < group_off[g + 1]; ++i) {
+        const uint64_t p = mv[i].pair;
+        const bool present = s.pflags[p] & PAIR_PRESENT;
+        if (present) ipcount_add(s, p, -1);
+        reinterpret_cast<uint2*>(const_cast<uint32_t*>(s.ipg))[p] = make_uint2(mv[i].g0, mv[i].g1);
+        if (present) ipcount_add(s, p, +1);
+    }
+}
+hipError_t launch_set_ips(const DevState& s, const DevIpMove* mv, const uint32_t* group_off, uint32_t n_groups,
+                          hipStream_t st) {
+    if (n_groups == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_set_ips, dim3(blocks_for(n_groups, 64)), dim3(64), 0, st, s, mv, group_off, n_groups);
+    return hipGetLastError();
+}
+
+// Sets mask[p] = val for every pair of the listed observers (incremental
+// re-scoring after events, gsx_score).
+__global__ __launch_bounds__(256) void k_mark_rows(const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ obs,
+                                                   uint32_t n, uint8_t* __restrict__ mask, uint8_t val) {
+    // one wave per observer, its lanes over the row
+    const uint32_t lane = threadIdx.x % 64;
+    for (uint32_t i = blockIdx.x * 4u + threadIdx.x / 64; i < n; i += gridDim.x * 4u) {
+        const uint32_t o = obs[i];
+        for (int64_t p = row_ptr[o] + lane; p < row_ptr[o + 1]; p += 64) mask[p] = val;
+    }
+}
+hipError_t launch_mark_rows(const int64_t* row_ptr, const uint32_t* obs, uint32_t n, uint8_t* mask, uint8_t val,
+                            hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mark_rows, dim3(std::min<uint32_t>((n + 3) / 4, 4096)), dim3(256), 0, st, row_ptr, obs, n, mask,
+                       val);
+    return hipGetLastError();
+}
+
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
                                const uint32_t* group_off, uint32_t n_groups, hipStream_t st) {
     if (n_groups == 0) return hipSuccess;

@@ -361,6 +361,7 @@ SIGNATURES = {
     "gsx_prop_results": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_int32)]),
     "gsx_prop_set_tracking": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_prop_duplicates": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
+    "gsx_set_pair_ips": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_size_t]),
     "gsx_prop_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_replace_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_pending_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

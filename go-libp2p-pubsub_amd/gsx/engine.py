@@ -142,6 +142,15 @@ class Engine:
         self._chk(self.lib.gsx_scores(self.h, _ptr(out, C.c_double), self.n_pairs), "gsx_scores")
         return out
 
+    def set_pair_ips(self, pairs, ips):
+        """gsx_set_pair_ips: setIPs for these pairs (ips: [n, 2] u32, GSX_NO_IP for none)."""
+        pairs = np.ascontiguousarray(pairs, dtype=np.uint64).reshape(-1)
+        ips = np.ascontiguousarray(ips, dtype=np.uint32).reshape(-1, 2)
+        if len(ips) != len(pairs):
+            raise ValueError("one IP pair per pair")
+        self._chk(self.lib.gsx_set_pair_ips(self.h, _ptr(pairs, C.c_uint64), _ptr(ips, C.c_uint32), len(pairs)),
+                  "gsx_set_pair_ips")
+
     def score(self, pair: int) -> float:
         v = C.c_double()
         self._chk(self.lib.gsx_score(self.h, pair, C.byref(v)), "gsx_score")

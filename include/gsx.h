@@ -178,6 +178,15 @@ int gsx_set_ip_whitelist(gsx_engine* e, const uint32_t* ip_ids, size_t n);
 
 /* AppSpecificScore snapshot (score.go:320): app[p] for every pair. */
 int gsx_set_app_scores(gsx_engine* e, const double* app, size_t n_pairs);
+/* setIPs (score.go:1021-1059) for pairs whose peer the observer now sees on
+ * other addresses: refreshIPs (score.go:560-586) calls it for its connected
+ * peers, a shim's AddPeer before the GSX_EV_ADD_PEER of a peer whose
+ * addresses changed.  ips: 2 per pair (GSX_NO_IP for none; an IPv6 peer's
+ * address + /64).  A present pair (connected or retained) leaves the
+ * (observer, IP) sets of its old list and joins those of the new one; an
+ * absent pair only records the list, counted by its next AddPeer.  Applied
+ * after the queued events, in the order given. */
+int gsx_set_pair_ips(gsx_engine* e, const uint64_t* pairs, const uint32_t* ips, size_t n);
 
 /* ---- events: the RawTracer calls that mutate counters --------------------- */
 

@@ -12,6 +12,7 @@
 // (the reference reads time.Now(); score.go:501,636,657,711,839).
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -312,8 +313,15 @@ class PeerScore {
     }
     void sync_app() {  // AppSpecificScore(p) is called at score time (:320)
         if (!params_.AppSpecificScore) return;
-        for (size_t i = 0; i < ids_.size(); ++i) app_[i] = params_.AppSpecificScore(ids_[i]);
-        check(gsx_set_app_scores(e_, app_.data(), app_.size()), "gsx_set_app_scores");
+        bool changed = !app_synced_;
+        for (size_t i = 0; i < ids_.size(); ++i) {
+            const double a = params_.AppSpecificScore(ids_[i]);
+            changed |= a != app_[i] || std::signbit(a) != std::signbit(app_[i]);
+            app_[i] = a;
+        }
+        // an unchanged snapshot leaves the engine's scores (and its host copy) valid
+        if (changed) check(gsx_set_app_scores(e_, app_.data(), app_.size()), "gsx_set_app_scores");
+        app_synced_ = true;
     }
 
     PeerScoreParams params_;
@@ -325,6 +333,7 @@ class PeerScore {
     std::map<std::string, uint32_t> topics_;
     std::unordered_map<std::string, uint64_t> msgs_;
     std::vector<double> app_;
+    bool app_synced_ = false;
 };
 
 }  // namespace pubsub

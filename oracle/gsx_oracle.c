@@ -58,7 +58,7 @@ typedef struct {
 typedef struct {
     uint64_t* keys;
     uint32_t* vals;
-    size_t cap;
+    size_t cap, used;
 } ipcount_map;
 
 struct orc_engine;
@@ -133,6 +133,7 @@ struct orc_engine {
     int64_t* row_ptr;
     int32_t* col;
     uint32_t* node_ips;
+    uint32_t* pair_ip; /* [pair][2]: the IP list the observer holds for the peer (peerStats.ips) */
     uint32_t* pair_obs;
 
     orc_peer_stats* ps;
@@ -312,6 +313,7 @@ void orc_destroy(orc_engine* o) {
     free(o->row_ptr);
     free(o->col);
     free(o->node_ips);
+    free(o->pair_ip);
     free(o->pair_obs);
     free(o->ps);
     free(o->ts);
@@ -429,13 +431,15 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     o->row_ptr = (int64_t*)malloc(sizeof(int64_t) * (n_nodes + 1));
     o->col = (int32_t*)malloc(sizeof(int32_t) * (E ? E : 1));
     o->node_ips = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (n_nodes ? n_nodes : 1));
+    free(o->pair_ip);
+    o->pair_ip = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (E ? E : 1));
     o->pair_obs = (uint32_t*)malloc(sizeof(uint32_t) * (E ? E : 1));
     o->ps = (orc_peer_stats*)calloc(E ? E : 1, sizeof(orc_peer_stats));
     o->ts = (orc_topic_stats*)calloc((E ? E : 1) * o->T, sizeof(orc_topic_stats));
     o->app = (double*)calloc(E ? E : 1, sizeof(double));
     o->q_head = (int64_t*)malloc(sizeof(int64_t) * (n_nodes ? n_nodes : 1));
     o->q_tail = (int64_t*)malloc(sizeof(int64_t) * (n_nodes ? n_nodes : 1));
-    if (!o->row_ptr || !o->col || !o->node_ips || !o->pair_obs || !o->ps || !o->ts || !o->app ||
+    if (!o->row_ptr || !o->col || !o->node_ips || !o->pair_ip || !o->pair_obs || !o->ps || !o->ts || !o->app ||
         !o->q_head || !o->q_tail)
         return GSX_ENOMEM;
     memcpy(o->row_ptr, row_ptr, sizeof(int64_t) * (n_nodes + 1));
@@ -446,6 +450,9 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
         o->q_head[i] = o->q_tail[i] = -1;
         for (int64_t p = row_ptr[i]; p < row_ptr[i + 1]; p++) o->pair_obs[p] = i;
     }
+    for (uint64_t p = 0; p < E; p++)
+        for (int k = 0; k < 2; k++)
+            o->pair_ip[2 * p + k] = node_ips ? node_ips[2 * (size_t)col[p] + k] : GSX_NO_IP;
     if (ipcount_init(o)) return GSX_ENOMEM;
     o->n_buckets = 1024;
     o->buckets = (int64_t*)malloc(sizeof(int64_t) * o->n_buckets);
@@ -473,12 +480,12 @@ static bool whitelisted(const orc_engine* o, uint32_t ip) {
     return false;
 }
 
-/* the IP list of the peer behind pair q (peerStats.ips; getIPs score.go:977-1017) */
+/* the IP list of the peer behind pair q (peerStats.ips; getIPs score.go:977-1017):
+ * its node's addresses at load, or what orc_set_pair_ips set since */
 static int pair_ips(const orc_engine* o, uint64_t q, uint32_t out[2]) {
-    uint32_t node = (uint32_t)o->col[q];
     int n = 0;
     for (int k = 0; k < 2; k++) {
-        uint32_t ip = o->node_ips[2 * node + k];
+        uint32_t ip = o->pair_ip[2 * q + k];
         if (ip != GSX_NO_IP) out[n++] = ip;
     }
     return n;
@@ -501,6 +508,7 @@ static uint32_t* ipcount_slot(ipcount_map* m, uint64_t key, bool insert) {
             if (!insert) return NULL;
             m->keys[i] = key;
             m->vals[i] = 0;
+            m->used++;
             return &m->vals[i];
         }
         i = (i + 1) & (m->cap - 1);
@@ -514,6 +522,7 @@ static int ipcount_init(orc_engine* o) {
     size_t need = 2 * (size_t)o->E + 16, cap = 16;
     while (cap < 2 * need) cap <<= 1;
     m->cap = cap;
+    m->used = 0;
     m->keys = (uint64_t*)malloc(sizeof(uint64_t) * cap);
     m->vals = (uint32_t*)malloc(sizeof(uint32_t) * cap);
     if (!m->keys || !m->vals) return GSX_ENOMEM;
@@ -531,6 +540,43 @@ static void ipcount_add(orc_engine* o, uint64_t q, int delta) {
         uint64_t key = ((uint64_t)o->pair_obs[q] << 32) | ips[j];
         *ipcount_slot(&o->ipc, key, true) += (uint32_t)delta;
     }
+}
+
+/* room for `more` new keys at a load factor <= 1/2 (rehash into a larger table) */
+static int ipcount_reserve(orc_engine* o, size_t more) {
+    ipcount_map* m = &o->ipc;
+    if (2 * (m->used + more) <= m->cap) return 0;
+    ipcount_map old = *m;
+    size_t cap = m->cap;
+    while (2 * (m->used + more) > cap) cap <<= 1;
+    m->keys = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+    m->vals = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    if (!m->keys || !m->vals) return GSX_ENOMEM;
+    memset(m->keys, 0xff, sizeof(uint64_t) * cap);
+    m->cap = cap;
+    m->used = 0;
+    for (size_t i = 0; i < old.cap; i++)
+        if (old.keys[i] != UINT64_MAX) *ipcount_slot(m, old.keys[i], true) = old.vals[i];
+    free(old.keys);
+    free(old.vals);
+    return 0;
+}
+
+/* setIPs (score.go:1021-1059) for pairs whose peer now has other addresses
+ * (refreshIPs, score.go:560-586): a present peer leaves the sets of its old
+ * IPs and joins those of the new list; an absent one only records it. */
+int orc_set_pair_ips(orc_engine* o, const uint64_t* pairs, const uint32_t* ips, size_t n) {
+    for (size_t i = 0; i < n; i++)
+        if (pairs[i] >= o->E) return GSX_ERANGE;
+    if (ipcount_reserve(o, 2 * n)) return GSX_ENOMEM;
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t q = pairs[i];
+        if (o->ps[q].present) ipcount_add(o, q, -1);
+        o->pair_ip[2 * q] = ips[2 * i];
+        o->pair_ip[2 * q + 1] = ips[2 * i + 1];
+        if (o->ps[q].present) ipcount_add(o, q, +1);
+    }
+    return 0;
 }
 
 static void ipcount_rebuild(orc_engine* o) {

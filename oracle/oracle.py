@@ -33,6 +33,7 @@ _SIG = {
         C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int64), P(C.c_int32), P(C.c_uint8), P(C.c_uint32)]),
     "orc_set_thresholds": (C.c_int, [C.c_void_p, P(abi.Thresholds)]),
     "orc_prop_set_dup_tracking": (C.c_int, [C.c_void_p, C.c_int]),
+    "orc_set_pair_ips": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_size_t]),
     "orc_prop_duplicates": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
     "orc_propagate": (
         C.c_int,
@@ -159,6 +160,13 @@ class Oracle:
             "orc_propagate",
         )
         return out, hop, frm
+
+    def set_pair_ips(self, pairs, ips):
+        """setIPs for these pairs (orc_set_pair_ips; ips [n, 2] u32)."""
+        pairs = np.ascontiguousarray(pairs, dtype=np.uint64).reshape(-1)
+        ips = np.ascontiguousarray(ips, dtype=np.uint32).reshape(-1, 2)
+        self._chk(self.lib.orc_set_pair_ips(self.h, _p(pairs, C.c_uint64), _p(ips, C.c_uint32), len(pairs)),
+                  "orc_set_pair_ips")
 
     def set_dup_tracking(self, on: bool = True):
         """Record which copies of the next propagations are duplicates (orc_prop_duplicates)."""

@@ -62,6 +62,11 @@ def small_overlay(n, d, seed, n_ip_pool):
     return ov
 
 
+def n_ip_pool(ov):
+    ips = ov.node_ips[ov.node_ips != abi.GSX_NO_IP]
+    return int(ips.max()) + 1 if len(ips) else 8
+
+
 def make_ops(ov, n_topics, seed, n_steps=400):
     rng = np.random.default_rng(seed + 1)
     E = ov.n_pairs
@@ -132,6 +137,14 @@ def make_ops(ov, n_topics, seed, n_steps=400):
             ops.append(("topic_params", t, tp))
         elif r < 0.92:
             ops.append(("gc", now + int(rng.integers(0, 200)) * S))
+        elif r < 0.95:  # refreshIPs / AddPeer on new addresses: some pairs' IP lists change
+            k = int(rng.integers(1, 12))
+            pairs = rng.integers(0, E, k)
+            ips = rng.integers(0, n_ip_pool(ov) + 4, (k, 2)).astype(np.uint32)
+            ips[rng.random((k, 2)) < 0.25] = abi.GSX_NO_IP
+            dup = rng.random(k) < 0.1
+            ips[dup, 1] = ips[dup, 0]
+            ops.append(("ips", pairs, ips))
         else:
             ops.append(("check",))
         if step % 50 == 49:
@@ -165,6 +178,56 @@ def replay(be, ov, n_topics, ops, whitelist=(3,)):
             be.set_topic_params(op[1], op[2])
         elif k == "gc":
             be.gc_deliveries(op[1])
+        elif k == "ips":
+            be.set_pair_ips(op[1], op[2])
         elif k == "check":
             snaps.append((be.scores(), be.export_state(), be.num_delivery_records()))
     return snaps
+
+
+def interleaved_score_calls(be, ov, n_topics, ops, seed, per_call=2):
+    """Replay ``ops`` one call at a time (every event and tracer call on its
+    own), asking Score() of a few random pairs after each: what a router does
+    between RPCs (gossipsub.go:589 AcceptFrom, :960-989 Publish).  Returns
+    the scores asked, in order."""
+    rng = np.random.default_rng(seed + 99)
+    pp, tps = scenario_params(n_topics)
+    be.set_peer_params(pp)
+    for t, tp in tps.items():
+        be.set_topic_params(t, tp)
+    be.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    be.set_ip_whitelist([3])
+    E = ov.n_pairs
+    out = []
+
+    def ask():
+        for p in rng.integers(0, E, per_call).tolist():
+            out.append(be.score(int(p)))
+
+    for op in ops:
+        k = op[0]
+        if k == "events":
+            if len(op[1]) >= 50:  # the initial AddPeer / Graft batches go in one call
+                be.apply_events(np.array(op[1], dtype=abi.event_dtype()))
+                ask()
+                continue
+            for ev in op[1]:
+                be.apply_events(np.array([ev], dtype=abi.event_dtype()))
+                ask()
+        elif k == "trace":
+            for c in op[1]:
+                getattr(be, "trace_" + c[0])(*c[1:])
+                ask()
+        elif k == "refresh":
+            be.refresh(op[1])
+            ask()
+        elif k == "app":
+            be.set_app_scores(op[1])
+            ask()
+        elif k == "topic_params":
+            be.set_topic_params(op[1], op[2])
+            ask()
+        elif k == "ips":
+            be.set_pair_ips(op[1], op[2])
+            ask()
+    return np.array(out)

@@ -54,6 +54,19 @@ def test_engine_matches_oracle_random_calls(gpu_ok, seed, n, d, T):
         assert_same_state(gst, wst, f"check {i}")
 
 
+@pytest.mark.parametrize("seed,n,d,T", [(3, 200, 3, 3), (5, 3000, 6, 2), (9, 9000, 4, 2)])
+def test_engine_score_calls_interleaved(gpu_ok, seed, n, d, T):
+    """Score() after every single event / tracer call (incremental re-scoring of
+    the flushed observers' rows, the host score copy of small engines, and the
+    full re-score of engines above it) == the oracle's score() at the same point."""
+    ov = R.small_overlay(n, d, seed, max(8, n // 6))
+    ops = R.make_ops(ov, T, seed, n_steps=120)
+    got = R.interleaved_score_calls(gsx.Engine(T), ov, T, ops, seed)
+    want = R.interleaved_score_calls(orc.Oracle(T), ov, T, ops, seed)
+    assert len(got) == len(want) > 100
+    assert_same_scores(got, want, "interleaved Score()")
+
+
 @pytest.mark.parametrize("n,T,p_disc,p_abs", [(20000, 8, 0.0, 0.0), (30000, 8, 0.1, 0.05), (40000, 1, 0.05, 0.05),
                                               (5000, 5, 0.2, 0.2)])
 def test_engine_refresh_matches_oracle_synthetic(gpu_ok, n, T, p_disc, p_abs):
@@ -122,3 +135,13 @@ def test_engine_scores_full_size_properties(gpu_ok):
     ora.set_app_scores(np.zeros(p1))
     ora.refresh(now + abi.SECOND)
     assert_same_scores(s1[:p1], ora.scores(), "sample")
+
+
+def test_engine_set_pair_ips_matches_oracle(gpu_ok):
+    """gsx_set_pair_ips (refreshIPs / setIPs) == the oracle, step by step."""
+    import ip_cases as ic
+
+    got, _ = ic.run(gsx.Engine(1))
+    want, _ = ic.run(orc.Oracle(1))
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert_same_scores(g, w, f"step {i}")
