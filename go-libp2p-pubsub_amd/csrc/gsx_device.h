@@ -425,6 +425,7 @@ struct DevIpMove {
 };
 hipError_t launch_set_ips(const DevState& s, const DevIpMove* mv, const uint32_t* group_off, uint32_t n_groups,
                           hipStream_t st);
+hipError_t launch_ip_colocation_export(const DevState& s, const DevPeerParams& pp, double* out, hipStream_t st);
 hipError_t launch_mark_rows(const int64_t* row_ptr, const uint32_t* obs, uint32_t n, uint8_t* mask, uint8_t val,
                             hipStream_t st);
 hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const uint8_t* only, hipStream_t st);

@@ -1621,6 +1621,36 @@ int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
     return GSX_OK;
 }
 
+// inspectScoresExtended, score.go:463-493
+int gsx_peer_score_snapshot(gsx_engine* e, gsx_score_snapshot* s) {
+    if (!e || !s) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = ensure_scores(e)) return rc;
+    const size_t E = e->E;
+    if (s->score) HIPCHK(e, hipMemcpyAsync(s->score, e->d_score, 8 * E, hipMemcpyDeviceToHost, e->stream));
+    if (s->app_specific_score) HIPCHK(e, hipMemcpyAsync(s->app_specific_score, e->d_app, 8 * E, hipMemcpyDeviceToHost, e->stream));
+    if (s->ip_colocation_factor && E) {
+        double* d = nullptr;
+        if (int rc = dalloc(e, &d, E)) return rc;
+        HIPCHK(e, gsx::launch_ip_colocation_export(dev_state(e), dev_peer_params(e), d, e->stream));
+        HIPCHK(e, hipMemcpyAsync(s->ip_colocation_factor, d, 8 * E, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(d);
+    }
+    std::vector<uint8_t> pf;
+    if (s->present) pf.resize(E);
+    gsx_state_view v{};
+    v.pair_flags = s->present ? pf.data() : nullptr;
+    v.behaviour_penalty = s->behaviour_penalty;
+    v.first_message_deliveries = s->first_message_deliveries;
+    v.mesh_message_deliveries = s->mesh_message_deliveries;
+    v.invalid_message_deliveries = s->invalid_message_deliveries;
+    v.mesh_time_ns = s->time_in_mesh_ns;  // 0 outside the mesh, as the snapshot (score.go:479-481)
+    if (int rc = gsx_export_state(e, &v)) return rc;
+    for (size_t p = 0; p < pf.size(); ++p) s->present[p] = (pf[p] & GSX_PAIR_PRESENT) ? 1 : 0;
+    return GSX_OK;
+}
+
 // Message propagation, see gsx.h and gsx_propagate.hip.
 namespace {
 

@@ -316,6 +316,19 @@ hipError_t launch_set_ips(const DevState& s, const DevIpMove* mv, const uint32_t
     return hipGetLastError();
 }
 
+// ipColocationFactor (score.go:337-381) of every pair, unweighted: the
+// PeerScoreSnapshot's IPColocationFactor (score.go:487); 0 without peerStats.
+__global__ __launch_bounds__(256) void k_ip_colocation_export(DevState s, DevPeerParams pp, double* __restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= s.n_pairs) return;
+    out[p] = (s.pflags[p] & PAIR_PRESENT) ? ip_colocation(s, pp, p) : 0.0;
+}
+hipError_t launch_ip_colocation_export(const DevState& s, const DevPeerParams& pp, double* out, hipStream_t st) {
+    if (s.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ip_colocation_export, dim3(blocks_for(s.n_pairs, 256)), dim3(256), 0, st, s, pp, out);
+    return hipGetLastError();
+}
+
 // Sets mask[p] = val for every pair of the listed observers (incremental
 // re-scoring after events, gsx_score).
 __global__ __launch_bounds__(256) void k_mark_rows(const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ obs,

@@ -179,6 +179,27 @@ STATE_DTYPES = {
     "behaviour_penalty": "<f8",
 }
 
+class ScoreSnapshot(C.Structure):
+    """gsx_score_snapshot: PeerScoreSnapshot / TopicScoreSnapshot (score.go:125-138)."""
+    _fields_ = [
+        ("present", C.POINTER(C.c_uint8)),
+        ("score", C.POINTER(C.c_double)),
+        ("app_specific_score", C.POINTER(C.c_double)),
+        ("ip_colocation_factor", C.POINTER(C.c_double)),
+        ("behaviour_penalty", C.POINTER(C.c_double)),
+        ("time_in_mesh_ns", C.POINTER(C.c_int64)),
+        ("first_message_deliveries", C.POINTER(C.c_double)),
+        ("mesh_message_deliveries", C.POINTER(C.c_double)),
+        ("invalid_message_deliveries", C.POINTER(C.c_double)),
+    ]
+
+
+SNAPSHOT_PAIR = {"present": "u1", "score": "<f8", "app_specific_score": "<f8", "ip_colocation_factor": "<f8",
+                 "behaviour_penalty": "<f8"}
+SNAPSHOT_RECORD = {"time_in_mesh_ns": "<i8", "first_message_deliveries": "<f8", "mesh_message_deliveries": "<f8",
+                   "invalid_message_deliveries": "<f8"}
+
+
 class SynthSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -362,6 +383,7 @@ SIGNATURES = {
     "gsx_prop_set_tracking": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_prop_duplicates": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
     "gsx_set_pair_ips": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_size_t]),
+    "gsx_peer_score_snapshot": (C.c_int, [C.c_void_p, P(ScoreSnapshot)]),
     "gsx_prop_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_replace_pending_invalid": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_pending_credits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

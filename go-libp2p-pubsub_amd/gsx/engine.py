@@ -450,6 +450,15 @@ class Engine:
     def synthesize_state(self, spec: abi.SynthSpec):
         self._chk(self.lib.gsx_synthesize_state(self.h, C.byref(spec)), "gsx_synthesize_state")
 
+    def snapshot(self) -> Dict[str, np.ndarray]:
+        """gsx_peer_score_snapshot (inspectScoresExtended, score.go:463-493): per pair and
+        per [topic][pair] record, the PeerScoreSnapshot / TopicScoreSnapshot fields."""
+        out = {f: np.empty(self.n_pairs, dtype=d) for f, d in abi.SNAPSHOT_PAIR.items()}
+        out.update({f: np.empty(self.n_topics * self.n_pairs, dtype=d) for f, d in abi.SNAPSHOT_RECORD.items()})
+        sv = abi.ScoreSnapshot(**{f: out[f].ctypes.data_as(dict(abi.ScoreSnapshot._fields_)[f]) for f in out})
+        self._chk(self.lib.gsx_peer_score_snapshot(self.h, C.byref(sv)), "gsx_peer_score_snapshot")
+        return out
+
     def export_state(self) -> Dict[str, np.ndarray]:
         R = self.n_topics * self.n_pairs
         out = {}

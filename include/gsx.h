@@ -303,6 +303,28 @@ typedef struct gsx_state_view {
 int gsx_import_state(gsx_engine* e, const gsx_state_view* s);
 int gsx_export_state(gsx_engine* e, gsx_state_view* s);
 
+/* WithPeerScoreInspect's extended view (ExtendedPeerScoreInspectFn,
+ * inspectScoresExtended score.go:463-493): a PeerScoreSnapshot per pair
+ * whose observer keeps peerStats for the peer (present = 1), its
+ * TopicScoreSnapshot per topic.  NULL members are skipped.
+ * Differences: Topics covers every topic index (a topicStats the reference
+ * never created reads as zeros, which is what it contributes); the app score
+ * is the last gsx_set_app_scores snapshot, not a fresh closure call. */
+typedef struct gsx_score_snapshot {
+    /* per pair, n_pairs (PeerScoreSnapshot, score.go:125-131) */
+    uint8_t* present;
+    double* score;
+    double* app_specific_score;
+    double* ip_colocation_factor; /* unweighted P6 */
+    double* behaviour_penalty;
+    /* per record, [topic][pair] (TopicScoreSnapshot, score.go:133-138) */
+    int64_t* time_in_mesh_ns; /* meshTime while in the mesh, else 0 */
+    double* first_message_deliveries;
+    double* mesh_message_deliveries;
+    double* invalid_message_deliveries;
+} gsx_score_snapshot;
+int gsx_peer_score_snapshot(gsx_engine* e, gsx_score_snapshot* s);
+
 /* Seeded synthetic counter state, generated on the device (BASELINE.md cfg3
  * initialisation).  Every draw is u = (h(seed, 4, a, k) >> 11) * 2^-53 with
  * h the SplitMix64-based counter hash of gsx/synth.py, a = t*n_pairs + p for

@@ -579,6 +579,9 @@ int orc_set_pair_ips(orc_engine* o, const uint64_t* pairs, const uint32_t* ips, 
     return 0;
 }
 
+/* PeerScoreSnapshot.IPColocationFactor of every pair (inspectScoresExtended, score.go:487) */
+int orc_ip_colocation_factors(orc_engine* o, double* out);
+
 static void ipcount_rebuild(orc_engine* o) {
     memset(o->ipc.vals, 0, sizeof(uint32_t) * o->ipc.cap);
     for (uint64_t q = 0; q < o->E; q++)
@@ -603,6 +606,11 @@ static double ip_colocation_factor(const orc_engine* o, uint64_t p) {
         }
     }
     return result;
+}
+
+int orc_ip_colocation_factors(orc_engine* o, double* out) {
+    for (uint64_t p = 0; p < o->E; p++) out[p] = ip_colocation_factor(o, p);
+    return 0;
 }
 
 /* score(), score.go:258-335; topics in ascending index order */

@@ -80,6 +80,7 @@ int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_wind
 int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);
 int orc_set_app_scores(orc_engine* o, const double* app, size_t n_pairs);
 int orc_set_pair_ips(orc_engine* o, const uint64_t* pairs, const uint32_t* ips, size_t n);
+int orc_ip_colocation_factors(orc_engine* o, double* out);
 
 int orc_apply_events(orc_engine* o, const gsx_event* ev, size_t n);
 

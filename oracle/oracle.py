@@ -34,6 +34,7 @@ _SIG = {
     "orc_set_thresholds": (C.c_int, [C.c_void_p, P(abi.Thresholds)]),
     "orc_prop_set_dup_tracking": (C.c_int, [C.c_void_p, C.c_int]),
     "orc_set_pair_ips": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_size_t]),
+    "orc_ip_colocation_factors": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "orc_prop_duplicates": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
     "orc_propagate": (
         C.c_int,
@@ -167,6 +168,17 @@ class Oracle:
         ips = np.ascontiguousarray(ips, dtype=np.uint32).reshape(-1, 2)
         self._chk(self.lib.orc_set_pair_ips(self.h, _p(pairs, C.c_uint64), _p(ips, C.c_uint32), len(pairs)),
                   "orc_set_pair_ips")
+
+    def snapshot(self):
+        """The PeerScoreSnapshot fields (gsx_peer_score_snapshot's layout) from the oracle's state."""
+        st = self.export_state()
+        p6 = np.zeros(self.n_pairs)
+        self._chk(self.lib.orc_ip_colocation_factors(self.h, _p(p6, C.c_double)), "orc_ip_colocation_factors")
+        return {"present": (st["pair_flags"] & abi.GSX_PAIR_PRESENT != 0).astype(np.uint8), "score": self.scores(),
+                "ip_colocation_factor": p6, "behaviour_penalty": st["behaviour_penalty"],
+                "time_in_mesh_ns": st["mesh_time_ns"], "first_message_deliveries": st["first_message_deliveries"],
+                "mesh_message_deliveries": st["mesh_message_deliveries"],
+                "invalid_message_deliveries": st["invalid_message_deliveries"]}
 
     def set_dup_tracking(self, on: bool = True):
         """Record which copies of the next propagations are duplicates (orc_prop_duplicates)."""

@@ -145,3 +145,20 @@ def test_engine_set_pair_ips_matches_oracle(gpu_ok):
     want, _ = ic.run(orc.Oracle(1))
     for i, (g, w) in enumerate(zip(got, want)):
         assert_same_scores(g, w, f"step {i}")
+
+
+@pytest.mark.parametrize("seed", [4, 12])
+def test_engine_snapshot_matches_oracle(gpu_ok, seed):
+    """gsx_peer_score_snapshot (inspectScoresExtended, score.go:463-493) == the
+    oracle's PeerScoreSnapshot fields after a random call sequence (IP moves,
+    retention, grafts, deliveries)."""
+    T = 3
+    ov = R.small_overlay(900, 4, seed, 150)
+    ops = R.make_ops(ov, T, seed, n_steps=150)
+    g, w = gsx.Engine(T), orc.Oracle(T)
+    R.replay(g, ov, T, ops)
+    R.replay(w, ov, T, ops)
+    gs, ws = g.snapshot(), w.snapshot()
+    assert int(gs["present"].sum()) > 0
+    for f in ws:
+        assert np.array_equal(np.asarray(gs[f]).view(np.uint8), np.asarray(ws[f]).view(np.uint8)), f

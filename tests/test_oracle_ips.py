@@ -19,3 +19,12 @@ def test_set_pair_ips_moves_p6():
     np.testing.assert_array_equal(out[4], [-1, 0, 0, -1, 0])
     # retained A leaves 1 for 3: {A} (E's 3 was never E's), D alone on 1
     np.testing.assert_array_equal(out[5], [0, 0, 0, 0, 0])
+
+
+def test_oracle_snapshot_ip_factor():
+    """PeerScoreSnapshot.IPColocationFactor is the unweighted P6 (weight -1 here: -score)."""
+    o = orc.Oracle(1)
+    out, K = ic.run(o)
+    snap = o.snapshot()
+    np.testing.assert_array_equal(snap["ip_colocation_factor"], -out[-1] + 0.0)
+    assert snap["present"].tolist() == [1, 1, 1, 1, 1]
