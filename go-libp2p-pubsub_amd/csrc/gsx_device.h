@@ -215,6 +215,19 @@ struct PropState {
     uint64_t seed;
     uint32_t* hop_flag;  // host-mapped, [hop]: k_prop_mark(h) stores (hop_seq << 1) | (hop h-1 delivered); null: off
     uint32_t hop_seq;
+    // Compacted senders for k_prop_hop_fast: node u's pairs whose pin is not
+    // NO_PAIR, packed at the front of its own pair range (row_ptr[u] ..
+    // cend[u]) as (pin, pair).  Kept current with pin: rebuilt for the nodes
+    // whose pins a changed fwd byte touched (k_prop_fwd's change list).
+    uint2* cent;
+    uint32_t* cend;
+    uint8_t* rfwd;       // [pair q]: fwd of the reverse pair (k_prop_pin), so k_prop_dups reads it coalesced
+    uint32_t* chg;       // [chg_cap] pairs whose fwd byte changed this call (k_prop_fwd)
+    uint32_t* nchg;      // their count (> chg_cap: rebuild every pin)
+    uint64_t* ndirty;    // [node / 64] nodes whose compacted row must be rebuilt
+    uint32_t chg_cap;
+    uint32_t inc;        // fwd / pin / cent hold the previous call's values: update them incrementally
+    uint32_t flast_every;  // k_prop_hop_fast keeps flast at every hop (stepped calls), else at max_hops only
 };
 
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st);

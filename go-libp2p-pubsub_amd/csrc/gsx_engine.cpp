@@ -188,6 +188,11 @@ struct gsx_engine {
         gsx::DevMsg* msgs = nullptr;
         unsigned long long* stats = nullptr;
         unsigned long long* gray_pairs = nullptr;  // pairs with FWD_GIN of the current fwd (k_prop_fwd)
+        uint2* cent = nullptr;                     // compacted senders (k_prop_compact)
+        uint8_t* rfwd = nullptr;                   // fwd of each pair's reverse (k_prop_pin)
+        uint32_t *cend = nullptr, *chg = nullptr, *nchg = nullptr;
+        uint64_t* ndirty = nullptr;
+        uint32_t chg_cap = 0;
         uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
         size_t dig_cap = 0;
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
@@ -464,6 +469,7 @@ void free_state(gsx_engine* e) {
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
                   e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
+                  e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
                   e->prop.d_dig};
     for (void* p : pp)
         if (p) (void)hipFree(p);
@@ -1746,6 +1752,13 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.eflags = e->d_eflags;
     ps.fwd = P.fwd;
     ps.pin = P.pin;
+    ps.cent = P.cent;
+    ps.rfwd = P.rfwd;
+    ps.cend = P.cend;
+    ps.chg = P.chg;
+    ps.nchg = P.nchg;
+    ps.ndirty = P.ndirty;
+    ps.chg_cap = P.chg_cap;
     ps.corr = P.corr;
     ps.occ = P.occ;
     ps.max_hops = cfg->max_hops;
@@ -1868,10 +1881,17 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
             (rc = dalloc(e, &P.stats, (size_t)gsx::STAT_WORDS)))
             return rc;
         if (!P.fwd) {
+            P.chg_cap = (uint32_t)std::min<size_t>(std::max<size_t>(E / 16, 1024), 1u << 24);
             if ((rc = dalloc(e, &P.fwd, E)) || (rc = dalloc(e, &P.pin, E)) || (rc = dalloc(e, &P.dup, E)) ||
                 (rc = dalloc(e, &P.corr, E)) || (rc = dalloc(e, &P.fcnt, E)) || (rc = dalloc(e, &P.flast, E)) ||
-                (rc = dalloc(e, &P.first, E)) || (rc = dalloc(e, &P.inv, E)) || (rc = dalloc(e, &P.gray_pairs, 1)))
+                (rc = dalloc(e, &P.first, E)) || (rc = dalloc(e, &P.inv, E)) || (rc = dalloc(e, &P.gray_pairs, 1)) ||
+                (rc = dalloc(e, &P.cent, E)) || (rc = dalloc(e, &P.cend, std::max<size_t>(N, 1))) ||
+                (rc = dalloc(e, &P.rfwd, E)) ||
+                (rc = dalloc(e, &P.chg, P.chg_cap)) || (rc = dalloc(e, &P.nchg, 1)) ||
+                (rc = dalloc(e, &P.ndirty, (N + 63) / 64 + 1)))
                 return rc;
+            HIPCHK(e, hipMemsetAsync(P.nchg, 0, 4, e->stream));
+            HIPCHK(e, hipMemsetAsync(P.ndirty, 0, 8 * ((N + 63) / 64 + 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * std::max<size_t>(E, 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * std::max<size_t>(E, 1), e->stream));
             HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -1969,10 +1989,10 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, msgs[k].validation, msgs[k].msg_id};
     HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.hist, 0, 8 * (size_t)W * N, e->stream));  // row 0: the publishes
+    // hist row 0 and origin: only the sources' rows are read (under occupancy
+    // row 0) and cleared (k_prop_zero_src in launch_prop_init)
     HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
     HIPCHK(e, hipMemsetAsync(P.touch, 0, 16 * ((N + 63) / 64), e->stream));  // both buffers (k_prop_mark clears them after)
-    HIPCHK(e, hipMemsetAsync(P.origin, 0, 8 * (size_t)W * N, e->stream));
     if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
     HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
     HIPCHK(e, hipMemsetAsync(P.fcnt, 0, 4 * std::max<size_t>(E, 1), e->stream));
@@ -2011,7 +2031,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
                           (!need_score || K.score_gen == e->score_gen);
     if (!fwd_same) {
         HIPCHK(e, hipMemsetAsync(P.gray_pairs, 0, 8, e->stream));
-        HIPCHK(e, gsx::launch_prop_fwd(ps, ds, e->stream));
+        // the last call's fwd bytes, pins and compacted senders stand: update
+        // what the changed bytes feed (unsharded: a shard's reverse pairs are its plan's)
+        gsx::PropState pf = ps;
+        pf.inc = (K.valid && !e->sharded()) ? 1u : 0u;
+        HIPCHK(e, gsx::launch_prop_fwd(pf, ds, e->stream));
         K.valid = true;
         K.router = cfg->router;
         K.topic = cfg->topic;
@@ -2258,7 +2282,9 @@ int gsx_prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
         return fail(e, GSX_ESTATE, "shard plan incomplete: gsx_shard_send_plan first");
     if (e->loaded && e->sharded() && e->n_ranks == 1 && e->n_total != e->n_nodes)
         return fail(e, GSX_ESTATE, "shard plan missing: gsx_shard_recv_plan / gsx_shard_send_plan first");
-    return prop_begin(e, msgs, m, cfg);
+    if (int rc = prop_begin(e, msgs, m, cfg)) return rc;
+    e->prop.last.flast_every = 1;  // the caller may end the call after any hop
+    return GSX_OK;
 }
 
 int gsx_prop_pack(gsx_engine* e, uint64_t* send) {

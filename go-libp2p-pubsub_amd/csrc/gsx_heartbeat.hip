@@ -850,28 +850,43 @@ __device__ __forceinline__ bool gossip_target(const DevState& s, const HbState& 
            live_score(s, h, r) >= h.gossip_threshold;
 }
 
-// A cached batch's per-node summary (count, digest of its ids): once per batch.
+// A cached batch's per-node summary (count, digest of its ids): once per
+// batch.  G lanes per node, each over 4-word chunks of the row, so a wave
+// reads whole 128-B rows (G = 4 at 16 words) instead of one word per lane
+// at a 128-B stride; the group sums its counts and digests with shuffles.
+template <int G>
 __global__ __launch_bounds__(256) void k_mc_summary(const uint64_t* __restrict__ seen, uint32_t n_nodes,
                                                     uint32_t n_words, uint32_t n_msgs,
                                                     const uint64_t* __restrict__ msg_dig,
                                                     const uint64_t* __restrict__ word_dig, uint64_t* __restrict__ dig,
                                                     uint32_t* __restrict__ cnt) {
-    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n_nodes; v += gridDim.x * 256u) {
+    const uint32_t lc = threadIdx.x % G;
+    const uint32_t CWv = G > 1 ? 4 : n_words;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t / G < n_nodes; t += gridDim.x * 256u) {
+        const uint32_t v = t / G;
         uint32_t L = 0;
         uint64_t d = 0;
-        for (uint32_t w = 0; w < n_words; ++w) {
-            uint64_t word = seen[(size_t)v * n_words + w];
-            L += (uint32_t)__popcll(word);
-            const uint32_t left = n_msgs > w * 64 ? n_msgs - w * 64 : 0;
-            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
-            if (word && word == full) {  // every message of the word (the common case once a batch has spread)
-                d += word_dig[w];
-                continue;
+        for (uint32_t w0 = lc * CWv; w0 < n_words; w0 += G * CWv)
+            for (uint32_t w = w0; w < w0 + CWv; ++w) {
+                uint64_t word = seen[(size_t)v * n_words + w];
+                L += (uint32_t)__popcll(word);
+                const uint32_t left = n_msgs > w * 64 ? n_msgs - w * 64 : 0;
+                const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                if (word && word == full) {  // every message of the word (the common case once a batch has spread)
+                    d += word_dig[w];
+                    continue;
+                }
+                for (; word; word &= word - 1) d += msg_dig[w * 64 + (uint32_t)__builtin_ctzll(word)];
             }
-            for (; word; word &= word - 1) d += msg_dig[w * 64 + (uint32_t)__builtin_ctzll(word)];
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            L += __shfl_xor(L, o, G);
+            d += __shfl_xor(d, o, G);
         }
-        dig[v] = d;
-        cnt[v] = L;
+        if (lc == 0) {
+            dig[v] = d;
+            cnt[v] = L;
+        }
     }
 }
 
@@ -1525,8 +1540,16 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
                              const uint64_t* msg_dig, const uint64_t* word_dig, uint64_t* dig, uint32_t* cnt,
                              hipStream_t st) {
     if (n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mc_summary, dim3(grid_cap(n_nodes, 256)), dim3(256), 0, st, seen, n_nodes, n_words, n_msgs,
-                       msg_dig, word_dig, dig, cnt);
+    const uint64_t nn = n_nodes;
+    if (n_words % 16 == 0)
+        hipLaunchKernelGGL(k_mc_summary<4>, dim3(grid_cap(4 * nn, 256)), dim3(256), 0, st, seen, n_nodes, n_words,
+                           n_msgs, msg_dig, word_dig, dig, cnt);
+    else if (n_words % 8 == 0)
+        hipLaunchKernelGGL(k_mc_summary<2>, dim3(grid_cap(2 * nn, 256)), dim3(256), 0, st, seen, n_nodes, n_words,
+                           n_msgs, msg_dig, word_dig, dig, cnt);
+    else
+        hipLaunchKernelGGL(k_mc_summary<1>, dim3(grid_cap(nn, 256)), dim3(256), 0, st, seen, n_nodes, n_words, n_msgs,
+                           msg_dig, word_dig, dig, cnt);
     return hipGetLastError();
 }
 

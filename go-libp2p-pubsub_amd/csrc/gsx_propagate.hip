@@ -71,7 +71,15 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
             out |= FWD_GIN;
             ++n_gray[0];
         }
-        ps.fwd[r] = out;
+        if (ps.inc) {  // the pins of the last call stand but for the pairs whose byte changed
+            if (ps.fwd[r] != out) {
+                const uint32_t k = atomicAdd(ps.nchg, 1u);
+                if (k < ps.chg_cap) ps.chg[k] = (uint32_t)r;
+                ps.fwd[r] = out;
+            }
+        } else {
+            ps.fwd[r] = out;
+        }
     }
     const uint32_t slot[1] = {0};
     block_count<1>(n_gray, ps.gray_pairs, slot);
@@ -84,25 +92,92 @@ __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
 // candidates have neither and go through `sel`).  (Gathering fwd per q here
 // is cheaper than scattering pin from k_prop_fwd: 1-byte reads from a small
 // array vs 4-byte partial-line writes.)
-__global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
-    const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (q >= ps.n_pairs) return;
+// Also keeps rfwd[q] = fwd[rev q], the reverse pair's byte (k_prop_dups reads
+// it coalesced instead of gathering it).
+__device__ __forceinline__ uint32_t pin_of(const PropState& ps, uint64_t q) {
     const uint32_t r = ps.rev[q];
     const bool gin = ps.fwd[q] & FWD_GIN;  // u drops whatever v sends (AcceptFrom)
     uint32_t out = NO_PAIR;
+    uint8_t rf = 0;
     if (r != NO_PAIR) {
         if (r & HALO) {
             // remote v: its rank packs what it sends either way; u counts the
             // copies it drops (k_prop_hop)
             out = gin ? (r | HALO_GRAY) : r;
-        } else if (!gin) {
+        } else {
             const uint8_t fw = ps.fwd[r];
-            if (fw & FWD_SEND)
+            rf = fw;
+            if (!gin && (fw & FWD_SEND))
                 out = ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | ((fw & FWD_GIN) ? PIN_RDROP : 0u) |
                       ((uint32_t)ps.col[q] - ps.node_lo);
         }
     }
-    ps.pin[q] = out;
+    ps.rfwd[q] = rf;
+    return out;
+}
+
+// Every pin (first call, or more changed fwd bytes than the change list
+// holds), or (ps.inc) only the pins a changed byte feeds: pin[r] (its GIN
+// bit) and pin[rev r] (what it lets through), marking their observers for
+// k_prop_compact.  One launch over all pairs either way; in the incremental
+// case every thread past the list returns at once.
+__global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
+    const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (q >= ps.n_pairs) return;
+    const uint32_t n = ps.inc ? *ps.nchg : 0;
+    if (!ps.inc || n > ps.chg_cap) {
+        ps.pin[q] = pin_of(ps, q);
+        return;
+    }
+    if (q >= n) return;
+    const uint32_t r = ps.chg[q];
+    ps.pin[r] = pin_of(ps, r);
+    const uint32_t v = ps.pair_obs[r];
+    atomicOr((unsigned long long*)&ps.ndirty[v / 64], 1ull << (v % 64));
+    const uint32_t q2 = ps.rev[r];
+    if (q2 != NO_PAIR && !(q2 & HALO)) {
+        ps.pin[q2] = pin_of(ps, q2);
+        const uint32_t u = ps.pair_obs[q2];
+        atomicOr((unsigned long long*)&ps.ndirty[u / 64], 1ull << (u % 64));
+    }
+}
+
+// Node u's compacted senders (ps.cent / ps.cend): every node after a full
+// pin pass, else the nodes k_prop_pin marked (their marks cleared here).
+__global__ __launch_bounds__(256) void k_prop_compact(PropState ps) {
+    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
+    if (u >= ps.n_nodes) return;
+    const bool full = !ps.inc || *ps.nchg > ps.chg_cap;
+    if (!full) {
+        const uint64_t w = ps.ndirty[u / 64];
+        if (!((w >> (u % 64)) & 1)) return;
+    }
+    const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
+    int64_t k = q0;
+    for (int64_t q = q0; q < q1; ++q) {
+        const uint32_t pn = ps.pin[q];
+        if (pn != NO_PAIR) ps.cent[k++] = make_uint2(pn, (uint32_t)q);
+    }
+    ps.cend[u] = (uint32_t)k;
+}
+__global__ __launch_bounds__(256) void k_prop_compact_done(PropState ps) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < (ps.n_nodes + 63) / 64) ps.ndirty[i] = 0;
+    if (i == 0) *ps.nchg = 0;  // the next call's change list starts empty
+}
+
+// The origin and hop-0 rows are read only for nodes with their row-0
+// occupancy bit (the call's sources), so only the sources' rows are cleared
+// (k_prop_zero_src), not the whole [node][W] arrays.
+__global__ __launch_bounds__(256) void k_prop_zero_src(PropState ps, uint64_t* front) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t W = ps.n_words;
+    if (i >= (uint64_t)ps.n_msgs * W) return;
+    const uint32_t src = ps.msgs[i / W].source;
+    if (src < ps.node_lo || src - ps.node_lo >= ps.n_nodes) return;
+    const size_t r = (size_t)(src - ps.node_lo) * W + i % W;
+    ps.origin[r] = 0;
+    front[r] = 0;
 }
 
 // Sources on this shard: seen / frontier / origin bits and hop 0 (the local publish).
@@ -204,7 +279,7 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
             const uint64_t f = front[(size_t)v * W + w];
             uint64_t c = 0;
             if (f) {
-                const uint64_t own = ps.origin[(size_t)v * W + w];
+                const uint64_t own = occ_bit(ps.occ, v) ? ps.origin[(size_t)v * W + w] : 0;  // rows of sources only
                 uint64_t el = elig_word(fw, own);
                 if (ps.sel) el |= ps.sel[(size_t)r * W + w];
                 c = f & el;
@@ -249,7 +324,7 @@ __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const u
                 for (uint32_t w = 0; w < W; ++w) {
                     const uint64_t f = front[(size_t)v * W + w];
                     if (!f) continue;
-                    uint64_t el = elig_word(fw, ps.origin[(size_t)v * W + w]);
+                    uint64_t el = elig_word(fw, occ_bit(ps.occ, v) ? ps.origin[(size_t)v * W + w] : 0);
                     if (ps.sel) el |= ps.sel[(size_t)r * W + w];
                     uint64_t c = f & el;
                     nsend[0] += c != 0;
@@ -271,7 +346,7 @@ __global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const u
                 const uint64_t f = front[(size_t)v * W + w];
                 uint64_t c = 0;
                 if (f) {
-                    uint64_t el = elig_word(fw, ps.origin[(size_t)v * W + w]);
+                    uint64_t el = elig_word(fw, occ_bit(ps.occ, v) ? ps.origin[(size_t)v * W + w] : 0);
                     if (ps.sel) el |= ps.sel[(size_t)r * W + w];
                     c = f & el & ~hf[w];
                 }
@@ -408,7 +483,8 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     if (h > 1 && prev == 0) return;
-    const bool use_occ = prev < ps.n_nodes / 4;
+    // (hop 1 always: the rows of hop 0 are written for the sources only)
+    const bool use_occ = h == 1 || prev < ps.n_nodes / 4;
     const bool use_mark = mark_hop(ps, h);
     // rows of hop h - 1 can be stale only if that hop left nodes untouched
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
@@ -421,7 +497,8 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
         bool touch = u < ps.n_nodes;
         if (touch && use_mark) touch = occ_bit(touch_h, u);
         if (touch) {
-            const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
+            // only the pairs whose neighbour sends to u at all (compacted, k_prop_compact)
+            const int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
             const size_t un = (size_t)u * W;
             // (u's own messages need no mask here: they are in `seen` since
             // hop 0, and duplicates are counted at the end of the call)
@@ -434,15 +511,16 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                 }
 #pragma unroll
                 for (int i = 0; i < CW; ++i) sa[i] = seen[i];
-                uint32_t pn[U];
+                uint2 pn[U];
 #pragma unroll
-                for (int j = 0; j < U; ++j) pn[j] = q0 + j < q1 ? ps.pin[q0 + j] : NO_PAIR;
+                for (int j = 0; j < U; ++j) pn[j] = q0 + j < q1 ? ps.cent[q0 + j] : make_uint2(NO_PAIR, 0u);
                 for (int64_t qb = q0; qb < q1; qb += U) {
-                    uint32_t pv[U];
+                    uint32_t pv[U], qv[U];
                     uint64_t c[U][CW];
 #pragma unroll
                     for (int j = 0; j < U; ++j) {
-                        pv[j] = pn[j];
+                        pv[j] = pn[j].x;
+                        qv[j] = pn[j].y;
                         if (use_occ && pv[j] != NO_PAIR && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK)) pv[j] = NO_PAIR;
                     }
 #pragma unroll
@@ -452,11 +530,8 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] = 0;
                     }
-                    uint32_t fc[U];
 #pragma unroll
-                    for (int j = 0; j < U; ++j) fc[j] = lc == 0 && pv[j] != NO_PAIR ? ps.fcnt[qb + j] : 0;
-#pragma unroll
-                    for (int j = 0; j < U; ++j) pn[j] = qb + U + j < q1 ? ps.pin[qb + U + j] : NO_PAIR;
+                    for (int j = 0; j < U; ++j) pn[j] = qb + U + j < q1 ? ps.cent[qb + U + j] : make_uint2(NO_PAIR, 0u);
                     if (check_rows)
 #pragma unroll
                         for (int j = 0; j < U; ++j)
@@ -503,11 +578,17 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                         if (LPN > 1) fresh = group_sum<LPN>(fresh);
                         if (DROP && LPN > 1) inv = group_sum<LPN>(inv);
                         if (lc == 0 && fresh) {
-                            const int64_t q = qb + j;
-                            ps.fcnt[q] = fc[j] + fresh;
-                            ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
+                            // first receipts from the pair: an add at L2, nothing read back
+                            // (every pair has one writer per hop, but no load round trip)
+                            const uint32_t q = qv[j];
+                            atomicAdd(&ps.fcnt[q], fresh);
+                            // the last hop's receipts matter only if that hop is the
+                            // max_hops cut (a run that ends with an empty hop forwarded
+                            // everything, k_prop_dups); flast is zeroed per call
+                            if (h == ps.max_hops || ps.flast_every)
+                                ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
                         }
-                        if (DROP && lc == 0 && inv && ps.credit) ps.invcnt[qb + j] += inv;  // P4
+                        if (DROP && lc == 0 && inv && ps.credit) ps.invcnt[qv[j]] += inv;  // P4
                     }
                 }
 #pragma unroll
@@ -576,7 +657,8 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
     // a node no sender marked is left untouched (no row loads, no row
     // writes, occupancy bit 0).  Dense: rows are gathered beside their
     // occupancy bits.
-    const bool use_occ = prev < ps.n_nodes / 4;
+    // (hop 1 always: the rows of hop 0 are written for the sources only)
+    const bool use_occ = h == 1 || prev < ps.n_nodes / 4;
     const bool use_mark = mark_hop(ps, h);
     // rows of hop h - 1 can be stale only if that hop left nodes untouched
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
@@ -908,11 +990,12 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             va[i] = in ? ps.pair_obs[r] : 0;
             ua[i] = in ? (uint32_t)ps.col[r] - ps.node_lo : 0;
         }
-        bool ga[DU];  // u drops v's copies
+        bool ga[DU];  // u drops v's copies: the GIN bit of u's pair (v's reverse), kept beside r by k_prop_pin
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
+            const uint64_t r = r0 + i * stride;
             const bool local = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
-            ga[i] = local && ps.gate && (ps.fwd[qa[i]] & FWD_GIN);
+            ga[i] = local && ps.gate && (ps.rfwd[r] & FWD_GIN);
             if (GRAY_ONLY && !ga[i]) qa[i] = NO_PAIR;
         }
         uint64_t vca[DU], fla[DU];
@@ -1183,7 +1266,8 @@ __global__ __launch_bounds__(256) void k_prop_uncache(PropState ps, bool mask_ca
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < (uint64_t)ps.n_nodes * W; i += (uint64_t)gridDim.x * 256u) {
         const uint32_t w = (uint32_t)(i % W);
         const uint64_t d = ps.drop[w];
-        const uint64_t rx = d & ps.seen[i] & ~ps.origin[i];
+        const uint32_t u = (uint32_t)(i / W);
+        const uint64_t rx = d & ps.seen[i] & ~(occ_bit(ps.occ, u) ? ps.origin[i] : 0ull);  // origin rows: sources only
         ps.dseen[i] = rx;
         if (mask_cache && rx) ps.seen[i] &= ~rx;
     }
@@ -1212,10 +1296,15 @@ hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t s
     if (s.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
     hipLaunchKernelGGL(k_prop_pin, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
+    if (ps.n_nodes) {
+        hipLaunchKernelGGL(k_prop_compact, dim3(nblk(ps.n_nodes, 256)), dim3(256), 0, st, ps);
+        hipLaunchKernelGGL(k_prop_compact_done, dim3(nblk((ps.n_nodes + 63) / 64, 256)), dim3(256), 0, st, ps);
+    }
     return hipGetLastError();
 }
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st) {
     if (ps.n_msgs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_zero_src, dim3(nblk((uint64_t)ps.n_msgs * ps.n_words, 256)), dim3(256), 0, st, ps, front);
     hipLaunchKernelGGL(k_prop_init, dim3(nblk(ps.n_msgs, 256)), dim3(256), 0, st, ps, front);
     return hipGetLastError();
 }
