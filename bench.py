@@ -366,7 +366,10 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
         out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
     else:
         out["exchange"] = {"compacted": runner.compact, "bytes_sent_per_batch_rank": runner.sent_bytes / (args.prop_steps + 1),
-                           "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8}
+                           "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8,
+                           "hops_per_batch": runner.hops_run / (args.prop_steps + 1),
+                           "host_syncs_per_hop": runner.host_syncs / max(runner.hops_run, 1),
+                           "ms_per_hop": el / max(runner.hops_run * args.prop_steps / (args.prop_steps + 1), 1) * 1e3}
     return out
 
 

@@ -111,7 +111,8 @@ struct DevSynthSpec {
 };
 
 // ---- propagation (gsx_propagate.hip) -------------------------------------------
-constexpr uint8_t EDGE_OUTBOUND = 0x01, EDGE_DIRECT = 0x02, EDGE_GOSSIPSUB = 0x04, EDGE_FLOODSUB = 0x08;
+constexpr uint8_t EDGE_OUTBOUND = 0x01, EDGE_DIRECT = 0x02, EDGE_GOSSIPSUB = 0x04, EDGE_FLOODSUB = 0x08,
+                  EDGE_NO_PX = 0x10;
 constexpr uint32_t ROUTER_FLOODSUB = 0, ROUTER_GOSSIPSUB = 1, ROUTER_RANDOMSUB = 2;
 constexpr uint32_t NO_PAIR = 0xFFFFFFFFu;
 constexpr uint8_t FWD_FORWARD = 0x01;    // v sends messages it received to u
@@ -237,6 +238,8 @@ hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const ui
                             hipStream_t st);
 hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, const uint64_t* front_occ,
                                     uint64_t* out, unsigned long long* dcount, hipStream_t st);
+hipError_t launch_pack_counts(const unsigned long long* dcount, const unsigned long long* hop_new, uint32_t world,
+                              int64_t* out, hipStream_t st);
 hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st);
 hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
                                uint64_t* halo_occ, uint32_t h, hipStream_t st);
@@ -277,6 +280,10 @@ enum {
     HB_GOSSIP_DELIVERED,
     HB_GOSSIP_REJECTED,
     HB_GOSSIP_DUPLICATES,
+    HB_PX_PRUNES,
+    HB_PX_PEERS,
+    HB_PX_IGNORED,
+    HB_PX_CONNECT,
     HB_STAT_WORDS
 };  // the order of gsx_heartbeat_out
 
@@ -289,6 +296,7 @@ struct DevGossipParams {
     int32_t max_ihave_msgs, retransmission;  // MaxIHaveMessages, GossipRetransmission
     int64_t followup_ns;                      // IWantFollowupTime
     int64_t fanout_ttl;                       // FanoutTTL
+    int32_t do_px, prune_peers;               // WithPeerExchange, PrunePeers
 };
 
 // One advertised batch of the gossip exchange (heartbeat step (D)): the
@@ -310,7 +318,7 @@ __device__ __forceinline__ bool topic_peer(const uint64_t* psub, uint64_t r, uin
 __device__ __forceinline__ bool joined_node(const uint64_t* sub, uint32_t v, uint32_t t) {
     return !sub || ((sub[v] >> t) & 1);
 }
-constexpr uint64_t TAG_HEARTBEAT = 8, TAG_FANOUT = 10, TAG_JOIN = 11;  // draw tags (gsx.h)
+constexpr uint64_t TAG_HEARTBEAT = 8, TAG_FANOUT = 10, TAG_JOIN = 11, TAG_PX = 12;  // draw tags (gsx.h)
 constexpr int GX_PROMISE_SLOTS = 8;  // outstanding promises per pair (gossip_tracer.go:24-27)
 constexpr uint64_t TAG_IWANT = 9;
 
@@ -375,6 +383,11 @@ struct HbState {
     uint32_t fan_mode;     // k_hb_gossip: 0 the joined units' mesh gossip, 1 the fanout units' (:1553)
     uint32_t* mscratch;    // [pair]: candidate lists of the membership kernels (each row one lane's)
     const uint32_t* pair_obs;  // [pair]: its owner (local node; set with sub)
+    // peer exchange on PRUNE (do_px; null otherwise)
+    uint8_t* pxno;         // [pair]: bit 0 = (A) pruned it without PX, bit 1 = its (B) answers go without PX
+    uint32_t* px_log;      // [px_cap][4]: connection candidates (receiver, candidate, pruner, topic | kind << 8)
+    uint64_t px_cap;
+    double accept_px;      // AcceptPXThreshold
     double publish_threshold;
     const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
     uint32_t* long_nodes;  // nodes whose gossip list needs per-target truncation
@@ -426,6 +439,8 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
                              const uint64_t* msg_dig, const uint64_t* word_dig, uint64_t* dig, uint32_t* cnt,
                              hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
+// Peer exchange of the round's PRUNEs (gsx.h): kind 0 = (A) PRUNEs, 1 = (B) answers.
+hipError_t launch_hb_px(const DevState& s, const HbState& h, uint32_t kind, hipStream_t st);
 hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
                           uint64_t* out, hipStream_t st);
 

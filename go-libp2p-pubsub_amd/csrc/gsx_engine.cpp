@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -158,6 +159,12 @@ struct gsx_engine {
     int64_t* d_lastpub = nullptr;
     uint32_t *d_mscratch = nullptr, *d_mlist = nullptr;
     size_t mlist_cap = 0;
+    // peer exchange on PRUNE (do_px): per-pair noPX bits, the candidate-list
+    // scratch when membership is off, the connection-candidate log
+    uint8_t* d_pxno = nullptr;
+    uint32_t *d_pxscratch = nullptr, *d_pxlog = nullptr;
+    size_t px_cap = 0, pxlog_alloc = 0;
+    uint64_t px_last = 0;  // the last round's connection candidates
     std::vector<uint64_t> h_sub;  // host copy of the joined topics per node
     gsx::GxBatch* d_gx = nullptr;
     uint32_t* d_gx_off = nullptr;
@@ -524,6 +531,13 @@ void free_state(gsx_engine* e) {
         e->mlist_cap = 0;
         e->members_on = false;
         e->h_sub.clear();
+        void* pxp[] = {e->d_pxno, e->d_pxscratch, e->d_pxlog};
+        for (void* x : pxp)
+            if (x) (void)hipFree(x);
+        e->d_pxno = nullptr;
+        e->d_pxscratch = e->d_pxlog = nullptr;
+        e->pxlog_alloc = 0;
+        e->px_last = 0;
     }
     e->d_rngk = e->d_ihave_len = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
@@ -2325,15 +2339,16 @@ int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new) {
     return GSX_OK;
 }
 
-int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
-    if (!e || !counts) return GSX_EINVAL;
+namespace {
+// Pack the compacted exchange of hop P.h + 1 (the entry counts stay in P.dcount).
+int pack_compact(gsx_engine* e, uint64_t* out, bool* packed) {
     auto& P = e->prop;
+    *packed = false;
     if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
     if (e->n_send && !out) return GSX_EINVAL;
     if (e->n_send && !e->d_dest_halo_base) return fail(e, GSX_ESTATE, "gsx_shard_set_halo_bases first");
     if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
     const gsx::PropState& ps = P.last;
-    std::memset(counts, 0, 8 * (size_t)e->n_ranks);
     if (ps.n_msgs == 0 || e->n_send == 0) return GSX_OK;
     const uint64_t* front = P.hist + (size_t)P.h * ps.n_nodes * ps.n_words;
     const uint64_t* front_occ = P.occ + (size_t)P.h * ((ps.n_nodes + 63) / 64);
@@ -2346,8 +2361,29 @@ int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
     ++P.launches;
     HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, front_occ, out, P.dcount, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
-    HIPCHK(e, hipMemcpyAsync(counts, P.dcount, 8 * (size_t)e->n_ranks, hipMemcpyDeviceToHost, e->stream));
+    *packed = true;
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts) {
+    if (!e || !counts) return GSX_EINVAL;
+    bool packed = false;
+    if (int rc = pack_compact(e, out, &packed)) return rc;
+    std::memset(counts, 0, 8 * (size_t)e->n_ranks);
+    if (!packed) return GSX_OK;
+    HIPCHK(e, hipMemcpyAsync(counts, e->prop.dcount, 8 * (size_t)e->n_ranks, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_pack_compact_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts) {
+    if (!e || !d_counts) return GSX_EINVAL;
+    bool packed = false;
+    if (int rc = pack_compact(e, out, &packed)) return rc;
+    auto& P = e->prop;
+    const unsigned long long* hop_new = P.last.n_msgs ? P.stats + gsx::STAT_HOP0 + P.h : nullptr;
+    HIPCHK(e, gsx::launch_pack_counts(packed ? P.dcount : nullptr, hop_new, e->n_ranks, d_counts, e->stream));
     return GSX_OK;
 }
 
@@ -2508,6 +2544,8 @@ int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
     p->iwant_followup_ns = 3LL * 1000000000LL;
     p->gossip_exchange = 0;
     p->fanout_ttl_ns = 60LL * 1000000000LL;
+    p->do_px = 0;           // WithPeerExchange is opt-in (:325-333)
+    p->prune_peers = 16;    // GossipSubPrunePeers
     return GSX_OK;
 }
 
@@ -2525,6 +2563,8 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
                                    "MaxIHaveLength, GossipFactor >= 0");
     if (p->gossip_exchange && (p->max_ihave_messages < 0 || p->gossip_retransmission < 0 || p->iwant_followup_ns < 0))
         return fail(e, GSX_EINVAL, "need MaxIHaveMessages, GossipRetransmission, IWantFollowupTime >= 0");
+    if (p->do_px && p->prune_peers < 0) return fail(e, GSX_EINVAL, "need PrunePeers >= 0");
+    if (p->do_px != e->gp.do_px) e->hb_clean = false;  // PX reads every (A) PRUNE word: start from zeros
     e->gp = *p;
     return GSX_OK;
 }
@@ -2668,7 +2708,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                 e->gp.max_ihave_messages,
                                 e->gp.gossip_retransmission,
                                 e->gp.iwant_followup_ns,
-                                e->gp.fanout_ttl_ns};
+                                e->gp.fanout_ttl_ns,
+                                e->gp.do_px,
+                                e->gp.prune_peers};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
     if (gx_on) {
@@ -2682,6 +2724,28 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.prom_e = e->d_prom_e;
         HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 16, e->stream));
+    }
+    if (e->gp.do_px && !state_only) {  // peer exchange on the round's PRUNEs (gsx.h)
+        if (e->sharded()) return fail(e, GSX_ESTATE, "peer exchange (do_px) runs on unsharded engines only");
+        const size_t E = std::max<size_t>(e->E, 1);
+        if (!e->d_pxno)
+            if (int rc = dalloc(e, &e->d_pxno, E)) return rc;
+        if (!e->members_on && !e->d_pxscratch)
+            if (int rc = dalloc(e, &e->d_pxscratch, E)) return rc;
+        if (e->px_cap > e->pxlog_alloc) {
+            if (e->d_pxlog) (void)hipFree(e->d_pxlog);
+            e->d_pxlog = nullptr;
+            e->pxlog_alloc = 0;
+            if (int rc = dalloc(e, &e->d_pxlog, 4 * e->px_cap)) return rc;
+            e->pxlog_alloc = e->px_cap;
+        }
+        HIPCHK(e, hipMemsetAsync(e->d_pxno, 0, E, e->stream));
+        h.pxno = e->d_pxno;
+        h.px_log = e->px_cap ? e->d_pxlog : nullptr;
+        h.px_cap = e->px_cap;
+        h.accept_px = e->th.accept_px_threshold;
+        h.col = e->d_col;
+        if (!e->members_on) h.mscratch = e->d_pxscratch;
     }
     const size_t E8 = 8 * (e->E ? e->E : 1);
     // Unsharded, (B) and (C) clear the control words, answers and marks they
@@ -2782,8 +2846,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // the receivers score the senders as the round left them: the pairs (A)
     // touched that (B) reads (marked in the inbox) are re-scored
     // (a shard's (B) reads every pair with remote control: all touched pairs)
+    // (with PX every touched pair: the PX lists read the owner's whole row)
     uint8_t* sel = h.dirty;
-    if (!e->sharded()) {
+    if (!e->sharded() && !h.pxno) {
         sel = e->d_dirty + 3 * e->E;
         HIPCHK(e, gsx::launch_mask_and(h.dirty, h.inbox, sel, e->E, e->stream));
     }
@@ -2802,11 +2867,13 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     gsx::HbState h = e->hb;
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
+    HIPCHK(e, gsx::launch_hb_px(ds, h, 0, e->stream));  // the (A) PRUNEs' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
     // the pairs touched so far that (C) reads: those marked with an answer
-    // (a shard's (C) reads every pair with a remote answer: all touched pairs)
+    // (a shard's (C) reads every pair with a remote answer: all touched pairs;
+    // with PX every touched pair: the answers' PX lists read the whole row)
     uint8_t* sel = h.dirty;
-    if (!e->sharded()) {
+    if (!e->sharded() && !h.pxno) {
         sel = e->d_dirty + 3 * e->E;
         HIPCHK(e, gsx::launch_mask_and(h.dirty, h.answer, sel, e->E, e->stream));
     }
@@ -2821,6 +2888,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     const gsx::DevState ds = dev_state(e);
     e->hb_active = false;
     std::memset(out, 0, sizeof(*out));
+    HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
     HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
@@ -2893,6 +2961,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
+    e->px_last = h.pxno ? st[gsx::HB_PX_CONNECT] : 0;
     // mcache.Shift (mcache.go:94-104, gossipsub.go:1563), after the stream drained
     while (e->mc.size() >= hist) {
         for (auto& b : e->mc.back()) batch_release(e, b);
@@ -3105,6 +3174,27 @@ int gsx_hb_trace_words(gsx_engine* e, uint64_t* sent_graft, uint64_t* sent_prune
         if (handled_prune) HIPCHK(e, hipMemcpyAsync(handled_prune, e->d_tr_hp, n, hipMemcpyDeviceToHost, e->stream));
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_hb_set_px_log(gsx_engine* e, size_t cap) {
+    if (!e) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    e->px_cap = cap;
+    return GSX_OK;
+}
+
+int gsx_hb_px_records(gsx_engine* e, uint32_t* out, size_t cap, size_t* n) {
+    if (!e || !n || (cap && !out)) return GSX_EINVAL;
+    if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
+    const size_t kept = std::min<size_t>((size_t)e->px_last, std::min(e->px_cap, e->pxlog_alloc));
+    *n = kept;
+    if (!kept || !cap) return GSX_OK;
+    std::vector<std::array<uint32_t, 4>> rec(kept);
+    HIPCHK(e, hipMemcpyAsync(rec.data(), e->d_pxlog, 16 * kept, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    std::sort(rec.begin(), rec.end());
+    std::memcpy(out, rec.data(), 16 * std::min(kept, cap));
     return GSX_OK;
 }
 

@@ -150,6 +150,7 @@ constexpr uint8_t ST_BACKOFF = 8;  // gs.backoff[topic][p] present (map presence
 constexpr uint8_t ST_GRAFT = 16;   // maintain() grafted the pair (effects applied by apply_events)
 constexpr uint8_t ST_PRUNE = 32;   // maintain() pruned the pair
 constexpr uint8_t ST_ACTIVE = 64;  // the record's mesh-delivery counting is active (REC_ACTIVE)
+constexpr uint8_t ST_NOPX = 128;   // pruned for a negative score: its PRUNE carries no PX (:1361-1368)
 
 __device__ __forceinline__ uint8_t stage_pack(uint8_t pf, uint8_t ef, uint8_t rf, bool bo, bool in_t = true) {
     uint8_t f = 0;
@@ -307,7 +308,10 @@ struct HbUnit {
         // drop all peers with negative score, without PX (:1361-1368)
         int n = mesh_list(plst);
         for (int i = 0; i < n; ++i)
-            if (score(plst[i]) < 0) prune(plst[i]);
+            if (score(plst[i]) < 0) {
+                prune(plst[i]);
+                fl[plst[i]] |= ST_NOPX;
+            }
         HBPU(0);
         // do we have enough peers? (:1370-1385)
         n = mesh_list(plst);
@@ -403,6 +407,7 @@ __device__ __forceinline__ void apply_events(const DevState& s, const HbState& h
         }
         add_backoff(h, r, t, h.gp.prune_backoff_ns);
         atomicOr((unsigned long long*)&h.ctl_prune[r], 1ull << t);
+        if ((f & ST_NOPX) && h.pxno) h.pxno[r] |= 1;  // noPX[p] (topic launches are sequential)
     }
     h.dirty[r] = 1;
     if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
@@ -1217,6 +1222,9 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             uint32_t r;
             uint64_t grafts, prunes;
             if (!recv_control(h, q, true, r, grafts, prunes)) continue;
+            // doPX = false for this RPC's PRUNE answers (:721-781): a GRAFT of a topic u
+            // has not joined, from a direct peer, inside the backoff or of a negative score
+            bool nopx = h.sub && (grafts & ~h.sub[u]);
             if (h.sub) {  // GRAFT / PRUNE of a topic u has not joined: ignored (:727-733, :816-819)
                 grafts &= h.sub[u];
                 prunes &= h.sub[u];
@@ -1236,10 +1244,12 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 if (ef & EDGE_DIRECT) {
                     resp |= 1ull << t;
                     ++rejected;
+                    nopx = true;
                     continue;
                 }
                 const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
                 if (expire != 0 && h.now < expire) {
+                    nopx = true;
                     ev_penalty(s, q, 1);
                     ++penalties;
                     if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
@@ -1255,6 +1265,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                     resp |= 1ull << t;
                     add_backoff(h, q, t, gp.prune_backoff_ns);
                     ++rejected;
+                    nopx = true;
                     continue;
                 }
                 // the mesh size (A) left, kept current by this lane's accepts and prunes
@@ -1276,6 +1287,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
             }
             h.resp[q] = resp;
             if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
+            if (h.pxno && nopx) h.pxno[q] |= 2;
             for (; prunes; prunes &= prunes - 1) {  // handlePrune
                 const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
                 if (handle_prune(s, h, q, t)) {
@@ -1322,6 +1334,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
                 if (w0 && !(r & HALO) && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                bool nopx = h.sub && (grafts & ~h.sub[u]);  // doPX = false (:721-781)
                 if (h.sub) {  // topics u has not joined: ignored (:727-733, :816-819)
                     grafts &= h.sub[u];
                     prunes &= h.sub[u];
@@ -1338,10 +1351,12 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                     if (ef & EDGE_DIRECT) {
                         resp |= 1ull << t;
                         rejected += w0;
+                        nopx = true;
                         continue;
                     }
                     const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
                     if (expire != 0 && h.now < expire) {
+                        nopx = true;
                         const bool twice = h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns);
                         if (w0) {
                             ev_penalty(s, q, 1);
@@ -1358,6 +1373,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                         resp |= 1ull << t;
                         if (w0) add_backoff(h, q, t, gp.prune_backoff_ns);
                         rejected += w0;
+                        nopx = true;
                         __syncthreads();
                         continue;
                     }
@@ -1385,6 +1401,7 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 if (w0) {
                     h.resp[q] = resp;
                     if (resp && !(r & HALO)) h.answer[r] = 1;
+                    if (h.pxno && nopx) h.pxno[q] |= 2;
                 }
                 for (; prunes; prunes &= prunes - 1) {
                     const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
@@ -1553,9 +1570,102 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
     return hipGetLastError();
 }
 
+// ---- peer exchange on PRUNE (gossipsub.go:811-843, 861-910, 1814-1850) ----------
+
+// One lane per pruning node u (kind 0: the (A) PRUNEs in ctl_prune, before
+// (B) reads them; kind 1: the (B) answers in resp, before (C) reads them),
+// its pairs ascending, each pruned topic ascending.  makePrune's
+// getPeers(topic, PrunePeers, xp != p && score(xp) >= 0) is staged in
+// mscratch over u's own row, shuffled with the draws of gsx.h and truncated;
+// then the receiver p's side: AcceptFrom, the joined-topic check of
+// handlePrune, AcceptPXThreshold on its score of u, and pxConnect's "not
+// connected" filter (p's row is sorted by peer: a binary search).  The scores
+// are the cache as the receiving step reads it (gsx.h).  PX is off by
+// default and this kernel runs only with do_px: candidates are logged with
+// one L2 atomic each.
+__global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t kind) {
+    uint64_t lists = 0, listed = 0, ignored = 0, connect = 0;
+    const uint8_t nobit = kind ? 2 : 1;
+    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        for (int64_t r = r0; r < r1; ++r) {  // r = (u -> p)
+            uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+            if (!bits) continue;
+            const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (unsharded: never HALO)
+            // (B) never reads nor clears the words of a pair its receiver does not
+            // track: cleared here, so each round's (A) bits start from zeros
+            if (q == NO_PAIR && !kind && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+            if ((h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
+            const uint32_t p = (uint32_t)h.col[r];
+            bool heard = q != NO_PAIR;
+            double rs = 0.0;
+            if (heard) {
+                rs = s.score[q];
+                if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) heard = false;  // AcceptFrom drops the RPC
+            }
+            for (; bits; bits &= bits - 1) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(bits);
+                int n = 0;
+                for (int64_t x = r0; x < r1; ++x) {  // getPeers' candidates, ascending peer
+                    if (x == r) continue;
+                    if ((s.pflags[x] & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED)) continue;
+                    if (!topic_peer(h.psub, (uint64_t)x, t) || !(h.eflags[x] & EDGE_GOSSIPSUB)) continue;
+                    if (!(s.score[x] >= 0.0)) continue;
+                    h.mscratch[r0 + n++] = (uint32_t)(x - r0);
+                }
+                Rng g{h.seed, TAG_PX, ((uint64_t)(h.node_lo + u) << 32) | (uint64_t)(h.node_lo + p),
+                      (h.tick << 32) | ((uint64_t)t << 24) | ((uint64_t)kind << 23), 0};
+                g.shuffle(h.mscratch + r0, n);
+                if (n > h.gp.prune_peers) n = h.gp.prune_peers;
+                if (n <= 0) continue;
+                ++lists;
+                listed += (uint64_t)n;
+                if (!heard || !joined_node(h.sub, p, t)) continue;  // handlePrune never reads it (:816-819)
+                if (rs < h.accept_px) {  // :833-838
+                    ++ignored;
+                    continue;
+                }
+                const int64_t p0 = h.row_ptr[p], p1 = h.row_ptr[p + 1];
+                for (int i = 0; i < n; ++i) {  // pxConnect (:861-910): the peers p is not connected to
+                    const int32_t xp = h.col[r0 + h.mscratch[r0 + i]];
+                    int64_t lo = p0, hi = p1;
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi) >> 1;
+                        if (h.col[mid] < xp) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    if (lo < p1 && h.col[lo] == xp && (s.pflags[lo] & PAIR_CONNECTED)) continue;
+                    if (h.px_log) {
+                        const unsigned long long k = atomicAdd(&h.stats[HB_PX_CONNECT], 1ull);
+                        if (k < h.px_cap) {
+                            uint32_t* o = h.px_log + 4 * k;
+                            o[0] = h.node_lo + p;
+                            o[1] = h.node_lo + (uint32_t)xp;
+                            o[2] = h.node_lo + u;
+                            o[3] = t | (kind << 8);
+                        }
+                    } else {
+                        ++connect;
+                    }
+                }
+            }
+        }
+    }
+    flush_count(h.stats, HB_PX_PRUNES, lists);
+    flush_count(h.stats, HB_PX_PEERS, listed);
+    flush_count(h.stats, HB_PX_IGNORED, ignored);
+    flush_count(h.stats, HB_PX_CONNECT, connect);
+}
+
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hb_answer, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_px(const DevState& s, const HbState& h, uint32_t kind, hipStream_t st) {
+    if (h.n_nodes == 0 || !h.pxno) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_px, dim3(grid_cap(h.n_nodes, 64)), dim3(64), 0, st, s, h, kind);
     return hipGetLastError();
 }
 

@@ -1327,6 +1327,22 @@ hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, 
                        front, front_occ, out, dcount);
     return hipGetLastError();
 }
+// The compacted exchange's count words, device-side: out[d] = (entries for
+// rank d, this rank's first receipts of its latest hop), so that one
+// all-to-all tells every receiver both its entry count and whether the hop
+// before delivered anything anywhere (no host round trip in between).
+__global__ void k_pack_counts(const unsigned long long* __restrict__ dcount,
+                              const unsigned long long* __restrict__ hop_new, uint32_t world, int64_t* __restrict__ out) {
+    const uint32_t d = threadIdx.x;
+    if (d >= world) return;
+    out[2 * d] = dcount ? (int64_t)dcount[d] : 0;
+    out[2 * d + 1] = hop_new ? (int64_t)*hop_new : 0;
+}
+hipError_t launch_pack_counts(const unsigned long long* dcount, const unsigned long long* hop_new, uint32_t world,
+                              int64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(MAX_RANKS), 0, st, dcount, hop_new, world, out);
+    return hipGetLastError();
+}
 hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_halo_clear, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, idx, n);

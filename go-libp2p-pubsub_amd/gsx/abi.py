@@ -27,6 +27,7 @@ GSX_EDGE_OUTBOUND = 0x01
 GSX_EDGE_DIRECT = 0x02
 GSX_EDGE_GOSSIPSUB = 0x04
 GSX_EDGE_FLOODSUB = 0x08
+GSX_EDGE_NO_PX = 0x10
 
 GSX_REC_IN_MESH = 0x01
 GSX_REC_ACTIVE = 0x02
@@ -308,6 +309,8 @@ class GossipSubParams(C.Structure):
         ("gossip_exchange", C.c_int32),
         ("reserved0", C.c_int32),
         ("fanout_ttl_ns", C.c_int64),
+        ("do_px", C.c_int32),
+        ("prune_peers", C.c_int32),
     ]
 
 
@@ -331,6 +334,10 @@ class HeartbeatOut(C.Structure):
         ("gossip_delivered", C.c_uint64),
         ("gossip_rejected", C.c_uint64),
         ("gossip_duplicates", C.c_uint64),
+        ("px_prunes", C.c_uint64),
+        ("px_peers", C.c_uint64),
+        ("px_ignored", C.c_uint64),
+        ("px_connect", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -399,6 +406,9 @@ SIGNATURES = {
     "gsx_shard_set_halo_bases": (C.c_int, [C.c_void_p, _u64p]),
     "gsx_prop_pack_compact": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),
     "gsx_prop_step_compact": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, _u64p]),
+    "gsx_prop_pack_compact_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_hb_set_px_log": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "gsx_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
     "gsx_prop_begin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig)]),
     "gsx_prop_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_prop_step": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),

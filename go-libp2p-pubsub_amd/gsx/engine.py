@@ -254,12 +254,21 @@ class Engine:
                   "gsx_prop_pack_compact")
         return cnt
 
-    def prop_step_compact(self, entries, n: int) -> int:
+    def prop_pack_compact_dev(self, out, counts):
+        """As prop_pack_compact, the counts left on the device: counts (device
+        tensor [n_ranks, 2] i64) = (entries for rank k, this rank's first
+        receipts of the hop just run); no host sync."""
+        p = out.data_ptr() if hasattr(out, "data_ptr") else out
+        self._chk(self.lib.gsx_prop_pack_compact_dev(self.h, C.c_void_p(p or None), C.c_void_p(counts.data_ptr())),
+                  "gsx_prop_pack_compact_dev")
+
+    def prop_step_compact(self, entries, n: int, sync: bool = True):
+        """-> this hop's first receipts on this rank; sync=False: no host sync, -> None."""
         p = entries.data_ptr() if hasattr(entries, "data_ptr") else entries
         v = C.c_uint64()
-        self._chk(self.lib.gsx_prop_step_compact(self.h, C.c_void_p(p or None), n, C.byref(v)),
+        self._chk(self.lib.gsx_prop_step_compact(self.h, C.c_void_p(p or None), n, C.byref(v) if sync else None),
                   "gsx_prop_step_compact")
-        return int(v.value)
+        return int(v.value) if sync else None
 
     def shard_counts(self):
         a, b = C.c_uint64(), C.c_uint64()
@@ -399,6 +408,19 @@ class Engine:
 
     def hb_set_tracing(self, on: bool = True):
         self._chk(self.lib.gsx_hb_set_tracing(self.h, 1 if on else 0), "gsx_hb_set_tracing")
+
+    def hb_set_px_log(self, cap: int):
+        """Keep up to cap PX connection candidates per heartbeat (gsx_hb_set_px_log)."""
+        self._chk(self.lib.gsx_hb_set_px_log(self.h, cap), "gsx_hb_set_px_log")
+
+    def hb_px_records(self):
+        """-> [n, 4] u32 (receiver, candidate, pruner, topic | kind << 8) of the last
+        heartbeat, sorted (gsx_hb_px_records: min(px_connect, log cap) of them are kept)."""
+        n = C.c_size_t()
+        self._chk(self.lib.gsx_hb_px_records(self.h, None, 0, C.byref(n)), "gsx_hb_px_records")
+        out = np.zeros((n.value, 4), dtype=np.uint32)
+        self._chk(self.lib.gsx_hb_px_records(self.h, _ptr(out, C.c_uint32), n.value, C.byref(n)), "gsx_hb_px_records")
+        return out
 
     def hb_trace_words(self):
         """-> (sent_graft, sent_prune, acc_graft, handled_prune) [E] u64 topic words

@@ -73,6 +73,15 @@ class DistTransport:
         if r is not recv:
             recv.copy_(r)
 
+    def all_to_all_parts(self, recv, recv_splits, send_parts):
+        """send_parts[k] (contiguous rows) -> rank k; recv gets rank k's rows at
+        the k-th split.  On RCCL the parts go as views (no gather copy)."""
+        if not self.stage and self.dist.get_backend(self.group) == "nccl":
+            outs = list(recv.split([int(x) for x in recv_splits], 0))
+            self.dist.all_to_all(outs, list(send_parts), group=self.group)
+            return
+        _parts_via_single(self, recv, recv_splits, send_parts)
+
     def all_reduce_sum(self, t):
         h = self._h(t)
         self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
@@ -84,6 +93,13 @@ class DistTransport:
         self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
         if h is not t:
             t.copy_(h)
+
+
+def _parts_via_single(tp, recv, recv_splits, send_parts) -> None:
+    """all_to_all_parts for transports without a list all-to-all: one gather copy."""
+    torch = _torch()
+    send = torch.cat(list(send_parts), 0)
+    tp.all_to_all(recv, send, recv_splits, [len(p) for p in send_parts])
 
 
 def exchange_plan(backend, rank_lo, transport) -> None:
@@ -130,6 +146,8 @@ class RangeSharded:
         self.n_recv = int(self.recv_counts.sum())
         self._bufs = {}
         self.sent_bytes = 0  # exchange volume this rank sent (cumulative)
+        self.hops_run = 0  # hops run (cumulative) and host round trips they took
+        self.host_syncs = 0
         dev = getattr(transport, "device", None)
         if hasattr(backend, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
             # engine kernels and the collectives on one stream: pack -> all-to-all -> step in order
@@ -149,24 +167,37 @@ class RangeSharded:
         if key not in self._bufs:
             dev = self.tp.device
             self._bufs = {key: (torch.zeros((max(self.n_send, 1), W + 1), dtype=torch.int64, device=dev),
-                                torch.zeros((max(self.n_recv, 1), W + 1), dtype=torch.int64, device=dev))}
+                                torch.zeros((max(self.n_recv, 1), W + 1), dtype=torch.int64, device=dev),
+                                torch.zeros((self.tp.world, 2), dtype=torch.int64, device=dev),
+                                torch.zeros((self.tp.world, 2), dtype=torch.int64, device=dev))}
         return self._bufs[key]
 
-    def _hop_compact(self, W):
+    def _hop_compact(self, W, first: bool) -> bool:
+        """One hop of the compacted exchange with ONE host round trip: the pack
+        leaves (entries for rank k, this rank's receipts of the hop before) on
+        the device, one all-to-all of those pairs, one copy of both count
+        vectors to the host (the entry splits must be host lists); the
+        entries go out as per-destination views of the pack buffer, and the
+        hop runs without a sync.  -> False when the hop before delivered
+        nothing on any rank (the call is over; this hop is not run)."""
         torch = _torch()
         be, tp = self.be, self.tp
-        out, recv = self._compact_buffers(W)
-        cnt = be.prop_pack_compact(out).astype(np.int64)  # entries per destination
-        sc = torch.tensor(cnt, dtype=torch.int64, device=tp.device)
-        rc = torch.empty_like(sc)
+        out, recv, sc, rc = self._compact_buffers(W)
+        be.prop_pack_compact_dev(out, sc)
         tp.all_to_all(rc, sc, [1] * tp.world, [1] * tp.world)
-        rcnt = rc.cpu().numpy()
+        hc = torch.cat([sc, rc], 0).cpu().numpy()  # the hop's one host sync
+        self.host_syncs += 1
+        cnt, rcnt = hc[: tp.world, 0], hc[tp.world :, 0]
+        if not first and int(hc[tp.world :, 1].sum()) == 0:
+            return False
         sb = np.concatenate([[0], np.cumsum(self.send_counts)[:-1]])
-        send = torch.cat([out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(tp.world)], 0)
+        parts = [out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(tp.world)]
         n = int(rcnt.sum())
-        tp.all_to_all(recv[:n], send, rcnt, cnt)
+        tp.all_to_all_parts(recv[:n], rcnt, parts)
         self.sent_bytes += int(cnt.sum()) * (W + 1) * 8
-        return be.prop_step_compact(recv, n)
+        be.prop_step_compact(recv, n, sync=False)
+        self.hops_run += 1
+        return True
 
     def propagate(self, msgs, cfg: abi.PropConfig):
         """-> (this rank's PropOut as a dict, global totals dict)."""
@@ -177,16 +208,18 @@ class RangeSharded:
             send, recv = self._buffers(W)
         be.prop_begin(msgs, cfg)
         flag = torch.zeros(1, dtype=torch.int64, device=tp.device)
-        for _ in range(cfg.max_hops):
+        for h in range(cfg.max_hops):
             if self.compact:
-                n_new = self._hop_compact(W)
-            else:
-                be.prop_pack(send)
-                tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
-                self.sent_bytes += self.n_send * W * 8
-                n_new = be.prop_step(recv)
-            flag.fill_(n_new)
+                if not self._hop_compact(W, h == 0):
+                    break
+                continue
+            be.prop_pack(send)
+            tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
+            self.sent_bytes += self.n_send * W * 8
+            flag.fill_(be.prop_step(recv))
             tp.all_reduce_sum(flag)
+            self.hops_run += 1
+            self.host_syncs += 2
             if int(flag.item()) == 0:
                 break
         out = be.prop_end()
@@ -326,6 +359,9 @@ class LocalTransport:
         if recv.is_cuda:
             torch.cuda.synchronize(recv.device)
         self._gather(None)  # senders may reuse their buffers only after everyone copied
+
+    def all_to_all_parts(self, recv, recv_splits, send_parts):
+        _parts_via_single(self, recv, recv_splits, send_parts)
 
     def all_reduce_sum(self, t):
         vals = self._gather(t.clone())

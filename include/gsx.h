@@ -160,6 +160,9 @@ int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_pa
 #define GSX_EDGE_DIRECT 0x02u    /* gs.direct[p]                               */
 #define GSX_EDGE_GOSSIPSUB 0x04u /* peer speaks a mesh protocol (feature Mesh) */
 #define GSX_EDGE_FLOODSUB 0x08u  /* peer speaks floodsub                       */
+#define GSX_EDGE_NO_PX 0x10u     /* mesh peer without feature PX (gossipsub v1.0,
+                                    gossipsub_feat.go:28-34): its PRUNEs carry no
+                                    peer exchange (makePrune, gossipsub.go:1815-1818) */
 
 #define GSX_NO_IP 0xFFFFFFFFu
 
@@ -547,6 +550,13 @@ int gsx_prop_end(gsx_engine* e, gsx_prop_out* out);
  * into the engine's own halo and runs the hop. */
 int gsx_prop_pack_compact(gsx_engine* e, uint64_t* out, uint64_t* counts);
 int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_entries, uint64_t* n_new);
+/* As gsx_prop_pack_compact with the counts left on the device, ordered on the
+ * engine's stream (no host sync): d_counts (device, n_ranks x 2 i64) gets
+ * (entries for rank k, this rank's first receipts of hop P.h — the hop just
+ * run).  One all-to-all of these pairs gives every receiver its entry counts
+ * and, summed, whether the previous hop delivered anything on any rank, so a
+ * sharded hop needs one host round trip (RangeSharded). */
+int gsx_prop_pack_compact_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts);
 
 /* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
 
@@ -569,6 +579,8 @@ typedef struct gsx_gossipsub_params {
     int32_t gossip_exchange;                /* 1: run step (D) below; 0: IHAVEs are only emitted */
     int32_t reserved0;
     int64_t fanout_ttl_ns;                  /* :45 (GossipSubFanoutTTL)          */
+    int32_t do_px;                          /* WithPeerExchange (:325-333); default 0 */
+    int32_t prune_peers;                    /* :46 (GossipSubPrunePeers = 16)    */
 } gsx_gossipsub_params;
 
 int gsx_default_gossipsub_params(gsx_gossipsub_params* out);
@@ -646,6 +658,12 @@ typedef struct gsx_heartbeat_out {
     uint64_t gossip_delivered;  /* first receipts of served messages, accepted (D) */
     uint64_t gossip_rejected;   /* first receipts validation did not accept (D)    */
     uint64_t gossip_duplicates; /* further copies of served messages (D)           */
+    uint64_t px_prunes;       /* PRUNEs sent with a non-empty PX list (do_px)      */
+    uint64_t px_peers;        /* peer ids listed in them                           */
+    uint64_t px_ignored;      /* PX lists ignored: receiver's score of the sender
+                                 below AcceptPXThreshold (:833-838)               */
+    uint64_t px_connect;      /* listed peers the receiver is not connected to:
+                                 pxConnect's connection candidates (:861-910)     */
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
@@ -707,6 +725,41 @@ int gsx_leave(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size
  * peer is in the owner's fanout), lastpub per [node][topic] (0 = none); any
  * pointer may be NULL */
 int gsx_export_membership(gsx_engine* e, uint64_t* joined, uint64_t* fanout, int64_t* lastpub);
+
+/* ---- peer exchange on PRUNE (gossipsub.go:811-843, 861-910, 1814-1850) -----
+ * With do_px set (gsx_set_gossipsub_params; off by default, as in the
+ * reference) every PRUNE of a heartbeat round (step (A), sendGraftPrune
+ * :1630-1667, and the (B) answers to rejected GRAFTs, handleGraft :718-809)
+ * carries a PX list unless
+ *   - the pruned peer has GSX_EDGE_NO_PX (makePrune :1815-1818),
+ *   - (A) pruned it for a negative score (noPX, :1361-1368; then all of the
+ *     node's PRUNEs to it that round go without PX),
+ *   - it is a (B) answer and the same GRAFT RPC held a GRAFT of a topic the
+ *     node has not joined, from a direct peer, inside the backoff or from a
+ *     negative-score peer (doPX = false, :721-781).
+ * The list is getPeers(topic, PrunePeers, xp != pruned peer && score(xp) >= 0)
+ * (:1822-1826; mesh-capable connected topic peers, direct ones included),
+ * candidates in ascending peer order shuffled with draws h(seed, 12, node << 32
+ * | pruned peer, tick << 32 | topic << 24 | kind << 23 | k) (kind 0 = (A), 1 =
+ * answer) and truncated.  The receiver, if it accepts the RPC (AcceptFrom)
+ * and has joined the topic, ignores the list when its score of the pruner is
+ * below AcceptPXThreshold, else every listed peer it has no connection to is
+ * a connection candidate (pxConnect): recorded, never dialled (the overlay
+ * is fixed).  Scores: the list of an (A) PRUNE and the (B) receiver's check
+ * read the scores as (A) left them (the snapshot (B) reads); an answer's
+ * list and the (C) receiver's check read the scores as (B) left them (the
+ * snapshot (C) reads) — the reference builds an answer's list right after
+ * handling that one RPC's GRAFTs.  PX runs in gsx_heartbeat and the gsx_hb_*
+ * steps of an unsharded engine (GSX_ESTATE on a range shard with do_px), not
+ * in gsx_join / gsx_leave rounds.
+ * gsx_hb_set_px_log(e, cap) keeps up to cap connection candidates of each
+ * round (0, the default: counters only); gsx_hb_px_records copies those of the
+ * last round as [n][4] u32 (receiver, candidate, pruner, topic | kind << 8),
+ * sorted ascending, *n = the records kept (min(px_connect, log cap); which
+ * ones are kept when the round had more is unspecified); up to cap rows are
+ * written. */
+int gsx_hb_set_px_log(gsx_engine* e, size_t cap);
+int gsx_hb_px_records(gsx_engine* e, uint32_t* out, size_t cap, size_t* n);
 
 /* The tracer's GRAFT / PRUNE calls of the last heartbeat, as topic bit words
  * per pair p = (observer -> peer), E words each (any pointer may be NULL):

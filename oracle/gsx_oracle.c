@@ -123,6 +123,13 @@ struct orc_engine {
     uint64_t* fanout;  /* [pair]: topics whose fanout holds the peer */
     uint64_t* fan_has; /* [node]: topics with a fanout entry */
     int64_t* lastpub;  /* [node][topic] */
+    /* peer exchange (do_px) during orc_heartbeat: per pair bit 0 = (A) pruned it
+     * without PX, bit 1 = its (B) answers go without PX (NULL otherwise); the
+     * round's connection candidates (receiver, candidate, pruner, topic | kind << 8) */
+    uint8_t* pxno;
+    uint32_t* pxlog;
+    size_t n_px, cap_px;
+    uint64_t px_tick, px_seed;
     gsx_gossipsub_params gp; /* for Publish / Join (D, fanout) */ /* the last heartbeat sent an IHAVE list longer than MaxIHaveLength */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
@@ -336,6 +343,7 @@ void orc_destroy(orc_engine* o) {
     free(o->fanout);
     free(o->fan_has);
     free(o->lastpub);
+    free(o->pxlog);
     free(o->prom);
     free(o->ptx_key);
     free(o->ptx_pair);
@@ -1445,6 +1453,8 @@ int orc_default_gossipsub_params(gsx_gossipsub_params* p) { /* DefaultGossipSubP
     p->iwant_followup_ns = 3LL * 1000000000LL;
     p->gossip_exchange = 0;
     p->fanout_ttl_ns = 60LL * 1000000000LL;
+    p->do_px = 0;
+    p->prune_peers = 16; /* GossipSubPrunePeers, :46 */
     return 0;
 }
 
@@ -1541,7 +1551,10 @@ static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* gr, uint64_t* pl
     /* drop all peers with negative score, without PX (:1361-1368) */
     int n = mesh_list(o, v, t, plst);
     for (int i = 0; i < n; i++)
-        if (c->cache[plst[i]] < 0) hb_prune(c, plst[i], t);
+        if (c->cache[plst[i]] < 0) {
+            hb_prune(c, plst[i], t);
+            if (o->pxno) o->pxno[plst[i]] |= 1; /* noPX[p] = true */
+        }
     /* do we have enough peers? (:1370-1385) */
     n = mesh_list(o, v, t, plst);
     if (n < gp->d_lo) {
@@ -1973,6 +1986,79 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
 
 /* (B) every node handles the GRAFTs then PRUNEs sent to it (ctl[t][pair of
  * the sender] 1 / 2), senders ascending; PRUNE answers into resp (:718-843) */
+/* ---- peer exchange on PRUNE (gossipsub.go:811-843, 861-910, 1814-1850; gsx.h) ---- */
+
+static void px_record(orc_engine* o, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (o->n_px == o->cap_px) {
+        o->cap_px = o->cap_px ? 2 * o->cap_px : 256;
+        o->pxlog = (uint32_t*)realloc(o->pxlog, 16 * o->cap_px);
+    }
+    uint32_t* x = o->pxlog + 4 * o->n_px++;
+    x[0] = a;
+    x[1] = b;
+    x[2] = c;
+    x[3] = d;
+}
+
+/* The PX of the round's PRUNEs: kind 0 those of the heartbeats (A) (ctl == 2,
+ * sendGraftPrune :1630-1667), kind 1 the (B) answers (resp, handleGraft
+ * :800-806).  makePrune (:1814-1850) lists getPeers(topic, PrunePeers, xp != p
+ * && score(xp) >= 0) unless the peer lacks feature PX or doPX is off for it;
+ * the receiver, if it accepts the RPC and joined the topic, ignores the list
+ * below AcceptPXThreshold (:833-838), else pxConnect (:861-910) queues the
+ * listed peers it is not connected to (recorded, never dialled).  `cache` is
+ * the score snapshot the receiving step reads, which also feeds the lists. */
+static void hb_px(orc_engine* o, const gsx_gossipsub_params* gp, int kind, const uint8_t* w, const double* cache,
+                  gsx_heartbeat_out* out) {
+    const uint64_t E = o->E;
+    uint64_t max_deg = 1;
+    for (uint32_t i = 0; i < o->n_nodes; i++)
+        if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > max_deg) max_deg = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+    uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
+    for (uint32_t u = 0; u < o->n_nodes; u++)
+        for (int64_t r = o->row_ptr[u]; r < o->row_ptr[u + 1]; r++)
+            for (uint32_t t = 0; t < o->T; t++) {
+                const uint8_t x = w[(size_t)t * E + r];
+                if (kind == 0 ? x != 2 : x == 0) continue;
+                if ((o->eflags[r] & GSX_EDGE_NO_PX) || (o->pxno[r] >> kind & 1)) continue;
+                const uint32_t p = (uint32_t)o->col[r];
+                int n = 0;
+                for (int64_t y = o->row_ptr[u]; y < o->row_ptr[u + 1]; y++) {
+                    if (y == r || !in_topic(o, (uint64_t)y, t) || !(o->eflags[y] & GSX_EDGE_GOSSIPSUB)) continue;
+                    if (!(cache[y] >= 0)) continue;
+                    tmp[n++] = (uint64_t)y;
+                }
+                orc_rng g = {o->px_seed, 12, ((uint64_t)u << 32) | p,
+                             (o->px_tick << 32) | ((uint64_t)t << 24) | ((uint64_t)kind << 23), 0};
+                shuffle_pairs(tmp, n, &g);
+                if (n > gp->prune_peers) n = gp->prune_peers;
+                if (n <= 0) continue;
+                out->px_prunes++;
+                out->px_peers += (uint64_t)n;
+                const int64_t q = reverse_pair(o, (uint64_t)r); /* (p -> u) */
+                if (q < 0) continue;
+                if (!(o->eflags[q] & GSX_EDGE_DIRECT) && cache[q] < o->th.graylist_threshold) continue; /* AcceptFrom */
+                if (!joined(o, p, t)) continue;                                                        /* :816-819 */
+                if (cache[q] < o->th.accept_px_threshold) {
+                    out->px_ignored++;
+                    continue;
+                }
+                for (int i = 0; i < n; i++) {
+                    const uint32_t xp = (uint32_t)o->col[tmp[i]];
+                    bool connected = false; /* _, connected := gs.peers[p] (:869-872) */
+                    for (int64_t z = o->row_ptr[p]; z < o->row_ptr[p + 1]; z++)
+                        if ((uint32_t)o->col[z] == xp) {
+                            connected = o->ps[z].connected;
+                            break;
+                        }
+                    if (connected) continue;
+                    out->px_connect++;
+                    px_record(o, p, xp, u, t | (uint32_t)kind << 8);
+                }
+            }
+    free(tmp);
+}
+
 static void hb_receive(orc_engine* o, const gsx_gossipsub_params* gp, const uint8_t* ctl, uint8_t* resp, double* cache,
                        int64_t now, gsx_heartbeat_out* out) {
     const uint64_t E = o->E;
@@ -1985,18 +2071,24 @@ static void hb_receive(orc_engine* o, const gsx_gossipsub_params* gp, const uint
             const double score = cache[q];
             /* AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped */
             if (!(o->eflags[q] & GSX_EDGE_DIRECT) && score < o->th.graylist_threshold) continue;
+            bool nopx = false; /* doPX = false for this RPC's PRUNE answers (:721-781) */
             for (uint32_t t = 0; t < T; t++) { /* handleGraft, :718-809 */
                 if (ctl[(size_t)t * E + r] != 1) continue;
-                if (!joined(o, u, t)) continue; /* unknown topic: ignored (:727-733) */
+                if (!joined(o, u, t)) { /* unknown topic: ignored (:727-733) */
+                    nopx = true;
+                    continue;
+                }
                 if (hb_in_mesh(o, (uint64_t)q, t)) continue;
                 const uint8_t ef = o->eflags[q];
                 if (ef & GSX_EDGE_DIRECT) {
                     resp[(size_t)t * E + q] = 1;
                     out->graft_rejected++;
+                    nopx = true;
                     continue;
                 }
                 const int64_t expire = *hb_backoff(o, (uint64_t)q, t);
                 if (expire != 0 && now < expire) {
+                    nopx = true;
                     add_penalty(o, (uint64_t)q, 1);
                     out->penalties++;
                     if (now < expire + (gp->graft_flood_threshold_ns - gp->prune_backoff_ns)) {
@@ -2012,6 +2104,7 @@ static void hb_receive(orc_engine* o, const gsx_gossipsub_params* gp, const uint
                     resp[(size_t)t * E + q] = 1;
                     add_backoff(o, (uint64_t)q, t, now, gp->prune_backoff_ns);
                     out->graft_rejected++;
+                    nopx = true;
                     continue;
                 }
                 int n = 0;
@@ -2026,6 +2119,7 @@ static void hb_receive(orc_engine* o, const gsx_gossipsub_params* gp, const uint
                 o->tr_ag[q] |= 1ull << t;
                 out->graft_accepted++;
             }
+            if (nopx && o->pxno) o->pxno[q] |= 2;
             for (uint32_t t = 0; t < T; t++) /* handlePrune */
                 if (ctl[(size_t)t * E + r] == 2 && joined(o, u, t)) /* (:816-819) */
                     handle_prune(o, gp, (uint64_t)q, t, now, out);
@@ -2039,6 +2133,7 @@ static void hb_answers(orc_engine* o, const gsx_gossipsub_params* gp, const uint
     const uint64_t E = o->E;
     const uint32_t T = o->T;
     for (uint64_t q = 0; q < E; q++) cache[q] = score_pair(o, q);
+    if (o->pxno) hb_px(o, gp, 1, resp, cache, out); /* the answers' PX, on the snapshot (C) reads */
     for (uint32_t v = 0; v < o->n_nodes; v++)
         for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
             const int64_t q = reverse_pair(o, (uint64_t)r);
@@ -2084,6 +2179,11 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     }
     double* cache = (double*)malloc(sizeof(double) * (E ? E : 1));
     uint8_t* ctl = (uint8_t*)calloc((size_t)T * (E ? E : 1), 1);
+    o->n_px = 0;
+    free(o->pxno);
+    o->pxno = gp->do_px ? (uint8_t*)calloc(E ? E : 1, 1) : NULL;
+    o->px_tick = tick;
+    o->px_seed = seed;
     memset(o->tr_sg, 0, 8 * (E ? E : 1));
     memset(o->tr_sp, 0, 8 * (E ? E : 1));
     memset(o->tr_ag, 0, 8 * (E ? E : 1));
@@ -2138,9 +2238,12 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
         }
     }
     free(mids);
-    /* (B) receivers, (C) the PRUNE answers */
+    /* (B) receivers, (C) the PRUNE answers; the (A) PRUNEs' PX on the snapshot (B) read */
     hb_receive(o, gp, ctl, resp, cache, now, out);
+    if (o->pxno) hb_px(o, gp, 0, ctl, cache, out);
     hb_answers(o, gp, resp, cache, now, out);
+    free(o->pxno);
+    o->pxno = NULL;
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
     /* (D) the IHAVEs just emitted are answered across the Shift */
@@ -2312,6 +2415,19 @@ int orc_leave(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size
     free(ctl);
     free(resp);
     free(cache);
+    return 0;
+}
+
+static int px_cmp(const void* a, const void* b) {
+    const uint32_t *x = (const uint32_t*)a, *y = (const uint32_t*)b;
+    for (int i = 0; i < 4; i++)
+        if (x[i] != y[i]) return x[i] < y[i] ? -1 : 1;
+    return 0;
+}
+int orc_hb_px_records(orc_engine* o, uint32_t* out, size_t cap, size_t* n) {
+    *n = o->n_px;
+    qsort(o->pxlog, o->n_px, 16, px_cmp);
+    if (cap && out) memcpy(out, o->pxlog, 16 * (cap < o->n_px ? cap : o->n_px));
     return 0;
 }
 

@@ -71,6 +71,8 @@ int orc_leave(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size
               gsx_heartbeat_out* out);
 int orc_hb_trace_words(orc_engine* o, uint64_t* sent_graft, uint64_t* sent_prune, uint64_t* acc_graft,
                        uint64_t* handled_prune);
+/* gsx_hb_px_records of the last orc_heartbeat (every candidate is kept). */
+int orc_hb_px_records(orc_engine* o, uint32_t* out, size_t cap, size_t* n);
 int orc_export_backoff(orc_engine* o, int64_t* out);
 int orc_import_backoff(orc_engine* o, const int64_t* in);
 int orc_gossip_results(orc_engine* o, uint32_t* len, uint64_t* hash);

@@ -71,6 +71,7 @@ _SIG = {
                            P(abi.HeartbeatOut)]),
     "orc_leave": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, P(abi.HeartbeatOut)]),
     "orc_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
+    "orc_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
     "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
 }
@@ -255,6 +256,17 @@ class Oracle:
         w = [np.empty(self.n_pairs, dtype=np.uint64) for _ in range(4)]
         self._chk(self.lib.orc_hb_trace_words(self.h, *[_p(x, C.c_uint64) for x in w]), "orc_hb_trace_words")
         return tuple(w)
+
+    def hb_set_px_log(self, cap: int):
+        """(the oracle keeps every PX candidate)"""
+
+    def hb_px_records(self):
+        """-> [n, 4] u32 (receiver, candidate, pruner, topic | kind << 8), sorted"""
+        n = C.c_size_t()
+        self._chk(self.lib.orc_hb_px_records(self.h, None, 0, C.byref(n)), "orc_hb_px_records")
+        out = np.zeros((n.value, 4), dtype=np.uint32)
+        self._chk(self.lib.orc_hb_px_records(self.h, _p(out, C.c_uint32), n.value, C.byref(n)), "orc_hb_px_records")
+        return out
 
     def mcache_ids(self, node, topic, n_windows):
         n = C.c_size_t()

@@ -208,12 +208,20 @@ class EmuShard:
             out[: len(a)].copy_(_as_tensor(a.view(np.int64)))
         return cnt
 
-    def prop_step_compact(self, entries, n):
+    def prop_pack_compact_dev(self, out, counts):
+        """gsx_prop_pack_compact_dev: (entries for rank k, first receipts of the hop just run)."""
+        cnt = self.prop_pack_compact(out)
+        prev = self.stats["hop"][self.h] if self.h < len(self.stats["hop"]) else 0
+        a = np.stack([cnt.astype(np.int64), np.full(len(cnt), prev, dtype=np.int64)], 1)
+        counts.copy_(_as_tensor(a).reshape(counts.shape))
+
+    def prop_step_compact(self, entries, n, sync=True):
         halo = np.zeros((max(self.n_recv, 1), self.W), dtype=np.uint64)
         e = entries[:n].numpy().view(np.uint64)
         for row in e:
             halo[int(row[0])] = row[1:]
-        return self.prop_step(_as_tensor(halo.view(np.int64)))
+        v = self.prop_step(_as_tensor(halo.view(np.int64)))
+        return v if sync else None
 
     def prop_step(self, recv):
         halo = recv.numpy().view(np.uint64) if len(recv) else None
