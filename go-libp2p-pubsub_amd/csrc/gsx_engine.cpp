@@ -943,6 +943,34 @@ namespace {
 // gsx_load_overlay and gsx_load_overlay_shard: rows for nodes
 // node_lo .. node_lo + n_nodes - 1 of an n_total-node overlay; col holds
 // global ids, node_ips covers all n_total nodes.
+// The heartbeat's per-pair / per-node state, allocated with the overlay (so
+// the first round does not pay for it) or on first use.
+int hb_alloc(gsx_engine* e) {
+    const size_t TE = (size_t)e->T * e->E;
+    int rc = 0;
+    const size_t E = e->E;
+    if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
+        (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
+        (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
+        (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
+        (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
+        (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
+        (rc = dalloc(e, &e->d_mcount, (size_t)e->T * e->n_nodes + 1)) ||
+        (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
+        (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
+        (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
+        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
+        return rc;
+    HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+    if (!e->hubs_host.empty())
+        HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
+                                 e->stream));
+    e->gossip_prev.assign(e->T, 0);
+    e->hb_clean = false;
+    return GSX_OK;
+}
+
 int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_nodes, const int64_t* row_ptr,
                  const int32_t* col, const uint8_t* edge_flags, const uint32_t* node_ips) {
     if (!e || !row_ptr || (!col && row_ptr[n_nodes] > 0)) return GSX_EINVAL;
@@ -1081,6 +1109,7 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
     else HIPCHK(e, hipMemsetAsync(e->d_eflags, 0, e->rs, e->stream));
     rc = upload_ipg(e);
     if (rc) return rc;
+    if ((rc = hb_alloc(e))) return rc;
     e->loaded = true;
     e->invalidate_scores();
     e->state_changed();
@@ -2585,30 +2614,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
     if (e->max_deg > gsx::HB_HUB_MAX)
         return fail(e, GSX_ERANGE, "heartbeat supports at most " + std::to_string(gsx::HB_HUB_MAX) + " peers per node");
-    const size_t TE = (size_t)e->T * e->E;
-    if (!e->d_hbstats) {
-        int rc = 0;
-        const size_t E = e->E;
-        if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
-            (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
-            (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
-            (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
-            (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
-            (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
-            (rc = dalloc(e, &e->d_mcount, (size_t)e->T * e->n_nodes + 1)) ||
-            (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
-            (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
-            (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
-            (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
-            return rc;
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
-        if (!e->hubs_host.empty())
-            HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
-                                     e->stream));
-        e->gossip_prev.assign(e->T, 0);
-        e->hb_clean = false;
-    }
+    if (!e->d_hbstats)
+        if (int rc = hb_alloc(e)) return rc;
     const bool gx_on = e->gp.gossip_exchange != 0;
     if (gx_on && e->sharded()) return fail(e, GSX_ESTATE, "the gossip exchange runs on unsharded engines only");
     if (gx_on && !e->d_prom_e) {

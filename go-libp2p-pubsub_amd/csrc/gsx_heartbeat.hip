@@ -1195,6 +1195,102 @@ __device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool 
 }
 
 
+// Per-lane counters of (B).
+struct RecvCounts {
+    uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
+    int64_t links = 0;
+    __device__ void flush(const HbState& h) const {
+        flush_count(h.stats, HB_ACCEPTED, accepted);
+        flush_count(h.stats, HB_REJECTED, rejected);
+        flush_count(h.stats, HB_PENALTIES, penalties);
+        flush_count(h.stats, HB_PRUNES_HANDLED, handled);
+        flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
+    }
+};
+
+// handleGraft then handlePrune (:718-843) of the control the peer of pair q
+// (u -> v) sent u, AcceptFrom-gated (:582-593).  The caller walks u's senders
+// in ascending order: the Dhi check reads the running mesh count.
+__device__ __forceinline__ void recv_pair(const DevState& s, const HbState& h, uint32_t u, uint64_t q, bool write,
+                                          RecvCounts& c) {
+    uint32_t r;
+    uint64_t grafts, prunes;
+    if (!recv_control(h, q, write, r, grafts, prunes)) return;
+    // doPX = false for this RPC's PRUNE answers (:721-781): a GRAFT of a topic u
+    // has not joined, from a direct peer, inside the backoff or of a negative score
+    bool nopx = h.sub && (grafts & ~h.sub[u]);
+    if (h.sub) {  // GRAFT / PRUNE of a topic u has not joined: ignored (:727-733, :816-819)
+        grafts &= h.sub[u];
+        prunes &= h.sub[u];
+        if (!(grafts | prunes)) return;
+    }
+    // gs.score.Score(p) once per control message (the cache holds the round's
+    // state for every pair read here: k_mask_and + the subset re-score after (A))
+    const double score = s.score[q];
+    const uint8_t ef = h.eflags[q];
+    if (!(ef & EDGE_DIRECT) && score < h.graylist) return;
+    h.dirty[q] = 1;  // its record may change below: re-scored before (C) reads it and at the end
+    const DevGossipParams& gp = h.gp;
+    uint64_t resp = 0;
+    for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
+        const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
+        if (hb_in_mesh(s, q, t)) continue;
+        if (ef & EDGE_DIRECT) {
+            resp |= 1ull << t;
+            ++c.rejected;
+            nopx = true;
+            continue;
+        }
+        const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
+        if (expire != 0 && h.now < expire) {
+            nopx = true;
+            ev_penalty(s, q, 1);
+            ++c.penalties;
+            if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
+                ev_penalty(s, q, 1);
+                ++c.penalties;
+            }
+            add_backoff(h, q, t, gp.prune_backoff_ns);
+            resp |= 1ull << t;
+            ++c.rejected;
+            continue;
+        }
+        if (score < 0) {
+            resp |= 1ull << t;
+            add_backoff(h, q, t, gp.prune_backoff_ns);
+            ++c.rejected;
+            nopx = true;
+            continue;
+        }
+        // the mesh size (A) left, kept current by this receiver's accepts and prunes
+        uint16_t* mc = h.mcount + (size_t)t * h.n_nodes + u;
+        if (*mc >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
+            resp |= 1ull << t;
+            add_backoff(h, q, t, gp.prune_backoff_ns);
+            ++c.rejected;
+            continue;
+        }
+        ev_graft(s, q, t, h.now);
+        if (h.tr_acc) h.tr_acc[q] |= 1ull << t;  // tracer.Graft, :795
+        ++c.accepted;
+        if (scored_topic(s, q, t)) {
+            ++c.links;
+            *mc = (uint16_t)(*mc + 1);
+        }
+    }
+    h.resp[q] = resp;
+    if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
+    if (h.pxno && nopx) h.pxno[q] |= 2;
+    for (; prunes; prunes &= prunes - 1) {  // handlePrune
+        const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
+        if (handle_prune(s, h, q, t)) {
+            --c.links;
+            h.mcount[(size_t)t * h.n_nodes + u] -= 1;
+        }
+        ++c.handled;
+    }
+}
+
 // (B) one lane per receiving node u (up to HB_LANE_DEG peers; hubs run in
 // k_hb_recv_hub), senders in ascending order: handleGraft then handlePrune
 // per sender (:718-843), AcceptFrom-gated (:582-593).  The Dhi check reads
@@ -1202,9 +1298,7 @@ __device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool 
 // running count per topic, taken from the row on first use.
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     const uint32_t lane = threadIdx.x;
-    uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
-    int64_t links = 0;
-    const DevGossipParams& gp = h.gp;
+    RecvCounts c;
     for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
@@ -1219,91 +1313,11 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 if (!ib[j]) continue;
                 h.inbox[q] = 0;
             }
-            uint32_t r;
-            uint64_t grafts, prunes;
-            if (!recv_control(h, q, true, r, grafts, prunes)) continue;
-            // doPX = false for this RPC's PRUNE answers (:721-781): a GRAFT of a topic u
-            // has not joined, from a direct peer, inside the backoff or of a negative score
-            bool nopx = h.sub && (grafts & ~h.sub[u]);
-            if (h.sub) {  // GRAFT / PRUNE of a topic u has not joined: ignored (:727-733, :816-819)
-                grafts &= h.sub[u];
-                prunes &= h.sub[u];
-                if (!(grafts | prunes)) continue;
-            }
-            // gs.score.Score(p) once per control message (the cache holds the round's
-            // state for every pair read here: k_mask_and + the subset re-score after (A))
-            const double score = s.score[q];
-            const uint8_t ef = h.eflags[q];
-            // AcceptFrom (gossipsub.go:582-593): a graylisted non-direct sender's RPC is dropped
-            if (!(ef & EDGE_DIRECT) && score < h.graylist) continue;
-            h.dirty[q] = 1;  // its record may change below: re-scored before (C) reads it and at the end
-            uint64_t resp = 0;
-            for (; grafts; grafts &= grafts - 1) {  // handleGraft, :718-809, topics ascending
-                const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
-                if (hb_in_mesh(s, q, t)) continue;
-                if (ef & EDGE_DIRECT) {
-                    resp |= 1ull << t;
-                    ++rejected;
-                    nopx = true;
-                    continue;
-                }
-                const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
-                if (expire != 0 && h.now < expire) {
-                    nopx = true;
-                    ev_penalty(s, q, 1);
-                    ++penalties;
-                    if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
-                        ev_penalty(s, q, 1);
-                        ++penalties;
-                    }
-                    add_backoff(h, q, t, gp.prune_backoff_ns);
-                    resp |= 1ull << t;
-                    ++rejected;
-                    continue;
-                }
-                if (score < 0) {
-                    resp |= 1ull << t;
-                    add_backoff(h, q, t, gp.prune_backoff_ns);
-                    ++rejected;
-                    nopx = true;
-                    continue;
-                }
-                // the mesh size (A) left, kept current by this lane's accepts and prunes
-                uint16_t* mc = h.mcount + (size_t)t * h.n_nodes + u;
-                const int n = *mc;
-                if (n >= gp.d_hi && !(ef & EDGE_OUTBOUND)) {
-                    resp |= 1ull << t;
-                    add_backoff(h, q, t, gp.prune_backoff_ns);
-                    ++rejected;
-                    continue;
-                }
-                ev_graft(s, q, t, h.now);
-                if (h.tr_acc) h.tr_acc[q] |= 1ull << t;  // tracer.Graft, :795
-                ++accepted;
-                if (scored_topic(s, q, t)) {
-                    ++links;
-                    *mc = (uint16_t)(n + 1);
-                }
-            }
-            h.resp[q] = resp;
-            if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
-            if (h.pxno && nopx) h.pxno[q] |= 2;
-            for (; prunes; prunes &= prunes - 1) {  // handlePrune
-                const uint32_t t = (uint32_t)__builtin_ctzll(prunes);
-                if (handle_prune(s, h, q, t)) {
-                    --links;
-                    h.mcount[(size_t)t * h.n_nodes + u] -= 1;
-                }
-                ++handled;
-            }
+            recv_pair(s, h, u, (uint64_t)q, true, c);
           }
         }
     }
-    flush_count(h.stats, HB_ACCEPTED, accepted);
-    flush_count(h.stats, HB_REJECTED, rejected);
-    flush_count(h.stats, HB_PENALTIES, penalties);
-    flush_count(h.stats, HB_PRUNES_HANDLED, handled);
-    flush_count(h.stats, HB_MESH_LINKS, (uint64_t)links);
+    c.flush(h);
 }
 
 // (B) for hub receivers (more than HB_LANE_DEG peers): one wave per node.
