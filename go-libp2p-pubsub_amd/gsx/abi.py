@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgsx.so")
+LIB_PATH = os.environ.get("GSX_LIB") or os.path.join(HERE, "libgsx.so")  # GSX_LIB: a tuning build
 
 GSX_OK = 0
 GSX_EINVAL = -22
