@@ -75,11 +75,10 @@ class DistTransport:
 
     def all_to_all_parts(self, recv, recv_splits, send_parts):
         """send_parts[k] (contiguous rows) -> rank k; recv gets rank k's rows at
-        the k-th split.  On RCCL the parts go as views (no gather copy)."""
-        if not self.stage and self.dist.get_backend(self.group) == "nccl":
-            outs = list(recv.split([int(x) for x in recv_splits], 0))
-            self.dist.all_to_all(outs, list(send_parts), group=self.group)
-            return
+        the k-th split.  One gather copy on the device, then the same
+        all_to_all_single every backend runs (the list form would skip the
+        copy on RCCL, but this path is the one the tests and the rehearsal
+        exercise; the copy is small next to the exchange itself)."""
         _parts_via_single(self, recv, recv_splits, send_parts)
 
     def all_reduce_sum(self, t):
@@ -149,9 +148,20 @@ class RangeSharded:
         self.hops_run = 0  # hops run (cumulative) and host round trips they took
         self.host_syncs = 0
         dev = getattr(transport, "device", None)
+        self._stream = None
         if hasattr(backend, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
-            # engine kernels and the collectives on one stream: pack -> all-to-all -> step in order
-            backend.set_stream(_torch().cuda.current_stream(dev).cuda_stream)
+            # engine kernels and the collectives on one stream: pack -> all-to-all -> step in order.
+            # A stream of our own, made current around every round: torch's default stream has
+            # handle 0, which the engine reads as "its own (non-blocking) stream", unordered
+            # with the copies and collectives torch issues.
+            torch = _torch()
+            self._stream = torch.cuda.Stream(device=dev)
+            backend.set_stream(self._stream.cuda_stream)
+
+    def _on_stream(self):
+        import contextlib
+
+        return _torch().cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
 
     def _buffers(self, W):
         torch = _torch()
@@ -201,6 +211,10 @@ class RangeSharded:
 
     def propagate(self, msgs, cfg: abi.PropConfig):
         """-> (this rank's PropOut as a dict, global totals dict)."""
+        with self._on_stream():
+            return self._propagate(msgs, cfg)
+
+    def _propagate(self, msgs, cfg: abi.PropConfig):
         torch = _torch()
         be, tp = self.be, self.tp
         W = prop_words(len(msgs))
@@ -232,6 +246,10 @@ class RangeSharded:
         cross-shard pairs go to the receivers' ranks (one all-to-all), the
         PRUNE answers come back (a second, smaller one).  -> (this rank's
         counters, summed counters)."""
+        with self._on_stream():
+            return self._heartbeat(tick, now, seed)
+
+    def _heartbeat(self, tick: int, now: int, seed: int):
         torch = _torch()
         be, tp = self.be, self.tp
         dev = tp.device
