@@ -620,6 +620,125 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
     block_count<5>(cnt, ps.stats, slot);
 }
 
+// k_prop_hop_fast for one-word rows (64-message calls): a group of 4 lanes
+// per node splits the node's compacted SENDERS (lane c takes senders c, c +
+// 4, ...) instead of row words, two rounds of 4 in flight.  The group reads
+// 4 consecutive sender entries at once and runs to the longest of 16 nodes
+// per wave instead of 64; "not from a lower sender" becomes an exclusive
+// prefix-OR over the quad.  Same results as k_prop_hop_fast<1, 1, DROP>.
+template <bool DROP, int G, int R>  // lanes per node, rounds of G senders in flight
+__global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
+                                                        uint64_t* __restrict__ nxt) {
+    constexpr uint32_t NB = 256 / G, NW = 64 / G;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint64_t* __restrict__ occ_src = ps.occ;
+    const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
+    uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    if (h > 1 && prev == 0) return;
+    const bool use_occ = h == 1 || prev < ps.n_nodes / 4;
+    const bool use_mark = mark_hop(ps, h);
+    const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
+    const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
+    const uint32_t gi = threadIdx.x / G, lc = threadIdx.x % G;
+    const uint64_t drp = DROP ? ps.drop[0] : 0ull, rej = DROP ? ps.reject[0] : 0ull;
+    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0;
+    for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
+        const uint32_t u = tile + gi;
+        bool any_new = false;
+        bool touch = u < ps.n_nodes;
+        if (touch && use_mark) touch = occ_bit(touch_h, u);
+        if (touch) {
+            const int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
+            const uint64_t seen = ps.seen[u];
+            uint64_t sa = seen;
+            uint2 pn[R];
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int64_t j = q0 + k * G + lc;
+                pn[k] = j < q1 ? ps.cent[j] : make_uint2(NO_PAIR, 0u);
+            }
+            for (int64_t qb = q0; qb < q1; qb += R * G) {
+                uint32_t pv[R], qv[R];
+                uint64_t c[R];
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    pv[k] = pn[k].x;
+                    qv[k] = pn[k].y;
+                    if (use_occ && pv[k] != NO_PAIR && !occ_bit(occ_front, pv[k] & PIN_NODE_MASK)) pv[k] = NO_PAIR;
+                }
+#pragma unroll
+                for (int k = 0; k < R; ++k) c[k] = pv[k] != NO_PAIR ? front[pv[k] & PIN_NODE_MASK] : 0ull;
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const int64_t j = qb + R * G + k * G + lc;
+                    pn[k] = j < q1 ? ps.cent[j] : make_uint2(NO_PAIR, 0u);
+                }
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    if (check_rows && pv[k] != NO_PAIR && !occ_bit(occ_front, pv[k] & PIN_NODE_MASK)) c[k] = 0;
+                    const uint32_t m = pv[k] == NO_PAIR ? 0u : pv[k] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
+                    if (m == FWD_FORWARD || m == FWD_PUBLISH) {  // one-sided eligibility
+                        const uint32_t v = pv[k] & PIN_NODE_MASK;
+                        const uint64_t own = occ_bit(occ_src, v) ? ps.origin[v] : 0ull;
+                        c[k] &= m == FWD_FORWARD ? ~own : own;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < R; ++k) {  // round k: the quad's senders in order
+                    const uint64_t x = c[k];
+                    n_send += x != 0;
+                    uint64_t incl = x;
+#pragma unroll
+                    for (uint32_t off = 1; off < (uint32_t)G; off <<= 1) {
+                        const uint64_t y = __shfl_up(incl, off, G);
+                        if (lc >= off) incl |= y;
+                    }
+                    uint64_t excl = __shfl_up(incl, 1, G);
+                    if (lc == 0) excl = 0;
+                    const uint64_t nb = x & ~sa & ~excl;  // not seen, not from a lower sender
+                    sa |= __shfl(incl, G - 1, G);
+                    uint32_t fresh, inv = 0;
+                    if (DROP) {
+                        const uint64_t dv = nb & drp;
+                        n_rej += __popcll(dv & rej);
+                        n_ign += __popcll(dv & ~rej);
+                        inv = __popcll(dv & rej);
+                        fresh = __popcll(nb & ~drp);
+                    } else {
+                        fresh = __popcll(nb);
+                    }
+                    n_new += fresh;
+                    if (fresh) {
+                        atomicAdd(&ps.fcnt[qv[k]], fresh);
+                        if (h == ps.max_hops || ps.flast_every) ps.flast[qv[k]] = last_count(ps, qv[k], h, fresh, false);
+                    }
+                    if (DROP && inv && ps.credit) ps.invcnt[qv[k]] += inv;  // P4
+                }
+            }
+            const uint64_t acc = sa ^ seen;
+            const uint64_t fwd_row = DROP ? acc & ~drp : acc;
+            if (lc == 0) {
+                nxt[u] = fwd_row;
+                if (acc) {
+                    ps.seen[u] = sa;
+                    ++n_vnew;
+                }
+            }
+            any_new = fwd_row != 0;
+        }
+        uint64_t wb = __ballot(any_new && lc == 0);
+        uint64_t r = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < NW; ++i) r |= ((wb >> (i * G)) & 1ull) << i;
+        const uint32_t u0 = tile + (threadIdx.x / 64) * NW;
+        if ((threadIdx.x & 63) == 0 && r) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(r << (u0 % 64)));
+    }
+    unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
+    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
+    block_count<5>(cnt, ps.stats, slot);
+}
+
 // The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
 // is never looked up here: a message v would send back to the peer u it
 // first got it from is one u has already seen, so it can only ever count as
@@ -1359,7 +1478,25 @@ template <int CW, int LPN>
 static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
     static const bool no_fast = getenv("GSX_HOP_GENERAL") != nullptr;  // tuning / cross-checks
-    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast) {
+    static const bool no_fast1 = getenv("GSX_HOP_NO_FAST1") != nullptr;  // tuning / cross-checks
+    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast && ps.n_words == 1 && !no_fast1) {
+        static const int gv = [] {  // lanes per node x rounds (tuning): 42 (default), 41, 81, 22, 82
+            const char* v = getenv("GSX_HOP_GR");
+            return v ? atoi(v) : 42;
+        }();
+#define GSX_FAST1(GG, RR)                                                                                     \
+    {                                                                                                         \
+        const dim3 g1(std::min(nblk(ps.n_nodes, 256 / GG), COUNTER_GRID));                                    \
+        if (ps.drop) hipLaunchKernelGGL((k_prop_hop_fast1<true, GG, RR>), g1, b, 0, st, ps, h, front, nxt);   \
+        else hipLaunchKernelGGL((k_prop_hop_fast1<false, GG, RR>), g1, b, 0, st, ps, h, front, nxt);          \
+    }
+        if (gv == 41) GSX_FAST1(4, 1)
+        else if (gv == 81) GSX_FAST1(8, 1)
+        else if (gv == 82) GSX_FAST1(8, 2)
+        else if (gv == 22) GSX_FAST1(2, 2)
+        else GSX_FAST1(4, 2)
+#undef GSX_FAST1
+    } else if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast) {
         if (ps.drop) hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
         else hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
     }
