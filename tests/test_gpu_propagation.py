@@ -18,6 +18,10 @@ CASES = [
     (800, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 64, 10, True, 0.0, 0.03),
     (2000, 8, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 70, 1, False, 0.0, 0.0),
     (3000, 6, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 192, 1, False, 0.0, 0.0),
+    # one-word calls (k_prop_hop_fast1 in the "late" mode: senders split over 4 lanes)
+    (1500, 7, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 50, 10, True, 0.03, 0.02),
+    (1200, 9, 2, abi.GSX_ROUTER_GOSSIPSUB, 1, 64, 1, False, 0.0, 0.03),
+    (900, 14, 1, abi.GSX_ROUTER_FLOODSUB, 0, 33, 10, True, 0.02, 0.0),
     # wide batches: the hop kernel's lane groups (2 lanes per node at 8 words,
     # 4 at 16 and 32 words) and the one-lane multi-chunk walk (12 words)
     (600, 4, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 480, 10, True, 0.0, 0.03),
@@ -100,6 +104,7 @@ VCASES = [
     (600, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 1024, 10, 3.0, 0.2, True),
     (500, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 130, 4, 12.0, 0.3, False),
     (800, 5, 1, abi.GSX_ROUTER_RANDOMSUB, 0, 100, 6, 2.0, 0.2, True),
+    (1500, 8, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 60, 5, 1.0, 0.25, True),  # one word: fast1 with drops
 ]
 
 

@@ -158,10 +158,12 @@ def test_message_parallel_matches_single_engine(gpu_ok, world, invalid):
         assert np.array_equal(e.scores().view(np.uint64), sc1.view(np.uint64))
 
 
-def test_stepped_api_equals_propagate(gpu_ok):
+@pytest.mark.parametrize("m", [130, 40])
+def test_stepped_api_equals_propagate(gpu_ok, m):
     """gsx_prop_begin + steps + end on an unsharded engine == gsx_propagate;
-    deferred credits folded later == credits folded at once."""
-    n, T, m = 2500, 1, 130
+    deferred credits folded later == credits folded at once (m = 40: one-word
+    rows, k_prop_hop_fast1 with flast kept every hop)."""
+    n, T = 2500, 1
     ov = pc.overlay(n, 5, 5, mix_protocols=True)
     msgs = pc.messages(n, m, 5)
     cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, latency_ms=7)
