@@ -2732,7 +2732,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 16, e->stream));
     }
-    if (e->gp.do_px && !state_only) {  // peer exchange on the round's PRUNEs (gsx.h)
+    if (e->gp.do_px) {  // peer exchange on the round's PRUNEs (gsx.h; heartbeats and Join / Leave rounds)
         if (e->sharded()) return fail(e, GSX_ESTATE, "peer exchange (do_px) runs on unsharded engines only");
         const size_t E = std::max<size_t>(e->E, 1);
         if (!e->d_pxno)
@@ -3139,6 +3139,7 @@ int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, s
     if (int rc = hb_recv(e, nullptr)) return rc;
     std::memset(out, 0, sizeof(*out));
     e->hb_active = false;
+    HIPCHK(e, gsx::launch_hb_px(ds, e->hb, 1, e->stream));  // the answers' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_answer(ds, e->hb, e->stream));
     e->hb_clean = !e->hb_tracing;
     HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));
@@ -3146,6 +3147,7 @@ int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, s
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     std::memcpy(out, st, sizeof(st));
+    e->px_last = e->hb.pxno ? st[gsx::HB_PX_CONNECT] : 0;
     return GSX_OK;
 }
 }  // namespace

@@ -750,8 +750,10 @@ int gsx_export_membership(gsx_engine* e, uint64_t* joined, uint64_t* fanout, int
  * list and the (C) receiver's check read the scores as (B) left them (the
  * snapshot (C) reads) — the reference builds an answer's list right after
  * handling that one RPC's GRAFTs.  PX runs in gsx_heartbeat and the gsx_hb_*
- * steps of an unsharded engine (GSX_ESTATE on a range shard with do_px), not
- * in gsx_join / gsx_leave rounds.
+ * steps of an unsharded engine (GSX_ESTATE on a range shard with do_px) and
+ * in gsx_join / gsx_leave rounds: every Leave PRUNE carries PX (sendPrune,
+ * :1089-1093), Join's GRAFT answers as above; their draws use tick 0 and the
+ * call's seed (0 for gsx_leave), the snapshot the round's (B) reads.
  * gsx_hb_set_px_log(e, cap) keeps up to cap connection candidates of each
  * round (0, the default: counters only); gsx_hb_px_records copies those of the
  * last round as [n][4] u32 (receiver, candidate, pruner, topic | kind << 8),

@@ -2374,8 +2374,14 @@ int orc_join(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size_
     }
     free(todo);
     gsx_gossipsub_params gp = o->gp;
+    o->n_px = 0;  /* PX of the GRAFT answers (makePrune in handleGraft, gsx.h) */
+    o->pxno = gp.do_px ? (uint8_t*)calloc(E ? E : 1, 1) : NULL;
+    o->px_tick = 0;
+    o->px_seed = seed;
     hb_receive(o, &gp, ctl, resp, cache, now, out);
     hb_answers(o, &gp, resp, cache, now, out);
+    free(o->pxno);
+    o->pxno = NULL;
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
     free(ctl);
@@ -2409,7 +2415,14 @@ int orc_leave(orc_engine* o, const uint32_t* nodes, const uint32_t* topics, size
         }
     }
     gsx_gossipsub_params gp = o->gp;
+    o->n_px = 0;  /* sendPrune -> makePrune(p, topic, doPX) (:1089-1093): PX on every Leave PRUNE */
+    o->pxno = gp.do_px ? (uint8_t*)calloc(E ? E : 1, 1) : NULL;
+    o->px_tick = 0;
+    o->px_seed = 0;
     hb_receive(o, &gp, ctl, resp, cache, now, out);
+    if (o->pxno) hb_px(o, &gp, 0, ctl, cache, out);
+    free(o->pxno);
+    o->pxno = NULL;
     for (uint64_t r = 0; r < E; r++)
         for (uint32_t t = 0; t < T; t++) out->mesh_links += hb_in_mesh(o, r, t);
     free(ctl);

@@ -101,3 +101,32 @@ def px_run(be, n, d, T, seed, ticks, mesh_degree=14, no_px_frac=0.1, accept_px=0
             be.propagate(pc.messages(n, prop_msgs, seed + 1000 * k), cfg)
         be.refresh(now + 500 * abi.MILLISECOND)
     return ov, outs, recs, snaps
+
+
+def px_member_run(be, n=500, d=8, T=2, seed=13):
+    """PX in Join / Leave rounds (gsx.h): a mesh with partial subscriptions,
+    some nodes leave a topic (every Leave PRUNE carries PX), others join one
+    (their GRAFTs' answers may).  Returns per-call (counters, px records)."""
+    ov = pc.overlay(n, d, seed, mix_protocols=True, direct_frac=0.02)
+    rng = np.random.default_rng(seed + 5)
+    pc.setup(be, ov, T, seed, mesh_degree=4, disconnect_frac=0.02)
+    be.set_app_scores(np.where(rng.random(ov.n_pairs) < 0.08, -500.0, np.abs(rng.normal(1, 2, ov.n_pairs))))
+    joined = np.zeros(n, dtype=np.uint64)
+    for t in range(T):
+        joined |= (rng.random(n) < 0.8).astype(np.uint64) << np.uint64(t)
+    be.set_subscriptions(joined)
+    gp = _px_params(prune_peers=5)
+    gp.d_hi = 6
+    be.set_gossipsub_params(gp)
+    be.hb_set_px_log(1 << 20)
+    res = []
+    now = T0 + 3 * S
+    res.append((be.heartbeat(1, now, seed).as_dict(), be.hb_px_records()))
+    leavers = np.nonzero((joined & np.uint64(1)) != 0)[0][:40].astype(np.uint32)
+    out = be.leave(leavers, np.zeros(len(leavers), dtype=np.uint32), now + S)
+    res.append((out.as_dict(), be.hb_px_records()))
+    joiners = np.nonzero((joined & np.uint64(2)) == 0)[0][:40].astype(np.uint32)
+    out = be.join(joiners, np.ones(len(joiners), dtype=np.uint32) if T > 1 else np.zeros(len(joiners), dtype=np.uint32),
+                  now + 2 * S, seed + 1)
+    res.append((out.as_dict(), be.hb_px_records()))
+    return res

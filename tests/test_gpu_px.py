@@ -51,3 +51,12 @@ def test_px_log_capacity_keeps_count(gpu_ok):
     full = xc.star_case(orc.Oracle(1))[1]
     assert out["px_connect"] == 104 and len(rec) == 10
     assert all(any((r == f).all() for f in full) for r in rec)
+
+
+def test_px_member_rounds_match_oracle(gpu_ok):
+    g = xc.px_member_run(gsx.Engine(2))
+    w = xc.px_member_run(orc.Oracle(2))
+    for (go, gr), (wo, wr) in zip(g, w):
+        assert go == wo
+        assert np.array_equal(gr, wr)
+    assert g[1][0]["px_prunes"] > 0  # the Leave PRUNEs carried lists

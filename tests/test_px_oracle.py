@@ -85,3 +85,11 @@ def test_px_run_invariants():
         if len(rec):
             _, cnt = np.unique(rec[:, [0, 2, 3]], axis=0, return_counts=True)
             assert cnt.max() <= 4
+
+
+def test_px_leave_and_join_rounds():
+    res = xc.px_member_run(orc.Oracle(2))
+    (hb, _), (lv, lrec), (jn, jrec) = res
+    assert lv["prunes"] > 0 and lv["px_prunes"] > 0 and lv["px_connect"] == len(lrec)
+    assert (lrec[:, 3] >> 8 == 0).all() and (lrec[:, 3] & 0xFF == 0).all()  # Leave PRUNEs of topic 0
+    assert jn["px_connect"] == len(jrec)
