@@ -34,6 +34,7 @@ from gsx import shard as shard_mod  # noqa: E402
 
 METRIC = "peer-topic score updates/s + msg deliveries/s @1M peers, 1-8 GPUs, %HBM BW"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0  # measured float4 copy on MI355X (MI355X_MICROARCH.md): the achievable rate
 BYTES_PER_RECORD = 82  # read fmd,mmd,mfp,imd,graftTime,flags; write the same with meshTime
 BYTES_PER_PAIR = 49  # read bp, app, p6, expire, connected; write bp, score
 T0 = 1_700_000_000 * abi.SECOND
@@ -795,6 +796,8 @@ def main():
             # stream and unchanged zero counters are never stored)
             "achieved_traffic": (traffic / (kavg_ms * 1e-3) / 1e9) if traffic else None,
             "frac_traffic": (traffic / (kavg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            # also against the achievable copy rate the microarch guide measures
+            "frac_traffic_of_copy": (traffic / (kavg_ms * 1e-3) / 1e9 / HBM_COPY_GBS) if traffic else None,
         },
         "single_observer": single_obs,
         "cpu_baseline": cpu,
