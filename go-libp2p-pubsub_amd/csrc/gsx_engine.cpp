@@ -669,9 +669,10 @@ hipError_t rescore_all(gsx_engine* e, const gsx::DevState& ds, int64_t now, bool
     ++e->score_writes;
     return gsx::launch_refresh_score(ds, kern_params(e), now, refresh, e->stream);
 }
-hipError_t rescore_subset(gsx_engine* e, const gsx::DevState& ds, const gsx::KernParams& kp, const uint8_t* mask) {
+hipError_t rescore_subset(gsx_engine* e, const gsx::DevState& ds, const gsx::KernParams& kp, const uint8_t* mask,
+                          const uint8_t* mask2 = nullptr) {
     ++e->score_writes;
-    return gsx::launch_score_subset(ds, kp, mask, e->stream);
+    return gsx::launch_score_subset(ds, kp, mask, e->stream, mask2);
 }
 
 int ensure_scores(gsx_engine* e) {
@@ -2854,12 +2855,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // touched that (B) reads (marked in the inbox) are re-scored
     // (a shard's (B) reads every pair with remote control: all touched pairs)
     // (with PX every touched pair: the PX lists read the owner's whole row)
-    uint8_t* sel = h.dirty;
-    if (!e->sharded() && !h.pxno) {
-        sel = e->d_dirty + 3 * e->E;
-        HIPCHK(e, gsx::launch_mask_and(h.dirty, h.inbox, sel, e->E, e->stream));
-    }
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), sel));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.inbox : nullptr));
     e->hb = h;
     e->hb_active = true;
     return GSX_OK;
@@ -2879,12 +2875,7 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     // the pairs touched so far that (C) reads: those marked with an answer
     // (a shard's (C) reads every pair with a remote answer: all touched pairs;
     // with PX every touched pair: the answers' PX lists read the whole row)
-    uint8_t* sel = h.dirty;
-    if (!e->sharded() && !h.pxno) {
-        sel = e->d_dirty + 3 * e->E;
-        HIPCHK(e, gsx::launch_mask_and(h.dirty, h.answer, sel, e->E, e->stream));
-    }
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), sel));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.answer : nullptr));
     return GSX_OK;
 }
 

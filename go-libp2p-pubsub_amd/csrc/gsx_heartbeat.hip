@@ -1225,7 +1225,7 @@ __device__ __forceinline__ void recv_pair(const DevState& s, const HbState& h, u
         if (!(grafts | prunes)) return;
     }
     // gs.score.Score(p) once per control message (the cache holds the round's
-    // state for every pair read here: k_mask_and + the subset re-score after (A))
+    // state for every pair read here: the subset re-score of dirty && inbox after (A))
     const double score = s.score[q];
     const uint8_t ef = h.eflags[q];
     if (!(ef & EDGE_DIRECT) && score < h.graylist) return;
