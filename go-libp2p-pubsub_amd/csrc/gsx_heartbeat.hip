@@ -73,27 +73,33 @@ __device__ __forceinline__ bool backoff_present(const HbState& h, uint64_t r, ui
 // presence byte; only the set bits' entries are read.
 __global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint32_t n_topics) {
     uint64_t cleared = 0;
-    const uint64_t n_bytes = (uint64_t)((n_topics + 7) / 8) * h.n_pairs;
-    for (uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x; x < n_bytes; x += (uint64_t)gridDim.x * 256u) {
-        const uint8_t b = h.bo8[x];
-        if (!b) continue;
-        const uint32_t c = (uint32_t)(x / h.n_pairs);
-        const uint64_t r = x % h.n_pairs;
-        // every bit's entry loaded at once: a clear bit loads the first set bit's
-        // entry again (a valid address, a cache hit), so no load waits alone
-        const uint32_t k0 = (uint32_t)__builtin_ctz(b);
-        int64_t ex[8];
+    const uint32_t n_chunks = (n_topics + 7) / 8;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    // chunk outer, pair inner: no 64-bit division per byte
+    for (uint32_t c = 0; c < n_chunks; ++c) {
+        const uint8_t* __restrict__ bo = h.bo8 + (size_t)c * h.n_pairs;
+        const uint32_t kmax = min(8u, n_topics - 8 * c);
+        for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += stride) {
+            const uint8_t b = bo[r];
+            if (!b) continue;
+            // every bit's entry loaded at once: a clear bit loads the first set bit's
+            // entry again (a valid address, a cache hit), so no load waits alone;
+            // only the chunk's topics (kmax, uniform): one load per lane when T = 1
+            const uint32_t k0 = (uint32_t)__builtin_ctz(b);
+            int64_t ex[8];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) ex[k] = h.backoff[(size_t)(8 * c + ((b >> k & 1) ? k : k0)) * h.n_pairs + r];
-        uint8_t keep = b;
+            for (uint32_t k = 0; k < 8; ++k)
+                if (k < kmax) ex[k] = h.backoff[(size_t)(8 * c + ((b >> k & 1) ? k : k0)) * h.n_pairs + r];
+            uint8_t keep = b;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-            if ((b >> k & 1) && ex[k] + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
-                h.backoff[(size_t)(8 * c + k) * h.n_pairs + r] = 0;
-                keep &= (uint8_t)~(1u << k);
-                ++cleared;
-            }
-        if (keep != b) h.bo8[x] = keep;
+            for (uint32_t k = 0; k < 8; ++k)
+                if (k < kmax && (b >> k & 1) && ex[k] + 2 * HEARTBEAT_INTERVAL_NS < h.now) {
+                    h.backoff[(size_t)(8 * c + k) * h.n_pairs + r] = 0;
+                    keep &= (uint8_t)~(1u << k);
+                    ++cleared;
+                }
+            if (keep != b) h.bo8[(size_t)c * h.n_pairs + r] = keep;
+        }
     }
     flush_count(h.stats, HB_BACKOFF_CLEARED, cleared);
 }
