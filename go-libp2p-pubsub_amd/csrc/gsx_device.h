@@ -124,7 +124,6 @@ constexpr uint8_t FWD_SEND = 0x07;       // any of the above: v sends something 
 // peer, gossipsub.go:583-594, pubsub.go:1014-1017), this call.
 constexpr uint8_t FWD_GIN = 0x08;
 constexpr int RANDOMSUB_D = 6;           // randomsub.go:16-18
-constexpr int RSUB_MAX_DEG = 256;
 constexpr int MAX_HOPS = 64;
 // Propagation counters: duplicates, first receipts per hop, and the
 // push-minimal traffic terms of SURVEY.md §8d (summed over hops and 64-message
@@ -180,6 +179,7 @@ struct PropState {
     uint64_t* touch;           // [2][node / 64] bit per node, buffer h & 1: some sender's row is non-empty (very sparse hops)
     const uint32_t* halo_node; // per receive slot: the local node whose pair it feeds
     uint64_t* sel;             // [pair][word] RandomSub draws (null for other routers)
+    uint32_t* rcand;           // [pair] RandomSub candidate lists, each node's staged over its own pair range
     const uint64_t* hist;      // [hop][node][word]: messages first received at that hop (row 0: published)
     uint32_t n_rows;           // valid history rows (hops run + 1)
     uint32_t win_hops;         // P3 window in hops: floor(window / latency)

@@ -198,6 +198,7 @@ struct gsx_engine {
         uint2* cent = nullptr;                     // compacted senders (k_prop_compact)
         uint8_t* rfwd = nullptr;                   // fwd of each pair's reverse (k_prop_pin)
         uint32_t *cend = nullptr, *chg = nullptr, *nchg = nullptr;
+        uint32_t* rcand = nullptr;  // [pair] RandomSub candidate lists (each node's over its own pair range)
         uint64_t* ndirty = nullptr;
         uint32_t chg_cap = 0;
         uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
@@ -477,7 +478,7 @@ void free_state(gsx_engine* e) {
                   e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
                   e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
-                  e->prop.d_dig};
+                  e->prop.d_dig, e->prop.rcand};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
@@ -1822,6 +1823,7 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.touch = P.touch;
     ps.halo_node = e->d_halo_node;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
+    ps.rcand = P.rcand;
     ps.hist = P.hist;
     ps.n_rows = 1;
     ps.dupcnt = P.dup;
@@ -1897,8 +1899,6 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     }
     if (cfg->validation_delay_ns < 0) return fail(e, GSX_EINVAL, "negative validation delay");
     if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^28 nodes per engine");
-    if (cfg->router == GSX_ROUTER_RANDOMSUB && e->max_deg > (int64_t)gsx::RSUB_MAX_DEG)
-        return fail(e, GSX_ERANGE, "RandomSub draws support at most " + std::to_string(gsx::RSUB_MAX_DEG) + " peers per node");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
     if (cfg->credit_scores && scored && P.credit_pending && P.credit_topic != cfg->topic)
@@ -1953,6 +1953,9 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     const bool rsub = cfg->router == GSX_ROUTER_RANDOMSUB;
     if (rsub && !P.sel) {
         if (int rc = dalloc(e, &P.sel, (size_t)P.words_cap * E)) return rc;
+    }
+    if (rsub && !P.rcand) {
+        if (int rc = dalloc(e, &P.rcand, std::max<size_t>(E, 1))) return rc;
     }
     const bool track = e->prop_track || rsub;
     if (track && P.from_words < (size_t)P.words_cap * E) {

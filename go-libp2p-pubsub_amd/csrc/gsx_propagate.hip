@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
     if (v >= ps.n_nodes || !occ_bit(front_occ, v)) return;
     const int64_t r0 = ps.row_ptr[v], r1 = ps.row_ptr[v + 1];
     const uint32_t W = ps.n_words;
-    uint32_t cand[RSUB_MAX_DEG];
+    uint32_t* const cand = ps.rcand + r0;  // the node's own pair range: no degree limit
     for (uint32_t w = 0; w < W; ++w) {
         uint64_t f = front[(size_t)v * W + w];
         while (f) {
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
             const uint32_t k = w * 64 + b;
             const uint32_t origin = ps.msgs[k].source;
             int n = 0;
-            for (int64_t r = r0; r < r1 && n < RSUB_MAX_DEG; ++r) {
+            for (int64_t r = r0; r < r1; ++r) {
                 if (!(ps.fwd[r] & FWD_RSUB_CAND)) continue;
                 if ((uint32_t)ps.col[r] == origin) continue;
                 if (ps.from_mask[(size_t)r * W + w] & (1ull << b)) continue;  // u == from

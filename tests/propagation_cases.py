@@ -92,3 +92,23 @@ def config(router, topic=0, flood_publish=0, max_hops=40, latency_ms=10, credit=
     return abi.PropConfig(router=router, topic=topic, flood_publish=flood_publish, max_hops=max_hops,
                           hop_latency_ns=latency_ms * abi.MILLISECOND, now_ns=T0 + 3 * S, credit_scores=credit,
                           randomsub_size=size, seed=seed, validation_delay_ns=int(delay_ms * abi.MILLISECOND))
+
+
+def with_hub(ov, hub: int, k: int, seed: int, flags=None):
+    """ov plus undirected links from `hub` to k random other nodes (a node of
+    degree > 256: RandomSub's candidate lists and the heartbeat's hub paths)."""
+    import dataclasses
+
+    rng = np.random.default_rng(seed)
+    obs = ov.pair_observer()
+    edges = {(int(u), int(v)): int(f) for u, v, f in zip(obs, ov.col, ov.edge_flags)}
+    f0 = int(ov.edge_flags[0]) if flags is None else flags
+    for v in rng.choice(np.arange(ov.n)[np.arange(ov.n) != hub], size=k, replace=False):
+        edges.setdefault((hub, int(v)), f0)
+        edges.setdefault((int(v), hub), f0)
+    keys = sorted(edges)
+    row_ptr = np.zeros(ov.n + 1, dtype=np.int64)
+    for u, _ in keys:
+        row_ptr[u + 1] += 1
+    return dataclasses.replace(ov, row_ptr=np.cumsum(row_ptr), col=np.array([v for _, v in keys], dtype=np.int32),
+                               edge_flags=np.array([edges[kk] for kk in keys], dtype=np.uint8))

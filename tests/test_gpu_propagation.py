@@ -211,13 +211,18 @@ def test_propagation_edge_cases_match_oracle(gpu_ok, case):
         assert go["deliveries"] == 0 and go["transmissions"] == 0
 
 
-def test_randomsub_degree_limit_fails_loudly(gpu_ok):
-    """RandomSub draws hold at most 256 candidates per node: a hub above that is refused, not truncated."""
+def test_randomsub_full_hub_matches_oracle(gpu_ok):
+    """A node linked to every other node (399 peers): RandomSub's candidate
+    lists have no degree cap (they are staged over the node's own pairs)."""
     ov = _hub_overlay(400, seed=1)
-    e = gsx.Engine(1)
-    pc.setup(e, ov, 1, seed=5)
-    with pytest.raises(gsx.GsxError):
-        e.propagate(pc.messages(400, 10, seed=3), pc.config(abi.GSX_ROUTER_RANDOMSUB, size=50))
+    ms = pc.messages(400, 10, seed=3)
+    res = []
+    for be in (gsx.Engine(1), orc.Oracle(1)):
+        pc.setup(be, ov, 1, seed=5)
+        out, hop, _ = be.propagate(ms, pc.config(abi.GSX_ROUTER_RANDOMSUB, size=50), want_results=True)
+        res.append((out.as_dict(), hop, be.scores()))
+    assert res[0][0] == res[1][0] and np.array_equal(res[0][1], res[1][1])
+    assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))
 
 
 @pytest.mark.parametrize("mix", [False, True], ids=["gossipsub-only", "with-floodsub-peers"])
@@ -275,3 +280,25 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         for f in abi.STATE_FIELDS:
             assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), (name, f)
         assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
+
+
+@pytest.mark.parametrize("router", [abi.GSX_ROUTER_RANDOMSUB, abi.GSX_ROUTER_GOSSIPSUB])
+def test_hub_above_256_peers_matches_oracle(gpu_ok, router):
+    """A node with ~600 peers: RandomSub stages its candidate lists over the
+    node's own pair range (no degree cap); counters, hops, first deliverers,
+    credits and scores == oracle."""
+    n, seed = 1500, 77
+    ov = pc.with_hub(pc.overlay(n, 5, seed, mix_protocols=True), hub=3, k=600, seed=seed)
+    assert np.diff(ov.row_ptr).max() > 256
+    ms = pc.messages(n, 100, seed)
+    ms["source"][:8] = 3  # the hub publishes too
+    cfg = pc.config(router, latency_ms=5, size=50)
+    res = []
+    for be in (gsx.Engine(1), orc.Oracle(1)):
+        pc.setup(be, ov, 1, seed)
+        out, hop, frm = be.propagate(ms, cfg, want_results=True)
+        res.append((out.as_dict(), hop, frm, be.scores()))
+    (go, gh, gf, gsc), (wo, wh, wf, wsc) = res
+    assert go == wo
+    assert np.array_equal(gh, wh) and np.array_equal(gf, wf)
+    assert np.array_equal(gsc.view(np.uint64), wsc.view(np.uint64))
