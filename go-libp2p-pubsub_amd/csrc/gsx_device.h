@@ -424,7 +424,8 @@ hipError_t launch_join(const DevState& s, const HbState& h, const uint32_t* node
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
                            hipStream_t st);
-hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st);
+hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
+                              hipStream_t st);  // topics t_base .. t_base + n_t - 1
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
                             uint32_t max_ids, int64_t max_deg, hipStream_t st);
 constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)

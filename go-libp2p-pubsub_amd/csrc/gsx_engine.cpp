@@ -2837,10 +2837,17 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         e->gossip_prev[t] = now_g;
     }
     e->have_gossip = !e->gb_host.empty();
-    // (A) the scan of every unit, then per topic, ascending: maintenance, then emitGossip
+    // (A) the scan of every unit, then per topic, ascending: maintenance, then
+    // emitGossip.  A unit changes only its own topic's records, backoff entries
+    // and control bits, so the maintenance of a run of topics is one launch; a
+    // topic's gossip reads the live scores maintenance left (gossipsub.go:1514), so it goes
+    // after its own topic's run and before the next
     HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
-    for (uint32_t t = 0; t < e->T; ++t) {
-        HIPCHK(e, gsx::launch_hb_maintain(ds, h, t, e->max_deg, e->stream));
+    for (uint32_t t = 0, tb = 0; t < e->T; ++t) {
+        const bool g = gb_off[t + 1] > gb_off[t] && max_ids[t] > 0;
+        if (!g && t + 1 < e->T) continue;
+        HIPCHK(e, gsx::launch_hb_maintain(ds, h, tb, t + 1 - tb, e->max_deg, e->stream));
+        tb = t + 1;
         HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
                                         e->max_deg, e->stream));
     }

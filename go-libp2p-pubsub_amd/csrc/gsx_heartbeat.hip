@@ -413,7 +413,7 @@ __device__ __forceinline__ void apply_events(const DevState& s, const HbState& h
         }
         add_backoff(h, r, t, h.gp.prune_backoff_ns);
         atomicOr((unsigned long long*)&h.ctl_prune[r], 1ull << t);
-        if ((f & ST_NOPX) && h.pxno) h.pxno[r] |= 1;  // noPX[p] (topic launches are sequential)
+        if ((f & ST_NOPX) && h.pxno) h.pxno[r] |= 1;  // noPX[p] ((A) sets only this bit: racing topics agree)
     }
     h.dirty[r] = 1;
     if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
@@ -646,7 +646,8 @@ constexpr int MAINT_UNROLL = 4;    // staged pairs per lane in flight
 constexpr uint32_t MAINT_GROUP = 4;  // tiles per maintenance wave (up to 256 listed units, 64 at a time)
 constexpr int HB_STAGE = 1024;       // pairs staged at once (14 KB of LDS per wave)
 
-__global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint32_t t) {
+__global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint32_t t_base) {
+    const uint32_t t = t_base + blockIdx.y;  // a run of topics per launch: the units are independent
     __shared__ double sc[HB_STAGE];  // scores; after maintain(): the events' receiver pairs (u32)
     __shared__ uint8_t fl[HB_STAGE];
     __shared__ uint8_t owner[HB_STAGE];  // the lane whose row holds the item
@@ -798,7 +799,8 @@ __global__ __launch_bounds__(64) void k_hb_maintain(DevState s, HbState h, uint3
 
 // (A) per topic: hub units (more than HB_LANE_DEG peers), one wave each, the
 // row in dynamic LDS (13 B per pair); the wave stages it, lane 0 runs maintain().
-__global__ __launch_bounds__(64) void k_hb_maintain_hub(DevState s, HbState h, uint32_t t) {
+__global__ __launch_bounds__(64) void k_hb_maintain_hub(DevState s, HbState h, uint32_t t_base) {
+    const uint32_t t = t_base + blockIdx.y;
     extern __shared__ double dyn[];
     const uint32_t lane = threadIdx.x;
     const uint32_t nw = h.n_hub[t];
@@ -1517,12 +1519,13 @@ hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, int64_t max_deg, hipStream_t st) {
-    if (h.n_nodes == 0) return hipSuccess;
-    // a wave per group of MAINT_GROUP tiles (the per-tile lists of k_hb_scan)
+hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
+                              hipStream_t st) {
+    if (h.n_nodes == 0 || n_t == 0) return hipSuccess;
+    // a wave per group of MAINT_GROUP tiles (the per-tile lists of k_hb_scan), blockIdx.y the topic
     const uint64_t groups = ((uint64_t)h.n_nodes + 64 * MAINT_GROUP - 1) / (64 * MAINT_GROUP);
-    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384)),
-                       dim3(64), 0, st, s, h, t);
+    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384), n_t),
+                       dim3(64), 0, st, s, h, t_base);
     if (max_deg > HB_LANE_DEG) {
         const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
         static bool attr = false;
@@ -1532,7 +1535,7 @@ hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t, i
             if (e != hipSuccess) return e;
             attr = true;
         }
-        hipLaunchKernelGGL(k_hb_maintain_hub, dim3(1024), dim3(64), lds, st, s, h, t);
+        hipLaunchKernelGGL(k_hb_maintain_hub, dim3(1024, n_t), dim3(64), lds, st, s, h, t_base);
     }
     return hipGetLastError();
 }
