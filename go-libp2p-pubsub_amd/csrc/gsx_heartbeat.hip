@@ -1524,7 +1524,8 @@ hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_ba
     if (h.n_nodes == 0 || n_t == 0) return hipSuccess;
     // a wave per group of MAINT_GROUP tiles (the per-tile lists of k_hb_scan), blockIdx.y the topic
     const uint64_t groups = ((uint64_t)h.n_nodes + 64 * MAINT_GROUP - 1) / (64 * MAINT_GROUP);
-    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, 16384), n_t),
+    // (≈ 8192 waves over the run: one resident round; a wave loops over groups)
+    hipLaunchKernelGGL(k_hb_maintain, dim3((unsigned)std::min<uint64_t>(groups, std::max(8192u / n_t, 256u)), n_t),
                        dim3(64), 0, st, s, h, t_base);
     if (max_deg > HB_LANE_DEG) {
         const size_t lds = (size_t)max_deg * (sizeof(double) + 2 * sizeof(uint16_t) + 1);
