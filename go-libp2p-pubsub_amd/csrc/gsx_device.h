@@ -249,7 +249,7 @@ hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, 
 // gray_only: count the sends on pairs whose receiver graylists the sender
 // (STAT_GRAY) and nothing else (per-hop accounting); else the late accounting.
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, bool gray_only, hipStream_t st);
-hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
+hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* first, uint32_t* dup,
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st);

@@ -2149,10 +2149,8 @@ bool hop_delivered(gsx_engine* e, uint32_t h) {
 
 int prop_fold(gsx_engine* e, const gsx::PropState& ps) {
     auto& P = e->prop;
+    // (k_prop_fold leaves P.first / P.dup / P.inv (= ps.invcnt) empty)
     HIPCHK(e, gsx::launch_prop_fold(ps, dev_state(e), P.first, P.dup, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.first, 0, 4 * e->E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.dup, 0, 4 * e->E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.inv, 0, 4 * e->E, e->stream));
     P.credit_pending = false;
     e->invalidate_scores();
     ++e->score_gen;

@@ -1264,16 +1264,22 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
 }
 
 // Fold of pending counts (gsx_prop_fold_credits; GSX_CREDIT_NOW folds in k_prop_count).
-__global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, const uint32_t* __restrict__ first,
-                                                   const uint32_t* __restrict__ dup) {
+// The counts are left empty: only the nonzero ones are rewritten (no full clears).
+__global__ __launch_bounds__(256) void k_prop_fold(PropState ps, DevState s, uint32_t* __restrict__ first,
+                                                   uint32_t* __restrict__ dup) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= s.n_pairs) return;
-    if (!(s.pflags[q] & PAIR_PRESENT) || ps.topic >= s.n_topics) return;
-    if (!s.tp[ps.topic].scored) return;
     const uint32_t k1 = first[q];
     const uint32_t k2 = dup[q];
     const uint32_t k4 = ps.invcnt ? ps.invcnt[q] : 0;
     if (k1 == 0 && k2 == 0 && k4 == 0) return;
+    if (k1 | k2) {
+        first[q] = 0;
+        dup[q] = 0;
+    }
+    if (k4) ps.invcnt[q] = 0;
+    if (!(s.pflags[q] & PAIR_PRESENT) || ps.topic >= s.n_topics) return;
+    if (!s.tp[ps.topic].scored) return;
     fold_pair(ps, s, q, k1, k2, k4);
 }
 
@@ -1553,7 +1559,7 @@ hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, 
     else hipLaunchKernelGGL(k_prop_count<false>, g, b, 0, st, ps, s);
     return hipGetLastError();
 }
-hipError_t launch_prop_fold(const PropState& ps, const DevState& s, const uint32_t* first, const uint32_t* dup,
+hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* first, uint32_t* dup,
                             hipStream_t st) {
     if (s.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_fold, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps, s, first, dup);
