@@ -523,12 +523,13 @@ def dropin_leg(args):
             subprocess.run(["g++", "-std=c++17", "-O2", src, f"-L{libdir}", "-lgsx", f"-Wl,-rpath,{libdir}", "-o", exe],
                            check=True, timeout=120)
         out = {}
-        for k in (100, 1000):
+        for k in (100, 1000, 10000):
             r = subprocess.run([exe, str(k), "2000"], capture_output=True, text=True, timeout=120, check=True)
             out[f"peers_{k}"] = json.loads(r.stdout.strip().splitlines()[-1])
         out["note"] = ("per call through include/gsx_pubsub.hpp on one GPU engine holding one router's peers; "
-                       "Score() with no change since the last is a host lookup, after a tracer call it re-scores "
-                       "the observer's row on the GPU and copies the vector back")
+                       "Score() with no change since the last is a host lookup (AppSpecificScore is called for the "
+                       "scored peer only, score.go:320), after a tracer call it re-scores the observer's row on the "
+                       "GPU and copies the vector back")
         return out
     except (subprocess.SubprocessError, OSError, ValueError) as ex:
         return {"error": str(ex)[:300]}

@@ -72,7 +72,7 @@ struct DevState {
     uint8_t* pflags;      // per pair: PRESENT | CONNECTED
     int64_t* expire;      // per pair: retention expiry
     double* bp;           // per pair: behaviourPenalty
-    const double* app;    // per pair: AppSpecificScore snapshot
+    double* app;          // per pair: AppSpecificScore snapshot (GSX_EV_APP_SCORE updates one)
     const uint32_t* ipg;  // 2 per pair: (observer, ip) group id | WL bit, or NONE
     uint32_t* ipcount;    // per group: number of present pairs carrying it
     double* score;        // per pair: output
@@ -309,7 +309,20 @@ struct GxBatch {
     uint64_t* x;          // [node][word]: received in this exchange
     const uint32_t* val;  // [message]: GSX_VALIDATION_*
     uint8_t* got;         // set to 1 when some node delivers a message of the set
+    const uint8_t* full;  // [node]: the node has seen every message of the set (nothing to ask)
     uint32_t n_words, serial, topic, avail;  // avail: still cached after this heartbeat's Shift
+    uint32_t row_off;     // word offset of the batch in its topic's gossip rows (GxSub)
+};
+// The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
+// list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
+// row_off * 64 + k = message k of the batch at row_off), valid where the
+// receiver's ihave_tr bit of the topic is set; rows are handed out by an
+// atomic counter below cap (a bound on the round's targets).
+struct GxSub {
+    uint64_t* pool;
+    uint32_t* idx;  // [pair (sender's side)]
+    uint32_t* cnt;  // rows handed out
+    uint32_t tw, cap;
 };
 // gs.p.topics[t] holds the peer of pair r / node v has joined t (null: all)
 __device__ __forceinline__ bool topic_peer(const uint64_t* psub, uint64_t r, uint32_t t) {
@@ -319,8 +332,8 @@ __device__ __forceinline__ bool joined_node(const uint64_t* sub, uint32_t v, uin
     return !sub || ((sub[v] >> t) & 1);
 }
 constexpr uint64_t TAG_HEARTBEAT = 8, TAG_FANOUT = 10, TAG_JOIN = 11, TAG_PX = 12;  // draw tags (gsx.h)
-constexpr int GX_PROMISE_SLOTS = 8;  // outstanding promises per pair (gossip_tracer.go:24-27)
-constexpr uint64_t TAG_IWANT = 9;
+constexpr uint32_t GX_PROMISE_SLOTS0 = 4;  // initial promise slots per pair (gossip_tracer.go:24-27; grown on demand)
+constexpr uint64_t TAG_IWANT = 9, TAG_IHAVE_SUB = 13;
 
 // One cached gossipsub batch (a gsx_propagate call) of an mcache window:
 // node v has message k iff bit k % 64 of seen[v * n_words + k / 64].
@@ -329,9 +342,10 @@ struct GossipBatch {
     const uint64_t* dig;  // [node]: multiset digest of the node's ids in this batch (k_mc_summary)
     const uint32_t* cnt;  // [node]: how many ids the node holds in this batch
     uint32_t n_words;
-    uint32_t slot_base;  // slot of message 0 in HbState::mc_digest
+    uint32_t slot_base;  // slot of message 0 in HbState::mc_digest (64 x the batch's first word of all topics)
     uint32_t wdig_base;  // HbState::mc_digest[wdig_base + w]: digest sum of all of word w's messages
     uint32_t n_msgs;
+    uint32_t row_off;    // word offset of the batch in its topic's gossip rows (slot_base / 64 - the topic's first)
 };
 
 struct HbState {
@@ -364,16 +378,21 @@ struct HbState {
     uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)
     uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
     // the gossip exchange (step (D)); null when it is off
-    uint64_t* ihave_bits;  // [pair (v -> u)]: topics v sent an IHAVE for this round
-    uint32_t* ihave_trunc; // set when an IHAVE list was truncated (not exchanged)
-    const int32_t* col;    // [pair]: the peer (local node id)
+    uint64_t* ihave_bits;  // [pair (u -> v), the receiver's]: topics v sent u an IHAVE for this round
+    uint64_t* ihave_tr;    // [pair (u -> v)]: topics whose IHAVE from v was truncated (a GxSub row)
+    GxSub gsub;            // k_hb_gossip of one topic: its truncated-list rows (pool null: none kept)
+    const GxSub* gsubs;    // [topic]: the exchange's view of every topic's rows
+    uint32_t* gx_err;      // [4]: 0 = a GxSub bound broken (an internal error)
+    const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;
     uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
     uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
     uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none)
-    uint64_t* prom_h;      // [pair][GX_PROMISE_SLOTS]: promised message handle
-    int64_t* prom_e;       // [pair][GX_PROMISE_SLOTS]: its expiry (0 = free slot)
+    uint64_t* prom_h;      // [pair][prom_slots]: promised message handle
+    int64_t* prom_e;       // [pair][prom_slots]: its expiry (0 = free slot)
+    uint32_t prom_slots;   // slots per pair (grown by the host while every pair keeps one free)
+    uint32_t* prom_occ;    // max over pairs of the slots in use after the exchange
     // topic membership (null: every node joined every topic, no fanout)
     const uint64_t* psub;  // [pair]: topics the peer has joined (gs.p.topics)
     const uint64_t* sub;   // [node]: topics the node has joined (gs.mesh)
@@ -422,13 +441,22 @@ hipError_t launch_hb_fanout(const DevState& s, const HbState& h, uint32_t t, hip
 hipError_t launch_join(const DevState& s, const HbState& h, const uint32_t* nodes, const uint32_t* topics,
                        uint32_t n, uint32_t leave, hipStream_t st);
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
+// full[v] = node v has seen every one of the set's n_msgs messages (its `all` row is full)
+hipError_t launch_gx_full(const uint64_t* all, uint32_t n_words, uint32_t n_msgs, uint32_t n_nodes, uint8_t* full,
+                          hipStream_t st);
+// Promise slots [pair][from] -> [pair][to] (to > from; new slots free).
+hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
+                               int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);
+// GetBrokenPromises without the penalty (gsx_promise_broken): counts per pair, frees them.
+hipError_t launch_gx_broken(const HbState& h, uint32_t* counts, hipStream_t st);
 hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
                            hipStream_t st);
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
                               hipStream_t st);  // topics t_base .. t_base + n_t - 1
+// tw: the topic's gossip row words (sum of its batches' n_words)
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
-                            uint32_t max_ids, int64_t max_deg, hipStream_t st);
-constexpr uint32_t HB_GOSSIP_MAX_IDS = 14336;  // LDS list of one node's gossip window (56 KB)
+                            uint32_t tw, int64_t max_deg, hipStream_t st);
+constexpr uint32_t HB_GOSSIP_MAX_WORDS = 4096;  // a topic's gossip rows: 262,144 ids (the long path's LDS rows)
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st);
 // out[i] = a[i] && b[i] (the pairs a heartbeat step re-scores before the next reads them)
 hipError_t launch_mask_and(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n, hipStream_t st);

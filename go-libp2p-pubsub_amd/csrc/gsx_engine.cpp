@@ -133,6 +133,8 @@ struct gsx_engine {
         uint32_t* d_val = nullptr;  // [message] GSX_VALIDATION_*
         uint64_t* d_acc = nullptr;  // [word] accepted messages
         uint64_t* d_dg = nullptr;   // [W * 64] id digests + [W] word digests (k_mc_summary)
+        uint8_t* d_full = nullptr;  // [node]: every message seen (the exchange skips the set there)
+        bool full_ok = false;       // d_full matches d_all
         std::vector<uint64_t> ids;
         int refs = 0;
     };
@@ -149,9 +151,25 @@ struct gsx_engine {
     };
     std::deque<std::vector<McBatch>> mc;
     // gossip exchange state (allocated when first enabled)
-    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gxflag = nullptr;
-    uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;
+    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr;
+    uint32_t* d_gxflag = nullptr;  // [0] a GxSub bound broken, [1] a promise without a slot, [4] slots in use (max)
+    uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
     int64_t* d_prom_e = nullptr;
+    uint32_t prom_slots = 0;  // promise slots per pair (grown while every pair keeps one free before an exchange)
+    // the truncated IHAVE lists of a round (GxSub per topic): rows for at most
+    // tgt_bound targets of tw words each
+    struct SubPool {
+        uint64_t* pool = nullptr;
+        uint32_t* idx = nullptr;
+        size_t rows = 0, tw = 0;  // allocated
+    };
+    std::vector<SubPool> subp;
+    uint32_t* d_sub_cnt = nullptr;  // [T]
+    gsx::GxSub* d_gsubs = nullptr;  // [T]
+    std::vector<gsx::GxSub> gsub_host;
+    uint64_t tgt_bound = 0;  // sum over nodes of the most gossip targets it can pick (d_lazy, gossip_factor below)
+    int32_t tgt_dlazy = -1;
+    double tgt_gf = -1;
     // topic membership (A13), on once subscriptions / Join / Leave are used
     bool members_on = false;
     uint64_t mem_gen = 0;  // bumped whenever subscriptions or a fanout may have changed
@@ -430,6 +448,7 @@ void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
     if (st->d_val) (void)hipFree(st->d_val);
     if (st->d_acc) (void)hipFree(st->d_acc);
     if (st->d_dg) (void)hipFree(st->d_dg);
+    if (st->d_full) (void)hipFree(st->d_full);
     delete st;
 }
 void batch_release(gsx_engine* e, gsx_engine::McBatch& b) {
@@ -519,6 +538,17 @@ void free_state(gsx_engine* e) {
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
         e->d_prom_e = nullptr;
+        e->prom_slots = 0;
+        for (auto& sp : e->subp) {
+            if (sp.pool) (void)hipFree(sp.pool);
+            if (sp.idx) (void)hipFree(sp.idx);
+        }
+        e->subp.clear();
+        if (e->d_sub_cnt) (void)hipFree(e->d_sub_cnt);
+        if (e->d_gsubs) (void)hipFree(e->d_gsubs);
+        e->d_sub_cnt = nullptr;
+        e->d_gsubs = nullptr;
+        e->tgt_dlazy = -1;
         e->d_gx = nullptr;
         e->d_gx_off = nullptr;
         e->d_gx_got = nullptr;
@@ -1358,7 +1388,7 @@ int gsx_apply_events(gsx_engine* e, const gsx_event* ev, size_t n) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     for (size_t i = 0; i < n; ++i) {
         if (ev[i].pair >= e->E) return fail(e, GSX_ERANGE, "event pair out of range");
-        if (ev[i].kind < GSX_EV_ADD_PEER || ev[i].kind > GSX_EV_PENALTY) return fail(e, GSX_EINVAL, "bad event kind");
+        if (ev[i].kind < GSX_EV_ADD_PEER || ev[i].kind > GSX_EV_APP_SCORE) return fail(e, GSX_EINVAL, "bad event kind");
     }
     e->pending.insert(e->pending.end(), ev, ev + n);
     return GSX_OK;
@@ -2601,6 +2631,98 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
 }
 
 namespace {
+// The gossip exchange's per-pair state, allocated when it is first enabled:
+// IHAVE counters, the promises (prom_slots per pair), the receiver-side IHAVE
+// topic bits (and truncated ones), the error / occupancy words.
+int gx_alloc(gsx_engine* e) {
+    if (e->d_prom_e) return GSX_OK;
+    int rc = 0;
+    const size_t E = std::max<size_t>(e->E, 1);
+    const uint32_t S = gsx::GX_PROMISE_SLOTS0;
+    if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
+        (rc = dalloc(e, &e->d_prom_h, E * S)) || (rc = dalloc(e, &e->d_prom_e, E * S)) ||
+        (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) || (rc = dalloc(e, &e->d_gxflag, 8)) ||
+        (rc = dalloc(e, &e->d_sub_cnt, std::max<size_t>(e->T, 1))) ||
+        (rc = dalloc(e, &e->d_gsubs, std::max<size_t>(e->T, 1))))
+        return rc;
+    e->prom_slots = S;
+    HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * S, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
+    e->subp.assign(e->T, gsx_engine::SubPool{});
+    e->gsub_host.assign(e->T, gsx::GxSub{});
+    return GSX_OK;
+}
+
+// Doubles the promise slots of every pair (kept promises stay in order).
+int gx_prom_grow(gsx_engine* e) {
+    const size_t E = std::max<size_t>(e->E, 1);
+    const uint32_t S = e->prom_slots, S2 = 2 * S;
+    uint64_t* nh = nullptr;
+    int64_t* ne = nullptr;
+    if (int rc = dalloc(e, &nh, E * S2)) return rc;
+    if (int rc = dalloc(e, &ne, E * S2)) {
+        (void)hipFree(nh);
+        return rc;
+    }
+    HIPCHK(e, gsx::launch_gx_prom_grow(e->d_prom_h, e->d_prom_e, S, nh, ne, S2, E, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    (void)hipFree(e->d_prom_h);
+    (void)hipFree(e->d_prom_e);
+    e->d_prom_h = nh;
+    e->d_prom_e = ne;
+    e->prom_slots = S2;
+    return GSX_OK;
+}
+
+// The rows of this round's truncated IHAVE lists: a topic whose gossip window
+// can exceed MaxIHaveLength gets rows for every target the round can pick
+// (the sum over nodes of min(degree, max(Dlazy, GossipFactor * degree)): a
+// node picks at most that many from its eligible peers), tw words each.
+int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const std::vector<uint32_t>& tw) {
+    if (e->tgt_dlazy != e->gp.d_lazy || e->tgt_gf != e->gp.gossip_factor) {
+        uint64_t b = 0;
+        for (uint32_t v = 0; v < e->n_nodes; ++v) {
+            const int64_t deg = e->row_ptr[v + 1] - e->row_ptr[v];
+            int64_t tg = e->gp.d_lazy;
+            const int64_t f = (int64_t)(e->gp.gossip_factor * (double)deg);
+            if (f > tg) tg = f;
+            b += (uint64_t)std::min<int64_t>(tg, deg);
+        }
+        e->tgt_bound = b * (e->members_on ? 2 : 1);  // (a fanout pass gossips too)
+        e->tgt_dlazy = e->gp.d_lazy;
+        e->tgt_gf = e->gp.gossip_factor;
+    }
+    const size_t E = std::max<size_t>(e->E, 1);
+    for (uint32_t t = 0; t < e->T; ++t) {
+        gsx::GxSub& g = e->gsub_host[t];
+        g = gsx::GxSub{};
+        if (max_ids[t] <= (uint32_t)std::max(e->gp.max_ihave_length, 0) || e->tgt_bound == 0) continue;
+        gsx_engine::SubPool& sp = e->subp[t];
+        if (sp.rows < e->tgt_bound || sp.tw < tw[t]) {
+            if (sp.pool) (void)hipFree(sp.pool);
+            sp.pool = nullptr;
+            sp.rows = sp.tw = 0;
+            const size_t tw_a = std::max<size_t>(tw[t], sp.tw);
+            if (int rc = dalloc(e, &sp.pool, (size_t)e->tgt_bound * tw_a)) return rc;
+            sp.rows = e->tgt_bound;
+            sp.tw = tw_a;
+        }
+        if (!sp.idx)
+            if (int rc = dalloc(e, &sp.idx, E)) return rc;
+        g.pool = sp.pool;
+        g.idx = sp.idx;
+        g.cnt = e->d_sub_cnt + t;
+        g.tw = tw[t];
+        g.cap = (uint32_t)std::min<size_t>(sp.rows, 0xFFFFFFFFu);
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_sub_cnt, 0, 4 * std::max<size_t>(e->T, 1), e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_gsubs, e->gsub_host.data(), sizeof(gsx::GxSub) * e->T, hipMemcpyHostToDevice,
+                             e->stream));
+    return GSX_OK;
+}
+
 // The heartbeat round in three steps, so that a range shard can exchange the
 // control words of its cross-shard pairs between them (gsx.h):
 //   hb_begin  (A) maintenance + emitGossip of every (node, topic), GRAFT/PRUNE bits per pair;
@@ -2620,17 +2742,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         if (int rc = hb_alloc(e)) return rc;
     const bool gx_on = e->gp.gossip_exchange != 0;
     if (gx_on && e->sharded()) return fail(e, GSX_ESTATE, "the gossip exchange runs on unsharded engines only");
-    if (gx_on && !e->d_prom_e) {
-        int rc = 0;
-        const size_t E = std::max<size_t>(e->E, 1);
-        if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
-            (rc = dalloc(e, &e->d_prom_h, E * gsx::GX_PROMISE_SLOTS)) ||
-            (rc = dalloc(e, &e->d_prom_e, E * gsx::GX_PROMISE_SLOTS)) || (rc = dalloc(e, &e->d_ihave_bits, E)) ||
-            (rc = dalloc(e, &e->d_gxflag, 4)))
-            return rc;
-        HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * gsx::GX_PROMISE_SLOTS, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
-    }
+    if (gx_on)
+        if (int rc = gx_alloc(e)) return rc;
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     uint8_t* pen_mask = nullptr;
     if (e->d_prom_e && !state_only) {
@@ -2646,6 +2759,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         hp.now = now;
         hp.prom_h = e->d_prom_h;
         hp.prom_e = e->d_prom_e;
+        hp.prom_slots = e->prom_slots;
         hp.stats = e->d_hbstats;
         hp.dirty = pen_mask;
         HIPCHK(e, gsx::launch_gx_promises(dev_state(e), hp, e->stream));
@@ -2682,6 +2796,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     h.tcnt = e->d_tcnt;
     h.mcount = e->d_mcount;
     h.publish_threshold = e->th.publish_threshold;
+    h.col = e->d_col;  // (the truncated lists' draw streams are keyed by the peer)
     member_fill(e, h);
     if (e->hb_tracing) {
         if (!e->d_tr_acc) {
@@ -2724,15 +2839,18 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
     if (gx_on) {
         h.ihave_bits = e->d_ihave_bits;
-        h.ihave_trunc = e->d_gxflag;
-        h.col = e->d_col;
+        h.ihave_tr = e->d_ihave_bits + std::max<size_t>(e->E, 1);
+        h.gx_err = e->d_gxflag;
+        h.prom_occ = e->d_gxflag + 4;
         h.peerhave = e->d_peerhave;
         h.iasked = e->d_iasked;
         h.gx_req = e->d_gxreq;
         h.prom_h = e->d_prom_h;
         h.prom_e = e->d_prom_e;
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 16, e->stream));
+        h.prom_slots = e->prom_slots;
+        h.gsubs = e->d_gsubs;
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32, e->stream));
     }
     if (e->gp.do_px) {  // peer exchange on the round's PRUNEs (gsx.h; heartbeats and Join / Leave rounds)
         if (e->sharded()) return fail(e, GSX_ESTATE, "peer exchange (do_px) runs on unsharded engines only");
@@ -2774,10 +2892,13 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         return GSX_OK;
     }
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
-    // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order
+    // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order.
+    // Cache slots are word-aligned: message k of a batch is slot 64 * (the
+    // batch's first word over all topics) + k, and bit (row_off * 64 + k) of
+    // the topic's gossip rows (the truncated lists' layout, GxSub)
     e->gb_host.clear();
     e->mc_digest_host.clear();
-    std::vector<uint32_t> gb_off(e->T + 1, 0), max_ids(e->T, 0);
+    std::vector<uint32_t> gb_off(e->T + 1, 0), max_ids(e->T, 0), tw(e->T, 0);
     std::vector<uint64_t> wdig;  // per batch word: the digest sum of all its messages (a full word's digest)
     const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
     for (uint32_t t = 0; t < e->T; ++t) {
@@ -2787,20 +2908,20 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                 if (b.topic != t) continue;
                 e->gb_host.push_back(gsx::GossipBatch{b.d_seen, b.d_dig, b.d_cnt, b.n_words,
                                                       (uint32_t)e->mc_digest_host.size(), (uint32_t)wdig.size(),
-                                                      b.n_msgs});
-                for (size_t k = 0; k < b.ids.size(); ++k) {
-                    const uint64_t d = id_digest(b.ids[k]);
+                                                      b.n_msgs, tw[t]});
+                for (size_t k = 0; k < (size_t)b.n_words * 64; ++k) {
+                    const uint64_t d = k < b.ids.size() ? id_digest(b.ids[k]) : 0;
                     e->mc_digest_host.push_back(d);
                     if (k % 64 == 0) wdig.push_back(0);
                     wdig.back() += d;
                 }
-                for (size_t k = (b.ids.size() + 63) / 64; k < b.n_words; ++k) wdig.push_back(0);
                 max_ids[t] += b.n_msgs;
+                tw[t] += b.n_words;
             }
-        if (max_ids[t] > gsx::HB_GOSSIP_MAX_IDS)
-            return fail(e, GSX_ERANGE, "gossip window of topic " + std::to_string(t) + " holds " +
-                                           std::to_string(max_ids[t]) + " messages, more than " +
-                                           std::to_string(gsx::HB_GOSSIP_MAX_IDS) + " (shift the cache more often)");
+        if (tw[t] > gsx::HB_GOSSIP_MAX_WORDS)
+            return fail(e, GSX_ERANGE, "gossip window of topic " + std::to_string(t) + " spans " +
+                                           std::to_string(tw[t]) + " words, more than " +
+                                           std::to_string(gsx::HB_GOSSIP_MAX_WORDS) + " (shift the cache more often)");
     }
     gb_off[e->T] = (uint32_t)e->gb_host.size();
     for (auto& g : e->gb_host) g.wdig_base += (uint32_t)e->mc_digest_host.size();  // word digests follow the slots
@@ -2824,6 +2945,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                  hipMemcpyHostToDevice, e->stream));
     }
     h.mc_digest = e->d_mc_digest;
+    // the truncated IHAVE lists' rows (exchange on, a window longer than MaxIHaveLength)
+    if (gx_on)
+        if (int rc = gx_sub_prepare(e, max_ids, tw)) return rc;
     // IHAVE slots: a topic with gossip this round has its slots rewritten by
     // k_hb_gossip; one that had gossip last round but none now is cleared here
     for (uint32_t t = 0; t < e->T; ++t) {
@@ -2846,16 +2970,19 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         if (!g && t + 1 < e->T) continue;
         HIPCHK(e, gsx::launch_hb_maintain(ds, h, tb, t + 1 - tb, e->max_deg, e->stream));
         tb = t + 1;
-        HIPCHK(e, gsx::launch_hb_gossip(ds, h, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
-                                        e->max_deg, e->stream));
+        gsx::HbState ht = h;
+        if (gx_on) ht.gsub = e->gsub_host[t];
+        HIPCHK(e, gsx::launch_hb_gossip(ds, ht, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t],
+                                        max_ids[t] ? tw[t] : 0, e->max_deg, e->stream));
     }
     if (e->members_on) {  // the fanout of topics published to but not joined (:1517-1554)
         for (uint32_t t = 0; t < e->T; ++t) {
             HIPCHK(e, gsx::launch_hb_fanout(ds, h, t, e->stream));
             gsx::HbState hf = h;
             hf.fan_mode = 1;
-            HIPCHK(e, gsx::launch_hb_gossip(ds, hf, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t], max_ids[t],
-                                            e->max_deg, e->stream));
+            if (gx_on) hf.gsub = e->gsub_host[t];
+            HIPCHK(e, gsx::launch_hb_gossip(ds, hf, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t],
+                                            max_ids[t] ? tw[t] : 0, e->max_deg, e->stream));
         }
         ++e->mem_gen;
     }
@@ -2911,9 +3038,13 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         const size_t N = e->n_nodes;
         for (uint32_t t = 0; t < e->T; ++t) {
             off[t] = (uint32_t)gx.size();
+            uint32_t row_off = 0;  // the batch's words in the topic's gossip rows (hb_begin's layout)
             for (size_t w = 0; w < n_win; ++w)
                 for (auto& b : e->mc[w]) {
-                    if (b.topic != t || !b.set) continue;
+                    if (b.topic != t) continue;
+                    const uint32_t ro = row_off;
+                    row_off += b.n_words;
+                    if (!b.set) continue;
                     size_t i = 0;
                     while (i < gx_sets.size() && gx_sets[i] != b.set) ++i;
                     if (i == gx_sets.size()) {
@@ -2921,11 +3052,21 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                         uint64_t* x = seen_acquire(e, words);
                         if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
                         HIPCHK(e, hipMemsetAsync(x, 0, 8 * (size_t)b.set->n_words * N, e->stream));
+                        gsx_engine::MsgSet* ms = b.set;
+                        if (!ms->full_ok) {  // which nodes have seen the whole set (skipped by the walk)
+                            if (!ms->d_full)
+                                if (int rc = dalloc(e, &ms->d_full, N)) return rc;
+                            HIPCHK(e, gsx::launch_gx_full(ms->d_all, ms->n_words, ms->n_msgs, (uint32_t)N, ms->d_full,
+                                                          e->stream));
+                            ms->full_ok = true;
+                        }
+                        ++ms->refs;  // held until the recovered copies are cached (the Shift may drop its batches)
                         gx_sets.push_back(b.set);
                         gx_x.push_back(x);
                     }
-                    gx.push_back(gsx::GxBatch{b.d_seen, b.set->d_all, gx_x[i], b.set->d_val, nullptr, b.n_words,
-                                              b.set->serial, t, (uint32_t)(e->mc.size() < hist || w + 1 < hist)});
+                    gx.push_back(gsx::GxBatch{b.d_seen, b.set->d_all, gx_x[i], b.set->d_val, nullptr, b.set->d_full,
+                                              b.n_words, b.set->serial, t,
+                                              (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
                     gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
                 }
         }
@@ -2948,6 +3089,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         HIPCHK(e, hipMemcpy(e->d_gx_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice));
         h.gx = e->d_gx;
         h.gx_off = e->d_gx_off;
+        h.gsubs = e->d_gsubs;
         HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
         for (size_t i = 0; i < gx_sets.size(); ++i)
             HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
@@ -2957,7 +3099,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     }
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
-    uint32_t gflag[4] = {0, 0, 0, 0};
+    uint32_t gflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> got(gx_sets.size(), 0);
     if (gx_run) {
         HIPCHK(e, hipMemcpyAsync(gflag, e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
@@ -2997,12 +3139,155 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                                          ms->d_dg + (size_t)ms->n_words * 64, b.d_dig, b.d_cnt, e->stream));
         e->mc.front().push_back(std::move(b));
     }
-    if (gflag[0] == 1) return fail(e, GSX_ERANGE, "gossip exchange: an IHAVE list was longer than MaxIHaveLength");
-    if (gflag[0] == 2) return fail(e, GSX_ERANGE, "gossip exchange: more than 8 promises outstanding on a pair");
+    const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] > 0;
+    for (auto* ms : gx_sets) {
+        if (merged) ms->full_ok = false;  // the receipts were merged into their seen rows
+        set_release(e, ms);
+    }
+    if (gflag[0] || gflag[1])
+        return fail(e, GSX_ESTATE, "gossip exchange: internal bound broken (truncated-list rows / promise slots)");
+    // every pair keeps a free promise slot for the next exchange (one promise per pair each)
+    if (gx_run && gflag[4] >= e->prom_slots)
+        if (int rc = gx_prom_grow(e)) return rc;
     return GSX_OK;
 }
 
 }  // namespace
+
+// ---- the gossipTracer's promises (gossip_tracer.go:48-185), one router per observer
+
+namespace {
+uint64_t host_smix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// Go's Int31n over draws h(seed, tag, a, base | k) (the kernels' Rng, gsx_ops.h)
+int32_t host_int31n(uint64_t seed, uint64_t tag, uint64_t a, uint64_t base, int32_t n) {
+    uint32_t k = 0;
+    auto draw = [&]() {
+        const uint64_t x = host_smix(seed + 0x9E3779B97F4A7C15ull *
+                                               (1ull + host_smix(tag ^ host_smix(a ^ host_smix(base | k++)))));
+        return (int32_t)(x >> 33);
+    };
+    if ((n & (n - 1)) == 0) return draw() & (n - 1);
+    const int32_t mx = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
+    int32_t v = draw();
+    while (v > mx) v = draw();
+    return v % n;
+}
+int prom_ready(gsx_engine* e) {
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->sharded()) return fail(e, GSX_ESTATE, "promises live on unsharded engines (the gossip exchange)");
+    return gx_alloc(e);
+}
+}  // namespace
+
+int gsx_promise_add(gsx_engine* e, uint64_t pair, const uint64_t* handles, uint32_t n, int64_t expire_ns,
+                    uint64_t seed) {
+    if (!e || !handles || n == 0 || n > 0x7FFFFFFFu) return GSX_EINVAL;
+    if (int rc = prom_ready(e)) return rc;
+    if (pair >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
+    const uint64_t handle = handles[host_int31n(seed, gsx::TAG_IWANT, pair, 0, (int32_t)n)];  // :53
+    for (;;) {
+        const uint32_t S = e->prom_slots;
+        std::vector<uint64_t> hs(S);
+        std::vector<int64_t> es(S);
+        HIPCHK(e, hipMemcpyAsync(hs.data(), e->d_prom_h + pair * S, 8 * S, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(es.data(), e->d_prom_e + pair * S, 8 * S, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        uint32_t used = 0, fr = S;
+        for (uint32_t k = 0; k < S; ++k) {
+            if (es[k] == 0) {
+                if (fr == S) fr = k;
+                continue;
+            }
+            ++used;
+            if (hs[k] == handle) return GSX_OK;  // promises[mid][p] exists (:66)
+        }
+        if (fr == S || used + 1 >= S) {  // keep a free slot on every pair (the next exchange adds one)
+            if (int rc = gx_prom_grow(e)) return rc;
+            if (fr == S) continue;  // (a free slot keeps its index through the grow)
+        }
+        const uint32_t S2 = e->prom_slots;
+        HIPCHK(e, hipMemcpy(e->d_prom_h + pair * S2 + fr, &handle, 8, hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_prom_e + pair * S2 + fr, &expire_ns, 8, hipMemcpyHostToDevice));
+        return GSX_OK;
+    }
+}
+
+int gsx_promise_broken(gsx_engine* e, int64_t now_ns, uint32_t* counts, uint64_t* total) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = prom_ready(e)) return rc;
+    const size_t E = std::max<size_t>(e->E, 1);
+    uint32_t* d_cnt = nullptr;
+    unsigned long long* d_tot = nullptr;
+    if (int rc = dalloc(e, &d_cnt, E)) return rc;
+    if (int rc = dalloc(e, &d_tot, gsx::HB_STAT_WORDS)) {
+        (void)hipFree(d_cnt);
+        return rc;
+    }
+    gsx::HbState h{};
+    h.n_pairs = e->E;
+    h.now = now_ns;
+    h.prom_h = e->d_prom_h;
+    h.prom_e = e->d_prom_e;
+    h.prom_slots = e->prom_slots;
+    h.stats = d_tot;
+    unsigned long long st[gsx::HB_STAT_WORDS];
+    hipError_t he = hipMemsetAsync(d_tot, 0, sizeof(st), e->stream);
+    if (he == hipSuccess) he = gsx::launch_gx_broken(h, d_cnt, e->stream);
+    if (he == hipSuccess && counts)
+        he = hipMemcpyAsync(counts, d_cnt, 4 * (size_t)e->E, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(st, d_tot, sizeof(st), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_tot);
+    if (he != hipSuccess) return fail(e, GSX_EDEVICE, std::string("gsx_promise_broken: ") + hipGetErrorString(he));
+    if (total) *total = st[gsx::HB_BROKEN_PROMISES];
+    return GSX_OK;
+}
+
+int gsx_promise_fulfill(gsx_engine* e, uint32_t node, uint64_t handle) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = prom_ready(e)) return rc;
+    if (node >= e->n_nodes) return fail(e, GSX_ERANGE, "node out of range");
+    const uint32_t S = e->prom_slots;
+    const size_t p0 = (size_t)e->row_ptr[node] * S, n = (size_t)(e->row_ptr[node + 1] - e->row_ptr[node]) * S;
+    if (n == 0) return GSX_OK;
+    std::vector<uint64_t> hs(n);
+    std::vector<int64_t> es(n);
+    HIPCHK(e, hipMemcpyAsync(hs.data(), e->d_prom_h + p0, 8 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(es.data(), e->d_prom_e + p0, 8 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    bool any = false;
+    for (size_t i = 0; i < n; ++i)
+        if (es[i] != 0 && hs[i] == handle) {  // delete(gt.promises, mid): every peer's promise for it (:119-126)
+            es[i] = 0;
+            any = true;
+        }
+    if (any) HIPCHK(e, hipMemcpy(e->d_prom_e + p0, es.data(), 8 * n, hipMemcpyHostToDevice));
+    return GSX_OK;
+}
+
+int gsx_promise_throttle(gsx_engine* e, uint64_t pair) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = prom_ready(e)) return rc;
+    if (pair >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
+    HIPCHK(e, hipMemsetAsync(e->d_prom_e + pair * e->prom_slots, 0, 8 * (size_t)e->prom_slots, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_promise_count(gsx_engine* e, uint64_t* n) {
+    if (!e || !n) return GSX_EINVAL;
+    *n = 0;
+    if (!e->d_prom_e) return GSX_OK;
+    std::vector<int64_t> es((size_t)e->E * e->prom_slots);
+    HIPCHK(e, hipMemcpy(es.data(), e->d_prom_e, 8 * es.size(), hipMemcpyDeviceToHost));
+    for (int64_t x : es) *n += x != 0;
+    return GSX_OK;
+}
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
     if (!e || !out) return GSX_EINVAL;

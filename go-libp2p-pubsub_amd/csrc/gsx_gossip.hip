@@ -30,18 +30,29 @@ __device__ __forceinline__ void gx_flush(unsigned long long* stats, int k, uint6
     if ((threadIdx.x % 64) == 0 && c) atomicAdd(&stats[k], (unsigned long long)c);
 }
 
-// Streams the ids v advertised on the topics of `tb` that u had not seen:
-// f(batch index, message index) for each, in canonical order; returns false
-// when f asks to stop.
+// Streams the ids v advertised to u (pair q = (u -> v), r its reverse) on
+// the topics of `tb` that u had not seen: f(batch index, message index) for
+// each, in canonical order; returns false when f asks to stop.  A truncated
+// list (ihave_tr) is the subset row the sender kept (GxSub); a batch whose
+// every message u has seen is skipped without reading its rows.
 template <typename F>
-__device__ __forceinline__ bool gx_walk(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, F&& f) {
+__device__ __forceinline__ bool gx_walk(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q, uint32_t r,
+                                        F&& f) {
+    const uint64_t tr = h.ihave_tr[q];
     for (; tb; tb &= tb - 1) {
         const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        const uint64_t* sub = nullptr;
+        if ((tr >> t) & 1) {
+            const GxSub& G = h.gsubs[t];
+            sub = G.pool + (size_t)G.idx[r] * G.tw;
+        }
         for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
             const GxBatch& b = h.gx[g];
+            if (b.full[u]) continue;
             const uint32_t W = b.n_words;
             for (uint32_t w = 0; w < W; ++w) {
                 uint64_t m = b.mem[(size_t)v * W + w] & ~b.all[(size_t)u * W + w];
+                if (sub) m &= sub[b.row_off + w];
                 for (; m; m &= m - 1)
                     if (!f(g, w * 64 + (uint32_t)__builtin_ctzll(m))) return false;
             }
@@ -50,25 +61,22 @@ __device__ __forceinline__ bool gx_walk(const HbState& h, uint64_t tb, uint32_t 
     return true;
 }
 
-__device__ __forceinline__ uint64_t gx_topics(const HbState& h, uint32_t r) { return h.ihave_bits[r]; }
-
 }  // namespace
 
 // applyIwantPenalties at the heartbeat start: a promise whose expiry is
 // before now is broken, AddPenalty(peer, count) (GetBrokenPromises :79-115).
 __global__ __launch_bounds__(256) void k_gx_promises(DevState s, HbState h) {
     uint64_t broken = 0;
+    const uint32_t S = h.prom_slots;
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
-        int64_t e[GX_PROMISE_SLOTS];
-#pragma unroll
-        for (int k = 0; k < GX_PROMISE_SLOTS; ++k) e[k] = h.prom_e[q * GX_PROMISE_SLOTS + k];
         int c = 0;
-#pragma unroll
-        for (int k = 0; k < GX_PROMISE_SLOTS; ++k)
-            if (e[k] != 0 && e[k] < h.now) {
-                h.prom_e[q * GX_PROMISE_SLOTS + k] = 0;
+        for (uint32_t k = 0; k < S; ++k) {
+            const int64_t e = h.prom_e[q * S + k];
+            if (e != 0 && e < h.now) {
+                h.prom_e[q * S + k] = 0;
                 ++c;
             }
+        }
         if (c) {
             ev_penalty(s, q, c);
             broken += (uint64_t)c;
@@ -80,18 +88,60 @@ __global__ __launch_bounds__(256) void k_gx_promises(DevState s, HbState h) {
     block_count<1>(v, h.stats, slot);
 }
 
+// GetBrokenPromises alone (gsx_promise_broken): per-pair counts, freed.
+__global__ __launch_bounds__(256) void k_gx_broken(HbState h, uint32_t* __restrict__ counts) {
+    uint64_t broken = 0;
+    const uint32_t S = h.prom_slots;
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < S; ++k) {
+            const int64_t e = h.prom_e[q * S + k];
+            if (e != 0 && e < h.now) {
+                h.prom_e[q * S + k] = 0;
+                ++c;
+            }
+        }
+        counts[q] = c;
+        broken += c;
+    }
+    unsigned long long v[1] = {broken};
+    const uint32_t slot[1] = {HB_BROKEN_PROMISES};
+    block_count<1>(v, h.stats, slot);
+}
+
+__global__ __launch_bounds__(256) void k_gx_prom_grow(const uint64_t* __restrict__ h_in, const int64_t* __restrict__ e_in,
+                                                      uint32_t from, uint64_t* __restrict__ h_out,
+                                                      int64_t* __restrict__ e_out, uint32_t to, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n * to; i += (uint64_t)gridDim.x * 256u) {
+        const uint64_t q = i / to, k = i % to;
+        h_out[i] = k < from ? h_in[q * from + k] : 0;
+        e_out[i] = k < from ? e_in[q * from + k] : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gx_full(const uint64_t* __restrict__ all, uint32_t W, uint32_t n_msgs,
+                                                 uint32_t n, uint8_t* __restrict__ full) {
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < W; ++w) c += (uint32_t)__popcll(all[(size_t)v * W + w]);
+        full[v] = c == n_msgs;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
-    if (*h.ihave_trunc) return;  // truncated IHAVE lists are not exchanged (the host reports GSX_ERANGE)
     const DevGossipParams& gp = h.gp;
+    const uint32_t S = h.prom_slots;
     uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0, served = 0, delivered = 0, rejected = 0, dups = 0;
+    uint32_t occ = 0;
     for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         // ---- pass 1: handleIHave (:615-679), senders ascending
         for (int64_t q = r0; q < r1; ++q) {
+            const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
+            if (!tall) continue;
             const uint32_t r = h.rev[q];
             if (r == NO_PAIR || (r & HALO)) continue;
-            const uint64_t tb = gx_topics(h, r) & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
-            if (!gx_topics(h, r)) continue;
+            const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
             if (s.score[q] < h.gossip_threshold) {  // :617-621
                 ++ignored;
                 continue;
@@ -109,7 +159,7 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             }
             const uint32_t v = (uint32_t)h.col[q];
             uint32_t n = 0;
-            gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+            gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
                 ++n;
                 return true;
             });
@@ -123,7 +173,7 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             if (kk == n) {
                 const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
                 uint32_t i = 0;
-                gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+                gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
                     if (i++ < j) return true;
                     pick_g = gi;
                     pick_k = k;
@@ -131,7 +181,7 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
                 });
             } else {
                 uint32_t i = 0, sel = 0;
-                gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+                gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
                     if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
                     ++i;
                     return sel < kk;
@@ -140,7 +190,7 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
                 Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
                 i = 0;
                 sel = 0;
-                gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+                gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
                     const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
                     ++i;
                     if (!take) return true;
@@ -154,25 +204,30 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             h.gx_req[q] = kk;
             ++iw_msgs;
             iw_ids += kk;
-            // AddPromise (:59-74): once per (message, peer)
+            // AddPromise (:59-74): once per (message, peer); the host keeps a
+            // free slot on every pair before each exchange (one promise per pair)
             const uint64_t handle = ((uint64_t)h.gx[pick_g].serial << 32) | pick_k;
-            uint64_t* ph_ = h.prom_h + (size_t)q * GX_PROMISE_SLOTS;
-            int64_t* pe_ = h.prom_e + (size_t)q * GX_PROMISE_SLOTS;
+            uint64_t* ph_ = h.prom_h + (size_t)q * S;
+            int64_t* pe_ = h.prom_e + (size_t)q * S;
             int free_slot = -1;
             bool have = false;
-            for (int k = 0; k < GX_PROMISE_SLOTS; ++k) {
+            uint32_t used = 0;
+            for (uint32_t k = 0; k < S; ++k) {
                 if (pe_[k] == 0) {
-                    if (free_slot < 0) free_slot = k;
-                } else if (ph_[k] == handle) {
-                    have = true;
+                    if (free_slot < 0) free_slot = (int)k;
+                } else {
+                    ++used;
+                    if (ph_[k] == handle) have = true;
                 }
             }
             if (!have && free_slot >= 0) {
                 ph_[free_slot] = handle;
                 pe_[free_slot] = h.now + gp.followup_ns;
+                ++used;
             } else if (!have) {
-                *h.ihave_trunc = 2;  // promise table full: reported as an error by the host
+                h.gx_err[1] = 1;  // (the host's invariant broken: never)
             }
+            occ = used > occ ? used : occ;
         }
         // ---- pass 2: v answers (handleIWant :681-716), u receives, senders ascending
         for (int64_t q = r0; q < r1; ++q) {
@@ -183,15 +238,15 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             if (s.score[r] < h.gossip_threshold) continue;  // v ignores u's IWANT
             if (!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) continue;  // AcceptFrom at u
             const uint32_t v = (uint32_t)h.col[q];
-            const uint64_t tb = gx_topics(h, r) & (h.sub ? h.sub[u] : ~0ull);
+            const uint64_t tb = h.ihave_bits[q] & (h.sub ? h.sub[u] : ~0ull);
             uint32_t n = 0;  // |iwant| again (the selection depends on it)
-            gx_walk(h, tb, u, v, [&](uint32_t, uint32_t) {
+            gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
                 ++n;
                 return true;
             });
             Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
             uint32_t i = 0, sel = 0;
-            gx_walk(h, tb, u, v, [&](uint32_t gi, uint32_t k) {
+            gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
                 bool take = true;
                 if (kk < n) {
                     take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
@@ -217,10 +272,9 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
                     // fulfillPromise (:119-126): every promise of u for this message
                     const uint64_t handle = ((uint64_t)b.serial << 32) | k;
                     for (int64_t p = r0; p < r1; ++p)
-                        for (int z = 0; z < GX_PROMISE_SLOTS; ++z)
-                            if (h.prom_e[(size_t)p * GX_PROMISE_SLOTS + z] != 0 &&
-                                h.prom_h[(size_t)p * GX_PROMISE_SLOTS + z] == handle)
-                                h.prom_e[(size_t)p * GX_PROMISE_SLOTS + z] = 0;
+                        for (uint32_t z = 0; z < S; ++z)
+                            if (h.prom_e[(size_t)p * S + z] != 0 && h.prom_h[(size_t)p * S + z] == handle)
+                                h.prom_e[(size_t)p * S + z] = 0;
                     if (val == VAL_ACCEPT) {
                         ++delivered;
                         ev_first(s, (uint64_t)q, t);
@@ -241,6 +295,12 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
     gx_flush(h.stats, HB_GOSSIP_DELIVERED, delivered);
     gx_flush(h.stats, HB_GOSSIP_REJECTED, rejected);
     gx_flush(h.stats, HB_GOSSIP_DUPLICATES, dups);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)occ, off, 64);
+        occ = o > occ ? o : occ;
+    }
+    if ((threadIdx.x % 64) == 0 && occ) atomicMax(h.prom_occ, occ);
 }
 
 // The exchange's receipts into the message set: seen |= x; the receipt rows
@@ -269,6 +329,28 @@ hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t s
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_exchange, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_broken(const HbState& h, uint32_t* counts, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_broken, dim3(gx_blocks(h.n_pairs, 256, COUNTER_GRID)), dim3(256), 0, st, h, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
+                               int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st) {
+    if (n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_prom_grow, dim3(gx_blocks(n_pairs * to, 256, 8192)), dim3(256), 0, st, h_in, e_in, from,
+                       h_out, e_out, to, n_pairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_full(const uint64_t* all, uint32_t n_words, uint32_t n_msgs, uint32_t n_nodes, uint8_t* full,
+                          hipStream_t st) {
+    if (n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_full, dim3(gx_blocks(n_nodes, 256, 8192)), dim3(256), 0, st, all, n_words, n_msgs, n_nodes,
+                       full);
     return hipGetLastError();
 }
 

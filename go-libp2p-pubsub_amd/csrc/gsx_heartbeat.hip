@@ -1017,7 +1017,8 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                             const size_t x = tslot + rs[lane] + peers[q];
                             h.ihave_len[x] = L;
                             h.ihave_hash[x] = dig;
-                            if (h.ihave_bits) h.ihave_bits[rs[lane] + peers[q]] |= 1ull << t;  // (D) reads it
+                            if (h.ihave_bits && h.rev[rs[lane] + peers[q]] != NO_PAIR)  // (D) reads it, receiver-side
+                                h.ihave_bits[h.rev[rs[lane] + peers[q]]] |= 1ull << t;
                         }
                         cnt[0] += (uint64_t)target;
                         cnt[1] += (uint64_t)target * L;
@@ -1033,32 +1034,75 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
 
 // ---- lists longer than MaxIHaveLength: one wave per queued node -------------
 
-// shuffleStrings of a[0..L) in LDS; g is wave-uniform.  64 Int31s are drawn
-// at once (one per lane, Go's rejection rule resolved by a ballot); lane 0
-// applies the swaps in order.
-__device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uint32_t lane) {
+// The r-th (0-based) set bit of w (r < popcount(w)).
+__device__ __forceinline__ uint32_t select64(uint64_t w, uint32_t r) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t sh = 32; sh > 0; sh >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(w & ((1ull << sh) - 1));
+        if (r >= c) {
+            r -= c;
+            w >>= sh;
+            pos += sh;
+        }
+    }
+    return pos;
+}
+
+// Position -> row bit in a node's gossip list: the list is the set bits of
+// row[0 .. tw) in order (GetGossipIDs order), pre[w] the bits before word w.
+__device__ __forceinline__ uint32_t list_bit(const uint64_t* row, const uint32_t* pre, uint32_t tw, uint32_t pos) {
+    uint32_t lo = 0, hi = tw;  // pre[lo] <= pos, and pos < pre[hi] (pre[tw] = L, never read)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (pre[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    return lo * 64 + select64(row[lo], pos - pre[lo]);
+}
+
+// Floyd's sampling of kk of the list's L positions (gsx.h, truncated IHAVE
+// lists): for j = L - kk .. L - 1, x = Int31n(j + 1) (Go's rejection rule),
+// take x unless already taken, then j.  The chosen positions' row bits are
+// set in sel (zeroed first).  64 steps at a time: one draw per lane (a
+// ballot resolves rejections, as in Go a rejected draw is redrawn with the
+// next counter); then in step order each step's outcome is final and is
+// broadcast to the later lanes, whose x it may take.
+__device__ void wave_floyd(uint64_t* sel, const uint64_t* row, const uint32_t* pre, uint32_t tw, uint32_t L,
+                           uint32_t kk, Rng g, uint32_t lane) {
+    for (uint32_t w = lane; w < tw; w += 64) sel[w] = 0;
+    wave_lds_sync();
     uint32_t i = 0;
-    while (i < L) {
+    while (i < kk) {
         const uint32_t step = i + lane;
-        const bool valid = step < L;
-        const uint32_t n = step + 1;
+        const bool valid = step < kk;
+        const uint32_t j = L - kk + step;
+        const uint32_t n = j + 1;
         const int32_t x = (int32_t)(h4(g.seed, g.tag, g.vertex, g.base | (g.k + lane)) >> 33);
         const bool pow2 = (n & (n - 1)) == 0;
         const int32_t maxv = pow2 ? 0 : (int32_t)((1u << 31) - 1 - (1u << 31) % n);
         const bool rej = valid && !pow2 && x > maxv;
         const uint64_t rb = __ballot(rej);
         const uint32_t l0 = rb ? (uint32_t)__builtin_ctzll(rb) : 64u;
-        const uint32_t nvalid = l0 < L - i ? l0 : L - i;
-        if (lane < nvalid) jbuf[lane] = pow2 ? (x & (int32_t)(n - 1)) : (x % (int32_t)n);
-        __syncthreads();
-        if (lane == 0)
-            for (uint32_t k = 0; k < nvalid; ++k) {
-                const uint32_t j = (uint32_t)jbuf[k];
-                const uint32_t tmp = a[i + k];
-                a[i + k] = a[j];
-                a[j] = tmp;
-            }
-        __syncthreads();
+        const uint32_t nvalid = l0 < kk - i ? l0 : kk - i;
+        const bool act = lane < nvalid;
+        uint32_t bx = 0xFFFFFFFFu, bj = 0xFFFFFFFEu;
+        bool hit = false;
+        if (act) {
+            const uint32_t xv = pow2 ? ((uint32_t)x & (n - 1)) : ((uint32_t)x % n);
+            bx = list_bit(row, pre, tw, xv);
+            bj = list_bit(row, pre, tw, j);
+            hit = (sel[bx / 64] >> (bx % 64)) & 1;
+        }
+        for (uint32_t q = 0; q < nvalid; ++q) {
+            const uint32_t y = __shfl(hit ? bj : bx, (int)q, 64);
+            if (lane > q && y == bx) hit = true;
+        }
+        if (act) {
+            const uint32_t y = hit ? bj : bx;
+            atomicOr(reinterpret_cast<unsigned long long*>(&sel[y / 64]), 1ull << (y % 64));
+        }
+        wave_lds_sync();
         if (l0 < 64) {  // step i + l0 redraws after its rejected draw
             i += l0;
             g.k += l0 + 1;
@@ -1070,41 +1114,34 @@ __device__ void wave_shuffle(uint32_t* a, uint32_t L, Rng& g, int32_t* jbuf, uin
 }
 
 // One wave per queued node: lists longer than MaxIHaveLength, and nodes of
-// tiles whose rows did not fit the stage.  Dynamic LDS: the message slots
-// (max_ids u32, GetGossipIDs order) then the eligible peers (max_deg u16).
+// tiles whose rows did not fit the stage.  Dynamic LDS: the node's gossip
+// row (tw u64: its cache bits of the topic's batches at their row_off), the
+// Floyd marks (tw u64), the row's prefix counts (tw u32), then the eligible
+// peers (max_deg u16).  Each target of a truncated list gets the subset of
+// Floyd's sampling over its own draw stream h(seed, 13, node << 32 | peer,
+// tick << 32 | topic << 24 | fan << 23 | k): the marked positions when
+// min(MaxIHaveLength, L - MaxIHaveLength) == MaxIHaveLength, else the
+// unmarked ones; with the exchange on, its row goes to the topic's GxSub.
 __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, uint32_t t,
                                                        const GossipBatch* __restrict__ gb, uint32_t n_gb,
-                                                       uint32_t max_ids) {
-    extern __shared__ uint32_t mids[];  // message slots, GetGossipIDs order
-    uint16_t* peers = reinterpret_cast<uint16_t*>(mids + max_ids);
-    __shared__ int32_t jbuf[64];
+                                                       uint32_t tw) {
+    extern __shared__ uint64_t lds_long[];
+    uint64_t* row = lds_long;
+    uint64_t* sel = row + tw;
+    uint32_t* pre = reinterpret_cast<uint32_t*>(sel + tw);
+    uint16_t* peers = reinterpret_cast<uint16_t*>(pre + tw + (tw & 1));
     __shared__ uint32_t kshare;
     const uint32_t lane = threadIdx.x;
     const uint32_t n_long = *h.n_long;
     const size_t tslot = (size_t)t * h.n_pairs;
+    const uint32_t slot0 = gb[0].slot_base;
+    const uint32_t maxl = (uint32_t)h.gp.max_ihave;
     uint64_t msgs = 0, ids = 0;
     for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
         const uint32_t v = h.long_nodes[li];
-        // GetGossipIDs: windows newest first, batches in Put order, ids ascending
-        uint32_t L = 0;
-        for (uint32_t b = 0; b < n_gb; ++b) {
-            const GossipBatch B = gb[b];
-            for (uint32_t w0 = 0; w0 < B.n_words; w0 += 64) {
-                const uint32_t w = w0 + lane;
-                uint64_t word = w < B.n_words ? B.seen[(size_t)v * B.n_words + w] : 0;
-                const uint32_t c = (uint32_t)__popcll(word);
-                uint32_t pos = L + wave_prefix(c, lane);
-                while (word) {
-                    mids[pos++] = B.slot_base + w * 64 + (uint32_t)__builtin_ctzll(word);
-                    word &= word - 1;
-                }
-                L = __shfl(pos, 63, 64);  // lane 63's end = the new total
-            }
-        }
-        __syncthreads();
-        const uint32_t maxl = (uint32_t)h.gp.max_ihave;
+        uint64_t dall;
+        const uint32_t L = gossip_ids(h, v, gb, n_gb, dall);  // GetGossipIDs: length and digest (k_mc_summary)
         Rng g = hb_rng(h, v, t, h.rngk[(size_t)t * h.n_nodes + v]);
-        if (L > maxl) wave_shuffle(mids, L, g, jbuf, lane);  // shuffleStrings, then truncation (:1708-1716)
         const int64_t r0 = h.row_ptr[v];
         const int deg = (int)(h.row_ptr[v + 1] - r0);
         int np = 0;
@@ -1115,7 +1152,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
             if (ok) peers[np + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)i;
             np += __popcll(bal);
         }
-        __syncthreads();
+        wave_lds_sync();
         int target = h.gp.d_lazy;
         const int factor = (int)(h.gp.gossip_factor * (double)np);
         if (factor > target) target = factor;
@@ -1126,48 +1163,79 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 g.shuffle(peers, np);
                 kshare = g.k;
             }
-            __syncthreads();
+            wave_lds_sync();
             g.k = kshare;
         }
         if (L <= maxl) {  // the whole list to every target
-            uint64_t d = 0;
-            for (uint32_t e = lane; e < L; e += 64) d += h.mc_digest[mids[e]];
-            d = wave_sum64(d);
             for (int p = lane; p < target; p += 64) {
-                const size_t x = tslot + r0 + peers[p];
-                h.ihave_len[x] = L;
-                h.ihave_hash[x] = d;
-                if (h.ihave_bits) h.ihave_bits[r0 + peers[p]] |= 1ull << t;
+                const int64_t r = r0 + peers[p];
+                h.ihave_len[tslot + r] = L;
+                h.ihave_hash[tslot + r] = dall;
+                if (h.ihave_bits && h.rev[r] != NO_PAIR) h.ihave_bits[h.rev[r]] |= 1ull << t;  // (D) reads it
             }
-            if (lane == 0) {
-                msgs += (uint64_t)target;
-                ids += (uint64_t)target * L;
+            msgs += (uint64_t)target;
+            ids += (uint64_t)target * L;
+        } else if (target > 0) {
+            // the node's gossip row and its prefix counts
+            for (uint32_t b = 0; b < n_gb; ++b) {
+                const GossipBatch B = gb[b];
+                for (uint32_t w = lane; w < B.n_words; w += 64) row[B.row_off + w] = B.seen[(size_t)v * B.n_words + w];
             }
-        } else {
+            wave_lds_sync();
+            uint32_t carry = 0;
+            for (uint32_t w0 = 0; w0 < tw; w0 += 64) {
+                const uint32_t w = w0 + lane;
+                const uint32_t c = w < tw ? (uint32_t)__popcll(row[w]) : 0u;
+                const uint32_t p = wave_prefix(c, lane);
+                if (w < tw) pre[w] = carry + p;
+                carry += __shfl(p + c, 63, 64);
+            }
+            wave_lds_sync();
+            const uint32_t kk = maxl < L - maxl ? maxl : L - maxl;
+            const bool take = kk == maxl;  // the marked positions are the list, else the unmarked ones
             for (int p = 0; p < target; ++p) {
-                wave_shuffle(mids, L, g, jbuf, lane);
+                const int64_t r = r0 + peers[p];
+                const Rng gs{h.seed, TAG_IHAVE_SUB, ((uint64_t)(h.node_lo + v) << 32) | (uint32_t)h.col[r],
+                             (h.tick << 32) | ((uint64_t)t << 24) | (h.fan_mode ? (1ull << 23) : 0ull), 0};
+                wave_floyd(sel, row, pre, tw, L, kk, gs, lane);
                 uint64_t d = 0;
-                for (uint32_t e = lane; e < maxl; e += 64) d += h.mc_digest[mids[e]];
+                for (uint32_t w = lane; w < tw; w += 64)
+                    for (uint64_t m = sel[w]; m; m &= m - 1) d += h.mc_digest[slot0 + w * 64 + (uint32_t)__builtin_ctzll(m)];
                 d = wave_sum64(d);
+                const uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
                 if (lane == 0) {
-                    const size_t x = tslot + r0 + peers[p];
-                    h.ihave_len[x] = maxl;
-                    h.ihave_hash[x] = d;
-                    if (h.ihave_bits) {
-                        h.ihave_bits[r0 + peers[p]] |= 1ull << t;
-                        *h.ihave_trunc = 1;  // a truncated list: not exchanged
+                    h.ihave_len[tslot + r] = maxl;
+                    h.ihave_hash[tslot + r] = take ? d : dall - d;
+                    if (q != NO_PAIR) h.ihave_bits[q] |= 1ull << t;
+                }
+                if (q != NO_PAIR && h.gsub.pool) {  // the subset the receiver's handleIHave reads (D)
+                    uint32_t x = 0;
+                    if (lane == 0) {
+                        x = atomicAdd(h.gsub.cnt, 1u);
+                        if (x < h.gsub.cap) {
+                            h.gsub.idx[r] = x;
+                            h.ihave_tr[q] |= 1ull << t;
+                        } else {
+                            h.gx_err[0] = 1;  // (the host bounds the targets: never)
+                        }
+                    }
+                    x = __shfl(x, 0, 64);
+                    if (x < h.gsub.cap) {
+                        uint64_t* dst = h.gsub.pool + (size_t)x * h.gsub.tw;
+                        for (uint32_t w = lane; w < tw; w += 64) dst[w] = take ? sel[w] : (row[w] & ~sel[w]);
                     }
                 }
+                wave_lds_sync();  // sel is redrawn for the next target
             }
-            if (lane == 0) {
-                msgs += (uint64_t)target;
-                ids += (uint64_t)target * maxl;
-            }
+            msgs += (uint64_t)target;
+            ids += (uint64_t)target * maxl;
         }
-        __syncthreads();
+        wave_lds_sync();
     }
-    flush_count(h.stats, HB_IHAVE_MSGS, msgs);
-    flush_count(h.stats, HB_IHAVE_IDS, ids);
+    if (lane == 0) {
+        if (msgs) atomicAdd(&h.stats[HB_IHAVE_MSGS], (unsigned long long)msgs);
+        if (ids) atomicAdd(&h.stats[HB_IHAVE_IDS], (unsigned long long)ids);
+    }
 }
 
 // ---- (B) receivers -------------------------------------------------------------
@@ -1542,20 +1610,20 @@ hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_ba
 }
 
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
-                            uint32_t max_ids, int64_t max_deg, hipStream_t st) {
-    if (h.n_nodes == 0 || n_gb == 0 || max_ids == 0) return hipSuccess;
+                            uint32_t tw, int64_t max_deg, hipStream_t st) {
+    if (h.n_nodes == 0 || n_gb == 0 || tw == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hb_gossip, dim3(grid_cap(h.n_nodes, 256)), dim3(256), 0, st, s, h, t, gb, n_gb);
     // queued nodes (long lists, tiles with hub rows): the kernel returns at once without any
-    const size_t lds = sizeof(uint32_t) * max_ids + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
+    const size_t lds = (size_t)tw * 20 + 4 + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
     static size_t attr = 0;
     if (lds > 65536 && lds > attr) {
         e = hipFuncSetAttribute((const void*)k_hb_gossip_long, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = lds;
     }
-    hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), lds, st, s, h, t, gb, n_gb, max_ids);
+    hipLaunchKernelGGL(k_hb_gossip_long, dim3(grid_cap(h.n_nodes, 1)), dim3(64), lds, st, s, h, t, gb, n_gb, tw);
     return hipGetLastError();
 }
 

@@ -155,6 +155,7 @@ __global__ __launch_bounds__(64) void k_apply_events(DevState s, DevPeerParams p
         case 6: ev_mesh(s, e.pair, e.topic); break;
         case 7: ev_invalid(s, e.pair, e.topic); break;
         case 8: ev_penalty(s, e.pair, e.arg); break;
+        case 9: s.app[e.pair] = __longlong_as_double((long long)e.arg); break;  // AppSpecificScore(p), :320
         default: break;
         }
     }

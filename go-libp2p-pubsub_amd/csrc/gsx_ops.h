@@ -273,12 +273,12 @@ __device__ __forceinline__ void block_count(unsigned long long (&v)[NV], unsigne
 }
 
 // ---- canonical RNG ---------------------------------------------
-__device__ __forceinline__ uint64_t smix(uint64_t z) {  // SplitMix64 finaliser
+__host__ __device__ __forceinline__ uint64_t smix(uint64_t z) {  // SplitMix64 finaliser
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
+__host__ __device__ __forceinline__ uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, uint64_t b) {
     return smix(seed + 0x9E3779B97F4A7C15ull * (1ull + smix(tag ^ smix(a ^ smix(b)))));
 }
 // math/rand's Int31n over Int31 draws h(seed, tag, vertex, base | k), standing
@@ -286,8 +286,8 @@ __device__ __forceinline__ uint64_t h4(uint64_t seed, uint64_t tag, uint64_t a, 
 struct Rng {
     uint64_t seed, tag, vertex, base;
     uint32_t k;
-    __device__ int32_t int31() { return (int32_t)(h4(seed, tag, vertex, base | k++) >> 33); }
-    __device__ int32_t int31n(int32_t n) {
+    __host__ __device__ int32_t int31() { return (int32_t)(h4(seed, tag, vertex, base | k++) >> 33); }
+    __host__ __device__ int32_t int31n(int32_t n) {
         if ((n & (n - 1)) == 0) return int31() & (n - 1);
         const int32_t max = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
         int32_t v = int31();

@@ -43,6 +43,7 @@ EV_FIRST_DELIVERY = 5
 EV_MESH_DELIVERY = 6
 EV_INVALID_DELIVERY = 7
 EV_PENALTY = 8
+EV_APP_SCORE = 9  # arg = the float64 bits of the pair's new AppSpecificScore (score.go:320)
 
 # gsx_reject_reason, with the reference's strings (tracer.go:28-38)
 REJECT_REASONS = {
@@ -432,6 +433,11 @@ SIGNATURES = {
     "gsx_leave": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, P(HeartbeatOut)]),
     "gsx_export_membership": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_int64)]),
     "gsx_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
+    "gsx_promise_add": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint64), C.c_uint32, C.c_int64, C.c_uint64]),
+    "gsx_promise_broken": (C.c_int, [C.c_void_p, C.c_int64, P(C.c_uint32), P(C.c_uint64)]),
+    "gsx_promise_fulfill": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64]),
+    "gsx_promise_throttle": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "gsx_promise_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "gsx_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
     "gsx_timing_begin": (C.c_int, [C.c_void_p, C.c_uint32]),

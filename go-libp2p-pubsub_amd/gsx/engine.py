@@ -438,6 +438,30 @@ class Engine:
                                           C.byref(n)), "gsx_mcache_ids")
         return out
 
+    # -- the gossipTracer's promises (gossip_tracer.go:48-185) ------------------------------
+    def promise_add(self, pair: int, handles, expire: int, seed: int = 0):
+        """AddPromise(p, msgIDs): one of `handles` (Int31n, draws h(seed, 9, pair, k)) expiring at `expire`."""
+        h = np.ascontiguousarray(handles, dtype=np.uint64)
+        self._chk(self.lib.gsx_promise_add(self.h, pair, _ptr(h, C.c_uint64), len(h), expire, seed), "gsx_promise_add")
+
+    def promise_broken(self, now: int):
+        """GetBrokenPromises: -> (per-pair counts [n_pairs] u32, total); the broken ones are dropped."""
+        cnt = np.zeros(self.n_pairs, dtype=np.uint32)
+        tot = C.c_uint64()
+        self._chk(self.lib.gsx_promise_broken(self.h, now, _ptr(cnt, C.c_uint32), C.byref(tot)), "gsx_promise_broken")
+        return cnt, tot.value
+
+    def promise_fulfill(self, node: int, handle: int):
+        self._chk(self.lib.gsx_promise_fulfill(self.h, node, handle), "gsx_promise_fulfill")
+
+    def promise_throttle(self, pair: int):
+        self._chk(self.lib.gsx_promise_throttle(self.h, pair), "gsx_promise_throttle")
+
+    def promise_count(self) -> int:
+        n = C.c_uint64()
+        self._chk(self.lib.gsx_promise_count(self.h, C.byref(n)), "gsx_promise_count")
+        return n.value
+
     def timing_begin(self, max_launches: int):
         self._chk(self.lib.gsx_timing_begin(self.h, max_launches), "gsx_timing_begin")
 

@@ -202,11 +202,16 @@ enum gsx_event_kind {
     GSX_EV_MESH_DELIVERY = 6,    /* markDuplicateMessageDelivery score.go:944-974,
                                     window already checked by the caller               */
     GSX_EV_INVALID_DELIVERY = 7, /* markInvalidMessageDelivery   score.go:894-907      */
-    GSX_EV_PENALTY = 8           /* AddPenalty(p, arg) score.go:384-398                */
+    GSX_EV_PENALTY = 8,          /* AddPenalty(p, arg) score.go:384-398                */
+    GSX_EV_APP_SCORE = 9         /* AppSpecificScore(p) as score() reads it (score.go:320):
+                                    arg = the IEEE-754 bits of the pair's new value    */
 };
 
 /* 32-byte event record.  `pair` selects (observer, peer); `topic` is used by
- * GRAFT, PRUNE and the DELIVERY kinds; `arg` is the penalty count for PENALTY. */
+ * GRAFT, PRUNE and the DELIVERY kinds; `arg` is the penalty count for PENALTY
+ * and the application score's bits for APP_SCORE (a one-pair
+ * gsx_set_app_scores: a router re-reads AppSpecificScore(p) only for the peer
+ * it scores, and the engine re-scores only that observer's row). */
 typedef struct gsx_event {
     uint32_t kind;
     uint32_t topic;
@@ -620,7 +625,9 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      forwarded further within the round.  At the start of every heartbeat
  *      the IHAVE counters are cleared (:1566-1576) and promises that expired
  *      before now are broken: AddPenalty(peer, count) (:1578-1583, P7).
- *      Lists longer than MaxIHaveLength are not exchanged (GSX_ERANGE).
+ *      A truncated IHAVE list (below) is handled as the subset its target
+ *      got.  The promises of a pair are unbounded (gossip_tracer.go:59-74:
+ *      the engine doubles its per-pair slots whenever a pair could fill them).
  * Randomness (shufflePeers, :1890-1895) is Go's Int31n rejection rule over
  * draws h(seed, 8, node, tick << 32 | topic << 24 | k); candidate lists are in
  * ascending peer order; the unstable sort.Slice of :1393 is a stable sort
@@ -632,12 +639,19 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  * of the gossipsub batches it saw (gsx_propagate with the gossipsub router
  * Puts every message a node receives or publishes into its cache window 0;
  * within a batch the insertion order is ascending message index), read
- * newest window first over HistoryGossip windows; a list longer than
- * MaxIHaveLength is shuffled with the same draw stream (a shorter one is sent
- * whole, so its order is never observable and consumes no draws); targets are the non-mesh, non-direct mesh-capable topic peers
- * whose live score (after the node's maintenance of topics <= t) is >=
- * GossipThreshold, max(Dlazy, GossipFactor * |eligible|) of them, shuffled;
- * lists longer than MaxIHaveLength are reshuffled per target and truncated.
+ * newest window first over HistoryGossip windows; the list's order is never
+ * observable (a receiver collects it into a set, :643-650), so it is not
+ * shuffled and draws nothing; targets are the non-mesh, non-direct
+ * mesh-capable topic peers whose live score (after the node's maintenance of
+ * topics <= t) is >= GossipThreshold, max(Dlazy, GossipFactor * |eligible|)
+ * of them, shuffled.  A list of L > MaxIHaveLength ids reaches each target
+ * as its own uniform MaxIHaveLength-subset (the reference reshuffles the list
+ * per target and keeps a prefix, :1708-1720, which gives i.i.d. uniform
+ * subsets): Floyd's sampling of k = min(MaxIHaveLength, L - MaxIHaveLength)
+ * positions of the list (for j = L - k .. L - 1: x = Int31n(j + 1), take x
+ * unless taken, else j) with draws h(seed, 13, node << 32 | peer, tick << 32
+ * | topic << 24 | fan << 23 | k) (fan: the fanout pass), the taken positions
+ * when k == MaxIHaveLength, else the others.
  * Every heartbeat ends with mcache.Shift() (:1563).  */
 typedef struct gsx_heartbeat_out {
     uint64_t grafts;          /* peers grafted by the heartbeats (A)              */
@@ -667,6 +681,28 @@ typedef struct gsx_heartbeat_out {
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
+
+/* The gossipTracer's promises of every router (gossip_tracer.go:48-185; one
+ * router per observer, keyed by its pair to the promising peer and the
+ * message handle: the message set's serial << 32 | index inside the engine,
+ * any 64-bit id through these calls), the state step (D) keeps:
+ *  gsx_promise_add      AddPromise(p, msgIDs) (:48-75): tracks handles[Int31n(n)]
+ *                       (draws h(seed, 9, pair, k)) expiring at expire_ns,
+ *                       unless that (pair, message) promise exists;
+ *  gsx_promise_broken   GetBrokenPromises (:79-115): the promises expired
+ *                       before now are dropped and counted per pair (counts
+ *                       [n_pairs], may be NULL; no penalty: the heartbeat
+ *                       applies AddPenalty itself);
+ *  gsx_promise_fulfill  fulfillPromise (:119-126, Deliver / Validate / Reject):
+ *                       drops every promise of the node for the message;
+ *  gsx_promise_throttle ThrottlePeer (:167-185): drops the pair's promises;
+ *  gsx_promise_count    promises outstanding. */
+int gsx_promise_add(gsx_engine* e, uint64_t pair, const uint64_t* handles, uint32_t n, int64_t expire_ns,
+                    uint64_t seed);
+int gsx_promise_broken(gsx_engine* e, int64_t now_ns, uint32_t* counts, uint64_t* total);
+int gsx_promise_fulfill(gsx_engine* e, uint32_t node, uint64_t handle);
+int gsx_promise_throttle(gsx_engine* e, uint64_t pair);
+int gsx_promise_count(gsx_engine* e, uint64_t* n);
 /* The same round in steps, for a range shard (required there; any engine
  * may use them): gsx_hb_begin runs (A); gsx_hb_pack_ctl writes, per send
  * slot of the shard plan, the GRAFT and PRUNE bits of the pair it carries

@@ -13,6 +13,7 @@
 #pragma once
 
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -221,7 +222,7 @@ class PeerScore {
     double Score(const std::string& p) {  // score.go:247-256
         auto it = peers_.find(p);
         if (it == peers_.end()) return 0;
-        sync_app();
+        sync_app(it->second);  // score() calls AppSpecificScore(p) for p only (:320)
         double s = 0;
         check(gsx_score(e_, it->second, &s), "gsx_score");
         return s;
@@ -236,8 +237,7 @@ class PeerScore {
         params_.Topics[topic] = p;
         return {};
     }
-    void refreshScores() {  // :497-558
-        sync_app();
+    void refreshScores() {  // :497-558 (no AppSpecificScore call: Score(p) reads p's when it scores)
         check(gsx_refresh(e_, clock_->Now()), "gsx_refresh");
     }
     void gcDeliveryRecords() { check(gsx_gc_deliveries(e_, clock_->Now()), "gsx_gc_deliveries"); }  // :580-585
@@ -245,7 +245,8 @@ class PeerScore {
     // ---- RawTracer (score.go:588-830) ---------------------------------------------------
     void AddPeer(const std::string& p, const std::string& /*proto*/) { event(GSX_EV_ADD_PEER, p); }
     void RemovePeer(const std::string& p) {
-        sync_app();  // RemovePeer evaluates score() (:615)
+        auto it = peers_.find(p);
+        if (it != peers_.end()) sync_app(it->second);  // RemovePeer evaluates score(p) (:615)
         event(GSX_EV_REMOVE_PEER, p);
     }
     void Graft(const std::string& p, const std::string& topic) { event(GSX_EV_GRAFT, p, topic); }
@@ -311,15 +312,33 @@ class PeerScore {
         if (it == peers_.end()) return;
         check(fn(e_, it->second, msg_id(m.ID), topic_or_unscored(m.Topic), clock_->Now()), "gsx_trace");
     }
-    void sync_app() {  // AppSpecificScore(p) is called at score time (:320)
+    static bool same(double a, double b) { return a == b && std::signbit(a) == std::signbit(b); }
+    // AppSpecificScore(p) is called at score time (:320), for the scored peer
+    // only: a changed value is one GSX_EV_APP_SCORE event (the engine then
+    // re-scores that observer's row); an unchanged one leaves the engine's
+    // scores, and their host copy, valid.  The first call takes every peer's.
+    void sync_app(uint32_t i) {
+        if (!params_.AppSpecificScore) return;
+        if (!app_synced_) {
+            sync_app_all();
+            return;
+        }
+        const double a = params_.AppSpecificScore(ids_[i]);
+        if (same(a, app_[i])) return;
+        app_[i] = a;
+        int64_t bits;
+        std::memcpy(&bits, &a, sizeof bits);
+        gsx_event ev{GSX_EV_APP_SCORE, 0u, i, clock_->Now(), bits};
+        check(gsx_apply_events(e_, &ev, 1), "gsx_apply_events");
+    }
+    void sync_app_all() {  // a snapshot of every peer's (construction, inspection)
         if (!params_.AppSpecificScore) return;
         bool changed = !app_synced_;
         for (size_t i = 0; i < ids_.size(); ++i) {
             const double a = params_.AppSpecificScore(ids_[i]);
-            changed |= a != app_[i] || std::signbit(a) != std::signbit(app_[i]);
+            changed |= !same(a, app_[i]);
             app_[i] = a;
         }
-        // an unchanged snapshot leaves the engine's scores (and its host copy) valid
         if (changed) check(gsx_set_app_scores(e_, app_.data(), app_.size()), "gsx_set_app_scores");
         app_synced_ = true;
     }

@@ -82,6 +82,7 @@ typedef struct {
 typedef struct {
     uint64_t q, handle; /* the asker's pair (u -> v); message set serial << 32 | index */
     int64_t expire;
+    uint64_t used; /* slot occupied (open addressing, backward-shift deletion) */
 } orc_promise;
 typedef struct orc_mc_window {
     orc_mc_batch* b;
@@ -97,7 +98,7 @@ struct orc_engine {
     uint8_t* eflags; /* GSX_EDGE_* per pair */
     int64_t* backoff; /* gs.backoff[topic][peer] per [t][pair], 0 = no entry (gossipsub.go:436) */
     /* mcache (mcache.go): window w holds the gossipsub batches Put while it was
-     * window 0; node v has message k of a batch iff has[k * n + v] */
+     * window 0; node v has message k of a batch iff has[v * m + k] (node-major) */
     struct orc_mc_window* mc;
     uint32_t mc_n; /* windows alive (history[0..mc_n-1]) */
     uint32_t* ihave_len;   /* [t][pair] of the last heartbeat */
@@ -109,14 +110,21 @@ struct orc_engine {
      * the promises of gossipTracer (gossip_tracer.go:24-27) and mcache.peertx
      * (mcache.go:40) as (responder pair, handle) -> count */
     uint32_t *peerhave, *iasked;
-    orc_promise* prom;
+    orc_promise* prom; /* hash table keyed (pair, handle): promises[mid][p] of one router per observer */
     size_t n_prom, cap_prom;
+    /* the truncated IHAVE lists of the last heartbeat (gsx.h, emitGossip): per
+     * topic, the row of each (topic, pair) sent one (sub_idx[t][pair], UINT32_MAX
+     * none; allocated on first use) in a pool of sub_tw[t]-word bitmasks over the
+     * topic's gossip positions (the windows' batches in GetGossipIDs order) */
+    uint32_t* sub_idx[GSX_MAX_TOPICS];
+    uint64_t* sub_rows[GSX_MAX_TOPICS];
+    size_t sub_n[GSX_MAX_TOPICS], sub_cap[GSX_MAX_TOPICS]; /* rows handed out; words allocated */
+    uint32_t sub_tw[GSX_MAX_TOPICS];
     uint64_t* ptx_key; /* (pair << 0) ^ handle mixed; open addressing */
     uint64_t* ptx_pair;
     uint32_t* ptx_cnt;
     size_t ptx_cap, ptx_n;
     uint32_t msg_serial;
-    bool ihave_trunc;
     /* topic membership (A13): joined topics per node (gs.mesh[topic] exists;
      * its neighbours know it: gs.p.topics), fanout (gs.fanout, gs.lastpub) */
     uint64_t* sub;     /* [node] */
@@ -130,7 +138,7 @@ struct orc_engine {
     uint32_t* pxlog;
     size_t n_px, cap_px;
     uint64_t px_tick, px_seed;
-    gsx_gossipsub_params gp; /* for Publish / Join (D, fanout) */ /* the last heartbeat sent an IHAVE list longer than MaxIHaveLength */
+    gsx_gossipsub_params gp; /* for Publish / Join (D, fanout) */
     gsx_peer_score_params pp;
     gsx_topic_score_params tp[GSX_MAX_TOPICS];
     bool scored[GSX_MAX_TOPICS]; /* ps.params.Topics[topic] exists */
@@ -345,6 +353,10 @@ void orc_destroy(orc_engine* o) {
     free(o->lastpub);
     free(o->pxlog);
     free(o->prom);
+    for (int t = 0; t < GSX_MAX_TOPICS; t++) {
+        free(o->sub_idx[t]);
+        free(o->sub_rows[t]);
+    }
     free(o->ptx_key);
     free(o->ptx_pair);
     free(o->ptx_cnt);
@@ -414,8 +426,20 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     o->iasked = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
     if (!o->peerhave || !o->iasked) return GSX_ENOMEM;
     o->n_prom = 0;
-    o->ptx_n = 0;
-    if (o->ptx_key) memset(o->ptx_key, 0, sizeof(uint64_t) * o->ptx_cap);
+    if (o->prom) memset(o->prom, 0, sizeof(orc_promise) * o->cap_prom);
+    for (int t = 0; t < GSX_MAX_TOPICS; t++) { /* per-pair rows: sized by the new overlay on first use */
+        free(o->sub_idx[t]);
+        o->sub_idx[t] = NULL;
+        o->sub_n[t] = 0;
+    }
+    /* the GetForPeer counts start empty: a slot is occupied iff its count is
+     * nonzero, so the counts (and keys) of the last overlay are dropped whole */
+    free(o->ptx_key);
+    free(o->ptx_pair);
+    free(o->ptx_cnt);
+    o->ptx_key = o->ptx_pair = NULL;
+    o->ptx_cnt = NULL;
+    o->ptx_cap = o->ptx_n = 0;
     uint64_t** tw[4] = {&o->tr_sg, &o->tr_sp, &o->tr_ag, &o->tr_hp};
     for (int i = 0; i < 4; i++) {
         free(*tw[i]);
@@ -900,6 +924,7 @@ int orc_apply_events(orc_engine* o, const gsx_event* ev, size_t n) {
         case GSX_EV_MESH_DELIVERY: mark_duplicate(o, e->pair, e->topic, false, 0, e->now_ns); break;
         case GSX_EV_INVALID_DELIVERY: mark_invalid(o, e->pair, e->topic); break;
         case GSX_EV_PENALTY: add_penalty(o, e->pair, e->arg); break;
+        case GSX_EV_APP_SCORE: memcpy(&o->app[e->pair], &e->arg, sizeof(double)); break; /* score.go:320 */
         default: return GSX_EINVAL;
         }
     }
@@ -1402,8 +1427,8 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         if (from_out) memcpy(from_out + k * (size_t)N, from, sizeof(int32_t) * N);
         if (mcb) /* Publish Puts what a node processes: a dropped message only at its source */
             for (uint32_t i = 0; i < N; i++) {
-                mcb->has[k * (size_t)N + i] = hop[i] != 0xFF && (!dropped || i == src);
-                mcb->set->seen[k * (size_t)N + i] = hop[i] != 0xFF;
+                mcb->has[(size_t)i * m + k] = hop[i] != 0xFF && (!dropped || i == src);
+                mcb->set->seen[(size_t)i * m + k] = hop[i] != 0xFF;
             }
     }
     free(hop);
@@ -1468,6 +1493,11 @@ typedef struct {
     uint64_t tick;
     int64_t now;
     gsx_heartbeat_out* out;
+    uint64_t seed;
+    uint64_t* mids; /* emitGossip scratch: ids, gossip positions, Floyd marks */
+    uint32_t* mpos;
+    uint8_t* msel;
+    size_t mcap;
 } hb_ctx;
 
 static bool hb_in_mesh(const orc_engine* o, uint64_t r, uint32_t t) {
@@ -1623,48 +1653,79 @@ static void hb_unit(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* gr, uint64_t* pl
 #undef g
 }
 
-static void shuffle_ids(uint64_t* a, size_t n, orc_rng* g) { /* shuffleStrings, gossipsub.go:1897-1902 */
-    for (size_t i = 0; i < n; i++) {
-        size_t j = (size_t)rng_int31n(g, (int32_t)(i + 1));
-        uint64_t t = a[i];
-        a[i] = a[j];
-        a[j] = t;
-    }
-}
-
 static uint64_t ihave_digest(const uint64_t* ids, size_t n) { /* gsx.h, gsx_gossip_results */
     uint64_t d = 0;
     for (size_t i = 0; i < n; i++) d += splitmix(ids[i] + 0x9E3779B97F4A7C15ULL);
     return d;
 }
 
+/* Floyd's sampling (gsx.h, truncated IHAVE lists): k distinct positions of
+ * [0, L) marked in sel, draws Int31n(j + 1) for j = L - k .. L - 1 */
+static void floyd_select(uint8_t* sel, uint32_t L, uint32_t k, orc_rng* g) {
+    memset(sel, 0, L);
+    for (uint32_t j = L - k; j < L; j++) {
+        uint32_t x = (uint32_t)rng_int31n(g, (int32_t)(j + 1));
+        if (sel[x]) x = j;
+        sel[x] = 1;
+    }
+}
+
+/* the truncated list's row of (topic, pair), zeroed (allocated on first use) */
+static uint64_t* sub_row(orc_engine* o, uint32_t t, uint64_t r) {
+    const size_t E = o->E ? o->E : 1, tw = o->sub_tw[t];
+    if (!o->sub_idx[t]) {
+        o->sub_idx[t] = (uint32_t*)malloc(sizeof(uint32_t) * E);
+        memset(o->sub_idx[t], 0xFF, sizeof(uint32_t) * E);
+    }
+    if ((o->sub_n[t] + 1) * tw > o->sub_cap[t]) { /* capacity in words: tw changes between rounds */
+        size_t cap = o->sub_cap[t] ? 2 * o->sub_cap[t] : 1024 * tw;
+        while (cap < (o->sub_n[t] + 1) * tw) cap *= 2;
+        o->sub_cap[t] = cap;
+        o->sub_rows[t] = (uint64_t*)realloc(o->sub_rows[t], sizeof(uint64_t) * cap);
+    }
+    o->sub_idx[t][r] = (uint32_t)o->sub_n[t];
+    uint64_t* row = o->sub_rows[t] + tw * o->sub_n[t]++;
+    memset(row, 0, sizeof(uint64_t) * tw);
+    return row;
+}
+
 /* emitGossip (gossipsub.go:1669-1723) for (v, t) after its maintenance, with
- * mcache.GetGossipIDs (mcache.go:82-92) over the first HistoryGossip windows */
-static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t* peers, uint64_t** mids,
-                        size_t* mids_cap, bool fan) {
+ * mcache.GetGossipIDs (mcache.go:82-92) over the first HistoryGossip windows.
+ * The list's own order is never observable (a receiver collects it into a
+ * set, :643-650), so it is not shuffled and draws nothing; a list longer than
+ * MaxIHaveLength reaches each target as its own uniform MaxIHaveLength-subset
+ * (the reference reshuffles the list per target and keeps a prefix,
+ * :1712-1720: i.i.d. uniform subsets), drawn by Floyd's sampling of
+ * min(MaxIHaveLength, L - MaxIHaveLength) positions with draws h(seed, 13,
+ * node << 32 | peer, tick << 32 | topic << 24 | fan << 23 | k): the marked positions when
+ * that is MaxIHaveLength, else the unmarked ones.  The subset is kept per
+ * (topic, pair) as a bitmask over the topic's gossip positions for the
+ * exchange (D). */
+static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t* peers, bool fan) {
     orc_engine* o = c->o;
     const gsx_gossipsub_params* gp = c->gp;
     size_t L = 0;
+    uint32_t base = 0; /* gossip position of the batch's message 0 */
     const uint32_t nw = (uint32_t)gp->history_gossip < o->mc_n ? (uint32_t)gp->history_gossip : o->mc_n;
     for (uint32_t w = 0; w < nw; w++)
         for (size_t b = 0; b < o->mc[w].nb; b++) {
             const orc_mc_batch* mb = &o->mc[w].b[b];
             if (mb->topic != t) continue;
+            const uint8_t* has = mb->has + (size_t)v * mb->m;
             for (uint32_t k = 0; k < mb->m; k++) {
-                if (!mb->has[(size_t)k * mb->n + v]) continue;
-                if (L == *mids_cap) {
-                    *mids_cap = *mids_cap ? 2 * *mids_cap : 1024;
-                    *mids = (uint64_t*)realloc(*mids, sizeof(uint64_t) * *mids_cap);
+                if (!has[k]) continue;
+                if (L == c->mcap) {
+                    c->mcap = c->mcap ? 2 * c->mcap : 1024;
+                    c->mids = (uint64_t*)realloc(c->mids, sizeof(uint64_t) * c->mcap);
+                    c->mpos = (uint32_t*)realloc(c->mpos, sizeof(uint32_t) * c->mcap);
+                    c->msel = (uint8_t*)realloc(c->msel, c->mcap);
                 }
-                (*mids)[L++] = mb->ids[k];
+                c->mids[L] = mb->ids[k];
+                c->mpos[L++] = base + k;
             }
+            base += mb->m;
         }
     if (L == 0) return;
-    uint64_t* ids = *mids;
-    /* shuffleStrings(mids) (:1676): the order is observable only through the
-     * per-target truncation, so the canonical draws shuffle only a list
-     * longer than MaxIHaveLength (gsx.h, heartbeat draws) */
-    if (L > (size_t)gp->max_ihave_length) shuffle_ids(ids, L, g);
     int np = 0;
     for (int64_t r = o->row_ptr[v]; r < o->row_ptr[v + 1]; r++) {
         if (!in_topic(o, (uint64_t)r, t)) continue;
@@ -1680,16 +1741,33 @@ static void emit_gossip(hb_ctx* c, uint32_t v, uint32_t t, orc_rng* g, uint64_t*
     if (factor > target) target = factor;
     if (target > np) target = np;
     else shuffle_pairs(peers, np, g);
+    const size_t maxl = (size_t)(gp->max_ihave_length > 0 ? gp->max_ihave_length : 0);
+    uint64_t all = 0;
+    if (L <= maxl) all = ihave_digest(c->mids, L);
     for (int i = 0; i < target; i++) {
+        const uint64_t r = peers[i];
+        const size_t x = (size_t)t * o->E + r;
         size_t len = L;
-        if (L > (size_t)gp->max_ihave_length) {
-            shuffle_ids(ids, L, g);
-            len = (size_t)gp->max_ihave_length;
-            o->ihave_trunc = true;
+        uint64_t d = all;
+        if (L > maxl) {
+            const uint32_t kk = (uint32_t)(maxl < L - maxl ? maxl : L - maxl);
+            const bool take = kk == maxl; /* the marked positions are the list, else the unmarked ones */
+            orc_rng gs = {c->seed, 13, ((uint64_t)v << 32) | (uint32_t)o->col[r],
+                          (c->tick << 32) | ((uint64_t)t << 24) | ((uint64_t)fan << 23), 0};
+            floyd_select(c->msel, (uint32_t)L, kk, &gs);
+            uint64_t* row = sub_row(o, t, r);
+            len = maxl;
+            d = 0;
+            for (size_t e = 0; e < L; e++)
+                if ((c->msel[e] != 0) == take) {
+                    d += splitmix(c->mids[e] + 0x9E3779B97F4A7C15ULL);
+                    row[c->mpos[e] / 64] |= 1ull << (c->mpos[e] % 64);
+                }
+        } else if (o->sub_idx[t]) {
+            o->sub_idx[t][r] = UINT32_MAX; /* (a fanout pass after a truncated mesh pass) */
         }
-        const size_t x = (size_t)t * o->E + peers[i];
         o->ihave_len[x] = (uint32_t)len;
-        o->ihave_hash[x] = ihave_digest(ids, len);
+        o->ihave_hash[x] = d;
         c->out->ihave_msgs++;
         c->out->ihave_ids += len;
     }
@@ -1725,24 +1803,127 @@ static void handle_prune(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t
 /* ---- (D) the gossip exchange: handleIHave / handleIWant (gossipsub.go:615-716)
  * and the gossipTracer's promises (gossip_tracer.go:48-153) -------------- */
 
-static void add_promise(orc_engine* o, uint64_t q, uint64_t handle, int64_t expire) { /* AddPromise :59-74 */
-    for (size_t i = 0; i < o->n_prom; i++)
-        if (o->prom[i].q == q && o->prom[i].handle == handle) return;
-    if (o->n_prom == o->cap_prom) {
-        o->cap_prom = o->cap_prom ? 2 * o->cap_prom : 64;
-        o->prom = (orc_promise*)realloc(o->prom, sizeof(orc_promise) * o->cap_prom);
+/* The promises of every router's gossipTracer (gossip_tracer.go:24-27),
+ * promises[mid][p] of observer u as one hash table keyed (pair (u -> p),
+ * handle): linear probing with backward-shift deletion, no bound on the
+ * number outstanding (AddPromise never refuses one, :59-74). */
+static size_t prom_home(uint64_t q, uint64_t handle, size_t cap) {
+    return (size_t)mix64(q * 0x9E3779B97F4A7C15ULL ^ handle) & (cap - 1);
+}
+static int64_t prom_find(const orc_engine* o, uint64_t q, uint64_t handle) {
+    if (!o->cap_prom) return -1;
+    for (size_t j = prom_home(q, handle, o->cap_prom);; j = (j + 1) & (o->cap_prom - 1)) {
+        if (!o->prom[j].used) return -1;
+        if (o->prom[j].q == q && o->prom[j].handle == handle) return (int64_t)j;
     }
-    o->prom[o->n_prom].q = q;
-    o->prom[o->n_prom].handle = handle;
-    o->prom[o->n_prom].expire = expire;
+}
+static void prom_put(orc_engine* o, uint64_t q, uint64_t handle, int64_t expire) { /* (q, handle) absent */
+    if (2 * (o->n_prom + 1) > o->cap_prom) {
+        const size_t oc = o->cap_prom, nc = oc ? 2 * oc : 1024;
+        orc_promise* old = o->prom;
+        o->prom = (orc_promise*)calloc(nc, sizeof(orc_promise));
+        o->cap_prom = nc;
+        o->n_prom = 0;
+        for (size_t i = 0; i < oc; i++)
+            if (old[i].used) prom_put(o, old[i].q, old[i].handle, old[i].expire);
+        free(old);
+    }
+    size_t j = prom_home(q, handle, o->cap_prom);
+    while (o->prom[j].used) j = (j + 1) & (o->cap_prom - 1);
+    o->prom[j].q = q;
+    o->prom[j].handle = handle;
+    o->prom[j].expire = expire;
+    o->prom[j].used = 1;
     o->n_prom++;
+}
+static void prom_erase(orc_engine* o, size_t i) {
+    const size_t m = o->cap_prom - 1;
+    for (size_t j = (i + 1) & m; o->prom[j].used; j = (j + 1) & m) {
+        const size_t k = prom_home(o->prom[j].q, o->prom[j].handle, o->cap_prom);
+        /* the entry at j may fill the hole at i iff its home is not cyclically in (i, j] */
+        const bool in = i <= j ? (k > i && k <= j) : (k > i || k <= j);
+        if (!in) {
+            o->prom[i] = o->prom[j];
+            i = j;
+        }
+    }
+    memset(&o->prom[i], 0, sizeof(orc_promise));
+    o->n_prom--;
+}
+/* Keeps the promises keep(entry) accepts, rebuilding the table. */
+static void prom_filter(orc_engine* o, bool (*keep)(const orc_promise*, const void*), const void* arg) {
+    const size_t oc = o->cap_prom;
+    orc_promise* old = o->prom;
+    o->prom = oc ? (orc_promise*)calloc(oc, sizeof(orc_promise)) : NULL;
+    o->n_prom = 0;
+    for (size_t i = 0; i < oc; i++)
+        if (old[i].used && keep(&old[i], arg)) prom_put(o, old[i].q, old[i].handle, old[i].expire);
+    free(old);
+}
+
+static void add_promise(orc_engine* o, uint64_t q, uint64_t handle, int64_t expire) { /* AddPromise :59-74 */
+    if (prom_find(o, q, handle) < 0) prom_put(o, q, handle, expire);
 }
 
 static void fulfill_promises(orc_engine* o, uint32_t u, uint64_t handle) { /* fulfillPromise :119-126 */
-    for (size_t i = 0; i < o->n_prom;) {
-        if (o->pair_obs[o->prom[i].q] == u && o->prom[i].handle == handle) o->prom[i] = o->prom[--o->n_prom];
-        else i++;
+    if (!o->n_prom) return;
+    for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) {
+        const int64_t i = prom_find(o, (uint64_t)q, handle);
+        if (i >= 0) prom_erase(o, (size_t)i);
     }
+}
+
+typedef struct {
+    int64_t now;
+    uint32_t* cnt;
+    uint64_t total;
+} broken_ctx;
+static bool prom_keep_unbroken(const orc_promise* p, const void* arg) {
+    broken_ctx* c = (broken_ctx*)arg;
+    if (!(p->expire < c->now)) return true;
+    c->cnt[p->q]++;
+    c->total++;
+    return false;
+}
+/* GetBrokenPromises (:79-115): the promises that expired before now are
+ * removed and counted per pair; returns their number */
+static uint64_t broken_promises(orc_engine* o, int64_t now, uint32_t* cnt) {
+    broken_ctx c = {now, cnt, 0};
+    if (o->n_prom) prom_filter(o, prom_keep_unbroken, &c);
+    return c.total;
+}
+static bool prom_keep_other_pair(const orc_promise* p, const void* arg) { return p->q != *(const uint64_t*)arg; }
+
+/* The gossipTracer's methods on one router's promises (gsx.h: the tracer
+ * API, gossip_tracer.go:48-185): AddPromise's pick is Int31n(n) with draws
+ * h(seed, 9, pair, k). */
+int orc_promise_add(orc_engine* o, uint64_t q, const uint64_t* handles, uint32_t n, int64_t expire, uint64_t seed) {
+    if (q >= o->E || n == 0 || n > 0x7FFFFFFFu) return GSX_EINVAL;
+    orc_rng g = {seed, 9, q, 0, 0};
+    add_promise(o, q, handles[rng_int31n(&g, (int32_t)n)], expire);
+    return 0;
+}
+int orc_promise_broken(orc_engine* o, int64_t now, uint32_t* counts, uint64_t* total) {
+    uint32_t* cnt = (uint32_t*)calloc(o->E ? o->E : 1, sizeof(uint32_t));
+    const uint64_t n = broken_promises(o, now, cnt);
+    if (counts) memcpy(counts, cnt, sizeof(uint32_t) * o->E);
+    if (total) *total = n;
+    free(cnt);
+    return 0;
+}
+int orc_promise_fulfill(orc_engine* o, uint32_t node, uint64_t handle) {
+    if (node >= o->n_nodes) return GSX_EINVAL;
+    fulfill_promises(o, node, handle);
+    return 0;
+}
+int orc_promise_throttle(orc_engine* o, uint64_t q) { /* ThrottlePeer :167-185 */
+    if (q >= o->E) return GSX_EINVAL;
+    if (o->n_prom) prom_filter(o, prom_keep_other_pair, &q);
+    return 0;
+}
+int orc_promise_count(orc_engine* o, uint64_t* n) {
+    *n = o->n_prom;
+    return 0;
 }
 
 /* mcache.GetForPeer's per-(message, peer) count (mcache.go:66-80), keyed by
@@ -1817,7 +1998,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
     gx_item* items = (gx_item*)malloc(sizeof(gx_item) * cap_it);
     gx_req* reqs = (gx_req*)malloc(sizeof(gx_req) * cap_rq);
     gx_item* W = (gx_item*)malloc(sizeof(gx_item) * cap_w);
-    int rc = o->ihave_trunc ? GSX_ERANGE : 0; /* truncated lists are not exchanged (gsx.h) */
+    int rc = 0;
     /* handleIHave at every node u, one IHAVE RPC per sending peer v, senders ascending */
     for (uint32_t u = 0; u < N && !rc; u++)
         for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) {
@@ -1831,12 +2012,19 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             size_t n = 0;
             for (uint32_t t = 0; t < T; t++) {
                 if (!(tb >> t & 1) || !joined(o, u, t)) continue; /* gs.mesh[topic] (:638-641) */
+                /* a truncated list: the subset v sent u (emitGossip) */
+                const uint32_t si = o->sub_idx[t] ? o->sub_idx[t][r] : UINT32_MAX;
+                const uint64_t* sub = si != UINT32_MAX ? o->sub_rows[t] + (size_t)o->sub_tw[t] * si : NULL;
+                uint32_t base = 0; /* gossip position of the batch's message 0 */
                 for (size_t i = 0; i < nb; i++) {
                     const orc_mc_batch* b = gb[i].b;
                     if (b->topic != t) continue;
+                    const uint32_t b0 = base;
+                    base += b->m;
                     for (uint32_t k = 0; k < b->m; k++) {
-                        if (!b->has[(size_t)k * b->n + v]) continue;
-                        if (b->set->seen[(size_t)k * N + u]) continue; /* seenMessage (:645) */
+                        if (!b->has[(size_t)v * b->m + k]) continue;
+                        if (sub && !(sub[(b0 + k) / 64] >> ((b0 + k) % 64) & 1)) continue;
+                        if (b->set->seen[(size_t)u * b->m + k]) continue; /* seenMessage (:645) */
                         if (n == cap_w) {
                             cap_w *= 2;
                             W = (gx_item*)realloc(W, sizeof(gx_item) * cap_w);
@@ -1926,7 +2114,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             const orc_mc_batch* b = gb[items[j].gb].b;
             orc_msgset* st = b->set;
             const uint32_t k = items[j].k, t = b->topic, val = st->val[k];
-            uint8_t* sn = &st->seen[(size_t)k * N + u];
+            uint8_t* sn = &st->seen[(size_t)u * st->m + k];
             if (*sn) { /* DuplicateMessage */
                 out->gossip_duplicates++;
                 if (val == GSX_VALIDATION_ACCEPT) mark_duplicate(o, q, t, true, now, now);
@@ -1949,7 +2137,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
                     rt[nr] = t;
                     nr++;
                 }
-                rh[x][(size_t)k * N + u] = 1; /* Put into u's cache */
+                rh[x][(size_t)u * st->m + k] = 1; /* Put into u's cache */
             } else {
                 out->gossip_rejected++;
                 if (val == GSX_VALIDATION_REJECT) mark_invalid(o, q, t);
@@ -2159,20 +2347,11 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
             }
     /* clearIHaveCounters (:1566-1576), applyIwantPenalties (:1578-1583): a
      * promise whose expiry is before now is broken (GetBrokenPromises, :79-115) */
-    o->ihave_trunc = false;
     memset(o->peerhave, 0, sizeof(uint32_t) * (E ? E : 1));
     memset(o->iasked, 0, sizeof(uint32_t) * (E ? E : 1));
     if (o->n_prom) {
         uint32_t* cnt = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
-        for (size_t i = 0; i < o->n_prom;) {
-            if (o->prom[i].expire < now) {
-                cnt[o->prom[i].q]++;
-                out->broken_promises++;
-                o->prom[i] = o->prom[--o->n_prom];
-            } else {
-                i++;
-            }
-        }
+        out->broken_promises += broken_promises(o, now, cnt);
         for (uint64_t q = 0; q < E; q++) /* AddPenalty(p, count): one addition of the count */
             if (cnt[q]) add_penalty(o, q, cnt[q]);
         free(cnt);
@@ -2195,11 +2374,21 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     uint64_t* plst = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
     uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
     for (uint64_t r = 0; r < E; r++) cache[r] = score_pair(o, r); /* the heartbeat's score cache */
-    hb_ctx c = {o, gp, cache, ctl, tick, now, out};
+    hb_ctx c = {o, gp, cache, ctl, tick, now, out, seed, NULL, NULL, NULL, 0};
+    /* the truncated IHAVE rows of this round: per topic, one bit per gossip position */
+    {
+        const uint32_t nwin = (uint32_t)gp->history_gossip < o->mc_n ? (uint32_t)gp->history_gossip : o->mc_n;
+        size_t pos[GSX_MAX_TOPICS] = {0};
+        for (uint32_t w = 0; w < nwin; w++)
+            for (size_t b = 0; b < o->mc[w].nb; b++) pos[o->mc[w].b[b].topic] += o->mc[w].b[b].m;
+        for (uint32_t t = 0; t < T; t++) {
+            o->sub_tw[t] = (uint32_t)((pos[t] + 63) / 64);
+            o->sub_n[t] = 0;
+            if (o->sub_idx[t]) memset(o->sub_idx[t], 0xFF, sizeof(uint32_t) * (E ? E : 1));
+        }
+    }
     memset(o->ihave_len, 0, sizeof(uint32_t) * (size_t)T * (E ? E : 1));
     memset(o->ihave_hash, 0, sizeof(uint64_t) * (size_t)T * (E ? E : 1));
-    uint64_t* mids = NULL;
-    size_t mids_cap = 0;
     /* (A) every node's heartbeat, every joined topic in ascending order:
      * mesh maintenance, then IHAVE gossip, one draw stream per (node, topic) */
     for (uint32_t v = 0; v < o->n_nodes; v++) {
@@ -2207,7 +2396,7 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
             if (!joined(o, v, t)) continue; /* gs.mesh holds the joined topics */
             orc_rng g = {seed, 8, v, (tick << 32) | ((uint64_t)t << 24), 0};
             hb_unit(&c, v, t, &g, plst, tmp);
-            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap, false);
+            emit_gossip(&c, v, t, &g, tmp, false);
         }
         /* expire fanout for topics not published to in a while (:1517-1524) */
         for (uint32_t t = 0; t < T; t++) {
@@ -2234,10 +2423,12 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
                                         tmp, &g);
                 for (int i = 0; i < k; i++) o->fanout[tmp[i]] |= 1ull << t;
             }
-            emit_gossip(&c, v, t, &g, tmp, &mids, &mids_cap, true);
+            emit_gossip(&c, v, t, &g, tmp, true);
         }
     }
-    free(mids);
+    free(c.mids);
+    free(c.mpos);
+    free(c.msel);
     /* (B) receivers, (C) the PRUNE answers; the (A) PRUNEs' PX on the snapshot (B) read */
     hb_receive(o, gp, ctl, resp, cache, now, out);
     if (o->pxno) hb_px(o, gp, 0, ctl, cache, out);
@@ -2468,7 +2659,7 @@ int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_wind
             const orc_mc_batch* mb = &o->mc[w].b[b];
             if (topic != GSX_ANY_TOPIC && mb->topic != topic) continue;
             for (uint32_t k = 0; k < mb->m; k++)
-                if (mb->has[(size_t)k * mb->n + node]) {
+                if (mb->has[(size_t)node * mb->m + k]) {
                     if (n < cap) out[n] = mb->ids[k];
                     n++;
                 }

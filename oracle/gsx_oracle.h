@@ -76,6 +76,12 @@ int orc_hb_px_records(orc_engine* o, uint32_t* out, size_t cap, size_t* n);
 int orc_export_backoff(orc_engine* o, int64_t* out);
 int orc_import_backoff(orc_engine* o, const int64_t* in);
 int orc_gossip_results(orc_engine* o, uint32_t* len, uint64_t* hash);
+/* the gossipTracer's promises (gossip_tracer.go:48-185; gsx.h gsx_promise_*) */
+int orc_promise_add(orc_engine* o, uint64_t pair, const uint64_t* handles, uint32_t n, int64_t expire, uint64_t seed);
+int orc_promise_broken(orc_engine* o, int64_t now, uint32_t* counts, uint64_t* total);
+int orc_promise_fulfill(orc_engine* o, uint32_t node, uint64_t handle);
+int orc_promise_throttle(orc_engine* o, uint64_t pair);
+int orc_promise_count(orc_engine* o, uint64_t* n);
 int orc_mcache_clear(orc_engine* o);
 int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
                    size_t* n_out);

@@ -72,6 +72,11 @@ _SIG = {
     "orc_leave": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, P(abi.HeartbeatOut)]),
     "orc_hb_trace_words": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]),
     "orc_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
+    "orc_promise_add": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint64), C.c_uint32, C.c_int64, C.c_uint64]),
+    "orc_promise_broken": (C.c_int, [C.c_void_p, C.c_int64, P(C.c_uint32), P(C.c_uint64)]),
+    "orc_promise_fulfill": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64]),
+    "orc_promise_throttle": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "orc_promise_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
 }
@@ -275,6 +280,29 @@ class Oracle:
         self._chk(self.lib.orc_mcache_ids(self.h, node, topic, n_windows, _p(out, C.c_uint64), len(out), C.byref(n)),
                   "orc_mcache_ids")
         return out
+
+    # the gossipTracer's promises (gossip_tracer.go:48-185)
+    def promise_add(self, pair, handles, expire, seed=0):
+        h = np.ascontiguousarray(handles, dtype=np.uint64)
+        self._chk(self.lib.orc_promise_add(self.h, pair, _p(h, C.c_uint64), len(h), expire, seed), "orc_promise_add")
+
+    def promise_broken(self, now):
+        """GetBrokenPromises: -> (per-pair counts [n_pairs] u32, total); the broken ones are dropped."""
+        cnt = np.zeros(self.n_pairs, dtype=np.uint32)
+        tot = C.c_uint64()
+        self._chk(self.lib.orc_promise_broken(self.h, now, _p(cnt, C.c_uint32), C.byref(tot)), "orc_promise_broken")
+        return cnt, tot.value
+
+    def promise_fulfill(self, node, handle):
+        self._chk(self.lib.orc_promise_fulfill(self.h, node, handle), "orc_promise_fulfill")
+
+    def promise_throttle(self, pair):
+        self._chk(self.lib.orc_promise_throttle(self.h, pair), "orc_promise_throttle")
+
+    def promise_count(self):
+        n = C.c_uint64()
+        self._chk(self.lib.orc_promise_count(self.h, C.byref(n)), "orc_promise_count")
+        return n.value
 
     def set_ip_whitelist(self, ips: Iterable[int]):
         a = np.ascontiguousarray(list(ips), dtype=np.uint32)

@@ -15,7 +15,8 @@ assert an inequality because of real sleeps (TimeInMesh ">=", TimeInMeshCap
 exact value the same expression gives under the simulated clock and keeps the
 Go relation in `go_assert` for reference.
 
-Run:  python tests/golden/make_golden.py   (writes score_kat.json, params_validation.json)
+Run:  python tests/golden/make_golden.py
+      (writes score_kat.json, params_validation.json, promise_kat.json)
 """
 from __future__ import annotations
 
@@ -432,7 +433,43 @@ def decay_cases():
     return [dict(ref="score_params_test.go:323-328", decay_ns=HOUR, expected=0.9987216039048303)]
 
 
+def promise_cases():
+    """gossip_tracer_test.go: the gossipTracer's promise bookkeeping.
+
+    Peers A, B, C are the observer's pairs 0, 1, 2; mids are the handles
+    1 << 32 | i of 100 messages.  Times are offsets from the moment of the
+    AddPromise calls.  `followup_ns` is the tracer's followUpTime; a
+    GetBrokenPromises step lists the per-peer counts the test asserts (an
+    empty dict for "expected no broken promises", i.e. a nil map)."""
+    mids = [(1 << 32) | i for i in range(100)]
+    broken = dict(
+        name="TestBrokenPromises", ref="gossip_tracer_test.go:12-57",
+        # gt.followUpTime = 100 ms; the sleep is GossipSubIWantFollowupTime (3 s) + 10 ms
+        followup_ns=100 * MS, peers=["A", "B", "C"], mids=mids,
+        steps=[
+            dict(op="add", peer="A"), dict(op="add", peer="B"), dict(op="add", peer="C"),
+            dict(op="broken", at_ns=0, expect={}),
+            dict(op="throttle", peer="C"),
+            dict(op="broken", at_ns=3 * S + 10 * MS, expect={"A": 1, "B": 1}),
+        ],
+    )
+    none = dict(
+        name="TestNoBrokenPromises", ref="gossip_tracer_test.go:59-97",
+        # newGossipTracer() without Start: followUpTime is the zero Duration, the
+        # promises expire at once; DeliverMessage fulfils all of them first
+        followup_ns=0, peers=["A", "B"], mids=mids,
+        steps=[
+            dict(op="add", peer="A"), dict(op="add", peer="B"),
+            dict(op="deliver_all"),
+            dict(op="broken", at_ns=110 * MS, expect={}),
+        ],
+    )
+    return [broken, none]
+
+
 def main():
+    with open(os.path.join(OUT, "promise_kat.json"), "w") as f:
+        json.dump(promise_cases(), f, indent=1)
     sc = scenarios()
     with open(os.path.join(OUT, "score_kat.json"), "w") as f:
         json.dump(_enc(sc), f, indent=0)

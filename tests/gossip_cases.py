@@ -24,15 +24,21 @@ def params(**kw):
     return gp
 
 
-def exchange_run(be, n=300, d=6, T=2, seed=5, ticks=8, hops=2, msgs=24, invalid=0.0, exchange_from=0, **gp_kw):
+def exchange_run(be, n=300, d=6, T=2, seed=5, ticks=8, hops=2, msgs=24, invalid=0.0, exchange_from=0, prefill=0,
+                 **gp_kw):
     """pc.setup's random mesh; every round: a heartbeat (with the exchange),
     then a gossipsub batch that travels only `hops` hops (so most nodes miss
     it and learn of it by IHAVE), then a refresh.  Rounds before
-    `exchange_from` only emit IHAVEs.  Returns per-tick counters
+    `exchange_from` only emit IHAVEs; `prefill` promises per pair are made
+    before the first round (the engine's per-pair slots fill and grow).
+    Returns per-tick counters
     and snapshots (records, backoff, scores, IHAVEs) plus every node's cached
     ids after the last round."""
     ov = pc.overlay(n, d, seed)
     pc.setup(be, ov, T, seed, mesh_degree=6)
+    for q in range(ov.n_pairs if prefill else 0):  # promises no exchange fulfils, expiring late
+        for j in range(prefill):
+            be.promise_add(q, [(0xFFFF << 32) | (q * prefill + j)], hc.T0 + 10**6 * S)
     outs, snaps = [], []
     for k in range(ticks):
         if k <= exchange_from:  # no exchange before round exchange_from

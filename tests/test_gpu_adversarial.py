@@ -40,6 +40,16 @@ def test_invalid_message_spam_stops_at_graylist(gpu_ok):
     by AcceptFrom (tests/spam_cases.py); every call matches the oracle."""
     import spam_cases as sc
 
-    g = sc.run(gsx.Engine(1))
+    e, o = gsx.Engine(1), orc.Oracle(1)
+    g = sc.run(e)
     sc.check(g)
-    assert g == sc.run(orc.Oracle(1))
+    assert g == sc.run(o)
+    # the legit node PRUNEs the attacker once its score is negative
+    # (gossipsub_spam_test.go:745-750): its heartbeat drops the negative-score
+    # mesh peer (gossipsub.go:1361-1368) and sends PRUNE; the attacker is backed off
+    hb = [be.heartbeat(1, sc.T0 + sc.S, 3).as_dict() for be in (e, o)]
+    assert hb[0] == hb[1] and hb[0]["prunes"] == 1
+    st = e.export_state()
+    assert not (st["rec_flags"][0] & abi.GSX_REC_IN_MESH)  # out of the legit node's mesh
+    assert e.export_backoff()[0][0] > sc.T0 + sc.S  # PRUNE backoff on the attacker
+    assert np.array_equal(e.export_backoff(), o.export_backoff())

@@ -5,9 +5,12 @@
 - cfg2  10k-peer random d=6 overlay, floodsub and gossipsub propagation == oracle;
 - cfg3  1M peers x 8 topics: heartbeats (the OpportunisticGraftTicks round and the
         next one) == oracle on the exported state, mesh maintenance, IHAVE gossip,
-        backoff, scores bit for bit;
+        backoff, scores bit for bit; and five rounds with the gossip exchange on
+        (IWANT, recovery, promises, P7) == oracle;
 - cfg4  10M-peer overlay on one GPU, floodsub: arrival hops == BFS distances on
-        sampled messages, totals consistent (each node reached at most once);
+        sampled messages, totals consistent (each node reached at most once); and
+        the same overlay range-sharded in two (RangeSharded over a local transport)
+        == the unsharded engine, hop for hop;
 - cfg5  4M peers, 20 % colocated sybils with invalid-message counters: sybils at
         their victims score below GraylistThreshold, and after heartbeats no peer
         whose round-start score was negative is in any mesh, while honest nodes keep
@@ -124,6 +127,56 @@ def test_cfg3_heartbeat_1m_x_8_matches_oracle(gpu_ok):
         del gs, ws
 
 
+@pytest.mark.timeout(1500)
+def test_cfg3_gossip_exchange_1m_x_8_matches_oracle(gpu_ok):
+    """cfg3 with the gossip exchange on (handleIHave / handleIWant, promises,
+    P7): five rounds of a 256-message gossipsub batch that travels 5 hops
+    (most nodes miss it and learn of it by IHAVE) then a heartbeat; every
+    round's counters (IWANTs, served, recovered, broken promises), scores,
+    backoff and state equal the oracle's."""
+    import gossip_cases as gc
+
+    n, T, seed = 1_000_000, 8, synth.SEED
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    e = gsx.Engine(T)
+    e.set_peer_params(synth.bench_peer_params())
+    for t in range(T):
+        e.set_topic_params(t, synth.spam_test_topic_params())
+    e.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    e.synthesize_state(abi.SynthSpec(seed=seed, now_ns=pc.T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0,
+                                     imd_max_sybil=100.0, p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0,
+                                     p_disconnected=0.0, p_absent=0.0, expire_jitter_ns=4 * S, sybil_first_node=n))
+    e.set_app_scores(np.zeros(ov.n_pairs))
+    e.refresh(pc.T0 + S)
+    st = e.export_state()
+    o = orc.Oracle(T)
+    _cfg3_backend(o, ov, T, st)
+    _cfg3_backend(e, ov, T, st)
+    del st
+    gp = gc.params(iwant_followup_ns=S)  # promises of round k break at round k + 2 (P7 within the run)
+    for be in (e, o):
+        be.set_gossipsub_params(gp)
+    tot = {}
+    for k in range(5):
+        now = pc.T0 + (2 + k) * S
+        cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % 2, max_hops=5, latency_ms=10, seed=7 + k)
+        cfg.now_ns = now
+        ms = pc.messages(n, 256, 100 + k)
+        outs = [be.propagate(ms, cfg)[0].as_dict() for be in (e, o)]
+        assert outs[0] == outs[1], k
+        ho = [be.heartbeat(61 + k, now + 500 * abi.MILLISECOND, seed).as_dict() for be in (e, o)]
+        assert ho[0] == ho[1], (k, {x: (ho[0][x], ho[1][x]) for x in ho[0] if ho[0][x] != ho[1][x]})
+        for x, v in ho[0].items():
+            tot[x] = tot.get(x, 0) + v
+        _same(e.scores(), o.scores(), (k, "scores"))
+        _same(e.export_backoff(), o.export_backoff(), (k, "backoff"))
+        gs, ws = e.export_state(), o.export_state()
+        for f in abi.STATE_FIELDS:
+            _same(gs[f], ws[f], (k, f))
+        del gs, ws
+    assert tot["iwant_msgs"] > 0 and tot["gossip_delivered"] > 0 and tot["broken_promises"] > 0, tot
+
+
 def _bfs(row_ptr, col, src):
     """Level-synchronous BFS over a CSR overlay (numpy): hop distance per node, -1 unreached."""
     n = len(row_ptr) - 1
@@ -161,6 +214,67 @@ def test_cfg4_10m_floodsub_properties(gpu_ok):
     assert out.deliveries == int(reached.sum()) - len(ms)  # each (node, message) reached at most once
     assert out.transmissions == out.deliveries + out.duplicates
     assert reached.mean() > 0.999
+    for k in range(2):
+        dist = _bfs(ov.row_ptr, ov.col.astype(np.int64), int(ms["source"][k]))
+        r = dist >= 0
+        assert np.array_equal(reached[k], r)
+        assert np.array_equal(hop[k][r].astype(np.int64), dist[r])
+
+
+@pytest.mark.timeout(1200)
+def test_cfg4_10m_range_sharded_matches_single_engine(gpu_ok):
+    """cfg4's own layout: the 10M overlay split into two RangeSharded shards
+    (gsx/shard.py, the per-hop compacted frontier exchange) run as lock-step
+    threads on one GPU, BASELINE's 64-message floodsub batch.  The stitched
+    arrival hops equal the unsharded engine's, the totals equal, and sampled
+    messages' hops are BFS distances."""
+    import torch  # noqa: F401  (the shard threads' streams)
+
+    from gsx import shard
+
+    n, seed, world = 10_000_000, synth.SEED + 1, 2
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    spec = abi.SynthSpec(seed=seed, now_ns=pc.T0, fmd_max=10, mmd_max=10, mfp_max=1, imd_max_sybil=0, p_in_mesh=0.5,
+                         graft_window_ns=abi.HOUR, bp_max=0, p_disconnected=0, p_absent=0, expire_jitter_ns=0,
+                         sybil_first_node=n)
+
+    def params(e):
+        e.set_peer_params(synth.bench_peer_params())
+        e.set_topic_params(0, synth.spam_test_topic_params())
+
+    ms = pc.messages(n, 64, 12)
+    cfg = pc.config(abi.GSX_ROUTER_FLOODSUB, credit=0)
+    full = gsx.Engine(1)
+    params(full)
+    full.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    full.synthesize_state(spec)
+    full.set_prop_tracking(False)
+    out, hop, _ = full.propagate(ms, cfg, want_results=True)
+    full.close()
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        e = gsx.Engine(1)
+        params(e)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.synthesize_state(spec)  # (every pair present and connected: floodsub without credits reads nothing else)
+        e.set_prop_tracking(False)
+        engines.append(e)
+        del sh
+    res = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp).propagate(ms, cfg),
+                          [(e,) for e in engines])
+    tot, want = res[0][1], out.as_dict()
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries"):
+        assert tot[k] == want[k], k
+    for k, e in enumerate(engines):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        h, _ = e.prop_results(len(ms))
+        assert np.array_equal(h, hop[:, lo:hi]), (k, np.argwhere(h != hop[:, lo:hi])[:5])
+        e.close()
+    reached = hop != 0xFF
+    assert out.deliveries == int(reached.sum()) - len(ms) and reached.mean() > 0.999
     for k in range(2):
         dist = _bfs(ov.row_ptr, ov.col.astype(np.int64), int(ms["source"][k]))
         r = dist >= 0

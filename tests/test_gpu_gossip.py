@@ -9,6 +9,7 @@ import pytest
 import gossip_cases as gc
 import gsx
 import oracle as orc
+import promise_cases as pc
 from gsx import abi
 
 pytestmark = pytest.mark.gpu
@@ -38,10 +39,54 @@ def _same(g, w):
     dict(exchange_from=5, ticks=10),          # unanswered IHAVEs: broken promises, P7
     dict(invalid=0.3, ticks=6),               # recovered invalid messages: P4
     dict(T=1, n=500, d=8, msgs=70, ticks=6),  # two words per batch
-])
+    dict(max_ihave_length=9, ticks=6),        # every list truncated per target (Floyd subsets)
+    dict(max_ihave_length=40, msgs=30, ticks=8, invalid=0.2),  # lists cross MaxIHaveLength as the window fills
+    dict(prefill=3, ticks=6, exchange_from=2),  # 3 of 4 promise slots taken: the exchange's promises grow them
+], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill"])
 def test_gossip_exchange_matches_oracle(gpu_ok, kw):
     T = kw.get("T", 2)
     g = gc.exchange_run(gsx.Engine(T), **kw)
     w = gc.exchange_run(orc.Oracle(T), **kw)
     _same(g, w)
     assert sum(o["iwant_msgs"] for o in g[1]) > 0
+
+
+@pytest.mark.timeout(600)
+def test_gossip_exchange_1024_per_heartbeat(gpu_ok):
+    """1024 messages between heartbeats: the five-window gossip list holds up
+    to 5,120 ids > MaxIHaveLength 5,000, so lists are truncated per target and
+    the receivers ask from their subsets (done criterion of f1)."""
+    kw = dict(T=1, n=2000, d=8, msgs=1300, hops=4, ticks=7)
+    g = gc.exchange_run(gsx.Engine(1), **kw)
+    w = gc.exchange_run(orc.Oracle(1), **kw)
+    _same(g, w)
+    outs = g[1]
+    assert (g[2][-1]["ihave_len"] == 5000).sum() > 1000  # truncated lists went out (the snapshot of the last round)
+    assert outs[-1]["iwant_msgs"] > 0 and outs[-1]["gossip_delivered"] > 0
+
+
+@pytest.mark.parametrize("case", pc.load(), ids=lambda c: c["name"])
+def test_promise_kat_gpu(gpu_ok, case):
+    """gossip_tracer_test.go:12-97 through gsx_promise_* (tests/golden/promise_kat.json)."""
+    assert pc.run(gsx.Engine(1), case) == []
+
+
+def test_promise_slots_grow_gpu(gpu_ok):
+    """1000 promises on one pair (AddPromise never refuses): the engine's per-pair
+    slots double on demand; counts and GetBrokenPromises equal the oracle's."""
+    from gsx import synth
+
+    res = []
+    for be in (gsx.Engine(1), orc.Oracle(1)):
+        row_ptr, col = pc.star(3)
+        be.set_peer_params(synth.bench_peer_params())
+        be.load_overlay(row_ptr, col)
+        for k in range(1000):
+            be.promise_add(k % 2, [k, k + 1, k + 2], pc.T0 + k, seed=k)
+        a = be.promise_count()
+        cnt, tot = be.promise_broken(pc.T0 + 500)
+        for k in range(0, 1000, 7):
+            be.promise_fulfill(0, k)
+        be.promise_throttle(1)
+        res.append((a, cnt.tolist(), tot, be.promise_count()))
+    assert res[0] == res[1]

@@ -15,6 +15,8 @@
 using namespace pubsub;
 using Clk = std::chrono::steady_clock;
 
+static long app_calls = 0;  // AppSpecificScore closure calls (score.go:320: one per score(p))
+
 static double us_since(Clk::time_point t0, int n) {
     return std::chrono::duration<double, std::micro>(Clk::now() - t0).count() / n;
 }
@@ -23,7 +25,10 @@ int main(int argc, char** argv) {
     const int K = argc > 1 ? std::atoi(argv[1]) : 1000;  // connected peers of the router
     const int N = argc > 2 ? std::atoi(argv[2]) : 2000;  // calls per leg
     PeerScoreParams p;
-    p.AppSpecificScore = [](const std::string&) { return 0.0; };
+    p.AppSpecificScore = [](const std::string&) {
+        ++app_calls;
+        return 0.0;
+    };
     p.DecayInterval = Second;
     p.DecayToZero = 0.01;
     p.IPColocationFactorWeight = -10;
@@ -70,12 +75,14 @@ int main(int argc, char** argv) {
     for (int i = 0; i < N; ++i) ps.DeliverMessage(Message{"m" + std::to_string(i), "t", peers[i % K]});
     const double deliver = us_since(t0, N);
 
+    const long app0 = app_calls;
     t0 = Clk::now();
     for (int i = 0; i < N; ++i) {
         ps.DeliverMessage(Message{"x" + std::to_string(i), "t", peers[i % K]});
         sink += ps.Score(peers[(i * 7) % K]);
     }
     const double deliver_then_score = us_since(t0, N);
+    const double app_per_score = (double)(app_calls - app0) / N;
 
     t0 = Clk::now();
     for (int i = 0; i < N; ++i) {  // one RPC: AcceptFrom, then the message, then Publish to the mesh
@@ -96,8 +103,8 @@ int main(int argc, char** argv) {
     const double refresh = us_since(t0, R);
     std::printf(
         "{\"peers\": %d, \"calls_per_leg\": %d, \"score_unchanged_us\": %.3f, \"deliver_message_us\": %.3f, "
-        "\"deliver_then_score_us\": %.3f, \"rpc_accept_deliver_publish6_us\": %.3f, \"refresh_scores_us\": %.3f, "
-        "\"sink\": %g}\n",
-        K, N, score_cached, deliver, deliver_then_score, rpc, refresh, (double)sink);
+        "\"deliver_then_score_us\": %.3f, \"app_score_calls_per_score\": %.2f, "
+        "\"rpc_accept_deliver_publish6_us\": %.3f, \"refresh_scores_us\": %.3f, \"sink\": %g}\n",
+        K, N, score_cached, deliver, deliver_then_score, app_per_score, rpc, refresh, (double)sink);
     return 0;
 }
