@@ -11,6 +11,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -2731,8 +2732,19 @@ int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const st
 //             mcache.Shift.
 // state_only: the round's buffers and kernel state (e->hb) without
 // maintenance, gossip or the promise penalties (Join / Leave use it)
+static int dbg_sync_mask() {
+    static int m = -1;
+    if (m < 0) {
+        const char* s = getenv("GSX_DBG_SYNC");
+        m = s ? atoi(s) : 0;
+    }
+    return m;
+}
+#define DBG_SYNC(bit) \
+    if (dbg_sync_mask() & (bit)) HIPCHK(e, hipStreamSynchronize(e->stream))
 int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, bool state_only) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    DBG_SYNC(1);
     e->state_changed();
     if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
         return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
@@ -2945,6 +2957,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                  hipMemcpyHostToDevice, e->stream));
     }
     h.mc_digest = e->d_mc_digest;
+    DBG_SYNC(2);
     // the truncated IHAVE lists' rows (exchange on, a window longer than MaxIHaveLength)
     if (gx_on)
         if (int rc = gx_sub_prepare(e, max_ids, tw)) return rc;
@@ -2972,6 +2985,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         tb = t + 1;
         gsx::HbState ht = h;
         if (gx_on) ht.gsub = e->gsub_host[t];
+        DBG_SYNC(4);
         HIPCHK(e, gsx::launch_hb_gossip(ds, ht, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t],
                                         max_ids[t] ? tw[t] : 0, e->max_deg, e->stream));
     }
@@ -3117,8 +3131,13 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     }
     e->mc.emplace_front();
     // the recovered copies: one batch per message set, Put into the new window 0
+    // in ascending set serial (the sets' creation order: gsx.h)
     const size_t N = e->n_nodes;
-    for (size_t i = 0; i < gx_sets.size(); ++i) {
+    std::vector<size_t> by_serial(gx_sets.size());
+    for (size_t i = 0; i < by_serial.size(); ++i) by_serial[i] = i;
+    std::sort(by_serial.begin(), by_serial.end(),
+              [&](size_t a, size_t b) { return gx_sets[a]->serial < gx_sets[b]->serial; });
+    for (size_t i : by_serial) {
         gsx_engine::MsgSet* ms = gx_sets[i];
         if (!got[i]) {
             seen_release(e, gx_x[i], (size_t)ms->n_words * N + 2 * N);

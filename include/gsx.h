@@ -621,7 +621,8 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      order: a first receipt is delivered (P2/P3 credit, or P4 when its
  *      validation rejects it), fulfils the node's promises for it
  *      (gossip_tracer.go:119-153) and is Put into its cache window 0 (after
- *      the Shift); a further copy is a duplicate.  Recovered messages are not
+ *      the Shift: one batch per message set, in the sets' creation order);
+ *      a further copy is a duplicate.  Recovered messages are not
  *      forwarded further within the round.  At the start of every heartbeat
  *      the IHAVE counters are cleared (:1566-1576) and promises that expired
  *      before now are broken: AddPenalty(peer, count) (:1578-1583, P7).

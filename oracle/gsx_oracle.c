@@ -2144,7 +2144,20 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             }
         }
     }
-    /* the recovered copies: one batch per message set, Put after the Shift */
+    /* the recovered copies: one batch per message set, Put after the Shift in
+     * ascending set serial (the sets' creation order, gsx.h) */
+    for (size_t a = 1; a < nr; a++)
+        for (size_t b = a; b > 0 && rs[b - 1]->serial > rs[b]->serial; b--) {
+            orc_msgset* ts = rs[b];
+            rs[b] = rs[b - 1];
+            rs[b - 1] = ts;
+            uint8_t* th = rh[b];
+            rh[b] = rh[b - 1];
+            rh[b - 1] = th;
+            uint32_t tt = rt[b];
+            rt[b] = rt[b - 1];
+            rt[b - 1] = tt;
+        }
     *rec_out = (orc_mc_batch*)calloc(nr ? nr : 1, sizeof(orc_mc_batch));
     *n_rec = nr;
     for (size_t x = 0; x < nr; x++) {
