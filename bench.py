@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "go-libp2p-pubsub_amd"))
 
 import gsx  # noqa: E402
 from gsx import abi, synth  # noqa: E402
+from gsx import engine as gsx_engine_mod  # noqa: E402
 from gsx import shard as shard_mod  # noqa: E402
 
 METRIC = "peer-topic score updates/s + msg deliveries/s @1M peers, 1-8 GPUs, %HBM BW"
@@ -324,7 +325,8 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     e = prop_engine(n, int(rl[rank]), int(rl[rank + 1]), args.degree, synth.SEED + 1, local, th,
                     (rank, world) if world > 1 else None)
     cfg = prop_config(args, n)
-    M = args.prop_msgs
+    M = args.shard_msgs  # 64-message batches
+    steps = 4 * args.prop_steps
     runner = None
     if dist is not None:
         runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
@@ -344,7 +346,7 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    res = [once(1 + b) for b in range(args.prop_steps)]
+    res = [once(1 + b) for b in range(steps)]
     torch.cuda.synchronize(dev)
     el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     dl = sum(r[0][1]["deliveries"] for r in res)
@@ -356,7 +358,7 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
         "value": dl / el,
         "peers": n,
         "messages_per_batch": M,
-        "ms_per_batch": el / args.prop_steps * 1e3,
+        "ms_per_batch": el / steps * 1e3,
         "deliveries_per_batch": tot["deliveries"],
         "duplicates_per_batch": tot["duplicates"],
         "hops": tot["hops"],
@@ -366,11 +368,11 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     if world == 1:
         out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
     else:
-        out["exchange"] = {"compacted": runner.compact, "bytes_sent_per_batch_rank": runner.sent_bytes / (args.prop_steps + 1),
+        out["exchange"] = {"compacted": runner.compact, "bytes_sent_per_batch_rank": runner.sent_bytes / (steps + 1),
                            "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8,
-                           "hops_per_batch": runner.hops_run / (args.prop_steps + 1),
+                           "hops_per_batch": runner.hops_run / (steps + 1),
                            "host_syncs_per_hop": runner.host_syncs / max(runner.hops_run, 1),
-                           "ms_per_hop": el / max(runner.hops_run * args.prop_steps / (args.prop_steps + 1), 1) * 1e3}
+                           "ms_per_hop": el / max(runner.hops_run * steps / (steps + 1), 1) * 1e3}
     return out
 
 
@@ -550,10 +552,13 @@ def main():
     ap.add_argument("--prop-msgs", type=int, default=1024,
                     help="messages per propagation batch (0: skip); 1024 = 16 words, one 128-B line per frontier row")
     ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
+    ap.add_argument("--shard-msgs", type=int, default=64, help="messages per batch of the cfg4 range-sharded leg")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
     ap.add_argument("--hb-msgs", type=int, default=256, help="gossipsub messages propagated before every heartbeat")
+    ap.add_argument("--no-hb-exchange", dest="hb_exchange", action="store_false",
+                    help="heartbeats without the gossip exchange (IHAVEs emitted, not handled)")
     ap.add_argument("--hb-settle", type=int, default=8,
                     help="untimed heartbeat rounds before the timed ones (the synthesized meshes rebalance)")
     ap.add_argument("--adv-peers", type=int, default=4_000_000, help="cfg5 adversarial overlay (0: skip)")
@@ -653,6 +658,9 @@ def main():
         th_hb = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                                accept_px_threshold=0, opportunistic_graft_threshold=5)
         e.set_thresholds(th_hb)
+        # the reference's HandleRPC always runs handleIHave / handleIWant
+        # (gossipsub.go:596-613): the gossip exchange (D) is part of the round
+        e.set_gossipsub_params(gsx_engine_mod.default_gossipsub_params(gossip_exchange=1 if args.hb_exchange else 0))
         tick = 58 - args.hb_settle
         hb_cfg = prop_config(args, n)
         rounds, settle = [], []
@@ -696,6 +704,10 @@ def main():
             "ms_per_round": tot_ms / len(rounds),
             "rounds": len(rounds),
             "messages_between_rounds": args.hb_msgs,
+            "gossip_exchange": bool(args.hb_exchange),
+            "iwant_msgs_per_round": mean([r["iwant_msgs"] for r in rounds]),
+            "iwant_ids_per_round": mean([r["iwant_ids"] for r in rounds]),
+            "gossip_delivered_per_round": mean([r["gossip_delivered"] for r in rounds]),
             "steady_ms_per_round": steady_ms,
             "active_ms_per_round": active_ms,
             "roofline_steady": roof(steady_ms),

@@ -231,7 +231,9 @@ struct PropState {
     uint32_t flast_every;  // k_prop_hop_fast keeps flast at every hop (stepped calls), else at max_hops only
 };
 
-hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st);
+// pins_only: the fwd bytes stand (a RESCORE count kept them), update the
+// pins / compacted senders of the listed changes only
+hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only = false);
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
 hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, uint64_t* send,
@@ -245,7 +247,8 @@ hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64
                                uint64_t* halo_occ, uint32_t h, hipStream_t st);
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
-hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st);
+hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, bool rescore, const DevPeerParams& pp,
+                             hipStream_t st);
 // gray_only: count the sends on pairs whose receiver graylists the sender
 // (STAT_GRAY) and nothing else (per-hop accounting); else the late accounting.
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, bool gray_only, hipStream_t st);

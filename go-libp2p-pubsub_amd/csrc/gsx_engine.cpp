@@ -157,6 +157,7 @@ struct gsx_engine {
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
     int64_t* d_prom_e = nullptr;
     uint32_t prom_slots = 0;  // promise slots per pair (grown while every pair keeps one free before an exchange)
+    bool gx_clean = false;    // IHAVE bits and counters all zero (the exchange clears what it reads)
     // the truncated IHAVE lists of a round (GxSub per topic): rows for at most
     // tgt_bound targets of tw words each
     struct SubPool {
@@ -252,6 +253,8 @@ struct gsx_engine {
             uint64_t flag_gen = 0, score_gen = 0, mem_gen = 0;
             double publish_threshold = 0, graylist_threshold = 0;
         } fwd_key;
+        bool fold_chg = false;  // the last call's fold listed fwd changes for the next call's pins
+        bool flast_dirty = true;  // flast may hold a hop-tagged count of an earlier call (cleared before the next)
         // compacted shard exchange: the dense halo the received entries are
         // scattered into, the slots filled last hop, per-destination counts
         uint64_t* halo = nullptr;
@@ -2072,9 +2075,14 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
     HIPCHK(e, hipMemsetAsync(P.touch, 0, 16 * ((N + 63) / 64), e->stream));  // both buffers (k_prop_mark clears them after)
     if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
+    // corr: the per-hop accounting adds to it; the late one writes every
+    // pair it reads (k_prop_dups -> k_prop_count under the reverse pair's SEND bit)
+    if (!ps.late) HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
     HIPCHK(e, hipMemsetAsync(P.fcnt, 0, 4 * std::max<size_t>(E, 1), e->stream));
-    HIPCHK(e, hipMemsetAsync(P.flast, 0, 8 * std::max<size_t>(E, 1), e->stream));
+    if (P.flast_dirty) {  // only hops that may stop a call early write flast (k_prop_hop_fast: the max_hops cut)
+        HIPCHK(e, hipMemsetAsync(P.flast, 0, 8 * std::max<size_t>(E, 1), e->stream));
+        P.flast_dirty = false;
+    }
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
     // fwd / pin (k_prop_fwd, k_prop_pin) read the router config, the pair and
@@ -2107,6 +2115,12 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
                           K.publish_threshold == e->th.publish_threshold &&
                           K.graylist_threshold == e->th.graylist_threshold && K.mem_gen == e->mem_gen &&
                           (!need_score || K.score_gen == e->score_gen);
+    if (fwd_same && P.fold_chg) {  // the last call's fold kept the bytes: its listed changes reach the pins
+        gsx::PropState pf = ps;
+        pf.inc = 1u;
+        HIPCHK(e, gsx::launch_prop_fwd(pf, ds, e->stream, true));
+    }
+    P.fold_chg = false;
     if (!fwd_same) {
         HIPCHK(e, hipMemsetAsync(P.gray_pairs, 0, 8, e->stream));
         // the last call's fwd bytes, pins and compacted senders stand: update
@@ -2194,19 +2208,36 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     std::memset(out, 0, sizeof(*out));
     P.active = false;
     if (ps.n_msgs == 0) return GSX_OK;
+    {  // the lean hop kernels write flast only at the max_hops cut (or every hop when stepped)
+        static const bool general = getenv("GSX_HOP_GENERAL") != nullptr;
+        const bool lean = ps.late && !ps.sharded && !ps.sel && !ps.from_mask && !general;
+        if (!lean || ps.flast_every || P.h >= ps.max_hops) P.flast_dirty = true;
+    }
     if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, false, e->stream));
     // per-hop accounting counts duplicates on arrival; the copies graylisting
     // receivers drop from local senders are counted here (the kernels return at
     // once when no pair is gated)
     else if (ps.gate) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, true, e->stream));
     const bool fold_now = ps.credit && P.cfg.credit_scores != GSX_CREDIT_DEFER;
-    if (ps.credit || ps.late) HIPCHK(e, gsx::launch_prop_count(ps, dev_state(e), fold_now, e->stream));
+    // the folded pairs are re-scored in the fold when every other score is
+    // exact (gossipsub calls start from exact scores) and the fwd bytes match
+    // this call's settings (unsharded, incremental fwd state)
+    const bool rescore = fold_now && e->scores_valid && e->pending.empty() && !e->sharded() && P.fwd_key.valid &&
+                         P.fwd_key.score_gen == e->score_gen && P.cfg.router == GSX_ROUTER_GOSSIPSUB;
+    if (ps.credit || ps.late)
+        HIPCHK(e, gsx::launch_prop_count(ps, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
     if (ps.credit) {
         // GSX_CREDIT_NOW: k_prop_count folded this call's counts (and any
         // pending ones of the topic) and left the pending counts empty
         P.credit_pending = !fold_now;
         P.credit_topic = ps.topic;
-        if (fold_now) {
+        if (rescore) {  // every score exact again, the fwd bytes with them
+            ++e->score_writes;
+            e->scores_exact();
+            ++e->score_gen;
+            P.fwd_key.score_gen = e->score_gen;
+            P.fold_chg = true;
+        } else if (fold_now) {
             e->invalidate_scores();
             ++e->score_gen;
         }
@@ -2647,6 +2678,7 @@ int gx_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_gsubs, std::max<size_t>(e->T, 1))))
         return rc;
     e->prom_slots = S;
+    e->gx_clean = false;
     HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * S, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
@@ -2762,8 +2794,10 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         // clearIHaveCounters (:1566-1576); applyIwantPenalties (:1578-1583):
         // promises expired before now are broken, AddPenalty (P7) on their pairs
         const size_t E = std::max<size_t>(e->E, 1);
-        HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
+        if (!e->gx_clean) {
+            HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
+            HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
+        }
         pen_mask = e->d_dirty + 3 * e->E;
         HIPCHK(e, hipMemsetAsync(pen_mask, 0, E, e->stream));
         gsx::HbState hp{};
@@ -2861,8 +2895,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.prom_e = e->d_prom_e;
         h.prom_slots = e->prom_slots;
         h.gsubs = e->d_gsubs;
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
+        if (!e->gx_clean) HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32, e->stream));
+        e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
     }
     if (e->gp.do_px) {  // peer exchange on the round's PRUNEs (gsx.h; heartbeats and Join / Leave rounds)
         if (e->sharded()) return fail(e, GSX_ESTATE, "peer exchange (do_px) runs on unsharded engines only");
@@ -3158,6 +3193,9 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                                          ms->d_dg + (size_t)ms->n_words * 64, b.d_dig, b.d_cnt, e->stream));
         e->mc.front().push_back(std::move(b));
     }
+    // the exchange cleared the bits and counters it read; a round without
+    // gossip set none (the counters were cleared at its start)
+    if (e->d_prom_e) e->gx_clean = gx_run || (e->gp.gossip_exchange && !e->have_gossip);
     const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] > 0;
     for (auto* ms : gx_sets) {
         if (merged) ms->full_ok = false;  // the receipts were merged into their seen rows

@@ -128,6 +128,65 @@ __global__ __launch_bounds__(256) void k_gx_full(const uint64_t* __restrict__ al
     }
 }
 
+// handleIWant at v and the receipt at u of what v sends (pass 2 of
+// k_gx_exchange): the kk ids u asked v for (selection sampling again, the same
+// draws), each still in v's cache delivered / rejected / counted duplicate.
+__device__ __forceinline__ void gx_receive(const DevState& s, const HbState& h, uint32_t u, int64_t r0, int64_t r1,
+                                           uint64_t q, uint32_t r, uint64_t tall, uint32_t kk, uint64_t& served,
+                                           uint64_t& delivered, uint64_t& rejected, uint64_t& dups) {
+    const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
+    const uint32_t v = (uint32_t)h.col[q];
+    const DevGossipParams& gp = h.gp;
+    const uint32_t S = h.prom_slots;
+    uint32_t n = 0;  // |iwant| again (the selection depends on it)
+    gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
+        ++n;
+        return true;
+    });
+    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+    uint32_t i = 0, sel = 0;
+    gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
+        bool take = true;
+        if (kk < n) {
+            take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
+            ++i;
+            if (!take) return true;
+        }
+        ++sel;
+        const GxBatch& b = h.gx[gi];
+        // no longer in v's cache; or GetForPeer's count (1: every (peer,
+        // message) is asked at most once per answer it can receive) above
+        // GossipRetransmission
+        if (!b.avail || gp.retransmission < 1) return sel < kk || kk == n;
+        ++served;
+        const uint32_t W = b.n_words, t = b.topic, val = b.val[k];
+        uint64_t* xw = b.x + (size_t)u * W + k / 64;
+        const uint64_t bit = 1ull << (k % 64);
+        if (*xw & bit) {  // DuplicateMessage
+            ++dups;
+            if (val == VAL_ACCEPT) ev_mesh(s, (uint64_t)q, t);
+            else if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+        } else {
+            *xw |= bit;
+            // fulfillPromise (:119-126): every promise of u for this message
+            const uint64_t handle = ((uint64_t)b.serial << 32) | k;
+            for (int64_t p = r0; p < r1; ++p)
+                for (uint32_t z = 0; z < S; ++z)
+                    if (h.prom_e[(size_t)p * S + z] != 0 && h.prom_h[(size_t)p * S + z] == handle)
+                        h.prom_e[(size_t)p * S + z] = 0;
+            if (val == VAL_ACCEPT) {
+                ++delivered;
+                ev_first(s, (uint64_t)q, t);
+                *b.got = 1;
+            } else {
+                ++rejected;
+                if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+            }
+        }
+        return sel < kk || kk == n;
+    });
+}
+
 __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
     const DevGossipParams& gp = h.gp;
     const uint32_t S = h.prom_slots;
@@ -229,63 +288,20 @@ __global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
             }
             occ = used > occ ? used : occ;
         }
-        // ---- pass 2: v answers (handleIWant :681-716), u receives, senders ascending
+        // ---- pass 2: v answers (handleIWant :681-716), u receives, senders ascending;
+        // the pair's IHAVE bits and counters are cleared once read (clearIHaveCounters
+        // :1566-1576 then finds them zero: the host skips its memsets)
         for (int64_t q = r0; q < r1; ++q) {
+            const uint64_t tall = h.ihave_bits[q];
+            if (!tall) continue;
             const uint32_t kk = h.gx_req[q];
-            if (!kk) continue;
-            h.gx_req[q] = 0;
+            if (kk) h.gx_req[q] = 0;
             const uint32_t r = h.rev[q];
-            if (s.score[r] < h.gossip_threshold) continue;  // v ignores u's IWANT
-            if (!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) continue;  // AcceptFrom at u
-            const uint32_t v = (uint32_t)h.col[q];
-            const uint64_t tb = h.ihave_bits[q] & (h.sub ? h.sub[u] : ~0ull);
-            uint32_t n = 0;  // |iwant| again (the selection depends on it)
-            gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
-                ++n;
-                return true;
-            });
-            Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
-            uint32_t i = 0, sel = 0;
-            gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
-                bool take = true;
-                if (kk < n) {
-                    take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
-                    ++i;
-                    if (!take) return true;
-                }
-                ++sel;
-                const GxBatch& b = h.gx[gi];
-                // no longer in v's cache; or GetForPeer's count (1: every (peer,
-                // message) is asked at most once per answer it can receive) above
-                // GossipRetransmission
-                if (!b.avail || gp.retransmission < 1) return sel < kk || kk == n;
-                ++served;
-                const uint32_t W = b.n_words, t = b.topic, val = b.val[k];
-                uint64_t* xw = b.x + (size_t)u * W + k / 64;
-                const uint64_t bit = 1ull << (k % 64);
-                if (*xw & bit) {  // DuplicateMessage
-                    ++dups;
-                    if (val == VAL_ACCEPT) ev_mesh(s, (uint64_t)q, t);
-                    else if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
-                } else {
-                    *xw |= bit;
-                    // fulfillPromise (:119-126): every promise of u for this message
-                    const uint64_t handle = ((uint64_t)b.serial << 32) | k;
-                    for (int64_t p = r0; p < r1; ++p)
-                        for (uint32_t z = 0; z < S; ++z)
-                            if (h.prom_e[(size_t)p * S + z] != 0 && h.prom_h[(size_t)p * S + z] == handle)
-                                h.prom_e[(size_t)p * S + z] = 0;
-                    if (val == VAL_ACCEPT) {
-                        ++delivered;
-                        ev_first(s, (uint64_t)q, t);
-                        *b.got = 1;
-                    } else {
-                        ++rejected;
-                        if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
-                    }
-                }
-                return sel < kk || kk == n;
-            });
+            const bool answered = kk && !(s.score[r] < h.gossip_threshold) &&           // v ignores u's IWANT
+                                  ((h.eflags[q] & EDGE_DIRECT) || !(s.score[q] < h.graylist));  // AcceptFrom at u
+            if (answered) gx_receive(s, h, u, r0, r1, q, r, tall, kk, served, delivered, rejected, dups);
+            h.ihave_bits[q] = h.ihave_tr[q] = 0;
+            h.peerhave[q] = h.iasked[q] = 0;
         }
     }
     gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);

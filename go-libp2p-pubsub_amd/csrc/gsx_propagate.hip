@@ -39,38 +39,41 @@ namespace gsx {
 // gossipsub.go:583-594 -> pubsub.go:1014-1017: the payload is never pushed,
 // so no seen mark, no trace, no P2/P3/P4).  Floodsub and RandomSub accept all.
 // The score is the one of the call start, like the publishThreshold tests.
+__device__ __forceinline__ uint8_t fwd_byte(const PropState& ps, const DevState& s, uint64_t r) {
+    const uint8_t pf = s.pflags[r];
+    const uint8_t ef = ps.eflags[r];
+    uint8_t out = 0;
+    if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
+        topic_peer(ps.psub, r, ps.topic)) {  // in ps.topics[topic]
+        if (ps.router == ROUTER_FLOODSUB) {  // every topic peer (floodsub.go:81-90)
+            out = FWD_FORWARD | FWD_PUBLISH;
+        } else if (ps.router == ROUTER_RANDOMSUB) {  // FloodSub peers always, the rest by draw (randomsub.go:112-143)
+            out = (ef & EDGE_FLOODSUB) ? (FWD_FORWARD | FWD_PUBLISH) : FWD_RSUB_CAND;
+        } else {  // gossipsub
+            const bool direct = ef & EDGE_DIRECT;
+            // the score is read only where a threshold decides (floodsub peers, flood publish)
+            const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
+            const bool above = need_score && s.score[r] >= ps.publish_threshold;
+            bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
+            if (!fwd && ps.topic < s.n_topics)  // mesh peers, or the fanout when not joined (:977-999)
+                fwd = joined_node(ps.sub, ps.pair_obs[r], ps.topic)
+                          ? (s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH) != 0
+                          : ((ps.fanout[r] >> ps.topic) & 1) != 0;
+            const bool pub = ps.flood_publish ? (direct || above) : fwd;  // flood publish (:953-960)
+            out = (fwd ? FWD_FORWARD : 0) | (pub ? FWD_PUBLISH : 0);
+        }
+    }
+    // Score() of a peer without peerStats is 0 (score.go:247-256), never below the
+    // (non-positive) threshold; the score vector holds 0 for those pairs.
+    if (ps.gate && !(ef & EDGE_DIRECT) && s.score[r] < ps.graylist_threshold) out |= FWD_GIN;
+    return out;
+}
+
 __global__ __launch_bounds__(256) void k_prop_fwd(PropState ps, DevState s) {
     unsigned long long n_gray[1] = {0};
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < s.n_pairs; r += (uint64_t)gridDim.x * 256u) {
-        const uint8_t pf = s.pflags[r];
-        const uint8_t ef = ps.eflags[r];
-        uint8_t out = 0;
-        if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) &&
-            topic_peer(ps.psub, r, ps.topic)) {  // in ps.topics[topic]
-            if (ps.router == ROUTER_FLOODSUB) {  // every topic peer (floodsub.go:81-90)
-                out = FWD_FORWARD | FWD_PUBLISH;
-            } else if (ps.router == ROUTER_RANDOMSUB) {  // FloodSub peers always, the rest by draw (randomsub.go:112-143)
-                out = (ef & EDGE_FLOODSUB) ? (FWD_FORWARD | FWD_PUBLISH) : FWD_RSUB_CAND;
-            } else {  // gossipsub
-                const bool direct = ef & EDGE_DIRECT;
-                // the score is read only where a threshold decides (floodsub peers, flood publish)
-                const bool need_score = !direct && (!(ef & EDGE_GOSSIPSUB) || ps.flood_publish);
-                const bool above = need_score && s.score[r] >= ps.publish_threshold;
-                bool fwd = direct || (!(ef & EDGE_GOSSIPSUB) && above);  // direct + floodsub peers (:962-975)
-                if (!fwd && ps.topic < s.n_topics)  // mesh peers, or the fanout when not joined (:977-999)
-                    fwd = joined_node(ps.sub, ps.pair_obs[r], ps.topic)
-                              ? (s.rflags[flag_index(r, ps.topic, s.n_topics)] & REC_IN_MESH) != 0
-                              : ((ps.fanout[r] >> ps.topic) & 1) != 0;
-                const bool pub = ps.flood_publish ? (direct || above) : fwd;  // flood publish (:953-960)
-                out = (fwd ? FWD_FORWARD : 0) | (pub ? FWD_PUBLISH : 0);
-            }
-        }
-        // Score() of a peer without peerStats is 0 (score.go:247-256), never below the
-        // (non-positive) threshold; the score vector holds 0 for those pairs.
-        if (ps.gate && !(ef & EDGE_DIRECT) && s.score[r] < ps.graylist_threshold) {
-            out |= FWD_GIN;
-            ++n_gray[0];
-        }
+        const uint8_t out = fwd_byte(ps, s, r);
+        if (out & FWD_GIN) ++n_gray[0];
         if (ps.inc) {  // the pins of the last call stand but for the pairs whose byte changed
             if (ps.fwd[r] != out) {
                 const uint32_t k = atomicAdd(ps.nchg, 1u);
@@ -1207,9 +1210,14 @@ __device__ __forceinline__ void fold_pair(const PropState& ps, const DevState& s
 
 // Per receiver pair q = (u -> v): this call's first receipts from v (the hop
 // kernel's fcnt) and in-window duplicates join the pending counts; with FOLD
-// (GSX_CREDIT_NOW) they are folded into the record at once.
-template <bool FOLD>
-__global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
+// (GSX_CREDIT_NOW) they are folded into the record at once.  RESCORE (the
+// scores were exact when the call started, the last fwd pass used this
+// call's settings): a folded pair is re-scored here, its forwarding byte
+// recomputed and, when it changed, listed for the next call's pins — the only
+// scores and bytes the credits can change, so neither a full re-score nor a
+// k_prop_fwd pass is needed before the next call (or heartbeat).
+template <bool FOLD, bool RESCORE>
+__global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, DevPeerParams pp) {
     unsigned long long cnt[1] = {0};
     const bool fold_topic = FOLD && ps.topic < s.n_topics && s.tp[ps.topic].scored;
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -1224,8 +1232,12 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
         }
 #pragma unroll
         for (int i = 0; i < DU; ++i) {  // the sender pair's sends (k_prop_dups), one gather per pair
+            const uint64_t q = q0 + i * stride;
             const bool local = ra[i] != NO_PAIR && !(ra[i] & HALO);
-            ca[i] = (local && ps.credit) ? ps.corr[ra[i]] : 0;
+            // late accounting: k_prop_dups wrote corr of the senders whose byte has SEND
+            // (rfwd: the reverse pair's byte as this call's pins read it), nothing else
+            const bool wrote = !ps.late || (q < ps.n_pairs && (ps.rfwd[q] & FWD_SEND));
+            ca[i] = (local && ps.credit && wrote) ? ps.corr[ra[i]] : 0;
         }
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
@@ -1250,7 +1262,20 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s) {
                     }
                     uint32_t k4 = 0;
                     if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
-                    if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) fold_pair(ps, s, q, first, dup, k4);
+                    if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) {
+                        fold_pair(ps, s, q, first, dup, k4);
+                        if (RESCORE) {
+                            s.score[q] = eval_pair(s, pp, q);
+                            const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
+                            if (nb != ob) {
+                                ps.fwd[q] = nb;
+                                const uint32_t k = atomicAdd(ps.nchg, 1u);
+                                if (k < ps.chg_cap) ps.chg[k] = (uint32_t)q;
+                                if ((nb ^ ob) & FWD_GIN)
+                                    atomicAdd(ps.gray_pairs, (nb & FWD_GIN) ? 1ull : ~0ull);  // (+1 / -1)
+                            }
+                        }
+                    }
                 } else {
                     ps.firstcnt[q] = first;
                     ps.dupcnt[q] = dup;
@@ -1417,9 +1442,10 @@ hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStre
     hipLaunchKernelGGL(k_prop_hops_export, dim3(nblk(ps.n_nodes, 256), ps.n_words), dim3(256), 0, st, ps, hop_mn);
     return hipGetLastError();
 }
-hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st) {
+hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only) {
     if (s.n_pairs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
+    if (!pins_only)
+        hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
     hipLaunchKernelGGL(k_prop_pin, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
     if (ps.n_nodes) {
         hipLaunchKernelGGL(k_prop_compact, dim3(nblk(ps.n_nodes, 256)), dim3(256), 0, st, ps);
@@ -1552,11 +1578,13 @@ hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt,
     else hipLaunchKernelGGL(k_prop_dups<false>, gd, dim3(256), 0, st, ps, h_run, vcnt);
     return hipGetLastError();
 }
-hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, hipStream_t st) {
+hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, bool rescore, const DevPeerParams& pp,
+                             hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
     const dim3 g(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), b(256);
-    if (fold) hipLaunchKernelGGL(k_prop_count<true>, g, b, 0, st, ps, s);
-    else hipLaunchKernelGGL(k_prop_count<false>, g, b, 0, st, ps, s);
+    if (fold && rescore) hipLaunchKernelGGL((k_prop_count<true, true>), g, b, 0, st, ps, s, pp);
+    else if (fold) hipLaunchKernelGGL((k_prop_count<true, false>), g, b, 0, st, ps, s, pp);
+    else hipLaunchKernelGGL((k_prop_count<false, false>), g, b, 0, st, ps, s, pp);
     return hipGetLastError();
 }
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* first, uint32_t* dup,

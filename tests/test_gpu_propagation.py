@@ -282,6 +282,37 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
 
 
+@pytest.mark.parametrize("flood_publish", [0, 1])
+def test_credit_threshold_crossings_between_calls(gpu_ok, flood_publish):
+    """Consecutive gossipsub calls whose own credits move scores across the
+    graylist and publish thresholds (invalid messages: P4): the fold re-scores
+    the credited pairs and keeps their forwarding bytes, so the next call runs
+    without a full re-score or k_prop_fwd pass (gsx_propagate.hip
+    k_prop_count<.., RESCORE>); every call must match the oracle."""
+    n, T = 1500, 1
+    ov = pc.overlay(n, 6, seed=47, mix_protocols=True, direct_frac=0.02)
+    eng, ref = gsx.Engine(T), orc.Oracle(T)
+    for be in (eng, ref):
+        pc.setup(be, ov, T, 47, disconnect_frac=0.01)
+    few = np.random.default_rng(47).choice(n, 25, replace=False)  # a few publishers: their P4 piles up fast
+    s0 = eng.scores()
+    for k in range(10):
+        ms = pc.messages(n, 70 if k % 2 else 40, seed=300 + k, invalid=0.4)
+        ms["source"] = few[np.arange(len(ms)) % len(few)]
+        cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, flood_publish=flood_publish, latency_ms=10, seed=9 + k)
+        cfg.now_ns = pc.T0 + (2 + k) * pc.S
+        res = [be.propagate(ms, cfg, want_results=True) for be in (eng, ref)]
+        (go, gh, gf), (wo, wh, wf) = res
+        assert go.as_dict() == wo.as_dict(), k
+        assert np.array_equal(gh, wh) and np.array_equal(gf, wf), k
+        assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), k
+    gs, ws = eng.export_state(), ref.export_state()
+    for f in abi.STATE_FIELDS:
+        assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
+    s1 = eng.scores()
+    assert ((s1 < -300) != (s0 < -300)).sum() > 10  # the credits graylisted senders between calls
+
+
 @pytest.mark.parametrize("router", [abi.GSX_ROUTER_RANDOMSUB, abi.GSX_ROUTER_GOSSIPSUB])
 def test_hub_above_256_peers_matches_oracle(gpu_ok, router):
     """A node with ~600 peers: RandomSub stages its candidate lists over the
