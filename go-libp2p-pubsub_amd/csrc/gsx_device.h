@@ -404,6 +404,7 @@ struct HbState {
     int64_t* lastpub;      // [node][topic] (gs.lastpub; 0 = none)
     uint32_t fan_mode;     // k_hb_gossip: 0 the joined units' mesh gossip, 1 the fanout units' (:1553)
     uint32_t* mscratch;    // [pair]: candidate lists of the membership kernels (each row one lane's)
+    uint32_t* pxbase;      // [pair]: k_hb_px's per-topic candidate list over each pruning node's row
     const uint32_t* pair_obs;  // [pair]: its owner (local node; set with sub)
     // peer exchange on PRUNE (do_px; null otherwise)
     uint8_t* pxno;         // [pair]: bit 0 = (A) pruned it without PX, bit 1 = its (B) answers go without PX

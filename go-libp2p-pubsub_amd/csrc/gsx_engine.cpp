@@ -182,7 +182,7 @@ struct gsx_engine {
     // peer exchange on PRUNE (do_px): per-pair noPX bits, the candidate-list
     // scratch when membership is off, the connection-candidate log
     uint8_t* d_pxno = nullptr;
-    uint32_t *d_pxscratch = nullptr, *d_pxlog = nullptr;
+    uint32_t *d_pxscratch = nullptr, *d_pxlog = nullptr, *d_pxbase = nullptr;
     size_t px_cap = 0, pxlog_alloc = 0;
     uint64_t px_last = 0;  // the last round's connection candidates
     std::vector<uint64_t> h_sub;  // host copy of the joined topics per node
@@ -566,11 +566,11 @@ void free_state(gsx_engine* e) {
         e->mlist_cap = 0;
         e->members_on = false;
         e->h_sub.clear();
-        void* pxp[] = {e->d_pxno, e->d_pxscratch, e->d_pxlog};
+        void* pxp[] = {e->d_pxno, e->d_pxscratch, e->d_pxlog, e->d_pxbase};
         for (void* x : pxp)
             if (x) (void)hipFree(x);
         e->d_pxno = nullptr;
-        e->d_pxscratch = e->d_pxlog = nullptr;
+        e->d_pxscratch = e->d_pxlog = e->d_pxbase = nullptr;
         e->pxlog_alloc = 0;
         e->px_last = 0;
     }
@@ -2906,6 +2906,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
             if (int rc = dalloc(e, &e->d_pxno, E)) return rc;
         if (!e->members_on && !e->d_pxscratch)
             if (int rc = dalloc(e, &e->d_pxscratch, E)) return rc;
+        if (!e->d_pxbase)
+            if (int rc = dalloc(e, &e->d_pxbase, E)) return rc;
         if (e->px_cap > e->pxlog_alloc) {
             if (e->d_pxlog) (void)hipFree(e->d_pxlog);
             e->d_pxlog = nullptr;
@@ -2920,6 +2922,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.accept_px = e->th.accept_px_threshold;
         h.col = e->d_col;
         if (!e->members_on) h.mscratch = e->d_pxscratch;
+        h.pxbase = e->d_pxbase;
     }
     const size_t E8 = 8 * (e->E ? e->E : 1);
     // Unsharded, (B) and (C) clear the control words, answers and marks they

@@ -1665,11 +1665,12 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
 // ---- peer exchange on PRUNE (gossipsub.go:811-843, 861-910, 1814-1850) ----------
 
 // One lane per pruning node u (kind 0: the (A) PRUNEs in ctl_prune, before
-// (B) reads them; kind 1: the (B) answers in resp, before (C) reads them),
-// its pairs ascending, each pruned topic ascending.  makePrune's
-// getPeers(topic, PrunePeers, xp != p && score(xp) >= 0) is staged in
-// mscratch over u's own row, shuffled with the draws of gsx.h and truncated;
-// then the receiver p's side: AcceptFrom, the joined-topic check of
+// (B) reads them; kind 1: the (B) answers in resp, before (C) reads them).
+// makePrune's getPeers(topic, PrunePeers, xp != p && score(xp) >= 0): per
+// pruned topic t of u, the candidates of u's row (ascending peer) are staged
+// once in pxbase over u's own row range; every PRUNE of t copies them without
+// its own peer into mscratch, shuffles with the draws of gsx.h and truncates.
+// Then the receiver p's side: AcceptFrom, the joined-topic check of
 // handlePrune, AcceptPXThreshold on its score of u, and pxConnect's "not
 // connected" filter (p's row is sorted by peer: a binary search).  The scores
 // are the cache as the receiving step reads it (gsx.h).  PX is off by
@@ -1680,30 +1681,37 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
     const uint8_t nobit = kind ? 2 : 1;
     for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        for (int64_t r = r0; r < r1; ++r) {  // r = (u -> p)
-            uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
-            if (!bits) continue;
-            const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (unsharded: never HALO)
-            // (B) never reads nor clears the words of a pair its receiver does not
-            // track: cleared here, so each round's (A) bits start from zeros
-            if (q == NO_PAIR && !kind && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
-            if ((h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
-            const uint32_t p = (uint32_t)h.col[r];
-            bool heard = q != NO_PAIR;
-            double rs = 0.0;
-            if (heard) {
-                rs = s.score[q];
-                if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) heard = false;  // AcceptFrom drops the RPC
+        uint64_t any = 0;  // the topics some PRUNE of u carries a list for
+        for (int64_t r = r0; r < r1; ++r) {
+            const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+            if (!bits || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
+            any |= bits;
+        }
+        for (; any; any &= any - 1) {
+            const uint32_t t = (uint32_t)__builtin_ctzll(any);
+            int nb = 0;
+            for (int64_t x = r0; x < r1; ++x) {  // getPeers' candidates of t, ascending peer
+                if ((s.pflags[x] & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED)) continue;
+                if (!topic_peer(h.psub, (uint64_t)x, t) || !(h.eflags[x] & EDGE_GOSSIPSUB)) continue;
+                if (!(s.score[x] >= 0.0)) continue;
+                h.pxbase[r0 + nb++] = (uint32_t)(x - r0);
             }
-            for (; bits; bits &= bits - 1) {
-                const uint32_t t = (uint32_t)__builtin_ctzll(bits);
+            for (int64_t r = r0; r < r1; ++r) {  // r = (u -> p), a PRUNE of t with PX
+                const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+                if (!((bits >> t) & 1) || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
+                const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (unsharded: never HALO)
+                const uint32_t p = (uint32_t)h.col[r];
+                bool heard = q != NO_PAIR;
+                double rs = 0.0;
+                if (heard) {
+                    rs = s.score[q];
+                    if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) heard = false;  // AcceptFrom drops the RPC
+                }
                 int n = 0;
-                for (int64_t x = r0; x < r1; ++x) {  // getPeers' candidates, ascending peer
-                    if (x == r) continue;
-                    if ((s.pflags[x] & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED)) continue;
-                    if (!topic_peer(h.psub, (uint64_t)x, t) || !(h.eflags[x] & EDGE_GOSSIPSUB)) continue;
-                    if (!(s.score[x] >= 0.0)) continue;
-                    h.mscratch[r0 + n++] = (uint32_t)(x - r0);
+                const uint32_t self = (uint32_t)(r - r0);
+                for (int i = 0; i < nb; ++i) {
+                    const uint32_t x = h.pxbase[r0 + i];
+                    if (x != self) h.mscratch[r0 + n++] = x;  // xp != p
                 }
                 Rng g{h.seed, TAG_PX, ((uint64_t)(h.node_lo + u) << 32) | (uint64_t)(h.node_lo + p),
                       (h.tick << 32) | ((uint64_t)t << 24) | ((uint64_t)kind << 23), 0};
@@ -1742,6 +1750,11 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
                 }
             }
         }
+        // (B) never reads nor clears the words of a pair its receiver does not
+        // track: cleared here, so each round's (A) bits start from zeros
+        if (!kind && !h.keep_ctl)
+            for (int64_t r = r0; r < r1; ++r)
+                if (h.rev[r] == NO_PAIR && h.ctl_prune[r]) h.ctl_graft[r] = h.ctl_prune[r] = 0;
     }
     flush_count(h.stats, HB_PX_PRUNES, lists);
     flush_count(h.stats, HB_PX_PEERS, listed);

@@ -18,6 +18,7 @@
 """
 import numpy as np
 import pytest
+import torch  # noqa: F401  (initialised before any engine: the shard test's threads use its streams)
 
 import adversarial_cases as ac
 import gsx
@@ -228,8 +229,6 @@ def test_cfg4_10m_range_sharded_matches_single_engine(gpu_ok):
     threads on one GPU, BASELINE's 64-message floodsub batch.  The stitched
     arrival hops equal the unsharded engine's, the totals equal, and sampled
     messages' hops are BFS distances."""
-    import torch  # noqa: F401  (the shard threads' streams)
-
     from gsx import shard
 
     n, seed, world = 10_000_000, synth.SEED + 1, 2

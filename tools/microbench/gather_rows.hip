@@ -5,6 +5,9 @@
 //   N4  4 lanes per node, a 32-B chunk each, W = 16 (1024 messages)
 //   P1  lane per pair (pairs coalesced), W = 4, result per pair
 //   S1  N1 over the same overlay renumbered in BFS order (locality)
+//   W1  one-word rows (64-message batches): thread per node, LPN lanes per
+//       node splitting its pairs (k_prop_hop_fast1's shape), lane per pair;
+//       random and BFS order
 // Every variant ORs the gathered rows and writes one row per node (or pair),
 // so the loads stay live.  Half the pairs are "not in mesh" (pin = NONE).
 #include <hip/hip_runtime.h>
@@ -81,6 +84,33 @@ __global__ __launch_bounds__(256) void k_group(const int64_t* __restrict__ rp, c
         }
 #pragma unroll
         for (int i = 0; i < CW; ++i) nxt[(size_t)u * W + lc * CW + i] = acc[i];
+    }
+}
+
+// LPN lanes per node, each taking every LPN-th pair of the row; the lanes'
+// ORs are combined with shuffles (one-word rows: the pairs are split, not the row)
+template <int LPN, int U>
+__global__ __launch_bounds__(256) void k_split1(const int64_t* __restrict__ rp, const uint32_t* __restrict__ pin,
+                                               const uint64_t* __restrict__ front, uint64_t* __restrict__ nxt,
+                                               uint32_t n) {
+    const uint32_t lc = threadIdx.x % LPN;
+    for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t / LPN < n; t += gridDim.x * 256) {
+        const uint32_t u = t / LPN;
+        const int64_t q0 = rp[u], q1 = rp[u + 1];
+        uint64_t acc = 0;
+        for (int64_t qb = q0 + lc; qb < q1; qb += LPN * U) {
+            uint32_t p[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) p[j] = qb + j * LPN < q1 ? pin[qb + j * LPN] : NONE;
+            uint64_t c[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) c[j] = p[j] != NONE ? front[p[j]] : 0;
+#pragma unroll
+            for (int j = 0; j < U; ++j) acc |= c[j];
+        }
+#pragma unroll
+        for (int o = 1; o < LPN; o <<= 1) acc |= __shfl_xor(acc, o, LPN);
+        if (lc == 0) nxt[u] = acc;
     }
 }
 
@@ -189,7 +219,7 @@ int main(int argc, char** argv) {
     Overlay ov = connect_some(n, 6, 42);
     const uint64_t E = ov.rp[n];
     printf("n=%u E=%llu\n", n, (unsigned long long)E);
-    for (int order = 0; order < 1; ++order) {
+    for (int order = 0; order < 2; ++order) {
         Overlay o = order ? renumber_bfs(ov, n) : ov;
         std::vector<uint32_t> pin(E);
         uint64_t x = 7;
@@ -216,6 +246,13 @@ int main(int argc, char** argv) {
             printf("%s %-22s %8.1f us  %6.1f GB/s of row bytes (%d words)\n", order ? "bfs " : "rand", name, us,
                    gb / (us * 1e-6), W);
         };
+        report("node W1 U4", time_it([&] { k_node<1, 4><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 1);
+        report("node W1 U8", time_it([&] { k_node<1, 8><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 1);
+        report("split W1 lpn4 U2", time_it([&] { k_split1<4, 2><<<grid(4ull * n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 1);
+        report("split W1 lpn4 U1", time_it([&] { k_split1<4, 1><<<grid(4ull * n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 1);
+        report("split W1 lpn8 U1", time_it([&] { k_split1<8, 1><<<grid(8ull * n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 1);
+        report("pair W1", time_it([&] { k_pair<1><<<grid(E), B>>>(d_pin, d_front, d_nxt, E); }), 1);
+        if (!order) {  // (the BFS order only for one-word rows)
         report("node W4 U4", time_it([&] { k_node<4, 4><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 4);
         report("node W4 U8", time_it([&] { k_node<4, 8><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 4);
         report("node W4 U2", time_it([&] { k_node<4, 2><<<grid(n), B>>>(d_rp, d_pin, d_front, d_nxt, n); }), 4);
@@ -234,6 +271,7 @@ int main(int argc, char** argv) {
         }
         report("pair W4", time_it([&] { k_pair<4><<<grid(E), B>>>(d_pin, d_front, d_nxt, E); }), 4);
         report("pair W16", time_it([&] { k_pair<16><<<grid(E), B>>>(d_pin, d_front, d_nxt, E); }), 16);
+        }
         CHK(hipFree(d_rp));
         CHK(hipFree(d_pin));
         CHK(hipFree(d_front));
