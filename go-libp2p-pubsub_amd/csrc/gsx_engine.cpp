@@ -2503,12 +2503,24 @@ int gsx_prop_end(gsx_engine* e, gsx_prop_out* out) {
     return prop_end(e, out);
 }
 
+// Device memory on both sides: the copies stay ordered on the engine's
+// stream (a caller's stream via gsx_set_stream) and the call returns at once;
+// host memory: the call waits for them.
+bool on_device(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory: not a HIP allocation
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
 int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup) {
     if (!e) return GSX_EINVAL;
     if (!e->loaded || !e->prop.first) return fail(e, GSX_ESTATE, "no propagation yet");
     if (first) HIPCHK(e, hipMemcpyAsync(first, e->prop.first, 4 * e->E, hipMemcpyDefault, e->stream));
     if (dup) HIPCHK(e, hipMemcpyAsync(dup, e->prop.dup, 4 * e->E, hipMemcpyDefault, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if ((first && !on_device(first)) || (dup && !on_device(dup))) HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
 
@@ -2516,7 +2528,7 @@ int gsx_prop_pending_invalid(gsx_engine* e, uint32_t* inv) {
     if (!e || !inv) return GSX_EINVAL;
     if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
     HIPCHK(e, hipMemcpyAsync(inv, e->prop.inv, 4 * e->E, hipMemcpyDefault, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (!on_device(inv)) HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
 
@@ -2525,7 +2537,7 @@ int gsx_prop_replace_pending_invalid(gsx_engine* e, const uint32_t* inv) {
     if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
     HIPCHK(e, hipMemcpyAsync(e->prop.inv, inv, 4 * e->E, hipMemcpyDefault, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (!on_device(inv)) HIPCHK(e, hipStreamSynchronize(e->stream));
     e->prop.credit_pending = true;
     return GSX_OK;
 }
@@ -2545,7 +2557,7 @@ int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* 
     gsx::PropState ps = P.last;
     ps.topic = P.credit_pending ? P.credit_topic : P.cfg.topic;
     if (int rc = prop_fold(e, ps)) return rc;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (first && (!on_device(first) || !on_device(dup))) HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
 

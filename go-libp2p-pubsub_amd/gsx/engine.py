@@ -26,7 +26,7 @@ _CTYPES = {"<f8": C.c_double, "<i8": C.c_int64, "u1": C.c_uint8}
 def default_gossipsub_params(**kw) -> abi.GossipSubParams:
     """DefaultGossipSubParams (gossipsub.go:230-260, gsx_default_gossipsub_params) with overrides."""
     gp = abi.GossipSubParams()
-    rc = load_library().gsx_default_gossipsub_params(C.byref(gp))
+    rc = abi.load_library().gsx_default_gossipsub_params(C.byref(gp))
     if rc != 0:
         raise RuntimeError(f"gsx_default_gossipsub_params -> {rc}")
     for k, v in kw.items():

@@ -272,11 +272,34 @@ class RangeSharded:
 
 
 class MessageParallel:
-    """Every rank propagates its block of the messages over the full overlay."""
+    """Every rank propagates its block of the messages over the full overlay.
 
-    def __init__(self, engine, transport):
+    The engine runs on a torch stream of its own (set_stream), so its kernels,
+    the credit copies and the collective are ordered on one stream with no
+    host synchronisation between them.  epoch=False (default): each batch's
+    deferred P2/P3/P4 counts are summed over ranks and folded right away (the
+    single engine with GSX_CREDIT_NOW, batch by batch).  epoch=True: batches
+    only accumulate their counts on every rank; end_epoch() (before a
+    heartbeat) sums them with one all-reduce and folds them:
+    equal to one engine propagating the same batches with GSX_CREDIT_DEFER and
+    folding once."""
+
+    def __init__(self, engine, transport, epoch: bool = False):
         self.e = engine
         self.tp = transport
+        self.epoch = epoch
+        self.pending = False
+        self._stream = None
+        dev = getattr(transport, "device", None)
+        if hasattr(engine, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
+            torch = _torch()
+            self._stream = torch.cuda.Stream(device=dev)
+            engine.set_stream(self._stream.cuda_stream)
+
+    def _on_stream(self):
+        import contextlib
+
+        return _torch().cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
 
     def share(self, msgs):
         m = len(msgs)
@@ -284,30 +307,36 @@ class MessageParallel:
         return msgs[(m * r) // w : (m * (r + 1)) // w]
 
     def propagate(self, msgs, cfg: abi.PropConfig):
-        torch = _torch()
-        mine = self.share(msgs)
-        credit = cfg.credit_scores
-        c = abi.PropConfig()
-        C_fields = [f for f, _ in abi.PropConfig._fields_]
-        for f in C_fields:
-            setattr(c, f, getattr(cfg, f))
-        if credit:
-            c.credit_scores = abi.GSX_CREDIT_DEFER
-        out = self.e.propagate(mine, c)[0]
-        if credit:
+        with self._on_stream():
+            mine = self.share(msgs)
+            credit = cfg.credit_scores
+            c = abi.PropConfig()
+            for f, _ in abi.PropConfig._fields_:
+                setattr(c, f, getattr(cfg, f))
+            if credit:
+                c.credit_scores = abi.GSX_CREDIT_DEFER
+            out = self.e.propagate(mine, c)[0]
+            if credit:
+                self.pending = True
+                if not self.epoch:
+                    self.end_epoch()
+            return out_dict(out), totals(out, self.tp)
+
+    def end_epoch(self):
+        """Sum every rank's pending first receipts, in-window duplicates and
+        invalid deliveries (P4) and fold them (one all-reduce of 3 x E x 4 B)."""
+        if not self.pending:
+            return
+        with self._on_stream():
+            torch = _torch()
             E = self.e.n_pairs
-            # first receipts, in-window duplicates and invalid deliveries (P4)
             cnt = torch.empty((3, max(E, 1)), dtype=torch.int32, device=self.tp.device)
-            if cnt.is_cuda:
-                torch.cuda.synchronize(cnt.device)
             self.e.pending_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
             self.e.pending_invalid(cnt[2].data_ptr())
             self.tp.all_reduce_sum(cnt)
-            if cnt.is_cuda:
-                torch.cuda.synchronize(cnt.device)
             self.e.replace_pending_invalid(cnt[2].data_ptr())
             self.e.fold_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
-        return out_dict(out), totals(out, self.tp)
+        self.pending = False
 
 
 def out_dict(out) -> dict:
