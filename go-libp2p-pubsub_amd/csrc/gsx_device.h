@@ -410,6 +410,18 @@ struct HbState {
     uint8_t* pxno;         // [pair]: bit 0 = (A) pruned it without PX, bit 1 = its (B) answers go without PX
     uint32_t* px_log;      // [px_cap][4]: connection candidates (receiver, candidate, pruner, topic | kind << 8)
     uint64_t px_cap;
+    // peer exchange across range shards: a PRUNE of a cross-shard pair carries
+    // its PX list to the receiver's rank as an entry (receive slot there,
+    // topic | kind << 8, n, ids[PrunePeers]: pxs_w u32), grouped per destination
+    const uint32_t* send_slot;        // [pair]: the pair's send slot (NO_PAIR: the peer does not track it)
+    const uint8_t* send_dest;         // [send slot]: destination rank
+    const uint64_t* send_base;        // [rank + 1]: first send slot of each destination
+    const uint64_t* dest_halo_base;   // [rank]: the destination's receive slot of this rank's first
+    uint32_t* pxs_out;                // entries (null: the count pass)
+    const uint64_t* pxs_off;          // [rank]: first entry of each destination
+    unsigned long long* pxs_cnt;      // [rank]: entries counted / written
+    uint32_t pxs_w;
+    const uint32_t* halo_pair;        // [receive slot]: the local pair (u -> v) whose peer v is remote
     double accept_px;      // AcceptPXThreshold
     double publish_threshold;
     const uint64_t* mc_digest;  // per cache slot: mix64(id + golden)
@@ -470,6 +482,20 @@ hipError_t launch_mask_and(const uint8_t* a, const uint8_t* b, uint8_t* out, uin
 // word w's messages' digests.
 hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_words, uint32_t n_msgs,
                              const uint64_t* msg_dig, const uint64_t* word_dig, uint64_t* dig, uint32_t* cnt,
+                             hipStream_t st);
+// One message block of a batch (gsx_mcache_put): its rows [node][words], its
+// messages are the batch's [off, off + n).
+struct McPart {
+    const uint64_t* rows;
+    uint32_t off, n, words;
+};
+hipError_t launch_mc_merge(const McPart* parts, uint32_t n_parts, uint64_t* dst, uint32_t n_nodes, uint32_t n_words,
+                           hipStream_t st);
+// Peer exchange across range shards: the count pass of the cross-shard PX
+// PRUNEs (per destination, into h.pxs_cnt) and the receivers' side of the
+// entries other ranks sent.
+hipError_t launch_hb_px_count(const HbState& h, uint32_t kind, hipStream_t st);
+hipError_t launch_hb_px_recv(const DevState& s, const HbState& h, const uint32_t* entries, uint64_t n,
                              hipStream_t st);
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
 // Peer exchange of the round's PRUNEs (gsx.h): kind 0 = (A) PRUNEs, 1 = (B) answers.

@@ -178,6 +178,8 @@ struct gsx_engine {
     uint64_t *d_sub = nullptr, *d_psub = nullptr, *d_fanout = nullptr, *d_fan_has = nullptr;
     int64_t* d_lastpub = nullptr;
     uint32_t *d_mscratch = nullptr, *d_mlist = nullptr;
+    uint8_t* d_mparts = nullptr;  // gsx_mcache_put's block descriptors
+    size_t mparts_cap = 0;
     size_t mlist_cap = 0;
     // peer exchange on PRUNE (do_px): per-pair noPX bits, the candidate-list
     // scratch when membership is off, the connection-candidate log
@@ -279,6 +281,13 @@ struct gsx_engine {
     uint64_t *d_send_base = nullptr, *d_dest_halo_base = nullptr;
     uint32_t* d_pair_obs = nullptr;
     uint32_t* d_halo_node = nullptr;  // per receive slot: local node of its pair
+    uint32_t* d_halo_pair = nullptr;  // per receive slot: its local pair (peer exchange)
+    uint32_t* d_send_slot = nullptr;  // per pair: its send slot, NO_PAIR if none (peer exchange)
+    // peer exchange across shards: entries of this round's pack, per destination
+    unsigned long long* d_pxs_cnt = nullptr;
+    uint64_t* d_pxs_off = nullptr;
+    std::vector<uint64_t> pxs_counts;
+    bool pxs_packed[2] = {false, false};
     std::vector<uint32_t> rev_host;
     bool sharded() const { return n_ranks > 1 || node_lo != 0 || n_total != n_nodes; }
     hipStream_t own_stream = nullptr;
@@ -501,6 +510,7 @@ void free_state(gsx_engine* e) {
                   e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
                   e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
+                  e->d_halo_pair, e->d_send_slot,
                   e->prop.d_dig, e->prop.rcand};
     for (void* p : pp)
         if (p) (void)hipFree(p);
@@ -512,7 +522,7 @@ void free_state(gsx_engine* e) {
     e->prop.hop_flag = hf;
     e->prop.d_hop_flag = dhf;
     e->prop.hop_seq = hseq;
-    e->d_send_pair = e->d_pair_obs = e->d_halo_node = nullptr;
+    e->d_send_pair = e->d_pair_obs = e->d_halo_node = e->d_halo_pair = e->d_send_slot = nullptr;
     e->d_send_dest = nullptr;
     e->d_send_base = e->d_dest_halo_base = nullptr;
     e->n_ranks = 1;
@@ -911,6 +921,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_state(e);
     if (e->d_tp) (void)hipFree(e->d_tp);
+    if (e->d_mparts) (void)hipFree(e->d_mparts);
     if (e->d_stage) (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
@@ -1193,13 +1204,14 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     for (uint32_t k = 0; k < n_ranks; ++k) base[k + 1] = base[k] + cnt[k];
     if (base[n_ranks] > gsx::HALO_SLOT) return fail(e, GSX_ERANGE, "too many cross-shard pairs (2^30 receive slots)");
     std::vector<uint64_t> fill(base.begin(), base.end() - 1);
-    std::vector<uint32_t> hnode(base[n_ranks]);
+    std::vector<uint32_t> hnode(base[n_ranks]), hpair(base[n_ranks]);
     for (uint64_t q = 0; q < e->E; ++q) {
         const uint32_t v = (uint32_t)e->col_host[q];
         if (v >= self_lo && v - self_lo < self_n) continue;
         const uint64_t slot = fill[own[q]]++;
         e->rev_host[q] = gsx::HALO | (uint32_t)slot;
         hnode[slot] = e->pair_obs[q];
+        hpair[slot] = (uint32_t)q;
         if (recv_u) recv_u[slot] = e->pair_obs[q] + self_lo;
         if (recv_v) recv_v[slot] = v;
     }
@@ -1215,6 +1227,11 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     if (int rc = dalloc(e, &e->d_halo_node, hnode.size())) return rc;
     if (!hnode.empty())
         HIPCHK(e, hipMemcpy(e->d_halo_node, hnode.data(), sizeof(uint32_t) * hnode.size(), hipMemcpyHostToDevice));
+    if (e->d_halo_pair) (void)hipFree(e->d_halo_pair);
+    e->d_halo_pair = nullptr;
+    if (int rc = dalloc(e, &e->d_halo_pair, hpair.size())) return rc;
+    if (!hpair.empty())
+        HIPCHK(e, hipMemcpy(e->d_halo_pair, hpair.data(), sizeof(uint32_t) * hpair.size(), hipMemcpyHostToDevice));
     return GSX_OK;
 }
 
@@ -1255,6 +1272,15 @@ int gsx_shard_send_plan(gsx_engine* e, const uint64_t* send_counts, const uint32
         return rc;
     if (n) HIPCHK(e, hipMemcpy(e->d_send_pair, sp.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
     if (n) HIPCHK(e, hipMemcpy(e->d_send_dest, dest.data(), n, hipMemcpyHostToDevice));
+    {  // pair -> its send slot (a pair is asked for by at most one destination: its peer's owner)
+        std::vector<uint32_t> slot_of(std::max<size_t>(e->E, 1), gsx::NO_PAIR);
+        for (uint64_t j = 0; j < n; ++j)
+            if (sp[j] != gsx::NO_PAIR) slot_of[sp[j]] = (uint32_t)j;
+        if (e->d_send_slot) (void)hipFree(e->d_send_slot);
+        e->d_send_slot = nullptr;
+        if ((rc = dalloc(e, &e->d_send_slot, slot_of.size()))) return rc;
+        HIPCHK(e, hipMemcpy(e->d_send_slot, slot_of.data(), sizeof(uint32_t) * slot_of.size(), hipMemcpyHostToDevice));
+    }
     HIPCHK(e, hipMemcpy(e->d_send_base, base.data(), 8 * base.size(), hipMemcpyHostToDevice));
     e->send_counts.assign(send_counts, send_counts + e->n_ranks);
     e->n_send = n;
@@ -1921,6 +1947,30 @@ int prop_event_pair(gsx_engine* e, hipEvent_t* a, hipEvent_t* b) {
     return GSX_OK;
 }
 
+// Publish at sources that have not joined the topic: their fanout (gossipsub.go:981-998)
+int fanout_publish(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
+    if (!(e->members_on && cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < e->T))
+        return GSX_OK;
+    const size_t N = e->n_nodes;
+    std::vector<uint32_t> src;
+    std::vector<uint8_t> done(N, 0);
+    for (size_t k = 0; k < m; ++k) {
+        const uint32_t v = msgs[k].source;
+        if (v < N && !done[v] && !((e->h_sub[v] >> cfg->topic) & 1)) {
+            done[v] = 1;
+            src.push_back(v);
+        }
+    }
+    if (src.empty()) return GSX_OK;
+    if (int rc = member_list(e, src)) return rc;
+    gsx::HbState hm = member_state(e);
+    HIPCHK(e, gsx::launch_fanout_pick(dev_state(e), hm, e->d_mlist, (uint32_t)src.size(), cfg->topic, cfg->now_ns,
+                                      cfg->seed, e->th.publish_threshold, e->stream));
+    ++e->mem_gen;
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // `src` is on the host stack
+    return GSX_OK;
+}
+
 int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
     if (!e || !cfg || (m && !msgs)) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
@@ -2089,26 +2139,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     // record flags, the overlay and, where a threshold decides, the scores:
     // the last call's are reused while none of those moved (unsharded only:
     // a shard plan rewrites the reverse pairs)
-    // Publish at sources that have not joined the topic: their fanout (gossipsub.go:981-998)
-    if (e->members_on && cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < e->T) {
-        std::vector<uint32_t> src;
-        std::vector<uint8_t> done(N, 0);
-        for (size_t k = 0; k < m; ++k) {
-            const uint32_t v = msgs[k].source;
-            if (v < N && !done[v] && !((e->h_sub[v] >> cfg->topic) & 1)) {
-                done[v] = 1;
-                src.push_back(v);
-            }
-        }
-        if (!src.empty()) {
-            if (int rc = member_list(e, src)) return rc;
-            gsx::HbState hm = member_state(e);
-            HIPCHK(e, gsx::launch_fanout_pick(ds, hm, e->d_mlist, (uint32_t)src.size(), cfg->topic, cfg->now_ns,
-                                              cfg->seed, e->th.publish_threshold, e->stream));
-            ++e->mem_gen;
-            HIPCHK(e, hipStreamSynchronize(e->stream));  // `src` is on the host stack
-        }
-    }
+    if (int rc = fanout_publish(e, msgs, m, cfg)) return rc;
     auto& K = P.fwd_key;
     const bool fwd_same = K.valid && !e->sharded() && K.router == cfg->router && K.topic == cfg->topic &&
                           K.flood_publish == cfg->flood_publish && K.flag_gen == e->flag_gen &&
@@ -2912,7 +2943,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
     }
     if (e->gp.do_px) {  // peer exchange on the round's PRUNEs (gsx.h; heartbeats and Join / Leave rounds)
-        if (e->sharded()) return fail(e, GSX_ESTATE, "peer exchange (do_px) runs on unsharded engines only");
+        if (e->sharded() && e->n_ranks > 1 && !e->d_dest_halo_base)
+            return fail(e, GSX_ESTATE, "peer exchange on a shard: gsx_shard_set_halo_bases first");
         const size_t E = std::max<size_t>(e->E, 1);
         if (!e->d_pxno)
             if (int rc = dalloc(e, &e->d_pxno, E)) return rc;
@@ -2935,7 +2967,23 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.col = e->d_col;
         if (!e->members_on) h.mscratch = e->d_pxscratch;
         h.pxbase = e->d_pxbase;
+        if (e->sharded()) {  // PX lists of cross-shard PRUNEs travel (gsx_hb_px_*)
+            if (!e->d_pxs_cnt) {
+                if (int rc = dalloc(e, &e->d_pxs_cnt, (size_t)gsx::MAX_RANKS)) return rc;
+                if (int rc = dalloc(e, &e->d_pxs_off, (size_t)gsx::MAX_RANKS)) return rc;
+            }
+            h.send_slot = e->d_send_slot;
+            h.send_dest = e->d_send_dest;
+            h.send_base = e->d_send_base;
+            h.dest_halo_base = e->d_dest_halo_base;
+            h.halo_pair = e->d_halo_pair;
+            h.pair_obs = e->d_pair_obs;
+            h.pxs_cnt = e->d_pxs_cnt;
+            h.pxs_off = e->d_pxs_off;
+            h.pxs_w = 3u + (uint32_t)std::max(e->gp.prune_peers, 0);
+        }
     }
+    e->pxs_packed[0] = e->pxs_packed[1] = false;
     const size_t E8 = 8 * (e->E ? e->E : 1);
     // Unsharded, (B) and (C) clear the control words, answers and marks they
     // read, and nothing else is ever set: after one cleared round they stay
@@ -3069,7 +3117,9 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     gsx::HbState h = e->hb;
     h.halo_ctl = halo_ctl;
     const gsx::DevState ds = dev_state(e);
-    HIPCHK(e, gsx::launch_hb_px(ds, h, 0, e->stream));  // the (A) PRUNEs' peer exchange (do_px)
+    if (h.pxno && e->sharded() && !e->pxs_packed[0])
+        return fail(e, GSX_ESTATE, "peer exchange on a shard: gsx_hb_px_pack(0) before gsx_hb_recv");
+    if (!e->sharded()) HIPCHK(e, gsx::launch_hb_px(ds, h, 0, e->stream));  // the (A) PRUNEs' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_recv(ds, h, e->stream));
     // the pairs touched so far that (C) reads: those marked with an answer
     // (a shard's (C) reads every pair with a remote answer: all touched pairs;
@@ -3085,7 +3135,9 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     const gsx::DevState ds = dev_state(e);
     e->hb_active = false;
     std::memset(out, 0, sizeof(*out));
-    HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
+    if (h.pxno && e->sharded() && !e->pxs_packed[1])
+        return fail(e, GSX_ESTATE, "peer exchange on a shard: gsx_hb_px_pack(1) before gsx_hb_end");
+    if (!e->sharded()) HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
     HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
@@ -3401,6 +3453,71 @@ int gsx_hb_pack_resp(gsx_engine* e, uint64_t* send) {
     return GSX_OK;
 }
 
+// ---- peer exchange across range shards (gsx.h) -------------------------------------
+
+namespace {
+int px_shard_ready(gsx_engine* e, uint32_t kind) {
+    if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
+    if (kind > 1) return fail(e, GSX_EINVAL, "kind is 0 (the (A) PRUNEs) or 1 (the (B) answers)");
+    if (!e->hb.pxno) return fail(e, GSX_ESTATE, "peer exchange is off (do_px)");
+    if (!e->sharded()) return fail(e, GSX_ESTATE, "unsharded engines run the peer exchange inside the round");
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_hb_px_entry_words(gsx_engine* e, uint32_t* words) {
+    if (!e || !words) return GSX_EINVAL;
+    *words = 3u + (uint32_t)std::max(e->gp.prune_peers, 0);
+    return GSX_OK;
+}
+
+int gsx_hb_px_count(gsx_engine* e, uint32_t kind, uint64_t* counts) {
+    if (!e || !counts) return GSX_EINVAL;
+    if (int rc = px_shard_ready(e, kind)) return rc;
+    gsx::HbState h = e->hb;
+    const uint32_t R = std::max<uint32_t>(e->n_ranks, 1);
+    HIPCHK(e, hipMemsetAsync(e->d_pxs_cnt, 0, 8 * (size_t)R, e->stream));
+    if (e->n_send) HIPCHK(e, gsx::launch_hb_px_count(h, kind, e->stream));
+    e->pxs_counts.assign(R, 0);
+    HIPCHK(e, hipMemcpyAsync(e->pxs_counts.data(), e->d_pxs_cnt, 8 * (size_t)R, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    std::memcpy(counts, e->pxs_counts.data(), 8 * (size_t)R);
+    return GSX_OK;
+}
+
+int gsx_hb_px_pack(gsx_engine* e, uint32_t kind, uint32_t* out) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = px_shard_ready(e, kind)) return rc;
+    const uint32_t R = std::max<uint32_t>(e->n_ranks, 1);
+    if (e->pxs_counts.size() != R) return fail(e, GSX_ESTATE, "gsx_hb_px_count first");
+    uint64_t tot = 0;
+    std::vector<uint64_t> off(R);
+    for (uint32_t d = 0; d < R; ++d) {
+        off[d] = tot;
+        tot += e->pxs_counts[d];
+    }
+    if (tot && !out) return GSX_EINVAL;
+    gsx::HbState h = e->hb;
+    h.pxs_out = out;
+    HIPCHK(e, hipMemcpyAsync(e->d_pxs_off, off.data(), 8 * (size_t)R, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_pxs_cnt, 0, 8 * (size_t)R, e->stream));
+    // every PX PRUNE of this rank's nodes: local receivers handled here, the
+    // others' lists written out (kind 0 reads the (A) PRUNE words, 1 the (B) answers)
+    HIPCHK(e, gsx::launch_hb_px(dev_state(e), h, kind, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // `off` is on the host stack
+    e->pxs_counts.clear();
+    e->pxs_packed[kind] = true;
+    return GSX_OK;
+}
+
+int gsx_hb_px_recv(gsx_engine* e, uint32_t kind, const uint32_t* entries, uint64_t n) {
+    if (!e || (n && !entries)) return GSX_EINVAL;
+    if (int rc = px_shard_ready(e, kind)) return rc;
+    if (!e->pxs_packed[kind]) return fail(e, GSX_ESTATE, "gsx_hb_px_pack first (the round's own lists)");
+    HIPCHK(e, gsx::launch_hb_px_recv(dev_state(e), e->hb, entries, n, e->stream));
+    return GSX_OK;
+}
+
 int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     if (!e || !out) return GSX_EINVAL;
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
@@ -3609,6 +3726,138 @@ int gsx_mcache_clear(gsx_engine* e) {
     if (!e) return GSX_EINVAL;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     mcache_clear(e);
+    return GSX_OK;
+}
+
+// ---- message-parallel replicas: one batch from its message blocks (gsx.h) ----
+
+namespace {
+int mcache_ready(gsx_engine* e) {
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->sharded()) return fail(e, GSX_ESTATE, "block merging runs on unsharded engines (replicas)");
+    if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    return GSX_OK;
+}
+const gsx_engine::McBatch* mcache_newest(gsx_engine* e) {
+    if (e->mc.empty() || e->mc.front().empty()) return nullptr;
+    return &e->mc.front().back();
+}
+}  // namespace
+
+int gsx_mcache_last(gsx_engine* e, uint32_t* n_words, uint32_t* n_msgs) {
+    if (!e || !n_words || !n_msgs) return GSX_EINVAL;
+    if (int rc = mcache_ready(e)) return rc;
+    const auto* b = mcache_newest(e);
+    if (!b) return fail(e, GSX_ESTATE, "the current cache window is empty");
+    *n_words = b->n_words;
+    *n_msgs = b->n_msgs;
+    return GSX_OK;
+}
+
+int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows) {
+    if (!e || !cache_rows || !set_rows) return GSX_EINVAL;
+    if (int rc = mcache_ready(e)) return rc;
+    const auto* b = mcache_newest(e);
+    if (!b || !b->set) return fail(e, GSX_ESTATE, "no cached gossipsub batch with a message set");
+    const size_t words = (size_t)b->n_words * e->n_nodes;
+    HIPCHK(e, hipMemcpyAsync(cache_rows, b->d_seen, 8 * words, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(set_rows, b->set->d_all, 8 * words, hipMemcpyDeviceToDevice, e->stream));
+    return GSX_OK;
+}
+
+int gsx_mcache_pop(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = mcache_ready(e)) return rc;
+    if (!mcache_newest(e)) return fail(e, GSX_ESTATE, "the current cache window is empty");
+    auto& w = e->mc.front();
+    if (w.back().set && w.back().set->serial == e->msg_serial && w.back().set->refs == 1) --e->msg_serial;
+    batch_release(e, w.back());  // (the buffers go back to the pool: stream-ordered reuse)
+    w.pop_back();
+    return GSX_OK;
+}
+
+int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
+                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts) {
+    if (!e || !cfg || !msgs || !m || !n_parts || !part_msgs || !cache_parts || !set_parts) return GSX_EINVAL;
+    if (int rc = mcache_ready(e)) return rc;
+    if (cfg->router != GSX_ROUTER_GOSSIPSUB) return fail(e, GSX_EINVAL, "only gossipsub batches are cached");
+    if (m > 0xFFFFFFFFull) return fail(e, GSX_ERANGE, "batch too large");
+    for (size_t k = 0; k < m; ++k) {
+        if (msgs[k].source >= e->n_total) return fail(e, GSX_ERANGE, "message source out of range");
+        if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return fail(e, GSX_EINVAL, "bad message validation outcome");
+    }
+    std::vector<gsx::McPart> cp(n_parts), sp(n_parts);
+    uint64_t off = 0;
+    for (uint32_t k = 0; k < n_parts; ++k) {
+        if (part_msgs[k] && (!cache_parts[k] || !set_parts[k])) return fail(e, GSX_EINVAL, "missing block rows");
+        cp[k] = gsx::McPart{cache_parts[k], (uint32_t)off, part_msgs[k], prop_words(part_msgs[k])};
+        sp[k] = gsx::McPart{set_parts[k], (uint32_t)off, part_msgs[k], prop_words(part_msgs[k])};
+        off += part_msgs[k];
+    }
+    if (off != m) return fail(e, GSX_EINVAL, "the blocks do not add up to the batch");
+    if (int rc = fanout_publish(e, msgs, m, cfg)) return rc;
+    const uint32_t W = prop_words(m);
+    const size_t N = e->n_nodes;
+    // the blocks' descriptors (cache, then set) on the device
+    const size_t need = 2 * (size_t)n_parts * sizeof(gsx::McPart);
+    if (need > e->mparts_cap) {
+        if (e->d_mparts) (void)hipFree(e->d_mparts);
+        e->d_mparts = nullptr;
+        e->mparts_cap = 0;
+        if (int rc = dalloc(e, &e->d_mparts, need)) return rc;
+        e->mparts_cap = need;
+    }
+    cp.insert(cp.end(), sp.begin(), sp.end());
+    auto* dparts = reinterpret_cast<gsx::McPart*>(e->d_mparts);
+    HIPCHK(e, hipMemcpyAsync(dparts, cp.data(), need, hipMemcpyHostToDevice, e->stream));
+    gsx_engine::MsgSet* set = new gsx_engine::MsgSet;
+    set->serial = ++e->msg_serial;
+    set->n_msgs = (uint32_t)m;
+    set->n_words = W;
+    set->topic = cfg->topic;
+    set->ids.resize(m);
+    for (size_t k = 0; k < m; ++k) set->ids[k] = msgs[k].msg_id;
+    set->refs = 1;
+    set->all_words = (size_t)W * N;
+    set->d_all = seen_acquire(e, set->all_words);
+    gsx_engine::McBatch b;
+    b.topic = cfg->topic;
+    b.n_msgs = (uint32_t)m;
+    b.n_words = W;
+    b.seen_words = (size_t)W * N + 2 * N;
+    b.d_seen = seen_acquire(e, b.seen_words);
+    b.ids = set->ids;
+    b.set = set;
+    if (!set->d_all || !b.d_seen) {
+        batch_release(e, b);
+        return fail(e, GSX_ENOMEM, "seen rows of the merged batch");
+    }
+    HIPCHK(e, gsx::launch_mc_merge(dparts, n_parts, b.d_seen, (uint32_t)N, W, e->stream));
+    HIPCHK(e, gsx::launch_mc_merge(dparts + n_parts, n_parts, set->d_all, (uint32_t)N, W, e->stream));
+    std::vector<uint64_t> acc(W, 0), dg((size_t)W * 64 + W, 0);
+    std::vector<uint32_t> vals(m);
+    for (size_t k = 0; k < m; ++k) {
+        vals[k] = msgs[k].validation;
+        if (vals[k] == GSX_VALIDATION_ACCEPT) acc[k / 64] |= 1ull << (k % 64);
+        dg[k] = id_digest(msgs[k].msg_id);
+        dg[(size_t)W * 64 + k / 64] += dg[k];
+    }
+    int rc = 0;
+    if ((rc = dalloc(e, &set->d_val, m)) || (rc = dalloc(e, &set->d_acc, (size_t)W)) ||
+        (rc = dalloc(e, &set->d_dg, dg.size()))) {
+        batch_release(e, b);
+        return rc;
+    }
+    HIPCHK(e, hipMemcpyAsync(set->d_val, vals.data(), 4 * m, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
+    b.d_dig = b.d_seen + (size_t)W * N;
+    b.d_cnt = reinterpret_cast<uint32_t*>(b.d_seen + (size_t)W * N + N);
+    HIPCHK(e, gsx::launch_mc_summary(b.d_seen, (uint32_t)N, W, (uint32_t)m, set->d_dg, set->d_dg + (size_t)W * 64,
+                                     b.d_dig, b.d_cnt, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // the host vectors above
+    if (e->mc.empty()) e->mc.emplace_back();
+    e->mc.front().push_back(std::move(b));
     return GSX_OK;
 }
 

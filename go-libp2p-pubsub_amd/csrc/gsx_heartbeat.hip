@@ -1396,6 +1396,147 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     c.flush(h);
 }
 
+// (B) pair-parallel: RG lanes per receiving node u (up to HB_LANE_DEG peers),
+// one lane per sender pair, the row RG pairs at a time.  Everything handleGraft
+// / handlePrune (:718-843) does to one pair — its control words, AcceptFrom,
+// the direct / backoff / negative-score rejections with their penalties and
+// backoffs, the tracer bits, the records — belongs to that pair alone, so the
+// lanes do it side by side with coalesced per-pair loads.  The one thing the
+// senders share is the Dhi check (:786-795): a non-outbound GRAFT is refused
+// once the mesh holds Dhi peers, and the mesh size is what the earlier senders'
+// accepts and prunes left.  The group resolves that recurrence per topic over
+// its lanes in ascending pair order, on a 5-bit code per lane (candidate,
+// outbound, scored, PRUNE, in the mesh before) moved by shuffles, then every
+// lane applies its own outcome.  Bit-identical to the sequential walk.
+constexpr int RG = 16;
+enum : uint32_t { RC_CAND = 1, RC_OUT = 2, RC_SC = 4, RC_PR = 8, RC_INM = 16 };
+
+__global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
+    const uint32_t gl = threadIdx.x % RG;                 // the lane's place in its node's group
+    const uint32_t gbase = (threadIdx.x % 64) & ~(RG - 1);  // the group's first lane in the wave
+    const uint32_t gpb = 256 / RG;
+    const DevGossipParams& gp = h.gp;
+    RecvCounts c;
+    for (uint32_t u = blockIdx.x * gpb + threadIdx.x / RG; u < h.n_nodes; u += gridDim.x * gpb) {
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
+        for (int64_t c0 = r0; c0 < r1; c0 += RG) {  // group-uniform
+            const int64_t q = c0 + gl;  // q = (u -> v), ascending v
+            bool live = false, nopx = false, outb = false;
+            uint32_t r = NO_PAIR;
+            uint64_t cand = 0, prn = 0, inm = 0, scd = 0, resp = 0;
+            if (q < r1) {
+                bool act = true;
+                if (!h.halo_ctl) {
+                    act = h.inbox[q] != 0;
+                    if (act) h.inbox[q] = 0;
+                }
+                uint64_t grafts = 0, prunes = 0;
+                if (act && recv_control(h, (uint64_t)q, true, r, grafts, prunes)) {
+                    nopx = h.sub && (grafts & ~h.sub[u]);  // doPX = false (:721-781)
+                    if (h.sub) {  // topics u has not joined: ignored (:727-733, :816-819)
+                        grafts &= h.sub[u];
+                        prunes &= h.sub[u];
+                    }
+                    const double score = (grafts | prunes) ? s.score[q] : 0.0;
+                    const uint8_t ef = (grafts | prunes) ? h.eflags[q] : 0;
+                    if ((grafts | prunes) && ((ef & EDGE_DIRECT) || score >= h.graylist)) {
+                        live = true;
+                        h.dirty[q] = 1;
+                        outb = ef & EDGE_OUTBOUND;
+                        for (; grafts; grafts &= grafts - 1) {  // handleGraft up to the Dhi check
+                            const uint32_t t = (uint32_t)__builtin_ctzll(grafts);
+                            if (hb_in_mesh(s, q, t)) continue;
+                            if (ef & EDGE_DIRECT) {
+                                resp |= 1ull << t;
+                                ++c.rejected;
+                                nopx = true;
+                                continue;
+                            }
+                            const int64_t expire = h.backoff[(size_t)t * h.n_pairs + q];
+                            if (expire != 0 && h.now < expire) {
+                                nopx = true;
+                                ev_penalty(s, q, 1);
+                                ++c.penalties;
+                                if (h.now < expire + (gp.graft_flood_threshold_ns - gp.prune_backoff_ns)) {
+                                    ev_penalty(s, q, 1);
+                                    ++c.penalties;
+                                }
+                                add_backoff(h, q, t, gp.prune_backoff_ns);
+                                resp |= 1ull << t;
+                                ++c.rejected;
+                                continue;
+                            }
+                            if (score < 0) {
+                                resp |= 1ull << t;
+                                add_backoff(h, q, t, gp.prune_backoff_ns);
+                                ++c.rejected;
+                                nopx = true;
+                                continue;
+                            }
+                            cand |= 1ull << t;
+                        }
+                        prn = prunes;
+                        for (uint64_t m = cand | prn; m; m &= m - 1) {
+                            const uint32_t t = (uint32_t)__builtin_ctzll(m);
+                            if (scored_topic(s, q, t)) scd |= 1ull << t;
+                            if ((prn >> t & 1) && hb_in_mesh(s, q, t)) inm |= 1ull << t;
+                        }
+                    }
+                }
+            }
+            // the Dhi recurrence, per topic any lane of the group has an event for
+            uint64_t any = cand | prn;
+#pragma unroll
+            for (int off = RG / 2; off > 0; off >>= 1) any |= __shfl_xor(any, off, RG);
+            uint64_t acc = 0;
+            for (; any; any &= any - 1) {  // group-uniform
+                const uint32_t t = (uint32_t)__builtin_ctzll(any);
+                const uint32_t code = (uint32_t)(cand >> t & 1) * RC_CAND | (outb ? RC_OUT : 0u) |
+                                      (uint32_t)(scd >> t & 1) * RC_SC | (uint32_t)(prn >> t & 1) * RC_PR |
+                                      (uint32_t)(inm >> t & 1) * RC_INM;
+                const bool ev = code & (RC_CAND | RC_PR);
+                uint32_t lanes = (uint32_t)((__ballot(ev) >> gbase) & ((1ull << RG) - 1));
+                uint16_t* mcp = h.mcount + (size_t)t * h.n_nodes + u;
+                const int n0 = *mcp;
+                int n = n0;
+                for (; lanes; lanes &= lanes - 1) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(lanes);
+                    const uint32_t cj = (uint32_t)__shfl((int)code, (int)j, RG);
+                    const bool a = (cj & RC_CAND) && ((cj & RC_OUT) || n < gp.d_hi);
+                    if (a && (cj & RC_SC)) ++n;
+                    if ((cj & RC_PR) && (cj & RC_SC) && ((cj & RC_INM) || a)) --n;
+                    if (gl == j && a) acc |= 1ull << t;
+                }
+                if (gl == 0 && n != n0) *mcp = (uint16_t)n;
+            }
+            __threadfence_block();  // the next chunk's lanes read the counts written here
+            if (!live) continue;
+            for (uint64_t m = cand; m; m &= m - 1) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(m);
+                if (acc >> t & 1) {
+                    ev_graft(s, q, t, h.now);
+                    if (h.tr_acc) h.tr_acc[q] |= 1ull << t;  // tracer.Graft, :795
+                    ++c.accepted;
+                    if (scd >> t & 1) ++c.links;
+                } else {  // the mesh is full (Dhi)
+                    resp |= 1ull << t;
+                    add_backoff(h, q, t, gp.prune_backoff_ns);
+                    ++c.rejected;
+                }
+            }
+            h.resp[q] = resp;
+            if (resp && !(r & HALO)) h.answer[r] = 1;  // the GRAFT sender has an answer to read in (C)
+            if (h.pxno && nopx) h.pxno[q] |= 2;
+            for (uint64_t m = prn; m; m &= m - 1) {  // handlePrune
+                if (handle_prune(s, h, q, (uint32_t)__builtin_ctzll(m))) --c.links;
+                ++c.handled;
+            }
+        }
+    }
+    c.flush(h);
+}
+
 // (B) for hub receivers (more than HB_LANE_DEG peers): one wave per node.
 // The wave finds the marked pairs 64 at a time (ballot); every lane then runs
 // the same sequential handling of each sender in ascending order (its values
@@ -1629,7 +1770,12 @@ hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, con
 
 hipError_t launch_hb_recv(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
+    // GSX_HB_RECV_LANE=1 selects the lane-per-receiver kernel (A/B measurement)
+    static const bool lane_per_node = getenv("GSX_HB_RECV_LANE") != nullptr;
+    if (lane_per_node)
+        hipLaunchKernelGGL(k_hb_recv, dim3(wave_grid(h.n_nodes)), dim3(64), 0, st, s, h);
+    else
+        hipLaunchKernelGGL(k_hb_recv_grp, dim3(grid_cap((uint64_t)h.n_nodes * RG, 256)), dim3(256), 0, st, s, h);
     if (h.n_hubs) hipLaunchKernelGGL(k_hb_recv_hub, dim3(std::min<uint32_t>(h.n_hubs, 4096)), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
@@ -1662,6 +1808,40 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
     return hipGetLastError();
 }
 
+// The seen rows of a whole batch from its message blocks (message-parallel
+// replicas, gsx_mcache_put): word w of node v holds the batch's messages
+// [64w, 64w + 64); each block overlapping them contributes its bits, shifted
+// from the block's own numbering.  A lane per (node, word), coalesced writes.
+__global__ __launch_bounds__(256) void k_mc_merge(const McPart* __restrict__ parts, uint32_t n_parts,
+                                                  uint64_t* __restrict__ dst, uint32_t n_nodes, uint32_t W) {
+    const uint64_t n = (uint64_t)n_nodes * W;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t v = (uint32_t)(i / W), w = (uint32_t)(i % W);
+        const uint32_t g0 = 64u * w, g1 = g0 + 64u;
+        uint64_t x = 0;
+        for (uint32_t p = 0; p < n_parts; ++p) {
+            const McPart P = parts[p];
+            const uint32_t lo = max(g0, P.off), hi = min(g1, P.off + P.n);
+            if (lo >= hi) continue;
+            const uint32_t b0 = lo - P.off, wa = b0 / 64u, sa = b0 % 64u, len = hi - lo;
+            const uint64_t* row = P.rows + (size_t)v * P.words;
+            uint64_t bits = row[wa] >> sa;
+            if (sa && wa + 1 < P.words) bits |= row[wa + 1] << (64u - sa);
+            if (len < 64u) bits &= (1ull << len) - 1;
+            x |= bits << (lo - g0);
+        }
+        dst[i] = x;
+    }
+}
+
+hipError_t launch_mc_merge(const McPart* parts, uint32_t n_parts, uint64_t* dst, uint32_t n_nodes, uint32_t n_words,
+                           hipStream_t st) {
+    const uint64_t n = (uint64_t)n_nodes * n_words;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_merge, dim3(grid_cap(n, 256)), dim3(256), 0, st, parts, n_parts, dst, n_nodes, n_words);
+    return hipGetLastError();
+}
+
 // ---- peer exchange on PRUNE (gossipsub.go:811-843, 861-910, 1814-1850) ----------
 
 // One lane per pruning node u (kind 0: the (A) PRUNEs in ctl_prune, before
@@ -1676,6 +1856,77 @@ hipError_t launch_mc_summary(const uint64_t* seen, uint32_t n_nodes, uint32_t n_
 // are the cache as the receiving step reads it (gsx.h).  PX is off by
 // default and this kernel runs only with do_px: candidates are logged with
 // one L2 atomic each.
+// pxConnect's candidates of one PX list at the receiver p (local node) of the
+// pruner ug (global id): AcceptPXThreshold on its score of the pruner (pair q),
+// then the peers p is not connected to (p's row is sorted by peer: a binary
+// search; ids global on a shard).  Logs (p, candidate, pruner, topic | kind).
+__device__ __forceinline__ void px_connect(const DevState& s, const HbState& h, uint32_t p, uint32_t ug, double rs,
+                                           const uint32_t* ids, int n, uint32_t t, uint32_t kind, uint64_t& ignored,
+                                           uint64_t& connect) {
+    if (rs < h.accept_px) {  // :833-838
+        ++ignored;
+        return;
+    }
+    const int64_t p0 = h.row_ptr[p], p1 = h.row_ptr[p + 1];
+    for (int i = 0; i < n; ++i) {  // pxConnect (:861-910): the peers p is not connected to
+        const int32_t xp = (int32_t)ids[i];
+        int64_t lo = p0, hi = p1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (h.col[mid] < xp) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < p1 && h.col[lo] == xp && (s.pflags[lo] & PAIR_CONNECTED)) continue;
+        if (h.px_log) {
+            const unsigned long long k = atomicAdd(&h.stats[HB_PX_CONNECT], 1ull);
+            if (k < h.px_cap) {
+                uint32_t* o = h.px_log + 4 * k;
+                o[0] = h.node_lo + p;
+                o[1] = (uint32_t)xp;
+                o[2] = ug;
+                o[3] = t | (kind << 8);
+            }
+        } else {
+            ++connect;
+        }
+    }
+}
+
+// Count pass of the shard exchange: the PX PRUNEs of cross-shard pairs whose
+// peer tracks the pruner, per destination rank (one entry each).
+__global__ __launch_bounds__(256) void k_hb_px_count(HbState h, uint32_t kind) {
+    const uint8_t nobit = kind ? 2 : 1;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {
+        const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+        if (!bits || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
+        const uint32_t q = h.rev[r];
+        if (q == NO_PAIR || !(q & HALO)) continue;
+        const uint32_t j = h.send_slot[r];
+        if (j == NO_PAIR) continue;
+        atomicAdd(&h.pxs_cnt[h.send_dest[j]], (unsigned long long)__popcll(bits));
+    }
+}
+
+// The receivers' side of the PX lists other ranks sent (one lane per entry).
+__global__ __launch_bounds__(256) void k_hb_px_recv(DevState s, HbState h, const uint32_t* __restrict__ ent,
+                                                    uint64_t n_ent) {
+    uint64_t ignored = 0, connect = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n_ent; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t* o = ent + i * h.pxs_w;
+        const int n = (int)o[2];
+        if (n <= 0) continue;
+        const uint32_t t = o[1] & 0xFFu, kind = o[1] >> 8;
+        const uint32_t q = h.halo_pair[o[0]];  // (p -> u): the receiver's pair
+        const uint32_t p = h.pair_obs[q];
+        const double rs = s.score[q];
+        if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) continue;  // AcceptFrom drops the RPC
+        if (!joined_node(h.sub, p, t)) continue;                         // handlePrune never reads it (:816-819)
+        px_connect(s, h, p, (uint32_t)h.col[q], rs, o + 3, n, t, kind, ignored, connect);
+    }
+    flush_count(h.stats, HB_PX_IGNORED, ignored);
+    flush_count(h.stats, HB_PX_CONNECT, connect);
+}
+
 __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t kind) {
     uint64_t lists = 0, listed = 0, ignored = 0, connect = 0;
     const uint8_t nobit = kind ? 2 : 1;
@@ -1699,55 +1950,45 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
             for (int64_t r = r0; r < r1; ++r) {  // r = (u -> p), a PRUNE of t with PX
                 const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
                 if (!((bits >> t) & 1) || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
-                const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (unsharded: never HALO)
-                const uint32_t p = (uint32_t)h.col[r];
-                bool heard = q != NO_PAIR;
-                double rs = 0.0;
-                if (heard) {
-                    rs = s.score[q];
-                    if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) heard = false;  // AcceptFrom drops the RPC
-                }
+                const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (HALO: p on another shard)
+                const uint32_t pg = (uint32_t)h.col[r];  // p's global id (= the local one unsharded)
                 int n = 0;
                 const uint32_t self = (uint32_t)(r - r0);
                 for (int i = 0; i < nb; ++i) {
                     const uint32_t x = h.pxbase[r0 + i];
                     if (x != self) h.mscratch[r0 + n++] = x;  // xp != p
                 }
-                Rng g{h.seed, TAG_PX, ((uint64_t)(h.node_lo + u) << 32) | (uint64_t)(h.node_lo + p),
+                Rng g{h.seed, TAG_PX, ((uint64_t)(h.node_lo + u) << 32) | (uint64_t)pg,
                       (h.tick << 32) | ((uint64_t)t << 24) | ((uint64_t)kind << 23), 0};
                 g.shuffle(h.mscratch + r0, n);
                 if (n > h.gp.prune_peers) n = h.gp.prune_peers;
+                if (q != NO_PAIR && (q & HALO)) {  // the list travels to p's rank (k_hb_px_recv there)
+                    const uint32_t j = h.send_slot[r];
+                    if (j != NO_PAIR) {  // (else p does not track u: nobody reads it)
+                        const uint32_t d = h.send_dest[j];
+                        const unsigned long long k = atomicAdd(&h.pxs_cnt[d], 1ull);
+                        uint32_t* o = h.pxs_out + (size_t)(h.pxs_off[d] + k) * h.pxs_w;
+                        o[0] = (uint32_t)(h.dest_halo_base[d] + (j - h.send_base[d]));
+                        o[1] = t | (kind << 8);
+                        o[2] = n > 0 ? (uint32_t)n : 0u;
+                        for (int i = 0; i < n; ++i) o[3 + i] = (uint32_t)h.col[r0 + h.mscratch[r0 + i]];
+                    }
+                    if (n > 0) {
+                        ++lists;
+                        listed += (uint64_t)n;
+                    }
+                    continue;
+                }
                 if (n <= 0) continue;
                 ++lists;
                 listed += (uint64_t)n;
-                if (!heard || !joined_node(h.sub, p, t)) continue;  // handlePrune never reads it (:816-819)
-                if (rs < h.accept_px) {  // :833-838
-                    ++ignored;
-                    continue;
-                }
-                const int64_t p0 = h.row_ptr[p], p1 = h.row_ptr[p + 1];
-                for (int i = 0; i < n; ++i) {  // pxConnect (:861-910): the peers p is not connected to
-                    const int32_t xp = h.col[r0 + h.mscratch[r0 + i]];
-                    int64_t lo = p0, hi = p1;
-                    while (lo < hi) {
-                        const int64_t mid = (lo + hi) >> 1;
-                        if (h.col[mid] < xp) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    if (lo < p1 && h.col[lo] == xp && (s.pflags[lo] & PAIR_CONNECTED)) continue;
-                    if (h.px_log) {
-                        const unsigned long long k = atomicAdd(&h.stats[HB_PX_CONNECT], 1ull);
-                        if (k < h.px_cap) {
-                            uint32_t* o = h.px_log + 4 * k;
-                            o[0] = h.node_lo + p;
-                            o[1] = h.node_lo + (uint32_t)xp;
-                            o[2] = h.node_lo + u;
-                            o[3] = t | (kind << 8);
-                        }
-                    } else {
-                        ++connect;
-                    }
-                }
+                if (q == NO_PAIR) continue;  // p does not track u
+                const uint32_t p = pg - h.node_lo;
+                const double rs = s.score[q];
+                if (!(h.eflags[q] & EDGE_DIRECT) && rs < h.graylist) continue;  // AcceptFrom drops the RPC
+                if (!joined_node(h.sub, p, t)) continue;  // handlePrune never reads it (:816-819)
+                for (int i = 0; i < n; ++i) h.mscratch[r0 + i] = (uint32_t)h.col[r0 + h.mscratch[r0 + i]];
+                px_connect(s, h, p, h.node_lo + u, rs, h.mscratch + r0, n, t, kind, ignored, connect);
             }
         }
         // (B) never reads nor clears the words of a pair its receiver does not
@@ -1771,6 +2012,19 @@ hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st)
 hipError_t launch_hb_px(const DevState& s, const HbState& h, uint32_t kind, hipStream_t st) {
     if (h.n_nodes == 0 || !h.pxno) return hipSuccess;
     hipLaunchKernelGGL(k_hb_px, dim3(grid_cap(h.n_nodes, 64)), dim3(64), 0, st, s, h, kind);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_px_count(const HbState& h, uint32_t kind, hipStream_t st) {
+    if (h.n_pairs == 0 || !h.pxno) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_px_count, dim3(grid_cap(h.n_pairs, 256)), dim3(256), 0, st, h, kind);
+    return hipGetLastError();
+}
+
+hipError_t launch_hb_px_recv(const DevState& s, const HbState& h, const uint32_t* entries, uint64_t n,
+                             hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_px_recv, dim3(grid_cap(n, 256)), dim3(256), 0, st, s, h, entries, n);
     return hipGetLastError();
 }
 

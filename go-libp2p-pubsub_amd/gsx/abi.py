@@ -234,6 +234,14 @@ GSX_ANY_TOPIC = 0xFFFFFFFF
 GSX_VALIDATION_ACCEPT, GSX_VALIDATION_REJECT, GSX_VALIDATION_IGNORE, GSX_VALIDATION_THROTTLE = 0, 1, 2, 3
 
 
+def prop_words(m: int) -> int:
+    """Words per call (gsx.h): 1, 2, or ceil(m/64) rounded up to a multiple of 4."""
+    w = (m + 63) // 64
+    if w <= 2:
+        return max(w, 1)
+    return (w + 3) & ~3
+
+
 class PropConfig(C.Structure):
     _fields_ = [
         ("router", C.c_uint32),
@@ -426,6 +434,15 @@ SIGNATURES = {
     "gsx_import_backoff": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "gsx_gossip_results": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint64)]),
     "gsx_mcache_clear": (C.c_int, [C.c_void_p]),
+    "gsx_hb_px_entry_words": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_hb_px_count": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint64)]),
+    "gsx_hb_px_pack": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "gsx_hb_px_recv": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "gsx_mcache_last": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32)]),
+    "gsx_mcache_copy_last": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_mcache_pop": (C.c_int, [C.c_void_p]),
+    "gsx_mcache_put": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), C.c_uint32, P(C.c_uint32),
+                                 P(C.c_void_p), P(C.c_void_p)]),
     "gsx_hb_set_tracing": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_set_subscriptions": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "gsx_join": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, C.c_uint64,

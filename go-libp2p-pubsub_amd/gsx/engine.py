@@ -11,7 +11,7 @@ from typing import Dict, Iterable, Optional
 import numpy as np
 
 from . import abi
-from .abi import GsxError
+from .abi import GsxError, prop_words
 
 
 def _ptr(a: Optional[np.ndarray], ctype):
@@ -340,6 +340,29 @@ class Engine:
     # -- heartbeat (gossipsub.go:1303-1604) ----------------------------------------------
     def set_gossipsub_params(self, gp: abi.GossipSubParams):
         self._chk(self.lib.gsx_set_gossipsub_params(self.h, C.byref(gp)), "gsx_set_gossipsub_params")
+        self._do_px = bool(gp.do_px)
+
+    _do_px = False
+
+    def hb_px_enabled(self) -> bool:
+        return self._do_px
+
+    # peer exchange on range shards (gsx.h gsx_hb_px_*)
+    def hb_px_entry_words(self) -> int:
+        w = C.c_uint32()
+        self._chk(self.lib.gsx_hb_px_entry_words(self.h, C.byref(w)), "gsx_hb_px_entry_words")
+        return int(w.value)
+
+    def hb_px_count(self, kind: int, n_ranks: int) -> np.ndarray:
+        c = np.zeros(n_ranks, dtype=np.uint64)
+        self._chk(self.lib.gsx_hb_px_count(self.h, kind, _ptr(c, C.c_uint64)), "gsx_hb_px_count")
+        return c
+
+    def hb_px_pack(self, kind: int, out):
+        self._chk(self.lib.gsx_hb_px_pack(self.h, kind, self._p(out)), "gsx_hb_px_pack")
+
+    def hb_px_recv(self, kind: int, entries, n: int):
+        self._chk(self.lib.gsx_hb_px_recv(self.h, kind, self._p(entries), n), "gsx_hb_px_recv")
 
     def heartbeat(self, tick: int, now: int, seed: int) -> abi.HeartbeatOut:
         out = abi.HeartbeatOut()
@@ -386,6 +409,43 @@ class Engine:
 
     def mcache_clear(self):
         self._chk(self.lib.gsx_mcache_clear(self.h), "gsx_mcache_clear")
+
+    # -- message-parallel replicas: a batch from its message blocks (gsx.h gsx_mcache_*) --------
+    # A block travels as one 1-D int64 device tensor: the cache rows, then the
+    # message set's rows, [n_nodes][words(n_msgs)] u64 each.
+    def mcache_part_size(self, n_msgs: int) -> int:
+        return 2 * self.n_nodes * prop_words(n_msgs)
+
+    def mcache_take_block(self, pad: int, device):
+        """The newest cached batch (this replica's block) out of the cache ->
+        (tensor of max(pad, its size) int64 on `device`, n_msgs); stream-ordered."""
+        import torch
+
+        W, m = C.c_uint32(), C.c_uint32()
+        self._chk(self.lib.gsx_mcache_last(self.h, C.byref(W), C.byref(m)), "gsx_mcache_last")
+        n = self.n_nodes * W.value
+        t = torch.zeros(max(pad, 2 * n), dtype=torch.int64, device=device)
+        self._chk(self.lib.gsx_mcache_copy_last(self.h, C.c_void_p(t.data_ptr()), C.c_void_p(t.data_ptr() + 8 * n)),
+                  "gsx_mcache_copy_last")
+        self._chk(self.lib.gsx_mcache_pop(self.h), "gsx_mcache_pop")
+        return t, m.value
+
+    def mcache_empty_block(self, pad: int, device):
+        import torch
+
+        return torch.zeros(pad, dtype=torch.int64, device=device)
+
+    def mcache_put(self, msgs, cfg: abi.PropConfig, blocks, part_msgs):
+        """gsx_mcache_put: msgs as one cached batch from the blocks (tensors as
+        mcache_take_block returns them, block k = part_msgs[k] messages)."""
+        ms = np.ascontiguousarray(msgs, dtype=abi.msg_dtype())
+        k = len(blocks)
+        cp = (C.c_void_p * k)(*[b.data_ptr() for b in blocks])
+        sp = (C.c_void_p * k)(*[b.data_ptr() + 8 * self.n_nodes * prop_words(int(n))
+                                for b, n in zip(blocks, part_msgs)])
+        pm = np.ascontiguousarray(part_msgs, dtype=np.uint32)
+        self._chk(self.lib.gsx_mcache_put(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg), k,
+                                          _ptr(pm, C.c_uint32), cp, sp), "gsx_mcache_put")
 
     def set_subscriptions(self, joined):
         """Joined topics per node (bit t of joined[v]); gsx_set_subscriptions."""

@@ -28,17 +28,12 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import abi
+from .abi import prop_words  # noqa: F401  (re-exported)
 
 _STAT_KEYS = ("deliveries", "duplicates", "transmissions", "edge_sends", "new_words", "rejected", "ignored",
               "graylisted")
 
 
-def prop_words(m: int) -> int:
-    """Words per call (gsx.h): 1, 2, or ceil(m/64) rounded up to a multiple of 4."""
-    w = (m + 63) // 64
-    if w <= 2:
-        return max(w, 1)
-    return (w + 3) & ~3
 
 
 def _torch():
@@ -80,6 +75,15 @@ class DistTransport:
         copy on RCCL, but this path is the one the tests and the rehearsal
         exercise; the copy is small next to the exchange itself)."""
         _parts_via_single(self, recv, recv_splits, send_parts)
+
+    def all_gather(self, t):
+        """-> [rank k's t] (equal shapes on every rank)."""
+        h = self._h(t)
+        out = [h.new_empty(h.shape) for _ in range(self.world)]
+        self.dist.all_gather(out, h, group=self.group)
+        if h is not t:
+            out = [o.to(t.device) for o in out]
+        return out
 
     def all_reduce_sum(self, t):
         h = self._h(t)
@@ -255,10 +259,15 @@ class RangeSharded:
         dev = tp.device
         s2 = torch.zeros((max(self.n_send, 1), 2), dtype=torch.int64, device=dev)
         r2 = torch.zeros((max(self.n_recv, 1), 2), dtype=torch.int64, device=dev)
+        px = getattr(be, "hb_px_enabled", lambda: False)()
         be.hb_begin(tick, now, seed)
+        if px:  # the (A) PRUNEs' PX lists to the receivers' ranks, before their (B)
+            self._px_exchange(0)
         be.hb_pack_ctl(s2)
         tp.all_to_all(r2[: self.n_recv], s2[: self.n_send], self.recv_counts, self.send_counts)
         be.hb_recv(r2)
+        if px:  # the (B) answers' PX lists, before the GRAFT senders' (C)
+            self._px_exchange(1)
         s1 = torch.zeros(max(self.n_send, 1), dtype=torch.int64, device=dev)
         r1 = torch.zeros(max(self.n_recv, 1), dtype=torch.int64, device=dev)
         be.hb_pack_resp(s1)
@@ -271,24 +280,55 @@ class RangeSharded:
         return d, {k: int(t[i]) for i, (k, _) in enumerate(abi.HeartbeatOut._fields_)}
 
 
+    def _px_exchange(self, kind: int):
+        """Peer exchange across shards (gsx_hb_px_*): the PX lists of this rank's
+        cross-shard PRUNEs go to the receivers' ranks (one count all-to-all,
+        one entry all-to-all), which handle them."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        w = be.hb_px_entry_words()
+        cnt = be.hb_px_count(kind, tp.world).astype(np.int64)
+        send = torch.zeros((max(int(cnt.sum()), 1), w), dtype=torch.int32, device=tp.device)
+        be.hb_px_pack(kind, send)
+        sc = torch.tensor(cnt, dtype=torch.int64, device=tp.device)
+        rc = torch.empty(tp.world, dtype=torch.int64, device=tp.device)
+        tp.all_to_all(rc, sc, [1] * tp.world, [1] * tp.world)
+        rcnt = rc.cpu().numpy()
+        n = int(rcnt.sum())
+        recv = torch.zeros((max(n, 1), w), dtype=torch.int32, device=tp.device)
+        tp.all_to_all(recv[:n], send[: int(cnt.sum())], rcnt, cnt)
+        be.hb_px_recv(kind, recv, n)
+
+
 class MessageParallel:
     """Every rank propagates its block of the messages over the full overlay.
 
     The engine runs on a torch stream of its own (set_stream), so its kernels,
-    the credit copies and the collective are ordered on one stream with no
+    the credit copies and the collectives are ordered on one stream with no
     host synchronisation between them.  epoch=False (default): each batch's
     deferred P2/P3/P4 counts are summed over ranks and folded right away (the
     single engine with GSX_CREDIT_NOW, batch by batch).  epoch=True: batches
     only accumulate their counts on every rank; end_epoch() (before a
     heartbeat) sums them with one all-reduce and folds them:
     equal to one engine propagating the same batches with GSX_CREDIT_DEFER and
-    folding once."""
+    folding once.
 
-    def __init__(self, engine, transport, epoch: bool = False):
+    cache=True (default): after a gossipsub batch every replica takes its
+    block out of its message cache, the blocks are all-gathered and every
+    replica Puts the whole batch back (gsx_mcache_put), so every replica's
+    cache — and with it emitGossip and the gossip exchange of its heartbeats —
+    equals one engine's (gossipsub.go:943-944, mcache.go:55-59).  heartbeat()
+    then runs the same round on every replica with no exchange: the replicas'
+    states are equal, so are their decisions (the round is replicated, not
+    split)."""
+
+    def __init__(self, engine, transport, epoch: bool = False, cache: bool = True):
         self.e = engine
         self.tp = transport
         self.epoch = epoch
+        self.cache = cache
         self.pending = False
+        self.gathered_bytes = 0  # cache blocks received (cumulative)
         self._stream = None
         dev = getattr(transport, "device", None)
         if hasattr(engine, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
@@ -301,10 +341,13 @@ class MessageParallel:
 
         return _torch().cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
 
-    def share(self, msgs):
-        m = len(msgs)
+    def bounds(self, m: int):
         r, w = self.tp.rank, self.tp.world
-        return msgs[(m * r) // w : (m * (r + 1)) // w]
+        return (m * r) // w, (m * (r + 1)) // w
+
+    def share(self, msgs):
+        lo, hi = self.bounds(len(msgs))
+        return msgs[lo:hi]
 
     def propagate(self, msgs, cfg: abi.PropConfig):
         with self._on_stream():
@@ -316,11 +359,28 @@ class MessageParallel:
             if credit:
                 c.credit_scores = abi.GSX_CREDIT_DEFER
             out = self.e.propagate(mine, c)[0]
+            if self.cache and cfg.router == abi.GSX_ROUTER_GOSSIPSUB and len(msgs):
+                self._merge_cache(msgs, cfg, len(mine))
             if credit:
                 self.pending = True
                 if not self.epoch:
                     self.end_epoch()
             return out_dict(out), totals(out, self.tp)
+
+    def _merge_cache(self, msgs, cfg, n_mine: int):
+        """One all-gather of the replicas' cache blocks; every replica Puts the whole batch."""
+        m, w = len(msgs), self.tp.world
+        counts = [(m * (k + 1)) // w - (m * k) // w for k in range(w)]
+        pad = max(self.e.mcache_part_size(n) for n in counts)
+        if n_mine:
+            mine, got = self.e.mcache_take_block(pad, self.tp.device)
+            if got != n_mine:
+                raise RuntimeError(f"the newest cached batch holds {got} messages, not this replica's {n_mine}")
+        else:
+            mine = self.e.mcache_empty_block(pad, self.tp.device)
+        blocks = self.tp.all_gather(mine)
+        self.gathered_bytes += (w - 1) * mine.numel() * mine.element_size()
+        self.e.mcache_put(msgs, cfg, blocks, counts)
 
     def end_epoch(self):
         """Sum every rank's pending first receipts, in-window duplicates and
@@ -337,6 +397,16 @@ class MessageParallel:
             self.e.replace_pending_invalid(cnt[2].data_ptr())
             self.e.fold_credits(cnt[0].data_ptr(), cnt[1].data_ptr())
         self.pending = False
+
+    def heartbeat(self, tick: int, now: int, seed: int):
+        """One heartbeat (gossipsub.go:1303-1564, with the gossip exchange when
+        on) on every replica: pending credits are folded first, then each
+        replica runs the whole round on its equal state.  -> (this replica's
+        counters, the round's counters) — the same dict: the round is not split."""
+        self.end_epoch()
+        with self._on_stream():
+            d = self.e.heartbeat(tick, now, seed).as_dict()
+        return d, dict(d)
 
 
 def out_dict(out) -> dict:
@@ -409,6 +479,15 @@ class LocalTransport:
 
     def all_to_all_parts(self, recv, recv_splits, send_parts):
         _parts_via_single(self, recv, recv_splits, send_parts)
+
+    def all_gather(self, t):
+        torch = _torch()
+        c = t.clone()
+        if c.is_cuda:
+            torch.cuda.synchronize(c.device)
+        vals = self._gather(c)
+        self._gather(None)
+        return vals
 
     def all_reduce_sum(self, t):
         vals = self._gather(t.clone())

@@ -798,6 +798,23 @@ int gsx_export_membership(gsx_engine* e, uint64_t* joined, uint64_t* fanout, int
  * ones are kept when the round had more is unspecified); up to cap rows are
  * written. */
 int gsx_hb_set_px_log(gsx_engine* e, size_t cap);
+/* Peer exchange on range shards: a PRUNE of a cross-shard pair carries its PX
+ * list (makePrune, gossipsub.go:1814-1850) to the receiver's rank, whose
+ * handlePrune reads it (:811-843, pxConnect :861-910).  kind 0 = the (A)
+ * PRUNEs, between gsx_hb_begin and gsx_hb_recv; kind 1 = the (B) answers,
+ * between gsx_hb_recv and gsx_hb_end.  Per kind:
+ *   gsx_hb_px_count  entries this rank sends to each rank (host, n_ranks u64);
+ *   gsx_hb_px_pack   writes them to `out` (device), grouped by destination in
+ *                    rank order; an entry is gsx_hb_px_entry_words u32:
+ *                    (receive slot at the destination, topic | kind << 8, n,
+ *                    n peer ids, global) — and handles the PRUNEs whose
+ *                    receiver is local;
+ *   gsx_hb_px_recv   the receivers' side of the entries the other ranks sent.
+ * The counters and PX records summed over ranks equal one engine's round. */
+int gsx_hb_px_entry_words(gsx_engine* e, uint32_t* words);
+int gsx_hb_px_count(gsx_engine* e, uint32_t kind, uint64_t* counts);
+int gsx_hb_px_pack(gsx_engine* e, uint32_t kind, uint32_t* out);
+int gsx_hb_px_recv(gsx_engine* e, uint32_t kind, const uint32_t* entries, uint64_t n);
 int gsx_hb_px_records(gsx_engine* e, uint32_t* out, size_t cap, size_t* n);
 
 /* The tracer's GRAFT / PRUNE calls of the last heartbeat, as topic bit words
@@ -822,6 +839,34 @@ int gsx_mcache_clear(gsx_engine* e);
 #define GSX_ANY_TOPIC 0xFFFFFFFFu
 int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
                    size_t* n_out);
+
+/* Message-parallel replicas (gsx/shard.py MessageParallel): every replica
+ * holds the whole overlay and propagates one block of a gossipsub batch, so
+ * its cache (mcache.go Put, gossipsub.go:943-944) holds that block only.  To
+ * leave every replica's cache — and the heartbeats that read it (emitGossip,
+ * the gossip exchange) — equal to one engine's that propagated the whole
+ * batch, each replica takes its block's rows out of the cache and the blocks
+ * go back in as one batch:
+ *   gsx_mcache_last       the newest cached batch's rows: n_words per node, n_msgs;
+ *   gsx_mcache_copy_last  its cache rows (after the uncache of dropped
+ *                         messages) and its message set's rows (every node
+ *                         that saw each message), [node][n_words] u64 each,
+ *                         into caller device buffers (engine stream order);
+ *   gsx_mcache_pop        drops it (the next message set reuses its serial);
+ *   gsx_mcache_put        Puts msgs[0..m) of cfg's topic as one batch: block k
+ *                         is messages [sum part_msgs[<k], + part_msgs[k]) with
+ *                         its rows (device, [node][words(part_msgs[k])],
+ *                         words() = the propagation's row width, gsx.h
+ *                         gsx_propagate) at cache_parts[k] / set_parts[k].
+ *                         Publishing at unjoined sources (the fanout pick of
+ *                         gossipsub.go:981-998, idempotent) runs for every
+ *                         source of msgs, as the whole call would have.
+ * Unsharded engines, gossipsub batches. */
+int gsx_mcache_last(gsx_engine* e, uint32_t* n_words, uint32_t* n_msgs);
+int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows);
+int gsx_mcache_pop(gsx_engine* e);
+int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
+                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts);
 
 /* Per-launch timing of the fused refresh+score kernel over a region: after
  * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls

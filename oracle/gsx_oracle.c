@@ -1258,6 +1258,49 @@ static int64_t arrival_time(const gsx_prop_config* cfg, uint32_t h) {
     return cfg->now_ns + (int64_t)h * cfg->hop_latency_ns + (h ? (int64_t)(h - 1) * cfg->validation_delay_ns : 0);
 }
 
+/* Publish at a source that has not joined the topic (gossipsub.go:981-998):
+ * its fanout, picked when empty (getPeers(D) of non-direct peers with
+ * score >= PublishThreshold, draws h(seed, 10, source, topic << 24 | k)),
+ * and lastpub = now; once per source at the call start.  score0: the scores
+ * the call starts from (NULL: the current ones). */
+static void fanout_publish(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg,
+                           const double* score0) {
+    if (!(cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < o->T)) return;
+    const uint32_t N = o->n_nodes;
+    const uint32_t t = cfg->topic;
+    uint64_t max_deg = 0;
+    for (uint32_t i = 0; i < N; i++)
+        if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > max_deg) max_deg = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+    uint64_t* tg = (uint64_t*)malloc(sizeof(uint64_t) * (max_deg ? max_deg : 1));
+    uint8_t* done = (uint8_t*)calloc(N ? N : 1, 1);
+    for (size_t k = 0; k < m; k++) {
+        const uint32_t src = msgs[k].source;
+        if (src >= N || done[src] || joined(o, src, t)) continue;
+        done[src] = 1;
+        bool empty = true;
+        for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1] && empty; r++)
+            if (o->fanout[r] >> t & 1) empty = false;
+        if (empty) {
+            int n = 0;
+            for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1]; r++) {
+                const uint8_t ef = o->eflags[r];
+                if (!in_topic(o, (uint64_t)r, t) || !(ef & GSX_EDGE_GOSSIPSUB) || (ef & GSX_EDGE_DIRECT)) continue;
+                const double sc = score0 ? score0[r] : score_pair(o, (uint64_t)r);
+                if (!(sc >= o->th.publish_threshold)) continue;
+                tg[n++] = (uint64_t)r;
+            }
+            orc_rng g = {cfg->seed, 10, src, (uint64_t)t << 24, 0};
+            shuffle_pairs(tg, n, &g);
+            if (n > o->gp.d) n = o->gp.d;
+            for (int i = 0; i < n; i++) o->fanout[tg[i]] |= 1ull << t;
+            if (n > 0) o->fan_has[src] |= 1ull << t;
+        }
+        o->lastpub[(size_t)src * o->T + t] = cfg->now_ns;
+    }
+    free(done);
+    free(tg);
+}
+
 int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out,
                   uint8_t* hop_out, int32_t* from_out) {
     if (cfg->max_hops > GSX_MAX_HOPS || cfg->validation_delay_ns < 0) return GSX_EINVAL;
@@ -1288,38 +1331,7 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
      * call's own credits (P2/P3, and P4 of rejected messages) land at its end. */
     double* score0 = (double*)malloc(sizeof(double) * (o->E ? o->E : 1));
     for (uint64_t r = 0; r < o->E; r++) score0[r] = score_pair(o, r);
-    /* Publish at a source that has not joined the topic (gossipsub.go:981-998):
-     * its fanout, picked when empty (getPeers(D) of non-direct peers with
-     * score >= PublishThreshold, draws h(seed, 10, source, topic << 24 | k)),
-     * and lastpub = now; once per source at the call start */
-    if (cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < o->T) {
-        const uint32_t t = cfg->topic;
-        uint8_t* done = (uint8_t*)calloc(N ? N : 1, 1);
-        for (size_t k = 0; k < m; k++) {
-            const uint32_t src = msgs[k].source;
-            if (src >= N || done[src] || joined(o, src, t)) continue;
-            done[src] = 1;
-            bool empty = true;
-            for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1] && empty; r++)
-                if (o->fanout[r] >> t & 1) empty = false;
-            if (empty) {
-                int n = 0;
-                for (int64_t r = o->row_ptr[src]; r < o->row_ptr[src + 1]; r++) {
-                    const uint8_t ef = o->eflags[r];
-                    if (!in_topic(o, (uint64_t)r, t) || !(ef & GSX_EDGE_GOSSIPSUB) || (ef & GSX_EDGE_DIRECT)) continue;
-                    if (!(score0[r] >= o->th.publish_threshold)) continue;
-                    tg[n++] = (uint64_t)r;
-                }
-                orc_rng g = {cfg->seed, 10, src, (uint64_t)t << 24, 0};
-                shuffle_pairs(tg, n, &g);
-                if (n > o->gp.d) n = o->gp.d;
-                for (int i = 0; i < n; i++) o->fanout[tg[i]] |= 1ull << t;
-                if (n > 0) o->fan_has[src] |= 1ull << t;
-            }
-            o->lastpub[(size_t)src * o->T + t] = cfg->now_ns;
-        }
-        free(done);
-    }
+    fanout_publish(o, msgs, m, cfg, score0);
     /* gossipsub's Publish Puts every message a node processes into its
      * mcache (gossipsub.go:944); one batch entry in window 0 */
     orc_mc_batch* mcb = NULL;
@@ -2678,6 +2690,82 @@ int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_wind
                 }
         }
     *n_out = n;
+    return 0;
+}
+
+/* Message-parallel replicas (gsx.h gsx_mcache_*): the newest cached batch's
+ * cache membership and message-set rows, [node][n_msgs] bytes each; pop;
+ * and Put of a whole batch from its message blocks (block k: the batch's
+ * messages [sum part_msgs[<k], + part_msgs[k]), rows [node][part_msgs[k]]),
+ * with the publish step's fanout pick for every source (idempotent). */
+static orc_mc_batch* mcache_newest(orc_engine* o) {
+    if (!o->mc || o->mc_n == 0 || o->mc[0].nb == 0) return NULL;
+    return &o->mc[0].b[o->mc[0].nb - 1];
+}
+
+int orc_mcache_last(orc_engine* o, uint32_t* n_msgs) {
+    const orc_mc_batch* b = mcache_newest(o);
+    if (!b) return GSX_ESTATE;
+    *n_msgs = b->m;
+    return 0;
+}
+
+int orc_mcache_copy_last(orc_engine* o, uint8_t* cache_rows, uint8_t* set_rows) {
+    const orc_mc_batch* b = mcache_newest(o);
+    if (!b || !b->set) return GSX_ESTATE;
+    memcpy(cache_rows, b->has, (size_t)b->m * b->n);
+    memcpy(set_rows, b->set->seen, (size_t)b->m * b->n);
+    return 0;
+}
+
+int orc_mcache_pop(orc_engine* o) {
+    orc_mc_batch* b = mcache_newest(o);
+    if (!b) return GSX_ESTATE;
+    if (b->set && b->set->serial == o->msg_serial && b->set->refs == 1) o->msg_serial--;
+    batch_free(b);
+    o->mc[0].nb--;
+    return 0;
+}
+
+int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
+                   const uint32_t* part_msgs, const uint8_t* const* cache_parts, const uint8_t* const* set_parts) {
+    if (!o->mc || !m || cfg->router != GSX_ROUTER_GOSSIPSUB) return GSX_EINVAL;
+    size_t tot = 0;
+    for (uint32_t k = 0; k < n_parts; k++) tot += part_msgs[k];
+    if (tot != m) return GSX_EINVAL;
+    fanout_publish(o, msgs, m, cfg, NULL);
+    const uint32_t N = o->n_nodes;
+    orc_mc_window* w0 = &o->mc[0];
+    if (w0->nb == w0->cap) {
+        w0->cap = w0->cap ? 2 * w0->cap : 4;
+        w0->b = (orc_mc_batch*)realloc(w0->b, sizeof(orc_mc_batch) * w0->cap);
+    }
+    orc_mc_batch* b = &w0->b[w0->nb++];
+    b->topic = cfg->topic;
+    b->m = (uint32_t)m;
+    b->n = N;
+    b->ids = (uint64_t*)malloc(sizeof(uint64_t) * m);
+    b->has = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
+    b->set = (orc_msgset*)calloc(1, sizeof(orc_msgset));
+    b->set->serial = ++o->msg_serial;
+    b->set->m = (uint32_t)m;
+    b->set->n = N;
+    b->set->refs = 1;
+    b->set->val = (uint32_t*)malloc(sizeof(uint32_t) * m);
+    b->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
+    for (size_t k = 0; k < m; k++) {
+        b->ids[k] = msgs[k].msg_id;
+        b->set->val[k] = msgs[k].validation;
+    }
+    size_t off = 0;
+    for (uint32_t k = 0; k < n_parts; k++) {
+        const size_t nk = part_msgs[k];
+        for (uint32_t i = 0; i < N && nk; i++) {
+            memcpy(b->has + (size_t)i * m + off, cache_parts[k] + (size_t)i * nk, nk);
+            memcpy(b->set->seen + (size_t)i * m + off, set_parts[k] + (size_t)i * nk, nk);
+        }
+        off += nk;
+    }
     return 0;
 }
 

@@ -25,12 +25,14 @@ def params(**kw):
 
 
 def exchange_run(be, n=300, d=6, T=2, seed=5, ticks=8, hops=2, msgs=24, invalid=0.0, exchange_from=0, prefill=0,
-                 **gp_kw):
+                 runner=None, credit=None, **gp_kw):
     """pc.setup's random mesh; every round: a heartbeat (with the exchange),
     then a gossipsub batch that travels only `hops` hops (so most nodes miss
     it and learn of it by IHAVE), then a refresh.  Rounds before
     `exchange_from` only emit IHAVEs; `prefill` promises per pair are made
     before the first round (the engine's per-pair slots fill and grow).
+    runner: a gsx.shard.MessageParallel over `be` (its propagate and
+    heartbeat replace the backend's); credit: the batches' credit mode.
     Returns per-tick counters
     and snapshots (records, backoff, scores, IHAVEs) plus every node's cached
     ids after the last round."""
@@ -47,11 +49,17 @@ def exchange_run(be, n=300, d=6, T=2, seed=5, ticks=8, hops=2, msgs=24, invalid=
                 gp.gossip_exchange = 0
             be.set_gossipsub_params(gp)
         now = hc.T0 + (3 + k) * S
-        outs.append(be.heartbeat(1 + k, now, seed * 31 + 7).as_dict())
+        if runner is None:
+            outs.append(be.heartbeat(1 + k, now, seed * 31 + 7).as_dict())
+        else:
+            outs.append(runner.heartbeat(1 + k, now, seed * 31 + 7)[0])
         snaps.append(hc.snapshot(be))
         cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % T, max_hops=hops, latency_ms=5, seed=seed + k)
+        if credit is not None:
+            cfg.credit_scores = credit
         cfg.now_ns = now + 100 * MS
-        be.propagate(pc.messages(n, msgs, seed + 1000 * k, invalid=invalid), cfg)
+        ms = pc.messages(n, msgs, seed + 1000 * k, invalid=invalid)
+        (runner or be).propagate(ms, cfg)
         be.refresh(now + 500 * MS)
     cached = [be.mcache_ids(v, abi.GSX_ANY_TOPIC, 5) for v in range(n)]
     return ov, outs, snaps, cached

@@ -241,3 +241,87 @@ def test_sharded_heartbeat_matches_single_engine(gpu_ok, world):
             shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(msgs, cfg))[1],
                             [(r,) for r in runners])
     assert want["grafts"] + want["prunes"] > 0
+
+
+@pytest.mark.parametrize("world,invalid", [(2, 0.0), (3, 0.2)])
+def test_message_parallel_heartbeat_matches_single_engine(gpu_ok, world, invalid):
+    """Message-parallel replicas through propagate -> heartbeat cycles with the
+    gossip exchange on: every replica propagates its block, the cache blocks
+    are all-gathered and Put back whole (gsx_mcache_put, k_mc_merge), the
+    credits are summed and folded, and every replica runs the whole round.
+    Counters, records, backoff, scores, IHAVEs and cached ids == one engine."""
+    import gossip_cases as gc
+
+    kw = dict(n=1500, ticks=4, msgs=150, invalid=invalid)
+    _, want_outs, want_snaps, want_cached = gc.exchange_run(gsx.Engine(2), **kw)
+    assert sum(o["iwant_msgs"] for o in want_outs) > 0 and sum(o["gossip_delivered"] for o in want_outs) > 0
+
+    def run(tp, e):
+        r = shard.MessageParallel(e, tp)
+        _, outs, snaps, cached = gc.exchange_run(e, runner=r, **kw)
+        return outs, snaps, cached, r.gathered_bytes
+
+    res = shard.run_local(world, "cuda:0", run, [(gsx.Engine(2),) for _ in range(world)])
+    for rank, (outs, snaps, cached, gathered) in enumerate(res):
+        assert outs == want_outs, rank
+        for k, (a, b) in enumerate(zip(snaps, want_snaps)):
+            for f in a:
+                assert np.array_equal(np.asarray(a[f]).reshape(-1).view(np.uint8),
+                                      np.asarray(b[f]).reshape(-1).view(np.uint8)), (rank, k, f)
+        for v in range(0, len(cached), 7):
+            assert np.array_equal(np.sort(cached[v]), np.sort(want_cached[v])), (rank, v)
+        assert gathered > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_heartbeat_peer_exchange_matches_single_engine(gpu_ok, world):
+    """WithPeerExchange on range shards: the PX lists of cross-shard PRUNEs
+    travel to the receivers' ranks (gsx_hb_px_*), which apply
+    AcceptPXThreshold and pxConnect.  Counters summed over ranks and the PX
+    connection records of all ranks == one engine; states equal too."""
+    import heartbeat_cases as hc
+
+    n, d, T, seed = 1500, 8, 2, 43
+    ov = pc.overlay(n, d, seed, mix_protocols=True, direct_frac=0.02)
+    gp = hc.be_default_params()
+    gp.do_px = 1
+    full = gsx.Engine(T)
+    app = pc.setup(full, ov, T, seed, mesh_degree=10, disconnect_frac=0.05)
+    full.set_gossipsub_params(gp)
+    full.hb_set_px_log(1 << 20)
+    st0 = full.export_state()
+    E = ov.n_pairs
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        e = gsx.Engine(T)
+        _params(e, T)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(_slice_state(st0, T, E, a, b))
+        e.set_app_scores(app[a:b])
+        e.set_gossipsub_params(gp)
+        e.hb_set_px_log(1 << 20)
+        engines.append((e, a, b))
+    runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
+                              [(e,) for e, _, _ in engines])
+    tot_px = 0
+    for k in range(3):
+        tick, now = 60 + k, pc.T0 + (3 + k) * abi.SECOND
+        want = full.heartbeat(tick, now, seed).as_dict()
+        res = shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.heartbeat(tick, now, seed))[1],
+                              [(r,) for r in runners])
+        assert res[0][1] == want, (k, res[0][1], want)
+        recs = np.concatenate([e.hb_px_records() for e, _, _ in engines])
+        recs = recs[np.lexsort(recs.T[::-1])]
+        assert np.array_equal(recs, full.hb_px_records()), k
+        snap = hc.snapshot(full)
+        for (e, a, b) in engines:
+            got = hc.snapshot(e)
+            for f in abi.STATE_FIELDS:
+                assert np.array_equal(got[f].view(np.uint8), _slice_state(snap, T, E, a, b)[f].view(np.uint8)), (k, f)
+            assert np.array_equal(np.asarray(got["backoff"]).reshape(-1), _slice_te(snap["backoff"], T, E, a, b)), k
+        tot_px += want["px_prunes"]
+    assert tot_px > 0 and want["px_connect"] + want["px_ignored"] >= 0

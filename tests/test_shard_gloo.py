@@ -46,7 +46,7 @@ def _worker(rank, world, port, payload, q):
         from gsx import shard as gs
         from gsx.abi import PropConfig
 
-        cfg = PropConfig(**payload["cfg"])
+        cfg = PropConfig(**payload["cfg"]) if "cfg" in payload else None
         tp = gs.DistTransport("cpu")
         if payload["mode"] == "range":
             import shard_emulator as emu
@@ -62,6 +62,13 @@ def _worker(rank, world, port, payload, q):
                 local, tot = rs.propagate(payload["msgs"], cfg)
                 hop, frm = be.prop_results(len(payload["msgs"]))
                 q.put((rank, local, tot, hop, frm))
+        elif payload["mode"] == "replica_hb":
+            import gossip_cases as gc
+
+            o = orc.Oracle(2)
+            run = gs.MessageParallel(o, tp)
+            _, outs, snaps, cached = gc.exchange_run(o, runner=run, **payload["kw"])
+            q.put((rank, outs, snaps, cached, run.gathered_bytes))
         else:
             o = orc.Oracle(1)
             pc.setup(o, payload["ov"], 1, payload["seed"])
@@ -181,3 +188,28 @@ def test_sharded_heartbeat_exchange_gloo(world):
     owner = np.searchsorted(rank_lo.astype(np.int64), np.arange(n), side="right") - 1
     cross = owner[obs] != owner[ov.col]
     assert sum(r[3] for r in res) == 2 * int(cross.sum()) > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_message_parallel_heartbeat_gloo(world):
+    """Message-parallel replicas with heartbeats: each replica propagates its
+    block of every gossipsub batch, the cache blocks are all-gathered and Put
+    back as whole batches (gsx_mcache_put), and every replica runs the whole
+    heartbeat with the gossip exchange.  Every replica's counters, records,
+    backoff, scores, IHAVEs and cached ids must equal one oracle's over the
+    same rounds (batches that travel two hops: most nodes learn by IHAVE)."""
+    import gossip_cases as gc
+    import heartbeat_cases as hc
+
+    kw = dict(n=240, ticks=4, msgs=30, invalid=0.2, credit=0)
+    _, want_outs, want_snaps, want_cached = gc.exchange_run(orc.Oracle(2), **kw)
+    res = _run(world, dict(mode="replica_hb", kw=kw))
+    assert sum(o["iwant_msgs"] for o in want_outs) > 0 and sum(o["gossip_delivered"] for o in want_outs) > 0
+    for rank, outs, snaps, cached, gathered in res:
+        assert outs == want_outs, rank
+        for k, (a, b) in enumerate(zip(snaps, want_snaps)):
+            for f in list(a):
+                assert np.array_equal(np.asarray(a[f]).reshape(-1).view(np.uint8), np.asarray(b[f]).reshape(-1).view(np.uint8)), (rank, k, f)
+        for v in range(len(cached)):
+            assert np.array_equal(np.sort(cached[v]), np.sort(want_cached[v])), (rank, v)
+        assert gathered > 0

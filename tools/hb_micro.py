@@ -26,12 +26,17 @@ ap.add_argument("--first-tick", type=int, default=61)
 ap.add_argument("--peers", type=int, default=1_000_000)
 ap.add_argument("--topics", type=int, default=8)
 ap.add_argument("--msgs", type=int, default=256)
+ap.add_argument("--exchange", action="store_true", help="the gossip exchange (D) on, as in bench.py")
 a = ap.parse_args()
 
 ov, e = bench.build_engine(a.peers, a.topics, 6, synth.SEED, 0)
 e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                                 accept_px_threshold=0, opportunistic_graft_threshold=5))
 now = bench.T0
+if a.exchange:
+    from gsx import engine as gsx_engine_mod
+
+    e.set_gossipsub_params(gsx_engine_mod.default_gossipsub_params(gossip_exchange=1))
 args = argparse.Namespace(prop_hops=24)
 cfg = bench.prop_config(args, a.peers)
 tick = a.first_tick - 3
@@ -45,5 +50,5 @@ for k in range(3 + a.rounds):
     o = e.heartbeat(tick, now, synth.SEED).as_dict()
     e.sync()
     print(f"tick {tick}: {(time.perf_counter() - t0) * 1e3:.3f} ms grafts={o['grafts']} prunes={o['prunes']} "
-          f"ihave={o['ihave_msgs']}", flush=True)
+          f"ihave={o['ihave_msgs']} iwant={o['iwant_msgs']} delivered={o['gossip_delivered']}", flush=True)
 e.close()
