@@ -385,7 +385,9 @@ struct HbState {
     uint64_t* ihave_tr;    // [pair (u -> v)]: topics whose IHAVE from v was truncated (a GxSub row)
     GxSub gsub;            // k_hb_gossip of one topic: its truncated-list rows (pool null: none kept)
     const GxSub* gsubs;    // [topic]: the exchange's view of every topic's rows
-    uint32_t* gx_err;      // [4]: 0 = a GxSub bound broken (an internal error)
+    uint32_t* gx_err;      // [8]: 0 = a GxSub bound broken (an internal error), 6 = nodes listed in gx_nodes
+    uint32_t* gx_nodes;    // [node]: the nodes with an asked pair (k_gx_ask -> k_gx_receive)
+    uint8_t* gx_mark;      // [pair]: answered pairs (their records took the receipts' credits; re-scored after)
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;

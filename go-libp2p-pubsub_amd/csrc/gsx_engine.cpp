@@ -152,7 +152,7 @@ struct gsx_engine {
     };
     std::deque<std::vector<McBatch>> mc;
     // gossip exchange state (allocated when first enabled)
-    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr;
+    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gx_nodes = nullptr;
     uint32_t* d_gxflag = nullptr;  // [0] a GxSub bound broken, [1] a promise without a slot, [4] slots in use (max)
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
     int64_t* d_prom_e = nullptr;
@@ -546,10 +546,10 @@ void free_state(gsx_engine* e) {
     e->d_tr_acc = e->d_tr_hp = nullptr;
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
-                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got};
+                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
-        e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = nullptr;
+        e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
         e->d_prom_e = nullptr;
         e->prom_slots = 0;
@@ -2717,6 +2717,7 @@ int gx_alloc(gsx_engine* e) {
     if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
         (rc = dalloc(e, &e->d_prom_h, E * S)) || (rc = dalloc(e, &e->d_prom_e, E * S)) ||
         (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) || (rc = dalloc(e, &e->d_gxflag, 8)) ||
+        (rc = dalloc(e, &e->d_gx_nodes, std::max<size_t>(e->n_nodes, 1))) ||
         (rc = dalloc(e, &e->d_sub_cnt, std::max<size_t>(e->T, 1))) ||
         (rc = dalloc(e, &e->d_gsubs, std::max<size_t>(e->T, 1))))
         return rc;
@@ -2930,6 +2931,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.ihave_bits = e->d_ihave_bits;
         h.ihave_tr = e->d_ihave_bits + std::max<size_t>(e->E, 1);
         h.gx_err = e->d_gxflag;
+        h.gx_nodes = e->d_gx_nodes;
         h.prom_occ = e->d_gxflag + 4;
         h.peerhave = e->d_peerhave;
         h.iasked = e->d_iasked;
@@ -3187,6 +3189,12 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                 }
         }
         off[e->T] = (uint32_t)gx.size();
+        static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
+        if (dbg) {
+            fprintf(stderr, "[gx] sets=%zu batches=%zu:", gx_sets.size(), gx.size());
+            for (const auto& g : gx) fprintf(stderr, " (t%u w%u s%u a%u)", g.topic, g.n_words, g.serial, g.avail);
+            fprintf(stderr, "\n");
+        }
         if (gx.size() > e->gx_cap || !e->d_gx) {
             if (e->d_gx) (void)hipFree(e->d_gx);
             if (e->d_gx_off) (void)hipFree(e->d_gx_off);
@@ -3206,11 +3214,22 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         h.gx = e->d_gx;
         h.gx_off = e->d_gx_off;
         h.gsubs = e->d_gsubs;
+        // the answered pairs' records take the receipts' credits: re-scored after
+        // (the rest stays exact), when the scores were exact before
+        const bool exact = e->scores_valid;
+        if (exact) {
+            h.gx_mark = e->d_dirty + 3 * e->E;  // (the broken-promise mask of hb_begin, read by then)
+            HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
+        }
         HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
         for (size_t i = 0; i < gx_sets.size(); ++i)
             HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
                                            e->stream));
-        e->invalidate_scores();  // the receipts credited P2 / P3 / P4
+        if (exact) {  // the receipts credited P2 / P3 / P4 of the answered pairs
+            HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.gx_mark));
+        } else {
+            e->invalidate_scores();
+        }
         ++e->score_gen;
     }
     unsigned long long st[gsx::HB_STAT_WORDS];

@@ -128,195 +128,347 @@ __global__ __launch_bounds__(256) void k_gx_full(const uint64_t* __restrict__ al
     }
 }
 
-// handleIWant at v and the receipt at u of what v sends (pass 2 of
-// k_gx_exchange): the kk ids u asked v for (selection sampling again, the same
-// draws), each still in v's cache delivered / rejected / counted duplicate.
-__device__ __forceinline__ void gx_receive(const DevState& s, const HbState& h, uint32_t u, int64_t r0, int64_t r1,
-                                           uint64_t q, uint32_t r, uint64_t tall, uint32_t kk, uint64_t& served,
-                                           uint64_t& delivered, uint64_t& rejected, uint64_t& dups) {
-    const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
+// The candidate word (batch b, word w) of the ids v advertised to u that u
+// had not seen, within the subset row of a truncated list.
+__device__ __forceinline__ uint64_t gx_word(const GxBatch& b, uint32_t u, uint32_t v, uint32_t w, const uint64_t* sub) {
+    const uint32_t W = b.n_words;
+    uint64_t m = b.mem[(size_t)v * W + w] & ~b.all[(size_t)u * W + w];
+    if (sub) m &= sub[b.row_off + w];
+    return m;
+}
+
+__device__ __forceinline__ const uint64_t* gx_subrow(const HbState& h, uint64_t tr, uint32_t t, uint32_t r) {
+    if (!((tr >> t) & 1)) return nullptr;
+    const GxSub& G = h.gsubs[t];
+    return G.pool + (size_t)G.idx[r] * G.tw;
+}
+
+// |iwant| before the budget: popcounts of the candidate words (no bit walk).
+__device__ __forceinline__ uint32_t gx_count(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q,
+                                             uint32_t r) {
+    const uint64_t tr = h.ihave_tr[q];
+    uint32_t n = 0;
+    for (; tb; tb &= tb - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        const uint64_t* sub = gx_subrow(h, tr, t, r);
+        for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
+            const GxBatch& b = h.gx[g];
+            if (b.full[u]) continue;
+            for (uint32_t w = 0; w < b.n_words; ++w) n += (uint32_t)__popcll(gx_word(b, u, v, w, sub));
+        }
+    }
+    return n;
+}
+
+// The j-th candidate in canonical order (word popcounts, then a bit walk in one word).
+__device__ __forceinline__ void gx_nth(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q, uint32_t r,
+                                       uint32_t j, uint32_t& pick_g, uint32_t& pick_k) {
+    const uint64_t tr = h.ihave_tr[q];
+    for (; tb; tb &= tb - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        const uint64_t* sub = gx_subrow(h, tr, t, r);
+        for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
+            const GxBatch& b = h.gx[g];
+            if (b.full[u]) continue;
+            for (uint32_t w = 0; w < b.n_words; ++w) {
+                uint64_t m = gx_word(b, u, v, w, sub);
+                const uint32_t c = (uint32_t)__popcll(m);
+                if (j >= c) {
+                    j -= c;
+                    continue;
+                }
+                for (; j; --j) m &= m - 1;
+                pick_g = g;
+                pick_k = w * 64 + (uint32_t)__builtin_ctzll(m);
+                return;
+            }
+        }
+    }
+}
+
+// Per-(pair, topic) credits of the received ids, as the one-at-a-time tracer
+// calls would leave them (score.go:894-974): k1 first deliveries (FMD, and MMD
+// in the mesh), k2 accepted duplicates (MMD in the mesh), k4 invalid ones (IMD)
+// — every step of a counter is the same capped +1, so their order is free.
+__device__ __forceinline__ void gx_credit(const DevState& s, uint64_t q, uint32_t t, uint32_t k1, uint32_t k2,
+                                          uint32_t k4) {
+    if (!(k1 | k2 | k4) || !scored_topic(s, q, t)) return;
+    const DevTopicParams& tp = s.tp[t];
+    const size_t b = rec_index(q, t, s.n_topics, FMD);
+    if (k4) s.rec[b + IMD * TILE] = add_ones_capped(s.rec[b + IMD * TILE], k4, __builtin_inf());
+    if (k1) s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], k1, tp.cap2);
+    if ((k1 | k2) && (s.rflags[flag_index(q, t, s.n_topics)] & REC_IN_MESH))
+        s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
+}
+
+// handleIWant at v and the receipt at u, one id at a time (pass 2 for a pair
+// whose asked subset was sampled, kk < n: the same draws select it again),
+// each receipt credited by its own tracer call.
+__device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbState& h, uint32_t u, uint64_t q,
+                                                   uint32_t r, uint64_t tb, uint32_t kk, uint32_t n, uint64_t& served,
+                                                   uint64_t& delivered, uint64_t& rejected, uint64_t& dups) {
     const uint32_t v = (uint32_t)h.col[q];
     const DevGossipParams& gp = h.gp;
-    const uint32_t S = h.prom_slots;
-    uint32_t n = 0;  // |iwant| again (the selection depends on it)
-    gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
-        ++n;
-        return true;
-    });
     Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
     uint32_t i = 0, sel = 0;
     gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
-        bool take = true;
-        if (kk < n) {
-            take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
-            ++i;
-            if (!take) return true;
-        }
+        const bool take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
+        ++i;
+        if (!take) return true;
         ++sel;
         const GxBatch& b = h.gx[gi];
-        // no longer in v's cache; or GetForPeer's count (1: every (peer,
-        // message) is asked at most once per answer it can receive) above
-        // GossipRetransmission
-        if (!b.avail || gp.retransmission < 1) return sel < kk || kk == n;
+        // no longer in v's cache; or GetForPeer's count above GossipRetransmission
+        if (!b.avail || gp.retransmission < 1) return sel < kk;
         ++served;
         const uint32_t W = b.n_words, t = b.topic, val = b.val[k];
         uint64_t* xw = b.x + (size_t)u * W + k / 64;
         const uint64_t bit = 1ull << (k % 64);
         if (*xw & bit) {  // DuplicateMessage
             ++dups;
-            if (val == VAL_ACCEPT) ev_mesh(s, (uint64_t)q, t);
-            else if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+            if (val == VAL_ACCEPT) ev_mesh(s, q, t);
+            else if (val == VAL_REJECT) ev_invalid(s, q, t);
         } else {
             *xw |= bit;
-            // fulfillPromise (:119-126): every promise of u for this message
-            const uint64_t handle = ((uint64_t)b.serial << 32) | k;
-            for (int64_t p = r0; p < r1; ++p)
-                for (uint32_t z = 0; z < S; ++z)
-                    if (h.prom_e[(size_t)p * S + z] != 0 && h.prom_h[(size_t)p * S + z] == handle)
-                        h.prom_e[(size_t)p * S + z] = 0;
             if (val == VAL_ACCEPT) {
                 ++delivered;
-                ev_first(s, (uint64_t)q, t);
+                ev_first(s, q, t);
                 *b.got = 1;
             } else {
                 ++rejected;
-                if (val == VAL_REJECT) ev_invalid(s, (uint64_t)q, t);
+                if (val == VAL_REJECT) ev_invalid(s, q, t);
             }
         }
-        return sel < kk || kk == n;
+        return sel < kk;
     });
 }
 
-__global__ __launch_bounds__(64) void k_gx_exchange(DevState s, HbState h) {
+// Pass 1, one lane per receiving node u: handleIHave (:615-679) for the one
+// IHAVE RPC each sender v sent (every topic), senders ascending: the score /
+// MaxIHaveMessages / iasked gates, |iwant| from word popcounts, the asked
+// subset (all; or a uniform kk-subset by selection sampling) and AddPromise's
+// pick (gossip_tracer.go:53).  Pairs with nothing asked are cleared here
+// (clearIHaveCounters, :1566-1576, then finds them zero); a node with an asked
+// pair is listed for pass 2.
+__global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
     const DevGossipParams& gp = h.gp;
     const uint32_t S = h.prom_slots;
-    uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0, served = 0, delivered = 0, rejected = 0, dups = 0;
+    uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0;
     uint32_t occ = 0;
     for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        // ---- pass 1: handleIHave (:615-679), senders ascending
+        bool asked = false;
         for (int64_t q = r0; q < r1; ++q) {
             const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
             if (!tall) continue;
+            uint32_t kk = 0;
             const uint32_t r = h.rev[q];
-            if (r == NO_PAIR || (r & HALO)) continue;
-            const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
-            if (s.score[q] < h.gossip_threshold) {  // :617-621
-                ++ignored;
-                continue;
-            }
-            const uint32_t ph = h.peerhave[q] + 1;  // :624-628
-            h.peerhave[q] = ph;
-            if ((int64_t)ph > (int64_t)gp.max_ihave_msgs) {
-                ++ignored;
-                continue;
-            }
-            const uint32_t ia = h.iasked[q];
-            if ((int64_t)ia >= (int64_t)gp.max_ihave) {  // :630-633
-                ++ignored;
-                continue;
-            }
-            const uint32_t v = (uint32_t)h.col[q];
-            uint32_t n = 0;
-            gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
-                ++n;
-                return true;
-            });
-            if (n == 0) continue;  // :652-654
-            const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)ia);
-            const uint32_t kk = n < budget ? n : budget;
-            Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
-            // the asked subset: all, or a uniform kk-subset by selection sampling;
-            // then AddPromise's pick (gossip_tracer.go:53)
-            uint32_t pick_g = 0, pick_k = 0;
-            if (kk == n) {
-                const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-                uint32_t i = 0;
-                gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
-                    if (i++ < j) return true;
-                    pick_g = gi;
-                    pick_k = k;
-                    return false;
-                });
-            } else {
-                uint32_t i = 0, sel = 0;
-                gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
-                    if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
-                    ++i;
-                    return sel < kk;
-                });
-                const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-                Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
-                i = 0;
-                sel = 0;
-                gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
-                    const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
-                    ++i;
-                    if (!take) return true;
-                    if (sel++ < j) return true;
-                    pick_g = gi;
-                    pick_k = k;
-                    return false;
-                });
-            }
-            h.iasked[q] = ia + kk;
-            h.gx_req[q] = kk;
-            ++iw_msgs;
-            iw_ids += kk;
-            // AddPromise (:59-74): once per (message, peer); the host keeps a
-            // free slot on every pair before each exchange (one promise per pair)
-            const uint64_t handle = ((uint64_t)h.gx[pick_g].serial << 32) | pick_k;
-            uint64_t* ph_ = h.prom_h + (size_t)q * S;
-            int64_t* pe_ = h.prom_e + (size_t)q * S;
-            int free_slot = -1;
-            bool have = false;
-            uint32_t used = 0;
-            for (uint32_t k = 0; k < S; ++k) {
-                if (pe_[k] == 0) {
-                    if (free_slot < 0) free_slot = (int)k;
-                } else {
-                    ++used;
-                    if (ph_[k] == handle) have = true;
+            do {
+                if (r == NO_PAIR || (r & HALO)) break;
+                const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
+                if (s.score[q] < h.gossip_threshold) {  // :617-621
+                    ++ignored;
+                    break;
                 }
+                const uint32_t ph = h.peerhave[q] + 1;  // :624-628
+                if ((int64_t)ph > (int64_t)gp.max_ihave_msgs) {
+                    ++ignored;
+                    break;
+                }
+                const uint32_t ia = h.iasked[q];
+                if ((int64_t)ia >= (int64_t)gp.max_ihave) {  // :630-633
+                    ++ignored;
+                    break;
+                }
+                const uint32_t v = (uint32_t)h.col[q];
+                const uint32_t n = gx_count(h, tb, u, v, q, r);
+                if (n == 0) break;  // :652-654
+                const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)ia);
+                kk = n < budget ? n : budget;
+                Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+                uint32_t pick_g = 0, pick_k = 0;
+                if (kk == n) {
+                    gx_nth(h, tb, u, v, q, r, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
+                } else {
+                    uint32_t i = 0, sel = 0;
+                    gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
+                        if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
+                        ++i;
+                        return sel < kk;
+                    });
+                    const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
+                    Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
+                    i = 0;
+                    sel = 0;
+                    gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
+                        const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
+                        ++i;
+                        if (!take) return true;
+                        if (sel++ < j) return true;
+                        pick_g = gi;
+                        pick_k = k;
+                        return false;
+                    });
+                }
+                ++iw_msgs;
+                iw_ids += kk;
+                // AddPromise (:59-74): once per (message, peer); the host keeps a
+                // free slot on every pair before each exchange (one promise per pair)
+                const uint64_t handle = ((uint64_t)h.gx[pick_g].serial << 32) | pick_k;
+                uint64_t* ph_ = h.prom_h + (size_t)q * S;
+                int64_t* pe_ = h.prom_e + (size_t)q * S;
+                int free_slot = -1;
+                bool have = false;
+                uint32_t used = 0;
+                for (uint32_t k = 0; k < S; ++k) {
+                    if (pe_[k] == 0) {
+                        if (free_slot < 0) free_slot = (int)k;
+                    } else {
+                        ++used;
+                        if (ph_[k] == handle) have = true;
+                    }
+                }
+                if (!have && free_slot >= 0) {
+                    ph_[free_slot] = handle;
+                    pe_[free_slot] = h.now + gp.followup_ns;
+                    ++used;
+                } else if (!have) {
+                    h.gx_err[1] = 1;  // (the host's invariant broken: never)
+                }
+                occ = used > occ ? used : occ;
+            } while (false);
+            if (kk) {  // pass 2 reads the pair's bits, then clears them
+                h.peerhave[q] += 1;
+                h.iasked[q] += kk;
+                h.gx_req[q] = kk;
+                asked = true;
+            } else {
+                h.ihave_bits[q] = h.ihave_tr[q] = 0;
+                h.peerhave[q] = h.iasked[q] = 0;
             }
-            if (!have && free_slot >= 0) {
-                ph_[free_slot] = handle;
-                pe_[free_slot] = h.now + gp.followup_ns;
-                ++used;
-            } else if (!have) {
-                h.gx_err[1] = 1;  // (the host's invariant broken: never)
-            }
-            occ = used > occ ? used : occ;
         }
-        // ---- pass 2: v answers (handleIWant :681-716), u receives, senders ascending;
-        // the pair's IHAVE bits and counters are cleared once read (clearIHaveCounters
-        // :1566-1576 then finds them zero: the host skips its memsets)
-        for (int64_t q = r0; q < r1; ++q) {
-            const uint64_t tall = h.ihave_bits[q];
-            if (!tall) continue;
-            const uint32_t kk = h.gx_req[q];
-            if (kk) h.gx_req[q] = 0;
-            const uint32_t r = h.rev[q];
-            const bool answered = kk && !(s.score[r] < h.gossip_threshold) &&           // v ignores u's IWANT
-                                  ((h.eflags[q] & EDGE_DIRECT) || !(s.score[q] < h.graylist));  // AcceptFrom at u
-            if (answered) gx_receive(s, h, u, r0, r1, q, r, tall, kk, served, delivered, rejected, dups);
-            h.ihave_bits[q] = h.ihave_tr[q] = 0;
-            h.peerhave[q] = h.iasked[q] = 0;
-        }
+        if (asked) h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u;
     }
     gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);
     gx_flush(h.stats, HB_IWANT_MSGS, iw_msgs);
     gx_flush(h.stats, HB_IWANT_IDS, iw_ids);
-    gx_flush(h.stats, HB_IWANT_SERVED, served);
-    gx_flush(h.stats, HB_GOSSIP_DELIVERED, delivered);
-    gx_flush(h.stats, HB_GOSSIP_REJECTED, rejected);
-    gx_flush(h.stats, HB_GOSSIP_DUPLICATES, dups);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o = (uint32_t)__shfl_xor((int)occ, off, 64);
         occ = o > occ ? o : occ;
     }
     if ((threadIdx.x % 64) == 0 && occ) atomicMax(h.prom_occ, occ);
+}
+
+// Pass 2, one wave per listed node u: v answers u's IWANT (handleIWant
+// :681-716: its score of u, its cache after the Shift) and u receives the
+// answer, senders ascending.  A pair that asked for everything it lacked (kk
+// = n, the common case) is received word-parallel: lane i takes the words i,
+// i + 64, ... of each advertised batch (a batch word always goes to the same
+// lane, so a later pair's duplicate test reads what that lane wrote); per
+// topic the lanes' first deliveries, accepted duplicates and invalid ones are
+// summed and credited once (gx_credit).  A sampled pair (kk < n) is received
+// by lane 0 one id at a time.  Then fulfillPromise (:119-126) for every id u
+// received this exchange: the node's promise slots whose message is now in
+// its receipt rows (promises are only added in pass 1).
+__global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t S = h.prom_slots;
+    const DevGossipParams& gp = h.gp;
+    uint64_t served = 0, delivered = 0, rejected = 0, dups = 0;
+    const uint32_t n_list = h.gx_err[6];
+    const uint32_t n_gx = h.gx_off[s.n_topics];
+    for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+        const uint32_t u = h.gx_nodes[li];
+        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        for (int64_t q = r0; q < r1; ++q) {
+            const uint32_t kk = h.gx_req[q];  // (wave-uniform)
+            if (!kk) continue;
+            const uint64_t tall = h.ihave_bits[q];
+            const uint32_t r = h.rev[q];
+            const bool answered = !(s.score[r] < h.gossip_threshold) &&  // v ignores u's IWANT
+                                  ((h.eflags[q] & EDGE_DIRECT) || !(s.score[q] < h.graylist));  // AcceptFrom at u
+            const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
+            if (answered) {
+                const uint32_t v = (uint32_t)h.col[q];
+                const uint32_t n = gx_count(h, tb, u, v, q, r);  // (uniform: every lane counts)
+                if (kk == n) {
+                    const uint64_t tr = h.ihave_tr[q];
+                    for (uint64_t tm = tb; tm; tm &= tm - 1) {
+                        const uint32_t t = (uint32_t)__builtin_ctzll(tm);
+                        const uint64_t* sub = gx_subrow(h, tr, t, r);
+                        uint32_t k1 = 0, k2 = 0, k4 = 0;
+                        for (uint32_t gi = h.gx_off[t]; gi < h.gx_off[t + 1]; ++gi) {
+                            const GxBatch& b = h.gx[gi];
+                            const uint32_t W = b.n_words;
+                            if (!b.avail || gp.retransmission < 1 || b.full[u]) continue;
+                            bool got = false;
+                            for (uint32_t w = lane; w < W; w += 64) {
+                                const uint64_t m = gx_word(b, u, v, w, sub);
+                                if (!m) continue;
+                                uint64_t* xw = b.x + (size_t)u * W + w;
+                                const uint64_t x0 = *xw;
+                                *xw = x0 | m;
+                                served += (uint64_t)__popcll(m);
+                                for (uint64_t z = m & ~x0; z; z &= z - 1) {
+                                    const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
+                                    if (val == VAL_ACCEPT) {
+                                        ++delivered;
+                                        ++k1;
+                                        got = true;
+                                    } else {
+                                        ++rejected;
+                                        if (val == VAL_REJECT) ++k4;
+                                    }
+                                }
+                                for (uint64_t z = m & x0; z; z &= z - 1) {  // DuplicateMessage
+                                    const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
+                                    ++dups;
+                                    if (val == VAL_ACCEPT) ++k2;
+                                    else if (val == VAL_REJECT) ++k4;
+                                }
+                            }
+                            if (got) *b.got = 1;
+                        }
+#pragma unroll
+                        for (int off = 32; off > 0; off >>= 1) {
+                            k1 += (uint32_t)__shfl_xor((int)k1, off, 64);
+                            k2 += (uint32_t)__shfl_xor((int)k2, off, 64);
+                            k4 += (uint32_t)__shfl_xor((int)k4, off, 64);
+                        }
+                        if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
+                    }
+                } else if (lane == 0) {
+                    gx_receive_sampled(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
+                }
+                __threadfence_block();  // this pair's receipts before the next pair's duplicate tests
+            }
+            if (lane == 0) {
+                if (answered && h.gx_mark) h.gx_mark[q] = 1;
+                h.gx_req[q] = 0;
+                h.ihave_bits[q] = h.ihave_tr[q] = 0;
+                h.peerhave[q] = h.iasked[q] = 0;
+            }
+        }
+        __threadfence_block();
+        // fulfillPromise: u's promises whose message u received in this exchange
+        const uint64_t slots = (uint64_t)(r1 - r0) * S;
+        for (uint64_t i = lane; i < slots; i += 64) {
+            const size_t z = (size_t)r0 * S + i;
+            if (h.prom_e[z] == 0) continue;
+            const uint64_t hd = h.prom_h[z];
+            const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
+            for (uint32_t gi = 0; gi < n_gx; ++gi) {
+                const GxBatch& b = h.gx[gi];
+                if (b.serial != ser) continue;
+                if ((b.x[(size_t)u * b.n_words + k / 64] >> (k % 64)) & 1) h.prom_e[z] = 0;
+                break;
+            }
+        }
+    }
+    gx_flush(h.stats, HB_IWANT_SERVED, served);
+    gx_flush(h.stats, HB_GOSSIP_DELIVERED, delivered);
+    gx_flush(h.stats, HB_GOSSIP_REJECTED, rejected);
+    gx_flush(h.stats, HB_GOSSIP_DUPLICATES, dups);
 }
 
 // The exchange's receipts into the message set: seen |= x; the receipt rows
@@ -344,7 +496,9 @@ hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t s
 
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gx_exchange, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
+    hipLaunchKernelGGL(k_gx_ask, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
+    // the listed nodes (their count is on the device): a wave each, grid-stride
+    hipLaunchKernelGGL(k_gx_receive, dim3(4096), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
 
