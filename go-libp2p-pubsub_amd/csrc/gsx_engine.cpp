@@ -2940,7 +2940,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.prom_e = e->d_prom_e;
         h.prom_slots = e->prom_slots;
         h.gsubs = e->d_gsubs;
-        if (!e->gx_clean) HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
+        // the IHAVE topic bits of the last round (one bulk clear: cheaper than the
+        // exchange clearing the pairs it read one by one)
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32, e->stream));
         e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
     }

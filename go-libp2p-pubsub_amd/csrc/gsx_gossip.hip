@@ -143,17 +143,27 @@ __device__ __forceinline__ const uint64_t* gx_subrow(const HbState& h, uint64_t 
     return G.pool + (size_t)G.idx[r] * G.tw;
 }
 
+// The advertised batches a receiver has not seen whole: bit g of the mask
+// (batches past 64 always walked); every other batch holds no candidate.
+__device__ __forceinline__ uint64_t gx_unseen(const HbState& h, uint32_t n_gx, uint32_t u) {
+    uint64_t nf = n_gx > 64 ? ~0ull : 0ull;
+    for (uint32_t g = 0; g < n_gx && g < 64; ++g)
+        if (!h.gx[g].full[u]) nf |= 1ull << g;
+    return nf;
+}
+__device__ __forceinline__ bool gx_skip(uint64_t nf, uint32_t g) { return g < 64 && !((nf >> g) & 1); }
+
 // |iwant| before the budget: popcounts of the candidate words (no bit walk).
 __device__ __forceinline__ uint32_t gx_count(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q,
-                                             uint32_t r) {
+                                             uint32_t r, uint64_t nf) {
     const uint64_t tr = h.ihave_tr[q];
     uint32_t n = 0;
     for (; tb; tb &= tb - 1) {
         const uint32_t t = (uint32_t)__builtin_ctzll(tb);
         const uint64_t* sub = gx_subrow(h, tr, t, r);
         for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
+            if (gx_skip(nf, g)) continue;
             const GxBatch& b = h.gx[g];
-            if (b.full[u]) continue;
             for (uint32_t w = 0; w < b.n_words; ++w) n += (uint32_t)__popcll(gx_word(b, u, v, w, sub));
         }
     }
@@ -162,14 +172,14 @@ __device__ __forceinline__ uint32_t gx_count(const HbState& h, uint64_t tb, uint
 
 // The j-th candidate in canonical order (word popcounts, then a bit walk in one word).
 __device__ __forceinline__ void gx_nth(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q, uint32_t r,
-                                       uint32_t j, uint32_t& pick_g, uint32_t& pick_k) {
+                                       uint64_t nf, uint32_t j, uint32_t& pick_g, uint32_t& pick_k) {
     const uint64_t tr = h.ihave_tr[q];
     for (; tb; tb &= tb - 1) {
         const uint32_t t = (uint32_t)__builtin_ctzll(tb);
         const uint64_t* sub = gx_subrow(h, tr, t, r);
         for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
+            if (gx_skip(nf, g)) continue;
             const GxBatch& b = h.gx[g];
-            if (b.full[u]) continue;
             for (uint32_t w = 0; w < b.n_words; ++w) {
                 uint64_t m = gx_word(b, u, v, w, sub);
                 const uint32_t c = (uint32_t)__popcll(m);
@@ -254,8 +264,10 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
     const uint32_t S = h.prom_slots;
     uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0;
     uint32_t occ = 0;
+    const uint32_t n_gx = h.gx_off[s.n_topics];
     for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        const uint64_t nf = gx_unseen(h, n_gx, u);  // nothing unseen: no IHAVE of u asks for anything
         bool asked = false;
         for (int64_t q = r0; q < r1; ++q) {
             const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
@@ -279,15 +291,16 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                     ++ignored;
                     break;
                 }
+                if (!nf) break;
                 const uint32_t v = (uint32_t)h.col[q];
-                const uint32_t n = gx_count(h, tb, u, v, q, r);
+                const uint32_t n = gx_count(h, tb, u, v, q, r, nf);
                 if (n == 0) break;  // :652-654
                 const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)ia);
                 kk = n < budget ? n : budget;
                 Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
                 uint32_t pick_g = 0, pick_k = 0;
                 if (kk == n) {
-                    gx_nth(h, tb, u, v, q, r, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
+                    gx_nth(h, tb, u, v, q, r, nf, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
                 } else {
                     uint32_t i = 0, sel = 0;
                     gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
@@ -336,14 +349,11 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                 }
                 occ = used > occ ? used : occ;
             } while (false);
-            if (kk) {  // pass 2 reads the pair's bits, then clears them
-                h.peerhave[q] += 1;
-                h.iasked[q] += kk;
+            // (a pair's IHAVE counters only matter within this one RPC: none is
+            // kept; the IHAVE bits are cleared before the next round's gossip)
+            if (kk) {
                 h.gx_req[q] = kk;
                 asked = true;
-            } else {
-                h.ihave_bits[q] = h.ihave_tr[q] = 0;
-                h.peerhave[q] = h.iasked[q] = 0;
             }
         }
         if (asked) h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u;
@@ -380,6 +390,7 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
     for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
         const uint32_t u = h.gx_nodes[li];
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
+        const uint64_t nf = gx_unseen(h, n_gx, u);
         for (int64_t q = r0; q < r1; ++q) {
             const uint32_t kk = h.gx_req[q];  // (wave-uniform)
             if (!kk) continue;
@@ -390,7 +401,7 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
             const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
             if (answered) {
                 const uint32_t v = (uint32_t)h.col[q];
-                const uint32_t n = gx_count(h, tb, u, v, q, r);  // (uniform: every lane counts)
+                const uint32_t n = gx_count(h, tb, u, v, q, r, nf);  // (uniform: every lane counts)
                 if (kk == n) {
                     const uint64_t tr = h.ihave_tr[q];
                     for (uint64_t tm = tb; tm; tm &= tm - 1) {
@@ -400,7 +411,7 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
                         for (uint32_t gi = h.gx_off[t]; gi < h.gx_off[t + 1]; ++gi) {
                             const GxBatch& b = h.gx[gi];
                             const uint32_t W = b.n_words;
-                            if (!b.avail || gp.retransmission < 1 || b.full[u]) continue;
+                            if (!b.avail || gp.retransmission < 1 || gx_skip(nf, gi)) continue;
                             bool got = false;
                             for (uint32_t w = lane; w < W; w += 64) {
                                 const uint64_t m = gx_word(b, u, v, w, sub);
@@ -445,8 +456,6 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
             if (lane == 0) {
                 if (answered && h.gx_mark) h.gx_mark[q] = 1;
                 h.gx_req[q] = 0;
-                h.ihave_bits[q] = h.ihave_tr[q] = 0;
-                h.peerhave[q] = h.iasked[q] = 0;
             }
         }
         __threadfence_block();

@@ -1425,12 +1425,11 @@ __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
             bool live = false, nopx = false, outb = false;
             uint32_t r = NO_PAIR;
             uint64_t cand = 0, prn = 0, inm = 0, scd = 0, resp = 0;
-            if (q < r1) {
-                bool act = true;
-                if (!h.halo_ctl) {
-                    act = h.inbox[q] != 0;
-                    if (act) h.inbox[q] = 0;
-                }
+            // unsharded, only marked pairs carry control: a chunk without one is done
+            const bool act = q < r1 && (h.halo_ctl || h.inbox[q] != 0);
+            if (!((__ballot(act) >> gbase) & ((1ull << RG) - 1))) continue;  // (group-uniform)
+            if (act) {
+                if (!h.halo_ctl) h.inbox[q] = 0;
                 uint64_t grafts = 0, prunes = 0;
                 if (act && recv_control(h, (uint64_t)q, true, r, grafts, prunes)) {
                     nopx = h.sub && (grafts & ~h.sub[u]);  // doPX = false (:721-781)
@@ -1440,7 +1439,7 @@ __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
                     }
                     const double score = (grafts | prunes) ? s.score[q] : 0.0;
                     const uint8_t ef = (grafts | prunes) ? h.eflags[q] : 0;
-                    if ((grafts | prunes) && ((ef & EDGE_DIRECT) || score >= h.graylist)) {
+                    if ((grafts | prunes) && ((ef & EDGE_DIRECT) || !(score < h.graylist))) {
                         live = true;
                         h.dirty[q] = 1;
                         outb = ef & EDGE_OUTBOUND;
