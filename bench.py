@@ -66,9 +66,22 @@ def build_engine(n, T, d, seed, device):
     return ov, e
 
 
+def load_pmc():
+    """The PMC byte counts of tools/pmc_r03.sh committed under profiles/
+    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or {}."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_r03.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def load_traffic(cfg_key):
     """Per-launch HBM bytes of the fused kernel from the rocprofv3 PMC pass
     committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)."""
+    pm = load_pmc().get("k_refresh_score<8, true>")
+    if pm and load_pmc().get("config") == cfg_key:
+        return pm["hbm_bytes_per_launch"]
     path = os.path.join(ROOT, "profiles", "pmc_refresh_score.json")
     try:
         with open(path) as f:
@@ -188,6 +201,15 @@ def prop_config(args, n):
                           credit_scores=abi.GSX_CREDIT_NOW, randomsub_size=n, seed=synth.SEED)
 
 
+def with_traffic(roof, traffic, ms):
+    """Adds the PMC-measured bytes (profiles/pmc_r03.json) beside the algorithmic ones."""
+    if roof is not None and traffic and ms:
+        ach = traffic / (ms * 1e-3) / 1e9
+        roof.update(traffic=traffic, achieved_traffic=ach, frac_traffic=ach / HBM_PEAK_GBS,
+                    traffic_source="profiles/pmc_r03.json (tools/pmc_r03.sh)")
+    return roof
+
+
 def prop_roofline(tot, msgs, kernel_ms):
     """SURVEY.md §8d push-minimal bytes: 8 per frontier (vertex, word), 12 per
     eligible (edge, word) send, 16 per (vertex, word) gaining bits; the
@@ -227,7 +249,9 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     cfg = prop_config(args, n)
     M = args.prop_msgs * world
     tp = shard_mod.DistTransport(dev, stage_host=args.rehearse) if dist is not None else None
-    runner = shard_mod.MessageParallel(e, tp) if tp is not None else None
+    # no heartbeat follows this leg: the replicas' cache blocks are not merged
+    # (MessageParallel(cache=True) all-gathers them for replicated heartbeats)
+    runner = shard_mod.MessageParallel(e, tp, cache=False) if tp is not None else None
 
     def once(b):
         msgs = prop_messages(n, M, synth.SEED, first=b * M)
@@ -256,7 +280,8 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     return {
         "variants": legs,
         "metric": "msg deliveries/s",
-        "mode": "message-parallel replicas (weak): full overlay per GPU, own messages, one all-reduce of credits",
+        "mode": "message-parallel replicas (weak): full overlay per GPU, own messages, one all-reduce of credits "
+                "(cache blocks not merged: no heartbeat in this leg)",
         "value": dl / el,
         "peers": n,
         "messages_per_batch_per_gpu": args.prop_msgs,
@@ -265,7 +290,8 @@ def prop_replica(args, rank, world, local, dist, dev, th):
         "duplicates_per_batch": tot["duplicates"],
         "hops": tot["hops"],
         "router": "gossipsub (synthesized mesh, ~6 of ~12 peers), P2/P3 credits on",
-        "roofline_rank0": prop_roofline(loc, mine, loc["hop_kernel_ms"]),
+        "roofline_rank0": with_traffic(prop_roofline(loc, mine, loc["hop_kernel_ms"]),
+                                       load_pmc().get("p1024", {}).get("hop_bytes_per_batch"), loc["hop_kernel_ms"]),
     }
 
 
@@ -290,7 +316,7 @@ def prop_leg(e, n, M, cfg, steps, seed, first):
     return {"value": sum(o["deliveries"] for o in outs) / el, "unit": "msg deliveries/s", "messages_per_batch": M,
             "ms_per_batch": el / steps * 1e3, "hop_kernel_ms_per_batch": kms, "hops": last["hops"],
             "deliveries_per_batch": last["deliveries"], "duplicates_per_batch": last["duplicates"],
-            "graylisted_per_batch": last["graylisted"], "roofline": prop_roofline(last, msgs, last["hop_kernel_ms"])}
+            "graylisted_per_batch": last["graylisted"], "roofline": prop_roofline(last, msgs, kms)}
 
 
 def prop_variant_legs(args, e, n):
@@ -303,6 +329,8 @@ def prop_variant_legs(args, e, n):
     out = {}
     cfg = prop_config(args, n)
     out["gossipsub_64msg"] = prop_leg(e, n, 64, cfg, 4 * steps, seed, 10_000_000)
+    with_traffic(out["gossipsub_64msg"]["roofline"], load_pmc().get("p64", {}).get("hop_bytes_per_batch"),
+                 out["gossipsub_64msg"]["hop_kernel_ms_per_batch"])
     fcfg = prop_config(args, n)
     fcfg.router = abi.GSX_ROUTER_FLOODSUB
     out["floodsub_1024msg"] = prop_leg(e, n, args.prop_msgs, fcfg, steps, seed, 20_000_000)
@@ -710,7 +738,8 @@ def main():
             "gossip_delivered_per_round": mean([r["gossip_delivered"] for r in rounds]),
             "steady_ms_per_round": steady_ms,
             "active_ms_per_round": active_ms,
-            "roofline_steady": roof(steady_ms),
+            "roofline_steady": with_traffic(roof(steady_ms), load_pmc().get("heartbeat_last_round", {}).get("hbm_bytes"),
+                                            steady_ms),
             "roofline_active": roof(active_ms),
             "per_round": rounds,
             "settle_per_round": [{k: r[k] for k in ("tick", "ms", "grafts", "prunes")} for r in settle],

@@ -260,6 +260,13 @@ hipError_t launch_prop_dup_rows(const PropState& ps, uint64_t* out, hipStream_t 
 hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st);
 
 // ---- heartbeat (gsx_heartbeat.hip) -------------------------------------------
+// A round whose (A) sent more control messages than pairs / 32 leaves the
+// control words for one bulk clear at the next round's start: (B) does not
+// clear them one by one (a scattered line write per message).
+__host__ __device__ __forceinline__ bool hb_bulk_round(unsigned long long grafts, unsigned long long prunes,
+                                                       uint64_t n_pairs) {
+    return grafts + prunes > n_pairs / 32;
+}
 constexpr int HB_LANE_DEG = 64;     // units up to this degree: one lane each, row staged in LDS
 constexpr int HB_HUB_MAX = 12000;   // hub rows (one wave each) live in dynamic LDS: 13 B per pair
 constexpr int64_t HEARTBEAT_INTERVAL_NS = 1000000000LL;  // GossipSubHeartbeatInterval (clearBackoff slack)
@@ -315,6 +322,9 @@ struct GxBatch {
     const uint8_t* full;  // [node]: the node has seen every message of the set (nothing to ask)
     uint32_t n_words, serial, topic, avail;  // avail: still cached after this heartbeat's Shift
     uint32_t row_off;     // word offset of the batch in its topic's gossip rows (GxSub)
+    uint32_t woff;        // word offset of the batch in the flat word list of all advertised batches
+    uint32_t n_msgs;      // messages of the set (bits of the last word past it are never set)
+    const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_common)
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
@@ -357,8 +367,8 @@ struct HbState {
     const uint8_t* eflags;
     int64_t* backoff;     // [topic][pair] expiry, 0 = no entry
     uint8_t* bo8;         // [topic / 8][pair]: bit topic % 8, backoff entry present (kept with `backoff`; 4-B aligned)
-    uint64_t* ctl_graft;  // per pair (v -> u): bit t = v sent GRAFT(t) this round
-    uint64_t* ctl_prune;  // per pair (v -> u): bit t = v sent PRUNE(t)
+    uint64_t* ctl;        // [pair][2] (v -> u): bit t of [0] = v sent GRAFT(t) this round, of [1] PRUNE(t)
+                          // (one 16-B load per control message: (B) reads both)
     uint64_t* resp;       // per pair (u -> v): bit t = u answers v's GRAFT(t) with PRUNE
     const uint64_t* halo_ctl;   // [receive slot][2]: GRAFT / PRUNE bits of remote senders (shards)
     const uint64_t* halo_resp;  // [receive slot]: PRUNE answers of remote receivers (shards)
@@ -388,6 +398,7 @@ struct HbState {
     uint32_t* gx_err;      // [8]: 0 = a GxSub bound broken (an internal error), 6 = nodes listed in gx_nodes
     uint32_t* gx_nodes;    // [node]: the nodes with an asked pair (k_gx_ask -> k_gx_receive)
     uint8_t* gx_mark;      // [pair]: answered pairs (their records took the receipts' credits; re-scored after)
+    const uint64_t* gx_rhm;  // [node]: bit g = its row of advertised batch g holds a not-everywhere message
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;
@@ -459,6 +470,12 @@ hipError_t launch_hb_fanout(const DevState& s, const HbState& h, uint32_t t, hip
 hipError_t launch_join(const DevState& s, const HbState& h, const uint32_t* nodes, const uint32_t* topics,
                        uint32_t n, uint32_t leave, hipStream_t st);
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
+// The messages of a set every node has seen (AND of its seen rows; common
+// preset to ~0 by the caller, n_words <= 64); per node, the advertised batches
+// whose cache row holds any other message (gx_rhm: only there can the node
+// hold a message some receiver lacks).
+hipError_t launch_gx_common(const uint64_t* all, uint32_t n_words, uint32_t n_nodes, uint64_t* common, hipStream_t st);
+hipError_t launch_gx_rhm(const GxBatch* gx, uint32_t n_gx, uint32_t n_nodes, uint64_t* rhm, hipStream_t st);
 // full[v] = node v has seen every one of the set's n_msgs messages (its `all` row is full)
 hipError_t launch_gx_full(const uint64_t* all, uint32_t n_words, uint32_t n_msgs, uint32_t n_nodes, uint8_t* full,
                           hipStream_t st);
@@ -502,7 +519,7 @@ hipError_t launch_hb_px_recv(const DevState& s, const HbState& h, const uint32_t
 hipError_t launch_hb_answer(const DevState& s, const HbState& h, hipStream_t st);
 // Peer exchange of the round's PRUNEs (gsx.h): kind 0 = (A) PRUNEs, 1 = (B) answers.
 hipError_t launch_hb_px(const DevState& s, const HbState& h, uint32_t kind, hipStream_t st);
-hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
+hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, uint32_t stride, const uint64_t* a, const uint64_t* b,
                           uint64_t* out, hipStream_t st);
 
 // ---- launchers (gsx_kernels.hip) ---------------------------------------------

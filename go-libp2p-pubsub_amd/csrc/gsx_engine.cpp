@@ -104,7 +104,7 @@ struct gsx_engine {
     gsx_gossipsub_params gp{};
     int64_t* d_backoff = nullptr;
     uint8_t* d_bo8 = nullptr;  // [topic / 8][pair] backoff presence bits
-    uint64_t *d_ctl_graft = nullptr, *d_ctl_prune = nullptr, *d_resp = nullptr;
+    uint64_t *d_ctl = nullptr, *d_resp = nullptr;  // d_ctl: [pair][2] GRAFT / PRUNE topic bits
     uint8_t* d_dirty = nullptr;
     uint32_t *d_long = nullptr, *d_nlong = nullptr;
     unsigned long long* d_hbstats = nullptr;
@@ -135,6 +135,8 @@ struct gsx_engine {
         uint64_t* d_acc = nullptr;  // [word] accepted messages
         uint64_t* d_dg = nullptr;   // [W * 64] id digests + [W] word digests (k_mc_summary)
         uint8_t* d_full = nullptr;  // [node]: every message seen (the exchange skips the set there)
+        uint8_t* d_small = nullptr;  // the pooled block d_val / d_acc / d_dg live in
+        size_t small_bytes = 0, full_bytes = 0;
         bool full_ok = false;       // d_full matches d_all
         std::vector<uint64_t> ids;
         int refs = 0;
@@ -192,9 +194,13 @@ struct gsx_engine {
     uint32_t* d_gx_off = nullptr;
     uint8_t* d_gx_got = nullptr;
     size_t gx_cap = 0;
+    uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
+    uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
+    size_t gx_common_cap = 0;         // (sets)
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
+    std::vector<std::pair<size_t, uint8_t*>> small_pool;  // message sets' small device arrays, recycled
     gsx::GossipBatch* d_gb = nullptr;
     uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
@@ -236,6 +242,7 @@ struct gsx_engine {
         gsx_prop_config cfg{};
         std::vector<uint64_t> ids;
         std::vector<uint32_t> vals;  // validation outcomes of this call
+        std::vector<uint64_t> h_acc;  // accepted-message words (host copy, alive until the call's stream sync)
         // pending (deferred) credits: topic they belong to
         bool credit_pending = false;
         uint32_t credit_topic = 0;
@@ -453,15 +460,45 @@ uint64_t* seen_acquire(gsx_engine* e, size_t words) {
 void seen_pool_free(gsx_engine* e) {
     for (auto& x : e->seen_pool) (void)hipFree(x.second);
     e->seen_pool.clear();
+    for (auto& x : e->small_pool) (void)hipFree(x.second);
+    e->small_pool.clear();
+}
+// Small per-set device arrays (validation outcomes, accepted words, id
+// digests, the `full` bytes) from a recycled pool: no hipMalloc / hipFree per
+// propagation call (a hipFree waits for the whole device).
+uint8_t* small_acquire(gsx_engine* e, size_t bytes, size_t* got) {
+    for (size_t i = 0; i < e->small_pool.size(); ++i)
+        if (e->small_pool[i].first >= bytes && e->small_pool[i].first <= 4 * bytes + 4096) {
+            uint8_t* p = e->small_pool[i].second;
+            *got = e->small_pool[i].first;
+            e->small_pool.erase(e->small_pool.begin() + (long)i);
+            return p;
+        }
+    uint8_t* p = nullptr;
+    if (hipMalloc((void**)&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
+    *got = std::max<size_t>(bytes, 256);
+    return p;
+}
+void small_release(gsx_engine* e, uint8_t* p, size_t bytes) {
+    if (p) e->small_pool.emplace_back(bytes, p);
+}
+// A message set's d_val (m u32) / d_acc (W u64) / d_dg (W * 64 + W u64) in one pooled block.
+bool set_small_alloc(gsx_engine* e, gsx_engine::MsgSet* set, size_t m, uint32_t W) {
+    const size_t val_b = (4 * std::max<size_t>(m, 1) + 7) & ~(size_t)7;
+    const size_t bytes = val_b + 8 * (size_t)W + 8 * ((size_t)W * 64 + W);
+    set->d_small = small_acquire(e, bytes, &set->small_bytes);
+    if (!set->d_small) return false;
+    set->d_val = reinterpret_cast<uint32_t*>(set->d_small);
+    set->d_acc = reinterpret_cast<uint64_t*>(set->d_small + val_b);
+    set->d_dg = set->d_acc + W;
+    return true;
 }
 
 void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
     if (!st || --st->refs > 0) return;
     seen_release(e, st->d_all, st->all_words);
-    if (st->d_val) (void)hipFree(st->d_val);
-    if (st->d_acc) (void)hipFree(st->d_acc);
-    if (st->d_dg) (void)hipFree(st->d_dg);
-    if (st->d_full) (void)hipFree(st->d_full);
+    small_release(e, st->d_small, st->small_bytes);
+    small_release(e, st->d_full, st->full_bytes);
     delete st;
 }
 void batch_release(gsx_engine* e, gsx_engine::McBatch& b) {
@@ -532,21 +569,22 @@ void free_state(gsx_engine* e) {
     e->n_recv = e->n_send = 0;
     e->d_col = nullptr;
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
-                  e->d_backoff, e->d_bo8, e->d_ctl_graft, e->d_ctl_prune, e->d_resp,   e->d_dirty,     e->d_long,
+                  e->d_backoff, e->d_bo8, e->d_ctl, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
     e->d_backoff = nullptr;
     e->d_bo8 = nullptr;
-    e->d_ctl_graft = e->d_ctl_prune = e->d_resp = nullptr;
+    e->d_ctl = e->d_resp = nullptr;
     e->d_dirty = nullptr;
     e->d_long = e->d_nlong = nullptr;
     e->d_hbstats = nullptr;
     e->d_tr_acc = e->d_tr_hp = nullptr;
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
-                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes};
+                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
+                       e->d_gx_rhm, e->d_gx_common};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
@@ -567,6 +605,8 @@ void free_state(gsx_engine* e) {
         e->d_gx_off = nullptr;
         e->d_gx_got = nullptr;
         e->gx_cap = 0;
+        e->d_gx_rhm = e->d_gx_common = nullptr;
+        e->gx_common_cap = 0;
         void* mbp[] = {e->d_sub, e->d_psub, e->d_fanout, e->d_fan_has, e->d_lastpub, e->d_mscratch, e->d_mlist};
         for (void* x : mbp)
             if (x) (void)hipFree(x);
@@ -996,7 +1036,7 @@ int hb_alloc(gsx_engine* e) {
     const size_t TE = (size_t)e->T * e->E;
     int rc = 0;
     const size_t E = e->E;
-    if ((rc = dalloc(e, &e->d_ctl_graft, E)) || (rc = dalloc(e, &e->d_ctl_prune, E)) ||
+    if ((rc = dalloc(e, &e->d_ctl, 2 * E)) ||
         (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
         (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
         (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
@@ -2291,13 +2331,13 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
             return fail(e, GSX_ENOMEM, "seen rows of the message set");
         }
         HIPCHK(e, hipMemcpyAsync(set->d_all, P.seen, 8 * set->all_words, hipMemcpyDeviceToDevice, e->stream));
-        std::vector<uint64_t> acc(W, 0);
+        std::vector<uint64_t>& acc = P.h_acc;
+        acc.assign(W, 0);
         for (size_t k = 0; k < P.vals.size(); ++k)
             if (P.vals[k] == GSX_VALIDATION_ACCEPT) acc[k / 64] |= 1ull << (k % 64);
-        if (int rc = dalloc(e, &set->d_val, std::max<size_t>(P.vals.size(), 1))) return rc;
-        if (int rc = dalloc(e, &set->d_acc, std::max<size_t>(W, 1))) return rc;
-        HIPCHK(e, hipMemcpy(set->d_val, P.vals.data(), 4 * P.vals.size(), hipMemcpyHostToDevice));
-        HIPCHK(e, hipMemcpy(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice));
+        if (!set_small_alloc(e, set, P.vals.size(), W)) return fail(e, GSX_ENOMEM, "message set arrays");
+        HIPCHK(e, hipMemcpyAsync(set->d_val, P.vals.data(), 4 * P.vals.size(), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
     }
     if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
@@ -2322,10 +2362,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
                 P.dig_cap = dg.size();
             }
             HIPCHK(e, hipMemcpyAsync(P.d_dig, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
-            if (set) {
-                if (int rc = dalloc(e, &set->d_dg, dg.size())) return rc;
-                HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
-            }
+            if (set) HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
             b.d_dig = P.seen + (size_t)W * N;
             b.d_cnt = reinterpret_cast<uint32_t*>(P.seen + (size_t)W * N + N);
             HIPCHK(e, gsx::launch_mc_summary(P.seen, (uint32_t)N, W, ps.n_msgs, P.d_dig, P.d_dig + (size_t)W * 64,
@@ -2863,8 +2900,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     h.eflags = e->d_eflags;
     h.backoff = e->d_backoff;
     h.bo8 = e->d_bo8;
-    h.ctl_graft = e->d_ctl_graft;
-    h.ctl_prune = e->d_ctl_prune;
+    h.ctl = e->d_ctl;
     h.resp = e->d_resp;
     h.dirty = e->d_dirty;
     h.inbox = e->d_dirty + e->E;
@@ -2993,8 +3029,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // read, and nothing else is ever set: after one cleared round they stay
     // clean.  Shards pack them for the exchange and clear them here.
     if (e->sharded() || !e->hb_clean) {
-        HIPCHK(e, hipMemsetAsync(e->d_ctl_graft, 0, E8, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_ctl_prune, 0, E8, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_ctl, 0, 2 * E8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_resp, 0, E8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, 3 * (e->E ? e->E : 1), e->stream));
     } else {
@@ -3174,8 +3209,12 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                         HIPCHK(e, hipMemsetAsync(x, 0, 8 * (size_t)b.set->n_words * N, e->stream));
                         gsx_engine::MsgSet* ms = b.set;
                         if (!ms->full_ok) {  // which nodes have seen the whole set (skipped by the walk)
-                            if (!ms->d_full)
-                                if (int rc = dalloc(e, &ms->d_full, N)) return rc;
+                            if (!ms->d_full) {
+                                size_t got = 0;
+                                ms->d_full = small_acquire(e, N, &got);
+                                if (!ms->d_full) return fail(e, GSX_ENOMEM, "message set full bytes");
+                                ms->full_bytes = got;
+                            }
                             HIPCHK(e, gsx::launch_gx_full(ms->d_all, ms->n_words, ms->n_msgs, (uint32_t)N, ms->d_full,
                                                           e->stream));
                             ms->full_ok = true;
@@ -3191,9 +3230,26 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                 }
         }
         off[e->T] = (uint32_t)gx.size();
+        {  // the flat word list of all advertised batches (k_gx_node's rounds)
+            uint32_t fw = 0;
+            for (size_t i = 0; i < gx.size(); ++i) {
+                gx[i].woff = fw;
+                fw += gx[i].n_words;
+                gx[i].n_msgs = gx_sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
+            }
+        }
         static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
         if (dbg) {
-            fprintf(stderr, "[gx] sets=%zu batches=%zu:", gx_sets.size(), gx.size());
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            std::vector<uint8_t> fb(N);
+            fprintf(stderr, "[gx] not full per set:");
+            for (auto* ms : gx_sets) {
+                HIPCHK(e, hipMemcpy(fb.data(), ms->d_full, N, hipMemcpyDeviceToHost));
+                size_t nf = 0;
+                for (uint8_t x : fb) nf += x == 0;
+                fprintf(stderr, " s%u:%zu", ms->serial, nf);
+            }
+            fprintf(stderr, "\n[gx] sets=%zu batches=%zu:", gx_sets.size(), gx.size());
             for (const auto& g : gx) fprintf(stderr, " (t%u w%u s%u a%u)", g.topic, g.n_words, g.serial, g.avail);
             fprintf(stderr, "\n");
         }
@@ -3209,12 +3265,35 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             if (int rc = dalloc(e, &e->d_gx_off, (size_t)GSX_MAX_TOPICS + 1)) return rc;
             if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
         }
-        for (auto& g : gx) g.got = e->d_gx_got + reinterpret_cast<size_t>(g.got);
+        // per set, the messages every node had seen as the exchange began (a
+        // set wider than 64 words keeps none: its rows are filtered by emptiness)
+        if (gx_sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
+            if (e->d_gx_common) (void)hipFree(e->d_gx_common);
+            e->d_gx_common = nullptr;
+            e->gx_common_cap = std::max<size_t>(gx_sets.size(), 8);
+            if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
+            if (!e->d_gx_rhm)
+                if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
+        }
+        for (size_t i = 0; i < gx_sets.size(); ++i) {
+            uint64_t* cm = e->d_gx_common + 64 * i;
+            const uint32_t W = gx_sets[i]->n_words;
+            if (W > 64) continue;
+            HIPCHK(e, hipMemsetAsync(cm, 0xff, 8 * (size_t)W, e->stream));
+            HIPCHK(e, gsx::launch_gx_common(gx_sets[i]->d_all, W, (uint32_t)N, cm, e->stream));
+        }
+        for (auto& g : gx) {
+            const size_t si = reinterpret_cast<size_t>(g.got);
+            g.common = gx_sets[si]->n_words <= 64 ? e->d_gx_common + 64 * si : nullptr;
+            g.got = e->d_gx_got + si;
+        }
         HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
         HIPCHK(e, hipMemcpy(e->d_gx, gx.data(), sizeof(gsx::GxBatch) * gx.size(), hipMemcpyHostToDevice));
         HIPCHK(e, hipMemcpy(e->d_gx_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice));
         h.gx = e->d_gx;
         h.gx_off = e->d_gx_off;
+        HIPCHK(e, gsx::launch_gx_rhm(e->d_gx, (uint32_t)gx.size(), (uint32_t)N, e->d_gx_rhm, e->stream));
+        h.gx_rhm = e->d_gx_rhm;
         h.gsubs = e->d_gsubs;
         // the answered pairs' records take the receipts' credits: re-scored after
         // (the rest stays exact), when the scores were exact before
@@ -3246,6 +3325,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
+    // a bulk round's (B) left the control words: one clear at the next round's start
+    if (gsx::hb_bulk_round(st[gsx::HB_GRAFTS], st[gsx::HB_PRUNES], e->E)) e->hb_clean = false;
     e->px_last = h.pxno ? st[gsx::HB_PX_CONNECT] : 0;
     // mcache.Shift (mcache.go:94-104, gossipsub.go:1563), after the stream drained
     while (e->mc.size() >= hist) {
@@ -3453,7 +3534,7 @@ int gsx_hb_pack_ctl(gsx_engine* e, uint64_t* send) {
     if (!e) return GSX_EINVAL;
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_send && !send) return GSX_EINVAL;
-    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, e->d_ctl_graft, e->d_ctl_prune, send, e->stream));
+    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, 2, e->d_ctl, e->d_ctl + 1, send, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
@@ -3469,7 +3550,7 @@ int gsx_hb_pack_resp(gsx_engine* e, uint64_t* send) {
     if (!e) return GSX_EINVAL;
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_send && !send) return GSX_EINVAL;
-    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, e->d_resp, nullptr, send, e->stream));
+    HIPCHK(e, gsx::launch_hb_pack(e->d_send_pair, e->n_send, 1, e->d_resp, nullptr, send, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
 }
@@ -3641,6 +3722,7 @@ int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, s
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     std::memcpy(out, st, sizeof(st));
+    if (gsx::hb_bulk_round(st[gsx::HB_GRAFTS], st[gsx::HB_PRUNES], e->E)) e->hb_clean = false;
     e->px_last = e->hb.pxno ? st[gsx::HB_PX_CONNECT] : 0;
     return GSX_OK;
 }
@@ -3671,8 +3753,11 @@ int gsx_hb_trace_words(gsx_engine* e, uint64_t* sent_graft, uint64_t* sent_prune
     if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
     const size_t n = 8 * (size_t)e->E;
     if (n) {
-        if (sent_graft) HIPCHK(e, hipMemcpyAsync(sent_graft, e->d_ctl_graft, n, hipMemcpyDeviceToHost, e->stream));
-        if (sent_prune) HIPCHK(e, hipMemcpyAsync(sent_prune, e->d_ctl_prune, n, hipMemcpyDeviceToHost, e->stream));
+        // (the [pair][2] control words, one column each)
+        if (sent_graft)
+            HIPCHK(e, hipMemcpy2DAsync(sent_graft, 8, e->d_ctl, 16, 8, e->E, hipMemcpyDeviceToHost, e->stream));
+        if (sent_prune)
+            HIPCHK(e, hipMemcpy2DAsync(sent_prune, 8, e->d_ctl + 1, 16, 8, e->E, hipMemcpyDeviceToHost, e->stream));
         if (acc_graft) HIPCHK(e, hipMemcpyAsync(acc_graft, e->d_tr_acc, n, hipMemcpyDeviceToHost, e->stream));
         if (handled_prune) HIPCHK(e, hipMemcpyAsync(handled_prune, e->d_tr_hp, n, hipMemcpyDeviceToHost, e->stream));
     }
@@ -3863,11 +3948,9 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
         dg[k] = id_digest(msgs[k].msg_id);
         dg[(size_t)W * 64 + k / 64] += dg[k];
     }
-    int rc = 0;
-    if ((rc = dalloc(e, &set->d_val, m)) || (rc = dalloc(e, &set->d_acc, (size_t)W)) ||
-        (rc = dalloc(e, &set->d_dg, dg.size()))) {
+    if (!set_small_alloc(e, set, m, W)) {
         batch_release(e, b);
-        return rc;
+        return fail(e, GSX_ENOMEM, "message set arrays");
     }
     HIPCHK(e, hipMemcpyAsync(set->d_val, vals.data(), 4 * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));

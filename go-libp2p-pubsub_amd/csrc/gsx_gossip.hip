@@ -130,9 +130,15 @@ __global__ __launch_bounds__(256) void k_gx_full(const uint64_t* __restrict__ al
 
 // The candidate word (batch b, word w) of the ids v advertised to u that u
 // had not seen, within the subset row of a truncated list.
+// u's own row first: v's cache word is read only where u lacks a message
+// (mem has no bit past n_msgs, so this is mem & ~all exactly).
 __device__ __forceinline__ uint64_t gx_word(const GxBatch& b, uint32_t u, uint32_t v, uint32_t w, const uint64_t* sub) {
     const uint32_t W = b.n_words;
-    uint64_t m = b.mem[(size_t)v * W + w] & ~b.all[(size_t)u * W + w];
+    const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
+    const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+    const uint64_t miss = ~b.all[(size_t)u * W + w] & valid;
+    if (!miss) return 0;
+    uint64_t m = b.mem[(size_t)v * W + w] & miss;
     if (sub) m &= sub[b.row_off + w];
     return m;
 }
@@ -252,111 +258,275 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
     });
 }
 
+// handleIHave's gates (:615-633) for the IHAVE RPC on pair q = (u -> v):
+// 0 = nobody to answer (v untracked or on another shard), 1 = ignored (v's
+// score below GossipThreshold, MaxIHaveMessages, MaxIHaveLength asked), 2 = handled.
+__device__ __forceinline__ int gx_gate(const DevState& s, const HbState& h, uint64_t q, uint32_t r) {
+    if (r == NO_PAIR || (r & HALO)) return 0;
+    if (s.score[q] < h.gossip_threshold) return 1;  // :617-621
+    const uint32_t ph = h.peerhave[q] + 1;          // :624-628 (one RPC per pair per heartbeat)
+    if ((int64_t)ph > (int64_t)h.gp.max_ihave_msgs) return 1;
+    if ((int64_t)h.iasked[q] >= (int64_t)h.gp.max_ihave) return 1;  // :630-633
+    return 2;
+}
+
+__device__ __forceinline__ uint32_t gx_wsum(uint32_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += (uint32_t)__shfl_xor((int)x, off, 64);
+    return x;
+}
+__device__ __forceinline__ uint32_t gx_excl(uint32_t x, uint32_t lane) {  // exclusive prefix sum over the wave
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    return incl - x;
+}
+
+// The flat word list of the advertised batches (GxBatch::woff; canonical
+// order: topics ascending, then cache order) is walked in rounds of 64 words
+// aligned to 64: in round i lane L holds word base + 64 i + L, so a batch
+// word always belongs to the same lane and a round's words are in canonical
+// order by lane.  Topic t's words are [gx[g0].woff, gx[g1 - 1].woff + W).
+struct GxRange {
+    uint32_t g0, g1, f0, f1, base;
+};
+__device__ __forceinline__ GxRange gx_range(const HbState& h, uint32_t t) {
+    GxRange R{h.gx_off[t], h.gx_off[t + 1], 0, 0, 0};
+    if (R.g0 < R.g1) {
+        R.f0 = h.gx[R.g0].woff;
+        R.f1 = h.gx[R.g1 - 1].woff + h.gx[R.g1 - 1].n_words;
+        R.base = R.f0 & ~63u;
+    }
+    return R;
+}
+// The lane's word of a round: its batch (advanced monotonically in g) and word,
+// false when the lane has none.
+__device__ __forceinline__ bool gx_at(const HbState& h, const GxRange& R, uint32_t f, uint32_t& g, uint32_t& w) {
+    if (f < R.f0 || f >= R.f1) return false;
+    while (h.gx[g].woff + h.gx[g].n_words <= f) ++g;
+    w = f - h.gx[g].woff;
+    return true;
+}
+
+// |iwant| of pair q (every lane gets it): popcounts of the candidate words.
+__device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t tr,
+                                              uint32_t r, uint64_t nf, uint32_t lane) {
+    uint32_t c = 0;
+    for (; tb; tb &= tb - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        const GxRange R = gx_range(h, t);
+        const uint64_t* sub = gx_subrow(h, tr, t, r);
+        uint32_t g = R.g0, w = 0;
+        for (uint32_t f = R.base + lane; f < R.f1; f += 64)
+            if (gx_at(h, R, f, g, w) && !gx_skip(nf, g)) c += (uint32_t)__popcll(gx_word(h.gx[g], u, v, w, sub));
+    }
+    return gx_wsum(c);
+}
+
+// The j-th candidate of pair q in canonical order (every lane gets it).
+__device__ __forceinline__ void gx_wnth(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t tr,
+                                        uint32_t r, uint64_t nf, uint32_t lane, uint32_t j, uint32_t& pick_g,
+                                        uint32_t& pick_k) {
+    for (; tb; tb &= tb - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
+        const GxRange R = gx_range(h, t);
+        const uint64_t* sub = gx_subrow(h, tr, t, r);
+        uint32_t g = R.g0, w = 0;
+        for (uint32_t f0 = R.base; f0 < R.f1; f0 += 64) {  // (uniform rounds)
+            uint64_t m = 0;
+            if (gx_at(h, R, f0 + lane, g, w) && !gx_skip(nf, g)) m = gx_word(h.gx[g], u, v, w, sub);
+            const uint32_t c = (uint32_t)__popcll(m);
+            const uint32_t e = gx_excl(c, lane);
+            const uint32_t tot = (uint32_t)__shfl((int)(e + c), 63, 64);
+            if (j >= tot) {
+                j -= tot;
+                continue;
+            }
+            const bool mine = e <= j && j < e + c;
+            uint32_t k = 0;
+            if (mine) {
+                for (uint32_t i = j - e; i; --i) m &= m - 1;
+                k = w * 64 + (uint32_t)__builtin_ctzll(m);
+            }
+            const int src = __ffsll((long long)__ballot(mine)) - 1;
+            pick_g = (uint32_t)__shfl((int)g, src, 64);
+            pick_k = (uint32_t)__shfl((int)k, src, 64);
+            return;
+        }
+    }
+}
+
+// AddPromise (gossip_tracer.go:59-74): once per (message, peer); the host
+// keeps a free slot on every pair before each exchange (one promise per pair).
+__device__ __forceinline__ void gx_promise(const HbState& h, uint64_t q, uint64_t handle, uint32_t& occ) {
+    const uint32_t S = h.prom_slots;
+    uint64_t* ph_ = h.prom_h + (size_t)q * S;
+    int64_t* pe_ = h.prom_e + (size_t)q * S;
+    int free_slot = -1;
+    bool have = false;
+    uint32_t used = 0;
+    for (uint32_t k = 0; k < S; ++k) {
+        if (pe_[k] == 0) {
+            if (free_slot < 0) free_slot = (int)k;
+        } else {
+            ++used;
+            if (ph_[k] == handle) have = true;
+        }
+    }
+    if (!have && free_slot >= 0) {
+        ph_[free_slot] = handle;
+        pe_[free_slot] = h.now + h.gp.followup_ns;
+        ++used;
+    } else if (!have) {
+        h.gx_err[1] = 1;  // (the host's invariant broken: never)
+    }
+    occ = used > occ ? used : occ;
+}
+
+// The asked subset of a sampled pair (kk < n, selection sampling over the
+// canonical walk) and AddPromise's pick in it (the element at Int31n(kk)).
+__device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q,
+                                                uint32_t r, uint32_t n, uint32_t kk, uint32_t& pick_g,
+                                                uint32_t& pick_k) {
+    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+    uint32_t i = 0, sel = 0;
+    gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
+        if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
+        ++i;
+        return sel < kk;
+    });
+    const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
+    Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
+    i = 0;
+    sel = 0;
+    gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
+        const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
+        ++i;
+        if (!take) return true;
+        if (sel++ < j) return true;
+        pick_g = gi;
+        pick_k = k;
+        return false;
+    });
+}
+
+constexpr uint32_t GX_ML = 64;           // words a receiver's lane handles itself (else: a wave, GX_HEAVY)
+constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
+
 // Pass 1, one lane per receiving node u: handleIHave (:615-679) for the one
 // IHAVE RPC each sender v sent (every topic), senders ascending: the score /
 // MaxIHaveMessages / iasked gates, |iwant| from word popcounts, the asked
 // subset (all; or a uniform kk-subset by selection sampling) and AddPromise's
-// pick (gossip_tracer.go:53).  Pairs with nothing asked are cleared here
-// (clearIHaveCounters, :1566-1576, then finds them zero); a node with an asked
-// pair is listed for pass 2.
+// pick (gossip_tracer.go:53).  Only the advertised batches u has not seen
+// whole can hold a candidate: a node with none asks for nothing; one with at
+// most GX_ML such words is handled here; one with more (its lane would walk every
+// unseen batch per sender) is listed for k_gx_node's wave (GX_HEAVY), like
+// every node that asked (pass 2).
 __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
-    const DevGossipParams& gp = h.gp;
-    const uint32_t S = h.prom_slots;
+    // the node's miss list: (batch, word) of its unseen batches where u lacks a
+    // message, canonical order, [entry][lane] (a lane's entries strided: no
+    // bank conflicts); the bits are re-read from u's row (cached) per use
+    __shared__ uint16_t ml_gw[GX_ML][64];  // batch << 6 | word (W <= 64 words per batch here)
+    const uint32_t lane = threadIdx.x;
     uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0;
     uint32_t occ = 0;
     const uint32_t n_gx = h.gx_off[s.n_topics];
-    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 64u) {
+    for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        const uint64_t nf = gx_unseen(h, n_gx, u);  // nothing unseen: no IHAVE of u asks for anything
-        bool asked = false;
+        const uint64_t nf = gx_unseen(h, n_gx, u);
+        // the words u lacks something in (u's own rows, read once per node)
+        uint32_t nml = 0;
+        bool heavy = n_gx > 64 || n_gx > 1024;
+        for (uint64_t m = heavy ? 0 : nf; m && !heavy; m &= m - 1) {
+            const uint32_t g = (uint32_t)__builtin_ctzll(m);
+            const GxBatch& b = h.gx[g];
+            if (b.n_words > 64) {
+                heavy = true;
+                break;
+            }
+            for (uint32_t w = 0; w < b.n_words; ++w) {
+                const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
+                const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                const uint64_t miss = ~b.all[(size_t)u * b.n_words + w] & valid;
+                if (!miss) continue;
+                if (nml == GX_ML) {
+                    heavy = true;
+                    break;
+                }
+                ml_gw[nml][lane] = (uint16_t)(g << 6 | w);
+                ++nml;
+            }
+        }
+        bool list = false;
         for (int64_t q = r0; q < r1; ++q) {
             const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
             if (!tall) continue;
-            uint32_t kk = 0;
             const uint32_t r = h.rev[q];
-            do {
-                if (r == NO_PAIR || (r & HALO)) break;
-                const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
-                if (s.score[q] < h.gossip_threshold) {  // :617-621
-                    ++ignored;
-                    break;
-                }
-                const uint32_t ph = h.peerhave[q] + 1;  // :624-628
-                if ((int64_t)ph > (int64_t)gp.max_ihave_msgs) {
-                    ++ignored;
-                    break;
-                }
-                const uint32_t ia = h.iasked[q];
-                if ((int64_t)ia >= (int64_t)gp.max_ihave) {  // :630-633
-                    ++ignored;
-                    break;
-                }
-                if (!nf) break;
-                const uint32_t v = (uint32_t)h.col[q];
-                const uint32_t n = gx_count(h, tb, u, v, q, r, nf);
-                if (n == 0) break;  // :652-654
-                const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)ia);
-                kk = n < budget ? n : budget;
-                Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
-                uint32_t pick_g = 0, pick_k = 0;
-                if (kk == n) {
-                    gx_nth(h, tb, u, v, q, r, nf, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
-                } else {
-                    uint32_t i = 0, sel = 0;
-                    gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
-                        if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
-                        ++i;
-                        return sel < kk;
-                    });
-                    const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-                    Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
-                    i = 0;
-                    sel = 0;
-                    gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
-                        const bool take = (uint32_t)g2.int31n((int32_t)(n - i)) < kk - sel;
-                        ++i;
-                        if (!take) return true;
-                        if (sel++ < j) return true;
-                        pick_g = gi;
-                        pick_k = k;
-                        return false;
-                    });
-                }
-                ++iw_msgs;
-                iw_ids += kk;
-                // AddPromise (:59-74): once per (message, peer); the host keeps a
-                // free slot on every pair before each exchange (one promise per pair)
-                const uint64_t handle = ((uint64_t)h.gx[pick_g].serial << 32) | pick_k;
-                uint64_t* ph_ = h.prom_h + (size_t)q * S;
-                int64_t* pe_ = h.prom_e + (size_t)q * S;
-                int free_slot = -1;
-                bool have = false;
-                uint32_t used = 0;
-                for (uint32_t k = 0; k < S; ++k) {
-                    if (pe_[k] == 0) {
-                        if (free_slot < 0) free_slot = (int)k;
-                    } else {
-                        ++used;
-                        if (ph_[k] == handle) have = true;
-                    }
-                }
-                if (!have && free_slot >= 0) {
-                    ph_[free_slot] = handle;
-                    pe_[free_slot] = h.now + gp.followup_ns;
-                    ++used;
-                } else if (!have) {
-                    h.gx_err[1] = 1;  // (the host's invariant broken: never)
-                }
-                occ = used > occ ? used : occ;
-            } while (false);
-            // (a pair's IHAVE counters only matter within this one RPC: none is
-            // kept; the IHAVE bits are cleared before the next round's gossip)
-            if (kk) {
-                h.gx_req[q] = kk;
-                asked = true;
+            const int gt = gx_gate(s, h, (uint64_t)q, r);
+            ignored += gt == 1;
+            if (gt != 2 || !nf) continue;
+            if (heavy) {
+                list = true;
+                continue;
             }
+            const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
+            const uint32_t v = (uint32_t)h.col[q];
+            // the unseen batches whose row at v holds a message not every node had:
+            // only there can v hold one u lacks
+            const uint64_t cb = nf & h.gx_rhm[v];
+            if (!cb) continue;  // |iwant| = 0 (:652-654)
+            const uint64_t tr = h.ihave_tr[q];
+            // |iwant|: v's cache words where u lacks something (topics of the RPC,
+            // the subset row of a truncated list)
+            uint32_t n = 0;
+            for (uint32_t i = 0; i < nml; ++i) {
+                const uint32_t gw = ml_gw[i][lane], g = gw >> 6, w = gw & 63u;
+                if (!((cb >> g) & 1)) continue;
+                const GxBatch& b = h.gx[g];
+                if (!((tb >> b.topic) & 1)) continue;
+                uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)u * b.n_words + w];
+                const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
+                if (sub) c &= sub[b.row_off + w];
+                n += (uint32_t)__popcll(c);
+            }
+            if (n == 0) continue;  // :652-654
+            const uint32_t budget = (uint32_t)((int64_t)h.gp.max_ihave - (int64_t)h.iasked[q]);
+            const uint32_t kk = n < budget ? n : budget;
+            uint32_t pick_g = 0, pick_k = 0;
+            if (kk == n) {  // the element at Int31n(kk) of all of them, canonical order
+                Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+                uint32_t j = (uint32_t)g.int31n((int32_t)kk);
+                for (uint32_t i = 0; i < nml; ++i) {
+                    const uint32_t gw = ml_gw[i][lane], gi = gw >> 6, w = gw & 63u;
+                    if (!((cb >> gi) & 1)) continue;
+                    const GxBatch& b = h.gx[gi];
+                    if (!((tb >> b.topic) & 1)) continue;
+                    uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)u * b.n_words + w];
+                    const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
+                    if (sub) c &= sub[b.row_off + w];
+                    const uint32_t pc = (uint32_t)__popcll(c);
+                    if (j >= pc) {
+                        j -= pc;
+                        continue;
+                    }
+                    for (; j; --j) c &= c - 1;
+                    pick_g = gi;
+                    pick_k = w * 64 + (uint32_t)__builtin_ctzll(c);
+                    break;
+                }
+            } else {
+                gx_pick_sampled(h, tb, u, v, q, r, n, kk, pick_g, pick_k);
+            }
+            ++iw_msgs;
+            iw_ids += kk;
+            h.gx_req[q] = kk;
+            gx_promise(h, (uint64_t)q, ((uint64_t)h.gx[pick_g].serial << 32) | pick_k, occ);
+            list = true;
         }
-        if (asked) h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u;
+        if (list) h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u | (heavy ? GX_HEAVY : 0u);
     }
     gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);
     gx_flush(h.stats, HB_IWANT_MSGS, iw_msgs);
@@ -366,31 +536,68 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
         const uint32_t o = (uint32_t)__shfl_xor((int)occ, off, 64);
         occ = o > occ ? o : occ;
     }
-    if ((threadIdx.x % 64) == 0 && occ) atomicMax(h.prom_occ, occ);
+    if (lane == 0 && occ) atomicMax(h.prom_occ, occ);
 }
 
-// Pass 2, one wave per listed node u: v answers u's IWANT (handleIWant
-// :681-716: its score of u, its cache after the Shift) and u receives the
-// answer, senders ascending.  A pair that asked for everything it lacked (kk
-// = n, the common case) is received word-parallel: lane i takes the words i,
-// i + 64, ... of each advertised batch (a batch word always goes to the same
-// lane, so a later pair's duplicate test reads what that lane wrote); per
-// topic the lanes' first deliveries, accepted duplicates and invalid ones are
-// summed and credited once (gx_credit).  A sampled pair (kk < n) is received
-// by lane 0 one id at a time.  Then fulfillPromise (:119-126) for every id u
-// received this exchange: the node's promise slots whose message is now in
-// its receipt rows (promises are only added in pass 1).
-__global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
+// One wave per listed node u, senders ascending throughout (every per-pair
+// state — IHAVE counters, promises, records of q — is u's alone):
+//  pass 1 (GX_HEAVY nodes): k_gx_ask's handleIHave with the counts and the
+//          pick in rounds of 64 candidate words (gx_wcount, gx_wnth);
+//  pass 2: v answers (handleIWant :681-716: its score of u, its cache after
+//          the Shift) and u receives, word-parallel when u asked for every
+//          candidate (kk = n): lane i takes the words i, i + 64, ... of each
+//          advertised batch in cache order (a batch word always goes to the
+//          same lane, and the batches of one message set share their receipt
+//          rows word for word, so a later copy — another batch, a later pair —
+//          meets the receipt its lane wrote); per topic the first deliveries,
+//          accepted duplicates and invalid ones are summed and credited once
+//          (gx_credit); a sampled pair (kk < n) is received by lane 0 one id
+//          at a time;
+//  then fulfillPromise (:119-126): u's promises whose message is now in its
+//  receipt rows (promises are only added in pass 1).
+__global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
     const uint32_t lane = threadIdx.x;
     const uint32_t S = h.prom_slots;
     const DevGossipParams& gp = h.gp;
-    uint64_t served = 0, delivered = 0, rejected = 0, dups = 0;
+    uint64_t iw_msgs = 0, iw_ids = 0, served = 0, delivered = 0, rejected = 0, dups = 0;
+    uint32_t occ = 0;
     const uint32_t n_list = h.gx_err[6];
     const uint32_t n_gx = h.gx_off[s.n_topics];
     for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
-        const uint32_t u = h.gx_nodes[li];
+        const uint32_t entry = h.gx_nodes[li];
+        const uint32_t u = entry & ~GX_HEAVY;
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        const uint64_t nf = gx_unseen(h, n_gx, u);
+        uint64_t nf = n_gx > 64 ? ~0ull : __ballot(lane < n_gx && !h.gx[lane].full[u]);
+        if (entry & GX_HEAVY) {  // ---- pass 1 for a node with many unseen batches
+            for (int64_t q = r0; q < r1; ++q) {
+                const uint64_t tall = h.ihave_bits[q];
+                if (!tall) continue;
+                const uint32_t r = h.rev[q];
+                if (gx_gate(s, h, (uint64_t)q, r) != 2) continue;
+                const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
+                const uint32_t v = (uint32_t)h.col[q];
+                const uint64_t tr = h.ihave_tr[q];
+                const uint32_t n = gx_wcount(h, tb, u, v, tr, r, nf, lane);
+                if (n == 0) continue;
+                const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)h.iasked[q]);
+                const uint32_t kk = n < budget ? n : budget;
+                uint32_t pick_g = 0, pick_k = 0;
+                if (kk == n) {
+                    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+                    gx_wnth(h, tb, u, v, tr, r, nf, lane, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
+                } else if (lane == 0) {
+                    gx_pick_sampled(h, tb, u, v, q, r, n, kk, pick_g, pick_k);
+                }
+                if (lane == 0) {
+                    ++iw_msgs;
+                    iw_ids += kk;
+                    h.gx_req[q] = kk;
+                    gx_promise(h, (uint64_t)q, ((uint64_t)h.gx[pick_g].serial << 32) | pick_k, occ);
+                }
+            }
+            __threadfence_block();  // gx_req of every pair before pass 2 reads it
+        }
+        // ---- pass 2: v answers, u receives
         for (int64_t q = r0; q < r1; ++q) {
             const uint32_t kk = h.gx_req[q];  // (wave-uniform)
             if (!kk) continue;
@@ -401,17 +608,19 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
             const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
             if (answered) {
                 const uint32_t v = (uint32_t)h.col[q];
-                const uint32_t n = gx_count(h, tb, u, v, q, r, nf);  // (uniform: every lane counts)
+                const uint64_t tr = h.ihave_tr[q];
+                const uint32_t n = gx_wcount(h, tb, u, v, tr, r, nf, lane);
                 if (kk == n) {
-                    const uint64_t tr = h.ihave_tr[q];
                     for (uint64_t tm = tb; tm; tm &= tm - 1) {
                         const uint32_t t = (uint32_t)__builtin_ctzll(tm);
                         const uint64_t* sub = gx_subrow(h, tr, t, r);
                         uint32_t k1 = 0, k2 = 0, k4 = 0;
                         for (uint32_t gi = h.gx_off[t]; gi < h.gx_off[t + 1]; ++gi) {
+                            if (gx_skip(nf, gi)) continue;
                             const GxBatch& b = h.gx[gi];
+                            // no longer in v's cache; or GetForPeer's count above GossipRetransmission
+                            if (!b.avail || gp.retransmission < 1) continue;
                             const uint32_t W = b.n_words;
-                            if (!b.avail || gp.retransmission < 1 || gx_skip(nf, gi)) continue;
                             bool got = false;
                             for (uint32_t w = lane; w < W; w += 64) {
                                 const uint64_t m = gx_word(b, u, v, w, sub);
@@ -440,12 +649,9 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
                             }
                             if (got) *b.got = 1;
                         }
-#pragma unroll
-                        for (int off = 32; off > 0; off >>= 1) {
-                            k1 += (uint32_t)__shfl_xor((int)k1, off, 64);
-                            k2 += (uint32_t)__shfl_xor((int)k2, off, 64);
-                            k4 += (uint32_t)__shfl_xor((int)k4, off, 64);
-                        }
+                        k1 = gx_wsum(k1);
+                        k2 = gx_wsum(k2);
+                        k4 = gx_wsum(k4);
                         if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
                     }
                 } else if (lane == 0) {
@@ -474,10 +680,55 @@ __global__ __launch_bounds__(64) void k_gx_receive(DevState s, HbState h) {
             }
         }
     }
+    gx_flush(h.stats, HB_IWANT_MSGS, iw_msgs);
+    gx_flush(h.stats, HB_IWANT_IDS, iw_ids);
     gx_flush(h.stats, HB_IWANT_SERVED, served);
     gx_flush(h.stats, HB_GOSSIP_DELIVERED, delivered);
     gx_flush(h.stats, HB_GOSSIP_REJECTED, rejected);
     gx_flush(h.stats, HB_GOSSIP_DUPLICATES, dups);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)occ, off, 64);
+        occ = o > occ ? o : occ;
+    }
+    if (lane == 0 && occ) atomicMax(h.prom_occ, occ);
+}
+
+// AND of a set's seen rows over the nodes: a thread keeps one word (the
+// stride is a multiple of W), the block ANDs in LDS, one atomic per (block, word).
+__global__ __launch_bounds__(256) void k_gx_common(const uint64_t* __restrict__ all, uint32_t W, uint32_t n,
+                                                   unsigned long long* __restrict__ common) {
+    __shared__ unsigned long long sw[64];
+    if (threadIdx.x < 64) sw[threadIdx.x] = ~0ull;
+    __syncthreads();
+    const uint64_t threads = (uint64_t)gridDim.x * 256u;
+    const uint64_t stride = threads / W * W;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t0 < stride) {
+        unsigned long long acc = ~0ull;
+        for (uint64_t i = t0; i < (uint64_t)n * W; i += stride) acc &= all[i];
+        atomicAnd(&sw[t0 % W], acc);
+    }
+    __syncthreads();
+    if (threadIdx.x < W) atomicAnd(&common[threadIdx.x], sw[threadIdx.x]);
+}
+
+// Per node v, bit g: v's row of advertised batch g holds a message outside
+// its set's common words (batches past 64: always set).  Thread v reads its W
+// words of each batch row (adjacent nodes, adjacent rows: coalesced).
+__global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, uint32_t n_gx, uint32_t n,
+                                                uint64_t* __restrict__ rhm) {
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
+        uint64_t m = n_gx > 64 ? ~0ull : 0ull;
+        for (uint32_t g = 0; g < n_gx && g < 64; ++g) {
+            const GxBatch& b = gx[g];
+            const uint32_t W = b.n_words;
+            uint64_t any = 0;
+            for (uint32_t w = 0; w < W; ++w) any |= b.mem[(size_t)v * W + w] & ~(b.common ? b.common[w] : 0ull);
+            if (any) m |= 1ull << g;
+        }
+        rhm[v] = m;
+    }
 }
 
 // The exchange's receipts into the message set: seen |= x; the receipt rows
@@ -503,11 +754,24 @@ hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t s
     return hipGetLastError();
 }
 
+hipError_t launch_gx_common(const uint64_t* all, uint32_t n_words, uint32_t n_nodes, uint64_t* common, hipStream_t st) {
+    if (n_nodes == 0 || n_words == 0 || n_words > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gx_common, dim3(gx_blocks((uint64_t)n_nodes * n_words, 256, 1024)), dim3(256), 0, st, all,
+                       n_words, n_nodes, reinterpret_cast<unsigned long long*>(common));
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_rhm(const GxBatch* gx, uint32_t n_gx, uint32_t n_nodes, uint64_t* rhm, hipStream_t st) {
+    if (n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_rhm, dim3(gx_blocks(n_nodes, 256, 4096)), dim3(256), 0, st, gx, n_gx, n_nodes, rhm);
+    return hipGetLastError();
+}
+
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_ask, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
     // the listed nodes (their count is on the device): a wave each, grid-stride
-    hipLaunchKernelGGL(k_gx_receive, dim3(4096), dim3(64), 0, st, s, h);
+    hipLaunchKernelGGL(k_gx_node, dim3(8192), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
 

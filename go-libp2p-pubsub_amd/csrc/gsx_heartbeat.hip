@@ -394,7 +394,7 @@ __device__ __forceinline__ void apply_events(const DevState& s, const HbState& h
             reinterpret_cast<int64_t*>(s.rec)[rec_index(r, t, s.n_topics, GRAFT)] = h.now;
             s.rflags[flag_index(r, t, s.n_topics)] = REC_IN_MESH | REC_FRESH;
         }
-        atomicOr((unsigned long long*)&h.ctl_graft[r], 1ull << t);
+        atomicOr((unsigned long long*)&h.ctl[2 * (size_t)r], 1ull << t);
     }
     if (f & ST_PRUNE) {  // ev_prune (a pruned mesh peer is present)
         if (scored) {
@@ -412,7 +412,7 @@ __device__ __forceinline__ void apply_events(const DevState& s, const HbState& h
             s.rflags[flag_index(r, t, s.n_topics)] = active ? REC_ACTIVE : 0;
         }
         add_backoff(h, r, t, h.gp.prune_backoff_ns);
-        atomicOr((unsigned long long*)&h.ctl_prune[r], 1ull << t);
+        atomicOr((unsigned long long*)&h.ctl[2 * (size_t)r + 1], 1ull << t);
         if ((f & ST_NOPX) && h.pxno) h.pxno[r] |= 1;  // noPX[p] ((A) sets only this bit: racing topics agree)
     }
     h.dirty[r] = 1;
@@ -1263,9 +1263,11 @@ __device__ __forceinline__ bool recv_control(const HbState& h, uint64_t q, bool 
         grafts = h.halo_ctl[2 * (size_t)(r & ~HALO)];
         prunes = h.halo_ctl[2 * (size_t)(r & ~HALO) + 1];
     } else {
-        grafts = h.ctl_graft[r];
-        prunes = h.ctl_prune[r];
-        if (write && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+        const ulonglong2 c = reinterpret_cast<const ulonglong2*>(h.ctl)[r];
+        grafts = c.x;
+        prunes = c.y;
+        if (write && !h.halo_ctl && !h.keep_ctl && (grafts | prunes))
+            reinterpret_cast<ulonglong2*>(h.ctl)[r] = make_ulonglong2(0, 0);
     }
     return (grafts | prunes) != 0;
 }
@@ -1374,6 +1376,7 @@ __device__ __forceinline__ void recv_pair(const DevState& s, const HbState& h, u
 // running count per topic, taken from the row on first use.
 __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
     const uint32_t lane = threadIdx.x;
+    const bool clear = !hb_bulk_round(h.stats[HB_GRAFTS], h.stats[HB_PRUNES], h.n_pairs);
     RecvCounts c;
     for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
@@ -1389,7 +1392,7 @@ __global__ __launch_bounds__(64) void k_hb_recv(DevState s, HbState h) {
                 if (!ib[j]) continue;
                 h.inbox[q] = 0;
             }
-            recv_pair(s, h, u, (uint64_t)q, true, c);
+            recv_pair(s, h, u, (uint64_t)q, clear, c);
           }
         }
     }
@@ -1412,14 +1415,47 @@ constexpr int RG = 16;
 enum : uint32_t { RC_CAND = 1, RC_OUT = 2, RC_SC = 4, RC_PR = 8, RC_INM = 16 };
 
 __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
-    const uint32_t gl = threadIdx.x % RG;                 // the lane's place in its node's group
-    const uint32_t gbase = (threadIdx.x % 64) & ~(RG - 1);  // the group's first lane in the wave
-    const uint32_t gpb = 256 / RG;
+    const uint32_t lane = threadIdx.x % 64;
+    const uint32_t gl = lane % RG;         // the lane's place in its node's group
+    const uint32_t gbase = lane & ~(RG - 1);  // the group's first lane in the wave
+    const uint32_t grp = lane / RG;
     const DevGossipParams& gp = h.gp;
     RecvCounts c;
-    for (uint32_t u = blockIdx.x * gpb + threadIdx.x / RG; u < h.n_nodes; u += gridDim.x * gpb) {
+    const uint32_t wave = blockIdx.x * 4u + threadIdx.x / 64u, n_waves = gridDim.x * 4u;
+    // (a bulk round's control words are cleared at the next round's start)
+    const bool clear = !hb_bulk_round(h.stats[HB_GRAFTS], h.stats[HB_PRUNES], h.n_pairs);
+    for (uint32_t tile = wave * 64u; tile < h.n_nodes; tile += n_waves * 64u) {
+      // which of the tile's 64 nodes received control: a lane scans each row's
+      // marks (eight at a time, clamped); hubs run in k_hb_recv_hub
+      bool act = false;
+      {
+        const uint32_t un = tile + lane;
+        if (un < h.n_nodes) {
+            const int64_t a0 = h.row_ptr[un], a1 = h.row_ptr[un + 1];
+            if (a1 > a0 && a1 - a0 <= HB_LANE_DEG) {
+                if (h.halo_ctl) {
+                    act = true;
+                } else {
+                    for (int64_t c0 = a0; c0 < a1 && !act; c0 += 8) {
+                        uint8_t ib[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) ib[j] = h.inbox[min(c0 + j, a1 - 1)];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) act |= ib[j] != 0;
+                    }
+                }
+            }
+        }
+      }
+      // the active nodes, 64 / RG at a time: group g takes the g-th
+      for (uint64_t mask = __ballot(act); mask;) {  // (wave-uniform)
+        uint64_t mm = mask;
+        for (uint32_t i = 0; i < grp; ++i) mm &= mm - 1;
+#pragma unroll
+        for (uint32_t i = 0; i < 64u / RG; ++i) mask &= mask - 1;
+        if (!mm) continue;  // (group-uniform)
+        const uint32_t u = tile + (uint32_t)__builtin_ctzll(mm);
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        if (r1 - r0 > HB_LANE_DEG) continue;  // k_hb_recv_hub
         for (int64_t c0 = r0; c0 < r1; c0 += RG) {  // group-uniform
             const int64_t q = c0 + gl;  // q = (u -> v), ascending v
             bool live = false, nopx = false, outb = false;
@@ -1431,7 +1467,7 @@ __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
             if (act) {
                 if (!h.halo_ctl) h.inbox[q] = 0;
                 uint64_t grafts = 0, prunes = 0;
-                if (act && recv_control(h, (uint64_t)q, true, r, grafts, prunes)) {
+                if (act && recv_control(h, (uint64_t)q, clear, r, grafts, prunes)) {
                     nopx = h.sub && (grafts & ~h.sub[u]);  // doPX = false (:721-781)
                     if (h.sub) {  // topics u has not joined: ignored (:727-733, :816-819)
                         grafts &= h.sub[u];
@@ -1532,6 +1568,7 @@ __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
                 ++c.handled;
             }
         }
+      }
     }
     c.flush(h);
 }
@@ -1543,6 +1580,7 @@ __global__ __launch_bounds__(256) void k_hb_recv_grp(DevState s, HbState h) {
 // the whole wave.
 __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
     const uint32_t lane = threadIdx.x;
+    const bool bulk = hb_bulk_round(h.stats[HB_GRAFTS], h.stats[HB_PRUNES], h.n_pairs);
     const bool w0 = lane == 0;
     uint64_t accepted = 0, rejected = 0, penalties = 0, handled = 0;
     int64_t links = 0;
@@ -1563,7 +1601,8 @@ __global__ __launch_bounds__(64) void k_hb_recv_hub(DevState s, HbState h) {
                 uint64_t grafts, prunes;
                 if (!recv_control(h, q, false, r, grafts, prunes)) continue;
                 __syncthreads();  // every lane has the words before lane 0 clears them
-                if (w0 && !(r & HALO) && !h.halo_ctl && !h.keep_ctl) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                if (w0 && !(r & HALO) && !h.halo_ctl && !h.keep_ctl && !bulk)
+                    reinterpret_cast<ulonglong2*>(h.ctl)[r] = make_ulonglong2(0, 0);
                 bool nopx = h.sub && (grafts & ~h.sub[u]);  // doPX = false (:721-781)
                 if (h.sub) {  // topics u has not joined: ignored (:727-733, :816-819)
                     grafts &= h.sub[u];
@@ -1684,13 +1723,13 @@ __global__ __launch_bounds__(256) void k_hb_answer(DevState s, HbState h) {
 // Shard exchange of per-pair control words: send slot j carries the words of
 // the local pair send_pair[j] (0 for NO_PAIR), K words per slot.
 __global__ __launch_bounds__(256) void k_hb_pack(const uint32_t* __restrict__ send_pair, uint64_t n_send,
-                                                 const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
-                                                 uint64_t* __restrict__ out) {
+                                                 uint32_t stride, const uint64_t* __restrict__ a,
+                                                 const uint64_t* __restrict__ b, uint64_t* __restrict__ out) {
     const int K = b ? 2 : 1;
     for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n_send; j += (uint64_t)gridDim.x * 256u) {
         const uint32_t r = send_pair[j];
-        out[K * j] = r == NO_PAIR ? 0 : a[r];
-        if (b) out[K * j + 1] = r == NO_PAIR ? 0 : b[r];
+        out[K * j] = r == NO_PAIR ? 0 : a[(size_t)stride * r];
+        if (b) out[K * j + 1] = r == NO_PAIR ? 0 : b[(size_t)stride * r];
     }
 }
 
@@ -1896,7 +1935,7 @@ __device__ __forceinline__ void px_connect(const DevState& s, const HbState& h, 
 __global__ __launch_bounds__(256) void k_hb_px_count(HbState h, uint32_t kind) {
     const uint8_t nobit = kind ? 2 : 1;
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {
-        const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+        const uint64_t bits = kind ? h.resp[r] : h.ctl[2 * (size_t)r + 1];
         if (!bits || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
         const uint32_t q = h.rev[r];
         if (q == NO_PAIR || !(q & HALO)) continue;
@@ -1933,7 +1972,7 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
         const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
         uint64_t any = 0;  // the topics some PRUNE of u carries a list for
         for (int64_t r = r0; r < r1; ++r) {
-            const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+            const uint64_t bits = kind ? h.resp[r] : h.ctl[2 * (size_t)r + 1];
             if (!bits || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
             any |= bits;
         }
@@ -1947,7 +1986,7 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
                 h.pxbase[r0 + nb++] = (uint32_t)(x - r0);
             }
             for (int64_t r = r0; r < r1; ++r) {  // r = (u -> p), a PRUNE of t with PX
-                const uint64_t bits = kind ? h.resp[r] : h.ctl_prune[r];
+                const uint64_t bits = kind ? h.resp[r] : h.ctl[2 * (size_t)r + 1];
                 if (!((bits >> t) & 1) || (h.pxno[r] & nobit) || (h.eflags[r] & EDGE_NO_PX)) continue;
                 const uint32_t q = h.rev[r];  // (p -> u): the receiver's pair (HALO: p on another shard)
                 const uint32_t pg = (uint32_t)h.col[r];  // p's global id (= the local one unsharded)
@@ -1994,7 +2033,8 @@ __global__ __launch_bounds__(64) void k_hb_px(DevState s, HbState h, uint32_t ki
         // track: cleared here, so each round's (A) bits start from zeros
         if (!kind && !h.keep_ctl)
             for (int64_t r = r0; r < r1; ++r)
-                if (h.rev[r] == NO_PAIR && h.ctl_prune[r]) h.ctl_graft[r] = h.ctl_prune[r] = 0;
+                if (h.rev[r] == NO_PAIR && h.ctl[2 * (size_t)r + 1])
+                    reinterpret_cast<ulonglong2*>(h.ctl)[r] = make_ulonglong2(0, 0);
     }
     flush_count(h.stats, HB_PX_PRUNES, lists);
     flush_count(h.stats, HB_PX_PEERS, listed);
@@ -2027,10 +2067,10 @@ hipError_t launch_hb_px_recv(const DevState& s, const HbState& h, const uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, const uint64_t* a, const uint64_t* b,
+hipError_t launch_hb_pack(const uint32_t* send_pair, uint64_t n_send, uint32_t stride, const uint64_t* a, const uint64_t* b,
                           uint64_t* out, hipStream_t st) {
     if (n_send == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hb_pack, dim3(grid_cap(n_send, 256)), dim3(256), 0, st, send_pair, n_send, a, b, out);
+    hipLaunchKernelGGL(k_hb_pack, dim3(grid_cap(n_send, 256)), dim3(256), 0, st, send_pair, n_send, stride, a, b, out);
     return hipGetLastError();
 }
 

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void k_join(DevState s, HbState h, const uint32
             for (int64_t r = r0; r < r1; ++r) {
                 if (!((s.pflags[r] & PAIR_PRESENT) && (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH))) continue;
                 ev_prune(s, (uint64_t)r, t);
-                atomicOr((unsigned long long*)&h.ctl_prune[r], 1ull << t);
+                atomicOr((unsigned long long*)&h.ctl[2 * (size_t)r + 1], 1ull << t);
                 const uint32_t q = h.rev[r];
                 if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
                 h.dirty[r] = 1;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64) void k_join(DevState s, HbState h, const uint32
             if (!((h.fanout[r] >> t) & 1)) continue;
             h.fanout[r] &= ~(1ull << t);
             ev_graft(s, (uint64_t)r, t, h.now);
-            atomicOr((unsigned long long*)&h.ctl_graft[r], 1ull << t);
+            atomicOr((unsigned long long*)&h.ctl[2 * (size_t)r], 1ull << t);
             const uint32_t q = h.rev[r];
             if (q != NO_PAIR && !(q & HALO)) h.inbox[q] = 1;
             h.dirty[r] = 1;

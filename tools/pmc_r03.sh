@@ -1,0 +1,32 @@
+#!/bin/bash
+# HBM bytes from rocprofv3 PMC counters (one counter per pass, MI355X_MICROARCH.md
+# HBM section: FETCH_SIZE x 2 + WRITE_SIZE on gfx950, checked by the calibration
+# kernels) for the bench's kernels on the current tree:
+#   head  the headline k_refresh_score<8, true> (bench.py, scoring legs only)
+#   p1024 / p64  the propagation replica workload (tools/prop_profile.py)
+#   hb    cfg3 heartbeat rounds with the gossip exchange (tools/hb_micro.py)
+# then tools/pmc_r03.py writes the per-launch / per-batch / per-round bytes.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+O=gpurun_out/${1:-pmc_r03}
+mkdir -p "$O"
+run() {  # run NAME SECONDS COUNTER CMD...
+    local name=$1 secs=$2 c=$3
+    shift 3
+    echo "=== $name $c $(date +%T)"
+    timeout -s KILL "$secs" rocprofv3 --pmc "$c" --kernel-trace -d "$O/$name/$c" -o pmc --output-format csv -- "$@" \
+        > "$O/${name}_$c.log" 2>&1
+    local rc=$?
+    echo "=== $name $c rc=$rc"
+    if [ $rc -ne 0 ]; then tail -n 5 "$O/${name}_$c.log"; exit $rc; fi
+}
+for C in FETCH_SIZE WRITE_SIZE; do
+    run calib 120 $C ./tools/microbench/pmc_calib
+    run head 300 $C python3 bench.py --steps 5 --warmup 1 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
+        --prop-peers 0 --hb-steps 0 --adv-peers 0
+    run p1024 200 $C python3 tools/prop_profile.py --msgs 1024 --batches 3
+    run p64 200 $C python3 tools/prop_profile.py --msgs 64 --batches 3
+    run hb 200 $C python3 tools/hb_micro.py --exchange --rounds 3
+done
+python3 tools/pmc_r03.py "$O" > "$O/summary.json" && cat "$O/summary.json"
