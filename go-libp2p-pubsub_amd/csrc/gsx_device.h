@@ -229,6 +229,15 @@ struct PropState {
     uint32_t chg_cap;
     uint32_t inc;        // fwd / pin / cent hold the previous call's values: update them incrementally
     uint32_t flast_every;  // k_prop_hop_fast keeps flast at every hop (stepped calls), else at max_hops only
+    // Topic-term cache of the re-scoring fold (k_prop_count<true, true>):
+    // tterm[q * n_topics + t] = topic_score() of record (q, t) (times its
+    // weight), valid for pair q while tgen[q] == tepoch.  The host moves tepoch
+    // whenever anything but this fold may have changed a record, so a fold
+    // recomputes only its own topic's term and re-sums the cached ones in
+    // ascending topic order (bit-identical to eval_pair).  null: off.
+    double* tterm;
+    uint32_t* tgen;
+    uint32_t tepoch;
 };
 
 // pins_only: the fwd bytes stand (a RESCORE count kept them), update the

@@ -227,6 +227,10 @@ struct gsx_engine {
         uint8_t* rfwd = nullptr;                   // fwd of each pair's reverse (k_prop_pin)
         uint32_t *cend = nullptr, *chg = nullptr, *nchg = nullptr;
         uint32_t* rcand = nullptr;  // [pair] RandomSub candidate lists (each node's over its own pair range)
+        double* tterm = nullptr;    // [pair][topic] the re-scoring fold's topic-term cache (PropState::tterm)
+        uint32_t* tgen = nullptr;   // [pair] the epoch its terms were written in
+        uint32_t tepoch = 0;
+        uint64_t t_rec_gen = 0;     // rec_gen as the last caching fold left it (unchanged since: terms current)
         uint64_t* ndirty = nullptr;
         uint32_t chg_cap = 0;
         uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
@@ -324,6 +328,7 @@ struct gsx_engine {
     uint64_t score_writes = 0, h_score_tag = ~0ull;
     bool dirty_zeroed = true;  // d_smask not cleared yet
     void invalidate_scores() {
+        ++rec_gen;
         scores_valid = false;
         dirty_only = false;
         dirty_obs.clear();
@@ -337,7 +342,9 @@ struct gsx_engine {
     // flags, the overlay or the thresholds; score_gen with anything that may
     // change a score (both with the former)
     uint64_t flag_gen = 1, score_gen = 1;
+    uint64_t rec_gen = 1;  // with anything that may change a record other than the propagation fold
     void state_changed() {
+        ++rec_gen;
         ++flag_gen;
         ++score_gen;
     }
@@ -548,7 +555,7 @@ void free_state(gsx_engine* e) {
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
                   e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
                   e->d_halo_pair, e->d_send_slot,
-                  e->prop.d_dig, e->prop.rcand};
+                  e->prop.d_dig, e->prop.rcand, e->prop.tterm, e->prop.tgen};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
@@ -2295,8 +2302,26 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     // this call's settings (unsharded, incremental fwd state)
     const bool rescore = fold_now && e->scores_valid && e->pending.empty() && !e->sharded() && P.fwd_key.valid &&
                          P.fwd_key.score_gen == e->score_gen && P.cfg.router == GSX_ROUTER_GOSSIPSUB;
-    if (ps.credit || ps.late)
-        HIPCHK(e, gsx::launch_prop_count(ps, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
+    if (ps.credit || ps.late) {
+        gsx::PropState pc = ps;
+        // the topic-term cache (several topics: a fold then re-reads one topic's record, not all)
+        static const bool no_tt = getenv("GSX_NO_TERM_CACHE") != nullptr;
+        if (rescore && e->T >= 2 && e->T <= 16 && !no_tt) {
+            if (!P.tterm) {
+                if (int rc = dalloc(e, &P.tterm, (size_t)e->E * e->T)) return rc;
+                if (int rc = dalloc(e, &P.tgen, (size_t)e->E)) return rc;
+                HIPCHK(e, hipMemsetAsync(P.tgen, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
+                P.tepoch = 0;
+                P.t_rec_gen = 0;
+            }
+            if (P.t_rec_gen != e->rec_gen) ++P.tepoch;  // records changed since: every pair's terms stale
+            pc.tterm = P.tterm;
+            pc.tgen = P.tgen;
+            pc.tepoch = P.tepoch;
+        }
+        HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
+        if (pc.tterm) P.t_rec_gen = e->rec_gen;
+    }
     if (ps.credit) {
         // GSX_CREDIT_NOW: k_prop_count folded this call's counts (and any
         // pending ones of the topic) and left the pending counts empty

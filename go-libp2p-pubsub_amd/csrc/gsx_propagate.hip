@@ -1216,6 +1216,47 @@ __device__ __forceinline__ void fold_pair(const PropState& ps, const DevState& s
 // recomputed and, when it changed, listed for the next call's pins — the only
 // scores and bytes the credits can change, so neither a full re-score nor a
 // k_prop_fwd pass is needed before the next call (or heartbeat).
+// score(q) after a fold of topic ps.topic, through the topic-term cache
+// (PropState::tterm): a pair whose terms are current re-reads only the folded
+// topic's record; any other computes and stores every term.  Either way the
+// terms are summed from 0 in ascending topic order, as eval_pair does.
+__device__ __forceinline__ double eval_pair_cached(const PropState& ps, const DevState& s, const DevPeerParams& pp,
+                                                   uint64_t q) {
+    const uint32_t T = s.n_topics;
+    double* tt = ps.tterm + q * T;
+    double score = 0.0;
+    if (ps.tgen[q] == ps.tepoch) {
+        for (uint32_t t = 0; t < T; ++t) {
+            const DevTopicParams& tp = s.tp[t];
+            if (!tp.scored) continue;
+            double term;
+            if (t == ps.topic) {
+                const uint8_t fl = s.rflags[flag_index(q, t, T)];
+                const size_t b = rec_index(q, t, T, FMD);
+                term = topic_score(tp, fl, mesh_time_of(s, fl, q, t), s.rec[b], s.rec[b + MMD * TILE],
+                                   s.rec[b + MFP * TILE], s.rec[b + IMD * TILE]);
+                tt[t] = term;
+            } else {
+                term = tt[t];
+            }
+            score += term;
+        }
+    } else {
+        for (uint32_t t = 0; t < T; ++t) {
+            const DevTopicParams& tp = s.tp[t];
+            if (!tp.scored) continue;
+            const uint8_t fl = s.rflags[flag_index(q, t, T)];
+            const size_t b = rec_index(q, t, T, FMD);
+            const double term = topic_score(tp, fl, mesh_time_of(s, fl, q, t), s.rec[b], s.rec[b + MMD * TILE],
+                                            s.rec[b + MFP * TILE], s.rec[b + IMD * TILE]);
+            tt[t] = term;
+            score += term;
+        }
+        ps.tgen[q] = ps.tepoch;
+    }
+    return score_tail(s, pp, q, score, s.bp[q]);
+}
+
 template <bool FOLD, bool RESCORE>
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, DevPeerParams pp) {
     unsigned long long cnt[1] = {0};
@@ -1265,7 +1306,7 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
                     if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) {
                         fold_pair(ps, s, q, first, dup, k4);
                         if (RESCORE) {
-                            s.score[q] = eval_pair(s, pp, q);
+                            s.score[q] = ps.tterm ? eval_pair_cached(ps, s, pp, q) : eval_pair(s, pp, q);
                             const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
                             if (nb != ob) {
                                 ps.fwd[q] = nb;

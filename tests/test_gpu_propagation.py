@@ -251,6 +251,12 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         ("app scores", "app"),
         ("heartbeat", "heartbeat"),
         ("topic 1", None),
+        ("topic 0 after topic 1", None),  # the fold's topic-term cache: topic 1's cached term, topic 0's recomputed
+        ("topic 1 after topic 0", None),
+        ("trace deliver", "trace"),  # a record of topic 1 changed outside the fold: every cached term is stale
+        ("topic 0 after trace", None),
+        ("topic weight", "tparams"),  # topic 1's weight changed: its cached terms are stale
+        ("topic 0 after weight", None),
         ("floodsub", None),
         ("gossipsub after floodsub", None),
     ]
@@ -268,8 +274,15 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
             elif action == "heartbeat":
                 be.set_gossipsub_params(gp)
                 be.heartbeat(1, pc.T0 + 5 * pc.S, 77)
+            elif action == "trace":
+                for q in range(0, E, max(E // 40, 1)):
+                    be.trace_deliver(int(q), 10_000 + int(q), 1, pc.T0 + 5 * pc.S)
+            elif action == "tparams":
+                tp = synth.spam_test_topic_params()
+                tp.topic_weight = 0.5
+                be.set_topic_params(1, tp)
         router = abi.GSX_ROUTER_FLOODSUB if name == "floodsub" else abi.GSX_ROUTER_GOSSIPSUB
-        topic = 1 if name == "topic 1" else 0
+        topic = 1 if name.startswith("topic 1") else 0
         ms = pc.messages(n, 96, seed=100 + k)
         cfg = pc.config(router, topic=topic, latency_ms=10)
         res = [be.propagate(ms, cfg, want_results=True) for be in (eng, ref)]
