@@ -231,6 +231,7 @@ struct gsx_engine {
         uint32_t* tgen = nullptr;   // [pair] the epoch its terms were written in
         uint32_t tepoch = 0;
         uint64_t t_rec_gen = 0;     // rec_gen as the last caching fold left it (unchanged since: terms current)
+        uint64_t t_plain_gen = 0;   // rec_gen as the last re-scoring fold without the cache left it
         uint64_t* ndirty = nullptr;
         uint32_t chg_cap = 0;
         uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
@@ -2306,7 +2307,11 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         gsx::PropState pc = ps;
         // the topic-term cache (several topics: a fold then re-reads one topic's record, not all)
         static const bool no_tt = getenv("GSX_NO_TERM_CACHE") != nullptr;
-        if (rescore && e->T >= 2 && e->T <= 16 && !no_tt) {
+        // A fold right after other changes (e.g. alternating with heartbeats)
+        // runs without it (its terms would be stale before any later fold reads
+        // them); the second of consecutive folds starts a cache epoch.
+        const bool consecutive = P.t_rec_gen == e->rec_gen || P.t_plain_gen == e->rec_gen;
+        if (rescore && e->T >= 2 && e->T <= 16 && !no_tt && consecutive) {
             if (!P.tterm) {
                 if (int rc = dalloc(e, &P.tterm, (size_t)e->E * e->T)) return rc;
                 if (int rc = dalloc(e, &P.tgen, (size_t)e->E)) return rc;
@@ -2321,6 +2326,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         }
         HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
         if (pc.tterm) P.t_rec_gen = e->rec_gen;
+        else if (rescore) P.t_plain_gen = e->rec_gen;
     }
     if (ps.credit) {
         // GSX_CREDIT_NOW: k_prop_count folded this call's counts (and any
@@ -3328,6 +3334,23 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
         }
         HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
+        if (dbg) {  // the listed nodes of k_gx_ask: count, heavy ones, their pairs
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            uint32_t fl[8];
+            HIPCHK(e, hipMemcpy(fl, e->d_gxflag, sizeof(fl), hipMemcpyDeviceToHost));
+            std::vector<uint32_t> ln(fl[6]);
+            if (!ln.empty())
+                HIPCHK(e, hipMemcpy(ln.data(), e->d_gx_nodes, 4 * ln.size(), hipMemcpyDeviceToHost));
+            size_t heavy = 0, pairs = 0, maxdeg = 0;
+            for (uint32_t x : ln) {
+                heavy += (x >> 31) & 1;
+                const uint32_t u = x & 0x7FFFFFFFu;
+                const size_t d = (size_t)(e->row_ptr[u + 1] - e->row_ptr[u]);
+                pairs += d;
+                maxdeg = std::max(maxdeg, d);
+            }
+            fprintf(stderr, "[gx] listed=%zu heavy=%zu pairs=%zu maxdeg=%zu\n", ln.size(), heavy, pairs, maxdeg);
+        }
         for (size_t i = 0; i < gx_sets.size(); ++i)
             HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
                                            e->stream));

@@ -416,63 +416,87 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
 constexpr uint32_t GX_ML = 64;           // words a receiver's lane handles itself (else: a wave, GX_HEAVY)
 constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
 
-// Pass 1, one lane per receiving node u: handleIHave (:615-679) for the one
-// IHAVE RPC each sender v sent (every topic), senders ascending: the score /
-// MaxIHaveMessages / iasked gates, |iwant| from word popcounts, the asked
-// subset (all; or a uniform kk-subset by selection sampling) and AddPromise's
-// pick (gossip_tracer.go:53).  Only the advertised batches u has not seen
-// whole can hold a candidate: a node with none asks for nothing; one with at
-// most GX_ML such words is handled here; one with more (its lane would walk every
-// unseen batch per sender) is listed for k_gx_node's wave (GX_HEAVY), like
-// every node that asked (pass 2).
+// Pass 1: handleIHave (:615-679) for the one IHAVE RPC each sender v sent
+// (every topic): the score / MaxIHaveMessages / iasked gates, |iwant| from
+// word popcounts, the asked subset (all; or a uniform kk-subset by selection
+// sampling) and AddPromise's pick (gossip_tracer.go:53).  Everything it
+// touches is per pair (the IHAVE counters, the request, the promise of q), so
+// the pairs of a node are independent.  A wave takes 64 consecutive nodes:
+//  - a lane per node finds the advertised batches its node has not seen whole
+//    (only they can hold a candidate) and the words of them where the node
+//    lacks a message (its miss list, in LDS); a node with none asks for
+//    nothing; one with more than GX_ML such words is heavy (k_gx_node's wave
+//    runs its pass 1: GX_HEAVY);
+//  - the lanes then take the tile's pairs in order, a lane per pair (the
+//    per-pair arrays are read coalesced), each against its node's miss list;
+//  - a node with a heavy walk or an asked pair is listed for k_gx_node (pass 2).
 __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
-    // the node's miss list: (batch, word) of its unseen batches where u lacks a
-    // message, canonical order, [entry][lane] (a lane's entries strided: no
-    // bank conflicts); the bits are re-read from u's row (cached) per use
-    __shared__ uint16_t ml_gw[GX_ML][64];  // batch << 6 | word (W <= 64 words per batch here)
+    // miss lists [entry][node of the tile] (batch << 6 | word, W <= 64 words
+    // per batch here); the bits are re-read from u's row (cached) per use
+    __shared__ uint16_t ml_gw[GX_ML][64];
+    __shared__ int64_t rp[65];      // row_ptr of the tile's nodes
+    __shared__ uint64_t nfs[64];    // per node: the unseen-batch mask
+    __shared__ uint32_t nmls[64];   // per node: miss-list length | GX_HEAVY
+    __shared__ uint32_t lst[64];    // per node: listed for k_gx_node
     const uint32_t lane = threadIdx.x;
     uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0;
     uint32_t occ = 0;
     const uint32_t n_gx = h.gx_off[s.n_topics];
-    for (uint32_t u = blockIdx.x * 64u + lane; u < h.n_nodes; u += gridDim.x * 64u) {
-        const int64_t r0 = h.row_ptr[u], r1 = h.row_ptr[u + 1];
-        const uint64_t nf = gx_unseen(h, n_gx, u);
-        // the words u lacks something in (u's own rows, read once per node)
-        uint32_t nml = 0;
-        bool heavy = n_gx > 64 || n_gx > 1024;
-        for (uint64_t m = heavy ? 0 : nf; m && !heavy; m &= m - 1) {
-            const uint32_t g = (uint32_t)__builtin_ctzll(m);
-            const GxBatch& b = h.gx[g];
-            if (b.n_words > 64) {
-                heavy = true;
-                break;
-            }
-            for (uint32_t w = 0; w < b.n_words; ++w) {
-                const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
-                const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
-                const uint64_t miss = ~b.all[(size_t)u * b.n_words + w] & valid;
-                if (!miss) continue;
-                if (nml == GX_ML) {
-                    heavy = true;
-                    break;
+    for (uint32_t tile = blockIdx.x * 64u; tile < h.n_nodes; tile += gridDim.x * 64u) {
+        const uint32_t u = tile + lane;
+        {  // ---- lane per node: unseen batches and the miss list
+            uint64_t nf = 0;
+            uint32_t nml = 0;
+            bool heavy = n_gx > 64;
+            if (u < h.n_nodes) {
+                nf = gx_unseen(h, n_gx, u);
+                for (uint64_t m = heavy ? 0 : nf; m && !heavy; m &= m - 1) {
+                    const uint32_t g = (uint32_t)__builtin_ctzll(m);
+                    const GxBatch& b = h.gx[g];
+                    if (b.n_words > 64) {
+                        heavy = true;
+                        break;
+                    }
+                    for (uint32_t w = 0; w < b.n_words; ++w) {
+                        const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
+                        const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                        const uint64_t miss = ~b.all[(size_t)u * b.n_words + w] & valid;
+                        if (!miss) continue;
+                        if (nml == GX_ML) {
+                            heavy = true;
+                            break;
+                        }
+                        ml_gw[nml][lane] = (uint16_t)(g << 6 | w);
+                        ++nml;
+                    }
                 }
-                ml_gw[nml][lane] = (uint16_t)(g << 6 | w);
-                ++nml;
             }
+            nfs[lane] = nf;
+            nmls[lane] = nml | (heavy ? GX_HEAVY : 0u);
+            lst[lane] = 0;
+            rp[lane] = h.row_ptr[u < h.n_nodes ? u : h.n_nodes];
+            if (lane == 0) rp[64] = h.row_ptr[tile + 64 < h.n_nodes ? tile + 64 : h.n_nodes];
         }
-        bool list = false;
-        for (int64_t q = r0; q < r1; ++q) {
+        __syncthreads();
+        // ---- lane per pair, the tile's pairs in order
+        uint32_t k = 0;  // the node of pair q (monotonic: q only grows)
+        for (int64_t q = rp[0] + lane; q < rp[64]; q += 64) {
+            while (rp[k + 1] <= q) ++k;
             const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
             if (!tall) continue;
             const uint32_t r = h.rev[q];
             const int gt = gx_gate(s, h, (uint64_t)q, r);
             ignored += gt == 1;
+            const uint64_t nf = nfs[k];
             if (gt != 2 || !nf) continue;
-            if (heavy) {
-                list = true;
+            const uint32_t nm = nmls[k];
+            if (nm & GX_HEAVY) {
+                lst[k] = 1;
                 continue;
             }
-            const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);  // joined topics only (:638-641)
+            const uint32_t nml = nm;
+            const uint32_t uu = tile + k;
+            const uint64_t tb = tall & (h.sub ? h.sub[uu] : ~0ull);  // joined topics only (:638-641)
             const uint32_t v = (uint32_t)h.col[q];
             // the unseen batches whose row at v holds a message not every node had:
             // only there can v hold one u lacks
@@ -483,11 +507,11 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             // the subset row of a truncated list)
             uint32_t n = 0;
             for (uint32_t i = 0; i < nml; ++i) {
-                const uint32_t gw = ml_gw[i][lane], g = gw >> 6, w = gw & 63u;
+                const uint32_t gw = ml_gw[i][k], g = gw >> 6, w = gw & 63u;
                 if (!((cb >> g) & 1)) continue;
                 const GxBatch& b = h.gx[g];
                 if (!((tb >> b.topic) & 1)) continue;
-                uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)u * b.n_words + w];
+                uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)uu * b.n_words + w];
                 const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
                 if (sub) c &= sub[b.row_off + w];
                 n += (uint32_t)__popcll(c);
@@ -500,11 +524,11 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                 Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
                 uint32_t j = (uint32_t)g.int31n((int32_t)kk);
                 for (uint32_t i = 0; i < nml; ++i) {
-                    const uint32_t gw = ml_gw[i][lane], gi = gw >> 6, w = gw & 63u;
+                    const uint32_t gw = ml_gw[i][k], gi = gw >> 6, w = gw & 63u;
                     if (!((cb >> gi) & 1)) continue;
                     const GxBatch& b = h.gx[gi];
                     if (!((tb >> b.topic) & 1)) continue;
-                    uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)u * b.n_words + w];
+                    uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)uu * b.n_words + w];
                     const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
                     if (sub) c &= sub[b.row_off + w];
                     const uint32_t pc = (uint32_t)__popcll(c);
@@ -518,15 +542,18 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                     break;
                 }
             } else {
-                gx_pick_sampled(h, tb, u, v, q, r, n, kk, pick_g, pick_k);
+                gx_pick_sampled(h, tb, uu, v, q, r, n, kk, pick_g, pick_k);
             }
             ++iw_msgs;
             iw_ids += kk;
             h.gx_req[q] = kk;
             gx_promise(h, (uint64_t)q, ((uint64_t)h.gx[pick_g].serial << 32) | pick_k, occ);
-            list = true;
+            lst[k] = 1;
         }
-        if (list) h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u | (heavy ? GX_HEAVY : 0u);
+        __syncthreads();
+        if (u < h.n_nodes && lst[lane])  // ---- lane per node: the listed ones
+            h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u | (nmls[lane] & GX_HEAVY);
+        __syncthreads();  // (the tile's LDS is rewritten next)
     }
     gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);
     gx_flush(h.stats, HB_IWANT_MSGS, iw_msgs);
@@ -597,10 +624,13 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
             }
             __threadfence_block();  // gx_req of every pair before pass 2 reads it
         }
-        // ---- pass 2: v answers, u receives
-        for (int64_t q = r0; q < r1; ++q) {
-            const uint32_t kk = h.gx_req[q];  // (wave-uniform)
-            if (!kk) continue;
+        // ---- pass 2: v answers, u receives (the asked pairs found 64 at a time)
+        for (int64_t c0 = r0; c0 < r1; c0 += 64) {
+          const uint32_t kq = c0 + lane < r1 ? h.gx_req[c0 + lane] : 0u;
+          for (uint64_t am = __ballot(kq != 0); am; am &= am - 1) {  // (wave-uniform)
+            const int jb = __builtin_ctzll(am);
+            const int64_t q = c0 + jb;
+            const uint32_t kk = (uint32_t)__shfl((int)kq, jb, 64);
             const uint64_t tall = h.ihave_bits[q];
             const uint32_t r = h.rev[q];
             const bool answered = !(s.score[r] < h.gossip_threshold) &&  // v ignores u's IWANT
@@ -663,6 +693,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 if (answered && h.gx_mark) h.gx_mark[q] = 1;
                 h.gx_req[q] = 0;
             }
+          }
         }
         __threadfence_block();
         // fulfillPromise: u's promises whose message u received in this exchange

@@ -255,8 +255,12 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         ("topic 1 after topic 0", None),
         ("trace deliver", "trace"),  # a record of topic 1 changed outside the fold: every cached term is stale
         ("topic 0 after trace", None),
+        ("topic 1 after trace", None),  # (the cache is armed by consecutive folds: a new epoch here)
+        ("topic 0 after trace, cached", None),
         ("topic weight", "tparams"),  # topic 1's weight changed: its cached terms are stale
         ("topic 0 after weight", None),
+        ("topic 1 after weight", None),
+        ("topic 0 after weight, cached", None),
         ("floodsub", None),
         ("gossipsub after floodsub", None),
     ]

@@ -27,6 +27,7 @@ ap.add_argument("--peers", type=int, default=1_000_000)
 ap.add_argument("--topics", type=int, default=8)
 ap.add_argument("--msgs", type=int, default=256)
 ap.add_argument("--exchange", action="store_true", help="the gossip exchange (D) on, as in bench.py")
+ap.add_argument("--verbose", action="store_true", help="more heartbeat counters per round")
 a = ap.parse_args()
 
 ov, e = bench.build_engine(a.peers, a.topics, 6, synth.SEED, 0)
@@ -51,4 +52,7 @@ for k in range(3 + a.rounds):
     e.sync()
     print(f"tick {tick}: {(time.perf_counter() - t0) * 1e3:.3f} ms grafts={o['grafts']} prunes={o['prunes']} "
           f"ihave={o['ihave_msgs']} iwant={o['iwant_msgs']} delivered={o['gossip_delivered']}", flush=True)
+    if a.verbose:
+        print("   ", {k: o[k] for k in ("ihave_ids", "ihave_ignored", "iwant_ids", "iwant_served", "gossip_rejected",
+                                      "gossip_duplicates", "broken_promises", "penalties")}, flush=True)
 e.close()
