@@ -334,6 +334,7 @@ struct GxBatch {
     uint32_t woff;        // word offset of the batch in the flat word list of all advertised batches
     uint32_t n_msgs;      // messages of the set (bits of the last word past it are never set)
     const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_common)
+    uint32_t nxt;         // the next advertised batch of the same set, cache order (GX_END: none)
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
@@ -411,6 +412,10 @@ struct HbState {
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;
+    // per topic t, heads gx_hoff[t] .. gx_hoff[t + 1]: (first batch of a set in
+    // cache order, the set's word offset in the topic's set-word list)
+    const uint2* gx_heads;
+    const uint32_t* gx_hoff;
     uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
     uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
     uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none)

@@ -194,6 +194,7 @@ struct gsx_engine {
     uint32_t* d_gx_off = nullptr;
     uint8_t* d_gx_got = nullptr;
     size_t gx_cap = 0;
+    uint2* d_gx_heads = nullptr;      // [gx_cap] per topic, the first batch of each set (k_gx_node)
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
     size_t gx_common_cap = 0;         // (sets)
@@ -592,7 +593,7 @@ void free_state(gsx_engine* e) {
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
                        e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
-                       e->d_gx_rhm, e->d_gx_common};
+                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
@@ -614,6 +615,7 @@ void free_state(gsx_engine* e) {
         e->d_gx_got = nullptr;
         e->gx_cap = 0;
         e->d_gx_rhm = e->d_gx_common = nullptr;
+        e->d_gx_heads = nullptr;
         e->gx_common_cap = 0;
         void* mbp[] = {e->d_sub, e->d_psub, e->d_fanout, e->d_fan_has, e->d_lastpub, e->d_mscratch, e->d_mlist};
         for (void* x : mbp)
@@ -3269,6 +3271,30 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                 gx[i].n_msgs = gx_sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
             }
         }
+        // per topic, the sets of its batches: each set's first batch in cache
+        // order and its words' offset (k_gx_node's receipts: a lane per set word
+        // walks the set's batches through `nxt`)
+        std::vector<uint32_t> hoff(e->T + 1, 0);
+        std::vector<uint2> heads;
+        {
+            std::vector<uint32_t> last(gx_sets.size(), ~0u);
+            for (uint32_t t = 0; t < e->T; ++t) {
+                hoff[t] = (uint32_t)heads.size();
+                uint32_t sw = 0;
+                for (uint32_t g = off[t]; g < off[t + 1]; ++g) {
+                    const size_t si = reinterpret_cast<size_t>(gx[g].got);
+                    gx[g].nxt = ~0u;
+                    if (last[si] == ~0u || gx[last[si]].topic != t) {
+                        heads.push_back(make_uint2(g, sw));
+                        sw += gx[g].n_words;
+                    } else {
+                        gx[last[si]].nxt = g;
+                    }
+                    last[si] = g;
+                }
+            }
+            hoff[e->T] = (uint32_t)heads.size();
+        }
         static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
         if (dbg) {
             HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -3293,7 +3319,10 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             e->d_gx_got = nullptr;
             e->gx_cap = std::max<size_t>(gx.size(), 16);
             if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
-            if (int rc = dalloc(e, &e->d_gx_off, (size_t)GSX_MAX_TOPICS + 1)) return rc;
+            if (int rc = dalloc(e, &e->d_gx_off, 2 * ((size_t)GSX_MAX_TOPICS + 1))) return rc;  // off, hoff
+            if (e->d_gx_heads) (void)hipFree(e->d_gx_heads);
+            e->d_gx_heads = nullptr;
+            if (int rc = dalloc(e, &e->d_gx_heads, e->gx_cap)) return rc;
             if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
         }
         // per set, the messages every node had seen as the exchange began (a
@@ -3321,6 +3350,11 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
         HIPCHK(e, hipMemcpy(e->d_gx, gx.data(), sizeof(gsx::GxBatch) * gx.size(), hipMemcpyHostToDevice));
         HIPCHK(e, hipMemcpy(e->d_gx_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_gx_off + GSX_MAX_TOPICS + 1, hoff.data(), 4 * hoff.size(), hipMemcpyHostToDevice));
+        if (!heads.empty())
+            HIPCHK(e, hipMemcpy(e->d_gx_heads, heads.data(), sizeof(uint2) * heads.size(), hipMemcpyHostToDevice));
+        h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
+        h.gx_heads = e->d_gx_heads;
         h.gx = e->d_gx;
         h.gx_off = e->d_gx_off;
         HIPCHK(e, gsx::launch_gx_rhm(e->d_gx, (uint32_t)gx.size(), (uint32_t)N, e->d_gx_rhm, e->stream));

@@ -413,6 +413,7 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
     });
 }
 
+constexpr uint32_t GX_END = 0xFFFFFFFFu;  // GxBatch::nxt: the set's last batch
 constexpr uint32_t GX_ML = 64;           // words a receiver's lane handles itself (else: a wave, GX_HEAVY)
 constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
 
@@ -645,14 +646,23 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                         const uint32_t t = (uint32_t)__builtin_ctzll(tm);
                         const uint64_t* sub = gx_subrow(h, tr, t, r);
                         uint32_t k1 = 0, k2 = 0, k4 = 0;
-                        for (uint32_t gi = h.gx_off[t]; gi < h.gx_off[t + 1]; ++gi) {
+                        // a lane per (message set, word) of the topic: it walks the
+                        // set's batches in cache order (the one order its receipt word
+                        // sees); different sets touch different receipt rows
+                        const uint32_t h0 = h.gx_hoff[t], h1 = h.gx_hoff[t + 1];
+                        const uint32_t total = h0 < h1 ? h.gx_heads[h1 - 1].y + h.gx[h.gx_heads[h1 - 1].x].n_words : 0;
+                        uint32_t hi = h0;
+                        for (uint32_t f = lane; f < total; f += 64) {
+                          while (hi + 1 < h1 && h.gx_heads[hi + 1].y <= f) ++hi;
+                          const uint32_t w = f - h.gx_heads[hi].y;
+                          for (uint32_t gi = h.gx_heads[hi].x; gi != GX_END; gi = h.gx[gi].nxt) {
                             if (gx_skip(nf, gi)) continue;
                             const GxBatch& b = h.gx[gi];
                             // no longer in v's cache; or GetForPeer's count above GossipRetransmission
                             if (!b.avail || gp.retransmission < 1) continue;
                             const uint32_t W = b.n_words;
                             bool got = false;
-                            for (uint32_t w = lane; w < W; w += 64) {
+                            {
                                 const uint64_t m = gx_word(b, u, v, w, sub);
                                 if (!m) continue;
                                 uint64_t* xw = b.x + (size_t)u * W + w;
@@ -678,6 +688,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                 }
                             }
                             if (got) *b.got = 1;
+                          }
                         }
                         k1 = gx_wsum(k1);
                         k2 = gx_wsum(k2);
