@@ -333,7 +333,7 @@ struct GxBatch {
     uint32_t row_off;     // word offset of the batch in its topic's gossip rows (GxSub)
     uint32_t woff;        // word offset of the batch in the flat word list of all advertised batches
     uint32_t n_msgs;      // messages of the set (bits of the last word past it are never set)
-    const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_common)
+    const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_setprep)
     uint32_t nxt;         // the next advertised batch of the same set, cache order (GX_END: none)
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
@@ -484,15 +484,21 @@ hipError_t launch_hb_fanout(const DevState& s, const HbState& h, uint32_t t, hip
 hipError_t launch_join(const DevState& s, const HbState& h, const uint32_t* nodes, const uint32_t* topics,
                        uint32_t n, uint32_t leave, hipStream_t st);
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st);
-// The messages of a set every node has seen (AND of its seen rows; common
-// preset to ~0 by the caller, n_words <= 64); per node, the advertised batches
-// whose cache row holds any other message (gx_rhm: only there can the node
-// hold a message some receiver lacks).
-hipError_t launch_gx_common(const uint64_t* all, uint32_t n_words, uint32_t n_nodes, uint64_t* common, hipStream_t st);
+// Per node, the advertised batches whose cache row holds a message outside
+// its set's common words (gx_rhm: only there can the node hold a message some
+// receiver lacks).
 hipError_t launch_gx_rhm(const GxBatch* gx, uint32_t n_gx, uint32_t n_nodes, uint64_t* rhm, hipStream_t st);
-// full[v] = node v has seen every one of the set's n_msgs messages (its `all` row is full)
-hipError_t launch_gx_full(const uint64_t* all, uint32_t n_words, uint32_t n_msgs, uint32_t n_nodes, uint8_t* full,
-                          hipStream_t st);
+// One pass over the seen rows of every message set of an exchange (blockIdx.y =
+// set): the receipt rows zeroed, `full` recomputed (when non-null) and the
+// common words ANDed (when non-null; preset to ~0 by the caller).
+struct GxSetPrep {
+    const uint64_t* all;
+    uint64_t* x;
+    uint8_t* full;
+    uint64_t* common;
+    uint32_t n_words, n_msgs;
+};
+hipError_t launch_gx_setprep(const GxSetPrep* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // Promise slots [pair][from] -> [pair][to] (to > from; new slots free).
 hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
                                int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);

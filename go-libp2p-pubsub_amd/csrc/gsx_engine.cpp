@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -195,6 +196,9 @@ struct gsx_engine {
     uint8_t* d_gx_got = nullptr;
     size_t gx_cap = 0;
     uint2* d_gx_heads = nullptr;      // [gx_cap] per topic, the first batch of each set (k_gx_node)
+    gsx::GxSetPrep* d_gx_sp = nullptr;  // [gx_common_cap] the exchange's sets (k_gx_setprep)
+    void* h_gxstage = nullptr;        // pinned staging of the exchange's batch list (hb_end)
+    size_t h_gxstage_bytes = 0;
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
     size_t gx_common_cap = 0;         // (sets)
@@ -593,7 +597,7 @@ void free_state(gsx_engine* e) {
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
                        e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
-                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads};
+                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
@@ -616,6 +620,7 @@ void free_state(gsx_engine* e) {
         e->gx_cap = 0;
         e->d_gx_rhm = e->d_gx_common = nullptr;
         e->d_gx_heads = nullptr;
+        e->d_gx_sp = nullptr;
         e->gx_common_cap = 0;
         void* mbp[] = {e->d_sub, e->d_psub, e->d_fanout, e->d_fan_has, e->d_lastpub, e->d_mscratch, e->d_mlist};
         for (void* x : mbp)
@@ -974,6 +979,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->d_mparts) (void)hipFree(e->d_mparts);
     if (e->d_stage) (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
@@ -2848,10 +2854,12 @@ int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const st
         if (max_ids[t] <= (uint32_t)std::max(e->gp.max_ihave_length, 0) || e->tgt_bound == 0) continue;
         gsx_engine::SubPool& sp = e->subp[t];
         if (sp.rows < e->tgt_bound || sp.tw < tw[t]) {
+            // (grown by half again at least: the advertised windows widen over a
+            // run's first rounds, and a multi-GB free + malloc stalls the round)
+            const size_t tw_a = std::max<size_t>(tw[t], sp.tw + sp.tw / 2);
             if (sp.pool) (void)hipFree(sp.pool);
             sp.pool = nullptr;
             sp.rows = sp.tw = 0;
-            const size_t tw_a = std::max<size_t>(tw[t], sp.tw);
             if (int rc = dalloc(e, &sp.pool, (size_t)e->tgt_bound * tw_a)) return rc;
             sp.rows = e->tgt_bound;
             sp.tw = tw_a;
@@ -2888,9 +2896,20 @@ static int dbg_sync_mask() {
 }
 #define DBG_SYNC(bit) \
     if (dbg_sync_mask() & (bit)) HIPCHK(e, hipStreamSynchronize(e->stream))
+// GSX_DBG_HOST: host microseconds between checkpoints of a heartbeat (stderr)
+static void dbg_host(const char* what) {
+    static const bool on = getenv("GSX_DBG_HOST") != nullptr;
+    if (!on) return;
+    static auto last = std::chrono::steady_clock::now();
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[host] %-14s %8.1f us\n", what,
+            std::chrono::duration<double, std::micro>(now - last).count());
+    last = now;
+}
 int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, bool state_only) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     DBG_SYNC(1);
+    dbg_host("hb start");
     e->state_changed();
     if (e->sharded() && (e->n_ranks > 1 ? !e->d_send_pair : true))
         return fail(e, GSX_ESTATE, "heartbeat on a range shard needs its shard plan (gsx_shard_*_plan)");
@@ -3073,6 +3092,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         e->hb = h;
         return GSX_OK;
     }
+    dbg_host("hb memsets");
     if (tick % 15 == 0) HIPCHK(e, gsx::launch_hb_clear_backoff(h, e->T, e->stream));  // :1585-1604
     // GetGossipIDs inputs: per topic, the batches of windows [0, HistoryGossip) in order.
     // Cache slots are word-aligned: message k of a batch is slot 64 * (the
@@ -3127,6 +3147,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                  hipMemcpyHostToDevice, e->stream));
     }
     h.mc_digest = e->d_mc_digest;
+    dbg_host("hb gb lists");
     DBG_SYNC(2);
     // the truncated IHAVE lists' rows (exchange on, a window longer than MaxIHaveLength)
     if (gx_on)
@@ -3147,6 +3168,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // and control bits, so the maintenance of a run of topics is one launch; a
     // topic's gossip reads the live scores maintenance left (gossipsub.go:1514), so it goes
     // after its own topic's run and before the next
+    dbg_host("hb sub/ihave");
     HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
     for (uint32_t t = 0, tb = 0; t < e->T; ++t) {
         const bool g = gb_off[t + 1] > gb_off[t] && max_ids[t] > 0;
@@ -3177,6 +3199,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.inbox : nullptr));
     e->hb = h;
     e->hb_active = true;
+    dbg_host("hb (A) queued");
     return GSX_OK;
 }
 
@@ -3219,8 +3242,10 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     std::vector<gsx_engine::MsgSet*> gx_sets;
     std::vector<uint64_t*> gx_x;
     const bool gx_run = e->gp.gossip_exchange && h.ihave_bits && e->have_gossip;
+    dbg_host("hb (B)(C)");
     if (gx_run) {
         std::vector<gsx::GxBatch> gx;
+        std::vector<bool> gx_full_new;  // per set: its full bytes are recomputed this round
         std::vector<uint32_t> off(e->T + 1, 0);
         const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
         const size_t N = e->n_nodes;
@@ -3237,19 +3262,18 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                     while (i < gx_sets.size() && gx_sets[i] != b.set) ++i;
                     if (i == gx_sets.size()) {
                         const size_t words = (size_t)b.set->n_words * N + 2 * N;  // rows + (dig, cnt) tail
-                        uint64_t* x = seen_acquire(e, words);
+                        uint64_t* x = seen_acquire(e, words);  // (rows zeroed by k_gx_setprep)
                         if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
-                        HIPCHK(e, hipMemsetAsync(x, 0, 8 * (size_t)b.set->n_words * N, e->stream));
                         gsx_engine::MsgSet* ms = b.set;
-                        if (!ms->full_ok) {  // which nodes have seen the whole set (skipped by the walk)
+                        // which nodes have seen the whole set (skipped by the walk): k_gx_setprep
+                        gx_full_new.push_back(!ms->full_ok);
+                        if (!ms->full_ok) {
                             if (!ms->d_full) {
                                 size_t got = 0;
                                 ms->d_full = small_acquire(e, N, &got);
                                 if (!ms->d_full) return fail(e, GSX_ENOMEM, "message set full bytes");
                                 ms->full_bytes = got;
                             }
-                            HIPCHK(e, gsx::launch_gx_full(ms->d_all, ms->n_words, ms->n_msgs, (uint32_t)N, ms->d_full,
-                                                          e->stream));
                             ms->full_ok = true;
                         }
                         ++ms->refs;  // held until the recovered copies are cached (the Shift may drop its batches)
@@ -3295,6 +3319,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             }
             hoff[e->T] = (uint32_t)heads.size();
         }
+        dbg_host("gx sets");
         static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
         if (dbg) {
             HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -3317,7 +3342,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             e->d_gx = nullptr;
             e->d_gx_off = nullptr;
             e->d_gx_got = nullptr;
-            e->gx_cap = std::max<size_t>(gx.size(), 16);
+            // (doubling, 64 at least: a free here waits for every queued kernel)
+            e->gx_cap = std::max<size_t>(std::max<size_t>(gx.size(), 2 * e->gx_cap), 64);
             if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
             if (int rc = dalloc(e, &e->d_gx_off, 2 * ((size_t)GSX_MAX_TOPICS + 1))) return rc;  // off, hoff
             if (e->d_gx_heads) (void)hipFree(e->d_gx_heads);
@@ -3329,30 +3355,59 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         // set wider than 64 words keeps none: its rows are filtered by emptiness)
         if (gx_sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
             if (e->d_gx_common) (void)hipFree(e->d_gx_common);
+            if (e->d_gx_sp) (void)hipFree(e->d_gx_sp);
             e->d_gx_common = nullptr;
-            e->gx_common_cap = std::max<size_t>(gx_sets.size(), 8);
+            e->d_gx_sp = nullptr;
+            e->gx_common_cap = std::max<size_t>(std::max<size_t>(gx_sets.size(), 2 * e->gx_common_cap), 32);
             if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
+            if (int rc = dalloc(e, &e->d_gx_sp, e->gx_common_cap)) return rc;
             if (!e->d_gx_rhm)
                 if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
         }
+        std::vector<gsx::GxSetPrep> sprep(gx_sets.size());
         for (size_t i = 0; i < gx_sets.size(); ++i) {
-            uint64_t* cm = e->d_gx_common + 64 * i;
-            const uint32_t W = gx_sets[i]->n_words;
-            if (W > 64) continue;
-            HIPCHK(e, hipMemsetAsync(cm, 0xff, 8 * (size_t)W, e->stream));
-            HIPCHK(e, gsx::launch_gx_common(gx_sets[i]->d_all, W, (uint32_t)N, cm, e->stream));
+            const gsx_engine::MsgSet* ms = gx_sets[i];
+            sprep[i] = gsx::GxSetPrep{ms->d_all, gx_x[i], gx_full_new[i] ? ms->d_full : nullptr,
+                                      ms->n_words <= 64 ? e->d_gx_common + 64 * i : nullptr, ms->n_words, ms->n_msgs};
         }
+        HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * gx_sets.size(), e->stream));
         for (auto& g : gx) {
             const size_t si = reinterpret_cast<size_t>(g.got);
             g.common = gx_sets[si]->n_words <= 64 ? e->d_gx_common + 64 * si : nullptr;
             g.got = e->d_gx_got + si;
         }
         HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
-        HIPCHK(e, hipMemcpy(e->d_gx, gx.data(), sizeof(gsx::GxBatch) * gx.size(), hipMemcpyHostToDevice));
-        HIPCHK(e, hipMemcpy(e->d_gx_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice));
-        HIPCHK(e, hipMemcpy(e->d_gx_off + GSX_MAX_TOPICS + 1, hoff.data(), 4 * hoff.size(), hipMemcpyHostToDevice));
-        if (!heads.empty())
-            HIPCHK(e, hipMemcpy(e->d_gx_heads, heads.data(), sizeof(uint2) * heads.size(), hipMemcpyHostToDevice));
+        {  // the batch list, offsets and set heads through a pinned staging buffer:
+            // async copies, so the host keeps queueing instead of waiting for the
+            // kernels before them (the last round's copies drained at its end)
+            const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_hoff = 4 * hoff.size(),
+                         b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size();
+            const size_t a_sp = (b_gx + b_off + b_hoff + b_heads + 15) & ~(size_t)15;
+            const size_t need = a_sp + b_sp;
+            if (e->h_gxstage_bytes < need) {
+                if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+                e->h_gxstage = nullptr;
+                e->h_gxstage_bytes = 0;
+                HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
+                e->h_gxstage_bytes = 2 * need;
+            }
+            char* hs = static_cast<char*>(e->h_gxstage);
+            std::memcpy(hs, gx.data(), b_gx);
+            std::memcpy(hs + b_gx, off.data(), b_off);
+            std::memcpy(hs + b_gx + b_off, hoff.data(), b_hoff);
+            if (b_heads) std::memcpy(hs + b_gx + b_off + b_hoff, heads.data(), b_heads);
+            HIPCHK(e, hipMemcpyAsync(e->d_gx, hs, b_gx, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(e, hipMemcpyAsync(e->d_gx_off, hs + b_gx, b_off, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(e, hipMemcpyAsync(e->d_gx_off + GSX_MAX_TOPICS + 1, hs + b_gx + b_off, b_hoff, hipMemcpyHostToDevice,
+                                     e->stream));
+            if (b_heads)
+                HIPCHK(e, hipMemcpyAsync(e->d_gx_heads, hs + b_gx + b_off + b_hoff, b_heads, hipMemcpyHostToDevice,
+                                         e->stream));
+            std::memcpy(hs + a_sp, sprep.data(), b_sp);
+            HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
+            // receipt rows zeroed, full bytes, common words: every set in one pass
+            HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
+        }
         h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
         h.gx_heads = e->d_gx_heads;
         h.gx = e->d_gx;
@@ -3367,6 +3422,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             h.gx_mark = e->d_dirty + 3 * e->E;  // (the broken-promise mask of hb_begin, read by then)
             HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
         }
+        dbg_host("gx prepared");
         HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
         if (dbg) {  // the listed nodes of k_gx_ask: count, heavy ones, their pairs
             HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -3404,7 +3460,9 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         if (!got.empty())
             HIPCHK(e, hipMemcpyAsync(got.data(), e->d_gx_got, got.size(), hipMemcpyDeviceToHost, e->stream));
     }
+    dbg_host("gx queued");
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    dbg_host("hb drained");
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
     // a bulk round's (B) left the control words: one clear at the next round's start
@@ -3452,6 +3510,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         if (merged) ms->full_ok = false;  // the receipts were merged into their seen rows
         set_release(e, ms);
     }
+    dbg_host("hb shift+put");
     if (gflag[0] || gflag[1])
         return fail(e, GSX_ESTATE, "gossip exchange: internal bound broken (truncated-list rows / promise slots)");
     // every pair keeps a free promise slot for the next exchange (one promise per pair each)

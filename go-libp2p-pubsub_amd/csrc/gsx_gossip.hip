@@ -119,15 +119,6 @@ __global__ __launch_bounds__(256) void k_gx_prom_grow(const uint64_t* __restrict
     }
 }
 
-__global__ __launch_bounds__(256) void k_gx_full(const uint64_t* __restrict__ all, uint32_t W, uint32_t n_msgs,
-                                                 uint32_t n, uint8_t* __restrict__ full) {
-    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
-        uint32_t c = 0;
-        for (uint32_t w = 0; w < W; ++w) c += (uint32_t)__popcll(all[(size_t)v * W + w]);
-        full[v] = c == n_msgs;
-    }
-}
-
 // The candidate word (batch b, word w) of the ids v advertised to u that u
 // had not seen, within the subset row of a truncated list.
 // u's own row first: v's cache word is read only where u lacks a message
@@ -736,25 +727,6 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
     if (lane == 0 && occ) atomicMax(h.prom_occ, occ);
 }
 
-// AND of a set's seen rows over the nodes: a thread keeps one word (the
-// stride is a multiple of W), the block ANDs in LDS, one atomic per (block, word).
-__global__ __launch_bounds__(256) void k_gx_common(const uint64_t* __restrict__ all, uint32_t W, uint32_t n,
-                                                   unsigned long long* __restrict__ common) {
-    __shared__ unsigned long long sw[64];
-    if (threadIdx.x < 64) sw[threadIdx.x] = ~0ull;
-    __syncthreads();
-    const uint64_t threads = (uint64_t)gridDim.x * 256u;
-    const uint64_t stride = threads / W * W;
-    const uint64_t t0 = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (t0 < stride) {
-        unsigned long long acc = ~0ull;
-        for (uint64_t i = t0; i < (uint64_t)n * W; i += stride) acc &= all[i];
-        atomicAnd(&sw[t0 % W], acc);
-    }
-    __syncthreads();
-    if (threadIdx.x < W) atomicAnd(&common[threadIdx.x], sw[threadIdx.x]);
-}
-
 // Per node v, bit g: v's row of advertised batch g holds a message outside
 // its set's common words (batches past 64: always set).  Thread v reads its W
 // words of each batch row (adjacent nodes, adjacent rows: coalesced).
@@ -771,6 +743,41 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
         }
         rhm[v] = m;
     }
+}
+
+// Thread per node v of set blockIdx.y: its W seen words read once (popcount
+// for `full`, zeros to the receipt row, an AND per word reduced over the wave
+// and the block, one atomic per (block, word)).
+__global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict__ sets, uint32_t n) {
+    __shared__ unsigned long long sw[64];
+    const GxSetPrep S = sets[blockIdx.y];
+    const uint32_t W = S.n_words;
+    const bool and_words = S.common != nullptr && W <= 64;
+    if (threadIdx.x < 64) sw[threadIdx.x] = ~0ull;
+    __syncthreads();
+    const uint32_t stride = gridDim.x * 256u;
+    // (a uniform trip count: every lane takes part in the wave reductions)
+    for (uint32_t v0 = blockIdx.x * 256u; v0 < n; v0 += stride) {
+        const uint32_t v = v0 + threadIdx.x;
+        const bool in = v < n;
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            const uint64_t x = in ? S.all[(size_t)v * W + w] : ~0ull;
+            if (in) {
+                c += (uint32_t)__popcll(x);
+                S.x[(size_t)v * W + w] = 0;
+            }
+            if (and_words) {
+                uint64_t a = x;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) a &= (uint64_t)__shfl_xor((long long)a, off, 64);
+                if ((threadIdx.x % 64) == 0) atomicAnd(&sw[w], (unsigned long long)a);
+            }
+        }
+        if (in && S.full) S.full[v] = c == S.n_msgs;
+    }
+    __syncthreads();
+    if (and_words && threadIdx.x < W) atomicAnd(reinterpret_cast<unsigned long long*>(&S.common[threadIdx.x]), sw[threadIdx.x]);
 }
 
 // The exchange's receipts into the message set: seen |= x; the receipt rows
@@ -796,16 +803,15 @@ hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_gx_common(const uint64_t* all, uint32_t n_words, uint32_t n_nodes, uint64_t* common, hipStream_t st) {
-    if (n_nodes == 0 || n_words == 0 || n_words > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_gx_common, dim3(gx_blocks((uint64_t)n_nodes * n_words, 256, 1024)), dim3(256), 0, st, all,
-                       n_words, n_nodes, reinterpret_cast<unsigned long long*>(common));
-    return hipGetLastError();
-}
-
 hipError_t launch_gx_rhm(const GxBatch* gx, uint32_t n_gx, uint32_t n_nodes, uint64_t* rhm, hipStream_t st) {
     if (n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_rhm, dim3(gx_blocks(n_nodes, 256, 4096)), dim3(256), 0, st, gx, n_gx, n_nodes, rhm);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_setprep(const GxSetPrep* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st) {
+    if (n_sets == 0 || n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_setprep, dim3(gx_blocks(n_nodes, 256, 512), n_sets), dim3(256), 0, st, sets, n_nodes);
     return hipGetLastError();
 }
 
@@ -828,14 +834,6 @@ hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32
     if (n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_prom_grow, dim3(gx_blocks(n_pairs * to, 256, 8192)), dim3(256), 0, st, h_in, e_in, from,
                        h_out, e_out, to, n_pairs);
-    return hipGetLastError();
-}
-
-hipError_t launch_gx_full(const uint64_t* all, uint32_t n_words, uint32_t n_msgs, uint32_t n_nodes, uint8_t* full,
-                          hipStream_t st) {
-    if (n_nodes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gx_full, dim3(gx_blocks(n_nodes, 256, 8192)), dim3(256), 0, st, all, n_words, n_msgs, n_nodes,
-                       full);
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ step() {  # step NAME SECONDS CMD...
     tail -n 4 "$O/$name.log"
     if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
-[ -z "$K" ] || step tests 600 ./tools/gpu_keepalive.sh python -u -m pytest tests -m gpu -x -q -k "$K" \
+[ -z "$K" ] || step tests 900 ./tools/gpu_keepalive.sh python -u -m pytest tests -m gpu -x -q -k "$K" \
     --timeout 300 --timeout-method thread
 step p64 200 rocprofv3 --kernel-trace --stats -d "$O/p64" -o kt --output-format csv -- \
     python3 tools/prop_profile.py --msgs 64 --batches 8
