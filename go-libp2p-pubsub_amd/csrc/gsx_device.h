@@ -335,6 +335,7 @@ struct GxBatch {
     uint32_t n_msgs;      // messages of the set (bits of the last word past it are never set)
     const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_setprep)
     uint32_t nxt;         // the next advertised batch of the same set, cache order (GX_END: none)
+    uint32_t dense;       // a first-hand batch (most rows hold uncommon messages): k_gx_rhm sets its bit unread
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit

@@ -152,6 +152,7 @@ struct gsx_engine {
         uint32_t* d_cnt = nullptr;
         std::vector<uint64_t> ids;
         MsgSet* set = nullptr;  // (unsharded engines)
+        bool recovered = false;  // the receipt rows of an exchange (sparse: most nodes' rows empty)
     };
     std::deque<std::vector<McBatch>> mc;
     // gossip exchange state (allocated when first enabled)
@@ -2854,9 +2855,9 @@ int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const st
         if (max_ids[t] <= (uint32_t)std::max(e->gp.max_ihave_length, 0) || e->tgt_bound == 0) continue;
         gsx_engine::SubPool& sp = e->subp[t];
         if (sp.rows < e->tgt_bound || sp.tw < tw[t]) {
-            // (grown by half again at least: the advertised windows widen over a
-            // run's first rounds, and a multi-GB free + malloc stalls the round)
-            const size_t tw_a = std::max<size_t>(tw[t], sp.tw + sp.tw / 2);
+            // (doubled at least: the advertised windows widen over a run's first
+            // rounds, and a multi-GB free + malloc stalls the round)
+            const size_t tw_a = std::max<size_t>(std::max<size_t>(tw[t], 2 * sp.tw), 64);
             if (sp.pool) (void)hipFree(sp.pool);
             sp.pool = nullptr;
             sp.rows = sp.tw = 0;
@@ -3284,6 +3285,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                                               b.n_words, b.set->serial, t,
                                               (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
                     gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
+                    gx.back().dense = b.recovered ? 0u : 1u;
                 }
         }
         off[e->T] = (uint32_t)gx.size();
@@ -3497,6 +3499,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         b.d_cnt = reinterpret_cast<uint32_t*>(gx_x[i] + (size_t)ms->n_words * N + N);
         b.ids = ms->ids;
         b.set = ms;
+        b.recovered = true;
         ++ms->refs;
         HIPCHK(e, gsx::launch_mc_summary(b.d_seen, (uint32_t)N, ms->n_words, ms->n_msgs, ms->d_dg,
                                          ms->d_dg + (size_t)ms->n_words * 64, b.d_dig, b.d_cnt, e->stream));

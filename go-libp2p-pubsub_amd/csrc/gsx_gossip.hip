@@ -728,7 +728,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
 }
 
 // Per node v, bit g: v's row of advertised batch g holds a message outside
-// its set's common words (batches past 64: always set).  Thread v reads its W
+// its set's common words (batches past 64, first-hand batches: always set).  Thread v reads its W
 // words of each batch row (adjacent nodes, adjacent rows: coalesced).
 __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, uint32_t n_gx, uint32_t n,
                                                 uint64_t* __restrict__ rhm) {
@@ -736,6 +736,10 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
         uint64_t m = n_gx > 64 ? ~0ull : 0ull;
         for (uint32_t g = 0; g < n_gx && g < 64; ++g) {
             const GxBatch& b = gx[g];
+            if (b.dense) {  // (a set bit only lets the ask read the row: always safe)
+                m |= 1ull << g;
+                continue;
+            }
             const uint32_t W = b.n_words;
             uint64_t any = 0;
             for (uint32_t w = 0; w < W; ++w) any |= b.mem[(size_t)v * W + w] & ~(b.common ? b.common[w] : 0ull);
