@@ -1257,6 +1257,134 @@ __device__ __forceinline__ double eval_pair_cached(const PropState& ps, const De
     return score_tail(s, pp, q, score, s.bp[q]);
 }
 
+// k_prop_count's fold + re-score for one topic (the propagation engines'
+// shape), DU pairs at a time in three phases — the counts, then every load
+// the fold, score() and the forwarding byte need, then the arithmetic and the
+// stores — so a thread waits for one round of latencies per batch, not three
+// per pair (the stores of one pair no longer order the next pair's loads).
+// Bit-identical to fold_pair + eval_pair + fwd_byte pair by pair: the same
+// operations on the same values in the same order.
+__device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevState& s, const DevPeerParams& pp,
+                                               uint64_t q0, uint64_t stride, const uint32_t (&k1a)[DU],
+                                               const uint32_t (&ra)[DU], const uint32_t (&ca)[DU], bool fold_topic,
+                                               unsigned long long& backsends) {
+    const uint32_t t = ps.topic;
+    uint32_t fa[DU], da[DU], k4a[DU];
+    bool doit[DU];
+#pragma unroll
+    for (int i = 0; i < DU; ++i) {  // counts (as the general loop)
+        const uint64_t q = q0 + i * stride;
+        doit[i] = false;
+        fa[i] = da[i] = k4a[i] = 0;
+        if (q >= ps.n_pairs) continue;
+        const uint32_t k1 = k1a[i], r = ra[i];
+        const bool local = r != NO_PAIR && !(r & HALO);
+        if (ps.credit) {
+            const uint32_t f0 = ps.pending ? ps.firstcnt[q] : 0, d0 = ps.pending ? ps.dupcnt[q] : 0;
+            uint32_t first = f0 + k1, dup = d0;
+            if (local) {
+                if (ps.late) dup += ca[i] - k1;
+                else dup -= ca[i];
+            }
+            if (f0 | d0) {
+                ps.firstcnt[q] = 0;
+                ps.dupcnt[q] = 0;
+            }
+            uint32_t k4 = 0;
+            if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
+            fa[i] = first;
+            da[i] = dup;
+            k4a[i] = k4;
+            doit[i] = (first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT);
+        }
+        if (ps.late && local) backsends += k1;
+    }
+    uint8_t fl[DU];
+    double fmd[DU], mmd[DU], mfp[DU], imd[DU], app[DU], bp[DU];
+    int64_t graft[DU];
+    uint2 ipg[DU];
+#pragma unroll
+    for (int i = 0; i < DU; ++i) {  // every load of the batch
+        if (!doit[i]) continue;
+        const uint64_t q = q0 + i * stride;
+        const size_t b = rec_index(q, t, 1, FMD);
+        fl[i] = s.rflags[flag_index(q, t, 1)];
+        fmd[i] = s.rec[b + FMD * TILE];
+        mmd[i] = s.rec[b + MMD * TILE];
+        mfp[i] = s.rec[b + MFP * TILE];
+        imd[i] = s.rec[b + IMD * TILE];
+        graft[i] = reinterpret_cast<const int64_t*>(s.rec)[rec_index(q, t, 1, GRAFT)];
+        app[i] = s.app[q];
+        bp[i] = s.bp[q];
+        if (pp.w6 != 0.0) ipg[i] = reinterpret_cast<const uint2*>(s.ipg)[q];
+    }
+    uint32_t ipc[DU][2];
+    if (pp.w6 != 0.0) {
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            ipc[i][0] = ipc[i][1] = 0;
+            if (!doit[i]) continue;
+            const uint32_t gs[2] = {ipg[i].x, ipg[i].y};
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (!(gs[k] == IPG_NONE || (gs[k] & IPG_WL))) ipc[i][k] = s.ipcount[gs[k]];
+        }
+    }
+    const DevTopicParams& tp = s.tp[t];
+#pragma unroll
+    for (int i = 0; i < DU; ++i) {  // fold_pair, eval_pair, fwd_byte
+        if (!doit[i]) continue;
+        const uint64_t q = q0 + i * stride;
+        const size_t b = rec_index(q, t, 1, FMD);
+        const uint32_t k1 = fa[i], k2 = da[i], k4 = k4a[i];
+        if (k4) {
+            imd[i] = add_ones_capped(imd[i], k4, __builtin_inf());
+            s.rec[b + IMD * TILE] = imd[i];
+        }
+        if (k1 | k2) {
+            fmd[i] = add_ones_capped(fmd[i], k1, tp.cap2);
+            s.rec[b + FMD * TILE] = fmd[i];
+            if (fl[i] & REC_IN_MESH) {
+                mmd[i] = add_ones_capped(mmd[i], k1 + k2, tp.cap3);
+                s.rec[b + MMD * TILE] = mmd[i];
+            }
+        }
+        const int64_t mt = (!(fl[i] & REC_IN_MESH) || (fl[i] & REC_FRESH)) ? 0 : s.last_refresh - graft[i];
+        double score = 0.0;
+        score += topic_score(tp, fl[i], mt, fmd[i], mmd[i], mfp[i], imd[i]);
+        // score_tail with the loaded values
+        if (pp.topic_score_cap > 0 && score > pp.topic_score_cap) score = pp.topic_score_cap;
+        score += app[i] * pp.w5;
+        if (pp.w6 != 0.0) {
+            double p6 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t id = k ? ipg[i].y : ipg[i].x;
+                if (id == IPG_NONE || (id & IPG_WL)) continue;
+                const int64_t peers_in_ip = (int64_t)ipc[i][k];
+                if (peers_in_ip > pp.thr6) {
+                    const double surpluss = (double)(peers_in_ip - pp.thr6);
+                    p6 += surpluss * surpluss;
+                }
+            }
+            score += p6 * pp.w6;
+        }
+        if (bp[i] > pp.thr7) {
+            const double excess = bp[i] - pp.thr7;
+            const double p7 = excess * excess;
+            score += p7 * pp.w7;
+        }
+        s.score[q] = score;
+        const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
+        if (nb != ob) {
+            ps.fwd[q] = nb;
+            const uint32_t k = atomicAdd(ps.nchg, 1u);
+            if (k < ps.chg_cap) ps.chg[k] = (uint32_t)q;
+            if ((nb ^ ob) & FWD_GIN) atomicAdd(ps.gray_pairs, (nb & FWD_GIN) ? 1ull : ~0ull);  // (+1 / -1)
+        }
+    }
+}
+
 template <bool FOLD, bool RESCORE>
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, DevPeerParams pp) {
     unsigned long long cnt[1] = {0};
@@ -1279,6 +1407,10 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
             // (rfwd: the reverse pair's byte as this call's pins read it), nothing else
             const bool wrote = !ps.late || (q < ps.n_pairs && (ps.rfwd[q] & FWD_SEND));
             ca[i] = (local && ps.credit && wrote) ? ps.corr[ra[i]] : 0;
+        }
+        if (RESCORE && s.n_topics == 1) {  // (uniform) one topic: the batched fold + re-score
+            fold_rescore_1(ps, s, pp, q0, stride, k1a, ra, ca, fold_topic, cnt[0]);
+            continue;
         }
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
