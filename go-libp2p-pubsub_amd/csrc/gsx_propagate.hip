@@ -1385,7 +1385,7 @@ __device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevSta
     }
 }
 
-template <bool FOLD, bool RESCORE>
+template <bool FOLD, bool RESCORE, bool ONE_TOPIC = false>
 __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, DevPeerParams pp) {
     unsigned long long cnt[1] = {0};
     const bool fold_topic = FOLD && ps.topic < s.n_topics && s.tp[ps.topic].scored;
@@ -1408,7 +1408,8 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
             const bool wrote = !ps.late || (q < ps.n_pairs && (ps.rfwd[q] & FWD_SEND));
             ca[i] = (local && ps.credit && wrote) ? ps.corr[ra[i]] : 0;
         }
-        if (RESCORE && s.n_topics == 1) {  // (uniform) one topic: the batched fold + re-score
+        if (ONE_TOPIC) {  // the batched fold + re-score (its own instantiation: its registers do not
+                          // cost the general loop occupancy)
             fold_rescore_1(ps, s, pp, q0, stride, k1a, ra, ca, fold_topic, cnt[0]);
             continue;
         }
@@ -1755,7 +1756,8 @@ hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, 
                              hipStream_t st) {
     if (ps.n_pairs == 0) return hipSuccess;
     const dim3 g(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), b(256);
-    if (fold && rescore) hipLaunchKernelGGL((k_prop_count<true, true>), g, b, 0, st, ps, s, pp);
+    if (fold && rescore && s.n_topics == 1) hipLaunchKernelGGL((k_prop_count<true, true, true>), g, b, 0, st, ps, s, pp);
+    else if (fold && rescore) hipLaunchKernelGGL((k_prop_count<true, true>), g, b, 0, st, ps, s, pp);
     else if (fold) hipLaunchKernelGGL((k_prop_count<true, false>), g, b, 0, st, ps, s, pp);
     else hipLaunchKernelGGL((k_prop_count<false, false>), g, b, 0, st, ps, s, pp);
     return hipGetLastError();
