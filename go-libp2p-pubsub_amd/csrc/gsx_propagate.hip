@@ -1083,6 +1083,7 @@ __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_ru
 // issued together, so a thread waits for one round of latencies per batch
 // rather than one per pair.
 constexpr int DU = 4;
+constexpr int FH = 2;  // fold_rescore_1: pairs whose loads are in flight together
 // With the graylist gate (ps.gate), a pair whose receiver drops the sender's
 // RPCs (FWD_GIN on the receiver's pair q) sends the same copies, but they are
 // dropped at u before pushMsg: they count as STAT_GRAY, never as duplicates,
@@ -1299,69 +1300,73 @@ __device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevSta
         }
         if (ps.late && local) backsends += k1;
     }
-    uint8_t fl[DU];
-    double fmd[DU], mmd[DU], mfp[DU], imd[DU], app[DU], bp[DU];
-    int64_t graft[DU];
-    uint2 ipg[DU];
+    for (int h0 = 0; h0 < DU; h0 += FH) {  // (halves: fewer live registers per batch)
+    uint8_t fl[FH];
+    double fmd[FH], mmd[FH], mfp[FH], imd[FH], app[FH], bp[FH];
+    int64_t graft[FH];
+    uint2 ipg[FH];
 #pragma unroll
-    for (int i = 0; i < DU; ++i) {  // every load of the batch
+    for (int j = 0; j < FH; ++j) {  // every load of the half
+        const int i = h0 + j;
         if (!doit[i]) continue;
         const uint64_t q = q0 + i * stride;
         const size_t b = rec_index(q, t, 1, FMD);
-        fl[i] = s.rflags[flag_index(q, t, 1)];
-        fmd[i] = s.rec[b + FMD * TILE];
-        mmd[i] = s.rec[b + MMD * TILE];
-        mfp[i] = s.rec[b + MFP * TILE];
-        imd[i] = s.rec[b + IMD * TILE];
-        graft[i] = reinterpret_cast<const int64_t*>(s.rec)[rec_index(q, t, 1, GRAFT)];
-        app[i] = s.app[q];
-        bp[i] = s.bp[q];
-        if (pp.w6 != 0.0) ipg[i] = reinterpret_cast<const uint2*>(s.ipg)[q];
+        fl[j] = s.rflags[flag_index(q, t, 1)];
+        fmd[j] = s.rec[b + FMD * TILE];
+        mmd[j] = s.rec[b + MMD * TILE];
+        mfp[j] = s.rec[b + MFP * TILE];
+        imd[j] = s.rec[b + IMD * TILE];
+        graft[j] = reinterpret_cast<const int64_t*>(s.rec)[rec_index(q, t, 1, GRAFT)];
+        app[j] = s.app[q];
+        bp[j] = s.bp[q];
+        if (pp.w6 != 0.0) ipg[j] = reinterpret_cast<const uint2*>(s.ipg)[q];
     }
-    uint32_t ipc[DU][2];
+    uint32_t ipc[FH][2];
     if (pp.w6 != 0.0) {
 #pragma unroll
-        for (int i = 0; i < DU; ++i) {
-            ipc[i][0] = ipc[i][1] = 0;
+        for (int j = 0; j < FH; ++j) {
+            const int i = h0 + j;
+            ipc[j][0] = ipc[j][1] = 0;
             if (!doit[i]) continue;
-            const uint32_t gs[2] = {ipg[i].x, ipg[i].y};
+            const uint32_t gs[2] = {ipg[j].x, ipg[j].y};
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                if (!(gs[k] == IPG_NONE || (gs[k] & IPG_WL))) ipc[i][k] = s.ipcount[gs[k]];
+                if (!(gs[k] == IPG_NONE || (gs[k] & IPG_WL))) ipc[j][k] = s.ipcount[gs[k]];
         }
     }
     const DevTopicParams& tp = s.tp[t];
 #pragma unroll
-    for (int i = 0; i < DU; ++i) {  // fold_pair, eval_pair, fwd_byte
+    for (int j = 0; j < FH; ++j) {  // fold_pair, eval_pair, fwd_byte
+        const int i = h0 + j;
         if (!doit[i]) continue;
         const uint64_t q = q0 + i * stride;
         const size_t b = rec_index(q, t, 1, FMD);
         const uint32_t k1 = fa[i], k2 = da[i], k4 = k4a[i];
         if (k4) {
-            imd[i] = add_ones_capped(imd[i], k4, __builtin_inf());
-            s.rec[b + IMD * TILE] = imd[i];
+            imd[j] = add_ones_capped(imd[j], k4, __builtin_inf());
+            s.rec[b + IMD * TILE] = imd[j];
         }
         if (k1 | k2) {
-            fmd[i] = add_ones_capped(fmd[i], k1, tp.cap2);
-            s.rec[b + FMD * TILE] = fmd[i];
-            if (fl[i] & REC_IN_MESH) {
-                mmd[i] = add_ones_capped(mmd[i], k1 + k2, tp.cap3);
-                s.rec[b + MMD * TILE] = mmd[i];
+            fmd[j] = add_ones_capped(fmd[j], k1, tp.cap2);
+            s.rec[b + FMD * TILE] = fmd[j];
+            if (fl[j] & REC_IN_MESH) {
+                mmd[j] = add_ones_capped(mmd[j], k1 + k2, tp.cap3);
+                s.rec[b + MMD * TILE] = mmd[j];
             }
         }
-        const int64_t mt = (!(fl[i] & REC_IN_MESH) || (fl[i] & REC_FRESH)) ? 0 : s.last_refresh - graft[i];
+        const int64_t mt = (!(fl[j] & REC_IN_MESH) || (fl[j] & REC_FRESH)) ? 0 : s.last_refresh - graft[j];
         double score = 0.0;
-        score += topic_score(tp, fl[i], mt, fmd[i], mmd[i], mfp[i], imd[i]);
+        score += topic_score(tp, fl[j], mt, fmd[j], mmd[j], mfp[j], imd[j]);
         // score_tail with the loaded values
         if (pp.topic_score_cap > 0 && score > pp.topic_score_cap) score = pp.topic_score_cap;
-        score += app[i] * pp.w5;
+        score += app[j] * pp.w5;
         if (pp.w6 != 0.0) {
             double p6 = 0.0;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-                const uint32_t id = k ? ipg[i].y : ipg[i].x;
+                const uint32_t id = k ? ipg[j].y : ipg[j].x;
                 if (id == IPG_NONE || (id & IPG_WL)) continue;
-                const int64_t peers_in_ip = (int64_t)ipc[i][k];
+                const int64_t peers_in_ip = (int64_t)ipc[j][k];
                 if (peers_in_ip > pp.thr6) {
                     const double surpluss = (double)(peers_in_ip - pp.thr6);
                     p6 += surpluss * surpluss;
@@ -1369,8 +1374,8 @@ __device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevSta
             }
             score += p6 * pp.w6;
         }
-        if (bp[i] > pp.thr7) {
-            const double excess = bp[i] - pp.thr7;
+        if (bp[j] > pp.thr7) {
+            const double excess = bp[j] - pp.thr7;
             const double p7 = excess * excess;
             score += p7 * pp.w7;
         }
@@ -1382,6 +1387,7 @@ __device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevSta
             if (k < ps.chg_cap) ps.chg[k] = (uint32_t)q;
             if ((nb ^ ob) & FWD_GIN) atomicAdd(ps.gray_pairs, (nb & FWD_GIN) ? 1ull : ~0ull);  // (+1 / -1)
         }
+    }
     }
 }
 
