@@ -331,7 +331,8 @@ struct gsx_engine {
     // Host copy of the score vector for per-call Score() (engines up to
     // kHostScoreMax pairs, e.g. one router's peers): valid while no kernel has
     // written scores since it was taken (score_writes == h_score_tag).
-    std::vector<double> h_score;
+    double* h_score = nullptr;  // pinned (the copy is one DMA, no staging through pageable memory)
+    size_t h_score_cap = 0;
     uint64_t score_writes = 0, h_score_tag = ~0ull;
     bool dirty_zeroed = true;  // d_smask not cleared yet
     void invalidate_scores() {
@@ -981,6 +982,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->d_stage) (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+    if (e->h_score) (void)hipHostFree(e->h_score);
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
@@ -1665,8 +1667,15 @@ int gsx_score(gsx_engine* e, uint64_t pair, double* out) {
     }
     if (int rc = ensure_scores(e)) return rc;
     if (e->E <= kHostScoreMax) {  // small engine (one router's peers): keep the whole vector on the host
-        e->h_score.resize(e->E);
-        HIPCHK(e, hipMemcpyAsync(e->h_score.data(), e->d_score, sizeof(double) * e->E, hipMemcpyDeviceToHost, e->stream));
+        if (e->h_score_cap < e->E) {
+            if (e->h_score) (void)hipHostFree(e->h_score);
+            e->h_score = nullptr;
+            e->h_score_cap = 0;
+            HIPCHK(e, hipHostMalloc((void**)&e->h_score, sizeof(double) * std::max<size_t>(e->E, 1),
+                                    hipHostMallocDefault));
+            e->h_score_cap = e->E;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->h_score, e->d_score, sizeof(double) * e->E, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         e->h_score_tag = e->score_writes;
         *out = e->h_score[pair];
@@ -3388,6 +3397,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             const size_t need = a_sp + b_sp;
             if (e->h_gxstage_bytes < need) {
                 if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+    if (e->h_score) (void)hipHostFree(e->h_score);
                 e->h_gxstage = nullptr;
                 e->h_gxstage_bytes = 0;
                 HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
