@@ -472,8 +472,7 @@ hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStrea
 hipError_t launch_bo_rebuild(const int64_t* backoff, uint8_t* bo8, uint64_t n_pairs, uint32_t n_topics,
                              hipStream_t st);
 hipError_t launch_hb_scan(const DevState& s, const HbState& h, hipStream_t st);
-// The gossip exchange: broken promises at the heartbeat start (P7), step (D),
-// and folding an exchange's receipts into the message set (all |= x; x &= acc).
+// The gossip exchange: broken promises at the heartbeat start (P7); step (D) below.
 hipError_t launch_gx_promises(const DevState& s, const HbState& h, hipStream_t st);
 // Topic membership (gossipsub.go:943-1083, 1517-1554): psub from sub; the
 // fanout of unjoined publishers (one lane per source); the heartbeat's fanout
@@ -500,13 +499,25 @@ struct GxSetPrep {
     uint32_t n_words, n_msgs;
 };
 hipError_t launch_gx_setprep(const GxSetPrep* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
+// After the exchange, every set in one pass (blockIdx.y = set): seen |= the
+// receipts, the receipt rows keep the accepted messages only (the recovered
+// copies' cache rows) and their k_mc_summary (count, digest per node) is
+// written beside them, so the copies are Put without another pass.
+struct GxSetMerge {
+    uint64_t* all;
+    uint64_t* x;
+    const uint64_t* acc;       // [W] accepted messages
+    const uint64_t* msg_dig;   // [W * 64] id digests, then [W] word digests
+    uint64_t* dig;             // [node] summary digest of the recovered rows
+    uint32_t* cnt;             // [node] their message count
+    uint32_t n_words, n_msgs;
+};
+hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // Promise slots [pair][from] -> [pair][to] (to > from; new slots free).
 hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
                                int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);
 // GetBrokenPromises without the penalty (gsx_promise_broken): counts per pair, frees them.
 hipError_t launch_gx_broken(const HbState& h, uint32_t* counts, hipStream_t st);
-hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
-                           hipStream_t st);
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
                               hipStream_t st);  // topics t_base .. t_base + n_t - 1
 // tw: the topic's gossip row words (sum of its batches' n_words)

@@ -198,6 +198,7 @@ struct gsx_engine {
     size_t gx_cap = 0;
     uint2* d_gx_heads = nullptr;      // [gx_cap] per topic, the first batch of each set (k_gx_node)
     gsx::GxSetPrep* d_gx_sp = nullptr;  // [gx_common_cap] the exchange's sets (k_gx_setprep)
+    gsx::GxSetMerge* d_gx_mg = nullptr;  // [gx_common_cap] the same sets (k_gx_merge_sets)
     void* h_gxstage = nullptr;        // pinned staging of the exchange's batch list (hb_end)
     size_t h_gxstage_bytes = 0;
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
@@ -599,7 +600,7 @@ void free_state(gsx_engine* e) {
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
                        e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
-                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp};
+                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
@@ -623,6 +624,7 @@ void free_state(gsx_engine* e) {
         e->d_gx_rhm = e->d_gx_common = nullptr;
         e->d_gx_heads = nullptr;
         e->d_gx_sp = nullptr;
+        e->d_gx_mg = nullptr;
         e->gx_common_cap = 0;
         void* mbp[] = {e->d_sub, e->d_psub, e->d_fanout, e->d_fan_has, e->d_lastpub, e->d_mscratch, e->d_mlist};
         for (void* x : mbp)
@@ -3367,11 +3369,14 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         if (gx_sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
             if (e->d_gx_common) (void)hipFree(e->d_gx_common);
             if (e->d_gx_sp) (void)hipFree(e->d_gx_sp);
+            if (e->d_gx_mg) (void)hipFree(e->d_gx_mg);
             e->d_gx_common = nullptr;
             e->d_gx_sp = nullptr;
+            e->d_gx_mg = nullptr;
             e->gx_common_cap = std::max<size_t>(std::max<size_t>(gx_sets.size(), 2 * e->gx_common_cap), 32);
             if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
             if (int rc = dalloc(e, &e->d_gx_sp, e->gx_common_cap)) return rc;
+            if (int rc = dalloc(e, &e->d_gx_mg, e->gx_common_cap)) return rc;
             if (!e->d_gx_rhm)
                 if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
         }
@@ -3380,6 +3385,13 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             const gsx_engine::MsgSet* ms = gx_sets[i];
             sprep[i] = gsx::GxSetPrep{ms->d_all, gx_x[i], gx_full_new[i] ? ms->d_full : nullptr,
                                       ms->n_words <= 64 ? e->d_gx_common + 64 * i : nullptr, ms->n_words, ms->n_msgs};
+        }
+        std::vector<gsx::GxSetMerge> smerge(gx_sets.size());
+        for (size_t i = 0; i < gx_sets.size(); ++i) {
+            const gsx_engine::MsgSet* ms = gx_sets[i];
+            const size_t W = ms->n_words;
+            smerge[i] = gsx::GxSetMerge{ms->d_all, gx_x[i], ms->d_acc, ms->d_dg, gx_x[i] + W * N,
+                                        reinterpret_cast<uint32_t*>(gx_x[i] + W * N + N), ms->n_words, ms->n_msgs};
         }
         HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * gx_sets.size(), e->stream));
         for (auto& g : gx) {
@@ -3392,9 +3404,11 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             // async copies, so the host keeps queueing instead of waiting for the
             // kernels before them (the last round's copies drained at its end)
             const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_hoff = 4 * hoff.size(),
-                         b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size();
+                         b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size(),
+                         b_mg = sizeof(gsx::GxSetMerge) * smerge.size();
             const size_t a_sp = (b_gx + b_off + b_hoff + b_heads + 15) & ~(size_t)15;
-            const size_t need = a_sp + b_sp;
+            const size_t a_mg = (a_sp + b_sp + 15) & ~(size_t)15;
+            const size_t need = a_mg + b_mg;
             if (e->h_gxstage_bytes < need) {
                 if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
     if (e->h_score) (void)hipHostFree(e->h_score);
@@ -3417,6 +3431,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                                          e->stream));
             std::memcpy(hs + a_sp, sprep.data(), b_sp);
             HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
+            std::memcpy(hs + a_mg, smerge.data(), b_mg);
+            HIPCHK(e, hipMemcpyAsync(e->d_gx_mg, hs + a_mg, b_mg, hipMemcpyHostToDevice, e->stream));
             // receipt rows zeroed, full bytes, common words: every set in one pass
             HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
         }
@@ -3453,9 +3469,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             }
             fprintf(stderr, "[gx] listed=%zu heavy=%zu pairs=%zu maxdeg=%zu\n", ln.size(), heavy, pairs, maxdeg);
         }
-        for (size_t i = 0; i < gx_sets.size(); ++i)
-            HIPCHK(e, gsx::launch_gx_merge(gx_sets[i]->d_all, gx_x[i], gx_sets[i]->d_acc, N, gx_sets[i]->n_words,
-                                           e->stream));
+        // receipts merged into the sets, the recovered rows' summaries written (every set, one pass)
+        HIPCHK(e, gsx::launch_gx_merge_sets(e->d_gx_mg, (uint32_t)gx_sets.size(), (uint32_t)N, e->stream));
         if (exact) {  // the receipts credited P2 / P3 / P4 of the answered pairs
             HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.gx_mark));
         } else {
@@ -3510,9 +3525,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
         b.ids = ms->ids;
         b.set = ms;
         b.recovered = true;
-        ++ms->refs;
-        HIPCHK(e, gsx::launch_mc_summary(b.d_seen, (uint32_t)N, ms->n_words, ms->n_msgs, ms->d_dg,
-                                         ms->d_dg + (size_t)ms->n_words * 64, b.d_dig, b.d_cnt, e->stream));
+        ++ms->refs;  // (its summary: k_gx_merge_sets)
         e->mc.front().push_back(std::move(b));
     }
     // the exchange cleared the bits and counters it read; a round without

@@ -784,15 +784,34 @@ __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict_
     if (and_words && threadIdx.x < W) atomicAnd(reinterpret_cast<unsigned long long*>(&S.common[threadIdx.x]), sw[threadIdx.x]);
 }
 
-// The exchange's receipts into the message set: seen |= x; the receipt rows
-// keep only the accepted messages (they become the recovered copies' cache rows).
-__global__ __launch_bounds__(256) void k_gx_merge(uint64_t* __restrict__ all, uint64_t* __restrict__ x,
-                                                  const uint64_t* __restrict__ acc, uint64_t n, uint32_t W) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
-        const uint64_t v = x[i];
-        if (!v) continue;
-        all[i] |= v;
-        x[i] = v & acc[i % W];
+// Thread per node v of set blockIdx.y: merge its W receipt words and sum the
+// recovered row's count and digest as k_mc_summary does (a full word adds
+// its word digest, else the id digests of its bits: the same u64 sum).
+__global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restrict__ sets, uint32_t n) {
+    const GxSetMerge S = sets[blockIdx.y];
+    const uint32_t W = S.n_words;
+    const uint64_t* word_dig = S.msg_dig + (size_t)W * 64;
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
+        uint32_t L = 0;
+        uint64_t d = 0;
+        for (uint32_t w = 0; w < W; ++w) {
+            const size_t i = (size_t)v * W + w;
+            uint64_t word = S.x[i];
+            if (!word) continue;
+            S.all[i] |= word;
+            word &= S.acc[w];
+            S.x[i] = word;
+            L += (uint32_t)__popcll(word);
+            const uint32_t left = S.n_msgs > w * 64 ? S.n_msgs - w * 64 : 0;
+            const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
+            if (word && word == full) {
+                d += word_dig[w];
+                continue;
+            }
+            for (; word; word &= word - 1) d += S.msg_dig[w * 64 + (uint32_t)__builtin_ctzll(word)];
+        }
+        S.dig[v] = d;
+        S.cnt[v] = L;
     }
 }
 
@@ -819,6 +838,12 @@ hipError_t launch_gx_setprep(const GxSetPrep* sets, uint32_t n_sets, uint32_t n_
     return hipGetLastError();
 }
 
+hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st) {
+    if (n_sets == 0 || n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_merge_sets, dim3(gx_blocks(n_nodes, 256, 512), n_sets), dim3(256), 0, st, sets, n_nodes);
+    return hipGetLastError();
+}
+
 hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t st) {
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_ask, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
@@ -841,12 +866,5 @@ hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_gx_merge(uint64_t* all, uint64_t* x, const uint64_t* acc, uint64_t n_nodes, uint32_t n_words,
-                           hipStream_t st) {
-    const uint64_t n = n_nodes * n_words;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gx_merge, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, all, x, acc, n, n_words);
-    return hipGetLastError();
-}
 
 }  // namespace gsx
