@@ -303,6 +303,9 @@ enum {
     HB_PX_PEERS,
     HB_PX_IGNORED,
     HB_PX_CONNECT,
+    HB_FWD_DELIVERED,
+    HB_FWD_DUPLICATES,
+    HB_FWD_GRAYLISTED,
     HB_STAT_WORDS
 };  // the order of gsx_heartbeat_out
 
@@ -336,6 +339,8 @@ struct GxBatch {
     const uint64_t* common;  // [n_words]: the set's messages every node had seen as the exchange began (k_gx_setprep)
     uint32_t nxt;         // the next advertised batch of the same set, cache order (GX_END: none)
     uint32_t dense;       // a first-hand batch (most rows hold uncommon messages): k_gx_rhm sets its bit unread
+    const uint64_t* src;  // [n_msgs] the set's origins (node << 32 | index, ascending): the forwarding's back counts
+    uint32_t old_in;      // a copy of the set's messages validated before this round is inside the P3 window
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
@@ -417,6 +422,11 @@ struct HbState {
     // cache order, the set's word offset in the topic's set-word list)
     const uint2* gx_heads;
     const uint32_t* gx_hoff;
+    // the IWANT first receipts per (topic, pair) of this round (the forwarding's
+    // hop-1 back-sends, GxFwd); null when nothing is forwarded
+    uint32_t* gxb_st0;     // [pair] stamp: the pair's counts were written this round
+    uint32_t* gxb_cnt0;    // [topic][pair]: sets whose old copies are inside the P3 window | the others << 16
+    uint32_t gxb_stamp;
     uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
     uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
     uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none)
@@ -513,6 +523,47 @@ struct GxSetMerge {
     uint32_t n_words, n_msgs;
 };
 hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
+// The forwarding of the recovered messages (gsx.h (D): a delivered message is
+// published on at once, gossipsub.go:943-1013), in synchronous hops inside the
+// round.  One run covers up to 64 message sets of up to GXF_SLOTS topics (the
+// node-level frontier and receiver masks are one bit per set); runs are
+// independent (their messages are disjoint).
+constexpr uint32_t GXF_SLOTS = 8;
+constexpr uint32_t GXF_MAX_HOPS = 4096;  // hops of one run (the count arrays)
+struct GxFwdSet {
+    const uint64_t* all;  // [node][W] seen as the exchange began
+    uint64_t* x;          // [node][W] this round's receipts (the forwarded first receipts are added)
+    const uint64_t* acc;  // [W] accepted messages
+    const uint64_t* src;  // [n_msgs] origin node << 32 | message index, ascending
+    uint64_t* fr[2];      // [node][W] frontier rows by hop parity (valid under the node's fmask bit)
+    uint32_t n_words, n_msgs, topic, slot, serial;
+    uint32_t old_in;      // a copy of a message the receiver had before the round is inside the P3 window
+};
+struct GxFwd {
+    const GxFwdSet* sets;
+    uint32_t n_sets, n_slots;
+    uint32_t slot_topic[GXF_SLOTS];
+    uint64_t slot_sets[GXF_SLOTS];  // per topic slot: its sets
+    uint64_t* fmask[2];  // [node] the sets of the node's frontier, by hop parity
+    uint32_t* flist[2];  // frontier nodes, by hop parity
+    uint32_t* fcnt;      // [hop] frontier sizes (hop 0: the recovering nodes)
+    uint64_t* rmask;     // [node] this hop: the sets some frontier neighbour may send (cleared by the pull)
+    uint32_t* rlist;     // this hop's receivers
+    uint32_t* rcnt;      // [hop]
+    uint64_t* srcm;      // [node] the sets holding a message the node published
+    // back-sends (the `from` exclusion): first receipts of pair (x -> v) per topic,
+    // hop 0 (the IWANT answers, [topic][pair] u16 under stamp0) and later hops
+    // ([parity][pair][slot] u16 under stamps seq + hop)
+    const uint32_t* bst0;
+    const uint32_t* bcnt0;  // [topic][pair]: (sets with old_in) | (the others) << 16
+    uint32_t stamp0;
+    uint32_t* bst[2];
+    uint16_t* bcnt[2];
+    uint32_t seq;
+};
+hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
+                           hipStream_t st);
+hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st);
 // Promise slots [pair][from] -> [pair][to] (to > from; new slots free).
 hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
                                int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);

@@ -134,6 +134,8 @@ struct gsx_engine {
         size_t all_words = 0;
         uint32_t* d_val = nullptr;  // [message] GSX_VALIDATION_*
         uint64_t* d_acc = nullptr;  // [word] accepted messages
+        uint64_t* d_src = nullptr;  // [message] origin node << 32 | index, ascending (the forwarding's origin test)
+        int64_t t0 = 0;             // now_ns of the call that made the set (the validation time of old copies)
         uint64_t* d_dg = nullptr;   // [W * 64] id digests + [W] word digests (k_mc_summary)
         uint8_t* d_full = nullptr;  // [node]: every message seen (the exchange skips the set there)
         uint8_t* d_small = nullptr;  // the pooled block d_val / d_acc / d_dg live in
@@ -204,6 +206,19 @@ struct gsx_engine {
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
     size_t gx_common_cap = 0;         // (sets)
+    // the forwarding of recovered messages (gsx.h (D); GxFwd), allocated with its first use
+    uint64_t* d_gxf_mask = nullptr;   // fmask[2][N], rmask[N], srcm[N]
+    uint32_t* d_gxf_list = nullptr;   // flist[2][N], rlist[N]
+    uint32_t* d_gxf_cnt = nullptr;    // fcnt[GXF_MAX_HOPS + 1], rcnt[GXF_MAX_HOPS + 1]
+    uint32_t* d_gxf_bst = nullptr;    // stamps: bst0[E], bst[2][E] (zeroed once; stamps only grow)
+    uint32_t* d_gxf_b0 = nullptr;     // bcnt0[T][E]
+    uint16_t* d_gxf_b = nullptr;      // bcnt[2][E][GXF_SLOTS]
+    gsx::GxFwdSet* d_gxf_sets = nullptr;  // [gxf_sets_cap] descriptors of the round's runs
+    size_t gxf_sets_cap = 0;
+    uint32_t* h_gxf_cnt = nullptr;    // pinned: the hop count of a run's last launched hop
+    void* h_gxf_stage = nullptr;      // pinned: the runs' set descriptors
+    size_t h_gxf_stage_bytes = 0;
+    uint32_t gxf_stamp = 0;           // stamps of the IWANT back counts (one per round) and of the hops
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
@@ -254,6 +269,7 @@ struct gsx_engine {
         gsx_prop_config cfg{};
         std::vector<uint64_t> ids;
         std::vector<uint32_t> vals;  // validation outcomes of this call
+        std::vector<uint64_t> h_src;  // origins of this call's messages (set_sources; alive until the stream sync)
         std::vector<uint64_t> h_acc;  // accepted-message words (host copy, alive until the call's stream sync)
         // pending (deferred) credits: topic they belong to
         bool credit_pending = false;
@@ -498,16 +514,24 @@ uint8_t* small_acquire(gsx_engine* e, size_t bytes, size_t* got) {
 void small_release(gsx_engine* e, uint8_t* p, size_t bytes) {
     if (p) e->small_pool.emplace_back(bytes, p);
 }
-// A message set's d_val (m u32) / d_acc (W u64) / d_dg (W * 64 + W u64) in one pooled block.
+// A message set's d_val (m u32) / d_acc (W u64) / d_dg (W * 64 + W u64) /
+// d_src (m u64) in one pooled block.
 bool set_small_alloc(gsx_engine* e, gsx_engine::MsgSet* set, size_t m, uint32_t W) {
     const size_t val_b = (4 * std::max<size_t>(m, 1) + 7) & ~(size_t)7;
-    const size_t bytes = val_b + 8 * (size_t)W + 8 * ((size_t)W * 64 + W);
+    const size_t bytes = val_b + 8 * (size_t)W + 8 * ((size_t)W * 64 + W) + 8 * std::max<size_t>(m, 1);
     set->d_small = small_acquire(e, bytes, &set->small_bytes);
     if (!set->d_small) return false;
     set->d_val = reinterpret_cast<uint32_t*>(set->d_small);
     set->d_acc = reinterpret_cast<uint64_t*>(set->d_small + val_b);
     set->d_dg = set->d_acc + W;
+    set->d_src = set->d_dg + (size_t)W * 64 + W;
     return true;
+}
+// The origins of a set's messages, (source << 32 | index) ascending.
+void set_sources(std::vector<uint64_t>& out, const gsx_msg* msgs, size_t m) {
+    out.resize(m);
+    for (size_t k = 0; k < m; ++k) out[k] = (uint64_t)msgs[k].source << 32 | (uint64_t)k;
+    std::sort(out.begin(), out.end());
 }
 
 void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
@@ -600,9 +624,17 @@ void free_state(gsx_engine* e) {
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
                        e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
-                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg};
+                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg,
+                       e->d_gxf_mask, e->d_gxf_list, e->d_gxf_cnt, e->d_gxf_bst, e->d_gxf_b0, e->d_gxf_b,
+                       e->d_gxf_sets};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
+        e->d_gxf_mask = nullptr;
+        e->d_gxf_list = e->d_gxf_cnt = e->d_gxf_bst = nullptr;
+        e->d_gxf_b0 = nullptr;
+        e->d_gxf_b = nullptr;
+        e->d_gxf_sets = nullptr;
+        e->gxf_sets_cap = 0;
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
         e->d_prom_e = nullptr;
@@ -984,6 +1016,8 @@ int gsx_destroy(gsx_engine* e) {
     if (e->d_stage) (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+    if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
+    if (e->h_gxf_cnt) (void)hipHostFree(e->h_gxf_cnt);
     if (e->h_score) (void)hipHostFree(e->h_score);
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
@@ -2181,6 +2215,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         P.ids[k] = msgs[k].msg_id;
         P.vals[k] = msgs[k].validation;
     }
+    if (cfg->router == GSX_ROUTER_GOSSIPSUB) set_sources(P.h_src, msgs, m);
     P.active = true;
     HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
     if (m == 0) return GSX_OK;
@@ -2387,8 +2422,11 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         for (size_t k = 0; k < P.vals.size(); ++k)
             if (P.vals[k] == GSX_VALIDATION_ACCEPT) acc[k / 64] |= 1ull << (k % 64);
         if (!set_small_alloc(e, set, P.vals.size(), W)) return fail(e, GSX_ENOMEM, "message set arrays");
+        set->t0 = P.cfg.now_ns;
         HIPCHK(e, hipMemcpyAsync(set->d_val, P.vals.data(), 4 * P.vals.size(), hipMemcpyHostToDevice, e->stream));
         HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
+        if (!P.h_src.empty())
+            HIPCHK(e, hipMemcpyAsync(set->d_src, P.h_src.data(), 8 * P.h_src.size(), hipMemcpyHostToDevice, e->stream));
     }
     if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
@@ -3235,6 +3273,164 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     return GSX_OK;
 }
 
+// The forwarding of recovered messages (gsx.h (D), GxFwd): state allocated on
+// first use; the hop stamps only grow (re-zeroed before they could wrap).
+int gxf_alloc(gsx_engine* e) {
+    if (e->d_gxf_bst) {
+        if (e->gxf_stamp < 0xF0000000u) return GSX_OK;
+        HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * std::max<size_t>(e->E, 1), e->stream));
+        e->gxf_stamp = 0;
+        return GSX_OK;
+    }
+    const size_t N = std::max<size_t>(e->n_nodes, 1), E = std::max<size_t>(e->E, 1);
+    int rc = 0;
+    if ((rc = dalloc(e, &e->d_gxf_mask, 4 * N)) || (rc = dalloc(e, &e->d_gxf_list, 3 * N)) ||
+        (rc = dalloc(e, &e->d_gxf_cnt, 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) || (rc = dalloc(e, &e->d_gxf_bst, 3 * E)) ||
+        (rc = dalloc(e, &e->d_gxf_b0, (size_t)std::max<uint32_t>(e->T, 1) * E)) ||
+        (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)))
+        return rc;
+    if (!e->h_gxf_cnt) HIPCHK(e, hipHostMalloc((void**)&e->h_gxf_cnt, 64, hipHostMallocDefault));
+    HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * E, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_gxf_mask + 2 * N, 0, 8 * N, e->stream));  // rmask: kept clear by the pulls
+    e->gxf_stamp = 0;
+    return GSX_OK;
+}
+
+// Runs the forwarding over the exchange's sets (their receipt rows x as the
+// exchange left them: first receipts, the hop-0 frontier once masked by the
+// accepted words).  A run takes up to 64 sets of up to GXF_SLOTS topics, and
+// all sets of each of its topics (the IWANT back counts are per topic); the
+// hops of a run are launched in chunks with one host check of the last hop's
+// frontier size per chunk.  `scratch` gets the frontier-row buffers (released
+// by the caller after its stream sync).
+int gx_forward(gsx_engine* e, const gsx::HbState& h, const gsx::DevState& ds,
+               const std::vector<gsx_engine::MsgSet*>& sets, const std::vector<uint64_t*>& xs, int64_t now,
+               std::vector<std::pair<uint64_t*, size_t>>& scratch) {
+    const size_t N = e->n_nodes;
+    if (sets.empty() || N == 0) return GSX_OK;
+    std::vector<uint32_t> topics;
+    std::vector<std::vector<size_t>> by_topic;
+    for (size_t i = 0; i < sets.size(); ++i) {
+        size_t ti = 0;
+        while (ti < topics.size() && topics[ti] != sets[i]->topic) ++ti;
+        if (ti == topics.size()) {
+            topics.push_back(sets[i]->topic);
+            by_topic.emplace_back();
+        }
+        by_topic[ti].push_back(i);
+    }
+    for (size_t ti = 0; ti < topics.size(); ++ti) {
+        size_t msgs = 0;
+        for (size_t i : by_topic[ti]) msgs += sets[i]->n_msgs;
+        if (by_topic[ti].size() > 64 || msgs > 65535)
+            return fail(e, GSX_ERANGE, "gossip exchange: topic " + std::to_string(topics[ti]) +
+                                           " advertises more than 64 message sets or 65,535 messages in one round");
+    }
+    // the runs: topics in first-seen order, greedily
+    std::vector<std::vector<size_t>> runs;  // topic indices per run
+    {
+        size_t n_sets = 0;
+        for (size_t ti = 0; ti < topics.size(); ++ti) {
+            if (runs.empty() || runs.back().size() == gsx::GXF_SLOTS || n_sets + by_topic[ti].size() > 64) {
+                runs.emplace_back();
+                n_sets = 0;
+            }
+            runs.back().push_back(ti);
+            n_sets += by_topic[ti].size();
+        }
+    }
+    if (sets.size() > e->gxf_sets_cap) {
+        if (e->d_gxf_sets) (void)hipFree(e->d_gxf_sets);
+        e->d_gxf_sets = nullptr;
+        e->gxf_sets_cap = std::max<size_t>(std::max<size_t>(sets.size(), 2 * e->gxf_sets_cap), 64);
+        if (int rc = dalloc(e, &e->d_gxf_sets, e->gxf_sets_cap)) return rc;
+    }
+    const size_t stage_bytes = sizeof(gsx::GxFwdSet) * sets.size();
+    if (e->h_gxf_stage_bytes < stage_bytes) {
+        if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
+        e->h_gxf_stage = nullptr;
+        e->h_gxf_stage_bytes = 0;
+        HIPCHK(e, hipHostMalloc(&e->h_gxf_stage, 2 * stage_bytes, hipHostMallocDefault));
+        e->h_gxf_stage_bytes = 2 * stage_bytes;
+    }
+    auto* stage = static_cast<gsx::GxFwdSet*>(e->h_gxf_stage);
+    size_t base = 0;
+    for (const auto& run : runs) {
+        gsx::GxFwd f{};
+        f.sets = e->d_gxf_sets + base;
+        f.n_slots = (uint32_t)run.size();
+        uint32_t n_src = 0;
+        for (size_t ts = 0; ts < run.size(); ++ts) {
+            const uint32_t t = topics[run[ts]];
+            f.slot_topic[ts] = t;
+            for (size_t i : by_topic[run[ts]]) {
+                const gsx_engine::MsgSet* ms = sets[i];
+                const size_t words = (size_t)ms->n_words * N;
+                gsx::GxFwdSet S{};
+                S.all = ms->d_all;
+                S.x = xs[i];
+                S.acc = ms->d_acc;
+                S.src = ms->d_src;
+                for (int k = 0; k < 2; ++k) {
+                    S.fr[k] = seen_acquire(e, words);
+                    if (!S.fr[k]) return fail(e, GSX_ENOMEM, "forwarding frontier rows");
+                    scratch.emplace_back(S.fr[k], words);
+                }
+                S.n_words = ms->n_words;
+                S.n_msgs = ms->n_msgs;
+                S.topic = t;
+                S.slot = (uint32_t)ts;
+                S.serial = ms->serial;
+                // an old copy counts as validated when its set's call ran (gsx.h)
+                S.old_in = now - ms->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
+                f.slot_sets[ts] |= 1ull << f.n_sets;
+                stage[base + f.n_sets] = S;
+                ++f.n_sets;
+                n_src += ms->n_msgs;
+            }
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_gxf_sets + base, stage + base, sizeof(gsx::GxFwdSet) * f.n_sets,
+                                 hipMemcpyHostToDevice, e->stream));
+        f.fmask[0] = e->d_gxf_mask;
+        f.fmask[1] = e->d_gxf_mask + N;
+        f.rmask = e->d_gxf_mask + 2 * N;
+        f.srcm = e->d_gxf_mask + 3 * N;
+        f.flist[0] = e->d_gxf_list;
+        f.flist[1] = e->d_gxf_list + N;
+        f.rlist = e->d_gxf_list + 2 * N;
+        f.fcnt = e->d_gxf_cnt;
+        f.rcnt = e->d_gxf_cnt + gsx::GXF_MAX_HOPS + 1;
+        const size_t E = std::max<size_t>(e->E, 1);
+        f.bst0 = e->d_gxf_bst;
+        f.bcnt0 = e->d_gxf_b0;
+        f.stamp0 = h.gxb_stamp;
+        f.bst[0] = e->d_gxf_bst + E;
+        f.bst[1] = e->d_gxf_bst + 2 * E;
+        f.bcnt[0] = e->d_gxf_b;
+        f.bcnt[1] = e->d_gxf_b + E * gsx::GXF_SLOTS;
+        f.seq = e->gxf_stamp + 1;
+        HIPCHK(e, hipMemsetAsync(e->d_gxf_mask, 0, 8 * 2 * N, e->stream));   // fmask
+        HIPCHK(e, hipMemsetAsync(f.srcm, 0, 8 * N, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_gxf_cnt, 0, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1), e->stream));
+        HIPCHK(e, gsx::launch_gxf_init(ds, h, f, n_src, e->stream));
+        uint32_t hop = 1;
+        for (;;) {
+            const uint32_t chunk = hop == 1 ? 6 : 8;
+            if (hop + chunk > gsx::GXF_MAX_HOPS)
+                return fail(e, GSX_ERANGE, "forwarding of recovered messages: more than " +
+                                               std::to_string(gsx::GXF_MAX_HOPS) + " hops");
+            for (uint32_t k = 0; k < chunk; ++k) HIPCHK(e, gsx::launch_gxf_hop(ds, h, f, hop + k, e->stream));
+            hop += chunk;
+            HIPCHK(e, hipMemcpyAsync(e->h_gxf_cnt, e->d_gxf_cnt + hop - 1, 4, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (*e->h_gxf_cnt == 0) break;
+        }
+        e->gxf_stamp = f.seq + hop + 1;
+        base += f.n_sets;
+    }
+    return GSX_OK;
+}
+
 int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     e->state_changed();
     gsx::HbState h = e->hb;
@@ -3253,6 +3449,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     // windows of hb_begin's list), answered across the Shift below
     std::vector<gsx_engine::MsgSet*> gx_sets;
     std::vector<uint64_t*> gx_x;
+    std::vector<std::pair<uint64_t*, size_t>> gxf_scratch;  // the forwarding's frontier rows (released after the sync)
     const bool gx_run = e->gp.gossip_exchange && h.ihave_bits && e->have_gossip;
     dbg_host("hb (B)(C)");
     if (gx_run) {
@@ -3297,6 +3494,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
                                               (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
                     gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
                     gx.back().dense = b.recovered ? 0u : 1u;
+                    gx.back().src = b.set->d_src;
+                    gx.back().old_in = h.now - b.set->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
                 }
         }
         off[e->T] = (uint32_t)gx.size();
@@ -3411,7 +3610,6 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             const size_t need = a_mg + b_mg;
             if (e->h_gxstage_bytes < need) {
                 if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
-    if (e->h_score) (void)hipHostFree(e->h_score);
                 e->h_gxstage = nullptr;
                 e->h_gxstage_bytes = 0;
                 HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
@@ -3451,6 +3649,10 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
         }
         dbg_host("gx prepared");
+        if (int rc = gxf_alloc(e)) return rc;
+        h.gxb_st0 = e->d_gxf_bst;
+        h.gxb_cnt0 = e->d_gxf_b0;
+        h.gxb_stamp = ++e->gxf_stamp;
         HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
         if (dbg) {  // the listed nodes of k_gx_ask: count, heavy ones, their pairs
             HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -3469,6 +3671,8 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
             }
             fprintf(stderr, "[gx] listed=%zu heavy=%zu pairs=%zu maxdeg=%zu\n", ln.size(), heavy, pairs, maxdeg);
         }
+        // the recovered messages published on (their forwarded first receipts join the receipt rows)
+        if (int rc = gx_forward(e, h, ds, gx_sets, gx_x, h.now, gxf_scratch)) return rc;
         // receipts merged into the sets, the recovered rows' summaries written (every set, one pass)
         HIPCHK(e, gsx::launch_gx_merge_sets(e->d_gx_mg, (uint32_t)gx_sets.size(), (uint32_t)N, e->stream));
         if (exact) {  // the receipts credited P2 / P3 / P4 of the answered pairs
@@ -3489,6 +3693,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     }
     dbg_host("gx queued");
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (auto& fr : gxf_scratch) seen_release(e, fr.first, fr.second);
     dbg_host("hb drained");
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
@@ -4119,9 +4324,13 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
         batch_release(e, b);
         return fail(e, GSX_ENOMEM, "message set arrays");
     }
+    std::vector<uint64_t> srcs;
+    set_sources(srcs, msgs, m);
+    set->t0 = cfg->now_ns;
     HIPCHK(e, hipMemcpyAsync(set->d_val, vals.data(), 4 * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(set->d_src, srcs.data(), 8 * m, hipMemcpyHostToDevice, e->stream));
     b.d_dig = b.d_seen + (size_t)W * N;
     b.d_cnt = reinterpret_cast<uint32_t*>(b.d_seen + (size_t)W * N + N);
     HIPCHK(e, gsx::launch_mc_summary(b.d_seen, (uint32_t)N, W, (uint32_t)m, set->d_dg, set->d_dg + (size_t)W * 64,

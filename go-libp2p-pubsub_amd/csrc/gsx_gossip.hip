@@ -18,6 +18,8 @@
 #include "gsx_device.h"
 #include "gsx_ops.h"
 
+#include <algorithm>
+
 namespace gsx {
 
 constexpr uint32_t VAL_ACCEPT = 0, VAL_REJECT = 1;  // GSX_VALIDATION_ACCEPT / _REJECT (gsx.h)
@@ -208,6 +210,39 @@ __device__ __forceinline__ void gx_credit(const DevState& s, uint64_t q, uint32_
         s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], k1 + k2, tp.cap3);
 }
 
+// The words w of a set whose message node x published (src: node << 32 |
+// index, ascending, n entries).
+__device__ __forceinline__ uint64_t origin_word(const uint64_t* src, uint32_t n, uint32_t x, uint32_t w) {
+    uint32_t lo = 0, hi = n;
+    const uint64_t key = (uint64_t)x << 32;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (src[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    uint64_t m = 0;
+    for (uint32_t i = lo; i < n && (src[i] >> 32) == x; ++i) {
+        const uint32_t k = (uint32_t)src[i];
+        if (k / 64 == w) m |= 1ull << (k % 64);
+    }
+    return m;
+}
+
+// The IWANT first receipts of pair q = (u -> v) per topic this round that u
+// would forward back to v but for the `from` exclusion (those v published are
+// excluded as the origin already): the forwarding's hop-1 back-sends (GxFwd).
+// At v those copies are old (v served them from its cache): counted apart by
+// the old_in of their set (inside the P3 window or not).
+__device__ __forceinline__ void gx_back0(const DevState& s, const HbState& h, uint64_t q, uint32_t t, uint32_t k_in,
+                                         uint32_t k_out) {
+    if (!h.gxb_st0 || !(k_in | k_out)) return;
+    if (h.gxb_st0[q] != h.gxb_stamp) {
+        h.gxb_st0[q] = h.gxb_stamp;
+        for (uint32_t i = 0; i < s.n_topics; ++i) h.gxb_cnt0[(size_t)i * h.n_pairs + q] = 0;
+    }
+    h.gxb_cnt0[(size_t)t * h.n_pairs + q] += k_in | k_out << 16;
+}
+
 // handleIWant at v and the receipt at u, one id at a time (pass 2 for a pair
 // whose asked subset was sampled, kk < n: the same draws select it again),
 // each receipt credited by its own tracer call.
@@ -239,6 +274,8 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
             if (val == VAL_ACCEPT) {
                 ++delivered;
                 ev_first(s, q, t);
+                if (h.gxb_st0 && !((origin_word(b.src, b.n_msgs, v, k / 64) >> (k % 64)) & 1))
+                    gx_back0(s, h, q, t, b.old_in, !b.old_in);
                 *b.got = 1;
             } else {
                 ++rejected;
@@ -636,7 +673,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                     for (uint64_t tm = tb; tm; tm &= tm - 1) {
                         const uint32_t t = (uint32_t)__builtin_ctzll(tm);
                         const uint64_t* sub = gx_subrow(h, tr, t, r);
-                        uint32_t k1 = 0, k2 = 0, k4 = 0;
+                        uint32_t k1 = 0, k2 = 0, k4 = 0, kb = 0, kbo = 0;  // kb / kbo: the back-sends of k1 (GxFwd)
                         // a lane per (message set, word) of the topic: it walks the
                         // set's batches in cache order (the one order its receipt word
                         // sees); different sets touch different receipt rows
@@ -660,11 +697,13 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                 const uint64_t x0 = *xw;
                                 *xw = x0 | m;
                                 served += (uint64_t)__popcll(m);
+                                uint64_t acc1 = 0;
                                 for (uint64_t z = m & ~x0; z; z &= z - 1) {
                                     const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
                                     if (val == VAL_ACCEPT) {
                                         ++delivered;
                                         ++k1;
+                                        acc1 |= z & (~z + 1);
                                         got = true;
                                     } else {
                                         ++rejected;
@@ -677,6 +716,11 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                     if (val == VAL_ACCEPT) ++k2;
                                     else if (val == VAL_REJECT) ++k4;
                                 }
+                                if (acc1 && h.gxb_st0) {
+                                    const uint32_t nb = (uint32_t)__popcll(acc1 & ~origin_word(b.src, b.n_msgs, v, w));
+                                    if (b.old_in) kb += nb;
+                                    else kbo += nb;
+                                }
                             }
                             if (got) *b.got = 1;
                           }
@@ -684,7 +728,12 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                         k1 = gx_wsum(k1);
                         k2 = gx_wsum(k2);
                         k4 = gx_wsum(k4);
-                        if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
+                        kb = gx_wsum(kb);
+                        kbo = gx_wsum(kbo);
+                        if (lane == 0) {
+                            gx_credit(s, q, t, k1, k2, k4);
+                            gx_back0(s, h, q, t, kb, kbo);
+                        }
                     }
                 } else if (lane == 0) {
                     gx_receive_sampled(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
@@ -815,6 +864,214 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
     }
 }
 
+// ---- the forwarding of recovered messages (gsx.h (D), GxFwd) -------------------
+//
+// A delivered message is published on at once (pushMsg -> publishMessage ->
+// GossipSubRouter.Publish: pubsub.go:1046-1128, gossipsub.go:943-1013), so the
+// nodes that recovered messages by IWANT are the hop-0 frontier of a
+// propagation inside the round.  Per hop:
+//  k_gxf_mark: a lane per frontier node v pushes "you may get set s" bits to
+//    the neighbours v forwards set s's topic to (one atomicOr per pair; the
+//    first one lists the receiver);
+//  k_gxf_pull: a lane per listed receiver x walks its pairs (x -> v) in
+//    ascending v and pulls v's frontier rows (senders ascending: the first
+//    deliverer is the lowest sender), with the AcceptFrom gate of x, the
+//    origin exclusion and, for the `from` exclusion, the first receipts v took
+//    from x at the hop before (counted per (pair, topic), subtracted from the
+//    duplicates: a back-sent copy is always one); first receipts are
+//    delivered (P2, P3 in the mesh), added to the round's receipt rows (the
+//    recovered batch: cached) and fulfil x's promises; duplicates count for P3
+//    when x got the message in this round (or, for an old copy, when the set's
+//    old_in holds).  Every per-pair state touched belongs to the receiver x.
+
+// v forwards topic t to the peer of pair r = (v -> w) (the gossipsub targets
+// of Publish with ReceivedFrom != self: fwd_byte without flood publish, and
+// the scores (D) started from).
+__device__ __forceinline__ bool gxf_elig(const DevState& s, const HbState& h, uint64_t r, uint32_t v, uint32_t t) {
+    const uint8_t pf = s.pflags[r];
+    if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) != (PAIR_PRESENT | PAIR_CONNECTED) || !topic_peer(h.psub, r, t))
+        return false;
+    const uint8_t ef = h.eflags[r];
+    if (ef & EDGE_DIRECT) return true;                                                  // :962-968
+    if (!(ef & EDGE_GOSSIPSUB) && s.score[r] >= h.publish_threshold) return true;       // :970-975
+    if (t >= s.n_topics) return false;
+    return joined_node(h.sub, v, t) ? (s.rflags[flag_index(r, t, s.n_topics)] & REC_IN_MESH) != 0  // :977-999
+                                    : ((h.fanout[r] >> t) & 1) != 0;
+}
+
+// The words of set S whose message node x published.
+__device__ __forceinline__ uint64_t gxf_origin(const GxFwdSet& S, uint32_t x, uint32_t w) {
+    return origin_word(S.src, S.n_msgs, x, w);
+}
+
+// Hop 0: every node's accepted receipts of the round per set (its frontier
+// rows), the frontier list; and each set's origins into srcm (a thread per
+// (set, message) in the grid's second half).
+__global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t n_src_total) {
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u) {
+        uint64_t m = 0;
+        for (uint32_t si = 0; si < f.n_sets; ++si) {
+            const GxFwdSet& S = f.sets[si];
+            const uint32_t W = S.n_words;
+            uint64_t any = 0;
+            for (uint32_t w = 0; w < W; ++w) {
+                const uint64_t row = S.x[(size_t)u * W + w] & S.acc[w];
+                S.fr[0][(size_t)u * W + w] = row;
+                any |= row;
+            }
+            if (any) m |= 1ull << si;
+        }
+        if (m) {
+            f.fmask[0][u] = m;
+            f.flist[0][atomicAdd(&f.fcnt[0], 1u)] = u;
+        }
+    }
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_src_total; i += gridDim.x * 256u) {
+        uint32_t si = 0, base = 0;
+        while (base + f.sets[si].n_msgs <= i) base += f.sets[si++].n_msgs;
+        const uint32_t x = (uint32_t)(f.sets[si].src[i - base] >> 32);
+        if (x < n) atomicOr(reinterpret_cast<unsigned long long*>(&f.srcm[x]), 1ull << si);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f, uint32_t hop) {
+    const uint32_t p = (hop - 1) & 1;
+    const uint32_t stride = gridDim.x * 256u;
+    if (hop >= 2) {  // the frontier two hops back (this hop's parity): its masks cleared
+        const uint32_t n2 = f.fcnt[hop - 2];
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n2; i += stride) f.fmask[hop & 1][f.flist[hop & 1][i]] = 0;
+    }
+    const uint32_t nf = f.fcnt[hop - 1];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nf; i += stride) {
+        const uint32_t v = f.flist[p][i];
+        const uint64_t M = f.fmask[p][v];
+        for (int64_t r = h.row_ptr[v]; r < h.row_ptr[v + 1]; ++r) {
+            uint64_t ok = 0;
+            for (uint32_t ts = 0; ts < f.n_slots; ++ts)
+                if ((M & f.slot_sets[ts]) && gxf_elig(s, h, (uint64_t)r, v, f.slot_topic[ts])) ok |= M & f.slot_sets[ts];
+            if (!ok) continue;
+            const uint32_t w = (uint32_t)h.col[r];
+            const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[w]), ok);
+            if (old == 0) f.rlist[atomicAdd(&f.rcnt[hop], 1u)] = w;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f, uint32_t hop) {
+    const uint32_t p = (hop - 1) & 1, pw = hop & 1;
+    const uint32_t seq_prev = f.seq + hop - 1, seq_cur = f.seq + hop;
+    const uint32_t S_ = h.prom_slots;
+    unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
+    const uint32_t nr = f.rcnt[hop];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nr; i += gridDim.x * 256u) {
+        const uint32_t x = f.rlist[i];
+        const uint64_t M = f.rmask[x];
+        f.rmask[x] = 0;
+        const uint64_t srcm = f.srcm[x] & M;
+        uint64_t newsets = 0;
+        const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
+        for (int64_t q = r0; q < r1; ++q) {
+            const uint32_t v = (uint32_t)h.col[q];
+            const uint64_t fv = f.fmask[p][v] & M;
+            if (!fv) continue;
+            const uint32_t r = h.rev[q];
+            if (r == NO_PAIR || (r & HALO)) continue;
+            const bool gray = !(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist;  // AcceptFrom at x
+            for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
+                const uint64_t sm = fv & f.slot_sets[ts];
+                if (!sm) continue;
+                const uint32_t t = f.slot_topic[ts];
+                if (!gxf_elig(s, h, r, v, t)) continue;
+                uint32_t n1 = 0, dt = 0, dw = 0, g = 0;
+                for (uint64_t mm = sm; mm; mm &= mm - 1) {
+                    const uint32_t si = (uint32_t)__builtin_ctzll(mm);
+                    const GxFwdSet& S = f.sets[si];
+                    const uint32_t W = S.n_words;
+                    const uint64_t* F = S.fr[p] + (size_t)v * W;
+                    uint64_t* X = S.x + (size_t)x * W;
+                    const uint64_t* A = S.all + (size_t)x * W;
+                    uint64_t* NF = S.fr[pw] + (size_t)x * W;
+                    const bool isrc = (srcm >> si) & 1;
+                    for (uint32_t w = 0; w < W; ++w) {
+                        uint64_t snd = F[w];
+                        if (isrc && snd) snd &= ~gxf_origin(S, x, w);  // not back to the origin (:1006-1009)
+                        if (!snd) continue;
+                        if (gray) {
+                            g += (uint32_t)__popcll(snd);
+                            continue;
+                        }
+                        const uint64_t xw = X[w];
+                        const uint64_t nw = snd & ~(A[w] | xw);
+                        const uint64_t dup = snd & ~nw;
+                        dt += (uint32_t)__popcll(dup);
+                        dw += (uint32_t)__popcll(S.old_in ? dup : (dup & xw));
+                        if (nw) {
+                            n1 += (uint32_t)__popcll(nw);
+                            X[w] = xw | nw;
+                            if (!((newsets >> si) & 1)) {
+                                newsets |= 1ull << si;
+                                for (uint32_t z = 0; z < W; ++z) NF[z] = 0;
+                            }
+                            NF[w] |= nw;
+                        }
+                    }
+                }
+                // the copies v would send back to x: the first receipts v took from x last hop
+                // (hop 1: the copies v served x from its cache, old at x: inside the
+                // window by their set's old_in; later hops: x got them in this round)
+                uint32_t back = 0, back_w = 0;
+                if (hop == 1) {
+                    if (f.bst0 && f.bst0[r] == f.stamp0) {
+                        const uint32_t b2 = f.bcnt0[(size_t)t * h.n_pairs + r];
+                        back_w = b2 & 0xFFFFu;
+                        back = back_w + (b2 >> 16);
+                    }
+                } else if (f.bst[p][r] == seq_prev) {
+                    back = back_w = f.bcnt[p][(size_t)r * GXF_SLOTS + ts];
+                }
+                if (gray) {
+                    g -= back;
+                } else {
+                    dt -= back;
+                    dw -= back_w;
+                }
+                c_new += n1;
+                c_dup += dt;
+                c_gray += g;
+                if (n1 | dw) {
+                    gx_credit(s, (uint64_t)q, t, n1, dw, 0);
+                    if (h.gx_mark) h.gx_mark[q] = 1;
+                }
+                if (n1) {
+                    if (f.bst[pw][q] != seq_cur) {
+                        f.bst[pw][q] = seq_cur;
+                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][(size_t)q * GXF_SLOTS + z] = 0;
+                    }
+                    f.bcnt[pw][(size_t)q * GXF_SLOTS + ts] = (uint16_t)n1;
+                }
+            }
+        }
+        if (!newsets) continue;
+        f.fmask[pw][x] = newsets;
+        f.flist[pw][atomicAdd(&f.fcnt[hop], 1u)] = x;
+        // fulfillPromise (:119-126): x's promises of messages it now has
+        for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
+            if (h.prom_e[z] == 0) continue;
+            const uint64_t hd = h.prom_h[z];
+            const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
+            for (uint64_t mm = newsets; mm; mm &= mm - 1) {
+                const GxFwdSet& S = f.sets[__builtin_ctzll(mm)];
+                if (S.serial != ser) continue;
+                if (k < S.n_msgs && ((S.x[(size_t)x * S.n_words + k / 64] >> (k % 64)) & 1)) h.prom_e[z] = 0;
+                break;
+            }
+        }
+    }
+    unsigned long long v[3] = {c_new, c_dup, c_gray};
+    const uint32_t slot[3] = {HB_FWD_DELIVERED, HB_FWD_DUPLICATES, HB_FWD_GRAYLISTED};
+    block_count<3>(v, h.stats, slot);
+}
+
 static inline unsigned gx_blocks(uint64_t n, unsigned bs, unsigned cap) {
     const uint64_t b = (n + bs - 1) / bs;
     return (unsigned)(b < cap ? b : cap);
@@ -849,6 +1106,22 @@ hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t s
     hipLaunchKernelGGL(k_gx_ask, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
     // the listed nodes (their count is on the device): a wave each, grid-stride
     hipLaunchKernelGGL(k_gx_node, dim3(8192), dim3(64), 0, st, s, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_gxf_init(const DevState&, const HbState& h, const GxFwd& f, uint32_t n_src_total,
+                           hipStream_t st) {
+    const uint64_t n = std::max<uint64_t>(h.n_nodes, n_src_total);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, f, h.n_nodes, n_src_total);
+    return hipGetLastError();
+}
+
+// One hop (hop >= 1): its grids are sized for the largest frontier / receiver
+// list (the counts are on the device: an empty hop's threads exit at once).
+hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
+    hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
+    hipLaunchKernelGGL(k_gxf_pull, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
     return hipGetLastError();
 }
 

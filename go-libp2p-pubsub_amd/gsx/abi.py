@@ -347,6 +347,9 @@ class HeartbeatOut(C.Structure):
         ("px_peers", C.c_uint64),
         ("px_ignored", C.c_uint64),
         ("px_connect", C.c_uint64),
+        ("fwd_delivered", C.c_uint64),
+        ("fwd_duplicates", C.c_uint64),
+        ("fwd_graylisted", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSX_ABI_VERSION 4
+#define GSX_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define GSX_OK 0
@@ -622,8 +622,21 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      validation rejects it), fulfils the node's promises for it
  *      (gossip_tracer.go:119-153) and is Put into its cache window 0 (after
  *      the Shift: one batch per message set, in the sets' creation order);
- *      a further copy is a duplicate.  Recovered messages are not
- *      forwarded further within the round.  At the start of every heartbeat
+ *      a further copy is a duplicate.  A delivered message is published on
+ *      at once (pushMsg -> Publish, pubsub.go:1046-1128, gossipsub.go:943-1013):
+ *      the recovering node forwards it to its gossipsub targets (direct
+ *      peers, floodsub peers >= PublishThreshold, its mesh) but the peer that
+ *      served it and the origin, and every node receiving it first does the
+ *      same, in synchronous hops within the round (every copy at `now`;
+ *      per receiver senders ascending; the publishThreshold and AcceptFrom
+ *      tests read the scores as (D) started); a forwarded first receipt is
+ *      delivered (P2, P3 in the mesh), fulfils promises and is Put into the
+ *      same recovered batch; a forwarded duplicate counts for P3 (in the
+ *      mesh) iff the receiver got the message in this round, or else iff
+ *      now - the now_ns of the call that made the message set <=
+ *      MeshMessageDeliveriesWindow (the engine keeps one validation time per
+ *      set, not per node: an old copy counts as validated at that time).
+ *      At the start of every heartbeat
  *      the IHAVE counters are cleared (:1566-1576) and promises that expired
  *      before now are broken: AddPenalty(peer, count) (:1578-1583, P7).
  *      A truncated IHAVE list (below) is handled as the subset its target
@@ -679,6 +692,9 @@ typedef struct gsx_heartbeat_out {
                                  below AcceptPXThreshold (:833-838)               */
     uint64_t px_connect;      /* listed peers the receiver is not connected to:
                                  pxConnect's connection candidates (:861-910)     */
+    uint64_t fwd_delivered;   /* first receipts of recovered messages forwarded on (D) */
+    uint64_t fwd_duplicates;  /* further copies of them                             */
+    uint64_t fwd_graylisted;  /* copies of them the receiver's AcceptFrom dropped   */
 } gsx_heartbeat_out;
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);

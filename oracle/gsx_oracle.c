@@ -13,6 +13,20 @@
 #include <string.h>
 
 #define TIME_CACHE_DURATION_NS (120LL * 1000000000LL) /* pubsub.go:30 */
+#include <stdio.h>
+#include <time.h>
+/* ORC_PROF=1: wall time of the heartbeat's phases on stderr (checker tuning only) */
+static void orc_prof(const char* what) {
+    static int on = -1;
+    static double last = 0;
+    if (on < 0) on = getenv("ORC_PROF") != NULL;
+    if (!on) return;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double t = ts.tv_sec + 1e-9 * ts.tv_nsec;
+    if (what) fprintf(stderr, "[orc] %-12s %8.3f s\n", what, t - last);
+    last = t;
+}
 
 /* topicStats, score.go:37-62 */
 typedef struct {
@@ -71,6 +85,8 @@ static int ipcount_init(struct orc_engine* o);
 typedef struct {
     uint32_t serial, m, n, refs;
     uint32_t* val;
+    uint32_t* src; /* [message] the publishing node (the origin, excluded by forwarding) */
+    int64_t t0;    /* now_ns of the call that made the set (the validation time of old copies, gsx.h) */
     uint8_t* seen;
 } orc_msgset;
 typedef struct {
@@ -112,6 +128,7 @@ struct orc_engine {
     uint32_t *peerhave, *iasked;
     orc_promise* prom; /* hash table keyed (pair, handle): promises[mid][p] of one router per observer */
     size_t n_prom, cap_prom;
+    uint32_t* prom_node; /* [node]: promises its router keeps (fulfillPromise skips nodes with none) */
     /* the truncated IHAVE lists of the last heartbeat (gsx.h, emitGossip): per
      * topic, the row of each (topic, pair) sent one (sub_idx[t][pair], UINT32_MAX
      * none; allocated on first use) in a pool of sub_tw[t]-word bitmasks over the
@@ -307,6 +324,7 @@ static void batch_free(orc_mc_batch* b) {
     free(b->has);
     if (b->set && --b->set->refs == 0) {
         free(b->set->val);
+        free(b->set->src);
         free(b->set->seen);
         free(b->set);
     }
@@ -353,6 +371,7 @@ void orc_destroy(orc_engine* o) {
     free(o->lastpub);
     free(o->pxlog);
     free(o->prom);
+    free(o->prom_node);
     for (int t = 0; t < GSX_MAX_TOPICS; t++) {
         free(o->sub_idx[t]);
         free(o->sub_rows[t]);
@@ -427,6 +446,9 @@ int orc_load_overlay(orc_engine* o, uint32_t n_nodes, const int64_t* row_ptr, co
     if (!o->peerhave || !o->iasked) return GSX_ENOMEM;
     o->n_prom = 0;
     if (o->prom) memset(o->prom, 0, sizeof(orc_promise) * o->cap_prom);
+    free(o->prom_node);
+    o->prom_node = (uint32_t*)calloc(n_nodes ? n_nodes : 1, sizeof(uint32_t));
+    if (!o->prom_node) return GSX_ENOMEM;
     for (int t = 0; t < GSX_MAX_TOPICS; t++) { /* per-pair rows: sized by the new overlay on first use */
         free(o->sub_idx[t]);
         o->sub_idx[t] = NULL;
@@ -1354,8 +1376,13 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         mcb->set->n = N;
         mcb->set->refs = 1;
         mcb->set->val = (uint32_t*)malloc(sizeof(uint32_t) * m);
+        mcb->set->src = (uint32_t*)malloc(sizeof(uint32_t) * m);
+        mcb->set->t0 = cfg->now_ns;
         mcb->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
-        for (size_t k = 0; k < m; k++) mcb->set->val[k] = msgs[k].validation;
+        for (size_t k = 0; k < m; k++) {
+            mcb->set->val[k] = msgs[k].validation;
+            mcb->set->src[k] = msgs[k].source;
+        }
     }
     for (size_t k = 0; k < m; k++) {
         const uint32_t src = msgs[k].source;
@@ -1871,17 +1898,26 @@ static void prom_filter(orc_engine* o, bool (*keep)(const orc_promise*, const vo
     for (size_t i = 0; i < oc; i++)
         if (old[i].used && keep(&old[i], arg)) prom_put(o, old[i].q, old[i].handle, old[i].expire);
     free(old);
+    memset(o->prom_node, 0, sizeof(uint32_t) * (o->n_nodes ? o->n_nodes : 1));
+    for (size_t i = 0; i < oc; i++)
+        if (o->prom[i].used) o->prom_node[o->pair_obs[o->prom[i].q]]++;
 }
 
 static void add_promise(orc_engine* o, uint64_t q, uint64_t handle, int64_t expire) { /* AddPromise :59-74 */
-    if (prom_find(o, q, handle) < 0) prom_put(o, q, handle, expire);
+    if (prom_find(o, q, handle) < 0) {
+        prom_put(o, q, handle, expire);
+        o->prom_node[o->pair_obs[q]]++;
+    }
 }
 
 static void fulfill_promises(orc_engine* o, uint32_t u, uint64_t handle) { /* fulfillPromise :119-126 */
-    if (!o->n_prom) return;
+    if (!o->n_prom || !o->prom_node[u]) return;
     for (int64_t q = o->row_ptr[u]; q < o->row_ptr[u + 1]; q++) {
         const int64_t i = prom_find(o, (uint64_t)q, handle);
-        if (i >= 0) prom_erase(o, (size_t)i);
+        if (i >= 0) {
+            prom_erase(o, (size_t)i);
+            o->prom_node[u]--;
+        }
     }
 }
 
@@ -1985,6 +2021,21 @@ typedef struct {
     size_t i0, n; /* selected items[i0 .. i0 + n) */
     bool served;
 } gx_req;
+typedef struct {
+    uint32_t x, k, u, v; /* recovered set, message, receiver, the peer that served it */
+} gx_recv;
+static int u32_cmp(const void* a, const void* b) {
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+static int gx_recv_cmp(const void* a, const void* b) {
+    const gx_recv* p = (const gx_recv*)a;
+    const gx_recv* q = (const gx_recv*)b;
+    if (p->x != q->x) return p->x < q->x ? -1 : 1;
+    if (p->k != q->k) return p->k < q->k ? -1 : 1;
+    if (p->u != q->u) return p->u < q->u ? -1 : 1;
+    return 0;
+}
 
 static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now,
                            uint64_t seed, gsx_heartbeat_out* out, orc_mc_batch** rec_out, size_t* n_rec) {
@@ -2096,6 +2147,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             reqs[n_rq].served = false;
             n_rq++;
         }
+    orc_prof("(D) ihave");
     /* handleIWant at each asked peer v (:681-716): the asker's score, the cache, GetForPeer's count */
     for (size_t i = 0; i < n_rq && !rc; i++) {
         const int64_t r = reverse_pair(o, reqs[i].q);
@@ -2116,6 +2168,8 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
     uint8_t** rh = NULL;
     uint32_t* rt = NULL;
     size_t nr = 0;
+    gx_recv* fr = NULL; /* the accepted first receipts: each one's hop-0 frontier entry */
+    size_t n_fr = 0, cap_fr = 0;
     for (size_t i = 0; i < n_rq && !rc; i++) {
         if (!reqs[i].served) continue;
         const uint64_t q = reqs[i].q;
@@ -2150,12 +2204,182 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
                     nr++;
                 }
                 rh[x][(size_t)u * st->m + k] = 1; /* Put into u's cache */
+                if (n_fr == cap_fr) {
+                    cap_fr = cap_fr ? 2 * cap_fr : 1024;
+                    fr = (gx_recv*)realloc(fr, sizeof(gx_recv) * cap_fr);
+                }
+                fr[n_fr].x = (uint32_t)x; /* u forwards it on, not back to v (below) */
+                fr[n_fr].k = k;
+                fr[n_fr].u = u;
+                fr[n_fr].v = (uint32_t)o->col[q];
+                n_fr++;
             } else {
                 out->gossip_rejected++;
                 if (val == GSX_VALIDATION_REJECT) mark_invalid(o, q, t);
             }
         }
     }
+    /* A delivered message is published on at once (pushMsg -> publishMessage
+     * -> GossipSubRouter.Publish: pubsub.go:1046-1090, 1124-1128,
+     * gossipsub.go:943-1013): each recovering node forwards it to its gossipsub
+     * targets but the peer it came from and the origin, and every node that
+     * receives it first does the same, in synchronous hops inside the round
+     * (every copy at `now`, senders ascending per receiver as in orc_propagate)
+     * with the exchange's score snapshot for the publishThreshold and AcceptFrom
+     * tests.  A receiver delivers (P2, P3 in the mesh), fulfils its promises,
+     * Puts the copy into its cache (the set's recovered batch) and forwards it;
+     * a duplicate is inside the P3 window iff the receiver got the message in
+     * this round, or else (an old copy: the engine keeps no per-node time)
+     * iff now - the set's call time <= MeshMessageDeliveriesWindow. */
+    orc_prof("(D) receive");
+    if (n_fr) qsort(fr, n_fr, sizeof(gx_recv), gx_recv_cmp);
+    if (n_fr) {
+        /* the messages' propagations are independent but for the records they
+         * credit, the promise table and the counters: threads take whole
+         * messages, count the credits per pair (every step of a counter is the
+         * same capped +1, so their order is free), log the fulfilments, and
+         * everything shared is applied after, in message order */
+        size_t n_grp = 0;
+        size_t* grp = (size_t*)malloc(sizeof(size_t) * (n_fr + 1));
+        for (size_t a = 0; a < n_fr; a++)
+            if (a == 0 || fr[a].x != fr[a - 1].x || fr[a].k != fr[a - 1].k) grp[n_grp++] = a;
+        grp[n_grp] = n_fr;
+        /* every pair's reverse, once (u's peerStats for the sender of each copy) */
+        int64_t* rv = (int64_t*)malloc(sizeof(int64_t) * (E ? E : 1));
+#pragma omp parallel for schedule(static)
+        for (uint64_t r = 0; r < E; r++) rv[r] = reverse_pair(o, r);
+        uint32_t* c_first = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t)); /* per pair: first receipts (P2, P3) */
+        uint32_t* c_win = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));   /* duplicates inside the window (P3) */
+        uint64_t** ful = (uint64_t**)calloc(n_grp, sizeof(uint64_t*));    /* per message: nodes delivered */
+        uint32_t* n_ful = (uint32_t*)calloc(n_grp, sizeof(uint32_t));
+        uint64_t s_new = 0, s_dup = 0, s_gray = 0;
+        uint64_t max_deg = 1;
+        for (uint32_t i = 0; i < N; i++)
+            if ((uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]) > max_deg) max_deg = (uint64_t)(o->row_ptr[i + 1] - o->row_ptr[i]);
+        /* one topic at a time: the per-pair counts are then one topic's */
+        for (size_t xt = 0; xt < nr; xt++) {
+          bool first_of_topic = true;
+          for (size_t y = 0; y < xt; y++) first_of_topic &= rt[y] != rt[xt];
+          if (!first_of_topic) continue;
+          const uint32_t topic = rt[xt];
+#pragma omp parallel reduction(+ : s_new, s_dup, s_gray)
+        {
+            int32_t* from = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
+            for (uint32_t i = 0; i < N; i++) from[i] = -1;
+            uint32_t* front = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+            uint32_t* next = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+            uint32_t* touched = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+            uint8_t* infront = (uint8_t*)calloc(N ? N : 1, 1);
+            uint64_t* tg = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
+            uint64_t* scratch = (uint64_t*)malloc(sizeof(uint64_t) * max_deg);
+#pragma omp for schedule(dynamic, 1)
+            for (size_t gi = 0; gi < n_grp; gi++) {
+                const uint32_t x = fr[grp[gi]].x, k = fr[grp[gi]].k;
+                if (rt[x] != topic) continue;
+                orc_msgset* st = rs[x];
+                const uint32_t t = rt[x], m = st->m;
+                uint8_t* has = rh[x];
+                gsx_prop_config cfg;
+                memset(&cfg, 0, sizeof(cfg));
+                cfg.router = GSX_ROUTER_GOSSIPSUB;
+                cfg.topic = t;
+                uint32_t nf = 0, n_t = 0;
+                for (size_t a = grp[gi]; a < grp[gi + 1]; a++) {
+                    front[nf++] = fr[a].u;
+                    from[fr[a].u] = (int32_t)fr[a].v;
+                    touched[n_t++] = fr[a].u;
+                }
+                const uint32_t n_t0 = n_t;
+                while (nf > 0) {
+                    /* senders ascending: a receiver meets its copies lowest sender
+                     * first (the arrival order of orc_propagate), so each copy is
+                     * handled as it is sent; the next frontier is sorted after */
+                    uint32_t nn = 0;
+                    for (uint32_t i = 0; i < nf; i++) {
+                        const uint32_t v = front[i];
+                        const int nt = router_targets(o, &cfg, v, st->src[k], from[v], 0, tg, scratch, score0);
+                        for (int j = 0; j < nt; j++) {
+                            const uint32_t u = (uint32_t)o->col[tg[j]];
+                            const int64_t qr = rv[tg[j]]; /* u's peerStats for v */
+                            if (qr >= 0 && !(o->eflags[qr] & GSX_EDGE_DIRECT) &&
+                                score0[qr] < o->th.graylist_threshold) {
+                                s_gray++; /* AcceptFrom (gossipsub.go:583-594) */
+                                continue;
+                            }
+                            uint8_t* sn = &st->seen[(size_t)u * m + k];
+                            if (!*sn) { /* Deliver (P2, P3 in the mesh), Put, Publish on */
+                                *sn = 1;
+                                from[u] = (int32_t)v;
+                                touched[n_t++] = u;
+                                has[(size_t)u * m + k] = 1;
+                                next[nn++] = u;
+                                infront[u] = 1;
+                                s_new++;
+                                if (qr >= 0) __atomic_fetch_add(&c_first[qr], 1u, __ATOMIC_RELAXED);
+                            } else { /* DuplicateMessage: P3 inside the window (gsx.h) */
+                                s_dup++;
+                                const int64_t validated = has[(size_t)u * m + k] ? now : st->t0;
+                                if (qr >= 0 && now - validated <= o->tp[t < GSX_MAX_TOPICS ? t : 0].mesh_message_deliveries_window_ns)
+                                    __atomic_fetch_add(&c_win[qr], 1u, __ATOMIC_RELAXED);
+                            }
+                        }
+                    }
+                    /* the next frontier, ascending (a scan when it is large) */
+                    if ((uint64_t)nn * 16 > N) {
+                        uint32_t c = 0;
+                        for (uint32_t u = 0; u < N; u++)
+                            if (infront[u]) {
+                                front[c++] = u;
+                                infront[u] = 0;
+                            }
+                        nf = c;
+                    } else {
+                        qsort(next, nn, sizeof(uint32_t), u32_cmp);
+                        for (uint32_t i = 0; i < nn; i++) infront[next[i]] = 0;
+                        memcpy(front, next, sizeof(uint32_t) * nn);
+                        nf = nn;
+                    }
+                }
+                if (n_t > n_t0) { /* the delivered nodes, for fulfillPromise */
+                    ful[gi] = (uint64_t*)malloc(sizeof(uint64_t) * (n_t - n_t0));
+                    for (uint32_t i = n_t0; i < n_t; i++) ful[gi][i - n_t0] = touched[i];
+                    n_ful[gi] = n_t - n_t0;
+                }
+                for (uint32_t i = 0; i < n_t; i++) from[touched[i]] = -1;
+            }
+            free(from);
+            free(front);
+            free(next);
+            free(touched);
+            free(infront);
+            free(tg);
+            free(scratch);
+        }
+          /* the topic's credits, pair by pair: c_first deliveries (markFirstMessageDelivery),
+           * c_win duplicates inside the window (markDuplicateMessageDelivery) */
+          for (uint64_t q = 0; q < E; q++) {
+              for (uint32_t i = 0; i < c_first[q]; i++) mark_first(o, q, topic);
+              for (uint32_t i = 0; i < c_win[q]; i++) mark_duplicate(o, q, topic, true, now, now);
+              c_first[q] = c_win[q] = 0;
+          }
+        }
+        out->fwd_delivered += s_new;
+        out->fwd_duplicates += s_dup;
+        out->fwd_graylisted += s_gray;
+        for (size_t gi = 0; gi < n_grp; gi++) {
+            const orc_msgset* st = rs[fr[grp[gi]].x];
+            const uint64_t handle = ((uint64_t)st->serial << 32) | fr[grp[gi]].k;
+            for (uint32_t i = 0; i < n_ful[gi]; i++) fulfill_promises(o, (uint32_t)ful[gi][i], handle);
+            free(ful[gi]);
+        }
+        free(ful);
+        free(n_ful);
+        free(grp);
+        free(rv);
+        free(c_first);
+        free(c_win);
+    }
+    free(fr);
     /* the recovered copies: one batch per message set, Put after the Shift in
      * ascending set serial (the sets' creation order, gsx.h) */
     for (size_t a = 1; a < nr; a++)
@@ -2360,6 +2584,7 @@ static void hb_answers(orc_engine* o, const gsx_gossipsub_params* gp, const uint
 int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, int64_t now, uint64_t seed,
                   gsx_heartbeat_out* out) {
     memset(out, 0, sizeof(*out));
+    orc_prof(NULL);
     o->gp = *gp;
     const uint64_t E = o->E;
     const uint32_t T = o->T;
@@ -2454,6 +2679,7 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     free(c.mids);
     free(c.mpos);
     free(c.msel);
+    orc_prof("(A)");
     /* (B) receivers, (C) the PRUNE answers; the (A) PRUNEs' PX on the snapshot (B) read */
     hb_receive(o, gp, ctl, resp, cache, now, out);
     if (o->pxno) hb_px(o, gp, 0, ctl, cache, out);
@@ -2465,7 +2691,9 @@ int orc_heartbeat(orc_engine* o, const gsx_gossipsub_params* gp, uint64_t tick, 
     /* (D) the IHAVEs just emitted are answered across the Shift */
     orc_mc_batch* rec = NULL;
     size_t n_rec = 0;
+    orc_prof("(B)(C)");
     int rc = gp->gossip_exchange ? gossip_exchange(o, gp, tick, now, seed, out, &rec, &n_rec) : 0;
+    orc_prof("(D)");
     mcache_shift(o, (uint32_t)gp->history_length); /* :1563 */
     if (n_rec && o->mc_n) {
         orc_mc_window* w0 = &o->mc[0];
@@ -2752,10 +2980,13 @@ int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_
     b->set->n = N;
     b->set->refs = 1;
     b->set->val = (uint32_t*)malloc(sizeof(uint32_t) * m);
+    b->set->src = (uint32_t*)malloc(sizeof(uint32_t) * m);
+    b->set->t0 = cfg->now_ns;
     b->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
     for (size_t k = 0; k < m; k++) {
         b->ids[k] = msgs[k].msg_id;
         b->set->val[k] = msgs[k].validation;
+        b->set->src[k] = msgs[k].source;
     }
     size_t off = 0;
     for (uint32_t k = 0; k < n_parts; k++) {

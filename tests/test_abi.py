@@ -46,7 +46,7 @@ def test_library_is_gfx950_code_object():
 
 def test_load_and_abi_version():
     lib = gsx.load_library()
-    assert lib.gsx_abi_version() == 4
+    assert lib.gsx_abi_version() == 5
 
 
 def test_create_fails_loudly_without_gfx950():

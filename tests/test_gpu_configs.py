@@ -5,8 +5,8 @@
 - cfg2  10k-peer random d=6 overlay, floodsub and gossipsub propagation == oracle;
 - cfg3  1M peers x 8 topics: heartbeats (the OpportunisticGraftTicks round and the
         next one) == oracle on the exported state, mesh maintenance, IHAVE gossip,
-        backoff, scores bit for bit; and five rounds with the gossip exchange on
-        (IWANT, recovery, promises, P7) == oracle;
+        backoff, scores bit for bit; and two rounds with the gossip exchange on
+        (IWANT, recovery, forwarding, promises, P7) == oracle;
 - cfg4  10M-peer overlay on one GPU, floodsub: arrival hops == BFS distances on
         sampled messages, totals consistent (each node reached at most once); and
         the same overlay range-sharded in two (RangeSharded over a local transport)
@@ -130,11 +130,12 @@ def test_cfg3_heartbeat_1m_x_8_matches_oracle(gpu_ok):
 
 @pytest.mark.timeout(1500)
 def test_cfg3_gossip_exchange_1m_x_8_matches_oracle(gpu_ok):
-    """cfg3 with the gossip exchange on (handleIHave / handleIWant, promises,
-    P7): five rounds of a 256-message gossipsub batch that travels 5 hops
-    (most nodes miss it and learn of it by IHAVE) then a heartbeat; every
-    round's counters (IWANTs, served, recovered, broken promises), scores,
-    backoff and state equal the oracle's."""
+    """cfg3 with the gossip exchange on (handleIHave / handleIWant, the
+    forwarding of recovered messages, promises, P7): two rounds of a
+    64-message gossipsub batch that travels 5 hops (most nodes miss it and
+    learn of it by IHAVE, then by the recovering nodes' forwarding) then a
+    heartbeat; every round's counters (IWANTs, served, recovered, forwarded,
+    broken promises), scores, backoff and state equal the oracle's."""
     import gossip_cases as gc
 
     n, T, seed = 1_000_000, 8, synth.SEED
@@ -154,15 +155,15 @@ def test_cfg3_gossip_exchange_1m_x_8_matches_oracle(gpu_ok):
     _cfg3_backend(o, ov, T, st)
     _cfg3_backend(e, ov, T, st)
     del st
-    gp = gc.params(iwant_followup_ns=S)  # promises of round k break at round k + 2 (P7 within the run)
+    gp = gc.params(iwant_followup_ns=S // 2)  # promises of round k break at round k + 1 (P7 within the run)
     for be in (e, o):
         be.set_gossipsub_params(gp)
     tot = {}
-    for k in range(5):
+    for k in range(2):
         now = pc.T0 + (2 + k) * S
         cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % 2, max_hops=5, latency_ms=10, seed=7 + k)
         cfg.now_ns = now
-        ms = pc.messages(n, 256, 100 + k)
+        ms = pc.messages(n, 64, 100 + k)
         outs = [be.propagate(ms, cfg)[0].as_dict() for be in (e, o)]
         assert outs[0] == outs[1], k
         ho = [be.heartbeat(61 + k, now + 500 * abi.MILLISECOND, seed).as_dict() for be in (e, o)]
@@ -176,6 +177,7 @@ def test_cfg3_gossip_exchange_1m_x_8_matches_oracle(gpu_ok):
             _same(gs[f], ws[f], (k, f))
         del gs, ws
     assert tot["iwant_msgs"] > 0 and tot["gossip_delivered"] > 0 and tot["broken_promises"] > 0, tot
+    assert tot["fwd_delivered"] > 0 and tot["fwd_duplicates"] > 0, tot
 
 
 def _bfs(row_ptr, col, src):
