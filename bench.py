@@ -66,31 +66,33 @@ def build_engine(n, T, d, seed, device):
     return ov, e
 
 
+PMC_FILE = "pmc_r04.json"  # written by tools/pmc_r04.sh (tools/pmc_r04.py)
+
+
 def load_pmc():
-    """The PMC byte counts of tools/pmc_r03.sh committed under profiles/
-    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or {}."""
+    """The PMC byte counts committed under profiles/ (FETCH_SIZE x 2 + WRITE_SIZE,
+    gfx950 correction), or {}."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_r03.json")) as f:
+        with open(os.path.join(ROOT, "profiles", PMC_FILE)) as f:
             return json.load(f)
     except (OSError, ValueError):
         return {}
 
 
+def pmc_bytes(section, key, workload):
+    """One PMC figure of a profiled workload, only when the leg ran that same
+    workload (peers, topics, messages, exchange ...); else None: the bytes of
+    another shape say nothing about this leg's traffic."""
+    d = load_pmc().get(section) or {}
+    if d.get("workload") != workload:
+        return None
+    return d.get(key)
+
+
 def load_traffic(cfg_key):
     """Per-launch HBM bytes of the fused kernel from the rocprofv3 PMC pass
     committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)."""
-    pm = load_pmc().get("k_refresh_score<8, true>")
-    if pm and load_pmc().get("config") == cfg_key:
-        return pm["hbm_bytes_per_launch"]
-    path = os.path.join(ROOT, "profiles", "pmc_refresh_score.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("config") == cfg_key:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+    return pmc_bytes("k_refresh_score<8, true>", "hbm_bytes_per_launch", {"config": cfg_key})
 
 
 def single_observer_leg(args, device):
@@ -202,12 +204,27 @@ def prop_config(args, n):
 
 
 def with_traffic(roof, traffic, ms):
-    """Adds the PMC-measured bytes (profiles/pmc_r03.json) beside the algorithmic ones."""
-    if roof is not None and traffic and ms:
+    """Adds the PMC-measured bytes (profiles/PMC_FILE) beside the algorithmic
+    ones; traffic None (no PMC pass of this leg's workload) is reported as null."""
+    if roof is None:
+        return roof
+    if traffic and ms:
         ach = traffic / (ms * 1e-3) / 1e9
         roof.update(traffic=traffic, achieved_traffic=ach, frac_traffic=ach / HBM_PEAK_GBS,
-                    traffic_source="profiles/pmc_r03.json (tools/pmc_r03.sh)")
+                    traffic_source=f"profiles/{PMC_FILE} (tools/pmc_r04.sh)")
+    else:
+        roof.update(traffic=None, traffic_source=f"none: profiles/{PMC_FILE} holds no PMC pass of this workload")
     return roof
+
+
+def prop_workload(n, msgs):
+    """The propagation workload key shared with tools/pmc_r04.py (tools/prop_profile.py)."""
+    return {"peers": int(n), "msgs": int(msgs), "router": "gossipsub", "credit": "now"}
+
+
+def hb_workload(n, T, msgs, exchange):
+    """The heartbeat workload key shared with tools/pmc_r04.py (tools/hb_micro.py)."""
+    return {"peers": int(n), "topics": int(T), "msgs_between_rounds": int(msgs), "exchange": bool(exchange)}
 
 
 def prop_roofline(tot, msgs, kernel_ms):
@@ -291,7 +308,8 @@ def prop_replica(args, rank, world, local, dist, dev, th):
         "hops": tot["hops"],
         "router": "gossipsub (synthesized mesh, ~6 of ~12 peers), P2/P3 credits on",
         "roofline_rank0": with_traffic(prop_roofline(loc, mine, loc["hop_kernel_ms"]),
-                                       load_pmc().get("p1024", {}).get("hop_bytes_per_batch"), loc["hop_kernel_ms"]),
+                                       pmc_bytes("p1024", "hop_bytes_per_batch", prop_workload(n, args.prop_msgs)),
+                                       loc["hop_kernel_ms"]),
     }
 
 
@@ -329,7 +347,7 @@ def prop_variant_legs(args, e, n):
     out = {}
     cfg = prop_config(args, n)
     out["gossipsub_64msg"] = prop_leg(e, n, 64, cfg, 4 * steps, seed, 10_000_000)
-    with_traffic(out["gossipsub_64msg"]["roofline"], load_pmc().get("p64", {}).get("hop_bytes_per_batch"),
+    with_traffic(out["gossipsub_64msg"]["roofline"], pmc_bytes("p64", "hop_bytes_per_batch", prop_workload(n, 64)),
                  out["gossipsub_64msg"]["hop_kernel_ms_per_batch"])
     fcfg = prop_config(args, n)
     fcfg.router = abi.GSX_ROUTER_FLOODSUB
@@ -738,7 +756,9 @@ def main():
             "gossip_delivered_per_round": mean([r["gossip_delivered"] for r in rounds]),
             "steady_ms_per_round": steady_ms,
             "active_ms_per_round": active_ms,
-            "roofline_steady": with_traffic(roof(steady_ms), load_pmc().get("heartbeat_last_round", {}).get("hbm_bytes"),
+            "roofline_steady": with_traffic(roof(steady_ms),
+                                            pmc_bytes("heartbeat_last_round", "hbm_bytes",
+                                                      hb_workload(n, args.topics, args.hb_msgs, args.hb_exchange)),
                                             steady_ms),
             "roofline_active": roof(active_ms),
             "per_round": rounds,

@@ -433,6 +433,7 @@ struct HbState {
     uint64_t* prom_h;      // [pair][prom_slots]: promised message handle
     int64_t* prom_e;       // [pair][prom_slots]: its expiry (0 = free slot)
     uint32_t prom_slots;   // slots per pair (grown by the host while every pair keeps one free)
+    uint8_t* prom_any;     // [pair]: some slot may be in use (set on every add, recomputed by k_gx_promises)
     uint32_t* prom_occ;    // max over pairs of the slots in use after the exchange
     // topic membership (null: every node joined every topic, no fanout)
     const uint64_t* psub;  // [pair]: topics the peer has joined (gs.p.topics)
@@ -560,7 +561,15 @@ struct GxFwd {
     uint32_t* bst[2];
     uint16_t* bcnt[2];
     uint32_t seq;
+    // per pair, this run: fout[r] = the slots whose topic the pair's owner
+    // forwards over r; fin[q] = fout[rev q] | GXF_GRAY (the receiver's AcceptFrom
+    // drops the peer of q)
+    uint8_t* fout;
+    uint16_t* fin;
+    uint64_t all_sets;
+    uint64_t* fbit[2];  // [node / 64] bit per node: in the frontier (the pull's filter: L2-resident)
 };
+constexpr uint16_t GXF_GRAY = 0x100;
 hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
                            hipStream_t st);
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st);
@@ -569,6 +578,8 @@ hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32
                                int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);
 // GetBrokenPromises without the penalty (gsx_promise_broken): counts per pair, frees them.
 hipError_t launch_gx_broken(const HbState& h, uint32_t* counts, hipStream_t st);
+// The promises outstanding (gsx_promise_count): summed into *n (zeroed by the caller).
+hipError_t launch_gx_count(const HbState& h, unsigned long long* n, hipStream_t st);
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
                               hipStream_t st);  // topics t_base .. t_base + n_t - 1
 // tw: the topic's gossip row words (sum of its batches' n_words)

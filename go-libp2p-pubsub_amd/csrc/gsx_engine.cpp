@@ -162,6 +162,8 @@ struct gsx_engine {
     uint32_t* d_gxflag = nullptr;  // [0] a GxSub bound broken, [1] a promise without a slot, [4] slots in use (max)
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
     int64_t* d_prom_e = nullptr;
+    uint8_t* d_prom_any = nullptr;  // [pair] some promise slot may be in use (HbState::prom_any)
+    unsigned long long* d_prom_cnt = nullptr;  // gsx_promise_count's device sum
     uint32_t prom_slots = 0;  // promise slots per pair (grown while every pair keeps one free before an exchange)
     bool gx_clean = false;    // IHAVE bits and counters all zero (the exchange clears what it reads)
     // the truncated IHAVE lists of a round (GxSub per topic): rows for at most
@@ -213,6 +215,8 @@ struct gsx_engine {
     uint32_t* d_gxf_bst = nullptr;    // stamps: bst0[E], bst[2][E] (zeroed once; stamps only grow)
     uint32_t* d_gxf_b0 = nullptr;     // bcnt0[T][E]
     uint16_t* d_gxf_b = nullptr;      // bcnt[2][E][GXF_SLOTS]
+    uint16_t* d_gxf_fin = nullptr;    // [E] per run (GxFwd::fin)
+    uint8_t* d_gxf_fout = nullptr;    // [E] per run (GxFwd::fout)
     gsx::GxFwdSet* d_gxf_sets = nullptr;  // [gxf_sets_cap] descriptors of the round's runs
     size_t gxf_sets_cap = 0;
     uint32_t* h_gxf_cnt = nullptr;    // pinned: the hop count of a run's last launched hop
@@ -623,10 +627,11 @@ void free_state(gsx_engine* e) {
     e->d_tr_acc = e->d_tr_hp = nullptr;
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
-                       e->d_ihave_bits, e->d_prom_e, e->d_gx, e->d_gx_off, e->d_gx_got, e->d_gx_nodes,
+                       e->d_ihave_bits, e->d_prom_e, e->d_prom_any, e->d_prom_cnt, e->d_gx, e->d_gx_off,
+                       e->d_gx_got, e->d_gx_nodes,
                        e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg,
                        e->d_gxf_mask, e->d_gxf_list, e->d_gxf_cnt, e->d_gxf_bst, e->d_gxf_b0, e->d_gxf_b,
-                       e->d_gxf_sets};
+                       e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_gxf_mask = nullptr;
@@ -634,10 +639,14 @@ void free_state(gsx_engine* e) {
         e->d_gxf_b0 = nullptr;
         e->d_gxf_b = nullptr;
         e->d_gxf_sets = nullptr;
+        e->d_gxf_fin = nullptr;
+        e->d_gxf_fout = nullptr;
         e->gxf_sets_cap = 0;
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
         e->d_prom_e = nullptr;
+        e->d_prom_any = nullptr;
+        e->d_prom_cnt = nullptr;
         e->prom_slots = 0;
         for (auto& sp : e->subp) {
             if (sp.pool) (void)hipFree(sp.pool);
@@ -2842,6 +2851,7 @@ int gx_alloc(gsx_engine* e) {
     const uint32_t S = gsx::GX_PROMISE_SLOTS0;
     if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
         (rc = dalloc(e, &e->d_prom_h, E * S)) || (rc = dalloc(e, &e->d_prom_e, E * S)) ||
+        (rc = dalloc(e, &e->d_prom_any, E)) || (rc = dalloc(e, &e->d_prom_cnt, 1)) ||
         (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) || (rc = dalloc(e, &e->d_gxflag, 8)) ||
         (rc = dalloc(e, &e->d_gx_nodes, std::max<size_t>(e->n_nodes, 1))) ||
         (rc = dalloc(e, &e->d_sub_cnt, std::max<size_t>(e->T, 1))) ||
@@ -2850,6 +2860,7 @@ int gx_alloc(gsx_engine* e) {
     e->prom_slots = S;
     e->gx_clean = false;
     HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * S, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_prom_any, 0, E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
@@ -2988,6 +2999,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         hp.now = now;
         hp.prom_h = e->d_prom_h;
         hp.prom_e = e->d_prom_e;
+        hp.prom_any = e->d_prom_any;
         hp.prom_slots = e->prom_slots;
         hp.stats = e->d_hbstats;
         hp.dirty = pen_mask;
@@ -3076,6 +3088,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.gx_req = e->d_gxreq;
         h.prom_h = e->d_prom_h;
         h.prom_e = e->d_prom_e;
+        h.prom_any = e->d_prom_any;
         h.prom_slots = e->prom_slots;
         h.gsubs = e->d_gsubs;
         // the IHAVE topic bits of the last round (one bulk clear: cheaper than the
@@ -3284,10 +3297,11 @@ int gxf_alloc(gsx_engine* e) {
     }
     const size_t N = std::max<size_t>(e->n_nodes, 1), E = std::max<size_t>(e->E, 1);
     int rc = 0;
-    if ((rc = dalloc(e, &e->d_gxf_mask, 4 * N)) || (rc = dalloc(e, &e->d_gxf_list, 3 * N)) ||
+    if ((rc = dalloc(e, &e->d_gxf_mask, 4 * N + 2 * ((N + 63) / 64))) || (rc = dalloc(e, &e->d_gxf_list, 3 * N)) ||
         (rc = dalloc(e, &e->d_gxf_cnt, 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) || (rc = dalloc(e, &e->d_gxf_bst, 3 * E)) ||
         (rc = dalloc(e, &e->d_gxf_b0, (size_t)std::max<uint32_t>(e->T, 1) * E)) ||
-        (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)))
+        (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fin, E)) ||
+        (rc = dalloc(e, &e->d_gxf_fout, E)))
         return rc;
     if (!e->h_gxf_cnt) HIPCHK(e, hipHostMalloc((void**)&e->h_gxf_cnt, 64, hipHostMallocDefault));
     HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * E, e->stream));
@@ -3409,6 +3423,12 @@ int gx_forward(gsx_engine* e, const gsx::HbState& h, const gsx::DevState& ds,
         f.bcnt[0] = e->d_gxf_b;
         f.bcnt[1] = e->d_gxf_b + E * gsx::GXF_SLOTS;
         f.seq = e->gxf_stamp + 1;
+        f.fout = e->d_gxf_fout;
+        f.fin = e->d_gxf_fin;
+        f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
+        f.fbit[0] = e->d_gxf_mask + 4 * N;
+        f.fbit[1] = f.fbit[0] + (N + 63) / 64;
+        HIPCHK(e, hipMemsetAsync(f.fbit[0], 0, 8 * 2 * ((N + 63) / 64), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxf_mask, 0, 8 * 2 * N, e->stream));   // fmask
         HIPCHK(e, hipMemsetAsync(f.srcm, 0, 8 * N, e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxf_cnt, 0, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1), e->stream));
@@ -3783,7 +3803,8 @@ int prom_ready(gsx_engine* e) {
 
 int gsx_promise_add(gsx_engine* e, uint64_t pair, const uint64_t* handles, uint32_t n, int64_t expire_ns,
                     uint64_t seed) {
-    if (!e || !handles || n == 0 || n > 0x7FFFFFFFu) return GSX_EINVAL;
+    // (expiry 0 marks a free slot; a promise's expiry is now + IWantFollowupTime, never the zero time)
+    if (!e || !handles || n == 0 || n > 0x7FFFFFFFu || expire_ns == 0) return GSX_EINVAL;
     if (int rc = prom_ready(e)) return rc;
     if (pair >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
     const uint64_t handle = handles[host_int31n(seed, gsx::TAG_IWANT, pair, 0, (int32_t)n)];  // :53
@@ -3810,6 +3831,8 @@ int gsx_promise_add(gsx_engine* e, uint64_t pair, const uint64_t* handles, uint3
         const uint32_t S2 = e->prom_slots;
         HIPCHK(e, hipMemcpy(e->d_prom_h + pair * S2 + fr, &handle, 8, hipMemcpyHostToDevice));
         HIPCHK(e, hipMemcpy(e->d_prom_e + pair * S2 + fr, &expire_ns, 8, hipMemcpyHostToDevice));
+        const uint8_t one = 1;
+        HIPCHK(e, hipMemcpy(e->d_prom_any + pair, &one, 1, hipMemcpyHostToDevice));
         return GSX_OK;
     }
 }
@@ -3830,6 +3853,7 @@ int gsx_promise_broken(gsx_engine* e, int64_t now_ns, uint32_t* counts, uint64_t
     h.now = now_ns;
     h.prom_h = e->d_prom_h;
     h.prom_e = e->d_prom_e;
+    h.prom_any = e->d_prom_any;
     h.prom_slots = e->prom_slots;
     h.stats = d_tot;
     unsigned long long st[gsx::HB_STAT_WORDS];
@@ -3881,9 +3905,18 @@ int gsx_promise_count(gsx_engine* e, uint64_t* n) {
     if (!e || !n) return GSX_EINVAL;
     *n = 0;
     if (!e->d_prom_e) return GSX_OK;
-    std::vector<int64_t> es((size_t)e->E * e->prom_slots);
-    HIPCHK(e, hipMemcpy(es.data(), e->d_prom_e, 8 * es.size(), hipMemcpyDeviceToHost));
-    for (int64_t x : es) *n += x != 0;
+    // counted on the device, ordered on the engine's stream; one u64 comes back
+    gsx::HbState h{};
+    h.n_pairs = e->E;
+    h.prom_e = e->d_prom_e;
+    h.prom_any = e->d_prom_any;
+    h.prom_slots = e->prom_slots;
+    HIPCHK(e, hipMemsetAsync(e->d_prom_cnt, 0, 8, e->stream));
+    HIPCHK(e, gsx::launch_gx_count(h, e->d_prom_cnt, e->stream));
+    unsigned long long c = 0;
+    HIPCHK(e, hipMemcpyAsync(&c, e->d_prom_cnt, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    *n = c;
     return GSX_OK;
 }
 

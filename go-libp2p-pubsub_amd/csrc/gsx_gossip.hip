@@ -71,14 +71,19 @@ __global__ __launch_bounds__(256) void k_gx_promises(DevState s, HbState h) {
     uint64_t broken = 0;
     const uint32_t S = h.prom_slots;
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        if (!h.prom_any[q]) continue;
         int c = 0;
+        bool left = false;
         for (uint32_t k = 0; k < S; ++k) {
             const int64_t e = h.prom_e[q * S + k];
             if (e != 0 && e < h.now) {
                 h.prom_e[q * S + k] = 0;
                 ++c;
+            } else {
+                left |= e != 0;
             }
         }
+        if (!left) h.prom_any[q] = 0;
         if (c) {
             ev_penalty(s, q, c);
             broken += (uint64_t)c;
@@ -96,19 +101,32 @@ __global__ __launch_bounds__(256) void k_gx_broken(HbState h, uint32_t* __restri
     const uint32_t S = h.prom_slots;
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
         uint32_t c = 0;
+        bool left = false;
         for (uint32_t k = 0; k < S; ++k) {
             const int64_t e = h.prom_e[q * S + k];
             if (e != 0 && e < h.now) {
                 h.prom_e[q * S + k] = 0;
                 ++c;
+            } else {
+                left |= e != 0;
             }
         }
+        if (!left) h.prom_any[q] = 0;
         counts[q] = c;
         broken += c;
     }
     unsigned long long v[1] = {broken};
     const uint32_t slot[1] = {HB_BROKEN_PROMISES};
     block_count<1>(v, h.stats, slot);
+}
+
+__global__ __launch_bounds__(256) void k_gx_count(HbState h, unsigned long long* n) {
+    unsigned long long c[1] = {0};
+    const uint64_t tot = h.n_pairs * h.prom_slots;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * 256u)
+        c[0] += h.prom_e[i] != 0;
+    const uint32_t slot[1] = {0};
+    block_count<1>(c, n, slot);
 }
 
 __global__ __launch_bounds__(256) void k_gx_prom_grow(const uint64_t* __restrict__ h_in, const int64_t* __restrict__ e_in,
@@ -407,6 +425,7 @@ __device__ __forceinline__ void gx_promise(const HbState& h, uint64_t q, uint64_
     if (!have && free_slot >= 0) {
         ph_[free_slot] = handle;
         pe_[free_slot] = h.now + h.gp.followup_ns;
+        h.prom_any[q] = 1;
         ++used;
     } else if (!have) {
         h.gx_err[1] = 1;  // (the host's invariant broken: never)
@@ -751,7 +770,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
         const uint64_t slots = (uint64_t)(r1 - r0) * S;
         for (uint64_t i = lane; i < slots; i += 64) {
             const size_t z = (size_t)r0 * S + i;
-            if (h.prom_e[z] == 0) continue;
+            if (!h.prom_any[z / S] || h.prom_e[z] == 0) continue;
             const uint64_t hd = h.prom_h[z];
             const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
             for (uint32_t gi = 0; gi < n_gx; ++gi) {
@@ -924,6 +943,7 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
         if (m) {
             f.fmask[0][u] = m;
             f.flist[0][atomicAdd(&f.fcnt[0], 1u)] = u;
+            atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[0][u >> 6]), 1ull << (u & 63));
         }
     }
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_src_total; i += gridDim.x * 256u) {
@@ -934,21 +954,53 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
     }
 }
 
+// The run's per-pair forwarding slots (fout, by the owner's row) and their
+// receiver-side view (fin, one gather of the reverse pair's byte).
+__global__ __launch_bounds__(256) void k_gxf_fout(DevState s, HbState h, GxFwd f) {
+    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 256u)
+        for (int64_t r = h.row_ptr[v]; r < h.row_ptr[v + 1]; ++r) {
+            uint32_t b = 0;
+            for (uint32_t ts = 0; ts < f.n_slots; ++ts)
+                if (gxf_elig(s, h, (uint64_t)r, v, f.slot_topic[ts])) b |= 1u << ts;
+            f.fout[r] = (uint8_t)b;
+        }
+}
+__global__ __launch_bounds__(256) void k_gxf_fin(DevState s, HbState h, GxFwd f) {
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = h.rev[q];
+        uint16_t b = (r == NO_PAIR || (r & HALO)) ? 0 : f.fout[r];
+        if (!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) b |= GXF_GRAY;  // AcceptFrom at the owner
+        f.fin[q] = b;
+    }
+}
+
+__device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots) {
+    uint64_t m = 0;
+    for (; slots; slots &= slots - 1) m |= f.slot_sets[__builtin_ctz(slots)];
+    return m;
+}
+// A hop whose frontier holds more than n / GXF_DENSE nodes pulls at every node
+// (no marking): cheaper than its atomics and lists.
+constexpr uint32_t GXF_DENSE = 16;
+
 __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1;
     const uint32_t stride = gridDim.x * 256u;
-    if (hop >= 2) {  // the frontier two hops back (this hop's parity): its masks cleared
+    if (hop >= 2) {  // the frontier two hops back (this hop's parity): its masks and bits cleared
         const uint32_t n2 = f.fcnt[hop - 2];
         for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n2; i += stride) f.fmask[hop & 1][f.flist[hop & 1][i]] = 0;
+        if (n2)
+            for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (h.n_nodes + 63) / 64; i += stride) f.fbit[hop & 1][i] = 0;
     }
     const uint32_t nf = f.fcnt[hop - 1];
+    if ((uint64_t)nf * GXF_DENSE > h.n_nodes) return;  // a dense hop: the pull visits every node
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nf; i += stride) {
         const uint32_t v = f.flist[p][i];
         const uint64_t M = f.fmask[p][v];
         for (int64_t r = h.row_ptr[v]; r < h.row_ptr[v + 1]; ++r) {
-            uint64_t ok = 0;
-            for (uint32_t ts = 0; ts < f.n_slots; ++ts)
-                if ((M & f.slot_sets[ts]) && gxf_elig(s, h, (uint64_t)r, v, f.slot_topic[ts])) ok |= M & f.slot_sets[ts];
+            const uint32_t fo = f.fout[r];
+            if (!fo) continue;
+            const uint64_t ok = M & gxf_slot_sets(f, fo);
             if (!ok) continue;
             const uint32_t w = (uint32_t)h.col[r];
             const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[w]), ok);
@@ -962,26 +1014,47 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
     const uint32_t seq_prev = f.seq + hop - 1, seq_cur = f.seq + hop;
     const uint32_t S_ = h.prom_slots;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
-    const uint32_t nr = f.rcnt[hop];
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nr; i += gridDim.x * 256u) {
-        const uint32_t x = f.rlist[i];
-        const uint64_t M = f.rmask[x];
-        f.rmask[x] = 0;
+        const uint32_t x = dense ? i : f.rlist[i];
+        uint64_t M = f.all_sets;
+        if (!dense) {
+            M = f.rmask[x];
+            f.rmask[x] = 0;
+        }
         const uint64_t srcm = f.srcm[x] & M;
         uint64_t newsets = 0;
         const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
-        for (int64_t q = r0; q < r1; ++q) {
-            const uint32_t v = (uint32_t)h.col[q];
-            const uint64_t fv = f.fmask[p][v] & M;
-            if (!fv) continue;
+        // x's pairs in blocks of GXF_PB: the filter's loads (eligibility, the
+        // frontier bit and mask of the sender) of a block are issued together,
+        // then the senders that send are pulled in ascending order
+        constexpr int GXF_PB = 8;
+        for (int64_t q0 = r0; q0 < r1; q0 += GXF_PB) {
+          uint32_t fis[GXF_PB], vs[GXF_PB];
+          uint64_t fms[GXF_PB];
+#pragma unroll
+          for (int j = 0; j < GXF_PB; ++j) {
+              fis[j] = q0 + j < r1 ? (uint32_t)f.fin[q0 + j] : 0u;
+              vs[j] = (fis[j] & 0xFFu) ? (uint32_t)h.col[q0 + j] : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < GXF_PB; ++j)
+              fms[j] = ((fis[j] & 0xFFu) && ((f.fbit[p][vs[j] >> 6] >> (vs[j] & 63)) & 1)) ? 1ull : 0ull;
+#pragma unroll
+          for (int j = 0; j < GXF_PB; ++j)
+              if (fms[j]) fms[j] = f.fmask[p][vs[j]] & M & gxf_slot_sets(f, fis[j] & 0xFFu);
+          for (int j = 0; j < GXF_PB; ++j) {
+            const uint64_t fv = fms[j];
+            if (!fv) continue;  // v forwards none of the run's topics to x, or sends nothing new this hop
+            const int64_t q = q0 + j;
+            const uint32_t fi = fis[j], v = vs[j];
             const uint32_t r = h.rev[q];
-            if (r == NO_PAIR || (r & HALO)) continue;
-            const bool gray = !(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist;  // AcceptFrom at x
+            const bool gray = (fi & GXF_GRAY) != 0;  // AcceptFrom at x
             for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
                 const uint64_t sm = fv & f.slot_sets[ts];
                 if (!sm) continue;
                 const uint32_t t = f.slot_topic[ts];
-                if (!gxf_elig(s, h, r, v, t)) continue;
                 uint32_t n1 = 0, dt = 0, dw = 0, g = 0;
                 for (uint64_t mm = sm; mm; mm &= mm - 1) {
                     const uint32_t si = (uint32_t)__builtin_ctzll(mm);
@@ -1050,12 +1123,18 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                     f.bcnt[pw][(size_t)q * GXF_SLOTS + ts] = (uint16_t)n1;
                 }
             }
+          }
         }
         if (!newsets) continue;
         f.fmask[pw][x] = newsets;
         f.flist[pw][atomicAdd(&f.fcnt[hop], 1u)] = x;
+        atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
         // fulfillPromise (:119-126): x's promises of messages it now has
         for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
+            if (z % S_ == 0 && !h.prom_any[z / S_]) {  // no promise on this pair
+                z += S_ - 1;
+                continue;
+            }
             if (h.prom_e[z] == 0) continue;
             const uint64_t hd = h.prom_h[z];
             const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
@@ -1109,11 +1188,13 @@ hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_gxf_init(const DevState&, const HbState& h, const GxFwd& f, uint32_t n_src_total,
+hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
                            hipStream_t st) {
     const uint64_t n = std::max<uint64_t>(h.n_nodes, n_src_total);
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, f, h.n_nodes, n_src_total);
+    hipLaunchKernelGGL(k_gxf_fout, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f);
+    hipLaunchKernelGGL(k_gxf_fin, dim3(gx_blocks(h.n_pairs, 256, 8192)), dim3(256), 0, st, s, h, f);
     return hipGetLastError();
 }
 
@@ -1128,6 +1209,12 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
 hipError_t launch_gx_broken(const HbState& h, uint32_t* counts, hipStream_t st) {
     if (h.n_pairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_broken, dim3(gx_blocks(h.n_pairs, 256, COUNTER_GRID)), dim3(256), 0, st, h, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_gx_count(const HbState& h, unsigned long long* n, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gx_count, dim3(gx_blocks(h.n_pairs * h.prom_slots, 256, COUNTER_GRID)), dim3(256), 0, st, h, n);
     return hipGetLastError();
 }
 

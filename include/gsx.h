@@ -706,6 +706,8 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, g
  *  gsx_promise_add      AddPromise(p, msgIDs) (:48-75): tracks handles[Int31n(n)]
  *                       (draws h(seed, 9, pair, k)) expiring at expire_ns,
  *                       unless that (pair, message) promise exists;
+ *                       GSX_EINVAL for expire_ns == 0 (the engine's free-slot
+ *                       mark; AddPromise's expiry is now + IWantFollowupTime);
  *  gsx_promise_broken   GetBrokenPromises (:79-115): the promises expired
  *                       before now are dropped and counted per pair (counts
  *                       [n_pairs], may be NULL; no penalty: the heartbeat

@@ -1946,7 +1946,7 @@ static bool prom_keep_other_pair(const orc_promise* p, const void* arg) { return
  * API, gossip_tracer.go:48-185): AddPromise's pick is Int31n(n) with draws
  * h(seed, 9, pair, k). */
 int orc_promise_add(orc_engine* o, uint64_t q, const uint64_t* handles, uint32_t n, int64_t expire, uint64_t seed) {
-    if (q >= o->E || n == 0 || n > 0x7FFFFFFFu) return GSX_EINVAL;
+    if (q >= o->E || n == 0 || n > 0x7FFFFFFFu || expire == 0) return GSX_EINVAL; /* (gsx.h: expiry 0 is no time) */
     orc_rng g = {seed, 9, q, 0, 0};
     add_promise(o, q, handles[rng_int31n(&g, (int32_t)n)], expire);
     return 0;

@@ -71,6 +71,33 @@ def run(be):
     return rows
 
 
+def heartbeat(be):
+    """The legit node's first heartbeat after the spam (gossipsub_spam_test.go:
+    728-750: wait for GossipSubHeartbeatInitialDelay + 100 ms, then the
+    attacker's score is below zero and the legit node has sent a PRUNE):
+    (A) prunes a negative-score mesh peer (gossipsub.go:1361-1368).  Returns
+    (the round's counters, the attacker's score at the legit node before the
+    round, whether it is still in the legit node's mesh, the topics of the
+    PRUNEs the legit node sent to it)."""
+    before = float(be.scores()[0])
+    be.hb_set_tracing(True)
+    now = T0 + N_MSGS * abi.MILLISECOND + 200 * abi.MILLISECOND  # initial delay (gossipsub.go:44) + 100 ms
+    out = be.heartbeat(1, now, 1).as_dict()
+    st = be.export_state()
+    in_mesh = bool(st["rec_flags"][0] & abi.GSX_REC_IN_MESH)  # pair 0: the legit node's record of the attacker
+    sent_prune = int(be.hb_trace_words()[1][0])
+    return out, before, in_mesh, sent_prune
+
+
+def check_prune(res):
+    """The reference test's last assertion: the legit node PRUNEs the attacker
+    once its score is negative (gossipsub_spam_test.go:743-750)."""
+    out, before, in_mesh, sent_prune = res
+    assert before < 0
+    assert out["prunes"] == 1 and sent_prune == 1  # one PRUNE, topic 0, on the legit node's pair
+    assert not in_mesh
+
+
 def check(rows):
     """The reference test's assertions plus the graylist cut-off."""
     assert [r[0] for r in rows[:4]] == [1, 1, 1, 1]

@@ -47,9 +47,8 @@ def test_invalid_message_spam_stops_at_graylist(gpu_ok):
     # the legit node PRUNEs the attacker once its score is negative
     # (gossipsub_spam_test.go:745-750): its heartbeat drops the negative-score
     # mesh peer (gossipsub.go:1361-1368) and sends PRUNE; the attacker is backed off
-    hb = [be.heartbeat(1, sc.T0 + sc.S, 3).as_dict() for be in (e, o)]
-    assert hb[0] == hb[1] and hb[0]["prunes"] == 1
-    st = e.export_state()
-    assert not (st["rec_flags"][0] & abi.GSX_REC_IN_MESH)  # out of the legit node's mesh
+    hb = [sc.heartbeat(be) for be in (e, o)]
+    sc.check_prune(hb[0])
+    assert hb[0] == hb[1]
     assert e.export_backoff()[0][0] > sc.T0 + sc.S  # PRUNE backoff on the attacker
     assert np.array_equal(e.export_backoff(), o.export_backoff())

@@ -84,6 +84,8 @@ def test_promise_slots_grow_gpu(gpu_ok):
         be.load_overlay(row_ptr, col)
         for k in range(1000):
             be.promise_add(k % 2, [k, k + 1, k + 2], pc.T0 + k, seed=k)
+        with pytest.raises(Exception):  # expiry 0: the free-slot mark, refused by both (gsx.h)
+            be.promise_add(0, [7], 0)
         a = be.promise_count()
         cnt, tot = be.promise_broken(pc.T0 + 500)
         for k in range(0, 1000, 7):

@@ -307,7 +307,7 @@ def test_sharded_heartbeat_peer_exchange_matches_single_engine(gpu_ok, world):
         engines.append((e, a, b))
     runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
                               [(e,) for e, _, _ in engines])
-    tot_px = 0
+    tot_px = tot_connect = cross = 0
     for k in range(3):
         tick, now = 60 + k, pc.T0 + (3 + k) * abi.SECOND
         want = full.heartbeat(tick, now, seed).as_dict()
@@ -324,4 +324,7 @@ def test_sharded_heartbeat_peer_exchange_matches_single_engine(gpu_ok, world):
                 assert np.array_equal(got[f].view(np.uint8), _slice_state(snap, T, E, a, b)[f].view(np.uint8)), (k, f)
             assert np.array_equal(np.asarray(got["backoff"]).reshape(-1), _slice_te(snap["backoff"], T, E, a, b)), k
         tot_px += want["px_prunes"]
-    assert tot_px > 0 and want["px_connect"] + want["px_ignored"] >= 0
+        tot_connect += want["px_connect"]
+        rk = np.searchsorted(rank_lo, recs[:, [0, 2]].astype(np.int64), side="right") - 1
+        cross += int((rk[:, 0] != rk[:, 1]).sum())  # PX lists that travelled to another rank
+    assert tot_px > 0 and tot_connect > 0 and cross > 0, (tot_px, tot_connect, cross)

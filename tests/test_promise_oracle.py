@@ -29,3 +29,17 @@ def test_promise_table_is_unbounded():
     assert o.promise_count() == 499
     o.promise_throttle(0)
     assert o.promise_count() == 0
+
+
+def test_promise_expiry_zero_is_refused():
+    """Expiry 0 is the engine's free-slot mark (gsx.h): both backends refuse it
+    instead of storing a promise one of them would not see."""
+    o = orc.Oracle(1)
+    row_ptr, col = pc.star(2)
+    from gsx import synth
+
+    o.set_peer_params(synth.bench_peer_params())
+    o.load_overlay(row_ptr, col)
+    with pytest.raises(Exception):
+        o.promise_add(0, [1], 0)
+    assert o.promise_count() == 0

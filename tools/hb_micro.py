@@ -54,5 +54,6 @@ for k in range(3 + a.rounds):
           f"ihave={o['ihave_msgs']} iwant={o['iwant_msgs']} delivered={o['gossip_delivered']}", flush=True)
     if a.verbose:
         print("   ", {k: o[k] for k in ("ihave_ids", "ihave_ignored", "iwant_ids", "iwant_served", "gossip_rejected",
-                                      "gossip_duplicates", "broken_promises", "penalties")}, flush=True)
+                                      "gossip_duplicates", "fwd_delivered", "fwd_duplicates", "fwd_graylisted",
+                                      "broken_promises", "penalties")}, flush=True)
 e.close()

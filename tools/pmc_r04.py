@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
-"""Summarise tools/pmc_r03.sh: HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB
+"""Summarise tools/pmc_r04.sh: HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB
 (gfx950, checked by tools/microbench/pmc_calib.hip) per launch of the headline
 kernel, per batch of the propagation hops and per-call passes, per heartbeat
-round (last round of tools/hb_micro.py).  usage: pmc_r03.py <dir>"""
+round (last round of tools/hb_micro.py).  Each section carries the workload
+it measured, in bench.py's keys (bench.pmc_bytes compares them).
+usage: pmc_r04.py <dir> <headline config key, e.g. n=1000000,T=8,d=6,E=11999954>"""
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def dispatches(path):
@@ -30,12 +35,15 @@ def short(n):
 
 
 def main():
+    import bench
+
     d = sys.argv[1]
     out = {"bytes": "2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), gfx950"}
     cal = load(d, "calib")
     out["calibration"] = {short(n): {"read": r / 2**30, "write": w / 2**30} for n, r, w in cal}
     head = [x for x in load(d, "head") if short(x[0]) == "k_refresh_score<8, true>"]
     out["k_refresh_score<8, true>"] = {
+        "workload": {"config": sys.argv[2]},
         "launches": len(head),
         "read_bytes_per_launch": sum(x[1] for x in head) / len(head),
         "write_bytes_per_launch": sum(x[2] for x in head) / len(head),
@@ -49,6 +57,7 @@ def main():
         for n, r, w in call:
             per[short(n)] += (r + w) / batches
         out[name] = {
+            "workload": bench.prop_workload(1_000_000, 1024 if name == "p1024" else 64),
             "batches": batches,
             "hop_launches": len(hop),
             "hop_bytes_per_batch": sum(r + w for _, r, w in hop) / batches,
@@ -70,7 +79,8 @@ def main():
         if cur is not None:
             cur[s] = cur.get(s, 0.0) + r + w
     last = rounds[-1]
-    out["heartbeat_last_round"] = {"hbm_bytes": sum(last.values()),
+    out["heartbeat_last_round"] = {"workload": bench.hb_workload(1_000_000, 8, 256, True),
+                                   "hbm_bytes": sum(last.values()),
                                    "kernels": dict(sorted(last.items(), key=lambda kv: -kv[1]))}
     print(json.dumps(out, indent=1))
 

@@ -5,11 +5,13 @@
 #   head  the headline k_refresh_score<8, true> (bench.py, scoring legs only)
 #   p1024 / p64  the propagation replica workload (tools/prop_profile.py)
 #   hb    cfg3 heartbeat rounds with the gossip exchange (tools/hb_micro.py)
-# then tools/pmc_r03.py writes the per-launch / per-batch / per-round bytes.
+# then tools/pmc_r04.py writes the per-launch / per-batch / per-round bytes, each
+# section tagged with the workload it measured (bench.py attaches a section's
+# bytes only to a leg that ran the same workload).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-O=gpurun_out/${1:-pmc_r03}
+O=gpurun_out/${1:-pmc_r04}
 mkdir -p "$O"
 run() {  # run NAME SECONDS COUNTER CMD...
     local name=$1 secs=$2 c=$3
@@ -29,4 +31,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     run p64 200 $C python3 tools/prop_profile.py --msgs 64 --batches 3
     run hb 200 $C python3 tools/hb_micro.py --exchange --rounds 3
 done
-python3 tools/pmc_r03.py "$O" > "$O/summary.json" && cat "$O/summary.json"
+python3 tools/pmc_r04.py "$O" "n=1000000,T=8,d=6,E=11999954" > "$O/summary.json" && cat "$O/summary.json"
