@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <array>
 #include <cmath>
@@ -352,8 +353,14 @@ struct gsx_engine {
     // Host copy of the score vector for per-call Score() (engines up to
     // kHostScoreMax pairs, e.g. one router's peers): valid while no kernel has
     // written scores since it was taken (score_writes == h_score_tag).
-    double* h_score = nullptr;  // pinned (the copy is one DMA, no staging through pageable memory)
+    double* h_score = nullptr;  // pinned, host-mapped (k_dropin writes it; the full copy is one DMA)
+    double* h_score_dev = nullptr;  // its device address
     size_t h_score_cap = 0;
+    // the drop-in round trip (k_dropin): host-mapped [flag | events | groups | observers]
+    void* h_dropin = nullptr;
+    char* d_dropin = nullptr;  // its device address
+    size_t h_dropin_bytes = 0;
+    uint32_t dropin_tag = 0;
     uint64_t score_writes = 0, h_score_tag = ~0ull;
     bool dirty_zeroed = true;  // d_smask not cleared yet
     void invalidate_scores() {
@@ -1028,6 +1035,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
     if (e->h_gxf_cnt) (void)hipHostFree(e->h_gxf_cnt);
     if (e->h_score) (void)hipHostFree(e->h_score);
+    if (e->h_dropin) (void)hipHostFree(e->h_dropin);
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
@@ -1702,32 +1710,148 @@ int gsx_scores(gsx_engine* e, double* out, size_t n) {
     return GSX_OK;
 }
 
+// The drop-in round trip in one launch (k_dropin): the queued tracer events
+// of a small engine whose host score copy was current are applied and their
+// observers' rows re-scored into both copies; the host polls a mapped flag.
+// Returns 1 when it ran, 0 when the case does not apply (the general path
+// follows), < 0 on error.
+constexpr size_t kDropinMaxEvents = 4096, kDropinMaxObs = 64;
+int dropin_fast(gsx_engine* e) {
+    if (e->pending.empty() || e->E > kHostScoreMax || !e->h_score_dev || e->h_score_cap < e->E ||
+        e->h_score_tag != e->score_writes || !e->scores_valid || e->dirty_only || e->pending.size() > kDropinMaxEvents)
+        return 0;
+    const size_t n = e->pending.size();
+    std::vector<uint32_t> obs(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (e->pending[i].pair >= e->E) {
+            e->pending.clear();
+            return fail(e, GSX_ERANGE, "event pair out of range");
+        }
+        obs[i] = e->pair_obs[e->pending[i].pair];
+    }
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return obs[a] < obs[b]; });
+    std::vector<uint32_t> goff, gobs;
+    for (size_t i = 0; i < n; ++i)
+        if (i == 0 || obs[order[i]] != obs[order[i - 1]]) {
+            goff.push_back((uint32_t)i);
+            gobs.push_back(obs[order[i]]);
+        }
+    if (gobs.size() > kDropinMaxObs) return 0;
+    goff.push_back((uint32_t)n);
+    const size_t ev_off = 64, ev_b = sizeof(gsx::DevEvent) * n;
+    const size_t go_off = ev_off + ev_b, go_b = 4 * goff.size();
+    const size_t ob_off = go_off + go_b, ob_b = 4 * gobs.size();
+    const size_t need = ob_off + ob_b;
+    if (e->h_dropin_bytes < need) {
+        if (e->h_dropin) (void)hipHostFree(e->h_dropin);
+        e->h_dropin = nullptr;
+        e->h_dropin_bytes = 0;
+        const size_t want = std::max<size_t>(need, 64 + (sizeof(gsx::DevEvent) + 8) * kDropinMaxEvents + 4 * kDropinMaxObs);
+        HIPCHK(e, hipHostMalloc(&e->h_dropin, want, hipHostMallocMapped | hipHostMallocCoherent));
+        void* dp = nullptr;
+        HIPCHK(e, hipHostGetDevicePointer(&dp, e->h_dropin, 0));
+        e->d_dropin = static_cast<char*>(dp);
+        e->h_dropin_bytes = want;
+        *static_cast<volatile uint32_t*>(e->h_dropin) = e->dropin_tag;
+    }
+    char* hb = static_cast<char*>(e->h_dropin);
+    auto* hev = reinterpret_cast<gsx::DevEvent*>(hb + ev_off);
+    for (size_t i = 0; i < n; ++i) {
+        const gsx_event& x = e->pending[order[i]];
+        hev[i] = gsx::DevEvent{x.kind, x.topic, x.pair, x.now_ns, x.arg};
+    }
+    std::memcpy(hb + go_off, goff.data(), go_b);
+    std::memcpy(hb + ob_off, gobs.data(), ob_b);
+    std::atomic_thread_fence(std::memory_order_release);
+    const uint32_t tag = ++e->dropin_tag;
+    HIPCHK(e, gsx::launch_dropin(dev_state(e), dev_peer_params(e), reinterpret_cast<const gsx::DevEvent*>(e->d_dropin + ev_off),
+                                 reinterpret_cast<const uint32_t*>(e->d_dropin + go_off), (uint32_t)gobs.size(),
+                                 reinterpret_cast<const uint32_t*>(e->d_dropin + ob_off), (uint32_t)gobs.size(),
+                                 e->d_row_ptr, e->h_score_dev, reinterpret_cast<uint32_t*>(e->d_dropin), tag, e->stream));
+    e->pending.clear();
+    const volatile uint32_t* flag = static_cast<const volatile uint32_t*>(e->h_dropin);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; *flag != tag; ++spin) {
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));  // (a busy device: wait for the stream instead)
+            if (*flag != tag) return fail(e, GSX_EDEVICE, "drop-in round trip: the kernel did not signal");
+            break;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    e->state_changed();
+    ++e->score_writes;
+    e->scores_exact();
+    e->h_score_tag = e->score_writes;
+    return 1;
+}
+
+// The host copy of every score (engines up to kHostScoreMax pairs), current.
+int host_scores(gsx_engine* e) {
+    if (e->pending.empty() && e->scores_valid && e->h_score_tag == e->score_writes) return GSX_OK;
+    if (int r = dropin_fast(e)) return r < 0 ? r : GSX_OK;
+    if (int rc = ensure_scores(e)) return rc;
+    if (e->h_score_cap < e->E) {
+        if (e->h_score) (void)hipHostFree(e->h_score);
+        e->h_score = e->h_score_dev = nullptr;
+        e->h_score_cap = 0;
+        HIPCHK(e, hipHostMalloc((void**)&e->h_score, sizeof(double) * std::max<size_t>(e->E, 1),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+        void* dp = nullptr;
+        HIPCHK(e, hipHostGetDevicePointer(&dp, e->h_score, 0));
+        e->h_score_dev = static_cast<double*>(dp);
+        e->h_score_cap = e->E;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->h_score, e->d_score, sizeof(double) * e->E, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->h_score_tag = e->score_writes;
+    return GSX_OK;
+}
+
 // Score(p), score.go:247-256
 int gsx_score(gsx_engine* e, uint64_t pair, double* out) {
     if (!e || !out) return GSX_EINVAL;
     if (int rc = check_pair(e, pair)) return rc;
-    if (e->pending.empty() && e->scores_valid && e->h_score_tag == e->score_writes) {
-        *out = e->h_score[pair];  // nothing changed since the copy: no device round trip
-        return GSX_OK;
-    }
-    if (int rc = ensure_scores(e)) return rc;
     if (e->E <= kHostScoreMax) {  // small engine (one router's peers): keep the whole vector on the host
-        if (e->h_score_cap < e->E) {
-            if (e->h_score) (void)hipHostFree(e->h_score);
-            e->h_score = nullptr;
-            e->h_score_cap = 0;
-            HIPCHK(e, hipHostMalloc((void**)&e->h_score, sizeof(double) * std::max<size_t>(e->E, 1),
-                                    hipHostMallocDefault));
-            e->h_score_cap = e->E;
-        }
-        HIPCHK(e, hipMemcpyAsync(e->h_score, e->d_score, sizeof(double) * e->E, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        e->h_score_tag = e->score_writes;
+        if (int rc = host_scores(e)) return rc;
         *out = e->h_score[pair];
         return GSX_OK;
     }
+    if (int rc = ensure_scores(e)) return rc;
     HIPCHK(e, hipMemcpyAsync(out, e->d_score + pair, sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+// Score(p) of many pairs: one flush, one re-score, one copy (gsx.h)
+int gsx_score_many(gsx_engine* e, const uint64_t* pairs, size_t n, double* out) {
+    if (!e || (n && (!pairs || !out))) return GSX_EINVAL;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    for (size_t i = 0; i < n; ++i)
+        if (pairs[i] >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
+    if (e->E <= kHostScoreMax) {
+        if (int rc = host_scores(e)) return rc;
+        for (size_t i = 0; i < n; ++i) out[i] = e->h_score[pairs[i]];
+        return GSX_OK;
+    }
+    if (int rc = ensure_scores(e)) return rc;
+    if (n == 0) return GSX_OK;
+    uint64_t* dp = nullptr;
+    double* dout = nullptr;
+    if (int rc = dalloc(e, &dp, n)) return rc;
+    if (int rc = dalloc(e, &dout, n)) {
+        (void)hipFree(dp);
+        return rc;
+    }
+    hipError_t st = hipMemcpyAsync(dp, pairs, 8 * n, hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess) st = gsx::launch_gather_scores(e->d_score, dp, n, dout, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(out, dout, 8 * n, hipMemcpyDeviceToHost, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    (void)hipFree(dp);
+    (void)hipFree(dout);
+    if (st != hipSuccess) return fail(e, GSX_EDEVICE, std::string("gsx_score_many: ") + hipGetErrorString(st));
     return GSX_OK;
 }
 

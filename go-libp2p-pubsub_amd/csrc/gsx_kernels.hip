@@ -140,25 +140,62 @@ __global__ __launch_bounds__(256) void k_purge(DevState s, int64_t now) {
 // Events are grouped by observer (all state an event touches belongs to its
 // observer, so groups are independent); within a group they run in the order
 // the caller issued them.
+__device__ __forceinline__ void apply_event(const DevState& s, const DevPeerParams& pp, const DevEvent& e) {
+    switch (e.kind) {
+    case 1: ev_add_peer(s, e.pair); break;
+    case 2: ev_remove_peer(s, pp, e.pair, e.now_ns); break;
+    case 3: ev_graft(s, e.pair, e.topic, e.now_ns); break;
+    case 4: ev_prune(s, e.pair, e.topic); break;
+    case 5: ev_first(s, e.pair, e.topic); break;
+    case 6: ev_mesh(s, e.pair, e.topic); break;
+    case 7: ev_invalid(s, e.pair, e.topic); break;
+    case 8: ev_penalty(s, e.pair, e.arg); break;
+    case 9: s.app[e.pair] = __longlong_as_double((long long)e.arg); break;  // AppSpecificScore(p), :320
+    default: break;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_apply_events(DevState s, DevPeerParams pp, const DevEvent* __restrict__ ev,
                                                      const uint32_t* __restrict__ group_off, uint32_t n_groups) {
     const uint32_t g = blockIdx.x * 64u + threadIdx.x;
     if (g >= n_groups) return;
-    for (uint32_t i = group_off[g]; i < group_off[g + 1]; ++i) {
-        const DevEvent e = ev[i];
-        switch (e.kind) {
-        case 1: ev_add_peer(s, e.pair); break;
-        case 2: ev_remove_peer(s, pp, e.pair, e.now_ns); break;
-        case 3: ev_graft(s, e.pair, e.topic, e.now_ns); break;
-        case 4: ev_prune(s, e.pair, e.topic); break;
-        case 5: ev_first(s, e.pair, e.topic); break;
-        case 6: ev_mesh(s, e.pair, e.topic); break;
-        case 7: ev_invalid(s, e.pair, e.topic); break;
-        case 8: ev_penalty(s, e.pair, e.arg); break;
-        case 9: s.app[e.pair] = __longlong_as_double((long long)e.arg); break;  // AppSpecificScore(p), :320
-        default: break;
+    for (uint32_t i = group_off[g]; i < group_off[g + 1]; ++i) apply_event(s, pp, ev[i]);
+}
+
+// The drop-in scorer's round trip in one launch (gsx_score / gsx_score_many
+// on an engine small enough to keep a host copy of its scores, when that copy
+// was current before the queued tracer events): one workgroup applies the
+// events (read from host-mapped memory, grouped by observer), then score()s
+// the rows of those observers (eval_pair: the same operations as the score
+// pass) into the device vector and the host copy (host-mapped), then stores
+// `tag` to a host-mapped flag at system scope; the host polls the flag instead
+// of synchronising the stream.
+__global__ __launch_bounds__(1024) void k_dropin(DevState s, DevPeerParams pp, const DevEvent* ev,
+                                                 const uint32_t* goff, uint32_t n_groups, const uint32_t* obs,
+                                                 uint32_t n_obs, const int64_t* __restrict__ row_ptr, double* hscore,
+                                                 uint32_t* flag, uint32_t tag) {
+    for (uint32_t g = threadIdx.x; g < n_groups; g += blockDim.x)
+        for (uint32_t i = goff[g]; i < goff[g + 1]; ++i) apply_event(s, pp, ev[i]);
+    __threadfence();
+    __syncthreads();
+    for (uint32_t k = 0; k < n_obs; ++k) {
+        const int64_t a = row_ptr[obs[k]], b = row_ptr[obs[k] + 1];
+        for (int64_t p = a + threadIdx.x; p < b; p += blockDim.x) {
+            const double v = eval_pair(s, pp, (uint64_t)p);
+            s.score[p] = v;
+            hscore[p] = v;
         }
     }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// out[i] = score[pairs[i]] (gsx_score_many on a large engine)
+__global__ __launch_bounds__(256) void k_gather_scores(const double* __restrict__ score, const uint64_t* __restrict__ pairs,
+                                                       uint64_t n, double* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+        out[i] = score[pairs[i]];
 }
 
 // SetTopicScoreParams recap (score.go:217-231)
@@ -358,6 +395,21 @@ hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const
     if (n_groups == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_events, dim3(blocks_for(n_groups, 64)), dim3(64), 0, st, s, pp, ev, group_off,
                        n_groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_dropin(const DevState& s, const DevPeerParams& pp, const DevEvent* ev, const uint32_t* goff,
+                         uint32_t n_groups, const uint32_t* obs, uint32_t n_obs, const int64_t* row_ptr,
+                         double* hscore, uint32_t* flag, uint32_t tag, hipStream_t st) {
+    hipLaunchKernelGGL(k_dropin, dim3(1), dim3(1024), 0, st, s, pp, ev, goff, n_groups, obs, n_obs, row_ptr, hscore,
+                       flag, tag);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_scores(const double* score, const uint64_t* pairs, uint64_t n, double* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t b = (n + 255) / 256;
+    hipLaunchKernelGGL(k_gather_scores, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, st, score, pairs, n, out);
     return hipGetLastError();
 }
 

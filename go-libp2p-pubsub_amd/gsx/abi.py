@@ -391,6 +391,7 @@ SIGNATURES = {
     "gsx_refresh": (C.c_int, [C.c_void_p, C.c_int64]),
     "gsx_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
     "gsx_score": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_double)]),
+    "gsx_score_many": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t, P(C.c_double)]),
     "gsx_device_scores": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "gsx_sync": (C.c_int, [C.c_void_p]),
     "gsx_import_state": (C.c_int, [C.c_void_p, P(StateView)]),

@@ -167,6 +167,14 @@ class Engine:
         self._chk(self.lib.gsx_score(self.h, pair, C.byref(v)), "gsx_score")
         return float(v.value)
 
+    def score_many(self, pairs) -> np.ndarray:
+        """Score(p) of many pairs with one flush / re-score / copy (gsx_score_many)."""
+        pairs = np.ascontiguousarray(pairs, dtype=np.uint64)
+        out = np.empty(len(pairs), dtype=np.float64)
+        self._chk(self.lib.gsx_score_many(self.h, _ptr(pairs, C.c_uint64), len(pairs), _ptr(out, C.c_double)),
+                  "gsx_score_many")
+        return out
+
     def device_scores_ptr(self) -> int:
         v = C.c_void_p()
         self._chk(self.lib.gsx_device_scores(self.h, C.byref(v)), "gsx_device_scores")

@@ -267,6 +267,14 @@ int gsx_refresh(gsx_engine* e, int64_t now_ns);
 int gsx_scores(gsx_engine* e, double* out, size_t n_pairs);
 /* Score(p) for one pair (score.go:247-256). */
 int gsx_score(gsx_engine* e, uint64_t pair, double* out);
+/* Score(p) for n pairs at once (out[i] for pairs[i]): what one RPC of a
+ * router asks (AcceptFrom, gossipsub.go:589; the Publish targets and their
+ * thresholds, :960-989) with one flush of the queued tracer calls, one
+ * re-score and one copy.  On an engine of at most 65,536 pairs whose host
+ * score copy was current, the flush, the re-score of the touched observers'
+ * rows and the copy are one kernel launch that writes the host-mapped copy and
+ * signals a host-mapped flag (no stream synchronisation). */
+int gsx_score_many(gsx_engine* e, const uint64_t* pairs, size_t n, double* out);
 /* Device pointer of the score vector (valid until the next call). */
 int gsx_device_scores(gsx_engine* e, const double** dptr);
 

@@ -227,6 +227,25 @@ class PeerScore {
         check(gsx_score(e_, it->second, &s), "gsx_score");
         return s;
     }
+    // Score(p) of every peer one RPC asks about (AcceptFrom :589, the Publish
+    // targets :960-989): one flush, one re-score and one copy (gsx_score_many).
+    // Unknown peers score 0, as in Score.
+    std::vector<double> ScoreMany(const std::vector<std::string>& ps) {
+        std::vector<uint64_t> idx;
+        std::vector<size_t> at;
+        idx.reserve(ps.size());
+        for (size_t i = 0; i < ps.size(); ++i) {
+            auto it = peers_.find(ps[i]);
+            if (it == peers_.end()) continue;
+            sync_app(it->second);
+            idx.push_back(it->second);
+            at.push_back(i);
+        }
+        std::vector<double> got(idx.size()), out(ps.size(), 0.0);
+        check(gsx_score_many(e_, idx.data(), idx.size(), got.data()), "gsx_score_many");
+        for (size_t k = 0; k < at.size(); ++k) out[at[k]] = got[k];
+        return out;
+    }
     void AddPenalty(const std::string& p, int count) { event(GSX_EV_PENALTY, p, "", count); }  // :384-398
     Error SetTopicScoreParams(const std::string& topic, const TopicScoreParams& p) {  // :194-234
         uint32_t t = topic_index(topic, false);

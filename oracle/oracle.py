@@ -387,6 +387,10 @@ class Oracle:
     def score(self, pair):
         return float(self.lib.orc_score(self.h, pair))
 
+    def score_many(self, pairs):
+        """Score(p) of each pair (the checker of gsx_score_many)."""
+        return np.array([self.score(int(q)) for q in pairs], dtype=np.float64)
+
     def refresh_scores_range(self, now, p0, p1):
         out = np.empty(p1 - p0, dtype=np.float64)
         self._chk(self.lib.orc_refresh_scores_range(self.h, now, p0, p1, _p(out, C.c_double)), "orc_refresh_scores_range")

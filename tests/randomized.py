@@ -185,11 +185,12 @@ def replay(be, ov, n_topics, ops, whitelist=(3,)):
     return snaps
 
 
-def interleaved_score_calls(be, ov, n_topics, ops, seed, per_call=2):
+def interleaved_score_calls(be, ov, n_topics, ops, seed, per_call=2, many=False):
     """Replay ``ops`` one call at a time (every event and tracer call on its
     own), asking Score() of a few random pairs after each: what a router does
-    between RPCs (gossipsub.go:589 AcceptFrom, :960-989 Publish).  Returns
-    the scores asked, in order."""
+    between RPCs (gossipsub.go:589 AcceptFrom, :960-989 Publish); with
+    `many` the pairs of one ask go through one score_many call
+    (gsx_score_many).  Returns the scores asked, in order."""
     rng = np.random.default_rng(seed + 99)
     pp, tps = scenario_params(n_topics)
     be.set_peer_params(pp)
@@ -201,7 +202,11 @@ def interleaved_score_calls(be, ov, n_topics, ops, seed, per_call=2):
     out = []
 
     def ask():
-        for p in rng.integers(0, E, per_call).tolist():
+        ps = rng.integers(0, E, per_call)
+        if many:
+            out.extend(float(x) for x in be.score_many(ps.astype(np.uint64)))
+            return
+        for p in ps.tolist():
             out.append(be.score(int(p)))
 
     for op in ops:

@@ -67,6 +67,21 @@ def test_engine_score_calls_interleaved(gpu_ok, seed, n, d, T):
     assert_same_scores(got, want, "interleaved Score()")
 
 
+@pytest.mark.parametrize("seed,n,d,T", [(4, 200, 3, 3), (6, 3000, 6, 2), (11, 16000, 6, 1)])
+def test_engine_score_many_interleaved(gpu_ok, seed, n, d, T):
+    """gsx_score_many (one RPC's gates and Publish targets at once) after
+    every single event / tracer call: the one-launch drop-in round trip
+    (k_dropin: events, the touched rows re-scored into the host-mapped copy)
+    on small engines, the gather on the 16000-node one (above the host-copy
+    size) == the oracle's score() of the same pairs."""
+    ov = R.small_overlay(n, d, seed, max(8, n // 6))
+    ops = R.make_ops(ov, T, seed, n_steps=120)
+    got = R.interleaved_score_calls(gsx.Engine(T), ov, T, ops, seed, per_call=6, many=True)
+    want = R.interleaved_score_calls(orc.Oracle(T), ov, T, ops, seed, per_call=6, many=True)
+    assert len(got) == len(want) > 100
+    assert_same_scores(np.array(got), np.array(want), "interleaved score_many")
+
+
 @pytest.mark.parametrize("n,T,p_disc,p_abs", [(20000, 8, 0.0, 0.0), (30000, 8, 0.1, 0.05), (40000, 1, 0.05, 0.05),
                                               (5000, 5, 0.2, 0.2)])
 def test_engine_refresh_matches_oracle_synthetic(gpu_ok, n, T, p_disc, p_abs):

@@ -94,6 +94,17 @@ int main(int argc, char** argv) {
     }
     const double rpc = us_since(t0, N);
 
+    std::vector<std::string> targets(peers.begin(), peers.begin() + 6);
+    t0 = Clk::now();
+    for (int i = 0; i < N; ++i) {  // the same RPC with the batched call: AcceptFrom, message, one ScoreMany
+        sink += ps.Score(peers[i % K]);
+        const Message m{"z" + std::to_string(i), "t", peers[i % K]};
+        ps.ValidateMessage(m);
+        ps.DeliverMessage(m);
+        for (double v : ps.ScoreMany(targets)) sink += v;
+    }
+    const double rpc_many = us_since(t0, N);
+
     const int R = N / 10 > 0 ? N / 10 : 1;
     t0 = Clk::now();
     for (int i = 0; i < R; ++i) {
@@ -104,7 +115,8 @@ int main(int argc, char** argv) {
     std::printf(
         "{\"peers\": %d, \"calls_per_leg\": %d, \"score_unchanged_us\": %.3f, \"deliver_message_us\": %.3f, "
         "\"deliver_then_score_us\": %.3f, \"app_score_calls_per_score\": %.2f, "
-        "\"rpc_accept_deliver_publish6_us\": %.3f, \"refresh_scores_us\": %.3f, \"sink\": %g}\n",
-        K, N, score_cached, deliver, deliver_then_score, app_per_score, rpc, refresh, (double)sink);
+        "\"rpc_accept_deliver_publish6_us\": %.3f, \"rpc_accept_deliver_publish6_many_us\": %.3f, "
+        "\"refresh_scores_us\": %.3f, \"sink\": %g}\n",
+        K, N, score_cached, deliver, deliver_then_score, app_per_score, rpc, rpc_many, refresh, (double)sink);
     return 0;
 }
