@@ -238,6 +238,17 @@ struct PropState {
     double* tterm;
     uint32_t* tgen;
     uint32_t tepoch;
+    // Lazy re-scoring of the fold (k_prop_count<true, true>; null: off).  The
+    // credits of P2 / P3 only raise a score when every scored topic has
+    // TopicWeight >= 0, FirstMessageDeliveriesWeight >= 0 and
+    // MeshMessageDeliveriesWeight <= 0 (the signs score_params.go:207-260
+    // validates), so a pair whose stored score is >= lazy_thr (the largest
+    // threshold a fwd byte tests) keeps its fwd byte: its re-score is left to
+    // the next score reader (the host settles stale[] pairs, gsx_engine.cpp
+    // ensure_scores), and stale[q] = 1 marks it.  P4 credits lower a score:
+    // such pairs are always re-scored.
+    uint8_t* stale;
+    double lazy_thr;
 };
 
 // pins_only: the fwd bytes stand (a RESCORE count kept them), update the
@@ -422,6 +433,17 @@ struct HbState {
     // cache order, the set's word offset in the topic's set-word list)
     const uint2* gx_heads;
     const uint32_t* gx_hoff;
+    // the exchange on a range shard (null unsharded): the IHAVEs this rank's
+    // nodes sent over cross-shard pairs (sender side, [pair]: topic bits), and
+    // per cross-shard pair (u -> v), receiver side: v answers u's IWANT
+    // (v's score of u >= GossipThreshold), and the index of v's cache rows in
+    // the rows v's rank sent (gxs_rows: entries of 1 + gxs_fw words, the flat
+    // word list of the advertised batches; NO_PAIR: v holds only common messages)
+    uint64_t* gxs_out;
+    uint8_t* gxs_rans;
+    uint32_t* gxs_hidx;
+    const uint64_t* gxs_rows;
+    uint32_t gxs_fw;
     // the IWANT first receipts per (topic, pair) of this round (the forwarding's
     // hop-1 back-sends, GxFwd); null when nothing is forwarded
     uint32_t* gxb_st0;     // [pair] stamp: the pair's counts were written this round
@@ -538,6 +560,8 @@ struct GxFwdSet {
     const uint64_t* src;  // [n_msgs] origin node << 32 | message index, ascending
     uint64_t* fr[2];      // [node][W] frontier rows by hop parity (valid under the node's fmask bit)
     uint32_t n_words, n_msgs, topic, slot, serial;
+    uint32_t woff;        // word offset of the set's rows in a cross-shard frontier entry (range shards)
+    uint8_t* got;         // set to 1 when a node delivers a message of the set (its recovered batch is Put)
     uint32_t old_in;      // a copy of a message the receiver had before the round is inside the P3 window
 };
 struct GxFwd {
@@ -568,11 +592,49 @@ struct GxFwd {
     uint16_t* fin;
     uint64_t all_sets;
     uint64_t* fbit[2];  // [node / 64] bit per node: in the frontier (the pull's filter: L2-resident)
+    // range shards: the frontier of remote senders, per hop, as entries of
+    // GXF_HDR + rw words (receive slot, set mask, back-send counts per slot and
+    // their in-window part as 8 x u16 each, then the rows of every run set at
+    // its woff); per cross-shard pair (x -> v): the entry of v this hop
+    // (hstamp == seq + hop) and its index
+    uint32_t* hstamp;
+    uint32_t* hidx;
+    const uint64_t* hent;
+    uint32_t rw;
 };
+constexpr uint32_t GXF_HDR = 6;
 constexpr uint16_t GXF_GRAY = 0x100;
 hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
                            hipStream_t st);
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st);
+// The exchange across range shards (gsx.h, gsx_gx_*): per send slot, the
+// IHAVE topic bits and the answer bit of its pair ([n_send][2]); their
+// receipt per receive slot; the entries of the senders' cache rows (a count
+// pass per destination with out null, then the pack into out at off[dest]);
+// their receipt; the forwarding's per-pair topic slots (fout) per send slot
+// and their receipt; a hop's frontier entries (count / pack) and their receipt.
+struct GxsPlan {  // the shard plan's send side (gsx_shard_send_plan)
+    const uint32_t* send_pair;       // [send slot]: the local pair (v -> u) it carries, NO_PAIR = none
+    const uint8_t* send_dest;        // [send slot]: destination rank
+    const uint64_t* send_base;       // [rank + 1]: first send slot of each destination
+    const uint64_t* dest_halo_base;  // [rank]: the destination's receive slot of this rank's first
+    const uint32_t* pair_obs;        // [pair]: its local owner
+    uint64_t n_send;
+};
+hipError_t launch_gxs_pack_ihave(const DevState& s, const HbState& h, const GxsPlan& P, uint64_t* out, hipStream_t st);
+hipError_t launch_gxs_recv_ihave(const HbState& h, const uint64_t* in, const uint32_t* halo_pair, uint64_t n_recv,
+                                 hipStream_t st);
+hipError_t launch_gxs_rows(const HbState& h, const GxsPlan& P, const GxBatch* gx, uint32_t n_gx,
+                           unsigned long long* cnt, const uint64_t* off, uint64_t* out, hipStream_t st);
+hipError_t launch_gxs_rows_recv(const HbState& h, const uint64_t* in, uint64_t n, const uint32_t* halo_pair,
+                                hipStream_t st);
+hipError_t launch_gxf_pack_fout(const GxFwd& f, const GxsPlan& P, uint64_t* out, hipStream_t st);
+hipError_t launch_gxf_recv_fout(const GxFwd& f, const uint64_t* in, const uint32_t* halo_pair, uint64_t n_recv,
+                                hipStream_t st);
+hipError_t launch_gxf_halo(const HbState& h, const GxFwd& f, const GxsPlan& P, uint32_t hop, unsigned long long* cnt,
+                           const uint64_t* off, uint64_t* out, hipStream_t st);
+hipError_t launch_gxf_halo_recv(const HbState& h, const GxFwd& f, uint32_t hop, const uint64_t* in, uint64_t n,
+                                const uint32_t* halo_pair, const uint32_t* halo_node, hipStream_t st);
 // Promise slots [pair][from] -> [pair][to] (to > from; new slots free).
 hipError_t launch_gx_prom_grow(const uint64_t* h_in, const int64_t* e_in, uint32_t from, uint64_t* h_out,
                                int64_t* e_out, uint32_t to, uint64_t n_pairs, hipStream_t st);

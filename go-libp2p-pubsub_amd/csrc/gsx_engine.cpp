@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -224,6 +225,34 @@ struct gsx_engine {
     void* h_gxf_stage = nullptr;      // pinned: the runs' set descriptors
     size_t h_gxf_stage_bytes = 0;
     uint32_t gxf_stamp = 0;           // stamps of the IWANT back counts (one per round) and of the hops
+    uint32_t* d_gxf_hst = nullptr;    // range shards: [2][E] GxFwd::hstamp, hidx
+    uint64_t* d_gxs_out = nullptr;    // range shards: [E] HbState::gxs_out
+    uint8_t* d_gxs_rans = nullptr;    // range shards: [E] HbState::gxs_rans
+    uint32_t* d_gxs_hidx = nullptr;   // range shards: [E] HbState::gxs_hidx
+    unsigned long long* d_gxs_cnt = nullptr;  // range shards: [MAX_RANKS] entries per destination
+    uint64_t* d_gxs_off = nullptr;            // range shards: [MAX_RANKS] their first entry
+    uint64_t* d_gxs_send = nullptr;           // range shards: the entries this rank sends (grown)
+    size_t gxs_send_cap = 0;
+    std::vector<uint64_t> gxs_counts;         // the last count pass, per destination
+    // The exchange (D) of the round in flight: hb_end prepares it; unsharded it
+    // runs at once, on a range shard the gsx_gx_* / gsx_gxf_* steps run it and
+    // gsx_gx_end finishes the round.
+    struct GxfRun {
+        std::vector<size_t> sets;   // indices into GxRound::sets
+        std::vector<uint32_t> topics;
+    };
+    struct GxRound {
+        bool run = false, pending = false, exact = false, fwd_active = false;
+        int stage = 0;  // range shards: 1 prepared, 2 common set, 3 IHAVEs in, 4 rows in, 5 exchanged
+        gsx::HbState h{};
+        std::vector<MsgSet*> sets;
+        std::vector<uint64_t*> xs;
+        std::vector<std::pair<uint64_t*, size_t>> scratch;  // frontier rows, released after the round's sync
+        uint32_t n_gx = 0, fw = 0;
+        std::vector<GxfRun> runs;
+        gsx::GxFwd f{};
+        uint32_t hops = 0;
+    } gxr;
     std::vector<gsx::GossipBatch> gb_host;  // per heartbeat: batch descriptors of every topic
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
@@ -363,15 +392,24 @@ struct gsx_engine {
     uint32_t dropin_tag = 0;
     uint64_t score_writes = 0, h_score_tag = ~0ull;
     bool dirty_zeroed = true;  // d_smask not cleared yet
+    // Lazy folds (PropState::stale): the scores are exact but for the pairs
+    // d_stale marks, whose stored score is a lower bound >= lazy_thr (every
+    // fwd byte exact for thresholds up to lazy_thr); ensure_scores settles them.
+    bool lazy = false;
+    bool stale_marks = false;  // d_stale may hold marks (cleared before a lazy fold starts a new set)
+    double lazy_thr = 0;
+    uint8_t* d_stale = nullptr;
     void invalidate_scores() {
         ++rec_gen;
         scores_valid = false;
         dirty_only = false;
+        lazy = false;
         dirty_obs.clear();
     }
     void scores_exact() {  // every score was just computed
         scores_valid = true;
         dirty_only = false;
+        lazy = false;
         dirty_obs.clear();
     }
     // generations: flag_gen moves with anything that may change pair / record
@@ -585,6 +623,9 @@ void free_state(gsx_engine* e) {
     e->d_rev = nullptr;
     if (e->d_smask) (void)hipFree(e->d_smask);
     if (e->d_dirty_obs) (void)hipFree(e->d_dirty_obs);
+    if (e->d_stale) (void)hipFree(e->d_stale);
+    e->d_stale = nullptr;
+    e->stale_marks = false;
     e->d_smask = nullptr;
     e->d_dirty_obs = nullptr;
     e->d_dirty_obs_cap = 0;
@@ -638,7 +679,8 @@ void free_state(gsx_engine* e) {
                        e->d_gx_got, e->d_gx_nodes,
                        e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg,
                        e->d_gxf_mask, e->d_gxf_list, e->d_gxf_cnt, e->d_gxf_bst, e->d_gxf_b0, e->d_gxf_b,
-                       e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout};
+                       e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout, e->d_gxf_hst, e->d_gxs_out, e->d_gxs_rans,
+                       e->d_gxs_hidx, e->d_gxs_cnt, e->d_gxs_off, e->d_gxs_send};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
         e->d_gxf_mask = nullptr;
@@ -648,6 +690,14 @@ void free_state(gsx_engine* e) {
         e->d_gxf_sets = nullptr;
         e->d_gxf_fin = nullptr;
         e->d_gxf_fout = nullptr;
+        e->d_gxf_hst = nullptr;
+        e->d_gxs_out = nullptr;
+        e->d_gxs_rans = nullptr;
+        e->d_gxs_hidx = nullptr;
+        e->d_gxs_cnt = nullptr;
+        e->d_gxs_off = nullptr;
+        e->d_gxs_send = nullptr;
+        e->gxs_send_cap = 0;
         e->gxf_sets_cap = 0;
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
@@ -799,7 +849,7 @@ int flush(gsx_engine* e) {
     const auto* doff = reinterpret_cast<const uint32_t*>(static_cast<const char*>(e->d_stage) + ev_bytes);
     HIPCHK(e, gsx::launch_apply_events(dev_state(e), dev_peer_params(e), dev, doff, n_groups, e->stream));
     e->pending.clear();
-    if (e->scores_valid || e->dirty_only) {  // exact but for these observers
+    if (e->scores_valid || e->dirty_only || e->lazy) {  // exact but for these observers (and the stale pairs)
         for (uint32_t g = 0; g < n_groups; ++g) e->dirty_obs.push_back(obs[order[group_off[g]]]);
         e->scores_valid = false;
         e->dirty_only = true;
@@ -827,10 +877,62 @@ hipError_t rescore_subset(gsx_engine* e, const gsx::DevState& ds, const gsx::Ker
     return gsx::launch_score_subset(ds, kp, mask, e->stream, mask2);
 }
 
+// The largest threshold a propagation fwd byte tests (k_prop_fwd: publishThreshold, graylistThreshold).
+double lazy_threshold(const gsx_engine* e) {
+    return std::max(e->th.publish_threshold, e->th.graylist_threshold);
+}
+
+// Whether P2 / P3 credits can only raise a score: every scored topic has the
+// signs TopicScoreParams.validate asks (score_params.go:207-236).
+bool credits_raise_scores(const gsx_engine* e) {
+    for (uint32_t t = 0; t < e->T; ++t) {
+        if (!e->scored[t]) continue;
+        const gsx_topic_score_params& p = e->tp[t];
+        if (!(p.topic_weight >= 0 && p.first_message_deliveries_weight >= 0 && p.mesh_message_deliveries_weight <= 0))
+            return false;
+    }
+    return true;
+}
+
+// The dirty observer list on the device (sorted, unique) -> GSX_OK.
+int upload_dirty_obs(gsx_engine* e) {
+    std::vector<uint32_t>& d = e->dirty_obs;
+    if (!e->d_dirty_obs || e->d_dirty_obs_cap < d.size()) {
+        if (e->d_dirty_obs) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            (void)hipFree(e->d_dirty_obs);
+            e->d_dirty_obs = nullptr;
+        }
+        e->d_dirty_obs_cap = std::max<size_t>(d.size(), 2 * e->d_dirty_obs_cap);
+        if (int rc = dalloc(e, &e->d_dirty_obs, e->d_dirty_obs_cap)) return rc;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_dirty_obs, d.data(), 4 * d.size(), hipMemcpyHostToDevice, e->stream));
+    return GSX_OK;
+}
+
+// Lazy folds left stale pairs (PropState::stale): re-score them and the
+// dirty observers' rows (events since), then clear the marks.
+int settle_stale(gsx_engine* e) {
+    std::vector<uint32_t>& d = e->dirty_obs;
+    if (e->dirty_only && !d.empty()) {
+        std::sort(d.begin(), d.end());
+        d.erase(std::unique(d.begin(), d.end()), d.end());
+        if (int rc = upload_dirty_obs(e)) return rc;
+        HIPCHK(e, gsx::launch_mark_rows(e->d_row_ptr, e->d_dirty_obs, (uint32_t)d.size(), e->d_stale, 1, e->stream));
+    }
+    HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), e->d_stale));
+    HIPCHK(e, hipMemsetAsync(e->d_stale, 0, std::max<size_t>(e->E, 1), e->stream));
+    e->stale_marks = false;
+    if (e->dirty_only && !d.empty()) HIPCHK(e, hipStreamSynchronize(e->stream));  // (the list was read)
+    e->scores_exact();
+    return GSX_OK;
+}
+
 int ensure_scores(gsx_engine* e) {
     int rc = flush(e);
     if (rc) return rc;
     if (e->scores_valid) return GSX_OK;
+    if (e->lazy) return settle_stale(e);
     std::vector<uint32_t>& d = e->dirty_obs;
     uint64_t n_dirty = 0;
     if (e->dirty_only) {
@@ -840,20 +942,11 @@ int ensure_scores(gsx_engine* e) {
     }
     if (e->dirty_only && n_dirty * 8 < e->E) {  // a few observers: their rows only
         if (!e->d_smask && (rc = dalloc(e, &e->d_smask, e->E))) return rc;
-        if (!e->d_dirty_obs || e->d_dirty_obs_cap < d.size()) {
-            if (e->d_dirty_obs) {
-                HIPCHK(e, hipStreamSynchronize(e->stream));
-                (void)hipFree(e->d_dirty_obs);
-                e->d_dirty_obs = nullptr;
-            }
-            e->d_dirty_obs_cap = std::max<size_t>(d.size(), 2 * e->d_dirty_obs_cap);
-            if ((rc = dalloc(e, &e->d_dirty_obs, e->d_dirty_obs_cap))) return rc;
-        }
+        if ((rc = upload_dirty_obs(e))) return rc;
         if (e->dirty_zeroed) {  // first use: the mask starts all-zero
             HIPCHK(e, hipMemsetAsync(e->d_smask, 0, e->E, e->stream));
             e->dirty_zeroed = false;
         }
-        HIPCHK(e, hipMemcpyAsync(e->d_dirty_obs, d.data(), 4 * d.size(), hipMemcpyHostToDevice, e->stream));
         HIPCHK(e, gsx::launch_mark_rows(e->d_row_ptr, e->d_dirty_obs, (uint32_t)d.size(), e->d_smask, 1, e->stream));
         HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), e->d_smask));
         HIPCHK(e, gsx::launch_mark_rows(e->d_row_ptr, e->d_dirty_obs, (uint32_t)d.size(), e->d_smask, 0, e->stream));
@@ -1516,7 +1609,7 @@ int gsx_set_pair_ips(gsx_engine* e, const uint64_t* pairs, const uint32_t* ips, 
     HIPCHK(e, hipStreamSynchronize(e->stream));
     (void)hipFree(d_mv);
     (void)hipFree(d_off);
-    if (e->scores_valid || e->dirty_only) {  // only these observers' P6 moved
+    if (e->scores_valid || e->dirty_only || e->lazy) {  // only these observers' P6 moved
         for (uint32_t g = 0; g < n_grp; ++g) e->dirty_obs.push_back(obs[order[off[g]]]);
         e->scores_valid = false;
         e->dirty_only = true;
@@ -2226,7 +2319,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     // publishThreshold for floodsub peers and flood publishing: k_prop_fwd);
     // the other routers never
     const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB;
-    if (int rc = need_score ? ensure_scores(e) : flush(e)) return rc;  // queued events land first either way
+    if (int rc = flush(e)) return rc;  // queued events land first either way
+    // (after lazy folds the fwd bytes stand for thresholds up to lazy_thr: the stale scores wait)
+    const bool lazy_ok = e->lazy && !e->dirty_only && lazy_threshold(e) <= e->lazy_thr;
+    if (need_score && !lazy_ok)
+        if (int rc = ensure_scores(e)) return rc;
     const uint32_t W = prop_words(m);
     const size_t N = e->n_nodes, E = e->E;
     const uint32_t rows = cfg->max_hops + 1;
@@ -2489,8 +2586,13 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     // the folded pairs are re-scored in the fold when every other score is
     // exact (gossipsub calls start from exact scores) and the fwd bytes match
     // this call's settings (unsharded, incremental fwd state)
-    const bool rescore = fold_now && e->scores_valid && e->pending.empty() && !e->sharded() && P.fwd_key.valid &&
-                         P.fwd_key.score_gen == e->score_gen && P.cfg.router == GSX_ROUTER_GOSSIPSUB;
+    const bool rescore = fold_now && (e->scores_valid || (e->lazy && !e->dirty_only)) && e->pending.empty() &&
+                         !e->sharded() && P.fwd_key.valid && P.fwd_key.score_gen == e->score_gen &&
+                         P.cfg.router == GSX_ROUTER_GOSSIPSUB;
+    // lazy: the credited pairs at or above every threshold keep a stale score (PropState::stale)
+    static const bool no_lazy = getenv("GSX_NO_LAZY_FOLD") != nullptr;
+    const double thr = lazy_threshold(e);
+    const bool lazy = rescore && !no_lazy && credits_raise_scores(e) && (!e->lazy || thr <= e->lazy_thr);
     if (ps.credit || ps.late) {
         gsx::PropState pc = ps;
         // the topic-term cache (several topics: a fold then re-reads one topic's record, not all)
@@ -2512,6 +2614,16 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
             pc.tgen = P.tgen;
             pc.tepoch = P.tepoch;
         }
+        if (lazy) {
+            if (!e->d_stale) {
+                if (int rc = dalloc(e, &e->d_stale, std::max<size_t>(e->E, 1))) return rc;
+                e->stale_marks = true;
+            }
+            if (!e->lazy && e->stale_marks)  // a new stale set
+                HIPCHK(e, hipMemsetAsync(e->d_stale, 0, std::max<size_t>(e->E, 1), e->stream));
+            pc.stale = e->d_stale;
+            pc.lazy_thr = thr;
+        }
         HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
         if (pc.tterm) P.t_rec_gen = e->rec_gen;
         else if (rescore) P.t_plain_gen = e->rec_gen;
@@ -2521,7 +2633,18 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         // pending ones of the topic) and left the pending counts empty
         P.credit_pending = !fold_now;
         P.credit_topic = ps.topic;
-        if (rescore) {  // every score exact again, the fwd bytes with them
+        if (rescore && lazy) {  // every fwd byte exact, every score but the stale pairs'
+            ++e->score_writes;
+            const bool was = e->lazy;
+            e->scores_exact();
+            e->scores_valid = false;
+            e->lazy = true;
+            e->stale_marks = true;
+            e->lazy_thr = was ? std::min(e->lazy_thr, thr) : thr;
+            ++e->score_gen;
+            P.fwd_key.score_gen = e->score_gen;
+            P.fold_chg = true;
+        } else if (rescore) {  // every score exact again, the fwd bytes with them
             ++e->score_writes;
             e->scores_exact();
             ++e->score_gen;
@@ -2534,7 +2657,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     }
     const uint32_t W = ps.n_words;
     gsx_engine::MsgSet* set = nullptr;
-    if (P.cfg.router == GSX_ROUTER_GOSSIPSUB && !ps.sharded) {  // the call's seen rows, before the uncache
+    if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // the call's seen rows, before the uncache (a shard: its nodes')
         const size_t N = ps.n_nodes;
         set = new gsx_engine::MsgSet;
         set->serial = ++e->msg_serial;
@@ -2937,7 +3060,7 @@ int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
     p->max_ihave_messages = 10;
     p->gossip_retransmission = 3;
     p->iwant_followup_ns = 3LL * 1000000000LL;
-    p->gossip_exchange = 0;
+    p->gossip_exchange = 1;  // the reference always handles IHAVE/IWANT (gossipsub.go:615-720)
     p->fanout_ttl_ns = 60LL * 1000000000LL;
     p->do_px = 0;           // WithPeerExchange is opt-in (:325-333)
     p->prune_peers = 16;    // GossipSubPrunePeers
@@ -3103,7 +3226,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     if (!e->d_hbstats)
         if (int rc = hb_alloc(e)) return rc;
     const bool gx_on = e->gp.gossip_exchange != 0;
-    if (gx_on && e->sharded()) return fail(e, GSX_ESTATE, "the gossip exchange runs on unsharded engines only");
+    if (gx_on && e->sharded() && e->n_ranks > 1 && !e->d_dest_halo_base)
+        return fail(e, GSX_ESTATE, "gossip exchange on a shard: gsx_shard_set_halo_bases first");
     if (gx_on)
         if (int rc = gx_alloc(e)) return rc;
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
@@ -3220,6 +3344,20 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32, e->stream));
         e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
+        if (e->sharded()) {  // the IHAVEs of cross-shard pairs, sender side (gsx_gx_pack_ihave)
+            const size_t E = std::max<size_t>(e->E, 1);
+            if (!e->d_gxs_out) {
+                int rc = 0;
+                if ((rc = dalloc(e, &e->d_gxs_out, E)) || (rc = dalloc(e, &e->d_gxs_rans, E)) ||
+                    (rc = dalloc(e, &e->d_gxs_hidx, E)) || (rc = dalloc(e, &e->d_gxs_cnt, (size_t)gsx::MAX_RANKS)) ||
+                    (rc = dalloc(e, &e->d_gxs_off, (size_t)gsx::MAX_RANKS)))
+                    return rc;
+            }
+            HIPCHK(e, hipMemsetAsync(e->d_gxs_out, 0, 8 * E, e->stream));
+            h.gxs_out = e->d_gxs_out;
+            h.gxs_rans = e->d_gxs_rans;
+            h.gxs_hidx = e->d_gxs_hidx;
+        }
     }
     if (e->gp.do_px) {  // peer exchange on the round's PRUNEs (gsx.h; heartbeats and Join / Leave rounds)
         if (e->sharded() && e->n_ranks > 1 && !e->d_dest_halo_base)
@@ -3416,6 +3554,7 @@ int gxf_alloc(gsx_engine* e) {
     if (e->d_gxf_bst) {
         if (e->gxf_stamp < 0xF0000000u) return GSX_OK;
         HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * std::max<size_t>(e->E, 1), e->stream));
+        if (e->d_gxf_hst) HIPCHK(e, hipMemsetAsync(e->d_gxf_hst, 0, 4 * 2 * std::max<size_t>(e->E, 1), e->stream));
         e->gxf_stamp = 0;
         return GSX_OK;
     }
@@ -3427,6 +3566,8 @@ int gxf_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fin, E)) ||
         (rc = dalloc(e, &e->d_gxf_fout, E)))
         return rc;
+    if (e->sharded() && (rc = dalloc(e, &e->d_gxf_hst, 2 * E))) return rc;
+    if (e->d_gxf_hst) HIPCHK(e, hipMemsetAsync(e->d_gxf_hst, 0, 4 * 2 * E, e->stream));
     if (!e->h_gxf_cnt) HIPCHK(e, hipHostMalloc((void**)&e->h_gxf_cnt, 64, hipHostMallocDefault));
     HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_gxf_mask + 2 * N, 0, 8 * N, e->stream));  // rmask: kept clear by the pulls
@@ -3434,18 +3575,12 @@ int gxf_alloc(gsx_engine* e) {
     return GSX_OK;
 }
 
-// Runs the forwarding over the exchange's sets (their receipt rows x as the
-// exchange left them: first receipts, the hop-0 frontier once masked by the
-// accepted words).  A run takes up to 64 sets of up to GXF_SLOTS topics, and
-// all sets of each of its topics (the IWANT back counts are per topic); the
-// hops of a run are launched in chunks with one host check of the last hop's
-// frontier size per chunk.  `scratch` gets the frontier-row buffers (released
-// by the caller after its stream sync).
-int gx_forward(gsx_engine* e, const gsx::HbState& h, const gsx::DevState& ds,
-               const std::vector<gsx_engine::MsgSet*>& sets, const std::vector<uint64_t*>& xs, int64_t now,
-               std::vector<std::pair<uint64_t*, size_t>>& scratch) {
-    const size_t N = e->n_nodes;
-    if (sets.empty() || N == 0) return GSX_OK;
+// The forwarding runs over the exchange's sets: up to 64 sets of up to
+// GXF_SLOTS topics each, and all sets of each of its topics (the IWANT back
+// counts are per topic); topics in first-seen order, greedily.
+int gxf_plan(gsx_engine* e, gsx_engine::GxRound& R) {
+    R.runs.clear();
+    const auto& sets = R.sets;
     std::vector<uint32_t> topics;
     std::vector<std::vector<size_t>> by_topic;
     for (size_t i = 0; i < sets.size(); ++i) {
@@ -3457,387 +3592,411 @@ int gx_forward(gsx_engine* e, const gsx::HbState& h, const gsx::DevState& ds,
         }
         by_topic[ti].push_back(i);
     }
+    size_t n_sets = 0;
     for (size_t ti = 0; ti < topics.size(); ++ti) {
         size_t msgs = 0;
         for (size_t i : by_topic[ti]) msgs += sets[i]->n_msgs;
         if (by_topic[ti].size() > 64 || msgs > 65535)
             return fail(e, GSX_ERANGE, "gossip exchange: topic " + std::to_string(topics[ti]) +
                                            " advertises more than 64 message sets or 65,535 messages in one round");
-    }
-    // the runs: topics in first-seen order, greedily
-    std::vector<std::vector<size_t>> runs;  // topic indices per run
-    {
-        size_t n_sets = 0;
-        for (size_t ti = 0; ti < topics.size(); ++ti) {
-            if (runs.empty() || runs.back().size() == gsx::GXF_SLOTS || n_sets + by_topic[ti].size() > 64) {
-                runs.emplace_back();
-                n_sets = 0;
-            }
-            runs.back().push_back(ti);
-            n_sets += by_topic[ti].size();
+        if (R.runs.empty() || R.runs.back().topics.size() == gsx::GXF_SLOTS || n_sets + by_topic[ti].size() > 64) {
+            R.runs.emplace_back();
+            n_sets = 0;
         }
+        R.runs.back().topics.push_back(topics[ti]);
+        for (size_t i : by_topic[ti]) R.runs.back().sets.push_back(i);
+        n_sets += by_topic[ti].size();
     }
-    if (sets.size() > e->gxf_sets_cap) {
+    return GSX_OK;
+}
+
+// Sets up run k (descriptors, frontier rows, cleared masks and counts) and
+// launches its hop 0 (the recovering nodes' accepted receipts) and the
+// per-pair forwarding slots.
+int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
+    const size_t N = e->n_nodes;
+    const auto& run = R.runs[k];
+    const size_t ns = run.sets.size();
+    if (ns > e->gxf_sets_cap) {
         if (e->d_gxf_sets) (void)hipFree(e->d_gxf_sets);
         e->d_gxf_sets = nullptr;
-        e->gxf_sets_cap = std::max<size_t>(std::max<size_t>(sets.size(), 2 * e->gxf_sets_cap), 64);
+        e->gxf_sets_cap = std::max<size_t>(std::max<size_t>(ns, 2 * e->gxf_sets_cap), 64);
         if (int rc = dalloc(e, &e->d_gxf_sets, e->gxf_sets_cap)) return rc;
     }
-    const size_t stage_bytes = sizeof(gsx::GxFwdSet) * sets.size();
+    const size_t stage_bytes = sizeof(gsx::GxFwdSet) * 64;
     if (e->h_gxf_stage_bytes < stage_bytes) {
         if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
         e->h_gxf_stage = nullptr;
         e->h_gxf_stage_bytes = 0;
-        HIPCHK(e, hipHostMalloc(&e->h_gxf_stage, 2 * stage_bytes, hipHostMallocDefault));
-        e->h_gxf_stage_bytes = 2 * stage_bytes;
+        HIPCHK(e, hipHostMalloc(&e->h_gxf_stage, stage_bytes, hipHostMallocDefault));
+        e->h_gxf_stage_bytes = stage_bytes;
     }
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // the staging buffer of the run before
     auto* stage = static_cast<gsx::GxFwdSet*>(e->h_gxf_stage);
-    size_t base = 0;
-    for (const auto& run : runs) {
-        gsx::GxFwd f{};
-        f.sets = e->d_gxf_sets + base;
-        f.n_slots = (uint32_t)run.size();
-        uint32_t n_src = 0;
-        for (size_t ts = 0; ts < run.size(); ++ts) {
-            const uint32_t t = topics[run[ts]];
-            f.slot_topic[ts] = t;
-            for (size_t i : by_topic[run[ts]]) {
-                const gsx_engine::MsgSet* ms = sets[i];
-                const size_t words = (size_t)ms->n_words * N;
-                gsx::GxFwdSet S{};
-                S.all = ms->d_all;
-                S.x = xs[i];
-                S.acc = ms->d_acc;
-                S.src = ms->d_src;
-                for (int k = 0; k < 2; ++k) {
-                    S.fr[k] = seen_acquire(e, words);
-                    if (!S.fr[k]) return fail(e, GSX_ENOMEM, "forwarding frontier rows");
-                    scratch.emplace_back(S.fr[k], words);
-                }
-                S.n_words = ms->n_words;
-                S.n_msgs = ms->n_msgs;
-                S.topic = t;
-                S.slot = (uint32_t)ts;
-                S.serial = ms->serial;
-                // an old copy counts as validated when its set's call ran (gsx.h)
-                S.old_in = now - ms->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
-                f.slot_sets[ts] |= 1ull << f.n_sets;
-                stage[base + f.n_sets] = S;
-                ++f.n_sets;
-                n_src += ms->n_msgs;
+    gsx::GxFwd f{};
+    f.sets = e->d_gxf_sets;
+    f.n_slots = (uint32_t)run.topics.size();
+    uint32_t n_src = 0, rw = 0;
+    for (size_t ts = 0; ts < run.topics.size(); ++ts) {
+        const uint32_t t = run.topics[ts];
+        f.slot_topic[ts] = t;
+        for (size_t i : run.sets) {
+            const gsx_engine::MsgSet* ms = R.sets[i];
+            if (ms->topic != t) continue;
+            const size_t words = (size_t)ms->n_words * N;
+            gsx::GxFwdSet S{};
+            S.all = ms->d_all;
+            S.x = R.xs[i];
+            S.acc = ms->d_acc;
+            S.src = ms->d_src;
+            for (int z = 0; z < 2; ++z) {
+                S.fr[z] = seen_acquire(e, std::max<size_t>(words, 1));
+                if (!S.fr[z]) return fail(e, GSX_ENOMEM, "forwarding frontier rows");
+                R.scratch.emplace_back(S.fr[z], std::max<size_t>(words, 1));
             }
+            S.n_words = ms->n_words;
+            S.n_msgs = ms->n_msgs;
+            S.topic = t;
+            S.slot = (uint32_t)ts;
+            S.serial = ms->serial;
+            S.woff = rw;
+            S.got = e->d_gx_got + i;
+            rw += ms->n_words;
+            // an old copy counts as validated when its set's call ran (gsx.h)
+            S.old_in = R.h.now - ms->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
+            f.slot_sets[ts] |= 1ull << f.n_sets;
+            stage[f.n_sets] = S;
+            ++f.n_sets;
+            n_src += ms->n_msgs;
         }
-        HIPCHK(e, hipMemcpyAsync(e->d_gxf_sets + base, stage + base, sizeof(gsx::GxFwdSet) * f.n_sets,
-                                 hipMemcpyHostToDevice, e->stream));
-        f.fmask[0] = e->d_gxf_mask;
-        f.fmask[1] = e->d_gxf_mask + N;
-        f.rmask = e->d_gxf_mask + 2 * N;
-        f.srcm = e->d_gxf_mask + 3 * N;
-        f.flist[0] = e->d_gxf_list;
-        f.flist[1] = e->d_gxf_list + N;
-        f.rlist = e->d_gxf_list + 2 * N;
-        f.fcnt = e->d_gxf_cnt;
-        f.rcnt = e->d_gxf_cnt + gsx::GXF_MAX_HOPS + 1;
-        const size_t E = std::max<size_t>(e->E, 1);
-        f.bst0 = e->d_gxf_bst;
-        f.bcnt0 = e->d_gxf_b0;
-        f.stamp0 = h.gxb_stamp;
-        f.bst[0] = e->d_gxf_bst + E;
-        f.bst[1] = e->d_gxf_bst + 2 * E;
-        f.bcnt[0] = e->d_gxf_b;
-        f.bcnt[1] = e->d_gxf_b + E * gsx::GXF_SLOTS;
-        f.seq = e->gxf_stamp + 1;
-        f.fout = e->d_gxf_fout;
-        f.fin = e->d_gxf_fin;
-        f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
-        f.fbit[0] = e->d_gxf_mask + 4 * N;
-        f.fbit[1] = f.fbit[0] + (N + 63) / 64;
-        HIPCHK(e, hipMemsetAsync(f.fbit[0], 0, 8 * 2 * ((N + 63) / 64), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxf_mask, 0, 8 * 2 * N, e->stream));   // fmask
-        HIPCHK(e, hipMemsetAsync(f.srcm, 0, 8 * N, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxf_cnt, 0, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1), e->stream));
-        HIPCHK(e, gsx::launch_gxf_init(ds, h, f, n_src, e->stream));
+    }
+    f.rw = rw;
+    HIPCHK(e, hipMemcpyAsync(e->d_gxf_sets, stage, sizeof(gsx::GxFwdSet) * f.n_sets, hipMemcpyHostToDevice, e->stream));
+    f.fmask[0] = e->d_gxf_mask;
+    f.fmask[1] = e->d_gxf_mask + N;
+    f.rmask = e->d_gxf_mask + 2 * N;
+    f.srcm = e->d_gxf_mask + 3 * N;
+    f.fbit[0] = e->d_gxf_mask + 4 * N;
+    f.fbit[1] = f.fbit[0] + (N + 63) / 64;
+    f.flist[0] = e->d_gxf_list;
+    f.flist[1] = e->d_gxf_list + N;
+    f.rlist = e->d_gxf_list + 2 * N;
+    f.fcnt = e->d_gxf_cnt;
+    f.rcnt = e->d_gxf_cnt + gsx::GXF_MAX_HOPS + 1;
+    const size_t E = std::max<size_t>(e->E, 1);
+    f.bst0 = e->d_gxf_bst;
+    f.bcnt0 = e->d_gxf_b0;
+    f.stamp0 = R.h.gxb_stamp;
+    f.bst[0] = e->d_gxf_bst + E;
+    f.bst[1] = e->d_gxf_bst + 2 * E;
+    f.bcnt[0] = e->d_gxf_b;
+    f.bcnt[1] = e->d_gxf_b + E * gsx::GXF_SLOTS;
+    f.seq = e->gxf_stamp + 1;
+    f.fout = e->d_gxf_fout;
+    f.fin = e->d_gxf_fin;
+    f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
+    if (e->d_gxf_hst) {
+        f.hstamp = e->d_gxf_hst;
+        f.hidx = e->d_gxf_hst + E;
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_gxf_mask, 0, 8 * 2 * N, e->stream));  // fmask
+    HIPCHK(e, hipMemsetAsync(f.srcm, 0, 8 * N, e->stream));
+    HIPCHK(e, hipMemsetAsync(f.fbit[0], 0, 8 * 2 * ((N + 63) / 64), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_gxf_cnt, 0, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1), e->stream));
+    HIPCHK(e, gsx::launch_gxf_init(dev_state(e), R.h, f, n_src, e->stream));
+    R.f = f;
+    R.hops = 0;
+    R.fwd_active = true;
+    return GSX_OK;
+}
+
+int gxf_run_end(gsx_engine* e, gsx_engine::GxRound& R) {
+    e->gxf_stamp = R.f.seq + R.hops + 1;
+    R.fwd_active = false;
+    return GSX_OK;
+}
+
+// The forwarding on one engine: every run, its hops launched in chunks with
+// one host check of the last hop's frontier size per chunk.
+int gx_forward(gsx_engine* e, gsx_engine::GxRound& R) {
+    if (R.sets.empty() || e->n_nodes == 0) return GSX_OK;
+    if (int rc = gxf_plan(e, R)) return rc;
+    const gsx::DevState ds = dev_state(e);
+    for (size_t k = 0; k < R.runs.size(); ++k) {
+        if (int rc = gxf_run_begin(e, R, k)) return rc;
         uint32_t hop = 1;
         for (;;) {
             const uint32_t chunk = hop == 1 ? 6 : 8;
             if (hop + chunk > gsx::GXF_MAX_HOPS)
                 return fail(e, GSX_ERANGE, "forwarding of recovered messages: more than " +
                                                std::to_string(gsx::GXF_MAX_HOPS) + " hops");
-            for (uint32_t k = 0; k < chunk; ++k) HIPCHK(e, gsx::launch_gxf_hop(ds, h, f, hop + k, e->stream));
+            for (uint32_t z = 0; z < chunk; ++z) HIPCHK(e, gsx::launch_gxf_hop(ds, R.h, R.f, hop + z, e->stream));
             hop += chunk;
             HIPCHK(e, hipMemcpyAsync(e->h_gxf_cnt, e->d_gxf_cnt + hop - 1, 4, hipMemcpyDeviceToHost, e->stream));
             HIPCHK(e, hipStreamSynchronize(e->stream));
             if (*e->h_gxf_cnt == 0) break;
         }
-        e->gxf_stamp = f.seq + hop + 1;
-        base += f.n_sets;
+        R.hops = hop;
+        if (int rc = gxf_run_end(e, R)) return rc;
     }
     return GSX_OK;
 }
 
-int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
-    e->state_changed();
-    gsx::HbState h = e->hb;
-    h.halo_resp = halo_resp;
-    const gsx::DevState ds = dev_state(e);
-    e->hb_active = false;
-    std::memset(out, 0, sizeof(*out));
-    if (h.pxno && e->sharded() && !e->pxs_packed[1])
-        return fail(e, GSX_ESTATE, "peer exchange on a shard: gsx_hb_px_pack(1) before gsx_hb_end");
-    if (!e->sharded()) HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
-    HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
-    e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
+// (D), first part: the advertised batches of hb_begin's windows (per topic,
+// cache order), their message sets and receipt rows, the set heads and the
+// flat word list; receipt rows zeroed, full bytes and common words (k_gx_setprep).
+int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
     const size_t hist = (size_t)std::max(e->gp.history_length, 1);
-    // (D) the gossip exchange over the batches the IHAVEs advertised (the
-    // windows of hb_begin's list), answered across the Shift below
-    std::vector<gsx_engine::MsgSet*> gx_sets;
-    std::vector<uint64_t*> gx_x;
-    std::vector<std::pair<uint64_t*, size_t>> gxf_scratch;  // the forwarding's frontier rows (released after the sync)
-    const bool gx_run = e->gp.gossip_exchange && h.ihave_bits && e->have_gossip;
-    dbg_host("hb (B)(C)");
-    if (gx_run) {
-        std::vector<gsx::GxBatch> gx;
-        std::vector<bool> gx_full_new;  // per set: its full bytes are recomputed this round
-        std::vector<uint32_t> off(e->T + 1, 0);
-        const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
-        const size_t N = e->n_nodes;
-        for (uint32_t t = 0; t < e->T; ++t) {
-            off[t] = (uint32_t)gx.size();
-            uint32_t row_off = 0;  // the batch's words in the topic's gossip rows (hb_begin's layout)
-            for (size_t w = 0; w < n_win; ++w)
-                for (auto& b : e->mc[w]) {
-                    if (b.topic != t) continue;
-                    const uint32_t ro = row_off;
-                    row_off += b.n_words;
-                    if (!b.set) continue;
-                    size_t i = 0;
-                    while (i < gx_sets.size() && gx_sets[i] != b.set) ++i;
-                    if (i == gx_sets.size()) {
-                        const size_t words = (size_t)b.set->n_words * N + 2 * N;  // rows + (dig, cnt) tail
-                        uint64_t* x = seen_acquire(e, words);  // (rows zeroed by k_gx_setprep)
-                        if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
-                        gsx_engine::MsgSet* ms = b.set;
-                        // which nodes have seen the whole set (skipped by the walk): k_gx_setprep
-                        gx_full_new.push_back(!ms->full_ok);
-                        if (!ms->full_ok) {
-                            if (!ms->d_full) {
-                                size_t got = 0;
-                                ms->d_full = small_acquire(e, N, &got);
-                                if (!ms->d_full) return fail(e, GSX_ENOMEM, "message set full bytes");
-                                ms->full_bytes = got;
-                            }
-                            ms->full_ok = true;
+    std::vector<gsx::GxBatch> gx;
+    std::vector<bool> gx_full_new;  // per set: its full bytes are recomputed this round
+    std::vector<uint32_t> off(e->T + 1, 0);
+    const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
+    const size_t N = e->n_nodes;
+    for (uint32_t t = 0; t < e->T; ++t) {
+        off[t] = (uint32_t)gx.size();
+        uint32_t row_off = 0;  // the batch's words in the topic's gossip rows (hb_begin's layout)
+        for (size_t w = 0; w < n_win; ++w)
+            for (auto& b : e->mc[w]) {
+                if (b.topic != t) continue;
+                const uint32_t ro = row_off;
+                row_off += b.n_words;
+                if (!b.set) continue;
+                size_t i = 0;
+                while (i < R.sets.size() && R.sets[i] != b.set) ++i;
+                if (i == R.sets.size()) {
+                    const size_t words = (size_t)b.set->n_words * N + 2 * N;  // rows + (dig, cnt) tail
+                    uint64_t* x = seen_acquire(e, words);  // (rows zeroed by k_gx_setprep)
+                    if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
+                    gsx_engine::MsgSet* ms = b.set;
+                    // which nodes have seen the whole set (skipped by the walk): k_gx_setprep
+                    gx_full_new.push_back(!ms->full_ok);
+                    if (!ms->full_ok) {
+                        if (!ms->d_full) {
+                            size_t got = 0;
+                            ms->d_full = small_acquire(e, N, &got);
+                            if (!ms->d_full) return fail(e, GSX_ENOMEM, "message set full bytes");
+                            ms->full_bytes = got;
                         }
-                        ++ms->refs;  // held until the recovered copies are cached (the Shift may drop its batches)
-                        gx_sets.push_back(b.set);
-                        gx_x.push_back(x);
+                        ms->full_ok = true;
                     }
-                    gx.push_back(gsx::GxBatch{b.d_seen, b.set->d_all, gx_x[i], b.set->d_val, nullptr, b.set->d_full,
-                                              b.n_words, b.set->serial, t,
-                                              (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
-                    gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
-                    gx.back().dense = b.recovered ? 0u : 1u;
-                    gx.back().src = b.set->d_src;
-                    gx.back().old_in = h.now - b.set->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
+                    ++ms->refs;  // held until the recovered copies are cached (the Shift may drop its batches)
+                    R.sets.push_back(b.set);
+                    R.xs.push_back(x);
                 }
-        }
-        off[e->T] = (uint32_t)gx.size();
-        {  // the flat word list of all advertised batches (k_gx_node's rounds)
-            uint32_t fw = 0;
-            for (size_t i = 0; i < gx.size(); ++i) {
-                gx[i].woff = fw;
-                fw += gx[i].n_words;
-                gx[i].n_msgs = gx_sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
+                gx.push_back(gsx::GxBatch{b.d_seen, b.set->d_all, R.xs[i], b.set->d_val, nullptr, b.set->d_full,
+                                          b.n_words, b.set->serial, t,
+                                          (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
+                gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
+                gx.back().dense = b.recovered ? 0u : 1u;
+                gx.back().src = b.set->d_src;
+                gx.back().old_in = R.h.now - b.set->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
             }
-        }
-        // per topic, the sets of its batches: each set's first batch in cache
-        // order and its words' offset (k_gx_node's receipts: a lane per set word
-        // walks the set's batches through `nxt`)
-        std::vector<uint32_t> hoff(e->T + 1, 0);
-        std::vector<uint2> heads;
-        {
-            std::vector<uint32_t> last(gx_sets.size(), ~0u);
-            for (uint32_t t = 0; t < e->T; ++t) {
-                hoff[t] = (uint32_t)heads.size();
-                uint32_t sw = 0;
-                for (uint32_t g = off[t]; g < off[t + 1]; ++g) {
-                    const size_t si = reinterpret_cast<size_t>(gx[g].got);
-                    gx[g].nxt = ~0u;
-                    if (last[si] == ~0u || gx[last[si]].topic != t) {
-                        heads.push_back(make_uint2(g, sw));
-                        sw += gx[g].n_words;
-                    } else {
-                        gx[last[si]].nxt = g;
-                    }
-                    last[si] = g;
-                }
-            }
-            hoff[e->T] = (uint32_t)heads.size();
-        }
-        dbg_host("gx sets");
-        static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
-        if (dbg) {
-            HIPCHK(e, hipStreamSynchronize(e->stream));
-            std::vector<uint8_t> fb(N);
-            fprintf(stderr, "[gx] not full per set:");
-            for (auto* ms : gx_sets) {
-                HIPCHK(e, hipMemcpy(fb.data(), ms->d_full, N, hipMemcpyDeviceToHost));
-                size_t nf = 0;
-                for (uint8_t x : fb) nf += x == 0;
-                fprintf(stderr, " s%u:%zu", ms->serial, nf);
-            }
-            fprintf(stderr, "\n[gx] sets=%zu batches=%zu:", gx_sets.size(), gx.size());
-            for (const auto& g : gx) fprintf(stderr, " (t%u w%u s%u a%u)", g.topic, g.n_words, g.serial, g.avail);
-            fprintf(stderr, "\n");
-        }
-        if (gx.size() > e->gx_cap || !e->d_gx) {
-            if (e->d_gx) (void)hipFree(e->d_gx);
-            if (e->d_gx_off) (void)hipFree(e->d_gx_off);
-            if (e->d_gx_got) (void)hipFree(e->d_gx_got);
-            e->d_gx = nullptr;
-            e->d_gx_off = nullptr;
-            e->d_gx_got = nullptr;
-            // (doubling, 64 at least: a free here waits for every queued kernel)
-            e->gx_cap = std::max<size_t>(std::max<size_t>(gx.size(), 2 * e->gx_cap), 64);
-            if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
-            if (int rc = dalloc(e, &e->d_gx_off, 2 * ((size_t)GSX_MAX_TOPICS + 1))) return rc;  // off, hoff
-            if (e->d_gx_heads) (void)hipFree(e->d_gx_heads);
-            e->d_gx_heads = nullptr;
-            if (int rc = dalloc(e, &e->d_gx_heads, e->gx_cap)) return rc;
-            if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
-        }
-        // per set, the messages every node had seen as the exchange began (a
-        // set wider than 64 words keeps none: its rows are filtered by emptiness)
-        if (gx_sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
-            if (e->d_gx_common) (void)hipFree(e->d_gx_common);
-            if (e->d_gx_sp) (void)hipFree(e->d_gx_sp);
-            if (e->d_gx_mg) (void)hipFree(e->d_gx_mg);
-            e->d_gx_common = nullptr;
-            e->d_gx_sp = nullptr;
-            e->d_gx_mg = nullptr;
-            e->gx_common_cap = std::max<size_t>(std::max<size_t>(gx_sets.size(), 2 * e->gx_common_cap), 32);
-            if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
-            if (int rc = dalloc(e, &e->d_gx_sp, e->gx_common_cap)) return rc;
-            if (int rc = dalloc(e, &e->d_gx_mg, e->gx_common_cap)) return rc;
-            if (!e->d_gx_rhm)
-                if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
-        }
-        std::vector<gsx::GxSetPrep> sprep(gx_sets.size());
-        for (size_t i = 0; i < gx_sets.size(); ++i) {
-            const gsx_engine::MsgSet* ms = gx_sets[i];
-            sprep[i] = gsx::GxSetPrep{ms->d_all, gx_x[i], gx_full_new[i] ? ms->d_full : nullptr,
-                                      ms->n_words <= 64 ? e->d_gx_common + 64 * i : nullptr, ms->n_words, ms->n_msgs};
-        }
-        std::vector<gsx::GxSetMerge> smerge(gx_sets.size());
-        for (size_t i = 0; i < gx_sets.size(); ++i) {
-            const gsx_engine::MsgSet* ms = gx_sets[i];
-            const size_t W = ms->n_words;
-            smerge[i] = gsx::GxSetMerge{ms->d_all, gx_x[i], ms->d_acc, ms->d_dg, gx_x[i] + W * N,
-                                        reinterpret_cast<uint32_t*>(gx_x[i] + W * N + N), ms->n_words, ms->n_msgs};
-        }
-        HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * gx_sets.size(), e->stream));
-        for (auto& g : gx) {
-            const size_t si = reinterpret_cast<size_t>(g.got);
-            g.common = gx_sets[si]->n_words <= 64 ? e->d_gx_common + 64 * si : nullptr;
-            g.got = e->d_gx_got + si;
-        }
-        HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
-        {  // the batch list, offsets and set heads through a pinned staging buffer:
-            // async copies, so the host keeps queueing instead of waiting for the
-            // kernels before them (the last round's copies drained at its end)
-            const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_hoff = 4 * hoff.size(),
-                         b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size(),
-                         b_mg = sizeof(gsx::GxSetMerge) * smerge.size();
-            const size_t a_sp = (b_gx + b_off + b_hoff + b_heads + 15) & ~(size_t)15;
-            const size_t a_mg = (a_sp + b_sp + 15) & ~(size_t)15;
-            const size_t need = a_mg + b_mg;
-            if (e->h_gxstage_bytes < need) {
-                if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
-                e->h_gxstage = nullptr;
-                e->h_gxstage_bytes = 0;
-                HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
-                e->h_gxstage_bytes = 2 * need;
-            }
-            char* hs = static_cast<char*>(e->h_gxstage);
-            std::memcpy(hs, gx.data(), b_gx);
-            std::memcpy(hs + b_gx, off.data(), b_off);
-            std::memcpy(hs + b_gx + b_off, hoff.data(), b_hoff);
-            if (b_heads) std::memcpy(hs + b_gx + b_off + b_hoff, heads.data(), b_heads);
-            HIPCHK(e, hipMemcpyAsync(e->d_gx, hs, b_gx, hipMemcpyHostToDevice, e->stream));
-            HIPCHK(e, hipMemcpyAsync(e->d_gx_off, hs + b_gx, b_off, hipMemcpyHostToDevice, e->stream));
-            HIPCHK(e, hipMemcpyAsync(e->d_gx_off + GSX_MAX_TOPICS + 1, hs + b_gx + b_off, b_hoff, hipMemcpyHostToDevice,
-                                     e->stream));
-            if (b_heads)
-                HIPCHK(e, hipMemcpyAsync(e->d_gx_heads, hs + b_gx + b_off + b_hoff, b_heads, hipMemcpyHostToDevice,
-                                         e->stream));
-            std::memcpy(hs + a_sp, sprep.data(), b_sp);
-            HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
-            std::memcpy(hs + a_mg, smerge.data(), b_mg);
-            HIPCHK(e, hipMemcpyAsync(e->d_gx_mg, hs + a_mg, b_mg, hipMemcpyHostToDevice, e->stream));
-            // receipt rows zeroed, full bytes, common words: every set in one pass
-            HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
-        }
-        h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
-        h.gx_heads = e->d_gx_heads;
-        h.gx = e->d_gx;
-        h.gx_off = e->d_gx_off;
-        HIPCHK(e, gsx::launch_gx_rhm(e->d_gx, (uint32_t)gx.size(), (uint32_t)N, e->d_gx_rhm, e->stream));
-        h.gx_rhm = e->d_gx_rhm;
-        h.gsubs = e->d_gsubs;
-        // the answered pairs' records take the receipts' credits: re-scored after
-        // (the rest stays exact), when the scores were exact before
-        const bool exact = e->scores_valid;
-        if (exact) {
-            h.gx_mark = e->d_dirty + 3 * e->E;  // (the broken-promise mask of hb_begin, read by then)
-            HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
-        }
-        dbg_host("gx prepared");
-        if (int rc = gxf_alloc(e)) return rc;
-        h.gxb_st0 = e->d_gxf_bst;
-        h.gxb_cnt0 = e->d_gxf_b0;
-        h.gxb_stamp = ++e->gxf_stamp;
-        HIPCHK(e, gsx::launch_gx_exchange(ds, h, e->stream));
-        if (dbg) {  // the listed nodes of k_gx_ask: count, heavy ones, their pairs
-            HIPCHK(e, hipStreamSynchronize(e->stream));
-            uint32_t fl[8];
-            HIPCHK(e, hipMemcpy(fl, e->d_gxflag, sizeof(fl), hipMemcpyDeviceToHost));
-            std::vector<uint32_t> ln(fl[6]);
-            if (!ln.empty())
-                HIPCHK(e, hipMemcpy(ln.data(), e->d_gx_nodes, 4 * ln.size(), hipMemcpyDeviceToHost));
-            size_t heavy = 0, pairs = 0, maxdeg = 0;
-            for (uint32_t x : ln) {
-                heavy += (x >> 31) & 1;
-                const uint32_t u = x & 0x7FFFFFFFu;
-                const size_t d = (size_t)(e->row_ptr[u + 1] - e->row_ptr[u]);
-                pairs += d;
-                maxdeg = std::max(maxdeg, d);
-            }
-            fprintf(stderr, "[gx] listed=%zu heavy=%zu pairs=%zu maxdeg=%zu\n", ln.size(), heavy, pairs, maxdeg);
-        }
-        // the recovered messages published on (their forwarded first receipts join the receipt rows)
-        if (int rc = gx_forward(e, h, ds, gx_sets, gx_x, h.now, gxf_scratch)) return rc;
-        // receipts merged into the sets, the recovered rows' summaries written (every set, one pass)
-        HIPCHK(e, gsx::launch_gx_merge_sets(e->d_gx_mg, (uint32_t)gx_sets.size(), (uint32_t)N, e->stream));
-        if (exact) {  // the receipts credited P2 / P3 / P4 of the answered pairs
-            HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.gx_mark));
-        } else {
-            e->invalidate_scores();
-        }
-        ++e->score_gen;
     }
+    off[e->T] = (uint32_t)gx.size();
+    {  // the flat word list of all advertised batches (k_gx_node's rounds)
+        uint32_t fw = 0;
+        for (size_t i = 0; i < gx.size(); ++i) {
+            gx[i].woff = fw;
+            fw += gx[i].n_words;
+            gx[i].n_msgs = R.sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
+        }
+    }
+    // per topic, the sets of its batches: each set's first batch in cache
+    // order and its words' offset (k_gx_node's receipts: a lane per set word
+    // walks the set's batches through `nxt`)
+    std::vector<uint32_t> hoff(e->T + 1, 0);
+    std::vector<uint2> heads;
+    {
+        std::vector<uint32_t> last(R.sets.size(), ~0u);
+        for (uint32_t t = 0; t < e->T; ++t) {
+            hoff[t] = (uint32_t)heads.size();
+            uint32_t sw = 0;
+            for (uint32_t g = off[t]; g < off[t + 1]; ++g) {
+                const size_t si = reinterpret_cast<size_t>(gx[g].got);
+                gx[g].nxt = ~0u;
+                if (last[si] == ~0u || gx[last[si]].topic != t) {
+                    heads.push_back(make_uint2(g, sw));
+                    sw += gx[g].n_words;
+                } else {
+                    gx[last[si]].nxt = g;
+                }
+                last[si] = g;
+            }
+        }
+        hoff[e->T] = (uint32_t)heads.size();
+    }
+    dbg_host("gx sets");
+    static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
+    if (dbg) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        std::vector<uint8_t> fb(N);
+        fprintf(stderr, "[gx] not full per set:");
+        for (auto* ms : R.sets) {
+            HIPCHK(e, hipMemcpy(fb.data(), ms->d_full, N, hipMemcpyDeviceToHost));
+            size_t nf = 0;
+            for (uint8_t x : fb) nf += x == 0;
+            fprintf(stderr, " s%u:%zu", ms->serial, nf);
+        }
+        fprintf(stderr, "\n[gx] sets=%zu batches=%zu:", R.sets.size(), gx.size());
+        for (const auto& g : gx) fprintf(stderr, " (t%u w%u s%u a%u)", g.topic, g.n_words, g.serial, g.avail);
+        fprintf(stderr, "\n");
+    }
+    if (gx.size() > e->gx_cap || !e->d_gx) {
+        if (e->d_gx) (void)hipFree(e->d_gx);
+        if (e->d_gx_off) (void)hipFree(e->d_gx_off);
+        if (e->d_gx_got) (void)hipFree(e->d_gx_got);
+        e->d_gx = nullptr;
+        e->d_gx_off = nullptr;
+        e->d_gx_got = nullptr;
+        // (doubling, 64 at least: a free here waits for every queued kernel)
+        e->gx_cap = std::max<size_t>(std::max<size_t>(gx.size(), 2 * e->gx_cap), 64);
+        if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
+        if (int rc = dalloc(e, &e->d_gx_off, 2 * ((size_t)GSX_MAX_TOPICS + 1))) return rc;  // off, hoff
+        if (e->d_gx_heads) (void)hipFree(e->d_gx_heads);
+        e->d_gx_heads = nullptr;
+        if (int rc = dalloc(e, &e->d_gx_heads, e->gx_cap)) return rc;
+        if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
+    }
+    // per set, the messages every node had seen as the exchange began (a
+    // set wider than 64 words keeps none: its rows are filtered by emptiness)
+    if (R.sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
+        if (e->d_gx_common) (void)hipFree(e->d_gx_common);
+        if (e->d_gx_sp) (void)hipFree(e->d_gx_sp);
+        if (e->d_gx_mg) (void)hipFree(e->d_gx_mg);
+        e->d_gx_common = nullptr;
+        e->d_gx_sp = nullptr;
+        e->d_gx_mg = nullptr;
+        e->gx_common_cap = std::max<size_t>(std::max<size_t>(R.sets.size(), 2 * e->gx_common_cap), 32);
+        if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
+        if (int rc = dalloc(e, &e->d_gx_sp, e->gx_common_cap)) return rc;
+        if (int rc = dalloc(e, &e->d_gx_mg, e->gx_common_cap)) return rc;
+        if (!e->d_gx_rhm)
+            if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
+    }
+    std::vector<gsx::GxSetPrep> sprep(R.sets.size());
+    for (size_t i = 0; i < R.sets.size(); ++i) {
+        const gsx_engine::MsgSet* ms = R.sets[i];
+        sprep[i] = gsx::GxSetPrep{ms->d_all, R.xs[i], gx_full_new[i] ? ms->d_full : nullptr,
+                                  ms->n_words <= 64 ? e->d_gx_common + 64 * i : nullptr, ms->n_words, ms->n_msgs};
+    }
+    std::vector<gsx::GxSetMerge> smerge(R.sets.size());
+    for (size_t i = 0; i < R.sets.size(); ++i) {
+        const gsx_engine::MsgSet* ms = R.sets[i];
+        const size_t W = ms->n_words;
+        smerge[i] = gsx::GxSetMerge{ms->d_all, R.xs[i], ms->d_acc, ms->d_dg, R.xs[i] + W * N,
+                                    reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs};
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
+    for (auto& g : gx) {
+        const size_t si = reinterpret_cast<size_t>(g.got);
+        g.common = R.sets[si]->n_words <= 64 ? e->d_gx_common + 64 * si : nullptr;
+        g.got = e->d_gx_got + si;
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
+    {  // the batch list, offsets and set heads through a pinned staging buffer:
+        // async copies, so the host keeps queueing instead of waiting for the
+        // kernels before them (the last round's copies drained at its end)
+        const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_hoff = 4 * hoff.size(),
+                     b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size(),
+                     b_mg = sizeof(gsx::GxSetMerge) * smerge.size();
+        const size_t a_sp = (b_gx + b_off + b_hoff + b_heads + 15) & ~(size_t)15;
+        const size_t a_mg = (a_sp + b_sp + 15) & ~(size_t)15;
+        const size_t need = a_mg + b_mg;
+        if (e->h_gxstage_bytes < need) {
+            if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+            e->h_gxstage = nullptr;
+            e->h_gxstage_bytes = 0;
+            HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
+            e->h_gxstage_bytes = 2 * need;
+        }
+        char* hs = static_cast<char*>(e->h_gxstage);
+        std::memcpy(hs, gx.data(), b_gx);
+        std::memcpy(hs + b_gx, off.data(), b_off);
+        std::memcpy(hs + b_gx + b_off, hoff.data(), b_hoff);
+        if (b_heads) std::memcpy(hs + b_gx + b_off + b_hoff, heads.data(), b_heads);
+        HIPCHK(e, hipMemcpyAsync(e->d_gx, hs, b_gx, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_gx_off, hs + b_gx, b_off, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->d_gx_off + GSX_MAX_TOPICS + 1, hs + b_gx + b_off, b_hoff, hipMemcpyHostToDevice,
+                                 e->stream));
+        if (b_heads)
+            HIPCHK(e, hipMemcpyAsync(e->d_gx_heads, hs + b_gx + b_off + b_hoff, b_heads, hipMemcpyHostToDevice,
+                                     e->stream));
+        std::memcpy(hs + a_sp, sprep.data(), b_sp);
+        HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
+        std::memcpy(hs + a_mg, smerge.data(), b_mg);
+        HIPCHK(e, hipMemcpyAsync(e->d_gx_mg, hs + a_mg, b_mg, hipMemcpyHostToDevice, e->stream));
+        // receipt rows zeroed, full bytes, common words: every set in one pass
+        HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
+    }
+    R.h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
+    R.h.gx_heads = e->d_gx_heads;
+    R.h.gx = e->d_gx;
+    R.h.gx_off = e->d_gx_off;
+    R.n_gx = (uint32_t)gx.size();
+    R.fw = gx.empty() ? 0u : gx.back().woff + gx.back().n_words;
+    return GSX_OK;
+}
+
+// (D), second part: the uncommon-row masks (k_gx_rhm, over the common words of
+// every rank on a shard), the answered-pair mask and the round's back-count stamp.
+int gx_ready(gsx_engine* e, gsx_engine::GxRound& R) {
+    gsx::HbState& h = R.h;
+    HIPCHK(e, gsx::launch_gx_rhm(e->d_gx, R.n_gx, (uint32_t)e->n_nodes, e->d_gx_rhm, e->stream));
+    h.gx_rhm = e->d_gx_rhm;
+    h.gsubs = e->d_gsubs;
+    // the answered pairs' records take the receipts' credits: re-scored after
+    // (the rest stays exact), when the scores were exact before
+    R.exact = e->scores_valid;
+    if (R.exact) {
+        h.gx_mark = e->d_dirty + 3 * e->E;  // (the broken-promise mask of hb_begin, read by then)
+        HIPCHK(e, hipMemsetAsync(h.gx_mark, 0, std::max<size_t>(e->E, 1), e->stream));
+    }
+    if (int rc = gxf_alloc(e)) return rc;
+    h.gxb_st0 = e->d_gxf_bst;
+    h.gxb_cnt0 = e->d_gxf_b0;
+    h.gxb_stamp = ++e->gxf_stamp;
+    dbg_host("gx prepared");
+    return GSX_OK;
+}
+
+// (D), last part: receipts merged into the sets, the recovered rows'
+// summaries written (every set, one pass); the credited pairs re-scored.
+int gx_merge(gsx_engine* e, gsx_engine::GxRound& R) {
+    HIPCHK(e, gsx::launch_gx_merge_sets(e->d_gx_mg, (uint32_t)R.sets.size(), (uint32_t)e->n_nodes, e->stream));
+    if (R.exact) {  // the receipts credited P2 / P3 / P4 of the answered pairs
+        HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), R.h.gx_mark));
+    } else {
+        e->invalidate_scores();
+    }
+    ++e->score_gen;
+    return GSX_OK;
+}
+
+// The round's end: counters, mcache.Shift, the recovered copies Put (one
+// batch per message set some node received in: got_all, every rank's on a
+// shard; null: this engine's), promise slots kept free.
+int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, const uint8_t* got_all) {
+    const gsx::HbState& h = R.h;
+    const bool gx_run = R.run;
+    const size_t hist = (size_t)std::max(e->gp.history_length, 1);
+    auto& gx_sets = R.sets;
+    auto& gx_x = R.xs;
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     uint32_t gflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> got(gx_sets.size(), 0);
     if (gx_run) {
         HIPCHK(e, hipMemcpyAsync(gflag, e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
-        if (!got.empty())
+        if (!got.empty() && !got_all)
             HIPCHK(e, hipMemcpyAsync(got.data(), e->d_gx_got, got.size(), hipMemcpyDeviceToHost, e->stream));
     }
     dbg_host("gx queued");
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    for (auto& fr : gxf_scratch) seen_release(e, fr.first, fr.second);
+    if (got_all) std::memcpy(got.data(), got_all, got.size());
+    for (auto& fr : R.scratch) seen_release(e, fr.first, fr.second);
+    R.scratch.clear();
+    R.pending = false;
+    R.stage = 0;
     dbg_host("hb drained");
     static_assert(sizeof(gsx_heartbeat_out) == sizeof(st), "gsx_heartbeat_out mirrors HB_STAT_WORDS");
     std::memcpy(out, st, sizeof(st));
@@ -3880,18 +4039,64 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     // the exchange cleared the bits and counters it read; a round without
     // gossip set none (the counters were cleared at its start)
     if (e->d_prom_e) e->gx_clean = gx_run || (e->gp.gossip_exchange && !e->have_gossip);
-    const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] > 0;
+    const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] +
+                                          st[gsx::HB_FWD_DELIVERED] > 0;
     for (auto* ms : gx_sets) {
-        if (merged) ms->full_ok = false;  // the receipts were merged into their seen rows
+        if (merged || e->sharded()) ms->full_ok = false;  // the receipts were merged into their seen rows
         set_release(e, ms);
     }
+    gx_sets.clear();
+    gx_x.clear();
     dbg_host("hb shift+put");
     if (gflag[0] || gflag[1])
         return fail(e, GSX_ESTATE, "gossip exchange: internal bound broken (truncated-list rows / promise slots)");
+    if (gflag[2])
+        return fail(e, GSX_ERANGE, "gossip exchange across range shards: an IHAVE list was truncated "
+                                   "(MaxIHaveLength) on a cross-shard pair, which the shard exchange does not carry");
     // every pair keeps a free promise slot for the next exchange (one promise per pair each)
     if (gx_run && gflag[4] >= e->prom_slots)
         if (int rc = gx_prom_grow(e)) return rc;
     return GSX_OK;
+}
+
+int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
+    e->state_changed();
+    gsx::HbState h = e->hb;
+    h.halo_resp = halo_resp;
+    const gsx::DevState ds = dev_state(e);
+    e->hb_active = false;
+    std::memset(out, 0, sizeof(*out));
+    if (h.pxno && e->sharded() && !e->pxs_packed[1])
+        return fail(e, GSX_ESTATE, "peer exchange on a shard: gsx_hb_px_pack(1) before gsx_hb_end");
+    if (!e->sharded()) HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
+    HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
+    e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
+    // (D) the gossip exchange over the batches the IHAVEs advertised (the
+    // windows of hb_begin's list), answered across the Shift
+    gsx_engine::GxRound& R = e->gxr;
+    R.run = e->gp.gossip_exchange && h.ihave_bits && e->have_gossip;
+    R.pending = false;
+    R.stage = 0;
+    R.sets.clear();
+    R.xs.clear();
+    R.scratch.clear();
+    R.h = h;
+    dbg_host("hb (B)(C)");
+    if (R.run) {
+        if (int rc = gx_prepare(e, R)) return rc;
+        if (e->sharded()) {  // the gsx_gx_* steps carry (D) across the ranks, gsx_gx_end finishes the round
+            R.pending = true;
+            R.stage = 1;
+            return GSX_OK;
+        }
+        if (int rc = gx_ready(e, R)) return rc;
+        HIPCHK(e, gsx::launch_gx_exchange(ds, R.h, e->stream));
+        // the recovered messages published on (their forwarded first receipts join the receipt rows)
+        if (int rc = gx_forward(e, R)) return rc;
+        if (int rc = gx_merge(e, R)) return rc;
+    }
+    return hb_finish(e, R, out, nullptr);
 }
 
 }  // namespace
@@ -4154,6 +4359,213 @@ int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out)
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_recv && !halo_resp) return GSX_EINVAL;
     return hb_end(e, halo_resp, out);
+}
+
+// ---- the gossip exchange across range shards (gsx.h: gsx_gx_*, gsx_gxf_*) ----------
+
+namespace {
+int gxs_step(gsx_engine* e, int stage) {
+    if (!e->gxr.pending) return fail(e, GSX_ESTATE, "no sharded gossip exchange in flight (gsx_hb_end prepares one)");
+    if (stage >= 0 && e->gxr.stage != stage) return fail(e, GSX_ESTATE, "gossip exchange steps out of order");
+    return GSX_OK;
+}
+gsx::GxsPlan gxs_plan(gsx_engine* e) {
+    return gsx::GxsPlan{e->d_send_pair, e->d_send_dest, e->d_send_base, e->d_dest_halo_base, e->d_pair_obs, e->n_send};
+}
+// A count pass, then the pack into the engine's send buffer in destination order.
+using GxsLaunch = std::function<hipError_t(unsigned long long*, const uint64_t*, uint64_t*)>;
+// out null: the count pass (counts[n_ranks] per destination, kept); else the
+// pack of those entries into out, destination by destination.
+int gxs_pack(gsx_engine* e, uint64_t* counts, uint64_t* out, const GxsLaunch& launch) {
+    const uint32_t R = std::max<uint32_t>(e->n_ranks, 1);
+    if (!out) {
+        HIPCHK(e, hipMemsetAsync(e->d_gxs_cnt, 0, 8 * (size_t)R, e->stream));
+        HIPCHK(e, launch(e->d_gxs_cnt, nullptr, nullptr));
+        e->gxs_counts.assign(R, 0);
+        HIPCHK(e, hipMemcpyAsync(e->gxs_counts.data(), e->d_gxs_cnt, 8 * (size_t)R, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (counts) std::memcpy(counts, e->gxs_counts.data(), 8 * (size_t)R);
+        return GSX_OK;
+    }
+    if (e->gxs_counts.size() != R) return fail(e, GSX_ESTATE, "the count pass (out null) first");
+    std::vector<uint64_t> off(R);
+    uint64_t tot = 0;
+    for (uint32_t d = 0; d < R; ++d) {
+        off[d] = tot;
+        tot += e->gxs_counts[d];
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_gxs_off, off.data(), 8 * (size_t)R, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_gxs_cnt, 0, 8 * (size_t)R, e->stream));
+    if (tot) HIPCHK(e, launch(e->d_gxs_cnt, e->d_gxs_off, out));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // `off` is on the host stack
+    e->gxs_counts.clear();
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_gx_pending(gsx_engine* e, uint32_t* n_sets) {
+    if (!e || !n_sets) return GSX_EINVAL;
+    *n_sets = e->gxr.pending ? (uint32_t)e->gxr.sets.size() : 0u;
+    return e->gxr.pending ? 1 : 0;
+}
+
+int gsx_gx_common(gsx_engine* e, uint64_t* common) {
+    if (!e || !common) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 1)) return rc;
+    const size_t n = 64 * e->gxr.sets.size();
+    if (n) HIPCHK(e, hipMemcpyAsync(common, e->d_gx_common, 8 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_gx_set_common(gsx_engine* e, const uint64_t* common) {
+    if (!e || !common) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 1)) return rc;
+    const size_t n = 64 * e->gxr.sets.size();
+    if (n) HIPCHK(e, hipMemcpy(e->d_gx_common, common, 8 * n, hipMemcpyHostToDevice));
+    if (int rc = gx_ready(e, e->gxr)) return rc;
+    e->gxr.stage = 2;
+    return GSX_OK;
+}
+
+int gsx_gx_pack_ihave(gsx_engine* e, uint64_t* send) {
+    if (!e || (e->n_send && !send)) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 2)) return rc;
+    HIPCHK(e, gsx::launch_gxs_pack_ihave(dev_state(e), e->gxr.h, gxs_plan(e), send, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_gx_recv_ihave(gsx_engine* e, const uint64_t* recv) {
+    if (!e || (e->n_recv && !recv)) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 2)) return rc;
+    HIPCHK(e, gsx::launch_gxs_recv_ihave(e->gxr.h, recv, e->d_halo_pair, e->n_recv, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->gxr.stage = 3;
+    return GSX_OK;
+}
+
+int gsx_gx_rows_words(gsx_engine* e, uint32_t* words) {
+    if (!e || !words) return GSX_EINVAL;
+    if (int rc = gxs_step(e, -1)) return rc;
+    *words = e->gxr.fw + 1;
+    return GSX_OK;
+}
+
+int gsx_gx_rows_pack(gsx_engine* e, uint64_t* counts, uint64_t* out) {
+    if (!e || (!counts && !out)) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 3)) return rc;
+    gsx::HbState h = e->gxr.h;
+    h.gxs_fw = e->gxr.fw;
+    const gsx::GxsPlan P = gxs_plan(e);
+    return gxs_pack(e, counts, out, [&](unsigned long long* c, const uint64_t* off, uint64_t* out) {
+        return gsx::launch_gxs_rows(h, P, e->d_gx, e->gxr.n_gx, c, off, out, e->stream);
+    });
+}
+
+int gsx_gx_rows_recv(gsx_engine* e, const uint64_t* entries, uint64_t n) {
+    if (!e || (n && !entries)) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 3)) return rc;
+    gsx::HbState& h = e->gxr.h;
+    h.gxs_rows = entries;
+    h.gxs_fw = e->gxr.fw;
+    HIPCHK(e, gsx::launch_gxs_rows_recv(h, entries, n, e->d_halo_pair, e->stream));
+    e->gxr.stage = 4;
+    return GSX_OK;
+}
+
+int gsx_gx_exchange(gsx_engine* e, uint32_t* n_runs) {
+    if (!e || !n_runs) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 4)) return rc;
+    HIPCHK(e, gsx::launch_gx_exchange(dev_state(e), e->gxr.h, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // (the received rows are read by then)
+    e->gxr.h.gxs_rows = nullptr;
+    if (int rc = gxf_plan(e, e->gxr)) return rc;
+    *n_runs = (uint32_t)e->gxr.runs.size();
+    e->gxr.stage = 5;
+    return GSX_OK;
+}
+
+int gsx_gxf_begin(gsx_engine* e, uint32_t run) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 5)) return rc;
+    if (e->gxr.fwd_active || run >= e->gxr.runs.size()) return fail(e, GSX_ESTATE, "no such forwarding run / one in flight");
+    return gxf_run_begin(e, e->gxr, run);
+}
+
+int gsx_gxf_entry_words(gsx_engine* e, uint32_t* words) {
+    if (!e || !words) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    *words = gsx::GXF_HDR + e->gxr.f.rw;
+    return GSX_OK;
+}
+
+int gsx_gxf_pack_fout(gsx_engine* e, uint64_t* send) {
+    if (!e || (e->n_send && !send)) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    HIPCHK(e, gsx::launch_gxf_pack_fout(e->gxr.f, gxs_plan(e), send, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_gxf_recv_fout(gsx_engine* e, const uint64_t* recv) {
+    if (!e || (e->n_recv && !recv)) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    HIPCHK(e, gsx::launch_gxf_recv_fout(e->gxr.f, recv, e->d_halo_pair, e->n_recv, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_gxf_pack(gsx_engine* e, uint32_t hop, uint64_t* counts, uint64_t* out) {
+    if (!e || (!counts && !out)) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    if (hop == 0 || hop >= gsx::GXF_MAX_HOPS) return fail(e, GSX_ERANGE, "hop out of range");
+    const gsx::GxsPlan P = gxs_plan(e);
+    const gsx::GxFwd f = e->gxr.f;
+    const gsx::HbState h = e->gxr.h;
+    return gxs_pack(e, counts, out, [&](unsigned long long* c, const uint64_t* off, uint64_t* out) {
+        return gsx::launch_gxf_halo(h, f, P, hop, c, off, out, e->stream);
+    });
+}
+
+int gsx_gxf_step(gsx_engine* e, uint32_t hop, const uint64_t* entries, uint64_t n, uint64_t* n_front) {
+    if (!e || (n && !entries) || !n_front) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    if (hop == 0 || hop >= gsx::GXF_MAX_HOPS) return fail(e, GSX_ERANGE, "hop out of range");
+    gsx::GxFwd& f = e->gxr.f;
+    f.hent = entries;
+    HIPCHK(e, gsx::launch_gxf_halo_recv(e->gxr.h, f, hop, entries, n, e->d_halo_pair, e->d_halo_node, e->stream));
+    HIPCHK(e, gsx::launch_gxf_hop(dev_state(e), e->gxr.h, f, hop, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->h_gxf_cnt, e->d_gxf_cnt + hop, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    f.hent = nullptr;
+    e->gxr.hops = std::max(e->gxr.hops, hop + 1);
+    *n_front = *e->h_gxf_cnt;
+    return GSX_OK;
+}
+
+int gsx_gxf_end(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    return gxf_run_end(e, e->gxr);
+}
+
+int gsx_gx_got(gsx_engine* e, uint8_t* got) {
+    if (!e || !got) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 5)) return rc;
+    if (e->gxr.fwd_active) return fail(e, GSX_ESTATE, "a forwarding run is in flight");
+    if (!e->gxr.sets.empty())
+        HIPCHK(e, hipMemcpyAsync(got, e->d_gx_got, e->gxr.sets.size(), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
+}
+
+int gsx_gx_end(gsx_engine* e, const uint8_t* got_all, gsx_heartbeat_out* out) {
+    if (!e || !out || (!got_all && !e->gxr.sets.empty())) return GSX_EINVAL;
+    if (int rc = gxs_step(e, 5)) return rc;
+    if (e->gxr.fwd_active) return fail(e, GSX_ESTATE, "a forwarding run is in flight");
+    if (int rc = gx_merge(e, e->gxr)) return rc;
+    return hb_finish(e, e->gxr, out, got_all);
 }
 
 // ---- topic membership API (gsx.h) ------------------------------------------------

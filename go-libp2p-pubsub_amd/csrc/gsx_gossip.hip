@@ -32,6 +32,28 @@ __device__ __forceinline__ void gx_flush(unsigned long long* stats, int k, uint6
     if ((threadIdx.x % 64) == 0 && c) atomicAdd(&stats[k], (unsigned long long)c);
 }
 
+// Word w of the sender's cache row of batch b, the sender being v, the peer
+// of the receiver's pair q: a local sender's row; on a range shard a remote
+// one's from the rows its rank sent (gxs_rows), none when it sent none (every
+// message v holds is common: nothing to ask).  v is a global node id.
+__device__ __forceinline__ uint64_t gx_mem(const HbState& h, const GxBatch& b, uint64_t q, uint32_t v, uint32_t w) {
+    if (h.gxs_hidx && (h.rev[q] & HALO)) {
+        const uint32_t k = h.gxs_hidx[q];
+        return k == NO_PAIR ? 0ull : h.gxs_rows[(size_t)k * (h.gxs_fw + 1) + 1 + b.woff + w];
+    }
+    return b.mem[(size_t)(v - h.node_lo) * b.n_words + w];
+}
+// The advertised batches whose row at the sender holds an uncommon message (gx_rhm).
+__device__ __forceinline__ uint64_t gx_rhm_of(const HbState& h, uint64_t q, uint32_t v) {
+    if (h.gxs_hidx && (h.rev[q] & HALO)) return h.gxs_hidx[q] == NO_PAIR ? 0ull : ~0ull;
+    return h.gx_rhm[v - h.node_lo];
+}
+// handleIWant's gate at the peer v of q (r its pair to u): v's score of u.
+__device__ __forceinline__ bool gx_answers(const DevState& s, const HbState& h, uint64_t q, uint32_t r) {
+    if (r & HALO) return h.gxs_rans && h.gxs_rans[q];
+    return !(s.score[r] < h.gossip_threshold);
+}
+
 // Streams the ids v advertised to u (pair q = (u -> v), r its reverse) on
 // the topics of `tb` that u had not seen: f(batch index, message index) for
 // each, in canonical order; returns false when f asks to stop.  A truncated
@@ -53,7 +75,7 @@ __device__ __forceinline__ bool gx_walk(const HbState& h, uint64_t tb, uint32_t 
             if (b.full[u]) continue;
             const uint32_t W = b.n_words;
             for (uint32_t w = 0; w < W; ++w) {
-                uint64_t m = b.mem[(size_t)v * W + w] & ~b.all[(size_t)u * W + w];
+                uint64_t m = gx_mem(h, b, q, v, w) & ~b.all[(size_t)u * W + w];
                 if (sub) m &= sub[b.row_off + w];
                 for (; m; m &= m - 1)
                     if (!f(g, w * 64 + (uint32_t)__builtin_ctzll(m))) return false;
@@ -143,13 +165,14 @@ __global__ __launch_bounds__(256) void k_gx_prom_grow(const uint64_t* __restrict
 // had not seen, within the subset row of a truncated list.
 // u's own row first: v's cache word is read only where u lacks a message
 // (mem has no bit past n_msgs, so this is mem & ~all exactly).
-__device__ __forceinline__ uint64_t gx_word(const GxBatch& b, uint32_t u, uint32_t v, uint32_t w, const uint64_t* sub) {
+__device__ __forceinline__ uint64_t gx_word(const HbState& h, const GxBatch& b, uint32_t u, uint64_t q, uint32_t v,
+                                            uint32_t w, const uint64_t* sub) {
     const uint32_t W = b.n_words;
     const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
     const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
     const uint64_t miss = ~b.all[(size_t)u * W + w] & valid;
     if (!miss) return 0;
-    uint64_t m = b.mem[(size_t)v * W + w] & miss;
+    uint64_t m = gx_mem(h, b, q, v, w) & miss;
     if (sub) m &= sub[b.row_off + w];
     return m;
 }
@@ -181,7 +204,7 @@ __device__ __forceinline__ uint32_t gx_count(const HbState& h, uint64_t tb, uint
         for (uint32_t g = h.gx_off[t]; g < h.gx_off[t + 1]; ++g) {
             if (gx_skip(nf, g)) continue;
             const GxBatch& b = h.gx[g];
-            for (uint32_t w = 0; w < b.n_words; ++w) n += (uint32_t)__popcll(gx_word(b, u, v, w, sub));
+            for (uint32_t w = 0; w < b.n_words; ++w) n += (uint32_t)__popcll(gx_word(h, b, u, q, v, w, sub));
         }
     }
     return n;
@@ -198,7 +221,7 @@ __device__ __forceinline__ void gx_nth(const HbState& h, uint64_t tb, uint32_t u
             if (gx_skip(nf, g)) continue;
             const GxBatch& b = h.gx[g];
             for (uint32_t w = 0; w < b.n_words; ++w) {
-                uint64_t m = gx_word(b, u, v, w, sub);
+                uint64_t m = gx_word(h, b, u, q, v, w, sub);
                 const uint32_t c = (uint32_t)__popcll(m);
                 if (j >= c) {
                     j -= c;
@@ -308,7 +331,7 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
 // 0 = nobody to answer (v untracked or on another shard), 1 = ignored (v's
 // score below GossipThreshold, MaxIHaveMessages, MaxIHaveLength asked), 2 = handled.
 __device__ __forceinline__ int gx_gate(const DevState& s, const HbState& h, uint64_t q, uint32_t r) {
-    if (r == NO_PAIR || (r & HALO)) return 0;
+    if (r == NO_PAIR || ((r & HALO) && !h.gxs_hidx)) return 0;
     if (s.score[q] < h.gossip_threshold) return 1;  // :617-621
     const uint32_t ph = h.peerhave[q] + 1;          // :624-628 (one RPC per pair per heartbeat)
     if ((int64_t)ph > (int64_t)h.gp.max_ihave_msgs) return 1;
@@ -358,8 +381,8 @@ __device__ __forceinline__ bool gx_at(const HbState& h, const GxRange& R, uint32
 }
 
 // |iwant| of pair q (every lane gets it): popcounts of the candidate words.
-__device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t tr,
-                                              uint32_t r, uint64_t nf, uint32_t lane) {
+__device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uint32_t u, uint64_t q, uint32_t v,
+                                              uint64_t tr, uint32_t r, uint64_t nf, uint32_t lane) {
     uint32_t c = 0;
     for (; tb; tb &= tb - 1) {
         const uint32_t t = (uint32_t)__builtin_ctzll(tb);
@@ -367,15 +390,15 @@ __device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uin
         const uint64_t* sub = gx_subrow(h, tr, t, r);
         uint32_t g = R.g0, w = 0;
         for (uint32_t f = R.base + lane; f < R.f1; f += 64)
-            if (gx_at(h, R, f, g, w) && !gx_skip(nf, g)) c += (uint32_t)__popcll(gx_word(h.gx[g], u, v, w, sub));
+            if (gx_at(h, R, f, g, w) && !gx_skip(nf, g)) c += (uint32_t)__popcll(gx_word(h, h.gx[g], u, q, v, w, sub));
     }
     return gx_wsum(c);
 }
 
 // The j-th candidate of pair q in canonical order (every lane gets it).
-__device__ __forceinline__ void gx_wnth(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t tr,
-                                        uint32_t r, uint64_t nf, uint32_t lane, uint32_t j, uint32_t& pick_g,
-                                        uint32_t& pick_k) {
+__device__ __forceinline__ void gx_wnth(const HbState& h, uint64_t tb, uint32_t u, uint64_t q, uint32_t v,
+                                        uint64_t tr, uint32_t r, uint64_t nf, uint32_t lane, uint32_t j,
+                                        uint32_t& pick_g, uint32_t& pick_k) {
     for (; tb; tb &= tb - 1) {
         const uint32_t t = (uint32_t)__builtin_ctzll(tb);
         const GxRange R = gx_range(h, t);
@@ -383,7 +406,7 @@ __device__ __forceinline__ void gx_wnth(const HbState& h, uint64_t tb, uint32_t 
         uint32_t g = R.g0, w = 0;
         for (uint32_t f0 = R.base; f0 < R.f1; f0 += 64) {  // (uniform rounds)
             uint64_t m = 0;
-            if (gx_at(h, R, f0 + lane, g, w) && !gx_skip(nf, g)) m = gx_word(h.gx[g], u, v, w, sub);
+            if (gx_at(h, R, f0 + lane, g, w) && !gx_skip(nf, g)) m = gx_word(h, h.gx[g], u, q, v, w, sub);
             const uint32_t c = (uint32_t)__popcll(m);
             const uint32_t e = gx_excl(c, lane);
             const uint32_t tot = (uint32_t)__shfl((int)(e + c), 63, 64);
@@ -548,7 +571,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             const uint32_t v = (uint32_t)h.col[q];
             // the unseen batches whose row at v holds a message not every node had:
             // only there can v hold one u lacks
-            const uint64_t cb = nf & h.gx_rhm[v];
+            const uint64_t cb = nf & gx_rhm_of(h, (uint64_t)q, v);
             if (!cb) continue;  // |iwant| = 0 (:652-654)
             const uint64_t tr = h.ihave_tr[q];
             // |iwant|: v's cache words where u lacks something (topics of the RPC,
@@ -559,7 +582,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                 if (!((cb >> g) & 1)) continue;
                 const GxBatch& b = h.gx[g];
                 if (!((tb >> b.topic) & 1)) continue;
-                uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)uu * b.n_words + w];
+                uint64_t c = gx_mem(h, b, (uint64_t)q, v, w) & ~b.all[(size_t)uu * b.n_words + w];
                 const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
                 if (sub) c &= sub[b.row_off + w];
                 n += (uint32_t)__popcll(c);
@@ -576,7 +599,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                     if (!((cb >> gi) & 1)) continue;
                     const GxBatch& b = h.gx[gi];
                     if (!((tb >> b.topic) & 1)) continue;
-                    uint64_t c = b.mem[(size_t)v * b.n_words + w] & ~b.all[(size_t)uu * b.n_words + w];
+                    uint64_t c = gx_mem(h, b, (uint64_t)q, v, w) & ~b.all[(size_t)uu * b.n_words + w];
                     const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
                     if (sub) c &= sub[b.row_off + w];
                     const uint32_t pc = (uint32_t)__popcll(c);
@@ -652,14 +675,14 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
                 const uint32_t v = (uint32_t)h.col[q];
                 const uint64_t tr = h.ihave_tr[q];
-                const uint32_t n = gx_wcount(h, tb, u, v, tr, r, nf, lane);
+                const uint32_t n = gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
                 if (n == 0) continue;
                 const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)h.iasked[q]);
                 const uint32_t kk = n < budget ? n : budget;
                 uint32_t pick_g = 0, pick_k = 0;
                 if (kk == n) {
                     Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
-                    gx_wnth(h, tb, u, v, tr, r, nf, lane, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
+                    gx_wnth(h, tb, u, (uint64_t)q, v, tr, r, nf, lane, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
                 } else if (lane == 0) {
                     gx_pick_sampled(h, tb, u, v, q, r, n, kk, pick_g, pick_k);
                 }
@@ -681,13 +704,13 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
             const uint32_t kk = (uint32_t)__shfl((int)kq, jb, 64);
             const uint64_t tall = h.ihave_bits[q];
             const uint32_t r = h.rev[q];
-            const bool answered = !(s.score[r] < h.gossip_threshold) &&  // v ignores u's IWANT
+            const bool answered = gx_answers(s, h, (uint64_t)q, r) &&  // v ignores u's IWANT
                                   ((h.eflags[q] & EDGE_DIRECT) || !(s.score[q] < h.graylist));  // AcceptFrom at u
             const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
             if (answered) {
                 const uint32_t v = (uint32_t)h.col[q];
                 const uint64_t tr = h.ihave_tr[q];
-                const uint32_t n = gx_wcount(h, tb, u, v, tr, r, nf, lane);
+                const uint32_t n = gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
                 if (kk == n) {
                     for (uint64_t tm = tb; tm; tm &= tm - 1) {
                         const uint32_t t = (uint32_t)__builtin_ctzll(tm);
@@ -710,7 +733,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                             const uint32_t W = b.n_words;
                             bool got = false;
                             {
-                                const uint64_t m = gx_word(b, u, v, w, sub);
+                                const uint64_t m = gx_word(h, b, u, (uint64_t)q, v, w, sub);
                                 if (!m) continue;
                                 uint64_t* xw = b.x + (size_t)u * W + w;
                                 const uint64_t x0 = *xw;
@@ -926,7 +949,7 @@ __device__ __forceinline__ uint64_t gxf_origin(const GxFwdSet& S, uint32_t x, ui
 // Hop 0: every node's accepted receipts of the round per set (its frontier
 // rows), the frontier list; and each set's origins into srcm (a thread per
 // (set, message) in the grid's second half).
-__global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t n_src_total) {
+__global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t n_src_total, uint32_t node_lo) {
     for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u) {
         uint64_t m = 0;
         for (uint32_t si = 0; si < f.n_sets; ++si) {
@@ -949,7 +972,7 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_src_total; i += gridDim.x * 256u) {
         uint32_t si = 0, base = 0;
         while (base + f.sets[si].n_msgs <= i) base += f.sets[si++].n_msgs;
-        const uint32_t x = (uint32_t)(f.sets[si].src[i - base] >> 32);
+        const uint32_t x = (uint32_t)(f.sets[si].src[i - base] >> 32) - node_lo;  // (origins are global ids)
         if (x < n) atomicOr(reinterpret_cast<unsigned long long*>(&f.srcm[x]), 1ull << si);
     }
 }
@@ -1002,16 +1025,37 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
             if (!fo) continue;
             const uint64_t ok = M & gxf_slot_sets(f, fo);
             if (!ok) continue;
-            const uint32_t w = (uint32_t)h.col[r];
+            if (h.rev[r] & HALO) continue;  // a remote receiver: its rank marks it from this rank's entries
+            const uint32_t w = (uint32_t)h.col[r] - h.node_lo;
             const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[w]), ok);
             if (old == 0) f.rlist[atomicAdd(&f.rcnt[hop], 1u)] = w;
         }
     }
 }
 
+// The copies v would send back to x (pair r = (v -> x), topic slot ts): the
+// first receipts v took from x at the hop before; hop 1: the IWANT answers x
+// served v, old at x (inside the window by their set's old_in); later hops:
+// copies x got in this round.  (back: all of them, back_w: those inside x's
+// P3 window.)
+__device__ __forceinline__ void gxf_back(const HbState& h, const GxFwd& f, uint32_t hop, uint64_t r, uint32_t ts,
+                                         uint32_t& back, uint32_t& back_w) {
+    back = back_w = 0;
+    const uint32_t p = (hop - 1) & 1;
+    if (hop == 1) {
+        if (f.bst0 && f.bst0[r] == f.stamp0) {
+            const uint32_t b2 = f.bcnt0[(size_t)f.slot_topic[ts] * h.n_pairs + r];
+            back_w = b2 & 0xFFFFu;
+            back = back_w + (b2 >> 16);
+        }
+    } else if (f.bst[p][r] == f.seq + hop - 1) {
+        back = back_w = f.bcnt[p][(size_t)r * GXF_SLOTS + ts];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1, pw = hop & 1;
-    const uint32_t seq_prev = f.seq + hop - 1, seq_cur = f.seq + hop;
+    const uint32_t seq_cur = f.seq + hop;
     const uint32_t S_ = h.prom_slots;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
     const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
@@ -1031,25 +1075,32 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
         // then the senders that send are pulled in ascending order
         constexpr int GXF_PB = 8;
         for (int64_t q0 = r0; q0 < r1; q0 += GXF_PB) {
-          uint32_t fis[GXF_PB], vs[GXF_PB];
+          uint32_t fis[GXF_PB], vs[GXF_PB], rs[GXF_PB];
           uint64_t fms[GXF_PB];
 #pragma unroll
           for (int j = 0; j < GXF_PB; ++j) {
               fis[j] = q0 + j < r1 ? (uint32_t)f.fin[q0 + j] : 0u;
-              vs[j] = (fis[j] & 0xFFu) ? (uint32_t)h.col[q0 + j] : 0u;
+              rs[j] = (fis[j] & 0xFFu) ? h.rev[q0 + j] : NO_PAIR;
+              vs[j] = (fis[j] & 0xFFu) ? (uint32_t)h.col[q0 + j] - h.node_lo : 0u;  // (local index; unused if remote)
+          }
+#pragma unroll
+          for (int j = 0; j < GXF_PB; ++j) {
+              if (!(fis[j] & 0xFFu)) fms[j] = 0;
+              else if (rs[j] & HALO) fms[j] = f.hstamp && f.hstamp[q0 + j] == seq_cur;  // a remote sender's entry this hop
+              else fms[j] = (f.fbit[p][vs[j] >> 6] >> (vs[j] & 63)) & 1;
           }
 #pragma unroll
           for (int j = 0; j < GXF_PB; ++j)
-              fms[j] = ((fis[j] & 0xFFu) && ((f.fbit[p][vs[j] >> 6] >> (vs[j] & 63)) & 1)) ? 1ull : 0ull;
-#pragma unroll
-          for (int j = 0; j < GXF_PB; ++j)
-              if (fms[j]) fms[j] = f.fmask[p][vs[j]] & M & gxf_slot_sets(f, fis[j] & 0xFFu);
+              if (fms[j])
+                  fms[j] = ((rs[j] & HALO) ? f.hent[(size_t)f.hidx[q0 + j] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vs[j]]) &
+                           M & gxf_slot_sets(f, fis[j] & 0xFFu);
           for (int j = 0; j < GXF_PB; ++j) {
             const uint64_t fv = fms[j];
             if (!fv) continue;  // v forwards none of the run's topics to x, or sends nothing new this hop
             const int64_t q = q0 + j;
             const uint32_t fi = fis[j], v = vs[j];
-            const uint32_t r = h.rev[q];
+            const uint32_t r = rs[j];
+            const uint64_t* hdr = (r & HALO) ? f.hent + (size_t)f.hidx[q] * (GXF_HDR + f.rw) : nullptr;
             const bool gray = (fi & GXF_GRAY) != 0;  // AcceptFrom at x
             for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
                 const uint64_t sm = fv & f.slot_sets[ts];
@@ -1060,14 +1111,14 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                     const uint32_t si = (uint32_t)__builtin_ctzll(mm);
                     const GxFwdSet& S = f.sets[si];
                     const uint32_t W = S.n_words;
-                    const uint64_t* F = S.fr[p] + (size_t)v * W;
+                    const uint64_t* F = hdr ? hdr + GXF_HDR + S.woff : S.fr[p] + (size_t)v * W;
                     uint64_t* X = S.x + (size_t)x * W;
                     const uint64_t* A = S.all + (size_t)x * W;
                     uint64_t* NF = S.fr[pw] + (size_t)x * W;
                     const bool isrc = (srcm >> si) & 1;
                     for (uint32_t w = 0; w < W; ++w) {
                         uint64_t snd = F[w];
-                        if (isrc && snd) snd &= ~gxf_origin(S, x, w);  // not back to the origin (:1006-1009)
+                        if (isrc && snd) snd &= ~gxf_origin(S, x + h.node_lo, w);  // not back to the origin (:1006-1009)
                         if (!snd) continue;
                         if (gray) {
                             g += (uint32_t)__popcll(snd);
@@ -1093,14 +1144,11 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                 // (hop 1: the copies v served x from its cache, old at x: inside the
                 // window by their set's old_in; later hops: x got them in this round)
                 uint32_t back = 0, back_w = 0;
-                if (hop == 1) {
-                    if (f.bst0 && f.bst0[r] == f.stamp0) {
-                        const uint32_t b2 = f.bcnt0[(size_t)t * h.n_pairs + r];
-                        back_w = b2 & 0xFFFFu;
-                        back = back_w + (b2 >> 16);
-                    }
-                } else if (f.bst[p][r] == seq_prev) {
-                    back = back_w = f.bcnt[p][(size_t)r * GXF_SLOTS + ts];
+                if (hdr) {  // counted by the sender's rank (k_gxf_halo)
+                    back = (uint32_t)(hdr[2 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
+                    back_w = (uint32_t)(hdr[4 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
+                } else {
+                    gxf_back(h, f, hop, r, ts, back, back_w);
                 }
                 if (gray) {
                     g -= back;
@@ -1126,6 +1174,10 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
           }
         }
         if (!newsets) continue;
+        for (uint64_t mm = newsets; mm; mm &= mm - 1) {  // (read first: one writer in a thousand stores)
+            uint8_t* g = f.sets[__builtin_ctzll(mm)].got;
+            if (!*g) *g = 1;
+        }
         f.fmask[pw][x] = newsets;
         f.flist[pw][atomicAdd(&f.fcnt[hop], 1u)] = x;
         atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
@@ -1149,6 +1201,139 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
     unsigned long long v[3] = {c_new, c_dup, c_gray};
     const uint32_t slot[3] = {HB_FWD_DELIVERED, HB_FWD_DUPLICATES, HB_FWD_GRAYLISTED};
     block_count<3>(v, h.stats, slot);
+}
+
+// ---- the exchange across range shards (gsx_gx_*; gsx.h) -------------------------
+//
+// Everything (D) computes belongs to the receiver of an IHAVE (its counters,
+// promises, records, receipts and cache), so a cross-shard pair needs from the
+// sender's rank only: the topics of the IHAVE and whether the sender answers
+// IWANTs (its score of the receiver), and the sender's cache rows of the
+// advertised batches when they hold an uncommon message (gx_rhm over the
+// common words of every rank).  The forwarding needs per cross-shard pair the
+// sender's topic slots (fout) once per run, and per hop the sender's frontier
+// rows with its back-send counts: all fixed-size entries routed by the shard
+// plan's receive slots.
+
+
+__global__ __launch_bounds__(256) void k_gxs_pack_ihave(DevState s, HbState h, GxsPlan P, uint64_t* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < P.n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = P.send_pair[j];
+        uint64_t w0 = 0, w1 = 0;
+        if (r != NO_PAIR) {
+            w0 = h.gxs_out[r];
+            w1 = !(s.score[r] < h.gossip_threshold);  // handleIWant's gate at the sender (:683-688)
+        }
+        out[2 * j] = w0;
+        out[2 * j + 1] = w1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gxs_recv_ihave(HbState h, const uint64_t* in, const uint32_t* halo_pair,
+                                                        uint64_t n_recv) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n_recv; k += (uint64_t)gridDim.x * 256u) {
+        const uint32_t q = halo_pair[k];
+        h.ihave_bits[q] = in[2 * k];
+        h.gxs_rans[q] = (uint8_t)(in[2 * k + 1] & 1);
+        h.gxs_hidx[q] = NO_PAIR;
+    }
+}
+
+// out null: count the entries per destination; else pack them at off[dest].
+__global__ __launch_bounds__(256) void k_gxs_rows(HbState h, GxsPlan P, const GxBatch* __restrict__ gx, uint32_t n_gx,
+                                                  unsigned long long* cnt, const uint64_t* off, uint64_t* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < P.n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = P.send_pair[j];
+        if (r == NO_PAIR || !h.gxs_out[r]) continue;
+        const uint32_t v = P.pair_obs[r];
+        if (!h.gx_rhm[v]) continue;  // only common messages in v's rows: nothing to ask
+        const uint32_t d = P.send_dest[j];
+        const unsigned long long k = atomicAdd(&cnt[d], 1ull);
+        if (!out) continue;
+        uint64_t* e = out + (size_t)(off[d] + k) * (h.gxs_fw + 1);
+        e[0] = P.dest_halo_base[d] + (j - P.send_base[d]);  // the receive slot at the destination
+        for (uint32_t g = 0; g < n_gx; ++g) {
+            const GxBatch& b = gx[g];
+            for (uint32_t w = 0; w < b.n_words; ++w) e[1 + b.woff + w] = b.mem[(size_t)v * b.n_words + w];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gxs_rows_recv(HbState h, const uint64_t* in, uint64_t n,
+                                                       const uint32_t* halo_pair) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256u)
+        h.gxs_hidx[halo_pair[in[k * (h.gxs_fw + 1)]]] = (uint32_t)k;
+}
+
+__global__ __launch_bounds__(256) void k_gxf_pack_fout(GxFwd f, GxsPlan P, uint64_t* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < P.n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = P.send_pair[j];
+        out[j] = r == NO_PAIR ? 0ull : f.fout[r];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gxf_recv_fout(GxFwd f, const uint64_t* in, const uint32_t* halo_pair,
+                                                       uint64_t n_recv) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n_recv; k += (uint64_t)gridDim.x * 256u)
+        f.fin[halo_pair[k]] |= (uint16_t)(in[k] & 0xFFu);
+}
+
+// A hop's frontier entries of this rank's senders to remote receivers (out
+// null: counted per destination).
+__global__ __launch_bounds__(256) void k_gxf_halo(HbState h, GxFwd f, GxsPlan P, uint32_t hop,
+                                                  unsigned long long* cnt, const uint64_t* off, uint64_t* out) {
+    const uint32_t p = (hop - 1) & 1;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < P.n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = P.send_pair[j];
+        if (r == NO_PAIR) continue;
+        const uint32_t fo = f.fout[r];
+        if (!fo) continue;
+        const uint32_t v = P.pair_obs[r];
+        if (!((f.fbit[p][v >> 6] >> (v & 63)) & 1)) continue;
+        const uint64_t M = f.fmask[p][v] & gxf_slot_sets(f, fo);
+        if (!M) continue;
+        const uint32_t d = P.send_dest[j];
+        const unsigned long long k = atomicAdd(&cnt[d], 1ull);
+        if (!out) continue;
+        uint64_t* e = out + (size_t)(off[d] + k) * (GXF_HDR + f.rw);
+        e[0] = P.dest_halo_base[d] + (j - P.send_base[d]);
+        e[1] = M;
+        uint64_t b01[2] = {0, 0}, w01[2] = {0, 0};
+        for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
+            uint32_t back, back_w;
+            gxf_back(h, f, hop, r, ts, back, back_w);
+            b01[ts / 4] |= (uint64_t)back << (16 * (ts % 4));
+            w01[ts / 4] |= (uint64_t)back_w << (16 * (ts % 4));
+        }
+        e[2] = b01[0];
+        e[3] = b01[1];
+        e[4] = w01[0];
+        e[5] = w01[1];
+        for (uint32_t si = 0; si < f.n_sets; ++si) {
+            const GxFwdSet& S = f.sets[si];
+            const bool in = (M >> si) & 1;
+            for (uint32_t w = 0; w < S.n_words; ++w)
+                e[GXF_HDR + S.woff + w] = in ? S.fr[p][(size_t)v * S.n_words + w] : 0ull;
+        }
+    }
+}
+
+// The entries other ranks sent for this hop: per receive slot the entry, and
+// its receiver marked (sparse hops; a dense hop pulls at every node).
+__global__ __launch_bounds__(256) void k_gxf_halo_recv(HbState h, GxFwd f, uint32_t hop, const uint64_t* in,
+                                                       uint64_t n, const uint32_t* halo_pair,
+                                                       const uint32_t* halo_node) {
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256u) {
+        const uint64_t* e = in + (size_t)k * (GXF_HDR + f.rw);
+        const uint64_t slot = e[0];
+        const uint32_t q = halo_pair[slot], x = halo_node[slot];
+        f.hstamp[q] = f.seq + hop;
+        f.hidx[q] = (uint32_t)k;
+        if (dense) continue;
+        const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[x]), e[1]);
+        if (old == 0) f.rlist[atomicAdd(&f.rcnt[hop], 1u)] = x;
+    }
 }
 
 static inline unsigned gx_blocks(uint64_t n, unsigned bs, unsigned cap) {
@@ -1192,7 +1377,8 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
                            hipStream_t st) {
     const uint64_t n = std::max<uint64_t>(h.n_nodes, n_src_total);
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, f, h.n_nodes, n_src_total);
+    hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, f, h.n_nodes, n_src_total,
+                       h.node_lo);
     hipLaunchKernelGGL(k_gxf_fout, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f);
     hipLaunchKernelGGL(k_gxf_fin, dim3(gx_blocks(h.n_pairs, 256, 8192)), dim3(256), 0, st, s, h, f);
     return hipGetLastError();
@@ -1203,6 +1389,55 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
     hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
     hipLaunchKernelGGL(k_gxf_pull, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
+    return hipGetLastError();
+}
+
+static inline unsigned gx_grid(uint64_t n) { return gx_blocks(n ? n : 1, 256, 4096); }
+
+hipError_t launch_gxs_pack_ihave(const DevState& s, const HbState& h, const GxsPlan& P, uint64_t* out, hipStream_t st) {
+    if (P.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxs_pack_ihave, dim3(gx_grid(P.n_send)), dim3(256), 0, st, s, h, P, out);
+    return hipGetLastError();
+}
+hipError_t launch_gxs_recv_ihave(const HbState& h, const uint64_t* in, const uint32_t* halo_pair, uint64_t n_recv,
+                                 hipStream_t st) {
+    if (n_recv == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxs_recv_ihave, dim3(gx_grid(n_recv)), dim3(256), 0, st, h, in, halo_pair, n_recv);
+    return hipGetLastError();
+}
+hipError_t launch_gxs_rows(const HbState& h, const GxsPlan& P, const GxBatch* gx, uint32_t n_gx,
+                           unsigned long long* cnt, const uint64_t* off, uint64_t* out, hipStream_t st) {
+    if (P.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxs_rows, dim3(gx_grid(P.n_send)), dim3(256), 0, st, h, P, gx, n_gx, cnt, off, out);
+    return hipGetLastError();
+}
+hipError_t launch_gxs_rows_recv(const HbState& h, const uint64_t* in, uint64_t n, const uint32_t* halo_pair,
+                                hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxs_rows_recv, dim3(gx_grid(n)), dim3(256), 0, st, h, in, n, halo_pair);
+    return hipGetLastError();
+}
+hipError_t launch_gxf_pack_fout(const GxFwd& f, const GxsPlan& P, uint64_t* out, hipStream_t st) {
+    if (P.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxf_pack_fout, dim3(gx_grid(P.n_send)), dim3(256), 0, st, f, P, out);
+    return hipGetLastError();
+}
+hipError_t launch_gxf_recv_fout(const GxFwd& f, const uint64_t* in, const uint32_t* halo_pair, uint64_t n_recv,
+                                hipStream_t st) {
+    if (n_recv == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxf_recv_fout, dim3(gx_grid(n_recv)), dim3(256), 0, st, f, in, halo_pair, n_recv);
+    return hipGetLastError();
+}
+hipError_t launch_gxf_halo(const HbState& h, const GxFwd& f, const GxsPlan& P, uint32_t hop, unsigned long long* cnt,
+                           const uint64_t* off, uint64_t* out, hipStream_t st) {
+    if (P.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxf_halo, dim3(gx_grid(P.n_send)), dim3(256), 0, st, h, f, P, hop, cnt, off, out);
+    return hipGetLastError();
+}
+hipError_t launch_gxf_halo_recv(const HbState& h, const GxFwd& f, uint32_t hop, const uint64_t* in, uint64_t n,
+                                const uint32_t* halo_pair, const uint32_t* halo_node, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gxf_halo_recv, dim3(gx_grid(n)), dim3(256), 0, st, h, f, hop, in, n, halo_pair, halo_node);
     return hipGetLastError();
 }
 

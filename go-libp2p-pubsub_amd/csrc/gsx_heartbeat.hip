@@ -71,6 +71,19 @@ __device__ __forceinline__ bool backoff_present(const HbState& h, uint64_t r, ui
 
 // clearBackoff, gossipsub.go:1585-1604: a lane per (pair, 8-topic chunk)
 // presence byte; only the set bits' entries are read.
+// Marks the IHAVE of topic t that the owner of pair r sends its peer: at the
+// receiver's pair (the exchange (D) reads it there), or, when the peer lives
+// on another range shard, at r for the shard exchange (gsx_gx_pack_ihave).
+__device__ __forceinline__ void ihave_mark(const HbState& h, uint64_t r, uint32_t t) {
+    const uint32_t q = h.rev[r];
+    if (!h.ihave_bits || q == NO_PAIR) return;
+    if (q & HALO) {
+        if (h.gxs_out) h.gxs_out[r] |= 1ull << t;
+        return;
+    }
+    h.ihave_bits[q] |= 1ull << t;
+}
+
 __global__ __launch_bounds__(256) void k_hb_clear_backoff(HbState h, uint32_t n_topics) {
     uint64_t cleared = 0;
     const uint32_t n_chunks = (n_topics + 7) / 8;
@@ -1017,8 +1030,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                             const size_t x = tslot + rs[lane] + peers[q];
                             h.ihave_len[x] = L;
                             h.ihave_hash[x] = dig;
-                            if (h.ihave_bits && h.rev[rs[lane] + peers[q]] != NO_PAIR)  // (D) reads it, receiver-side
-                                h.ihave_bits[h.rev[rs[lane] + peers[q]]] |= 1ull << t;
+                            ihave_mark(h, (uint64_t)(rs[lane] + peers[q]), t);  // (D) reads it
                         }
                         cnt[0] += (uint64_t)target;
                         cnt[1] += (uint64_t)target * L;
@@ -1171,7 +1183,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 const int64_t r = r0 + peers[p];
                 h.ihave_len[tslot + r] = L;
                 h.ihave_hash[tslot + r] = dall;
-                if (h.ihave_bits && h.rev[r] != NO_PAIR) h.ihave_bits[h.rev[r]] |= 1ull << t;  // (D) reads it
+                ihave_mark(h, (uint64_t)r, t);  // (D) reads it
             }
             msgs += (uint64_t)target;
             ids += (uint64_t)target * L;
@@ -1202,11 +1214,15 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 for (uint32_t w = lane; w < tw; w += 64)
                     for (uint64_t m = sel[w]; m; m &= m - 1) d += h.mc_digest[slot0 + w * 64 + (uint32_t)__builtin_ctzll(m)];
                 d = wave_sum64(d);
-                const uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
+                uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
                 if (lane == 0) {
                     h.ihave_len[tslot + r] = maxl;
                     h.ihave_hash[tslot + r] = take ? d : dall - d;
-                    if (q != NO_PAIR) h.ihave_bits[q] |= 1ull << t;
+                    ihave_mark(h, (uint64_t)r, t);
+                }
+                if (q != NO_PAIR && (q & HALO)) {  // a truncated list across shards: refused (gsx.h)
+                    if (lane == 0) h.gx_err[2] = 1;
+                    q = NO_PAIR;
                 }
                 if (q != NO_PAIR && h.gsub.pool) {  // the subset the receiver's handleIHave reads (D)
                     uint32_t x = 0;

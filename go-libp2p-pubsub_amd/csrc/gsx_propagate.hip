@@ -1300,6 +1300,23 @@ __device__ __forceinline__ void fold_rescore_1(const PropState& ps, const DevSta
         }
         if (ps.late && local) backsends += k1;
     }
+    if (ps.stale) {  // lazy: credits only (no P4) of pairs at or above every threshold fold without a re-score
+        bool lz[DU];
+#pragma unroll
+        for (int i = 0; i < DU; ++i) lz[i] = doit[i] && k4a[i] == 0 && s.score[q0 + i * stride] >= ps.lazy_thr;
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            if (!lz[i]) continue;
+            const uint64_t q = q0 + i * stride;
+            doit[i] = false;
+            ps.stale[q] = 1;
+            if (!(fa[i] | da[i])) continue;
+            const size_t b = rec_index(q, t, 1, FMD);
+            const uint8_t fl = s.rflags[flag_index(q, t, 1)];
+            s.rec[b + FMD * TILE] = add_ones_capped(s.rec[b + FMD * TILE], fa[i], s.tp[t].cap2);
+            if (fl & REC_IN_MESH) s.rec[b + MMD * TILE] = add_ones_capped(s.rec[b + MMD * TILE], fa[i] + da[i], s.tp[t].cap3);
+        }
+    }
     for (int h0 = 0; h0 < DU; h0 += FH) {  // (halves: fewer live registers per batch)
     uint8_t fl[FH];
     double fmd[FH], mmd[FH], mfp[FH], imd[FH], app[FH], bp[FH];
@@ -1444,7 +1461,10 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
                     if ((ps.drop || ps.pending) && (k4 = ps.invcnt[q])) ps.invcnt[q] = 0;
                     if ((first | dup | k4) && fold_topic && (s.pflags[q] & PAIR_PRESENT)) {
                         fold_pair(ps, s, q, first, dup, k4);
-                        if (RESCORE) {
+                        if (RESCORE && ps.stale && k4 == 0 && s.score[q] >= ps.lazy_thr) {  // lazy (PropState::stale)
+                            ps.stale[q] = 1;
+                            if (ps.tterm) ps.tgen[q] = 0;  // (its cached term of this topic is stale too)
+                        } else if (RESCORE) {
                             s.score[q] = ps.tterm ? eval_pair_cached(ps, s, pp, q) : eval_pair(s, pp, q);
                             const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
                             if (nb != ob) {

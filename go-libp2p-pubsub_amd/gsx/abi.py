@@ -392,6 +392,24 @@ SIGNATURES = {
     "gsx_scores": (C.c_int, [C.c_void_p, P(C.c_double), C.c_size_t]),
     "gsx_score": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_double)]),
     "gsx_score_many": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t, P(C.c_double)]),
+    "gsx_gx_pending": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_gx_common": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "gsx_gx_set_common": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "gsx_gx_pack_ihave": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_gx_recv_ihave": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_gx_rows_words": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_gx_rows_pack": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_void_p]),
+    "gsx_gx_rows_recv": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "gsx_gx_exchange": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_gxf_begin": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_gxf_entry_words": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_gxf_pack_fout": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_gxf_recv_fout": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_gxf_pack": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint64), C.c_void_p]),
+    "gsx_gxf_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "gsx_gxf_end": (C.c_int, [C.c_void_p]),
+    "gsx_gx_got": (C.c_int, [C.c_void_p, P(C.c_uint8)]),
+    "gsx_gx_end": (C.c_int, [C.c_void_p, P(C.c_uint8), P(HeartbeatOut)]),
     "gsx_device_scores": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "gsx_sync": (C.c_int, [C.c_void_p]),
     "gsx_import_state": (C.c_int, [C.c_void_p, P(StateView)]),

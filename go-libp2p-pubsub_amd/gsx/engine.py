@@ -398,6 +398,89 @@ class Engine:
         self._chk(self.lib.gsx_hb_end(self.h, self._p(halo_resp), C.byref(out)), "gsx_hb_end")
         return out
 
+    # ---- the gossip exchange across range shards (gsx_gx_*, gsx_gxf_*) ----
+    def gx_pending(self):
+        """-> the message sets of the sharded exchange in flight, or None."""
+        n = C.c_uint32()
+        rc = self.lib.gsx_gx_pending(self.h, C.byref(n))
+        return int(n.value) if rc == 1 else None
+
+    def gx_common(self, n_sets: int) -> np.ndarray:
+        c = np.empty(64 * n_sets, dtype=np.uint64)
+        self._chk(self.lib.gsx_gx_common(self.h, _ptr(c, C.c_uint64)), "gsx_gx_common")
+        return c
+
+    def gx_set_common(self, c: np.ndarray):
+        c = np.ascontiguousarray(c, dtype=np.uint64)
+        self._chk(self.lib.gsx_gx_set_common(self.h, _ptr(c, C.c_uint64)), "gsx_gx_set_common")
+
+    def gx_pack_ihave(self, send):
+        self._chk(self.lib.gsx_gx_pack_ihave(self.h, self._p(send)), "gsx_gx_pack_ihave")
+
+    def gx_recv_ihave(self, recv):
+        self._chk(self.lib.gsx_gx_recv_ihave(self.h, self._p(recv)), "gsx_gx_recv_ihave")
+
+    def gx_rows_words(self) -> int:
+        w = C.c_uint32()
+        self._chk(self.lib.gsx_gx_rows_words(self.h, C.byref(w)), "gsx_gx_rows_words")
+        return int(w.value)
+
+    def gx_rows_pack(self, n_ranks: int, out=None) -> np.ndarray:
+        """out None: the count pass -> entries per destination; else the pack."""
+        cnt = np.zeros(n_ranks, dtype=np.uint64)
+        self._chk(self.lib.gsx_gx_rows_pack(self.h, _ptr(cnt, C.c_uint64), self._p(out) if out is not None else None),
+                  "gsx_gx_rows_pack")
+        return cnt
+
+    def gx_rows_recv(self, entries, n: int):
+        self._chk(self.lib.gsx_gx_rows_recv(self.h, self._p(entries), n), "gsx_gx_rows_recv")
+
+    def gx_exchange(self) -> int:
+        n = C.c_uint32()
+        self._chk(self.lib.gsx_gx_exchange(self.h, C.byref(n)), "gsx_gx_exchange")
+        return int(n.value)
+
+    def gxf_begin(self, run: int):
+        self._chk(self.lib.gsx_gxf_begin(self.h, run), "gsx_gxf_begin")
+
+    def gxf_entry_words(self) -> int:
+        w = C.c_uint32()
+        self._chk(self.lib.gsx_gxf_entry_words(self.h, C.byref(w)), "gsx_gxf_entry_words")
+        return int(w.value)
+
+    def gxf_pack_fout(self, send):
+        self._chk(self.lib.gsx_gxf_pack_fout(self.h, self._p(send)), "gsx_gxf_pack_fout")
+
+    def gxf_recv_fout(self, recv):
+        self._chk(self.lib.gsx_gxf_recv_fout(self.h, self._p(recv)), "gsx_gxf_recv_fout")
+
+    def gxf_pack(self, hop: int, n_ranks: int, out=None) -> np.ndarray:
+        cnt = np.zeros(n_ranks, dtype=np.uint64)
+        self._chk(self.lib.gsx_gxf_pack(self.h, hop, _ptr(cnt, C.c_uint64), self._p(out) if out is not None else None),
+                  "gsx_gxf_pack")
+        return cnt
+
+    def gxf_step(self, hop: int, entries, n: int) -> int:
+        f = C.c_uint64()
+        self._chk(self.lib.gsx_gxf_step(self.h, hop, self._p(entries), n, C.byref(f)), "gsx_gxf_step")
+        return int(f.value)
+
+    def gxf_end(self):
+        self._chk(self.lib.gsx_gxf_end(self.h), "gsx_gxf_end")
+
+    def gx_got(self, n_sets: int) -> np.ndarray:
+        g = np.zeros(max(n_sets, 1), dtype=np.uint8)
+        self._chk(self.lib.gsx_gx_got(self.h, _ptr(g, C.c_uint8)), "gsx_gx_got")
+        return g[:n_sets]
+
+    def gx_end(self, got_all) -> abi.HeartbeatOut:
+        out = abi.HeartbeatOut()
+        g = np.ascontiguousarray(got_all, dtype=np.uint8)
+        if len(g) == 0:
+            g = np.zeros(1, dtype=np.uint8)
+        self._chk(self.lib.gsx_gx_end(self.h, _ptr(g, C.c_uint8), C.byref(out)), "gsx_gx_end")
+        return out
+
     def export_backoff(self) -> np.ndarray:
         b = np.empty((self.n_topics, self.n_pairs), dtype=np.int64)
         self._chk(self.lib.gsx_export_backoff(self.h, _ptr(b, C.c_int64)), "gsx_export_backoff")

@@ -273,12 +273,83 @@ class RangeSharded:
         be.hb_pack_resp(s1)
         tp.all_to_all(r1[: self.n_recv], s1[: self.n_send], self.recv_counts, self.send_counts)
         out = be.hb_end(r1)
+        n_sets = be.gx_pending() if hasattr(be, "gx_pending") else None
+        if n_sets is not None:  # the gossip exchange (D) across the ranks
+            out = self._gx_exchange(n_sets)
         d = out.as_dict()
         t = torch.tensor([d[k] for k, _ in abi.HeartbeatOut._fields_], dtype=torch.int64, device=dev)
         tp.all_reduce_sum(t)
         t = t.cpu().numpy()
         return d, {k: int(t[i]) for i, (k, _) in enumerate(abi.HeartbeatOut._fields_)}
 
+
+    def _entries(self, counts, words, pack):
+        """Variable entry all-to-all: counts[k] entries of `words` u64 for rank
+        k (pack(out) writes them, destination by destination) -> (the received
+        entries, their number)."""
+        torch = _torch()
+        tp = self.tp
+        sc = torch.tensor(counts.astype(np.int64), dtype=torch.int64, device=tp.device)
+        rc = torch.empty(tp.world, dtype=torch.int64, device=tp.device)
+        tp.all_to_all(rc, sc, [1] * tp.world, [1] * tp.world)
+        rcnt = rc.cpu().numpy()
+        n_out, n_in = int(counts.sum()), int(rcnt.sum())
+        send = torch.zeros((max(n_out, 1), words), dtype=torch.int64, device=tp.device)
+        pack(send)
+        recv = torch.zeros((max(n_in, 1), words), dtype=torch.int64, device=tp.device)
+        tp.all_to_all(recv[:n_in], send[:n_out], rcnt, counts.astype(np.int64))
+        return recv, n_in
+
+    def _gx_exchange(self, n_sets: int):
+        """The gossip exchange of a sharded heartbeat (gsx.h, gsx_gx_*): the
+        common words ANDed over ranks, the IHAVE bits and answer bits of the
+        cross-shard pairs (fixed words per pair), the senders' cache rows
+        (entries), the exchange at the receivers, then the forwarding of the
+        recovered messages hop by hop (frontier entries, a frontier count
+        summed over ranks per hop), and the round's end with every rank's
+        got flags.  -> this rank's counters."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        dev = tp.device
+        W = tp.world
+        c = be.gx_common(n_sets)
+        if n_sets:  # (the set count is the same on every rank: the cache is global)
+            parts = tp.all_gather(torch.tensor(c.view(np.int64), dtype=torch.int64, device=dev))
+            c = np.bitwise_and.reduce(np.stack([p.cpu().numpy().view(np.uint64) for p in parts]), axis=0)
+        be.gx_set_common(c)
+        s2 = torch.zeros((max(self.n_send, 1), 2), dtype=torch.int64, device=dev)
+        r2 = torch.zeros((max(self.n_recv, 1), 2), dtype=torch.int64, device=dev)
+        be.gx_pack_ihave(s2)
+        tp.all_to_all(r2[: self.n_recv], s2[: self.n_send], self.recv_counts, self.send_counts)
+        be.gx_recv_ihave(r2)
+        rows, n_rows = self._entries(be.gx_rows_pack(W), be.gx_rows_words(), lambda out: be.gx_rows_pack(W, out))
+        be.gx_rows_recv(rows, n_rows)
+        n_runs = be.gx_exchange()
+        del rows
+        for run in range(n_runs):
+            be.gxf_begin(run)
+            s1 = torch.zeros(max(self.n_send, 1), dtype=torch.int64, device=dev)
+            r1 = torch.zeros(max(self.n_recv, 1), dtype=torch.int64, device=dev)
+            be.gxf_pack_fout(s1)
+            tp.all_to_all(r1[: self.n_recv], s1[: self.n_send], self.recv_counts, self.send_counts)
+            be.gxf_recv_fout(r1)
+            words = be.gxf_entry_words()
+            hop = 1
+            while True:
+                ent, n_ent = self._entries(be.gxf_pack(hop, W), words, lambda out, h=hop: be.gxf_pack(h, W, out))
+                front = be.gxf_step(hop, ent, n_ent)
+                t = torch.tensor([front], dtype=torch.int64, device=dev)
+                tp.all_reduce_sum(t)
+                if int(t.item()) == 0:
+                    break
+                hop += 1
+            be.gxf_end()
+        got = be.gx_got(n_sets)
+        if n_sets:
+            g = torch.tensor(got.astype(np.int64), dtype=torch.int64, device=dev)
+            tp.all_reduce_max(g)
+            got = g.cpu().numpy().astype(np.uint8)
+        return be.gx_end(got)
 
     def _px_exchange(self, kind: int):
         """Peer exchange across shards (gsx_hb_px_*): the PX lists of this rank's

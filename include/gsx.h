@@ -531,7 +531,7 @@ int gsx_set_stream(gsx_engine* e, void* stream);
  *   received rows) until a hop delivers nothing on any rank, gsx_prop_end.
  * Words per call: 1 for m <= 64, 2 for m <= 128, else ceil(m/64) rounded up
  * to a multiple of 4.  Per-rank results equal the single-engine run's rows
- * of those nodes bit for bit.  Heartbeats are not supported on a shard. */
+ * of those nodes bit for bit. */
 int gsx_load_overlay_shard(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_local,
                            const int64_t* row_ptr, const int32_t* col, const uint8_t* edge_flags,
                            const uint32_t* node_ips);
@@ -589,7 +589,8 @@ typedef struct gsx_gossipsub_params {
     int32_t max_ihave_messages;             /* :57                               */
     int32_t gossip_retransmission;          /* :42                               */
     int64_t iwant_followup_ns;              /* :58                               */
-    int32_t gossip_exchange;                /* 1: run step (D) below; 0: IHAVEs are only emitted */
+    int32_t gossip_exchange;                /* 1 (default): run step (D) below (handleIHave /
+                                               handleIWant, :615-720); 0: IHAVEs are only emitted */
     int32_t reserved0;
     int64_t fanout_ttl_ns;                  /* :45 (GossipSubFanoutTTL)          */
     int32_t do_px;                          /* WithPeerExchange (:325-333); default 0 */
@@ -742,6 +743,55 @@ int gsx_hb_pack_ctl(gsx_engine* e, uint64_t* send);
 int gsx_hb_recv(gsx_engine* e, const uint64_t* halo_ctl);
 int gsx_hb_pack_resp(gsx_engine* e, uint64_t* send);
 int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out);
+/* The gossip exchange (D) on a range shard (gossip_exchange on): gsx_hb_end
+ * runs (C) and prepares (D); these steps carry it across the ranks and
+ * gsx_gx_end ends the round (its counters then; gsx_hb_end's *out is zero).
+ * Everything (D) computes belongs to the receiver of an IHAVE (its counters,
+ * promises, records, receipts and cache), so a cross-shard pair needs from
+ * the sender's rank only the IHAVE's topics, whether the sender answers
+ * IWANTs (its score of the receiver), and its cache rows of the advertised
+ * batches when they hold a message some node lacks; the forwarding of
+ * recovered messages needs the senders' topic slots and, per hop, their
+ * frontier rows and back-send counts.  All travel as entries routed by the
+ * shard plan's receive slots.  An IHAVE list truncated to MaxIHaveLength on
+ * a cross-shard pair is refused (GSX_ERANGE at gsx_gx_end).
+ *   gsx_gx_pending      1 when one is in flight (*n_sets: its message sets), else 0
+ *   gsx_gx_common       this rank's common words, [n_sets][64] u64 (host): the
+ *                       messages every node of the rank had seen
+ *   gsx_gx_set_common   their AND over every rank (the caller's all-gather)
+ *   gsx_gx_pack_ihave   per send slot: IHAVE topic bits, answer bit ([n_send][2], device)
+ *   gsx_gx_recv_ihave   the received [n_recv][2] words
+ *   gsx_gx_rows_words   the sender-row entry width (1 + the advertised batches' words)
+ *   gsx_gx_rows_pack    this rank's sender-row entries: with out null the
+ *                       count pass (counts[n_ranks]), then the pack into out
+ *                       (device, destination by destination; the same for gsx_gxf_pack)
+ *   gsx_gx_rows_recv    the received entries (read until gsx_gx_exchange returns)
+ *   gsx_gx_exchange     handleIHave / handleIWant and the receipts; *n_runs:
+ *                       forwarding runs (each: begin, pack_fout / recv_fout,
+ *                       then per hop h = 1, 2, ...: pack, the all-to-all, step,
+ *                       until a hop leaves no frontier on any rank; end)
+ *   gsx_gxf_step        hop h with the received entries; *n_front: this rank's new frontier
+ *   gsx_gx_got          per message set: a node of this rank delivered one of its messages
+ *   gsx_gx_end          with their OR over every rank: the merge, the Shift, the
+ *                       recovered copies Put (the same batches on every rank) */
+int gsx_gx_pending(gsx_engine* e, uint32_t* n_sets);
+int gsx_gx_common(gsx_engine* e, uint64_t* common);
+int gsx_gx_set_common(gsx_engine* e, const uint64_t* common);
+int gsx_gx_pack_ihave(gsx_engine* e, uint64_t* send);
+int gsx_gx_recv_ihave(gsx_engine* e, const uint64_t* recv);
+int gsx_gx_rows_words(gsx_engine* e, uint32_t* words);
+int gsx_gx_rows_pack(gsx_engine* e, uint64_t* counts, uint64_t* out);
+int gsx_gx_rows_recv(gsx_engine* e, const uint64_t* entries, uint64_t n);
+int gsx_gx_exchange(gsx_engine* e, uint32_t* n_runs);
+int gsx_gxf_begin(gsx_engine* e, uint32_t run);
+int gsx_gxf_entry_words(gsx_engine* e, uint32_t* words);
+int gsx_gxf_pack_fout(gsx_engine* e, uint64_t* send);
+int gsx_gxf_recv_fout(gsx_engine* e, const uint64_t* recv);
+int gsx_gxf_pack(gsx_engine* e, uint32_t hop, uint64_t* counts, uint64_t* out);
+int gsx_gxf_step(gsx_engine* e, uint32_t hop, const uint64_t* entries, uint64_t n, uint64_t* n_front);
+int gsx_gxf_end(gsx_engine* e);
+int gsx_gx_got(gsx_engine* e, uint8_t* got);
+int gsx_gx_end(gsx_engine* e, const uint8_t* got_all, gsx_heartbeat_out* out);
 /* backoff expiry per [topic][pair] (0 = no entry), n_topics * n_pairs
  * (gs.backoff, gossipsub.go:436; zeroed by gsx_load_overlay) */
 int gsx_export_backoff(gsx_engine* e, int64_t* out);

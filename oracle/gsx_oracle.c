@@ -1515,7 +1515,7 @@ int orc_default_gossipsub_params(gsx_gossipsub_params* p) { /* DefaultGossipSubP
     p->max_ihave_messages = 10;
     p->gossip_retransmission = 3;
     p->iwant_followup_ns = 3LL * 1000000000LL;
-    p->gossip_exchange = 0;
+    p->gossip_exchange = 1; /* handleIHave / handleIWant always run in the reference (gossipsub.go:615-720) */
     p->fanout_ttl_ns = 60LL * 1000000000LL;
     p->do_px = 0;
     p->prune_peers = 16; /* GossipSubPrunePeers, :46 */

@@ -83,6 +83,7 @@ class EmuShard:
     # -- plan ---------------------------------------------------------------------
     def shard_recv_plan(self, rank_lo):
         rank_lo = np.asarray(rank_lo, dtype=np.int64)
+        self.rank_lo = rank_lo
         world = len(rank_lo) - 1
         owner = np.searchsorted(rank_lo, self.col, side="right") - 1
         remote = (self.col < self.lo) | (self.col >= self.lo + self.n)
@@ -154,6 +155,163 @@ class EmuShard:
             self.hb_checked += 1
         out = abi.HeartbeatOut()
         out.mesh_links = self.hb_checked
+        return out
+
+    # -- the sharded gossip exchange (gsx_gx_*, gsx_gxf_*): plumbing only ---------------
+    # With gx_sets set, hb_end leaves an exchange of that many message sets
+    # pending.  Every stand-in word names its pair (or the rank), every
+    # receive side checks it got exactly what its senders packed: the common
+    # words (rank k clears bit k of word 0, so the AND clears bits 0..world-1),
+    # IHAVE/answer words per cross pair, variable row entries for the send
+    # slots with (7v + u) % 3 == 0, per-run fout words, and per-hop frontier
+    # entries for the slots with (v + u + hop + run) even; run k forwards for
+    # exactly 2 + k hops (the frontier count is 0 from then on), the got flags
+    # of rank k mark set k % n_sets.
+    gx_sets = None
+    gx_runs = 2
+
+    def _rank(self):
+        return int(np.searchsorted(self.rank_lo, self.lo, side="right") - 1)
+
+    def gx_pending(self):
+        return self.gx_sets
+
+    def gx_common(self, n_sets):
+        assert n_sets == self.gx_sets
+        c = np.full(64 * n_sets, M64, dtype=np.uint64)
+        if n_sets:
+            c[0] = np.uint64(M64 & ~(1 << self._rank()))
+        return c
+
+    def gx_set_common(self, c):
+        world = len(self.rank_lo) - 1
+        assert len(c) == 64 * self.gx_sets
+        if self.gx_sets:
+            assert int(c[0]) == M64 & ~((1 << world) - 1) and all(int(x) == M64 for x in c[1:])
+        self.hb_checked += 1
+
+    def _send_ids(self):
+        for j, r in enumerate(self.send_pair):
+            if r is not None:
+                v, u = self._pair_ids(r)
+                yield j, v, u
+
+    def gx_pack_ihave(self, send):
+        a = np.zeros((len(self.send_pair), 2), dtype=np.uint64)
+        for j, v, u in self._send_ids():
+            a[j] = ((v << 32 | u) ^ 0x1111, u << 32 | v)
+        send[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+
+    def gx_recv_ihave(self, recv):
+        h = recv.numpy().view(np.uint64)
+        for q, slot in self._halo_pairs():
+            u, v = self._pair_ids(q)
+            assert int(h[slot, 0]) == (v << 32 | u) ^ 0x1111 and int(h[slot, 1]) == (u << 32 | v), (q, slot)
+            self.hb_checked += 1
+
+    def _entries(self, keep, words, out):
+        cnt = np.zeros(len(self.send_counts), dtype=np.uint64)
+        rows = []
+        for d in range(len(self.send_counts)):
+            for j in range(int(self.send_base[d]), int(self.send_base[d + 1])):
+                r = self.send_pair[j]
+                if r is None:
+                    continue
+                v, u = self._pair_ids(r)
+                if keep(v, u):
+                    rows.append([int(self.halo_base[d] + j - self.send_base[d])] + words(v, u))
+                    cnt[d] += 1
+        if out is not None and rows:
+            out[: len(rows)].copy_(_as_tensor(np.array(rows, dtype=np.uint64).view(np.int64)))
+        return cnt
+
+    def _check_entries(self, entries, n, keep, words):
+        e = entries[:n].numpy().view(np.uint64)
+        want = {slot: q for q, slot in self._halo_pairs()}
+        seen = set()
+        for row in e:
+            slot = int(row[0])
+            u, v = self._pair_ids(want[slot])
+            assert keep(v, u) and [int(x) for x in row[1:]] == words(v, u), (slot, row)
+            assert slot not in seen
+            seen.add(slot)
+        assert seen == {s for s, q in want.items() if keep(*self._pair_ids(q)[::-1])}
+        return len(seen)
+
+    @staticmethod
+    def _row_keep(v, u):
+        return (7 * v + u) % 3 == 0
+
+    def gx_rows_words(self):
+        return 3
+
+    def gx_rows_pack(self, n_ranks, out=None):
+        return self._entries(self._row_keep, lambda v, u: [v << 32 | u, 0xABC], out)
+
+    def gx_rows_recv(self, entries, n):
+        self.gx_rows = self._check_entries(entries, n, self._row_keep, lambda v, u: [v << 32 | u, 0xABC])
+
+    def gx_exchange(self):
+        self.gx_hops = []
+        self.gx_fwd = 0
+        return self.gx_runs
+
+    def gxf_begin(self, run):
+        assert run == len(self.gx_hops)
+        self.gx_run = run
+        self.gx_hops.append(0)
+
+    def gxf_entry_words(self):
+        return 4
+
+    def gxf_pack_fout(self, send):
+        a = np.zeros(len(self.send_pair), dtype=np.uint64)
+        for j, v, u in self._send_ids():
+            a[j] = (v << 32 | u) + self.gx_run
+        send[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+
+    def gxf_recv_fout(self, recv):
+        h = recv.numpy().view(np.uint64)
+        for q, slot in self._halo_pairs():
+            u, v = self._pair_ids(q)
+            assert int(h[slot]) == (v << 32 | u) + self.gx_run, (q, slot)
+            self.hb_checked += 1
+
+    def _fwd_keep(self, hop):
+        return lambda v, u: (v + u + hop + self.gx_run) % 2 == 0
+
+    def gxf_pack(self, hop, n_ranks, out=None):
+        return self._entries(self._fwd_keep(hop), lambda v, u: [v << 32 | u, hop, self.gx_run], out)
+
+    def gxf_step(self, hop, entries, n):
+        assert hop == self.gx_hops[-1] + 1
+        self.gx_hops[-1] = hop
+        self.gx_fwd += self._check_entries(entries, n, self._fwd_keep(hop), lambda v, u: [v << 32 | u, hop, self.gx_run])
+        return 1 if hop < 2 + self.gx_run else 0
+
+    def gxf_end(self):
+        assert self.gx_hops[-1] == 2 + self.gx_run
+
+    def gx_got(self, n_sets):
+        g = np.zeros(n_sets, dtype=np.uint8)
+        if n_sets:
+            g[self._rank() % n_sets] = 1
+        return g
+
+    def gx_end(self, got_all):
+        world = len(self.rank_lo) - 1
+        n = self.gx_sets
+        want = np.zeros(n, dtype=np.uint8)
+        for k in range(world):
+            if n:
+                want[k % n] = 1
+        assert list(got_all) == list(want)
+        assert len(self.gx_hops) == self.gx_runs
+        out = abi.HeartbeatOut()
+        out.mesh_links = self.hb_checked
+        out.fwd_delivered = self.gx_fwd
+        out.fwd_duplicates = sum(self.gx_hops)
+        out.iwant_ids = self.gx_rows
         return out
 
     # -- stepped propagation ----------------------------------------------------------

@@ -225,13 +225,17 @@ def test_randomsub_full_hub_matches_oracle(gpu_ok):
     assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))
 
 
-@pytest.mark.parametrize("mix", [False, True], ids=["gossipsub-only", "with-floodsub-peers"])
-def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
+@pytest.mark.parametrize("mix,scores_each", [(False, True), (True, True), (False, False), (True, False)],
+                         ids=["gossipsub-only", "with-floodsub-peers", "gossipsub-only-lazy", "with-floodsub-peers-lazy"])
+def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix, scores_each):
     """One engine, many calls: the forwarding state (k_prop_fwd / k_prop_pin)
     is kept between calls while nothing it reads changed and rebuilt after
     GRAFT / PRUNE / RemovePeer events, a refresh, new thresholds, app scores
     (floodsub peers are score-gated), a heartbeat, a topic or router switch.
-    Every call must match the oracle running the same sequence."""
+    Every call must match the oracle running the same sequence.  Without
+    scores_each the scores are read only at the end, so the lazy folds'
+    stale pairs (PropState::stale) carry across calls, events, raised
+    thresholds and heartbeats (which settle them)."""
     n, T = 600, 2
     ov = pc.overlay(n, 5, seed=31, mix_protocols=mix)
     E = ov.n_pairs
@@ -248,6 +252,8 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         ("remove peers", [(abi.EV_REMOVE_PEER, 0, int(q), pc.T0 + 3 * pc.S, 0) for q in rng.choice(E, 25, replace=False)]),
         ("refresh", "refresh"),
         ("thresholds", "thresholds"),
+        ("gossipsub after thresholds", None),
+        ("thresholds up", "thresholds up"),  # above the stale pairs' bound: they settle first
         ("app scores", "app"),
         ("heartbeat", "heartbeat"),
         ("topic 1", None),
@@ -273,6 +279,9 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
             elif action == "thresholds":
                 be.set_thresholds(abi.Thresholds(gossip_threshold=-50, publish_threshold=-60, graylist_threshold=-300,
                                                  accept_px_threshold=0, opportunistic_graft_threshold=0))
+            elif action == "thresholds up":
+                be.set_thresholds(abi.Thresholds(gossip_threshold=-0.5, publish_threshold=-1, graylist_threshold=-2,
+                                                 accept_px_threshold=0, opportunistic_graft_threshold=0))
             elif action == "app":
                 be.set_app_scores(np.where(np.arange(E) % 7 == 0, -1000.0, 1.0))
             elif action == "heartbeat":
@@ -296,11 +305,13 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix):
         gs, ws = eng.export_state(), ref.export_state()
         for f in abi.STATE_FIELDS:
             assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), (name, f)
-        assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
+        if scores_each:
+            assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
+    assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64))
 
 
-@pytest.mark.parametrize("flood_publish", [0, 1])
-def test_credit_threshold_crossings_between_calls(gpu_ok, flood_publish):
+@pytest.mark.parametrize("flood_publish,scores_each", [(0, True), (1, True), (0, False), (1, False)])
+def test_credit_threshold_crossings_between_calls(gpu_ok, flood_publish, scores_each):
     """Consecutive gossipsub calls whose own credits move scores across the
     graylist and publish thresholds (invalid messages: P4): the fold re-scores
     the credited pairs and keeps their forwarding bytes, so the next call runs
@@ -322,7 +333,8 @@ def test_credit_threshold_crossings_between_calls(gpu_ok, flood_publish):
         (go, gh, gf), (wo, wh, wf) = res
         assert go.as_dict() == wo.as_dict(), k
         assert np.array_equal(gh, wh) and np.array_equal(gf, wf), k
-        assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), k
+        if scores_each or k == 9:
+            assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), k
     gs, ws = eng.export_state(), ref.export_state()
     for f in abi.STATE_FIELDS:
         assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f

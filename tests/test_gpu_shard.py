@@ -243,6 +243,75 @@ def test_sharded_heartbeat_matches_single_engine(gpu_ok, world):
     assert want["grafts"] + want["prunes"] > 0
 
 
+@pytest.mark.parametrize("world,invalid,T", [(2, 0.0, 2), (3, 0.2, 2), (2, 0.0, 1)])
+def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid, T):
+    """The gossip exchange on range shards (gsx_gx_*: IHAVE bits and answer
+    bits of cross-shard pairs, the senders' cache rows, the forwarding of
+    recovered messages hop by hop with frontier entries): rounds of a
+    heartbeat with the exchange on, then a gossipsub batch that travels two
+    hops (most nodes miss it and recover it by IHAVE / IWANT and the
+    recovering nodes' forwarding), == one engine: counters summed over ranks,
+    every node's records, backoff, IHAVEs, scores and cached ids."""
+    import gossip_cases as gc
+    import heartbeat_cases as hc
+
+    n, d, seed = 1200, 6, 47
+    ov = pc.overlay(n, d, seed)
+    full = gsx.Engine(T)
+    app = pc.setup(full, ov, T, seed, mesh_degree=6)
+    gp = gc.params()
+    full.set_gossipsub_params(gp)
+    st0 = full.export_state()
+    E = ov.n_pairs
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        e = gsx.Engine(T)
+        _params(e, T)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(_slice_state(st0, T, E, a, b))
+        e.set_app_scores(app[a:b])
+        e.set_gossipsub_params(gp)
+        engines.append((e, a, b, lo, hi))
+    runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
+                              [(x[0],) for x in engines])
+    tot = {}
+    for k in range(6):
+        tick, now = 1 + k, pc.T0 + (3 + k) * abi.SECOND
+        want = full.heartbeat(tick, now, seed * 31 + 7).as_dict()
+        res = shard.run_local(world, "cuda:0",
+                              lambda tp, r: (setattr(r, "tp", tp), r.heartbeat(tick, now, seed * 31 + 7))[1],
+                              [(r,) for r in runners])
+        assert res[0][1] == want, (k, {x: (res[0][1][x], want[x]) for x in want if res[0][1][x] != want[x]})
+        for x, v in want.items():
+            tot[x] = tot.get(x, 0) + v
+        snap = hc.snapshot(full)
+        for (e, a, b, lo, hi) in engines:
+            got = hc.snapshot(e)
+            for f in abi.STATE_FIELDS:
+                w = _slice_state(snap, T, E, a, b)[f]
+                assert np.array_equal(got[f].view(np.uint8), w.view(np.uint8)), (k, f)
+            for f in ("backoff", "ihave_len", "ihave_digest"):
+                assert np.array_equal(np.asarray(got[f]).reshape(-1), _slice_te(snap[f], T, E, a, b)), (k, f)
+            assert np.array_equal(got["scores"].view(np.uint64), snap["scores"][a:b].view(np.uint64)), k
+            for v in range(lo, hi, 37):  # the caches (recovered copies Put)
+                assert sorted(e.mcache_ids(v - lo, abi.GSX_ANY_TOPIC, 5).tolist()) == \
+                    sorted(full.mcache_ids(v, abi.GSX_ANY_TOPIC, 5).tolist()), (k, v)
+        cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % T, max_hops=2, latency_ms=5, seed=seed + k)
+        cfg.now_ns = now + 100 * abi.MILLISECOND
+        ms = pc.messages(n, 24, seed + 1000 * k, invalid=invalid)
+        full.propagate(ms, cfg)
+        shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(ms, cfg))[1],
+                        [(r,) for r in runners])
+        full.refresh(now + 500 * abi.MILLISECOND)
+        for (e, _, _, _, _) in engines:
+            e.refresh(now + 500 * abi.MILLISECOND)
+    assert tot["iwant_msgs"] > 0 and tot["gossip_delivered"] > 0 and tot["fwd_delivered"] > 0, tot
+
+
 @pytest.mark.parametrize("world,invalid", [(2, 0.0), (3, 0.2)])
 def test_message_parallel_heartbeat_matches_single_engine(gpu_ok, world, invalid):
     """Message-parallel replicas through propagate -> heartbeat cycles with the

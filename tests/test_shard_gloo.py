@@ -56,6 +56,7 @@ def _worker(rank, world, port, payload, q):
             be = emu.EmuShard(sh, payload["fwd"][int(rp[sh.node_lo]) : int(rp[sh.node_hi])])
             rs = gs.RangeSharded(be, payload["rank_lo"], tp, compact=payload["compact"])
             if payload.get("heartbeat"):
+                be.gx_sets = payload.get("gx_sets")
                 local, tot = rs.heartbeat(1, 0, 0)
                 q.put((rank, local, tot, be.hb_checked, None))
             else:
@@ -188,6 +189,37 @@ def test_sharded_heartbeat_exchange_gloo(world):
     owner = np.searchsorted(rank_lo.astype(np.int64), np.arange(n), side="right") - 1
     cross = owner[obs] != owner[ov.col]
     assert sum(r[3] for r in res) == 2 * int(cross.sum()) > 0
+
+
+@pytest.mark.parametrize("world,n_sets", [(2, 3), (3, 2), (2, 0)])
+def test_sharded_gossip_exchange_gloo(world, n_sets):
+    """The gossip exchange of a sharded heartbeat (RangeSharded._gx_exchange
+    over gsx_gx_* / gsx_gxf_*): the common words ANDed over ranks, the IHAVE
+    words and the cache-row entries of the cross pairs, then every forwarding
+    run's fout words and per-hop frontier entries until the frontier count
+    summed over the ranks is 0, and the OR of the got flags.  The emulator's
+    receive side checks every word and entry against its pair (with no
+    message sets, the collectives of the set words are skipped)."""
+    n = 240
+    ov = pc.overlay(n, 4, 3)
+    rank_lo = synth.shard_ranges(n, world)
+    shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
+    cfg = pc.config(abi.GSX_ROUTER_FLOODSUB)
+    payload = dict(mode="range", shards=shards, fwd=np.zeros(ov.n_pairs, np.uint8), row_ptr=ov.row_ptr,
+                   rank_lo=rank_lo, msgs=pc.messages(n, 1, 3), cfg=_cfg_dict(cfg), compact=False, heartbeat=True,
+                   gx_sets=n_sets)
+    res = _run(world, payload)
+    obs = ov.pair_observer()
+    owner = np.searchsorted(rank_lo.astype(np.int64), np.arange(n), side="right") - 1
+    cross = owner[obs] != owner[ov.col]
+    tot = res[0][2]
+    # GRAFT/PRUNE words, answers, IHAVE words, two runs' fout words; one set-common check per rank
+    assert tot["mesh_links"] == 5 * int(cross.sum()) + world
+    v, u = obs[cross].astype(np.int64), ov.col[cross].astype(np.int64)
+    assert tot["iwant_ids"] == int(((7 * v + u) % 3 == 0).sum())
+    want_fwd = sum(int(((v + u + h + run) % 2 == 0).sum()) for run in range(2) for h in range(1, 3 + run))
+    assert tot["fwd_delivered"] == want_fwd
+    assert tot["fwd_duplicates"] == world * (2 + 3)
 
 
 @pytest.mark.parametrize("world", [2, 3])
