@@ -267,13 +267,19 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     M = args.prop_msgs * world
     tp = shard_mod.DistTransport(dev, stage_host=args.rehearse) if dist is not None else None
     # no heartbeat follows this leg: the replicas' cache blocks are not merged
-    # (MessageParallel(cache=True) all-gathers them for replicated heartbeats)
-    runner = shard_mod.MessageParallel(e, tp, cache=False) if tp is not None else None
+    # (MessageParallel(cache=True) all-gathers them for replicated heartbeats).
+    # Credits accumulate over a heartbeat epoch of --epoch-batches batches and
+    # are summed over the replicas once per epoch, not per batch.
+    runner = shard_mod.MessageParallel(e, tp, epoch=True, cache=False) if tp is not None else None
+    eb = max(1, args.epoch_batches)
 
     def once(b):
         msgs = prop_messages(n, M, synth.SEED, first=b * M)
         if runner is not None:
-            return runner.propagate(msgs, cfg), msgs
+            r = runner.propagate(msgs, cfg)
+            if b % eb == 0:  # (warm-up batch 0 closes its own epoch; then every eb batches)
+                runner.end_epoch()
+            return r, msgs
         out = e.propagate(msgs, cfg)[0]
         d = shard_mod.out_dict(out)
         d2 = dict(d)
@@ -286,6 +292,8 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     res = [once(1 + b) for b in range(args.prop_steps)]
+    if runner is not None:
+        runner.end_epoch()  # the last (partial) epoch's credits, inside the timed region
     torch.cuda.synchronize(dev)
     el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     dl = sum(r[0][1]["deliveries"] for r in res)
@@ -297,8 +305,10 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     return {
         "variants": legs,
         "metric": "msg deliveries/s",
-        "mode": "message-parallel replicas (weak): full overlay per GPU, own messages, one all-reduce of credits "
-                "(cache blocks not merged: no heartbeat in this leg)",
+        "mode": ("message-parallel replicas (weak): full overlay per GPU, own messages, credits deferred and summed "
+                 f"with one all-reduce per epoch of {eb} batches (cache blocks not merged: no heartbeat in this "
+                 "leg)") if world > 1 else
+                "one engine, full overlay (the 1-GPU point of the message-parallel leg: no collective)",
         "value": dl / el,
         "peers": n,
         "messages_per_batch_per_gpu": args.prop_msgs,
@@ -400,7 +410,9 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     e.close()
     out = {
         "metric": "msg deliveries/s",
-        "mode": f"range-sharded (strong): {n} peers over {world} GPU(s), per-hop all-to-all of packed cross-shard sends",
+        "mode": (f"range-sharded (strong): {n} peers over {world} GPUs, per-hop all-to-all of packed cross-shard sends"
+                 if world > 1 else f"one engine holding all {n} peers (the 1-GPU point of the range-sharded leg: "
+                 "no cross-shard pairs, no all-to-all)"),
         "value": dl / el,
         "peers": n,
         "messages_per_batch": M,
@@ -600,6 +612,8 @@ def main():
     ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
     ap.add_argument("--shard-msgs", type=int, default=64, help="messages per batch of the cfg4 range-sharded leg")
     ap.add_argument("--prop-steps", type=int, default=5)
+    ap.add_argument("--epoch-batches", type=int, default=4,
+                    help="message-parallel leg: batches per heartbeat epoch (one credit all-reduce each)")
     ap.add_argument("--prop-hops", type=int, default=24)
     ap.add_argument("--hb-steps", type=int, default=5, help="timed heartbeat rounds (0: skip)")
     ap.add_argument("--hb-msgs", type=int, default=256, help="gossipsub messages propagated before every heartbeat")

@@ -622,8 +622,11 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             lst[k] = 1;
         }
         __syncthreads();
-        if (u < h.n_nodes && lst[lane])  // ---- lane per node: the listed ones
-            h.gx_nodes[atomicAdd(&h.gx_err[6], 1u)] = u | (nmls[lane] & GX_HEAVY);
+        {  // ---- lane per node: the listed ones
+            const bool take = u < h.n_nodes && lst[lane];
+            const uint32_t k = wave_append(&h.gx_err[6], take);
+            if (take) h.gx_nodes[k] = u | (nmls[lane] & GX_HEAVY);
+        }
         __syncthreads();  // (the tile's LDS is rewritten next)
     }
     gx_flush(h.stats, HB_IHAVE_IGNORED, ignored);
@@ -963,9 +966,10 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
             }
             if (any) m |= 1ull << si;
         }
+        const uint32_t k = wave_append(&f.fcnt[0], m != 0);
         if (m) {
             f.fmask[0][u] = m;
-            f.flist[0][atomicAdd(&f.fcnt[0], 1u)] = u;
+            f.flist[0][k] = u;
             atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[0][u >> 6]), 1ull << (u & 63));
         }
     }
@@ -1028,7 +1032,8 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
             if (h.rev[r] & HALO) continue;  // a remote receiver: its rank marks it from this rank's entries
             const uint32_t w = (uint32_t)h.col[r] - h.node_lo;
             const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[w]), ok);
-            if (old == 0) f.rlist[atomicAdd(&f.rcnt[hop], 1u)] = w;
+            const uint32_t k = wave_append(&f.rcnt[hop], old == 0);
+            if (old == 0) f.rlist[k] = w;
         }
     }
 }
@@ -1173,13 +1178,14 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
             }
           }
         }
+        const uint32_t slot_x = wave_append(&f.fcnt[hop], newsets != 0);
         if (!newsets) continue;
         for (uint64_t mm = newsets; mm; mm &= mm - 1) {  // (read first: one writer in a thousand stores)
             uint8_t* g = f.sets[__builtin_ctzll(mm)].got;
             if (!*g) *g = 1;
         }
         f.fmask[pw][x] = newsets;
-        f.flist[pw][atomicAdd(&f.fcnt[hop], 1u)] = x;
+        f.flist[pw][slot_x] = x;
         atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
         // fulfillPromise (:119-126): x's promises of messages it now has
         for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
@@ -1201,6 +1207,170 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
     unsigned long long v[3] = {c_new, c_dup, c_gray};
     const uint32_t slot[3] = {HB_FWD_DELIVERED, HB_FWD_DUPLICATES, HB_FWD_GRAYLISTED};
     block_count<3>(v, h.stats, slot);
+}
+
+// k_gxf_pull with G lanes per receiver x splitting its SENDERS (lane c takes
+// pairs c, c + G, ... in rounds of G), as k_prop_hop_fast1 does: a round's G
+// senders are gathered together and "not from a lower sender" becomes an
+// exclusive prefix-OR over the group's sends, word by word.  Every per-pair
+// count (first receipts, duplicates, graylisted copies, back-sends) and credit
+// stays with the pair's lane; every lane writes x's receipt / frontier words
+// with the same values (so each re-reads its own stores).  Same results as
+// k_gxf_pull.
+template <int G>
+__device__ __forceinline__ uint64_t gxf_gor(uint64_t x) {  // OR over the group (aligned), every lane
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, o, G);
+    return x;
+}
+template <int G>
+__global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd f, uint32_t hop) {
+    const uint32_t p = (hop - 1) & 1, pw = hop & 1;
+    const uint32_t seq_cur = f.seq + hop;
+    const uint32_t S_ = h.prom_slots;
+    const uint32_t lc = threadIdx.x % G;
+    unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
+    for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G; i < nr; i += gridDim.x * (256u / G)) {
+        const uint32_t x = dense ? i : f.rlist[i];
+        uint64_t M = f.all_sets;
+        if (!dense) {
+            M = f.rmask[x];
+            if (lc == 0) f.rmask[x] = 0;
+        }
+        const uint64_t srcm = f.srcm[x] & M;
+        uint64_t newsets = 0;  // (the same in every lane of the group)
+        const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
+        for (int64_t qb = r0; qb < r1; qb += G) {
+            const int64_t q = qb + lc;
+            const uint32_t fi = q < r1 ? (uint32_t)f.fin[q] : 0u;
+            const uint32_t r = (fi & 0xFFu) ? h.rev[q] : NO_PAIR;
+            const uint32_t v = (fi & 0xFFu) ? (uint32_t)h.col[q] - h.node_lo : 0u;  // (local index; unused if remote)
+            uint64_t fv = 0;
+            if (fi & 0xFFu) {
+                const bool on = (r & HALO) ? (f.hstamp && f.hstamp[q] == seq_cur)  // a remote sender's entry this hop
+                                           : ((f.fbit[p][v >> 6] >> (v & 63)) & 1);
+                if (on)
+                    fv = ((r & HALO) ? f.hent[(size_t)f.hidx[q] * (GXF_HDR + f.rw) + 1] : f.fmask[p][v]) & M &
+                         gxf_slot_sets(f, fi & 0xFFu);
+            }
+            if (!gxf_gor<G>(fv)) continue;  // no sender of the round sends anything new
+            const uint64_t* hdr = (fv && (r & HALO)) ? f.hent + (size_t)f.hidx[q] * (GXF_HDR + f.rw) : nullptr;
+            const bool gray = (fi & GXF_GRAY) != 0;  // AcceptFrom at x
+            for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
+                const uint64_t sm = fv & f.slot_sets[ts];
+                const uint64_t smg = gxf_gor<G>(sm);
+                if (!smg) continue;
+                const uint32_t t = f.slot_topic[ts];
+                uint32_t n1 = 0, dt = 0, dw = 0, g = 0;
+                for (uint64_t mm = smg; mm; mm &= mm - 1) {
+                    const uint32_t si = (uint32_t)__builtin_ctzll(mm);
+                    const GxFwdSet& S = f.sets[si];
+                    const uint32_t W = S.n_words;
+                    const bool mine = (sm >> si) & 1;
+                    const uint64_t* F = !mine ? nullptr : hdr ? hdr + GXF_HDR + S.woff : S.fr[p] + (size_t)v * W;
+                    uint64_t* X = S.x + (size_t)x * W;
+                    const uint64_t* A = S.all + (size_t)x * W;
+                    uint64_t* NF = S.fr[pw] + (size_t)x * W;
+                    const bool isrc = (srcm >> si) & 1;
+                    for (uint32_t w = 0; w < W; ++w) {
+                        uint64_t snd = mine ? F[w] : 0ull;
+                        if (isrc && snd) snd &= ~gxf_origin(S, x + h.node_lo, w);  // not back to the origin (:1006-1009)
+                        if (gray) {
+                            g += (uint32_t)__popcll(snd);
+                            snd = 0;  // dropped at x: delivers nothing
+                        }
+                        const uint64_t xw = X[w], have = A[w] | xw;
+                        uint64_t incl = snd;  // the group's sends so far, in sender order
+#pragma unroll
+                        for (int o = 1; o < G; o <<= 1) {
+                            const uint64_t y = (uint64_t)__shfl_up((unsigned long long)incl, o, G);
+                            if (lc >= (uint32_t)o) incl |= y;
+                        }
+                        uint64_t excl = (uint64_t)__shfl_up((unsigned long long)incl, 1, G);
+                        if (lc == 0) excl = 0;
+                        const uint64_t all_g = (uint64_t)__shfl((unsigned long long)incl, G - 1, G);
+                        const uint64_t nw = snd & ~(have | excl);  // not seen, not from a lower sender
+                        const uint64_t dup = snd & ~nw;
+                        dt += (uint32_t)__popcll(dup);
+                        // in-window duplicates: an old copy by the set's old_in; else those x got this
+                        // round (before this hop, or first from a lower sender of this one)
+                        dw += (uint32_t)__popcll(S.old_in ? dup : (dup & (xw | (excl & ~have))));
+                        n1 += (uint32_t)__popcll(nw);
+                        const uint64_t gn = all_g & ~have;  // the group's first receipts of the word
+                        if (gn) {
+                            X[w] = xw | gn;
+                            if (!((newsets >> si) & 1)) {
+                                newsets |= 1ull << si;
+                                for (uint32_t z = 0; z < W; ++z) NF[z] = 0;
+                            }
+                            NF[w] |= gn;
+                        }
+                    }
+                }
+                if (!sm) continue;  // (this lane's pair sends nothing of the slot)
+                // the copies v would send back to x: the first receipts v took from x last hop
+                uint32_t back = 0, back_w = 0;
+                if (hdr) {  // counted by the sender's rank (k_gxf_halo)
+                    back = (uint32_t)(hdr[2 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
+                    back_w = (uint32_t)(hdr[4 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
+                } else {
+                    gxf_back(h, f, hop, r, ts, back, back_w);
+                }
+                if (gray) {
+                    g -= back;
+                } else {
+                    dt -= back;
+                    dw -= back_w;
+                }
+                c_new += n1;
+                c_dup += dt;
+                c_gray += g;
+                if (n1 | dw) {
+                    gx_credit(s, (uint64_t)q, t, n1, dw, 0);
+                    if (h.gx_mark) h.gx_mark[q] = 1;
+                }
+                if (n1) {
+                    if (f.bst[pw][q] != seq_cur) {
+                        f.bst[pw][q] = seq_cur;
+                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][(size_t)q * GXF_SLOTS + z] = 0;
+                    }
+                    f.bcnt[pw][(size_t)q * GXF_SLOTS + ts] = (uint16_t)n1;
+                }
+            }
+        }
+        const uint32_t slot_x = wave_append(&f.fcnt[hop], newsets != 0 && lc == 0);
+        if (!newsets) continue;
+        if (lc == 0) {
+            for (uint64_t mm = newsets; mm; mm &= mm - 1) {  // (read first: one writer in a thousand stores)
+                uint8_t* gp = f.sets[__builtin_ctzll(mm)].got;
+                if (!*gp) *gp = 1;
+            }
+            f.fmask[pw][x] = newsets;
+            f.flist[pw][slot_x] = x;
+            atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
+            // fulfillPromise (:119-126): x's promises of messages it now has
+            for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
+                if (z % S_ == 0 && !h.prom_any[z / S_]) {  // no promise on this pair
+                    z += S_ - 1;
+                    continue;
+                }
+                if (h.prom_e[z] == 0) continue;
+                const uint64_t hd = h.prom_h[z];
+                const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
+                for (uint64_t mm = newsets; mm; mm &= mm - 1) {
+                    const GxFwdSet& S = f.sets[__builtin_ctzll(mm)];
+                    if (S.serial != ser) continue;
+                    if (k < S.n_msgs && ((S.x[(size_t)x * S.n_words + k / 64] >> (k % 64)) & 1)) h.prom_e[z] = 0;
+                    break;
+                }
+            }
+        }
+    }
+    unsigned long long vv[3] = {c_new, c_dup, c_gray};
+    const uint32_t slot[3] = {HB_FWD_DELIVERED, HB_FWD_DUPLICATES, HB_FWD_GRAYLISTED};
+    block_count<3>(vv, h.stats, slot);
 }
 
 // ---- the exchange across range shards (gsx_gx_*; gsx.h) -------------------------
@@ -1332,7 +1502,8 @@ __global__ __launch_bounds__(256) void k_gxf_halo_recv(HbState h, GxFwd f, uint3
         f.hidx[q] = (uint32_t)k;
         if (dense) continue;
         const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&f.rmask[x]), e[1]);
-        if (old == 0) f.rlist[atomicAdd(&f.rcnt[hop], 1u)] = x;
+        const uint32_t at = wave_append(&f.rcnt[hop], old == 0);
+        if (old == 0) f.rlist[at] = x;
     }
 }
 
@@ -1388,7 +1559,15 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
 // list (the counts are on the device: an empty hop's threads exit at once).
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
     hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
-    hipLaunchKernelGGL(k_gxf_pull, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
+    static const int gl = [] {  // receivers' lanes: GSX_GXF_G = 1 (k_gxf_pull), 2, 4 (default), 8
+        const char* v = getenv("GSX_GXF_G");
+        return v ? atoi(v) : 4;
+    }();
+    const unsigned gp = gx_blocks(h.n_nodes, 256, 2048);
+    if (gl == 8) hipLaunchKernelGGL(k_gxf_pull_g<8>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (gl == 4) hipLaunchKernelGGL(k_gxf_pull_g<4>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (gl == 2) hipLaunchKernelGGL(k_gxf_pull_g<2>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else hipLaunchKernelGGL(k_gxf_pull, dim3(gp), dim3(256), 0, st, s, h, f, hop);
     return hipGetLastError();
 }
 

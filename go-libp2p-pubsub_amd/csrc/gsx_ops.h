@@ -272,6 +272,22 @@ __device__ __forceinline__ void block_count(unsigned long long (&v)[NV], unsigne
     }
 }
 
+// Appends to a shared list with ONE atomic per wave: the active lanes with
+// `take` get consecutive slots in lane order (-> the lane's slot; callable in
+// divergent code: the ballot and the broadcast see the active lanes only).  A
+// per-lane atomicAdd on one counter serialises every append of the grid at
+// one L2 channel.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool take) {
+    const uint64_t b = __ballot(take);
+    if (b == 0) return 0;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((long long)b) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    return base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+}
+
 // ---- canonical RNG ---------------------------------------------
 __host__ __device__ __forceinline__ uint64_t smix(uint64_t z) {  // SplitMix64 finaliser
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

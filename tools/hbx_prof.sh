@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel traces of the heartbeat with the gossip exchange (cfg3 rounds,
 # tools/hb_micro.py --exchange) and of the cfg5 attack round (tools/adv_micro.py)
-# with both (B) kernels; per-round breakdowns with tools/hb_rounds.py.
+# per-round breakdowns with tools/hb_rounds.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -25,7 +25,4 @@ python3 tools/kt_top.py "$O/hbx/kt_kernel_stats.csv" 24 > "$O/hbx_top.txt"
 step adv 300 rocprofv3 --kernel-trace --stats -d "$O/adv" -o kt --output-format csv -- \
     python3 tools/adv_micro.py --no-spam
 python3 tools/hb_rounds.py "$O/adv/kt_kernel_trace.csv" > "$O/adv_rounds.txt"
-GSX_HB_RECV_LANE=1 step adv_lane 300 rocprofv3 --kernel-trace --stats -d "$O/adv_lane" -o kt --output-format csv -- \
-    python3 tools/adv_micro.py --no-spam
-python3 tools/hb_rounds.py "$O/adv_lane/kt_kernel_trace.csv" > "$O/adv_lane_rounds.txt"
-cat "$O/hbx_rounds.txt" "$O/hbx_top.txt" "$O/adv_rounds.txt" "$O/adv_lane_rounds.txt"
+cat "$O/hbx_rounds.txt" "$O/hbx_top.txt" "$O/adv_rounds.txt"
