@@ -294,6 +294,7 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     res = [once(1 + b) for b in range(args.prop_steps)]
     if runner is not None:
         runner.end_epoch()  # the last (partial) epoch's credits, inside the timed region
+    e.settle_scores()  # deferred re-scores of the lazy folds (timed)
     torch.cuda.synchronize(dev)
     el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     dl = sum(r[0][1]["deliveries"] for r in res)
@@ -337,6 +338,7 @@ def prop_leg(e, n, M, cfg, steps, seed, first):
     for b in range(steps):
         msgs = prop_messages(n, M, seed, first=first + (1 + b) * M)
         outs.append(shard_mod.out_dict(e.propagate(msgs, cfg)[0]))
+    e.settle_scores()  # the re-scores the credit folds deferred (lazy fold): timed, once per leg
     e.sync()
     el = time.perf_counter() - t0
     last = outs[-1]
@@ -520,6 +522,7 @@ def adversarial_leg(args, rank, world, local, dist, dev):
             d = shard_mod.out_dict(e.propagate(ms, cfg)[0])
         else:
             d = sp_runner.propagate(ms, cfg)[1]
+        e.settle_scores()  # (the batch's deferred re-scores, timed with it)
         e.sync()
         torch.cuda.synchronize(dev)
         out["spam"] = {
@@ -729,6 +732,7 @@ def main():
             now += abi.SECOND
             hb_cfg.now_ns = now - abi.SECOND // 2
             e.propagate(prop_messages(n, args.hb_msgs, seed, first=50_000_000 + k * args.hb_msgs), hb_cfg)
+            e.settle_scores()  # the batch's own (deferred) re-scores finish with it, outside the round
             e.sync()
             barrier()
             torch.cuda.synchronize(dev)

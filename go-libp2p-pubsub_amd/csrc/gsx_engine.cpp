@@ -1956,6 +1956,12 @@ int gsx_device_scores(gsx_engine* e, const double** dptr) {
     return GSX_OK;
 }
 
+int gsx_settle_scores(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    if (!e->loaded) return GSX_OK;
+    return ensure_scores(e);
+}
+
 int gsx_sync(gsx_engine* e) {
     if (!e) return GSX_EINVAL;
     if (int rc = flush(e)) return rc;

@@ -412,6 +412,7 @@ SIGNATURES = {
     "gsx_gx_end": (C.c_int, [C.c_void_p, P(C.c_uint8), P(HeartbeatOut)]),
     "gsx_device_scores": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "gsx_sync": (C.c_int, [C.c_void_p]),
+    "gsx_settle_scores": (C.c_int, [C.c_void_p]),
     "gsx_import_state": (C.c_int, [C.c_void_p, P(StateView)]),
     "gsx_export_state": (C.c_int, [C.c_void_p, P(StateView)]),
     "gsx_last_refresh_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),

@@ -183,6 +183,10 @@ class Engine:
     def sync(self):
         self._chk(self.lib.gsx_sync(self.h), "gsx_sync")
 
+    def settle_scores(self):
+        """gsx_settle_scores: the deferred re-scores of lazy credit folds, queued now."""
+        self._chk(self.lib.gsx_settle_scores(self.h), "gsx_settle_scores")
+
     def last_refresh_ms(self) -> float:
         v = C.c_float()
         self._chk(self.lib.gsx_last_refresh_ms(self.h, C.byref(v)), "gsx_last_refresh_ms")

@@ -279,6 +279,13 @@ int gsx_score_many(gsx_engine* e, const uint64_t* pairs, size_t n, double* out);
 int gsx_device_scores(gsx_engine* e, const double** dptr);
 
 int gsx_sync(gsx_engine* e);
+/* Queues every deferred score update: the queued events, and the re-scores a
+ * gossipsub propagation's credit fold leaves to the next score reader (pairs
+ * whose score was at or above every forwarding threshold and only rose: the
+ * fwd bytes stay exact meanwhile).  Every score reader settles them itself;
+ * this puts the work at a point of the caller's choosing (e.g. right after a
+ * batch, as the fold would have done). */
+int gsx_settle_scores(gsx_engine* e);
 
 /* ---- state import / export (inspection, synthetic workloads, checkpoints) -- */
 /* Record arrays are topic-major: element [t * n_pairs + p].  Mirrors the

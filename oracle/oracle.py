@@ -406,6 +406,9 @@ class Oracle:
     def sync(self):
         pass
 
+    def settle_scores(self):  # (the restatement re-scores eagerly: nothing deferred)
+        pass
+
     def _view(self, arrays: Dict[str, np.ndarray]):
         sv = abi.StateView()
         for f in abi.STATE_FIELDS:

@@ -46,6 +46,7 @@ for k in range(3 + a.rounds):
     now += abi.SECOND
     cfg.now_ns = now - abi.SECOND // 2
     e.propagate(bench.prop_messages(a.peers, a.msgs, 5, first=k * a.msgs), cfg)
+    e.settle_scores()  # (as bench.py: the batch's deferred re-scores outside the round)
     e.sync()
     t0 = time.perf_counter()
     o = e.heartbeat(tick, now, synth.SEED).as_dict()

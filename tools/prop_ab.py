@@ -42,6 +42,7 @@ def child(a):
     for b in range(a.batches):
         out = e.propagate(bench.prop_messages(a.peers, a.msgs, synth.SEED, first=(3 + b) * a.msgs), cfg)[0]
         kms += out.hop_kernel_ms
+    e.settle_scores()
     e.sync()
     el = time.perf_counter() - t0
     print(json.dumps({"variant": a.variant, "msgs": a.msgs, "router": a.router, "ms_per_batch": el / a.batches * 1e3,
