@@ -352,6 +352,7 @@ struct GxBatch {
     uint32_t dense;       // a first-hand batch (most rows hold uncommon messages): k_gx_rhm sets its bit unread
     const uint64_t* src;  // [n_msgs] the set's origins (node << 32 | index, ascending): the forwarding's back counts
     uint32_t old_in;      // a copy of the set's messages validated before this round is inside the P3 window
+    uint32_t grp;         // the set's group: up to 64 sets of one topic (the forwarding's hop-1 back counts)
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
@@ -447,7 +448,8 @@ struct HbState {
     // the IWANT first receipts per (topic, pair) of this round (the forwarding's
     // hop-1 back-sends, GxFwd); null when nothing is forwarded
     uint32_t* gxb_st0;     // [pair] stamp: the pair's counts were written this round
-    uint32_t* gxb_cnt0;    // [topic][pair]: sets whose old copies are inside the P3 window | the others << 16
+    uint32_t* gxb_cnt0;    // [group][pair]: sets whose old copies are inside the P3 window | the others << 16
+    uint32_t gxb_ngrp;     // set groups this round (GxBatch::grp)
     uint32_t gxb_stamp;
     uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
     uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
@@ -568,6 +570,7 @@ struct GxFwd {
     const GxFwdSet* sets;
     uint32_t n_sets, n_slots;
     uint32_t slot_topic[GXF_SLOTS];
+    uint32_t slot_grp[GXF_SLOTS];  // the slot's set group (hop-1 back counts)
     uint64_t slot_sets[GXF_SLOTS];  // per topic slot: its sets
     uint64_t* fmask[2];  // [node] the sets of the node's frontier, by hop parity
     uint32_t* flist[2];  // frontier nodes, by hop parity

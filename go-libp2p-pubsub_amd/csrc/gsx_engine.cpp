@@ -215,7 +215,8 @@ struct gsx_engine {
     uint32_t* d_gxf_list = nullptr;   // flist[2][N], rlist[N]
     uint32_t* d_gxf_cnt = nullptr;    // fcnt[GXF_MAX_HOPS + 1], rcnt[GXF_MAX_HOPS + 1]
     uint32_t* d_gxf_bst = nullptr;    // stamps: bst0[E], bst[2][E] (zeroed once; stamps only grow)
-    uint32_t* d_gxf_b0 = nullptr;     // bcnt0[T][E]
+    uint32_t* d_gxf_b0 = nullptr;     // bcnt0[group][E]
+    size_t gxf_b0_grps = 0;           // its groups
     uint16_t* d_gxf_b = nullptr;      // bcnt[2][E][GXF_SLOTS]
     uint16_t* d_gxf_fin = nullptr;    // [E] per run (GxFwd::fin)
     uint8_t* d_gxf_fout = nullptr;    // [E] per run (GxFwd::fout)
@@ -239,13 +240,15 @@ struct gsx_engine {
     // gsx_gx_end finishes the round.
     struct GxfRun {
         std::vector<size_t> sets;   // indices into GxRound::sets
-        std::vector<uint32_t> topics;
+        std::vector<uint32_t> grps;  // its set groups (topic slots), GxRound::grp_*
     };
     struct GxRound {
         bool run = false, pending = false, exact = false, fwd_active = false;
         int stage = 0;  // range shards: 1 prepared, 2 common set, 3 IHAVEs in, 4 rows in, 5 exchanged
         gsx::HbState h{};
         std::vector<MsgSet*> sets;
+        std::vector<uint32_t> set_grp;   // per set: its group (up to 64 sets / 65,535 messages of one topic)
+        std::vector<uint32_t> grp_topic;  // per group
         std::vector<uint64_t*> xs;
         std::vector<std::pair<uint64_t*, size_t>> scratch;  // frontier rows, released after the round's sync
         uint32_t n_gx = 0, fw = 0;
@@ -686,6 +689,7 @@ void free_state(gsx_engine* e) {
         e->d_gxf_mask = nullptr;
         e->d_gxf_list = e->d_gxf_cnt = e->d_gxf_bst = nullptr;
         e->d_gxf_b0 = nullptr;
+        e->gxf_b0_grps = 0;
         e->d_gxf_b = nullptr;
         e->d_gxf_sets = nullptr;
         e->d_gxf_fin = nullptr;
@@ -3557,6 +3561,15 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
 // The forwarding of recovered messages (gsx.h (D), GxFwd): state allocated on
 // first use; the hop stamps only grow (re-zeroed before they could wrap).
 int gxf_alloc(gsx_engine* e) {
+    const size_t n_grp = std::max<size_t>({e->gxr.grp_topic.size(), (size_t)e->T, 1});
+    if (e->d_gxf_b0 && n_grp > e->gxf_b0_grps) {  // more set groups than topics this round
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(e->d_gxf_b0);
+        e->d_gxf_b0 = nullptr;
+        e->gxf_b0_grps = std::max(n_grp, 2 * e->gxf_b0_grps);
+        if (int rc = dalloc(e, &e->d_gxf_b0, e->gxf_b0_grps * std::max<size_t>(e->E, 1))) return rc;
+        HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * std::max<size_t>(e->E, 1), e->stream));  // (bst0: no stale stamps)
+    }
     if (e->d_gxf_bst) {
         if (e->gxf_stamp < 0xF0000000u) return GSX_OK;
         HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * std::max<size_t>(e->E, 1), e->stream));
@@ -3568,10 +3581,11 @@ int gxf_alloc(gsx_engine* e) {
     int rc = 0;
     if ((rc = dalloc(e, &e->d_gxf_mask, 4 * N + 2 * ((N + 63) / 64))) || (rc = dalloc(e, &e->d_gxf_list, 3 * N)) ||
         (rc = dalloc(e, &e->d_gxf_cnt, 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) || (rc = dalloc(e, &e->d_gxf_bst, 3 * E)) ||
-        (rc = dalloc(e, &e->d_gxf_b0, (size_t)std::max<uint32_t>(e->T, 1) * E)) ||
+        (rc = dalloc(e, &e->d_gxf_b0, n_grp * E)) ||
         (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fin, E)) ||
         (rc = dalloc(e, &e->d_gxf_fout, E)))
         return rc;
+    e->gxf_b0_grps = n_grp;
     if (e->sharded() && (rc = dalloc(e, &e->d_gxf_hst, 2 * E))) return rc;
     if (e->d_gxf_hst) HIPCHK(e, hipMemsetAsync(e->d_gxf_hst, 0, 4 * 2 * E, e->stream));
     if (!e->h_gxf_cnt) HIPCHK(e, hipHostMalloc((void**)&e->h_gxf_cnt, 64, hipHostMallocDefault));
@@ -3581,37 +3595,23 @@ int gxf_alloc(gsx_engine* e) {
     return GSX_OK;
 }
 
-// The forwarding runs over the exchange's sets: up to 64 sets of up to
-// GXF_SLOTS topics each, and all sets of each of its topics (the IWANT back
-// counts are per topic); topics in first-seen order, greedily.
+// The forwarding runs over the exchange's sets: up to 64 sets in up to
+// GXF_SLOTS set groups each (a group: up to 64 sets / 65,535 messages of one
+// topic, gx_prepare; the IWANT back counts are per group), greedily in order.
 int gxf_plan(gsx_engine* e, gsx_engine::GxRound& R) {
     R.runs.clear();
-    const auto& sets = R.sets;
-    std::vector<uint32_t> topics;
-    std::vector<std::vector<size_t>> by_topic;
-    for (size_t i = 0; i < sets.size(); ++i) {
-        size_t ti = 0;
-        while (ti < topics.size() && topics[ti] != sets[i]->topic) ++ti;
-        if (ti == topics.size()) {
-            topics.push_back(sets[i]->topic);
-            by_topic.emplace_back();
-        }
-        by_topic[ti].push_back(i);
-    }
+    const uint32_t G = (uint32_t)R.grp_topic.size();
+    std::vector<std::vector<size_t>> by_grp(G);
+    for (size_t i = 0; i < R.sets.size(); ++i) by_grp[R.set_grp[i]].push_back(i);
     size_t n_sets = 0;
-    for (size_t ti = 0; ti < topics.size(); ++ti) {
-        size_t msgs = 0;
-        for (size_t i : by_topic[ti]) msgs += sets[i]->n_msgs;
-        if (by_topic[ti].size() > 64 || msgs > 65535)
-            return fail(e, GSX_ERANGE, "gossip exchange: topic " + std::to_string(topics[ti]) +
-                                           " advertises more than 64 message sets or 65,535 messages in one round");
-        if (R.runs.empty() || R.runs.back().topics.size() == gsx::GXF_SLOTS || n_sets + by_topic[ti].size() > 64) {
+    for (uint32_t g = 0; g < G; ++g) {  // (groups are in the sets' order: topics first seen first)
+        if (R.runs.empty() || R.runs.back().grps.size() == gsx::GXF_SLOTS || n_sets + by_grp[g].size() > 64) {
             R.runs.emplace_back();
             n_sets = 0;
         }
-        R.runs.back().topics.push_back(topics[ti]);
-        for (size_t i : by_topic[ti]) R.runs.back().sets.push_back(i);
-        n_sets += by_topic[ti].size();
+        R.runs.back().grps.push_back(g);
+        for (size_t i : by_grp[g]) R.runs.back().sets.push_back(i);
+        n_sets += by_grp[g].size();
     }
     return GSX_OK;
 }
@@ -3641,14 +3641,15 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
     auto* stage = static_cast<gsx::GxFwdSet*>(e->h_gxf_stage);
     gsx::GxFwd f{};
     f.sets = e->d_gxf_sets;
-    f.n_slots = (uint32_t)run.topics.size();
+    f.n_slots = (uint32_t)run.grps.size();
     uint32_t n_src = 0, rw = 0;
-    for (size_t ts = 0; ts < run.topics.size(); ++ts) {
-        const uint32_t t = run.topics[ts];
+    for (size_t ts = 0; ts < run.grps.size(); ++ts) {
+        const uint32_t t = R.grp_topic[run.grps[ts]];
         f.slot_topic[ts] = t;
+        f.slot_grp[ts] = run.grps[ts];
         for (size_t i : run.sets) {
             const gsx_engine::MsgSet* ms = R.sets[i];
-            if (ms->topic != t) continue;
+            if (R.set_grp[i] != run.grps[ts]) continue;
             const size_t words = (size_t)ms->n_words * N;
             gsx::GxFwdSet S{};
             S.all = ms->d_all;
@@ -3799,12 +3800,33 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
             }
     }
     off[e->T] = (uint32_t)gx.size();
+    // the set groups: consecutive sets of one topic, up to 64 sets and 65,535
+    // messages each (the u16 back counts of the forwarding)
+    R.set_grp.assign(R.sets.size(), 0);
+    R.grp_topic.clear();
+    {
+        uint32_t cnt = 0;
+        size_t msgs = 0;
+        for (size_t i = 0; i < R.sets.size(); ++i) {
+            const gsx_engine::MsgSet* ms = R.sets[i];
+            if (ms->n_msgs > 65535) return fail(e, GSX_ERANGE, "gossip exchange: a message set above 65,535 messages");
+            if (R.grp_topic.empty() || R.grp_topic.back() != ms->topic || cnt == 64 || msgs + ms->n_msgs > 65535) {
+                R.grp_topic.push_back(ms->topic);
+                cnt = 0;
+                msgs = 0;
+            }
+            R.set_grp[i] = (uint32_t)R.grp_topic.size() - 1;
+            ++cnt;
+            msgs += ms->n_msgs;
+        }
+    }
     {  // the flat word list of all advertised batches (k_gx_node's rounds)
         uint32_t fw = 0;
         for (size_t i = 0; i < gx.size(); ++i) {
             gx[i].woff = fw;
             fw += gx[i].n_words;
             gx[i].n_msgs = R.sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
+            gx[i].grp = R.set_grp[reinterpret_cast<size_t>(gx[i].got)];
         }
     }
     // per topic, the sets of its batches: each set's first batch in cache
@@ -3960,6 +3982,7 @@ int gx_ready(gsx_engine* e, gsx_engine::GxRound& R) {
     if (int rc = gxf_alloc(e)) return rc;
     h.gxb_st0 = e->d_gxf_bst;
     h.gxb_cnt0 = e->d_gxf_b0;
+    h.gxb_ngrp = (uint32_t)R.grp_topic.size();
     h.gxb_stamp = ++e->gxf_stamp;
     dbg_host("gx prepared");
     return GSX_OK;

@@ -274,14 +274,16 @@ __device__ __forceinline__ uint64_t origin_word(const uint64_t* src, uint32_t n,
 // excluded as the origin already): the forwarding's hop-1 back-sends (GxFwd).
 // At v those copies are old (v served them from its cache): counted apart by
 // the old_in of their set (inside the P3 window or not).
-__device__ __forceinline__ void gx_back0(const DevState& s, const HbState& h, uint64_t q, uint32_t t, uint32_t k_in,
-                                         uint32_t k_out) {
+// Counted per set group (GxBatch::grp: up to 64 sets of one topic).
+__device__ __forceinline__ void gx_back0_clear(const HbState& h, uint64_t q) {  // (once per answered pair)
+    if (!h.gxb_st0 || h.gxb_st0[q] == h.gxb_stamp) return;
+    h.gxb_st0[q] = h.gxb_stamp;
+    for (uint32_t i = 0; i < h.gxb_ngrp; ++i) h.gxb_cnt0[(size_t)i * h.n_pairs + q] = 0;
+}
+__device__ __forceinline__ void gx_back0(const HbState& h, uint64_t q, uint32_t grp, uint32_t k_in, uint32_t k_out) {
     if (!h.gxb_st0 || !(k_in | k_out)) return;
-    if (h.gxb_st0[q] != h.gxb_stamp) {
-        h.gxb_st0[q] = h.gxb_stamp;
-        for (uint32_t i = 0; i < s.n_topics; ++i) h.gxb_cnt0[(size_t)i * h.n_pairs + q] = 0;
-    }
-    h.gxb_cnt0[(size_t)t * h.n_pairs + q] += k_in | k_out << 16;
+    gx_back0_clear(h, q);
+    h.gxb_cnt0[(size_t)grp * h.n_pairs + q] += k_in | k_out << 16;
 }
 
 // handleIWant at v and the receipt at u, one id at a time (pass 2 for a pair
@@ -316,7 +318,7 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
                 ++delivered;
                 ev_first(s, q, t);
                 if (h.gxb_st0 && !((origin_word(b.src, b.n_msgs, v, k / 64) >> (k % 64)) & 1))
-                    gx_back0(s, h, q, t, b.old_in, !b.old_in);
+                    gx_back0(h, q, b.grp, b.old_in, !b.old_in);
                 *b.got = 1;
             } else {
                 ++rejected;
@@ -710,6 +712,8 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
             const bool answered = gx_answers(s, h, (uint64_t)q, r) &&  // v ignores u's IWANT
                                   ((h.eflags[q] & EDGE_DIRECT) || !(s.score[q] < h.graylist));  // AcceptFrom at u
             const uint64_t tb = tall & (h.sub ? h.sub[u] : ~0ull);
+            if (answered && lane == 0) gx_back0_clear(h, (uint64_t)q);  // (the lanes below add to the counts)
+            __threadfence_block();
             if (answered) {
                 const uint32_t v = (uint32_t)h.col[q];
                 const uint64_t tr = h.ihave_tr[q];
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                     for (uint64_t tm = tb; tm; tm &= tm - 1) {
                         const uint32_t t = (uint32_t)__builtin_ctzll(tm);
                         const uint64_t* sub = gx_subrow(h, tr, t, r);
-                        uint32_t k1 = 0, k2 = 0, k4 = 0, kb = 0, kbo = 0;  // kb / kbo: the back-sends of k1 (GxFwd)
+                        uint32_t k1 = 0, k2 = 0, k4 = 0;
                         // a lane per (message set, word) of the topic: it walks the
                         // set's batches in cache order (the one order its receipt word
                         // sees); different sets touch different receipt rows
@@ -761,10 +765,11 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                     if (val == VAL_ACCEPT) ++k2;
                                     else if (val == VAL_REJECT) ++k4;
                                 }
-                                if (acc1 && h.gxb_st0) {
+                                if (acc1 && h.gxb_st0) {  // the back-sends of these first receipts (GxFwd)
                                     const uint32_t nb = (uint32_t)__popcll(acc1 & ~origin_word(b.src, b.n_msgs, v, w));
-                                    if (b.old_in) kb += nb;
-                                    else kbo += nb;
+                                    if (nb)
+                                        atomicAdd(&h.gxb_cnt0[(size_t)b.grp * h.n_pairs + q],
+                                                  b.old_in ? nb : nb << 16);  // (cleared before the walk)
                                 }
                             }
                             if (got) *b.got = 1;
@@ -773,12 +778,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                         k1 = gx_wsum(k1);
                         k2 = gx_wsum(k2);
                         k4 = gx_wsum(k4);
-                        kb = gx_wsum(kb);
-                        kbo = gx_wsum(kbo);
-                        if (lane == 0) {
-                            gx_credit(s, q, t, k1, k2, k4);
-                            gx_back0(s, h, q, t, kb, kbo);
-                        }
+                        if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
                     }
                 } else if (lane == 0) {
                     gx_receive_sampled(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void gxf_back(const HbState& h, const GxFwd& f, uint3
     const uint32_t p = (hop - 1) & 1;
     if (hop == 1) {
         if (f.bst0 && f.bst0[r] == f.stamp0) {
-            const uint32_t b2 = f.bcnt0[(size_t)f.slot_topic[ts] * h.n_pairs + r];
+            const uint32_t b2 = f.bcnt0[(size_t)f.slot_grp[ts] * h.n_pairs + r];
             back_w = b2 & 0xFFFFu;
             back = back_w + (b2 >> 16);
         }
