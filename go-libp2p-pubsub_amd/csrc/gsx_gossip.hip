@@ -959,12 +959,10 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
             const GxFwdSet& S = f.sets[si];
             const uint32_t W = S.n_words;
             uint64_t any = 0;
-            for (uint32_t w = 0; w < W; ++w) {
-                const uint64_t row = S.x[(size_t)u * W + w] & S.acc[w];
-                S.fr[0][(size_t)u * W + w] = row;
-                any |= row;
-            }
-            if (any) m |= 1ull << si;
+            for (uint32_t w = 0; w < W; ++w) any |= S.x[(size_t)u * W + w] & S.acc[w];
+            if (!any) continue;  // (a row is read only where fmask has its set)
+            m |= 1ull << si;
+            for (uint32_t w = 0; w < W; ++w) S.fr[0][(size_t)u * W + w] = S.x[(size_t)u * W + w] & S.acc[w];
         }
         const uint32_t k = wave_append(&f.fcnt[0], m != 0);
         if (m) {
@@ -1281,6 +1279,8 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                             g += (uint32_t)__popcll(snd);
                             snd = 0;  // dropped at x: delivers nothing
                         }
+                        // a word no sender of the round sends: nothing to receive or count
+                        if (!((__ballot(snd != 0) >> (__lane_id() & ~(uint32_t)(G - 1))) & ((1ull << G) - 1))) continue;
                         const uint64_t xw = X[w], have = A[w] | xw;
                         uint64_t incl = snd;  // the group's sends so far, in sender order
 #pragma unroll
