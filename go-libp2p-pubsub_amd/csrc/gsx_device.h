@@ -255,6 +255,7 @@ struct PropState {
 // pins / compacted senders of the listed changes only
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only = false);
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
+hipError_t launch_prop_clear(const PropState& ps, bool clear_flast, bool clear_corr, hipStream_t st);
 hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, uint64_t* send,
                             hipStream_t st);

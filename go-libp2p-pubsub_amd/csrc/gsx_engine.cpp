@@ -260,6 +260,7 @@ struct gsx_engine {
     std::vector<uint64_t> mc_digest_host;  // per cache slot: mix64(id + golden)
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
     std::vector<std::pair<size_t, uint8_t*>> small_pool;  // message sets' small device arrays, recycled
+    std::vector<void*> pool_slabs;  // the allocations both pools carve their buffers from (freed at teardown)
     gsx::GossipBatch* d_gb = nullptr;
     uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
@@ -295,6 +296,8 @@ struct gsx_engine {
         uint32_t chg_cap = 0;
         uint64_t* d_dig = nullptr;                 // message / word id digests of the call (k_mc_summary)
         size_t dig_cap = 0;
+        void* h_stage = nullptr;  // pinned staging of a call's host-side inputs (messages, masks, set arrays)
+        size_t h_stage_bytes = 0;
         uint32_t words_cap = 0, msgs_cap = 0, rows_cap = 0;
         size_t seen_words = 0;
         gsx::PropState last{};
@@ -537,15 +540,26 @@ uint64_t* seen_acquire(gsx_engine* e, size_t words) {
             e->seen_pool.erase(e->seen_pool.begin() + (long)i);
             return p;
         }
+    // none free: a slab of kSlab buffers at once (one hipMalloc per kSlab
+    // acquisitions, not per propagation call: the call's host time is the
+    // device's idle time between calls)
+    constexpr size_t kSlab = 4;
+    const size_t w = (std::max<size_t>(words, 1) + 31) & ~(size_t)31;  // (256-B aligned buffers)
     uint64_t* p = nullptr;
-    if (hipMalloc((void**)&p, 8 * std::max<size_t>(words, 1)) != hipSuccess) return nullptr;
+    if (hipMalloc((void**)&p, 8 * w * kSlab) != hipSuccess) {
+        if (hipMalloc((void**)&p, 8 * w) != hipSuccess) return nullptr;  // (a tight device: one buffer)
+        e->pool_slabs.push_back(p);
+        return p;
+    }
+    e->pool_slabs.push_back(p);
+    for (size_t k = 1; k < kSlab; ++k) e->seen_pool.emplace_back(w, p + k * w);
     return p;
 }
 void seen_pool_free(gsx_engine* e) {
-    for (auto& x : e->seen_pool) (void)hipFree(x.second);
     e->seen_pool.clear();
-    for (auto& x : e->small_pool) (void)hipFree(x.second);
     e->small_pool.clear();
+    for (void* x : e->pool_slabs) (void)hipFree(x);
+    e->pool_slabs.clear();
 }
 // Small per-set device arrays (validation outcomes, accepted words, id
 // digests, the `full` bytes) from a recycled pool: no hipMalloc / hipFree per
@@ -558,9 +572,13 @@ uint8_t* small_acquire(gsx_engine* e, size_t bytes, size_t* got) {
             e->small_pool.erase(e->small_pool.begin() + (long)i);
             return p;
         }
+    constexpr size_t kSlab = 16;  // (as seen_acquire: one hipMalloc per kSlab arrays)
+    const size_t b = (std::max<size_t>(bytes, 256) + 255) & ~(size_t)255;
     uint8_t* p = nullptr;
-    if (hipMalloc((void**)&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
-    *got = std::max<size_t>(bytes, 256);
+    if (hipMalloc((void**)&p, b * kSlab) != hipSuccess) return nullptr;
+    e->pool_slabs.push_back(p);
+    for (size_t k = 1; k < kSlab; ++k) e->small_pool.emplace_back(b, p + k * b);
+    *got = b;
     return p;
 }
 void small_release(gsx_engine* e, uint8_t* p, size_t bytes) {
@@ -635,7 +653,8 @@ void free_state(gsx_engine* e) {
     e->dirty_zeroed = true;
     e->invalidate_scores();
     e->h_score_tag = ~0ull;
-    void* pp[] = {e->prop.seen, e->prop.hist, e->prop.origin, e->prop.from,
+    // (prop.seen is a pool buffer: seen_pool_free below frees its slab)
+    void* pp[] = {e->prop.hist, e->prop.origin, e->prop.from,
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
                   e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
@@ -2420,7 +2439,22 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     if (!P.dcount) {
         if (int rc = dalloc(e, &P.dcount, (size_t)gsx::MAX_RANKS)) return rc;
     }
-    std::vector<uint64_t> vm(2 * (size_t)W, 0);  // (copied before the stream sync at the end)
+    // pinned staging of the call's host inputs (the previous call ended with a
+    // stream sync: nothing still reads it): [messages | drop / reject masks]
+    // here, [the message set's arrays] in prop_end
+    const size_t st_msgs = (sizeof(gsx::DevMsg) * m + 255) & ~(size_t)255;
+    const size_t st_vm = (16 * (size_t)W + 255) & ~(size_t)255;
+    const size_t st_set = ((4 * m + 7) & ~(size_t)7) + 8 * (size_t)W + 8 * ((size_t)W * 64 + W) + 8 * m + 256;
+    if (P.h_stage_bytes < st_msgs + st_vm + st_set) {
+        if (P.h_stage) (void)hipHostFree(P.h_stage);
+        P.h_stage = nullptr;
+        P.h_stage_bytes = 0;
+        const size_t want = 2 * (st_msgs + st_vm + st_set);
+        HIPCHK(e, hipHostMalloc(&P.h_stage, want, hipHostMallocDefault));
+        P.h_stage_bytes = want;
+    }
+    uint64_t* vm = reinterpret_cast<uint64_t*>(static_cast<char*>(P.h_stage) + st_msgs);
+    std::fill(vm, vm + 2 * (size_t)W, 0ull);
     {  // validation outcomes of this call: dropped / rejected message bits
         P.has_drop = false;
         for (size_t k = 0; k < m; ++k)
@@ -2430,7 +2464,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
                 P.has_drop = true;
             }
         if (P.has_drop) {
-            HIPCHK(e, hipMemcpyAsync(P.vmask, vm.data(), 8 * vm.size(), hipMemcpyHostToDevice, e->stream));
+            HIPCHK(e, hipMemcpyAsync(P.vmask, vm, 16 * (size_t)W, hipMemcpyHostToDevice, e->stream));
             if (P.dseen_words < (size_t)W * N) {
                 if (P.dseen) (void)hipFree(P.dseen);
                 P.dseen = nullptr;
@@ -2457,25 +2491,21 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     }
     if (cfg->router == GSX_ROUTER_GOSSIPSUB) set_sources(P.h_src, msgs, m);
     P.active = true;
-    HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
-    if (m == 0) return GSX_OK;
-    std::vector<gsx::DevMsg> hm(m);
-    for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, msgs[k].validation, msgs[k].msg_id};
-    HIPCHK(e, hipMemcpyAsync(P.msgs, hm.data(), sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemsetAsync(P.seen, 0, 8 * (size_t)W * N, e->stream));
-    // hist row 0 and origin: only the sources' rows are read (under occupancy
-    // row 0) and cleared (k_prop_zero_src in launch_prop_init)
-    HIPCHK(e, hipMemsetAsync(P.occ, 0, 8 * ((N + 63) / 64), e->stream));
-    HIPCHK(e, hipMemsetAsync(P.touch, 0, 16 * ((N + 63) / 64), e->stream));  // both buffers (k_prop_mark clears them after)
-    if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
-    // corr: the per-hop accounting adds to it; the late one writes every
-    // pair it reads (k_prop_dups -> k_prop_count under the reverse pair's SEND bit)
-    if (!ps.late) HIPCHK(e, hipMemsetAsync(P.corr, 0, 4 * std::max<size_t>(E, 1), e->stream));
-    HIPCHK(e, hipMemsetAsync(P.fcnt, 0, 4 * std::max<size_t>(E, 1), e->stream));
-    if (P.flast_dirty) {  // only hops that may stop a call early write flast (k_prop_hop_fast: the max_hops cut)
-        HIPCHK(e, hipMemsetAsync(P.flast, 0, 8 * std::max<size_t>(E, 1), e->stream));
-        P.flast_dirty = false;
+    if (m == 0) {
+        HIPCHK(e, hipMemsetAsync(P.stats, 0, 8 * (size_t)gsx::STAT_WORDS, e->stream));
+        return GSX_OK;
     }
+    auto* hm = static_cast<gsx::DevMsg*>(P.h_stage);
+    for (size_t k = 0; k < m; ++k) hm[k] = gsx::DevMsg{msgs[k].source, msgs[k].validation, msgs[k].msg_id};
+    HIPCHK(e, hipMemcpyAsync(P.msgs, hm, sizeof(gsx::DevMsg) * m, hipMemcpyHostToDevice, e->stream));
+    // one launch clears the seen rows, first-receipt counts, occupancy row 0
+    // (hist row 0 and origin: only the sources' rows are read, under it, and
+    // cleared by k_prop_zero_src), both touch buffers, the counters; flast
+    // only when a hop wrote it (k_prop_hop_fast: the max_hops cut), corr when
+    // the per-hop accounting adds to it (the late one writes every pair it reads)
+    HIPCHK(e, gsx::launch_prop_clear(ps, P.flast_dirty, !ps.late, e->stream));
+    P.flast_dirty = false;
+    if (track) HIPCHK(e, hipMemsetAsync(P.from, 0, 8 * (size_t)W * E, e->stream));
     if (rsub) HIPCHK(e, hipMemsetAsync(P.sel, 0, 8 * (size_t)W * E, e->stream));
     const gsx::DevState ds = dev_state(e);
     // fwd / pin (k_prop_fwd, k_prop_pin) read the router config, the pair and
@@ -2513,7 +2543,6 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         K.graylist_threshold = e->th.graylist_threshold;
     }
     HIPCHK(e, gsx::launch_prop_init(ps, P.hist, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));  // `hm` is on the host stack
     return GSX_OK;
 }
 
@@ -2687,12 +2716,26 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         acc.assign(W, 0);
         for (size_t k = 0; k < P.vals.size(); ++k)
             if (P.vals[k] == GSX_VALIDATION_ACCEPT) acc[k / 64] |= 1ull << (k % 64);
-        if (!set_small_alloc(e, set, P.vals.size(), W)) return fail(e, GSX_ENOMEM, "message set arrays");
+        const size_t mv = P.vals.size();
+        if (!set_small_alloc(e, set, mv, W)) return fail(e, GSX_ENOMEM, "message set arrays");
         set->t0 = P.cfg.now_ns;
-        HIPCHK(e, hipMemcpyAsync(set->d_val, P.vals.data(), 4 * P.vals.size(), hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
-        if (!P.h_src.empty())
-            HIPCHK(e, hipMemcpyAsync(set->d_src, P.h_src.data(), 8 * P.h_src.size(), hipMemcpyHostToDevice, e->stream));
+        {  // the set's block [validation | accepted words | id digests | origins], staged and copied at once
+            const size_t st_off = ((sizeof(gsx::DevMsg) * mv + 255) & ~(size_t)255) + ((16 * (size_t)W + 255) & ~(size_t)255);
+            char* blk = static_cast<char*>(P.h_stage) + st_off;
+            const size_t val_b = (4 * std::max<size_t>(mv, 1) + 7) & ~(size_t)7;
+            const size_t bytes = val_b + 8 * (size_t)W + 8 * ((size_t)W * 64 + W) + 8 * std::max<size_t>(mv, 1);
+            std::memset(blk, 0, bytes);
+            std::memcpy(blk, P.vals.data(), 4 * mv);
+            std::memcpy(blk + val_b, acc.data(), 8 * (size_t)W);
+            auto* dg = reinterpret_cast<uint64_t*>(blk + val_b + 8 * (size_t)W);  // ids: gsx.h (k_mc_summary)
+            for (size_t k = 0; k < P.ids.size(); ++k) {
+                dg[k] = id_digest(P.ids[k]);
+                dg[(size_t)W * 64 + k / 64] += dg[k];
+            }
+            if (!P.h_src.empty())
+                std::memcpy(blk + val_b + 8 * (size_t)W + 8 * ((size_t)W * 64 + W), P.h_src.data(), 8 * P.h_src.size());
+            HIPCHK(e, hipMemcpyAsync(set->d_small, blk, bytes, hipMemcpyHostToDevice, e->stream));
+        }
     }
     if (ps.drop) HIPCHK(e, gsx::launch_prop_uncache(ps, P.cfg.router == GSX_ROUTER_GOSSIPSUB, e->stream));
     if (P.cfg.router == GSX_ROUTER_GOSSIPSUB) {  // Publish Puts each processed message into the mcache
@@ -2702,27 +2745,12 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         b.n_words = W;
         b.d_seen = P.seen;  // the cache keeps this call's seen rows; the next call takes a pooled buffer
         b.seen_words = P.seen_words;
-        {  // per-node (count, digest) summary of the batch for emitGossip (id digests: gsx.h)
+        {  // per-node (count, digest) summary of the batch for emitGossip (the set's id digests: gsx.h)
             const size_t N = ps.n_nodes;
-            std::vector<uint64_t> dg((size_t)W * 64 + W, 0);
-            for (size_t k = 0; k < P.ids.size(); ++k) {
-                dg[k] = id_digest(P.ids[k]);
-                dg[(size_t)W * 64 + k / 64] += dg[k];
-            }
-            if (P.dig_cap < dg.size()) {
-                if (P.d_dig) (void)hipFree(P.d_dig);
-                P.d_dig = nullptr;
-                P.dig_cap = 0;
-                if (int rc = dalloc(e, &P.d_dig, dg.size())) return rc;
-                P.dig_cap = dg.size();
-            }
-            HIPCHK(e, hipMemcpyAsync(P.d_dig, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
-            if (set) HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));
             b.d_dig = P.seen + (size_t)W * N;
             b.d_cnt = reinterpret_cast<uint32_t*>(P.seen + (size_t)W * N + N);
-            HIPCHK(e, gsx::launch_mc_summary(P.seen, (uint32_t)N, W, ps.n_msgs, P.d_dig, P.d_dig + (size_t)W * 64,
+            HIPCHK(e, gsx::launch_mc_summary(P.seen, (uint32_t)N, W, ps.n_msgs, set->d_dg, set->d_dg + (size_t)W * 64,
                                              b.d_dig, b.d_cnt, e->stream));
-            HIPCHK(e, hipStreamSynchronize(e->stream));  // `dg` is on the host stack
         }
         P.seen = nullptr;
         b.ids = P.ids;

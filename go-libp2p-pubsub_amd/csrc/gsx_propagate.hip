@@ -184,6 +184,31 @@ __global__ __launch_bounds__(256) void k_prop_zero_src(PropState ps, uint64_t* f
 }
 
 // Sources on this shard: seen / frontier / origin bits and hop 0 (the local publish).
+// The per-call clears of gsx_propagate in one launch (was a memset each):
+// seen rows, first-receipt counts (and their last-hop words, the per-hop
+// back-send corrections when those are used), occupancy row 0, both touch
+// buffers and the counters.
+__global__ __launch_bounds__(256) void k_prop_clear(PropState ps, uint32_t clear_flast, uint32_t clear_corr) {
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const size_t nseen = (size_t)ps.n_words * ps.n_nodes;
+    const size_t n = nseen > ps.n_pairs ? nseen : ps.n_pairs;
+    const size_t stride = (size_t)gridDim.x * 256u;
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < n; i += stride) {
+        if (i < nseen) ps.seen[i] = 0;
+        if (i < ps.n_pairs) {
+            ps.fcnt[i] = 0;
+            if (clear_flast) ps.flast[i] = 0;
+            if (clear_corr) ps.corr[i] = 0;
+        }
+        if (i < occ_row) {
+            ps.occ[i] = 0;
+            ps.touch[i] = 0;
+            ps.touch[occ_row + i] = 0;
+        }
+        if (i < STAT_WORDS) ps.stats[i] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_prop_init(PropState ps, uint64_t* front) {
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     if (k >= ps.n_msgs) return;
@@ -1657,6 +1682,12 @@ hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st
     if (ps.n_msgs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_zero_src, dim3(nblk((uint64_t)ps.n_msgs * ps.n_words, 256)), dim3(256), 0, st, ps, front);
     hipLaunchKernelGGL(k_prop_init, dim3(nblk(ps.n_msgs, 256)), dim3(256), 0, st, ps, front);
+    return hipGetLastError();
+}
+hipError_t launch_prop_clear(const PropState& ps, bool clear_flast, bool clear_corr, hipStream_t st) {
+    const size_t n = std::max<size_t>({(size_t)ps.n_words * ps.n_nodes, (size_t)ps.n_pairs, (size_t)STAT_WORDS});
+    hipLaunchKernelGGL(k_prop_clear, dim3(std::min(nblk(n, 256), 8192u)), dim3(256), 0, st, ps, clear_flast ? 1u : 0u,
+                       clear_corr ? 1u : 0u);
     return hipGetLastError();
 }
 hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, hipStream_t st) {

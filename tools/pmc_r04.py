@@ -2,7 +2,7 @@
 """Summarise tools/pmc_r04.sh: HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB
 (gfx950, checked by tools/microbench/pmc_calib.hip) per launch of the headline
 kernel, per batch of the propagation hops and per-call passes, per heartbeat
-round (last round of tools/hb_micro.py).  Each section carries the workload
+round (the last round of bench.py's heartbeat leg).  Each section carries the workload
 it measured, in bench.py's keys (bench.pmc_bytes compares them).
 usage: pmc_r04.py <dir> <headline config key, e.g. n=1000000,T=8,d=6,E=11999954>"""
 import collections

@@ -4,7 +4,7 @@
 # kernels) for the bench's kernels on the current tree:
 #   head  the headline k_refresh_score<8, true> (bench.py, scoring legs only)
 #   p1024 / p64  the propagation replica workload (tools/prop_profile.py)
-#   hb    cfg3 heartbeat rounds with the gossip exchange (tools/hb_micro.py)
+#   hb    cfg3 heartbeat rounds with the gossip exchange (bench.py's heartbeat leg: its last round)
 # then tools/pmc_r04.py writes the per-launch / per-batch / per-round bytes, each
 # section tagged with the workload it measured (bench.py attaches a section's
 # bytes only to a leg that ran the same workload).
@@ -29,6 +29,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
         --prop-peers 0 --hb-steps 0 --adv-peers 0
     run p1024 200 $C python3 tools/prop_profile.py --msgs 1024 --batches 3
     run p64 200 $C python3 tools/prop_profile.py --msgs 64 --batches 3
-    run hb 200 $C python3 tools/hb_micro.py --exchange --rounds 3
+    run hb 300 $C python3 bench.py --steps 1 --warmup 0 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
+        --prop-peers 0 --adv-peers 0 --hb-steps 5
 done
 python3 tools/pmc_r04.py "$O" "n=1000000,T=8,d=6,E=11999954" > "$O/summary.json" && cat "$O/summary.json"
