@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) void k_prop_zero_src(PropState ps, uint64_t* f
 __global__ __launch_bounds__(256) void k_prop_clear(PropState ps, uint32_t clear_flast, uint32_t clear_corr) {
     const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
     const size_t nseen = (size_t)ps.n_words * ps.n_nodes;
-    const size_t n = nseen > ps.n_pairs ? nseen : ps.n_pairs;
+    size_t n = nseen > ps.n_pairs ? nseen : ps.n_pairs;
+    if (n < STAT_WORDS) n = STAT_WORDS;  // (tiny overlays: the stat words are the longest array)
     const size_t stride = (size_t)gridDim.x * 256u;
     for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < n; i += stride) {
         if (i < nseen) ps.seen[i] = 0;
