@@ -1040,9 +1040,11 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
 // first receipts v took from x at the hop before; hop 1: the IWANT answers x
 // served v, old at x (inside the window by their set's old_in); later hops:
 // copies x got in this round.  (back: all of them, back_w: those inside x's
-// P3 window.)
-__device__ __forceinline__ void gxf_back(const HbState& h, const GxFwd& f, uint32_t hop, uint64_t r, uint32_t ts,
-                                         uint32_t& back, uint32_t& back_w) {
+// P3 window.)  Hop 1's counts are at r (k_gx_node's pair); a later hop's at
+// gxf_bidx of the pull that took them: x's own pair q = (x -> v) when v is
+// local (the reads then run along x's row), r when x is on another rank.
+__device__ __forceinline__ void gxf_back(const HbState& h, const GxFwd& f, uint32_t hop, uint64_t r, uint64_t q,
+                                         uint32_t ts, uint32_t& back, uint32_t& back_w) {
     back = back_w = 0;
     const uint32_t p = (hop - 1) & 1;
     if (hop == 1) {
@@ -1051,10 +1053,14 @@ __device__ __forceinline__ void gxf_back(const HbState& h, const GxFwd& f, uint3
             back_w = b2 & 0xFFFFu;
             back = back_w + (b2 >> 16);
         }
-    } else if (f.bst[p][r] == f.seq + hop - 1) {
-        back = back_w = f.bcnt[p][(size_t)r * GXF_SLOTS + ts];
+    } else if (f.bst[p][q] == f.seq + hop - 1) {
+        back = back_w = f.bcnt[p][(size_t)q * GXF_SLOTS + ts];
     }
 }
+// Where the pull of pair q (reverse r) leaves its first-receipt counts for the
+// next hop's back-sends: at the reverse pair (read by its owner), or at q
+// itself when the peer is on another rank (read by k_gxf_halo here).
+__device__ __forceinline__ uint64_t gxf_bidx(uint64_t q, uint32_t r) { return (r & HALO) ? q : (uint64_t)r; }
 
 __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1, pw = hop & 1;
@@ -1151,7 +1157,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                     back = (uint32_t)(hdr[2 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
                     back_w = (uint32_t)(hdr[4 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
                 } else {
-                    gxf_back(h, f, hop, r, ts, back, back_w);
+                    gxf_back(h, f, hop, r, (uint64_t)q, ts, back, back_w);
                 }
                 if (gray) {
                     g -= back;
@@ -1167,11 +1173,12 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                     if (h.gx_mark) h.gx_mark[q] = 1;
                 }
                 if (n1) {
-                    if (f.bst[pw][q] != seq_cur) {
-                        f.bst[pw][q] = seq_cur;
-                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][(size_t)q * GXF_SLOTS + z] = 0;
+                    const uint64_t bi = gxf_bidx((uint64_t)q, r);
+                    if (f.bst[pw][bi] != seq_cur) {
+                        f.bst[pw][bi] = seq_cur;
+                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][bi * GXF_SLOTS + z] = 0;
                     }
-                    f.bcnt[pw][(size_t)q * GXF_SLOTS + ts] = (uint16_t)n1;
+                    f.bcnt[pw][bi * GXF_SLOTS + ts] = (uint16_t)n1;
                 }
             }
           }
@@ -1221,7 +1228,9 @@ __device__ __forceinline__ uint64_t gxf_gor(uint64_t x) {  // OR over the group 
     for (int o = 1; o < G; o <<= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, o, G);
     return x;
 }
-template <int G>
+// B rounds of G senders have their filter loads (slot byte, reverse pair, peer;
+// frontier bit; frontier mask) issued together, three latencies per B rounds.
+template <int G, int B>
 __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1, pw = hop & 1;
     const uint32_t seq_cur = f.seq + hop;
@@ -1240,19 +1249,40 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
         const uint64_t srcm = f.srcm[x] & M;
         uint64_t newsets = 0;  // (the same in every lane of the group)
         const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
-        for (int64_t qb = r0; qb < r1; qb += G) {
+        for (int64_t qb0 = r0; qb0 < r1; qb0 += G * B) {
+          uint32_t fis[B], rqs[B], vqs[B];
+          uint64_t fms[B];
+#pragma unroll
+          for (int j = 0; j < B; ++j) {
+              const int64_t q = qb0 + j * G + lc;
+              const bool in = q < r1;
+              fis[j] = in ? (uint32_t)f.fin[q] : 0u;
+              rqs[j] = in ? h.rev[q] : NO_PAIR;
+              vqs[j] = in ? (uint32_t)h.col[q] - h.node_lo : 0u;  // (local index; unused if remote)
+          }
+#pragma unroll
+          for (int j = 0; j < B; ++j) {
+              const int64_t q = qb0 + j * G + lc;
+              fms[j] = 0;
+              if (!(fis[j] & 0xFFu)) continue;
+              if (rqs[j] & HALO) fms[j] = f.hstamp && f.hstamp[q] == seq_cur;  // a remote sender's entry this hop
+              else fms[j] = (f.fbit[p][vqs[j] >> 6] >> (vqs[j] & 63)) & 1;  // (L2-resident: filters the mask loads)
+          }
+#pragma unroll
+          for (int j = 0; j < B; ++j) {
+              const int64_t q = qb0 + j * G + lc;
+              if (fms[j])
+                  fms[j] = ((rqs[j] & HALO) ? f.hent[(size_t)f.hidx[q] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vqs[j]]) &
+                           M & gxf_slot_sets(f, fis[j] & 0xFFu);
+          }
+          for (int j = 0; j < B; ++j) {  // the rounds in sender order
+            const int64_t qb = qb0 + j * G;
+            if (qb >= r1) break;
             const int64_t q = qb + lc;
-            const uint32_t fi = q < r1 ? (uint32_t)f.fin[q] : 0u;
-            const uint32_t r = (fi & 0xFFu) ? h.rev[q] : NO_PAIR;
-            const uint32_t v = (fi & 0xFFu) ? (uint32_t)h.col[q] - h.node_lo : 0u;  // (local index; unused if remote)
-            uint64_t fv = 0;
-            if (fi & 0xFFu) {
-                const bool on = (r & HALO) ? (f.hstamp && f.hstamp[q] == seq_cur)  // a remote sender's entry this hop
-                                           : ((f.fbit[p][v >> 6] >> (v & 63)) & 1);
-                if (on)
-                    fv = ((r & HALO) ? f.hent[(size_t)f.hidx[q] * (GXF_HDR + f.rw) + 1] : f.fmask[p][v]) & M &
-                         gxf_slot_sets(f, fi & 0xFFu);
-            }
+            const uint32_t fi = fis[j];
+            const uint32_t r = (fi & 0xFFu) ? rqs[j] : NO_PAIR;
+            const uint32_t v = (fi & 0xFFu) ? vqs[j] : 0u;
+            const uint64_t fv = fms[j];
             if (!gxf_gor<G>(fv)) continue;  // no sender of the round sends anything new
             const uint64_t* hdr = (fv && (r & HALO)) ? f.hent + (size_t)f.hidx[q] * (GXF_HDR + f.rw) : nullptr;
             const bool gray = (fi & GXF_GRAY) != 0;  // AcceptFrom at x
@@ -1316,7 +1346,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                     back = (uint32_t)(hdr[2 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
                     back_w = (uint32_t)(hdr[4 + ts / 4] >> (16 * (ts % 4))) & 0xFFFFu;
                 } else {
-                    gxf_back(h, f, hop, r, ts, back, back_w);
+                    gxf_back(h, f, hop, r, (uint64_t)q, ts, back, back_w);
                 }
                 if (gray) {
                     g -= back;
@@ -1332,13 +1362,15 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                     if (h.gx_mark) h.gx_mark[q] = 1;
                 }
                 if (n1) {
-                    if (f.bst[pw][q] != seq_cur) {
-                        f.bst[pw][q] = seq_cur;
-                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][(size_t)q * GXF_SLOTS + z] = 0;
+                    const uint64_t bi = gxf_bidx((uint64_t)q, r);
+                    if (f.bst[pw][bi] != seq_cur) {
+                        f.bst[pw][bi] = seq_cur;
+                        for (uint32_t z = 0; z < GXF_SLOTS; ++z) f.bcnt[pw][bi * GXF_SLOTS + z] = 0;
                     }
-                    f.bcnt[pw][(size_t)q * GXF_SLOTS + ts] = (uint16_t)n1;
+                    f.bcnt[pw][bi * GXF_SLOTS + ts] = (uint16_t)n1;
                 }
             }
+          }
         }
         const uint32_t slot_x = wave_append(&f.fcnt[hop], newsets != 0 && lc == 0);
         if (!newsets) continue;
@@ -1350,12 +1382,12 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
             f.fmask[pw][x] = newsets;
             f.flist[pw][slot_x] = x;
             atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
-            // fulfillPromise (:119-126): x's promises of messages it now has
-            for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
-                if (z % S_ == 0 && !h.prom_any[z / S_]) {  // no promise on this pair
-                    z += S_ - 1;
-                    continue;
-                }
+        }
+        // fulfillPromise (:119-126): x's promises of messages it now has (a pair's
+        // promises are its own: the group's lanes take x's pairs c, c + G, ...)
+        for (int64_t qq = r0 + lc; qq < r1; qq += G) {
+            if (!h.prom_any[qq]) continue;  // no promise on this pair
+            for (uint64_t z = (uint64_t)qq * S_; z < (uint64_t)(qq + 1) * S_; ++z) {
                 if (h.prom_e[z] == 0) continue;
                 const uint64_t hd = h.prom_h[z];
                 const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
@@ -1471,7 +1503,7 @@ __global__ __launch_bounds__(256) void k_gxf_halo(HbState h, GxFwd f, GxsPlan P,
         uint64_t b01[2] = {0, 0}, w01[2] = {0, 0};
         for (uint32_t ts = 0; ts < f.n_slots; ++ts) {
             uint32_t back, back_w;
-            gxf_back(h, f, hop, r, ts, back, back_w);
+            gxf_back(h, f, hop, r, r, ts, back, back_w);  // (x remote: the counts are at r)
             b01[ts / 4] |= (uint64_t)back << (16 * (ts % 4));
             w01[ts / 4] |= (uint64_t)back_w << (16 * (ts % 4));
         }
@@ -1563,10 +1595,15 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
         const char* v = getenv("GSX_GXF_G");
         return v ? atoi(v) : 4;
     }();
+    static const int gb = [] {  // GSX_GXF_B = 2: filter batches of two rounds (G = 4)
+        const char* v = getenv("GSX_GXF_B");
+        return v ? atoi(v) : 1;
+    }();
     const unsigned gp = gx_blocks(h.n_nodes, 256, 2048);
-    if (gl == 8) hipLaunchKernelGGL(k_gxf_pull_g<8>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (gl == 4) hipLaunchKernelGGL(k_gxf_pull_g<4>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (gl == 2) hipLaunchKernelGGL(k_gxf_pull_g<2>, dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    if (gl == 8) hipLaunchKernelGGL((k_gxf_pull_g<8, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (gl == 4 && gb == 2) hipLaunchKernelGGL((k_gxf_pull_g<4, 2>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (gl == 4) hipLaunchKernelGGL((k_gxf_pull_g<4, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (gl == 2) hipLaunchKernelGGL((k_gxf_pull_g<2, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else hipLaunchKernelGGL(k_gxf_pull, dim3(gp), dim3(256), 0, st, s, h, f, hop);
     return hipGetLastError();
 }
