@@ -605,8 +605,10 @@ struct GxFwd {
     uint32_t* hidx;
     const uint64_t* hent;
     uint32_t rw;
+    uint32_t dense_div;  // a hop is dense when its last frontier exceeds n_nodes / dense_div
 };
 constexpr uint32_t GXF_HDR = 6;
+constexpr uint32_t GXF_DENSE = 16;
 constexpr uint16_t GXF_GRAY = 0x100;
 hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
                            hipStream_t st);

@@ -3730,6 +3730,11 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
     f.fout = e->d_gxf_fout;
     f.fin = e->d_gxf_fin;
     f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
+    static const uint32_t dense_div = [] {  // (GSX_GXF_DENSE: A/B of the dense-hop threshold)
+        const char* v = getenv("GSX_GXF_DENSE");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_DENSE;
+    }();
+    f.dense_div = dense_div;
     if (e->d_gxf_hst) {
         f.hstamp = e->d_gxf_hst;
         f.hidx = e->d_gxf_hst + E;

@@ -1004,9 +1004,8 @@ __device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots
     for (; slots; slots &= slots - 1) m |= f.slot_sets[__builtin_ctz(slots)];
     return m;
 }
-// A hop whose frontier holds more than n / GXF_DENSE nodes pulls at every node
-// (no marking): cheaper than its atomics and lists.
-constexpr uint32_t GXF_DENSE = 16;
+// A hop whose frontier holds more than n / f.dense_div nodes (GXF_DENSE by
+// default) pulls at every node (no marking): cheaper than its atomics and lists.
 
 __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1;
@@ -1018,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
             for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (h.n_nodes + 63) / 64; i += stride) f.fbit[hop & 1][i] = 0;
     }
     const uint32_t nf = f.fcnt[hop - 1];
-    if ((uint64_t)nf * GXF_DENSE > h.n_nodes) return;  // a dense hop: the pull visits every node
+    if ((uint64_t)nf * f.dense_div > h.n_nodes) return;  // a dense hop: the pull visits every node
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nf; i += stride) {
         const uint32_t v = f.flist[p][i];
         const uint64_t M = f.fmask[p][v];
@@ -1067,7 +1066,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
     const uint32_t seq_cur = f.seq + hop;
     const uint32_t S_ = h.prom_slots;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
-    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * f.dense_div > h.n_nodes;
     const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nr; i += gridDim.x * 256u) {
         const uint32_t x = dense ? i : f.rlist[i];
@@ -1237,7 +1236,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
     const uint32_t S_ = h.prom_slots;
     const uint32_t lc = threadIdx.x % G;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
-    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * f.dense_div > h.n_nodes;
     const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G; i < nr; i += gridDim.x * (256u / G)) {
         const uint32_t x = dense ? i : f.rlist[i];
@@ -1525,7 +1524,7 @@ __global__ __launch_bounds__(256) void k_gxf_halo(HbState h, GxFwd f, GxsPlan P,
 __global__ __launch_bounds__(256) void k_gxf_halo_recv(HbState h, GxFwd f, uint32_t hop, const uint64_t* in,
                                                        uint64_t n, const uint32_t* halo_pair,
                                                        const uint32_t* halo_node) {
-    const bool dense = (uint64_t)f.fcnt[hop - 1] * GXF_DENSE > h.n_nodes;
+    const bool dense = (uint64_t)f.fcnt[hop - 1] * f.dense_div > h.n_nodes;
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256u) {
         const uint64_t* e = in + (size_t)k * (GXF_HDR + f.rw);
         const uint64_t slot = e[0];
