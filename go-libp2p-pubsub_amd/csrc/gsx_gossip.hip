@@ -1330,11 +1330,12 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                         const uint64_t gn = all_g & ~have;  // the group's first receipts of the word
                         if (gn) {
                             X[w] = xw | gn;
-                            if (!((newsets >> si) & 1)) {
-                                newsets |= 1ull << si;
-                                for (uint32_t z = 0; z < W; ++z) NF[z] = 0;
+                            if (!((newsets >> si) & 1)) {  // x's first receipt of the set this hop: its row
+                                newsets |= 1ull << si;      // written whole (no read of the word back)
+                                for (uint32_t z = 0; z < W; ++z) NF[z] = z == w ? gn : 0ull;
+                            } else {
+                                NF[w] |= gn;
                             }
-                            NF[w] |= gn;
                         }
                     }
                 }
