@@ -1599,7 +1599,11 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
         const char* v = getenv("GSX_GXF_B");
         return v ? atoi(v) : 1;
     }();
-    const unsigned gp = gx_blocks(h.n_nodes, 256, 2048);
+    static const unsigned gcap = [] {  // GSX_GXF_GRID: the pull's block cap (A/B)
+        const char* v = getenv("GSX_GXF_GRID");
+        return v && atoi(v) > 0 ? (unsigned)atoi(v) : 2048u;
+    }();
+    const unsigned gp = gx_blocks(h.n_nodes, 256 / gl, gcap);
     if (gl == 8) hipLaunchKernelGGL((k_gxf_pull_g<8, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else if (gl == 4 && gb == 2) hipLaunchKernelGGL((k_gxf_pull_g<4, 2>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else if (gl == 4) hipLaunchKernelGGL((k_gxf_pull_g<4, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
