@@ -442,6 +442,8 @@ struct HbState {
     // the rows v's rank sent (gxs_rows: entries of 1 + gxs_fw words, the flat
     // word list of the advertised batches; NO_PAIR: v holds only common messages)
     uint64_t* gxs_out;
+    uint64_t* gxs_tro;  // [pair (sender side)]: topics whose IHAVE over the cross-shard pair was
+                        // truncated (its subset is row gsub.idx[pair]; k_gxs_rows masks the rows with it)
     uint8_t* gxs_rans;
     uint32_t* gxs_hidx;
     const uint64_t* gxs_rows;

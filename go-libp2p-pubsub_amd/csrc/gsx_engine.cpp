@@ -227,7 +227,7 @@ struct gsx_engine {
     size_t h_gxf_stage_bytes = 0;
     uint32_t gxf_stamp = 0;           // stamps of the IWANT back counts (one per round) and of the hops
     uint32_t* d_gxf_hst = nullptr;    // range shards: [2][E] GxFwd::hstamp, hidx
-    uint64_t* d_gxs_out = nullptr;    // range shards: [E] HbState::gxs_out
+    uint64_t* d_gxs_out = nullptr;    // range shards: [2][E] HbState::gxs_out, gxs_tro
     uint8_t* d_gxs_rans = nullptr;    // range shards: [E] HbState::gxs_rans
     uint32_t* d_gxs_hidx = nullptr;   // range shards: [E] HbState::gxs_hidx
     unsigned long long* d_gxs_cnt = nullptr;  // range shards: [MAX_RANKS] entries per destination
@@ -261,6 +261,7 @@ struct gsx_engine {
     std::vector<std::pair<size_t, uint64_t*>> seen_pool;  // (words, buffer) free seen-row buffers
     std::vector<std::pair<size_t, uint8_t*>> small_pool;  // message sets' small device arrays, recycled
     std::vector<void*> pool_slabs;  // the allocations both pools carve their buffers from (freed at teardown)
+    std::unordered_map<const uint64_t*, size_t> seen_cap;  // each seen-row buffer's real capacity (words)
     gsx::GossipBatch* d_gb = nullptr;
     uint64_t* d_mc_digest = nullptr;
     size_t gb_cap = 0, ids_cap = 0;
@@ -453,6 +454,14 @@ int fail(gsx_engine* e, int code, const std::string& msg) {
             return fail((e), GSX_EDEVICE, std::string(#call ": ") + hipGetErrorString(_st));    \
     } while (0)
 
+// A sharded gossip exchange (gsx_hb_end .. gsx_gx_end) holds the round's
+// message sets, receipt rows and the mcache Shift: nothing that starts other
+// work on the engine's state may run before gsx_gx_end.
+int gx_busy(gsx_engine* e) {
+    if (e->gxr.pending) return fail(e, GSX_ESTATE, "a sharded gossip exchange is in flight: gsx_gx_end first");
+    return GSX_OK;
+}
+
 gsx::DevState dev_state(const gsx_engine* e) {
     gsx::DevState s{};
     s.rec = e->d_rec;
@@ -530,34 +539,47 @@ int upload_topic_params(gsx_engine* e) {
 // Seen-row buffers cycle between the propagation call (its `seen`) and the
 // message cache (a gossipsub batch keeps the call's buffer): a call hands its
 // buffer to the cache instead of copying it, and takes one from this pool.
-void seen_release(gsx_engine* e, uint64_t* p, size_t words) {
-    if (p) e->seen_pool.emplace_back(words, p);
+// Every buffer keeps the capacity it was carved with (seen_cap), whatever
+// size the caller asked for, so a recycled buffer never looks smaller than
+// it is; an acquisition takes the smallest free buffer that fits.
+void seen_release(gsx_engine* e, uint64_t* p, size_t /*words*/) {
+    if (!p) return;
+    auto it = e->seen_cap.find(p);
+    e->seen_pool.emplace_back(it != e->seen_cap.end() ? it->second : 0, p);
 }
 uint64_t* seen_acquire(gsx_engine* e, size_t words) {
+    size_t best = e->seen_pool.size();
     for (size_t i = 0; i < e->seen_pool.size(); ++i)
-        if (e->seen_pool[i].first >= words) {
-            uint64_t* p = e->seen_pool[i].second;
-            e->seen_pool.erase(e->seen_pool.begin() + (long)i);
-            return p;
-        }
-    // none free: a slab of kSlab buffers at once (one hipMalloc per kSlab
+        if (e->seen_pool[i].first >= words && (best == e->seen_pool.size() || e->seen_pool[i].first < e->seen_pool[best].first))
+            best = i;
+    if (best < e->seen_pool.size()) {
+        uint64_t* p = e->seen_pool[best].second;
+        e->seen_pool.erase(e->seen_pool.begin() + (long)best);
+        return p;
+    }
+    // none free: small buffers come in slabs of kSlab (one hipMalloc per kSlab
     // acquisitions, not per propagation call: the call's host time is the
-    // device's idle time between calls)
-    constexpr size_t kSlab = 4;
+    // device's idle time between calls); a large one (a 10M-node overlay's
+    // rows) is allocated alone, so the pool never reserves 4x a peak
+    constexpr size_t kSlab = 4, kSlabMaxBytes = 64ull << 20;
     const size_t w = (std::max<size_t>(words, 1) + 31) & ~(size_t)31;  // (256-B aligned buffers)
+    const size_t n = 8 * w <= kSlabMaxBytes ? kSlab : 1;
     uint64_t* p = nullptr;
-    if (hipMalloc((void**)&p, 8 * w * kSlab) != hipSuccess) {
-        if (hipMalloc((void**)&p, 8 * w) != hipSuccess) return nullptr;  // (a tight device: one buffer)
+    if (hipMalloc((void**)&p, 8 * w * n) != hipSuccess) {
+        if (n == 1 || hipMalloc((void**)&p, 8 * w) != hipSuccess) return nullptr;  // (a tight device: one buffer)
         e->pool_slabs.push_back(p);
+        e->seen_cap[p] = w;
         return p;
     }
     e->pool_slabs.push_back(p);
-    for (size_t k = 1; k < kSlab; ++k) e->seen_pool.emplace_back(w, p + k * w);
+    for (size_t k = 0; k < n; ++k) e->seen_cap[p + k * w] = w;
+    for (size_t k = 1; k < n; ++k) e->seen_pool.emplace_back(w, p + k * w);
     return p;
 }
 void seen_pool_free(gsx_engine* e) {
     e->seen_pool.clear();
     e->small_pool.clear();
+    e->seen_cap.clear();
     for (void* x : e->pool_slabs) (void)hipFree(x);
     e->pool_slabs.clear();
 }
@@ -625,7 +647,28 @@ void mcache_clear(gsx_engine* e) {
     e->mc.emplace_back();  // history[0], empty
 }
 
+// Drops the exchange in flight (a failed step, or teardown): its receipt
+// rows, frontier rows and set references go back to the pools.
+void gx_abort(gsx_engine* e) {
+    auto& R = e->gxr;
+    (void)hipStreamSynchronize(e->stream);
+    for (auto& fr : R.scratch) seen_release(e, fr.first, fr.second);
+    for (size_t i = 0; i < R.xs.size() && i < R.sets.size(); ++i)
+        seen_release(e, R.xs[i], (size_t)R.sets[i]->n_words * e->n_nodes + 2 * (size_t)e->n_nodes);
+    for (auto* ms : R.sets) {
+        ms->full_ok = false;
+        set_release(e, ms);
+    }
+    R.scratch.clear();
+    R.sets.clear();
+    R.xs.clear();
+    R.runs.clear();
+    R.pending = R.run = R.fwd_active = false;
+    R.stage = 0;
+}
+
 void free_state(gsx_engine* e) {
+    gx_abort(e);
     void* ptrs[] = {e->d_rec,    e->d_rflags, e->d_tmp, e->d_nbad,    e->d_pflags, e->d_eflags,
                     e->d_expire, e->d_bp,     e->d_app, e->d_score,   e->d_ipg,    e->d_ipcount,
                     e->d_col};
@@ -1249,6 +1292,7 @@ int hb_alloc(gsx_engine* e) {
 int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_nodes, const int64_t* row_ptr,
                  const int32_t* col, const uint8_t* edge_flags, const uint32_t* node_ips) {
     if (!e || !row_ptr || (!col && row_ptr[n_nodes] > 0)) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if ((uint64_t)node_lo + n_nodes > n_total) return fail(e, GSX_EINVAL, "shard range outside the overlay");
     if (row_ptr[0] != 0) return fail(e, GSX_EINVAL, "row_ptr[0] must be 0");
     for (uint32_t i = 0; i < n_nodes; ++i)
@@ -1994,6 +2038,7 @@ int gsx_sync(gsx_engine* e) {
 
 int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
     if (!e || !s) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (!s->first_message_deliveries || !s->mesh_message_deliveries || !s->mesh_failure_penalty ||
         !s->invalid_message_deliveries || !s->graft_time_ns || !s->mesh_time_ns || !s->rec_flags ||
@@ -2032,6 +2077,7 @@ int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
 
 int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     if (!e || !sp) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (int rc = flush(e)) return rc;
     gsx::DevSynthSpec d{};
@@ -2060,6 +2106,7 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
 
 int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
     if (!e || !s) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (int rc = flush(e)) return rc;
     const size_t E = e->E, R = (size_t)e->T * E;
@@ -2339,6 +2386,9 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return fail(e, GSX_EINVAL, "bad message validation outcome");
     }
     if (cfg->validation_delay_ns < 0) return fail(e, GSX_EINVAL, "negative validation delay");
+    if (cfg->router == GSX_ROUTER_GOSSIPSUB && e->gp.gossip_exchange && m > GSX_GX_MAX_SET_MSGS)
+        return fail(e, GSX_ERANGE, "gossipsub batch above GSX_GX_MAX_SET_MSGS messages with the gossip exchange on "
+                                   "(split it over several calls)");
     if (e->n_nodes > gsx::PIN_NODE_MASK) return fail(e, GSX_ERANGE, "propagation needs < 2^28 nodes per engine");
     auto& P = e->prop;
     const bool scored = cfg->topic < e->T && e->scored[cfg->topic];
@@ -2794,6 +2844,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
 
 int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, gsx_prop_out* out) {
     if (!e || !cfg || !out) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->loaded && e->sharded())
         return fail(e, GSX_ESTATE, "sharded engine: drive hops with gsx_prop_begin/pack/step/end");
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
@@ -2835,6 +2886,7 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
 
 int gsx_prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
     if (!e) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
     if (e->loaded && e->sharded() && (e->n_ranks > 1) && !e->d_send_pair)
         return fail(e, GSX_ESTATE, "shard plan incomplete: gsx_shard_send_plan first");
@@ -3109,6 +3161,7 @@ int gsx_default_gossipsub_params(gsx_gossipsub_params* p) {
 // peer lists with D / Dscore, so negative or inverted degrees are refused.
 int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p) {
     if (!e || !p) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (p->d_lo < 0 || p->d < p->d_lo || p->d_hi < p->d || p->d_score < 0 || p->d_score > p->d_hi || p->d_out < 0 ||
         p->opportunistic_graft_peers < 0 || p->prune_backoff_ns < 0)
         return fail(e, GSX_EINVAL, "need 0 <= Dlo <= D <= Dhi, 0 <= Dscore <= Dhi, Dout, OG peers, backoff >= 0");
@@ -3386,13 +3439,14 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
             const size_t E = std::max<size_t>(e->E, 1);
             if (!e->d_gxs_out) {
                 int rc = 0;
-                if ((rc = dalloc(e, &e->d_gxs_out, E)) || (rc = dalloc(e, &e->d_gxs_rans, E)) ||
+                if ((rc = dalloc(e, &e->d_gxs_out, 2 * E)) || (rc = dalloc(e, &e->d_gxs_rans, E)) ||
                     (rc = dalloc(e, &e->d_gxs_hidx, E)) || (rc = dalloc(e, &e->d_gxs_cnt, (size_t)gsx::MAX_RANKS)) ||
                     (rc = dalloc(e, &e->d_gxs_off, (size_t)gsx::MAX_RANKS)))
                     return rc;
             }
-            HIPCHK(e, hipMemsetAsync(e->d_gxs_out, 0, 8 * E, e->stream));
+            HIPCHK(e, hipMemsetAsync(e->d_gxs_out, 0, 16 * E, e->stream));  // gxs_out, gxs_tro
             h.gxs_out = e->d_gxs_out;
+            h.gxs_tro = e->d_gxs_out + E;
             h.gxs_rans = e->d_gxs_rans;
             h.gxs_hidx = e->d_gxs_hidx;
         }
@@ -3594,9 +3648,19 @@ int gxf_alloc(gsx_engine* e) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         (void)hipFree(e->d_gxf_b0);
         e->d_gxf_b0 = nullptr;
-        e->gxf_b0_grps = std::max(n_grp, 2 * e->gxf_b0_grps);
-        if (int rc = dalloc(e, &e->d_gxf_b0, e->gxf_b0_grps * std::max<size_t>(e->E, 1))) return rc;
+        const size_t grps = std::max(n_grp, 2 * e->gxf_b0_grps);
+        e->gxf_b0_grps = 0;  // (a failed allocation leaves none: the next call retries)
+        if (int rc = dalloc(e, &e->d_gxf_b0, grps * std::max<size_t>(e->E, 1))) return rc;
+        e->gxf_b0_grps = grps;
         HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * std::max<size_t>(e->E, 1), e->stream));  // (bst0: no stale stamps)
+    }
+    if (e->d_gxf_bst && !e->d_gxf_b0) {  // a regrowth failed before: allocate the group counts again
+        e->gxf_b0_grps = std::max<size_t>(n_grp, 1);
+        if (int rc = dalloc(e, &e->d_gxf_b0, e->gxf_b0_grps * std::max<size_t>(e->E, 1))) {
+            e->gxf_b0_grps = 0;
+            return rc;
+        }
+        HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
     }
     if (e->d_gxf_bst) {
         if (e->gxf_stamp < 0xF0000000u) return GSX_OK;
@@ -3842,8 +3906,10 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         size_t msgs = 0;
         for (size_t i = 0; i < R.sets.size(); ++i) {
             const gsx_engine::MsgSet* ms = R.sets[i];
-            if (ms->n_msgs > 65535) return fail(e, GSX_ERANGE, "gossip exchange: a message set above 65,535 messages");
-            if (R.grp_topic.empty() || R.grp_topic.back() != ms->topic || cnt == 64 || msgs + ms->n_msgs > 65535) {
+            if (ms->n_msgs > GSX_GX_MAX_SET_MSGS)  // (cached before the exchange was turned on)
+                return fail(e, GSX_ERANGE, "gossip exchange: a cached message set above GSX_GX_MAX_SET_MSGS messages");
+            if (R.grp_topic.empty() || R.grp_topic.back() != ms->topic || cnt == 64 ||
+                msgs + ms->n_msgs > GSX_GX_MAX_SET_MSGS) {
                 R.grp_topic.push_back(ms->topic);
                 cnt = 0;
                 msgs = 0;
@@ -4112,9 +4178,6 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     dbg_host("hb shift+put");
     if (gflag[0] || gflag[1])
         return fail(e, GSX_ESTATE, "gossip exchange: internal bound broken (truncated-list rows / promise slots)");
-    if (gflag[2])
-        return fail(e, GSX_ERANGE, "gossip exchange across range shards: an IHAVE list was truncated "
-                                   "(MaxIHaveLength) on a cross-shard pair, which the shard exchange does not carry");
     // every pair keeps a free promise slot for the next exchange (one promise per pair each)
     if (gx_run && gflag[4] >= e->prom_slots)
         if (int rc = gx_prom_grow(e)) return rc;
@@ -4146,17 +4209,26 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     R.h = h;
     dbg_host("hb (B)(C)");
     if (R.run) {
-        if (int rc = gx_prepare(e, R)) return rc;
-        if (e->sharded()) {  // the gsx_gx_* steps carry (D) across the ranks, gsx_gx_end finishes the round
+        int rc = gx_prepare(e, R);
+        if (!rc && e->sharded()) {  // the gsx_gx_* steps carry (D) across the ranks, gsx_gx_end finishes the round
             R.pending = true;
             R.stage = 1;
             return GSX_OK;
         }
-        if (int rc = gx_ready(e, R)) return rc;
-        HIPCHK(e, gsx::launch_gx_exchange(ds, R.h, e->stream));
+        if (!rc) rc = gx_ready(e, R);
+        if (!rc) {
+            const hipError_t st = gsx::launch_gx_exchange(ds, R.h, e->stream);
+            if (st != hipSuccess) rc = fail(e, GSX_EDEVICE, std::string("launch_gx_exchange: ") + hipGetErrorString(st));
+        }
         // the recovered messages published on (their forwarded first receipts join the receipt rows)
-        if (int rc = gx_forward(e, R)) return rc;
-        if (int rc = gx_merge(e, R)) return rc;
+        if (!rc) rc = gx_forward(e, R);
+        if (!rc) rc = gx_merge(e, R);
+        if (rc) {  // the sets' references and rows back to the pools (the round is lost)
+            const std::string msg = e->err;
+            gx_abort(e);
+            e->err = msg;
+            return rc;
+        }
     }
     return hb_finish(e, R, out, nullptr);
 }
@@ -4313,6 +4385,7 @@ int gsx_promise_count(gsx_engine* e, uint64_t* n) {
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_heartbeat_out* out) {
     if (!e || !out) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->loaded && e->sharded()) return fail(e, GSX_ESTATE, "sharded engine: drive the round with gsx_hb_*");
     if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
     if (int rc = hb_begin(e, tick, now, seed)) return rc;
@@ -4322,6 +4395,7 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
 
 int gsx_hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {
     if (!e) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
     return hb_begin(e, tick, now, seed);
 }
@@ -4418,6 +4492,7 @@ int gsx_hb_px_recv(gsx_engine* e, uint32_t kind, const uint32_t* entries, uint64
 
 int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     if (!e || !out) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (!e->hb_active) return fail(e, GSX_ESTATE, "gsx_hb_begin first");
     if (e->n_recv && !halo_resp) return GSX_EINVAL;
     return hb_end(e, halo_resp, out);
@@ -4634,6 +4709,7 @@ int gsx_gx_end(gsx_engine* e, const uint8_t* got_all, gsx_heartbeat_out* out) {
 
 int gsx_set_subscriptions(gsx_engine* e, const uint64_t* joined) {
     if (!e || !joined) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
     if (int rc = members_init(e)) return rc;
     const uint64_t all = e->T >= 64 ? ~0ull : ((1ull << e->T) - 1);
@@ -4672,6 +4748,7 @@ namespace {
 int member_round(gsx_engine* e, const uint32_t* nodes, const uint32_t* topics, size_t n, int64_t now, uint64_t seed,
                  bool leave, gsx_heartbeat_out* out) {
     if (!e || (!nodes && n) || (!topics && n) || !out) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (e->hb_active) return fail(e, GSX_ESTATE, "a stepped heartbeat is in flight");
     if (e->max_deg > gsx::HB_HUB_MAX)
         return fail(e, GSX_ERANGE, "membership changes support at most " + std::to_string(gsx::HB_HUB_MAX) + " peers per node");
@@ -4833,6 +4910,7 @@ int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_wind
 
 int gsx_mcache_clear(gsx_engine* e) {
     if (!e) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     mcache_clear(e);
     return GSX_OK;
@@ -4842,6 +4920,7 @@ int gsx_mcache_clear(gsx_engine* e) {
 
 namespace {
 int mcache_ready(gsx_engine* e) {
+    if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (e->sharded()) return fail(e, GSX_ESTATE, "block merging runs on unsharded engines (replicas)");
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
@@ -4891,6 +4970,8 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
     if (int rc = mcache_ready(e)) return rc;
     if (cfg->router != GSX_ROUTER_GOSSIPSUB) return fail(e, GSX_EINVAL, "only gossipsub batches are cached");
     if (m > 0xFFFFFFFFull) return fail(e, GSX_ERANGE, "batch too large");
+    if (e->gp.gossip_exchange && m > GSX_GX_MAX_SET_MSGS)
+        return fail(e, GSX_ERANGE, "batch above GSX_GX_MAX_SET_MSGS messages with the gossip exchange on");
     for (size_t k = 0; k < m; ++k) {
         if (msgs[k].source >= e->n_total) return fail(e, GSX_ERANGE, "message source out of range");
         if (msgs[k].validation > GSX_VALIDATION_THROTTLE) return fail(e, GSX_EINVAL, "bad message validation outcome");
@@ -4983,6 +5064,7 @@ int gsx_export_backoff(gsx_engine* e, int64_t* out) {
 
 int gsx_import_backoff(gsx_engine* e, const int64_t* in) {
     if (!e || !in) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     const size_t TE = (size_t)e->T * e->E;
     if (TE) HIPCHK(e, hipMemcpyAsync(e->d_backoff, in, 8 * TE, hipMemcpyHostToDevice, e->stream));

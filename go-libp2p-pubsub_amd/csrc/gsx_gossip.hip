@@ -1454,9 +1454,21 @@ __global__ __launch_bounds__(256) void k_gxs_rows(HbState h, GxsPlan P, const Gx
         if (!out) continue;
         uint64_t* e = out + (size_t)(off[d] + k) * (h.gxs_fw + 1);
         e[0] = P.dest_halo_base[d] + (j - P.send_base[d]);  // the receive slot at the destination
+        // a truncated list reaches the receiver as its subset: the rows of that
+        // topic's batches go masked with the subset row v kept for this pair, so
+        // the receiver's handleIHave sees exactly the ids of the IHAVE it got
+        const uint64_t tro = h.gxs_tro ? h.gxs_tro[r] : 0ull;
         for (uint32_t g = 0; g < n_gx; ++g) {
             const GxBatch& b = gx[g];
-            for (uint32_t w = 0; w < b.n_words; ++w) e[1 + b.woff + w] = b.mem[(size_t)v * b.n_words + w];
+            const uint64_t* sub = nullptr;
+            if ((tro >> b.topic) & 1) {
+                const GxSub& G = h.gsubs[b.topic];
+                sub = G.pool + (size_t)G.idx[r] * G.tw + b.row_off;
+            }
+            for (uint32_t w = 0; w < b.n_words; ++w) {
+                const uint64_t m = b.mem[(size_t)v * b.n_words + w];
+                e[1 + b.woff + w] = sub ? m & sub[w] : m;
+            }
         }
     }
 }

@@ -1214,23 +1214,25 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 for (uint32_t w = lane; w < tw; w += 64)
                     for (uint64_t m = sel[w]; m; m &= m - 1) d += h.mc_digest[slot0 + w * 64 + (uint32_t)__builtin_ctzll(m)];
                 d = wave_sum64(d);
-                uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
+                const uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
                 if (lane == 0) {
                     h.ihave_len[tslot + r] = maxl;
                     h.ihave_hash[tslot + r] = take ? d : dall - d;
                     ihave_mark(h, (uint64_t)r, t);
                 }
-                if (q != NO_PAIR && (q & HALO)) {  // a truncated list across shards: refused (gsx.h)
-                    if (lane == 0) h.gx_err[2] = 1;
-                    q = NO_PAIR;
-                }
-                if (q != NO_PAIR && h.gsub.pool) {  // the subset the receiver's handleIHave reads (D)
+                // the subset the receiver's handleIHave reads (D): marked at the
+                // receiver's pair, or for a receiver on another range shard at the
+                // sender's pair, whose cache rows travel masked with it (k_gxs_rows)
+                if (q != NO_PAIR && h.gsub.pool && (!(q & HALO) || h.gxs_tro)) {
                     uint32_t x = 0;
                     if (lane == 0) {
                         x = atomicAdd(h.gsub.cnt, 1u);
                         if (x < h.gsub.cap) {
                             h.gsub.idx[r] = x;
-                            h.ihave_tr[q] |= 1ull << t;
+                            if (q & HALO)
+                                h.gxs_tro[r] |= 1ull << t;
+                            else
+                                h.ihave_tr[q] |= 1ull << t;
                         } else {
                             h.gx_err[0] = 1;  // (the host bounds the targets: never)
                         }

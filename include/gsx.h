@@ -604,6 +604,12 @@ typedef struct gsx_gossipsub_params {
     int32_t prune_peers;                    /* :46 (GossipSubPrunePeers = 16)    */
 } gsx_gossipsub_params;
 
+/* With gossip_exchange on, one gossipsub batch (a gsx_propagate / gsx_prop_begin
+ * call, or a gsx_mcache_put) holds at most this many messages (GSX_ERANGE
+ * otherwise: split the batch over several calls); the forwarding of recovered
+ * messages counts back-sends per message set group in 16 bits. */
+#define GSX_GX_MAX_SET_MSGS 65535u
+
 int gsx_default_gossipsub_params(gsx_gossipsub_params* out);
 int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
 
@@ -761,7 +767,13 @@ int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out)
  * recovered messages needs the senders' topic slots and, per hop, their
  * frontier rows and back-send counts.  All travel as entries routed by the
  * shard plan's receive slots.  An IHAVE list truncated to MaxIHaveLength on
- * a cross-shard pair is refused (GSX_ERANGE at gsx_gx_end).
+ * a cross-shard pair reaches the receiver as the subset its target got: the
+ * sender's rank draws it as one engine does (the draws are keyed by global
+ * node ids) and sends that topic's cache rows of the pair masked with it, so
+ * the entry layout is the same for whole and truncated lists.
+ * While a sharded exchange is in flight (gsx_gx_pending), every call that
+ * starts a round, a propagation, a Join / Leave or a state import / export
+ * fails with GSX_ESTATE until gsx_gx_end.
  *   gsx_gx_pending      1 when one is in flight (*n_sets: its message sets), else 0
  *   gsx_gx_common       this rank's common words, [n_sets][64] u64 (host): the
  *                       messages every node of the rank had seen

@@ -180,6 +180,99 @@ def test_cfg3_gossip_exchange_1m_x_8_matches_oracle(gpu_ok):
     assert tot["fwd_delivered"] > 0 and tot["fwd_duplicates"] > 0, tot
 
 
+@pytest.mark.timeout(1500)
+def test_cfg3_sharded_gossip_exchange_1m_matches_single_engine(gpu_ok):
+    """The gossip exchange on range shards at cfg3's size: 1M peers in two
+    RangeSharded shards (lock-step threads on one GPU) against the unsharded
+    engine, through propagate -> heartbeat rounds whose gossip windows hold
+    more ids than the reference's MaxIHaveLength of 5000 (2,048-message
+    batches that travel 3 hops), so most IHAVE lists are truncated per target
+    and cross the shards as subsets.  Counters summed over the ranks, scores,
+    backoff and records of every node equal the single engine's."""
+    import gossip_cases as gc
+    from gsx import shard
+
+    n, T, seed, world = 1_000_000, 2, synth.SEED, 2
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    spec = abi.SynthSpec(seed=seed, now_ns=pc.T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0, imd_max_sybil=100.0,
+                         p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0, p_disconnected=0.0, p_absent=0.0,
+                         expire_jitter_ns=4 * S, sybil_first_node=n)
+    gp = gc.params(iwant_followup_ns=S // 2)
+    full = gsx.Engine(T)
+    full.set_peer_params(synth.bench_peer_params())
+    for t in range(T):
+        full.set_topic_params(t, synth.spam_test_topic_params())
+    full.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                       accept_px_threshold=0, opportunistic_graft_threshold=5))
+    full.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    full.synthesize_state(spec)
+    full.set_app_scores(np.zeros(ov.n_pairs))
+    full.refresh(pc.T0 + S)
+    full.set_gossipsub_params(gp)
+    st = full.export_state()
+    E = ov.n_pairs
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        sh = synth.shard_of(ov, lo, hi)
+        e = gsx.Engine(T)
+        e.set_peer_params(synth.bench_peer_params())
+        for t in range(T):
+            e.set_topic_params(t, synth.spam_test_topic_params())
+        e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                                        accept_px_threshold=0, opportunistic_graft_threshold=5))
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        sl = {}
+        for f in abi.STATE_FIELDS:
+            x = st[f]
+            sl[f] = x.reshape(T, E)[:, a:b].reshape(-1).copy() if f in abi.RECORD_FIELDS else x[a:b].copy()
+        sl["last_refresh_ns"] = st["last_refresh_ns"]
+        e.import_state(sl)
+        e.set_app_scores(np.zeros(b - a))
+        e.set_gossipsub_params(gp)
+        engines.append((e, a, b, lo, hi))
+        del sh, sl
+    del st
+    runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
+                              [(x[0],) for x in engines])
+    tot, truncated = {}, 0
+    for k in range(4):
+        now = pc.T0 + (2 + k) * S
+        cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=0, max_hops=3, latency_ms=10, seed=7 + k)
+        cfg.now_ns = now
+        ms = pc.messages(n, 2048, 100 + k)
+        want = full.propagate(ms, cfg)[0].as_dict()
+        res = shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(ms, cfg))[1],
+                              [(r,) for r in runners])
+        for x in ("deliveries", "duplicates", "transmissions", "hops"):
+            assert res[0][1][x] == want[x], (k, x)
+        tick, hn = 61 + k, now + 500 * abi.MILLISECOND
+        want = full.heartbeat(tick, hn, seed).as_dict()
+        res = shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.heartbeat(tick, hn, seed))[1],
+                              [(r,) for r in runners])
+        assert res[0][1] == want, (k, {x: (res[0][1][x], want[x]) for x in want if res[0][1][x] != want[x]})
+        for x, v in want.items():
+            tot[x] = tot.get(x, 0) + v
+        sc, bo = full.scores(), np.asarray(full.export_backoff()).reshape(T, E)
+        il = np.asarray(full.gossip_results()[0]).reshape(T, E)
+        fs = full.export_state()
+        for (e, a, b, lo, hi) in engines:
+            _same(e.scores(), sc[a:b], (k, "scores"))
+            _same(np.asarray(e.export_backoff()).reshape(T, b - a), bo[:, a:b], (k, "backoff"))
+            es = e.export_state()
+            for f in abi.STATE_FIELDS:
+                w = fs[f].reshape(T, E)[:, a:b].reshape(-1) if f in abi.RECORD_FIELDS else fs[f][a:b]
+                _same(es[f], w, (k, f))
+            del es
+            cross = (ov.col[a:b] < lo) | (ov.col[a:b] >= hi)
+            truncated += int(((il[:, a:b] == gp.max_ihave_length) & cross[None, :]).sum())
+        del fs
+    assert tot["iwant_msgs"] > 0 and tot["gossip_delivered"] > 0 and tot["fwd_delivered"] > 0, tot
+    assert truncated > 0
+
+
 def _bfs(row_ptr, col, src):
     """Level-synchronous BFS over a CSR overlay (numpy): hop distance per node, -1 unreached."""
     n = len(row_ptr) - 1

@@ -243,15 +243,22 @@ def test_sharded_heartbeat_matches_single_engine(gpu_ok, world):
     assert want["grafts"] + want["prunes"] > 0
 
 
-@pytest.mark.parametrize("world,invalid,T", [(2, 0.0, 2), (3, 0.2, 2), (2, 0.0, 1)])
-def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid, T):
+@pytest.mark.parametrize("world,invalid,T,max_ihave,m",
+                         [(2, 0.0, 2, 5000, 24), (3, 0.2, 2, 5000, 24), (2, 0.0, 1, 5000, 24),
+                          (2, 0.0, 2, 20, 24), (3, 0.2, 1, 20, 24), (3, 0.0, 1, 5000, 2600)],
+                         ids=["w2-T2", "w3-T2-invalid", "w2-T1", "w2-T2-trunc20", "w3-T1-trunc20-invalid",
+                              "w3-T1-trunc5000"])
+def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid, T, max_ihave, m):
     """The gossip exchange on range shards (gsx_gx_*: IHAVE bits and answer
     bits of cross-shard pairs, the senders' cache rows, the forwarding of
     recovered messages hop by hop with frontier entries): rounds of a
     heartbeat with the exchange on, then a gossipsub batch that travels two
     hops (most nodes miss it and recover it by IHAVE / IWANT and the
     recovering nodes' forwarding), == one engine: counters summed over ranks,
-    every node's records, backoff, IHAVEs, scores and cached ids."""
+    every node's records, backoff, IHAVEs, scores and cached ids.  The trunc
+    cases hold more ids in the gossip window than MaxIHaveLength (20, or the
+    reference's 5000 with 2,600-message batches): every target gets its own
+    subset (gossipsub.go:1708-1720), which crosses the shards as masked rows."""
     import gossip_cases as gc
     import heartbeat_cases as hc
 
@@ -259,7 +266,7 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
     ov = pc.overlay(n, d, seed)
     full = gsx.Engine(T)
     app = pc.setup(full, ov, T, seed, mesh_degree=6)
-    gp = gc.params()
+    gp = gc.params(max_ihave_length=max_ihave)
     full.set_gossipsub_params(gp)
     st0 = full.export_state()
     E = ov.n_pairs
@@ -279,6 +286,7 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
     runners = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp),
                               [(x[0],) for x in engines])
     tot = {}
+    truncated = 0
     for k in range(6):
         tick, now = 1 + k, pc.T0 + (3 + k) * abi.SECOND
         want = full.heartbeat(tick, now, seed * 31 + 7).as_dict()
@@ -289,6 +297,7 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
         for x, v in want.items():
             tot[x] = tot.get(x, 0) + v
         snap = hc.snapshot(full)
+        il = np.asarray(snap["ihave_len"]).reshape(T, E)
         for (e, a, b, lo, hi) in engines:
             got = hc.snapshot(e)
             for f in abi.STATE_FIELDS:
@@ -300,9 +309,12 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
             for v in range(lo, hi, 37):  # the caches (recovered copies Put)
                 assert sorted(e.mcache_ids(v - lo, abi.GSX_ANY_TOPIC, 5).tolist()) == \
                     sorted(full.mcache_ids(v, abi.GSX_ANY_TOPIC, 5).tolist()), (k, v)
+            # truncated lists sent over this rank's cross-shard pairs (the case under test)
+            cross = (ov.col[a:b] < lo) | (ov.col[a:b] >= hi)
+            truncated += int(((il[:, a:b] == max_ihave) & cross[None, :]).sum())
         cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=k % T, max_hops=2, latency_ms=5, seed=seed + k)
         cfg.now_ns = now + 100 * abi.MILLISECOND
-        ms = pc.messages(n, 24, seed + 1000 * k, invalid=invalid)
+        ms = pc.messages(n, m, seed + 1000 * k, invalid=invalid)
         full.propagate(ms, cfg)
         shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(ms, cfg))[1],
                         [(r,) for r in runners])
@@ -310,6 +322,8 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
         for (e, _, _, _, _) in engines:
             e.refresh(now + 500 * abi.MILLISECOND)
     assert tot["iwant_msgs"] > 0 and tot["gossip_delivered"] > 0 and tot["fwd_delivered"] > 0, tot
+    if max_ihave < 5000 or m > 1000:
+        assert truncated > 0
 
 
 @pytest.mark.parametrize("world,invalid", [(2, 0.0), (3, 0.2)])
@@ -397,3 +411,57 @@ def test_sharded_heartbeat_peer_exchange_matches_single_engine(gpu_ok, world):
         rk = np.searchsorted(rank_lo, recs[:, [0, 2]].astype(np.int64), side="right") - 1
         cross += int((rk[:, 0] != rk[:, 1]).sum())  # PX lists that travelled to another rank
     assert tot_px > 0 and tot_connect > 0 and cross > 0, (tot_px, tot_connect, cross)
+
+
+def test_sharded_exchange_pending_refuses_other_calls(gpu_ok):
+    """While a sharded gossip exchange is in flight (gsx_hb_end .. gsx_gx_end)
+    a new round, a propagation, a state import / export or the backoff import
+    is refused with GSX_ESTATE (the exchange holds the round's sets and the
+    mcache Shift); the exchange then completes as usual."""
+    import gossip_cases as gc
+
+    n, d, seed, T, world = 600, 6, 53, 1, 2
+    ov = pc.overlay(n, d, seed)
+    full = gsx.Engine(T)
+    app = pc.setup(full, ov, T, seed, mesh_degree=6)
+    gp = gc.params()
+    st0 = full.export_state()
+    E = ov.n_pairs
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        sh = synth.shard_of(ov, lo, hi)
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        e = gsx.Engine(T)
+        _params(e, T)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(_slice_state(st0, T, E, a, b))
+        e.set_app_scores(app[a:b])
+        e.set_gossipsub_params(gp)
+        engines.append(e)
+    refused = []
+
+    class Probe(shard.RangeSharded):
+        def _gx_exchange(self, n_sets):
+            be = self.be
+            assert be.gx_pending() is not None
+            for call in (lambda: be.hb_begin(9, pc.T0, 1), lambda: be.export_state(),
+                         lambda: be.prop_begin(pc.messages(n, 4, 1), pc.config(abi.GSX_ROUTER_GOSSIPSUB)),
+                         lambda: be.import_backoff(np.zeros((T, be.n_pairs), dtype=np.int64))):
+                with pytest.raises(gsx.GsxError) as ex:
+                    call()
+                refused.append(ex.value.code == abi.GSX_ESTATE)
+            return super()._gx_exchange(n_sets)
+
+    runners = shard.run_local(world, "cuda:0", lambda tp, e: Probe(e, rank_lo, tp), [(e,) for e in engines])
+    cfg = pc.config(abi.GSX_ROUTER_GOSSIPSUB, topic=0, max_hops=2, latency_ms=5, seed=seed)
+    ms = pc.messages(n, 40, seed)
+    shard.run_local(world, "cuda:0", lambda tp, r: (setattr(r, "tp", tp), r.propagate(ms, cfg))[1],
+                    [(r,) for r in runners])
+    res = shard.run_local(world, "cuda:0",
+                          lambda tp, r: (setattr(r, "tp", tp), r.heartbeat(1, pc.T0 + abi.SECOND, 5))[1],
+                          [(r,) for r in runners])
+    assert refused and all(refused), refused
+    assert all(e.gx_pending() is None for e in engines)
+    assert res[0][1]["iwant_msgs"] > 0
