@@ -704,12 +704,13 @@ hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const ui
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
                                const uint32_t* group_off, uint32_t n_groups, hipStream_t st);
 hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st);
-// The drop-in round trip (k_dropin): events + score() of their observers' rows
-// into the device vector and the host-mapped copy, then `tag` into the
-// host-mapped flag (system scope).  One workgroup.
+// The drop-in round trip (k_dropin): events + score() of the pairs they change
+// (prs; the whole row of the observers in obs: AddPeer / RemovePeer move their
+// IP colocation counts) into the device vector and the host-mapped copy, then
+// `tag` into the host-mapped flag (system scope).  One workgroup.
 hipError_t launch_dropin(const DevState& s, const DevPeerParams& pp, const DevEvent* ev, const uint32_t* goff,
-                         uint32_t n_groups, const uint32_t* obs, uint32_t n_obs, const int64_t* row_ptr,
-                         double* hscore, uint32_t* flag, uint32_t tag, hipStream_t st);
+                         uint32_t n_groups, const uint32_t* obs, uint32_t n_obs, const uint64_t* prs, uint32_t n_prs,
+                         const int64_t* row_ptr, double* hscore, uint32_t* flag, uint32_t tag, hipStream_t st);
 hipError_t launch_gather_scores(const double* score, const uint64_t* pairs, uint64_t n, double* out, hipStream_t st);
 hipError_t launch_rebuild_ipcount(const DevState& s, uint32_t n_groups_ip, hipStream_t st);
 hipError_t launch_synthesize(const DevState& s, const int32_t* col, const DevSynthSpec& spec, hipStream_t st);

@@ -1871,10 +1871,12 @@ int gsx_scores(gsx_engine* e, double* out, size_t n) {
 }
 
 // The drop-in round trip in one launch (k_dropin): the queued tracer events
-// of a small engine whose host score copy was current are applied and their
-// observers' rows re-scored into both copies; the host polls a mapped flag.
-// Returns 1 when it ran, 0 when the case does not apply (the general path
-// follows), < 0 on error.
+// of a small engine whose host score copy was current are applied and the
+// scores they change re-scored into both copies — the event pairs, and the
+// rows of observers with an AddPeer / RemovePeer (their IP groups' P6) — so
+// the cost follows the events, not the router's peer count; the host polls a
+// mapped flag.  Returns 1 when it ran, 0 when the case does not apply (the
+// general path follows), < 0 on error.
 constexpr size_t kDropinMaxEvents = 4096, kDropinMaxObs = 64;
 int dropin_fast(gsx_engine* e) {
     if (e->pending.empty() || e->E > kHostScoreMax || !e->h_score_dev || e->h_score_cap < e->E ||
@@ -1892,7 +1894,8 @@ int dropin_fast(gsx_engine* e) {
     std::vector<uint32_t> order(n);
     for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return obs[a] < obs[b]; });
-    std::vector<uint32_t> goff, gobs;
+    std::vector<uint32_t> goff, gobs, rows;
+    std::vector<uint64_t> prs;
     for (size_t i = 0; i < n; ++i)
         if (i == 0 || obs[order[i]] != obs[order[i - 1]]) {
             goff.push_back((uint32_t)i);
@@ -1900,15 +1903,32 @@ int dropin_fast(gsx_engine* e) {
         }
     if (gobs.size() > kDropinMaxObs) return 0;
     goff.push_back((uint32_t)n);
+    for (size_t g = 0; g + 1 < goff.size(); ++g) {  // per observer: its whole row, or the event pairs
+        bool row = false;
+        for (uint32_t i = goff[g]; i < goff[g + 1] && !row; ++i) {
+            const uint32_t k = e->pending[order[i]].kind;
+            row = k == GSX_EV_ADD_PEER || k == GSX_EV_REMOVE_PEER;
+        }
+        if (row) {
+            rows.push_back(gobs[g]);
+            continue;
+        }
+        const size_t p0 = prs.size();
+        for (uint32_t i = goff[g]; i < goff[g + 1]; ++i) prs.push_back(e->pending[order[i]].pair);
+        std::sort(prs.begin() + (long)p0, prs.end());
+        prs.erase(std::unique(prs.begin() + (long)p0, prs.end()), prs.end());
+    }
     const size_t ev_off = 64, ev_b = sizeof(gsx::DevEvent) * n;
     const size_t go_off = ev_off + ev_b, go_b = 4 * goff.size();
-    const size_t ob_off = go_off + go_b, ob_b = 4 * gobs.size();
-    const size_t need = ob_off + ob_b;
+    const size_t ob_off = go_off + go_b, ob_b = 4 * std::max<size_t>(rows.size(), 1);
+    const size_t pr_off = (ob_off + ob_b + 7) & ~(size_t)7, pr_b = 8 * std::max<size_t>(prs.size(), 1);
+    const size_t need = pr_off + pr_b;
     if (e->h_dropin_bytes < need) {
         if (e->h_dropin) (void)hipHostFree(e->h_dropin);
         e->h_dropin = nullptr;
         e->h_dropin_bytes = 0;
-        const size_t want = std::max<size_t>(need, 64 + (sizeof(gsx::DevEvent) + 8) * kDropinMaxEvents + 4 * kDropinMaxObs);
+        const size_t want =
+            std::max<size_t>(need, 128 + (sizeof(gsx::DevEvent) + 16) * kDropinMaxEvents + 8 * kDropinMaxObs);
         HIPCHK(e, hipHostMalloc(&e->h_dropin, want, hipHostMallocMapped | hipHostMallocCoherent));
         void* dp = nullptr;
         HIPCHK(e, hipHostGetDevicePointer(&dp, e->h_dropin, 0));
@@ -1923,12 +1943,14 @@ int dropin_fast(gsx_engine* e) {
         hev[i] = gsx::DevEvent{x.kind, x.topic, x.pair, x.now_ns, x.arg};
     }
     std::memcpy(hb + go_off, goff.data(), go_b);
-    std::memcpy(hb + ob_off, gobs.data(), ob_b);
+    if (!rows.empty()) std::memcpy(hb + ob_off, rows.data(), 4 * rows.size());
+    if (!prs.empty()) std::memcpy(hb + pr_off, prs.data(), 8 * prs.size());
     std::atomic_thread_fence(std::memory_order_release);
     const uint32_t tag = ++e->dropin_tag;
     HIPCHK(e, gsx::launch_dropin(dev_state(e), dev_peer_params(e), reinterpret_cast<const gsx::DevEvent*>(e->d_dropin + ev_off),
                                  reinterpret_cast<const uint32_t*>(e->d_dropin + go_off), (uint32_t)gobs.size(),
-                                 reinterpret_cast<const uint32_t*>(e->d_dropin + ob_off), (uint32_t)gobs.size(),
+                                 reinterpret_cast<const uint32_t*>(e->d_dropin + ob_off), (uint32_t)rows.size(),
+                                 reinterpret_cast<const uint64_t*>(e->d_dropin + pr_off), (uint32_t)prs.size(),
                                  e->d_row_ptr, e->h_score_dev, reinterpret_cast<uint32_t*>(e->d_dropin), tag, e->stream));
     e->pending.clear();
     const volatile uint32_t* flag = static_cast<const volatile uint32_t*>(e->h_dropin);

@@ -286,6 +286,12 @@ __device__ __forceinline__ void gx_back0(const HbState& h, uint64_t q, uint32_t 
     h.gxb_cnt0[(size_t)grp * h.n_pairs + q] += k_in | k_out << 16;
 }
 
+// The IWANT draws of pair q = (u -> v) (the asked subset, AddPromise's pick):
+// keyed by the global node ids, so a range shard draws what one engine draws.
+__device__ __forceinline__ Rng gx_iwant_rng(const HbState& h, uint32_t u, uint32_t v) {
+    return Rng{h.seed, TAG_IWANT, ((uint64_t)(h.node_lo + u) << 32) | v, h.tick << 32, 0};
+}
+
 // handleIWant at v and the receipt at u, one id at a time (pass 2 for a pair
 // whose asked subset was sampled, kk < n: the same draws select it again),
 // each receipt credited by its own tracer call.
@@ -294,7 +300,7 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
                                                    uint64_t& delivered, uint64_t& rejected, uint64_t& dups) {
     const uint32_t v = (uint32_t)h.col[q];
     const DevGossipParams& gp = h.gp;
-    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+    Rng g = gx_iwant_rng(h, u, v);
     uint32_t i = 0, sel = 0;
     gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
         const bool take = (uint32_t)g.int31n((int32_t)(n - i)) < kk - sel;
@@ -463,7 +469,7 @@ __device__ __forceinline__ void gx_promise(const HbState& h, uint64_t q, uint64_
 __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, uint32_t u, uint32_t v, uint64_t q,
                                                 uint32_t r, uint32_t n, uint32_t kk, uint32_t& pick_g,
                                                 uint32_t& pick_k) {
-    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+    Rng g = gx_iwant_rng(h, u, v);
     uint32_t i = 0, sel = 0;
     gx_walk(h, tb, u, v, q, r, [&](uint32_t, uint32_t) {
         if ((uint32_t)g.int31n((int32_t)(n - i)) < kk - sel) ++sel;
@@ -471,7 +477,7 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
         return sel < kk;
     });
     const uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-    Rng g2{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};  // the same selection again
+    Rng g2 = gx_iwant_rng(h, u, v);  // the same selection again
     i = 0;
     sel = 0;
     gx_walk(h, tb, u, v, q, r, [&](uint32_t gi, uint32_t k) {
@@ -594,7 +600,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             const uint32_t kk = n < budget ? n : budget;
             uint32_t pick_g = 0, pick_k = 0;
             if (kk == n) {  // the element at Int31n(kk) of all of them, canonical order
-                Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+                Rng g = gx_iwant_rng(h, uu, v);
                 uint32_t j = (uint32_t)g.int31n((int32_t)kk);
                 for (uint32_t i = 0; i < nml; ++i) {
                     const uint32_t gw = ml_gw[i][k], gi = gw >> 6, w = gw & 63u;
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 const uint32_t kk = n < budget ? n : budget;
                 uint32_t pick_g = 0, pick_k = 0;
                 if (kk == n) {
-                    Rng g{h.seed, TAG_IWANT, (uint64_t)q, h.tick << 32, 0};
+                    Rng g = gx_iwant_rng(h, u, v);
                     gx_wnth(h, tb, u, (uint64_t)q, v, tr, r, nf, lane, (uint32_t)g.int31n((int32_t)kk), pick_g, pick_k);
                 } else if (lane == 0) {
                     gx_pick_sampled(h, tb, u, v, q, r, n, kk, pick_g, pick_k);

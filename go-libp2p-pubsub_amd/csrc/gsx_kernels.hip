@@ -166,14 +166,19 @@ __global__ __launch_bounds__(64) void k_apply_events(DevState s, DevPeerParams p
 // on an engine small enough to keep a host copy of its scores, when that copy
 // was current before the queued tracer events): one workgroup applies the
 // events (read from host-mapped memory, grouped by observer), then score()s
-// the rows of those observers (eval_pair: the same operations as the score
-// pass) into the device vector and the host copy (host-mapped), then stores
-// `tag` to a host-mapped flag at system scope; the host polls the flag instead
-// of synchronising the stream.
+// what they changed (eval_pair: the same operations as the score pass) into
+// the device vector and the host copy (host-mapped): the event pairs
+// themselves (a delivery, Graft / Prune, penalty or application score changes
+// only its own pair's score), and the whole row of an observer with an
+// AddPeer / RemovePeer (the IP colocation counts every pair of its IP groups
+// reads); then stores `tag` to a host-mapped flag at system scope, which the
+// host polls instead of synchronising the stream.  The work is the events',
+// not the router's peer count.
 __global__ __launch_bounds__(1024) void k_dropin(DevState s, DevPeerParams pp, const DevEvent* ev,
                                                  const uint32_t* goff, uint32_t n_groups, const uint32_t* obs,
-                                                 uint32_t n_obs, const int64_t* __restrict__ row_ptr, double* hscore,
-                                                 uint32_t* flag, uint32_t tag) {
+                                                 uint32_t n_obs, const uint64_t* prs, uint32_t n_prs,
+                                                 const int64_t* __restrict__ row_ptr, double* hscore, uint32_t* flag,
+                                                 uint32_t tag) {
     for (uint32_t g = threadIdx.x; g < n_groups; g += blockDim.x)
         for (uint32_t i = goff[g]; i < goff[g + 1]; ++i) apply_event(s, pp, ev[i]);
     __threadfence();
@@ -185,6 +190,12 @@ __global__ __launch_bounds__(1024) void k_dropin(DevState s, DevPeerParams pp, c
             s.score[p] = v;
             hscore[p] = v;
         }
+    }
+    for (uint32_t i = threadIdx.x; i < n_prs; i += blockDim.x) {
+        const uint64_t p = prs[i];
+        const double v = eval_pair(s, pp, p);
+        s.score[p] = v;
+        hscore[p] = v;
     }
     __threadfence_system();
     __syncthreads();
@@ -399,10 +410,10 @@ hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const
 }
 
 hipError_t launch_dropin(const DevState& s, const DevPeerParams& pp, const DevEvent* ev, const uint32_t* goff,
-                         uint32_t n_groups, const uint32_t* obs, uint32_t n_obs, const int64_t* row_ptr,
-                         double* hscore, uint32_t* flag, uint32_t tag, hipStream_t st) {
-    hipLaunchKernelGGL(k_dropin, dim3(1), dim3(1024), 0, st, s, pp, ev, goff, n_groups, obs, n_obs, row_ptr, hscore,
-                       flag, tag);
+                         uint32_t n_groups, const uint32_t* obs, uint32_t n_obs, const uint64_t* prs, uint32_t n_prs,
+                         const int64_t* row_ptr, double* hscore, uint32_t* flag, uint32_t tag, hipStream_t st) {
+    hipLaunchKernelGGL(k_dropin, dim3(1), dim3(n_obs ? 1024 : 256), 0, st, s, pp, ev, goff, n_groups, obs, n_obs, prs,
+                       n_prs, row_ptr, hscore, flag, tag);
     return hipGetLastError();
 }
 

@@ -631,7 +631,7 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      each peer (all topics): score >= GossipThreshold, peerhave <=
  *      MaxIHaveMessages, iasked < MaxIHaveLength, ids it has not seen; it
  *      asks for min(|iwant|, MaxIHaveLength - iasked) of them (a uniform
- *      subset, selection sampling with draws h(seed, 9, pair, tick << 32 | k)
+ *      subset, selection sampling with draws h(seed, 9, u << 32 | v, tick << 32 | k)
  *      over the canonical order topic / cache order / message index) and
  *      tracks one promise (AddPromise, gossip_tracer.go:48-75: the element at
  *      Int31n(asked) in canonical order, expiring IWantFollowupTime later);

@@ -2114,7 +2114,7 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             size_t kk = n;
             const size_t budget = (size_t)((int64_t)gp->max_ihave_length - (int64_t)o->iasked[q]);
             if (kk > budget) kk = budget;
-            orc_rng g = {seed, 9, (uint64_t)q, tick << 32, 0};
+            orc_rng g = {seed, 9, (uint64_t)u << 32 | v, tick << 32, 0}; /* (keyed by node ids: shard-invariant) */
             if (n_it + kk > cap_it) {
                 while (n_it + kk > cap_it) cap_it *= 2;
                 items = (gx_item*)realloc(items, sizeof(gx_item) * cap_it);
