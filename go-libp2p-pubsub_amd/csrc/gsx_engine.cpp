@@ -19,6 +19,7 @@
 #include <functional>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/gsx.h"
@@ -370,6 +371,11 @@ struct gsx_engine {
 
     // events
     std::vector<gsx_event> pending;
+    // what the queued events can change: their pairs' scores, and every score
+    // of an observer with an AddPeer / RemovePeer (its IP groups' P6), so a
+    // Score() of any other pair reads the host copy without a flush
+    std::unordered_set<uint64_t> pend_pairs;
+    std::unordered_set<uint32_t> pend_rows;
     void* h_stage = nullptr;
     size_t h_stage_bytes = 0;
     void* d_stage = nullptr;
@@ -856,6 +862,23 @@ int upload_ipg(gsx_engine* e) {
     return GSX_OK;
 }
 
+void pending_note(gsx_engine* e, uint32_t kind, uint64_t pair) {
+    if (kind == GSX_EV_ADD_PEER || kind == GSX_EV_REMOVE_PEER)
+        e->pend_rows.insert(pair < e->pair_obs.size() ? e->pair_obs[pair] : 0xFFFFFFFFu);
+    else
+        e->pend_pairs.insert(pair);
+}
+void pending_clear(gsx_engine* e) {
+    e->pending.clear();
+    e->pend_pairs.clear();
+    e->pend_rows.clear();
+}
+// Whether a queued event can change the score of `pair` (the pending sets).
+bool pending_touches(const gsx_engine* e, uint64_t pair) {
+    return e->pend_pairs.count(pair) || e->pend_rows.count(pair < e->pair_obs.size() ? e->pair_obs[pair] : 0u) ||
+           e->pend_rows.count(0xFFFFFFFFu);
+}
+
 // Applies queued events on the device (score.go:588-974 via k_apply_events).
 int flush(gsx_engine* e) {
     if (e->pending.empty()) return GSX_OK;
@@ -865,7 +888,7 @@ int flush(gsx_engine* e) {
     std::vector<uint32_t> obs(n);
     for (size_t i = 0; i < n; ++i) {
         if (e->pending[i].pair >= e->E) {
-            e->pending.clear();
+            pending_clear(e);
             return fail(e, GSX_ERANGE, "event pair out of range");
         }
         obs[i] = e->pair_obs[e->pending[i].pair];
@@ -914,7 +937,7 @@ int flush(gsx_engine* e) {
     const auto* dev = static_cast<const gsx::DevEvent*>(e->d_stage);
     const auto* doff = reinterpret_cast<const uint32_t*>(static_cast<const char*>(e->d_stage) + ev_bytes);
     HIPCHK(e, gsx::launch_apply_events(dev_state(e), dev_peer_params(e), dev, doff, n_groups, e->stream));
-    e->pending.clear();
+    pending_clear(e);
     if (e->scores_valid || e->dirty_only || e->lazy) {  // exact but for these observers (and the stale pairs)
         for (uint32_t g = 0; g < n_groups; ++g) e->dirty_obs.push_back(obs[order[group_off[g]]]);
         e->scores_valid = false;
@@ -1027,6 +1050,7 @@ int ensure_scores(gsx_engine* e) {
 
 void push_event(gsx_engine* e, uint32_t kind, uint64_t pair, uint32_t topic, int64_t now, int64_t arg) {
     e->pending.push_back(gsx_event{kind, topic, pair, now, arg});
+    pending_note(e, kind, pair);
 }
 
 // messageDeliveries.getRecord, score.go:833-854
@@ -1310,7 +1334,7 @@ int load_overlay(gsx_engine* e, uint32_t n_total, uint32_t node_lo, uint32_t n_n
     HIPCHK(e, hipStreamSynchronize(e->stream));
     free_state(e);
     e->loaded = false;
-    e->pending.clear();
+    pending_clear(e);
     e->recs.clear();
     e->rec_queue.clear();
     e->n_nodes = n_nodes;
@@ -1693,6 +1717,7 @@ int gsx_apply_events(gsx_engine* e, const gsx_event* ev, size_t n) {
         if (ev[i].kind < GSX_EV_ADD_PEER || ev[i].kind > GSX_EV_APP_SCORE) return fail(e, GSX_EINVAL, "bad event kind");
     }
     e->pending.insert(e->pending.end(), ev, ev + n);
+    for (size_t i = 0; i < n; ++i) pending_note(e, ev[i].kind, ev[i].pair);
     return GSX_OK;
 }
 
@@ -1886,7 +1911,7 @@ int dropin_fast(gsx_engine* e) {
     std::vector<uint32_t> obs(n);
     for (size_t i = 0; i < n; ++i) {
         if (e->pending[i].pair >= e->E) {
-            e->pending.clear();
+            pending_clear(e);
             return fail(e, GSX_ERANGE, "event pair out of range");
         }
         obs[i] = e->pair_obs[e->pending[i].pair];
@@ -1952,7 +1977,7 @@ int dropin_fast(gsx_engine* e) {
                                  reinterpret_cast<const uint32_t*>(e->d_dropin + ob_off), (uint32_t)rows.size(),
                                  reinterpret_cast<const uint64_t*>(e->d_dropin + pr_off), (uint32_t)prs.size(),
                                  e->d_row_ptr, e->h_score_dev, reinterpret_cast<uint32_t*>(e->d_dropin), tag, e->stream));
-    e->pending.clear();
+    pending_clear(e);
     const volatile uint32_t* flag = static_cast<const volatile uint32_t*>(e->h_dropin);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0; *flag != tag; ++spin) {
@@ -1968,6 +1993,12 @@ int dropin_fast(gsx_engine* e) {
     e->scores_exact();
     e->h_score_tag = e->score_writes;
     return 1;
+}
+
+// The host copy equals the device scores as the queued events found them.
+bool host_copy_current(const gsx_engine* e) {
+    return e->h_score && e->h_score_cap >= e->E && e->scores_valid && !e->dirty_only &&
+           e->h_score_tag == e->score_writes;
 }
 
 // The host copy of every score (engines up to kHostScoreMax pairs), current.
@@ -1997,6 +2028,12 @@ int gsx_score(gsx_engine* e, uint64_t pair, double* out) {
     if (!e || !out) return GSX_EINVAL;
     if (int rc = check_pair(e, pair)) return rc;
     if (e->E <= kHostScoreMax) {  // small engine (one router's peers): keep the whole vector on the host
+        // the host copy was current before the queued events, which leave this
+        // pair's score alone: no round trip (the events stay queued)
+        if (host_copy_current(e) && !pending_touches(e, pair)) {
+            *out = e->h_score[pair];
+            return GSX_OK;
+        }
         if (int rc = host_scores(e)) return rc;
         *out = e->h_score[pair];
         return GSX_OK;
@@ -2014,7 +2051,10 @@ int gsx_score_many(gsx_engine* e, const uint64_t* pairs, size_t n, double* out) 
     for (size_t i = 0; i < n; ++i)
         if (pairs[i] >= e->E) return fail(e, GSX_ERANGE, "pair out of range");
     if (e->E <= kHostScoreMax) {
-        if (int rc = host_scores(e)) return rc;
+        bool touched = !host_copy_current(e);
+        for (size_t i = 0; i < n && !touched; ++i) touched = pending_touches(e, pairs[i]);
+        if (touched)
+            if (int rc = host_scores(e)) return rc;
         for (size_t i = 0; i < n; ++i) out[i] = e->h_score[pairs[i]];
         return GSX_OK;
     }
