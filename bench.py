@@ -387,7 +387,8 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     steps = 4 * args.prop_steps
     runner = None
     if dist is not None:
-        runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
+        runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse),
+                                        compact=args.shard_exchange == "compact", chunk=args.shard_chunk)
 
     def once(b):
         msgs = prop_messages(n, M, synth.SEED + 1, first=b * M)
@@ -428,7 +429,8 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     if world == 1:
         out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
     else:
-        out["exchange"] = {"compacted": runner.compact, "bytes_sent_per_batch_rank": runner.sent_bytes / (steps + 1),
+        out["exchange"] = {"compacted": runner.compact, "chunk": None if runner.compact else runner.chunk,
+                           "bytes_sent_per_batch_rank": runner.sent_bytes / (steps + 1),
                            "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8,
                            "hops_per_batch": runner.hops_run / (steps + 1),
                            "host_syncs_per_hop": runner.host_syncs / max(runner.hops_run, 1),
@@ -564,6 +566,9 @@ def adversarial_leg(args, rank, world, local, dist, dev):
             ms.append(reduce_scalar(time.perf_counter() - t0, dist, dev, "max") * 1e3)
         out["heartbeat_ms_per_round"] = sum(ms) / len(ms)
         out["heartbeat_ms_rounds"] = ms
+        if runner is not None:  # the gossip exchange's forwarding hops across the shards and their host round trips
+            out["forwarding_exchange"] = {"hops": runner.gx_hops,
+                                          "host_syncs_per_hop": runner.gx_syncs / max(runner.gx_hops, 1)}
         out["sybil_mesh_links_before"] = int(before)
         out["sybil_mesh_links_after"] = int(sybil_links())
         out["heartbeat_first_round"] = hbs[0]
@@ -614,6 +619,10 @@ def main():
                     help="messages per propagation batch (0: skip); 1024 = 16 words, one 128-B line per frontier row")
     ap.add_argument("--prop-peers", type=int, default=10_000_000, help="cfg4 overlay for the range-sharded leg (0: skip)")
     ap.add_argument("--shard-msgs", type=int, default=64, help="messages per batch of the cfg4 range-sharded leg")
+    ap.add_argument("--shard-exchange", choices=("compact", "dense"), default="compact",
+                    help="cfg4 range-sharded leg: compacted entries (one host round trip per hop) or every cross "
+                         "pair's row with fixed splits (one host check per --shard-chunk hops)")
+    ap.add_argument("--shard-chunk", type=int, default=4, help="dense exchange: hops per host check")
     ap.add_argument("--prop-steps", type=int, default=5)
     ap.add_argument("--epoch-batches", type=int, default=4,
                     help="message-parallel leg: batches per heartbeat epoch (one credit all-reduce each)")

@@ -249,6 +249,17 @@ struct PropState {
     // such pairs are always re-scored.
     uint8_t* stale;
     double lazy_thr;
+    // Deferred folds (gsx_engine.cpp prop_end / fold_deferred; null: off): the
+    // credits of pairs that keep their stored score (>= lazy_thr, no P4 this
+    // call) are not folded per call but summed over calls — acc_s[r] the
+    // copies the sender pair r sent (k_prop_dups), acc_f[q] the first
+    // receipts of the receiver pair q — and folded once, before anything
+    // reads the records or scores: q's P2 / P3 steps are acc_f[q] first
+    // receipts and acc_s[rev q] - acc_f[q] duplicates.  Every step is the same
+    // capped +1 of an unchanged mesh flag, so the sums fold to the
+    // one-call-at-a-time result.
+    uint32_t* acc_s;
+    uint32_t* acc_f;
 };
 
 // pins_only: the fwd bytes stand (a RESCORE count kept them), update the
@@ -273,6 +284,14 @@ hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, 
 // gray_only: count the sends on pairs whose receiver graylists the sender
 // (STAT_GRAY) and nothing else (per-hop accounting); else the late accounting.
 hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt, bool gray_only, hipStream_t st);
+// The deferred-fold call's per-pair pass (instead of k_prop_count): the pairs
+// that must fold now (score below lazy_thr, or a P4 credit) fold their sums
+// and are re-scored with their fwd bytes; the rest keep accumulating.
+hipError_t launch_prop_defer(const PropState& ps, const DevState& s, const DevPeerParams& pp, hipStream_t st);
+// Folds every deferred sum (acc_s / acc_f of topic ps.topic) into the records
+// and marks the folded pairs stale (re-scored by the caller); the sums are
+// cleared by the caller.
+hipError_t launch_prop_fold_acc(const PropState& ps, const DevState& s, hipStream_t st);
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* first, uint32_t* dup,
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
@@ -596,6 +615,12 @@ struct GxFwd {
     // drops the peer of q)
     uint8_t* fout;
     uint16_t* fin;
+    // per receiver x, this run: its pairs whose sender forwards a run topic to
+    // it (fin & 0xFF), ascending, as (q, rev q, peer's local index, fin) at
+    // fent[row_ptr[x] .. fend[x]) (k_gxf_compact, before hop 1): the pull walks
+    // x's mesh senders instead of every pair of its row (null: every pair)
+    uint4* fent;
+    uint32_t* fend;
     uint64_t all_sets;
     uint64_t* fbit[2];  // [node / 64] bit per node: in the frontier (the pull's filter: L2-resident)
     // range shards: the frontier of remote senders, per hop, as entries of
@@ -641,6 +666,8 @@ hipError_t launch_gxf_recv_fout(const GxFwd& f, const uint64_t* in, const uint32
                                 hipStream_t st);
 hipError_t launch_gxf_halo(const HbState& h, const GxFwd& f, const GxsPlan& P, uint32_t hop, unsigned long long* cnt,
                            const uint64_t* off, uint64_t* out, hipStream_t st);
+hipError_t launch_gxf_pack_counts(const unsigned long long* cnt, const uint32_t* front, uint32_t world, int64_t* out,
+                                  hipStream_t st);
 hipError_t launch_gxf_halo_recv(const HbState& h, const GxFwd& f, uint32_t hop, const uint64_t* in, uint64_t n,
                                 const uint32_t* halo_pair, const uint32_t* halo_node, hipStream_t st);
 // Promise slots [pair][from] -> [pair][to] (to > from; new slots free).

@@ -221,6 +221,8 @@ struct gsx_engine {
     uint16_t* d_gxf_b = nullptr;      // bcnt[2][E][GXF_SLOTS]
     uint16_t* d_gxf_fin = nullptr;    // [E] per run (GxFwd::fin)
     uint8_t* d_gxf_fout = nullptr;    // [E] per run (GxFwd::fout)
+    uint4* d_gxf_fent = nullptr;      // [E] per run (GxFwd::fent; GSX_GXF_NO_COMPACT=1: null, the pull walks every pair)
+    uint32_t* d_gxf_fend = nullptr;   // [N] per run (GxFwd::fend)
     gsx::GxFwdSet* d_gxf_sets = nullptr;  // [gxf_sets_cap] descriptors of the round's runs
     size_t gxf_sets_cap = 0;
     uint32_t* h_gxf_cnt = nullptr;    // pinned: the hop count of a run's last launched hop
@@ -410,6 +412,12 @@ struct gsx_engine {
     // fwd byte exact for thresholds up to lazy_thr); ensure_scores settles them.
     bool lazy = false;
     bool stale_marks = false;  // d_stale may hold marks (cleared before a lazy fold starts a new set)
+    // Deferred folds (PropState::acc_s / acc_f): gossipsub calls sum the credits
+    // of the pairs that keep their score instead of folding them; fold_deferred
+    // folds the sums (topic def_topic) before anything reads records or scores.
+    uint32_t *d_acc_s = nullptr, *d_acc_f = nullptr;
+    bool deferred = false;
+    uint32_t def_topic = 0;
     double lazy_thr = 0;
     uint8_t* d_stale = nullptr;
     void invalidate_scores() {
@@ -695,6 +703,10 @@ void free_state(gsx_engine* e) {
     if (e->d_dirty_obs) (void)hipFree(e->d_dirty_obs);
     if (e->d_stale) (void)hipFree(e->d_stale);
     e->d_stale = nullptr;
+    if (e->d_acc_s) (void)hipFree(e->d_acc_s);
+    if (e->d_acc_f) (void)hipFree(e->d_acc_f);
+    e->d_acc_s = e->d_acc_f = nullptr;
+    e->deferred = false;
     e->stale_marks = false;
     e->d_smask = nullptr;
     e->d_dirty_obs = nullptr;
@@ -750,7 +762,7 @@ void free_state(gsx_engine* e) {
                        e->d_gx_got, e->d_gx_nodes,
                        e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg,
                        e->d_gxf_mask, e->d_gxf_list, e->d_gxf_cnt, e->d_gxf_bst, e->d_gxf_b0, e->d_gxf_b,
-                       e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout, e->d_gxf_hst, e->d_gxs_out, e->d_gxs_rans,
+                       e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout, e->d_gxf_fent, e->d_gxf_fend, e->d_gxf_hst, e->d_gxs_out, e->d_gxs_rans,
                        e->d_gxs_hidx, e->d_gxs_cnt, e->d_gxs_off, e->d_gxs_send};
         for (void* x : gxp)
             if (x) (void)hipFree(x);
@@ -762,6 +774,8 @@ void free_state(gsx_engine* e) {
         e->d_gxf_sets = nullptr;
         e->d_gxf_fin = nullptr;
         e->d_gxf_fout = nullptr;
+        e->d_gxf_fent = nullptr;
+        e->d_gxf_fend = nullptr;
         e->d_gxf_hst = nullptr;
         e->d_gxs_out = nullptr;
         e->d_gxs_rans = nullptr;
@@ -879,9 +893,12 @@ bool pending_touches(const gsx_engine* e, uint64_t pair) {
            e->pend_rows.count(0xFFFFFFFFu);
 }
 
+int fold_deferred(gsx_engine* e);
+
 // Applies queued events on the device (score.go:588-974 via k_apply_events).
 int flush(gsx_engine* e) {
     if (e->pending.empty()) return GSX_OK;
+    if (int rc = fold_deferred(e)) return rc;  // the queued events came after the deferred credits
     if (!e->loaded) return fail(e, GSX_ESTATE, "events before gsx_load_overlay");
     const size_t n = e->pending.size();
     // stable grouping by observer: order inside each observer is preserved
@@ -999,6 +1016,34 @@ int upload_dirty_obs(gsx_engine* e) {
     return GSX_OK;
 }
 
+// The deferred folds' sums into the records (their pairs marked stale: the
+// next settle re-scores them); a no-op when nothing is deferred.
+int fold_deferred(gsx_engine* e) {
+    if (!e->deferred) return GSX_OK;
+    e->deferred = false;
+    gsx::PropState ps{};
+    ps.n_pairs = e->E;
+    ps.topic = e->def_topic;
+    ps.rev = e->d_rev;
+    ps.acc_s = e->d_acc_s;
+    ps.acc_f = e->d_acc_f;
+    ps.stale = e->d_stale;
+    HIPCHK(e, gsx::launch_prop_fold_acc(ps, dev_state(e), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_acc_s, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_acc_f, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
+    e->stale_marks = true;
+    ++e->rec_gen;  // (records changed: the fold's topic-term cache starts a new epoch)
+    return GSX_OK;
+}
+// The records are being replaced (import, synthesis): the sums are dropped.
+int drop_deferred(gsx_engine* e) {
+    if (!e->deferred) return GSX_OK;
+    e->deferred = false;
+    HIPCHK(e, hipMemsetAsync(e->d_acc_s, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_acc_f, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
+    return GSX_OK;
+}
+
 // Lazy folds left stale pairs (PropState::stale): re-score them and the
 // dirty observers' rows (events since), then clear the marks.
 int settle_stale(gsx_engine* e) {
@@ -1018,6 +1063,7 @@ int settle_stale(gsx_engine* e) {
 }
 
 int ensure_scores(gsx_engine* e) {
+    if (int rc = fold_deferred(e)) return rc;
     int rc = flush(e);
     if (rc) return rc;
     if (e->scores_valid) return GSX_OK;
@@ -1262,6 +1308,7 @@ int gsx_set_topic_params(gsx_engine* e, uint32_t topic, const gsx_topic_score_pa
     if (topic >= e->T) return fail(e, GSX_ERANGE, "topic out of range");
     if (p->time_in_mesh_quantum_ns == 0)  // Go would panic dividing by it in score()
         return fail(e, GSX_EINVAL, "TimeInMeshQuantum must be non zero");
+    if (int rc = fold_deferred(e)) return rc;
     int rc = flush(e);
     if (rc) return rc;
     const bool exist = e->scored[topic];
@@ -1828,6 +1875,7 @@ int gsx_num_delivery_records(gsx_engine* e, uint64_t* out) {
 int gsx_refresh(gsx_engine* e, int64_t now) {
     if (!e) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = fold_deferred(e)) return rc;  // (the decay follows the credits)
     int rc = flush(e);
     if (rc) return rc;
     const gsx::DevState s = dev_state(e);
@@ -2107,6 +2155,7 @@ int gsx_import_state(gsx_engine* e, const gsx_state_view* s) {
         !s->pair_flags || !s->expire_ns || !s->behaviour_penalty)
         return fail(e, GSX_EINVAL, "import needs every state array");
     if (int rc = flush(e)) return rc;
+    if (int rc = drop_deferred(e)) return rc;
     const size_t E = e->E, R = (size_t)e->T * E;
     if (int rc = ensure_tmp(e)) return rc;
     e->last_refresh = s->last_refresh_ns;
@@ -2142,6 +2191,7 @@ int gsx_synthesize_state(gsx_engine* e, const gsx_synth_spec* sp) {
     if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     if (int rc = flush(e)) return rc;
+    if (int rc = drop_deferred(e)) return rc;
     gsx::DevSynthSpec d{};
     d.seed = sp->seed;
     d.now = sp->now_ns;
@@ -2170,6 +2220,7 @@ int gsx_export_state(gsx_engine* e, gsx_state_view* s) {
     if (!e || !s) return GSX_EINVAL;
     if (int rc = gx_busy(e)) return rc;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = fold_deferred(e)) return rc;
     if (int rc = flush(e)) return rc;
     const size_t E = e->E, R = (size_t)e->T * E;
     if (int rc = ensure_tmp(e)) return rc;
@@ -2460,6 +2511,9 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     // publishThreshold for floodsub peers and flood publishing: k_prop_fwd);
     // the other routers never
     const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB;
+    // deferred credits of another topic (or a call that folds its own way) land first
+    if (e->deferred && (cfg->topic != e->def_topic || cfg->credit_scores != GSX_CREDIT_NOW || cfg->router != GSX_ROUTER_GOSSIPSUB))
+        if (int rc = fold_deferred(e)) return rc;
     if (int rc = flush(e)) return rc;  // queued events land first either way
     // (after lazy folds the fwd bytes stand for thresholds up to lazy_thr: the stale scores wait)
     const bool lazy_ok = e->lazy && !e->dirty_only && lazy_threshold(e) <= e->lazy_thr;
@@ -2728,11 +2782,6 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         const bool lean = ps.late && !ps.sharded && !ps.sel && !ps.from_mask && !general;
         if (!lean || ps.flast_every || P.h >= ps.max_hops) P.flast_dirty = true;
     }
-    if (ps.late) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, false, e->stream));
-    // per-hop accounting counts duplicates on arrival; the copies graylisting
-    // receivers drop from local senders are counted here (the kernels return at
-    // once when no pair is gated)
-    else if (ps.gate) HIPCHK(e, gsx::launch_prop_dups(ps, P.h, P.vcnt, true, e->stream));
     const bool fold_now = ps.credit && P.cfg.credit_scores != GSX_CREDIT_DEFER;
     // the folded pairs are re-scored in the fold when every other score is
     // exact (gossipsub calls start from exact scores) and the fwd bytes match
@@ -2744,6 +2793,33 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     static const bool no_lazy = getenv("GSX_NO_LAZY_FOLD") != nullptr;
     const double thr = lazy_threshold(e);
     const bool lazy = rescore && !no_lazy && credits_raise_scores(e) && (!e->lazy || thr <= e->lazy_thr);
+    // deferred folds (PropState::acc_s / acc_f): the lazy pairs' credits are
+    // summed over calls instead of folded per call; only the pairs below the
+    // threshold (or with a P4 credit) fold now.  Late accounting on one engine
+    // with no user-deferred counts (GSX_CREDIT_NOW), one topic's sums at a time
+    static const bool no_defer = getenv("GSX_NO_DEFER_FOLD") != nullptr;
+    const bool defer = lazy && !no_defer && ps.late && ps.credit && !e->sharded() && !P.credit_pending &&
+                       P.cfg.credit_scores == GSX_CREDIT_NOW && ps.topic < e->T && e->scored[ps.topic] &&
+                       (!e->deferred || e->def_topic == ps.topic);
+    if (defer && !e->d_acc_s) {
+        const size_t E = std::max<size_t>(e->E, 1);
+        if (int rc = dalloc(e, &e->d_acc_s, E)) return rc;
+        if (int rc = dalloc(e, &e->d_acc_f, E)) return rc;
+        HIPCHK(e, hipMemsetAsync(e->d_acc_s, 0, 4 * E, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_acc_f, 0, 4 * E, e->stream));
+    }
+    {
+        gsx::PropState pd = ps;
+        if (defer) {
+            pd.acc_s = e->d_acc_s;
+            pd.acc_f = e->d_acc_f;
+        }
+        if (ps.late) HIPCHK(e, gsx::launch_prop_dups(pd, P.h, P.vcnt, false, e->stream));
+        // per-hop accounting counts duplicates on arrival; the copies graylisting
+        // receivers drop from local senders are counted here (the kernels return at
+        // once when no pair is gated)
+        else if (ps.gate) HIPCHK(e, gsx::launch_prop_dups(pd, P.h, P.vcnt, true, e->stream));
+    }
     if (ps.credit || ps.late) {
         gsx::PropState pc = ps;
         // the topic-term cache (several topics: a fold then re-reads one topic's record, not all)
@@ -2752,7 +2828,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         // runs without it (its terms would be stale before any later fold reads
         // them); the second of consecutive folds starts a cache epoch.
         const bool consecutive = P.t_rec_gen == e->rec_gen || P.t_plain_gen == e->rec_gen;
-        if (rescore && e->T >= 2 && e->T <= 16 && !no_tt && consecutive) {
+        if (rescore && !defer && e->T >= 2 && e->T <= 16 && !no_tt && consecutive) {
             if (!P.tterm) {
                 if (int rc = dalloc(e, &P.tterm, (size_t)e->E * e->T)) return rc;
                 if (int rc = dalloc(e, &P.tgen, (size_t)e->E)) return rc;
@@ -2775,9 +2851,18 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
             pc.stale = e->d_stale;
             pc.lazy_thr = thr;
         }
-        HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
-        if (pc.tterm) P.t_rec_gen = e->rec_gen;
-        else if (rescore) P.t_plain_gen = e->rec_gen;
+        if (defer) {
+            pc.acc_s = e->d_acc_s;
+            pc.acc_f = e->d_acc_f;
+            HIPCHK(e, gsx::launch_prop_defer(pc, dev_state(e), dev_peer_params(e), e->stream));
+            e->deferred = true;
+            e->def_topic = ps.topic;
+            ++e->rec_gen;  // (the immediate folds bypass the topic-term cache)
+        } else {
+            HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));
+            if (pc.tterm) P.t_rec_gen = e->rec_gen;
+            else if (rescore) P.t_plain_gen = e->rec_gen;
+        }
     }
     if (ps.credit) {
         // GSX_CREDIT_NOW: k_prop_count folded this call's counts (and any
@@ -2997,6 +3082,19 @@ int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new) {
     return GSX_OK;
 }
 
+int gsx_prop_hop_counts_dev(gsx_engine* e, int64_t* d_out) {
+    if (!e || !d_out) return GSX_EINVAL;
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (P.last.n_msgs == 0) {
+        HIPCHK(e, hipMemsetAsync(d_out, 0, 8 * (GSX_MAX_HOPS + 1), e->stream));
+        return GSX_OK;
+    }
+    HIPCHK(e, hipMemcpyAsync(d_out, P.stats + gsx::STAT_HOP0, 8 * (GSX_MAX_HOPS + 1), hipMemcpyDeviceToDevice,
+                             e->stream));
+    return GSX_OK;
+}
+
 namespace {
 // Pack the compacted exchange of hop P.h + 1 (the entry counts stay in P.dcount).
 int pack_compact(gsx_engine* e, uint64_t* out, bool* packed) {
@@ -3083,6 +3181,7 @@ bool on_device(const void* p) {
 int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup) {
     if (!e) return GSX_EINVAL;
     if (!e->loaded || !e->prop.first) return fail(e, GSX_ESTATE, "no propagation yet");
+    if (int rc = fold_deferred(e)) return rc;
     if (first) HIPCHK(e, hipMemcpyAsync(first, e->prop.first, 4 * e->E, hipMemcpyDefault, e->stream));
     if (dup) HIPCHK(e, hipMemcpyAsync(dup, e->prop.dup, 4 * e->E, hipMemcpyDefault, e->stream));
     if ((first && !on_device(first)) || (dup && !on_device(dup))) HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -3092,6 +3191,7 @@ int gsx_prop_pending_credits(gsx_engine* e, uint32_t* first, uint32_t* dup) {
 int gsx_prop_pending_invalid(gsx_engine* e, uint32_t* inv) {
     if (!e || !inv) return GSX_EINVAL;
     if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
+    if (int rc = fold_deferred(e)) return rc;
     HIPCHK(e, hipMemcpyAsync(inv, e->prop.inv, 4 * e->E, hipMemcpyDefault, e->stream));
     if (!on_device(inv)) HIPCHK(e, hipStreamSynchronize(e->stream));
     return GSX_OK;
@@ -3101,6 +3201,7 @@ int gsx_prop_replace_pending_invalid(gsx_engine* e, const uint32_t* inv) {
     if (!e || !inv) return GSX_EINVAL;
     if (!e->loaded || !e->prop.inv) return fail(e, GSX_ESTATE, "no propagation yet");
     if (e->prop.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (int rc = fold_deferred(e)) return rc;
     HIPCHK(e, hipMemcpyAsync(e->prop.inv, inv, 4 * e->E, hipMemcpyDefault, e->stream));
     if (!on_device(inv)) HIPCHK(e, hipStreamSynchronize(e->stream));
     e->prop.credit_pending = true;
@@ -3113,6 +3214,7 @@ int gsx_prop_fold_credits(gsx_engine* e, const uint32_t* first, const uint32_t* 
     if ((first == nullptr) != (dup == nullptr)) return GSX_EINVAL;
     auto& P = e->prop;
     if (P.active) return fail(e, GSX_ESTATE, "a stepped propagation is in flight");
+    if (int rc = fold_deferred(e)) return rc;
     if (first) {
         HIPCHK(e, hipMemcpyAsync(P.first, first, 4 * e->E, hipMemcpyDefault, e->stream));
         HIPCHK(e, hipMemcpyAsync(P.dup, dup, 4 * e->E, hipMemcpyDefault, e->stream));
@@ -3369,6 +3471,7 @@ static void dbg_host(const char* what) {
 }
 int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, bool state_only) {
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (int rc = fold_deferred(e)) return rc;  // (the round reads every record)
     DBG_SYNC(1);
     dbg_host("hb start");
     e->state_changed();
@@ -3737,7 +3840,8 @@ int gxf_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_gxf_cnt, 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) || (rc = dalloc(e, &e->d_gxf_bst, 3 * E)) ||
         (rc = dalloc(e, &e->d_gxf_b0, n_grp * E)) ||
         (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fin, E)) ||
-        (rc = dalloc(e, &e->d_gxf_fout, E)))
+        (rc = dalloc(e, &e->d_gxf_fout, E)) || (rc = dalloc(e, &e->d_gxf_fent, E)) ||
+        (rc = dalloc(e, &e->d_gxf_fend, N)))
         return rc;
     e->gxf_b0_grps = n_grp;
     if (e->sharded() && (rc = dalloc(e, &e->d_gxf_hst, 2 * E))) return rc;
@@ -3855,6 +3959,11 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
     f.seq = e->gxf_stamp + 1;
     f.fout = e->d_gxf_fout;
     f.fin = e->d_gxf_fin;
+    static const bool no_compact = getenv("GSX_GXF_NO_COMPACT") != nullptr;  // (A/B)
+    if (!no_compact) {
+        f.fent = e->d_gxf_fent;
+        f.fend = e->d_gxf_fend;
+    }
     f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
     static const uint32_t dense_div = [] {  // (GSX_GXF_DENSE: A/B of the dense-hop threshold)
         const char* v = getenv("GSX_GXF_DENSE");
@@ -4727,18 +4836,32 @@ int gsx_gxf_pack(gsx_engine* e, uint32_t hop, uint64_t* counts, uint64_t* out) {
     });
 }
 
+int gsx_gxf_pack_dev(gsx_engine* e, uint32_t hop, uint64_t* out, int64_t* d_counts) {
+    if (!e || !d_counts || (e->n_send && !out)) return GSX_EINVAL;
+    if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
+    if (hop == 0 || hop >= gsx::GXF_MAX_HOPS) return fail(e, GSX_ERANGE, "hop out of range");
+    const uint32_t R = std::max<uint32_t>(e->n_ranks, 1);
+    HIPCHK(e, hipMemsetAsync(e->d_gxs_cnt, 0, 8 * (size_t)R, e->stream));
+    if (e->n_send)  // destination d's entries from its dense segment's first slot (send_base[d]) on
+        HIPCHK(e, gsx::launch_gxf_halo(e->gxr.h, e->gxr.f, gxs_plan(e), hop, e->d_gxs_cnt, e->d_send_base, out,
+                                       e->stream));
+    HIPCHK(e, gsx::launch_gxf_pack_counts(e->d_gxs_cnt, e->gxr.f.fcnt + hop - 1, R, d_counts, e->stream));
+    return GSX_OK;
+}
+
 int gsx_gxf_step(gsx_engine* e, uint32_t hop, const uint64_t* entries, uint64_t n, uint64_t* n_front) {
-    if (!e || (n && !entries) || !n_front) return GSX_EINVAL;
+    if (!e || (n && !entries)) return GSX_EINVAL;
     if (!e->gxr.fwd_active) return fail(e, GSX_ESTATE, "gsx_gxf_begin first");
     if (hop == 0 || hop >= gsx::GXF_MAX_HOPS) return fail(e, GSX_ERANGE, "hop out of range");
     gsx::GxFwd& f = e->gxr.f;
     f.hent = entries;
     HIPCHK(e, gsx::launch_gxf_halo_recv(e->gxr.h, f, hop, entries, n, e->d_halo_pair, e->d_halo_node, e->stream));
     HIPCHK(e, gsx::launch_gxf_hop(dev_state(e), e->gxr.h, f, hop, e->stream));
+    f.hent = nullptr;  // (the launches hold it; the caller keeps the entries until they ran)
+    e->gxr.hops = std::max(e->gxr.hops, hop + 1);
+    if (!n_front) return GSX_OK;
     HIPCHK(e, hipMemcpyAsync(e->h_gxf_cnt, e->d_gxf_cnt + hop, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    f.hent = nullptr;
-    e->gxr.hops = std::max(e->gxr.hops, hop + 1);
     *n_front = *e->h_gxf_cnt;
     return GSX_OK;
 }

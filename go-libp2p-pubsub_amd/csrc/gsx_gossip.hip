@@ -1005,6 +1005,19 @@ __global__ __launch_bounds__(256) void k_gxf_fin(DevState s, HbState h, GxFwd f)
     }
 }
 
+// The run's eligible senders per receiver (GxFwd::fent), node-parallel, in pair order.
+__global__ __launch_bounds__(256) void k_gxf_compact(HbState h, GxFwd f) {
+    for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < h.n_nodes; x += gridDim.x * 256u) {
+        int64_t k = h.row_ptr[x];
+        for (int64_t q = h.row_ptr[x]; q < h.row_ptr[x + 1]; ++q) {
+            const uint32_t fi = f.fin[q];
+            if (!(fi & 0xFFu)) continue;
+            f.fent[k++] = make_uint4((uint32_t)q, h.rev[q], (uint32_t)h.col[q] - h.node_lo, fi);
+        }
+        f.fend[x] = (uint32_t)k;
+    }
+}
+
 __device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots) {
     uint64_t m = 0;
     for (; slots; slots &= slots - 1) m |= f.slot_sets[__builtin_ctz(slots)];
@@ -1254,36 +1267,44 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
         const uint64_t srcm = f.srcm[x] & M;
         uint64_t newsets = 0;  // (the same in every lane of the group)
         const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
-        for (int64_t qb0 = r0; qb0 < r1; qb0 += G * B) {
-          uint32_t fis[B], rqs[B], vqs[B];
+        const int64_t e1 = f.fent ? (int64_t)f.fend[x] : r1;  // x's eligible senders (or every pair)
+        for (int64_t qb0 = r0; qb0 < e1; qb0 += G * B) {
+          uint32_t fis[B], rqs[B], vqs[B], qs[B];
           uint64_t fms[B];
 #pragma unroll
           for (int j = 0; j < B; ++j) {
-              const int64_t q = qb0 + j * G + lc;
-              const bool in = q < r1;
-              fis[j] = in ? (uint32_t)f.fin[q] : 0u;
-              rqs[j] = in ? h.rev[q] : NO_PAIR;
-              vqs[j] = in ? (uint32_t)h.col[q] - h.node_lo : 0u;  // (local index; unused if remote)
+              const int64_t ei = qb0 + j * G + lc;
+              const bool in = ei < e1;
+              if (f.fent) {  // one 16-B load per sender: (q, rev q, peer, fin)
+                  const uint4 en = in ? f.fent[ei] : make_uint4(0u, NO_PAIR, 0u, 0u);
+                  qs[j] = en.x;
+                  rqs[j] = en.y;
+                  vqs[j] = en.z;
+                  fis[j] = en.w;
+              } else {
+                  qs[j] = (uint32_t)ei;
+                  fis[j] = in ? (uint32_t)f.fin[ei] : 0u;
+                  rqs[j] = in ? h.rev[ei] : NO_PAIR;
+                  vqs[j] = in ? (uint32_t)h.col[ei] - h.node_lo : 0u;  // (local index; unused if remote)
+              }
           }
 #pragma unroll
           for (int j = 0; j < B; ++j) {
-              const int64_t q = qb0 + j * G + lc;
               fms[j] = 0;
               if (!(fis[j] & 0xFFu)) continue;
-              if (rqs[j] & HALO) fms[j] = f.hstamp && f.hstamp[q] == seq_cur;  // a remote sender's entry this hop
+              if (rqs[j] & HALO) fms[j] = f.hstamp && f.hstamp[qs[j]] == seq_cur;  // a remote sender's entry this hop
               else fms[j] = (f.fbit[p][vqs[j] >> 6] >> (vqs[j] & 63)) & 1;  // (L2-resident: filters the mask loads)
           }
 #pragma unroll
           for (int j = 0; j < B; ++j) {
-              const int64_t q = qb0 + j * G + lc;
               if (fms[j])
-                  fms[j] = ((rqs[j] & HALO) ? f.hent[(size_t)f.hidx[q] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vqs[j]]) &
+                  fms[j] = ((rqs[j] & HALO) ? f.hent[(size_t)f.hidx[qs[j]] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vqs[j]]) &
                            M & gxf_slot_sets(f, fis[j] & 0xFFu);
           }
           for (int j = 0; j < B; ++j) {  // the rounds in sender order
             const int64_t qb = qb0 + j * G;
-            if (qb >= r1) break;
-            const int64_t q = qb + lc;
+            if (qb >= e1) break;
+            const int64_t q = qs[j];
             const uint32_t fi = fis[j];
             const uint32_t r = (fi & 0xFFu) ? rqs[j] : NO_PAIR;
             const uint32_t v = (fi & 0xFFu) ? vqs[j] : 0u;
@@ -1557,6 +1578,17 @@ __global__ __launch_bounds__(256) void k_gxf_halo_recv(HbState h, GxFwd f, uint3
     }
 }
 
+// (entries for rank d, this rank's frontier of the hop before) per destination
+// (gsx_gxf_pack_dev: one all-to-all of these pairs tells every rank its entry
+// splits and, summed, whether the last hop left a frontier anywhere).
+__global__ void k_gxf_pack_counts(const unsigned long long* __restrict__ cnt, const uint32_t* __restrict__ front,
+                                  uint32_t world, int64_t* __restrict__ out) {
+    const uint32_t d = threadIdx.x;
+    if (d >= world) return;
+    out[2 * d] = (int64_t)cnt[d];
+    out[2 * d + 1] = (int64_t)*front;
+}
+
 static inline unsigned gx_blocks(uint64_t n, unsigned bs, unsigned cap) {
     const uint64_t b = (n + bs - 1) / bs;
     return (unsigned)(b < cap ? b : cap);
@@ -1608,6 +1640,8 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
 // One hop (hop >= 1): its grids are sized for the largest frontier / receiver
 // list (the counts are on the device: an empty hop's threads exit at once).
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
+    if (hop == 1 && f.fent)  // the run's eligible senders (the remote ones' fin bits have arrived by now)
+        hipLaunchKernelGGL(k_gxf_compact, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, h, f);
     hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
     static const int gl = [] {  // receivers' lanes: GSX_GXF_G = 1 (k_gxf_pull), 2, 4 (default), 8
         const char* v = getenv("GSX_GXF_G");
@@ -1672,6 +1706,12 @@ hipError_t launch_gxf_halo(const HbState& h, const GxFwd& f, const GxsPlan& P, u
     hipLaunchKernelGGL(k_gxf_halo, dim3(gx_grid(P.n_send)), dim3(256), 0, st, h, f, P, hop, cnt, off, out);
     return hipGetLastError();
 }
+hipError_t launch_gxf_pack_counts(const unsigned long long* cnt, const uint32_t* front, uint32_t world, int64_t* out,
+                                  hipStream_t st) {
+    hipLaunchKernelGGL(k_gxf_pack_counts, dim3(1), dim3(MAX_RANKS), 0, st, cnt, front, world, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_gxf_halo_recv(const HbState& h, const GxFwd& f, uint32_t hop, const uint64_t* in, uint64_t n,
                                 const uint32_t* halo_pair, const uint32_t* halo_node, hipStream_t st) {
     if (n == 0) return hipSuccess;

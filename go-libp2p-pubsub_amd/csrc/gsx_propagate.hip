@@ -1121,7 +1121,7 @@ constexpr int FH = 2;  // fold_rescore_1: pairs whose loads are in flight togeth
 template <bool GRAY_ONLY>
 __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
     if (GRAY_ONLY && *ps.gray_pairs == 0) return;
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[3] = {0, 0, 0};
     const uint32_t W = ps.n_words;
     const DupsLast L = dups_last(ps, h_run);
     h_run = L.h_run;
@@ -1155,8 +1155,18 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             const bool live = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
             vca[i] = live ? vcnt[va[i]] : 0;
             const bool fl = live && !ps.from_mask && (fa[i] & FWD_FORWARD) && h_run >= 1;
-            fca[i] = fl ? ps.fcnt[r] : 0;
+            fca[i] = (fl || (ps.acc_f && r < ps.n_pairs)) ? ps.fcnt[r] : 0;
             fla[i] = fl ? ps.flast[r] : 0;
+        }
+        if (!GRAY_ONLY && ps.acc_f) {  // deferred folds: r as a receiver pair — its first receipts join its sum
+#pragma unroll
+            for (int i = 0; i < DU; ++i) {
+                const uint64_t r = r0 + i * stride;
+                if (r >= ps.n_pairs || !fca[i]) continue;
+                ps.acc_f[r] += fca[i];
+                const uint32_t rr = ps.rev[r];
+                if (rr != NO_PAIR && !(rr & HALO)) cnt[2] += fca[i];  // the back-sends (k_prop_count's count)
+            }
         }
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
@@ -1207,12 +1217,16 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
                 if (!GRAY_ONLY) ps.corr[r] = 0;
             } else {
                 cnt[0] += sends;
-                ps.corr[r] = sends;
+                if (ps.acc_s) {  // deferred folds: the sends join the sender pair's sum
+                    if (sends) ps.acc_s[r] += sends;
+                } else {
+                    ps.corr[r] = sends;
+                }
             }
         }
     }
-    const uint32_t slot[2] = {STAT_DUPS, STAT_GRAY};
-    block_count<2>(cnt, ps.stats, slot);
+    const uint32_t slot[3] = {STAT_DUPS, STAT_GRAY, STAT_BACKSENDS};
+    block_count<3>(cnt, ps.stats, slot);
 }
 
 // ---- P2/P3 credits ------------------------------------------------------------
@@ -1512,6 +1526,71 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
     }
     const uint32_t slot[1] = {STAT_BACKSENDS};
     block_count<1>(cnt, ps.stats, slot);
+}
+
+// Deferred folds, the call's pass (PropState::acc_s / acc_f): a pair folds
+// now only if its score is below lazy_thr (its fwd bytes may depend on the
+// credits) or it took a P4 credit this call (invalid deliveries lower a
+// score); it folds its whole sums (earlier calls' too: identical +1 steps)
+// and is re-scored with its fwd byte, as k_prop_count's RESCORE path does.
+__global__ __launch_bounds__(256) void k_prop_defer(PropState ps, DevState s, DevPeerParams pp) {
+    const bool fold_topic = ps.topic < s.n_topics && s.tp[ps.topic].scored;
+    if (!fold_topic) return;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; q0 < ps.n_pairs; q0 += stride * DU) {
+        double sc[DU];
+        uint32_t k4a[DU];
+        uint8_t pf[DU];
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t q = q0 + i * stride;
+            const bool in = q < ps.n_pairs;
+            sc[i] = in ? s.score[q] : 0.0;
+            k4a[i] = (in && ps.drop) ? ps.invcnt[q] : 0u;
+            pf[i] = in ? s.pflags[q] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t q = q0 + i * stride;
+            if (q >= ps.n_pairs) continue;
+            if (!(pf[i] & PAIR_PRESENT)) {  // no peerStats: nothing to credit (the sums are cleared at the fold)
+                if (k4a[i]) ps.invcnt[q] = 0;
+                continue;
+            }
+            if (k4a[i] == 0 && sc[i] >= ps.lazy_thr) continue;  // keeps its fwd byte: the sums wait
+            const uint32_t k1 = ps.acc_f[q];
+            const uint32_t r = ps.rev[q];
+            const bool local = r != NO_PAIR && !(r & HALO);
+            const uint32_t sends = local ? ps.acc_s[r] : 0u;
+            if (!(k1 | sends | k4a[i])) continue;
+            if (k1) ps.acc_f[q] = 0;
+            if (sends) ps.acc_s[r] = 0;
+            if (k4a[i]) ps.invcnt[q] = 0;
+            fold_pair(ps, s, q, k1, sends - k1, k4a[i]);
+            s.score[q] = eval_pair(s, pp, q);
+            const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
+            if (nb != ob) {
+                ps.fwd[q] = nb;
+                const uint32_t k = atomicAdd(ps.nchg, 1u);
+                if (k < ps.chg_cap) ps.chg[k] = (uint32_t)q;
+                if ((nb ^ ob) & FWD_GIN) atomicAdd(ps.gray_pairs, (nb & FWD_GIN) ? 1ull : ~0ull);  // (+1 / -1)
+            }
+        }
+    }
+}
+
+// Every deferred sum folded (before a reader of records or scores); the
+// folded pairs are marked stale for the caller's re-score.
+__global__ __launch_bounds__(256) void k_prop_fold_acc(PropState ps, DevState s) {
+    const bool fold_topic = ps.topic < s.n_topics && s.tp[ps.topic].scored;
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        const uint32_t k1 = ps.acc_f[q];
+        const uint32_t r = ps.rev[q];
+        const uint32_t sends = (r != NO_PAIR && !(r & HALO)) ? ps.acc_s[r] : 0u;
+        if (!(k1 | sends) || !fold_topic || !(s.pflags[q] & PAIR_PRESENT)) continue;
+        fold_pair(ps, s, q, k1, sends - k1, 0);
+        ps.stale[q] = 1;
+    }
 }
 
 // Fold of pending counts (gsx_prop_fold_credits; GSX_CREDIT_NOW folds in k_prop_count).
@@ -1818,6 +1897,16 @@ hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, 
     else if (fold && rescore) hipLaunchKernelGGL((k_prop_count<true, true>), g, b, 0, st, ps, s, pp);
     else if (fold) hipLaunchKernelGGL((k_prop_count<true, false>), g, b, 0, st, ps, s, pp);
     else hipLaunchKernelGGL((k_prop_count<false, false>), g, b, 0, st, ps, s, pp);
+    return hipGetLastError();
+}
+hipError_t launch_prop_defer(const PropState& ps, const DevState& s, const DevPeerParams& pp, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_defer, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s, pp);
+    return hipGetLastError();
+}
+hipError_t launch_prop_fold_acc(const PropState& ps, const DevState& s, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_fold_acc, dim3(std::min(nblk(ps.n_pairs, 256), 8192u)), dim3(256), 0, st, ps, s);
     return hipGetLastError();
 }
 hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* first, uint32_t* dup,

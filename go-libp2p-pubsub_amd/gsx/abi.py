@@ -225,6 +225,7 @@ GSX_ROUTER_FLOODSUB = 0
 GSX_ROUTER_GOSSIPSUB = 1
 GSX_ROUTER_RANDOMSUB = 2
 GSX_MAX_HOPS = 64
+GXF_MAX_HOPS = 4096  # hops of one forwarding run of the gossip exchange (gsx_device.h)
 GSX_CREDIT_OFF = 0
 GSX_CREDIT_NOW = 1
 GSX_CREDIT_DEFER = 2
@@ -407,6 +408,7 @@ SIGNATURES = {
     "gsx_gxf_recv_fout": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_gxf_pack": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint64), C.c_void_p]),
     "gsx_gxf_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "gsx_gxf_pack_dev": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     "gsx_gxf_end": (C.c_int, [C.c_void_p]),
     "gsx_gx_got": (C.c_int, [C.c_void_p, P(C.c_uint8)]),
     "gsx_gx_end": (C.c_int, [C.c_void_p, P(C.c_uint8), P(HeartbeatOut)]),
@@ -439,6 +441,7 @@ SIGNATURES = {
     "gsx_prop_pack_compact": (C.c_int, [C.c_void_p, C.c_void_p, _u64p]),
     "gsx_prop_step_compact": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, _u64p]),
     "gsx_prop_pack_compact_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_prop_hop_counts_dev": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_hb_set_px_log": (C.c_int, [C.c_void_p, C.c_size_t]),
     "gsx_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
     "gsx_prop_begin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig)]),

@@ -313,12 +313,19 @@ class Engine:
         p = send.data_ptr() if hasattr(send, "data_ptr") else send
         self._chk(self.lib.gsx_prop_pack(self.h, C.c_void_p(p or None)), "gsx_prop_pack")
 
-    def prop_step(self, recv) -> int:
-        """recv: device buffer (torch tensor or pointer) of the received rows; -> this hop's first receipts."""
+    def prop_step(self, recv, sync: bool = True):
+        """recv: device buffer (torch tensor or pointer) of the received rows; -> this hop's first
+        receipts (sync=False: no host sync, -> None)."""
         p = recv.data_ptr() if hasattr(recv, "data_ptr") else recv
         n = C.c_uint64()
-        self._chk(self.lib.gsx_prop_step(self.h, C.c_void_p(p or None), C.byref(n)), "gsx_prop_step")
-        return int(n.value)
+        self._chk(self.lib.gsx_prop_step(self.h, C.c_void_p(p or None), C.byref(n) if sync else None),
+                  "gsx_prop_step")
+        return int(n.value) if sync else None
+
+    def prop_hop_counts_dev(self, out):
+        """out: device int64 buffer of GSX_MAX_HOPS + 1: the call's first receipts per hop (no host sync)."""
+        p = out.data_ptr() if hasattr(out, "data_ptr") else out
+        self._chk(self.lib.gsx_prop_hop_counts_dev(self.h, C.c_void_p(p)), "gsx_prop_hop_counts_dev")
 
     def prop_end(self) -> abi.PropOut:
         out = abi.PropOut()
@@ -464,10 +471,16 @@ class Engine:
                   "gsx_gxf_pack")
         return cnt
 
-    def gxf_step(self, hop: int, entries, n: int) -> int:
+    def gxf_step(self, hop: int, entries, n: int, sync: bool = True):
+        """-> this rank's new frontier (sync=False: no host sync, -> None)."""
         f = C.c_uint64()
-        self._chk(self.lib.gsx_gxf_step(self.h, hop, self._p(entries), n, C.byref(f)), "gsx_gxf_step")
-        return int(f.value)
+        self._chk(self.lib.gsx_gxf_step(self.h, hop, self._p(entries), n, C.byref(f) if sync else None),
+                  "gsx_gxf_step")
+        return int(f.value) if sync else None
+
+    def gxf_pack_dev(self, hop: int, out, d_counts):
+        """Entries into out (dense segments), (entries per rank, frontier of hop - 1) into d_counts; no sync."""
+        self._chk(self.lib.gsx_gxf_pack_dev(self.h, hop, self._p(out), self._p(d_counts)), "gsx_gxf_pack_dev")
 
     def gxf_end(self):
         self._chk(self.lib.gsx_gxf_end(self.h), "gsx_gxf_end")

@@ -135,12 +135,17 @@ class RangeSharded:
 
     compact=True (default): per hop only the non-empty cross-shard rows
     travel, as (receive slot, row) entries — one small all-to-all of the
-    entry counts, then the entries; compact=False moves every cross pair's
-    row (fixed splits, one collective per hop)."""
+    entry counts, then the entries (one host round trip per hop: the entry
+    splits are host lists); compact=False moves every cross pair's row with
+    fixed splits, so hops run back to back with no host sync: every `chunk`
+    hops one all-reduce of the per-hop delivery counts (device) and one read
+    find the hop that delivered nothing on any rank — the hops after it were
+    empty and changed nothing (1 / chunk host syncs per hop)."""
 
-    def __init__(self, backend, rank_lo, transport, compact=True):
+    def __init__(self, backend, rank_lo, transport, compact=True, chunk=4):
         self.be = backend
         self.compact = compact
+        self.chunk = max(1, int(chunk))  # dense exchange: hops per host check of the global frontier
         self.rank_lo = np.asarray(rank_lo, dtype=np.uint32)
         self.tp = transport
         exchange_plan(backend, self.rank_lo, transport)
@@ -151,6 +156,8 @@ class RangeSharded:
         self.sent_bytes = 0  # exchange volume this rank sent (cumulative)
         self.hops_run = 0  # hops run (cumulative) and host round trips they took
         self.host_syncs = 0
+        self.gx_hops = 0  # heartbeat forwarding hops (gossip exchange) and their host round trips
+        self.gx_syncs = 0
         dev = getattr(transport, "device", None)
         self._stream = None
         if hasattr(backend, "set_stream") and dev is not None and _torch().device(dev).type == "cuda":
@@ -225,21 +232,28 @@ class RangeSharded:
         if not self.compact:
             send, recv = self._buffers(W)
         be.prop_begin(msgs, cfg)
-        flag = torch.zeros(1, dtype=torch.int64, device=tp.device)
-        for h in range(cfg.max_hops):
-            if self.compact:
+        if self.compact:
+            for h in range(cfg.max_hops):
                 if not self._hop_compact(W, h == 0):
                     break
-                continue
-            be.prop_pack(send)
-            tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
-            self.sent_bytes += self.n_send * W * 8
-            flag.fill_(be.prop_step(recv))
-            tp.all_reduce_sum(flag)
-            self.hops_run += 1
-            self.host_syncs += 2
-            if int(flag.item()) == 0:
-                break
+        else:
+            cnt = torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=tp.device)
+            h = 0
+            while h < cfg.max_hops:
+                k = min(self.chunk, cfg.max_hops - h)
+                for _ in range(k):  # no host sync inside the chunk
+                    be.prop_pack(send)
+                    tp.all_to_all(recv[: self.n_recv], send[: self.n_send], self.recv_counts, self.send_counts)
+                    self.sent_bytes += self.n_send * W * 8
+                    be.prop_step(recv, sync=False)
+                    self.hops_run += 1
+                h += k
+                be.prop_hop_counts_dev(cnt)
+                tp.all_reduce_sum(cnt)
+                c = cnt.cpu().numpy()  # the chunk's one host sync
+                self.host_syncs += 1
+                if (c[h - k + 1 : h + 1] == 0).any():
+                    break
         out = be.prop_end()
         return out_dict(out), totals(out, tp)
 
@@ -334,15 +348,45 @@ class RangeSharded:
             tp.all_to_all(r1[: self.n_recv], s1[: self.n_send], self.recv_counts, self.send_counts)
             be.gxf_recv_fout(r1)
             words = be.gxf_entry_words()
-            hop = 1
-            while True:
-                ent, n_ent = self._entries(be.gxf_pack(hop, W), words, lambda out, h=hop: be.gxf_pack(h, W, out))
-                front = be.gxf_step(hop, ent, n_ent)
-                t = torch.tensor([front], dtype=torch.int64, device=dev)
-                tp.all_reduce_sum(t)
-                if int(t.item()) == 0:
+            if not hasattr(be, "gxf_pack_dev"):  # (a backend without the device-count pack)
+                hop = 1
+                while True:
+                    ent, n_ent = self._entries(be.gxf_pack(hop, W), words, lambda out, h=hop: be.gxf_pack(h, W, out))
+                    front = be.gxf_step(hop, ent, n_ent)
+                    t = torch.tensor([front], dtype=torch.int64, device=dev)
+                    tp.all_reduce_sum(t)
+                    self.gx_hops += 1
+                    self.gx_syncs += 4
+                    if int(t.item()) == 0:
+                        break
+                    hop += 1
+                be.gxf_end()
+                continue
+            # one host round trip per hop: the pack leaves (entries for rank k, this
+            # rank's frontier of the hop before) on the device; one all-to-all of the
+            # pairs, one read; the run ends at the pack after a hop that left no
+            # frontier on any rank
+            out = torch.zeros((max(self.n_send, 1), words), dtype=torch.int64, device=dev)
+            sc = torch.zeros((W, 2), dtype=torch.int64, device=dev)
+            rc = torch.zeros((W, 2), dtype=torch.int64, device=dev)
+            sb = np.concatenate([[0], np.cumsum(self.send_counts)[:-1]])
+            hop, held = 1, None
+            while hop < abi.GXF_MAX_HOPS:
+                be.gxf_pack_dev(hop, out, sc)
+                tp.all_to_all(rc, sc, [1] * W, [1] * W)
+                hc = torch.cat([sc, rc], 0).cpu().numpy()  # the hop's one host sync
+                self.gx_syncs += 1
+                if hop > 1 and int(hc[W:, 1].sum()) == 0:
                     break
+                cnt, rcnt = hc[:W, 0], hc[W:, 0]
+                n_in = int(rcnt.sum())
+                recv = torch.zeros((max(n_in, 1), words), dtype=torch.int64, device=dev)
+                tp.all_to_all_parts(recv[:n_in], rcnt, [out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(W)])
+                be.gxf_step(hop, recv, n_in, sync=False)
+                held = recv  # (read by the hop's kernels: alive until the next sync)
+                self.gx_hops += 1
                 hop += 1
+            del held
             be.gxf_end()
         got = be.gx_got(n_sets)
         if n_sets:

@@ -577,6 +577,13 @@ int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_ent
  * and, summed, whether the previous hop delivered anything on any rank, so a
  * sharded hop needs one host round trip (RangeSharded). */
 int gsx_prop_pack_compact_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts);
+/* The first receipts of hops 0 .. GSX_MAX_HOPS of the call in flight on this
+ * rank, copied to d_out (device, GSX_MAX_HOPS + 1 i64) in stream order with no
+ * host sync: with the dense exchange (gsx_prop_pack / gsx_prop_step with
+ * n_new NULL) a driver runs several hops back to back and sums these over the
+ * ranks once per chunk to find the hop that delivered nothing anywhere (the
+ * hops after it deliver nothing and change nothing). */
+int gsx_prop_hop_counts_dev(gsx_engine* e, int64_t* d_out);
 
 /* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
 
@@ -790,6 +797,7 @@ int gsx_hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out)
  *                       then per hop h = 1, 2, ...: pack, the all-to-all, step,
  *                       until a hop leaves no frontier on any rank; end)
  *   gsx_gxf_step        hop h with the received entries; *n_front: this rank's new frontier
+ *                       (NULL: no host sync; see gsx_gxf_pack_dev)
  *   gsx_gx_got          per message set: a node of this rank delivered one of its messages
  *   gsx_gx_end          with their OR over every rank: the merge, the Shift, the
  *                       recovered copies Put (the same batches on every rank) */
@@ -808,6 +816,16 @@ int gsx_gxf_pack_fout(gsx_engine* e, uint64_t* send);
 int gsx_gxf_recv_fout(gsx_engine* e, const uint64_t* recv);
 int gsx_gxf_pack(gsx_engine* e, uint32_t hop, uint64_t* counts, uint64_t* out);
 int gsx_gxf_step(gsx_engine* e, uint32_t hop, const uint64_t* entries, uint64_t n, uint64_t* n_front);
+/* gsx_gxf_pack with no host sync: out (device, n_send entries of
+ * gsx_gxf_entry_words) gets destination d's entries from entry send_base[d]
+ * (the shard plan's send segment of d) on, and d_counts (device, n_ranks x 2
+ * i64) the pairs (entries for rank d, this rank's frontier size of hop - 1).
+ * One all-to-all of the pairs gives every rank its entry splits and, summed,
+ * whether hop - 1 left a frontier on any rank (the run is over when it did
+ * not), so a forwarding hop needs one host round trip; gsx_gxf_step with
+ * n_front NULL then runs the hop without a sync (keep the entries alive until
+ * the stream has run it). */
+int gsx_gxf_pack_dev(gsx_engine* e, uint32_t hop, uint64_t* out, int64_t* d_counts);
 int gsx_gxf_end(gsx_engine* e);
 int gsx_gx_got(gsx_engine* e, uint8_t* got);
 int gsx_gx_end(gsx_engine* e, const uint8_t* got_all, gsx_heartbeat_out* out);

@@ -283,11 +283,31 @@ class EmuShard:
     def gxf_pack(self, hop, n_ranks, out=None):
         return self._entries(self._fwd_keep(hop), lambda v, u: [v << 32 | u, hop, self.gx_run], out)
 
-    def gxf_step(self, hop, entries, n):
+    def gxf_pack_dev(self, hop, out, d_counts):
+        """gsx_gxf_pack_dev: destination d's entries from entry send_base[d] on, and
+        (entries for rank d, this rank's frontier of hop - 1) per destination."""
+        keep, words = self._fwd_keep(hop), (lambda v, u: [v << 32 | u, hop, self.gx_run])
+        cnt = np.zeros(len(self.send_counts), dtype=np.int64)
+        a = np.zeros((max(len(self.send_pair), 1), 4), dtype=np.uint64)
+        for d in range(len(self.send_counts)):
+            for j in range(int(self.send_base[d]), int(self.send_base[d + 1])):
+                r = self.send_pair[j]
+                if r is None:
+                    continue
+                v, u = self._pair_ids(r)
+                if keep(v, u):
+                    a[int(self.send_base[d]) + cnt[d]] = [int(self.halo_base[d] + j - self.send_base[d])] + words(v, u)
+                    cnt[d] += 1
+        out[: len(a)].copy_(_as_tensor(a.view(np.int64)))
+        front = 1 if hop == 1 else (1 if hop - 1 < 2 + self.gx_run else 0)
+        d_counts.copy_(_as_tensor(np.stack([cnt, np.full(len(cnt), front, dtype=np.int64)], 1)))
+
+    def gxf_step(self, hop, entries, n, sync=True):
         assert hop == self.gx_hops[-1] + 1
         self.gx_hops[-1] = hop
         self.gx_fwd += self._check_entries(entries, n, self._fwd_keep(hop), lambda v, u: [v << 32 | u, hop, self.gx_run])
-        return 1 if hop < 2 + self.gx_run else 0
+        f = 1 if hop < 2 + self.gx_run else 0
+        return f if sync else None
 
     def gxf_end(self):
         assert self.gx_hops[-1] == 2 + self.gx_run
@@ -378,10 +398,18 @@ class EmuShard:
         e = entries[:n].numpy().view(np.uint64)
         for row in e:
             halo[int(row[0])] = row[1:]
-        v = self.prop_step(_as_tensor(halo.view(np.int64)))
+        v = self._prop_step(_as_tensor(halo.view(np.int64)))
         return v if sync else None
 
-    def prop_step(self, recv):
+    def prop_hop_counts_dev(self, out):
+        """gsx_prop_hop_counts_dev: this rank's first receipts per hop."""
+        out.copy_(_as_tensor(np.array(self.stats["hop"], dtype=np.int64)))
+
+    def prop_step(self, recv, sync=True):
+        v = self._prop_step(recv)
+        return v if sync else None
+
+    def _prop_step(self, recv):
         halo = recv.numpy().view(np.uint64) if len(recv) else None
         self.h += 1
         h, W = self.h, self.W
