@@ -417,7 +417,7 @@ struct gsx_engine {
     // folds the sums (topic def_topic) before anything reads records or scores.
     uint32_t *d_acc_s = nullptr, *d_acc_f = nullptr;
     bool deferred = false;
-    uint32_t def_topic = 0;
+    uint32_t def_topic = 0, def_flood = 0;  // the topic and flood_publish setting the sums were deferred under
     double lazy_thr = 0;
     uint8_t* d_stale = nullptr;
     void invalidate_scores() {
@@ -2468,6 +2468,10 @@ int prop_event_pair(gsx_engine* e, hipEvent_t* a, hipEvent_t* b) {
 int fanout_publish(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg) {
     if (!(e->members_on && cfg->router == GSX_ROUTER_GOSSIPSUB && !cfg->flood_publish && cfg->topic < e->T))
         return GSX_OK;
+    // the pick reads scores against PublishThreshold, which deferred gossipsub pairs may not have reached yet
+    if (int rc = fold_deferred(e)) return rc;
+    if (e->lazy)
+        if (int rc = ensure_scores(e)) return rc;
     const size_t N = e->n_nodes;
     std::vector<uint32_t> src;
     std::vector<uint8_t> done(N, 0);
@@ -2512,7 +2516,9 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     // the other routers never
     const bool need_score = cfg->router == GSX_ROUTER_GOSSIPSUB;
     // deferred credits of another topic (or a call that folds its own way) land first
-    if (e->deferred && (cfg->topic != e->def_topic || cfg->credit_scores != GSX_CREDIT_NOW || cfg->router != GSX_ROUTER_GOSSIPSUB))
+    // (a gossipsub pair defers above the graylist threshold alone unless the call flood-publishes: k_prop_defer)
+    if (e->deferred && (cfg->topic != e->def_topic || cfg->credit_scores != GSX_CREDIT_NOW ||
+                        cfg->router != GSX_ROUTER_GOSSIPSUB || cfg->flood_publish != e->def_flood))
         if (int rc = fold_deferred(e)) return rc;
     if (int rc = flush(e)) return rc;  // queued events land first either way
     // (after lazy folds the fwd bytes stand for thresholds up to lazy_thr: the stale scores wait)
@@ -2800,7 +2806,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     static const bool no_defer = getenv("GSX_NO_DEFER_FOLD") != nullptr;
     const bool defer = lazy && !no_defer && ps.late && ps.credit && !e->sharded() && !P.credit_pending &&
                        P.cfg.credit_scores == GSX_CREDIT_NOW && ps.topic < e->T && e->scored[ps.topic] &&
-                       (!e->deferred || e->def_topic == ps.topic);
+                       (!e->deferred || (e->def_topic == ps.topic && e->def_flood == ps.flood_publish));
     if (defer && !e->d_acc_s) {
         const size_t E = std::max<size_t>(e->E, 1);
         if (int rc = dalloc(e, &e->d_acc_s, E)) return rc;
@@ -2857,6 +2863,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
             HIPCHK(e, gsx::launch_prop_defer(pc, dev_state(e), dev_peer_params(e), e->stream));
             e->deferred = true;
             e->def_topic = ps.topic;
+            e->def_flood = ps.flood_publish;
             ++e->rec_gen;  // (the immediate folds bypass the topic-term cache)
         } else {
             HIPCHK(e, gsx::launch_prop_count(pc, dev_state(e), fold_now, rescore, dev_peer_params(e), e->stream));

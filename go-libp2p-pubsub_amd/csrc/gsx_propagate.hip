@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
     const uint64_t* src_occ = ps.occ;  // row 0: nodes that published in this call
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     for (uint64_t r0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; r0 < ps.n_pairs; r0 += stride * DU) {
-        uint32_t qa[DU], va[DU], ua[DU];
+        uint32_t qa[DU], va[DU], ua[DU], af[DU], as_[DU];
         uint8_t fa[DU];
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
@@ -1138,6 +1138,9 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             fa[i] = in ? ps.fwd[r] : 0;
             va[i] = in ? ps.pair_obs[r] : 0;
             ua[i] = in ? (uint32_t)ps.col[r] - ps.node_lo : 0;
+            // deferred folds: the pair's sums, loaded with the rest (written back below)
+            af[i] = (!GRAY_ONLY && ps.acc_f && in) ? ps.acc_f[r] : 0u;
+            as_[i] = (!GRAY_ONLY && ps.acc_s && in) ? ps.acc_s[r] : 0u;
         }
         bool ga[DU];  // u drops v's copies: the GIN bit of u's pair (v's reverse), kept beside r by k_prop_pin
 #pragma unroll
@@ -1163,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             for (int i = 0; i < DU; ++i) {
                 const uint64_t r = r0 + i * stride;
                 if (r >= ps.n_pairs || !fca[i]) continue;
-                ps.acc_f[r] += fca[i];
+                ps.acc_f[r] = af[i] + fca[i];
                 const uint32_t rr = ps.rev[r];
                 if (rr != NO_PAIR && !(rr & HALO)) cnt[2] += fca[i];  // the back-sends (k_prop_count's count)
             }
@@ -1218,7 +1221,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             } else {
                 cnt[0] += sends;
                 if (ps.acc_s) {  // deferred folds: the sends join the sender pair's sum
-                    if (sends) ps.acc_s[r] += sends;
+                    if (sends) ps.acc_s[r] = as_[i] + sends;
                 } else {
                     ps.corr[r] = sends;
                 }
@@ -1536,11 +1539,18 @@ __global__ __launch_bounds__(256) void k_prop_count(PropState ps, DevState s, De
 __global__ __launch_bounds__(256) void k_prop_defer(PropState ps, DevState s, DevPeerParams pp) {
     const bool fold_topic = ps.topic < s.n_topics && s.tp[ps.topic].scored;
     if (!fold_topic) return;
+    // The score a pair's own fwd byte tests (fwd_byte): none for a direct peer;
+    // AcceptFrom's graylist threshold; the publish threshold too for a floodsub
+    // peer or flood publishing.  Credits only raise the score, so a pair at or
+    // above its threshold keeps its byte while its sums wait; a graylisted pair
+    // (FWD_GIN) accepts no copy of the sender, so it has no credits at all.
+    const double thr_gs = ps.gate ? ps.graylist_threshold : -__builtin_inf();
+    const double thr_all = ps.gate ? fmax(ps.graylist_threshold, ps.publish_threshold) : ps.publish_threshold;
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     for (uint64_t q0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; q0 < ps.n_pairs; q0 += stride * DU) {
         double sc[DU];
         uint32_t k4a[DU];
-        uint8_t pf[DU];
+        uint8_t pf[DU], ef[DU], fb[DU];
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
             const uint64_t q = q0 + i * stride;
@@ -1548,16 +1558,31 @@ __global__ __launch_bounds__(256) void k_prop_defer(PropState ps, DevState s, De
             sc[i] = in ? s.score[q] : 0.0;
             k4a[i] = (in && ps.drop) ? ps.invcnt[q] : 0u;
             pf[i] = in ? s.pflags[q] : 0;
+            ef[i] = in ? ps.eflags[q] : 0;
+            fb[i] = in ? ps.fwd[q] : 0;
         }
+        bool now_[DU];
 #pragma unroll
         for (int i = 0; i < DU; ++i) {
             const uint64_t q = q0 + i * stride;
+            now_[i] = false;
             if (q >= ps.n_pairs) continue;
             if (!(pf[i] & PAIR_PRESENT)) {  // no peerStats: nothing to credit (the sums are cleared at the fold)
                 if (k4a[i]) ps.invcnt[q] = 0;
                 continue;
             }
-            if (k4a[i] == 0 && sc[i] >= ps.lazy_thr) continue;  // keeps its fwd byte: the sums wait
+            if (k4a[i]) {  // invalid deliveries lower the score: fold now
+                now_[i] = true;
+                continue;
+            }
+            if ((ef[i] & EDGE_DIRECT) || (fb[i] & FWD_GIN)) continue;
+            const double thr = (!(ef[i] & EDGE_GOSSIPSUB) || ps.flood_publish) ? thr_all : thr_gs;
+            now_[i] = !(sc[i] >= thr);
+        }
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            if (!now_[i]) continue;
+            const uint64_t q = q0 + i * stride;
             const uint32_t k1 = ps.acc_f[q];
             const uint32_t r = ps.rev[q];
             const bool local = r != NO_PAIR && !(r & HALO);
@@ -1568,7 +1593,7 @@ __global__ __launch_bounds__(256) void k_prop_defer(PropState ps, DevState s, De
             if (k4a[i]) ps.invcnt[q] = 0;
             fold_pair(ps, s, q, k1, sends - k1, k4a[i]);
             s.score[q] = eval_pair(s, pp, q);
-            const uint8_t ob = ps.fwd[q], nb = fwd_byte(ps, s, q);
+            const uint8_t ob = fb[i], nb = fwd_byte(ps, s, q);
             if (nb != ob) {
                 ps.fwd[q] = nb;
                 const uint32_t k = atomicAdd(ps.nchg, 1u);

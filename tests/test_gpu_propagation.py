@@ -225,8 +225,10 @@ def test_randomsub_full_hub_matches_oracle(gpu_ok):
     assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))
 
 
-@pytest.mark.parametrize("mix,scores_each", [(False, True), (True, True), (False, False), (True, False)],
-                         ids=["gossipsub-only", "with-floodsub-peers", "gossipsub-only-lazy", "with-floodsub-peers-lazy"])
+@pytest.mark.parametrize("mix,scores_each", [(False, True), (True, True), (False, False), (True, False),
+                                             (False, None), (True, None)],
+                         ids=["gossipsub-only", "with-floodsub-peers", "gossipsub-only-lazy", "with-floodsub-peers-lazy",
+                              "gossipsub-only-deferred", "with-floodsub-peers-deferred"])
 def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix, scores_each):
     """One engine, many calls: the forwarding state (k_prop_fwd / k_prop_pin)
     is kept between calls while nothing it reads changed and rebuilt after
@@ -235,7 +237,10 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix, scores_each):
     Every call must match the oracle running the same sequence.  Without
     scores_each the scores are read only at the end, so the lazy folds'
     stale pairs (PropState::stale) carry across calls, events, raised
-    thresholds and heartbeats (which settle them)."""
+    thresholds and heartbeats (which settle them).  With scores_each None
+    neither the state nor the scores are read between calls, so the deferred
+    folds' sums (PropState::acc_s / acc_f) carry across calls until an event,
+    a refresh, new thresholds, a heartbeat or a topic switch folds them."""
     n, T = 600, 2
     ov = pc.overlay(n, 5, seed=31, mix_protocols=mix)
     E = ov.n_pairs
@@ -302,12 +307,17 @@ def test_propagation_sequence_reuses_forwarding_state(gpu_ok, mix, scores_each):
         (go, gh, _), (wo, wh, _) = res
         assert go.as_dict() == wo.as_dict(), name
         assert np.array_equal(gh, wh), name
+        if scores_each is None:
+            continue
         gs, ws = eng.export_state(), ref.export_state()
         for f in abi.STATE_FIELDS:
             assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), (name, f)
         if scores_each:
             assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64)), name
     assert np.array_equal(eng.scores().view(np.uint64), ref.scores().view(np.uint64))
+    gs, ws = eng.export_state(), ref.export_state()
+    for f in abi.STATE_FIELDS:
+        assert np.array_equal(gs[f].view(np.uint8), ws[f].view(np.uint8)), f
 
 
 @pytest.mark.parametrize("flood_publish,scores_each", [(0, True), (1, True), (0, False), (1, False)])
