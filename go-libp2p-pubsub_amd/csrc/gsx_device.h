@@ -611,8 +611,10 @@ struct GxFwd {
     uint16_t* bcnt[2];
     uint32_t seq;
     // per pair, this run: fout[r] = the slots whose topic the pair's owner
-    // forwards over r; fin[q] = fout[rev q] | GXF_GRAY (the receiver's AcceptFrom
-    // drops the peer of q)
+    // forwards over r (k_gxf_init); fin[q] = fout[rev q] | GXF_GRAY (the
+    // receiver's AcceptFrom drops the peer of q), a pass of its own on range
+    // shards only (remote senders' slots arrive there); null on one engine:
+    // the pull gathers fout[rev q] for the senders in the frontier alone
     uint8_t* fout;
     uint16_t* fin;
     // per receiver x, this run: its pairs whose sender forwards a run topic to

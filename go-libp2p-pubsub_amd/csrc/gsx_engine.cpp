@@ -3814,6 +3814,15 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
 
 // The forwarding of recovered messages (gsx.h (D), GxFwd): state allocated on
 // first use; the hop stamps only grow (re-zeroed before they could wrap).
+// The receiver-side slot pass (fin): range shards (the remote senders' slots
+// arrive as fin bits); one engine gathers fout[rev q] for the senders in the
+// frontier instead, in the pull or in the eligible-sender lists the first
+// dense hop builds (GSX_GXF_FIN=1: the pass on one engine too, A/B).
+bool gxf_fin_pass(const gsx_engine* e) {
+    static const bool env = getenv("GSX_GXF_FIN") != nullptr;
+    return e->sharded() || env;
+}
+
 int gxf_alloc(gsx_engine* e) {
     const size_t n_grp = std::max<size_t>({e->gxr.grp_topic.size(), (size_t)e->T, 1});
     if (e->d_gxf_b0 && n_grp > e->gxf_b0_grps) {  // more set groups than topics this round
@@ -3834,6 +3843,8 @@ int gxf_alloc(gsx_engine* e) {
         }
         HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * std::max<size_t>(e->E, 1), e->stream));
     }
+    if (gxf_fin_pass(e) && !e->d_gxf_fin)
+        if (int rc = dalloc(e, &e->d_gxf_fin, std::max<size_t>(e->E, 1))) return rc;
     if (e->d_gxf_bst) {
         if (e->gxf_stamp < 0xF0000000u) return GSX_OK;
         HIPCHK(e, hipMemsetAsync(e->d_gxf_bst, 0, 4 * 3 * std::max<size_t>(e->E, 1), e->stream));
@@ -3846,10 +3857,10 @@ int gxf_alloc(gsx_engine* e) {
     if ((rc = dalloc(e, &e->d_gxf_mask, 4 * N + 2 * ((N + 63) / 64))) || (rc = dalloc(e, &e->d_gxf_list, 3 * N)) ||
         (rc = dalloc(e, &e->d_gxf_cnt, 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) || (rc = dalloc(e, &e->d_gxf_bst, 3 * E)) ||
         (rc = dalloc(e, &e->d_gxf_b0, n_grp * E)) ||
-        (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fin, E)) ||
-        (rc = dalloc(e, &e->d_gxf_fout, E)) || (rc = dalloc(e, &e->d_gxf_fent, E)) ||
-        (rc = dalloc(e, &e->d_gxf_fend, N)))
+        (rc = dalloc(e, &e->d_gxf_b, 2 * E * gsx::GXF_SLOTS)) || (rc = dalloc(e, &e->d_gxf_fout, E)) ||
+        (rc = dalloc(e, &e->d_gxf_fent, E)) || (rc = dalloc(e, &e->d_gxf_fend, N)))
         return rc;
+
     e->gxf_b0_grps = n_grp;
     if (e->sharded() && (rc = dalloc(e, &e->d_gxf_hst, 2 * E))) return rc;
     if (e->d_gxf_hst) HIPCHK(e, hipMemsetAsync(e->d_gxf_hst, 0, 4 * 2 * E, e->stream));
@@ -3965,7 +3976,7 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
     f.bcnt[1] = e->d_gxf_b + E * gsx::GXF_SLOTS;
     f.seq = e->gxf_stamp + 1;
     f.fout = e->d_gxf_fout;
-    f.fin = e->d_gxf_fin;
+    f.fin = gxf_fin_pass(e) ? e->d_gxf_fin : nullptr;
     static const bool no_compact = getenv("GSX_GXF_NO_COMPACT") != nullptr;  // (A/B)
     if (!no_compact) {
         f.fent = e->d_gxf_fent;

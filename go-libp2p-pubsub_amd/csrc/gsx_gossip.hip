@@ -958,8 +958,18 @@ __device__ __forceinline__ uint64_t gxf_origin(const GxFwdSet& S, uint32_t x, ui
 // Hop 0: every node's accepted receipts of the round per set (its frontier
 // rows), the frontier list; and each set's origins into srcm (a thread per
 // (set, message) in the grid's second half).
-__global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t n_src_total, uint32_t node_lo) {
+__device__ __forceinline__ uint32_t gxf_fout_bits(const DevState& s, const HbState& h, const GxFwd& f, uint64_t r,
+                                                  uint32_t v) {
+    uint32_t b = 0;
+    for (uint32_t ts = 0; ts < f.n_slots; ++ts)
+        if (gxf_elig(s, h, r, v, f.slot_topic[ts])) b |= 1u << ts;
+    return b;
+}
+// Hop 0 and the run's forwarding slots (fout) of every node's row, node-parallel.
+__global__ __launch_bounds__(256) void k_gxf_init(DevState s, HbState h, GxFwd f, uint32_t n, uint32_t n_src_total,
+                                                  uint32_t node_lo) {
     for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u) {
+        for (int64_t r = h.row_ptr[u]; r < h.row_ptr[u + 1]; ++r) f.fout[r] = (uint8_t)gxf_fout_bits(s, h, f, (uint64_t)r, u);
         uint64_t m = 0;
         for (uint32_t si = 0; si < f.n_sets; ++si) {
             const GxFwdSet& S = f.sets[si];
@@ -985,17 +995,8 @@ __global__ __launch_bounds__(256) void k_gxf_init(GxFwd f, uint32_t n, uint32_t 
     }
 }
 
-// The run's per-pair forwarding slots (fout, by the owner's row) and their
-// receiver-side view (fin, one gather of the reverse pair's byte).
-__global__ __launch_bounds__(256) void k_gxf_fout(DevState s, HbState h, GxFwd f) {
-    for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < h.n_nodes; v += gridDim.x * 256u)
-        for (int64_t r = h.row_ptr[v]; r < h.row_ptr[v + 1]; ++r) {
-            uint32_t b = 0;
-            for (uint32_t ts = 0; ts < f.n_slots; ++ts)
-                if (gxf_elig(s, h, (uint64_t)r, v, f.slot_topic[ts])) b |= 1u << ts;
-            f.fout[r] = (uint8_t)b;
-        }
-}
+// The receiver-side view of the run's forwarding slots on a range shard (fin,
+// one gather of the reverse pair's byte; the remote ones arrive after).
 __global__ __launch_bounds__(256) void k_gxf_fin(DevState s, HbState h, GxFwd f) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < h.n_pairs; q += (uint64_t)gridDim.x * 256u) {
         const uint32_t r = h.rev[q];
@@ -1005,17 +1006,50 @@ __global__ __launch_bounds__(256) void k_gxf_fin(DevState s, HbState h, GxFwd f)
     }
 }
 
-// The run's eligible senders per receiver (GxFwd::fent), node-parallel, in pair order.
-__global__ __launch_bounds__(256) void k_gxf_compact(HbState h, GxFwd f) {
+// The run's eligible senders per receiver (GxFwd::fent), node-parallel, in
+// pair order: from fin on a range shard, else fout[rev q] and x's AcceptFrom.
+__device__ __forceinline__ void gxf_compact_rows(const DevState& s, const HbState& h, const GxFwd& f) {
+    constexpr int CB = 8;  // pairs whose loads are in flight together (rev, then the fout gathers)
     for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < h.n_nodes; x += gridDim.x * 256u) {
-        int64_t k = h.row_ptr[x];
-        for (int64_t q = h.row_ptr[x]; q < h.row_ptr[x + 1]; ++q) {
-            const uint32_t fi = f.fin[q];
-            if (!(fi & 0xFFu)) continue;
-            f.fent[k++] = make_uint4((uint32_t)q, h.rev[q], (uint32_t)h.col[q] - h.node_lo, fi);
+        const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
+        int64_t k = r0;
+        for (int64_t q0 = r0; q0 < r1; q0 += CB) {
+            uint32_t rr[CB], fi[CB];
+#pragma unroll
+            for (int j = 0; j < CB; ++j) rr[j] = q0 + j < r1 ? h.rev[q0 + j] : NO_PAIR;
+#pragma unroll
+            for (int j = 0; j < CB; ++j) {
+                if (f.fin) fi[j] = q0 + j < r1 ? (uint32_t)f.fin[q0 + j] : 0u;
+                else fi[j] = rr[j] == NO_PAIR ? 0u : (uint32_t)f.fout[rr[j]];
+            }
+#pragma unroll
+            for (int j = 0; j < CB; ++j) {
+                if (!(fi[j] & 0xFFu)) continue;
+                const int64_t q = q0 + j;
+                if (!f.fin && !(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) fi[j] |= GXF_GRAY;
+                f.fent[k++] = make_uint4((uint32_t)q, rr[j], (uint32_t)h.col[q] - h.node_lo, fi[j]);
+            }
         }
         f.fend[x] = (uint32_t)k;
     }
+}
+__global__ __launch_bounds__(256) void k_gxf_compact(DevState s, HbState h, GxFwd f) { gxf_compact_rows(s, h, f); }
+
+// A hop whose frontier holds more than n / f.dense_div nodes (GXF_DENSE by
+// default) pulls at every node (no marking): cheaper than its atomics and lists.
+__device__ __forceinline__ bool gxf_dense(const GxFwd& f, uint32_t hop, uint32_t n) {
+    return (uint64_t)f.fcnt[hop - 1] * f.dense_div > n;
+}
+// The eligible-sender lists are there for hop `hop`: on a range shard from hop
+// 1 on; on one engine from the run's first dense hop on (its k_gxf_mark builds
+// them: a sparse hop's few receivers walk their rows as cheaply, and a run of
+// sparse hops never pays for the lists).
+__device__ __forceinline__ bool gxf_fent_ready(const GxFwd& f, uint32_t hop, uint32_t n) {
+    if (!f.fent) return false;
+    if (f.fin) return true;
+    for (uint32_t z = 1; z <= hop; ++z)
+        if (gxf_dense(f, z, n)) return true;
+    return false;
 }
 
 __device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots) {
@@ -1023,9 +1057,6 @@ __device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots
     for (; slots; slots &= slots - 1) m |= f.slot_sets[__builtin_ctz(slots)];
     return m;
 }
-// A hop whose frontier holds more than n / f.dense_div nodes (GXF_DENSE by
-// default) pulls at every node (no marking): cheaper than its atomics and lists.
-
 __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1;
     const uint32_t stride = gridDim.x * 256u;
@@ -1036,7 +1067,10 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
             for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (h.n_nodes + 63) / 64; i += stride) f.fbit[hop & 1][i] = 0;
     }
     const uint32_t nf = f.fcnt[hop - 1];
-    if ((uint64_t)nf * f.dense_div > h.n_nodes) return;  // a dense hop: the pull visits every node
+    if (gxf_dense(f, hop, h.n_nodes)) {  // a dense hop: the pull visits every node
+        if (f.fent && !f.fin && !gxf_fent_ready(f, hop - 1, h.n_nodes)) gxf_compact_rows(s, h, f);  // the first
+        return;
+    }
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nf; i += stride) {
         const uint32_t v = f.flist[p][i];
         const uint64_t M = f.fmask[p][v];
@@ -1255,7 +1289,8 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
     const uint32_t S_ = h.prom_slots;
     const uint32_t lc = threadIdx.x % G;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
-    const bool dense = (uint64_t)f.fcnt[hop - 1] * f.dense_div > h.n_nodes;
+    const bool dense = gxf_dense(f, hop, h.n_nodes);
+    const bool fe = gxf_fent_ready(f, hop, h.n_nodes);
     const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G; i < nr; i += gridDim.x * (256u / G)) {
         const uint32_t x = dense ? i : f.rlist[i];
@@ -1267,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
         const uint64_t srcm = f.srcm[x] & M;
         uint64_t newsets = 0;  // (the same in every lane of the group)
         const int64_t r0 = h.row_ptr[x], r1 = h.row_ptr[x + 1];
-        const int64_t e1 = f.fent ? (int64_t)f.fend[x] : r1;  // x's eligible senders (or every pair)
+        const int64_t e1 = fe ? (int64_t)f.fend[x] : r1;  // x's eligible senders (or every pair)
         for (int64_t qb0 = r0; qb0 < e1; qb0 += G * B) {
           uint32_t fis[B], rqs[B], vqs[B], qs[B];
           uint64_t fms[B];
@@ -1275,7 +1310,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
           for (int j = 0; j < B; ++j) {
               const int64_t ei = qb0 + j * G + lc;
               const bool in = ei < e1;
-              if (f.fent) {  // one 16-B load per sender: (q, rev q, peer, fin)
+              if (fe) {  // one 16-B load per sender: (q, rev q, peer, fin)
                   const uint4 en = in ? f.fent[ei] : make_uint4(0u, NO_PAIR, 0u, 0u);
                   qs[j] = en.x;
                   rqs[j] = en.y;
@@ -1283,23 +1318,37 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                   fis[j] = en.w;
               } else {
                   qs[j] = (uint32_t)ei;
-                  fis[j] = in ? (uint32_t)f.fin[ei] : 0u;
+                  fis[j] = in && f.fin ? (uint32_t)f.fin[ei] : 0u;
                   rqs[j] = in ? h.rev[ei] : NO_PAIR;
                   vqs[j] = in ? (uint32_t)h.col[ei] - h.node_lo : 0u;  // (local index; unused if remote)
               }
           }
+          if (f.fin || fe) {
 #pragma unroll
-          for (int j = 0; j < B; ++j) {
-              fms[j] = 0;
-              if (!(fis[j] & 0xFFu)) continue;
-              if (rqs[j] & HALO) fms[j] = f.hstamp && f.hstamp[qs[j]] == seq_cur;  // a remote sender's entry this hop
-              else fms[j] = (f.fbit[p][vqs[j] >> 6] >> (vqs[j] & 63)) & 1;  // (L2-resident: filters the mask loads)
-          }
+            for (int j = 0; j < B; ++j) {
+                fms[j] = 0;
+                if (!(fis[j] & 0xFFu)) continue;
+                if (rqs[j] & HALO) fms[j] = f.hstamp && f.hstamp[qs[j]] == seq_cur;  // a remote sender's entry this hop
+                else fms[j] = (f.fbit[p][vqs[j] >> 6] >> (vqs[j] & 63)) & 1;  // (L2-resident: filters the mask loads)
+            }
 #pragma unroll
-          for (int j = 0; j < B; ++j) {
-              if (fms[j])
-                  fms[j] = ((rqs[j] & HALO) ? f.hent[(size_t)f.hidx[qs[j]] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vqs[j]]) &
-                           M & gxf_slot_sets(f, fis[j] & 0xFFu);
+            for (int j = 0; j < B; ++j) {
+                if (fms[j])
+                    fms[j] = ((rqs[j] & HALO) ? f.hent[(size_t)f.hidx[qs[j]] * (GXF_HDR + f.rw) + 1] : f.fmask[p][vqs[j]]) &
+                             M & gxf_slot_sets(f, fis[j] & 0xFFu);
+            }
+          } else {  // one engine: the frontier bit of every peer first, the slots of the senders in it
+#pragma unroll
+            for (int j = 0; j < B; ++j)
+                fms[j] = rqs[j] != NO_PAIR && ((f.fbit[p][vqs[j] >> 6] >> (vqs[j] & 63)) & 1);
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                if (!fms[j]) continue;
+                const uint64_t q = qs[j];
+                fis[j] = (uint32_t)f.fout[rqs[j]] |
+                         ((!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) ? GXF_GRAY : 0u);  // AcceptFrom at x
+                fms[j] = f.fmask[p][vqs[j]] & M & gxf_slot_sets(f, fis[j] & 0xFFu);
+            }
           }
           for (int j = 0; j < B; ++j) {  // the rounds in sender order
             const int64_t qb = qb0 + j * G;
@@ -1630,19 +1679,18 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
                            hipStream_t st) {
     const uint64_t n = std::max<uint64_t>(h.n_nodes, n_src_total);
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, f, h.n_nodes, n_src_total,
+    hipLaunchKernelGGL(k_gxf_init, dim3(gx_blocks(n, 256, 4096)), dim3(256), 0, st, s, h, f, h.n_nodes, n_src_total,
                        h.node_lo);
-    hipLaunchKernelGGL(k_gxf_fout, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f);
-    hipLaunchKernelGGL(k_gxf_fin, dim3(gx_blocks(h.n_pairs, 256, 8192)), dim3(256), 0, st, s, h, f);
+    if (f.fin) hipLaunchKernelGGL(k_gxf_fin, dim3(gx_blocks(h.n_pairs, 256, 8192)), dim3(256), 0, st, s, h, f);
     return hipGetLastError();
 }
 
 // One hop (hop >= 1): its grids are sized for the largest frontier / receiver
 // list (the counts are on the device: an empty hop's threads exit at once).
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
-    if (hop == 1 && f.fent)  // the run's eligible senders (the remote ones' fin bits have arrived by now)
-        hipLaunchKernelGGL(k_gxf_compact, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, h, f);
-    hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
+    if (hop == 1 && f.fent && f.fin)  // the shard's eligible senders (the remote ones' fin bits have arrived by now)
+        hipLaunchKernelGGL(k_gxf_compact, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f);
+    hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f, hop);
     static const int gl = [] {  // receivers' lanes: GSX_GXF_G = 1 (k_gxf_pull), 2, 4 (default), 8
         const char* v = getenv("GSX_GXF_G");
         return v ? atoi(v) : 4;
@@ -1660,6 +1708,7 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
     else if (gl == 4 && gb == 2) hipLaunchKernelGGL((k_gxf_pull_g<4, 2>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else if (gl == 4) hipLaunchKernelGGL((k_gxf_pull_g<4, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else if (gl == 2) hipLaunchKernelGGL((k_gxf_pull_g<2, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
+    else if (!f.fin) hipLaunchKernelGGL((k_gxf_pull_g<1, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
     else hipLaunchKernelGGL(k_gxf_pull, dim3(gp), dim3(256), 0, st, s, h, f, hop);
     return hipGetLastError();
 }
