@@ -181,6 +181,10 @@ def prop_engine(n_total, lo, hi, d, seed, device, th, sharded):
                       expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n_total))
     e.set_app_scores(np.zeros(n_pairs))
     e.refresh(T0 + abi.SECOND)
+    # a propagation-only engine: no heartbeat runs on it, so no gossip exchange
+    # reads its message sets' per-node validation times (gsx.h (D)) and the
+    # calls skip building them (the heartbeat / adversarial legs keep it on)
+    e.set_gossipsub_params(gsx_engine_mod.default_gossipsub_params(gossip_exchange=0))
     # throughput runs keep per-pair first-receipt counts, not first-deliverer
     # rows (gsx_prop_set_tracking; credits and duplicates are unchanged)
     e.set_prop_tracking(False)

@@ -296,6 +296,9 @@ hipError_t launch_prop_fold(const PropState& ps, const DevState& s, uint32_t* fi
                             hipStream_t st);
 hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_t st);
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st);
+// The call's arrival hops as the validation-code planes of its message set
+// (VcRef: [plane][node][word], n_planes <= 8; hist rows 1 .. n_rows - 1).
+hipError_t launch_prop_vcodes(const PropState& ps, uint64_t* vc, uint32_t n_planes, hipStream_t st);
 hipError_t launch_prop_dup_rows(const PropState& ps, uint64_t* out, hipStream_t st);
 hipError_t launch_prop_uncache(const PropState& ps, bool mask_cache, hipStream_t st);
 
@@ -352,6 +355,42 @@ struct DevGossipParams {
     int32_t do_px, prune_peers;               // WithPeerExchange, PrunePeers
 };
 
+// When each node's copy of a message set's messages finished validating
+// (score.go:944-974 keeps drec.validated per (observer, message); gsx.h (D)):
+// a code per (node, message) as bit planes [plane][node][word] (plane b holds
+// bit b of the codes of the node's word), codes indexing the set's validation
+// times on the host (the call's copies: code = arrival hop, validated at t0 +
+// hop * (hop_latency + validation_delay); every exchange round that recovered
+// copies of the set appends the code of its `now`).  `vin` bit c: a copy with
+// code c is inside this round's P3 window.
+constexpr uint32_t VC_MAX_PLANES = 16;
+struct VcRef {
+    const uint64_t* vc;   // null: every code 0
+    const uint64_t* vin;  // [codes / 64] (mixed sets; else null)
+    uint64_t plane;       // words per plane (nodes x n_words)
+    uint32_t n_planes, pad;
+};
+// The bits of `bits` (old copies in word idx = node * n_words + w) whose code is inside.
+__device__ __forceinline__ uint64_t vc_inside(const VcRef& V, size_t idx, uint64_t bits) {
+    if (!bits) return 0;
+    uint64_t pl[VC_MAX_PLANES];
+#pragma unroll
+    for (uint32_t b = 0; b < VC_MAX_PLANES; ++b) pl[b] = b < V.n_planes ? V.vc[b * V.plane + idx] : 0ull;
+    uint64_t in = 0;
+    for (uint64_t m = bits; m; m &= m - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(m);
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < VC_MAX_PLANES; ++b) c |= (uint32_t)((pl[b] >> i) & 1) << b;
+        if ((V.vin[c >> 6] >> (c & 63)) & 1) in |= 1ull << i;
+    }
+    return in;
+}
+// old_in: 0 no old copy of the set is inside the window, 1 every one, 2 by code (V)
+__device__ __forceinline__ uint64_t old_inside(uint32_t old_in, const VcRef& V, size_t idx, uint64_t bits) {
+    return old_in == 1 ? bits : old_in == 2 ? vc_inside(V, idx, bits) : 0ull;
+}
+
 // One advertised batch of the gossip exchange (heartbeat step (D)): the
 // batch's cache rows, and its message set's seen rows (exchange start),
 // receipts of this exchange, validation outcomes and serial (promise handles
@@ -371,8 +410,10 @@ struct GxBatch {
     uint32_t nxt;         // the next advertised batch of the same set, cache order (GX_END: none)
     uint32_t dense;       // a first-hand batch (most rows hold uncommon messages): k_gx_rhm sets its bit unread
     const uint64_t* src;  // [n_msgs] the set's origins (node << 32 | index, ascending): the forwarding's back counts
-    uint32_t old_in;      // a copy of the set's messages validated before this round is inside the P3 window
+    uint32_t old_in;      // a copy of the set's messages validated before this round is inside the P3 window (old_inside)
     uint32_t grp;         // the set's group: up to 64 sets of one topic (the forwarding's hop-1 back counts)
+    VcRef vc;             // the set's validation codes (old_in 2)
+    uint32_t vin_off;     // (range shards, old_in 2) word offset of the inside rows in a gxs_rows entry: 1 + fw + woff
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
@@ -467,6 +508,8 @@ struct HbState {
     uint32_t* gxs_hidx;
     const uint64_t* gxs_rows;
     uint32_t gxs_fw;
+    uint32_t gxs_vin;   // entries carry, after the rows, the sender's inside rows of the mixed sets (old_in 2):
+                        // the bits of its row whose copy at the sender is inside the P3 window (hop-1 back-sends)
     // the IWANT first receipts per (topic, pair) of this round (the forwarding's
     // hop-1 back-sends, GxFwd); null when nothing is forwarded
     uint32_t* gxb_st0;     // [pair] stamp: the pair's counts were written this round
@@ -568,6 +611,9 @@ struct GxSetMerge {
     uint64_t* dig;             // [node] summary digest of the recovered rows
     uint32_t* cnt;             // [node] their message count
     uint32_t n_words, n_msgs;
+    uint64_t* vc;              // the set's code planes: the recovered copies take `code` (null: none)
+    uint64_t plane;
+    uint32_t n_planes, code;
 };
 hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // The forwarding of the recovered messages (gsx.h (D): a delivered message is
@@ -586,7 +632,8 @@ struct GxFwdSet {
     uint32_t n_words, n_msgs, topic, slot, serial;
     uint32_t woff;        // word offset of the set's rows in a cross-shard frontier entry (range shards)
     uint8_t* got;         // set to 1 when a node delivers a message of the set (its recovered batch is Put)
-    uint32_t old_in;      // a copy of a message the receiver had before the round is inside the P3 window
+    uint32_t old_in;      // a copy of a message the receiver had before the round is inside the P3 window (old_inside)
+    VcRef vc;             // the set's validation codes (old_in 2)
 };
 struct GxFwd {
     const GxFwdSet* sets;

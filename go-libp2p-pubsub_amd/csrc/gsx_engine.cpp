@@ -138,7 +138,18 @@ struct gsx_engine {
         uint32_t* d_val = nullptr;  // [message] GSX_VALIDATION_*
         uint64_t* d_acc = nullptr;  // [word] accepted messages
         uint64_t* d_src = nullptr;  // [message] origin node << 32 | index, ascending (the forwarding's origin test)
-        int64_t t0 = 0;             // now_ns of the call that made the set (the validation time of old copies)
+        int64_t t0 = 0;             // now_ns of the call that made the set
+        // per-node validation times of the copies (gsx::VcRef): code planes
+        // [vc_p][node][word] (null: every code 0) and the time of each code
+        uint64_t* d_vc = nullptr;
+        size_t vc_words = 0;
+        uint32_t vc_p = 0;
+        std::vector<int64_t> vtime;
+        // the arrival hops were kept (codes 0 .. n_hop - 1 = hops); a set cached
+        // with the gossip exchange off keeps none: its copies' hop times may
+        // only be read as one (gx_vcodes refuses a round whose window splits them)
+        bool hops_kept = true;
+        uint32_t n_hop = 1;
         uint64_t* d_dg = nullptr;   // [W * 64] id digests + [W] word digests (k_mc_summary)
         uint8_t* d_full = nullptr;  // [node]: every message seen (the exchange skips the set there)
         uint8_t* d_small = nullptr;  // the pooled block d_val / d_acc / d_dg live in
@@ -209,6 +220,8 @@ struct gsx_engine {
     void* h_gxstage = nullptr;        // pinned staging of the exchange's batch list (hb_end)
     size_t h_gxstage_bytes = 0;
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
+    uint64_t* d_gx_vin = nullptr;  // the round's inside-code bits of the mixed sets (GxRound::vin_host)
+    size_t gx_vin_cap = 0;
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
     size_t gx_common_cap = 0;         // (sets)
     // the forwarding of recovered messages (gsx.h (D); GxFwd), allocated with its first use
@@ -255,6 +268,12 @@ struct gsx_engine {
         std::vector<uint64_t*> xs;
         std::vector<std::pair<uint64_t*, size_t>> scratch;  // frontier rows, released after the round's sync
         uint32_t n_gx = 0, fw = 0;
+        // per set: its old copies inside the P3 window (0 none, 1 all, 2 by
+        // code: vc), the code this round's recovered copies take; the mixed
+        // sets' inside-code bits (d_gx_vin)
+        std::vector<uint32_t> old_in, vc_code;
+        std::vector<gsx::VcRef> vc;
+        std::vector<uint64_t> vin_host;
         std::vector<GxfRun> runs;
         gsx::GxFwd f{};
         uint32_t hops = 0;
@@ -272,6 +291,10 @@ struct gsx_engine {
     // propagation buffers (grown on demand) and the current / last call's shape
     struct {
         uint64_t *seen = nullptr, *hist = nullptr, *origin = nullptr, *from = nullptr, *sel = nullptr, *occ = nullptr;
+        // the other frontier-history buffer: a gossipsub call's message set
+        // builds its validation codes from its rows on vc_stream while the next
+        // call writes these (allocated on the first such build)
+        uint64_t *hist_alt = nullptr, *occ_alt = nullptr;
         uint32_t* corr = nullptr;
         uint8_t* fwd = nullptr;
         uint32_t* pin = nullptr;
@@ -370,6 +393,13 @@ struct gsx_engine {
     std::vector<uint32_t> rev_host;
     bool sharded() const { return n_ranks > 1 || node_lo != 0 || n_total != n_nodes; }
     hipStream_t own_stream = nullptr;
+    // code-plane builds (k_prop_vcodes) beside the engine stream: vc_go marks
+    // the engine-stream point a build starts after, vc_done[b] the last build
+    // that read history buffer b (0: prop.hist as allocated, 1: hist_alt)
+    hipStream_t vc_stream = nullptr;
+    hipEvent_t vc_go = nullptr, vc_done[2] = {nullptr, nullptr};
+    bool vc_busy[2] = {false, false};
+    int hist_idx = 0, vc_last = -1;
 
     // events
     std::vector<gsx_event> pending;
@@ -640,9 +670,75 @@ void set_sources(std::vector<uint64_t>& out, const gsx_msg* msgs, size_t m) {
     std::sort(out.begin(), out.end());
 }
 
+template <class T>
+int dalloc(gsx_engine* e, T** p, size_t n);
+uint32_t bit_width32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
+// The engine stream waits for every queued code-plane build (before anything
+// reads, copies, regrows or pools a set's planes).
+int vc_fence(gsx_engine* e) {
+    if (e->vc_last < 0) return GSX_OK;
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->vc_done[e->vc_last], 0));
+    e->vc_last = -1;
+    return GSX_OK;
+}
+// A set's code planes grown to p planes (the new ones zero: code bits above
+// the old width are 0); p <= VC_MAX_PLANES.
+int vc_grow(gsx_engine* e, gsx_engine::MsgSet* st, uint32_t p) {
+    if (p <= st->vc_p) return GSX_OK;
+    if (st->d_vc)
+        if (int rc = vc_fence(e)) return rc;
+    if (p > gsx::VC_MAX_PLANES) return fail(e, GSX_ERANGE, "a message set's validation codes past 2^16 (recovered in 65k rounds)");
+    const size_t plane = (size_t)st->n_words * e->n_nodes;
+    const size_t words = std::max<size_t>(plane * p, 1);
+    uint64_t* vc = seen_acquire(e, words);
+    if (!vc) return fail(e, GSX_ENOMEM, "message set validation codes");
+    if (st->d_vc && plane)
+        HIPCHK(e, hipMemcpyAsync(vc, st->d_vc, 8 * plane * st->vc_p, hipMemcpyDeviceToDevice, e->stream));
+    if (plane) HIPCHK(e, hipMemsetAsync(vc + plane * st->vc_p, 0, 8 * plane * (p - st->vc_p), e->stream));
+    seen_release(e, st->d_vc, st->vc_words);
+    st->d_vc = vc;
+    st->vc_words = words;
+    st->vc_p = p;
+    return GSX_OK;
+}
+
+// A propagation call's arrival hops into its message set's code planes, on
+// vc_stream after the engine stream's work so far; the next call writes the
+// other history buffer (it waits for the build that read it two calls back).
+int vc_build(gsx_engine* e, const gsx::PropState& ps, gsx_engine::MsgSet* set) {
+    auto& P = e->prop;
+    if (!e->vc_stream) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->vc_stream, hipStreamNonBlocking));
+        HIPCHK(e, hipEventCreateWithFlags(&e->vc_go, hipEventDisableTiming));
+        for (auto& ev : e->vc_done) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    if (!P.hist_alt) {
+        const size_t N = e->n_nodes;
+        if (int rc = dalloc(e, &P.hist_alt, (size_t)P.rows_cap * P.words_cap * N)) return rc;
+        if (int rc = dalloc(e, &P.occ_alt, (size_t)P.rows_cap * ((N + 63) / 64))) return rc;
+    }
+    HIPCHK(e, hipEventRecord(e->vc_go, e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->vc_stream, e->vc_go, 0));
+    HIPCHK(e, gsx::launch_prop_vcodes(ps, set->d_vc, set->vc_p, e->vc_stream));
+    const int b = e->hist_idx;
+    HIPCHK(e, hipEventRecord(e->vc_done[b], e->vc_stream));
+    e->vc_busy[b] = true;
+    e->vc_last = b;
+    std::swap(P.hist, P.hist_alt);
+    std::swap(P.occ, P.occ_alt);
+    e->hist_idx ^= 1;
+    if (e->vc_busy[e->hist_idx]) {  // the buffer the next call writes: its build first
+        HIPCHK(e, hipStreamWaitEvent(e->stream, e->vc_done[e->hist_idx], 0));
+        e->vc_busy[e->hist_idx] = false;
+    }
+    return GSX_OK;
+}
+
 void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
     if (!st || --st->refs > 0) return;
+    if (st->d_vc) (void)vc_fence(e);  // (a build may still write the planes going back to the pool)
     seen_release(e, st->d_all, st->all_words);
+    seen_release(e, st->d_vc, st->vc_words);
     small_release(e, st->d_small, st->small_bytes);
     small_release(e, st->d_full, st->full_bytes);
     delete st;
@@ -682,6 +778,10 @@ void gx_abort(gsx_engine* e) {
 }
 
 void free_state(gsx_engine* e) {
+    if (e->vc_stream) (void)hipStreamSynchronize(e->vc_stream);  // (code-plane builds in flight)
+    e->vc_busy[0] = e->vc_busy[1] = false;
+    e->hist_idx = 0;
+    e->vc_last = -1;
     gx_abort(e);
     void* ptrs[] = {e->d_rec,    e->d_rflags, e->d_tmp, e->d_nbad,    e->d_pflags, e->d_eflags,
                     e->d_expire, e->d_bp,     e->d_app, e->d_score,   e->d_ipg,    e->d_ipcount,
@@ -723,7 +823,7 @@ void free_state(gsx_engine* e) {
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
                   e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
                   e->d_halo_pair, e->d_send_slot,
-                  e->prop.d_dig, e->prop.rcand, e->prop.tterm, e->prop.tgen};
+                  e->prop.d_dig, e->prop.rcand, e->prop.tterm, e->prop.tgen, e->prop.hist_alt, e->prop.occ_alt};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     std::vector<hipEvent_t> evs = std::move(e->prop.ev);
@@ -806,6 +906,9 @@ void free_state(gsx_engine* e) {
         e->d_gx_got = nullptr;
         e->gx_cap = 0;
         e->d_gx_rhm = e->d_gx_common = nullptr;
+        if (e->d_gx_vin) (void)hipFree(e->d_gx_vin);
+        e->d_gx_vin = nullptr;
+        e->gx_vin_cap = 0;
         e->d_gx_heads = nullptr;
         e->d_gx_sp = nullptr;
         e->d_gx_mg = nullptr;
@@ -1268,6 +1371,11 @@ int gsx_destroy(gsx_engine* e) {
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
+    if (e->vc_stream) (void)hipStreamSynchronize(e->vc_stream);
+    if (e->vc_go) (void)hipEventDestroy(e->vc_go);
+    for (hipEvent_t ev : e->vc_done)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->vc_stream) (void)hipStreamDestroy(e->vc_stream);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->prop.ev) (void)hipEventDestroy(ev);
     if (e->prop.hop_flag) (void)hipHostFree(e->prop.hop_flag);
@@ -2292,10 +2400,15 @@ uint32_t prop_words(size_t m) {
 int prop_free_buffers(gsx_engine* e) {
     auto& P = e->prop;
     seen_release(e, P.seen, P.seen_words);
-    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats, P.touch, P.vcnt, P.vmask};
+    if (e->vc_stream) (void)hipStreamSynchronize(e->vc_stream);  // (builds reading the history rows)
+    e->vc_busy[0] = e->vc_busy[1] = false;
+    e->hist_idx = 0;
+    e->vc_last = -1;
+    void* pp[] = {P.hist, P.origin, P.from, P.sel, P.occ, P.msgs, P.stats, P.touch, P.vcnt, P.vmask, P.hist_alt, P.occ_alt};
     for (void* p : pp)
         if (p) (void)hipFree(p);
     P.seen = P.hist = P.origin = P.from = P.sel = P.occ = P.touch = P.vcnt = P.vmask = nullptr;
+    P.hist_alt = P.occ_alt = nullptr;
     P.from_words = 0;
     P.msgs = nullptr;
     P.stats = nullptr;
@@ -2981,6 +3094,22 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
             P.rows_valid = h + 1;
             break;
         }
+    if (set) {  // the copies' validation times: code = arrival hop (gsx.h (D), VcRef)
+        const int64_t step = P.cfg.hop_latency_ns + P.cfg.validation_delay_ns;
+        const uint32_t H = P.h;  // hops run (every rank of a range shard runs the same)
+        set->vtime.resize(step > 0 ? H + 1 : 1);
+        for (uint32_t h = 0; h < set->vtime.size(); ++h) set->vtime[h] = P.cfg.now_ns + (int64_t)h * step;
+        set->n_hop = (uint32_t)set->vtime.size();
+        // only the gossip exchange reads them (a propagation-only engine skips the build)
+        if (step > 0 && H >= 1 && P.rows_valid > 1 && !e->gp.gossip_exchange) set->hops_kept = false;
+        else if (step > 0 && H >= 1 && P.rows_valid > 1) {
+            // (room for the next code: a recovery round's, without regrowing the planes)
+            if (int rc = vc_grow(e, set, bit_width32(H + 1))) return rc;
+            gsx::PropState pv = ps;
+            pv.n_rows = P.rows_valid;
+            if (int rc = vc_build(e, pv, set)) return rc;
+        }
+    }
     out->edge_sends = st[gsx::STAT_EDGE_SENDS];
     out->new_words = st[gsx::STAT_NEW_WORDS];
     double ms = 0;
@@ -3945,8 +4074,9 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
             S.woff = rw;
             S.got = e->d_gx_got + i;
             rw += ms->n_words;
-            // an old copy counts as validated when its set's call ran (gsx.h)
-            S.old_in = R.h.now - ms->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
+            // an old copy: inside the window by its code's validation time (gsx.h (D))
+            S.old_in = R.old_in[i];
+            S.vc = R.vc[i];
             f.slot_sets[ts] |= 1ull << f.n_sets;
             stage[f.n_sets] = S;
             ++f.n_sets;
@@ -4035,6 +4165,68 @@ int gx_forward(gsx_engine* e, gsx_engine::GxRound& R) {
     return GSX_OK;
 }
 
+// The sets' validation codes this round (gsx.h (D), VcRef): whether each
+// set's old copies are all / none / by code inside its topic's P3 window
+// (the mixed sets' inside-code bits staged for d_gx_vin), and the code this
+// round's recovered copies take (hb_finish drops it again from a set that
+// recovered nothing; every rank of a range shard decides alike: got_all).
+int gx_vcodes(gsx_engine* e, gsx_engine::GxRound& R) {
+    if (int rc = vc_fence(e)) return rc;
+    const size_t ns = R.sets.size();
+    R.old_in.assign(ns, 0);
+    R.vc_code.assign(ns, 0);
+    R.vc.assign(ns, gsx::VcRef{});
+    R.vin_host.clear();
+    std::vector<size_t> vin_off(ns, 0);
+    for (size_t i = 0; i < ns; ++i) {
+        gsx_engine::MsgSet* ms = R.sets[i];
+        if (ms->vtime.empty()) ms->vtime.push_back(ms->t0);
+        const int64_t win = e->tp[ms->topic < GSX_MAX_TOPICS ? ms->topic : 0].mesh_message_deliveries_window_ns;
+        if (!ms->hops_kept) {  // the hop codes stand as one (code 0): they must all fall on one side
+            const size_t nh = std::min<size_t>(ms->n_hop, ms->vtime.size());
+            bool hin = false, hout = false;
+            for (size_t c = 0; c < nh; ++c) (R.h.now - ms->vtime[c] <= win ? hin : hout) = true;
+            if (hin && hout)
+                return fail(e, GSX_ESTATE, "a message set cached while the gossip exchange was off keeps no arrival "
+                                           "hops, and this round's P3 window splits its copies (gsx.h (D))");
+        }
+        // the codes in use: code 0 alone without planes, else those the planes can hold
+        const size_t nc = ms->d_vc ? std::min<size_t>(ms->vtime.size(), (size_t)1 << ms->vc_p) : 1;
+        bool any_in = false, any_out = false;
+        for (size_t c = 0; c < nc; ++c) (R.h.now - ms->vtime[c] <= win ? any_in : any_out) = true;
+        R.old_in[i] = any_in && any_out ? 2u : any_in ? 1u : 0u;
+        if (R.old_in[i] == 2) {
+            vin_off[i] = R.vin_host.size();
+            R.vin_host.resize(R.vin_host.size() + (nc + 63) / 64, 0);
+            for (size_t c = 0; c < nc; ++c)
+                if (R.h.now - ms->vtime[c] <= win) R.vin_host[vin_off[i] + c / 64] |= 1ull << (c % 64);
+        }
+        const uint32_t code = (uint32_t)ms->vtime.size();  // provisional: this round's recoveries
+        if (int rc = vc_grow(e, ms, bit_width32(code))) return rc;
+        ms->vtime.push_back(R.h.now);
+        R.vc_code[i] = code;
+    }
+    if (R.vin_host.size() > e->gx_vin_cap) {
+        if (e->d_gx_vin) (void)hipFree(e->d_gx_vin);
+        e->d_gx_vin = nullptr;
+        e->gx_vin_cap = 0;
+        const size_t cap = std::max<size_t>(R.vin_host.size(), 64);
+        if (int rc = dalloc(e, &e->d_gx_vin, cap)) return rc;
+        e->gx_vin_cap = cap;
+    }
+    if (!R.vin_host.empty())
+        HIPCHK(e, hipMemcpyAsync(e->d_gx_vin, R.vin_host.data(), 8 * R.vin_host.size(), hipMemcpyHostToDevice,
+                                 e->stream));
+    // range shards: the rows entries carry the senders' inside rows when some set is mixed
+    R.h.gxs_vin = R.vin_host.empty() ? 0u : 1u;
+    for (size_t i = 0; i < ns; ++i) {
+        const gsx_engine::MsgSet* ms = R.sets[i];
+        R.vc[i] = gsx::VcRef{ms->d_vc, R.old_in[i] == 2 ? e->d_gx_vin + vin_off[i] : nullptr,
+                             (uint64_t)ms->n_words * e->n_nodes, ms->vc_p, 0u};
+    }
+    return GSX_OK;
+}
+
 // (D), first part: the advertised batches of hb_begin's windows (per topic,
 // cache order), their message sets and receipt rows, the set heads and the
 // flat word list; receipt rows zeroed, full bytes and common words (k_gx_setprep).
@@ -4082,10 +4274,10 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
                 gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
                 gx.back().dense = b.recovered ? 0u : 1u;
                 gx.back().src = b.set->d_src;
-                gx.back().old_in = R.h.now - b.set->t0 <= e->tp[t].mesh_message_deliveries_window_ns ? 1u : 0u;
             }
     }
     off[e->T] = (uint32_t)gx.size();
+    if (int rc = gx_vcodes(e, R)) return rc;
     // the set groups: consecutive sets of one topic, up to 64 sets and 65,535
     // messages each (the u16 back counts of the forwarding)
     R.set_grp.assign(R.sets.size(), 0);
@@ -4113,9 +4305,13 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         for (size_t i = 0; i < gx.size(); ++i) {
             gx[i].woff = fw;
             fw += gx[i].n_words;
-            gx[i].n_msgs = R.sets[reinterpret_cast<size_t>(gx[i].got)]->n_msgs;  // (got: the set's index yet)
-            gx[i].grp = R.set_grp[reinterpret_cast<size_t>(gx[i].got)];
+            const size_t si = reinterpret_cast<size_t>(gx[i].got);  // (got: the set's index yet)
+            gx[i].n_msgs = R.sets[si]->n_msgs;
+            gx[i].grp = R.set_grp[si];
+            gx[i].old_in = R.old_in[si];
+            gx[i].vc = R.vc[si];
         }
+        for (auto& g : gx) g.vin_off = 1 + fw + g.woff;  // (range shards: after the entry's rows)
     }
     // per topic, the sets of its batches: each set's first batch in cache
     // order and its words' offset (k_gx_node's receipts: a lane per set word
@@ -4200,7 +4396,8 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         const gsx_engine::MsgSet* ms = R.sets[i];
         const size_t W = ms->n_words;
         smerge[i] = gsx::GxSetMerge{ms->d_all, R.xs[i], ms->d_acc, ms->d_dg, R.xs[i] + W * N,
-                                    reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs};
+                                    reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs,
+                                    ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i]};
     }
     HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
     for (auto& g : gx) {
@@ -4337,6 +4534,8 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
         gsx_engine::MsgSet* ms = gx_sets[i];
         if (!got[i]) {
             seen_release(e, gx_x[i], (size_t)ms->n_words * N + 2 * N);
+            // nothing recovered: no copy took this round's code (k_gx_merge_sets writes accepted receipts only)
+            if (i < R.vc_code.size() && ms->vtime.size() == (size_t)R.vc_code[i] + 1) ms->vtime.pop_back();
             continue;
         }
         gsx_engine::McBatch b;
@@ -4774,7 +4973,7 @@ int gsx_gx_recv_ihave(gsx_engine* e, const uint64_t* recv) {
 int gsx_gx_rows_words(gsx_engine* e, uint32_t* words) {
     if (!e || !words) return GSX_EINVAL;
     if (int rc = gxs_step(e, -1)) return rc;
-    *words = e->gxr.fw + 1;
+    *words = 1 + e->gxr.fw * (e->gxr.h.gxs_vin ? 2u : 1u);  // (gxs_ew)
     return GSX_OK;
 }
 
@@ -5145,14 +5344,22 @@ int gsx_mcache_last(gsx_engine* e, uint32_t* n_words, uint32_t* n_msgs) {
     return GSX_OK;
 }
 
-int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows) {
-    if (!e || !cache_rows || !set_rows) return GSX_EINVAL;
+int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows, uint64_t* code_rows,
+                         uint32_t n_planes) {
+    if (!e || !cache_rows || !set_rows || (n_planes && !code_rows)) return GSX_EINVAL;
     if (int rc = mcache_ready(e)) return rc;
     const auto* b = mcache_newest(e);
     if (!b || !b->set) return fail(e, GSX_ESTATE, "no cached gossipsub batch with a message set");
+    if (b->set->vc_p > n_planes) return fail(e, GSX_ERANGE, "the set's validation codes need more planes");
+    if (int rc = vc_fence(e)) return rc;
     const size_t words = (size_t)b->n_words * e->n_nodes;
     HIPCHK(e, hipMemcpyAsync(cache_rows, b->d_seen, 8 * words, hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set_rows, b->set->d_all, 8 * words, hipMemcpyDeviceToDevice, e->stream));
+    if (n_planes) {
+        const uint32_t p = b->set->d_vc ? b->set->vc_p : 0u;
+        if (p) HIPCHK(e, hipMemcpyAsync(code_rows, b->set->d_vc, 8 * words * p, hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(e, hipMemsetAsync(code_rows + words * p, 0, 8 * words * (n_planes - p), e->stream));
+    }
     return GSX_OK;
 }
 
@@ -5168,8 +5375,11 @@ int gsx_mcache_pop(gsx_engine* e) {
 }
 
 int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
-                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts) {
-    if (!e || !cfg || !msgs || !m || !n_parts || !part_msgs || !cache_parts || !set_parts) return GSX_EINVAL;
+                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts,
+                   const uint64_t* const* code_parts, uint32_t n_planes) {
+    if (!e || !cfg || !msgs || !m || !n_parts || !part_msgs || !cache_parts || !set_parts || (n_planes && !code_parts))
+        return GSX_EINVAL;
+    if (n_planes > 8) return fail(e, GSX_EINVAL, "a propagated set's codes (arrival hops) take at most 8 planes");
     if (int rc = mcache_ready(e)) return rc;
     if (cfg->router != GSX_ROUTER_GOSSIPSUB) return fail(e, GSX_EINVAL, "only gossipsub batches are cached");
     if (m > 0xFFFFFFFFull) return fail(e, GSX_ERANGE, "batch too large");
@@ -5191,8 +5401,15 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
     if (int rc = fanout_publish(e, msgs, m, cfg)) return rc;
     const uint32_t W = prop_words(m);
     const size_t N = e->n_nodes;
-    // the blocks' descriptors (cache, then set) on the device
-    const size_t need = 2 * (size_t)n_parts * sizeof(gsx::McPart);
+    // the blocks' descriptors (cache, set, then each code plane) on the device
+    for (uint32_t b = 0; b < n_planes; ++b)
+        for (uint32_t k = 0; k < n_parts; ++k) {
+            if (part_msgs[k] && !code_parts[k]) return fail(e, GSX_EINVAL, "missing block codes");
+            const size_t pw = (size_t)prop_words(part_msgs[k]) * e->n_nodes;
+            cp.push_back(gsx::McPart{part_msgs[k] ? code_parts[k] + b * pw : nullptr, cp[k].off, part_msgs[k],
+                                     prop_words(part_msgs[k])});
+        }
+    const size_t need = (2 + (size_t)n_planes) * (size_t)n_parts * sizeof(gsx::McPart);
     if (need > e->mparts_cap) {
         if (e->d_mparts) (void)hipFree(e->d_mparts);
         e->d_mparts = nullptr;
@@ -5200,7 +5417,7 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
         if (int rc = dalloc(e, &e->d_mparts, need)) return rc;
         e->mparts_cap = need;
     }
-    cp.insert(cp.end(), sp.begin(), sp.end());
+    cp.insert(cp.begin() + n_parts, sp.begin(), sp.end());
     auto* dparts = reinterpret_cast<gsx::McPart*>(e->d_mparts);
     HIPCHK(e, hipMemcpyAsync(dparts, cp.data(), need, hipMemcpyHostToDevice, e->stream));
     gsx_engine::MsgSet* set = new gsx_engine::MsgSet;
@@ -5242,6 +5459,22 @@ int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_
     std::vector<uint64_t> srcs;
     set_sources(srcs, msgs, m);
     set->t0 = cfg->now_ns;
+    {  // the blocks' validation codes: their arrival hops (as gsx_propagate leaves them)
+        const int64_t step = cfg->hop_latency_ns + cfg->validation_delay_ns;
+        set->vtime.resize(step > 0 ? (size_t)cfg->max_hops + 1 : 1);
+        for (size_t h = 0; h < set->vtime.size(); ++h) set->vtime[h] = cfg->now_ns + (int64_t)h * step;
+        set->n_hop = (uint32_t)set->vtime.size();
+        set->hops_kept = n_planes > 0 || step <= 0;
+        if (n_planes && step > 0) {
+            if (int rc = vc_grow(e, set, n_planes)) {
+                batch_release(e, b);
+                return rc;
+            }
+            for (uint32_t p = 0; p < n_planes; ++p)
+                HIPCHK(e, gsx::launch_mc_merge(dparts + (2 + p) * (size_t)n_parts, n_parts,
+                                               set->d_vc + (size_t)p * W * N, (uint32_t)N, W, e->stream));
+        }
+    }
     HIPCHK(e, hipMemcpyAsync(set->d_val, vals.data(), 4 * m, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set->d_acc, acc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(set->d_dg, dg.data(), 8 * dg.size(), hipMemcpyHostToDevice, e->stream));

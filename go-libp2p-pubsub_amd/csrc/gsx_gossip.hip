@@ -32,6 +32,8 @@ __device__ __forceinline__ void gx_flush(unsigned long long* stats, int k, uint6
     if ((threadIdx.x % 64) == 0 && c) atomicAdd(&stats[k], (unsigned long long)c);
 }
 
+// Words per gxs_rows entry: the receive slot, the rows, the inside rows (gxs_vin).
+__device__ __forceinline__ size_t gxs_ew(const HbState& h) { return 1 + (size_t)h.gxs_fw * (h.gxs_vin ? 2 : 1); }
 // Word w of the sender's cache row of batch b, the sender being v, the peer
 // of the receiver's pair q: a local sender's row; on a range shard a remote
 // one's from the rows its rank sent (gxs_rows), none when it sent none (every
@@ -39,9 +41,21 @@ __device__ __forceinline__ void gx_flush(unsigned long long* stats, int k, uint6
 __device__ __forceinline__ uint64_t gx_mem(const HbState& h, const GxBatch& b, uint64_t q, uint32_t v, uint32_t w) {
     if (h.gxs_hidx && (h.rev[q] & HALO)) {
         const uint32_t k = h.gxs_hidx[q];
-        return k == NO_PAIR ? 0ull : h.gxs_rows[(size_t)k * (h.gxs_fw + 1) + 1 + b.woff + w];
+        return k == NO_PAIR ? 0ull : h.gxs_rows[(size_t)k * gxs_ew(h) + 1 + b.woff + w];
     }
     return b.mem[(size_t)(v - h.node_lo) * b.n_words + w];
+}
+// The bits of `bits` (messages v served u from its cache, word w of batch b)
+// whose copy at v is inside the P3 window: v's copies are old (validated
+// before the round: gsx.h (D)); a remote v's from the inside rows its rank sent.
+__device__ __forceinline__ uint64_t gx_in_at_sender(const HbState& h, const GxBatch& b, uint64_t q, uint32_t v,
+                                                    uint32_t w, uint64_t bits) {
+    if (b.old_in != 2 || !bits) return b.old_in ? bits : 0ull;
+    if (h.gxs_hidx && (h.rev[q] & HALO)) {
+        const uint32_t k = h.gxs_hidx[q];
+        return k == NO_PAIR ? 0ull : bits & h.gxs_rows[(size_t)k * gxs_ew(h) + b.vin_off + w];
+    }
+    return vc_inside(b.vc, (size_t)(v - h.node_lo) * b.n_words + w, bits);
 }
 // The advertised batches whose row at the sender holds an uncommon message (gx_rhm).
 __device__ __forceinline__ uint64_t gx_rhm_of(const HbState& h, uint64_t q, uint32_t v) {
@@ -323,8 +337,10 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
             if (val == VAL_ACCEPT) {
                 ++delivered;
                 ev_first(s, q, t);
-                if (h.gxb_st0 && !((origin_word(b.src, b.n_msgs, v, k / 64) >> (k % 64)) & 1))
-                    gx_back0(h, q, b.grp, b.old_in, !b.old_in);
+                if (h.gxb_st0 && !((origin_word(b.src, b.n_msgs, v, k / 64) >> (k % 64)) & 1)) {
+                    const uint32_t in = gx_in_at_sender(h, b, q, v, k / 64, bit) ? 1u : 0u;
+                    gx_back0(h, q, b.grp, in, 1u - in);
+                }
                 *b.got = 1;
             } else {
                 ++rejected;
@@ -772,10 +788,12 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                     else if (val == VAL_REJECT) ++k4;
                                 }
                                 if (acc1 && h.gxb_st0) {  // the back-sends of these first receipts (GxFwd)
-                                    const uint32_t nb = (uint32_t)__popcll(acc1 & ~origin_word(b.src, b.n_msgs, v, w));
-                                    if (nb)
+                                    const uint64_t bk = acc1 & ~origin_word(b.src, b.n_msgs, v, w);
+                                    if (bk) {
+                                        const uint64_t bin = gx_in_at_sender(h, b, (uint64_t)q, v, w, bk);
                                         atomicAdd(&h.gxb_cnt0[(size_t)b.grp * h.n_pairs + q],
-                                                  b.old_in ? nb : nb << 16);  // (cleared before the walk)
+                                                  (uint32_t)__popcll(bin) | (uint32_t)__popcll(bk & ~bin) << 16);
+                                    }  // (cleared before the walk)
                                 }
                             }
                             if (got) *b.got = 1;
@@ -901,6 +919,11 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
             S.all[i] |= word;
             word &= S.acc[w];
             S.x[i] = word;
+            if (S.vc && word)  // the recovered copies were validated now: this round's code
+                for (uint32_t b = 0; b < S.n_planes; ++b) {
+                    uint64_t* pw = S.vc + b * S.plane + i;
+                    *pw = (*pw & ~word) | (((S.code >> b) & 1) ? word : 0ull);
+                }
             L += (uint32_t)__popcll(word);
             const uint32_t left = S.n_msgs > w * 64 ? S.n_msgs - w * 64 : 0;
             const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
@@ -1189,7 +1212,8 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
                         const uint64_t nw = snd & ~(A[w] | xw);
                         const uint64_t dup = snd & ~nw;
                         dt += (uint32_t)__popcll(dup);
-                        dw += (uint32_t)__popcll(S.old_in ? dup : (dup & xw));
+                        // in-window duplicates: those x got this round; an old copy by its validation time
+                        dw += (uint32_t)__popcll((dup & xw) | old_inside(S.old_in, S.vc, (size_t)x * W + w, dup & ~xw));
                         if (nw) {
                             n1 += (uint32_t)__popcll(nw);
                             X[w] = xw | nw;
@@ -1399,9 +1423,10 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                         const uint64_t nw = snd & ~(have | excl);  // not seen, not from a lower sender
                         const uint64_t dup = snd & ~nw;
                         dt += (uint32_t)__popcll(dup);
-                        // in-window duplicates: an old copy by the set's old_in; else those x got this
-                        // round (before this hop, or first from a lower sender of this one)
-                        dw += (uint32_t)__popcll(S.old_in ? dup : (dup & (xw | (excl & ~have))));
+                        // in-window duplicates: those x got this round (before this hop, or first
+                        // from a lower sender of this one); an old copy by its validation time
+                        const uint64_t cur = dup & (xw | (excl & ~have));
+                        dw += (uint32_t)__popcll(cur | old_inside(S.old_in, S.vc, (size_t)x * W + w, dup & ~cur));
                         n1 += (uint32_t)__popcll(nw);
                         const uint64_t gn = all_g & ~have;  // the group's first receipts of the word
                         if (gn) {
@@ -1528,7 +1553,7 @@ __global__ __launch_bounds__(256) void k_gxs_rows(HbState h, GxsPlan P, const Gx
         const uint32_t d = P.send_dest[j];
         const unsigned long long k = atomicAdd(&cnt[d], 1ull);
         if (!out) continue;
-        uint64_t* e = out + (size_t)(off[d] + k) * (h.gxs_fw + 1);
+        uint64_t* e = out + (size_t)(off[d] + k) * gxs_ew(h);
         e[0] = P.dest_halo_base[d] + (j - P.send_base[d]);  // the receive slot at the destination
         // a truncated list reaches the receiver as its subset: the rows of that
         // topic's batches go masked with the subset row v kept for this pair, so
@@ -1542,8 +1567,11 @@ __global__ __launch_bounds__(256) void k_gxs_rows(HbState h, GxsPlan P, const Gx
                 sub = G.pool + (size_t)G.idx[r] * G.tw + b.row_off;
             }
             for (uint32_t w = 0; w < b.n_words; ++w) {
-                const uint64_t m = b.mem[(size_t)v * b.n_words + w];
-                e[1 + b.woff + w] = sub ? m & sub[w] : m;
+                uint64_t m = b.mem[(size_t)v * b.n_words + w];
+                if (sub) m &= sub[w];
+                e[1 + b.woff + w] = m;
+                // the mixed sets: which of v's copies are inside the window at v (hop-1 back-sends)
+                if (h.gxs_vin) e[b.vin_off + w] = b.old_in == 2 ? vc_inside(b.vc, (size_t)v * b.n_words + w, m) : 0ull;
             }
         }
     }
@@ -1552,7 +1580,7 @@ __global__ __launch_bounds__(256) void k_gxs_rows(HbState h, GxsPlan P, const Gx
 __global__ __launch_bounds__(256) void k_gxs_rows_recv(HbState h, const uint64_t* in, uint64_t n,
                                                        const uint32_t* halo_pair) {
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256u)
-        h.gxs_hidx[halo_pair[in[k * (h.gxs_fw + 1)]]] = (uint32_t)k;
+        h.gxs_hidx[halo_pair[in[k * gxs_ew(h)]]] = (uint32_t)k;
 }
 
 __global__ __launch_bounds__(256) void k_gxf_pack_fout(GxFwd f, GxsPlan P, uint64_t* out) {

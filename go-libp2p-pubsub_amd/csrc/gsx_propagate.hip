@@ -1657,6 +1657,46 @@ __global__ __launch_bounds__(256) void k_prop_from(PropState ps, int32_t* __rest
 
 // Arrival hops, [message][node] as the ABI lays them out: the hop whose
 // frontier row holds the message's bit (0 at the source), 0xFF never.
+// Thread per (node, word): the hops of its new bits (hist rows where the node
+// is occupied) spread over the code planes; sources and messages the node
+// never got keep code 0 (only old copies of received messages are looked up).
+// The node's occupied rows are found first (one occ word per row, shared by
+// the node's threads), then their words are loaded VB at a time, so a thread
+// waits for one load latency per VB rows instead of two per row.
+__global__ __launch_bounds__(256) void k_prop_vcodes(PropState ps, uint64_t* __restrict__ vc, uint32_t n_planes) {
+    constexpr int VB = 8;
+    const uint32_t W = ps.n_words;
+    const size_t plane = (size_t)ps.n_nodes * W;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint32_t rows = ps.n_rows < 64 ? ps.n_rows : 64;  // (hop 64, GSX_MAX_HOPS, apart below)
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < plane; i += (size_t)gridDim.x * 256u) {
+        const uint32_t u = (uint32_t)(i / W);
+        uint64_t rm = 0;  // bit h: the node is occupied at hop h
+        for (uint32_t h = 1; h < rows; ++h) rm |= (uint64_t)occ_bit(ps.occ + (size_t)h * occ_row, u) << h;
+        uint64_t pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ps.n_rows > 64 && occ_bit(ps.occ + (size_t)64 * occ_row, u)) pl[6] = ps.hist[(size_t)64 * plane + i];
+        while (rm) {
+            uint32_t hs[VB];
+            uint64_t x[VB];
+#pragma unroll
+            for (int j = 0; j < VB; ++j) {
+                hs[j] = rm ? (uint32_t)__builtin_ctzll(rm) : 0u;
+                rm &= rm - 1;
+            }
+#pragma unroll
+            for (int j = 0; j < VB; ++j) x[j] = hs[j] ? ps.hist[(size_t)hs[j] * plane + i] : 0ull;
+#pragma unroll
+            for (int j = 0; j < VB; ++j)
+#pragma unroll
+                for (uint32_t b = 0; b < 8; ++b)
+                    if ((hs[j] >> b) & 1) pl[b] |= x[j];
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < 8; ++b)
+            if (b < n_planes) vc[b * plane + i] = pl[b];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_prop_hops_export(PropState ps, uint8_t* __restrict__ out) {
     const uint32_t u = blockIdx.x * 256u + threadIdx.x;
     const uint32_t w = blockIdx.y;
@@ -1770,6 +1810,13 @@ hipError_t launch_prop_from(const PropState& ps, int32_t* first_from, hipStream_
 hipError_t launch_prop_hops_export(const PropState& ps, uint8_t* hop_mn, hipStream_t st) {
     if (ps.n_nodes == 0 || ps.n_msgs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prop_hops_export, dim3(nblk(ps.n_nodes, 256), ps.n_words), dim3(256), 0, st, ps, hop_mn);
+    return hipGetLastError();
+}
+hipError_t launch_prop_vcodes(const PropState& ps, uint64_t* vc, uint32_t n_planes, hipStream_t st) {
+    const uint64_t n = (uint64_t)ps.n_nodes * ps.n_words;
+    if (n == 0 || n_planes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prop_vcodes, dim3(std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, st, ps, vc,
+                       n_planes);
     return hipGetLastError();
 }
 hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only) {

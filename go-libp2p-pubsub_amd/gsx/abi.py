@@ -465,10 +465,10 @@ SIGNATURES = {
     "gsx_hb_px_pack": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "gsx_hb_px_recv": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "gsx_mcache_last": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32)]),
-    "gsx_mcache_copy_last": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_mcache_copy_last": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "gsx_mcache_pop": (C.c_int, [C.c_void_p]),
     "gsx_mcache_put": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig), C.c_uint32, P(C.c_uint32),
-                                 P(C.c_void_p), P(C.c_void_p)]),
+                                 P(C.c_void_p), P(C.c_void_p), P(C.c_void_p), C.c_uint32]),
     "gsx_hb_set_tracing": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gsx_set_subscriptions": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "gsx_join": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_size_t, C.c_int64, C.c_uint64,

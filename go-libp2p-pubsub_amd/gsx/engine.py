@@ -519,12 +519,23 @@ class Engine:
         self._chk(self.lib.gsx_mcache_clear(self.h), "gsx_mcache_clear")
 
     # -- message-parallel replicas: a batch from its message blocks (gsx.h gsx_mcache_*) --------
-    # A block travels as one 1-D int64 device tensor: the cache rows, then the
-    # message set's rows, [n_nodes][words(n_msgs)] u64 each.
-    def mcache_part_size(self, n_msgs: int) -> int:
-        return 2 * self.n_nodes * prop_words(n_msgs)
+    # A block travels as one 1-D int64 device tensor: the cache rows, the
+    # message set's rows, then its validation-code planes (the arrival hops,
+    # vc_planes(cfg) of them), [n_nodes][words(n_msgs)] u64 each.
+    @staticmethod
+    def vc_planes(cfg) -> int:
+        """Code planes a propagated block carries: the bits of its arrival hops
+        and the code after the last (the room gsx_propagate leaves for a
+        recovery round); none when every hop takes no time (every copy
+        validated at now_ns)."""
+        if cfg is None or cfg.hop_latency_ns + cfg.validation_delay_ns <= 0:
+            return 0
+        return int(cfg.max_hops + 1).bit_length()
 
-    def mcache_take_block(self, pad: int, device):
+    def mcache_part_size(self, n_msgs: int, cfg=None) -> int:
+        return (2 + self.vc_planes(cfg)) * self.n_nodes * prop_words(n_msgs)
+
+    def mcache_take_block(self, pad: int, device, cfg=None):
         """The newest cached batch (this replica's block) out of the cache ->
         (tensor of max(pad, its size) int64 on `device`, n_msgs); stream-ordered."""
         import torch
@@ -532,9 +543,10 @@ class Engine:
         W, m = C.c_uint32(), C.c_uint32()
         self._chk(self.lib.gsx_mcache_last(self.h, C.byref(W), C.byref(m)), "gsx_mcache_last")
         n = self.n_nodes * W.value
-        t = torch.zeros(max(pad, 2 * n), dtype=torch.int64, device=device)
-        self._chk(self.lib.gsx_mcache_copy_last(self.h, C.c_void_p(t.data_ptr()), C.c_void_p(t.data_ptr() + 8 * n)),
-                  "gsx_mcache_copy_last")
+        p = self.vc_planes(cfg)
+        t = torch.zeros(max(pad, (2 + p) * n), dtype=torch.int64, device=device)
+        self._chk(self.lib.gsx_mcache_copy_last(self.h, C.c_void_p(t.data_ptr()), C.c_void_p(t.data_ptr() + 8 * n),
+                                                C.c_void_p(t.data_ptr() + 16 * n), p), "gsx_mcache_copy_last")
         self._chk(self.lib.gsx_mcache_pop(self.h), "gsx_mcache_pop")
         return t, m.value
 
@@ -548,12 +560,13 @@ class Engine:
         mcache_take_block returns them, block k = part_msgs[k] messages)."""
         ms = np.ascontiguousarray(msgs, dtype=abi.msg_dtype())
         k = len(blocks)
+        sz = [self.n_nodes * prop_words(int(n)) for n in part_msgs]
         cp = (C.c_void_p * k)(*[b.data_ptr() for b in blocks])
-        sp = (C.c_void_p * k)(*[b.data_ptr() + 8 * self.n_nodes * prop_words(int(n))
-                                for b, n in zip(blocks, part_msgs)])
+        sp = (C.c_void_p * k)(*[b.data_ptr() + 8 * z for b, z in zip(blocks, sz)])
+        vp = (C.c_void_p * k)(*[b.data_ptr() + 16 * z for b, z in zip(blocks, sz)])
         pm = np.ascontiguousarray(part_msgs, dtype=np.uint32)
         self._chk(self.lib.gsx_mcache_put(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg), k,
-                                          _ptr(pm, C.c_uint32), cp, sp), "gsx_mcache_put")
+                                          _ptr(pm, C.c_uint32), cp, sp, vp, self.vc_planes(cfg)), "gsx_mcache_put")
 
     def set_subscriptions(self, joined):
         """Joined topics per node (bit t of joined[v]); gsx_set_subscriptions."""

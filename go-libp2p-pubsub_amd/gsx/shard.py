@@ -486,9 +486,9 @@ class MessageParallel:
         """One all-gather of the replicas' cache blocks; every replica Puts the whole batch."""
         m, w = len(msgs), self.tp.world
         counts = [(m * (k + 1)) // w - (m * k) // w for k in range(w)]
-        pad = max(self.e.mcache_part_size(n) for n in counts)
+        pad = max(self.e.mcache_part_size(n, cfg) for n in counts)
         if n_mine:
-            mine, got = self.e.mcache_take_block(pad, self.tp.device)
+            mine, got = self.e.mcache_take_block(pad, self.tp.device, cfg)
             if got != n_mine:
                 raise RuntimeError(f"the newest cached batch holds {got} messages, not this replica's {n_mine}")
         else:

@@ -661,10 +661,19 @@ int gsx_set_gossipsub_params(gsx_engine* e, const gsx_gossipsub_params* p);
  *      tests read the scores as (D) started); a forwarded first receipt is
  *      delivered (P2, P3 in the mesh), fulfils promises and is Put into the
  *      same recovered batch; a forwarded duplicate counts for P3 (in the
- *      mesh) iff the receiver got the message in this round, or else iff
- *      now - the now_ns of the call that made the message set <=
- *      MeshMessageDeliveriesWindow (the engine keeps one validation time per
- *      set, not per node: an old copy counts as validated at that time).
+ *      mesh) iff now - the time the receiver's copy finished validating <=
+ *      MeshMessageDeliveriesWindow (score.go:944-974: drec.validated per
+ *      (observer, message)): `now` for a copy of this round; for an older
+ *      one, the call's now_ns + arrival hop * (hop_latency_ns +
+ *      validation_delay_ns) (its source: now_ns) when it came with the
+ *      propagation, or the `now` of the heartbeat whose exchange recovered
+ *      it.  The engine keeps these times as a code per (node, message) over a
+ *      short per-set time list (bit planes beside the set's seen rows, built
+ *      from the call's arrival hops when hop_latency_ns + validation_delay_ns
+ *      > 0 and the gossip exchange is on), so a window boundary that falls
+ *      between two arrival hops splits the copies exactly as the reference
+ *      does.  A set cached while the exchange was off keeps no hops: a later
+ *      round whose window would split its copies fails with GSX_ESTATE.
  *      At the start of every heartbeat
  *      the IHAVE counters are cleared (:1566-1576) and promises that expired
  *      before now are broken: AddPenalty(peer, count) (:1578-1583, P7).
@@ -964,22 +973,31 @@ int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_wind
  *   gsx_mcache_copy_last  its cache rows (after the uncache of dropped
  *                         messages) and its message set's rows (every node
  *                         that saw each message), [node][n_words] u64 each,
- *                         into caller device buffers (engine stream order);
+ *                         and n_planes planes of the set's validation codes
+ *                         (each node's arrival hop of each message, bit b in
+ *                         plane b, [plane][node][n_words]; zero-extended, at
+ *                         least the set's; 0 planes: none copied) into caller
+ *                         device buffers (engine stream order);
  *   gsx_mcache_pop        drops it (the next message set reuses its serial);
  *   gsx_mcache_put        Puts msgs[0..m) of cfg's topic as one batch: block k
  *                         is messages [sum part_msgs[<k], + part_msgs[k]) with
  *                         its rows (device, [node][words(part_msgs[k])],
  *                         words() = the propagation's row width, gsx.h
- *                         gsx_propagate) at cache_parts[k] / set_parts[k].
+ *                         gsx_propagate) at cache_parts[k] / set_parts[k], and
+ *                         its code planes ([n_planes][node][words], n_planes
+ *                         <= 8) at code_parts[k] (n_planes 0: every copy
+ *                         validated at cfg's now_ns).
  *                         Publishing at unjoined sources (the fanout pick of
  *                         gossipsub.go:981-998, idempotent) runs for every
  *                         source of msgs, as the whole call would have.
  * Unsharded engines, gossipsub batches. */
 int gsx_mcache_last(gsx_engine* e, uint32_t* n_words, uint32_t* n_msgs);
-int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows);
+int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows, uint64_t* code_rows,
+                         uint32_t n_planes);
 int gsx_mcache_pop(gsx_engine* e);
 int gsx_mcache_put(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
-                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts);
+                   const uint32_t* part_msgs, const uint64_t* const* cache_parts, const uint64_t* const* set_parts,
+                   const uint64_t* const* code_parts, uint32_t n_planes);
 
 /* Per-launch timing of the fused refresh+score kernel over a region: after
  * gsx_timing_begin, each of the next (up to max_launches) gsx_refresh calls

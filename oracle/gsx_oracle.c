@@ -86,8 +86,16 @@ typedef struct {
     uint32_t serial, m, n, refs;
     uint32_t* val;
     uint32_t* src; /* [message] the publishing node (the origin, excluded by forwarding) */
-    int64_t t0;    /* now_ns of the call that made the set (the validation time of old copies, gsx.h) */
+    int64_t t0;    /* now_ns of the call that made the set */
     uint8_t* seen;
+    /* when each node's copy finished validating (score.go:944-974 keeps
+     * drec.validated per (observer, message)): [node * m + k] a code into
+     * vtime; the call's copies have code = arrival hop (validated at t0 + hop
+     * * (hop_latency + validation_delay), the source at t0), every exchange
+     * round that recovered copies of the set appends the code of its `now` */
+    uint16_t* vcode;
+    int64_t* vtime;
+    uint32_t n_vtime;
 } orc_msgset;
 typedef struct {
     uint32_t topic, m, n;
@@ -326,6 +334,8 @@ static void batch_free(orc_mc_batch* b) {
         free(b->set->val);
         free(b->set->src);
         free(b->set->seen);
+        free(b->set->vcode);
+        free(b->set->vtime);
         free(b->set);
     }
     b->set = NULL;
@@ -1379,6 +1389,11 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
         mcb->set->src = (uint32_t*)malloc(sizeof(uint32_t) * m);
         mcb->set->t0 = cfg->now_ns;
         mcb->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
+        mcb->set->vcode = (uint16_t*)calloc(m * (size_t)(N ? N : 1), sizeof(uint16_t));
+        mcb->set->n_vtime = cfg->max_hops + 1;
+        mcb->set->vtime = (int64_t*)malloc(sizeof(int64_t) * mcb->set->n_vtime);
+        for (uint32_t h = 0; h <= cfg->max_hops; h++)
+            mcb->set->vtime[h] = cfg->now_ns + (int64_t)h * (cfg->hop_latency_ns + cfg->validation_delay_ns);
         for (size_t k = 0; k < m; k++) {
             mcb->set->val[k] = msgs[k].validation;
             mcb->set->src[k] = msgs[k].source;
@@ -1468,6 +1483,7 @@ int orc_propagate(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_c
             for (uint32_t i = 0; i < N; i++) {
                 mcb->has[(size_t)i * m + k] = hop[i] != 0xFF && (!dropped || i == src);
                 mcb->set->seen[(size_t)i * m + k] = hop[i] != 0xFF;
+                mcb->set->vcode[(size_t)i * m + k] = hop[i] != 0xFF ? hop[i] : 0;
             }
     }
     free(hop);
@@ -2318,7 +2334,8 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
                                 if (qr >= 0) __atomic_fetch_add(&c_first[qr], 1u, __ATOMIC_RELAXED);
                             } else { /* DuplicateMessage: P3 inside the window (gsx.h) */
                                 s_dup++;
-                                const int64_t validated = has[(size_t)u * m + k] ? now : st->t0;
+                                const int64_t validated =
+                                    has[(size_t)u * m + k] ? now : st->vtime[st->vcode[(size_t)u * m + k]];
                                 if (qr >= 0 && now - validated <= o->tp[t < GSX_MAX_TOPICS ? t : 0].mesh_message_deliveries_window_ns)
                                     __atomic_fetch_add(&c_win[qr], 1u, __ATOMIC_RELAXED);
                             }
@@ -2394,6 +2411,22 @@ static int gossip_exchange(orc_engine* o, const gsx_gossipsub_params* gp, uint64
             rt[b] = rt[b - 1];
             rt[b - 1] = tt;
         }
+    /* the copies recovered in this round were validated at `now` (every copy
+     * of the exchange and its forwarding is handled at now): one new code per
+     * set */
+    for (size_t x = 0; x < nr; x++) {
+        orc_msgset* st = rs[x];
+        if (st->n_vtime >= 0xFFFF) {
+            rc = GSX_ERANGE; /* (a set recovered in 65k rounds) */
+            continue;
+        }
+        const uint16_t c = (uint16_t)st->n_vtime++;
+        st->vtime = (int64_t*)realloc(st->vtime, sizeof(int64_t) * st->n_vtime);
+        st->vtime[c] = now;
+        const size_t cells = (size_t)st->m * N;
+        for (size_t i = 0; i < cells; i++)
+            if (rh[x][i]) st->vcode[i] = c;
+    }
     *rec_out = (orc_mc_batch*)calloc(nr ? nr : 1, sizeof(orc_mc_batch));
     *n_rec = nr;
     for (size_t x = 0; x < nr; x++) {
@@ -2938,11 +2971,13 @@ int orc_mcache_last(orc_engine* o, uint32_t* n_msgs) {
     return 0;
 }
 
-int orc_mcache_copy_last(orc_engine* o, uint8_t* cache_rows, uint8_t* set_rows) {
+int orc_mcache_copy_last(orc_engine* o, uint8_t* cache_rows, uint8_t* set_rows, uint8_t* hop_rows) {
     const orc_mc_batch* b = mcache_newest(o);
     if (!b || !b->set) return GSX_ESTATE;
     memcpy(cache_rows, b->has, (size_t)b->m * b->n);
     memcpy(set_rows, b->set->seen, (size_t)b->m * b->n);
+    if (hop_rows) /* a propagated set's codes are its arrival hops (<= GSX_MAX_HOPS) */
+        for (size_t i = 0; i < (size_t)b->m * b->n; i++) hop_rows[i] = (uint8_t)b->set->vcode[i];
     return 0;
 }
 
@@ -2956,7 +2991,8 @@ int orc_mcache_pop(orc_engine* o) {
 }
 
 int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
-                   const uint32_t* part_msgs, const uint8_t* const* cache_parts, const uint8_t* const* set_parts) {
+                   const uint32_t* part_msgs, const uint8_t* const* cache_parts, const uint8_t* const* set_parts,
+                   const uint8_t* const* hop_parts) {
     if (!o->mc || !m || cfg->router != GSX_ROUTER_GOSSIPSUB) return GSX_EINVAL;
     size_t tot = 0;
     for (uint32_t k = 0; k < n_parts; k++) tot += part_msgs[k];
@@ -2983,6 +3019,11 @@ int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_
     b->set->src = (uint32_t*)malloc(sizeof(uint32_t) * m);
     b->set->t0 = cfg->now_ns;
     b->set->seen = (uint8_t*)calloc(m * (size_t)(N ? N : 1), 1);
+    b->set->vcode = (uint16_t*)calloc(m * (size_t)(N ? N : 1), sizeof(uint16_t));
+    b->set->n_vtime = cfg->max_hops + 1;
+    b->set->vtime = (int64_t*)malloc(sizeof(int64_t) * b->set->n_vtime);
+    for (uint32_t h = 0; h <= cfg->max_hops; h++)
+        b->set->vtime[h] = cfg->now_ns + (int64_t)h * (cfg->hop_latency_ns + cfg->validation_delay_ns);
     for (size_t k = 0; k < m; k++) {
         b->ids[k] = msgs[k].msg_id;
         b->set->val[k] = msgs[k].validation;
@@ -2994,6 +3035,9 @@ int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_
         for (uint32_t i = 0; i < N && nk; i++) {
             memcpy(b->has + (size_t)i * m + off, cache_parts[k] + (size_t)i * nk, nk);
             memcpy(b->set->seen + (size_t)i * m + off, set_parts[k] + (size_t)i * nk, nk);
+            if (hop_parts && hop_parts[k])
+                for (size_t j = 0; j < nk; j++)
+                    b->set->vcode[(size_t)i * m + off + j] = hop_parts[k][(size_t)i * nk + j];
         }
         off += nk;
     }

@@ -84,10 +84,13 @@ int orc_promise_throttle(orc_engine* o, uint64_t pair);
 int orc_promise_count(orc_engine* o, uint64_t* n);
 int orc_mcache_clear(orc_engine* o);
 int orc_mcache_last(orc_engine* o, uint32_t* n_msgs);
-int orc_mcache_copy_last(orc_engine* o, uint8_t* cache_rows, uint8_t* set_rows);
+/* hop_rows (may be NULL): the set's arrival hops ([node][message] bytes, the
+ * validation codes of a propagated set) */
+int orc_mcache_copy_last(orc_engine* o, uint8_t* cache_rows, uint8_t* set_rows, uint8_t* hop_rows);
 int orc_mcache_pop(orc_engine* o);
 int orc_mcache_put(orc_engine* o, const gsx_msg* msgs, size_t m, const gsx_prop_config* cfg, uint32_t n_parts,
-                   const uint32_t* part_msgs, const uint8_t* const* cache_parts, const uint8_t* const* set_parts);
+                   const uint32_t* part_msgs, const uint8_t* const* cache_parts, const uint8_t* const* set_parts,
+                   const uint8_t* const* hop_parts);
 int orc_mcache_ids(orc_engine* o, uint32_t node, uint32_t topic, uint32_t n_windows, uint64_t* out, size_t cap,
                    size_t* n_out);
 int orc_set_ip_whitelist(orc_engine* o, const uint32_t* ip_ids, size_t n);

@@ -80,10 +80,10 @@ _SIG = {
     "orc_mcache_ids": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint64), C.c_size_t,
                                  P(C.c_size_t)]),
     "orc_mcache_last": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
-    "orc_mcache_copy_last": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "orc_mcache_copy_last": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "orc_mcache_pop": (C.c_int, [C.c_void_p]),
     "orc_mcache_put": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(abi.PropConfig), C.c_uint32, P(C.c_uint32),
-                                 P(C.c_void_p), P(C.c_void_p)]),
+                                 P(C.c_void_p), P(C.c_void_p), P(C.c_void_p)]),
 }
 
 _lib = None
@@ -259,20 +259,22 @@ class Oracle:
     def mcache_clear(self):
         self._chk(self.lib.orc_mcache_clear(self.h), "orc_mcache_clear")
 
-    # message-parallel replicas (gsx.h gsx_mcache_*): blocks are [2, n_nodes, n_msgs]
-    # bytes (cache membership, then message-set rows), flattened
-    def mcache_part_size(self, n_msgs: int) -> int:
-        return 2 * self.n_nodes * n_msgs
+    # message-parallel replicas (gsx.h gsx_mcache_*): blocks are [3, n_nodes, n_msgs]
+    # bytes (cache membership, message-set rows, arrival hops: the set's
+    # validation codes), flattened
+    def mcache_part_size(self, n_msgs: int, cfg=None) -> int:
+        return 3 * self.n_nodes * n_msgs
 
-    def mcache_take_block(self, pad: int, device="cpu"):
+    def mcache_take_block(self, pad: int, device="cpu", cfg=None):
         """The newest cached batch out of the cache -> (1-D uint8 torch tensor of pad elements, n_msgs)."""
         import torch
 
         m = C.c_uint32()
         self._chk(self.lib.orc_mcache_last(self.h, C.byref(m)), "orc_mcache_last")
         n = self.n_nodes * m.value
-        buf = np.zeros(max(pad, 2 * n), dtype=np.uint8)
-        self._chk(self.lib.orc_mcache_copy_last(self.h, buf.ctypes.data, buf.ctypes.data + n), "orc_mcache_copy_last")
+        buf = np.zeros(max(pad, 3 * n), dtype=np.uint8)
+        self._chk(self.lib.orc_mcache_copy_last(self.h, buf.ctypes.data, buf.ctypes.data + n, buf.ctypes.data + 2 * n),
+                  "orc_mcache_copy_last")
         self._chk(self.lib.orc_mcache_pop(self.h), "orc_mcache_pop")
         return torch.from_numpy(buf), m.value
 
@@ -287,9 +289,10 @@ class Oracle:
         k = len(arrs)
         cp = (C.c_void_p * k)(*[a.ctypes.data for a in arrs])
         sp = (C.c_void_p * k)(*[a.ctypes.data + self.n_nodes * int(n) for a, n in zip(arrs, part_msgs)])
+        hp = (C.c_void_p * k)(*[a.ctypes.data + 2 * self.n_nodes * int(n) for a, n in zip(arrs, part_msgs)])
         pm = np.ascontiguousarray(part_msgs, dtype=np.uint32)
         self._chk(self.lib.orc_mcache_put(self.h, ms.ctypes.data_as(C.c_void_p), len(ms), C.byref(cfg), k,
-                                          _p(pm, C.c_uint32), cp, sp), "orc_mcache_put")
+                                          _p(pm, C.c_uint32), cp, sp, hp), "orc_mcache_put")
 
     def hb_set_tracing(self, on: bool = True):
         """(the oracle always records the trace words)"""

@@ -70,3 +70,18 @@ def test_recovered_copies_are_cached():
     be2 = orc.Oracle(2)
     _, _, _, cached2 = gc.exchange_run(be2, ticks=3, history_gossip=3, gossip_exchange=0)
     assert n_cached > sum(len(c) for c in cached2)
+
+
+def test_exchange_window_boundary_between_hops_splits_credits():
+    """The oracle keeps each node's validation time (score.go:944-974): with the
+    P3 window boundary between arrival hops (892 ms: hop 2 of the last batch
+    inside, hops 0-1 outside) the forwarded duplicates' MMD credits differ from
+    both a window that leaves every old copy outside (880 ms) and one that
+    takes every copy of the last batch in (905 ms)."""
+    mmd = {}
+    for win in (880, 892, 905):
+        _, outs, snaps, _ = gc.exchange_run(orc.Oracle(2), window_ms=win, hops=3, ticks=5)
+        assert sum(o["fwd_duplicates"] for o in outs) > 0
+        mmd[win] = np.concatenate([np.asarray(s["mesh_message_deliveries"]).reshape(-1) for s in snaps])
+    assert not np.array_equal(mmd[892], mmd[880])
+    assert not np.array_equal(mmd[892], mmd[905])

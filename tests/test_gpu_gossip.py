@@ -52,6 +52,66 @@ def test_gossip_exchange_matches_oracle(gpu_ok, kw):
     assert sum(o["iwant_msgs"] for o in g[1]) > 0
 
 
+# Heartbeats every second, batches 100 ms after one with 5 ms hops: an old
+# copy's validation time is the batch's now + 5 ms x its arrival hop, or the
+# heartbeat that recovered it.  892 ms: the window boundary falls between hops
+# 1 and 2 of the last batch (hop 2 inside, hops 0 and 1 outside); 897 ms:
+# between the source and hop 1; 1000 ms: the copies recovered one heartbeat
+# earlier are inside too; 2500 ms: two heartbeats back, older ones outside;
+# 2 ms hops + 1 ms validation delay with the boundary between hops 2 and 3.
+WINDOW_CASES = [
+    dict(window_ms=892, hops=3),
+    dict(window_ms=897, hops=3),
+    dict(window_ms=1000, hops=3, history_gossip=3),
+    dict(window_ms=2500, hops=2, ticks=6),
+    dict(window_ms=893.5, hops=4, latency_ms=2, delay_ms=1.0, T=1, msgs=40),
+]
+
+
+@pytest.mark.parametrize("kw", WINDOW_CASES, ids=["hop1_2", "src_hop1", "one_round", "two_rounds", "delay"])
+def test_gossip_exchange_per_node_validation_time(gpu_ok, kw):
+    """A forwarded duplicate counts for P3 iff now - the receiver's own
+    validation time <= MeshMessageDeliveriesWindow (score.go:944-974: per
+    (observer, message) drec.validated), with the window boundary between
+    arrival hops / recovery rounds: engine == oracle."""
+    T = kw.get("T", 2)
+    g = gc.exchange_run(gsx.Engine(T), **kw)
+    w = gc.exchange_run(orc.Oracle(T), **kw)
+    _same(g, w)
+    assert sum(o["fwd_duplicates"] for o in g[1]) > 0
+
+
+def test_sets_cached_with_exchange_off_refuse_a_split_window(gpu_ok):
+    """A batch propagated with the gossip exchange off keeps no arrival hops
+    (its per-node validation times are not built): once the exchange is on, a
+    heartbeat whose P3 window would split that set's copies is refused
+    (GSX_ESTATE) rather than credited inexactly; a window that leaves them all
+    on one side runs."""
+    import heartbeat_cases as hc
+    import propagation_cases as pcs
+
+    for win, ok in ((892, False), (25, True)):
+        e = gsx.Engine(1)
+        ov = pcs.overlay(300, 6, 5)
+        pcs.setup(e, ov, 1, 5, mesh_degree=6)
+        from gsx import synth
+
+        tp = synth.spam_test_topic_params()
+        tp.mesh_message_deliveries_window_ns = int(win * abi.MILLISECOND)
+        e.set_topic_params(0, tp)
+        e.set_gossipsub_params(gc.params(gossip_exchange=0))
+        now = hc.T0 + 3 * abi.SECOND
+        cfg = pcs.config(abi.GSX_ROUTER_GOSSIPSUB, max_hops=3, latency_ms=5, seed=9)
+        cfg.now_ns = now + 100 * abi.MILLISECOND
+        e.propagate(pcs.messages(300, 24, 9), cfg)
+        e.set_gossipsub_params(gc.params())
+        if ok:
+            e.heartbeat(1, now + abi.SECOND, 7)
+        else:
+            with pytest.raises(abi.GsxError):
+                e.heartbeat(1, now + abi.SECOND, 7)
+
+
 @pytest.mark.timeout(600)
 def test_gossip_exchange_1024_per_heartbeat(gpu_ok):
     """1024 messages between heartbeats: the five-window gossip list holds up

@@ -14,11 +14,11 @@ from gsx import abi, shard, synth
 pytestmark = pytest.mark.gpu
 
 
-def _params(e, T):
+def _params(e, T, window_ms=25):
     e.set_peer_params(synth.bench_peer_params())
     for t in range(T):
         tp = synth.spam_test_topic_params()
-        tp.mesh_message_deliveries_window_ns = 25 * abi.MILLISECOND
+        tp.mesh_message_deliveries_window_ns = int(window_ms * abi.MILLISECOND)
         e.set_topic_params(t, tp)
     e.set_thresholds(abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
                                     accept_px_threshold=0, opportunistic_graft_threshold=0))
@@ -243,12 +243,13 @@ def test_sharded_heartbeat_matches_single_engine(gpu_ok, world):
     assert want["grafts"] + want["prunes"] > 0
 
 
-@pytest.mark.parametrize("world,invalid,T,max_ihave,m",
-                         [(2, 0.0, 2, 5000, 24), (3, 0.2, 2, 5000, 24), (2, 0.0, 1, 5000, 24),
-                          (2, 0.0, 2, 20, 24), (3, 0.2, 1, 20, 24), (3, 0.0, 1, 5000, 2600)],
+@pytest.mark.parametrize("world,invalid,T,max_ihave,m,window",
+                         [(2, 0.0, 2, 5000, 24, None), (3, 0.2, 2, 5000, 24, None), (2, 0.0, 1, 5000, 24, None),
+                          (2, 0.0, 2, 20, 24, None), (3, 0.2, 1, 20, 24, None), (3, 0.0, 1, 5000, 2600, None),
+                          (2, 0.0, 2, 5000, 24, 892), (3, 0.2, 1, 20, 24, 1000)],
                          ids=["w2-T2", "w3-T2-invalid", "w2-T1", "w2-T2-trunc20", "w3-T1-trunc20-invalid",
-                              "w3-T1-trunc5000"])
-def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid, T, max_ihave, m):
+                              "w3-T1-trunc5000", "w2-T2-window-hop1_2", "w3-T1-trunc20-window-one_round"])
+def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid, T, max_ihave, m, window):
     """The gossip exchange on range shards (gsx_gx_*: IHAVE bits and answer
     bits of cross-shard pairs, the senders' cache rows, the forwarding of
     recovered messages hop by hop with frontier entries): rounds of a
@@ -258,7 +259,10 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
     every node's records, backoff, IHAVEs, scores and cached ids.  The trunc
     cases hold more ids in the gossip window than MaxIHaveLength (20, or the
     reference's 5000 with 2,600-message batches): every target gets its own
-    subset (gossipsub.go:1708-1720), which crosses the shards as masked rows."""
+    subset (gossipsub.go:1708-1720), which crosses the shards as masked rows.
+    The window cases put the P3 window boundary between arrival hops / recovery
+    rounds (per-node validation times): the senders' inside rows travel with
+    their cache rows for the hop-1 back-sends."""
     import gossip_cases as gc
     import heartbeat_cases as hc
 
@@ -266,6 +270,8 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
     ov = pc.overlay(n, d, seed)
     full = gsx.Engine(T)
     app = pc.setup(full, ov, T, seed, mesh_degree=6)
+    if window is not None:
+        _params(full, T, window)
     gp = gc.params(max_ihave_length=max_ihave)
     full.set_gossipsub_params(gp)
     st0 = full.export_state()
@@ -277,7 +283,7 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
         sh = synth.shard_of(ov, lo, hi)
         a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
         e = gsx.Engine(T)
-        _params(e, T)
+        _params(e, T, 25 if window is None else window)
         e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
         e.import_state(_slice_state(st0, T, E, a, b))
         e.set_app_scores(app[a:b])
@@ -326,8 +332,8 @@ def test_sharded_heartbeat_exchange_matches_single_engine(gpu_ok, world, invalid
         assert truncated > 0
 
 
-@pytest.mark.parametrize("world,invalid", [(2, 0.0), (3, 0.2)])
-def test_message_parallel_heartbeat_matches_single_engine(gpu_ok, world, invalid):
+@pytest.mark.parametrize("world,invalid,window", [(2, 0.0, None), (3, 0.2, None), (2, 0.0, 892)])
+def test_message_parallel_heartbeat_matches_single_engine(gpu_ok, world, invalid, window):
     """Message-parallel replicas through propagate -> heartbeat cycles with the
     gossip exchange on: every replica propagates its block, the cache blocks
     are all-gathered and Put back whole (gsx_mcache_put, k_mc_merge), the
@@ -336,6 +342,8 @@ def test_message_parallel_heartbeat_matches_single_engine(gpu_ok, world, invalid
     import gossip_cases as gc
 
     kw = dict(n=1500, ticks=4, msgs=150, invalid=invalid)
+    if window is not None:  # the window boundary between arrival hops: the blocks carry their code planes
+        kw.update(window_ms=window, hops=3)
     _, want_outs, want_snaps, want_cached = gc.exchange_run(gsx.Engine(2), **kw)
     assert sum(o["iwant_msgs"] for o in want_outs) > 0 and sum(o["gossip_delivered"] for o in want_outs) > 0
 
