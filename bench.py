@@ -66,7 +66,7 @@ def build_engine(n, T, d, seed, device):
     return ov, e
 
 
-PMC_FILE = "pmc_r04.json"  # written by tools/pmc_r04.sh (tools/pmc_r04.py)
+PMC_FILE = "pmc_r05.json"  # written by tools/pmc.sh (tools/pmc_bytes.py)
 
 
 def load_pmc():
@@ -215,19 +215,19 @@ def with_traffic(roof, traffic, ms):
     if traffic and ms:
         ach = traffic / (ms * 1e-3) / 1e9
         roof.update(traffic=traffic, achieved_traffic=ach, frac_traffic=ach / HBM_PEAK_GBS,
-                    traffic_source=f"profiles/{PMC_FILE} (tools/pmc_r04.sh)")
+                    traffic_source=f"profiles/{PMC_FILE} (tools/pmc.sh)")
     else:
         roof.update(traffic=None, traffic_source=f"none: profiles/{PMC_FILE} holds no PMC pass of this workload")
     return roof
 
 
 def prop_workload(n, msgs):
-    """The propagation workload key shared with tools/pmc_r04.py (tools/prop_profile.py)."""
+    """The propagation workload key shared with tools/pmc_bytes.py (tools/prop_profile.py)."""
     return {"peers": int(n), "msgs": int(msgs), "router": "gossipsub", "credit": "now"}
 
 
 def hb_workload(n, T, msgs, exchange):
-    """The heartbeat workload key shared with tools/pmc_r04.py (tools/hb_micro.py)."""
+    """The heartbeat workload key shared with tools/pmc_bytes.py (tools/hb_micro.py)."""
     return {"peers": int(n), "topics": int(T), "msgs_between_rounds": int(msgs), "exchange": bool(exchange)}
 
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel traces of the heartbeat with the gossip exchange (cfg3 rounds,
 # tools/hb_micro.py --exchange) and of the cfg5 attack round (tools/adv_micro.py)
-# per-round breakdowns with tools/hb_rounds.py.
+# per-round breakdowns with tools/kt_rounds.py (forwarding hops listed per dispatch).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -20,9 +20,9 @@ step() {  # step NAME SECONDS CMD...
 }
 step hbx 300 rocprofv3 --kernel-trace --stats -d "$O/hbx" -o kt --output-format csv -- \
     python3 tools/hb_micro.py --exchange --rounds 4
-python3 tools/hb_rounds.py "$O/hbx/kt_kernel_trace.csv" > "$O/hbx_rounds.txt"
+python3 tools/kt_rounds.py "$O/hbx/kt_kernel_trace.csv" 30 k_gxf_pull k_gxf_mark > "$O/hbx_rounds.txt"
 python3 tools/kt_top.py "$O/hbx/kt_kernel_stats.csv" 24 > "$O/hbx_top.txt"
 step adv 300 rocprofv3 --kernel-trace --stats -d "$O/adv" -o kt --output-format csv -- \
     python3 tools/adv_micro.py --no-spam
-python3 tools/hb_rounds.py "$O/adv/kt_kernel_trace.csv" > "$O/adv_rounds.txt"
+python3 tools/kt_rounds.py "$O/adv/kt_kernel_trace.csv" 30 k_gxf_pull k_gxf_mark > "$O/adv_rounds.txt"
 cat "$O/hbx_rounds.txt" "$O/hbx_top.txt" "$O/adv_rounds.txt"

@@ -3,7 +3,7 @@
 every kernel between it and the next round's scan, grouped by kernel name,
 largest first; propagation kernels (k_prop_*) between rounds are left out.
 
-    python tools/kt_rounds_all.py kt_kernel_trace.csv [top] [kernel ...]
+    python tools/kt_rounds.py kt_kernel_trace.csv [top] [kernel ...]
 
 Kernels named after `top` also get their dispatch durations listed in order
 (e.g. k_gxf_pull_g k_gxf_mark: the forwarding's per-hop times)."""

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise tools/pmc_r04.sh: HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB
+"""Summarise tools/pmc.sh: HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB
 (gfx950, checked by tools/microbench/pmc_calib.hip) per launch of the headline
 kernel, per batch of the propagation hops and per-call passes, per heartbeat
 round (the last round of bench.py's heartbeat leg).  Each section carries the workload
 it measured, in bench.py's keys (bench.pmc_bytes compares them).
-usage: pmc_r04.py <dir> <headline config key, e.g. n=1000000,T=8,d=6,E=11999954>"""
+usage: pmc_bytes.py <dir> <headline config key, e.g. n=1000000,T=8,d=6,E=11999954>"""
 import collections
 import csv
 import json
@@ -51,6 +51,9 @@ def main():
     }
     for name, batches in (("p1024", 3), ("p64", 3)):
         rows = load(d, name)
+        marks = [i for i, x in enumerate(rows) if short(x[0]) == "k_prop_hops_export"]
+        if marks:  # prop_profile.py --warmup: the batches after the marker (steady state)
+            rows = rows[marks[-1] + 1:]
         hop = [x for x in rows if short(x[0]).startswith("k_prop_hop")]
         call = [x for x in rows if short(x[0]).startswith(("k_prop", "k_mc_summary")) and x not in hop]
         per = collections.defaultdict(float)

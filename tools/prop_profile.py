@@ -16,6 +16,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--peers", type=int, default=1_000_000)
 ap.add_argument("--msgs", type=int, default=256)
 ap.add_argument("--batches", type=int, default=3)
+ap.add_argument("--warmup", type=int, default=0,
+                help="batches before the measured ones, then one k_prop_hops_export (gsx_prop_results) as the "
+                     "marker tools/pmc_bytes.py counts from (the first call's full fwd / pin passes stay out)")
 ap.add_argument("--router", type=int, default=abi.GSX_ROUTER_GOSSIPSUB)
 ap.add_argument("--track", type=int, default=0, help="keep first-deliverer rows (gsx_prop_set_tracking)")
 ap.add_argument("--credit", type=int, default=abi.GSX_CREDIT_NOW)
@@ -35,7 +38,9 @@ cfg = bench.prop_config(A, a.peers)
 cfg.router = a.router
 cfg.credit_scores = a.credit
 cfg.hop_latency_ns = a.latency_us * 1000
-for b in range(a.batches):
+for b in range(a.warmup + a.batches):
+    if a.warmup and b == a.warmup:
+        e.prop_results(a.msgs)  # (read-only: the marker dispatch)
     out = e.propagate(bench.prop_messages(a.peers, a.msgs, synth.SEED, first=b * a.msgs), cfg)[0]
     d = out.as_dict()
     print(json.dumps({"batch": b, "hop_kernel_ms": out.hop_kernel_ms, "deliveries": d["deliveries"],
