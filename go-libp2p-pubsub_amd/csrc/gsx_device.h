@@ -413,6 +413,7 @@ struct GxBatch {
     uint32_t old_in;      // a copy of the set's messages validated before this round is inside the P3 window (old_inside)
     uint32_t grp;         // the set's group: up to 64 sets of one topic (the forwarding's hop-1 back counts)
     VcRef vc;             // the set's validation codes (old_in 2)
+    const uint32_t* cnt;  // [node]: messages the node holds in this batch (k_mc_summary / k_gx_merge_sets)
     uint32_t vin_off;     // (range shards, old_in 2) word offset of the inside rows in a gxs_rows entry: 1 + fw + woff
 };
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
@@ -477,8 +478,10 @@ struct HbState {
     uint32_t* n_hub;       // [topic]
     const uint32_t* hubs;  // nodes with more than HB_LANE_DEG peers (k_hb_recv_hub)
     uint32_t n_hubs;
-    uint32_t* ihave_len;   // [topic][pair] ids advertised (0 = no IHAVE)
+    uint32_t* ihave_len;   // [topic][pair] ids advertised (valid under ihave_tag == ihave_cur; else no IHAVE)
     uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
+    uint8_t* ihave_tag;    // [topic][pair] the round that wrote the slot
+    uint8_t ihave_cur;     // this round's tag
     // the gossip exchange (step (D)); null when it is off
     uint64_t* ihave_bits;  // [pair (u -> v), the receiver's]: topics v sent u an IHAVE for this round
     uint64_t* ihave_tr;    // [pair (u -> v)]: topics whose IHAVE from v was truncated (a GxSub row)
@@ -588,9 +591,10 @@ hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t s
 // its set's common words (gx_rhm: only there can the node hold a message some
 // receiver lacks).
 hipError_t launch_gx_rhm(const GxBatch* gx, uint32_t n_gx, uint32_t n_nodes, uint64_t* rhm, hipStream_t st);
-// One pass over the seen rows of every message set of an exchange (blockIdx.y =
-// set): the receipt rows zeroed, `full` recomputed (when non-null) and the
-// common words ANDed (when non-null; preset to ~0 by the caller).
+// One pass over the seen rows of the message sets of an exchange that need
+// it (blockIdx.y = entry): the receipt rows zeroed (x non-null), `full`
+// recomputed (non-null) and the common words ANDed (non-null; preset to ~0 by
+// the caller); the seen rows are read only for the last two.
 struct GxSetPrep {
     const uint64_t* all;
     uint64_t* x;
@@ -614,6 +618,7 @@ struct GxSetMerge {
     uint64_t* vc;              // the set's code planes: the recovered copies take `code` (null: none)
     uint64_t plane;
     uint32_t n_planes, code;
+    uint8_t* chg;              // set to 1 when some receipt changes the set's seen rows
 };
 hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // The forwarding of the recovered messages (gsx.h (D): a delivered message is

@@ -119,6 +119,10 @@ struct gsx_engine {
     std::vector<uint32_t> hubs_host;  // nodes with more than HB_LANE_DEG pairs
     std::vector<uint8_t> gossip_prev;  // per topic: IHAVE slots written last round
     uint64_t* d_ihave_hash = nullptr;
+    // [topic][pair]: the heartbeat round that wrote the IHAVE slot (ihave_len /
+    // ihave_hash hold a slot only under the current round's tag: no per-round clear)
+    uint8_t* d_ihave_tag = nullptr;
+    uint8_t ihave_round = 0;
     bool have_gossip = false;
     bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
     bool hb_tracing = false;           // gsx_hb_set_tracing: keep the round's tracer Graft / Prune words
@@ -155,6 +159,13 @@ struct gsx_engine {
         uint8_t* d_small = nullptr;  // the pooled block d_val / d_acc / d_dg live in
         size_t small_bytes = 0, full_bytes = 0;
         bool full_ok = false;       // d_full matches d_all
+        // (one engine) the exchange's per-set prep kept across rounds while no
+        // receipt changes d_all: the messages every node had (64 words), and a
+        // receipt buffer a round left untouched (still zero)
+        uint64_t* d_common = nullptr;
+        size_t common_bytes = 0;
+        bool common_ok = false;
+        uint64_t* xs_spare = nullptr;
         std::vector<uint64_t> ids;
         int refs = 0;
     };
@@ -220,6 +231,7 @@ struct gsx_engine {
     void* h_gxstage = nullptr;        // pinned staging of the exchange's batch list (hb_end)
     size_t h_gxstage_bytes = 0;
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
+    uint8_t* d_gx_chg = nullptr;   // [set of the round]: a receipt changed its seen rows (k_gx_merge_sets)
     uint64_t* d_gx_vin = nullptr;  // the round's inside-code bits of the mixed sets (GxRound::vin_host)
     size_t gx_vin_cap = 0;
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
@@ -739,6 +751,8 @@ void set_release(gsx_engine* e, gsx_engine::MsgSet* st) {
     if (st->d_vc) (void)vc_fence(e);  // (a build may still write the planes going back to the pool)
     seen_release(e, st->d_all, st->all_words);
     seen_release(e, st->d_vc, st->vc_words);
+    seen_release(e, st->xs_spare, 0);
+    small_release(e, reinterpret_cast<uint8_t*>(st->d_common), st->common_bytes);
     small_release(e, st->d_small, st->small_bytes);
     small_release(e, st->d_full, st->full_bytes);
     delete st;
@@ -845,7 +859,7 @@ void free_state(gsx_engine* e) {
     e->d_col = nullptr;
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
                   e->d_backoff, e->d_bo8, e->d_ctl, e->d_resp,   e->d_dirty,     e->d_long,
-                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_gb,
+                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_ihave_tag, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
@@ -909,6 +923,8 @@ void free_state(gsx_engine* e) {
         if (e->d_gx_vin) (void)hipFree(e->d_gx_vin);
         e->d_gx_vin = nullptr;
         e->gx_vin_cap = 0;
+        if (e->d_gx_chg) (void)hipFree(e->d_gx_chg);
+        e->d_gx_chg = nullptr;
         e->d_gx_heads = nullptr;
         e->d_gx_sp = nullptr;
         e->d_gx_mg = nullptr;
@@ -935,6 +951,8 @@ void free_state(gsx_engine* e) {
     e->d_tcnt = nullptr;
     e->d_mcount = nullptr;
     e->d_ihave_hash = nullptr;
+    e->d_ihave_tag = nullptr;
+    e->ihave_round = 0;
     e->d_gb = nullptr;
     e->d_mc_digest = nullptr;
     e->gb_cap = e->ids_cap = 0;
@@ -1456,10 +1474,13 @@ int hb_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
         (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
         (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
-        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
+        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_ihave_tag, TE)) ||
+        (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
         return rc;
     HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, TE ? TE : 1, e->stream));
+    e->ihave_round = 0;
     if (!e->hubs_host.empty())
         HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
                                  e->stream));
@@ -3870,16 +3891,14 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // the truncated IHAVE lists' rows (exchange on, a window longer than MaxIHaveLength)
     if (gx_on)
         if (int rc = gx_sub_prepare(e, max_ids, tw)) return rc;
-    // IHAVE slots: a topic with gossip this round has its slots rewritten by
-    // k_hb_gossip; one that had gossip last round but none now is cleared here
-    for (uint32_t t = 0; t < e->T; ++t) {
-        const bool now_g = gb_off[t + 1] > gb_off[t] && max_ids[t] > 0;
-        if (!now_g && e->gossip_prev[t]) {
-            HIPCHK(e, hipMemsetAsync(e->d_ihave_len + (size_t)t * e->E, 0, 4 * e->E, e->stream));
-            HIPCHK(e, hipMemsetAsync(e->d_ihave_hash + (size_t)t * e->E, 0, 8 * e->E, e->stream));
-        }
-        e->gossip_prev[t] = now_g;
+    // IHAVE slots: this round's are written under its tag (k_hb_gossip); every
+    // other slot reads as empty, so nothing is cleared but once per 255 rounds
+    if (++e->ihave_round == 0) {
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, (size_t)e->T * e->E, e->stream));
+        e->ihave_round = 1;
     }
+    h.ihave_tag = e->d_ihave_tag;
+    h.ihave_cur = e->ihave_round;
     e->have_gossip = !e->gb_host.empty();
     // (A) the scan of every unit, then per topic, ascending: maintenance, then
     // emitGossip.  A unit changes only its own topic's records, backoff entries
@@ -4234,6 +4253,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
     const size_t hist = (size_t)std::max(e->gp.history_length, 1);
     std::vector<gsx::GxBatch> gx;
     std::vector<bool> gx_full_new;  // per set: its full bytes are recomputed this round
+    std::vector<bool> x_zero;       // per set: its receipt rows are zero already
     std::vector<uint32_t> off(e->T + 1, 0);
     const size_t n_win = std::min<size_t>((size_t)std::max(e->gp.history_gossip, 0), e->mc.size());
     const size_t N = e->n_nodes;
@@ -4250,9 +4270,13 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
                 while (i < R.sets.size() && R.sets[i] != b.set) ++i;
                 if (i == R.sets.size()) {
                     const size_t words = (size_t)b.set->n_words * N + 2 * N;  // rows + (dig, cnt) tail
-                    uint64_t* x = seen_acquire(e, words);  // (rows zeroed by k_gx_setprep)
-                    if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
                     gsx_engine::MsgSet* ms = b.set;
+                    // a receipt buffer the set's last round left untouched is still zero
+                    uint64_t* x = ms->xs_spare;
+                    x_zero.push_back(x != nullptr);
+                    ms->xs_spare = nullptr;
+                    if (!x) x = seen_acquire(e, words);  // (rows zeroed by k_gx_setprep)
+                    if (!x) return fail(e, GSX_ENOMEM, "gossip exchange receipts");
                     // which nodes have seen the whole set (skipped by the walk): k_gx_setprep
                     gx_full_new.push_back(!ms->full_ok);
                     if (!ms->full_ok) {
@@ -4273,6 +4297,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
                                           (uint32_t)(e->mc.size() < hist || w + 1 < hist), ro});
                 gx.back().got = reinterpret_cast<uint8_t*>(i);  // (index; rebased below)
                 gx.back().dense = b.recovered ? 0u : 1u;
+                gx.back().cnt = b.d_cnt;
                 gx.back().src = b.set->d_src;
             }
     }
@@ -4368,6 +4393,9 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         e->d_gx_heads = nullptr;
         if (int rc = dalloc(e, &e->d_gx_heads, e->gx_cap)) return rc;
         if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
+        if (e->d_gx_chg) (void)hipFree(e->d_gx_chg);
+        e->d_gx_chg = nullptr;
+        if (int rc = dalloc(e, &e->d_gx_chg, e->gx_cap)) return rc;
     }
     // per set, the messages every node had seen as the exchange began (a
     // set wider than 64 words keeps none: its rows are filtered by emptiness)
@@ -4385,11 +4413,36 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         if (!e->d_gx_rhm)
             if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
     }
-    std::vector<gsx::GxSetPrep> sprep(R.sets.size());
+    // per set what the prep pass has to do: zero the receipt rows, recompute
+    // the full bytes, AND the common words; a set with none of it is skipped
+    // (one engine keeps each set's common words while its seen rows stand;
+    // a range shard ANDs them over the ranks every round)
+    std::vector<gsx::GxSetPrep> sprep;
+    std::vector<uint64_t*> common_of(R.sets.size(), nullptr);
     for (size_t i = 0; i < R.sets.size(); ++i) {
-        const gsx_engine::MsgSet* ms = R.sets[i];
-        sprep[i] = gsx::GxSetPrep{ms->d_all, R.xs[i], gx_full_new[i] ? ms->d_full : nullptr,
-                                  ms->n_words <= 64 ? e->d_gx_common + 64 * i : nullptr, ms->n_words, ms->n_msgs};
+        gsx_engine::MsgSet* ms = R.sets[i];
+        uint64_t* common = nullptr;
+        bool redo_common = false;
+        if (ms->n_words <= 64) {
+            if (e->sharded()) {
+                common = e->d_gx_common + 64 * i;
+                redo_common = true;
+            } else {
+                if (!ms->d_common) {
+                    ms->d_common = reinterpret_cast<uint64_t*>(small_acquire(e, 8 * 64, &ms->common_bytes));
+                    if (!ms->d_common) return fail(e, GSX_ENOMEM, "message set common words");
+                    ms->common_ok = false;
+                }
+                common = ms->d_common;
+                redo_common = !ms->common_ok;
+                if (redo_common) HIPCHK(e, hipMemsetAsync(common, 0xff, 8 * 64, e->stream));
+                ms->common_ok = true;  // (hb_finish drops it when a receipt changes the rows)
+            }
+        }
+        common_of[i] = common;
+        gsx::GxSetPrep p{ms->d_all, x_zero[i] ? nullptr : R.xs[i], gx_full_new[i] ? ms->d_full : nullptr,
+                         redo_common ? common : nullptr, ms->n_words, ms->n_msgs};
+        if (p.x || p.full || p.common) sprep.push_back(p);
     }
     std::vector<gsx::GxSetMerge> smerge(R.sets.size());
     for (size_t i = 0; i < R.sets.size(); ++i) {
@@ -4397,15 +4450,16 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         const size_t W = ms->n_words;
         smerge[i] = gsx::GxSetMerge{ms->d_all, R.xs[i], ms->d_acc, ms->d_dg, R.xs[i] + W * N,
                                     reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs,
-                                    ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i]};
+                                    ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i], e->d_gx_chg + i};
     }
-    HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
+    if (e->sharded()) HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
     for (auto& g : gx) {
         const size_t si = reinterpret_cast<size_t>(g.got);
-        g.common = R.sets[si]->n_words <= 64 ? e->d_gx_common + 64 * si : nullptr;
+        g.common = common_of[si];
         g.got = e->d_gx_got + si;
     }
     HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_gx_chg, 0, e->gx_cap, e->stream));
     {  // the batch list, offsets and set heads through a pinned staging buffer:
         // async copies, so the host keeps queueing instead of waiting for the
         // kernels before them (the last round's copies drained at its end)
@@ -4438,7 +4492,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
         std::memcpy(hs + a_mg, smerge.data(), b_mg);
         HIPCHK(e, hipMemcpyAsync(e->d_gx_mg, hs + a_mg, b_mg, hipMemcpyHostToDevice, e->stream));
-        // receipt rows zeroed, full bytes, common words: every set in one pass
+        // receipt rows zeroed, full bytes, common words: every set that needs any, in one pass
         HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
     }
     R.h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
@@ -4498,11 +4552,13 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     unsigned long long st[gsx::HB_STAT_WORDS];
     HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     uint32_t gflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std::vector<uint8_t> got(gx_sets.size(), 0);
+    std::vector<uint8_t> got(gx_sets.size(), 0), chg(gx_sets.size(), 1);
     if (gx_run) {
         HIPCHK(e, hipMemcpyAsync(gflag, e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
         if (!got.empty() && !got_all)
             HIPCHK(e, hipMemcpyAsync(got.data(), e->d_gx_got, got.size(), hipMemcpyDeviceToHost, e->stream));
+        if (!chg.empty())
+            HIPCHK(e, hipMemcpyAsync(chg.data(), e->d_gx_chg, chg.size(), hipMemcpyDeviceToHost, e->stream));
     }
     dbg_host("gx queued");
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -4533,7 +4589,8 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     for (size_t i : by_serial) {
         gsx_engine::MsgSet* ms = gx_sets[i];
         if (!got[i]) {
-            seen_release(e, gx_x[i], (size_t)ms->n_words * N + 2 * N);
+            if (!chg[i] && !ms->xs_spare) ms->xs_spare = gx_x[i];  // untouched: still zero for the next round
+            else seen_release(e, gx_x[i], (size_t)ms->n_words * N + 2 * N);
             // nothing recovered: no copy took this round's code (k_gx_merge_sets writes accepted receipts only)
             if (i < R.vc_code.size() && ms->vtime.size() == (size_t)R.vc_code[i] + 1) ms->vtime.pop_back();
             continue;
@@ -4557,8 +4614,12 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     if (e->d_prom_e) e->gx_clean = gx_run || (e->gp.gossip_exchange && !e->have_gossip);
     const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] +
                                           st[gsx::HB_FWD_DELIVERED] > 0;
-    for (auto* ms : gx_sets) {
-        if (merged || e->sharded()) ms->full_ok = false;  // the receipts were merged into their seen rows
+    for (size_t i = 0; i < gx_sets.size(); ++i) {
+        gsx_engine::MsgSet* ms = gx_sets[i];
+        if (e->sharded() ? merged : chg[i] != 0) {  // the receipts were merged into its seen rows
+            ms->full_ok = false;
+            ms->common_ok = false;
+        }
         set_release(e, ms);
     }
     gx_sets.clear();
@@ -5280,7 +5341,15 @@ int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_diges
     if (ihave_len && TE) HIPCHK(e, hipMemcpyAsync(ihave_len, e->d_ihave_len, 4 * TE, hipMemcpyDeviceToHost, e->stream));
     if (ihave_digest && TE)
         HIPCHK(e, hipMemcpyAsync(ihave_digest, e->d_ihave_hash, 8 * TE, hipMemcpyDeviceToHost, e->stream));
+    std::vector<uint8_t> tag(TE);
+    if (TE) HIPCHK(e, hipMemcpyAsync(tag.data(), e->d_ihave_tag, TE, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    const uint8_t cur = e->ihave_round;  // (0: no heartbeat ran, every slot empty)
+    for (size_t i = 0; i < TE; ++i)
+        if (tag[i] != cur || cur == 0) {  // a slot of an earlier round
+            if (ihave_len) ihave_len[i] = 0;
+            if (ihave_digest) ihave_digest[i] = 0;
+        }
     return GSX_OK;
 }
 

@@ -846,8 +846,10 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
 }
 
 // Per node v, bit g: v's row of advertised batch g holds a message outside
-// its set's common words (batches past 64, first-hand batches: always set).  Thread v reads its W
-// words of each batch row (adjacent nodes, adjacent rows: coalesced).
+// its set's common words (batches past 64, first-hand batches: always set;
+// recovered batches: set when the node's row is non-empty, from the batch's
+// per-node counts).  Thread v reads its W words of any other batch row
+// (adjacent nodes, adjacent rows: coalesced).
 __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, uint32_t n_gx, uint32_t n,
                                                 uint64_t* __restrict__ rhm) {
     for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
@@ -856,6 +858,10 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
             const GxBatch& b = gx[g];
             if (b.dense) {  // (a set bit only lets the ask read the row: always safe)
                 m |= 1ull << g;
+                continue;
+            }
+            if (b.cnt) {  // a recovered batch: the node's count of it (its rows are sparse: most counts 0);
+                if (b.cnt[v]) m |= 1ull << g;  // a non-empty row is taken as uncommon (safe, as above)
                 continue;
             }
             const uint32_t W = b.n_words;
@@ -875,6 +881,7 @@ __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict_
     const GxSetPrep S = sets[blockIdx.y];
     const uint32_t W = S.n_words;
     const bool and_words = S.common != nullptr && W <= 64;
+    const bool read = and_words || S.full;
     if (threadIdx.x < 64) sw[threadIdx.x] = ~0ull;
     __syncthreads();
     const uint32_t stride = gridDim.x * 256u;
@@ -884,10 +891,10 @@ __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict_
         const bool in = v < n;
         uint32_t c = 0;
         for (uint32_t w = 0; w < W; ++w) {
-            const uint64_t x = in ? S.all[(size_t)v * W + w] : ~0ull;
+            const uint64_t x = in && read ? S.all[(size_t)v * W + w] : ~0ull;
             if (in) {
                 c += (uint32_t)__popcll(x);
-                S.x[(size_t)v * W + w] = 0;
+                if (S.x) S.x[(size_t)v * W + w] = 0;
             }
             if (and_words) {
                 uint64_t a = x;
@@ -917,6 +924,7 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
             uint64_t word = S.x[i];
             if (!word) continue;
             S.all[i] |= word;
+            if (S.chg && !*S.chg) *S.chg = 1;  // (read first: one writer in many stores)
             word &= S.acc[w];
             S.x[i] = word;
             if (S.vc && word)  // the recovered copies were validated now: this round's code

@@ -987,10 +987,6 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
             for (int j = 0; j < 4; ++j) {
                 const int64_t r = rb + 64 * j;
                 if (r >= pb) continue;
-                if (!h.fan_mode) {  // (the fanout pass adds to the slots the mesh pass rewrote)
-                    h.ihave_len[tslot + r] = 0;
-                    h.ihave_hash[tslot + r] = 0;
-                }
                 if (!staged) continue;
                 // gossip_target with the loads above (live score: dirty pairs re-evaluated)
                 bool ok = (pf[j] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && in_t[j] &&
@@ -1030,6 +1026,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                             const size_t x = tslot + rs[lane] + peers[q];
                             h.ihave_len[x] = L;
                             h.ihave_hash[x] = dig;
+                            h.ihave_tag[x] = h.ihave_cur;
                             ihave_mark(h, (uint64_t)(rs[lane] + peers[q]), t);  // (D) reads it
                         }
                         cnt[0] += (uint64_t)target;
@@ -1183,6 +1180,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 const int64_t r = r0 + peers[p];
                 h.ihave_len[tslot + r] = L;
                 h.ihave_hash[tslot + r] = dall;
+                h.ihave_tag[tslot + r] = h.ihave_cur;
                 ihave_mark(h, (uint64_t)r, t);  // (D) reads it
             }
             msgs += (uint64_t)target;
@@ -1218,6 +1216,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 if (lane == 0) {
                     h.ihave_len[tslot + r] = maxl;
                     h.ihave_hash[tslot + r] = take ? d : dall - d;
+                    h.ihave_tag[tslot + r] = h.ihave_cur;
                     ihave_mark(h, (uint64_t)r, t);
                 }
                 // the subset the receiver's handleIHave reads (D): marked at the

@@ -124,37 +124,32 @@ __device__ __forceinline__ uint32_t pin_of(const PropState& ps, uint64_t q) {
 // bit) and pin[rev r] (what it lets through), marking their observers for
 // k_prop_compact.  One launch over all pairs either way; in the incremental
 // case every thread past the list returns at once.
+// (A grid-stride loop on a capped grid: an incremental pass of a few changes
+// costs a few waves, not a launch over every pair.)
 __global__ __launch_bounds__(256) void k_prop_pin(PropState ps) {
-    const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (q >= ps.n_pairs) return;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
     const uint32_t n = ps.inc ? *ps.nchg : 0;
     if (!ps.inc || n > ps.chg_cap) {
-        ps.pin[q] = pin_of(ps, q);
+        for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += stride) ps.pin[q] = pin_of(ps, q);
         return;
     }
-    if (q >= n) return;
-    const uint32_t r = ps.chg[q];
-    ps.pin[r] = pin_of(ps, r);
-    const uint32_t v = ps.pair_obs[r];
-    atomicOr((unsigned long long*)&ps.ndirty[v / 64], 1ull << (v % 64));
-    const uint32_t q2 = ps.rev[r];
-    if (q2 != NO_PAIR && !(q2 & HALO)) {
-        ps.pin[q2] = pin_of(ps, q2);
-        const uint32_t u = ps.pair_obs[q2];
-        atomicOr((unsigned long long*)&ps.ndirty[u / 64], 1ull << (u % 64));
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < n; q += stride) {
+        const uint32_t r = ps.chg[q];
+        ps.pin[r] = pin_of(ps, r);
+        const uint32_t v = ps.pair_obs[r];
+        atomicOr((unsigned long long*)&ps.ndirty[v / 64], 1ull << (v % 64));
+        const uint32_t q2 = ps.rev[r];
+        if (q2 != NO_PAIR && !(q2 & HALO)) {
+            ps.pin[q2] = pin_of(ps, q2);
+            const uint32_t u = ps.pair_obs[q2];
+            atomicOr((unsigned long long*)&ps.ndirty[u / 64], 1ull << (u % 64));
+        }
     }
 }
 
 // Node u's compacted senders (ps.cent / ps.cend): every node after a full
 // pin pass, else the nodes k_prop_pin marked (their marks cleared here).
-__global__ __launch_bounds__(256) void k_prop_compact(PropState ps) {
-    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
-    if (u >= ps.n_nodes) return;
-    const bool full = !ps.inc || *ps.nchg > ps.chg_cap;
-    if (!full) {
-        const uint64_t w = ps.ndirty[u / 64];
-        if (!((w >> (u % 64)) & 1)) return;
-    }
+__device__ __forceinline__ void compact_node(const PropState& ps, uint32_t u) {
     const int64_t q0 = ps.row_ptr[u], q1 = ps.row_ptr[u + 1];
     int64_t k = q0;
     for (int64_t q = q0; q < q1; ++q) {
@@ -163,11 +158,29 @@ __global__ __launch_bounds__(256) void k_prop_compact(PropState ps) {
     }
     ps.cend[u] = (uint32_t)k;
 }
-__global__ __launch_bounds__(256) void k_prop_compact_done(PropState ps) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < (ps.n_nodes + 63) / 64) ps.ndirty[i] = 0;
-    if (i == 0) *ps.nchg = 0;  // the next call's change list starts empty
+// (incremental: a thread per 64-node word of marks, the marked nodes only;
+// the marks are cleared here, and the change list emptied by the last wave)
+__global__ __launch_bounds__(256) void k_prop_compact(PropState ps) {
+    const bool full = !ps.inc || *ps.nchg > ps.chg_cap;
+    const uint32_t stride = gridDim.x * 256u;
+    if (full) {
+        for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < ps.n_nodes; u += stride) compact_node(ps, u);
+        return;
+    }
+    const uint32_t nw = (ps.n_nodes + 63) / 64;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nw; i += stride) {
+        uint64_t w = ps.ndirty[i];
+        if (!w) continue;
+        ps.ndirty[i] = 0;
+        for (; w; w &= w - 1) compact_node(ps, i * 64 + (uint32_t)__builtin_ctzll(w));
+    }
 }
+__global__ __launch_bounds__(256) void k_prop_compact_done(PropState ps) {
+    const uint32_t stride = gridDim.x * 256u;
+    const bool full = !ps.inc || *ps.nchg > ps.chg_cap;  // (an incremental compact cleared its marks)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; full && i < (ps.n_nodes + 63) / 64; i += stride) ps.ndirty[i] = 0;
+}
+__global__ void k_prop_nchg_reset(PropState ps) { *ps.nchg = 0; }  // the next call's change list starts empty
 
 // The origin and hop-0 rows are read only for nodes with their row-0
 // occupancy bit (the call's sources), so only the sources' rows are cleared
@@ -1823,11 +1836,13 @@ hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t s
     if (s.n_pairs == 0) return hipSuccess;
     if (!pins_only)
         hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
-    hipLaunchKernelGGL(k_prop_pin, dim3(nblk(s.n_pairs, 256)), dim3(256), 0, st, ps);
+    hipLaunchKernelGGL(k_prop_pin, dim3(std::min(nblk(s.n_pairs, 256), 8192u)), dim3(256), 0, st, ps);
     if (ps.n_nodes) {
-        hipLaunchKernelGGL(k_prop_compact, dim3(nblk(ps.n_nodes, 256)), dim3(256), 0, st, ps);
-        hipLaunchKernelGGL(k_prop_compact_done, dim3(nblk((ps.n_nodes + 63) / 64, 256)), dim3(256), 0, st, ps);
+        hipLaunchKernelGGL(k_prop_compact, dim3(std::min(nblk(ps.n_nodes, 256), 4096u)), dim3(256), 0, st, ps);
+        hipLaunchKernelGGL(k_prop_compact_done, dim3(std::min(nblk((ps.n_nodes + 63) / 64, 256), 1024u)), dim3(256), 0,
+                           st, ps);
     }
+    hipLaunchKernelGGL(k_prop_nchg_reset, dim3(1), dim3(1), 0, st, ps);
     return hipGetLastError();
 }
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st) {
