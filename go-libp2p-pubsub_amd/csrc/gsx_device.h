@@ -482,6 +482,7 @@ struct HbState {
     uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
     uint8_t* ihave_tag;    // [topic][pair] the round that wrote the slot
     uint8_t ihave_cur;     // this round's tag
+    uint8_t* gelig;        // [pair] GELIG_TARGET | GELIG_SCORE as the round started (k_hb_gelig)
     // the gossip exchange (step (D)); null when it is off
     uint64_t* ihave_bits;  // [pair (u -> v), the receiver's]: topics v sent u an IHAVE for this round
     uint64_t* ihave_tr;    // [pair (u -> v)]: topics whose IHAVE from v was truncated (a GxSub row)
@@ -734,6 +735,8 @@ hipError_t launch_gx_count(const HbState& h, unsigned long long* n, hipStream_t 
 hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_base, uint32_t n_t, int64_t max_deg,
                               hipStream_t st);  // topics t_base .. t_base + n_t - 1
 // tw: the topic's gossip row words (sum of its batches' n_words)
+constexpr uint8_t GELIG_TARGET = 1, GELIG_SCORE = 2;
+hipError_t launch_hb_gelig(const DevState& s, const HbState& h, hipStream_t st);
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
                             uint32_t tw, int64_t max_deg, hipStream_t st);
 constexpr uint32_t HB_GOSSIP_MAX_WORDS = 4096;  // a topic's gossip rows: 262,144 ids (the long path's LDS rows)

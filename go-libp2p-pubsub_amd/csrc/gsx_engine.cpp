@@ -122,6 +122,7 @@ struct gsx_engine {
     // [topic][pair]: the heartbeat round that wrote the IHAVE slot (ihave_len /
     // ihave_hash hold a slot only under the current round's tag: no per-round clear)
     uint8_t* d_ihave_tag = nullptr;
+    uint8_t* d_gelig = nullptr;  // [pair] HbState::gelig
     uint8_t ihave_round = 0;
     bool have_gossip = false;
     bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
@@ -859,7 +860,7 @@ void free_state(gsx_engine* e) {
     e->d_col = nullptr;
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
                   e->d_backoff, e->d_bo8, e->d_ctl, e->d_resp,   e->d_dirty,     e->d_long,
-                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_ihave_tag, e->d_gb,
+                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_ihave_tag, e->d_gelig, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
@@ -952,6 +953,7 @@ void free_state(gsx_engine* e) {
     e->d_mcount = nullptr;
     e->d_ihave_hash = nullptr;
     e->d_ihave_tag = nullptr;
+    e->d_gelig = nullptr;
     e->ihave_round = 0;
     e->d_gb = nullptr;
     e->d_mc_digest = nullptr;
@@ -1466,7 +1468,7 @@ int hb_alloc(gsx_engine* e) {
     const size_t E = e->E;
     if ((rc = dalloc(e, &e->d_ctl, 2 * E)) ||
         (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
-        (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 1)) ||
+        (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 2 * std::max<size_t>(e->T, 1))) ||
         (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
         (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
         (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
@@ -1474,7 +1476,7 @@ int hb_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
         (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
         (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
-        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_ihave_tag, TE)) ||
+        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_ihave_tag, TE)) || (rc = dalloc(e, &e->d_gelig, E)) ||
         (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
         return rc;
     HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
@@ -3738,6 +3740,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                 e->gp.prune_peers};
     const gsx::DevState ds = dev_state(e);
     HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
+    // (per topic and gossip pass, mesh then fanout: k_hb_gossip's long-list counts)
+    HIPCHK(e, hipMemsetAsync(e->d_nlong, 0, 8 * (size_t)e->T, e->stream));
     if (gx_on) {
         h.ihave_bits = e->d_ihave_bits;
         h.ihave_tr = e->d_ihave_bits + std::max<size_t>(e->E, 1);
@@ -3899,6 +3903,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     }
     h.ihave_tag = e->d_ihave_tag;
     h.ihave_cur = e->ihave_round;
+    h.gelig = e->d_gelig;
     e->have_gossip = !e->gb_host.empty();
     // (A) the scan of every unit, then per topic, ascending: maintenance, then
     // emitGossip.  A unit changes only its own topic's records, backoff entries
@@ -3906,6 +3911,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // topic's gossip reads the live scores maintenance left (gossipsub.go:1514), so it goes
     // after its own topic's run and before the next
     dbg_host("hb sub/ihave");
+    if (e->have_gossip) HIPCHK(e, gsx::launch_hb_gelig(ds, h, e->stream));  // (emitGossip's per-pair byte)
     HIPCHK(e, gsx::launch_hb_scan(ds, h, e->stream));
     for (uint32_t t = 0, tb = 0; t < e->T; ++t) {
         const bool g = gb_off[t + 1] > gb_off[t] && max_ids[t] > 0;
@@ -3913,6 +3919,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         HIPCHK(e, gsx::launch_hb_maintain(ds, h, tb, t + 1 - tb, e->max_deg, e->stream));
         tb = t + 1;
         gsx::HbState ht = h;
+        ht.n_long = e->d_nlong + t;
         if (gx_on) ht.gsub = e->gsub_host[t];
         DBG_SYNC(4);
         HIPCHK(e, gsx::launch_hb_gossip(ds, ht, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t],
@@ -3923,6 +3930,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
             HIPCHK(e, gsx::launch_hb_fanout(ds, h, t, e->stream));
             gsx::HbState hf = h;
             hf.fan_mode = 1;
+            hf.n_long = e->d_nlong + e->T + t;
             if (gx_on) hf.gsub = e->gsub_host[t];
             HIPCHK(e, gsx::launch_hb_gossip(ds, hf, t, e->d_gb + gb_off[t], gb_off[t + 1] - gb_off[t],
                                             max_ids[t] ? tw[t] : 0, e->max_deg, e->stream));

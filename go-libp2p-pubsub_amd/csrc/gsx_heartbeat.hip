@@ -938,6 +938,23 @@ __device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, con
 // MaxIHaveLength (per-target reshuffle + truncation, :1708-1716), goes to
 // k_hb_gossip_long, one wave per node.  Blocks of four waves over a bounded
 // grid: one counter atomic per block.
+// Per pair, once per round (before any maintenance): GELIG_TARGET = the
+// topic-independent part of gossip_target (present, connected, a gossipsub
+// peer, not direct: gossipsub.go:1688-1703), GELIG_SCORE = its score as the
+// round started >= GossipThreshold; k_hb_gossip reads this byte per topic
+// instead of the flags and the score (a pair the round's maintenance touched
+// is re-evaluated live there).
+__global__ __launch_bounds__(256) void k_hb_gelig(DevState s, HbState h) {
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < h.n_pairs; r += (uint64_t)gridDim.x * 256u) {
+        const uint8_t pf = s.pflags[r], ef = h.eflags[r];
+        uint8_t g = 0;
+        if ((pf & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && (ef & EDGE_GOSSIPSUB) &&
+            !(ef & EDGE_DIRECT))
+            g = GELIG_TARGET | (s.score[r] >= h.gossip_threshold ? GELIG_SCORE : 0);
+        h.gelig[r] = g;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32_t t, const GossipBatch* __restrict__ gb,
                                                    uint32_t n_gb) {
     __shared__ int64_t rs_w[SCAN_WAVES][65];
@@ -962,17 +979,14 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
         const int64_t pa = nv ? rs[0] : 0, pb = nv ? rs[64] : 0;
         const bool staged = pb - pa <= GOSSIP_STAGE;
         for (int64_t rb = pa + lane; rb < pb; rb += 256) {
-            uint8_t pf[4], ef[4], rf[4], dt[4];
-            double sc[4];
+            uint8_t ge[4], rf[4], dt[4];
             bool in_t[4] = {true, true, true, true};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {  // unconditional loads of clamped addresses (see k_hb_scan)
                 const int64_t r = min(rb + 64 * j, pb - 1);
-                pf[j] = s.pflags[r];
-                ef[j] = h.eflags[r];
+                ge[j] = h.gelig[r];
                 rf[j] = s.rflags[flag_index(r, t, s.n_topics)];
                 dt[j] = h.dirty[r];
-                sc[j] = s.score[r];
             }
             if (h.psub) {  // (uniform) the peers' joined topics
 #pragma unroll
@@ -988,10 +1002,10 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                 const int64_t r = rb + 64 * j;
                 if (r >= pb) continue;
                 if (!staged) continue;
-                // gossip_target with the loads above (live score: dirty pairs re-evaluated)
-                bool ok = (pf[j] & (PAIR_PRESENT | PAIR_CONNECTED)) == (PAIR_PRESENT | PAIR_CONNECTED) && in_t[j] &&
-                          (ef[j] & EDGE_GOSSIPSUB) && !(ef[j] & EDGE_DIRECT) && !(rf[j] & REC_IN_MESH);
-                if (ok) ok = (dt[j] ? eval_pair(s, h.pp, r) : sc[j]) >= h.gossip_threshold;
+                // gossip_target from the round's eligibility byte (k_hb_gelig) and the
+                // topic's mesh flag; live score: dirty pairs re-evaluated
+                bool ok = (ge[j] & GELIG_TARGET) && in_t[j] && !(rf[j] & REC_IN_MESH);
+                if (ok) ok = dt[j] ? eval_pair(s, h.pp, r) >= h.gossip_threshold : (ge[j] & GELIG_SCORE) != 0;
                 el[r - pa] = ok;
             }
         }
@@ -1805,11 +1819,16 @@ hipError_t launch_hb_maintain(const DevState& s, const HbState& h, uint32_t t_ba
     return hipGetLastError();
 }
 
+hipError_t launch_hb_gelig(const DevState& s, const HbState& h, hipStream_t st) {
+    if (h.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hb_gelig, dim3((unsigned)std::min<uint64_t>((h.n_pairs + 255) / 256, 8192)), dim3(256), 0, st,
+                       s, h);
+    return hipGetLastError();
+}
 hipError_t launch_hb_gossip(const DevState& s, const HbState& h, uint32_t t, const GossipBatch* gb, uint32_t n_gb,
                             uint32_t tw, int64_t max_deg, hipStream_t st) {
     if (h.n_nodes == 0 || n_gb == 0 || tw == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(h.n_long, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;  // (h.n_long: the topic's counter, cleared at the round's start)
     hipLaunchKernelGGL(k_hb_gossip, dim3(grid_cap(h.n_nodes, 256)), dim3(256), 0, st, s, h, t, gb, n_gb);
     // queued nodes (long lists, tiles with hub rows): the kernel returns at once without any
     const size_t lds = (size_t)tw * 20 + 4 + sizeof(uint16_t) * (size_t)std::max<int64_t>(max_deg, 1);
