@@ -370,18 +370,16 @@ struct VcRef {
     uint64_t plane;       // words per plane (nodes x n_words)
     uint32_t n_planes, pad;
 };
-// The bits of `bits` (old copies in word idx = node * n_words + w) whose code is inside.
+// The bits of `bits` (old copies in word idx = node * n_words + w) whose code
+// is inside.  Bit by bit with the plane words re-read (cached) rather than held:
+// the mixed-window path is rare, and registers it held would count against
+// every caller's occupancy (the forwarding pull's).
 __device__ __forceinline__ uint64_t vc_inside(const VcRef& V, size_t idx, uint64_t bits) {
-    if (!bits) return 0;
-    uint64_t pl[VC_MAX_PLANES];
-#pragma unroll
-    for (uint32_t b = 0; b < VC_MAX_PLANES; ++b) pl[b] = b < V.n_planes ? V.vc[b * V.plane + idx] : 0ull;
     uint64_t in = 0;
     for (uint64_t m = bits; m; m &= m - 1) {
         const uint32_t i = (uint32_t)__builtin_ctzll(m);
         uint32_t c = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < VC_MAX_PLANES; ++b) c |= (uint32_t)((pl[b] >> i) & 1) << b;
+        for (uint32_t b = 0; b < V.n_planes; ++b) c |= (uint32_t)((V.vc[b * V.plane + idx] >> i) & 1) << b;
         if ((V.vin[c >> 6] >> (c & 63)) & 1) in |= 1ull << i;
     }
     return in;
@@ -512,6 +510,7 @@ struct HbState {
     uint32_t* gxs_hidx;
     const uint64_t* gxs_rows;
     uint32_t gxs_fw;
+    uint32_t gx_mixed;  // some set of the round has old_in 2 (per-copy validation codes)
     uint32_t gxs_vin;   // entries carry, after the rows, the sender's inside rows of the mixed sets (old_in 2):
                         // the bits of its row whose copy at the sender is inside the P3 window (hop-1 back-sends)
     // the IWANT first receipts per (topic, pair) of this round (the forwarding's
@@ -688,6 +687,7 @@ struct GxFwd {
     const uint64_t* hent;
     uint32_t rw;
     uint32_t dense_div;  // a hop is dense when its last frontier exceeds n_nodes / dense_div
+    uint32_t mixed;      // some set's old copies are split by the P3 window (old_in 2)
 };
 constexpr uint32_t GXF_HDR = 6;
 constexpr uint32_t GXF_DENSE = 16;

@@ -4104,6 +4104,7 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
             // an old copy: inside the window by its code's validation time (gsx.h (D))
             S.old_in = R.old_in[i];
             S.vc = R.vc[i];
+            if (S.old_in == 2) f.mixed = 1;
             f.slot_sets[ts] |= 1ull << f.n_sets;
             stage[f.n_sets] = S;
             ++f.n_sets;
@@ -4246,6 +4247,7 @@ int gx_vcodes(gsx_engine* e, gsx_engine::GxRound& R) {
                                  e->stream));
     // range shards: the rows entries carry the senders' inside rows when some set is mixed
     R.h.gxs_vin = R.vin_host.empty() ? 0u : 1u;
+    R.h.gx_mixed = R.h.gxs_vin;
     for (size_t i = 0; i < ns; ++i) {
         const gsx_engine::MsgSet* ms = R.sets[i];
         R.vc[i] = gsx::VcRef{ms->d_vc, R.old_in[i] == 2 ? e->d_gx_vin + vin_off[i] : nullptr,

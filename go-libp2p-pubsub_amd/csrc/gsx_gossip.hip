@@ -48,9 +48,11 @@ __device__ __forceinline__ uint64_t gx_mem(const HbState& h, const GxBatch& b, u
 // The bits of `bits` (messages v served u from its cache, word w of batch b)
 // whose copy at v is inside the P3 window: v's copies are old (validated
 // before the round: gsx.h (D)); a remote v's from the inside rows its rank sent.
+// (MIX: some set of the round is mixed; the instance without it keeps its registers)
+template <bool MIX>
 __device__ __forceinline__ uint64_t gx_in_at_sender(const HbState& h, const GxBatch& b, uint64_t q, uint32_t v,
                                                     uint32_t w, uint64_t bits) {
-    if (b.old_in != 2 || !bits) return b.old_in ? bits : 0ull;
+    if (!MIX || b.old_in != 2 || !bits) return b.old_in ? bits : 0ull;
     if (h.gxs_hidx && (h.rev[q] & HALO)) {
         const uint32_t k = h.gxs_hidx[q];
         return k == NO_PAIR ? 0ull : bits & h.gxs_rows[(size_t)k * gxs_ew(h) + b.vin_off + w];
@@ -309,6 +311,7 @@ __device__ __forceinline__ Rng gx_iwant_rng(const HbState& h, uint32_t u, uint32
 // handleIWant at v and the receipt at u, one id at a time (pass 2 for a pair
 // whose asked subset was sampled, kk < n: the same draws select it again),
 // each receipt credited by its own tracer call.
+template <bool MIX>
 __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbState& h, uint32_t u, uint64_t q,
                                                    uint32_t r, uint64_t tb, uint32_t kk, uint32_t n, uint64_t& served,
                                                    uint64_t& delivered, uint64_t& rejected, uint64_t& dups) {
@@ -338,7 +341,7 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
                 ++delivered;
                 ev_first(s, q, t);
                 if (h.gxb_st0 && !((origin_word(b.src, b.n_msgs, v, k / 64) >> (k % 64)) & 1)) {
-                    const uint32_t in = gx_in_at_sender(h, b, q, v, k / 64, bit) ? 1u : 0u;
+                    const uint32_t in = gx_in_at_sender<MIX>(h, b, q, v, k / 64, bit) ? 1u : 0u;
                     gx_back0(h, q, b.grp, in, 1u - in);
                 }
                 *b.got = 1;
@@ -680,6 +683,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
 //          at a time;
 //  then fulfillPromise (:119-126): u's promises whose message is now in its
 //  receipt rows (promises are only added in pass 1).
+template <bool MIX>
 __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
     const uint32_t lane = threadIdx.x;
     const uint32_t S = h.prom_slots;
@@ -790,7 +794,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                                 if (acc1 && h.gxb_st0) {  // the back-sends of these first receipts (GxFwd)
                                     const uint64_t bk = acc1 & ~origin_word(b.src, b.n_msgs, v, w);
                                     if (bk) {
-                                        const uint64_t bin = gx_in_at_sender(h, b, (uint64_t)q, v, w, bk);
+                                        const uint64_t bin = gx_in_at_sender<MIX>(h, b, (uint64_t)q, v, w, bk);
                                         atomicAdd(&h.gxb_cnt0[(size_t)b.grp * h.n_pairs + q],
                                                   (uint32_t)__popcll(bin) | (uint32_t)__popcll(bk & ~bin) << 16);
                                     }  // (cleared before the walk)
@@ -805,7 +809,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                         if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
                     }
                 } else if (lane == 0) {
-                    gx_receive_sampled(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
+                    gx_receive_sampled<MIX>(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
                 }
                 __threadfence_block();  // this pair's receipts before the next pair's duplicate tests
             }
@@ -927,11 +931,13 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
             if (S.chg && !*S.chg) *S.chg = 1;  // (read first: one writer in many stores)
             word &= S.acc[w];
             S.x[i] = word;
-            if (S.vc && word)  // the recovered copies were validated now: this round's code
-                for (uint32_t b = 0; b < S.n_planes; ++b) {
-                    uint64_t* pw = S.vc + b * S.plane + i;
-                    *pw = (*pw & ~word) | (((S.code >> b) & 1) ? word : 0ull);
-                }
+            // the recovered copies were validated now: this round's code, ORed into
+            // the planes of its 1-bits (a copy received now was unseen, so its
+            // code bits are all 0 yet: k_prop_vcodes writes 0 for them, and only
+            // accepted receipts ever take a code)
+            if (S.vc && word)
+                for (uint32_t c = S.code, b = 0; c; c >>= 1, ++b)
+                    if (c & 1) S.vc[b * S.plane + i] |= word;
             L += (uint32_t)__popcll(word);
             const uint32_t left = S.n_msgs > w * 64 ? S.n_msgs - w * 64 : 0;
             const uint64_t full = left >= 64 ? ~0ull : ((1ull << left) - 1);
@@ -1314,7 +1320,10 @@ __device__ __forceinline__ uint64_t gxf_gor(uint64_t x) {  // OR over the group 
 }
 // B rounds of G senders have their filter loads (slot byte, reverse pair, peer;
 // frontier bit; frontier mask) issued together, three latencies per B rounds.
-template <int G, int B>
+// MIX: some set of the run has a P3 window that splits its old copies (old_in
+// 2, per-copy codes: vc_inside); a separate instance, so the common one keeps
+// its registers (the per-copy path costs ~23 VGPRs, a wave per SIMD).
+template <int G, int B, bool MIX>
 __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd f, uint32_t hop) {
     const uint32_t p = (hop - 1) & 1, pw = hop & 1;
     const uint32_t seq_cur = f.seq + hop;
@@ -1434,7 +1443,8 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
                         // in-window duplicates: those x got this round (before this hop, or first
                         // from a lower sender of this one); an old copy by its validation time
                         const uint64_t cur = dup & (xw | (excl & ~have));
-                        dw += (uint32_t)__popcll(cur | old_inside(S.old_in, S.vc, (size_t)x * W + w, dup & ~cur));
+                        if (MIX) dw += (uint32_t)__popcll(cur | old_inside(S.old_in, S.vc, (size_t)x * W + w, dup & ~cur));
+                        else dw += (uint32_t)__popcll(S.old_in ? dup : cur);
                         n1 += (uint32_t)__popcll(nw);
                         const uint64_t gn = all_g & ~have;  // the group's first receipts of the word
                         if (gn) {
@@ -1707,7 +1717,8 @@ hipError_t launch_gx_exchange(const DevState& s, const HbState& h, hipStream_t s
     if (h.n_nodes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gx_ask, dim3(gx_blocks(h.n_nodes, 64, 8192)), dim3(64), 0, st, s, h);
     // the listed nodes (their count is on the device): a wave each, grid-stride
-    hipLaunchKernelGGL(k_gx_node, dim3(8192), dim3(64), 0, st, s, h);
+    if (h.gx_mixed) hipLaunchKernelGGL(k_gx_node<true>, dim3(8192), dim3(64), 0, st, s, h);
+    else hipLaunchKernelGGL(k_gx_node<false>, dim3(8192), dim3(64), 0, st, s, h);
     return hipGetLastError();
 }
 
@@ -1740,12 +1751,18 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
         return v && atoi(v) > 0 ? (unsigned)atoi(v) : 2048u;
     }();
     const unsigned gp = gx_blocks(h.n_nodes, 256 / gl, gcap);
-    if (gl == 8) hipLaunchKernelGGL((k_gxf_pull_g<8, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (gl == 4 && gb == 2) hipLaunchKernelGGL((k_gxf_pull_g<4, 2>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (gl == 4) hipLaunchKernelGGL((k_gxf_pull_g<4, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (gl == 2) hipLaunchKernelGGL((k_gxf_pull_g<2, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
-    else if (!f.fin) hipLaunchKernelGGL((k_gxf_pull_g<1, 1>), dim3(gp), dim3(256), 0, st, s, h, f, hop);
+#define GXF_PULL(G_, B_)                                                                            \
+    do {                                                                                            \
+        if (f.mixed) hipLaunchKernelGGL((k_gxf_pull_g<G_, B_, true>), dim3(gp), dim3(256), 0, st, s, h, f, hop);  \
+        else hipLaunchKernelGGL((k_gxf_pull_g<G_, B_, false>), dim3(gp), dim3(256), 0, st, s, h, f, hop);         \
+    } while (0)
+    if (gl == 8) GXF_PULL(8, 1);
+    else if (gl == 4 && gb == 2) GXF_PULL(4, 2);
+    else if (gl == 4) GXF_PULL(4, 1);
+    else if (gl == 2) GXF_PULL(2, 1);
+    else if (!f.fin) GXF_PULL(1, 1);
     else hipLaunchKernelGGL(k_gxf_pull, dim3(gp), dim3(256), 0, st, s, h, f, hop);
+#undef GXF_PULL
     return hipGetLastError();
 }
 
