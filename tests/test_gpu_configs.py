@@ -377,6 +377,84 @@ def test_cfg4_10m_range_sharded_matches_single_engine(gpu_ok):
 
 
 @pytest.mark.timeout(1200)
+def test_cfg4_10m_gossipsub_credits_range_sharded(gpu_ok):
+    """The router the cfg4 bench leg times (bench.py prop_engine/prop_config):
+    gossipsub over the synthesized mesh, P2/P3 credits on at delivery time,
+    per-pair first-receipt counts (no first-deliverer rows), BASELINE's
+    64-message batch on the 10M overlay.  Two RangeSharded shards holding the
+    single engine's state slices equal it bit for bit after the batch: arrival
+    hops, totals, every pair's state (the credited P2/P3 counters among them)
+    and every score."""
+    from gsx import shard
+
+    n, seed, world, T = 10_000_000, synth.SEED + 1, 2, 1
+    ov = synth.connect_some_overlay(n, d=6, seed=seed)
+    th = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                        accept_px_threshold=0, opportunistic_graft_threshold=0)
+
+    def params(e):
+        e.set_peer_params(synth.bench_peer_params())
+        e.set_topic_params(0, synth.spam_test_topic_params())
+        e.set_thresholds(th)
+        e.set_prop_tracking(False)
+
+    full = gsx.Engine(T)
+    params(full)
+    full.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    full.synthesize_state(
+        abi.SynthSpec(seed=seed, now_ns=pc.T0, fmd_max=1500.0, mmd_max=400.0, mfp_max=50.0, imd_max_sybil=100.0,
+                      p_in_mesh=0.5, graft_window_ns=2 * abi.HOUR, bp_max=5.0, p_disconnected=0.0, p_absent=0.0,
+                      expire_jitter_ns=4 * abi.SECOND, sybil_first_node=n))
+    full.set_app_scores(np.zeros(ov.n_pairs))
+    full.refresh(pc.T0 + S)
+    st0 = full.export_state()
+    ms = pc.messages(n, 64, 12)
+    cfg = abi.PropConfig(router=abi.GSX_ROUTER_GOSSIPSUB, topic=0, flood_publish=0, max_hops=40,
+                         hop_latency_ns=10 * abi.MILLISECOND, now_ns=pc.T0 + 2 * S,
+                         credit_scores=abi.GSX_CREDIT_NOW, randomsub_size=n, seed=synth.SEED)
+    out, hop, _ = full.propagate(ms, cfg, want_results=True)
+    st1, sc1 = full.export_state(), full.scores()
+    full.close()
+    E = ov.n_pairs
+
+    def part(st, a, b):
+        p = {f: (st[f].reshape(T, E)[:, a:b].reshape(-1).copy() if f in abi.RECORD_FIELDS else st[f][a:b].copy())
+             for f in abi.STATE_FIELDS}
+        p["last_refresh_ns"] = st["last_refresh_ns"]
+        return p
+
+    rank_lo = synth.shard_ranges(n, world)
+    engines = []
+    for k in range(world):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
+        sh = synth.shard_of(ov, lo, hi)
+        e = gsx.Engine(T)
+        params(e)
+        e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
+        e.import_state(part(st0, a, b))
+        e.set_app_scores(np.zeros(b - a))
+        engines.append((e, a, b))
+        del sh
+    del st0
+    res = shard.run_local(world, "cuda:0", lambda tp, e: shard.RangeSharded(e, rank_lo, tp).propagate(ms, cfg),
+                          [(e,) for e, _, _ in engines])
+    tot, want = res[0][1], out.as_dict()
+    for k in ("deliveries", "duplicates", "transmissions", "hops", "hop_deliveries", "graylisted"):
+        assert tot[k] == want[k], k
+    assert want["deliveries"] > 0.9 * len(ms) * n * 0.5
+    for k, (e, a, b) in enumerate(engines):
+        lo, hi = int(rank_lo[k]), int(rank_lo[k + 1])
+        h, _ = e.prop_results(len(ms))
+        assert np.array_equal(h, hop[:, lo:hi]), (k, np.argwhere(h != hop[:, lo:hi])[:5])
+        st, want_st = e.export_state(), part(st1, a, b)
+        for fld in abi.STATE_FIELDS:
+            assert np.array_equal(st[fld].view(np.uint8), want_st[fld].view(np.uint8)), (k, fld)
+        assert np.array_equal(e.scores().view(np.uint64), sc1[a:b].view(np.uint64)), k
+        e.close()
+
+
+@pytest.mark.timeout(1200)
 def test_cfg5_4m_adversarial_properties(gpu_ok):
     n = 4_000_000
     e = gsx.Engine(1)
