@@ -493,10 +493,14 @@ struct HbState {
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;
-    // per topic t, heads gx_hoff[t] .. gx_hoff[t + 1]: (first batch of a set in
-    // cache order, the set's word offset in the topic's set-word list)
-    const uint2* gx_heads;
-    const uint32_t* gx_hoff;
+    // every set's words in canonical order (topic, the set by its first batch
+    // in cache order, word): (first batch, word, topic, 0); gx_nsw of them
+    const uint4* gx_sw;
+    uint32_t gx_nsw;
+    // the flat word list of the advertised batches (GxBatch::woff): gx_fw
+    // words, gx_wb[f] the batch of word f
+    uint32_t gx_fw;
+    const uint32_t* gx_wb;
     // the exchange on a range shard (null unsharded): the IHAVEs this rank's
     // nodes sent over cross-shard pairs (sender side, [pair]: topic bits), and
     // per cross-shard pair (u -> v), receiver side: v answers u's IWANT

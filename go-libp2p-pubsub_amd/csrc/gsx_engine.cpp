@@ -222,17 +222,24 @@ struct gsx_engine {
     size_t px_cap = 0, pxlog_alloc = 0;
     uint64_t px_last = 0;  // the last round's connection candidates
     std::vector<uint64_t> h_sub;  // host copy of the joined topics per node
-    gsx::GxBatch* d_gx = nullptr;
-    uint32_t* d_gx_off = nullptr;
+    // the exchange's round tables, one device arena (d_gxa) filled by one copy
+    // from the pinned staging buffer: batches, offsets, word/set-word lists, prep + merge lists
+    uint8_t* d_gxa = nullptr;
+    size_t gxa_bytes = 0;
+    gsx::GxBatch* d_gx = nullptr;     // (views into d_gxa)
+    uint32_t* d_gx_off = nullptr;     // off[T + 1]: the batches of topic t
+    uint32_t* d_gx_wb = nullptr;      // the flat word list's batch per word
+    uint4* d_gx_sw = nullptr;         // every set's words (k_gx_node)
+    gsx::GxSetPrep* d_gx_sp = nullptr;  // the exchange's sets (k_gx_setprep)
+    gsx::GxSetMerge* d_gx_mg = nullptr;  // the same sets (k_gx_merge_sets)
     uint8_t* d_gx_got = nullptr;
     size_t gx_cap = 0;
-    uint2* d_gx_heads = nullptr;      // [gx_cap] per topic, the first batch of each set (k_gx_node)
-    gsx::GxSetPrep* d_gx_sp = nullptr;  // [gx_common_cap] the exchange's sets (k_gx_setprep)
-    gsx::GxSetMerge* d_gx_mg = nullptr;  // [gx_common_cap] the same sets (k_gx_merge_sets)
     void* h_gxstage = nullptr;        // pinned staging of the exchange's batch list (hb_end)
+    void* h_hbrb = nullptr;           // pinned: a round's counters, flags and per-set bytes (hb_finish)
+    size_t h_hbrb_bytes = 0;
     size_t h_gxstage_bytes = 0;
     uint64_t* d_gx_rhm = nullptr;     // [node]: the advertised batches whose row holds an uncommon message
-    uint8_t* d_gx_chg = nullptr;   // [set of the round]: a receipt changed its seen rows (k_gx_merge_sets)
+    uint8_t* d_gx_chg = nullptr;   // [set of the round]: a receipt changed its seen rows (k_gx_merge_sets; d_gx_got + gx_cap)
     uint64_t* d_gx_vin = nullptr;  // the round's inside-code bits of the mixed sets (GxRound::vin_host)
     size_t gx_vin_cap = 0;
     uint64_t* d_gx_common = nullptr;  // [set][64]: per message set of the exchange, the messages every node had
@@ -253,6 +260,8 @@ struct gsx_engine {
     size_t gxf_sets_cap = 0;
     uint32_t* h_gxf_cnt = nullptr;    // pinned: the hop count of a run's last launched hop
     void* h_gxf_stage = nullptr;      // pinned: the runs' set descriptors
+    hipEvent_t ev_gxf_stage = nullptr;  // recorded after the last copy out of h_gxf_stage
+    bool gxf_stage_queued = false;
     size_t h_gxf_stage_bytes = 0;
     uint32_t gxf_stamp = 0;           // stamps of the IWANT back counts (one per round) and of the hops
     uint32_t* d_gxf_hst = nullptr;    // range shards: [2][E] GxFwd::hstamp, hidx
@@ -873,9 +882,9 @@ void free_state(gsx_engine* e) {
     e->d_tr_acc = e->d_tr_hp = nullptr;
     {
         void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
-                       e->d_ihave_bits, e->d_prom_e, e->d_prom_any, e->d_prom_cnt, e->d_gx, e->d_gx_off,
+                       e->d_ihave_bits, e->d_prom_e, e->d_prom_any, e->d_prom_cnt, e->d_gxa,
                        e->d_gx_got, e->d_gx_nodes,
-                       e->d_gx_rhm, e->d_gx_common, e->d_gx_heads, e->d_gx_sp, e->d_gx_mg,
+                       e->d_gx_rhm, e->d_gx_common,
                        e->d_gxf_mask, e->d_gxf_list, e->d_gxf_cnt, e->d_gxf_bst, e->d_gxf_b0, e->d_gxf_b,
                        e->d_gxf_sets, e->d_gxf_fin, e->d_gxf_fout, e->d_gxf_fent, e->d_gxf_fend, e->d_gxf_hst, e->d_gxs_out, e->d_gxs_rans,
                        e->d_gxs_hidx, e->d_gxs_cnt, e->d_gxs_off, e->d_gxs_send};
@@ -916,6 +925,8 @@ void free_state(gsx_engine* e) {
         e->d_sub_cnt = nullptr;
         e->d_gsubs = nullptr;
         e->tgt_dlazy = -1;
+        e->d_gxa = nullptr;
+        e->gxa_bytes = 0;
         e->d_gx = nullptr;
         e->d_gx_off = nullptr;
         e->d_gx_got = nullptr;
@@ -924,9 +935,9 @@ void free_state(gsx_engine* e) {
         if (e->d_gx_vin) (void)hipFree(e->d_gx_vin);
         e->d_gx_vin = nullptr;
         e->gx_vin_cap = 0;
-        if (e->d_gx_chg) (void)hipFree(e->d_gx_chg);
-        e->d_gx_chg = nullptr;
-        e->d_gx_heads = nullptr;
+        e->d_gx_chg = nullptr;  // (d_gx_got's second half)
+        e->d_gx_wb = nullptr;
+        e->d_gx_sw = nullptr;
         e->d_gx_sp = nullptr;
         e->d_gx_mg = nullptr;
         e->gx_common_cap = 0;
@@ -1361,6 +1372,7 @@ int gsx_create(const gsx_config* cfg, gsx_engine** out) {
     if (hipSetDevice(e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev_start) != hipSuccess || hipEventCreate(&e->ev_stop) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_gxf_stage, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void**)&e->d_tp, sizeof(gsx::DevTopicParams) * GSX_MAX_TOPICS) != hipSuccess) {
         gsx_destroy(e);
         return GSX_EDEVICE;
@@ -1384,6 +1396,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->d_stage) (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
+    if (e->h_hbrb) (void)hipHostFree(e->h_hbrb);
     if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
     if (e->h_gxf_cnt) (void)hipHostFree(e->h_gxf_cnt);
     if (e->h_score) (void)hipHostFree(e->h_score);
@@ -1391,6 +1404,7 @@ int gsx_destroy(gsx_engine* e) {
     if (e->ev_start) (void)hipEventDestroy(e->ev_start);
     if (e->ev_stop) (void)hipEventDestroy(e->ev_stop);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
+    if (e->ev_gxf_stage) (void)hipEventDestroy(e->ev_gxf_stage);
     if (e->vc_stream) (void)hipStreamSynchronize(e->vc_stream);
     if (e->vc_go) (void)hipEventDestroy(e->vc_go);
     for (hipEvent_t ev : e->vc_done)
@@ -4062,6 +4076,10 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         if (int rc = dalloc(e, &e->d_gxf_sets, e->gxf_sets_cap)) return rc;
     }
     const size_t stage_bytes = sizeof(gsx::GxFwdSet) * 64;
+    // the staging buffer of the run before: its copy done (not the whole
+    // stream: the host keeps queueing the run behind the round's kernels)
+    if (e->gxf_stage_queued) HIPCHK(e, hipEventSynchronize(e->ev_gxf_stage));
+    e->gxf_stage_queued = false;
     if (e->h_gxf_stage_bytes < stage_bytes) {
         if (e->h_gxf_stage) (void)hipHostFree(e->h_gxf_stage);
         e->h_gxf_stage = nullptr;
@@ -4069,7 +4087,6 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         HIPCHK(e, hipHostMalloc(&e->h_gxf_stage, stage_bytes, hipHostMallocDefault));
         e->h_gxf_stage_bytes = stage_bytes;
     }
-    HIPCHK(e, hipStreamSynchronize(e->stream));  // the staging buffer of the run before
     auto* stage = static_cast<gsx::GxFwdSet*>(e->h_gxf_stage);
     gsx::GxFwd f{};
     f.sets = e->d_gxf_sets;
@@ -4113,6 +4130,8 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
     }
     f.rw = rw;
     HIPCHK(e, hipMemcpyAsync(e->d_gxf_sets, stage, sizeof(gsx::GxFwdSet) * f.n_sets, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipEventRecord(e->ev_gxf_stage, e->stream));
+    e->gxf_stage_queued = true;
     f.fmask[0] = e->d_gxf_mask;
     f.fmask[1] = e->d_gxf_mask + N;
     f.rmask = e->d_gxf_mask + 2 * N;
@@ -4348,29 +4367,25 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         }
         for (auto& g : gx) g.vin_off = 1 + fw + g.woff;  // (range shards: after the entry's rows)
     }
-    // per topic, the sets of its batches: each set's first batch in cache
-    // order and its words' offset (k_gx_node's receipts: a lane per set word
-    // walks the set's batches through `nxt`)
-    std::vector<uint32_t> hoff(e->T + 1, 0);
-    std::vector<uint2> heads;
+    // every set's words in canonical order, (its first batch in cache order,
+    // word, topic) (k_gx_node's receipts: a lane per set word walks the set's
+    // batches through `nxt`), and the flat word list's batch per word
+    std::vector<uint4> sw;
+    std::vector<uint32_t> wb;
     {
         std::vector<uint32_t> last(R.sets.size(), ~0u);
-        for (uint32_t t = 0; t < e->T; ++t) {
-            hoff[t] = (uint32_t)heads.size();
-            uint32_t sw = 0;
+        for (uint32_t t = 0; t < e->T; ++t)
             for (uint32_t g = off[t]; g < off[t + 1]; ++g) {
                 const size_t si = reinterpret_cast<size_t>(gx[g].got);
                 gx[g].nxt = ~0u;
                 if (last[si] == ~0u || gx[last[si]].topic != t) {
-                    heads.push_back(make_uint2(g, sw));
-                    sw += gx[g].n_words;
+                    for (uint32_t w = 0; w < gx[g].n_words; ++w) sw.push_back(make_uint4(g, w, t, 0u));
                 } else {
                     gx[last[si]].nxt = g;
                 }
                 last[si] = g;
             }
-        }
-        hoff[e->T] = (uint32_t)heads.size();
+        for (uint32_t g = 0; g < gx.size(); ++g) wb.insert(wb.end(), gx[g].n_words, g);  // (woff order)
     }
     dbg_host("gx sets");
     static const bool dbg = getenv("GSX_DBG_GX") != nullptr;
@@ -4388,38 +4403,21 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         for (const auto& g : gx) fprintf(stderr, " (t%u w%u s%u a%u)", g.topic, g.n_words, g.serial, g.avail);
         fprintf(stderr, "\n");
     }
-    if (gx.size() > e->gx_cap || !e->d_gx) {
-        if (e->d_gx) (void)hipFree(e->d_gx);
-        if (e->d_gx_off) (void)hipFree(e->d_gx_off);
+    if (std::max(gx.size(), R.sets.size()) > e->gx_cap || !e->d_gx_got) {  // (per set: got, chg)
         if (e->d_gx_got) (void)hipFree(e->d_gx_got);
-        e->d_gx = nullptr;
-        e->d_gx_off = nullptr;
         e->d_gx_got = nullptr;
         // (doubling, 64 at least: a free here waits for every queued kernel)
-        e->gx_cap = std::max<size_t>(std::max<size_t>(gx.size(), 2 * e->gx_cap), 64);
-        if (int rc = dalloc(e, &e->d_gx, e->gx_cap)) return rc;
-        if (int rc = dalloc(e, &e->d_gx_off, 2 * ((size_t)GSX_MAX_TOPICS + 1))) return rc;  // off, hoff
-        if (e->d_gx_heads) (void)hipFree(e->d_gx_heads);
-        e->d_gx_heads = nullptr;
-        if (int rc = dalloc(e, &e->d_gx_heads, e->gx_cap)) return rc;
-        if (int rc = dalloc(e, &e->d_gx_got, e->gx_cap)) return rc;
-        if (e->d_gx_chg) (void)hipFree(e->d_gx_chg);
-        e->d_gx_chg = nullptr;
-        if (int rc = dalloc(e, &e->d_gx_chg, e->gx_cap)) return rc;
+        e->gx_cap = std::max<size_t>(std::max<size_t>(std::max(gx.size(), R.sets.size()), 2 * e->gx_cap), 64);
+        if (int rc = dalloc(e, &e->d_gx_got, 2 * e->gx_cap)) return rc;  // got, then chg
+        e->d_gx_chg = e->d_gx_got + e->gx_cap;
     }
     // per set, the messages every node had seen as the exchange began (a
     // set wider than 64 words keeps none: its rows are filtered by emptiness)
     if (R.sets.size() > e->gx_common_cap || !e->d_gx_rhm) {
         if (e->d_gx_common) (void)hipFree(e->d_gx_common);
-        if (e->d_gx_sp) (void)hipFree(e->d_gx_sp);
-        if (e->d_gx_mg) (void)hipFree(e->d_gx_mg);
         e->d_gx_common = nullptr;
-        e->d_gx_sp = nullptr;
-        e->d_gx_mg = nullptr;
         e->gx_common_cap = std::max<size_t>(std::max<size_t>(R.sets.size(), 2 * e->gx_common_cap), 32);
         if (int rc = dalloc(e, &e->d_gx_common, 64 * e->gx_common_cap)) return rc;
-        if (int rc = dalloc(e, &e->d_gx_sp, e->gx_common_cap)) return rc;
-        if (int rc = dalloc(e, &e->d_gx_mg, e->gx_common_cap)) return rc;
         if (!e->d_gx_rhm)
             if (int rc = dalloc(e, &e->d_gx_rhm, N)) return rc;
     }
@@ -4468,16 +4466,16 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         g.common = common_of[si];
         g.got = e->d_gx_got + si;
     }
-    HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, e->gx_cap, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_gx_chg, 0, e->gx_cap, e->stream));
-    {  // the batch list, offsets and set heads through a pinned staging buffer:
-        // async copies, so the host keeps queueing instead of waiting for the
-        // kernels before them (the last round's copies drained at its end)
-        const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_hoff = 4 * hoff.size(),
-                     b_heads = sizeof(uint2) * heads.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size(),
+    HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, 2 * e->gx_cap, e->stream));  // got, chg
+    {  // the batch list, offsets, word and set-word lists, prep and merge lists: one pinned
+        // staging buffer, one async copy into the device arena d_gxa (the host
+        // keeps queueing; the last round's copy drained at its end)
+        const auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+        const size_t b_gx = sizeof(gsx::GxBatch) * gx.size(), b_off = 4 * off.size(), b_wb = 4 * wb.size(),
+                     b_sw = sizeof(uint4) * sw.size(), b_sp = sizeof(gsx::GxSetPrep) * sprep.size(),
                      b_mg = sizeof(gsx::GxSetMerge) * smerge.size();
-        const size_t a_sp = (b_gx + b_off + b_hoff + b_heads + 15) & ~(size_t)15;
-        const size_t a_mg = (a_sp + b_sp + 15) & ~(size_t)15;
+        const size_t a_off = al(b_gx), a_wb = al(a_off + b_off), a_sw = al(a_wb + b_wb), a_sp = al(a_sw + b_sw),
+                     a_mg = al(a_sp + b_sp);
         const size_t need = a_mg + b_mg;
         if (e->h_gxstage_bytes < need) {
             if (e->h_gxstage) (void)hipHostFree(e->h_gxstage);
@@ -4486,31 +4484,39 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
             HIPCHK(e, hipHostMalloc(&e->h_gxstage, 2 * need, hipHostMallocDefault));
             e->h_gxstage_bytes = 2 * need;
         }
+        if (e->gxa_bytes < need) {  // (a free here waits for every queued kernel)
+            if (e->d_gxa) (void)hipFree(e->d_gxa);
+            e->d_gxa = nullptr;
+            e->gxa_bytes = 0;
+            const size_t bytes = std::max<size_t>(2 * need, 64 << 10);
+            if (int rc = dalloc(e, &e->d_gxa, bytes)) return rc;
+            e->gxa_bytes = bytes;
+        }
         char* hs = static_cast<char*>(e->h_gxstage);
         std::memcpy(hs, gx.data(), b_gx);
-        std::memcpy(hs + b_gx, off.data(), b_off);
-        std::memcpy(hs + b_gx + b_off, hoff.data(), b_hoff);
-        if (b_heads) std::memcpy(hs + b_gx + b_off + b_hoff, heads.data(), b_heads);
-        HIPCHK(e, hipMemcpyAsync(e->d_gx, hs, b_gx, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_gx_off, hs + b_gx, b_off, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->d_gx_off + GSX_MAX_TOPICS + 1, hs + b_gx + b_off, b_hoff, hipMemcpyHostToDevice,
-                                 e->stream));
-        if (b_heads)
-            HIPCHK(e, hipMemcpyAsync(e->d_gx_heads, hs + b_gx + b_off + b_hoff, b_heads, hipMemcpyHostToDevice,
-                                     e->stream));
-        std::memcpy(hs + a_sp, sprep.data(), b_sp);
-        HIPCHK(e, hipMemcpyAsync(e->d_gx_sp, hs + a_sp, b_sp, hipMemcpyHostToDevice, e->stream));
-        std::memcpy(hs + a_mg, smerge.data(), b_mg);
-        HIPCHK(e, hipMemcpyAsync(e->d_gx_mg, hs + a_mg, b_mg, hipMemcpyHostToDevice, e->stream));
+        std::memcpy(hs + a_off, off.data(), b_off);
+        if (b_wb) std::memcpy(hs + a_wb, wb.data(), b_wb);
+        if (b_sw) std::memcpy(hs + a_sw, sw.data(), b_sw);
+        if (b_sp) std::memcpy(hs + a_sp, sprep.data(), b_sp);
+        if (b_mg) std::memcpy(hs + a_mg, smerge.data(), b_mg);
+        HIPCHK(e, hipMemcpyAsync(e->d_gxa, hs, need, hipMemcpyHostToDevice, e->stream));
+        e->d_gx = reinterpret_cast<gsx::GxBatch*>(e->d_gxa);
+        e->d_gx_off = reinterpret_cast<uint32_t*>(e->d_gxa + a_off);
+        e->d_gx_wb = reinterpret_cast<uint32_t*>(e->d_gxa + a_wb);
+        e->d_gx_sw = reinterpret_cast<uint4*>(e->d_gxa + a_sw);
+        e->d_gx_sp = reinterpret_cast<gsx::GxSetPrep*>(e->d_gxa + a_sp);
+        e->d_gx_mg = reinterpret_cast<gsx::GxSetMerge*>(e->d_gxa + a_mg);
         // receipt rows zeroed, full bytes, common words: every set that needs any, in one pass
         HIPCHK(e, gsx::launch_gx_setprep(e->d_gx_sp, (uint32_t)sprep.size(), (uint32_t)N, e->stream));
     }
-    R.h.gx_hoff = e->d_gx_off + GSX_MAX_TOPICS + 1;
-    R.h.gx_heads = e->d_gx_heads;
+    R.h.gx_sw = e->d_gx_sw;
+    R.h.gx_nsw = (uint32_t)sw.size();
+    R.h.gx_wb = e->d_gx_wb;
     R.h.gx = e->d_gx;
     R.h.gx_off = e->d_gx_off;
     R.n_gx = (uint32_t)gx.size();
     R.fw = gx.empty() ? 0u : gx.back().woff + gx.back().n_words;
+    R.h.gx_fw = R.fw;
     return GSX_OK;
 }
 
@@ -4560,18 +4566,37 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     auto& gx_sets = R.sets;
     auto& gx_x = R.xs;
     unsigned long long st[gsx::HB_STAT_WORDS];
-    HIPCHK(e, hipMemcpyAsync(st, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     uint32_t gflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> got(gx_sets.size(), 0), chg(gx_sets.size(), 1);
+    // the round's counters, flags and per-set bytes read back through one pinned
+    // buffer (async copies queued together; one drain)
+    const size_t nset = gx_run ? gx_sets.size() : 0;
+    const size_t rb_bytes = sizeof(st) + sizeof(gflag) + 2 * (gx_run ? e->gx_cap : 0);
+    if (e->h_hbrb_bytes < rb_bytes) {
+        if (e->h_hbrb) (void)hipHostFree(e->h_hbrb);  // (the last round's copies drained at its end)
+        e->h_hbrb = nullptr;
+        e->h_hbrb_bytes = 0;
+        HIPCHK(e, hipHostMalloc(&e->h_hbrb, 2 * rb_bytes, hipHostMallocDefault));
+        e->h_hbrb_bytes = 2 * rb_bytes;
+    }
+    uint8_t* rb = static_cast<uint8_t*>(e->h_hbrb);
+    HIPCHK(e, hipMemcpyAsync(rb, e->d_hbstats, sizeof(st), hipMemcpyDeviceToHost, e->stream));
     if (gx_run) {
-        HIPCHK(e, hipMemcpyAsync(gflag, e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
-        if (!got.empty() && !got_all)
-            HIPCHK(e, hipMemcpyAsync(got.data(), e->d_gx_got, got.size(), hipMemcpyDeviceToHost, e->stream));
-        if (!chg.empty())
-            HIPCHK(e, hipMemcpyAsync(chg.data(), e->d_gx_chg, chg.size(), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(rb + sizeof(st), e->d_gxflag, sizeof(gflag), hipMemcpyDeviceToHost, e->stream));
+        if (nset)  // got (this engine's: unless got_all) and chg, d_gx_got's two halves
+            HIPCHK(e, hipMemcpyAsync(rb + sizeof(st) + sizeof(gflag), e->d_gx_got, e->gx_cap + nset,
+                                     hipMemcpyDeviceToHost, e->stream));
     }
     dbg_host("gx queued");
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    std::memcpy(st, rb, sizeof(st));
+    if (gx_run) {
+        std::memcpy(gflag, rb + sizeof(st), sizeof(gflag));
+        if (nset) {
+            std::memcpy(got.data(), rb + sizeof(st) + sizeof(gflag), nset);
+            std::memcpy(chg.data(), rb + sizeof(st) + sizeof(gflag) + e->gx_cap, nset);
+        }
+    }
     if (got_all) std::memcpy(got.data(), got_all, got.size());
     for (auto& fr : R.scratch) seen_release(e, fr.first, fr.second);
     R.scratch.clear();

@@ -382,43 +382,31 @@ __device__ __forceinline__ uint32_t gx_excl(uint32_t x, uint32_t lane) {  // exc
 }
 
 // The flat word list of the advertised batches (GxBatch::woff; canonical
-// order: topics ascending, then cache order) is walked in rounds of 64 words
-// aligned to 64: in round i lane L holds word base + 64 i + L, so a batch
-// word always belongs to the same lane and a round's words are in canonical
-// order by lane.  Topic t's words are [gx[g0].woff, gx[g1 - 1].woff + W).
-struct GxRange {
-    uint32_t g0, g1, f0, f1, base;
-};
-__device__ __forceinline__ GxRange gx_range(const HbState& h, uint32_t t) {
-    GxRange R{h.gx_off[t], h.gx_off[t + 1], 0, 0, 0};
-    if (R.g0 < R.g1) {
-        R.f0 = h.gx[R.g0].woff;
-        R.f1 = h.gx[R.g1 - 1].woff + h.gx[R.g1 - 1].n_words;
-        R.base = R.f0 & ~63u;
-    }
-    return R;
-}
-// The lane's word of a round: its batch (advanced monotonically in g) and word,
-// false when the lane has none.
-__device__ __forceinline__ bool gx_at(const HbState& h, const GxRange& R, uint32_t f, uint32_t& g, uint32_t& w) {
-    if (f < R.f0 || f >= R.f1) return false;
-    while (h.gx[g].woff + h.gx[g].n_words <= f) ++g;
-    w = f - h.gx[g].woff;
-    return true;
+// order: topics ascending, then cache order) is walked in rounds of 64 words,
+// every topic at once: in round i lane L holds word 64 i + L (its batch from
+// gx_wb), so a batch word always belongs to the same lane and a round's words
+// are in canonical order by lane.  The lane's candidate word: its batch on a
+// topic of tb that u had not seen whole, within the subset row of a truncated
+// list; g: the word's batch.
+__device__ __forceinline__ uint64_t gx_fword(const HbState& h, uint64_t tb, uint32_t u, uint64_t q, uint32_t v,
+                                             uint64_t tr, uint32_t r, uint64_t nf, uint32_t f, uint32_t& g,
+                                             uint32_t& w) {
+    g = 0;
+    w = 0;
+    if (f >= h.gx_fw) return 0;
+    g = h.gx_wb[f];
+    if (gx_skip(nf, g)) return 0;
+    const GxBatch& b = h.gx[g];
+    if (!((tb >> b.topic) & 1)) return 0;
+    w = f - b.woff;
+    return gx_word(h, b, u, q, v, w, gx_subrow(h, tr, b.topic, r));
 }
 
 // |iwant| of pair q (every lane gets it): popcounts of the candidate words.
 __device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uint32_t u, uint64_t q, uint32_t v,
                                               uint64_t tr, uint32_t r, uint64_t nf, uint32_t lane) {
-    uint32_t c = 0;
-    for (; tb; tb &= tb - 1) {
-        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
-        const GxRange R = gx_range(h, t);
-        const uint64_t* sub = gx_subrow(h, tr, t, r);
-        uint32_t g = R.g0, w = 0;
-        for (uint32_t f = R.base + lane; f < R.f1; f += 64)
-            if (gx_at(h, R, f, g, w) && !gx_skip(nf, g)) c += (uint32_t)__popcll(gx_word(h, h.gx[g], u, q, v, w, sub));
-    }
+    uint32_t c = 0, g, w;
+    for (uint32_t f = lane; f < h.gx_fw; f += 64) c += (uint32_t)__popcll(gx_fword(h, tb, u, q, v, tr, r, nf, f, g, w));
     return gx_wsum(c);
 }
 
@@ -426,32 +414,26 @@ __device__ __forceinline__ uint32_t gx_wcount(const HbState& h, uint64_t tb, uin
 __device__ __forceinline__ void gx_wnth(const HbState& h, uint64_t tb, uint32_t u, uint64_t q, uint32_t v,
                                         uint64_t tr, uint32_t r, uint64_t nf, uint32_t lane, uint32_t j,
                                         uint32_t& pick_g, uint32_t& pick_k) {
-    for (; tb; tb &= tb - 1) {
-        const uint32_t t = (uint32_t)__builtin_ctzll(tb);
-        const GxRange R = gx_range(h, t);
-        const uint64_t* sub = gx_subrow(h, tr, t, r);
-        uint32_t g = R.g0, w = 0;
-        for (uint32_t f0 = R.base; f0 < R.f1; f0 += 64) {  // (uniform rounds)
-            uint64_t m = 0;
-            if (gx_at(h, R, f0 + lane, g, w) && !gx_skip(nf, g)) m = gx_word(h, h.gx[g], u, q, v, w, sub);
-            const uint32_t c = (uint32_t)__popcll(m);
-            const uint32_t e = gx_excl(c, lane);
-            const uint32_t tot = (uint32_t)__shfl((int)(e + c), 63, 64);
-            if (j >= tot) {
-                j -= tot;
-                continue;
-            }
-            const bool mine = e <= j && j < e + c;
-            uint32_t k = 0;
-            if (mine) {
-                for (uint32_t i = j - e; i; --i) m &= m - 1;
-                k = w * 64 + (uint32_t)__builtin_ctzll(m);
-            }
-            const int src = __ffsll((long long)__ballot(mine)) - 1;
-            pick_g = (uint32_t)__shfl((int)g, src, 64);
-            pick_k = (uint32_t)__shfl((int)k, src, 64);
-            return;
+    for (uint32_t f0 = 0; f0 < h.gx_fw; f0 += 64) {  // (uniform rounds)
+        uint32_t g, w;
+        uint64_t m = gx_fword(h, tb, u, q, v, tr, r, nf, f0 + lane, g, w);
+        const uint32_t c = (uint32_t)__popcll(m);
+        const uint32_t e = gx_excl(c, lane);
+        const uint32_t tot = (uint32_t)__shfl((int)(e + c), 63, 64);
+        if (j >= tot) {
+            j -= tot;
+            continue;
         }
+        const bool mine = e <= j && j < e + c;
+        uint32_t k = 0;
+        if (mine) {
+            for (uint32_t i = j - e; i; --i) m &= m - 1;
+            k = w * 64 + (uint32_t)__builtin_ctzll(m);
+        }
+        const int src = __ffsll((long long)__ballot(mine)) - 1;
+        pick_g = (uint32_t)__shfl((int)g, src, 64);
+        pick_k = (uint32_t)__shfl((int)k, src, 64);
+        return;
     }
 }
 
@@ -685,6 +667,7 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
 //  receipt rows (promises are only added in pass 1).
 template <bool MIX>
 __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
+    __shared__ uint32_t kc[3][64];  // per topic (GSX_MAX_TOPICS): k1, k2, k4 of the pair being received
     const uint32_t lane = threadIdx.x;
     const uint32_t S = h.prom_slots;
     const DevGossipParams& gp = h.gp;
@@ -745,69 +728,65 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 const uint64_t tr = h.ihave_tr[q];
                 const uint32_t n = gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
                 if (kk == n) {
-                    for (uint64_t tm = tb; tm; tm &= tm - 1) {
-                        const uint32_t t = (uint32_t)__builtin_ctzll(tm);
+                    // a lane per (message set, word) of every set on the topics of tb
+                    // (h.gx_sw, canonical order): it walks the set's batches in cache
+                    // order (the one order its receipt word sees); different sets touch
+                    // different receipt rows, so the topics run together; the per-topic
+                    // counts meet in LDS, credited once per topic by the topic's lane
+                    kc[0][lane] = kc[1][lane] = kc[2][lane] = 0;
+                    __syncthreads();
+                    for (uint32_t f = lane; f < h.gx_nsw; f += 64) {
+                        const uint4 sw = h.gx_sw[f];  // (first batch, word, topic)
+                        const uint32_t t = sw.z, w = sw.y;
+                        if (!((tb >> t) & 1)) continue;
                         const uint64_t* sub = gx_subrow(h, tr, t, r);
                         uint32_t k1 = 0, k2 = 0, k4 = 0;
-                        // a lane per (message set, word) of the topic: it walks the
-                        // set's batches in cache order (the one order its receipt word
-                        // sees); different sets touch different receipt rows
-                        const uint32_t h0 = h.gx_hoff[t], h1 = h.gx_hoff[t + 1];
-                        const uint32_t total = h0 < h1 ? h.gx_heads[h1 - 1].y + h.gx[h.gx_heads[h1 - 1].x].n_words : 0;
-                        uint32_t hi = h0;
-                        for (uint32_t f = lane; f < total; f += 64) {
-                          while (hi + 1 < h1 && h.gx_heads[hi + 1].y <= f) ++hi;
-                          const uint32_t w = f - h.gx_heads[hi].y;
-                          for (uint32_t gi = h.gx_heads[hi].x; gi != GX_END; gi = h.gx[gi].nxt) {
+                        for (uint32_t gi = sw.x; gi != GX_END; gi = h.gx[gi].nxt) {
                             if (gx_skip(nf, gi)) continue;
                             const GxBatch& b = h.gx[gi];
                             // no longer in v's cache; or GetForPeer's count above GossipRetransmission
                             if (!b.avail || gp.retransmission < 1) continue;
                             const uint32_t W = b.n_words;
-                            bool got = false;
-                            {
-                                const uint64_t m = gx_word(h, b, u, (uint64_t)q, v, w, sub);
-                                if (!m) continue;
-                                uint64_t* xw = b.x + (size_t)u * W + w;
-                                const uint64_t x0 = *xw;
-                                *xw = x0 | m;
-                                served += (uint64_t)__popcll(m);
-                                uint64_t acc1 = 0;
-                                for (uint64_t z = m & ~x0; z; z &= z - 1) {
-                                    const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
-                                    if (val == VAL_ACCEPT) {
-                                        ++delivered;
-                                        ++k1;
-                                        acc1 |= z & (~z + 1);
-                                        got = true;
-                                    } else {
-                                        ++rejected;
-                                        if (val == VAL_REJECT) ++k4;
-                                    }
-                                }
-                                for (uint64_t z = m & x0; z; z &= z - 1) {  // DuplicateMessage
-                                    const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
-                                    ++dups;
-                                    if (val == VAL_ACCEPT) ++k2;
-                                    else if (val == VAL_REJECT) ++k4;
-                                }
-                                if (acc1 && h.gxb_st0) {  // the back-sends of these first receipts (GxFwd)
-                                    const uint64_t bk = acc1 & ~origin_word(b.src, b.n_msgs, v, w);
-                                    if (bk) {
-                                        const uint64_t bin = gx_in_at_sender<MIX>(h, b, (uint64_t)q, v, w, bk);
-                                        atomicAdd(&h.gxb_cnt0[(size_t)b.grp * h.n_pairs + q],
-                                                  (uint32_t)__popcll(bin) | (uint32_t)__popcll(bk & ~bin) << 16);
-                                    }  // (cleared before the walk)
+                            const uint64_t m = gx_word(h, b, u, (uint64_t)q, v, w, sub);
+                            if (!m) continue;
+                            uint64_t* xw = b.x + (size_t)u * W + w;
+                            const uint64_t x0 = *xw;
+                            *xw = x0 | m;
+                            served += (uint64_t)__popcll(m);
+                            uint64_t acc1 = 0;
+                            for (uint64_t z = m & ~x0; z; z &= z - 1) {
+                                const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
+                                if (val == VAL_ACCEPT) {
+                                    ++delivered;
+                                    ++k1;
+                                    acc1 |= z & (~z + 1);
+                                } else {
+                                    ++rejected;
+                                    if (val == VAL_REJECT) ++k4;
                                 }
                             }
-                            if (got) *b.got = 1;
-                          }
+                            for (uint64_t z = m & x0; z; z &= z - 1) {  // DuplicateMessage
+                                const uint32_t val = b.val[w * 64 + (uint32_t)__builtin_ctzll(z)];
+                                ++dups;
+                                if (val == VAL_ACCEPT) ++k2;
+                                else if (val == VAL_REJECT) ++k4;
+                            }
+                            if (acc1 && h.gxb_st0) {  // the back-sends of these first receipts (GxFwd)
+                                const uint64_t bk = acc1 & ~origin_word(b.src, b.n_msgs, v, w);
+                                if (bk) {
+                                    const uint64_t bin = gx_in_at_sender<MIX>(h, b, (uint64_t)q, v, w, bk);
+                                    atomicAdd(&h.gxb_cnt0[(size_t)b.grp * h.n_pairs + q],
+                                              (uint32_t)__popcll(bin) | (uint32_t)__popcll(bk & ~bin) << 16);
+                                }  // (cleared before the walk)
+                            }
+                            if (acc1) *b.got = 1;
                         }
-                        k1 = gx_wsum(k1);
-                        k2 = gx_wsum(k2);
-                        k4 = gx_wsum(k4);
-                        if (lane == 0) gx_credit(s, q, t, k1, k2, k4);
+                        if (k1) atomicAdd(&kc[0][t], k1);
+                        if (k2) atomicAdd(&kc[1][t], k2);
+                        if (k4) atomicAdd(&kc[2][t], k4);
                     }
+                    __syncthreads();
+                    if ((tb >> lane) & 1) gx_credit(s, q, lane, kc[0][lane], kc[1][lane], kc[2][lane]);
                 } else if (lane == 0) {
                     gx_receive_sampled<MIX>(s, h, u, q, r, tb, kk, n, served, delivered, rejected, dups);
                 }
@@ -1324,13 +1303,12 @@ __device__ __forceinline__ uint64_t gxf_gor(uint64_t x) {  // OR over the group 
 // 2, per-copy codes: vc_inside); a separate instance, so the common one keeps
 // its registers (the per-copy path costs ~23 VGPRs, a wave per SIMD).
 template <int G, int B, bool MIX>
-__global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd f, uint32_t hop) {
+__device__ __forceinline__ void gxf_pull_run(DevState& s, HbState& h, GxFwd& f, uint32_t hop, bool dense) {
     const uint32_t p = (hop - 1) & 1, pw = hop & 1;
     const uint32_t seq_cur = f.seq + hop;
     const uint32_t S_ = h.prom_slots;
     const uint32_t lc = threadIdx.x % G;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
-    const bool dense = gxf_dense(f, hop, h.n_nodes);
     const bool fe = gxf_fent_ready(f, hop, h.n_nodes);
     const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G; i < nr; i += gridDim.x * (256u / G)) {
@@ -1522,6 +1500,15 @@ __global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd
     unsigned long long vv[3] = {c_new, c_dup, c_gray};
     const uint32_t slot[3] = {HB_FWD_DELIVERED, HB_FWD_DUPLICATES, HB_FWD_GRAYLISTED};
     block_count<3>(vv, h.stats, slot);
+}
+// GS lanes per receiver on a sparse hop (few receivers: a row spread over
+// more lanes), GD on a dense one (every node: more receivers per wave; measured
+// on the heartbeat's forwarding, 1M nodes: GD = 2 pulls a dense hop ~8 % faster
+// than 4, GS = 4 a sparse one faster than 2).  The hop's kind is uniform.
+template <int GS, int GD, int B, bool MIX>
+__global__ __launch_bounds__(256) void k_gxf_pull_g(DevState s, HbState h, GxFwd f, uint32_t hop) {
+    if (gxf_dense(f, hop, h.n_nodes)) gxf_pull_run<GD, B, MIX>(s, h, f, hop, true);
+    else gxf_pull_run<GS, B, MIX>(s, h, f, hop, false);
 }
 
 // ---- the exchange across range shards (gsx_gx_*; gsx.h) -------------------------
@@ -1742,6 +1729,10 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
         const char* v = getenv("GSX_GXF_G");
         return v ? atoi(v) : 4;
     }();
+    static const int gd = [] {  // GSX_GXF_GD = 4: G = 4 on dense hops too (default 2 there)
+        const char* v = getenv("GSX_GXF_GD");
+        return v ? atoi(v) : 2;
+    }();
     static const int gb = [] {  // GSX_GXF_B = 2: filter batches of two rounds (G = 4)
         const char* v = getenv("GSX_GXF_B");
         return v ? atoi(v) : 1;
@@ -1751,16 +1742,17 @@ hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, u
         return v && atoi(v) > 0 ? (unsigned)atoi(v) : 2048u;
     }();
     const unsigned gp = gx_blocks(h.n_nodes, 256 / gl, gcap);
-#define GXF_PULL(G_, B_)                                                                            \
-    do {                                                                                            \
-        if (f.mixed) hipLaunchKernelGGL((k_gxf_pull_g<G_, B_, true>), dim3(gp), dim3(256), 0, st, s, h, f, hop);  \
-        else hipLaunchKernelGGL((k_gxf_pull_g<G_, B_, false>), dim3(gp), dim3(256), 0, st, s, h, f, hop);         \
+#define GXF_PULL(G_, GD_, B_)                                                                                 \
+    do {                                                                                                      \
+        if (f.mixed) hipLaunchKernelGGL((k_gxf_pull_g<G_, GD_, B_, true>), dim3(gp), dim3(256), 0, st, s, h, f, hop); \
+        else hipLaunchKernelGGL((k_gxf_pull_g<G_, GD_, B_, false>), dim3(gp), dim3(256), 0, st, s, h, f, hop);        \
     } while (0)
-    if (gl == 8) GXF_PULL(8, 1);
-    else if (gl == 4 && gb == 2) GXF_PULL(4, 2);
-    else if (gl == 4) GXF_PULL(4, 1);
-    else if (gl == 2) GXF_PULL(2, 1);
-    else if (!f.fin) GXF_PULL(1, 1);
+    if (gl == 8) GXF_PULL(8, 8, 1);
+    else if (gl == 4 && gb == 2) GXF_PULL(4, 4, 2);
+    else if (gl == 4 && gd == 4) GXF_PULL(4, 4, 1);
+    else if (gl == 4) GXF_PULL(4, 2, 1);
+    else if (gl == 2) GXF_PULL(2, 2, 1);
+    else if (!f.fin) GXF_PULL(1, 1, 1);
     else hipLaunchKernelGGL(k_gxf_pull, dim3(gp), dim3(256), 0, st, s, h, f, hop);
 #undef GXF_PULL
     return hipGetLastError();
