@@ -493,8 +493,41 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
 }
 
 constexpr uint32_t GX_END = 0xFFFFFFFFu;  // GxBatch::nxt: the set's last batch
-constexpr uint32_t GX_ML = 64;           // words a receiver's lane handles itself (else: a wave, GX_HEAVY)
+constexpr uint32_t GX_MW = 128;  // words of unseen batches a receiver's lane walks itself (else: a wave, GX_HEAVY)
 constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
+
+// v's cache row of batch b (pair q = (u -> v)): a local sender's; on a range
+// shard a remote one's from the rows its rank sent; null when it sent none.
+__device__ __forceinline__ const uint64_t* gx_memrow(const HbState& h, const GxBatch& b, uint64_t q, uint32_t v) {
+    if (h.gxs_hidx && (h.rev[q] & HALO)) {
+        const uint32_t k = h.gxs_hidx[q];
+        return k == NO_PAIR ? nullptr : h.gxs_rows + (size_t)k * gxs_ew(h) + 1 + b.woff;
+    }
+    return b.mem + (size_t)(v - h.node_lo) * b.n_words;
+}
+// The candidate words of pair q in canonical order (the batches of cb on the
+// topics of tb, words ascending): f(batch, word, v's cache word & ~u's, within
+// the subset row of a truncated list) for each nonzero one; stops when f
+// returns false.  (mem has no bit past n_msgs: no validity mask.)
+template <typename F>
+__device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t tb, uint32_t uu, uint64_t q,
+                                         uint32_t v, uint64_t tr, uint32_t r, F&& f) {
+    for (; cb; cb &= cb - 1) {
+        const uint32_t g = (uint32_t)__builtin_ctzll(cb);
+        const GxBatch& b = h.gx[g];
+        if (!((tb >> b.topic) & 1)) continue;
+        const uint64_t* mrow = gx_memrow(h, b, q, v);
+        if (!mrow) return;  // (a remote sender with no uncommon rows: none in any batch)
+        const uint32_t W = b.n_words;
+        const uint64_t* arow = b.all + (size_t)uu * W;
+        const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
+        for (uint32_t w = 0; w < W; ++w) {
+            uint64_t c = mrow[w] & ~arow[w];
+            if (sub) c &= sub[b.row_off + w];
+            if (c && !f(g, w, c)) return;
+        }
+    }
+}
 
 // Pass 1: handleIHave (:615-679) for the one IHAVE RPC each sender v sent
 // (every topic): the score / MaxIHaveMessages / iasked gates, |iwant| from
@@ -503,20 +536,18 @@ constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_
 // touches is per pair (the IHAVE counters, the request, the promise of q), so
 // the pairs of a node are independent.  A wave takes 64 consecutive nodes:
 //  - a lane per node finds the advertised batches its node has not seen whole
-//    (only they can hold a candidate) and the words of them where the node
-//    lacks a message (its miss list, in LDS); a node with none asks for
-//    nothing; one with more than GX_ML such words is heavy (k_gx_node's wave
-//    runs its pass 1: GX_HEAVY);
+//    (only they can hold a candidate); a node with none asks for nothing; one
+//    whose unseen batches hold more than GX_MW words is heavy (k_gx_node's
+//    wave runs its pass 1: GX_HEAVY);
 //  - the lanes then take the tile's pairs in order, a lane per pair (the
-//    per-pair arrays are read coalesced), each against its node's miss list;
+//    per-pair arrays are read coalesced), each walking the words of its node's
+//    unseen batches (u's row and v's cache row side by side, no LDS list: the
+//    kernel keeps 6 waves per SIMD);
 //  - a node with a heavy walk or an asked pair is listed for k_gx_node (pass 2).
-__global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
-    // miss lists [entry][node of the tile] (batch << 6 | word, W <= 64 words
-    // per batch here); the bits are re-read from u's row (cached) per use
-    __shared__ uint16_t ml_gw[GX_ML][64];
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_gx_ask(DevState s, HbState h) {
     __shared__ int64_t rp[65];      // row_ptr of the tile's nodes
     __shared__ uint64_t nfs[64];    // per node: the unseen-batch mask
-    __shared__ uint32_t nmls[64];   // per node: miss-list length | GX_HEAVY
+    __shared__ uint32_t nmls[64];   // per node: GX_HEAVY
     __shared__ uint32_t lst[64];    // per node: listed for k_gx_node
     const uint32_t lane = threadIdx.x;
     uint64_t ignored = 0, iw_msgs = 0, iw_ids = 0;
@@ -524,35 +555,22 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
     const uint32_t n_gx = h.gx_off[s.n_topics];
     for (uint32_t tile = blockIdx.x * 64u; tile < h.n_nodes; tile += gridDim.x * 64u) {
         const uint32_t u = tile + lane;
-        {  // ---- lane per node: unseen batches and the miss list
+        {  // ---- lane per node: unseen batches, their words
             uint64_t nf = 0;
-            uint32_t nml = 0;
+            uint32_t nw = 0;
             bool heavy = n_gx > 64;
             if (u < h.n_nodes) {
                 nf = gx_unseen(h, n_gx, u);
-                for (uint64_t m = heavy ? 0 : nf; m && !heavy; m &= m - 1) {
-                    const uint32_t g = (uint32_t)__builtin_ctzll(m);
-                    const GxBatch& b = h.gx[g];
-                    if (b.n_words > 64) {
+                for (uint64_t m = heavy ? 0 : nf; m; m &= m - 1) {
+                    nw += h.gx[__builtin_ctzll(m)].n_words;
+                    if (nw > GX_MW) {
                         heavy = true;
                         break;
-                    }
-                    for (uint32_t w = 0; w < b.n_words; ++w) {
-                        const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
-                        const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
-                        const uint64_t miss = ~b.all[(size_t)u * b.n_words + w] & valid;
-                        if (!miss) continue;
-                        if (nml == GX_ML) {
-                            heavy = true;
-                            break;
-                        }
-                        ml_gw[nml][lane] = (uint16_t)(g << 6 | w);
-                        ++nml;
                     }
                 }
             }
             nfs[lane] = nf;
-            nmls[lane] = nml | (heavy ? GX_HEAVY : 0u);
+            nmls[lane] = heavy ? GX_HEAVY : 0u;
             lst[lane] = 0;
             rp[lane] = h.row_ptr[u < h.n_nodes ? u : h.n_nodes];
             if (lane == 0) rp[64] = h.row_ptr[tile + 64 < h.n_nodes ? tile + 64 : h.n_nodes];
@@ -574,7 +592,6 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
                 lst[k] = 1;
                 continue;
             }
-            const uint32_t nml = nm;
             const uint32_t uu = tile + k;
             const uint64_t tb = tall & (h.sub ? h.sub[uu] : ~0ull);  // joined topics only (:638-641)
             const uint32_t v = (uint32_t)h.col[q];
@@ -586,16 +603,10 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             // |iwant|: v's cache words where u lacks something (topics of the RPC,
             // the subset row of a truncated list)
             uint32_t n = 0;
-            for (uint32_t i = 0; i < nml; ++i) {
-                const uint32_t gw = ml_gw[i][k], g = gw >> 6, w = gw & 63u;
-                if (!((cb >> g) & 1)) continue;
-                const GxBatch& b = h.gx[g];
-                if (!((tb >> b.topic) & 1)) continue;
-                uint64_t c = gx_mem(h, b, (uint64_t)q, v, w) & ~b.all[(size_t)uu * b.n_words + w];
-                const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
-                if (sub) c &= sub[b.row_off + w];
+            gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, [&](uint32_t, uint32_t, uint64_t c) {
                 n += (uint32_t)__popcll(c);
-            }
+                return true;
+            });
             if (n == 0) continue;  // :652-654
             const uint32_t budget = (uint32_t)((int64_t)h.gp.max_ihave - (int64_t)h.iasked[q]);
             const uint32_t kk = n < budget ? n : budget;
@@ -603,24 +614,17 @@ __global__ __launch_bounds__(64) void k_gx_ask(DevState s, HbState h) {
             if (kk == n) {  // the element at Int31n(kk) of all of them, canonical order
                 Rng g = gx_iwant_rng(h, uu, v);
                 uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-                for (uint32_t i = 0; i < nml; ++i) {
-                    const uint32_t gw = ml_gw[i][k], gi = gw >> 6, w = gw & 63u;
-                    if (!((cb >> gi) & 1)) continue;
-                    const GxBatch& b = h.gx[gi];
-                    if (!((tb >> b.topic) & 1)) continue;
-                    uint64_t c = gx_mem(h, b, (uint64_t)q, v, w) & ~b.all[(size_t)uu * b.n_words + w];
-                    const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
-                    if (sub) c &= sub[b.row_off + w];
+                gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, [&](uint32_t gi, uint32_t w, uint64_t c) {
                     const uint32_t pc = (uint32_t)__popcll(c);
                     if (j >= pc) {
                         j -= pc;
-                        continue;
+                        return true;
                     }
                     for (; j; --j) c &= c - 1;
                     pick_g = gi;
                     pick_k = w * 64 + (uint32_t)__builtin_ctzll(c);
-                    break;
-                }
+                    return false;
+                });
             } else {
                 gx_pick_sampled(h, tb, uu, v, q, r, n, kk, pick_g, pick_k);
             }
