@@ -24,13 +24,16 @@ run() {  # run NAME SECONDS COUNTER CMD...
     echo "=== $name $c rc=$rc"
     if [ $rc -ne 0 ]; then tail -n 5 "$O/${name}_$c.log"; exit $rc; fi
 }
+# PMC_SECTIONS="calib hb": only those runs (tools/pmc_bytes.py then merges them
+# into the summary named by PMC_MERGE, e.g. profiles/pmc_r05.json)
+want() { [ -z "${PMC_SECTIONS:-}" ] || [[ " $PMC_SECTIONS " == *" $1 "* ]]; }
 for C in FETCH_SIZE WRITE_SIZE; do
-    run calib 120 $C ./tools/microbench/pmc_calib
-    run head 300 $C python3 bench.py --steps 5 --warmup 1 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
+    want calib && run calib 120 $C ./tools/microbench/pmc_calib
+    want head && run head 300 $C python3 bench.py --steps 5 --warmup 1 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
         --prop-peers 0 --hb-steps 0 --adv-peers 0
-    run p1024 200 $C python3 tools/prop_profile.py --msgs 1024 --batches 3 --warmup 2
-    run p64 200 $C python3 tools/prop_profile.py --msgs 64 --batches 3 --warmup 2
-    run hb 300 $C python3 bench.py --steps 1 --warmup 0 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
+    want p1024 && run p1024 200 $C python3 tools/prop_profile.py --msgs 1024 --batches 3 --warmup 2
+    want p64 && run p64 200 $C python3 tools/prop_profile.py --msgs 64 --batches 3 --warmup 2
+    want hb && run hb 300 $C python3 bench.py --steps 1 --warmup 0 --no-cpu --no-dropin --no-single-observer --prop-msgs 0 \
         --prop-peers 0 --adv-peers 0 --hb-steps 5
 done
-python3 tools/pmc_bytes.py "$O" "n=1000000,T=8,d=6,E=11999954" > "$O/summary.json" && cat "$O/summary.json"
+python3 tools/pmc_bytes.py "$O" "n=1000000,T=8,d=6,E=11999954" ${PMC_MERGE:-} > "$O/summary.json" && cat "$O/summary.json"
