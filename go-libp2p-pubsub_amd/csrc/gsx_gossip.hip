@@ -985,11 +985,16 @@ __device__ __forceinline__ uint32_t gxf_fout_bits(const DevState& s, const HbSta
         if (gxf_elig(s, h, r, v, f.slot_topic[ts])) b |= 1u << ts;
     return b;
 }
-// Hop 0 and the run's forwarding slots (fout) of every node's row, node-parallel.
+// The run's forwarding slots (fout) of every node's row, node-parallel; hop 0
+// over the nodes k_gx_ask listed (only they received in the exchange: every
+// other node's receipt rows are zero).
 __global__ __launch_bounds__(256) void k_gxf_init(DevState s, HbState h, GxFwd f, uint32_t n, uint32_t n_src_total,
                                                   uint32_t node_lo) {
-    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u) {
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u)
         for (int64_t r = h.row_ptr[u]; r < h.row_ptr[u + 1]; ++r) f.fout[r] = (uint8_t)gxf_fout_bits(s, h, f, (uint64_t)r, u);
+    const uint32_t n_list = h.gx_err[6];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_list; i += gridDim.x * 256u) {
+        const uint32_t u = h.gx_nodes[i] & ~GX_HEAVY;
         uint64_t m = 0;
         for (uint32_t si = 0; si < f.n_sets; ++si) {
             const GxFwdSet& S = f.sets[si];
