@@ -488,6 +488,8 @@ struct HbState {
     const GxSub* gsubs;    // [topic]: the exchange's view of every topic's rows
     uint32_t* gx_err;      // [8]: 0 = a GxSub bound broken (an internal error), 6 = nodes listed in gx_nodes
     uint32_t* gx_nodes;    // [node]: the nodes with an asked pair (k_gx_ask -> k_gx_receive)
+    uint64_t* gx_touch;    // [node bit]: the nodes whose receipt rows this round may hold a bit (listed by
+                           // k_gx_ask, or a forwarding receiver): k_gx_merge_sets reads only their rows
     uint8_t* gx_mark;      // [pair]: answered pairs (their records took the receipts' credits; re-scored after)
     const uint64_t* gx_rhm;  // [node]: bit g = its row of advertised batch g holds a not-everywhere message
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
@@ -623,6 +625,8 @@ struct GxSetMerge {
     uint64_t plane;
     uint32_t n_planes, code;
     uint8_t* chg;              // set to 1 when some receipt changes the set's seen rows
+    const uint64_t* touch;     // [node bit]: nodes whose rows may hold a receipt (null: every node); the
+                               // others' receipt rows, counts and digests are zero already (k_gx_setprep)
 };
 hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // The forwarding of the recovered messages (gsx.h (D): a delivered message is

@@ -3519,6 +3519,8 @@ namespace {
 // The gossip exchange's per-pair state, allocated when it is first enabled:
 // IHAVE counters, the promises (prom_slots per pair), the receiver-side IHAVE
 // topic bits (and truncated ones), the error / occupancy words.
+// The round's touch bits (HbState::gx_touch) after the 8 flag words of d_gxflag.
+size_t gx_touch_words(const gsx_engine* e) { return ((size_t)e->n_nodes + 63) / 64; }
 int gx_alloc(gsx_engine* e) {
     if (e->d_prom_e) return GSX_OK;
     int rc = 0;
@@ -3527,7 +3529,8 @@ int gx_alloc(gsx_engine* e) {
     if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
         (rc = dalloc(e, &e->d_prom_h, E * S)) || (rc = dalloc(e, &e->d_prom_e, E * S)) ||
         (rc = dalloc(e, &e->d_prom_any, E)) || (rc = dalloc(e, &e->d_prom_cnt, 1)) ||
-        (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) || (rc = dalloc(e, &e->d_gxflag, 8)) ||
+        (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) ||
+        (rc = dalloc(e, &e->d_gxflag, 8 + 2 * gx_touch_words(e))) ||
         (rc = dalloc(e, &e->d_gx_nodes, std::max<size_t>(e->n_nodes, 1))) ||
         (rc = dalloc(e, &e->d_sub_cnt, std::max<size_t>(e->T, 1))) ||
         (rc = dalloc(e, &e->d_gsubs, std::max<size_t>(e->T, 1))))
@@ -3773,7 +3776,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         // the IHAVE topic bits of the last round (one bulk clear: cheaper than the
         // exchange clearing the pairs it read one by one)
         HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32 + 8 * gx_touch_words(e), e->stream));  // flags, touch bits
+        h.gx_touch = reinterpret_cast<uint64_t*>(e->d_gxflag + 8);
         e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
         if (e->sharded()) {  // the IHAVEs of cross-shard pairs, sender side (gsx_gx_pack_ihave)
             const size_t E = std::max<size_t>(e->E, 1);
@@ -4458,7 +4462,8 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         const size_t W = ms->n_words;
         smerge[i] = gsx::GxSetMerge{ms->d_all, R.xs[i], ms->d_acc, ms->d_dg, R.xs[i] + W * N,
                                     reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs,
-                                    ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i], e->d_gx_chg + i};
+                                    ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i], e->d_gx_chg + i,
+                                    R.h.gx_touch};
     }
     if (e->sharded()) HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
     for (auto& g : gx) {

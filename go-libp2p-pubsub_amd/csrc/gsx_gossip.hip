@@ -639,6 +639,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             const bool take = u < h.n_nodes && lst[lane];
             const uint32_t k = wave_append(&h.gx_err[6], take);
             if (take) h.gx_nodes[k] = u | (nmls[lane] & GX_HEAVY);
+            const uint64_t tm = __ballot(take);  // (a tile is one word of the touch bits)
+            if (lane == 0 && tm && h.gx_touch) atomicOr(reinterpret_cast<unsigned long long*>(&h.gx_touch[tile >> 6]), tm);
         }
         __syncthreads();  // (the tile's LDS is rewritten next)
     }
@@ -891,6 +893,10 @@ __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict_
             }
         }
         if (in && S.full) S.full[v] = c == S.n_msgs;
+        if (in && S.x) {  // the recovered rows' summary beside them (k_gx_merge_sets writes touched nodes only)
+            S.x[(size_t)W * n + v] = 0;
+            reinterpret_cast<uint32_t*>(S.x + (size_t)W * n + n)[v] = 0;
+        }
     }
     __syncthreads();
     if (and_words && threadIdx.x < W) atomicAnd(reinterpret_cast<unsigned long long*>(&S.common[threadIdx.x]), sw[threadIdx.x]);
@@ -898,12 +904,14 @@ __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict_
 
 // Thread per node v of set blockIdx.y: merge its W receipt words and sum the
 // recovered row's count and digest as k_mc_summary does (a full word adds
-// its word digest, else the id digests of its bits: the same u64 sum).
+// its word digest, else the id digests of its bits: the same u64 sum).  Only
+// the round's touched nodes (GxSetMerge::touch): every other row is zero.
 __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restrict__ sets, uint32_t n) {
     const GxSetMerge S = sets[blockIdx.y];
     const uint32_t W = S.n_words;
     const uint64_t* word_dig = S.msg_dig + (size_t)W * 64;
     for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
+        if (S.touch && !((S.touch[v >> 6] >> (v & 63)) & 1)) continue;  // (rows, count, digest: zero)
         uint32_t L = 0;
         uint64_t d = 0;
         for (uint32_t w = 0; w < W; ++w) {
@@ -1270,6 +1278,7 @@ __global__ __launch_bounds__(256) void k_gxf_pull(DevState s, HbState h, GxFwd f
         f.fmask[pw][x] = newsets;
         f.flist[pw][slot_x] = x;
         atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
+        if (h.gx_touch) atomicOr(reinterpret_cast<unsigned long long*>(&h.gx_touch[x >> 6]), 1ull << (x & 63));
         // fulfillPromise (:119-126): x's promises of messages it now has
         for (uint64_t z = (uint64_t)r0 * S_; z < (uint64_t)r1 * S_; ++z) {
             if (z % S_ == 0 && !h.prom_any[z / S_]) {  // no promise on this pair
@@ -1488,6 +1497,7 @@ __device__ __forceinline__ void gxf_pull_run(DevState& s, HbState& h, GxFwd& f, 
             f.fmask[pw][x] = newsets;
             f.flist[pw][slot_x] = x;
             atomicOr(reinterpret_cast<unsigned long long*>(&f.fbit[pw][x >> 6]), 1ull << (x & 63));
+            if (h.gx_touch) atomicOr(reinterpret_cast<unsigned long long*>(&h.gx_touch[x >> 6]), 1ull << (x & 63));
         }
         // fulfillPromise (:119-126): x's promises of messages it now has (a pair's
         // promises are its own: the group's lanes take x's pairs c, c + G, ...)
