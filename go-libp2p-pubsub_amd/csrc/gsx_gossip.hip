@@ -674,7 +674,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 template <bool MIX>
 __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
     __shared__ uint32_t kc[3][64];  // per topic (GSX_MAX_TOPICS): k1, k2, k4 of the pair being received
+    __shared__ uint32_t gser[64];   // the first 64 advertised batches' set serials (fulfillPromise)
     const uint32_t lane = threadIdx.x;
+    gser[lane] = lane < h.gx_off[s.n_topics] ? h.gx[lane].serial : ~0u;
+    __syncthreads();
     const uint32_t S = h.prom_slots;
     const DevGossipParams& gp = h.gp;
     uint64_t iw_msgs = 0, iw_ids = 0, served = 0, delivered = 0, rejected = 0, dups = 0;
@@ -812,9 +815,9 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
             if (!h.prom_any[z / S] || h.prom_e[z] == 0) continue;
             const uint64_t hd = h.prom_h[z];
             const uint32_t ser = (uint32_t)(hd >> 32), k = (uint32_t)hd;
-            for (uint32_t gi = 0; gi < n_gx; ++gi) {
+            for (uint32_t gi = 0; gi < n_gx; ++gi) {  // (the serials from LDS: no chain of descriptor loads)
+                if ((gi < 64 ? gser[gi] : h.gx[gi].serial) != ser) continue;
                 const GxBatch& b = h.gx[gi];
-                if (b.serial != ser) continue;
                 if ((b.x[(size_t)u * b.n_words + k / 64] >> (k % 64)) & 1) h.prom_e[z] = 0;
                 break;
             }
