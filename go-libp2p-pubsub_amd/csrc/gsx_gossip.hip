@@ -203,8 +203,15 @@ __device__ __forceinline__ const uint64_t* gx_subrow(const HbState& h, uint64_t 
 // (batches past 64 always walked); every other batch holds no candidate.
 __device__ __forceinline__ uint64_t gx_unseen(const HbState& h, uint32_t n_gx, uint32_t u) {
     uint64_t nf = n_gx > 64 ? ~0ull : 0ull;
-    for (uint32_t g = 0; g < n_gx && g < 64; ++g)
-        if (!h.gx[g].full[u]) nf |= 1ull << g;
+    const uint32_t lim = n_gx < 64 ? n_gx : 64;
+    for (uint32_t g0 = 0; g0 < lim; g0 += 8) {  // eight batches' bytes in flight per round trip
+        uint8_t fb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fb[j] = g0 + j < lim ? h.gx[g0 + j].full[u] : 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (!fb[j]) nf |= 1ull << (g0 + j);
+    }
     return nf;
 }
 __device__ __forceinline__ bool gx_skip(uint64_t nf, uint32_t g) { return g < 64 && !((nf >> g) & 1); }
@@ -578,11 +585,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         __syncthreads();
         // ---- lane per pair, the tile's pairs in order
         uint32_t k = 0;  // the node of pair q (monotonic: q only grows)
-        for (int64_t q = rp[0] + lane; q < rp[64]; q += 64) {
+        const int64_t qe = rp[64];
+        // the next pair's IHAVE bits and reverse pair are loaded before this one's
+        // chain (gate, peer, rhm, rows) runs: one round trip fewer per pair
+        uint64_t tall_n = rp[0] + lane < qe ? h.ihave_bits[rp[0] + lane] : 0ull;
+        uint32_t rev_n = rp[0] + lane < qe ? h.rev[rp[0] + lane] : NO_PAIR;
+        for (int64_t q = rp[0] + lane; q < qe; q += 64) {
             while (rp[k + 1] <= q) ++k;
-            const uint64_t tall = h.ihave_bits[q];  // topics v sent u an IHAVE for (receiver-side)
+            const uint64_t tall = tall_n;  // topics v sent u an IHAVE for (receiver-side)
+            const uint32_t r = rev_n;
+            if (q + 64 < qe) {
+                tall_n = h.ihave_bits[q + 64];
+                rev_n = h.rev[q + 64];
+            }
             if (!tall) continue;
-            const uint32_t r = h.rev[q];
             const int gt = gx_gate(s, h, (uint64_t)q, r);
             ignored += gt == 1;
             const uint64_t nf = nfs[k];
