@@ -393,6 +393,13 @@ __device__ __forceinline__ uint64_t old_inside(uint32_t old_in, const VcRef& V, 
 // batch's cache rows, and its message set's seen rows (exchange start),
 // receipts of this exchange, validation outcomes and serial (promise handles
 // are serial << 32 | message index).
+// One (topic, pair) IHAVE slot, written whole by one 16-B store (emitGossip's
+// observable output: gsx_gossip_results): ids advertised, their multiset
+// digest, the round that wrote it (an older tag reads as no IHAVE).
+struct alignas(16) IhaveSlot {
+    uint64_t hash;
+    uint32_t len, tag;
+};
 struct GxBatch {
     const uint64_t* mem;  // [node][word]: in the node's cache
     const uint64_t* all;  // [node][word]: seen by the node
@@ -476,10 +483,8 @@ struct HbState {
     uint32_t* n_hub;       // [topic]
     const uint32_t* hubs;  // nodes with more than HB_LANE_DEG peers (k_hb_recv_hub)
     uint32_t n_hubs;
-    uint32_t* ihave_len;   // [topic][pair] ids advertised (valid under ihave_tag == ihave_cur; else no IHAVE)
-    uint64_t* ihave_hash;  // [topic][pair] multiset digest of the IHAVE ids
-    uint8_t* ihave_tag;    // [topic][pair] the round that wrote the slot
-    uint8_t ihave_cur;     // this round's tag
+    IhaveSlot* ihave_slot;  // [topic][pair] the IHAVE the pair's sender sent (valid under tag == ihave_cur)
+    uint32_t ihave_cur;    // this round's tag
     uint8_t* gelig;        // [pair] GELIG_TARGET | GELIG_SCORE as the round started (k_hb_gelig)
     // the gossip exchange (step (D)); null when it is off
     uint64_t* ihave_bits;  // [pair (u -> v), the receiver's]: topics v sent u an IHAVE for this round

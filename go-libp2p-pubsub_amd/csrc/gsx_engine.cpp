@@ -112,18 +112,17 @@ struct gsx_engine {
     uint8_t* d_dirty = nullptr;
     uint32_t *d_long = nullptr, *d_nlong = nullptr;
     unsigned long long* d_hbstats = nullptr;
-    uint32_t *d_rngk = nullptr, *d_ihave_len = nullptr;
+    uint32_t* d_rngk = nullptr;
+    gsx::IhaveSlot* d_ihave_slot = nullptr;  // [topic][pair] (emitGossip's IHAVE slots)
     uint32_t *d_work = nullptr, *d_nwork = nullptr, *d_hubwork = nullptr, *d_hubs = nullptr;  // heartbeat worklists
     uint8_t* d_tcnt = nullptr;
     uint16_t* d_mcount = nullptr;
     std::vector<uint32_t> hubs_host;  // nodes with more than HB_LANE_DEG pairs
     std::vector<uint8_t> gossip_prev;  // per topic: IHAVE slots written last round
-    uint64_t* d_ihave_hash = nullptr;
     // [topic][pair]: the heartbeat round that wrote the IHAVE slot (ihave_len /
     // ihave_hash hold a slot only under the current round's tag: no per-round clear)
-    uint8_t* d_ihave_tag = nullptr;
     uint8_t* d_gelig = nullptr;  // [pair] HbState::gelig
-    uint8_t ihave_round = 0;
+    uint32_t ihave_round = 0;  // the IHAVE slots' tag of the last round (0: none yet)
     bool have_gossip = false;
     bool hb_clean = false;  // control words / answers / marks all zero (unsharded rounds clear what they read)
     bool hb_tracing = false;           // gsx_hb_set_tracing: keep the round's tracer Graft / Prune words
@@ -869,7 +868,7 @@ void free_state(gsx_engine* e) {
     e->d_col = nullptr;
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
                   e->d_backoff, e->d_bo8, e->d_ctl, e->d_resp,   e->d_dirty,     e->d_long,
-                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_len, e->d_ihave_hash, e->d_ihave_tag, e->d_gelig, e->d_gb,
+                  e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_slot, e->d_gelig, e->d_gb,
                   e->d_mc_digest};
     for (void* p : hb)
         if (p) (void)hipFree(p);
@@ -958,12 +957,11 @@ void free_state(gsx_engine* e) {
         e->pxlog_alloc = 0;
         e->px_last = 0;
     }
-    e->d_rngk = e->d_ihave_len = nullptr;
+    e->d_rngk = nullptr;
+    e->d_ihave_slot = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_tcnt = nullptr;
     e->d_mcount = nullptr;
-    e->d_ihave_hash = nullptr;
-    e->d_ihave_tag = nullptr;
     e->d_gelig = nullptr;
     e->ihave_round = 0;
     e->d_gb = nullptr;
@@ -1483,19 +1481,17 @@ int hb_alloc(gsx_engine* e) {
     if ((rc = dalloc(e, &e->d_ctl, 2 * E)) ||
         (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
         (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 2 * std::max<size_t>(e->T, 1))) ||
-        (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_len, TE)) ||
+        (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_slot, TE)) ||
         (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
         (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
         (rc = dalloc(e, &e->d_mcount, (size_t)e->T * e->n_nodes + 1)) ||
         (rc = dalloc(e, &e->d_hubwork, (size_t)e->T * e->n_nodes)) ||
         (rc = dalloc(e, &e->d_nwork, 2 * (size_t)e->T)) ||
         (rc = dalloc(e, &e->d_hubs, std::max<size_t>(e->hubs_host.size(), 1))) ||
-        (rc = dalloc(e, &e->d_ihave_hash, TE)) || (rc = dalloc(e, &e->d_ihave_tag, TE)) || (rc = dalloc(e, &e->d_gelig, E)) ||
+        (rc = dalloc(e, &e->d_gelig, E)) ||
         (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
         return rc;
-    HIPCHK(e, hipMemsetAsync(e->d_ihave_len, 0, 4 * (TE ? TE : 1), e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_ihave_hash, 0, 8 * (TE ? TE : 1), e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, TE ? TE : 1, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ihave_slot, 0, sizeof(gsx::IhaveSlot) * (TE ? TE : 1), e->stream));
     e->ihave_round = 0;
     if (!e->hubs_host.empty())
         HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
@@ -3734,8 +3730,6 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     h.n_hub = e->d_nwork + e->T;
     h.hubs = e->d_hubs;
     h.n_hubs = (uint32_t)e->hubs_host.size();
-    h.ihave_len = e->d_ihave_len;
-    h.ihave_hash = e->d_ihave_hash;
     h.pp = dev_peer_params(e);
     h.gp = gsx::DevGossipParams{e->gp.d,
                                 e->gp.d_lo,
@@ -3914,12 +3908,12 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     if (gx_on)
         if (int rc = gx_sub_prepare(e, max_ids, tw)) return rc;
     // IHAVE slots: this round's are written under its tag (k_hb_gossip); every
-    // other slot reads as empty, so nothing is cleared but once per 255 rounds
+    // other slot reads as empty, so nothing is cleared (but at the tag's wrap)
     if (++e->ihave_round == 0) {
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, (size_t)e->T * e->E, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_slot, 0, sizeof(gsx::IhaveSlot) * (size_t)e->T * e->E, e->stream));
         e->ihave_round = 1;
     }
-    h.ihave_tag = e->d_ihave_tag;
+    h.ihave_slot = e->d_ihave_slot;
     h.ihave_cur = e->ihave_round;
     h.gelig = e->d_gelig;
     e->have_gossip = !e->gb_host.empty();
@@ -5373,23 +5367,21 @@ int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_diges
     if (!e) return GSX_EINVAL;
     if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
     const size_t TE = (size_t)e->T * e->E;
-    if (!e->d_ihave_len) {  // no heartbeat yet: nothing was sent
+    if (!e->d_ihave_slot) {  // no heartbeat yet: nothing was sent
         if (ihave_len) std::memset(ihave_len, 0, 4 * TE);
         if (ihave_digest) std::memset(ihave_digest, 0, 8 * TE);
         return GSX_OK;
     }
-    if (ihave_len && TE) HIPCHK(e, hipMemcpyAsync(ihave_len, e->d_ihave_len, 4 * TE, hipMemcpyDeviceToHost, e->stream));
-    if (ihave_digest && TE)
-        HIPCHK(e, hipMemcpyAsync(ihave_digest, e->d_ihave_hash, 8 * TE, hipMemcpyDeviceToHost, e->stream));
-    std::vector<uint8_t> tag(TE);
-    if (TE) HIPCHK(e, hipMemcpyAsync(tag.data(), e->d_ihave_tag, TE, hipMemcpyDeviceToHost, e->stream));
+    std::vector<gsx::IhaveSlot> sl(TE);
+    if (TE) HIPCHK(e, hipMemcpyAsync(sl.data(), e->d_ihave_slot, sizeof(gsx::IhaveSlot) * TE, hipMemcpyDeviceToHost,
+                                     e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    const uint8_t cur = e->ihave_round;  // (0: no heartbeat ran, every slot empty)
-    for (size_t i = 0; i < TE; ++i)
-        if (tag[i] != cur || cur == 0) {  // a slot of an earlier round
-            if (ihave_len) ihave_len[i] = 0;
-            if (ihave_digest) ihave_digest[i] = 0;
-        }
+    const uint32_t cur = e->ihave_round;  // (0: no heartbeat ran, every slot empty)
+    for (size_t i = 0; i < TE; ++i) {
+        const bool now = sl[i].tag == cur && cur != 0;  // (else a slot of an earlier round)
+        if (ihave_len) ihave_len[i] = now ? sl[i].len : 0;
+        if (ihave_digest) ihave_digest[i] = now ? sl[i].hash : 0;
+    }
     return GSX_OK;
 }
 

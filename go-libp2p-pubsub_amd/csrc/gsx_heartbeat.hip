@@ -1038,9 +1038,7 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                         }
                         for (int q = 0; q < target; ++q) {
                             const size_t x = tslot + rs[lane] + peers[q];
-                            h.ihave_len[x] = L;
-                            h.ihave_hash[x] = dig;
-                            h.ihave_tag[x] = h.ihave_cur;
+                            h.ihave_slot[x] = IhaveSlot{dig, L, h.ihave_cur};
                             ihave_mark(h, (uint64_t)(rs[lane] + peers[q]), t);  // (D) reads it
                         }
                         cnt[0] += (uint64_t)target;
@@ -1192,9 +1190,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
         if (L <= maxl) {  // the whole list to every target
             for (int p = lane; p < target; p += 64) {
                 const int64_t r = r0 + peers[p];
-                h.ihave_len[tslot + r] = L;
-                h.ihave_hash[tslot + r] = dall;
-                h.ihave_tag[tslot + r] = h.ihave_cur;
+                h.ihave_slot[tslot + r] = IhaveSlot{dall, L, h.ihave_cur};
                 ihave_mark(h, (uint64_t)r, t);  // (D) reads it
             }
             msgs += (uint64_t)target;
@@ -1228,9 +1224,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 d = wave_sum64(d);
                 const uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
                 if (lane == 0) {
-                    h.ihave_len[tslot + r] = maxl;
-                    h.ihave_hash[tslot + r] = take ? d : dall - d;
-                    h.ihave_tag[tslot + r] = h.ihave_cur;
+                    h.ihave_slot[tslot + r] = IhaveSlot{take ? d : dall - d, maxl, h.ihave_cur};
                     ihave_mark(h, (uint64_t)r, t);
                 }
                 // the subset the receiver's handleIHave reads (D): marked at the
