@@ -632,6 +632,7 @@ struct GxSetMerge {
     uint8_t* chg;              // set to 1 when some receipt changes the set's seen rows
     const uint64_t* touch;     // [node bit]: nodes whose rows may hold a receipt (null: every node); the
                                // others' receipt rows, counts and digests are zero already (k_gx_setprep)
+    uint8_t* full;             // the set's full bytes, kept exact at the touched nodes (null: recomputed later)
 };
 hipError_t launch_gx_merge_sets(const GxSetMerge* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // The forwarding of the recovered messages (gsx.h (D): a delivered message is

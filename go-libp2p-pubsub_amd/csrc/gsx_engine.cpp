@@ -4457,7 +4457,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         smerge[i] = gsx::GxSetMerge{ms->d_all, R.xs[i], ms->d_acc, ms->d_dg, R.xs[i] + W * N,
                                     reinterpret_cast<uint32_t*>(R.xs[i] + W * N + N), ms->n_words, ms->n_msgs,
                                     ms->d_vc, (uint64_t)W * N, ms->vc_p, R.vc_code[i], e->d_gx_chg + i,
-                                    R.h.gx_touch};
+                                    R.h.gx_touch, e->sharded() ? nullptr : ms->d_full};
     }
     if (e->sharded()) HIPCHK(e, hipMemsetAsync(e->d_gx_common, 0xff, 8 * 64 * R.sets.size(), e->stream));
     for (auto& g : gx) {
@@ -4650,7 +4650,11 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
                                           st[gsx::HB_FWD_DELIVERED] > 0;
     for (size_t i = 0; i < gx_sets.size(); ++i) {
         gsx_engine::MsgSet* ms = gx_sets[i];
-        if (e->sharded() ? merged : chg[i] != 0) {  // the receipts were merged into its seen rows
+        // the receipts were merged into its seen rows: one engine's merge kept the
+        // full bytes exact at the touched nodes, and its common words stand as a
+        // subset of the new ones (they only filter the rows the ask reads:
+        // k_gx_rhm), so only a range shard recomputes them
+        if (e->sharded() && merged) {
             ms->full_ok = false;
             ms->common_ok = false;
         }

@@ -931,11 +931,12 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
     const uint64_t* word_dig = S.msg_dig + (size_t)W * 64;
     for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += gridDim.x * 256u) {
         if (S.touch && !((S.touch[v >> 6] >> (v & 63)) & 1)) continue;  // (rows, count, digest: zero)
-        uint32_t L = 0;
+        uint32_t L = 0, seen = 0;
         uint64_t d = 0;
         for (uint32_t w = 0; w < W; ++w) {
             const size_t i = (size_t)v * W + w;
             uint64_t word = S.x[i];
+            if (S.full) seen += (uint32_t)__popcll(S.all[i] | word);  // (the node's seen count after the merge)
             if (!word) continue;
             S.all[i] |= word;
             if (S.chg && !*S.chg) *S.chg = 1;  // (read first: one writer in many stores)
@@ -959,6 +960,7 @@ __global__ __launch_bounds__(256) void k_gx_merge_sets(const GxSetMerge* __restr
         }
         S.dig[v] = d;
         S.cnt[v] = L;
+        if (S.full) S.full[v] = seen == S.n_msgs;
     }
 }
 
