@@ -701,6 +701,10 @@ struct GxFwd {
     const uint64_t* hent;
     uint32_t rw;
     uint32_t dense_div;  // a hop is dense when its last frontier exceeds n_nodes / dense_div
+    // one engine with the eligible-sender lists: fout is computed by the run's
+    // first dense hop (k_gxf_fout_pre, for its lists) and not at the run's
+    // start; a sparse hop evaluates its frontier senders' slots itself
+    uint32_t fout_lazy;
     uint32_t mixed;      // some set's old copies are split by the P3 window (old_in 2)
 };
 constexpr uint32_t GXF_HDR = 6;

@@ -4158,6 +4158,7 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         f.fend = e->d_gxf_fend;
     }
     f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
+    f.fout_lazy = (!f.fin && f.fent) ? 1u : 0u;  // (one engine: the first dense hop computes fout)
     static const uint32_t dense_div = [] {  // (GSX_GXF_DENSE: A/B of the dense-hop threshold)
         const char* v = getenv("GSX_GXF_DENSE");
         return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_DENSE;

@@ -1019,8 +1019,10 @@ __device__ __forceinline__ uint32_t gxf_fout_bits(const DevState& s, const HbSta
 // other node's receipt rows are zero).
 __global__ __launch_bounds__(256) void k_gxf_init(DevState s, HbState h, GxFwd f, uint32_t n, uint32_t n_src_total,
                                                   uint32_t node_lo) {
-    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u)
-        for (int64_t r = h.row_ptr[u]; r < h.row_ptr[u + 1]; ++r) f.fout[r] = (uint8_t)gxf_fout_bits(s, h, f, (uint64_t)r, u);
+    if (!f.fout_lazy)
+        for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < n; u += gridDim.x * 256u)
+            for (int64_t r = h.row_ptr[u]; r < h.row_ptr[u + 1]; ++r)
+                f.fout[r] = (uint8_t)gxf_fout_bits(s, h, f, (uint64_t)r, u);
     const uint32_t n_list = h.gx_err[6];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_list; i += gridDim.x * 256u) {
         const uint32_t u = h.gx_nodes[i] & ~GX_HEAVY;
@@ -1106,6 +1108,24 @@ __device__ __forceinline__ bool gxf_fent_ready(const GxFwd& f, uint32_t hop, uin
     return false;
 }
 
+// fout of every pair (fout_lazy) at the run's first hop whose frontier holds
+// more than n / GXF_FOUT_DIV nodes (so before its first dense hop, whose
+// eligible-sender lists gather it): a run of small frontiers (the light
+// heartbeat rounds) evaluates its few senders' slots in place and never
+// pays the pass.  Every other hop returns at once.
+constexpr uint32_t GXF_FOUT_DIV = 64;
+__device__ __forceinline__ bool gxf_fout_ready(const GxFwd& f, uint32_t hop, uint32_t n) {
+    if (!f.fout_lazy) return true;
+    for (uint32_t z = 1; z <= hop; ++z)
+        if ((uint64_t)f.fcnt[z - 1] * GXF_FOUT_DIV > n) return true;
+    return false;
+}
+__global__ __launch_bounds__(256) void k_gxf_fout_pre(DevState s, HbState h, GxFwd f, uint32_t hop) {
+    if (!gxf_fout_ready(f, hop, h.n_nodes) || gxf_fout_ready(f, hop - 1, h.n_nodes)) return;
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < h.n_nodes; u += gridDim.x * 256u)
+        for (int64_t r = h.row_ptr[u]; r < h.row_ptr[u + 1]; ++r) f.fout[r] = (uint8_t)gxf_fout_bits(s, h, f, (uint64_t)r, u);
+}
+
 __device__ __forceinline__ uint64_t gxf_slot_sets(const GxFwd& f, uint32_t slots) {
     uint64_t m = 0;
     for (; slots; slots &= slots - 1) m |= f.slot_sets[__builtin_ctz(slots)];
@@ -1125,11 +1145,12 @@ __global__ __launch_bounds__(256) void k_gxf_mark(DevState s, HbState h, GxFwd f
         if (f.fent && !f.fin && !gxf_fent_ready(f, hop - 1, h.n_nodes)) gxf_compact_rows(s, h, f);  // the first
         return;
     }
+    const bool fo_ready = gxf_fout_ready(f, hop, h.n_nodes);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nf; i += stride) {
         const uint32_t v = f.flist[p][i];
         const uint64_t M = f.fmask[p][v];
         for (int64_t r = h.row_ptr[v]; r < h.row_ptr[v + 1]; ++r) {
-            const uint32_t fo = f.fout[r];
+            const uint32_t fo = fo_ready ? f.fout[r] : gxf_fout_bits(s, h, f, (uint64_t)r, v);
             if (!fo) continue;
             const uint64_t ok = M & gxf_slot_sets(f, fo);
             if (!ok) continue;
@@ -1349,6 +1370,7 @@ __device__ __forceinline__ void gxf_pull_run(DevState& s, HbState& h, GxFwd& f, 
     const uint32_t lc = threadIdx.x % G;
     unsigned long long c_new = 0, c_dup = 0, c_gray = 0;
     const bool fe = gxf_fent_ready(f, hop, h.n_nodes);
+    const bool fo_ready = fe || gxf_fout_ready(f, hop, h.n_nodes);
     const uint32_t nr = dense ? h.n_nodes : f.rcnt[hop];
     for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G; i < nr; i += gridDim.x * (256u / G)) {
         const uint32_t x = dense ? i : f.rlist[i];
@@ -1403,7 +1425,7 @@ __device__ __forceinline__ void gxf_pull_run(DevState& s, HbState& h, GxFwd& f, 
             for (int j = 0; j < B; ++j) {
                 if (!fms[j]) continue;
                 const uint64_t q = qs[j];
-                fis[j] = (uint32_t)f.fout[rqs[j]] |
+                fis[j] = (fo_ready ? (uint32_t)f.fout[rqs[j]] : gxf_fout_bits(s, h, f, (uint64_t)rqs[j], vqs[j])) |
                          ((!(h.eflags[q] & EDGE_DIRECT) && s.score[q] < h.graylist) ? GXF_GRAY : 0u);  // AcceptFrom at x
                 fms[j] = f.fmask[p][vqs[j]] & M & gxf_slot_sets(f, fis[j] & 0xFFu);
             }
@@ -1764,6 +1786,7 @@ hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, 
 hipError_t launch_gxf_hop(const DevState& s, const HbState& h, const GxFwd& f, uint32_t hop, hipStream_t st) {
     if (hop == 1 && f.fent && f.fin)  // the shard's eligible senders (the remote ones' fin bits have arrived by now)
         hipLaunchKernelGGL(k_gxf_compact, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f);
+    if (f.fout_lazy) hipLaunchKernelGGL(k_gxf_fout_pre, dim3(gx_blocks(h.n_nodes, 256, 2048)), dim3(256), 0, st, s, h, f, hop);
     hipLaunchKernelGGL(k_gxf_mark, dim3(gx_blocks(h.n_nodes, 256, 4096)), dim3(256), 0, st, s, h, f, hop);
     static const int gl = [] {  // receivers' lanes: GSX_GXF_G = 1 (k_gxf_pull), 2, 4 (default), 8
         const char* v = getenv("GSX_GXF_G");
