@@ -516,9 +516,12 @@ __device__ __forceinline__ const uint64_t* gx_memrow(const HbState& h, const GxB
 // topics of tb, words ascending): f(batch, word, v's cache word & ~u's, within
 // the subset row of a truncated list) for each nonzero one; stops when f
 // returns false.  (mem has no bit past n_msgs: no validity mask.)
+// wm: u's miss masks from k_gx_ask's LDS (batch g's byte at wm[64 g]: bit w
+// = u lacks a message of word w; batches of at most 8 words), so v's words
+// are gathered only where u lacks something.
 template <typename F>
 __device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t tb, uint32_t uu, uint64_t q,
-                                         uint32_t v, uint64_t tr, uint32_t r, F&& f) {
+                                         uint32_t v, uint64_t tr, uint32_t r, const uint8_t* wm, F&& f) {
     for (; cb; cb &= cb - 1) {
         const uint32_t g = (uint32_t)__builtin_ctzll(cb);
         const GxBatch& b = h.gx[g];
@@ -528,7 +531,9 @@ __device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t
         const uint32_t W = b.n_words;
         const uint64_t* arow = b.all + (size_t)uu * W;
         const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
+        const uint32_t wmask = W <= 8 ? wm[64 * g] : 0xFFFFFFFFu;
         for (uint32_t w = 0; w < W; ++w) {
+            if (!((wmask >> (w < 32 ? w : 31)) & 1)) continue;
             uint64_t c = mrow[w] & ~arow[w];
             if (sub) c &= sub[b.row_off + w];
             if (c && !f(g, w, c)) return;
@@ -552,6 +557,7 @@ __device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t
 //    kernel keeps 6 waves per SIMD);
 //  - a node with a heavy walk or an asked pair is listed for k_gx_node (pass 2).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_gx_ask(DevState s, HbState h) {
+    __shared__ uint8_t wms[64][64];  // [batch][node of the tile]: words (<= 8 per batch) where the node lacks a message
     __shared__ int64_t rp[65];      // row_ptr of the tile's nodes
     __shared__ uint64_t nfs[64];    // per node: the unseen-batch mask
     __shared__ uint32_t nmls[64];   // per node: GX_HEAVY
@@ -569,10 +575,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             if (u < h.n_nodes) {
                 nf = gx_unseen(h, n_gx, u);
                 for (uint64_t m = heavy ? 0 : nf; m; m &= m - 1) {
-                    nw += h.gx[__builtin_ctzll(m)].n_words;
+                    const uint32_t g = (uint32_t)__builtin_ctzll(m);
+                    const GxBatch& b = h.gx[g];
+                    const uint32_t W = b.n_words;
+                    nw += W;
                     if (nw > GX_MW) {
                         heavy = true;
                         break;
+                    }
+                    if (W <= 8) {
+                        uint32_t mk = 0;
+                        for (uint32_t w = 0; w < W; ++w) {
+                            const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
+                            const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+                            if (~b.all[(size_t)u * W + w] & valid) mk |= 1u << w;
+                        }
+                        wms[g][lane] = (uint8_t)mk;
                     }
                 }
             }
@@ -619,7 +637,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             // |iwant|: v's cache words where u lacks something (topics of the RPC,
             // the subset row of a truncated list)
             uint32_t n = 0;
-            gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, [&](uint32_t, uint32_t, uint64_t c) {
+            gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, &wms[0][k], [&](uint32_t, uint32_t, uint64_t c) {
                 n += (uint32_t)__popcll(c);
                 return true;
             });
@@ -630,7 +648,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             if (kk == n) {  // the element at Int31n(kk) of all of them, canonical order
                 Rng g = gx_iwant_rng(h, uu, v);
                 uint32_t j = (uint32_t)g.int31n((int32_t)kk);
-                gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, [&](uint32_t gi, uint32_t w, uint64_t c) {
+                gx_cwalk(h, cb, tb, uu, (uint64_t)q, v, tr, r, &wms[0][k], [&](uint32_t gi, uint32_t w, uint64_t c) {
                     const uint32_t pc = (uint32_t)__popcll(c);
                     if (j >= pc) {
                         j -= pc;
