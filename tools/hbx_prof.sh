@@ -19,10 +19,10 @@ step() {  # step NAME SECONDS CMD...
     if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
 step hbx 300 rocprofv3 --kernel-trace --stats -d "$O/hbx" -o kt --output-format csv -- \
-    python3 tools/hb_micro.py --exchange --rounds 4
+    python3 tools/hb_micro.py --exchange --settle 8 --first-tick 59 --rounds 5
 python3 tools/kt_rounds.py "$O/hbx/kt_kernel_trace.csv" 30 k_gxf_pull k_gxf_mark > "$O/hbx_rounds.txt"
 python3 tools/kt_top.py "$O/hbx/kt_kernel_stats.csv" 24 > "$O/hbx_top.txt"
 step adv 300 rocprofv3 --kernel-trace --stats -d "$O/adv" -o kt --output-format csv -- \
-    python3 tools/adv_micro.py --no-spam
+    python3 tools/adv_micro.py
 python3 tools/kt_rounds.py "$O/adv/kt_kernel_trace.csv" 30 k_gxf_pull k_gxf_mark > "$O/adv_rounds.txt"
 cat "$O/hbx_rounds.txt" "$O/hbx_top.txt" "$O/adv_rounds.txt"
