@@ -4158,12 +4158,17 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         f.fend = e->d_gxf_fend;
     }
     f.all_sets = f.n_sets >= 64 ? ~0ull : ((1ull << f.n_sets) - 1);
-    f.fout_lazy = (!f.fin && f.fent) ? 1u : 0u;  // (one engine: the first dense hop computes fout)
+    static const uint32_t fout_div = [] {  // (GSX_GXF_FOUT_DIV: A/B of the fout pass's threshold)
+        const char* v = getenv("GSX_GXF_FOUT_DIV");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_FOUT_DIV;
+    }();
     static const uint32_t dense_div = [] {  // (GSX_GXF_DENSE: A/B of the dense-hop threshold)
         const char* v = getenv("GSX_GXF_DENSE");
         return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_DENSE;
     }();
     f.dense_div = dense_div;
+    // (one engine: fout computed once the frontier grows, at the first dense hop at the latest)
+    f.fout_lazy = (!f.fin && f.fent) ? std::max(fout_div, f.dense_div) : 0u;
     if (e->d_gxf_hst) {
         f.hstamp = e->d_gxf_hst;
         f.hidx = e->d_gxf_hst + E;
