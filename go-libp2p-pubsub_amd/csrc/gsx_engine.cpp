@@ -3191,8 +3191,13 @@ int gsx_propagate(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_c
         if (int rc = prop_event_pair(e, &a, &b)) return rc;
         HIPCHK(e, hipEventRecord(a, e->stream));
     }
+    // (GSX_PROP_AHEAD: hops queued past the one the host waits for, A/B)
+    static const uint32_t ahead = [] {
+        const char* v = getenv("GSX_PROP_AHEAD");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : 2u;
+    }();
     for (uint32_t h = 1; h <= cfg->max_hops; ++h) {
-        if (P.loop_timing && h >= 3 && !hop_delivered(e, h - 2)) break;
+        if (P.loop_timing && h > ahead && !hop_delivered(e, h - ahead)) break;
         if (int rc = prop_hop(e, nullptr)) return rc;
     }
     if (P.loop_timing) HIPCHK(e, hipEventRecord(b, e->stream));

@@ -5,6 +5,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -41,7 +42,10 @@ cfg.hop_latency_ns = a.latency_us * 1000
 for b in range(a.warmup + a.batches):
     if a.warmup and b == a.warmup:
         e.prop_results(a.msgs)  # (read-only: the marker dispatch)
-    out = e.propagate(bench.prop_messages(a.peers, a.msgs, synth.SEED, first=b * a.msgs), cfg)[0]
+    msgs = bench.prop_messages(a.peers, a.msgs, synth.SEED, first=b * a.msgs)
+    t0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)  # (the profiler's clock: tools/hb_api.py windows)
+    out = e.propagate(msgs, cfg)[0]
+    print(f"window {b} {t0} {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", flush=True)
     d = out.as_dict()
     print(json.dumps({"batch": b, "hop_kernel_ms": out.hop_kernel_ms, "deliveries": d["deliveries"],
                       "hop_deliveries": d["hop_deliveries"], "edge_sends": out.edge_sends,
