@@ -702,15 +702,17 @@ struct GxFwd {
     uint32_t rw;
     uint32_t dense_div;  // a hop is dense when its last frontier exceeds n_nodes / dense_div
     // one engine with the eligible-sender lists: fout is computed once a hop's
-    // frontier passes n / fout_lazy nodes (k_gxf_fout_pre; before the first
-    // dense hop's lists) and not at the run's start; a smaller frontier's hop
-    // evaluates its senders' slots itself (0: fout computed at the start)
+    // frontier holds more than fout_lazy nodes (k_gxf_fout_pre; before the
+    // first dense hop's lists) and not at the run's start; a smaller
+    // frontier's hop evaluates its senders' slots itself (0: fout computed at
+    // the start)
     uint32_t fout_lazy;
     uint32_t mixed;      // some set's old copies are split by the P3 window (old_in 2)
 };
 constexpr uint32_t GXF_HDR = 6;
 constexpr uint32_t GXF_DENSE = 16;
-constexpr uint32_t GXF_FOUT_DIV = 64;  // GxFwd::fout_lazy (GSX_GXF_FOUT_DIV: A/B)
+constexpr uint32_t GXF_FOUT_DIV = 64;     // GxFwd::fout_lazy = min(n / GXF_FOUT_DIV, GXF_FOUT_MAX)
+constexpr uint32_t GXF_FOUT_MAX = 16384;  // (GSX_GXF_FOUT_DIV / GSX_GXF_FOUT_MAX: A/B)
 constexpr uint16_t GXF_GRAY = 0x100;
 hipError_t launch_gxf_init(const DevState& s, const HbState& h, const GxFwd& f, uint32_t n_src_total,
                            hipStream_t st);

@@ -4172,8 +4172,16 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_DENSE;
     }();
     f.dense_div = dense_div;
-    // (one engine: fout computed once the frontier grows, at the first dense hop at the latest)
-    f.fout_lazy = (!f.fin && f.fent) ? std::max(fout_div, f.dense_div) : 0u;
+    // (one engine: fout computed once the frontier grows, before the first dense hop)
+    static const uint32_t fout_max = [] {
+        const char* v = getenv("GSX_GXF_FOUT_MAX");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : gsx::GXF_FOUT_MAX;
+    }();
+    {
+        const uint32_t n = (uint32_t)e->n_nodes;
+        const uint32_t thr = std::min({n / std::max(fout_div, 1u), fout_max, n / std::max(f.dense_div, 1u)});
+        f.fout_lazy = (!f.fin && f.fent) ? std::max(thr, 1u) : 0u;
+    }
     if (e->d_gxf_hst) {
         f.hstamp = e->d_gxf_hst;
         f.hidx = e->d_gxf_hst + E;

@@ -1126,15 +1126,15 @@ __device__ __forceinline__ bool gxf_fent_ready(const GxFwd& f, uint32_t hop, uin
     return false;
 }
 
-// fout of every pair (fout_lazy) at the run's first hop whose frontier holds
-// more than n / fout_lazy nodes (GXF_FOUT_DIV) (so before its first dense hop, whose
+// fout of every pair at the run's first hop whose frontier holds more than
+// fout_lazy nodes (min(n / GXF_FOUT_DIV, GXF_FOUT_MAX)) (so before its first dense hop, whose
 // eligible-sender lists gather it): a run of small frontiers (the light
 // heartbeat rounds) evaluates its few senders' slots in place and never
 // pays the pass.  Every other hop returns at once.
 __device__ __forceinline__ bool gxf_fout_ready(const GxFwd& f, uint32_t hop, uint32_t n) {
     if (!f.fout_lazy) return true;
     for (uint32_t z = 1; z <= hop; ++z)
-        if ((uint64_t)f.fcnt[z - 1] * f.fout_lazy > n) return true;
+        if (f.fcnt[z - 1] > f.fout_lazy) return true;
     return false;
 }
 __global__ __launch_bounds__(256) void k_gxf_fout_pre(DevState s, HbState h, GxFwd f, uint32_t hop) {
