@@ -502,6 +502,7 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
 constexpr uint32_t GX_END = 0xFFFFFFFFu;  // GxBatch::nxt: the set's last batch
 constexpr uint32_t GX_MW = 128;  // words of unseen batches a receiver's lane walks itself (else: a wave, GX_HEAVY)
 constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
+constexpr uint32_t GX_REQ_ALL = 1u << 31;  // gx_req: the pair asked for every candidate (kk = |iwant|)
 
 // v's cache row of batch b (pair q = (u -> v)): a local sender's; on a range
 // shard a remote one's from the rows its rank sent; null when it sent none.
@@ -664,7 +665,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             }
             ++iw_msgs;
             iw_ids += kk;
-            h.gx_req[q] = kk;
+            h.gx_req[q] = kk | (kk == n ? GX_REQ_ALL : 0u);
             gx_promise(h, (uint64_t)q, ((uint64_t)h.gx[pick_g].serial << 32) | pick_k, occ);
             lst[k] = 1;
         }
@@ -746,7 +747,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 if (lane == 0) {
                     ++iw_msgs;
                     iw_ids += kk;
-                    h.gx_req[q] = kk;
+                    h.gx_req[q] = kk | (kk == n ? GX_REQ_ALL : 0u);
                     gx_promise(h, (uint64_t)q, ((uint64_t)h.gx[pick_g].serial << 32) | pick_k, occ);
                 }
             }
@@ -758,7 +759,11 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
           for (uint64_t am = __ballot(kq != 0); am; am &= am - 1) {  // (wave-uniform)
             const int jb = __builtin_ctzll(am);
             const int64_t q = c0 + jb;
-            const uint32_t kk = (uint32_t)__shfl((int)kq, jb, 64);
+            const uint32_t kq_j = (uint32_t)__shfl((int)kq, jb, 64);
+            const uint32_t kk = kq_j & ~GX_REQ_ALL;
+            // (every candidate asked: |iwant| as k_gx_ask counted it, the rows it read
+            // unchanged since; else the sampled path needs the count again)
+            const bool ask_all = (kq_j & GX_REQ_ALL) != 0;
             const uint64_t tall = h.ihave_bits[q];
             const uint32_t r = h.rev[q];
             const bool answered = gx_answers(s, h, (uint64_t)q, r) &&  // v ignores u's IWANT
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
             if (answered) {
                 const uint32_t v = (uint32_t)h.col[q];
                 const uint64_t tr = h.ihave_tr[q];
-                const uint32_t n = gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
+                const uint32_t n = ask_all ? kk : gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
                 if (kk == n) {
                     // a lane per (message set, word) of every set on the topics of tb
                     // (h.gx_sw, canonical order): it walks the set's batches in cache
