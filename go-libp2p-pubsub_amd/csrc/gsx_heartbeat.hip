@@ -922,7 +922,22 @@ __device__ __forceinline__ uint32_t gossip_ids(const HbState& h, uint32_t v, con
                                                uint32_t n_gb, uint64_t& dig) {
     uint32_t L = 0;
     dig = 0;
-    for (uint32_t b = 0; b < n_gb; ++b) {
+    uint32_t b = 0;
+    for (; b + 4 <= n_gb; b += 4) {  // four batches' summaries in flight per round trip
+        uint32_t c[4];
+        uint64_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            c[j] = gb[b + j].cnt[v];
+            d[j] = gb[b + j].dig[v];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            L += c[j];
+            dig += d[j];
+        }
+    }
+    for (; b < n_gb; ++b) {
         L += gb[b].cnt[v];
         dig += gb[b].dig[v];
     }
