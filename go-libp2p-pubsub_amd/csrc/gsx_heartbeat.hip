@@ -902,6 +902,12 @@ __global__ __launch_bounds__(256) void k_mc_summary(const uint64_t* __restrict__
                     d += word_dig[w];
                     continue;
                 }
+                uint64_t miss = full & ~word;
+                if (word && __popcll(miss) < __popcll(word)) {  // most of the word: its digest less the missing ids
+                    d += word_dig[w];
+                    for (; miss; miss &= miss - 1) d -= msg_dig[w * 64 + (uint32_t)__builtin_ctzll(miss)];
+                    continue;
+                }
                 for (; word; word &= word - 1) d += msg_dig[w * 64 + (uint32_t)__builtin_ctzll(word)];
             }
 #pragma unroll
