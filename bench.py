@@ -156,6 +156,117 @@ def cpu_baseline(e, T, now, passes):
     return o, st
 
 
+def _oracle_mod():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # checker / CPU baseline only
+
+    return orc
+
+
+PROP_KEYS = ("deliveries", "duplicates", "transmissions", "graylisted", "rejected", "ignored", "hops")
+
+
+def cpu_prop_baseline(e, n, d, th, cfg, seed, budget_s=12.0):
+    """SURVEY §8d's CPU column for msg deliveries/s: the C oracle's propagate
+    (oracle/gsx_oracle.c orc_propagate, a message-at-a-time restatement of
+    floodsub.go:76-100 / gossipsub.go:943-1013 with the same P2/P3/P4
+    credits) on the propagation engine's exact state, one thread, on a bounded
+    sample: calls of a few messages each until about budget_s of CPU time.
+    The GPU engine runs the same calls afterwards and every call's counters
+    must agree (a parity check of the sample, not part of the timing)."""
+    orc = _oracle_mod()
+    t = time.time()
+    st = e.export_state()
+    o = orc.Oracle(1)
+    o.set_peer_params(synth.bench_peer_params())
+    o.set_topic_params(0, synth.spam_test_topic_params())
+    o.set_thresholds(th)
+    o.set_gossipsub_params(gsx_engine_mod.default_gossipsub_params(gossip_exchange=0))
+    ov = synth.connect_some_overlay(n, d=d, seed=seed)
+    o.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    del ov
+    o.import_state(st)
+    o.set_app_scores(np.zeros(e.n_pairs))
+    del st
+    log(f"[bench] oracle propagation state in {time.time() - t:.1f}s")
+    calls, secs, dl = [], 0.0, 0
+    per_call = 4
+    while secs < budget_s and len(calls) < 64:
+        msgs = prop_messages(n, per_call, seed, first=90_000_000 + per_call * len(calls))
+        t = time.perf_counter()
+        out = o.propagate(msgs, cfg)[0]
+        secs += time.perf_counter() - t
+        d = out.as_dict()
+        dl += d["deliveries"]
+        calls.append((msgs, {k: d[k] for k in PROP_KEYS}))
+    o.close()
+    bad = 0
+    for msgs, want in calls:
+        d = e.propagate(msgs, cfg)[0].as_dict()
+        bad += {k: d[k] for k in PROP_KEYS} != want
+    return {"value": dl / secs, "unit": "msg deliveries/s", "cores": 1, "kind": "port",
+            "sample": f"{len(calls)} gossipsub calls of {per_call} messages over the {n}-peer overlay of this leg, "
+                      f"P2/P3 credits on ({secs:.1f}s of one core; oracle/gsx_oracle.c orc_propagate, gcc -O3; "
+                      f"a message-at-a-time restatement, not reference Go: no Go on the box)",
+            "nproc": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "sample_parity_vs_gpu": "bit-exact counters" if bad == 0 else f"MISMATCH in {bad} of {len(calls)} calls"}
+
+
+def cpu_hb_baseline(args, local, seed, n_cpu=20_000, settle=3, timed=2):
+    """The CPU column for the heartbeat: the C oracle's heartbeat (orc_heartbeat:
+    gossipsub.go:1303-1564 with handleGraft/Prune and the gossip exchange,
+    :615-716) on a cfg3-shaped sample (n_cpu peers x --topics, the bench's
+    generator, --hb-msgs gossipsub messages propagated before every round),
+    one thread.  The GPU engine runs the same sequence beside it and every
+    round's counters must agree."""
+    orc = _oracle_mod()
+    T = args.topics
+    ov, g = build_engine(n_cpu, T, args.degree, seed, local)
+    g.refresh(T0 + abi.SECOND)
+    st = g.export_state()
+    o = orc.Oracle(T)
+    o.set_peer_params(synth.bench_peer_params())
+    for k in range(T):
+        o.set_topic_params(k, synth.spam_test_topic_params())
+    o.load_overlay(ov.row_ptr, ov.col, ov.edge_flags, ov.node_ips)
+    o.import_state(st)
+    o.set_app_scores(np.zeros(ov.n_pairs))
+    del st
+    th_hb = abi.Thresholds(gossip_threshold=-100, publish_threshold=-200, graylist_threshold=-300,
+                           accept_px_threshold=0, opportunistic_graft_threshold=5)
+    gp = gsx_engine_mod.default_gossipsub_params(gossip_exchange=1 if args.hb_exchange else 0)
+    for be in (g, o):
+        be.set_thresholds(th_hb)
+        be.set_gossipsub_params(gp)
+    cfg = prop_config(args, n_cpu)
+    now, tick = T0 + abi.SECOND, 59 - settle - timed
+    secs, bad, rounds = 0.0, 0, 0
+    for k in range(settle + timed):
+        tick += 1
+        now += abi.SECOND
+        cfg.now_ns = now - abi.SECOND // 2
+        msgs = prop_messages(n_cpu, args.hb_msgs, seed, first=70_000_000 + k * args.hb_msgs)
+        o.propagate(msgs, cfg)
+        g.propagate(msgs, cfg)
+        t = time.perf_counter()
+        oo = o.heartbeat(tick, now, seed).as_dict()
+        if k >= settle:
+            secs += time.perf_counter() - t
+            rounds += 1
+        bad += g.heartbeat(tick, now, seed).as_dict() != oo
+    o.close()
+    g.close()
+    return {"value": n_cpu * T * rounds / secs, "unit": "heartbeat (node, topic) mesh units/s", "cores": 1,
+            "kind": "port", "ms_per_round": secs / rounds * 1e3,
+            "sample": f"{n_cpu} peers x {T} topics (cfg3's generator and parameters), {settle} settle + {timed} "
+                      f"timed rounds (ticks {tick - timed + 1}-{tick}) with {args.hb_msgs} gossipsub messages "
+                      f"before each, gossip exchange {'on' if args.hb_exchange else 'off'}; oracle/gsx_oracle.c "
+                      f"orc_heartbeat, one core, {secs:.2f}s timed (restatement, not reference Go)",
+            "nproc": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "sample_parity_vs_gpu": "bit-exact counters every round" if bad == 0 else
+                                    f"MISMATCH in {bad} of {settle + timed} rounds"}
+
+
 def prop_engine(n_total, lo, hi, d, seed, device, th, sharded):
     """Engine for a propagation leg: T=1, spam-test params, synthesized state
     (mesh ~ half of each node's peers), one refresh so publishThreshold tests
@@ -306,9 +417,13 @@ def prop_replica(args, rank, world, local, dist, dev, th):
     mine = prop_messages(n, M, synth.SEED, first=args.prop_steps * M)
     mine = mine[(M * rank) // world : (M * (rank + 1)) // world]
     legs = prop_variant_legs(args, e, n) if world == 1 else None
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu:
+        cpu = cpu_prop_baseline(e, n, args.degree, th, cfg, synth.SEED)
     e.close()
     return {
         "variants": legs,
+        "cpu_baseline": cpu,
         "metric": "msg deliveries/s",
         "mode": ("message-parallel replicas (weak): full overlay per GPU, own messages, credits deferred and summed "
                  f"with one all-reduce per epoch of {eb} batches (cache blocks not merged: no heartbeat in this "
@@ -795,6 +910,8 @@ def main():
             "per_round": rounds,
             "settle_per_round": [{k: r[k] for k in ("tick", "ms", "grafts", "prunes")} for r in settle],
         }
+        if rank == 0 and world == 1 and not args.no_cpu:
+            hb["cpu_baseline"] = cpu_hb_baseline(args, local, seed)
 
     adv = adversarial_leg(args, rank, world, local, dist, dev) if args.adv_peers > 0 else None
 

@@ -138,7 +138,11 @@ enum {
     STAT_REJECTED,  // receipts of REJECT messages
     STAT_IGNORED,   // receipts of IGNORE / THROTTLE messages
     STAT_GRAY,      // copies the receiver's AcceptFrom dropped (graylisted sender), counted apart from STAT_DUPS
-    STAT_WORDS
+    // range shards, compacted exchange: [hop] entries scattered into the halo
+    // for that hop (k_halo_scatter), so a hop with no local frontier and no
+    // remote row returns at once
+    STAT_HALO0,
+    STAT_WORDS = STAT_HALO0 + MAX_HOPS + 1
 };
 // rev[q] of a pair whose neighbour lives on another shard: HALO | receive slot.
 constexpr uint32_t HALO = 0x80000000u;
@@ -174,8 +178,29 @@ struct PropState {
     uint64_t* from_mask;       // [pair (u -> v)][word] messages u first received from v (null: not tracked)
     uint32_t* fcnt;            // per pair (u -> v), this call: first receipts from v
     uint64_t* flast;           // per pair: hop << 32 | first receipts of the last hop that had any
-    uint64_t* hfrom;           // [receive slot][word]: first receipts from the remote sender at its latest such hop
-    const uint64_t* halo_occ;  // bit per receive slot: row received this hop (null: every row present)
+    uint64_t* hfrom;           // [pair q = (u -> v), v remote][word]: u's first receipts from v at its latest such hop
+    // compacted exchange: halo rows are [slot][tag | W words], a row empty unless its tag
+    // is halo_tag | hop (k_halo_scatter); 0: the dense exchange's untagged [slot][W] rows
+    uint64_t halo_tag;
+    const uint32_t* send_slot;  // per pair: its send slot (NO_PAIR: no remote receiver asked for it)
+    // Range shards, replicated frontier (rep != 0; the lean calls: late duplicate
+    // accounting, no RandomSub draws, no first-deliverer rows).  Every rank keeps
+    // the frontier rows of ALL n_total nodes, two hops deep: front_g
+    // [parity][n_total][W] and occ_g [parity][n_total / 64 + 1] (a row is valid
+    // only under its bit); pins hold global node ids, so the hop gathers a remote
+    // sender's row exactly as a local one.  Per hop each rank contributes its
+    // new frontier rows (k_rep_pack) and scatters the others' (k_rep_scatter).
+    uint32_t rep, n_total;
+    uint64_t* front_g;
+    uint64_t* occ_g;
+    uint64_t rep_in;            // remote frontier rows scattered for this hop (host-known)
+    const uint32_t* rmark_v;    // [n_recv] remote senders' global ids, ascending (their local receivers: rmark_u)
+    const uint32_t* rmark_u;
+    uint64_t n_rmark;
+    const uint64_t* src_bits;   // [n_total / 64 + 1] bit per global node: published in this call
+    const uint32_t* src_ids;    // [n_src] the sources' global ids, ascending, and their
+    const uint64_t* src_rows;   // [n_src][W] origin rows (every message each published)
+    uint32_t n_src;
     uint64_t* touch;           // [2][node / 64] bit per node, buffer h & 1: some sender's row is non-empty (very sparse hops)
     const uint32_t* halo_node; // per receive slot: the local node whose pair it feeds
     uint64_t* sel;             // [pair][word] RandomSub draws (null for other routers)
@@ -264,21 +289,37 @@ struct PropState {
 
 // pins_only: the fwd bytes stand (a RESCORE count kept them), update the
 // pins / compacted senders of the listed changes only
-hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only = false);
+hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only = false,
+                           bool compact = true);
+hipError_t launch_prop_compact(const PropState& ps, hipStream_t st);  // compacted senders from the pins
 hipError_t launch_prop_init(const PropState& ps, uint64_t* front, hipStream_t st);
 hipError_t launch_prop_clear(const PropState& ps, bool clear_flast, bool clear_corr, hipStream_t st);
 hipError_t launch_rsub_select(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const uint64_t* front_occ, uint64_t* send,
                             hipStream_t st);
 hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, const uint64_t* front_occ,
-                                    uint64_t* out, unsigned long long* dcount, hipStream_t st);
+                                    uint64_t* out, unsigned long long* dcount, uint32_t* tab, hipStream_t st);
+uint32_t pack_table_words(uint32_t n_nodes, uint32_t n_ranks);  // u32 words of its per-(block, rank) table
 hipError_t launch_pack_counts(const unsigned long long* dcount, const unsigned long long* hop_new, uint32_t world,
                               int64_t* out, hipStream_t st);
-hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st);
-hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
-                               uint64_t* halo_occ, uint32_t h, hipStream_t st);
+hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t h,
+                               hipStream_t st);
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st);
 hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st);
+bool hop_lean(const PropState& ps);  // the call's hops take k_prop_hop_fast[1] (no RandomSub, no from rows, late)
+// range shards, replicated frontier (PropState::rep)
+hipError_t launch_rep_init(const PropState& ps, hipStream_t st);
+hipError_t launch_rep_pack(const PropState& ps, uint32_t h, uint64_t* out, unsigned long long* cnt, hipStream_t st);
+struct RepParts {  // the other ranks' entries of a hop (k_rep_scatter: one launch for all of them)
+    const uint64_t* p[MAX_RANKS];
+    uint64_t off[MAX_RANKS + 1];  // entry offsets; off[n] = total
+    uint32_t n;
+};
+hipError_t launch_rep_scatter(const PropState& ps, uint32_t h, const RepParts& parts, hipStream_t st);
+hipError_t launch_rep_fwd_pack(const PropState& ps, uint8_t* out, hipStream_t st);
+hipError_t launch_rep_fwd_recv(const PropState& ps, const uint8_t* in, hipStream_t st);
+hipError_t launch_rep_sends(const PropState& ps, uint32_t h_run, uint64_t* vcnt, uint64_t* out, hipStream_t st);
+hipError_t launch_rep_sends_recv(const PropState& ps, const uint64_t* in, hipStream_t st);
 hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, bool rescore, const DevPeerParams& pp,
                              hipStream_t st);
 // gray_only: count the sends on pairs whose receiver graylists the sender

@@ -354,6 +354,7 @@ struct gsx_engine {
         bool active = false, sel_done = false;
         uint32_t h = 0;
         uint32_t rows_valid = 1;  // frontier-history rows written (skipped empty hops write none)
+        uint32_t global_last = UINT32_MAX;  // range shards: the last hop delivering on any rank (gsx_prop_set_last_hop)
         gsx_prop_config cfg{};
         std::vector<uint64_t> ids;
         std::vector<uint32_t> vals;  // validation outcomes of this call
@@ -382,13 +383,26 @@ struct gsx_engine {
         bool flast_dirty = true;  // flast may hold a hop-tagged count of an earlier call (cleared before the next)
         // compacted shard exchange: the dense halo the received entries are
         // scattered into, the slots filled last hop, per-destination counts
-        uint64_t* halo = nullptr;
-        uint32_t* halo_idx = nullptr;
-        uint64_t* halo_occ = nullptr;  // bit per receive slot: row received this hop
-        uint64_t* hfrom = nullptr;     // [receive slot][word]: first receipts from the remote sender, latest hop
+        uint64_t* halo = nullptr;      // [receive slot][hop tag | W words] (PropState::halo_tag)
+        uint64_t halo_tag = 0;         // this call's tag base: call serial << 8 (| hop)
+        // replicated frontier (range shards, lean calls; PropState::rep)
+        bool rep = false;
+        uint64_t* front_g = nullptr;   // [2][n_total][W]
+        uint64_t* occ_g = nullptr;     // [2][n_total / 64 + 1]
+        uint64_t* src_bits = nullptr;  // [n_total / 64 + 1]
+        uint64_t rep_words = 0;        // front_g capacity (words)
+        uint32_t* src_ids = nullptr;   // [m] + the origin rows [m][W]
+        uint64_t* src_rows = nullptr;
+        uint64_t src_cap = 0;          // (messages x words)
+        std::vector<uint32_t> h_src_ids;   // (host staging of the two above, alive until the call ends)
+        std::vector<uint64_t> h_src_rows;
+        uint64_t halo_calls = 0;
+        uint32_t* pack_tab = nullptr;  // [pack block][rank] entry counts / offsets (k_pack_front)
+        uint64_t pack_tab_cap = 0;
+        uint64_t* hfrom = nullptr;     // [pair][word]: first receipts from the pair's remote sender, latest hop
         uint64_t* touch = nullptr;     // bit per node: marked by a sender (very sparse hops)
         uint64_t* vcnt = nullptr;      // per node: forwarded-set sizes (late duplicate accounting)
-        uint64_t halo_cap = 0, halo_prev = 0, hfrom_cap = 0;
+        uint64_t halo_cap = 0, hfrom_cap = 0;
         unsigned long long* dcount = nullptr;
     } prop;
     bool prop_track = true;  // gsx_prop_set_tracking: keep first-deliverer rows (gsx_prop_results)
@@ -405,6 +419,10 @@ struct gsx_engine {
     uint32_t* d_pair_obs = nullptr;
     uint32_t* d_halo_node = nullptr;  // per receive slot: local node of its pair
     uint32_t* d_halo_pair = nullptr;  // per receive slot: its local pair (peer exchange)
+    // replicated frontier (PropState::rep): the remote senders' global ids ascending,
+    // and the local receiver of each (k_rep_scatter marks them on very sparse hops)
+    uint32_t* d_rmark_v = nullptr;
+    uint32_t* d_rmark_u = nullptr;
     uint32_t* d_send_slot = nullptr;  // per pair: its send slot, NO_PAIR if none (peer exchange)
     // peer exchange across shards: entries of this round's pack, per destination
     unsigned long long* d_pxs_cnt = nullptr;
@@ -841,11 +859,12 @@ void free_state(gsx_engine* e) {
     void* pp[] = {e->prop.hist, e->prop.origin, e->prop.from,
                   e->prop.sel,  e->prop.fwd,  e->prop.pin,    e->prop.dup,   e->prop.corr,
                   e->prop.first, e->prop.msgs, e->prop.stats, e->d_send_pair, e->d_pair_obs,
-                  e->prop.halo, e->prop.halo_idx, e->prop.dcount, e->d_send_dest, e->d_send_base,
-                  e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.halo_occ, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
+                  e->prop.halo, e->prop.pack_tab, e->prop.dcount, e->d_send_dest, e->d_send_base,
+                  e->d_dest_halo_base, e->prop.fcnt, e->prop.flast, e->prop.hfrom, e->prop.inv, e->prop.vmask, e->prop.dseen,
                   e->prop.touch, e->prop.vcnt, e->d_halo_node, e->prop.occ, e->prop.gray_pairs,
                   e->prop.cent, e->prop.cend, e->prop.chg, e->prop.nchg, e->prop.ndirty, e->prop.rfwd,
-                  e->d_halo_pair, e->d_send_slot,
+                  e->d_halo_pair, e->d_send_slot, e->d_rmark_v, e->d_rmark_u, e->prop.front_g, e->prop.occ_g,
+                  e->prop.src_bits, e->prop.src_ids, e->prop.src_rows,
                   e->prop.d_dig, e->prop.rcand, e->prop.tterm, e->prop.tgen, e->prop.hist_alt, e->prop.occ_alt};
     for (void* p : pp)
         if (p) (void)hipFree(p);
@@ -858,6 +877,7 @@ void free_state(gsx_engine* e) {
     e->prop.d_hop_flag = dhf;
     e->prop.hop_seq = hseq;
     e->d_send_pair = e->d_pair_obs = e->d_halo_node = e->d_halo_pair = e->d_send_slot = nullptr;
+    e->d_rmark_v = e->d_rmark_u = nullptr;
     e->d_send_dest = nullptr;
     e->d_send_base = e->d_dest_halo_base = nullptr;
     e->n_ranks = 1;
@@ -1716,6 +1736,26 @@ int gsx_shard_recv_plan(gsx_engine* e, uint32_t n_ranks, const uint32_t* rank_lo
     if (int rc = dalloc(e, &e->d_halo_pair, hpair.size())) return rc;
     if (!hpair.empty())
         HIPCHK(e, hipMemcpy(e->d_halo_pair, hpair.data(), sizeof(uint32_t) * hpair.size(), hipMemcpyHostToDevice));
+    {  // (remote sender, local receiver) by sender: the replicated frontier's receiver marks
+        std::vector<uint64_t> key(hpair.size());
+        for (size_t k = 0; k < hpair.size(); ++k) key[k] = ((uint64_t)e->col_host[hpair[k]] << 32) | hnode[k];
+        std::sort(key.begin(), key.end());
+        std::vector<uint32_t> mv(key.size()), mu(key.size());
+        for (size_t k = 0; k < key.size(); ++k) {
+            mv[k] = (uint32_t)(key[k] >> 32);
+            mu[k] = (uint32_t)key[k];
+        }
+        for (uint32_t** p : {&e->d_rmark_v, &e->d_rmark_u}) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+        }
+        if (int rc = dalloc(e, &e->d_rmark_v, mv.size())) return rc;
+        if (int rc = dalloc(e, &e->d_rmark_u, mu.size())) return rc;
+        if (!mv.empty()) {
+            HIPCHK(e, hipMemcpy(e->d_rmark_v, mv.data(), 4 * mv.size(), hipMemcpyHostToDevice));
+            HIPCHK(e, hipMemcpy(e->d_rmark_u, mu.data(), 4 * mu.size(), hipMemcpyHostToDevice));
+        }
+    }
     return GSX_OK;
 }
 
@@ -2542,7 +2582,8 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.dseen = P.has_drop ? P.dseen : nullptr;
     ps.reject = P.vmask ? P.vmask + W : nullptr;
     ps.hfrom = P.hfrom;
-    ps.halo_occ = nullptr;
+    ps.halo_tag = 0;
+    ps.send_slot = e->d_send_slot;
     ps.touch = P.touch;
     ps.halo_node = e->d_halo_node;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
@@ -2728,31 +2769,37 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         if (int rc = dalloc(e, &P.from, (size_t)P.words_cap * E)) return rc;
         P.from_words = (size_t)P.words_cap * E;
     }
-    if (e->n_recv) {  // compacted exchange: engine-owned dense halo, empty at the start of a call
-        if (P.halo_cap < (uint64_t)W * e->n_recv || !P.halo_idx) {
+    if (e->n_recv) {  // compacted exchange: engine-owned halo of tagged rows (no clears: a row
+                      // is empty unless its tag is this call's and hop's)
+        if (P.halo_cap < (uint64_t)(W + 1) * e->n_recv) {
             if (P.halo) (void)hipFree(P.halo);
-            if (P.halo_idx) (void)hipFree(P.halo_idx);
             P.halo = nullptr;
-            P.halo_idx = nullptr;
-            int rc = 0;
-            if ((rc = dalloc(e, &P.halo, (size_t)W * e->n_recv)) || (rc = dalloc(e, &P.halo_idx, e->n_recv))) return rc;
-            P.halo_cap = (uint64_t)W * e->n_recv;
+            P.halo_cap = 0;
+            if (int rc = dalloc(e, &P.halo, (size_t)(W + 1) * e->n_recv)) return rc;
+            HIPCHK(e, hipMemsetAsync(P.halo, 0, 8 * (size_t)(W + 1) * e->n_recv, e->stream));  // (tag 0: no call's)
+            P.halo_cap = (uint64_t)(W + 1) * e->n_recv;
         }
-        HIPCHK(e, hipMemsetAsync(P.halo, 0, 8 * (size_t)W * e->n_recv, e->stream));
-        P.halo_prev = 0;
+        P.halo_tag = (uint64_t)(++P.halo_calls) << 8;  // (hops < 256)
     }
-    if (e->n_recv) {  // receive-slot occupancy (compacted exchange) and first receipts per remote sender
-        if (P.hfrom_cap < (uint64_t)W * e->n_recv || !P.halo_occ) {
-            if (P.hfrom) (void)hipFree(P.hfrom);
-            if (P.halo_occ) (void)hipFree(P.halo_occ);
-            P.hfrom = nullptr;
-            P.halo_occ = nullptr;
-            int rc = 0;
-            if ((rc = dalloc(e, &P.hfrom, (size_t)W * e->n_recv)) || (rc = dalloc(e, &P.halo_occ, (e->n_recv + 63) / 64)))
-                return rc;
-            P.hfrom_cap = (uint64_t)W * e->n_recv;
+    if (e->n_send) {  // the compacted pack's per-(block, rank) table
+        const uint64_t words = gsx::pack_table_words((uint32_t)N, e->n_ranks);
+        if (P.pack_tab_cap < words) {
+            if (P.pack_tab) (void)hipFree(P.pack_tab);
+            P.pack_tab = nullptr;
+            P.pack_tab_cap = 0;
+            if (int rc = dalloc(e, &P.pack_tab, std::max<uint64_t>(words, 1))) return rc;
+            P.pack_tab_cap = words;
         }
-        HIPCHK(e, hipMemsetAsync(P.hfrom, 0, 8 * (size_t)W * e->n_recv, e->stream));
+    }
+    if (e->n_recv) {  // first receipts per remote sender, at the receiver's own pair (the pack reads
+                      // them along the sender's row)
+        if (P.hfrom_cap < (uint64_t)W * E) {
+            if (P.hfrom) (void)hipFree(P.hfrom);
+            P.hfrom = nullptr;
+            if (int rc = dalloc(e, &P.hfrom, (size_t)W * E)) return rc;
+            P.hfrom_cap = (uint64_t)W * E;
+        }
+        HIPCHK(e, hipMemsetAsync(P.hfrom, 0, 8 * (size_t)W * E, e->stream));
     }
     if (!P.dcount) {
         if (int rc = dalloc(e, &P.dcount, (size_t)gsx::MAX_RANKS)) return rc;
@@ -2793,10 +2840,70 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         }
     }
     gsx::PropState ps = prop_state(e, W, m, cfg);
+    // Range shards, lean calls: the replicated frontier (PropState::rep) instead
+    // of the per-pair halo (GSX_SHARD_PAIRS=1 keeps the per-pair exchange: A/B)
+    static const bool no_rep = getenv("GSX_SHARD_PAIRS") != nullptr;
+    P.rep = e->sharded() && e->n_ranks > 1 && m > 0 && gsx::hop_lean(ps) && !no_rep &&
+            e->n_total <= gsx::PIN_NODE_MASK;
+    if (P.rep) {
+        const size_t NT = e->n_total, ow = NT / 64 + 1;
+        if (P.rep_words < 2 * (uint64_t)NT * W) {
+            for (uint64_t** p : {&P.front_g, &P.occ_g, &P.src_bits}) {
+                if (*p) (void)hipFree(*p);
+                *p = nullptr;
+            }
+            P.rep_words = 0;
+            int rc = 0;
+            if ((rc = dalloc(e, &P.front_g, 2 * NT * W)) || (rc = dalloc(e, &P.occ_g, 2 * ow)) ||
+                (rc = dalloc(e, &P.src_bits, ow)))
+                return rc;
+            P.rep_words = 2 * (uint64_t)NT * W;
+        }
+        HIPCHK(e, hipMemsetAsync(P.occ_g, 0, 8 * ow, e->stream));  // parity 0: k_rep_init's sources
+        HIPCHK(e, hipMemsetAsync(P.src_bits, 0, 8 * ow, e->stream));
+        // the call's sources, ascending, with their origin rows (a remote receiver's own
+        // messages at the end-of-call accounting, k_rep_sends)
+        std::vector<std::pair<uint32_t, uint32_t>> sk(m);
+        for (size_t k = 0; k < m; ++k) sk[k] = {msgs[k].source, (uint32_t)k};
+        std::sort(sk.begin(), sk.end());
+        P.h_src_ids.clear();
+        P.h_src_rows.clear();
+        for (size_t i = 0; i < m; ++i) {
+            if (P.h_src_ids.empty() || P.h_src_ids.back() != sk[i].first) {
+                P.h_src_ids.push_back(sk[i].first);
+                P.h_src_rows.resize(P.h_src_rows.size() + W, 0);
+            }
+            P.h_src_rows[(P.h_src_ids.size() - 1) * W + sk[i].second / 64] |= 1ull << (sk[i].second % 64);
+        }
+        if (P.src_cap < (uint64_t)m * W || !P.src_ids) {
+            if (P.src_ids) (void)hipFree(P.src_ids);
+            if (P.src_rows) (void)hipFree(P.src_rows);
+            P.src_ids = nullptr;
+            P.src_rows = nullptr;
+            int rc = 0;
+            if ((rc = dalloc(e, &P.src_ids, m)) || (rc = dalloc(e, &P.src_rows, (size_t)m * W))) return rc;
+            P.src_cap = (uint64_t)m * W;
+        }
+        HIPCHK(e, hipMemcpyAsync(P.src_ids, P.h_src_ids.data(), 4 * P.h_src_ids.size(), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(P.src_rows, P.h_src_rows.data(), 8 * P.h_src_rows.size(), hipMemcpyHostToDevice,
+                                 e->stream));
+        ps.rep = 1;
+        ps.n_total = e->n_total;
+        ps.front_g = P.front_g;
+        ps.occ_g = P.occ_g;
+        ps.rmark_v = e->d_rmark_v;
+        ps.rmark_u = e->d_rmark_u;
+        ps.n_rmark = e->n_recv;
+        ps.src_bits = P.src_bits;
+        ps.src_ids = P.src_ids;
+        ps.src_rows = P.src_rows;
+        ps.n_src = (uint32_t)P.h_src_ids.size();
+    }
     P.last = ps;
     P.have_last = true;
     P.cfg = *cfg;
     P.h = 0;
+    P.global_last = UINT32_MAX;
     P.sel_done = false;
     P.ev_used = 0;
     P.launches = 0;
@@ -2849,7 +2956,8 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         // what the changed bytes feed (unsharded: a shard's reverse pairs are its plan's)
         gsx::PropState pf = ps;
         pf.inc = (K.valid && !e->sharded()) ? 1u : 0u;
-        HIPCHK(e, gsx::launch_prop_fwd(pf, ds, e->stream));
+        // (replicated frontier: the remote pins arrive with the senders' fwd bytes, then compaction)
+        HIPCHK(e, gsx::launch_prop_fwd(pf, ds, e->stream, false, !P.rep));
         K.valid = true;
         K.router = cfg->router;
         K.topic = cfg->topic;
@@ -2861,6 +2969,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
         K.graylist_threshold = e->th.graylist_threshold;
     }
     HIPCHK(e, gsx::launch_prop_init(ps, P.hist, e->stream));
+    if (P.rep) HIPCHK(e, gsx::launch_rep_init(ps, e->stream));
     return GSX_OK;
 }
 
@@ -2873,7 +2982,7 @@ int prop_hop(gsx_engine* e, const uint64_t* halo) {
         return GSX_OK;
     }
     ps.halo = halo;
-    ps.halo_occ = (halo && halo == P.halo) ? P.halo_occ : nullptr;  // compacted: rows not received are empty
+    ps.halo_tag = (halo && halo == P.halo) ? P.halo_tag : 0;  // compacted: tagged rows (the dense exchange's are not)
     const uint32_t h = ++P.h;
     ++P.launches;
     hipEvent_t a = nullptr, b = nullptr;
@@ -3129,7 +3238,16 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
         }
     if (set) {  // the copies' validation times: code = arrival hop (gsx.h (D), VcRef)
         const int64_t step = P.cfg.hop_latency_ns + P.cfg.validation_delay_ns;
-        const uint32_t H = P.h;  // hops run (every rank of a range shard runs the same)
+        // the last hop that delivered here: no code of this engine's nodes is later (the
+        // hops launched past it — gsx_propagate's look-ahead, a shard's empty chunk
+        // tail — differ between one engine and shards and hold no copy)
+        // (a range shard told the ranks' last delivering hop takes it: every rank keeps the
+        // same table, so the ranks classify the set's copies alike; not told: every hop run)
+        uint32_t H = 0;
+        if (ps.sharded) H = std::min(P.global_last, P.h);
+        else
+            for (uint32_t h = 1; h <= P.h && h <= GSX_MAX_HOPS; ++h)
+                if (st[gsx::STAT_HOP0 + h]) H = h;
         set->vtime.resize(step > 0 ? H + 1 : 1);
         for (uint32_t h = 0; h < set->vtime.size(); ++h) set->vtime[h] = P.cfg.now_ns + (int64_t)h * step;
         set->n_hop = (uint32_t)set->vtime.size();
@@ -3222,6 +3340,7 @@ int gsx_prop_pack(gsx_engine* e, uint64_t* send) {
     if (!e) return GSX_EINVAL;
     auto& P = e->prop;
     if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (P.rep) return fail(e, GSX_ESTATE, "this call runs the replicated frontier (gsx_prop_rep_*)");
     if (e->n_send && !send) return GSX_EINVAL;
     if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
     const gsx::PropState& ps = P.last;
@@ -3243,6 +3362,7 @@ int gsx_prop_step(gsx_engine* e, const uint64_t* recv, uint64_t* n_new) {
     if (!e) return GSX_EINVAL;
     auto& P = e->prop;
     if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (P.rep) return fail(e, GSX_ESTATE, "this call runs the replicated frontier (gsx_prop_rep_*)");
     if (e->n_recv && !recv) return GSX_EINVAL;
     if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
     if (int rc = prop_hop(e, recv)) return rc;
@@ -3275,6 +3395,7 @@ int pack_compact(gsx_engine* e, uint64_t* out, bool* packed) {
     auto& P = e->prop;
     *packed = false;
     if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (P.rep) return fail(e, GSX_ESTATE, "this call runs the replicated frontier (gsx_prop_rep_*)");
     if (e->n_send && !out) return GSX_EINVAL;
     if (e->n_send && !e->d_dest_halo_base) return fail(e, GSX_ESTATE, "gsx_shard_set_halo_bases first");
     if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
@@ -3289,7 +3410,7 @@ int pack_compact(gsx_engine* e, uint64_t* out, bool* packed) {
     P.sel_done = true;
     HIPCHK(e, hipMemsetAsync(P.dcount, 0, 8 * (size_t)e->n_ranks, e->stream));
     ++P.launches;
-    HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, front_occ, out, P.dcount, e->stream));
+    HIPCHK(e, gsx::launch_prop_pack_compact(ps, front, front_occ, out, P.dcount, P.pack_tab, e->stream));
     HIPCHK(e, hipEventRecord(b, e->stream));
     *packed = true;
     return GSX_OK;
@@ -3326,18 +3447,126 @@ int gsx_prop_step_compact(gsx_engine* e, const uint64_t* entries, uint64_t n_ent
     if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
     const gsx::PropState& ps = P.last;
     if (ps.n_msgs && e->n_recv) {
-        HIPCHK(e, gsx::launch_halo_clear(ps, P.halo, P.halo_idx, P.halo_prev, e->stream));
-        HIPCHK(e, hipMemsetAsync(P.halo_occ, 0, 8 * ((e->n_recv + 63) / 64), e->stream));
-        HIPCHK(e, gsx::launch_halo_scatter(ps, P.halo, entries, n_entries, P.halo_idx, P.halo_occ, P.h + 1, e->stream));
-        P.halo_prev = n_entries;
+        gsx::PropState pt = ps;
+        pt.halo = P.halo;
+        pt.halo_tag = P.halo_tag;
+        HIPCHK(e, gsx::launch_halo_scatter(pt, P.halo, entries, n_entries, P.h + 1, e->stream));
     }
     return gsx_prop_step(e, e->n_recv ? P.halo : nullptr, n_new);
+}
+
+int gsx_prop_set_last_hop(gsx_engine* e, uint32_t last_hop) {
+    if (!e) return GSX_EINVAL;
+    if (!e->prop.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (last_hop > GSX_MAX_HOPS) return fail(e, GSX_ERANGE, "last hop above GSX_MAX_HOPS");
+    e->prop.global_last = last_hop;
+    return GSX_OK;
 }
 
 int gsx_prop_end(gsx_engine* e, gsx_prop_out* out) {
     if (!e || !out) return GSX_EINVAL;
     if (!e->prop.active) return fail(e, GSX_ESTATE, "no propagation in flight");
     return prop_end(e, out);
+}
+
+// ---- range shards, replicated frontier (gsx.h) ----
+namespace {
+int rep_ready(gsx_engine* e, bool before_hops) {
+    auto& P = e->prop;
+    if (!P.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    if (!P.rep) return fail(e, GSX_ESTATE, "this call runs the per-pair exchange (gsx_prop_rep says 0)");
+    if (before_hops && P.h != 0) return fail(e, GSX_ESTATE, "the fwd bytes go before the first hop");
+    return GSX_OK;
+}
+}  // namespace
+
+int gsx_prop_rep(gsx_engine* e, uint32_t* on) {
+    if (!e || !on) return GSX_EINVAL;
+    if (!e->prop.active) return fail(e, GSX_ESTATE, "no propagation in flight");
+    *on = e->prop.rep ? 1u : 0u;
+    return GSX_OK;
+}
+
+int gsx_prop_rep_fwd_pack(gsx_engine* e, uint8_t* out) {
+    if (!e || (e->n_send && !out)) return GSX_EINVAL;
+    if (int rc = rep_ready(e, true)) return rc;
+    HIPCHK(e, gsx::launch_rep_fwd_pack(e->prop.last, out, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_rep_fwd_recv(gsx_engine* e, const uint8_t* in) {
+    if (!e || (e->n_recv && !in)) return GSX_EINVAL;
+    if (int rc = rep_ready(e, true)) return rc;
+    const gsx::PropState& ps = e->prop.last;
+    HIPCHK(e, gsx::launch_rep_fwd_recv(ps, in, e->stream));
+    HIPCHK(e, gsx::launch_prop_compact(ps, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_rep_pack_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts) {
+    if (!e || !out || !d_counts) return GSX_EINVAL;
+    if (int rc = rep_ready(e, false)) return rc;
+    auto& P = e->prop;
+    if (P.h == 0) return fail(e, GSX_ESTATE, "hop 0 is every rank's already: step hop 1 first");
+    hipEvent_t a, b;  // (in the call's hop_kernel_ms, with the hops and the scatters)
+    if (int rc = prop_event_pair(e, &a, &b)) return rc;
+    HIPCHK(e, hipEventRecord(a, e->stream));
+    HIPCHK(e, hipMemsetAsync(P.dcount, 0, 8, e->stream));
+    HIPCHK(e, gsx::launch_rep_pack(P.last, P.h, out, P.dcount, e->stream));
+    HIPCHK(e, gsx::launch_pack_counts(P.dcount, P.stats + gsx::STAT_HOP0 + P.h, 1, d_counts, e->stream));
+    HIPCHK(e, hipEventRecord(b, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_rep_step(gsx_engine* e, uint32_t n_parts, const uint64_t* const* parts, const uint64_t* counts) {
+    if (!e || (n_parts && (!parts || !counts))) return GSX_EINVAL;
+    if (n_parts > gsx::MAX_RANKS) return fail(e, GSX_ERANGE, "more parts than ranks");
+    if (int rc = rep_ready(e, false)) return rc;
+    auto& P = e->prop;
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < n_parts; ++k) {
+        if (counts[k] && !parts[k]) return GSX_EINVAL;
+        total += counts[k];
+    }
+    if (total > (uint64_t)e->n_total) return fail(e, GSX_ERANGE, "more frontier rows than nodes");
+    if (P.h > 0 && P.h < P.cfg.max_hops) {
+        P.last.rep_in = total;  // (hop P.h + 1's marking counts them: mark_hop)
+        if (total) {
+            hipEvent_t a, b;
+            if (int rc = prop_event_pair(e, &a, &b)) return rc;
+            HIPCHK(e, hipEventRecord(a, e->stream));
+            gsx::RepParts rp{};
+            for (uint32_t k = 0; k < n_parts; ++k) {
+                if (!counts[k]) continue;
+                rp.p[rp.n] = parts[k];
+                rp.off[rp.n + 1] = rp.off[rp.n] + counts[k];
+                ++rp.n;
+            }
+            HIPCHK(e, gsx::launch_rep_scatter(P.last, P.h, rp, e->stream));
+            HIPCHK(e, hipEventRecord(b, e->stream));
+        }
+    } else if (total) {
+        return fail(e, GSX_ESTATE, "hop 0's rows need no exchange");
+    } else {
+        P.last.rep_in = 0;
+    }
+    return prop_hop(e, nullptr);
+}
+
+int gsx_prop_rep_sends_pack(gsx_engine* e, uint64_t* out) {
+    if (!e || (e->n_send && !out)) return GSX_EINVAL;
+    if (int rc = rep_ready(e, false)) return rc;
+    auto& P = e->prop;
+    HIPCHK(e, gsx::launch_rep_sends(P.last, P.h, P.vcnt, out, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_rep_sends_recv(gsx_engine* e, const uint64_t* in) {
+    if (!e || (e->n_recv && !in)) return GSX_EINVAL;
+    if (int rc = rep_ready(e, false)) return rc;
+    HIPCHK(e, gsx::launch_rep_sends_recv(e->prop.last, in, e->stream));
+    return GSX_OK;
 }
 
 // Device memory on both sides: the copies stay ordered on the engine's
@@ -5475,6 +5704,10 @@ int gsx_mcache_copy_last(gsx_engine* e, uint64_t* cache_rows, uint64_t* set_rows
     const auto* b = mcache_newest(e);
     if (!b || !b->set) return fail(e, GSX_ESTATE, "no cached gossipsub batch with a message set");
     if (b->set->vc_p > n_planes) return fail(e, GSX_ERANGE, "the set's validation codes need more planes");
+    // a set propagated with the gossip exchange off kept no arrival hops: planes of
+    // zeros would claim every copy validated at now_ns (the merged set must keep none)
+    if (n_planes && !b->set->hops_kept)
+        return fail(e, GSX_ESTATE, "the cached set kept no validation codes (gossip exchange off): copy it with 0 planes");
     if (int rc = vc_fence(e)) return rc;
     const size_t words = (size_t)b->n_words * e->n_nodes;
     HIPCHK(e, hipMemcpyAsync(cache_rows, b->d_seen, 8 * words, hipMemcpyDeviceToDevice, e->stream));

@@ -1136,10 +1136,13 @@ __device__ __forceinline__ bool gxf_fent_ready(const GxFwd& f, uint32_t hop, uin
 // eligible-sender lists gather it): a run of small frontiers (the light
 // heartbeat rounds) evaluates its few senders' slots in place and never
 // pays the pass.  Every other hop returns at once.
+// A dense hop always finds fout computed (its k_gxf_mark builds the lists
+// from it), whatever fout_lazy is: on tiny overlays n / dense_div can fall
+// below fout_lazy's floor of one node.
 __device__ __forceinline__ bool gxf_fout_ready(const GxFwd& f, uint32_t hop, uint32_t n) {
     if (!f.fout_lazy) return true;
     for (uint32_t z = 1; z <= hop; ++z)
-        if (f.fcnt[z - 1] > f.fout_lazy) return true;
+        if (f.fcnt[z - 1] > f.fout_lazy || gxf_dense(f, z, n)) return true;
     return false;
 }
 __global__ __launch_bounds__(256) void k_gxf_fout_pre(DevState s, HbState h, GxFwd f, uint32_t hop) {

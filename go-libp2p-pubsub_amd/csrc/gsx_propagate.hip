@@ -105,14 +105,15 @@ __device__ __forceinline__ uint32_t pin_of(const PropState& ps, uint64_t q) {
     if (r != NO_PAIR) {
         if (r & HALO) {
             // remote v: its rank packs what it sends either way; u counts the
-            // copies it drops (k_prop_hop)
-            out = gin ? (r | HALO_GRAY) : r;
+            // copies it drops (k_prop_hop).  (Replicated frontier: the pin comes
+            // with v's fwd byte, k_rep_fwd_recv.)
+            out = ps.rep ? NO_PAIR : gin ? (r | HALO_GRAY) : r;
         } else {
             const uint8_t fw = ps.fwd[r];
             rf = fw;
             if (!gin && (fw & FWD_SEND))
                 out = ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | ((fw & FWD_GIN) ? PIN_RDROP : 0u) |
-                      ((uint32_t)ps.col[q] - ps.node_lo);
+                      ((uint32_t)ps.col[q] - (ps.rep ? 0u : ps.node_lo));  // (replicated frontier: global ids)
         }
     }
     ps.rfwd[q] = rf;
@@ -297,6 +298,45 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
     }
 }
 
+// Very sparse hops (at most n/16 first receipts last hop): the frontier
+// pushes "you have a sender" bits to its neighbours, so the hop kernel
+// skips every other node with one bitmap load instead of walking its pairs.
+// The touch bitmap was cleared before this hop (and before the halo scatter,
+// which marks the receivers of remote rows).
+__device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
+    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
+    // (replicated frontier: the remote rows of the hop mark their receivers too)
+    if (ps.rep) return prev + (h >= 2 ? ps.rep_in : 0) < ps.n_nodes / 16;
+    return prev < ps.n_nodes / 16 && !(ps.halo && !ps.halo_tag);
+}
+// Range shards: can a remote sender's row reach this hop?  The compacted
+// exchange counts the hop's scattered entries (STAT_HALO0); the dense one
+// (every cross pair's row, untagged) always may.
+__device__ __forceinline__ bool halo_rows(const PropState& ps, uint32_t h) {
+    return ps.halo && (!ps.halo_tag || ps.stats[STAT_HALO0 + h] != 0);
+}
+// A remote sender's row of hop h, words w0 .. w0 + CW: the compacted
+// exchange's tagged row (empty unless its tag is this hop's), or the dense
+// exchange's row as received.
+template <int CW>
+__device__ __forceinline__ void halo_row(const PropState& ps, uint32_t slot, uint32_t h, uint32_t w0,
+                                         uint64_t (&c)[CW]) {
+    const uint32_t W = ps.n_words;
+    if (ps.halo_tag) {
+        const uint64_t* r = ps.halo + (size_t)slot * (W + 1);
+        if (CW == 1 && W == 1) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(r);
+            c[0] = x.x == (ps.halo_tag | h) ? x.y : 0ull;
+            return;
+        }
+        const bool live = r[0] == (ps.halo_tag | h);
+#pragma unroll
+        for (int i = 0; i < CW; ++i) c[i] = live ? r[1 + w0 + i] : 0ull;
+    } else {
+#pragma unroll
+        for (int i = 0; i < CW; ++i) c[i] = ps.halo[(size_t)slot * W + w0 + i];
+    }
+}
 // ---- shard exchange: pack what each cross-shard pair (v -> u) sends ---------------
 // One thread per send slot (the order the receiving rank asked for).  The
 // receiver applies only its own origin mask; eligibility, RandomSub draws
@@ -316,7 +356,7 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
         const uint8_t fw = ps.fwd[r];
         // messages v first got from u at the frontier's hop (u is remote: the
         // receive slot of pair r), never sent back (floodsub.go:82)
-        const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
+        const uint64_t* hf = ps.hfrom + (size_t)r * W;  // (v's own pair for u: hfrom is per pair)
         for (uint32_t w = 0; w < W; ++w) {
             const uint64_t f = front[(size_t)v * W + w];
             uint64_t c = 0;
@@ -336,105 +376,140 @@ __global__ __launch_bounds__(256) void k_prop_pack(PropState ps, const uint64_t*
 }
 
 // Compacted exchange: only the non-empty rows travel, as entries
-// [halo slot at the receiver][W words].  Each destination rank d owns the
-// entry range of its dense send segment (send_base[d] .. +send_count[d]); a
-// block counts its non-empty rows per destination in LDS, reserves space with
-// one global atomic per (block, destination), and writes the entries.  The
-// order of entries is not deterministic, but each carries its slot, and the
-// receiver only scatters them (k_halo_scatter), so the hop is.
-__global__ __launch_bounds__(256) void k_prop_pack_compact(PropState ps, const uint64_t* __restrict__ front,
-                                                           const uint64_t* __restrict__ front_occ,
-                                                           uint64_t* __restrict__ out, unsigned long long* __restrict__ dcount) {
-    __shared__ uint32_t cnt[MAX_RANKS], base[MAX_RANKS];
+// [halo slot at the receiver][W words]; each destination rank d owns the
+// entry range of its dense send segment (send_base[d] .. +send_count[d]).
+// The pack walks the hop's FRONTIER, not the send slots: a node whose
+// frontier row is empty (one occupancy bit; a wave of 64 nodes per word) costs
+// nothing, so the sparse first and last hops of a call pack in microseconds.
+// Two passes over the same nodes: k_pack_front<false> counts each block's
+// entries per destination (LDS counters), k_pack_scan turns the counts into
+// per-(block, destination) offsets and the destinations' totals (dcount),
+// k_pack_front<true> recomputes the rows (cache-hot) and writes each entry at
+// its block's offset plus a position from an LDS counter.  The order of the
+// entries inside a block's range is not deterministic, but each carries its
+// slot and the receiver only scatters them (k_halo_scatter), so the hop is.
+constexpr uint32_t PACK_NPB = 256;  // nodes per block (few: the walk is a chain of dependent loads, latency-bound)
+constexpr uint32_t PACK_G = 4;       // lanes per node
+static inline uint32_t pack_blocks(uint32_t n_nodes) { return (n_nodes + PACK_NPB - 1) / PACK_NPB; }
+
+// What pair r = (v -> u), u remote, sends at this hop, word w (0: nothing):
+// v's frontier through the pair's eligibility (and RandomSub's draw), minus
+// what v first got from u (floodsub.go:82; hfrom of r, v's own pair for u).
+__device__ __forceinline__ uint64_t pack_word(const PropState& ps, const uint64_t* __restrict__ front, uint32_t v,
+                                              bool v_src, uint64_t r, uint8_t fw, const uint64_t* __restrict__ hf,
+                                              uint32_t w, uint64_t* elig_send) {
     const uint32_t W = ps.n_words;
-    unsigned long long nsend[1] = {0};
-    for (uint64_t j0 = (uint64_t)blockIdx.x * 256u; j0 < ps.n_send; j0 += (uint64_t)gridDim.x * 256u) {
-        const uint64_t j = j0 + threadIdx.x;
-        if (threadIdx.x < ps.n_ranks) cnt[threadIdx.x] = 0;
-        __syncthreads();
-        bool nz = false;
-        uint32_t d = 0, pos = 0;
-        uint32_t r = NO_PAIR, v = 0;
-        uint8_t fw = 0;
-        if (j < ps.n_send) {
-            r = ps.send_pair[j];
-            d = ps.send_dest[j];
-            if (r != NO_PAIR) v = ps.pair_obs[r];
-            if (r != NO_PAIR && occ_bit(front_occ, v)) {
-                fw = ps.fwd[r];
-                const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
-                for (uint32_t w = 0; w < W; ++w) {
-                    const uint64_t f = front[(size_t)v * W + w];
-                    if (!f) continue;
-                    uint64_t el = elig_word(fw, occ_bit(ps.occ, v) ? ps.origin[(size_t)v * W + w] : 0);
-                    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
-                    uint64_t c = f & el;
-                    nsend[0] += c != 0;
-                    if (c) c &= ~hf[w];
-                    nz |= c != 0;
-                }
-            }
-            if (nz) pos = atomicAdd(&cnt[d], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < ps.n_ranks && cnt[threadIdx.x])
-            base[threadIdx.x] = (uint32_t)atomicAdd(&dcount[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
-        __syncthreads();
-        if (nz) {  // recompute the row (its inputs are cache-hot) and write the entry
-            uint64_t* e = out + (ps.send_base[d] + base[d] + pos) * (uint64_t)(W + 1);
-            e[0] = ps.dest_halo_base[d] + (j - ps.send_base[d]);
-            const uint64_t* hf = ps.hfrom + (size_t)(ps.rev[r] & ~HALO) * W;
-            for (uint32_t w = 0; w < W; ++w) {
-                const uint64_t f = front[(size_t)v * W + w];
-                uint64_t c = 0;
-                if (f) {
-                    uint64_t el = elig_word(fw, occ_bit(ps.occ, v) ? ps.origin[(size_t)v * W + w] : 0);
-                    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
-                    c = f & el & ~hf[w];
-                }
-                e[1 + w] = c;
-            }
-        }
-        __syncthreads();  // cnt / base are reused by the next chunk
-    }
-    const uint32_t slot[1] = {STAT_EDGE_SENDS};
-    block_count<1>(nsend, ps.stats, slot);
+    const uint64_t f = front[(size_t)v * W + w];
+    if (!f) return 0;
+    uint64_t el = elig_word(fw, v_src ? ps.origin[(size_t)v * W + w] : 0);
+    if (ps.sel) el |= ps.sel[(size_t)r * W + w];
+    const uint64_t c = f & el;
+    if (elig_send) *elig_send += c != 0;
+    return c & ~hf[w];
 }
 
-// Receiver: clear the halo rows the previous hop filled, then scatter this
-// hop's entries into the dense halo (every slot not received stays empty).
-__global__ __launch_bounds__(256) void k_halo_clear(PropState ps, uint64_t* __restrict__ halo,
-                                                    const uint32_t* __restrict__ idx, uint64_t n) {
-    const uint32_t W = ps.n_words;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
-        for (uint32_t w = 0; w < W; ++w) halo[(size_t)idx[i] * W + w] = 0;
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_pack_front(PropState ps, const uint64_t* __restrict__ front,
+                                                    const uint64_t* __restrict__ front_occ, uint32_t* __restrict__ tab,
+                                                    uint64_t* __restrict__ out) {
+    __shared__ uint32_t cnt[MAX_RANKS];
+    __shared__ uint64_t base[MAX_RANKS];  // WRITE: this block's first entry per destination
+    const uint32_t W = ps.n_words, R = ps.n_ranks;
+    const uint32_t b = blockIdx.x;
+    if (threadIdx.x < R) {
+        cnt[threadIdx.x] = 0;
+        if (WRITE) base[threadIdx.x] = ps.send_base[threadIdx.x] + tab[(size_t)b * R + threadIdx.x];
+    }
+    __syncthreads();
+    uint64_t nsend = 0;
+    const uint32_t u0 = b * PACK_NPB;
+    // PACK_G lanes per node split its pairs (lane c: pairs c, c + PACK_G, ...), so a
+    // node's per-pair reads (rev, send_slot, fwd, hfrom) are adjacent across its lanes
+    const uint32_t gi = threadIdx.x / PACK_G, lc = threadIdx.x % PACK_G;
+    for (uint32_t v = u0 + gi; v < u0 + PACK_NPB && v < ps.n_nodes; v += 256 / PACK_G) {
+        if (!occ_bit(front_occ, v)) continue;  // v received nothing last hop (the whole wave, usually)
+        const bool v_src = occ_bit(ps.occ, v);
+        for (int64_t r = ps.row_ptr[v] + lc; r < ps.row_ptr[v + 1]; r += PACK_G) {
+            const uint32_t rv = ps.rev[r];
+            if (rv == NO_PAIR || !(rv & HALO)) continue;  // a local receiver pulls v's row itself
+            const uint32_t j = ps.send_slot[r];
+            if (j == NO_PAIR) continue;  // nobody asked for the pair (no reverse pair at u)
+            const uint8_t fw = ps.fwd[r];
+            if (!(fw & FWD_SEND)) continue;
+            const uint64_t* hf = ps.hfrom + (size_t)r * W;
+            bool nz = false;
+            for (uint32_t w = 0; w < W; ++w) nz |= pack_word(ps, front, v, v_src, r, fw, hf, w, WRITE ? nullptr : &nsend) != 0;
+            if (!nz) continue;
+            const uint32_t d = ps.send_dest[j];
+            const uint32_t pos = atomicAdd(&cnt[d], 1u);
+            if (WRITE) {
+                uint64_t* e = out + (base[d] + pos) * (uint64_t)(W + 1);
+                e[0] = ps.dest_halo_base[d] + (j - ps.send_base[d]);
+                for (uint32_t w = 0; w < W; ++w) e[1 + w] = pack_word(ps, front, v, v_src, r, fw, hf, w, nullptr);
+            }
+        }
+    }
+    if (!WRITE) {
+        __syncthreads();
+        if (threadIdx.x < R) tab[(size_t)b * R + threadIdx.x] = cnt[threadIdx.x];
+        unsigned long long c1[1] = {nsend};
+        const uint32_t slot[1] = {STAT_EDGE_SENDS};
+        block_count<1>(c1, ps.stats, slot);
+    }
 }
+// Per destination (one block each): exclusive scan of the blocks' counts in
+// place, the destination's total into dcount[d].
+__global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restrict__ tab, uint32_t n_blocks, uint32_t R,
+                                                    unsigned long long* __restrict__ dcount) {
+    __shared__ uint32_t part[1024];
+    const uint32_t d = blockIdx.x;
+    uint64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 1024) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t x = b < n_blocks ? tab[(size_t)b * R + d] : 0u;
+        part[threadIdx.x] = x;
+        __syncthreads();
+        for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+            const uint32_t y = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] += y;
+            __syncthreads();
+        }
+        if (b < n_blocks) tab[(size_t)b * R + d] = (uint32_t)(carry + part[threadIdx.x] - x);
+        carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dcount[d] = carry;
+}
+
+// Receiver (compacted exchange): each entry's row goes to its receive slot
+// as [hop tag | W words] (PropState::halo_tag); a row whose tag is not the
+// hop's is empty, so nothing is cleared between hops or calls.  On a hop the
+// receivers will mark (mark_hop), the entries also mark their receivers.
 __global__ __launch_bounds__(256) void k_halo_scatter(PropState ps, uint64_t* __restrict__ halo,
-                                                      const uint64_t* __restrict__ ent, uint64_t n,
-                                                      uint32_t* __restrict__ idx, uint64_t* __restrict__ halo_occ,
-                                                      uint32_t h) {
+                                                      const uint64_t* __restrict__ ent, uint64_t n, uint32_t h) {
     const uint32_t W = ps.n_words;
+    const uint64_t tag = ps.halo_tag | h;
+    const bool mark = mark_hop(ps, h);
     uint64_t* touch = ps.touch + (size_t)(h & 1) * (((size_t)ps.n_nodes + 63) / 64);  // the coming hop h's buffer
+    if (blockIdx.x == 0 && threadIdx.x == 0) ps.stats[STAT_HALO0 + h] = n;  // (launched only for n > 0)
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
         const uint64_t* e = ent + i * (uint64_t)(W + 1);
         const uint32_t slot = (uint32_t)e[0];
-        idx[i] = slot;
-        for (uint32_t w = 0; w < W; ++w) halo[(size_t)slot * W + w] = e[1 + w];
-        atomicOr((unsigned long long*)&halo_occ[slot / 64], 1ull << (slot % 64));  // occupancy (cleared per hop)
-        const uint32_t u = ps.halo_node[slot];
-        atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));  // u has a sender this hop
+        uint64_t* r = halo + (size_t)slot * (W + 1);
+        if (W == 1) {
+            *reinterpret_cast<ulonglong2*>(r) = make_ulonglong2(tag, e[1]);  // (16-B aligned rows)
+        } else {
+            r[0] = tag;
+            for (uint32_t w = 0; w < W; ++w) r[1 + w] = e[1 + w];
+        }
+        if (mark) {
+            const uint32_t u = ps.halo_node[slot];
+            atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));  // u has a sender this hop
+        }
     }
 }
 
-// Very sparse hops (at most n/16 first receipts last hop): the frontier
-// pushes "you have a sender" bits to its neighbours, so the hop kernel
-// skips every other node with one bitmap load instead of walking its pairs.
-// The touch bitmap was cleared before this hop (and before the halo scatter,
-// which marks the receivers of remote rows).
-__device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
-    const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
-    return prev < ps.n_nodes / 16 && !(ps.halo && !ps.halo_occ);
-}
 __global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, const uint64_t* __restrict__ front_occ) {
     // housekeeping of this hop: its occupancy row (the hop ORs bits in) and
     // the other touch buffer (the next hop's, marked by its halo scatter and
@@ -445,6 +520,11 @@ __global__ __launch_bounds__(256) void k_prop_mark(PropState ps, uint32_t h, con
     for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < occ_row; i += (size_t)gridDim.x * 256u) {
         occ_h[i] = 0;
         touch_next[i] = 0;
+    }
+    if (ps.rep) {  // the replicated rows of hop h: this hop writes this rank's part, k_rep_scatter the rest
+        const size_t og_row = ((size_t)ps.n_total + 63) / 64 + 1;
+        uint64_t* og = ps.occ_g + (size_t)(h & 1) * og_row;
+        for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < og_row; i += (size_t)gridDim.x * 256u) og[i] = 0;
     }
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     if (ps.hop_flag && blockIdx.x == 0 && threadIdx.x == 0)  // hop h - 1 is complete: tell the launching host
@@ -507,12 +587,28 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
     return x;
 }
 
-// The common case as its own lean kernel (k_prop_hop_fast): one engine (no
-// halo), no RandomSub draws, no first-deliverer rows, and late duplicate
-// accounting (every duplicate inside the P3 window, or no credits), so the
-// hop only moves first receipts: per pair and word, eligibility, "not seen,
-// not from a lower sender", and a popcount.  Same results as k_prop_hop.
-template <int CW, int LPN, bool DROP>
+// Bits of up to 64 consecutive nodes starting at global node g0 into a
+// global occupancy row (g0 need not be 64-aligned: a shard's range starts
+// anywhere; the row has one spare word).
+__device__ __forceinline__ void occ_g_or(uint64_t* og, uint32_t g0, uint64_t bits) {
+    const uint32_t sh = g0 % 64;
+    atomicOr((unsigned long long*)&og[g0 / 64], (unsigned long long)(bits << sh));
+    if (sh && (bits >> (64 - sh))) atomicOr((unsigned long long*)&og[g0 / 64 + 1], (unsigned long long)(bits >> (64 - sh)));
+}
+
+// The common case as its own lean kernel (k_prop_hop_fast): no RandomSub
+// draws, no first-deliverer rows, and late duplicate accounting (every
+// duplicate inside the P3 window, or no credits), so the hop only moves
+// first receipts: per pair and word, eligibility, "not seen, not from a lower
+// sender", and a popcount.  Same results as k_prop_hop.
+// SH (range shards): a compacted sender may be remote (pin HALO | slot): its
+// row comes from the halo, already filtered by the sender's rank (eligibility
+// and the `from` exclusion, k_prop_pack[_compact]); u masks its own messages
+// off it, its copies are counted as duplicates here (k_prop_dups sees only
+// local senders), a graylisted one's copies as STAT_GRAY, and its first
+// receipts go to hfrom for u's own pack.  A hop with no local frontier still
+// runs while remote rows arrived (halo_rows).
+template <int CW, int LPN, bool DROP, int SH>
 __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                        uint64_t* __restrict__ nxt) {
     constexpr int U = GSX_FAST_U;
@@ -524,15 +620,22 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
     const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
-    if (h > 1 && prev == 0) return;
-    // (hop 1 always: the rows of hop 0 are written for the sources only)
-    const bool use_occ = h == 1 || prev < ps.n_nodes / 4;
+    if (h > 1 && prev == 0 && !(SH == 1 && halo_rows(ps, h)) && !(SH == 2 && ps.rep_in)) return;
+    // (hop 1 always: the rows of hop 0 are written for the sources only; the
+    // replicated rows always: a remote row is valid only under its bit)
+    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / 4;
     const bool use_mark = mark_hop(ps, h);
     // rows of hop h - 1 can be stale only if that hop left nodes untouched
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
     const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
+    // SH == 2: the replicated rows of hop h - 1 (read) and h (this rank's part written)
+    const size_t occ_g_row = ((size_t)ps.n_total + 63) / 64 + 1;
+    const uint64_t* __restrict__ rg_front = SH == 2 ? ps.front_g + (size_t)((h - 1) & 1) * ps.n_total * W : nullptr;
+    const uint64_t* __restrict__ og_front = SH == 2 ? ps.occ_g + (size_t)((h - 1) & 1) * occ_g_row : nullptr;
+    uint64_t* __restrict__ rg_nxt = SH == 2 ? ps.front_g + (size_t)(h & 1) * ps.n_total * W : nullptr;
+    uint64_t* __restrict__ og_nxt = SH == 2 ? ps.occ_g + (size_t)(h & 1) * occ_g_row : nullptr;
     const uint32_t gi = threadIdx.x / LPN, lc = threadIdx.x % LPN;
-    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0;
+    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0, n_dup = 0, n_gray = 0;
     for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
         const uint32_t u = tile + gi;
         bool any_new = false;
@@ -542,17 +645,22 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
             // only the pairs whose neighbour sends to u at all (compacted, k_prop_compact)
             const int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
             const size_t un = (size_t)u * W;
-            // (u's own messages need no mask here: they are in `seen` since
-            // hop 0, and duplicates are counted at the end of the call)
+            // (u's own messages need no mask for local senders: they are in `seen`
+            // since hop 0, and those duplicates are counted at the end of the call)
+            const bool u_src = SH == 1 && occ_bit(occ_src, u);
             for (uint32_t w0 = lc * CW; w0 < W; w0 += LPN * CW) {
-                uint64_t seen[CW], sa[CW], drp[CW], rej[CW];
+                uint64_t seen[CW], sa[CW], drp[CW], rej[CW], mine[CW];
                 load_words<CW>(seen, ps.seen + un + w0);
                 if (DROP) {  // messages validation does not accept: seen, not delivered, not forwarded
                     load_words<CW>(drp, ps.drop + w0);
                     load_words<CW>(rej, ps.reject + w0);
                 }
 #pragma unroll
-                for (int i = 0; i < CW; ++i) sa[i] = seen[i];
+                for (int i = 0; i < CW; ++i) {
+                    sa[i] = seen[i];
+                    mine[i] = 0;
+                }
+                if (SH == 1 && u_src) load_words<CW>(mine, ps.origin + un + w0);
                 uint2 pn[U];
 #pragma unroll
                 for (int j = 0; j < U; ++j) pn[j] = q0 + j < q1 ? ps.cent[q0 + j] : make_uint2(NO_PAIR, 0u);
@@ -563,28 +671,46 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                     for (int j = 0; j < U; ++j) {
                         pv[j] = pn[j].x;
                         qv[j] = pn[j].y;
-                        if (use_occ && pv[j] != NO_PAIR && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK)) pv[j] = NO_PAIR;
+                        // (a remote row's own tag says whether it arrived this hop: halo_row)
+                        if (use_occ && pv[j] != NO_PAIR && !(SH == 1 && (pv[j] & HALO)) &&
+                            !occ_bit(SH == 2 ? og_front : occ_front, pv[j] & PIN_NODE_MASK))
+                            pv[j] = NO_PAIR;
                     }
 #pragma unroll
                     for (int j = 0; j < U; ++j) {
-                        if (pv[j] != NO_PAIR) load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
-                        else
+                        if (pv[j] == NO_PAIR) {
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] = 0;
+                        } else if (SH == 1 && (pv[j] & HALO)) {
+                            halo_row<CW>(ps, pv[j] & HALO_SLOT, h, w0, c[j]);
+                        } else {
+                            load_words<CW>(c[j], (SH == 2 ? rg_front : front) + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
+                        }
                     }
 #pragma unroll
                     for (int j = 0; j < U; ++j) pn[j] = qb + U + j < q1 ? ps.cent[qb + U + j] : make_uint2(NO_PAIR, 0u);
                     if (check_rows)
 #pragma unroll
                         for (int j = 0; j < U; ++j)
-                            if (pv[j] != NO_PAIR && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK))
+                            if (pv[j] != NO_PAIR && !(SH == 1 && (pv[j] & HALO)) && !occ_bit(occ_front, pv[j] & PIN_NODE_MASK))
 #pragma unroll
                                 for (int i = 0; i < CW; ++i) c[j][i] = 0;
 #pragma unroll
                     for (int j = 0; j < U; ++j) {
                         if (__ballot(pv[j] != NO_PAIR) == 0) continue;  // no lane of the wave has pair j
+                        // (the same in every lane of a group: the group walks pair j together)
+                        const bool hl = SH == 1 && pv[j] != NO_PAIR && (pv[j] & HALO);
                         // branch-free over the lanes: an absent pair carries an empty row
-                        const uint32_t m = pv[j] == NO_PAIR ? 0u : pv[j] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
+                        uint32_t m = (pv[j] == NO_PAIR || hl) ? 0u : pv[j] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
+                        if (SH == 2) {
+                            // a sender's row of hop h - 1 holds only what it published (h = 1) or
+                            // only what it received (h >= 2), so the pair lets it through whole
+                            // or not at all: PUBLISH at hop 1, FORWARD after (elig_word on that row)
+                            const bool pass = (m & (h == 1 ? FWD_PUBLISH : FWD_FORWARD)) != 0;
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] = pass ? c[j][i] : 0ull;
+                            m = 0;  // (no origin row to read)
+                        }
                         // eligibility: FORWARD lets through what v received, PUBLISH what v
                         // published.  An absent pair's row is empty and a FORWARD|PUBLISH pair
                         // passes everything, so only a wave holding a one-sided pair masks.
@@ -595,16 +721,31 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                             const uint32_t v = pv[j] & PIN_NODE_MASK;
                             if ((m == FWD_FORWARD || m == FWD_PUBLISH) && occ_bit(occ_src, v))
                                 load_words<CW>(own, ps.origin + (size_t)v * W + w0);
-                            const uint64_t fmask = (m & FWD_FORWARD) ? ~0ull : 0ull, pmask = (m & FWD_PUBLISH) ? ~0ull : 0ull;
+                            // (a remote sender's row is filtered already: it passes whole)
+                            const uint64_t fmask = (hl || (m & FWD_FORWARD)) ? ~0ull : 0ull;
+                            const uint64_t pmask = (hl || (m & FWD_PUBLISH)) ? ~0ull : 0ull;
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] &= (fmask & ~own[i]) | (pmask & own[i]);
                         }
-                        uint32_t fresh = 0, inv = 0;
+                        if (SH == 1 && hl) {  // never sent back to the origin; AcceptFrom drops a graylisted sender's
+#pragma unroll
+                            for (int i = 0; i < CW; ++i) c[j][i] &= ~mine[i];
+                            if (pv[j] & HALO_GRAY) {
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) {
+                                    n_gray += __popcll(c[j][i]);
+                                    c[j][i] = 0;
+                                }
+                            }
+                        }
+                        uint32_t fresh = 0, inv = 0, pc = 0;
+                        uint64_t nbs[CW];
 #pragma unroll
                         for (int i = 0; i < CW; ++i) {
                             const uint64_t cc = c[j][i];
-                            n_send += cc != 0;
+                            if (!hl) n_send += cc != 0;  // (a remote sender's are counted at its pack)
                             const uint64_t nb = cc & ~sa[i];  // not seen, not from a lower sender
+                            nbs[i] = nb;
                             sa[i] |= nb;
                             if (DROP) {
                                 const uint64_t dv = nb & drp[i];
@@ -612,13 +753,31 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                                 n_ign += __popcll(dv & ~rej[i]);
                                 inv += __popcll(dv & rej[i]);
                                 fresh += __popcll(nb & ~drp[i]);
+                                if (SH == 1) pc += __popcll(cc & ~drp[i]);
                             } else {
                                 fresh += __popcll(nb);
+                                if (SH == 1) pc += __popcll(cc);
                             }
                         }
                         n_new += fresh;
+                        uint32_t dup = 0;
+                        if (SH == 1) {
+                            dup = hl ? pc - fresh : 0u;  // a remote sender's duplicates, this hop
+                            n_dup += dup;
+                            if (hl) {  // what u must not send back to it (k_prop_pack)
+                                bool rx = false;
+#pragma unroll
+                                for (int i = 0; i < CW; ++i) rx |= nbs[i] != 0;
+                                if (rx) {
+                                    uint64_t* hf = ps.hfrom + (size_t)qv[j] * W + w0;
+#pragma unroll
+                                    for (int i = 0; i < CW; ++i) hf[i] = nbs[i];
+                                }
+                            }
+                        }
                         if (LPN > 1) fresh = group_sum<LPN>(fresh);
                         if (DROP && LPN > 1) inv = group_sum<LPN>(inv);
+                        if (SH == 1 && LPN > 1) dup = group_sum<LPN>(dup);
                         if (lc == 0 && fresh) {
                             // first receipts from the pair: an add at L2, nothing read back
                             // (every pair has one writer per hop, but no load round trip)
@@ -630,6 +789,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                             if (h == ps.max_hops || ps.flast_every)
                                 ps.flast[q] = last_count(ps, q, h, fresh, W > LPN * CW);
                         }
+                        if (SH == 1 && lc == 0 && dup && ps.credit) ps.dupcnt[qv[j]] += dup;  // (one writer per pair)
                         if (DROP && lc == 0 && inv && ps.credit) ps.invcnt[qv[j]] += inv;  // P4
                     }
                 }
@@ -638,6 +798,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
                     const uint64_t acc = sa[i] ^ seen[i];
                     const uint64_t fwd_row = DROP ? acc & ~drp[i] : acc;
                     nxt[un + w0 + i] = fwd_row;
+                    if (SH == 2) rg_nxt[(size_t)(ps.node_lo + u) * W + w0 + i] = fwd_row;  // (this rank's part)
                     if (acc) {
                         ps.seen[un + w0 + i] = sa[i];
                         ++n_vnew;
@@ -655,11 +816,21 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
             wb = r;
         }
         const uint32_t u0 = tile + (threadIdx.x / 64) * NW;
-        if ((threadIdx.x & 63) == 0 && wb) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
+        if ((threadIdx.x & 63) == 0 && wb) {
+            atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(wb << (u0 % 64)));
+            if (SH == 2) occ_g_or(og_nxt, ps.node_lo + u0, wb);
+        }
     }
-    unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
-    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
-    block_count<5>(cnt, ps.stats, slot);
+    if (SH == 1) {
+        unsigned long long cnt[7] = {n_new, n_send, n_vnew, n_rej, n_ign, n_dup, n_gray};
+        const uint32_t slot[7] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED,
+                                  STAT_DUPS, STAT_GRAY};
+        block_count<7>(cnt, ps.stats, slot);
+    } else {
+        unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
+        const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
+        block_count<5>(cnt, ps.stats, slot);
+    }
 }
 
 // k_prop_hop_fast for one-word rows (64-message calls): a group of 4 lanes
@@ -667,8 +838,9 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
 // 4, ...) instead of row words, two rounds of 4 in flight.  The group reads
 // 4 consecutive sender entries at once and runs to the longest of 16 nodes
 // per wave instead of 64; "not from a lower sender" becomes an exclusive
-// prefix-OR over the quad.  Same results as k_prop_hop_fast<1, 1, DROP>.
-template <bool DROP, int G, int R>  // lanes per node, rounds of G senders in flight
+// prefix-OR over the quad.  Same results as k_prop_hop_fast<1, 1, DROP, SH>
+// (SH: remote senders through the halo, as there).
+template <bool DROP, int G, int R, int SH>  // lanes per node, rounds of G senders in flight
 __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h, const uint64_t* __restrict__ front,
                                                         uint64_t* __restrict__ nxt) {
     constexpr uint32_t NB = 256 / G, NW = 64 / G;
@@ -677,14 +849,19 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
     const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
-    if (h > 1 && prev == 0) return;
-    const bool use_occ = h == 1 || prev < ps.n_nodes / 4;
+    if (h > 1 && prev == 0 && !(SH == 1 && halo_rows(ps, h)) && !(SH == 2 && ps.rep_in)) return;
+    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / 4;
     const bool use_mark = mark_hop(ps, h);
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
     const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
+    const size_t occ_g_row = ((size_t)ps.n_total + 63) / 64 + 1;
+    const uint64_t* __restrict__ rg_front = SH == 2 ? ps.front_g + (size_t)((h - 1) & 1) * ps.n_total : nullptr;
+    const uint64_t* __restrict__ og_front = SH == 2 ? ps.occ_g + (size_t)((h - 1) & 1) * occ_g_row : nullptr;
+    uint64_t* __restrict__ rg_nxt = SH == 2 ? ps.front_g + (size_t)(h & 1) * ps.n_total : nullptr;
+    uint64_t* __restrict__ og_nxt = SH == 2 ? ps.occ_g + (size_t)(h & 1) * occ_g_row : nullptr;
     const uint32_t gi = threadIdx.x / G, lc = threadIdx.x % G;
     const uint64_t drp = DROP ? ps.drop[0] : 0ull, rej = DROP ? ps.reject[0] : 0ull;
-    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0;
+    unsigned long long n_new = 0, n_send = 0, n_vnew = 0, n_rej = 0, n_ign = 0, n_dup = 0, n_gray = 0;
     for (uint32_t tile = blockIdx.x * NB; tile < ps.n_nodes; tile += gridDim.x * NB) {
         const uint32_t u = tile + gi;
         bool any_new = false;
@@ -693,6 +870,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
         if (touch) {
             const int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
             const uint64_t seen = ps.seen[u];
+            const uint64_t mine = (SH == 1 && occ_bit(occ_src, u)) ? ps.origin[u] : 0ull;  // (remote rows only)
             uint64_t sa = seen;
             uint2 pn[R];
 #pragma unroll
@@ -707,10 +885,21 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
                 for (int k = 0; k < R; ++k) {
                     pv[k] = pn[k].x;
                     qv[k] = pn[k].y;
-                    if (use_occ && pv[k] != NO_PAIR && !occ_bit(occ_front, pv[k] & PIN_NODE_MASK)) pv[k] = NO_PAIR;
+                    if (use_occ && pv[k] != NO_PAIR && !(SH == 1 && (pv[k] & HALO)) &&
+                        !occ_bit(SH == 2 ? og_front : occ_front, pv[k] & PIN_NODE_MASK))
+                        pv[k] = NO_PAIR;  // (a remote row's tag says whether it arrived: halo_row)
                 }
 #pragma unroll
-                for (int k = 0; k < R; ++k) c[k] = pv[k] != NO_PAIR ? front[pv[k] & PIN_NODE_MASK] : 0ull;
+                for (int k = 0; k < R; ++k) {
+                    uint64_t x[1] = {0ull};
+                    if (pv[k] == NO_PAIR) {
+                    } else if (SH == 1 && (pv[k] & HALO)) {
+                        halo_row<1>(ps, pv[k] & HALO_SLOT, h, 0, x);
+                    } else {
+                        x[0] = (SH == 2 ? rg_front : front)[pv[k] & PIN_NODE_MASK];
+                    }
+                    c[k] = x[0];
+                }
 #pragma unroll
                 for (int k = 0; k < R; ++k) {
                     const int64_t j = qb + R * G + k * G + lc;
@@ -718,18 +907,29 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
                 }
 #pragma unroll
                 for (int k = 0; k < R; ++k) {
-                    if (check_rows && pv[k] != NO_PAIR && !occ_bit(occ_front, pv[k] & PIN_NODE_MASK)) c[k] = 0;
-                    const uint32_t m = pv[k] == NO_PAIR ? 0u : pv[k] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
-                    if (m == FWD_FORWARD || m == FWD_PUBLISH) {  // one-sided eligibility
+                    const bool hl = SH == 1 && pv[k] != NO_PAIR && (pv[k] & HALO);
+                    if (check_rows && pv[k] != NO_PAIR && !hl && !occ_bit(occ_front, pv[k] & PIN_NODE_MASK)) c[k] = 0;
+                    const uint32_t m = (pv[k] == NO_PAIR || hl) ? 0u : pv[k] >> PIN_FWD_SHIFT;  // FORWARD | PUBLISH
+                    if (SH == 2) {  // (rows of hop h - 1: published at h = 1, received after; k_prop_hop_fast)
+                        if (!(m & (h == 1 ? FWD_PUBLISH : FWD_FORWARD))) c[k] = 0;
+                    } else if (m == FWD_FORWARD || m == FWD_PUBLISH) {  // one-sided eligibility
                         const uint32_t v = pv[k] & PIN_NODE_MASK;
                         const uint64_t own = occ_bit(occ_src, v) ? ps.origin[v] : 0ull;
                         c[k] &= m == FWD_FORWARD ? ~own : own;
+                    }
+                    if (SH == 1 && hl) {  // never sent back to the origin; AcceptFrom drops a graylisted sender's
+                        c[k] &= ~mine;
+                        if (pv[k] & HALO_GRAY) {
+                            n_gray += __popcll(c[k]);
+                            c[k] = 0;
+                        }
                     }
                 }
 #pragma unroll
                 for (int k = 0; k < R; ++k) {  // round k: the quad's senders in order
                     const uint64_t x = c[k];
-                    n_send += x != 0;
+                    const bool hl = SH == 1 && pv[k] != NO_PAIR && (pv[k] & HALO);
+                    if (!hl) n_send += x != 0;  // (a remote sender's are counted at its pack)
                     uint64_t incl = x;
 #pragma unroll
                     for (uint32_t off = 1; off < (uint32_t)G; off <<= 1) {
@@ -756,12 +956,19 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
                         if (h == ps.max_hops || ps.flast_every) ps.flast[qv[k]] = last_count(ps, qv[k], h, fresh, false);
                     }
                     if (DROP && inv && ps.credit) ps.invcnt[qv[k]] += inv;  // P4
+                    if (SH == 1 && hl) {  // a remote sender: its duplicates this hop, and u's `from` row for it
+                        const uint32_t dup = __popcll(DROP ? x & ~drp : x) - fresh;
+                        n_dup += dup;
+                        if (dup && ps.credit) ps.dupcnt[qv[k]] += dup;
+                        if (nb) ps.hfrom[qv[k]] = nb;
+                    }
                 }
             }
             const uint64_t acc = sa ^ seen;
             const uint64_t fwd_row = DROP ? acc & ~drp : acc;
             if (lc == 0) {
                 nxt[u] = fwd_row;
+                if (SH == 2) rg_nxt[ps.node_lo + u] = fwd_row;  // (this rank's part of the replicated rows)
                 if (acc) {
                     ps.seen[u] = sa;
                     ++n_vnew;
@@ -774,11 +981,21 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
 #pragma unroll
         for (uint32_t i = 0; i < NW; ++i) r |= ((wb >> (i * G)) & 1ull) << i;
         const uint32_t u0 = tile + (threadIdx.x / 64) * NW;
-        if ((threadIdx.x & 63) == 0 && r) atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(r << (u0 % 64)));
+        if ((threadIdx.x & 63) == 0 && r) {
+            atomicOr((unsigned long long*)&occ_nxt[u0 / 64], (unsigned long long)(r << (u0 % 64)));
+            if (SH == 2) occ_g_or(og_nxt, ps.node_lo + u0, r);
+        }
     }
-    unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
-    const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
-    block_count<5>(cnt, ps.stats, slot);
+    if (SH == 1) {
+        unsigned long long cnt[7] = {n_new, n_send, n_vnew, n_rej, n_ign, n_dup, n_gray};
+        const uint32_t slot[7] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED,
+                                  STAT_DUPS, STAT_GRAY};
+        block_count<7>(cnt, ps.stats, slot);
+    } else {
+        unsigned long long cnt[5] = {n_new, n_send, n_vnew, n_rej, n_ign};
+        const uint32_t slot[5] = {STAT_HOP0 + h, STAT_EDGE_SENDS, STAT_NEW_WORDS, STAT_REJECTED, STAT_IGNORED};
+        block_count<5>(cnt, ps.stats, slot);
+    }
 }
 
 // The `from` exclusion (floodsub.go:82, gossipsub.go:1007, randomsub.go:113)
@@ -812,7 +1029,9 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
     const uint64_t* __restrict__ occ_front = ps.occ + (size_t)(h - 1) * occ_row;
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
-    if (!ps.sharded && h > 1 && prev == 0) return;  // nothing arrived last hop: empty frontier, row h unused
+    // nothing arrived last hop (and, on a range shard, no remote row this hop):
+    // empty frontier, row h unused
+    if (h > 1 && prev == 0 && !(ps.sharded && halo_rows(ps, h))) return;
     // Sparse frontier (at most a quarter of the rows can be non-empty): a row
     // is gathered only after its occupancy bit.  Very sparse (k_prop_mark):
     // a node no sender marked is left untouched (no row loads, no row
@@ -891,8 +1110,8 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                         for (int j = 0; j < U; ++j)
                             if (pv[j] != NO_PAIR) {
-                                const bool live = (pv[j] & HALO) ? (!ps.halo_occ || occ_bit(ps.halo_occ, pv[j] & HALO_SLOT))
-                                                                 : occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
+                                // (a remote row's tag says whether it arrived: halo_row)
+                                const bool live = (pv[j] & HALO) || occ_bit(occ_front, pv[j] & PIN_NODE_MASK);
                                 if (!live) pv[j] = NO_PAIR;  // the sender's row is empty
                             }
                     }
@@ -902,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
 #pragma unroll
                             for (int i = 0; i < CW; ++i) c[j][i] = 0;
                         } else if (pv[j] & HALO) {  // remote sender: its rank packed exactly what it sends
-                            load_words<CW>(c[j], ps.halo + (size_t)(pv[j] & HALO_SLOT) * W + w0);
+                            halo_row<CW>(ps, pv[j] & HALO_SLOT, h, w0, c[j]);
                         } else {
                             load_words<CW>(c[j], front + (size_t)(pv[j] & PIN_NODE_MASK) * W + w0);
                         }
@@ -999,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_prop_hop(PropState ps, uint32_t h, cons
                                 for (int i = 0; i < CW; ++i) fr[i] = o[i] | nb[i];
                             }
                             if (halo) {  // what u must not send back to this remote sender (k_prop_pack)
-                                uint64_t* hf = ps.hfrom + (size_t)(p & HALO_SLOT) * W + w0;
+                                uint64_t* hf = ps.hfrom + (size_t)q * W + w0;
 #pragma unroll
                                 for (int i = 0; i < CW; ++i) hf[i] = nb[i];
                             }
@@ -1243,6 +1462,266 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
     }
     const uint32_t slot[3] = {STAT_DUPS, STAT_GRAY, STAT_BACKSENDS};
     block_count<3>(cnt, ps.stats, slot);
+}
+
+// ---- range shards, replicated frontier (PropState::rep) -------------------------
+// The lean calls (late duplicate accounting, no RandomSub draws, no
+// first-deliverer rows) on range shards keep every node's frontier row of the
+// last two hops on every rank (front_g / occ_g, global node ids), so a remote
+// sender's row is gathered exactly as a local one and nothing per pair
+// crosses shards during the hops:
+//  * hop 0 (the call's publishes) is known everywhere: every rank writes row 0
+//    of every source from the message list (k_rep_init);
+//  * after hop h each rank contributes the rows of its nodes that received at
+//    h (k_rep_pack: entries [global id][W words]) and the others' entries are
+//    scattered into row h (k_rep_scatter); the driver moves them with one
+//    all-gather per hop;
+//  * the eligibility of a remote pair (v -> u) comes with v's fwd byte once per
+//    call (k_rep_fwd_pack / k_rep_fwd_recv build u's pin from it);
+//  * the `from` exclusion never changes a first receipt (a message v sends back
+//    to u is one u has seen), so it is settled at the call's end like the local
+//    pairs' (k_prop_dups): v's rank computes what each cross pair sent over the
+//    call (k_rep_sends) and u's rank turns it into duplicates or graylisted
+//    copies (k_rep_sends_recv).
+__global__ __launch_bounds__(256) void k_rep_zero_src(PropState ps) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t W = ps.n_words;
+    if (i >= (uint64_t)ps.n_msgs * W) return;
+    ps.front_g[(size_t)ps.msgs[i / W].source * W + i % W] = 0;  // (parity 0)
+}
+// The first entry of rmark_v equal to g (n_rmark if none): the receivers of a
+// remote sender g are rmark_u[lo .. while rmark_v == g].
+__device__ __forceinline__ uint64_t rmark_lower(const PropState& ps, uint32_t g) {
+    uint64_t lo = 0, hi = ps.n_rmark;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (ps.rmark_v[mid] < g) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ void rep_mark_receivers(const PropState& ps, uint32_t g, uint64_t* touch) {
+    for (uint64_t i = rmark_lower(ps, g); i < ps.n_rmark && ps.rmark_v[i] == g; ++i) {
+        const uint32_t u = ps.rmark_u[i];
+        atomicOr((unsigned long long*)&touch[u / 64], 1ull << (u % 64));
+    }
+}
+__global__ __launch_bounds__(256) void k_rep_init(PropState ps) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= ps.n_msgs) return;
+    const uint32_t W = ps.n_words, g = ps.msgs[k].source;
+    atomicOr((unsigned long long*)&ps.front_g[(size_t)g * W + k / 64], 1ull << (k % 64));
+    atomicOr((unsigned long long*)&ps.occ_g[g / 64], 1ull << (g % 64));
+    atomicOr((unsigned long long*)&ps.src_bits[g / 64], 1ull << (g % 64));
+    // hop 1's very sparse marking (mark_hop): a remote source marks its receivers here
+    // (a local one is marked by k_prop_mark(1) with the rest of the local frontier)
+    const bool remote = g < ps.node_lo || g - ps.node_lo >= ps.n_nodes;
+    if (remote && mark_hop(ps, 1)) rep_mark_receivers(ps, g, ps.touch + (((size_t)ps.n_nodes + 63) / 64));
+}
+// This rank's entries of hop h: its nodes whose row h is non-empty, in node
+// order (a block scan places each thread's run of four nodes), so a
+// receiver's wave meets runs of neighbouring ids (k_rep_scatter's occupancy
+// words and row stores).
+__global__ __launch_bounds__(256) void k_rep_pack(PropState ps, uint32_t h, uint64_t* __restrict__ out,
+                                                  unsigned long long* __restrict__ cnt) {
+    __shared__ uint32_t wsum[4];
+    __shared__ uint64_t base;
+    const uint32_t W = ps.n_words;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    const uint64_t* occ_h = ps.occ + (size_t)h * occ_row;
+    const uint64_t* row_h = ps.hist + (size_t)h * ps.n_nodes * W;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t u0 = blockIdx.x * 1024u; u0 < ps.n_nodes; u0 += gridDim.x * 1024u) {
+        const uint32_t ub = u0 + threadIdx.x * 4;  // this thread's four nodes
+        uint32_t bits = 0;
+        if (ub < ps.n_nodes) {
+            const uint64_t ow = occ_h[ub / 64] >> (ub % 64);  // (4 | 64: the four share a word)
+            bits = (uint32_t)(ow & 0xF);
+            if (ub + 4 > ps.n_nodes) bits &= (1u << (ps.n_nodes - ub)) - 1;
+        }
+        const uint32_t mine = __popc(bits);
+        uint32_t incl = mine;  // inclusive scan over the wave
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            before += k < wv ? wsum[k] : 0u;
+            tot += wsum[k];
+        }
+        if (threadIdx.x == 0) base = tot ? atomicAdd(cnt, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        uint64_t pos = base + before + incl - mine;
+        for (uint32_t i = 0; i < 4; ++i) {
+            if (!((bits >> i) & 1)) continue;
+            const uint32_t u = ub + i;
+            uint64_t* e = out + pos++ * (uint64_t)(W + 1);
+            e[0] = ps.node_lo + u;
+            for (uint32_t w = 0; w < W; ++w) e[1 + w] = row_h[(size_t)u * W + w];
+        }
+        __syncthreads();  // (wsum / base are reused by the next chunk)
+    }
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t x) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o, 64);
+    return x;
+}
+// Another rank's entries of hop h into the replicated rows of hop h (parity
+// h & 1), their occupancy bits (the lanes of a wave that share a word OR
+// their bits first: one atomic per word, not per entry), and (when hop h + 1
+// is very sparse) the marks of their local receivers.
+__global__ __launch_bounds__(256) void k_rep_scatter(PropState ps, uint32_t h, RepParts parts) {
+    const uint64_t n = parts.off[parts.n];
+    const uint32_t W = ps.n_words;
+    const size_t occ_g_row = ((size_t)ps.n_total + 63) / 64 + 1;
+    uint64_t* rg = ps.front_g + (size_t)(h & 1) * ps.n_total * W;
+    uint64_t* og = ps.occ_g + (size_t)(h & 1) * occ_g_row;
+    const bool mark = mark_hop(ps, h + 1);
+    uint64_t* touch = ps.touch + (size_t)((h + 1) & 1) * (((size_t)ps.n_nodes + 63) / 64);
+    const uint32_t lane = threadIdx.x & 63;
+    // (a whole-wave loop: every lane runs the same trip count, the ballots stay uniform)
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); i0 < n; i0 += (uint64_t)gridDim.x * 256u) {
+        const uint64_t i = i0 + lane;
+        const bool valid = i < n;
+        uint32_t g = 0;
+        if (valid) {
+            uint32_t k = 0;  // the part holding entry i (every rank's entries in one launch)
+            while (parts.off[k + 1] <= i) ++k;
+            const uint64_t* e = parts.p[k] + (i - parts.off[k]) * (uint64_t)(W + 1);
+            g = (uint32_t)e[0];
+            for (uint32_t w = 0; w < W; ++w) rg[(size_t)g * W + w] = e[1 + w];
+            if (mark) rep_mark_receivers(ps, g, touch);
+        }
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t lw = __shfl(g / 64, leader, 64);
+            const bool same = valid && g / 64 == lw;
+            const uint64_t bits = wave_or(same ? 1ull << (g % 64) : 0ull);
+            if (lane == leader) atomicOr((unsigned long long*)&og[lw], (unsigned long long)bits);
+            todo &= ~__ballot(same);
+        }
+    }
+}
+// Once per call: the fwd byte of every pair a remote receiver asked for, in
+// send-slot order, and on the receiving side the pins they give.
+__global__ __launch_bounds__(256) void k_rep_fwd_pack(PropState ps, uint8_t* __restrict__ out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < ps.n_send; j += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = ps.send_pair[j];
+        out[j] = r == NO_PAIR ? 0 : ps.fwd[r];
+    }
+}
+// (pair order: a receive slot's pairs come ascending per owner rank, so the
+// slot reads run forward while the pair's own arrays are read coalesced)
+__global__ __launch_bounds__(256) void k_rep_fwd_recv(PropState ps, const uint8_t* __restrict__ in) {
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        const uint32_t rv = ps.rev[q];
+        if (rv == NO_PAIR || !(rv & HALO)) continue;
+        const uint8_t fw = in[rv & HALO_SLOT];
+        const bool gin = ps.fwd[q] & FWD_GIN;  // u drops whatever v sends (AcceptFrom)
+        ps.pin[q] = (!gin && (fw & (FWD_FORWARD | FWD_PUBLISH)))
+                        ? ((uint32_t)(fw & (FWD_FORWARD | FWD_PUBLISH)) << PIN_FWD_SHIFT) | (uint32_t)ps.col[q]
+                        : NO_PAIR;
+        ps.rfwd[q] = fw;
+    }
+}
+// The origin row word w of a (possibly remote) node g: the messages it published.
+__device__ __forceinline__ uint64_t rep_origin(const PropState& ps, uint32_t g, uint32_t w) {
+    if (!((ps.src_bits[g / 64] >> (g % 64)) & 1)) return 0;
+    uint32_t lo = 0, hi = ps.n_src;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (ps.src_ids[mid] < g) lo = mid + 1;
+        else hi = mid;
+    }
+    return ps.src_rows[(size_t)lo * ps.n_words + w];
+}
+// At the call's end, per send slot j (pair r = (v -> u), v here, u remote):
+// v's sends to u over the call, as k_prop_dups computes them for a local
+// receiver (its forwarded set through the pair's eligibility, minus what it
+// first got from u and never sends back, minus u's own messages), low word;
+// high word: v's own unaccepted messages it sent u at hop 1 (copies a
+// graylisting u drops too).  u's own messages v first got from u (from_pub)
+// are the ones in v's hop-1 row: only u had them at hop 1.
+__global__ __launch_bounds__(256) void k_rep_sends(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt,
+                                                   uint64_t* __restrict__ out) {
+    const uint32_t W = ps.n_words;
+    const DupsLast L = dups_last(ps, h_run);
+    h_run = L.h_run;
+    const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+    // (pair order: the pair's own arrays are read along the sender's row; one
+    // scattered store per cross pair)
+    for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < ps.n_pairs; r += (uint64_t)gridDim.x * 256u) {
+        const uint32_t j = ps.send_slot[r];
+        if (j == NO_PAIR) continue;  // a local receiver (k_prop_dups), or nobody asked
+        const uint8_t fw = ps.fwd[r];
+        if (!(fw & FWD_SEND)) {
+            out[j] = 0;
+            continue;
+        }
+        const uint32_t v = ps.pair_obs[r], g = (uint32_t)ps.col[r];
+        const bool v_src = occ_bit(ps.occ, v);
+        const bool u_src = (ps.src_bits[g / 64] >> (g % 64)) & 1;
+        uint32_t sends = 0, pub = 0, from_pub = 0, xdrop = 0;
+        if (!u_src) {
+            const uint64_t vc = vcnt[v];
+            const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
+            const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
+            sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
+                  : m == FWD_PUBLISH ? n_own : 0;
+        } else {
+            const bool v_last = !L.empty && occ_bit(L.occ, v);
+            const bool v_h1 = occ_bit(ps.occ + occ_row, v);
+            for (uint32_t w = 0; w < W; ++w) {
+                const size_t vw = (size_t)v * W + w;
+                uint64_t sb = ps.seen[vw];
+                if (v_last) sb &= ~L.row[vw];
+                sb &= elig_word(fw, v_src ? ps.origin[vw] : 0);
+                if (ps.drop) sb &= ~ps.drop[w];
+                const uint64_t ou = rep_origin(ps, g, w) & (ps.drop ? ~ps.drop[w] : ~0ull);
+                sends += __popcll(sb & ~ou);
+                pub += __popcll(ou);
+                if (v_h1) from_pub += __popcll(ps.hist[(size_t)ps.n_nodes * W + vw] & ou);
+            }
+        }
+        if ((fw & FWD_FORWARD) && h_run >= 1) {
+            const uint64_t fl = ps.flast[r];
+            const uint32_t from_last = (!L.empty && (uint32_t)(fl >> 32) == h_run) ? (uint32_t)fl : 0;
+            if (!pub) from_pub = 0;
+            sends -= ps.fcnt[r] - from_last - from_pub + ((h_run == 1 && !L.empty) ? from_pub : 0);
+        }
+        if (ps.drop && v_src && (fw & FWD_PUBLISH))
+            for (uint32_t w = 0; w < W; ++w) xdrop += __popcll(ps.origin[(size_t)v * W + w] & ps.drop[w]);
+        out[j] = (uint64_t)sends | ((uint64_t)xdrop << 32);
+    }
+}
+// At u's rank, per receive slot (pair q = (u -> v), v remote): v's sends
+// become duplicates (P3 credits through the pending counts: sends minus u's
+// first receipts from v) or, when u's AcceptFrom drops v, graylisted copies.
+__global__ __launch_bounds__(256) void k_rep_sends_recv(PropState ps, const uint64_t* __restrict__ in) {
+    unsigned long long cnt[2] = {0, 0};
+    for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
+        const uint32_t rv = ps.rev[q];
+        if (rv == NO_PAIR || !(rv & HALO)) continue;
+        const uint64_t x = in[rv & HALO_SLOT];
+        if (!x) continue;
+        const uint32_t sends = (uint32_t)x, xdrop = (uint32_t)(x >> 32);
+        if (ps.gate && (ps.fwd[q] & FWD_GIN)) {
+            cnt[1] += sends + xdrop;
+        } else {
+            const uint32_t dup = sends - ps.fcnt[q];
+            cnt[0] += dup;
+            if (dup && ps.credit) ps.dupcnt[q] += dup;
+        }
+    }
+    const uint32_t slot[2] = {STAT_DUPS, STAT_GRAY};
+    block_count<2>(cnt, ps.stats, slot);
 }
 
 // ---- P2/P3 credits ------------------------------------------------------------
@@ -1832,11 +2311,15 @@ hipError_t launch_prop_vcodes(const PropState& ps, uint64_t* vc, uint32_t n_plan
                        n_planes);
     return hipGetLastError();
 }
-hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only) {
+hipError_t launch_prop_fwd(const PropState& ps, const DevState& s, hipStream_t st, bool pins_only, bool compact) {
     if (s.n_pairs == 0) return hipSuccess;
     if (!pins_only)
         hipLaunchKernelGGL(k_prop_fwd, dim3(std::min(nblk(s.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, s);
     hipLaunchKernelGGL(k_prop_pin, dim3(std::min(nblk(s.n_pairs, 256), 8192u)), dim3(256), 0, st, ps);
+    if (!compact) return hipGetLastError();  // (the caller compacts once more pins are in: k_rep_fwd_recv)
+    return launch_prop_compact(ps, st);
+}
+hipError_t launch_prop_compact(const PropState& ps, hipStream_t st) {
     if (ps.n_nodes) {
         hipLaunchKernelGGL(k_prop_compact, dim3(std::min(nblk(ps.n_nodes, 256), 4096u)), dim3(256), 0, st, ps);
         hipLaunchKernelGGL(k_prop_compact_done, dim3(std::min(nblk((ps.n_nodes + 63) / 64, 256), 1024u)), dim3(256), 0,
@@ -1870,12 +2353,15 @@ hipError_t launch_prop_pack(const PropState& ps, const uint64_t* front, const ui
     return hipGetLastError();
 }
 hipError_t launch_prop_pack_compact(const PropState& ps, const uint64_t* front, const uint64_t* front_occ,
-                                    uint64_t* out, unsigned long long* dcount, hipStream_t st) {
-    if (ps.n_send == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prop_pack_compact, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps,
-                       front, front_occ, out, dcount);
+                                    uint64_t* out, unsigned long long* dcount, uint32_t* tab, hipStream_t st) {
+    if (ps.n_send == 0 || ps.n_nodes == 0) return hipSuccess;
+    const uint32_t nb = pack_blocks(ps.n_nodes);
+    hipLaunchKernelGGL(k_pack_front<false>, dim3(nb), dim3(256), 0, st, ps, front, front_occ, tab, out);
+    hipLaunchKernelGGL(k_pack_scan, dim3(ps.n_ranks), dim3(1024), 0, st, tab, nb, ps.n_ranks, dcount);
+    hipLaunchKernelGGL(k_pack_front<true>, dim3(nb), dim3(256), 0, st, ps, front, front_occ, tab, out);
     return hipGetLastError();
 }
+uint32_t pack_table_words(uint32_t n_nodes, uint32_t n_ranks) { return pack_blocks(n_nodes) * n_ranks; }
 // The compacted exchange's count words, device-side: out[d] = (entries for
 // rank d, this rank's first receipts of its latest hop), so that one
 // all-to-all tells every receiver both its entry count and whether the hop
@@ -1892,33 +2378,45 @@ hipError_t launch_pack_counts(const unsigned long long* dcount, const unsigned l
     hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(MAX_RANKS), 0, st, dcount, hop_new, world, out);
     return hipGetLastError();
 }
-hipError_t launch_halo_clear(const PropState& ps, uint64_t* halo, const uint32_t* idx, uint64_t n, hipStream_t st) {
+hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t h,
+                               hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_halo_clear, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, idx, n);
+    hipLaunchKernelGGL(k_halo_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, ent, n, h);
     return hipGetLastError();
 }
-hipError_t launch_halo_scatter(const PropState& ps, uint64_t* halo, const uint64_t* ent, uint64_t n, uint32_t* idx,
-                               uint64_t* halo_occ, uint32_t h, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_halo_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, halo, ent, n,
-                       idx, halo_occ, h);
-    return hipGetLastError();
+template <bool DROP, int G, int R>
+static void fast1_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
+    const dim3 g1(std::min(nblk(ps.n_nodes, 256 / G), COUNTER_GRID)), b(256);
+    if (ps.rep) hipLaunchKernelGGL((k_prop_hop_fast1<DROP, G, R, 2>), g1, b, 0, st, ps, h, front, nxt);
+    else if (ps.sharded) hipLaunchKernelGGL((k_prop_hop_fast1<DROP, G, R, 1>), g1, b, 0, st, ps, h, front, nxt);
+    else hipLaunchKernelGGL((k_prop_hop_fast1<DROP, G, R, 0>), g1, b, 0, st, ps, h, front, nxt);
+}
+template <int CW, int LPN, bool DROP>
+static void fast_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
+    const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
+    if (ps.rep) hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, DROP, 2>), g, b, 0, st, ps, h, front, nxt);
+    else if (ps.sharded) hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, DROP, 1>), g, b, 0, st, ps, h, front, nxt);
+    else hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, DROP, 0>), g, b, 0, st, ps, h, front, nxt);
+}
+bool hop_lean(const PropState& ps) {
+    static const bool no_fast = getenv("GSX_HOP_GENERAL") != nullptr;  // tuning / cross-checks
+    return !ps.sel && !ps.from_mask && ps.late && !no_fast;
 }
 template <int CW, int LPN>
 static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, uint64_t* nxt, hipStream_t st) {
     const dim3 g(std::min(nblk(ps.n_nodes, 256 / LPN), COUNTER_GRID)), b(256);
-    static const bool no_fast = getenv("GSX_HOP_GENERAL") != nullptr;  // tuning / cross-checks
     static const bool no_fast1 = getenv("GSX_HOP_NO_FAST1") != nullptr;  // tuning / cross-checks
-    if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast && ps.n_words == 1 && !no_fast1) {
+    // (range shards take the lean kernels too: SH = 1 reads remote rows from the
+    // halo, SH = 2 from the replicated frontier rows)
+    if (hop_lean(ps) && ps.n_words == 1 && !no_fast1) {
         static const int gv = [] {  // lanes per node x rounds (tuning): 42 (default), 41, 81, 22, 82
             const char* v = getenv("GSX_HOP_GR");
             return v ? atoi(v) : 42;
         }();
-#define GSX_FAST1(GG, RR)                                                                                     \
-    {                                                                                                         \
-        const dim3 g1(std::min(nblk(ps.n_nodes, 256 / GG), COUNTER_GRID));                                    \
-        if (ps.drop) hipLaunchKernelGGL((k_prop_hop_fast1<true, GG, RR>), g1, b, 0, st, ps, h, front, nxt);   \
-        else hipLaunchKernelGGL((k_prop_hop_fast1<false, GG, RR>), g1, b, 0, st, ps, h, front, nxt);          \
+#define GSX_FAST1(GG, RR)                                          \
+    {                                                              \
+        if (ps.drop) fast1_launch<true, GG, RR>(ps, h, front, nxt, st); \
+        else fast1_launch<false, GG, RR>(ps, h, front, nxt, st);   \
     }
         if (gv == 41) GSX_FAST1(4, 1)
         else if (gv == 81) GSX_FAST1(8, 1)
@@ -1926,9 +2424,9 @@ static void hop_launch(const PropState& ps, uint32_t h, const uint64_t* front, u
         else if (gv == 22) GSX_FAST1(2, 2)
         else GSX_FAST1(4, 2)
 #undef GSX_FAST1
-    } else if (!ps.sharded && !ps.sel && !ps.from_mask && ps.late && !no_fast) {
-        if (ps.drop) hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
-        else hipLaunchKernelGGL((k_prop_hop_fast<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
+    } else if (hop_lean(ps)) {
+        if (ps.drop) fast_launch<CW, LPN, true>(ps, h, front, nxt, st);
+        else fast_launch<CW, LPN, false>(ps, h, front, nxt, st);
     }
     else if (ps.from_mask) hipLaunchKernelGGL((k_prop_hop<CW, LPN, true>), g, b, 0, st, ps, h, front, nxt);
     else hipLaunchKernelGGL((k_prop_hop<CW, LPN, false>), g, b, 0, st, ps, h, front, nxt);
@@ -1954,6 +2452,47 @@ hipError_t launch_prop_hop(const PropState& ps, uint32_t h, const uint64_t* fron
         else if (W % 8 == 0) hop_launch<4, 2>(ps, h, front, nxt, st);
         else hop_launch<4, 1>(ps, h, front, nxt, st);
     }
+    return hipGetLastError();
+}
+hipError_t launch_rep_init(const PropState& ps, hipStream_t st) {
+    if (ps.n_msgs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_zero_src, dim3(nblk((uint64_t)ps.n_msgs * ps.n_words, 256)), dim3(256), 0, st, ps);
+    hipLaunchKernelGGL(k_rep_init, dim3(nblk(ps.n_msgs, 256)), dim3(256), 0, st, ps);
+    return hipGetLastError();
+}
+hipError_t launch_rep_pack(const PropState& ps, uint32_t h, uint64_t* out, unsigned long long* cnt, hipStream_t st) {
+    if (ps.n_nodes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_pack, dim3(std::min(nblk(ps.n_nodes, 1024), 4096u)), dim3(256), 0, st, ps, h, out, cnt);
+    return hipGetLastError();
+}
+hipError_t launch_rep_scatter(const PropState& ps, uint32_t h, const RepParts& parts, hipStream_t st) {
+    const uint64_t n = parts.off[parts.n];
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_scatter, dim3(std::min(nblk(n, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h, parts);
+    return hipGetLastError();
+}
+hipError_t launch_rep_fwd_pack(const PropState& ps, uint8_t* out, hipStream_t st) {
+    if (ps.n_send == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_fwd_pack, dim3(std::min(nblk(ps.n_send, 256), COUNTER_GRID)), dim3(256), 0, st, ps, out);
+    return hipGetLastError();
+}
+hipError_t launch_rep_fwd_recv(const PropState& ps, const uint8_t* in, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_fwd_recv, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, in);
+    return hipGetLastError();
+}
+hipError_t launch_rep_sends(const PropState& ps, uint32_t h_run, uint64_t* vcnt, uint64_t* out, hipStream_t st) {
+    if (ps.n_send == 0) return hipSuccess;
+    const dim3 gv(std::min(nblk(ps.n_nodes, 256), COUNTER_GRID));
+    if (ps.n_nodes) hipLaunchKernelGGL(k_prop_vcount<1>, gv, dim3(256), 0, st, ps, h_run, vcnt, false);
+    (void)hipMemsetAsync(out, 0, 8 * ps.n_send, st);  // (slots whose pair does not exist stay 0)
+    hipLaunchKernelGGL(k_rep_sends, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, h_run,
+                       vcnt, out);
+    return hipGetLastError();
+}
+hipError_t launch_rep_sends_recv(const PropState& ps, const uint64_t* in, hipStream_t st) {
+    if (ps.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rep_sends_recv, dim3(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID)), dim3(256), 0, st, ps, in);
     return hipGetLastError();
 }
 hipError_t launch_prop_mark(const PropState& ps, uint32_t h, const uint64_t* front_occ, hipStream_t st) {

@@ -442,6 +442,14 @@ SIGNATURES = {
     "gsx_prop_step_compact": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, _u64p]),
     "gsx_prop_pack_compact_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "gsx_prop_hop_counts_dev": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_set_last_hop": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_prop_rep": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "gsx_prop_rep_fwd_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_fwd_recv": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_pack_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_step": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_void_p), P(C.c_uint64)]),
+    "gsx_prop_rep_sends_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_sends_recv": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_hb_set_px_log": (C.c_int, [C.c_void_p, C.c_size_t]),
     "gsx_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
     "gsx_prop_begin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, P(PropConfig)]),

@@ -327,6 +327,39 @@ class Engine:
         p = out.data_ptr() if hasattr(out, "data_ptr") else out
         self._chk(self.lib.gsx_prop_hop_counts_dev(self.h, C.c_void_p(p)), "gsx_prop_hop_counts_dev")
 
+    # -- range shards, replicated frontier (gsx.h gsx_prop_rep_*) --
+    def prop_rep(self) -> bool:
+        v = C.c_uint32()
+        self._chk(self.lib.gsx_prop_rep(self.h, C.byref(v)), "gsx_prop_rep")
+        return bool(v.value)
+
+    def prop_rep_fwd_pack(self, out):
+        self._chk(self.lib.gsx_prop_rep_fwd_pack(self.h, self._p(out)), "gsx_prop_rep_fwd_pack")
+
+    def prop_rep_fwd_recv(self, inp):
+        self._chk(self.lib.gsx_prop_rep_fwd_recv(self.h, self._p(inp)), "gsx_prop_rep_fwd_recv")
+
+    def prop_rep_pack_dev(self, out, d_counts):
+        """This rank's frontier rows of the hop just run as entries into out; (entries, receipts) into d_counts."""
+        self._chk(self.lib.gsx_prop_rep_pack_dev(self.h, self._p(out), self._p(d_counts)), "gsx_prop_rep_pack_dev")
+
+    def prop_rep_step(self, parts=(), counts=()):
+        """The other ranks' entries (device tensors, counts[k] rows each), then the next hop."""
+        n = len(parts)
+        pp = (C.c_void_p * max(n, 1))(*[self._p(t).value for t in parts])
+        cc = (C.c_uint64 * max(n, 1))(*[int(c) for c in counts])
+        self._chk(self.lib.gsx_prop_rep_step(self.h, n, pp, cc), "gsx_prop_rep_step")
+
+    def prop_rep_sends_pack(self, out):
+        self._chk(self.lib.gsx_prop_rep_sends_pack(self.h, self._p(out)), "gsx_prop_rep_sends_pack")
+
+    def prop_rep_sends_recv(self, inp):
+        self._chk(self.lib.gsx_prop_rep_sends_recv(self.h, self._p(inp)), "gsx_prop_rep_sends_recv")
+
+    def prop_set_last_hop(self, last_hop: int):
+        """gsx_prop_set_last_hop: the last hop that delivered on any rank (range shards)."""
+        self._chk(self.lib.gsx_prop_set_last_hop(self.h, int(last_hop)), "gsx_prop_set_last_hop")
+
     def prop_end(self) -> abi.PropOut:
         out = abi.PropOut()
         self._chk(self.lib.gsx_prop_end(self.h, C.byref(out)), "gsx_prop_end")
@@ -360,6 +393,7 @@ class Engine:
     def set_gossipsub_params(self, gp: abi.GossipSubParams):
         self._chk(self.lib.gsx_set_gossipsub_params(self.h, C.byref(gp)), "gsx_set_gossipsub_params")
         self._do_px = bool(gp.do_px)
+        self._gx_on = bool(gp.gossip_exchange)
 
     _do_px = False
 
@@ -522,13 +556,14 @@ class Engine:
     # A block travels as one 1-D int64 device tensor: the cache rows, the
     # message set's rows, then its validation-code planes (the arrival hops,
     # vc_planes(cfg) of them), [n_nodes][words(n_msgs)] u64 each.
-    @staticmethod
-    def vc_planes(cfg) -> int:
+    def vc_planes(self, cfg) -> int:
         """Code planes a propagated block carries: the bits of its arrival hops
         and the code after the last (the room gsx_propagate leaves for a
         recovery round); none when every hop takes no time (every copy
-        validated at now_ns)."""
-        if cfg is None or cfg.hop_latency_ns + cfg.validation_delay_ns <= 0:
+        validated at now_ns), and none with the gossip exchange off (the
+        calls then keep no hop codes, so the merged set keeps none either,
+        as one engine's: gsx_mcache_copy_last refuses planes of such a set)."""
+        if cfg is None or cfg.hop_latency_ns + cfg.validation_delay_ns <= 0 or not getattr(self, "_gx_on", True):
             return 0
         return int(cfg.max_hops + 1).bit_length()
 

@@ -193,14 +193,15 @@ class RangeSharded:
                                 torch.zeros((self.tp.world, 2), dtype=torch.int64, device=dev))}
         return self._bufs[key]
 
-    def _hop_compact(self, W, first: bool) -> bool:
+    def _hop_compact(self, W, first: bool):
         """One hop of the compacted exchange with ONE host round trip: the pack
         leaves (entries for rank k, this rank's receipts of the hop before) on
         the device, one all-to-all of those pairs, one copy of both count
         vectors to the host (the entry splits must be host lists); the
         entries go out as per-destination views of the pack buffer, and the
-        hop runs without a sync.  -> False when the hop before delivered
-        nothing on any rank (the call is over; this hop is not run)."""
+        hop runs without a sync.  -> (whether this hop ran: False when the hop
+        before delivered nothing on any rank, the call is over; the first
+        receipts of the hop before summed over the ranks)."""
         torch = _torch()
         be, tp = self.be, self.tp
         out, recv, sc, rc = self._compact_buffers(W)
@@ -209,8 +210,9 @@ class RangeSharded:
         hc = torch.cat([sc, rc], 0).cpu().numpy()  # the hop's one host sync
         self.host_syncs += 1
         cnt, rcnt = hc[: tp.world, 0], hc[tp.world :, 0]
-        if not first and int(hc[tp.world :, 1].sum()) == 0:
-            return False
+        got = int(hc[tp.world :, 1].sum())
+        if not first and got == 0:
+            return False, 0
         sb = np.concatenate([[0], np.cumsum(self.send_counts)[:-1]])
         parts = [out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(tp.world)]
         n = int(rcnt.sum())
@@ -218,7 +220,7 @@ class RangeSharded:
         self.sent_bytes += int(cnt.sum()) * (W + 1) * 8
         be.prop_step_compact(recv, n, sync=False)
         self.hops_run += 1
-        return True
+        return True, got
 
     def propagate(self, msgs, cfg: abi.PropConfig):
         """-> (this rank's PropOut as a dict, global totals dict)."""
@@ -232,10 +234,25 @@ class RangeSharded:
         if not self.compact:
             send, recv = self._buffers(W)
         be.prop_begin(msgs, cfg)
-        if self.compact:
+        last = 0  # the last hop that delivered on any rank (gsx_prop_set_last_hop)
+        if getattr(be, "prop_rep", None) is not None and be.prop_rep():
+            last = self._propagate_rep(W, cfg)
+        elif self.compact:
+            ran = 0
             for h in range(cfg.max_hops):
-                if not self._hop_compact(W, h == 0):
+                more, got = self._hop_compact(W, h == 0)
+                if h and got:
+                    last = h
+                if not more:
                     break
+                ran += 1
+            if ran == cfg.max_hops and ran:  # cut by max_hops: the last hop's receipts, summed
+                cnt = torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=tp.device)
+                be.prop_hop_counts_dev(cnt)
+                tp.all_reduce_sum(cnt)
+                if int(cnt[ran].item()):
+                    last = ran
+                self.host_syncs += 1
         else:
             cnt = torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=tp.device)
             h = 0
@@ -252,11 +269,69 @@ class RangeSharded:
                 tp.all_reduce_sum(cnt)
                 c = cnt.cpu().numpy()  # the chunk's one host sync
                 self.host_syncs += 1
+                nz = np.nonzero(c[1 : h + 1])[0]
+                last = int(nz[-1]) + 1 if len(nz) else 0
                 if (c[h - k + 1 : h + 1] == 0).any():
                     break
+        be.prop_set_last_hop(last)
         out = be.prop_end()
         return out_dict(out), totals(out, tp)
 
+
+    def _propagate_rep(self, W, cfg) -> int:
+        """The replicated frontier (gsx.h gsx_prop_rep_*): the cross pairs' fwd
+        bytes once, hop 1 with no exchange (hop 0 is the message list), then per
+        hop one all-gather of the ranks' new frontier rows (padded to the
+        largest rank's count, which the one host read per hop gives along with
+        the hop's receipts summed over the ranks), and the cross pairs' sends of
+        the call at its end.  -> the last hop that delivered on any rank."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        dev, R = tp.device, tp.world
+        sf = torch.zeros(max(self.n_send, 1), dtype=torch.uint8, device=dev)
+        rf = torch.zeros(max(self.n_recv, 1), dtype=torch.uint8, device=dev)
+        be.prop_rep_fwd_pack(sf)
+        tp.all_to_all(rf[: self.n_recv], sf[: self.n_send], self.recv_counts, self.send_counts)
+        be.prop_rep_fwd_recv(rf)
+        last = 0
+        if cfg.max_hops >= 1:
+            be.prop_rep_step()
+            self.hops_run += 1
+            n_local = max(int(getattr(be, "n_nodes", 0) or 0), 1)
+            out = self._bufs.get(("rep", W, n_local))
+            if out is None:
+                out = torch.empty((n_local, W + 1), dtype=torch.int64, device=dev)
+                self._bufs = {("rep", W, n_local): out}
+            cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+            h, cut = 1, True
+            while h < cfg.max_hops:
+                be.prop_rep_pack_dev(out, cnt)
+                c = torch.stack(tp.all_gather(cnt)).cpu().numpy()  # the hop's one host sync
+                self.host_syncs += 1
+                if int(c[:, 1].sum()) == 0:
+                    cut = False
+                    break
+                last = h
+                m = int(c[:, 0].max())
+                parts = tp.all_gather(out[:m]) if m else []
+                others = [(parts[k], int(c[k, 0])) for k in range(R) if k != tp.rank and c[k, 0]]
+                self.sent_bytes += m * (W + 1) * 8 * (R - 1)  # (an all-gather delivers the padded rows to R - 1 ranks)
+                be.prop_rep_step([p for p, _ in others], [n for _, n in others])
+                self.hops_run += 1
+                h += 1
+            if cut:  # the last hop ran without a look at its receipts: sum them
+                hc = torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=dev)
+                be.prop_hop_counts_dev(hc)
+                tp.all_reduce_sum(hc)
+                self.host_syncs += 1
+                if int(hc[h].item()):
+                    last = h
+        ss = torch.zeros(max(self.n_send, 1), dtype=torch.int64, device=dev)
+        rs = torch.zeros(max(self.n_recv, 1), dtype=torch.int64, device=dev)
+        be.prop_rep_sends_pack(ss)
+        tp.all_to_all(rs[: self.n_recv], ss[: self.n_send], self.recv_counts, self.send_counts)
+        be.prop_rep_sends_recv(rs)
+        return last
 
     def heartbeat(self, tick: int, now: int, seed: int):
         """One heartbeat round of every node on every rank (gossipsub.go:1303-1564
@@ -382,10 +457,18 @@ class RangeSharded:
                 n_in = int(rcnt.sum())
                 recv = torch.zeros((max(n_in, 1), words), dtype=torch.int64, device=dev)
                 tp.all_to_all_parts(recv[:n_in], rcnt, [out[int(sb[d]) : int(sb[d] + cnt[d])] for d in range(W)])
-                be.gxf_step(hop, recv, n_in, sync=False)
+                last = hop == abi.GXF_MAX_HOPS - 1
+                front = be.gxf_step(hop, recv, n_in, sync=last)
                 held = recv  # (read by the hop's kernels: alive until the next sync)
                 self.gx_hops += 1
                 hop += 1
+                if last:  # the engine runs no hop past this one: a frontier left anywhere is an error
+                    t = torch.tensor([front], dtype=torch.int64, device=dev)
+                    tp.all_reduce_sum(t)
+                    self.gx_syncs += 1
+                    if int(t.item()):
+                        raise abi.GsxError(abi.GSX_ERANGE, f"heartbeat forwarding still has a frontier after "
+                                                           f"{abi.GXF_MAX_HOPS - 1} hops: gsx_gxf_step")
             del held
             be.gxf_end()
         got = be.gx_got(n_sets)
@@ -474,13 +557,20 @@ class MessageParallel:
             if credit:
                 c.credit_scores = abi.GSX_CREDIT_DEFER
             out = self.e.propagate(mine, c)[0]
+            tot = totals(out, self.tp)
             if self.cache and cfg.router == abi.GSX_ROUTER_GOSSIPSUB and len(msgs):
-                self._merge_cache(msgs, cfg, len(mine))
+                # the merged set keeps the validation times of hops 0 .. the last hop that
+                # delivered on any replica, as one engine propagating every message does
+                cm = abi.PropConfig()
+                for f, _ in abi.PropConfig._fields_:
+                    setattr(cm, f, getattr(cfg, f))
+                cm.max_hops = tot["hops"]
+                self._merge_cache(msgs, cm, len(mine))
             if credit:
                 self.pending = True
                 if not self.epoch:
                     self.end_epoch()
-            return out_dict(out), totals(out, self.tp)
+            return out_dict(out), tot
 
     def _merge_cache(self, msgs, cfg, n_mine: int):
         """One all-gather of the replicas' cache blocks; every replica Puts the whole batch."""
@@ -556,13 +646,18 @@ class LocalGroup:
     all members have called it, which happens because the members run as
     Python threads."""
 
-    def __init__(self, world: int, device):
+    def __init__(self, world: int, device, serial: bool = False):
         import threading
 
         self.world = world
         self.device = device
         self.barrier = threading.Barrier(world)
         self.slots: List[Optional[object]] = [None] * world
+        # serial: the members take turns between collectives, each turn drained
+        # before the next starts, so one member's kernels never overlap
+        # another's on the shared device (per-shard kernel times as if each
+        # shard had a GPU of its own: tools/shard_scaling.py)
+        self.turn = threading.Lock() if serial else None
 
 
 class LocalTransport:
@@ -573,10 +668,20 @@ class LocalTransport:
         self.device = group.device
 
     def _gather(self, obj):
-        self.g.slots[self.rank] = obj
-        self.g.barrier.wait()
-        vals = list(self.g.slots)
-        self.g.barrier.wait()
+        turn = self.g.turn
+        if turn is not None:  # end of this member's turn: drain its work, let the next one run
+            torch = _torch()
+            if torch.device(self.device).type == "cuda":
+                torch.cuda.synchronize(self.device)
+            turn.release()
+        try:
+            self.g.slots[self.rank] = obj
+            self.g.barrier.wait()
+            vals = list(self.g.slots)
+            self.g.barrier.wait()
+        finally:
+            if turn is not None:
+                turn.acquire()
         return vals
 
     def all_to_all(self, recv, send, recv_splits, send_splits):
@@ -621,24 +726,32 @@ class LocalTransport:
         self._gather(None)
 
 
-def run_local(world: int, device, fn: "callable", args: Sequence) -> list:
-    """Run fn(transport, *args[k]) for k in range(world) as lock-step threads."""
+def run_local(world: int, device, fn: "callable", args: Sequence, serial: bool = False) -> list:
+    """Run fn(transport, *args[k]) for k in range(world) as lock-step threads
+    (serial: one member's work at a time between collectives, LocalGroup)."""
     import threading
 
     torch = _torch()  # import and initialise the device runtime on the calling (main) thread
     if torch.device(device).type == "cuda":
         torch.cuda.init()
         torch.zeros(1, device=device)
-    g = LocalGroup(world, device)
+    g = LocalGroup(world, device, serial=serial)
     res: List[object] = [None] * world
     err: List[BaseException] = []
 
     def body(k):
+        if g.turn is not None:
+            g.turn.acquire()
         try:
             res[k] = fn(LocalTransport(g, k), *args[k])
+            if g.turn is not None and torch.device(device).type == "cuda":
+                torch.cuda.synchronize(device)
         except BaseException as ex:  # surface the first failure, release the others
             err.append(ex)
             g.barrier.abort()
+        finally:
+            if g.turn is not None:
+                g.turn.release()
 
     th = [threading.Thread(target=body, args=(k,)) for k in range(world)]
     for t in th:

@@ -584,6 +584,54 @@ int gsx_prop_pack_compact_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts);
  * ranks once per chunk to find the hop that delivered nothing anywhere (the
  * hops after it deliver nothing and change nothing). */
 int gsx_prop_hop_counts_dev(gsx_engine* e, int64_t* d_out);
+/* Range shards, before gsx_prop_end: the last hop of the call in flight that
+ * delivered on ANY rank (the ranks' hop counts summed; 0: none).  The call's
+ * message set keeps the validation times of hops 0 .. last_hop (gsx.h (D)),
+ * the same table on every rank and on one engine holding the whole overlay
+ * (which takes its own last delivering hop); without it a shard keeps every
+ * hop it launched.  Unsharded engines ignore it. */
+int gsx_prop_set_last_hop(gsx_engine* e, uint32_t last_hop);
+
+/* Range shards, the replicated frontier.  A lean call (every duplicate inside
+ * the P3 window or no credits, no RandomSub draws, no first-deliverer rows;
+ * GSX_SHARD_PAIRS=1 in the environment turns it off) keeps every node's
+ * frontier row of the last two hops on every rank, so a remote sender's row is
+ * gathered as a local one and the hops exchange whole frontier rows instead
+ * of per-pair rows (gsx_prop_pack* / gsx_prop_step* are then refused).  The
+ * reference's semantics are unchanged (floodsub.go:76-100, gossipsub.go:943-
+ * 1013): the `from` exclusion never changes a first receipt, so each cross
+ * pair's copies are accounted once, at the call's end.  A driver runs, after
+ * gsx_prop_begin:
+ *   gsx_prop_rep              whether this call does (1) or takes the per-pair
+ *                             exchange (0);
+ *   gsx_prop_rep_fwd_pack     the fwd byte of every send slot's pair (device,
+ *                             n_send bytes), moved like a hop's dense rows
+ *                             (send splits -> receive splits) and handed to
+ *   gsx_prop_rep_fwd_recv     (device, n_recv bytes): the remote pins;
+ *   gsx_prop_rep_step         hop 1 with no parts (hop 0 is known everywhere:
+ *                             the message list), then per hop h >= 2 ...
+ *   gsx_prop_rep_pack_dev     this rank's rows of the hop just run: entries
+ *                             [global node id][W words] into out (device,
+ *                             room for n_local entries), and d_counts[0] =
+ *                             entries, d_counts[1] = this rank's first
+ *                             receipts of that hop (device i64, no sync);
+ *   gsx_prop_rep_step         the other ranks' entries (parts[k]: device,
+ *                             counts[k] entries each, host arrays) and the
+ *                             next hop, until a hop delivered nothing on any
+ *                             rank;
+ *   gsx_prop_rep_sends_pack   per send slot, what its pair sent over the call
+ *                             (device u64: sends | own unaccepted copies << 32),
+ *                             moved like the fwd bytes to
+ *   gsx_prop_rep_sends_recv   (device u64 per receive slot): duplicates (P3
+ *                             credits) or graylisted copies at the receivers;
+ * then gsx_prop_set_last_hop and gsx_prop_end as for the per-pair exchange. */
+int gsx_prop_rep(gsx_engine* e, uint32_t* on);
+int gsx_prop_rep_fwd_pack(gsx_engine* e, uint8_t* out);
+int gsx_prop_rep_fwd_recv(gsx_engine* e, const uint8_t* in);
+int gsx_prop_rep_pack_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts);
+int gsx_prop_rep_step(gsx_engine* e, uint32_t n_parts, const uint64_t* const* parts, const uint64_t* counts);
+int gsx_prop_rep_sends_pack(gsx_engine* e, uint64_t* out);
+int gsx_prop_rep_sends_recv(gsx_engine* e, const uint64_t* in);
 
 /* ---- heartbeat mesh maintenance (gossipsub.go:1303-1564) ------------------- */
 
@@ -977,7 +1025,9 @@ int gsx_mcache_ids(gsx_engine* e, uint32_t node, uint32_t topic, uint32_t n_wind
  *                         (each node's arrival hop of each message, bit b in
  *                         plane b, [plane][node][n_words]; zero-extended, at
  *                         least the set's; 0 planes: none copied) into caller
- *                         device buffers (engine stream order);
+ *                         device buffers (engine stream order); a set
+ *                         propagated with the gossip exchange off kept no
+ *                         codes: n_planes must then be 0 (GSX_ESTATE);
  *   gsx_mcache_pop        drops it (the next message set reuses its serial);
  *   gsx_mcache_put        Puts msgs[0..m) of cfg's topic as one batch: block k
  *                         is messages [sum part_msgs[<k], + part_msgs[k]) with

@@ -449,6 +449,12 @@ class EmuShard:
         self.stats["deliveries"] += n_new
         return n_new
 
+    def prop_set_last_hop(self, last_hop):  # (the emulator keeps no validation-time table)
+        pass
+
+    def prop_rep(self):  # (the emulator runs the per-pair exchange)
+        return False
+
     def prop_end(self):
         out = abi.PropOut()
         out.deliveries = self.stats["deliveries"]

@@ -43,7 +43,8 @@ def _same(g, w):
     dict(max_ihave_length=40, msgs=30, ticks=8, invalid=0.2),  # lists cross MaxIHaveLength as the window fills
     dict(prefill=3, ticks=6, exchange_from=2),  # 3 of 4 promise slots taken: the exchange's promises grow them
     dict(T=1, n=300, msgs=4200, hops=2, ticks=4),  # 66-word sets: no common words, every asker heavy (k_gx_node)
-], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill", "wide"])
+    dict(T=1, n=10, d=3, msgs=6, hops=1, ticks=6),  # 10 nodes: a one-node frontier is already a dense hop
+], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill", "wide", "tiny10"])
 def test_gossip_exchange_matches_oracle(gpu_ok, kw):
     T = kw.get("T", 2)
     g = gc.exchange_run(gsx.Engine(T), **kw)

@@ -54,6 +54,18 @@ CASES = [
     # batches cut short by max_hops (the last hop still delivers), rows of several chunks per lane
     (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 1100, True, 0.02, "compact-counts-cut"),
     (3, 1200, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 2048, False, 0.0, "compact-cut"),
+    # every duplicate inside the P3 window ("late"): the shards run the lean hop
+    # kernels (k_prop_hop_fast1 / k_prop_hop_fast, SH instance: remote rows from
+    # the halo, their duplicates counted per hop, graylisted senders dropped)
+    (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 64, True, 0.02, "compact-counts-late"),
+    (3, 1800, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 40, True, 0.02, "dense-counts-late"),
+    (4, 1600, 4, 1, abi.GSX_ROUTER_FLOODSUB, 0, 64, False, 0.02, "compact-counts-invalid-late"),
+    (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 64, True, 0.02, "compact-counts-late-cut"),
+    (2, 2000, 6, 2, abi.GSX_ROUTER_GOSSIPSUB, 0, 1024, True, 0.03, "compact-counts-late"),
+    (3, 1500, 4, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 200, True, 0.02, "compact-counts-invalid-late"),
+    (3, 1200, 4, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 500, True, 0.0, "dense-counts-late"),
+    (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 0, 1100, True, 0.02, "compact-counts-late-cut"),
+    (2, 1500, 5, 1, abi.GSX_ROUTER_GOSSIPSUB, 1, 256, True, 0.02, "compact-counts-invalid-late"),
 ]
 
 
@@ -62,13 +74,15 @@ CASES = [
                               for c in CASES])
 def test_range_sharded_matches_single_engine(gpu_ok, case):
     world, n, d, T, router, fp, m, mix, disc, compact = case
-    track, invalid, delay, max_hops = True, 0.0, 0.0, 40
-    if isinstance(compact, str):  # "<exchange>[-counts][-invalid][-cut]"
+    track, invalid, delay, max_hops, window_ms = True, 0.0, 0.0, 40, 25
+    if isinstance(compact, str):  # "<exchange>[-counts][-invalid][-late][-cut]"
         track = "counts" not in compact
         if "invalid" in compact:  # messages validation drops, and a validation delay
             invalid, delay = 0.25, 3.0
         if "cut" in compact:
             max_hops = 3
+        if "late" in compact:  # a 5-minute P3 window: every duplicate inside it
+            window_ms = 300_000
         compact = compact.startswith("compact")
     seed = 3 * n + m
     ov = pc.overlay(n, d, seed, mix_protocols=mix, direct_frac=0.03 if mix else 0.0)
@@ -76,6 +90,8 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
     cfg = pc.config(router, topic=T - 1, flood_publish=fp, size=60, delay_ms=delay, max_hops=max_hops)
     full = gsx.Engine(T)
     app = pc.setup(full, ov, T, seed, disconnect_frac=disc)
+    if window_ms != 25:
+        _params(full, T, window_ms)
     st0 = full.export_state()
     out, hop, frm = full.propagate(msgs, cfg, want_results=True)
     st1, sc1 = full.export_state(), full.scores()
@@ -88,7 +104,7 @@ def test_range_sharded_matches_single_engine(gpu_ok, case):
         sh = synth.shard_of(ov, lo, hi)
         a, b = int(ov.row_ptr[lo]), int(ov.row_ptr[hi])
         e = gsx.Engine(T)
-        _params(e, T)
+        _params(e, T, window_ms)
         e.load_overlay_shard(n, lo, sh.row_ptr, sh.col, sh.edge_flags, sh.node_ips)
         e.import_state(_slice_state(st0, T, E, a, b))
         e.set_app_scores(app[a:b])
