@@ -548,7 +548,8 @@ def prop_sharded(args, rank, world, local, dist, dev, th):
     if world == 1:
         out["roofline"] = prop_roofline(tot, msgs, loc["hop_kernel_ms"])
     else:
-        out["exchange"] = {"compacted": runner.compact, "chunk": None if runner.compact else runner.chunk,
+        out["exchange"] = {"mode": runner.last_mode, "compacted": runner.compact,
+                           "chunk": None if runner.compact else runner.chunk,
                            "bytes_sent_per_batch_rank": runner.sent_bytes / (steps + 1),
                            "dense_bytes_per_hop_rank": runner.n_send * shard_mod.prop_words(M) * 8,
                            "hops_per_batch": runner.hops_run / (steps + 1),

@@ -156,6 +156,7 @@ class RangeSharded:
         self.sent_bytes = 0  # exchange volume this rank sent (cumulative)
         self.hops_run = 0  # hops run (cumulative) and host round trips they took
         self.host_syncs = 0
+        self.last_mode = None  # the exchange the last call ran: "replicated" | "compact" | "dense"
         self.gx_hops = 0  # heartbeat forwarding hops (gossip exchange) and their host round trips
         self.gx_syncs = 0
         dev = getattr(transport, "device", None)
@@ -236,8 +237,10 @@ class RangeSharded:
         be.prop_begin(msgs, cfg)
         last = 0  # the last hop that delivered on any rank (gsx_prop_set_last_hop)
         if getattr(be, "prop_rep", None) is not None and be.prop_rep():
+            self.last_mode = "replicated"
             last = self._propagate_rep(W, cfg)
         elif self.compact:
+            self.last_mode = "compact"
             ran = 0
             for h in range(cfg.max_hops):
                 more, got = self._hop_compact(W, h == 0)
@@ -254,6 +257,7 @@ class RangeSharded:
                     last = ran
                 self.host_syncs += 1
         else:
+            self.last_mode = "dense"
             cnt = torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=tp.device)
             h = 0
             while h < cfg.max_hops:

@@ -100,7 +100,11 @@ def main():
     ap.add_argument("--chunk", type=int, default=4)
     ap.add_argument("--max-hops", type=int, default=24)
     ap.add_argument("--no-single", dest="single", action="store_false")
+    ap.add_argument("--pairs", action="store_true", help="the per-pair halo exchange (GSX_SHARD_PAIRS=1), not the "
+                                                         "replicated frontier")
     args = ap.parse_args()
+    if args.pairs:
+        os.environ["GSX_SHARD_PAIRS"] = "1"
     n, seed = args.peers, synth.SEED + 1
     cfg = config(args.max_hops)
     batches = [bench.prop_messages(n, args.msgs, seed, first=b * args.msgs) for b in range(1 + args.batches)]
@@ -139,7 +143,7 @@ def main():
             for msgs in batches:
                 loc, tot = rs.propagate(msgs, cfg)
                 outs.append((loc["hop_kernel_ms"], tot, loc["hop_launches"]))
-            return outs, rs.sent_bytes, rs.hops_run, rs.host_syncs, rs.n_send
+            return outs, rs.sent_bytes, rs.hops_run, rs.host_syncs, rs.n_send, rs.last_mode
 
         t = time.time()
         res = shard_mod.run_local(world, "cuda:0", run, [(e,) for e in engines], serial=True)
@@ -153,7 +157,7 @@ def main():
             ok = all(norm(tots[b]) == ref[b] for b in range(len(batches)))
         nb = len(batches)
         print(json.dumps({
-            "shards": world, "peers": n, "msgs": args.msgs, "exchange": args.exchange,
+            "shards": world, "peers": n, "msgs": args.msgs, "exchange": args.exchange, "mode": res[0][5],
             "hop_kernel_ms_per_batch_max_rank": float(per_rank_ms.max(0).mean()),
             "hop_kernel_ms_per_batch_per_rank": [float(x) for x in per_rank_ms.mean(1)],
             "hop_kernel_ms_per_batch_sum_ranks": float(per_rank_ms.sum(0).mean()),
