@@ -190,6 +190,13 @@ struct PropState {
     // only under its bit); pins hold global node ids, so the hop gathers a remote
     // sender's row exactly as a local one.  Per hop each rank contributes its
     // new frontier rows (k_rep_pack) and scatters the others' (k_rep_scatter).
+    uint32_t occ_div;           // lean hops gather a sender's row after its occupancy bit below n / occ_div
+                                // receipts last hop (GSX_OCC_DIV: A/B; dense hops gather beside it)
+    // One-word lean calls on one engine: STAT_EDGE_SENDS is counted at the call's end
+    // (k_prop_dups, from each sender's forwarding hops), so k_prop_hop_fast1 can skip a
+    // receiver whose seen word holds every message of the call (full1)
+    uint32_t edge_late;
+    uint64_t full1;
     uint32_t rep, n_total;
     uint64_t* front_g;
     uint64_t* occ_g;

@@ -2584,6 +2584,11 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.hfrom = P.hfrom;
     ps.halo_tag = 0;
     ps.send_slot = e->d_send_slot;
+    static const uint32_t occ_div = [] {
+        const char* v = getenv("GSX_OCC_DIV");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : 4u;
+    }();
+    ps.occ_div = occ_div;
     ps.touch = P.touch;
     ps.halo_node = e->d_halo_node;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;
@@ -2636,6 +2641,12 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
     ps.gray_pairs = P.gray_pairs;
     ps.seed = cfg->seed;
     ps.sharded = e->sharded() ? 1 : 0;
+    {  // one-word lean calls on one engine: k_prop_hop_fast1 skips saturated receivers, and
+       // STAT_EDGE_SENDS is counted at the call's end (GSX_NO_SAT_SKIP=1: A/B)
+        static const bool no_skip = getenv("GSX_NO_SAT_SKIP") != nullptr || getenv("GSX_HOP_NO_FAST1") != nullptr;
+        ps.edge_late = (!e->sharded() && W == 1 && m > 0 && gsx::hop_lean(ps) && !no_skip) ? 1u : 0u;
+        ps.full1 = m >= 64 ? ~0ull : ((1ull << m) - 1);
+    }
     return ps;
 }
 

@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast(PropState ps, uint32_t h,
     if (h > 1 && prev == 0 && !(SH == 1 && halo_rows(ps, h)) && !(SH == 2 && ps.rep_in)) return;
     // (hop 1 always: the rows of hop 0 are written for the sources only; the
     // replicated rows always: a remote row is valid only under its bit)
-    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / 4;
+    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / ps.occ_div;
     const bool use_mark = mark_hop(ps, h);
     // rows of hop h - 1 can be stale only if that hop left nodes untouched
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
     uint64_t* __restrict__ occ_nxt = ps.occ + (size_t)h * occ_row;
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     if (h > 1 && prev == 0 && !(SH == 1 && halo_rows(ps, h)) && !(SH == 2 && ps.rep_in)) return;
-    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / 4;
+    const bool use_occ = SH == 2 || h == 1 || prev < ps.n_nodes / ps.occ_div;
     const bool use_mark = mark_hop(ps, h);
     const bool check_rows = !use_occ && h >= 2 && mark_hop(ps, h - 1);
     const uint64_t* __restrict__ touch_h = ps.touch + (size_t)(h & 1) * occ_row;
@@ -868,8 +868,11 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
         bool touch = u < ps.n_nodes;
         if (touch && use_mark) touch = occ_bit(touch_h, u);
         if (touch) {
-            const int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
+            int64_t q0 = ps.row_ptr[u], q1 = ps.cend[u];
             const uint64_t seen = ps.seen[u];
+            // a receiver that has seen every message of the call gets nothing new: its walk is
+            // skipped (its senders' STAT_EDGE_SENDS are counted at the call's end: edge_late)
+            if (SH == 0 && ps.edge_late && seen == ps.full1) q1 = q0;
             const uint64_t mine = (SH == 1 && occ_bit(occ_src, u)) ? ps.origin[u] : 0ull;  // (remote rows only)
             uint64_t sa = seen;
             uint2 pn[R];
@@ -929,7 +932,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
                 for (int k = 0; k < R; ++k) {  // round k: the quad's senders in order
                     const uint64_t x = c[k];
                     const bool hl = SH == 1 && pv[k] != NO_PAIR && (pv[k] & HALO);
-                    if (!hl) n_send += x != 0;  // (a remote sender's are counted at its pack)
+                    if (!hl && !(SH == 0 && ps.edge_late)) n_send += x != 0;  // (a remote sender's are counted at its pack)
                     uint64_t incl = x;
 #pragma unroll
                     for (uint32_t off = 1; off < (uint32_t)G; off <<= 1) {
@@ -1328,7 +1331,12 @@ __global__ __launch_bounds__(256) void k_prop_vcount(PropState ps, uint32_t h_ru
             n_all = group_sum<L>(n_all);
             n_own = group_sum<L>(n_own);
         }
-        if (lc == 0) vcnt[v] = (uint64_t)n_all | ((uint64_t)n_own << 32);
+        uint64_t fh = 0;  // edge_late: the hops 2 .. h_run at which v forwarded received messages
+        if (ps.edge_late && lc == 0) {
+            const size_t occ_row = ((size_t)ps.n_nodes + 63) / 64;
+            for (uint32_t hh = 1; hh + 1 <= L_.h_run; ++hh) fh += occ_bit(ps.occ + (size_t)hh * occ_row, v);
+        }
+        if (lc == 0) vcnt[v] = (uint64_t)n_all | ((uint64_t)n_own << 32) | (fh << 56);
     }
 }
 
@@ -1353,7 +1361,7 @@ constexpr int FH = 2;  // fold_rescore_1: pairs whose loads are in flight togeth
 template <bool GRAY_ONLY>
 __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
     if (GRAY_ONLY && *ps.gray_pairs == 0) return;
-    unsigned long long cnt[3] = {0, 0, 0};
+    unsigned long long cnt[4] = {0, 0, 0, 0};
     const uint32_t W = ps.n_words;
     const DupsLast L = dups_last(ps, h_run);
     h_run = L.h_run;
@@ -1381,6 +1389,20 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             const bool local = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
             ga[i] = local && ps.gate && (ps.rfwd[r] & FWD_GIN);
             if (GRAY_ONLY && !ga[i]) qa[i] = NO_PAIR;
+        }
+        if (!GRAY_ONLY && ps.edge_late) {  // STAT_EDGE_SENDS of one-word calls (k_prop_hop_fast1 skips
+                                           // saturated receivers): per pair u's pin lets through, the hops at
+                                           // which v's row was non-empty: hop 1 its publishes, later ones
+                                           // its receipts of the hop before (vcount's forwarding hops)
+#pragma unroll
+            for (int i = 0; i < DU; ++i) {
+                const uint64_t r = r0 + i * stride;
+                if (qa[i] == NO_PAIR || (qa[i] & HALO) || !(fa[i] & FWD_SEND) || ga[i] || (ps.rfwd[r] & FWD_GIN))
+                    continue;
+                const uint64_t vc = vcnt[va[i]];
+                cnt[3] += ((fa[i] & FWD_PUBLISH) && h_run >= 1 && occ_bit(src_occ, va[i]) ? 1u : 0u) +
+                          ((fa[i] & FWD_FORWARD) ? (uint32_t)(vc >> 56) : 0u);
+            }
         }
         uint64_t vca[DU], fla[DU];
         uint32_t fca[DU];
@@ -1415,7 +1437,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             uint32_t sends = 0, pub = 0;
             if (!u_src && !ps.sel && !ps.from_mask) {
                 const uint64_t vc = vca[i];
-                const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
+                const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32) & 0xFFFFFFu;
                 const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
                 sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
                       : m == FWD_PUBLISH ? n_own : 0;
@@ -1460,8 +1482,8 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             }
         }
     }
-    const uint32_t slot[3] = {STAT_DUPS, STAT_GRAY, STAT_BACKSENDS};
-    block_count<3>(cnt, ps.stats, slot);
+    const uint32_t slot[4] = {STAT_DUPS, STAT_GRAY, STAT_BACKSENDS, STAT_EDGE_SENDS};
+    block_count<4>(cnt, ps.stats, slot);
 }
 
 // ---- range shards, replicated frontier (PropState::rep) -------------------------
@@ -1671,7 +1693,7 @@ __global__ __launch_bounds__(256) void k_rep_sends(PropState ps, uint32_t h_run,
         uint32_t sends = 0, pub = 0, from_pub = 0, xdrop = 0;
         if (!u_src) {
             const uint64_t vc = vcnt[v];
-            const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32);
+            const uint32_t n_all = (uint32_t)vc, n_own = (uint32_t)(vc >> 32) & 0xFFFFFFu;
             const uint8_t m = fw & (FWD_FORWARD | FWD_PUBLISH);
             sends = m == (FWD_FORWARD | FWD_PUBLISH) ? n_all : m == FWD_FORWARD ? n_all - n_own
                   : m == FWD_PUBLISH ? n_own : 0;
