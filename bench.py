@@ -716,8 +716,9 @@ def dropin_leg(args):
             out[f"peers_{k}"] = json.loads(r.stdout.strip().splitlines()[-1])
         out["note"] = ("per call through include/gsx_pubsub.hpp on one GPU engine holding one router's peers; "
                        "Score() with no change since the last is a host lookup (AppSpecificScore is called for the "
-                       "scored peer only, score.go:320), after a tracer call it re-scores the observer's row on the "
-                       "GPU and copies the vector back")
+                       "scored peer only, score.go:320) or of the host-mapped score copy; after a tracer call one "
+                       "k_dropin launch applies the queued events and re-scores only the pairs and rows they touched, "
+                       "writing the asked scores to the mapped copy")
         return out
     except (subprocess.SubprocessError, OSError, ValueError) as ex:
         return {"error": str(ex)[:300]}
