@@ -190,6 +190,7 @@ struct PropState {
     // only under its bit); pins hold global node ids, so the hop gathers a remote
     // sender's row exactly as a local one.  Per hop each rank contributes its
     // new frontier rows (k_rep_pack) and scatters the others' (k_rep_scatter).
+    uint32_t mark_div;          // very sparse hops (k_prop_mark) below n / mark_div receipts (GSX_MARK_DIV: A/B)
     uint32_t occ_div;           // lean hops gather a sender's row after its occupancy bit below n / occ_div
                                 // receipts last hop (GSX_OCC_DIV: A/B; dense hops gather beside it)
     // One-word lean calls on one engine: STAT_EDGE_SENDS is counted at the call's end

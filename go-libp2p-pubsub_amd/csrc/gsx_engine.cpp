@@ -2589,6 +2589,13 @@ gsx::PropState prop_state(gsx_engine* e, uint32_t W, size_t m, const gsx_prop_co
         return v && atoi(v) > 0 ? (uint32_t)atoi(v) : 4u;
     }();
     ps.occ_div = occ_div;
+    // (one-word rows: pushing marks costs more than the lean hop's walk of a frontier up to n / 128
+    // — 64-message batch 1.42 -> 1.35 ms, tools/prop_ab.py; wider rows keep n / 16)
+    static const uint32_t mark_div = [] {
+        const char* v = getenv("GSX_MARK_DIV");
+        return v && atoi(v) > 0 ? (uint32_t)atoi(v) : 0u;
+    }();
+    ps.mark_div = mark_div ? mark_div : (W == 1 ? 128u : 16u);
     ps.touch = P.touch;
     ps.halo_node = e->d_halo_node;
     ps.sel = cfg->router == GSX_ROUTER_RANDOMSUB ? P.sel : nullptr;

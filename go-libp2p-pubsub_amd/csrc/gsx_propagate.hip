@@ -306,8 +306,8 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
 __device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     // (replicated frontier: the remote rows of the hop mark their receivers too)
-    if (ps.rep) return prev + (h >= 2 ? ps.rep_in : 0) < ps.n_nodes / 16;
-    return prev < ps.n_nodes / 16 && !(ps.halo && !ps.halo_tag);
+    if (ps.rep) return prev + (h >= 2 ? ps.rep_in : 0) < ps.n_nodes / ps.mark_div;
+    return prev < ps.n_nodes / ps.mark_div && !(ps.halo && !ps.halo_tag);
 }
 // Range shards: can a remote sender's row reach this hop?  The compacted
 // exchange counts the hop's scattered entries (STAT_HALO0); the dense one
@@ -1390,20 +1390,6 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             ga[i] = local && ps.gate && (ps.rfwd[r] & FWD_GIN);
             if (GRAY_ONLY && !ga[i]) qa[i] = NO_PAIR;
         }
-        if (!GRAY_ONLY && ps.edge_late) {  // STAT_EDGE_SENDS of one-word calls (k_prop_hop_fast1 skips
-                                           // saturated receivers): per pair u's pin lets through, the hops at
-                                           // which v's row was non-empty: hop 1 its publishes, later ones
-                                           // its receipts of the hop before (vcount's forwarding hops)
-#pragma unroll
-            for (int i = 0; i < DU; ++i) {
-                const uint64_t r = r0 + i * stride;
-                if (qa[i] == NO_PAIR || (qa[i] & HALO) || !(fa[i] & FWD_SEND) || ga[i] || (ps.rfwd[r] & FWD_GIN))
-                    continue;
-                const uint64_t vc = vcnt[va[i]];
-                cnt[3] += ((fa[i] & FWD_PUBLISH) && h_run >= 1 && occ_bit(src_occ, va[i]) ? 1u : 0u) +
-                          ((fa[i] & FWD_FORWARD) ? (uint32_t)(vc >> 56) : 0u);
-            }
-        }
         uint64_t vca[DU], fla[DU];
         uint32_t fca[DU];
 #pragma unroll
@@ -1414,6 +1400,19 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             const bool fl = live && !ps.from_mask && (fa[i] & FWD_FORWARD) && h_run >= 1;
             fca[i] = (fl || (ps.acc_f && r < ps.n_pairs)) ? ps.fcnt[r] : 0;
             fla[i] = fl ? ps.flast[r] : 0;
+        }
+        if (!GRAY_ONLY && ps.edge_late) {  // STAT_EDGE_SENDS of one-word calls (k_prop_hop_fast1 skips
+                                           // saturated receivers): per pair u's pin lets through, the hops at
+                                           // which v's row was non-empty: hop 1 its publishes, later ones
+                                           // its receipts of the hop before (vcount's forwarding hops)
+#pragma unroll
+            for (int i = 0; i < DU; ++i) {
+                const uint64_t r = r0 + i * stride;
+                if (qa[i] == NO_PAIR || (qa[i] & HALO) || !(fa[i] & FWD_SEND) || ga[i] || (ps.rfwd[r] & FWD_GIN))
+                    continue;
+                cnt[3] += ((fa[i] & FWD_PUBLISH) && h_run >= 1 && occ_bit(src_occ, va[i]) ? 1u : 0u) +
+                          ((fa[i] & FWD_FORWARD) ? (uint32_t)(vca[i] >> 56) : 0u);
+            }
         }
         if (!GRAY_ONLY && ps.acc_f) {  // deferred folds: r as a receiver pair — its first receipts join its sum
 #pragma unroll
