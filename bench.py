@@ -664,6 +664,10 @@ def adversarial_leg(args, rank, world, local, dist, dev):
         if dist is not None:
             runner = shard_mod.RangeSharded(e, rl, shard_mod.DistTransport(dev, stage_host=args.rehearse))
 
+        # the heartbeat's buffers, allocated once at setup (gsx_hb_reserve: the router's
+        # attach-time state), so the timed first round is the round's work
+        e.hb_reserve()
+
         def sybil_links():
             st = e.export_state()
             return reduce_scalar(float(np.count_nonzero(((st["rec_flags"] & abi.GSX_REC_IN_MESH) != 0) & syb)),
@@ -676,6 +680,7 @@ def adversarial_leg(args, rank, world, local, dist, dev):
         for k in range(2):  # the attack's first round (the synthesized meshes' sybils pruned), then round 60 (OG)
             now += abi.SECOND
             torch.cuda.synchronize(dev)
+            b0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)  # (the profiler's clock: tools/hb_api.py windows)
             t0 = time.perf_counter()
             if runner is None:
                 hbs.append(e.heartbeat(59 + k, now, synth.SEED).as_dict())
@@ -684,6 +689,8 @@ def adversarial_leg(args, rank, world, local, dist, dev):
             e.sync()
             torch.cuda.synchronize(dev)
             ms.append(reduce_scalar(time.perf_counter() - t0, dist, dev, "max") * 1e3)
+            if os.environ.get("GSX_HB_WINDOWS"):
+                log(f"window {59 + k} {b0} {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}")
         out["heartbeat_ms_per_round"] = sum(ms) / len(ms)
         out["heartbeat_ms_rounds"] = ms
         if runner is not None:  # the gossip exchange's forwarding hops across the shards and their host round trips
@@ -854,6 +861,7 @@ def main():
         # the reference's HandleRPC always runs handleIHave / handleIWant
         # (gossipsub.go:596-613): the gossip exchange (D) is part of the round
         e.set_gossipsub_params(gsx_engine_mod.default_gossipsub_params(gossip_exchange=1 if args.hb_exchange else 0))
+        e.hb_reserve()  # (setup: the heartbeat's buffers, gsx_hb_reserve)
         tick = 58 - args.hb_settle
         hb_cfg = prop_config(args, n)
         rounds, settle = [], []

@@ -3820,7 +3820,7 @@ int gx_prom_grow(gsx_engine* e) {
 // can exceed MaxIHaveLength gets rows for every target the round can pick
 // (the sum over nodes of min(degree, max(Dlazy, GossipFactor * degree)): a
 // node picks at most that many from its eligible peers), tw words each.
-int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const std::vector<uint32_t>& tw) {
+void gx_target_bound(gsx_engine* e) {
     if (e->tgt_dlazy != e->gp.d_lazy || e->tgt_gf != e->gp.gossip_factor) {
         uint64_t b = 0;
         for (uint32_t v = 0; v < e->n_nodes; ++v) {
@@ -3834,6 +3834,9 @@ int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const st
         e->tgt_dlazy = e->gp.d_lazy;
         e->tgt_gf = e->gp.gossip_factor;
     }
+}
+int gx_sub_prepare(gsx_engine* e, const std::vector<uint32_t>& max_ids, const std::vector<uint32_t>& tw) {
+    gx_target_bound(e);
     const size_t E = std::max<size_t>(e->E, 1);
     for (uint32_t t = 0; t < e->T; ++t) {
         gsx::GxSub& g = e->gsub_host[t];
@@ -5144,6 +5147,22 @@ int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, gsx_
     if (int rc = hb_begin(e, tick, now, seed)) return rc;
     if (int rc = hb_recv(e, nullptr)) return rc;
     return hb_end(e, nullptr, out);
+}
+
+int gsx_hb_reserve(gsx_engine* e) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = gx_busy(e)) return rc;
+    if (!e->loaded) return fail(e, GSX_ESTATE, "no overlay loaded");
+    if (e->max_deg > gsx::HB_HUB_MAX) return GSX_OK;  // (gsx_heartbeat refuses this overlay)
+    if (!e->d_hbstats)
+        if (int rc = hb_alloc(e)) return rc;
+    if (e->gp.gossip_exchange) {
+        if (int rc = gx_alloc(e)) return rc;
+        if (int rc = gxf_alloc(e)) return rc;
+        gx_target_bound(e);
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return GSX_OK;
 }
 
 int gsx_hb_begin(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed) {

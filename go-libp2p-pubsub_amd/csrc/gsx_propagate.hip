@@ -1358,7 +1358,7 @@ constexpr int FH = 2;  // fold_rescore_1: pairs whose loads are in flight togeth
 // receivers are rejected/ignored receipts of the hop kernels).  GRAY_ONLY
 // (per-hop accounting, where duplicates are counted on arrival) visits only
 // the gated pairs.
-template <bool GRAY_ONLY>
+template <bool GRAY_ONLY, int DD = DU>
 __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run, const uint64_t* __restrict__ vcnt) {
     if (GRAY_ONLY && *ps.gray_pairs == 0) return;
     unsigned long long cnt[4] = {0, 0, 0, 0};
@@ -1367,11 +1367,11 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
     h_run = L.h_run;
     const uint64_t* src_occ = ps.occ;  // row 0: nodes that published in this call
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    for (uint64_t r0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; r0 < ps.n_pairs; r0 += stride * DU) {
-        uint32_t qa[DU], va[DU], ua[DU], af[DU], as_[DU];
-        uint8_t fa[DU];
+    for (uint64_t r0 = (uint64_t)blockIdx.x * 256u + threadIdx.x; r0 < ps.n_pairs; r0 += stride * DD) {
+        uint32_t qa[DD], va[DD], ua[DD], af[DD], as_[DD];
+        uint8_t fa[DD];
 #pragma unroll
-        for (int i = 0; i < DU; ++i) {
+        for (int i = 0; i < DD; ++i) {
             const uint64_t r = r0 + i * stride;
             const bool in = r < ps.n_pairs;
             qa[i] = in ? ps.rev[r] : NO_PAIR;  // the receiver's pair (u -> v)
@@ -1382,18 +1382,18 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             af[i] = (!GRAY_ONLY && ps.acc_f && in) ? ps.acc_f[r] : 0u;
             as_[i] = (!GRAY_ONLY && ps.acc_s && in) ? ps.acc_s[r] : 0u;
         }
-        bool ga[DU];  // u drops v's copies: the GIN bit of u's pair (v's reverse), kept beside r by k_prop_pin
+        bool ga[DD];  // u drops v's copies: the GIN bit of u's pair (v's reverse), kept beside r by k_prop_pin
 #pragma unroll
-        for (int i = 0; i < DU; ++i) {
+        for (int i = 0; i < DD; ++i) {
             const uint64_t r = r0 + i * stride;
             const bool local = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
             ga[i] = local && ps.gate && (ps.rfwd[r] & FWD_GIN);
             if (GRAY_ONLY && !ga[i]) qa[i] = NO_PAIR;
         }
-        uint64_t vca[DU], fla[DU];
-        uint32_t fca[DU];
+        uint64_t vca[DD], fla[DD];
+        uint32_t fca[DD];
 #pragma unroll
-        for (int i = 0; i < DU; ++i) {
+        for (int i = 0; i < DD; ++i) {
             const uint64_t r = r0 + i * stride;
             const bool live = qa[i] != NO_PAIR && !(qa[i] & HALO) && (fa[i] & FWD_SEND);
             vca[i] = live ? vcnt[va[i]] : 0;
@@ -1406,7 +1406,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
                                            // which v's row was non-empty: hop 1 its publishes, later ones
                                            // its receipts of the hop before (vcount's forwarding hops)
 #pragma unroll
-            for (int i = 0; i < DU; ++i) {
+            for (int i = 0; i < DD; ++i) {
                 const uint64_t r = r0 + i * stride;
                 if (qa[i] == NO_PAIR || (qa[i] & HALO) || !(fa[i] & FWD_SEND) || ga[i] || (ps.rfwd[r] & FWD_GIN))
                     continue;
@@ -1416,7 +1416,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
         }
         if (!GRAY_ONLY && ps.acc_f) {  // deferred folds: r as a receiver pair — its first receipts join its sum
 #pragma unroll
-            for (int i = 0; i < DU; ++i) {
+            for (int i = 0; i < DD; ++i) {
                 const uint64_t r = r0 + i * stride;
                 if (r >= ps.n_pairs || !fca[i]) continue;
                 ps.acc_f[r] = af[i] + fca[i];
@@ -1425,7 +1425,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             }
         }
 #pragma unroll
-        for (int i = 0; i < DU; ++i) {
+        for (int i = 0; i < DD; ++i) {
             const uint64_t r = r0 + i * stride;
             const uint32_t q = qa[i];
             const uint8_t fw = fa[i];
@@ -2538,8 +2538,20 @@ hipError_t launch_prop_dups(const PropState& ps, uint32_t h_run, uint64_t* vcnt,
     else if (L == 2) hipLaunchKernelGGL(k_prop_vcount<2>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
     else hipLaunchKernelGGL(k_prop_vcount<1>, gv, dim3(256), 0, st, ps, h_run, vcnt, gray_only);
     const dim3 gd(std::min(nblk(ps.n_pairs, 256), COUNTER_GRID));
+    // A/B: GSX_DUPS_DU (pairs per thread batch: 1, 2 or 4) and GSX_DUPS_GRID (block cap)
+    static const int dd = [] {
+        const char* v = getenv("GSX_DUPS_DU");
+        return v ? atoi(v) : DU;
+    }();
+    static const unsigned dgrid = [] {
+        const char* v = getenv("GSX_DUPS_GRID");
+        return v && atoi(v) > 0 ? (unsigned)atoi(v) : COUNTER_GRID;
+    }();
+    const dim3 gdd(std::min(nblk(ps.n_pairs, 256), dgrid));
     if (gray_only) hipLaunchKernelGGL(k_prop_dups<true>, gd, dim3(256), 0, st, ps, h_run, vcnt);
-    else hipLaunchKernelGGL(k_prop_dups<false>, gd, dim3(256), 0, st, ps, h_run, vcnt);
+    else if (dd == 1) hipLaunchKernelGGL((k_prop_dups<false, 1>), gdd, dim3(256), 0, st, ps, h_run, vcnt);
+    else if (dd == 2) hipLaunchKernelGGL((k_prop_dups<false, 2>), gdd, dim3(256), 0, st, ps, h_run, vcnt);
+    else hipLaunchKernelGGL((k_prop_dups<false, 4>), gdd, dim3(256), 0, st, ps, h_run, vcnt);
     return hipGetLastError();
 }
 hipError_t launch_prop_count(const PropState& ps, const DevState& s, bool fold, bool rescore, const DevPeerParams& pp,

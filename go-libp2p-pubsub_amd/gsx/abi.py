@@ -459,6 +459,7 @@ SIGNATURES = {
     "gsx_default_gossipsub_params": (C.c_int, [P(GossipSubParams)]),
     "gsx_set_gossipsub_params": (C.c_int, [C.c_void_p, P(GossipSubParams)]),
     "gsx_heartbeat": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64, P(HeartbeatOut)]),
+    "gsx_hb_reserve": (C.c_int, [C.c_void_p]),
     "gsx_hb_begin": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int64, C.c_uint64]),
     "gsx_hb_pack_ctl": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_hb_recv": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -417,6 +417,10 @@ class Engine:
     def hb_px_recv(self, kind: int, entries, n: int):
         self._chk(self.lib.gsx_hb_px_recv(self.h, kind, self._p(entries), n), "gsx_hb_px_recv")
 
+    def hb_reserve(self):
+        """The heartbeat's device buffers allocated now (gsx_hb_reserve), not in the first round."""
+        self._chk(self.lib.gsx_hb_reserve(self.h), "gsx_hb_reserve")
+
     def heartbeat(self, tick: int, now: int, seed: int) -> abi.HeartbeatOut:
         out = abi.HeartbeatOut()
         self._chk(self.lib.gsx_heartbeat(self.h, tick, now, seed, C.byref(out)), "gsx_heartbeat")

@@ -785,6 +785,16 @@ typedef struct gsx_heartbeat_out {
 
 int gsx_heartbeat(gsx_engine* e, uint64_t tick, int64_t now_ns, uint64_t seed, gsx_heartbeat_out* out);
 
+/* Allocates (and clears) the heartbeat's device buffers for the loaded
+ * overlay and the current gossipsub params now instead of at the first
+ * gsx_heartbeat: the round state (GRAFT/PRUNE words, marks, IHAVE slots, mesh
+ * counts), with the gossip exchange on its promise / IHAVE / request arrays and
+ * the forwarding's frontier and per-pair buffers, and the truncated-list bound
+ * of the topics (a host pass over the rows).  The setup the reference's router
+ * does when it attaches (gossipsub.go:467-510, NewGossipSub's maps), so the
+ * first round costs what every round costs.  Optional; idempotent. */
+int gsx_hb_reserve(gsx_engine* e);
+
 /* The gossipTracer's promises of every router (gossip_tracer.go:48-185; one
  * router per observer, keyed by its pair to the promising peer and the
  * message handle: the message set's serial << 32 | index inside the engine,
