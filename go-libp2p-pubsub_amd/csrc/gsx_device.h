@@ -186,7 +186,7 @@ struct PropState {
     // Range shards, replicated frontier (rep != 0; the lean calls: late duplicate
     // accounting, no RandomSub draws, no first-deliverer rows).  Every rank keeps
     // the frontier rows of ALL n_total nodes, two hops deep: front_g
-    // [parity][n_total][W] and occ_g [parity][n_total / 64 + 1] (a row is valid
+    // [parity][n_total][W] and occ_g [parity][(n_total + 63) / 64 + 1] (a row is valid
     // only under its bit); pins hold global node ids, so the hop gathers a remote
     // sender's row exactly as a local one.  Per hop each rank contributes its
     // new frontier rows (k_rep_pack) and scatters the others' (k_rep_scatter).
@@ -199,13 +199,17 @@ struct PropState {
     uint32_t edge_late;
     uint64_t full1;
     uint32_t rep, n_total;
+    // rep_rows: the hop's rows move as every rank's dense slice of front_g (one
+    // all-gather) and its occupancy bits as a summed row, chunks of hops with no
+    // host read; no very sparse marking (remote rows would not mark)
+    uint32_t rep_rows;
     uint64_t* front_g;
     uint64_t* occ_g;
     uint64_t rep_in;            // remote frontier rows scattered for this hop (host-known)
     const uint32_t* rmark_v;    // [n_recv] remote senders' global ids, ascending (their local receivers: rmark_u)
     const uint32_t* rmark_u;
     uint64_t n_rmark;
-    const uint64_t* src_bits;   // [n_total / 64 + 1] bit per global node: published in this call
+    const uint64_t* src_bits;   // [(n_total + 63) / 64 + 1] bit per global node: published in this call
     const uint32_t* src_ids;    // [n_src] the sources' global ids, ascending, and their
     const uint64_t* src_rows;   // [n_src][W] origin rows (every message each published)
     uint32_t n_src;

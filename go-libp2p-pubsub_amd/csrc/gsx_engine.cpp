@@ -388,8 +388,8 @@ struct gsx_engine {
         // replicated frontier (range shards, lean calls; PropState::rep)
         bool rep = false;
         uint64_t* front_g = nullptr;   // [2][n_total][W]
-        uint64_t* occ_g = nullptr;     // [2][n_total / 64 + 1]
-        uint64_t* src_bits = nullptr;  // [n_total / 64 + 1]
+        uint64_t* occ_g = nullptr;     // [2][(n_total + 63) / 64 + 1]
+        uint64_t* src_bits = nullptr;  // [(n_total + 63) / 64 + 1]
         uint64_t rep_words = 0;        // front_g capacity (words)
         uint32_t* src_ids = nullptr;   // [m] + the origin rows [m][W]
         uint64_t* src_rows = nullptr;
@@ -2864,7 +2864,7 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     P.rep = e->sharded() && e->n_ranks > 1 && m > 0 && gsx::hop_lean(ps) && !no_rep &&
             e->n_total <= gsx::PIN_NODE_MASK;
     if (P.rep) {
-        const size_t NT = e->n_total, ow = NT / 64 + 1;
+        const size_t NT = e->n_total, ow = (NT + 63) / 64 + 1;  // (the kernels' occ_g row: one spare word)
         if (P.rep_words < 2 * (uint64_t)NT * W) {
             for (uint64_t** p : {&P.front_g, &P.occ_g, &P.src_bits}) {
                 if (*p) (void)hipFree(*p);
@@ -3569,6 +3569,54 @@ int gsx_prop_rep_step(gsx_engine* e, uint32_t n_parts, const uint64_t* const* pa
     } else {
         P.last.rep_in = 0;
     }
+    return prop_hop(e, nullptr);
+}
+
+int gsx_prop_rep_rows(gsx_engine* e, uint32_t on) {
+    if (!e) return GSX_EINVAL;
+    if (int rc = rep_ready(e, true)) return rc;
+    e->prop.last.rep_rows = on ? 1u : 0u;
+    return GSX_OK;
+}
+
+int gsx_prop_rep_rows_export(gsx_engine* e, uint64_t* rows, uint64_t* occ) {
+    if (!e || !rows || !occ) return GSX_EINVAL;
+    if (int rc = rep_ready(e, false)) return rc;
+    auto& P = e->prop;
+    if (!P.last.rep_rows) return fail(e, GSX_ESTATE, "gsx_prop_rep_rows(e, 1) before the first hop");
+    if (P.h == 0) return fail(e, GSX_ESTATE, "hop 0 is every rank's already: step hop 1 first");
+    const size_t W = P.last.n_words, NT = e->n_total, ow = (NT + 63) / 64 + 1;
+    const uint64_t* fg = P.front_g + (size_t)(P.h & 1) * NT * W;
+    HIPCHK(e, hipMemcpyAsync(rows, fg + (size_t)e->node_lo * W, 8 * W * e->n_nodes, hipMemcpyDeviceToDevice,
+                             e->stream));
+    HIPCHK(e, hipMemcpyAsync(occ, P.occ_g + (size_t)(P.h & 1) * ow, 8 * ow, hipMemcpyDeviceToDevice, e->stream));
+    return GSX_OK;
+}
+
+int gsx_prop_rep_rows_step(gsx_engine* e, uint32_t n_parts, const uint64_t* const* parts, const uint64_t* occ_sum) {
+    if (!e || !parts || !occ_sum) return GSX_EINVAL;
+    if (int rc = rep_ready(e, false)) return rc;
+    auto& P = e->prop;
+    if (!P.last.rep_rows) return fail(e, GSX_ESTATE, "gsx_prop_rep_rows(e, 1) before the first hop");
+    if (n_parts != e->n_ranks || e->rank_lo.size() != (size_t)n_parts + 1)
+        return fail(e, GSX_EINVAL, "one part per rank of the shard plan");
+    if (P.h == 0) return fail(e, GSX_ESTATE, "hop 0's rows need no exchange");
+    if (P.h >= P.cfg.max_hops) return fail(e, GSX_ERANGE, "max_hops reached");
+    const size_t W = P.last.n_words, NT = e->n_total, ow = (NT + 63) / 64 + 1;
+    uint64_t* fg = P.front_g + (size_t)(P.h & 1) * NT * W;
+    hipEvent_t a, b;  // (in the call's hop_kernel_ms, with the hops)
+    if (int rc = prop_event_pair(e, &a, &b)) return rc;
+    HIPCHK(e, hipEventRecord(a, e->stream));
+    for (uint32_t k = 0; k < n_parts; ++k) {  // every other rank's slice of the hop's rows, in place
+        const uint32_t lo = e->rank_lo[k], n = e->rank_lo[k + 1] - lo;
+        if (lo == e->node_lo || !n) continue;  // (this rank's rows are there already)
+        if (!parts[k]) return GSX_EINVAL;
+        HIPCHK(e, hipMemcpyAsync(fg + (size_t)lo * W, parts[k], 8 * W * n, hipMemcpyDeviceToDevice, e->stream));
+    }
+    // every rank's occupancy bits of the hop: the sum of bit rows whose ranks own disjoint bits
+    HIPCHK(e, hipMemcpyAsync(P.occ_g + (size_t)(P.h & 1) * ow, occ_sum, 8 * ow, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipEventRecord(b, e->stream));
+    P.last.rep_in = NT;  // (remote rows may reach every hop: it never returns early on the local count)
     return prop_hop(e, nullptr);
 }
 

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(64) void k_rsub_select(PropState ps, const uint64_t
 __device__ __forceinline__ bool mark_hop(const PropState& ps, uint32_t h) {
     const unsigned long long prev = h >= 2 ? ps.stats[STAT_HOP0 + h - 1] : ps.n_msgs;
     // (replicated frontier: the remote rows of the hop mark their receivers too)
-    if (ps.rep) return prev + (h >= 2 ? ps.rep_in : 0) < ps.n_nodes / ps.mark_div;
+    if (ps.rep) return !ps.rep_rows && prev + (h >= 2 ? ps.rep_in : 0) < ps.n_nodes / ps.mark_div;
     return prev < ps.n_nodes / ps.mark_div && !(ps.halo && !ps.halo_tag);
 }
 // Range shards: can a remote sender's row reach this hop?  The compacted

@@ -449,6 +449,9 @@ SIGNATURES = {
     "gsx_prop_rep_pack_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "gsx_prop_rep_step": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_void_p), P(C.c_uint64)]),
     "gsx_prop_rep_sends_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_rows": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gsx_prop_rep_rows_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gsx_prop_rep_rows_step": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_void_p), C.c_void_p]),
     "gsx_prop_rep_sends_recv": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gsx_hb_set_px_log": (C.c_int, [C.c_void_p, C.c_size_t]),
     "gsx_hb_px_records": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),

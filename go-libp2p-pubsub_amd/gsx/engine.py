@@ -350,6 +350,20 @@ class Engine:
         cc = (C.c_uint64 * max(n, 1))(*[int(c) for c in counts])
         self._chk(self.lib.gsx_prop_rep_step(self.h, n, pp, cc), "gsx_prop_rep_step")
 
+    def prop_rep_rows(self, on: bool = True):
+        """This call's replicated frontier moves as dense row slices (gsx_prop_rep_rows)."""
+        self._chk(self.lib.gsx_prop_rep_rows(self.h, 1 if on else 0), "gsx_prop_rep_rows")
+
+    def prop_rep_rows_export(self, rows, occ):
+        """This rank's rows of the hop just run (n_local x W) and its occupancy-bit row (device)."""
+        self._chk(self.lib.gsx_prop_rep_rows_export(self.h, self._p(rows), self._p(occ)), "gsx_prop_rep_rows_export")
+
+    def prop_rep_rows_step(self, parts, occ_sum):
+        """Every rank's rows of the hop (parts[k], the shard plan's ranges) and the summed bit row, then the next hop."""
+        n = len(parts)
+        pp = (C.c_void_p * max(n, 1))(*[self._p(t).value for t in parts])
+        self._chk(self.lib.gsx_prop_rep_rows_step(self.h, n, pp, self._p(occ_sum)), "gsx_prop_rep_rows_step")
+
     def prop_rep_sends_pack(self, out):
         self._chk(self.lib.gsx_prop_rep_sends_pack(self.h, self._p(out)), "gsx_prop_rep_sends_pack")
 

@@ -140,7 +140,13 @@ class RangeSharded:
     fixed splits, so hops run back to back with no host sync: every `chunk`
     hops one all-reduce of the per-hop delivery counts (device) and one read
     find the hop that delivered nothing on any rank — the hops after it were
-    empty and changed nothing (1 / chunk host syncs per hop)."""
+    empty and changed nothing (1 / chunk host syncs per hop).
+
+    The lean calls take the replicated frontier (gsx_prop_rep_*): compact=True
+    moves every rank's new frontier rows as (global id, row) entries, padded
+    to the largest rank's count (one host read per hop sizes the all-gather);
+    compact=False moves every rank's dense slice of the rows and a summed
+    occupancy-bit row per hop, chunked like the dense exchange (_rep_rows)."""
 
     def __init__(self, backend, rank_lo, transport, compact=True, chunk=4):
         self.be = backend
@@ -237,7 +243,7 @@ class RangeSharded:
         be.prop_begin(msgs, cfg)
         last = 0  # the last hop that delivered on any rank (gsx_prop_set_last_hop)
         if getattr(be, "prop_rep", None) is not None and be.prop_rep():
-            self.last_mode = "replicated"
+            self.last_mode = "replicated" if self.compact else "replicated-rows"
             last = self._propagate_rep(W, cfg)
         elif self.compact:
             self.last_mode = "compact"
@@ -298,7 +304,9 @@ class RangeSharded:
         tp.all_to_all(rf[: self.n_recv], sf[: self.n_send], self.recv_counts, self.send_counts)
         be.prop_rep_fwd_recv(rf)
         last = 0
-        if cfg.max_hops >= 1:
+        if cfg.max_hops >= 1 and not self.compact:
+            last = self._rep_rows(W, cfg)
+        elif cfg.max_hops >= 1:
             be.prop_rep_step()
             self.hops_run += 1
             n_local = max(int(getattr(be, "n_nodes", 0) or 0), 1)
@@ -335,6 +343,63 @@ class RangeSharded:
         be.prop_rep_sends_pack(ss)
         tp.all_to_all(rs[: self.n_recv], ss[: self.n_send], self.recv_counts, self.send_counts)
         be.prop_rep_sends_recv(rs)
+        return last
+
+    def _rep_rows(self, W, cfg) -> int:
+        """The replicated frontier as dense row slices (compact=False;
+        gsx_prop_rep_rows): hop 1 from the message list, then per hop one
+        all-gather of every rank's slice of the hop's rows (n_local x W words,
+        padded to the largest range) and one all-reduce of the occupancy-bit
+        rows (the ranks own disjoint bits: their sum is their union) — no host
+        read inside a chunk; every `chunk` hops one all-reduce of the per-hop
+        receipts and one read find the end (the hops after a hop that delivered
+        nothing on any rank run empty and change nothing: 1 / chunk host syncs
+        per hop, up to chunk - 1 empty hops).  -> the last hop that delivered."""
+        torch = _torch()
+        be, tp = self.be, self.tp
+        dev, R = tp.device, tp.world
+        lens = np.diff(self.rank_lo.astype(np.int64))
+        L = max(int(lens.max()), 1)
+        n_total = int(self.rank_lo[-1])
+        ow = (n_total + 63) // 64 + 1
+        key = ("rows", W, L, ow)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            bufs = (torch.zeros((L, W), dtype=torch.int64, device=dev), torch.zeros(ow, dtype=torch.int64, device=dev),
+                    torch.zeros(abi.GSX_MAX_HOPS + 1, dtype=torch.int64, device=dev))
+            self._bufs = {key: bufs}
+        rows, occ, cnt = bufs
+        n_local = int(lens[tp.rank])
+        be.prop_rep_rows(True)
+        be.prop_rep_step()  # hop 1: hop 0's rows are every rank's already
+        self.hops_run += 1
+        h, last = 1, 0
+        while h < cfg.max_hops:
+            k = min(self.chunk, cfg.max_hops - h)
+            for _ in range(k):  # no host sync inside the chunk
+                be.prop_rep_rows_export(rows[:n_local], occ)
+                parts = tp.all_gather(rows)
+                tp.all_reduce_sum(occ)
+                self.sent_bytes += L * W * 8 * (R - 1) + ow * 8
+                be.prop_rep_rows_step([parts[j][: int(lens[j])] for j in range(R)], occ)
+                self.hops_run += 1
+                h += 1
+            be.prop_hop_counts_dev(cnt)
+            tp.all_reduce_sum(cnt)
+            c = cnt.cpu().numpy()  # the chunk's one host sync
+            self.host_syncs += 1
+            nz = np.nonzero(c[1 : h + 1])[0]
+            last = int(nz[-1]) + 1 if len(nz) else 0
+            if (c[h - k + 1 : h + 1] == 0).any():
+                break
+        else:
+            if h == 1:  # (max_hops 1: no chunk ran, hop 1's receipts decide `last`)
+                be.prop_hop_counts_dev(cnt)
+                tp.all_reduce_sum(cnt)
+                c = cnt.cpu().numpy()
+                self.host_syncs += 1
+                nz = np.nonzero(c[1 : h + 1])[0]
+                last = int(nz[-1]) + 1 if len(nz) else 0
         return last
 
     def heartbeat(self, tick: int, now: int, seed: int):
@@ -713,20 +778,32 @@ class LocalTransport:
         self._gather(None)
         return vals
 
+    def _settled(self, t):
+        """A copy of t whose values are final (members run on streams of their own)."""
+        torch = _torch()
+        c = t.clone()
+        if c.is_cuda:
+            torch.cuda.synchronize(c.device)
+        return c
+
     def all_reduce_sum(self, t):
-        vals = self._gather(t.clone())
+        vals = self._gather(self._settled(t))
         acc = vals[0].clone()
         for v in vals[1:]:
             acc += v
         t.copy_(acc)
+        if t.is_cuda:
+            _torch().cuda.synchronize(t.device)
         self._gather(None)
 
     def all_reduce_max(self, t):
-        vals = self._gather(t.clone())
+        vals = self._gather(self._settled(t))
         acc = vals[0].clone()
         for v in vals[1:]:
             acc = acc.maximum(v)
         t.copy_(acc)
+        if t.is_cuda:
+            _torch().cuda.synchronize(t.device)
         self._gather(None)
 
 

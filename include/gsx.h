@@ -624,8 +624,27 @@ int gsx_prop_set_last_hop(gsx_engine* e, uint32_t last_hop);
  *                             moved like the fwd bytes to
  *   gsx_prop_rep_sends_recv   (device u64 per receive slot): duplicates (P3
  *                             credits) or graylisted copies at the receivers;
- * then gsx_prop_set_last_hop and gsx_prop_end as for the per-pair exchange. */
+ * then gsx_prop_set_last_hop and gsx_prop_end as for the per-pair exchange.
+ *
+ * Dense rows instead of entries (no host read per hop): after the fwd bytes,
+ *   gsx_prop_rep_rows(e, 1)   for this call (before hop 1: no very sparse
+ *                             marking, remote rows mark no receivers);
+ *   gsx_prop_rep_step         hop 1 with no parts, then per hop h >= 2:
+ *   gsx_prop_rep_rows_export  this rank's slice of the hop's rows (device,
+ *                             n_local x W words) and its occupancy-bit row
+ *                             (device, (n_total + 63) / 64 + 1 words) ...
+ *   gsx_prop_rep_rows_step    ... every rank's slice (parts[k]: rank k's
+ *                             rows, the shard plan's ranges; one all-gather)
+ *                             and the bit rows summed over the ranks (one
+ *                             all-reduce: the ranks own disjoint bits), then
+ *                             the next hop; the driver reads the summed
+ *                             per-hop receipts (gsx_prop_hop_counts_dev) once
+ *                             per chunk of hops to find the end: the hops
+ *                             after an empty one run empty and change nothing. */
 int gsx_prop_rep(gsx_engine* e, uint32_t* on);
+int gsx_prop_rep_rows(gsx_engine* e, uint32_t on);
+int gsx_prop_rep_rows_export(gsx_engine* e, uint64_t* rows, uint64_t* occ);
+int gsx_prop_rep_rows_step(gsx_engine* e, uint32_t n_parts, const uint64_t* const* parts, const uint64_t* occ_sum);
 int gsx_prop_rep_fwd_pack(gsx_engine* e, uint8_t* out);
 int gsx_prop_rep_fwd_recv(gsx_engine* e, const uint8_t* in);
 int gsx_prop_rep_pack_dev(gsx_engine* e, uint64_t* out, int64_t* d_counts);
