@@ -484,3 +484,134 @@ def _as_tensor(a):
     import torch
 
     return torch.from_numpy(np.ascontiguousarray(a))
+
+
+class RepRowsToy:
+    """Stand-in for one range shard in the replicated frontier's dense-row
+    exchange (gsx.h gsx_prop_rep_rows*, gsx/shard.py RangeSharded._rep_rows),
+    TEST INFRASTRUCTURE ONLY: floodsub over a CSR shard (every pair forwards
+    everything), arrival hops only.  Every rank keeps the frontier rows of ALL
+    nodes two hops deep and its own occupancy bits per hop, exactly the state
+    the driver moves (one all-gather of the ranks' row slices, one summed bit
+    row per hop; the per-hop receipts read once per chunk), so the driver's
+    collective sequence, its chunked end test and the max_hops cut run over
+    gloo against a plain BFS."""
+
+    def __init__(self, shard, n_total):
+        self.sh = shard
+        self.lo = shard.node_lo
+        self.n = shard.node_hi - shard.node_lo
+        self.n_nodes = self.n
+        self.n_total = n_total
+        self.row_ptr = shard.row_ptr
+        self.col = shard.col.astype(np.int64)
+        self.rows_on = False
+
+    # the shard plan: no per-pair exchange in this mode
+    def shard_recv_plan(self, rank_lo):
+        return np.zeros(len(rank_lo) - 1, dtype=np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint32)
+
+    def shard_send_plan(self, asked, u, v):
+        pass
+
+    def shard_set_halo_bases(self, b):
+        pass
+
+    def prop_begin(self, msgs, cfg):
+        self.m = len(msgs)
+        self.W = prop_words(self.m)
+        self.max_hops = int(cfg.max_hops)
+        self.ow = (self.n_total + 63) // 64 + 1
+        self.front = np.zeros((2, self.n_total, self.W), dtype=np.uint64)
+        self.occ = np.zeros((2, self.ow), dtype=np.uint64)
+        self.seen = np.zeros((self.n, self.W), dtype=np.uint64)
+        self.hop = np.full((self.m, self.n), -1, dtype=np.int32)
+        self.cnt = np.zeros(abi.GSX_MAX_HOPS + 1, dtype=np.int64)
+        self.h = 0
+        self.last = None
+        for k, s in enumerate(msgs["source"]):  # hop 0 is every rank's: the message list
+            s = int(s)
+            self.front[0, s, k // 64] |= np.uint64(1 << (k % 64))
+            self.occ[0, s // 64] |= np.uint64(1 << (s % 64))
+            if self.lo <= s < self.lo + self.n:
+                self.seen[s - self.lo, k // 64] |= np.uint64(1 << (k % 64))
+                self.hop[k, s - self.lo] = 0
+
+    def prop_rep(self):
+        return True
+
+    def prop_rep_fwd_pack(self, out):
+        pass
+
+    def prop_rep_fwd_recv(self, inp):
+        pass
+
+    def prop_rep_rows(self, on=True):
+        assert self.h == 0
+        self.rows_on = bool(on)
+
+    def _hop(self):
+        assert self.h < self.max_hops
+        self.h += 1
+        p, c = (self.h - 1) & 1, self.h & 1
+        self.occ[c] = 0
+        for u in range(self.n):
+            acc = np.zeros(self.W, dtype=np.uint64)
+            for q in range(self.row_ptr[u], self.row_ptr[u + 1]):
+                v = int(self.col[q])
+                if int(self.occ[p, v // 64]) >> (v % 64) & 1:
+                    acc |= self.front[p, v]
+            new = acc & ~self.seen[u]
+            self.front[c, self.lo + u] = new
+            if new.any():
+                g = self.lo + u
+                self.occ[c, g // 64] |= np.uint64(1 << (g % 64))
+                self.seen[u] |= new
+                for w in range(self.W):
+                    bits = int(new[w])
+                    for b in range(64):
+                        if bits >> b & 1:
+                            self.hop[w * 64 + b, u] = self.h
+                            self.cnt[self.h] += 1
+
+    def prop_rep_step(self, parts=(), counts=()):
+        assert self.h == 0 and not parts  # hop 1: no exchange
+        self._hop()
+
+    def prop_rep_rows_export(self, rows, occ):
+        assert self.rows_on and self.h >= 1
+        rows.copy_(_as_tensor(self.front[self.h & 1, self.lo : self.lo + self.n].view(np.int64)))
+        occ.copy_(_as_tensor(self.occ[self.h & 1].view(np.int64)))
+
+    def prop_rep_rows_step(self, parts, occ_sum):
+        c = self.h & 1
+        off = 0
+        for part in parts:  # (the ranks' slices in rank order: contiguous ranges)
+            a = part.cpu().numpy().view(np.uint64).reshape(-1, self.W)
+            self.front[c, off : off + len(a)] = a
+            off += len(a)
+        assert off == self.n_total
+        self.occ[c] = occ_sum.cpu().numpy().view(np.uint64)
+        self._hop()
+
+    def prop_hop_counts_dev(self, out):
+        out.copy_(_as_tensor(self.cnt))
+
+    def prop_rep_sends_pack(self, out):
+        pass
+
+    def prop_rep_sends_recv(self, inp):
+        pass
+
+    def prop_set_last_hop(self, last):
+        self.last = int(last)
+
+    def prop_end(self):
+        out = abi.PropOut()
+        out.deliveries = int(self.cnt.sum())
+        out.transmissions = out.deliveries
+        for h, c in enumerate(self.cnt):
+            out.hop_deliveries[h] = int(c)
+            if c:
+                out.hops = h
+        return out

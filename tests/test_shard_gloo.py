@@ -63,6 +63,13 @@ def _worker(rank, world, port, payload, q):
                 local, tot = rs.propagate(payload["msgs"], cfg)
                 hop, frm = be.prop_results(len(payload["msgs"]))
                 q.put((rank, local, tot, hop, frm))
+        elif payload["mode"] == "reprows":
+            import shard_emulator as emu
+
+            be = emu.RepRowsToy(payload["shards"][rank], payload["n"])
+            rs = gs.RangeSharded(be, payload["rank_lo"], tp, compact=False, chunk=payload["chunk"])
+            local, tot = rs.propagate(payload["msgs"], cfg)
+            q.put((rank, local, tot, be.hop, (rs.host_syncs, rs.hops_run, be.last, rs.last_mode)))
         elif payload["mode"] == "replica_hb":
             import gossip_cases as gc
 
@@ -245,3 +252,55 @@ def test_message_parallel_heartbeat_gloo(world):
         for v in range(len(cached)):
             assert np.array_equal(np.sort(cached[v]), np.sort(want_cached[v])), (rank, v)
         assert gathered > 0
+
+
+def _bfs_hops(ov, msgs, max_hops):
+    """Arrival hop of every (message, node) of a flood over the whole overlay (-1: never)."""
+    n = len(ov.row_ptr) - 1
+    hop = np.full((len(msgs), n), -1, dtype=np.int32)
+    for k, s in enumerate(msgs["source"]):
+        hop[k, int(s)] = 0
+        front = [int(s)]
+        for h in range(1, max_hops + 1):
+            nxt = []
+            for u in range(n):
+                if hop[k, u] >= 0:
+                    continue
+                nb = ov.col[ov.row_ptr[u] : ov.row_ptr[u + 1]]
+                if any(hop[k, int(v)] == h - 1 for v in nb):
+                    hop[k, u] = h
+                    nxt.append(u)
+            if not nxt:
+                break
+            front = nxt
+    return hop
+
+
+@pytest.mark.parametrize("world,chunk,max_hops", [(2, 4, 30), (3, 2, 30), (2, 3, 3), (3, 1, 30)])
+def test_replicated_rows_driver_gloo(world, chunk, max_hops):
+    """RangeSharded._rep_rows (the replicated frontier as dense row slices:
+    one all-gather + one summed occupancy row per hop, the per-hop receipts
+    read once per chunk) over gloo with the RepRowsToy shards: the stitched
+    arrival hops equal a BFS over the whole overlay, every rank ends on the
+    same last delivering hop, and the host reads are one per chunk of hops
+    (plus the max_hops cut's)."""
+    n, m = 150, 70
+    seed = 5 + world
+    ov = pc.overlay(n, 3, seed)
+    msgs = pc.messages(n, m, seed)
+    cfg = pc.config(abi.GSX_ROUTER_FLOODSUB, credit=0, max_hops=max_hops)
+    want = _bfs_hops(ov, msgs, max_hops)
+    rank_lo = synth.shard_ranges(n, world)
+    shards = [synth.shard_of(ov, int(rank_lo[k]), int(rank_lo[k + 1])) for k in range(world)]
+    res = _run(world, dict(mode="reprows", shards=shards, n=n, rank_lo=rank_lo, msgs=msgs, cfg=_cfg_dict(cfg),
+                           chunk=chunk))
+    got = np.concatenate([r[3] for r in res], axis=1)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    last_true = int(want.max())
+    syncs, hops, last, mode = res[0][4]
+    assert mode == "replicated-rows"
+    assert all(r[4][2] == last_true for r in res)  # gsx_prop_set_last_hop: the last hop that delivered anywhere
+    assert all(r[2] == res[0][2] for r in res)
+    assert res[0][2]["deliveries"] == int((want > 0).sum())
+    assert hops <= min(max_hops, last_true + chunk)  # at most chunk - 1 empty hops past the end
+    assert syncs <= -(-(hops - 1) // chunk) + 1  # one read per chunk (+ max_hops 1's)
