@@ -2863,6 +2863,11 @@ int prop_begin(gsx_engine* e, const gsx_msg* msgs, size_t m, const gsx_prop_conf
     static const bool no_rep = getenv("GSX_SHARD_PAIRS") != nullptr;
     P.rep = e->sharded() && e->n_ranks > 1 && m > 0 && gsx::hop_lean(ps) && !no_rep &&
             e->n_total <= gsx::PIN_NODE_MASK;
+    if (P.rep && W == 1 && !getenv("GSX_NO_SAT_SKIP") && !getenv("GSX_HOP_NO_FAST1")) {
+        // one-word lean calls on the replicated frontier: saturated receivers skipped as on
+        // one engine; a cross pair's edge sends go with its end-of-call sends (k_rep_sends)
+        ps.edge_late = 1;
+    }
     if (P.rep) {
         const size_t NT = e->n_total, ow = (NT + 63) / 64 + 1;  // (the kernels' occ_g row: one spare word)
         if (P.rep_words < 2 * (uint64_t)NT * W) {

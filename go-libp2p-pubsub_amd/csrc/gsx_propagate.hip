@@ -872,7 +872,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
             const uint64_t seen = ps.seen[u];
             // a receiver that has seen every message of the call gets nothing new: its walk is
             // skipped (its senders' STAT_EDGE_SENDS are counted at the call's end: edge_late)
-            if (SH == 0 && ps.edge_late && seen == ps.full1) q1 = q0;
+            if (SH != 1 && ps.edge_late && seen == ps.full1) q1 = q0;
             const uint64_t mine = (SH == 1 && occ_bit(occ_src, u)) ? ps.origin[u] : 0ull;  // (remote rows only)
             uint64_t sa = seen;
             uint2 pn[R];
@@ -932,7 +932,7 @@ __global__ __launch_bounds__(256) void k_prop_hop_fast1(PropState ps, uint32_t h
                 for (int k = 0; k < R; ++k) {  // round k: the quad's senders in order
                     const uint64_t x = c[k];
                     const bool hl = SH == 1 && pv[k] != NO_PAIR && (pv[k] & HALO);
-                    if (!hl && !(SH == 0 && ps.edge_late)) n_send += x != 0;  // (a remote sender's are counted at its pack)
+                    if (!hl && !(SH != 1 && ps.edge_late)) n_send += x != 0;  // (a remote sender's are counted at its pack)
                     uint64_t incl = x;
 #pragma unroll
                     for (uint32_t off = 1; off < (uint32_t)G; off <<= 1) {
@@ -1719,30 +1719,43 @@ __global__ __launch_bounds__(256) void k_rep_sends(PropState ps, uint32_t h_run,
         }
         if (ps.drop && v_src && (fw & FWD_PUBLISH))
             for (uint32_t w = 0; w < W; ++w) xdrop += __popcll(ps.origin[(size_t)v * W + w] & ps.drop[w]);
-        out[j] = (uint64_t)sends | ((uint64_t)xdrop << 32);
+        // edge_late (one-word calls: at most 64 sends and 64 own copies: 16-bit fields): the
+        // hops at which v's row to u was non-empty, as k_prop_dups counts a local pair's —
+        // hop 1 its publishes, later ones its receipts of the hop before (vcount's hops);
+        // the receiver's rank drops them with the sends when it graylists v
+        uint64_t edges = 0;
+        if (ps.edge_late)
+            edges = ((fw & FWD_PUBLISH) && h_run >= 1 && v_src ? 1u : 0u) +
+                    ((fw & FWD_FORWARD) ? (uint32_t)(vcnt[v] >> 56) : 0u);
+        out[j] = ps.edge_late ? (uint64_t)sends | ((uint64_t)xdrop << 16) | (edges << 32)
+                              : (uint64_t)sends | ((uint64_t)xdrop << 32);
     }
 }
 // At u's rank, per receive slot (pair q = (u -> v), v remote): v's sends
 // become duplicates (P3 credits through the pending counts: sends minus u's
 // first receipts from v) or, when u's AcceptFrom drops v, graylisted copies.
 __global__ __launch_bounds__(256) void k_rep_sends_recv(PropState ps, const uint64_t* __restrict__ in) {
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[3] = {0, 0, 0};
     for (uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x; q < ps.n_pairs; q += (uint64_t)gridDim.x * 256u) {
         const uint32_t rv = ps.rev[q];
         if (rv == NO_PAIR || !(rv & HALO)) continue;
         const uint64_t x = in[rv & HALO_SLOT];
         if (!x) continue;
-        const uint32_t sends = (uint32_t)x, xdrop = (uint32_t)(x >> 32);
-        if (ps.gate && (ps.fwd[q] & FWD_GIN)) {
+        const uint32_t sends = ps.edge_late ? (uint32_t)x & 0xFFFFu : (uint32_t)x;
+        const uint32_t xdrop = ps.edge_late ? (uint32_t)(x >> 16) & 0xFFFFu : (uint32_t)(x >> 32);
+        const uint32_t edges = ps.edge_late ? (uint32_t)(x >> 32) : 0u;
+        const bool gin = (ps.fwd[q] & FWD_GIN) != 0;  // u drops v's RPCs
+        if (ps.gate && gin) {
             cnt[1] += sends + xdrop;
         } else {
             const uint32_t dup = sends - ps.fcnt[q];
             cnt[0] += dup;
             if (dup && ps.credit) ps.dupcnt[q] += dup;
         }
+        if (!gin) cnt[2] += edges;  // (one engine's compacted senders leave a graylisted sender out)
     }
-    const uint32_t slot[2] = {STAT_DUPS, STAT_GRAY};
-    block_count<2>(cnt, ps.stats, slot);
+    const uint32_t slot[3] = {STAT_DUPS, STAT_GRAY, STAT_EDGE_SENDS};
+    block_count<3>(cnt, ps.stats, slot);
 }
 
 // ---- P2/P3 credits ------------------------------------------------------------

@@ -620,7 +620,9 @@ int gsx_prop_set_last_hop(gsx_engine* e, uint32_t last_hop);
  *                             next hop, until a hop delivered nothing on any
  *                             rank;
  *   gsx_prop_rep_sends_pack   per send slot, what its pair sent over the call
- *                             (device u64: sends | own unaccepted copies << 32),
+ *                             (device u64: sends | own unaccepted copies << 32;
+ *                             one-word calls: sends | copies << 16 | the hops
+ *                             its row was non-empty << 32, the edge sends),
  *                             moved like the fwd bytes to
  *   gsx_prop_rep_sends_recv   (device u64 per receive slot): duplicates (P3
  *                             credits) or graylisted copies at the receivers;
