@@ -66,7 +66,7 @@ def build_engine(n, T, d, seed, device):
     return ov, e
 
 
-PMC_FILE = "pmc_r05.json"  # written by tools/pmc.sh (tools/pmc_bytes.py)
+PMC_FILE = "pmc_r06.json"  # written by tools/pmc.sh (tools/pmc_bytes.py)
 
 
 def load_pmc():

@@ -266,6 +266,7 @@ struct PropState {
     uint32_t chg_cap;
     uint32_t inc;        // fwd / pin / cent hold the previous call's values: update them incrementally
     uint32_t flast_every;  // k_prop_hop_fast keeps flast at every hop (stepped calls), else at max_hops only
+    uint32_t flast_live;   // this call's hops wrote flast (else it is all zero: k_prop_dups skips its load)
     // Topic-term cache of the re-scoring fold (k_prop_count<true, true>):
     // tterm[q * n_topics + t] = topic_score() of record (q, t) (times its
     // weight), valid for pair q while tgen[q] == tepoch.  The host moves tepoch

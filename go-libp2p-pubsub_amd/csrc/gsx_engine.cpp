@@ -3094,6 +3094,7 @@ int prop_end(gsx_engine* e, gsx_prop_out* out) {
     }
     {
         gsx::PropState pd = ps;
+        pd.flast_live = P.flast_dirty ? 1u : 0u;  // (flast is cleared at a call's start once written)
         if (defer) {
             pd.acc_s = e->d_acc_s;
             pd.acc_f = e->d_acc_f;

@@ -1399,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_prop_dups(PropState ps, uint32_t h_run,
             vca[i] = live ? vcnt[va[i]] : 0;
             const bool fl = live && !ps.from_mask && (fa[i] & FWD_FORWARD) && h_run >= 1;
             fca[i] = (fl || (ps.acc_f && r < ps.n_pairs)) ? ps.fcnt[r] : 0;
-            fla[i] = fl ? ps.flast[r] : 0;
+            fla[i] = (fl && ps.flast_live) ? ps.flast[r] : 0;
         }
         if (!GRAY_ONLY && ps.edge_late) {  // STAT_EDGE_SENDS of one-word calls (k_prop_hop_fast1 skips
                                            // saturated receivers): per pair u's pin lets through, the hops at
