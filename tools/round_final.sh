@@ -15,10 +15,10 @@ mkdir -p "$O"
 step() {  # step NAME SECONDS CMD...
     local name=$1 secs=$2
     shift 2
-    echo "=== $name $(date +%T)"
+    echo "=== $name $(date +%T)" >&2
     timeout -k 10 "$secs" "$@"
     local rc=$?
-    echo "=== $name rc=$rc $(date +%T)"
+    echo "=== $name rc=$rc $(date +%T)" >&2
     return $rc
 }
 case "$PART" in
