@@ -454,6 +454,9 @@ struct alignas(16) IhaveSlot {
     uint64_t hash;
     uint32_t len, tag;
 };
+constexpr uint8_t IHAVE_OWN = 0x80;     // ihave_tag: the pair's own slot holds the list
+constexpr uint8_t IHAVE_FAN = 0x40;     // ihave_tag: sent by the fanout pass (its units' half of ihave_unit)
+constexpr uint32_t IHAVE_TAG_MAX = 0x3F;  // byte tags cycle 1..63 (the array is cleared at the wrap)
 struct GxBatch {
     const uint64_t* mem;  // [node][word]: in the node's cache
     const uint64_t* all;  // [node][word]: seen by the node
@@ -537,8 +540,15 @@ struct HbState {
     uint32_t* n_hub;       // [topic]
     const uint32_t* hubs;  // nodes with more than HB_LANE_DEG peers (k_hb_recv_hub)
     uint32_t n_hubs;
-    IhaveSlot* ihave_slot;  // [topic][pair] the IHAVE the pair's sender sent (valid under tag == ihave_cur)
+    // emitGossip's observable output (gsx_gossip_results), per (topic, pair): a
+    // one-byte mark of this round's targets (ihave_tag: IHAVE_TAG(cur8) = the
+    // sending unit's list, in ihave_unit [topic][node], written once per unit;
+    // | IHAVE_OWN = a truncated list's subset, in the pair's own ihave_slot)
+    IhaveSlot* ihave_slot;  // [topic][pair] a truncated list's subset (valid under tag == ihave_cur)
+    IhaveSlot* ihave_unit;  // [pass][topic][node] the unit's whole list (hash, len) of this round (pass 1: fanout)
+    uint8_t* ihave_tag;     // [topic][pair] cur8 (| IHAVE_OWN) on this round's targets
     uint32_t ihave_cur;    // this round's tag
+    uint32_t ihave_cur8;   // this round's byte tag (1..IHAVE_TAG_MAX)
     uint8_t* gelig;        // [pair] GELIG_TARGET | GELIG_SCORE as the round started (k_hb_gelig)
     // the gossip exchange (step (D)); null when it is off
     uint64_t* ihave_bits;  // [pair (u -> v), the receiver's]: topics v sent u an IHAVE for this round

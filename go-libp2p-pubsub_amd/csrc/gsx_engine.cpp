@@ -113,7 +113,9 @@ struct gsx_engine {
     uint32_t *d_long = nullptr, *d_nlong = nullptr;
     unsigned long long* d_hbstats = nullptr;
     uint32_t* d_rngk = nullptr;
-    gsx::IhaveSlot* d_ihave_slot = nullptr;  // [topic][pair] (emitGossip's IHAVE slots)
+    gsx::IhaveSlot* d_ihave_slot = nullptr;  // [topic][pair] (emitGossip's truncated-list IHAVE slots)
+    gsx::IhaveSlot* d_ihave_unit = nullptr;  // [topic][node] (a unit's whole IHAVE list of the round)
+    uint8_t* d_ihave_tag = nullptr;          // [topic][pair] this round's targets (HbState::ihave_tag)
     uint32_t *d_work = nullptr, *d_nwork = nullptr, *d_hubwork = nullptr, *d_hubs = nullptr;  // heartbeat worklists
     uint8_t* d_tcnt = nullptr;
     uint16_t* d_mcount = nullptr;
@@ -889,7 +891,7 @@ void free_state(gsx_engine* e) {
     void* hb[] = {e->d_work, e->d_hubwork, e->d_nwork, e->d_hubs, e->d_tcnt, e->d_mcount,
                   e->d_backoff, e->d_bo8, e->d_ctl, e->d_resp,   e->d_dirty,     e->d_long,
                   e->d_nlong,   e->d_hbstats,   e->d_tr_acc,    e->d_tr_hp,   e->d_rngk,      e->d_ihave_slot, e->d_gelig, e->d_gb,
-                  e->d_mc_digest};
+                  e->d_mc_digest, e->d_ihave_unit, e->d_ihave_tag};
     for (void* p : hb)
         if (p) (void)hipFree(p);
     e->d_backoff = nullptr;
@@ -978,7 +980,8 @@ void free_state(gsx_engine* e) {
         e->px_last = 0;
     }
     e->d_rngk = nullptr;
-    e->d_ihave_slot = nullptr;
+    e->d_ihave_slot = e->d_ihave_unit = nullptr;
+    e->d_ihave_tag = nullptr;
     e->d_work = e->d_hubwork = e->d_nwork = e->d_hubs = nullptr;
     e->d_tcnt = nullptr;
     e->d_mcount = nullptr;
@@ -1502,6 +1505,8 @@ int hb_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_resp, E)) || (rc = dalloc(e, &e->d_dirty, 4 * E)) ||
         (rc = dalloc(e, &e->d_long, (size_t)e->n_nodes)) || (rc = dalloc(e, &e->d_nlong, 2 * std::max<size_t>(e->T, 1))) ||
         (rc = dalloc(e, &e->d_rngk, (size_t)e->T * e->n_nodes)) || (rc = dalloc(e, &e->d_ihave_slot, TE)) ||
+        (rc = dalloc(e, &e->d_ihave_unit, 2 * (size_t)e->T * std::max<size_t>(e->n_nodes, 1))) ||
+        (rc = dalloc(e, &e->d_ihave_tag, std::max<size_t>(TE, 1))) ||
         (rc = dalloc(e, &e->d_work, (size_t)e->T * 64 * ((e->n_nodes + 63) / 64))) ||
         (rc = dalloc(e, &e->d_tcnt, (size_t)e->T * ((e->n_nodes + 63) / 64) + 1)) ||
         (rc = dalloc(e, &e->d_mcount, (size_t)e->T * e->n_nodes + 1)) ||
@@ -1512,6 +1517,7 @@ int hb_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_hbstats, (size_t)gsx::HB_STAT_WORDS)))
         return rc;
     HIPCHK(e, hipMemsetAsync(e->d_ihave_slot, 0, sizeof(gsx::IhaveSlot) * (TE ? TE : 1), e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, std::max<size_t>(TE, 1), e->stream));
     e->ihave_round = 0;
     if (!e->hubs_host.empty())
         HIPCHK(e, hipMemcpyAsync(e->d_hubs, e->hubs_host.data(), 4 * e->hubs_host.size(), hipMemcpyHostToDevice,
@@ -4222,8 +4228,16 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         HIPCHK(e, hipMemsetAsync(e->d_ihave_slot, 0, sizeof(gsx::IhaveSlot) * (size_t)e->T * e->E, e->stream));
         e->ihave_round = 1;
     }
+    // the targets' byte tags cycle 1..IHAVE_TAG_MAX: a stale byte equal to this
+    // round's can only be 127 rounds old, so the array is cleared as the cycle restarts
+    const uint32_t cur8 = (e->ihave_round - 1) % gsx::IHAVE_TAG_MAX + 1;
+    if (cur8 == 1 && e->ihave_round > 1)
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_tag, 0, (size_t)e->T * e->E, e->stream));
     h.ihave_slot = e->d_ihave_slot;
+    h.ihave_unit = e->d_ihave_unit;
+    h.ihave_tag = e->d_ihave_tag;
     h.ihave_cur = e->ihave_round;
+    h.ihave_cur8 = cur8;
     h.gelig = e->d_gelig;
     e->have_gossip = !e->gb_host.empty();
     // (A) the scan of every unit, then per topic, ascending: maintenance, then
@@ -5715,16 +5729,35 @@ int gsx_gossip_results(gsx_engine* e, uint32_t* ihave_len, uint64_t* ihave_diges
         if (ihave_digest) std::memset(ihave_digest, 0, 8 * TE);
         return GSX_OK;
     }
-    std::vector<gsx::IhaveSlot> sl(TE);
-    if (TE) HIPCHK(e, hipMemcpyAsync(sl.data(), e->d_ihave_slot, sizeof(gsx::IhaveSlot) * TE, hipMemcpyDeviceToHost,
+    // per (topic, pair): this round's byte tag says whether the pair's owner sent
+    // an IHAVE and where its (hash, len) is: the unit's record, or (IHAVE_OWN) a
+    // truncated list's subset in the pair's own slot
+    const size_t TN = 2 * (size_t)e->T * e->n_nodes;  // (the mesh pass's units, then the fanout pass's)
+    std::vector<gsx::IhaveSlot> sl(TE), un(TN);
+    std::vector<uint8_t> tg(TE);
+    if (TE) {
+        HIPCHK(e, hipMemcpyAsync(sl.data(), e->d_ihave_slot, sizeof(gsx::IhaveSlot) * TE, hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipMemcpyAsync(tg.data(), e->d_ihave_tag, TE, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (TN) HIPCHK(e, hipMemcpyAsync(un.data(), e->d_ihave_unit, sizeof(gsx::IhaveSlot) * TN, hipMemcpyDeviceToHost,
                                      e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     const uint32_t cur = e->ihave_round;  // (0: no heartbeat ran, every slot empty)
-    for (size_t i = 0; i < TE; ++i) {
-        const bool now = sl[i].tag == cur && cur != 0;  // (else a slot of an earlier round)
-        if (ihave_len) ihave_len[i] = now ? sl[i].len : 0;
-        if (ihave_digest) ihave_digest[i] = now ? sl[i].hash : 0;
-    }
+    const uint8_t cur8 = cur ? (uint8_t)((cur - 1) % gsx::IHAVE_TAG_MAX + 1) : 0;
+    for (uint32_t t = 0; t < e->T; ++t)
+        for (uint32_t v = 0; v < e->n_nodes; ++v)
+            for (int64_t r = e->row_ptr[v]; r < e->row_ptr[v + 1]; ++r) {
+                const size_t i = (size_t)t * e->E + (size_t)r;
+                const uint8_t b = tg[i];
+                const gsx::IhaveSlot* x = nullptr;  // (else a slot of an earlier round)
+                if (cur8 && (b & gsx::IHAVE_TAG_MAX) == cur8)
+                    x = (b & gsx::IHAVE_OWN) ? &sl[i]
+                                             : &un[((b & gsx::IHAVE_FAN) ? (size_t)e->T : 0) * e->n_nodes +
+                                                   (size_t)t * e->n_nodes + v];
+                if (ihave_len) ihave_len[i] = x ? x->len : 0;
+                if (ihave_digest) ihave_digest[i] = x ? x->hash : 0;
+            }
     return GSX_OK;
 }
 

@@ -1057,9 +1057,12 @@ __global__ __launch_bounds__(256) void k_hb_gossip(DevState s, HbState h, uint32
                             Rng g = hb_rng(h, v, t, h.rngk[(size_t)t * h.n_nodes + v]);
                             g.shuffle(peers, np);
                         }
+                        // the unit's list once (a lane per node: coalesced), a byte per target
+                        h.ihave_unit[((size_t)(h.fan_mode ? s.n_topics : 0) + t) * h.n_nodes + v] =
+                            IhaveSlot{dig, L, h.ihave_cur};
+                        const uint8_t tg = (uint8_t)(h.ihave_cur8 | (h.fan_mode ? IHAVE_FAN : 0));
                         for (int q = 0; q < target; ++q) {
-                            const size_t x = tslot + rs[lane] + peers[q];
-                            h.ihave_slot[x] = IhaveSlot{dig, L, h.ihave_cur};
+                            h.ihave_tag[tslot + rs[lane] + peers[q]] = tg;
                             ihave_mark(h, (uint64_t)(rs[lane] + peers[q]), t);  // (D) reads it
                         }
                         cnt[0] += (uint64_t)target;
@@ -1212,6 +1215,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
             for (int p = lane; p < target; p += 64) {
                 const int64_t r = r0 + peers[p];
                 h.ihave_slot[tslot + r] = IhaveSlot{dall, L, h.ihave_cur};
+                h.ihave_tag[tslot + r] = (uint8_t)(h.ihave_cur8 | IHAVE_OWN);
                 ihave_mark(h, (uint64_t)r, t);  // (D) reads it
             }
             msgs += (uint64_t)target;
@@ -1246,6 +1250,7 @@ __global__ __launch_bounds__(64) void k_hb_gossip_long(DevState s, HbState h, ui
                 const uint32_t q = h.ihave_bits ? h.rev[r] : NO_PAIR;
                 if (lane == 0) {
                     h.ihave_slot[tslot + r] = IhaveSlot{take ? d : dall - d, maxl, h.ihave_cur};
+                    h.ihave_tag[tslot + r] = (uint8_t)(h.ihave_cur8 | IHAVE_OWN);
                     ihave_mark(h, (uint64_t)r, t);
                 }
                 // the subset the receiver's handleIHave reads (D): marked at the
