@@ -869,8 +869,9 @@ hipError_t launch_ip_colocation_export(const DevState& s, const DevPeerParams& p
 hipError_t launch_mark_rows(const int64_t* row_ptr, const uint32_t* obs, uint32_t n, uint8_t* mask, uint8_t val,
                             hipStream_t st);
 // only2: re-score the pairs marked in both masks (null: in `only`)
+// gate (optional): two event counters whose marks fill only2; a zero sum skips the pass
 hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const uint8_t* only, hipStream_t st,
-                               const uint8_t* only2 = nullptr);
+                               const uint8_t* only2 = nullptr, const unsigned long long* gate = nullptr);
 hipError_t launch_apply_events(const DevState& s, const DevPeerParams& pp, const DevEvent* ev,
                                const uint32_t* group_off, uint32_t n_groups, hipStream_t st);
 hipError_t launch_recap(const DevState& s, uint32_t topic, double cap2, double cap3, hipStream_t st);

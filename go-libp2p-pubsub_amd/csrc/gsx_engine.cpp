@@ -188,6 +188,7 @@ struct gsx_engine {
     uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gx_nodes = nullptr;
     uint32_t* d_gxflag = nullptr;  // [0] a GxSub bound broken, [1] a promise without a slot, [4] slots in use (max)
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
+    bool ihave_tr_dirty = true;  // the truncated-list half of ihave_bits may hold bits (a round had a GxSub pool)
     int64_t* d_prom_e = nullptr;
     uint8_t* d_prom_any = nullptr;  // [pair] some promise slot may be in use (HbState::prom_any)
     unsigned long long* d_prom_cnt = nullptr;  // gsx_promise_count's device sum
@@ -932,6 +933,7 @@ void free_state(gsx_engine* e) {
         e->gxf_sets_cap = 0;
         e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
+        e->ihave_tr_dirty = true;  // (a new array is cleared whole)
         e->d_prom_e = nullptr;
         e->d_prom_any = nullptr;
         e->d_prom_cnt = nullptr;
@@ -1133,9 +1135,17 @@ hipError_t rescore_all(gsx_engine* e, const gsx::DevState& ds, int64_t now, bool
     return gsx::launch_refresh_score(ds, kern_params(e), now, refresh, e->stream);
 }
 hipError_t rescore_subset(gsx_engine* e, const gsx::DevState& ds, const gsx::KernParams& kp, const uint8_t* mask,
-                          const uint8_t* mask2 = nullptr) {
+                          const uint8_t* mask2 = nullptr, const unsigned long long* gate = nullptr) {
     ++e->score_writes;
-    return gsx::launch_score_subset(ds, kp, mask, e->stream, mask2);
+    return gsx::launch_score_subset(ds, kp, mask, e->stream, mask2, gate);
+}
+// The heartbeat's masked re-scores on one engine mark only pairs that carried
+// control (GRAFT / PRUNE sent in (A): dirty, inbox; handled in (B), answered in
+// (C)): with none sent the passes have nothing to do (the kernel reads the two
+// counters and returns).  A range shard's (B) takes control from other ranks:
+// never gated there.
+const unsigned long long* hb_ctl_gate(const gsx_engine* e) {
+    return e->sharded() ? nullptr : e->d_hbstats + gsx::HB_GRAFTS;  // (HB_GRAFTS, HB_PRUNES: adjacent)
 }
 
 // The largest threshold a propagation fwd byte tests (k_prop_fwd: publishThreshold, graylistThreshold).
@@ -3998,7 +4008,10 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     }
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
-    if (pen_mask) HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), pen_mask));
+    // (pen_mask holds exactly the pairs of the broken promises k_gx_promises counted)
+    if (pen_mask)
+        HIPCHK(e, rescore_subset(e, dev_state(e), kern_params(e), pen_mask, nullptr,
+                                 e->d_hbstats + gsx::HB_BROKEN_PROMISES));
     gsx::HbState h{};
     h.row_ptr = e->d_row_ptr;
     h.rev = e->d_rev;
@@ -4084,7 +4097,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.gsubs = e->d_gsubs;
         // the IHAVE topic bits of the last round (one bulk clear: cheaper than the
         // exchange clearing the pairs it read one by one)
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, 16 * std::max<size_t>(e->E, 1), e->stream));
+        // (the truncated-list bits only after a round that could set them: gx_sub_prepare)
+        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, (e->ihave_tr_dirty ? 16 : 8) * std::max<size_t>(e->E, 1),
+                                 e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32 + 8 * gx_touch_words(e), e->stream));  // flags, touch bits
         h.gx_touch = reinterpret_cast<uint64_t*>(e->d_gxflag + 8);
         e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
@@ -4220,8 +4235,12 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     dbg_host("hb gb lists");
     DBG_SYNC(2);
     // the truncated IHAVE lists' rows (exchange on, a window longer than MaxIHaveLength)
-    if (gx_on)
+    if (gx_on) {
         if (int rc = gx_sub_prepare(e, max_ids, tw)) return rc;
+        bool pool = false;  // (only a topic with rows can truncate a list: k_hb_gossip_long sets ihave_tr)
+        for (uint32_t t = 0; t < e->T; ++t) pool = pool || e->gsub_host[t].pool != nullptr;
+        e->ihave_tr_dirty = pool;
+    }
     // IHAVE slots: this round's are written under its tag (k_hb_gossip); every
     // other slot reads as empty, so nothing is cleared (but at the tag's wrap)
     if (++e->ihave_round == 0) {
@@ -4276,7 +4295,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // touched that (B) reads (marked in the inbox) are re-scored
     // (a shard's (B) reads every pair with remote control: all touched pairs)
     // (with PX every touched pair: the PX lists read the owner's whole row)
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.inbox : nullptr));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.inbox : nullptr,
+                             hb_ctl_gate(e)));
     e->hb = h;
     e->hb_active = true;
     dbg_host("hb (A) queued");
@@ -4299,7 +4319,8 @@ int hb_recv(gsx_engine* e, const uint64_t* halo_ctl) {
     // the pairs touched so far that (C) reads: those marked with an answer
     // (a shard's (C) reads every pair with a remote answer: all touched pairs;
     // with PX every touched pair: the answers' PX lists read the whole row)
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.answer : nullptr));
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, (!e->sharded() && !h.pxno) ? h.answer : nullptr,
+                             hb_ctl_gate(e)));
     return GSX_OK;
 }
 
@@ -5020,7 +5041,7 @@ int hb_end(gsx_engine* e, const uint64_t* halo_resp, gsx_heartbeat_out* out) {
     if (!e->sharded()) HIPCHK(e, gsx::launch_hb_px(ds, h, 1, e->stream));  // the (B) answers' peer exchange (do_px)
     HIPCHK(e, gsx::launch_hb_answer(ds, h, e->stream));
     e->hb_clean = !e->sharded() && !e->hb_tracing;  // (tracing keeps the control words)
-    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty));  // the cache leaves the round exact
+    HIPCHK(e, rescore_subset(e, ds, kern_params(e), h.dirty, nullptr, hb_ctl_gate(e)));  // the cache leaves the round exact
     // (D) the gossip exchange over the batches the IHAVEs advertised (the
     // windows of hb_begin's list), answered across the Shift
     gsx_engine::GxRound& R = e->gxr;

@@ -20,9 +20,13 @@ namespace gsx {
 template <int TT, bool REFRESH>
 __global__ __launch_bounds__(256) void k_refresh_score(DevState s, KernParams kp, int64_t now,
                                                        const uint8_t* __restrict__ only,
-                                                       const uint8_t* __restrict__ only2) {
+                                                       const uint8_t* __restrict__ only2,
+                                                       const unsigned long long* __restrict__ gate) {
     const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (p >= s.n_pairs) return;
+    // a masked pass whose marks all come from counted events (gate: their
+    // counters) has nothing to re-score when they sum to zero
+    if (!REFRESH && gate && gate[0] + gate[1] == 0) return;
     // score-only pass over a subset (the pairs a heartbeat step touched, and
     // with only2 also marked there): the others keep their cached score, a
     // wave without one returns at once
@@ -322,14 +326,14 @@ hipError_t launch_purge(const DevState& s, int64_t now, hipStream_t st) {
 
 template <bool R>
 static hipError_t launch_rs(const DevState& s, const KernParams& kp, int64_t now, const uint8_t* only,
-                            const uint8_t* only2, hipStream_t st) {
+                            const uint8_t* only2, hipStream_t st, const unsigned long long* gate = nullptr) {
     const dim3 grid(blocks_for(s.n_pairs, 256)), block(256);
     switch (s.n_topics) {
-    case 1: hipLaunchKernelGGL((k_refresh_score<1, R>), grid, block, 0, st, s, kp, now, only, only2); break;
-    case 2: hipLaunchKernelGGL((k_refresh_score<2, R>), grid, block, 0, st, s, kp, now, only, only2); break;
-    case 4: hipLaunchKernelGGL((k_refresh_score<4, R>), grid, block, 0, st, s, kp, now, only, only2); break;
-    case 8: hipLaunchKernelGGL((k_refresh_score<8, R>), grid, block, 0, st, s, kp, now, only, only2); break;
-    default: hipLaunchKernelGGL((k_refresh_score<0, R>), grid, block, 0, st, s, kp, now, only, only2); break;
+    case 1: hipLaunchKernelGGL((k_refresh_score<1, R>), grid, block, 0, st, s, kp, now, only, only2, gate); break;
+    case 2: hipLaunchKernelGGL((k_refresh_score<2, R>), grid, block, 0, st, s, kp, now, only, only2, gate); break;
+    case 4: hipLaunchKernelGGL((k_refresh_score<4, R>), grid, block, 0, st, s, kp, now, only, only2, gate); break;
+    case 8: hipLaunchKernelGGL((k_refresh_score<8, R>), grid, block, 0, st, s, kp, now, only, only2, gate); break;
+    default: hipLaunchKernelGGL((k_refresh_score<0, R>), grid, block, 0, st, s, kp, now, only, only2, gate); break;
     }
     return hipGetLastError();
 }
@@ -340,9 +344,9 @@ hipError_t launch_refresh_score(const DevState& s, const KernParams& kp, int64_t
 }
 
 hipError_t launch_score_subset(const DevState& s, const KernParams& kp, const uint8_t* only, hipStream_t st,
-                              const uint8_t* only2) {
+                              const uint8_t* only2, const unsigned long long* gate) {
     if (s.n_pairs == 0) return hipSuccess;
-    return launch_rs<false>(s, kp, 0, only, only2, st);
+    return launch_rs<false>(s, kp, 0, only, only2, st, gate);
 }
 
 // setIPs (score.go:1021-1059) for pairs whose peer's IP list changed
