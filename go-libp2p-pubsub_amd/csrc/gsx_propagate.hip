@@ -2081,11 +2081,21 @@ __global__ __launch_bounds__(256) void k_prop_defer(PropState ps, DevState s, De
         for (int i = 0; i < DU; ++i) {
             const uint64_t q = q0 + i * stride;
             const bool in = q < ps.n_pairs;
-            sc[i] = in ? s.score[q] : 0.0;
             k4a[i] = (in && ps.drop) ? ps.invcnt[q] : 0u;
             pf[i] = in ? s.pflags[q] : 0;
             ef[i] = in ? ps.eflags[q] : 0;
             fb[i] = in ? ps.fwd[q] : 0;
+        }
+        // The score decides only for a floodsub peer or under flood publish: a
+        // gossipsub edge's own threshold is AcceptFrom's (FWD_GIN is exactly
+        // score < graylist on the cached scores, and such pairs are skipped), so
+        // its score is never read — most of the pass's bytes on a gossipsub overlay
+#pragma unroll
+        for (int i = 0; i < DU; ++i) {
+            const uint64_t q = q0 + i * stride;
+            const bool need = q < ps.n_pairs && (pf[i] & PAIR_PRESENT) && !k4a[i] && !(ef[i] & EDGE_DIRECT) &&
+                              !(fb[i] & FWD_GIN) && (!(ef[i] & EDGE_GOSSIPSUB) || ps.flood_publish);
+            sc[i] = need ? s.score[q] : __builtin_inf();
         }
         bool now_[DU];
 #pragma unroll
