@@ -594,8 +594,6 @@ struct HbState {
     uint32_t* gxb_cnt0;    // [group][pair]: sets whose old copies are inside the P3 window | the others << 16
     uint32_t gxb_ngrp;     // set groups this round (GxBatch::grp)
     uint32_t gxb_stamp;
-    uint32_t* peerhave;    // [pair]: IHAVE RPCs handled this heartbeat (gossipsub.go:414)
-    uint32_t* iasked;      // [pair]: ids asked this heartbeat (:415)
     uint32_t* gx_req;      // [pair]: ids asked in this exchange (0 = none), GX_REQ_ALL: every candidate
     uint64_t* prom_h;      // [pair][prom_slots]: promised message handle
     int64_t* prom_e;       // [pair][prom_slots]: its expiry (0 = free slot)

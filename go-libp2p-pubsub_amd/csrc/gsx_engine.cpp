@@ -185,7 +185,7 @@ struct gsx_engine {
     };
     std::deque<std::vector<McBatch>> mc;
     // gossip exchange state (allocated when first enabled)
-    uint32_t *d_peerhave = nullptr, *d_iasked = nullptr, *d_gxreq = nullptr, *d_gx_nodes = nullptr;
+    uint32_t *d_gxreq = nullptr, *d_gx_nodes = nullptr;
     uint32_t* d_gxflag = nullptr;  // [0] a GxSub bound broken, [1] a promise without a slot, [4] slots in use (max)
     uint64_t *d_prom_h = nullptr, *d_ihave_bits = nullptr;  // ihave_bits [2][E]: IHAVE topics, truncated ones (receiver's pair)
     bool ihave_tr_dirty = true;  // the truncated-list half of ihave_bits may hold bits (a round had a GxSub pool)
@@ -193,7 +193,6 @@ struct gsx_engine {
     uint8_t* d_prom_any = nullptr;  // [pair] some promise slot may be in use (HbState::prom_any)
     unsigned long long* d_prom_cnt = nullptr;  // gsx_promise_count's device sum
     uint32_t prom_slots = 0;  // promise slots per pair (grown while every pair keeps one free before an exchange)
-    bool gx_clean = false;    // IHAVE bits and counters all zero (the exchange clears what it reads)
     // the truncated IHAVE lists of a round (GxSub per topic): rows for at most
     // tgt_bound targets of tw words each
     struct SubPool {
@@ -903,7 +902,7 @@ void free_state(gsx_engine* e) {
     e->d_hbstats = nullptr;
     e->d_tr_acc = e->d_tr_hp = nullptr;
     {
-        void* gxp[] = {e->d_peerhave, e->d_iasked, e->d_gxreq, e->d_gxflag, e->d_prom_h,
+        void* gxp[] = {e->d_gxreq, e->d_gxflag, e->d_prom_h,
                        e->d_ihave_bits, e->d_prom_e, e->d_prom_any, e->d_prom_cnt, e->d_gxa,
                        e->d_gx_got, e->d_gx_nodes,
                        e->d_gx_rhm, e->d_gx_common,
@@ -931,7 +930,7 @@ void free_state(gsx_engine* e) {
         e->d_gxs_send = nullptr;
         e->gxs_send_cap = 0;
         e->gxf_sets_cap = 0;
-        e->d_peerhave = e->d_iasked = e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
+        e->d_gxreq = e->d_gxflag = e->d_gx_nodes = nullptr;
         e->d_prom_h = e->d_ihave_bits = nullptr;
         e->ihave_tr_dirty = true;  // (a new array is cleared whole)
         e->d_prom_e = nullptr;
@@ -3844,7 +3843,7 @@ int gx_alloc(gsx_engine* e) {
     int rc = 0;
     const size_t E = std::max<size_t>(e->E, 1);
     const uint32_t S = gsx::GX_PROMISE_SLOTS0;
-    if ((rc = dalloc(e, &e->d_peerhave, E)) || (rc = dalloc(e, &e->d_iasked, E)) || (rc = dalloc(e, &e->d_gxreq, E)) ||
+    if ((rc = dalloc(e, &e->d_gxreq, E)) ||
         (rc = dalloc(e, &e->d_prom_h, E * S)) || (rc = dalloc(e, &e->d_prom_e, E * S)) ||
         (rc = dalloc(e, &e->d_prom_any, E)) || (rc = dalloc(e, &e->d_prom_cnt, 1)) ||
         (rc = dalloc(e, &e->d_ihave_bits, 2 * E)) ||
@@ -3854,12 +3853,9 @@ int gx_alloc(gsx_engine* e) {
         (rc = dalloc(e, &e->d_gsubs, std::max<size_t>(e->T, 1))))
         return rc;
     e->prom_slots = S;
-    e->gx_clean = false;
     HIPCHK(e, hipMemsetAsync(e->d_prom_e, 0, 8 * E * S, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_prom_any, 0, E, e->stream));
     HIPCHK(e, hipMemsetAsync(e->d_gxreq, 0, 4 * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
     e->subp.assign(e->T, gsx_engine::SubPool{});
     e->gsub_host.assign(e->T, gsx::GxSub{});
     return GSX_OK;
@@ -3986,13 +3982,11 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
     uint8_t* pen_mask = nullptr;
     if (e->d_prom_e && !state_only) {
-        // clearIHaveCounters (:1566-1576); applyIwantPenalties (:1578-1583):
-        // promises expired before now are broken, AddPenalty (P7) on their pairs
+        // clearIHaveCounters (:1566-1576): nothing to clear, the exchange's gate
+        // reads the counters' values at a heartbeat's one RPC per pair (gx_gate);
+        // applyIwantPenalties (:1578-1583): promises expired before now are
+        // broken, AddPenalty (P7) on their pairs
         const size_t E = std::max<size_t>(e->E, 1);
-        if (!e->gx_clean) {
-            HIPCHK(e, hipMemsetAsync(e->d_peerhave, 0, 4 * E, e->stream));
-            HIPCHK(e, hipMemsetAsync(e->d_iasked, 0, 4 * E, e->stream));
-        }
         pen_mask = e->d_dirty + 3 * e->E;
         HIPCHK(e, hipMemsetAsync(pen_mask, 0, E, e->stream));
         gsx::HbState hp{};
@@ -4087,8 +4081,6 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         h.gx_err = e->d_gxflag;
         h.gx_nodes = e->d_gx_nodes;
         h.prom_occ = e->d_gxflag + 4;
-        h.peerhave = e->d_peerhave;
-        h.iasked = e->d_iasked;
         h.gx_req = e->d_gxreq;
         h.prom_h = e->d_prom_h;
         h.prom_e = e->d_prom_e;
@@ -4102,7 +4094,6 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                  e->stream));
         HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32 + 8 * gx_touch_words(e), e->stream));  // flags, touch bits
         h.gx_touch = reinterpret_cast<uint64_t*>(e->d_gxflag + 8);
-        e->gx_clean = false;  // until an exchange has read (and cleared) this round's bits
         if (e->sharded()) {  // the IHAVEs of cross-shard pairs, sender side (gsx_gx_pack_ihave)
             const size_t E = std::max<size_t>(e->E, 1);
             if (!e->d_gxs_out) {
@@ -5001,9 +4992,6 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
         ++ms->refs;  // (its summary: k_gx_merge_sets)
         e->mc.front().push_back(std::move(b));
     }
-    // the exchange cleared the bits and counters it read; a round without
-    // gossip set none (the counters were cleared at its start)
-    if (e->d_prom_e) e->gx_clean = gx_run || (e->gp.gossip_exchange && !e->have_gossip);
     const bool merged = gx_run && st[gsx::HB_GOSSIP_DELIVERED] + st[gsx::HB_GOSSIP_REJECTED] +
                                           st[gsx::HB_FWD_DELIVERED] > 0;
     for (size_t i = 0; i < gx_sets.size(); ++i) {

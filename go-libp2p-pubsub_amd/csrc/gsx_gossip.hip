@@ -14,7 +14,7 @@
 //          is recorded in the set's receipt rows; a further copy is a duplicate.
 // Canonical order: topics ascending, then the advertised batches in cache
 // order (windows newest first, Put order), then message index.  Every
-// per-pair state (peerhave, iasked, promises, records of q) belongs to u's lane.
+// per-pair state (promises, records of q) belongs to u's lane.
 #include "gsx_device.h"
 #include "gsx_ops.h"
 
@@ -367,9 +367,11 @@ __device__ __forceinline__ void gx_receive_sampled(const DevState& s, const HbSt
 __device__ __forceinline__ int gx_gate(const DevState& s, const HbState& h, uint64_t q, uint32_t r) {
     if (r == NO_PAIR || ((r & HALO) && !h.gxs_hidx)) return 0;
     if (s.score[q] < h.gossip_threshold) return 1;  // :617-621
-    const uint32_t ph = h.peerhave[q] + 1;          // :624-628 (one RPC per pair per heartbeat)
-    if ((int64_t)ph > (int64_t)h.gp.max_ihave_msgs) return 1;
-    if ((int64_t)h.iasked[q] >= (int64_t)h.gp.max_ihave) return 1;  // :630-633
+    // peerhave / iasked (:624-633) are cleared at every heartbeat start (:1566-1576)
+    // and each pair handles one IHAVE RPC per heartbeat (every topic in it), so at
+    // this check they are 1 and 0: the limits only test the parameters
+    if ((int64_t)h.gp.max_ihave_msgs < 1) return 1;  // :624-628
+    if ((int64_t)h.gp.max_ihave <= 0) return 1;       // :630-633
     return 2;
 }
 
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 return true;
             });
             if (n == 0) continue;  // :652-654
-            const uint32_t budget = (uint32_t)((int64_t)h.gp.max_ihave - (int64_t)h.iasked[q]);
+            const uint32_t budget = (uint32_t)h.gp.max_ihave;  // MaxIHaveLength - iasked (0: above)
             const uint32_t kk = n < budget ? n : budget;
             uint32_t pick_g = 0, pick_k = 0;
             if (kk == n) {  // the element at Int31n(kk) of all of them, canonical order
@@ -735,7 +737,7 @@ __global__ __launch_bounds__(64) void k_gx_node(DevState s, HbState h) {
                 const uint64_t tr = h.ihave_tr[q];
                 const uint32_t n = gx_wcount(h, tb, u, (uint64_t)q, v, tr, r, nf, lane);
                 if (n == 0) continue;
-                const uint32_t budget = (uint32_t)((int64_t)gp.max_ihave - (int64_t)h.iasked[q]);
+                const uint32_t budget = (uint32_t)gp.max_ihave;  // MaxIHaveLength - iasked (0: gx_gate)
                 const uint32_t kk = n < budget ? n : budget;
                 uint32_t pick_g = 0, pick_k = 0;
                 if (kk == n) {

@@ -44,13 +44,18 @@ def _same(g, w):
     dict(prefill=3, ticks=6, exchange_from=2),  # 3 of 4 promise slots taken: the exchange's promises grow them
     dict(T=1, n=300, msgs=4200, hops=2, ticks=4),  # 66-word sets: no common words, every asker heavy (k_gx_node)
     dict(T=1, n=10, d=3, msgs=6, hops=1, ticks=6),  # 10 nodes: a one-node frontier is already a dense hop
-], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill", "wide", "tiny10"])
+    dict(max_ihave_messages=0, ticks=4),      # MaxIHaveMessages 0: every IHAVE RPC ignored (peerhave limit)
+], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill", "wide", "tiny10",
+        "no_ihave_msgs"])
 def test_gossip_exchange_matches_oracle(gpu_ok, kw):
     T = kw.get("T", 2)
     g = gc.exchange_run(gsx.Engine(T), **kw)
     w = gc.exchange_run(orc.Oracle(T), **kw)
     _same(g, w)
-    assert sum(o["iwant_msgs"] for o in g[1]) > 0
+    if kw.get("max_ihave_messages", 1) == 0:
+        assert sum(o["iwant_msgs"] for o in g[1]) == 0 and sum(o["ihave_ignored"] for o in g[1]) > 0
+    else:
+        assert sum(o["iwant_msgs"] for o in g[1]) > 0
 
 
 # Heartbeats every second, batches 100 ms after one with 5 ms hops: an old
