@@ -874,10 +874,13 @@ def main():
             e.sync()
             barrier()
             torch.cuda.synchronize(dev)
+            b0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)  # (the profiler's clock: tools/hb_api.py windows)
             t0 = time.perf_counter()
             o = e.heartbeat(tick, now, seed).as_dict()
             e.sync()
             ms = (time.perf_counter() - t0) * 1e3
+            if os.environ.get("GSX_HB_WINDOWS") and k >= args.hb_settle:
+                log(f"window {tick} {b0} {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}")
             ms = reduce_scalar(ms, dist, dev, "max")
             r = {"tick": tick, "og_tick": tick % 60 == 0, "ms": ms, **o}
             (rounds if k >= args.hb_settle else settle).append(r)

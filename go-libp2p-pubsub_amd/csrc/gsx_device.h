@@ -644,6 +644,15 @@ struct HbState {
 };
 
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st);
+// Byte ranges cleared in one launch (a round's per-round clears: one dispatch
+// instead of one fill each, every fill costing ~5 us of the stream however small).
+constexpr uint32_t ZERO_SPANS = 12;
+struct ZeroSpans {
+    uint8_t* p[ZERO_SPANS];
+    uint64_t n[ZERO_SPANS];
+    uint32_t k;
+};
+hipError_t launch_zero_spans(const ZeroSpans& z, hipStream_t st);
 // Rebuilds the backoff presence bits from the expiry array (gsx_import_backoff).
 hipError_t launch_bo_rebuild(const int64_t* backoff, uint8_t* bo8, uint64_t n_pairs, uint32_t n_topics,
                              hipStream_t st);

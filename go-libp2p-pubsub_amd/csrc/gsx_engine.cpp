@@ -539,6 +539,28 @@ int fail(gsx_engine* e, int code, const std::string& msg) {
             return fail((e), GSX_EDEVICE, std::string(#call ": ") + hipGetErrorString(_st));    \
     } while (0)
 
+// Consecutive clears of a round queued as one k_zero_spans launch (flushed
+// before the next kernel that reads them, or when full).
+struct ZeroBatch {
+    gsx_engine* e;
+    gsx::ZeroSpans z{};
+    explicit ZeroBatch(gsx_engine* e_) : e(e_) {}
+    int add(void* p, size_t bytes) {
+        if (!p || !bytes) return GSX_OK;
+        if (z.k == gsx::ZERO_SPANS)
+            if (int rc = flush()) return rc;
+        z.p[z.k] = static_cast<uint8_t*>(p);
+        z.n[z.k++] = bytes;
+        return GSX_OK;
+    }
+    int flush() {
+        if (!z.k) return GSX_OK;
+        HIPCHK(e, gsx::launch_zero_spans(z, e->stream));
+        z.k = 0;
+        return GSX_OK;
+    }
+};
+
 // A sharded gossip exchange (gsx_hb_end .. gsx_gx_end) holds the round's
 // message sets, receipt rows and the mcache Shift: nothing that starts other
 // work on the engine's state may run before gsx_gx_end.
@@ -3979,7 +4001,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         return fail(e, GSX_ESTATE, "gossip exchange on a shard: gsx_shard_set_halo_bases first");
     if (gx_on)
         if (int rc = gx_alloc(e)) return rc;
-    HIPCHK(e, hipMemsetAsync(e->d_hbstats, 0, sizeof(unsigned long long) * gsx::HB_STAT_WORDS, e->stream));
+    ZeroBatch za(e);
+    if (int rc = za.add(e->d_hbstats, sizeof(unsigned long long) * gsx::HB_STAT_WORDS)) return rc;
     uint8_t* pen_mask = nullptr;
     if (e->d_prom_e && !state_only) {
         // clearIHaveCounters (:1566-1576): nothing to clear, the exchange's gate
@@ -3988,7 +4011,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         // broken, AddPenalty (P7) on their pairs
         const size_t E = std::max<size_t>(e->E, 1);
         pen_mask = e->d_dirty + 3 * e->E;
-        HIPCHK(e, hipMemsetAsync(pen_mask, 0, E, e->stream));
+        if (int rc = za.add(pen_mask, E)) return rc;
+        if (int rc = za.flush()) return rc;
         gsx::HbState hp{};
         hp.n_pairs = e->E;
         hp.now = now;
@@ -4000,6 +4024,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         hp.dirty = pen_mask;
         HIPCHK(e, gsx::launch_gx_promises(dev_state(e), hp, e->stream));
     }
+    if (int rc = za.flush()) return rc;
     // the scores of the heartbeat start (gossipsub.go:1333-1341)
     if (int rc = ensure_scores(e)) return rc;
     // (pen_mask holds exactly the pairs of the broken promises k_gx_promises counted)
@@ -4041,8 +4066,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
             if (int rc = dalloc(e, &e->d_tr_acc, std::max<size_t>(e->E, 1))) return rc;
             if (int rc = dalloc(e, &e->d_tr_hp, std::max<size_t>(e->E, 1))) return rc;
         }
-        HIPCHK(e, hipMemsetAsync(e->d_tr_acc, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_tr_hp, 0, 8 * std::max<size_t>(e->E, 1), e->stream));
+        if (int rc = za.add(e->d_tr_acc, 8 * std::max<size_t>(e->E, 1))) return rc;
+        if (int rc = za.add(e->d_tr_hp, 8 * std::max<size_t>(e->E, 1))) return rc;
         h.tr_acc = e->d_tr_acc;
         h.tr_hp = e->d_tr_hp;
         h.keep_ctl = true;
@@ -4072,9 +4097,9 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                                 e->gp.do_px,
                                 e->gp.prune_peers};
     const gsx::DevState ds = dev_state(e);
-    HIPCHK(e, hipMemsetAsync(e->d_nwork, 0, 8 * (size_t)e->T, e->stream));
+    if (int rc = za.add(e->d_nwork, 8 * (size_t)e->T)) return rc;
     // (per topic and gossip pass, mesh then fanout: k_hb_gossip's long-list counts)
-    HIPCHK(e, hipMemsetAsync(e->d_nlong, 0, 8 * (size_t)e->T, e->stream));
+    if (int rc = za.add(e->d_nlong, 8 * (size_t)e->T)) return rc;
     if (gx_on) {
         h.ihave_bits = e->d_ihave_bits;
         h.ihave_tr = e->d_ihave_bits + std::max<size_t>(e->E, 1);
@@ -4090,9 +4115,8 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
         // the IHAVE topic bits of the last round (one bulk clear: cheaper than the
         // exchange clearing the pairs it read one by one)
         // (the truncated-list bits only after a round that could set them: gx_sub_prepare)
-        HIPCHK(e, hipMemsetAsync(e->d_ihave_bits, 0, (e->ihave_tr_dirty ? 16 : 8) * std::max<size_t>(e->E, 1),
-                                 e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_gxflag, 0, 32 + 8 * gx_touch_words(e), e->stream));  // flags, touch bits
+        if (int rc = za.add(e->d_ihave_bits, (e->ihave_tr_dirty ? 16 : 8) * std::max<size_t>(e->E, 1))) return rc;
+        if (int rc = za.add(e->d_gxflag, 32 + 8 * gx_touch_words(e))) return rc;  // flags, touch bits
         h.gx_touch = reinterpret_cast<uint64_t*>(e->d_gxflag + 8);
         if (e->sharded()) {  // the IHAVEs of cross-shard pairs, sender side (gsx_gx_pack_ihave)
             const size_t E = std::max<size_t>(e->E, 1);
@@ -4103,7 +4127,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
                     (rc = dalloc(e, &e->d_gxs_off, (size_t)gsx::MAX_RANKS)))
                     return rc;
             }
-            HIPCHK(e, hipMemsetAsync(e->d_gxs_out, 0, 16 * E, e->stream));  // gxs_out, gxs_tro
+            if (int rc = za.add(e->d_gxs_out, 16 * E)) return rc;  // gxs_out, gxs_tro
             h.gxs_out = e->d_gxs_out;
             h.gxs_tro = e->d_gxs_out + E;
             h.gxs_rans = e->d_gxs_rans;
@@ -4127,7 +4151,7 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
             if (int rc = dalloc(e, &e->d_pxlog, 4 * e->px_cap)) return rc;
             e->pxlog_alloc = e->px_cap;
         }
-        HIPCHK(e, hipMemsetAsync(e->d_pxno, 0, E, e->stream));
+        if (int rc = za.add(e->d_pxno, E)) return rc;
         h.pxno = e->d_pxno;
         h.px_log = e->px_cap ? e->d_pxlog : nullptr;
         h.px_cap = e->px_cap;
@@ -4157,12 +4181,13 @@ int hb_begin_state(gsx_engine* e, uint64_t tick, int64_t now, uint64_t seed, boo
     // read, and nothing else is ever set: after one cleared round they stay
     // clean.  Shards pack them for the exchange and clear them here.
     if (e->sharded() || !e->hb_clean) {
-        HIPCHK(e, hipMemsetAsync(e->d_ctl, 0, 2 * E8, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_resp, 0, E8, e->stream));
-        HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, 3 * (e->E ? e->E : 1), e->stream));
+        if (int rc = za.add(e->d_ctl, 2 * E8)) return rc;
+        if (int rc = za.add(e->d_resp, E8)) return rc;
+        if (int rc = za.add(e->d_dirty, 3 * (e->E ? e->E : 1))) return rc;
     } else {
-        HIPCHK(e, hipMemsetAsync(e->d_dirty, 0, e->E ? e->E : 1, e->stream));
+        if (int rc = za.add(e->d_dirty, e->E ? e->E : 1)) return rc;
     }
+    if (int rc = za.flush()) return rc;
     e->hb_clean = false;  // until this round's (C) has run
     if (state_only) {
         e->hb = h;
@@ -4516,10 +4541,14 @@ int gxf_run_begin(gsx_engine* e, gsx_engine::GxRound& R, size_t k) {
         f.hstamp = e->d_gxf_hst;
         f.hidx = e->d_gxf_hst + E;
     }
-    HIPCHK(e, hipMemsetAsync(e->d_gxf_mask, 0, 8 * 2 * N, e->stream));  // fmask
-    HIPCHK(e, hipMemsetAsync(f.srcm, 0, 8 * N, e->stream));
-    HIPCHK(e, hipMemsetAsync(f.fbit[0], 0, 8 * 2 * ((N + 63) / 64), e->stream));
-    HIPCHK(e, hipMemsetAsync(e->d_gxf_cnt, 0, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1), e->stream));
+    {
+        ZeroBatch zb(e);
+        if (int rc = zb.add(e->d_gxf_mask, 8 * 2 * N)) return rc;  // fmask
+        if (int rc = zb.add(f.srcm, 8 * N)) return rc;
+        if (int rc = zb.add(f.fbit[0], 8 * 2 * ((N + 63) / 64))) return rc;
+        if (int rc = zb.add(e->d_gxf_cnt, 4 * 2 * ((size_t)gsx::GXF_MAX_HOPS + 1))) return rc;
+        if (int rc = zb.flush()) return rc;
+    }
     HIPCHK(e, gsx::launch_gxf_init(dev_state(e), R.h, f, n_src, e->stream));
     R.f = f;
     R.hops = 0;

@@ -1796,6 +1796,32 @@ static inline unsigned wave_grid(uint64_t n) {
     return b < 8192 ? b : 8192;
 }
 
+// Every span: the bytes before the first 16-B boundary, 16-B stores, the tail.
+__global__ __launch_bounds__(256) void k_zero_spans(ZeroSpans z) {
+    const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, stride = (uint64_t)gridDim.x * 256u;
+    for (uint32_t j = 0; j < z.k; ++j) {
+        uint8_t* p = z.p[j];
+        const uint64_t n = z.n[j];
+        uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
+        head = head < n ? head : n;
+        if (tid < head) p[tid] = 0;
+        uint4* v = reinterpret_cast<uint4*>(p + head);
+        const uint64_t nv = (n - head) / 16;
+        for (uint64_t i = tid; i < nv; i += stride) v[i] = make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t done = head + 16 * nv;
+        if (tid < n - done) p[done + tid] = 0;
+    }
+}
+hipError_t launch_zero_spans(const ZeroSpans& z, hipStream_t st) {
+    uint64_t most = 0;
+    for (uint32_t j = 0; j < z.k; ++j) most = z.n[j] > most ? z.n[j] : most;
+    if (most == 0) return hipSuccess;
+    uint64_t b = (most / 16 + 1023) / 1024;  // ~4 stores per lane on the largest span
+    b = b < 1 ? 1 : b > 8192 ? 8192 : b;
+    hipLaunchKernelGGL(k_zero_spans, dim3((unsigned)b), dim3(256), 0, st, z);
+    return hipGetLastError();
+}
+
 hipError_t launch_hb_clear_backoff(const HbState& h, uint32_t n_topics, hipStream_t st) {
     const uint64_t n = (uint64_t)((n_topics + 7) / 8) * h.n_pairs;  // a lane per presence byte
     if (n == 0) return hipSuccess;
