@@ -4572,7 +4572,9 @@ int gx_forward(gsx_engine* e, gsx_engine::GxRound& R) {
         if (int rc = gxf_run_begin(e, R, k)) return rc;
         uint32_t hop = 1;
         for (;;) {
-            const uint32_t chunk = hop == 1 ? 6 : 8;
+            // (a steady round's runs end after two hops: a first chunk of three reads
+            // their empty frontier at once; long runs check every eight hops)
+            const uint32_t chunk = hop == 1 ? 3 : 8;
             if (hop + chunk > gsx::GXF_MAX_HOPS)
                 return fail(e, GSX_ERANGE, "forwarding of recovered messages: more than " +
                                                std::to_string(gsx::GXF_MAX_HOPS) + " hops");
