@@ -477,7 +477,14 @@ struct GxBatch {
     VcRef vc;             // the set's validation codes (old_in 2)
     const uint32_t* cnt;  // [node]: messages the node holds in this batch (k_mc_summary / k_gx_merge_sets)
     uint32_t vin_off;     // (range shards, old_in 2) word offset of the inside rows in a gxs_rows entry: 1 + fw + woff
+    // (one engine) [n_words]: the set's messages every node missing at most GX_POOR of them had seen
+    // (k_gx_setprep, after `common`); null on range shards
+    const uint64_t* common2;
 };
+// A node missing more than GX_POOR messages of a set is "poor" in it: the
+// common2 words leave it out, and k_gx_ask walks its pairs' rows of that set
+// unfiltered (every other node's missing messages lie outside common2).
+constexpr uint32_t GX_POOR = 16;
 // The truncated IHAVE lists of one topic this round (emitGossip, gsx.h): the
 // list the sender of pair r sent is row idx[r] of `pool` (tw words; bit
 // row_off * 64 + k = message k of the batch at row_off), valid where the
@@ -561,6 +568,8 @@ struct HbState {
                            // k_gx_ask, or a forwarding receiver): k_gx_merge_sets reads only their rows
     uint8_t* gx_mark;      // [pair]: answered pairs (their records took the receipts' credits; re-scored after)
     const uint64_t* gx_rhm;  // [node]: bit g = its row of advertised batch g holds a not-everywhere message
+                             // (one engine: outside the batch's common2 words, gx_poor)
+    uint32_t gx_poor;        // gx_rhm is over common2: k_gx_ask adds the batches its node is poor in (GX_POOR)
     const int32_t* col;    // [pair]: the peer (local node id; global on a shard)
     const GxBatch* gx;     // advertised batches, per topic gx_off[t] .. gx_off[t + 1]
     const uint32_t* gx_off;
@@ -683,6 +692,7 @@ struct GxSetPrep {
     uint8_t* full;
     uint64_t* common;
     uint32_t n_words, n_msgs;
+    uint64_t* common2;  // (one engine) AND over the nodes missing at most GX_POOR messages (GxBatch::common2)
 };
 hipError_t launch_gx_setprep(const GxSetPrep* sets, uint32_t n_sets, uint32_t n_nodes, hipStream_t st);
 // After the exchange, every set in one pass (blockIdx.y = set): seen |= the

@@ -4814,20 +4814,21 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
                 common = e->d_gx_common + 64 * i;
                 redo_common = true;
             } else {
-                if (!ms->d_common) {
-                    ms->d_common = reinterpret_cast<uint64_t*>(small_acquire(e, 8 * 64, &ms->common_bytes));
+                if (!ms->d_common) {  // (the common words, then common2: GxBatch::common2)
+                    ms->d_common = reinterpret_cast<uint64_t*>(small_acquire(e, 8 * 128, &ms->common_bytes));
                     if (!ms->d_common) return fail(e, GSX_ENOMEM, "message set common words");
                     ms->common_ok = false;
                 }
                 common = ms->d_common;
                 redo_common = !ms->common_ok;
-                if (redo_common) HIPCHK(e, hipMemsetAsync(common, 0xff, 8 * 64, e->stream));
+                if (redo_common) HIPCHK(e, hipMemsetAsync(common, 0xff, 8 * 128, e->stream));
                 ms->common_ok = true;  // (hb_finish drops it when a receipt changes the rows)
             }
         }
         common_of[i] = common;
         gsx::GxSetPrep p{ms->d_all, x_zero[i] ? nullptr : R.xs[i], gx_full_new[i] ? ms->d_full : nullptr,
                          redo_common ? common : nullptr, ms->n_words, ms->n_msgs};
+        p.common2 = (redo_common && !e->sharded()) ? common + 64 : nullptr;
         if (p.x || p.full || p.common) sprep.push_back(p);
     }
     std::vector<gsx::GxSetMerge> smerge(R.sets.size());
@@ -4843,6 +4844,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
     for (auto& g : gx) {
         const size_t si = reinterpret_cast<size_t>(g.got);
         g.common = common_of[si];
+        g.common2 = (common_of[si] && !e->sharded()) ? common_of[si] + 64 : nullptr;
         g.got = e->d_gx_got + si;
     }
     HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, 2 * e->gx_cap, e->stream));  // got, chg
@@ -4905,6 +4907,7 @@ int gx_ready(gsx_engine* e, gsx_engine::GxRound& R) {
     gsx::HbState& h = R.h;
     HIPCHK(e, gsx::launch_gx_rhm(e->d_gx, R.n_gx, (uint32_t)e->n_nodes, e->d_gx_rhm, e->stream));
     h.gx_rhm = e->d_gx_rhm;
+    h.gx_poor = e->sharded() ? 0u : 1u;  // (one engine: gx_rhm over common2)
     h.gsubs = e->d_gsubs;
     // the answered pairs' records take the receipts' credits: re-scored after
     // (the rest stays exact), when the scores were exact before
@@ -4938,7 +4941,13 @@ int gx_merge(gsx_engine* e, gsx_engine::GxRound& R) {
 // The round's end: counters, mcache.Shift, the recovered copies Put (one
 // batch per message set some node received in: got_all, every rank's on a
 // shard; null: this engine's), promise slots kept free.
+#ifdef GSX_GX_PROF
+extern "C" void gx_prof_dump();  // (gsx_gossip.hip, diagnostic build)
+#endif
 int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, const uint8_t* got_all) {
+#ifdef GSX_GX_PROF
+    gx_prof_dump();
+#endif
     const gsx::HbState& h = R.h;
     const bool gx_run = R.run;
     const size_t hist = (size_t)std::max(e->gp.history_length, 1);
@@ -5028,11 +5037,12 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
     for (size_t i = 0; i < gx_sets.size(); ++i) {
         gsx_engine::MsgSet* ms = gx_sets[i];
         // the receipts were merged into its seen rows: one engine's merge kept the
-        // full bytes exact at the touched nodes, and its common words stand as a
-        // subset of the new ones (they only filter the rows the ask reads:
-        // k_gx_rhm), so only a range shard recomputes them
-        if (e->sharded() && merged) {
-            ms->full_ok = false;
+        // full bytes exact at the touched nodes (only a range shard recomputes
+        // them); the common words would stand as a subset of the new ones, but
+        // common2 would not (a node that stopped being poor joins its AND), so
+        // both are recomputed
+        if (merged) {
+            if (e->sharded()) ms->full_ok = false;
             ms->common_ok = false;
         }
         set_release(e, ms);

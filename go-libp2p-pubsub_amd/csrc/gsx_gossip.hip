@@ -501,6 +501,22 @@ __device__ __forceinline__ void gx_pick_sampled(const HbState& h, uint64_t tb, u
     });
 }
 
+#ifdef GSX_GX_PROF  // (diagnostic build only: k_gx_ask's work counts, printed per round)
+__device__ unsigned long long gx_prof[16];
+#define GXP(i, v) atomicAdd(&gx_prof[i], (unsigned long long)(v))
+extern "C" void gx_prof_dump() {
+    unsigned long long c[16];
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gx_prof), sizeof(c));
+    fprintf(stderr, "gx_prof tall=%llu gate2=%llu gate2_nf=%llu heavy=%llu cb=%llu batches=%llu words=%llu n_pos=%llu "
+                    "nodes_nf=%llu nf_bits=%llu tr=%llu topic_skip=%llu nomrow=%llu poor_bits=%llu cb_rhm=%llu miss_sum=%llu\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15]);
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gx_prof), z, sizeof(z));
+}
+#else
+#define GXP(i, v) ((void)0)
+#endif
 constexpr uint32_t GX_END = 0xFFFFFFFFu;  // GxBatch::nxt: the set's last batch
 constexpr uint32_t GX_MW = 128;  // words of unseen batches a receiver's lane walks itself (else: a wave, GX_HEAVY)
 constexpr uint32_t GX_HEAVY = 1u << 31;  // gx_nodes entry: pass 1 runs in k_gx_node
@@ -528,15 +544,23 @@ __device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t
     for (; cb; cb &= cb - 1) {
         const uint32_t g = (uint32_t)__builtin_ctzll(cb);
         const GxBatch& b = h.gx[g];
-        if (!((tb >> b.topic) & 1)) continue;
+        if (!((tb >> b.topic) & 1)) {
+            GXP(11, 1);
+            continue;
+        }
+        GXP(5, 1);
         const uint64_t* mrow = gx_memrow(h, b, q, v);
-        if (!mrow) return;  // (a remote sender with no uncommon rows: none in any batch)
+        if (!mrow) {
+            GXP(12, 1);
+            return;  // (a remote sender with no uncommon rows: none in any batch)
+        }
         const uint32_t W = b.n_words;
         const uint64_t* arow = b.all + (size_t)uu * W;
         const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
         const uint32_t wmask = W <= 8 ? wm[64 * g] : 0xFFFFFFFFu;
         for (uint32_t w = 0; w < W; ++w) {
             if (!((wmask >> (w < 32 ? w : 31)) & 1)) continue;
+            GXP(6, 1);
             uint64_t c = mrow[w] & ~arow[w];
             if (sub) c &= sub[b.row_off + w];
             if (c && !f(g, w, c)) return;
@@ -563,6 +587,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     __shared__ uint8_t wms[64][64];  // [batch][node of the tile]: words (<= 8 per batch) where the node lacks a message
     __shared__ int64_t rp[65];      // row_ptr of the tile's nodes
     __shared__ uint64_t nfs[64];    // per node: the unseen-batch mask
+    __shared__ uint64_t pms[64];    // per node (gx_poor): the batches it misses more than GX_POOR messages of
     __shared__ uint32_t nmls[64];   // per node: GX_HEAVY
     __shared__ uint32_t lst[64];    // per node: listed for k_gx_node
     const uint32_t lane = threadIdx.x;
@@ -572,7 +597,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     for (uint32_t tile = blockIdx.x * 64u; tile < h.n_nodes; tile += gridDim.x * 64u) {
         const uint32_t u = tile + lane;
         {  // ---- lane per node: unseen batches, their words
-            uint64_t nf = 0;
+            uint64_t nf = 0, pm = 0;
             uint32_t nw = 0;
             bool heavy = n_gx > 64;
             if (u < h.n_nodes) {
@@ -587,17 +612,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                         break;
                     }
                     if (W <= 8) {
-                        uint32_t mk = 0;
+                        uint32_t mk = 0, miss = 0;
                         for (uint32_t w = 0; w < W; ++w) {
                             const uint32_t left = b.n_msgs > w * 64 ? b.n_msgs - w * 64 : 0;
                             const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
-                            if (~b.all[(size_t)u * W + w] & valid) mk |= 1u << w;
+                            const uint64_t lack = ~b.all[(size_t)u * W + w] & valid;
+                            if (lack) mk |= 1u << w;
+                            miss += (uint32_t)__popcll(lack);
                         }
                         wms[g][lane] = (uint8_t)mk;
+                        if (miss > GX_POOR) pm |= 1ull << g;  // (k_gx_setprep's test: n_msgs - seen > GX_POOR)
+                        GXP(15, miss);
+                    } else {
+                        pm |= 1ull << g;  // (no word masks: unfiltered)
                     }
                 }
             }
             nfs[lane] = nf;
+            pms[lane] = h.gx_poor ? pm : 0ull;
+            if (pm) GXP(13, __popcll(pm));
+            if (nf) {
+                GXP(8, 1);
+                GXP(9, __popcll(nf));
+            }
             nmls[lane] = heavy ? GX_HEAVY : 0u;
             lst[lane] = 0;
             rp[lane] = h.row_ptr[u < h.n_nodes ? u : h.n_nodes];
@@ -620,12 +657,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 rev_n = h.rev[q + 64];
             }
             if (!tall) continue;
+            GXP(0, 1);
             const int gt = gx_gate(s, h, (uint64_t)q, r);
             ignored += gt == 1;
             const uint64_t nf = nfs[k];
+            if (gt == 2) GXP(1, 1);
             if (gt != 2 || !nf) continue;
+            GXP(2, 1);
             const uint32_t nm = nmls[k];
             if (nm & GX_HEAVY) {
+                GXP(3, 1);
                 lst[k] = 1;
                 continue;
             }
@@ -634,9 +675,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             const uint32_t v = (uint32_t)h.col[q];
             // the unseen batches whose row at v holds a message not every node had:
             // only there can v hold one u lacks
-            const uint64_t cb = nf & gx_rhm_of(h, (uint64_t)q, v);
+            const uint64_t cb = nf & (gx_rhm_of(h, (uint64_t)q, v) | pms[k]);
+            if (nf & gx_rhm_of(h, (uint64_t)q, v)) GXP(14, 1);
             if (!cb) continue;  // |iwant| = 0 (:652-654)
+            GXP(4, 1);
             const uint64_t tr = h.ihave_tr[q];
+            if (tr) GXP(10, 1);
             // |iwant|: v's cache words where u lacks something (topics of the RPC,
             // the subset row of a truncated list)
             uint32_t n = 0;
@@ -645,6 +689,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 return true;
             });
             if (n == 0) continue;  // :652-654
+            GXP(7, 1);
             const uint32_t budget = (uint32_t)h.gp.max_ihave;  // MaxIHaveLength - iasked (0: above)
             const uint32_t kk = n < budget ? n : budget;
             uint32_t pick_g = 0, pick_k = 0;
@@ -889,17 +934,24 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
         uint64_t m = n_gx > 64 ? ~0ull : 0ull;
         for (uint32_t g = 0; g < n_gx && g < 64; ++g) {
             const GxBatch& b = gx[g];
-            if (b.dense) {  // (a set bit only lets the ask read the row: always safe)
+            // (one engine: the rows against common2, first-hand batches too — an
+            // isolated node empties `common`, not common2; k_gx_ask adds the
+            // batches its node is poor in)
+            const uint64_t* cw = b.common2 ? b.common2 : b.common;
+            if (b.dense && !b.common2) {  // (a set bit only lets the ask read the row: always safe)
                 m |= 1ull << g;
                 continue;
             }
-            if (b.cnt) {  // a recovered batch: the node's count of it (its rows are sparse: most counts 0);
-                if (b.cnt[v]) m |= 1ull << g;  // a non-empty row is taken as uncommon (safe, as above)
-                continue;
+            if (b.cnt && !b.dense) {  // a recovered batch: the node's count of it (its rows are sparse: most counts 0);
+                if (!b.cnt[v]) continue;
+                if (!b.common2) {  // a non-empty row is taken as uncommon (safe, as above)
+                    m |= 1ull << g;
+                    continue;
+                }  // (one engine: the non-empty rows against common2 — a round recovers copies at most nodes)
             }
             const uint32_t W = b.n_words;
             uint64_t any = 0;
-            for (uint32_t w = 0; w < W; ++w) any |= b.mem[(size_t)v * W + w] & ~(b.common ? b.common[w] : 0ull);
+            for (uint32_t w = 0; w < W; ++w) any |= b.mem[(size_t)v * W + w] & ~(cw ? cw[w] : 0ull);
             if (any) m |= 1ull << g;
         }
         rhm[v] = m;
@@ -910,40 +962,97 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
 // for `full`, zeros to the receipt row, an AND per word reduced over the wave
 // and the block, one atomic per (block, word)).
 __global__ __launch_bounds__(256) void k_gx_setprep(const GxSetPrep* __restrict__ sets, uint32_t n) {
-    __shared__ unsigned long long sw[64];
+    __shared__ unsigned long long sw[64], sw2[64];
     const GxSetPrep S = sets[blockIdx.y];
     const uint32_t W = S.n_words;
     const bool and_words = S.common != nullptr && W <= 64;
+    const bool and2 = and_words && S.common2 != nullptr;
     const bool read = and_words || S.full;
-    if (threadIdx.x < 64) sw[threadIdx.x] = ~0ull;
+    if (threadIdx.x < 64) sw[threadIdx.x] = sw2[threadIdx.x] = ~0ull;
     __syncthreads();
     const uint32_t stride = gridDim.x * 256u;
-    // (a uniform trip count: every lane takes part in the wave reductions)
-    for (uint32_t v0 = blockIdx.x * 256u; v0 < n; v0 += stride) {
-        const uint32_t v = v0 + threadIdx.x;
-        const bool in = v < n;
-        uint32_t c = 0;
-        for (uint32_t w = 0; w < W; ++w) {
-            const uint64_t x = in && read ? S.all[(size_t)v * W + w] : ~0ull;
-            if (in) {
-                c += (uint32_t)__popcll(x);
-                if (S.x) S.x[(size_t)v * W + w] = 0;
-            }
-            if (and_words) {
-                uint64_t a = x;
+    if (W <= 8) {
+        // (sets of up to eight words: the lane's words held in registers, ANDed into
+        // per-lane accumulators; one wave reduction per word at the end)
+        uint64_t a1[8], a2[8];
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) a &= (uint64_t)__shfl_xor((long long)a, off, 64);
-                if ((threadIdx.x % 64) == 0) atomicAnd(&sw[w], (unsigned long long)a);
+        for (int w = 0; w < 8; ++w) a1[w] = a2[w] = ~0ull;
+        for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < n; v += stride) {
+            uint64_t x[8];
+            uint32_t c = 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const bool on = (uint32_t)w < W;
+                x[w] = on && read ? S.all[(size_t)v * W + w] : ~0ull;
+                if (on && read) c += (uint32_t)__popcll(x[w]);
+                if (on && S.x) S.x[(size_t)v * W + w] = 0;
+            }
+            if (S.full) S.full[v] = c == S.n_msgs;
+            const bool rich = c + GX_POOR >= S.n_msgs;  // (k_gx_ask's poor test)
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                a1[w] &= x[w];
+                if (rich) a2[w] &= x[w];
+            }
+            if (S.x) {  // the recovered rows' summary beside them (k_gx_merge_sets writes touched nodes only)
+                S.x[(size_t)W * n + v] = 0;
+                reinterpret_cast<uint32_t*>(S.x + (size_t)W * n + n)[v] = 0;
             }
         }
-        if (in && S.full) S.full[v] = c == S.n_msgs;
-        if (in && S.x) {  // the recovered rows' summary beside them (k_gx_merge_sets writes touched nodes only)
-            S.x[(size_t)W * n + v] = 0;
-            reinterpret_cast<uint32_t*>(S.x + (size_t)W * n + n)[v] = 0;
+        if (and_words) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                if ((uint32_t)w >= W) break;
+                uint64_t b1 = a1[w], b2 = a2[w];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    b1 &= (uint64_t)__shfl_xor((long long)b1, off, 64);
+                    b2 &= (uint64_t)__shfl_xor((long long)b2, off, 64);
+                }
+                if ((threadIdx.x % 64) == 0) {
+                    atomicAnd(&sw[w], (unsigned long long)b1);
+                    if (and2) atomicAnd(&sw2[w], (unsigned long long)b2);
+                }
+            }
+        }
+    } else {
+        // (a uniform trip count: every lane takes part in the wave reductions)
+        for (uint32_t v0 = blockIdx.x * 256u; v0 < n; v0 += stride) {
+            const uint32_t v = v0 + threadIdx.x;
+            const bool in = v < n;
+            uint32_t c = 0;
+            for (uint32_t w = 0; w < W; ++w) {
+                const uint64_t x = in && read ? S.all[(size_t)v * W + w] : ~0ull;
+                if (in) {
+                    c += (uint32_t)__popcll(x);
+                    if (S.x) S.x[(size_t)v * W + w] = 0;
+                }
+                if (and_words) {
+                    uint64_t a = x;
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) a &= (uint64_t)__shfl_xor((long long)a, off, 64);
+                    if ((threadIdx.x % 64) == 0) atomicAnd(&sw[w], (unsigned long long)a);
+                }
+            }
+            if (in && S.full) S.full[v] = c == S.n_msgs;
+            if (and2) {  // the nodes missing at most GX_POOR messages: their words again (cached), ANDed
+                const bool rich = in && c + GX_POOR >= S.n_msgs;
+                for (uint32_t w = 0; w < W; ++w) {
+                    uint64_t a = rich ? S.all[(size_t)v * W + w] : ~0ull;
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) a &= (uint64_t)__shfl_xor((long long)a, off, 64);
+                    if ((threadIdx.x % 64) == 0) atomicAnd(&sw2[w], (unsigned long long)a);
+                }
+            }
+            if (in && S.x) {  // the recovered rows' summary beside them (k_gx_merge_sets writes touched nodes only)
+                S.x[(size_t)W * n + v] = 0;
+                reinterpret_cast<uint32_t*>(S.x + (size_t)W * n + n)[v] = 0;
+            }
         }
     }
     __syncthreads();
     if (and_words && threadIdx.x < W) atomicAnd(reinterpret_cast<unsigned long long*>(&S.common[threadIdx.x]), sw[threadIdx.x]);
+    if (and2 && threadIdx.x < W) atomicAnd(reinterpret_cast<unsigned long long*>(&S.common2[threadIdx.x]), sw2[threadIdx.x]);
 }
 
 // Thread per node v of set blockIdx.y: merge its W receipt words and sum the

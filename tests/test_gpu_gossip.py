@@ -45,8 +45,12 @@ def _same(g, w):
     dict(T=1, n=300, msgs=4200, hops=2, ticks=4),  # 66-word sets: no common words, every asker heavy (k_gx_node)
     dict(T=1, n=10, d=3, msgs=6, hops=1, ticks=6),  # 10 nodes: a one-node frontier is already a dense hop
     dict(max_ihave_messages=0, ticks=4),      # MaxIHaveMessages 0: every IHAVE RPC ignored (peerhave limit)
+    # batches that reach most nodes: most receivers miss a few messages (<= GX_POOR, k_gx_ask filters
+    # their senders by the common2 words), a few miss many (unfiltered)
+    dict(hops=5, msgs=40, ticks=6),
+    dict(T=1, n=400, d=8, hops=4, msgs=100, ticks=6, invalid=0.1),
 ], ids=["default", "hg3", "broken", "invalid", "two_words", "trunc9", "trunc40", "prefill", "wide", "tiny10",
-        "no_ihave_msgs"])
+        "no_ihave_msgs", "reach5", "reach4_two_words"])
 def test_gossip_exchange_matches_oracle(gpu_ok, kw):
     T = kw.get("T", 2)
     g = gc.exchange_run(gsx.Engine(T), **kw)
