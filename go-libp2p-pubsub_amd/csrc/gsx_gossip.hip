@@ -950,8 +950,15 @@ __global__ __launch_bounds__(256) void k_gx_rhm(const GxBatch* __restrict__ gx, 
                 }  // (one engine: the non-empty rows against common2 — a round recovers copies at most nodes)
             }
             const uint32_t W = b.n_words;
+            const uint64_t* row = b.mem + (size_t)v * W;
             uint64_t any = 0;
-            for (uint32_t w = 0; w < W; ++w) any |= b.mem[(size_t)v * W + w] & ~(cw ? cw[w] : 0ull);
+            uint32_t w = 0;
+            if (!(reinterpret_cast<uintptr_t>(row) & 15u))  // (16-B loads: two words each)
+                for (; w + 2 <= W; w += 2) {
+                    const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(row + w);
+                    any |= (p.x & ~(cw ? cw[w] : 0ull)) | (p.y & ~(cw ? cw[w + 1] : 0ull));
+                }
+            for (; w < W; ++w) any |= row[w] & ~(cw ? cw[w] : 0ull);
             if (any) m |= 1ull << g;
         }
         rhm[v] = m;
