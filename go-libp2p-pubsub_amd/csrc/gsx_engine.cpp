@@ -4828,7 +4828,9 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
         common_of[i] = common;
         gsx::GxSetPrep p{ms->d_all, x_zero[i] ? nullptr : R.xs[i], gx_full_new[i] ? ms->d_full : nullptr,
                          redo_common ? common : nullptr, ms->n_words, ms->n_msgs};
-        p.common2 = (redo_common && !e->sharded()) ? common + 64 : nullptr;
+        // (common2 on one engine for sets of up to eight words: k_gx_setprep's register
+        // path; wider sets keep the all-node words, cached, and are walked unfiltered)
+        p.common2 = (redo_common && !e->sharded() && ms->n_words <= 8) ? common + 64 : nullptr;
         if (p.x || p.full || p.common) sprep.push_back(p);
     }
     std::vector<gsx::GxSetMerge> smerge(R.sets.size());
@@ -4844,7 +4846,7 @@ int gx_prepare(gsx_engine* e, gsx_engine::GxRound& R) {
     for (auto& g : gx) {
         const size_t si = reinterpret_cast<size_t>(g.got);
         g.common = common_of[si];
-        g.common2 = (common_of[si] && !e->sharded()) ? common_of[si] + 64 : nullptr;
+        g.common2 = (common_of[si] && !e->sharded() && R.sets[si]->n_words <= 8) ? common_of[si] + 64 : nullptr;
         g.got = e->d_gx_got + si;
     }
     HIPCHK(e, hipMemsetAsync(e->d_gx_got, 0, 2 * e->gx_cap, e->stream));  // got, chg
@@ -5040,10 +5042,10 @@ int hb_finish(gsx_engine* e, gsx_engine::GxRound& R, gsx_heartbeat_out* out, con
         // full bytes exact at the touched nodes (only a range shard recomputes
         // them); the common words would stand as a subset of the new ones, but
         // common2 would not (a node that stopped being poor joins its AND), so
-        // both are recomputed
+        // a set with common2 recomputes both
         if (merged) {
             if (e->sharded()) ms->full_ok = false;
-            ms->common_ok = false;
+            if (e->sharded() || ms->n_words <= 8) ms->common_ok = false;  // (sets with common2)
         }
         set_release(e, ms);
     }
