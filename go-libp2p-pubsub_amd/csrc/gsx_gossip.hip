@@ -509,8 +509,8 @@ extern "C" void gx_prof_dump() {
     (void)hipDeviceSynchronize();
     (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gx_prof), sizeof(c));
     fprintf(stderr, "gx_prof tall=%llu gate2=%llu gate2_nf=%llu heavy=%llu cb=%llu batches=%llu words=%llu n_pos=%llu "
-                    "nodes_nf=%llu nf_bits=%llu tr=%llu topic_skip=%llu nomrow=%llu poor_bits=%llu cb_rhm=%llu miss_sum=%llu\n",
-            c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15]);
+                    "nodes_nf=%llu nf_bits=%llu tr=%llu poor_bits=%llu cb_rhm=%llu miss_sum=%llu\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[13], c[14], c[15]);
     unsigned long long z[16] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(gx_prof), z, sizeof(z));
 }
@@ -544,16 +544,10 @@ __device__ __forceinline__ void gx_cwalk(const HbState& h, uint64_t cb, uint64_t
     for (; cb; cb &= cb - 1) {
         const uint32_t g = (uint32_t)__builtin_ctzll(cb);
         const GxBatch& b = h.gx[g];
-        if (!((tb >> b.topic) & 1)) {
-            GXP(11, 1);
-            continue;
-        }
+        if (!((tb >> b.topic) & 1)) continue;
         GXP(5, 1);
         const uint64_t* mrow = gx_memrow(h, b, q, v);
-        if (!mrow) {
-            GXP(12, 1);
-            return;  // (a remote sender with no uncommon rows: none in any batch)
-        }
+        if (!mrow) return;  // (a remote sender with no uncommon rows: none in any batch)
         const uint32_t W = b.n_words;
         const uint64_t* arow = b.all + (size_t)uu * W;
         const uint64_t* sub = gx_subrow(h, tr, b.topic, r);
@@ -630,11 +624,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             }
             nfs[lane] = nf;
             pms[lane] = h.gx_poor ? pm : 0ull;
-            if (pm) GXP(13, __popcll(pm));
-            if (nf) {
-                GXP(8, 1);
-                GXP(9, __popcll(nf));
-            }
+            GXP(13, __popcll(pm));
+            GXP(8, nf != 0);
+            GXP(9, __popcll(nf));
             nmls[lane] = heavy ? GX_HEAVY : 0u;
             lst[lane] = 0;
             rp[lane] = h.row_ptr[u < h.n_nodes ? u : h.n_nodes];
@@ -661,7 +653,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             const int gt = gx_gate(s, h, (uint64_t)q, r);
             ignored += gt == 1;
             const uint64_t nf = nfs[k];
-            if (gt == 2) GXP(1, 1);
+            GXP(1, gt == 2);
             if (gt != 2 || !nf) continue;
             GXP(2, 1);
             const uint32_t nm = nmls[k];
@@ -676,11 +668,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             // the unseen batches whose row at v holds a message not every node had:
             // only there can v hold one u lacks
             const uint64_t cb = nf & (gx_rhm_of(h, (uint64_t)q, v) | pms[k]);
-            if (nf & gx_rhm_of(h, (uint64_t)q, v)) GXP(14, 1);
+            GXP(14, (nf & gx_rhm_of(h, (uint64_t)q, v)) != 0);
             if (!cb) continue;  // |iwant| = 0 (:652-654)
             GXP(4, 1);
             const uint64_t tr = h.ihave_tr[q];
-            if (tr) GXP(10, 1);
+            GXP(10, tr != 0);
             // |iwant|: v's cache words where u lacks something (topics of the RPC,
             // the subset row of a truncated list)
             uint32_t n = 0;
